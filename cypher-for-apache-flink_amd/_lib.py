@@ -1,0 +1,186 @@
+"""ctypes binding of libcapf_gpu.so (the C-ABI declared in include/capf_gpu.h).
+
+The product path has exactly one implementation: the HIP library.  If the
+shared object is missing or fails to load, every entry point raises — there is
+no CPU fallback (oracle/ is test infrastructure and is never imported here).
+
+Error mapping mirrors the okapi exception hierarchy the Scala shim would
+rethrow (okapi-api/src/main/scala/org/opencypher/okapi/impl/exception/
+InternalException.scala:36-65).
+"""
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_int32, c_int64, c_uint8, c_uint32, c_uint64, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcapf_gpu.so")
+
+
+class CypherException(RuntimeError):
+    """Base of the okapi exceptions raised through the C-ABI."""
+
+
+class IllegalArgumentException(CypherException):
+    pass
+
+
+class NotImplementedException(CypherException):
+    pass
+
+
+class IllegalStateException(CypherException):
+    pass
+
+
+class HipRuntimeException(CypherException):
+    pass
+
+
+class DeviceOutOfMemoryException(HipRuntimeException):
+    pass
+
+
+_ERRORS = {
+    -1: IllegalArgumentException,
+    -2: NotImplementedException,
+    -3: IllegalStateException,
+    -4: HipRuntimeException,
+    -5: DeviceOutOfMemoryException,
+}
+
+
+class CapfExpr(ctypes.Structure):
+    _fields_ = [
+        ("n", c_int32),
+        ("ops", POINTER(c_int32)),
+        ("iargs", POINTER(c_int64)),
+        ("fargs", POINTER(c_double)),
+        ("n_names", c_int32),
+        ("names", POINTER(c_char_p)),
+    ]
+
+
+_S = c_void_p  # capf_session*
+_T = c_void_p  # capf_table*
+_PT = POINTER(c_void_p)
+_STRS = POINTER(c_char_p)
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "capf_last_error": (c_char_p, []),
+    "capf_last_error_kind": (c_int32, []),
+    "capf_abi_version": (c_int32, []),
+    "capf_session_create": (c_int32, [c_int32, c_void_p, _PT]),
+    "capf_session_destroy": (c_int32, [_S]),
+    "capf_session_sync": (c_int32, [_S]),
+    "capf_session_set_profiling": (c_int32, [_S, c_int32]),
+    "capf_session_reset_profile": (c_int32, [_S]),
+    "capf_session_profile_count": (c_int32, [_S, POINTER(c_int32)]),
+    "capf_session_profile_entry": (c_int32, [_S, c_int32, POINTER(c_char_p), POINTER(c_int64),
+                                             POINTER(c_double), POINTER(c_double)]),
+    "capf_session_last_plan": (c_char_p, [_S]),
+    "capf_string_intern": (c_int32, [_S, c_char_p, POINTER(c_int64)]),
+    "capf_string_lookup": (c_int32, [_S, c_int64, POINTER(c_char_p)]),
+    "capf_table_from_host": (c_int32, [_S, c_int32, _STRS, POINTER(c_int32), POINTER(c_void_p),
+                                       POINTER(c_void_p), c_int64, _PT]),
+    "capf_table_from_device": (c_int32, [_S, c_int32, _STRS, POINTER(c_int32), POINTER(c_void_p),
+                                         POINTER(c_void_p), c_int64, c_int32, _PT]),
+    "capf_table_unit": (c_int32, [_S, _PT]),
+    "capf_table_empty": (c_int32, [_S, c_int32, _STRS, POINTER(c_int32), _PT]),
+    "capf_table_retain": (c_int32, [_T]),
+    "capf_table_release": (c_int32, [_T]),
+    "capf_table_num_columns": (c_int32, [_T, POINTER(c_int32)]),
+    "capf_table_column_name": (c_int32, [_T, c_int32, POINTER(c_char_p)]),
+    "capf_table_column_type": (c_int32, [_T, c_char_p, POINTER(c_int32)]),
+    "capf_table_size": (c_int32, [_T, POINTER(c_int64)]),
+    "capf_table_download": (c_int32, [_T, c_char_p, c_void_p, c_void_p]),
+    "capf_table_device_column": (c_int32, [_T, c_char_p, POINTER(c_void_p), POINTER(c_void_p),
+                                           POINTER(c_int64)]),
+    "capf_table_cache": (c_int32, [_T, _PT]),
+    "capf_table_select": (c_int32, [_T, c_int32, _STRS, _STRS, _PT]),
+    "capf_table_filter": (c_int32, [_T, POINTER(CapfExpr), _PT]),
+    "capf_table_drop": (c_int32, [_T, c_int32, _STRS, _PT]),
+    "capf_table_join": (c_int32, [_T, _T, c_int32, c_int32, _STRS, _STRS, _PT]),
+    "capf_table_union_all": (c_int32, [_T, _T, _PT]),
+    "capf_table_order_by": (c_int32, [_T, c_int32, POINTER(CapfExpr), POINTER(c_int32), _PT]),
+    "capf_table_skip": (c_int32, [_T, c_int64, _PT]),
+    "capf_table_limit": (c_int32, [_T, c_int64, _PT]),
+    "capf_table_distinct": (c_int32, [_T, _PT]),
+    "capf_table_distinct_cols": (c_int32, [_T, c_int32, _STRS, _PT]),
+    "capf_table_group": (c_int32, [_T, c_int32, _STRS, c_int32, POINTER(c_int32), POINTER(CapfExpr),
+                                   POINTER(c_int32), _STRS, _PT]),
+    "capf_table_with_columns": (c_int32, [_T, c_int32, POINTER(CapfExpr), _STRS, _PT]),
+    "capf_table_show": (c_int32, [_T, c_int32]),
+    "capf_rmat_rel_table": (c_int32, [_S, c_int32, c_uint64, c_uint32, c_uint32, c_uint32, c_int64,
+                                      c_int64, c_int64, c_char_p, c_char_p, c_char_p, _PT]),
+    "capf_range_node_table": (c_int32, [_S, c_int64, c_int64, c_uint64, c_char_p, c_char_p, _PT]),
+    "capf_chain2_local_hists": (c_int32, [_S, _T, c_char_p, c_char_p, c_int64, c_int64, c_void_p,
+                                          c_void_p, POINTER(c_int64)]),
+    "capf_dot_u32": (c_int32, [_S, c_void_p, c_void_p, c_int64, POINTER(c_uint64)]),
+}
+
+EXPORTED_SYMBOLS = sorted(_SIGS)
+
+_lib = None
+
+
+def load(path=LIB_PATH):
+    """Load libcapf_gpu.so (raises if absent — there is no fallback)."""
+    global _lib
+    if _lib is not None and path == LIB_PATH:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} not found: build the HIP extension first (python -c 'import __graft_entry__ as g; g.build()')")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path == LIB_PATH:
+        _lib = lib
+    return lib
+
+
+def check(status):
+    if status != 0:
+        lib = load()
+        msg = lib.capf_last_error().decode("utf-8", "replace")
+        raise _ERRORS.get(status, CypherException)(msg)
+    return status
+
+
+def call(name, *args):
+    return check(getattr(load(), name)(*args))
+
+
+def strs(values):
+    arr = (c_char_p * max(len(values), 1))()
+    for i, v in enumerate(values):
+        arr[i] = v.encode() if isinstance(v, str) else v
+    return arr
+
+
+def _keepalive_expr(program):
+    """Build a CapfExpr from (ops, iargs, fargs, names); returns (struct, refs)."""
+    ops, iargs, fargs, names = program
+    n = len(ops)
+    o = (c_int32 * n)(*ops)
+    i = (c_int64 * n)(*iargs)
+    f = (c_double * n)(*fargs)
+    nm = strs(names)
+    e = CapfExpr(n, o, i, f, len(names), nm)
+    return e, (o, i, f, nm)
+
+
+def expr_array(programs):
+    """ctypes array of CapfExpr plus the buffers that must stay alive."""
+    arr = (CapfExpr * max(len(programs), 1))()
+    keep = []
+    for k, p in enumerate(programs):
+        if p is None:
+            continue
+        e, refs = _keepalive_expr(p)
+        arr[k] = e
+        keep.append(refs)
+    return arr, keep

@@ -1,0 +1,286 @@
+// capf_internal.h — runtime data structures of the MI355X relational backend.
+//
+// Columnar SoA tables in HBM, immutable and reference-counted, behind the
+// lazy plan DAG that mirrors the okapi RelationalOperator tree
+// (okapi-relational/.../impl/operators/RelationalOperator.scala:48-514).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/capf_gpu.h"
+
+namespace capf {
+
+// ----------------------------------------------------------------- errors
+struct Error : std::runtime_error {
+  int32_t code;
+  Error(int32_t c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+[[noreturn]] inline void fail(int32_t code, const std::string &m) { throw Error(code, m); }
+[[noreturn]] inline void illegal(const std::string &m) { fail(CAPF_ERR_ILLEGAL_ARGUMENT, m); }
+[[noreturn]] inline void not_impl(const std::string &m) { fail(CAPF_ERR_NOT_IMPLEMENTED, m); }
+
+#define HIP_CHECK(expr)                                                                  \
+  do {                                                                                   \
+    hipError_t _e = (expr);                                                              \
+    if (_e != hipSuccess)                                                                \
+      ::capf::fail(_e == hipErrorOutOfMemory ? CAPF_ERR_OOM : CAPF_ERR_HIP,              \
+                   std::string(#expr) + ": " + hipGetErrorString(_e));                   \
+  } while (0)
+
+#define KERNEL_CHECK() HIP_CHECK(hipGetLastError())
+
+enum class Type : int32_t {
+  Null = CAPF_TYPE_NULL,
+  Int64 = CAPF_TYPE_INT64,
+  Float64 = CAPF_TYPE_FLOAT64,
+  Bool = CAPF_TYPE_BOOL,
+  String = CAPF_TYPE_STRING
+};
+inline size_t type_width(Type t) { return t == Type::Bool ? 1 : (t == Type::Null ? 0 : 8); }
+const char *type_name(Type t);
+
+struct Session;
+
+// ------------------------------------------------------------- device memory
+struct DevBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  bool owned = true;
+  Session *s = nullptr;
+  ~DevBuf();
+};
+using BufPtr = std::shared_ptr<DevBuf>;
+
+// Column statistics, computed once per column (ingest-time metadata like
+// ORC/Parquet min/max), used to pick dense vs hashed join structures.
+struct ColStats {
+  int64_t non_null = 0;
+  int64_t min = 0, max = -1;   // over non-null values (int-like columns)
+  bool dense_unique = false;   // values are exactly {min..max}, each once
+};
+
+struct Column {
+  Type type = Type::Null;
+  int64_t n = 0;
+  BufPtr data;   // n * width bytes (nullptr for Type::Null or n == 0)
+  BufPtr valid;  // n bytes (1 = present) or nullptr = no nulls
+  mutable std::mutex mu;
+  mutable std::optional<ColStats> stats;
+  bool is_all_null() const { return type == Type::Null; }
+};
+using ColPtr = std::shared_ptr<Column>;
+
+struct Data {  // a materialised table body
+  int64_t nrows = 0;
+  std::vector<ColPtr> cols;
+};
+using DataPtr = std::shared_ptr<Data>;
+
+// ------------------------------------------------------------- expressions
+enum Op : int32_t {
+  OP_COL = CAPF_OP_COL, OP_LIT_INT = CAPF_OP_LIT_INT, OP_LIT_FLOAT = CAPF_OP_LIT_FLOAT,
+  OP_LIT_BOOL = CAPF_OP_LIT_BOOL, OP_LIT_STRING = CAPF_OP_LIT_STRING,
+  OP_LIT_NULL = CAPF_OP_LIT_NULL, OP_EQ = CAPF_OP_EQ, OP_NEQ = CAPF_OP_NEQ, OP_LT = CAPF_OP_LT,
+  OP_LE = CAPF_OP_LE, OP_GT = CAPF_OP_GT, OP_GE = CAPF_OP_GE, OP_NOT = CAPF_OP_NOT,
+  OP_AND = CAPF_OP_AND, OP_OR = CAPF_OP_OR, OP_IS_NULL = CAPF_OP_IS_NULL,
+  OP_IS_NOT_NULL = CAPF_OP_IS_NOT_NULL, OP_ADD = CAPF_OP_ADD, OP_SUB = CAPF_OP_SUB,
+  OP_MUL = CAPF_OP_MUL, OP_DIV = CAPF_OP_DIV, OP_MOD = CAPF_OP_MOD, OP_NEG = CAPF_OP_NEG,
+  OP_TO_FLOAT = CAPF_OP_TO_FLOAT, OP_TO_INTEGER = CAPF_OP_TO_INTEGER,
+  OP_COALESCE = CAPF_OP_COALESCE
+};
+
+struct Instr {
+  int32_t op;
+  int32_t pad;
+  int64_t i;
+  double f;
+};
+
+// An owned copy of a capf_expr with column names kept as strings.
+struct Program {
+  std::vector<Instr> code;
+  std::vector<std::string> names;
+  static Program from_c(const capf_expr *e);
+  std::vector<std::string> referenced() const;
+};
+
+// Device-side view of a column for kernels.
+struct ColView {
+  const void *data;
+  const uint8_t *valid;
+  int32_t type;
+  int32_t pad;
+};
+
+// ------------------------------------------------------------- plan nodes
+enum class Kind {
+  Source, Select, Filter, Join, Union, Distinct, Group, WithColumns, OrderBy, Skip, Limit
+};
+
+struct AggSpec {
+  int32_t kind;
+  bool distinct;
+  Program arg;  // empty for COUNT_STAR
+  std::string name;
+  Type out_type;
+};
+
+struct Node {
+  Session *s;
+  Kind kind;
+  std::vector<std::string> names;
+  std::vector<Type> types;
+  std::vector<std::shared_ptr<Node>> kids;
+  // Select: source index of each output column
+  std::vector<int> sel_index;
+  // Filter
+  Program pred;
+  // Join
+  int32_t join_type = CAPF_JOIN_INNER;
+  std::vector<std::pair<int, int>> join_keys;  // (left col idx, right col idx)
+  // Distinct / Group
+  std::vector<int> key_index;
+  std::vector<AggSpec> aggs;
+  // WithColumns / OrderBy
+  std::vector<Program> exprs;
+  std::vector<int> target_index;  // WithColumns: output index per expr
+  std::vector<int32_t> desc;
+  // Skip / Limit
+  int64_t count = 0;
+
+  // memoised result
+  std::mutex mu;
+  DataPtr result;
+
+  int col_index(const std::string &name) const;  // -1 if absent
+  int col_index_or_throw(const std::string &name) const;
+};
+using NodePtr = std::shared_ptr<Node>;
+
+// ------------------------------------------------------------- session
+struct ProfileEntry {
+  int64_t launches = 0;
+  double total_ms = 0;
+  double bytes = 0;
+};
+
+struct PendingTiming {
+  std::string name;
+  double bytes;
+  hipEvent_t a, b;
+};
+
+struct Session {
+  int device = 0;
+  std::vector<PendingTiming> pending;   // recorded, not yet resolved
+  std::vector<hipEvent_t> event_pool;
+  hipEvent_t get_event();
+  void resolve_profile();
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  bool profiling = false;
+  std::map<std::string, ProfileEntry> profile;
+  std::string last_plan = "none";
+  // string dictionary
+  std::mutex str_mu;
+  std::vector<std::string> strings;
+  std::unordered_map<std::string, int64_t> string_codes;
+  // small device scratch for scalar results
+  int64_t *d_scalars = nullptr;  // 64 slots
+  int64_t *h_scalars = nullptr;  // pinned mirror
+
+  BufPtr alloc(size_t bytes);
+  void sync();
+};
+
+// Scoped HIP-event timer around one hot kernel (profiling only).
+struct KernelTimer {
+  Session *s;
+  const char *name;
+  double bytes;
+  hipEvent_t a = nullptr, b = nullptr;
+  KernelTimer(Session *s_, const char *n, double by);
+  ~KernelTimer();
+};
+
+// ------------------------------------------------------------- helpers
+DataPtr materialize(const NodePtr &n);
+int64_t node_size(const NodePtr &n);
+ColPtr make_column(Session *s, Type t, int64_t n, bool with_valid);
+ColPtr null_column(Session *s, Type t, int64_t n);
+const ColStats &column_stats(Session *s, const ColPtr &c);
+ColView view_of(const ColPtr &c);
+
+// Type inference of a program against a schema (host side).
+Type infer_type(const Program &p, const std::vector<std::string> &names,
+                const std::vector<Type> &types);
+
+// ---- kernels (implemented in *.hip)
+// Evaluate a program over `n` rows; writes a column of type `out_type`.
+ColPtr eval_program(Session *s, const Program &p, const std::vector<std::string> &names,
+                    const Data &d, Type out_type);
+// Predicate → compacted row index list (rows where predicate is TRUE).
+BufPtr eval_filter(Session *s, const Program &p, const std::vector<std::string> &names,
+                   const Data &d, int64_t *out_count);
+// Gather rows (int64 indices, -1 = null row) of a column.
+ColPtr gather_column(Session *s, const ColPtr &c, const int64_t *d_idx, int64_t n,
+                     bool idx_may_be_null = false);
+BufPtr iota_index(Session *s, int64_t start, int64_t m);
+void cross_index(Session *s, int64_t nl, int64_t nr, BufPtr &li, BufPtr &ri);
+// Compact indices of rows whose flag byte is non-zero.
+BufPtr compact_flags(Session *s, const uint8_t *d_flags, int64_t n, int64_t *out_count);
+// Concatenate columns.
+ColPtr concat_columns(Session *s, const ColPtr &a, const ColPtr &b, Type t);
+// Exclusive scan of int64 counts; returns total.
+int64_t exclusive_scan_i64(Session *s, const int64_t *d_in, int64_t *d_out, int64_t n);
+// Hash grouping: group id per row (dense, 0..ngroups-1) and representative row per group.
+struct Grouping {
+  BufPtr group_of_row;  // int64 [nrows]
+  BufPtr rep_row;       // int64 [ngroups]
+  int64_t ngroups = 0;
+};
+Grouping group_rows(Session *s, const Data &d, const std::vector<int> &keys);
+// Equi-join of two materialised tables on key columns → (left idx, right idx) pairs.
+struct JoinPairs {
+  BufPtr left, right;  // int64 [n], -1 for a null-extended side
+  int64_t n = 0;
+};
+JoinPairs hash_join(Session *s, const Data &l, const Data &r,
+                    const std::vector<std::pair<int, int>> &keys, int32_t join_type);
+// Aggregations over a grouping.
+ColPtr aggregate(Session *s, const Grouping &g, const Data &d, int64_t nrows, int32_t kind,
+                 const ColPtr &arg, Type out_type);
+// Sort permutation (stable) by key columns.
+BufPtr sort_permutation(Session *s, const std::vector<ColPtr> &keys,
+                        const std::vector<int32_t> &desc, int64_t n);
+// Column statistics kernel.
+ColStats compute_stats(Session *s, const Column &c);
+
+// Record an error for capf_last_error() (used by entry points outside runtime.cpp).
+int32_t record_error(int32_t code, const char *msg);
+
+// Fused counting over lazy inner-join trees (the Expand hot path).
+bool try_fused_count(const NodePtr &n, int64_t *out);
+
+}  // namespace capf
+
+// opaque handle given to C callers
+struct capf_table {
+  capf::NodePtr node;
+};
+struct capf_session {
+  capf::Session impl;
+};

@@ -1,0 +1,93 @@
+// device_common.h — wave64 building blocks shared by the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace capf {
+
+constexpr int WAVE = 64;  // CDNA wavefront width (never 32)
+
+__host__ __device__ inline uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// 64-bit finaliser used for hash tables (murmur3 fmix64).
+__host__ __device__ inline uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+__device__ inline int lane_id() { return threadIdx.x & (WAVE - 1); }
+
+// Inclusive wave64 prefix sum.
+template <typename T>
+__device__ inline T wave_inclusive_scan(T v) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < WAVE; d <<= 1) {
+    T u = __shfl_up(v, d, WAVE);
+    if (lane >= d) v += u;
+  }
+  return v;
+}
+
+template <typename T>
+__device__ inline T wave_reduce_sum(T v) {
+#pragma unroll
+  for (int d = WAVE / 2; d > 0; d >>= 1) v += __shfl_xor(v, d, WAVE);
+  return v;
+}
+
+// Block-wide exclusive scan (blockDim.x multiple of 64, <= 1024); returns the
+// exclusive prefix of `v` and the block total through `total`.
+template <typename T>
+__device__ inline T block_exclusive_scan(T v, T *lds /* >= 16 */, T &total) {
+  const int lane = lane_id();
+  const int wid = threadIdx.x / WAVE;
+  const int nw = blockDim.x / WAVE;
+  T inc = wave_inclusive_scan(v);
+  if (lane == WAVE - 1) lds[wid] = inc;
+  __syncthreads();
+  if (wid == 0) {
+    T w = lane < nw ? lds[lane] : T(0);
+    T winc = wave_inclusive_scan(w);
+    if (lane < nw) lds[lane] = winc - w;  // exclusive wave offsets
+    if (lane == nw - 1) lds[16] = winc;
+  }
+  __syncthreads();
+  T res = inc - v + lds[wid];
+  total = lds[16];
+  __syncthreads();
+  return res;
+}
+
+template <typename T>
+__device__ inline T block_reduce_sum(T v, T *lds /* >= 16 */) {
+  const int lane = lane_id();
+  const int wid = threadIdx.x / WAVE;
+  const int nw = blockDim.x / WAVE;
+  v = wave_reduce_sum(v);
+  if (lane == 0) lds[wid] = v;
+  __syncthreads();
+  T r = 0;
+  if (threadIdx.x == 0)
+    for (int i = 0; i < nw; ++i) r += lds[i];
+  __syncthreads();
+  return r;  // valid in thread 0 only
+}
+
+inline unsigned grid_for(int64_t n, int block, int64_t cap = 256 * 16) {
+  int64_t g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+}  // namespace capf

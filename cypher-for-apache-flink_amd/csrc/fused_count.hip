@@ -1,0 +1,859 @@
+// fused_count.hip — factorised count(*) over lazy inner-join trees.
+//
+// This is the hot path of the north star: the relational plan of
+//   MATCH (a)-->(b)-->(c) RETURN count(*)
+// as lowered by RelationalPlanner (okapi-relational/.../impl/planning/
+// RelationalPlanner.scala:130-165, Aggregate :111, Filter :113) is
+//   S_a ⋈[a=start(r1)] R1 ⋈[end(r1)=b] S_b ⋈[b=start(r2)] R2 ⋈[end(r2)=c] S_c
+//   → Filter(NOT(r1 = r2))  (front-end uniqueness rewrite, CypherParser.scala:72)
+//   → Aggregate(∅, count(*)) (RelationalOperator.scala:334-346 → Table.group)
+// Flink executes it as four materialising hash joins (FlinkTable.join,
+// FlinkTable.scala:171-187) over ~1e12 rows at R-MAT s24.  Here the same
+// result is computed exactly without materialising any joined row:
+//
+//  * the join tree is collected from the lazy plan DAG (Select/Alias are
+//    transparent, single-table predicates are pushed into their leaf);
+//  * count(*) of an acyclic equi-join is evaluated by message passing: every
+//    leaf sends its parent a histogram key → Σ weight (GROUP BY on the join
+//    key with a weighted count), the root sums its row weights;
+//  * relationship-uniqueness filters NOT(r_i = r_j) are removed by
+//    inclusion–exclusion: the r_i = r_j term merges both scans of the same
+//    rel table into one leaf (ids are unique), which turns the b-join into
+//    the intra-row predicate start = end (self-loops);
+//  * the exact 2-hop shape runs as ONE pass over the rel table
+//    (k_chain2_*): both histograms and the self-loop correction, followed by
+//    a dot product over the node range.
+#include <algorithm>
+#include <cstring>
+#include <functional>
+#include <numeric>
+#include <set>
+
+#include "capf_internal.h"
+#include "device_common.h"
+
+namespace capf {
+
+// ============================================================ device maps
+enum MapKind : int32_t { MAP_ONES = 0, MAP_DENSE = 1, MAP_HASH = 2, MAP_DENSE32 = 3 };
+
+struct DMap {
+  int32_t kind;
+  int32_t pad;
+  int64_t lo, hi;                 // dense / ones: key range [lo, hi]
+  unsigned long long *vals;       // dense: hi-lo+1 entries; hash: capacity entries
+  int64_t *keys;                  // hash keys (HASH_EMPTY = free)
+  uint64_t mask;                  // hash capacity - 1
+};
+
+constexpr int64_t HASH_EMPTY = INT64_MIN;
+
+__device__ inline unsigned long long map_get(const DMap &m, int64_t k) {
+  if (m.kind == MAP_ONES) return (k >= m.lo && k <= m.hi) ? 1ull : 0ull;
+  if (m.kind == MAP_DENSE) return (k >= m.lo && k <= m.hi) ? m.vals[k - m.lo] : 0ull;
+  if (m.kind == MAP_DENSE32)
+    return (k >= m.lo && k <= m.hi) ? (unsigned long long)((const uint32_t *)m.vals)[k - m.lo] : 0ull;
+  uint64_t slot = fmix64((uint64_t)k) & m.mask;
+  while (true) {
+    int64_t cur = m.keys[slot];
+    if (cur == k) return m.vals[slot];
+    if (cur == HASH_EMPTY) return 0ull;
+    slot = (slot + 1) & m.mask;
+  }
+}
+
+__device__ inline void map_add(const DMap &m, int64_t k, unsigned long long w) {
+  if (m.kind == MAP_DENSE) {
+    if (k >= m.lo && k <= m.hi) atomicAdd(&m.vals[k - m.lo], w);
+    return;
+  }
+  uint64_t slot = fmix64((uint64_t)k) & m.mask;
+  while (true) {
+    int64_t cur = m.keys[slot];
+    if (cur == HASH_EMPTY) {
+      unsigned long long old = atomicCAS((unsigned long long *)&m.keys[slot],
+                                         (unsigned long long)HASH_EMPTY, (unsigned long long)k);
+      cur = (int64_t)old;
+      if (cur == HASH_EMPTY) cur = k;
+    }
+    if (cur == k) {
+      atomicAdd(&m.vals[slot], w);
+      return;
+    }
+    slot = (slot + 1) & m.mask;
+  }
+}
+
+constexpr int MAX_CHILD = 6;
+
+struct MsgJob {
+  ColView cols[MAX_CHILD + 1];  // child key columns, then the parent key column
+  DMap child[MAX_CHILD];
+  int32_t nchild;
+  int32_t has_parent;
+  DMap out;
+};
+
+__device__ inline bool load_key(const ColView &c, int64_t r, int64_t &k) {
+  if (c.type == CAPF_TYPE_NULL || !c.data || (c.valid && !c.valid[r])) return false;
+  k = ((const int64_t *)c.data)[r];
+  return true;
+}
+
+// One message (or the root sum) of the message-passing count.
+__global__ void k_message(const MsgJob *jp, int64_t n, unsigned long long *root_acc) {
+  const MsgJob &j = *jp;
+  unsigned long long local = 0;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    unsigned long long w = 1;
+    for (int c = 0; c < j.nchild && w; ++c) {
+      int64_t k;
+      w = load_key(j.cols[c], r, k) ? w * map_get(j.child[c], k) : 0ull;
+    }
+    if (!w) continue;
+    if (j.has_parent) {
+      int64_t k;
+      if (load_key(j.cols[j.nchild], r, k)) map_add(j.out, k, w);
+    } else {
+      local += w;
+    }
+  }
+  if (!j.has_parent) {
+    local = wave_reduce_sum(local);
+    if (lane_id() == 0 && local) atomicAdd(root_acc, local);
+  }
+}
+
+// ============================================================ 2-hop fast path
+// One pass over the rel table computes, for the Sb key range [lo, hi]:
+//   h1[b] += Wa(u1)        for rels with v1 = b      (hop 1, message R1 → S_b)
+//   h2[b] += Wc(v2)        for rels with u2 = b      (hop 2, message R2 → S_b)
+//   loops += Wa(u1)·Wb(v1)·Wc(v2) for rels with v1 = u2 (the r1 = r2 term)
+// Node weights are 1 on a dense id range (MAP_ONES) or a per-id count array.
+struct Chain2Args {
+  const int64_t *u1, *v1, *u2, *v2;  // rel columns (u2/v2 may alias u1/v1)
+  int64_t n;
+  DMap wa, wb, wc;
+  int64_t lo, hi;
+  uint32_t *h1, *h2;
+  unsigned long long *loops;
+};
+
+template <bool ONES>
+__device__ inline unsigned long long w_of(const DMap &m, int64_t k) {
+  if (ONES) return (k >= m.lo && k <= m.hi) ? 1ull : 0ull;
+  return map_get(m, k);
+}
+
+template <bool ONES>
+__global__ __launch_bounds__(256) void k_chain2_hist(Chain2Args a) {
+  unsigned long long loops = 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.n; e += stride) {
+    const int64_t x1 = a.u1[e], y1 = a.v1[e];
+    const int64_t x2 = a.u2[e], y2 = a.v2[e];
+    const unsigned long long wa = w_of<ONES>(a.wa, x1);
+    const unsigned long long wc = w_of<ONES>(a.wc, y2);
+    if (wa && y1 >= a.lo && y1 <= a.hi) atomicAdd(&a.h1[y1 - a.lo], (uint32_t)wa);
+    if (wc && x2 >= a.lo && x2 <= a.hi) atomicAdd(&a.h2[x2 - a.lo], (uint32_t)wc);
+    if (y1 == x2 && wa && wc) loops += wa * wc * w_of<ONES>(a.wb, y1);
+  }
+  loops = wave_reduce_sum(loops);
+  if (lane_id() == 0 && loops) atomicAdd(a.loops, loops);
+}
+
+template <bool ONES>
+__global__ __launch_bounds__(256) void k_chain2_dot(const uint32_t *h1, const uint32_t *h2,
+                                                    DMap wb, int64_t lo, int64_t len,
+                                                    unsigned long long *acc) {
+  __shared__ unsigned long long lds[17];
+  unsigned long long s = 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  // 4 counters per thread per step: dwordx4 loads of both histograms
+  const int64_t n4 = len / 4;
+  const uint4 *a4 = (const uint4 *)h1;
+  const uint4 *b4 = (const uint4 *)h2;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    uint4 x = a4[i], y = b4[i];
+    if (ONES) {
+      s += (unsigned long long)x.x * y.x + (unsigned long long)x.y * y.y +
+           (unsigned long long)x.z * y.z + (unsigned long long)x.w * y.w;
+    } else {
+      int64_t k = lo + 4 * i;
+      s += (unsigned long long)x.x * y.x * w_of<false>(wb, k) +
+           (unsigned long long)x.y * y.y * w_of<false>(wb, k + 1) +
+           (unsigned long long)x.z * y.z * w_of<false>(wb, k + 2) +
+           (unsigned long long)x.w * y.w * w_of<false>(wb, k + 3);
+    }
+  }
+  for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < len; i += stride)
+    s += (unsigned long long)h1[i] * h2[i] * (ONES ? 1ull : w_of<false>(wb, lo + i));
+  s = block_reduce_sum(s, lds);
+  if (threadIdx.x == 0 && s) atomicAdd(acc, s);
+}
+
+// per-id count array of a node table's id column over [lo, hi]
+__global__ void k_count_ids(const int64_t *ids, const uint8_t *valid, int64_t n, int64_t lo,
+                            int64_t hi, uint32_t *cnt) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (valid && !valid[i]) continue;
+    int64_t k = ids[i];
+    if (k >= lo && k <= hi) atomicAdd(&cnt[k - lo], 1u);
+  }
+}
+
+// ============================================================ plan analysis
+struct ColRef {
+  int leaf = -1;
+  int col = -1;
+  bool operator==(const ColRef &o) const { return leaf == o.leaf && col == o.col; }
+};
+
+struct Leaf {
+  NodePtr node;                   // base plan node (materialisable)
+  std::vector<Program> filters;   // single-leaf predicates pushed down (leaf column names)
+  std::vector<std::pair<int, int>> col_eqs;  // intra-row equalities (after merges)
+};
+
+struct JoinGraph {
+  std::vector<Leaf> leaves;
+  std::vector<std::pair<ColRef, ColRef>> eqs;
+  std::vector<std::pair<ColRef, ColRef>> neqs;
+};
+
+static bool collect(const NodePtr &n, JoinGraph &g, std::vector<ColRef> &out);
+
+static bool program_is_uniqueness(const Program &p, std::vector<std::pair<int, int>> &pairs) {
+  // [COL a, COL b, EQ, NOT] | [COL a, COL b, NEQ], possibly combined by AND(k)
+  const auto &c = p.code;
+  size_t i = 0;
+  int terms = 0;
+  while (i < c.size()) {
+    if (i + 2 < c.size() && c[i].op == OP_COL && c[i + 1].op == OP_COL) {
+      if (c[i + 2].op == OP_NEQ) {
+        pairs.emplace_back((int)c[i].i, (int)c[i + 1].i);
+        i += 3;
+        ++terms;
+        continue;
+      }
+      if (i + 3 < c.size() && c[i + 2].op == OP_EQ && c[i + 3].op == OP_NOT) {
+        pairs.emplace_back((int)c[i].i, (int)c[i + 1].i);
+        i += 4;
+        ++terms;
+        continue;
+      }
+    }
+    if (c[i].op == OP_AND && i + 1 == c.size() && c[i].i == terms) {
+      ++i;
+      continue;
+    }
+    return false;
+  }
+  return terms > 0;
+}
+
+static bool collect(const NodePtr &n, JoinGraph &g, std::vector<ColRef> &out) {
+  out.clear();
+  {
+    std::lock_guard<std::mutex> lk(n->mu);
+    if (n->result) {  // already materialised: a leaf
+      int id = (int)g.leaves.size();
+      g.leaves.push_back(Leaf{n, {}, {}});
+      for (size_t i = 0; i < n->names.size(); ++i) out.push_back(ColRef{id, (int)i});
+      return true;
+    }
+  }
+  switch (n->kind) {
+    case Kind::Select: {
+      std::vector<ColRef> c;
+      if (!collect(n->kids[0], g, c)) return false;
+      for (int i : n->sel_index) out.push_back(c[i]);
+      return true;
+    }
+    case Kind::Join: {
+      if (n->join_type != CAPF_JOIN_INNER) break;
+      std::vector<ColRef> l, r;
+      if (!collect(n->kids[0], g, l)) return false;
+      if (!collect(n->kids[1], g, r)) return false;
+      for (auto &kp : n->join_keys) {
+        if (n->kids[0]->types[kp.first] != Type::Int64) return false;
+        g.eqs.emplace_back(l[kp.first], r[kp.second]);
+      }
+      out = l;
+      out.insert(out.end(), r.begin(), r.end());
+      return true;
+    }
+    case Kind::Filter: {
+      std::vector<ColRef> c;
+      if (!collect(n->kids[0], g, c)) return false;
+      out = c;
+      const NodePtr &kid = n->kids[0];
+      std::vector<int> refs;
+      for (auto &nm : n->pred.names) refs.push_back(kid->col_index(nm));
+      std::set<int> leaves;
+      for (int r : refs) leaves.insert(c[r].leaf);
+      if (leaves.size() == 1) {
+        // single-table predicate: push into the leaf with leaf column names
+        int lf = *leaves.begin();
+        Program p = n->pred;
+        for (size_t k = 0; k < p.names.size(); ++k)
+          p.names[k] = g.leaves[lf].node->names[c[refs[k]].col];
+        g.leaves[lf].filters.push_back(std::move(p));
+        return true;
+      }
+      std::vector<std::pair<int, int>> pairs;
+      if (!program_is_uniqueness(n->pred, pairs)) return false;
+      for (auto &pr : pairs) {
+        int a = refs[pr.first], b = refs[pr.second];
+        if (kid->types[a] != Type::Int64 || kid->types[b] != Type::Int64) return false;
+        g.neqs.emplace_back(c[a], c[b]);
+      }
+      return true;
+    }
+    default: break;
+  }
+  // any other operator is an opaque leaf
+  int id = (int)g.leaves.size();
+  g.leaves.push_back(Leaf{n, {}, {}});
+  for (size_t i = 0; i < n->names.size(); ++i) out.push_back(ColRef{id, (int)i});
+  return true;
+}
+
+// ============================================================ leaf data
+struct LeafData {
+  DataPtr data;
+  bool plain = false;  // unfiltered base data (eligible for column stats / merges)
+};
+
+static NodePtr filter_node(const NodePtr &base, const Program &p) {
+  auto f = std::make_shared<Node>();
+  f->s = base->s;
+  f->kind = Kind::Filter;
+  f->kids = {base};
+  f->pred = p;
+  f->names = base->names;
+  f->types = base->types;
+  return f;
+}
+
+static Program eq_program(const std::string &a, const std::string &b) {
+  Program p;
+  p.names = {a, b};
+  p.code = {Instr{OP_COL, 0, 0, 0}, Instr{OP_COL, 0, 1, 0}, Instr{OP_EQ, 0, 0, 0}};
+  return p;
+}
+
+static LeafData leaf_data(const Leaf &lf) {
+  LeafData ld;
+  NodePtr cur = lf.node;
+  for (auto &p : lf.filters) cur = filter_node(cur, p);
+  for (auto &e : lf.col_eqs)
+    cur = filter_node(cur, eq_program(lf.node->names[e.first], lf.node->names[e.second]));
+  ld.data = materialize(cur);
+  ld.plain = lf.filters.empty() && lf.col_eqs.empty();
+  return ld;
+}
+
+// ============================================================ message passing
+struct HostMap {
+  DMap m;
+  BufPtr vals, keys;
+};
+
+__global__ void k_fill_hash_empty(int64_t *k, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    k[i] = HASH_EMPTY;
+}
+
+static HostMap ones_map(int64_t lo, int64_t hi) {
+  HostMap h;
+  memset(&h.m, 0, sizeof(h.m));
+  h.m.kind = MAP_ONES;
+  h.m.lo = lo;
+  h.m.hi = hi;
+  return h;
+}
+
+static HostMap new_map_for(Session *s, const ColPtr &parent_key, int64_t sender_rows) {
+  HostMap h;
+  memset(&h.m, 0, sizeof(h.m));
+  const ColStats &st = column_stats(s, parent_key);
+  int64_t prow = parent_key->n;
+  uint64_t range = st.non_null > 0 ? (uint64_t)(st.max - st.min) + 1 : 0;
+  if (st.non_null > 0 && range <= (uint64_t(1) << 28) &&
+      range <= 16 * (uint64_t)std::max<int64_t>(std::max(prow, sender_rows), 1024)) {
+    h.m.kind = MAP_DENSE;
+    h.m.lo = st.min;
+    h.m.hi = st.max;
+    h.vals = s->alloc(8 * range);
+    HIP_CHECK(hipMemsetAsync(h.vals->p, 0, 8 * range, s->stream));
+    h.m.vals = (unsigned long long *)h.vals->p;
+  } else if (st.non_null == 0) {
+    h.m.kind = MAP_ONES;  // empty range: everything maps to 0
+    h.m.lo = 1;
+    h.m.hi = 0;
+  } else {
+    uint64_t cap = 1024;
+    while (cap < 2 * (uint64_t)std::max<int64_t>(sender_rows, 1)) cap <<= 1;
+    h.m.kind = MAP_HASH;
+    h.m.mask = cap - 1;
+    h.keys = s->alloc(8 * cap);
+    h.vals = s->alloc(8 * cap);
+    HIP_CHECK(hipMemsetAsync(h.vals->p, 0, 8 * cap, s->stream));
+    hipLaunchKernelGGL(k_fill_hash_empty, dim3(grid_for((int64_t)cap, 256)), dim3(256), 0,
+                       s->stream, (int64_t *)h.keys->p, cap);
+    KERNEL_CHECK();
+    h.m.keys = (int64_t *)h.keys->p;
+    h.m.vals = (unsigned long long *)h.vals->p;
+  }
+  return h;
+}
+
+// Count of the acyclic equi-join described by `g` (no inequalities).
+static bool tree_count(Session *s, JoinGraph &g, uint64_t *out) {
+  const int L = (int)g.leaves.size();
+  if (L == 0) return false;
+  // adjacency; reject cycles / multi-edges / disconnected graphs
+  std::vector<std::vector<std::pair<int, int>>> adj(L);  // (neighbour, eq index)
+  for (size_t e = 0; e < g.eqs.size(); ++e) {
+    int a = g.eqs[e].first.leaf, b = g.eqs[e].second.leaf;
+    if (a == b) return false;
+    adj[a].emplace_back(b, (int)e);
+    adj[b].emplace_back(a, (int)e);
+  }
+  if ((int)g.eqs.size() != L - 1) return false;
+  // choose the tree centre as root (shortest longest path)
+  auto ecc = [&](int r) {
+    std::vector<int> d(L, -1);
+    std::vector<int> q{r};
+    d[r] = 0;
+    for (size_t i = 0; i < q.size(); ++i)
+      for (auto &nb : adj[q[i]])
+        if (d[nb.first] < 0) {
+          d[nb.first] = d[q[i]] + 1;
+          q.push_back(nb.first);
+        }
+    int m = 0;
+    for (int x : d) {
+      if (x < 0) return -1;
+      m = std::max(m, x);
+    }
+    return m;
+  };
+  int root = 0, best = 1 << 30;
+  for (int r = 0; r < L; ++r) {
+    int e = ecc(r);
+    if (e < 0) return false;
+    if (e < best) {
+      best = e;
+      root = r;
+    }
+  }
+  std::vector<LeafData> data(L);
+  for (int i = 0; i < L; ++i) data[i] = leaf_data(g.leaves[i]);
+  for (int i = 0; i < L; ++i)
+    if (data[i].data->nrows >= (int64_t(1) << 40)) return false;
+
+  std::vector<HostMap> msg(L);
+  BufPtr job_buf = s->alloc(sizeof(MsgJob));
+  BufPtr acc = s->alloc(8);
+  HIP_CHECK(hipMemsetAsync(acc->p, 0, 8, s->stream));
+  std::function<void(int, int, int)> visit = [&](int v, int parent, int via_eq) {
+    MsgJob j;
+    memset(&j, 0, sizeof(j));
+    for (auto &nb : adj[v]) {
+      if (nb.first == parent) continue;
+      visit(nb.first, v, nb.second);
+      if (j.nchild >= MAX_CHILD) not_impl("join tree node with too many children");
+      const auto &eq = g.eqs[nb.second];
+      int mycol = eq.first.leaf == v ? eq.first.col : eq.second.col;
+      j.cols[j.nchild] = view_of(data[v].data->cols[mycol]);
+      j.child[j.nchild] = msg[nb.first].m;
+      j.nchild++;
+    }
+    const int64_t n = data[v].data->nrows;
+    if (parent >= 0) {
+      const auto &eq = g.eqs[via_eq];
+      int mycol = eq.first.leaf == v ? eq.first.col : eq.second.col;
+      int pcol = eq.first.leaf == v ? eq.second.col : eq.first.col;
+      const ColPtr &mykey = data[v].data->cols[mycol];
+      // leaf without children whose key is a dense unique id range: all ones
+      if (j.nchild == 0 && data[v].plain) {
+        const ColStats &st = column_stats(s, mykey);
+        if (st.dense_unique && st.non_null == n) {
+          msg[v] = ones_map(st.min, st.max);
+          return;
+        }
+      }
+      msg[v] = new_map_for(s, data[parent].data->cols[pcol], n);
+      j.cols[j.nchild] = view_of(mykey);
+      j.has_parent = 1;
+      j.out = msg[v].m;
+    }
+    if (n == 0) return;
+    HIP_CHECK(hipMemcpyAsync(job_buf->p, &j, sizeof(j), hipMemcpyHostToDevice, s->stream));
+    {
+      KernelTimer kt(s, "message_pass", 8.0 * n * (j.nchild + j.has_parent));
+      hipLaunchKernelGGL(k_message, dim3(grid_for(n, 256)), dim3(256), 0, s->stream,
+                         (const MsgJob *)job_buf->p, n, (unsigned long long *)acc->p);
+      KERNEL_CHECK();
+    }
+    s->sync();  // job_buf is reused by the next message
+  };
+  visit(root, -1, -1);
+  HIP_CHECK(hipMemcpyAsync(s->h_scalars, acc->p, 8, hipMemcpyDeviceToHost, s->stream));
+  s->sync();
+  *out = (uint64_t)s->h_scalars[0];
+  return true;
+}
+
+// Union-find merge of leaves for one inclusion–exclusion term.
+static bool apply_equalities(const JoinGraph &g, const std::vector<int> &subset, JoinGraph &out) {
+  const int L = (int)g.leaves.size();
+  std::vector<int> rep(L);
+  std::iota(rep.begin(), rep.end(), 0);
+  std::function<int(int)> find = [&](int x) { return rep[x] == x ? x : rep[x] = find(rep[x]); };
+  std::vector<std::pair<int, int>> intra_by_leaf;  // (leaf, col a, col b) gathered below
+  std::vector<std::tuple<int, int, int>> intra;
+  for (int k : subset) {
+    ColRef a = g.neqs[k].first, b = g.neqs[k].second;
+    if (a.leaf == b.leaf) {
+      if (a.col == b.col) continue;  // x = x: always true
+      intra.emplace_back(a.leaf, a.col, b.col);
+      continue;
+    }
+    // merging two scans requires the same base data and a unique id column
+    const Leaf &la = g.leaves[a.leaf], &lb = g.leaves[b.leaf];
+    if (la.node != lb.node || !la.filters.empty() || !lb.filters.empty() || a.col != b.col)
+      return false;
+    DataPtr d = materialize(la.node);
+    const ColStats &st = column_stats(la.node->s, d->cols[a.col]);
+    if (!(st.dense_unique && st.non_null == d->nrows)) {
+      // uniqueness of a non-dense id column: verify by grouping
+      Grouping gr = group_rows(la.node->s, *d, {a.col});
+      if (gr.ngroups != d->nrows) return false;
+    }
+    int ra = find(a.leaf), rb = find(b.leaf);
+    if (ra != rb) rep[rb] = ra;
+  }
+  // new leaves
+  std::vector<int> newid(L, -1);
+  out = JoinGraph();
+  for (int i = 0; i < L; ++i)
+    if (find(i) == i) {
+      newid[i] = (int)out.leaves.size();
+      out.leaves.push_back(g.leaves[i]);
+    }
+  for (auto &t : intra) out.leaves[newid[find(std::get<0>(t))]].col_eqs.emplace_back(std::get<1>(t), std::get<2>(t));
+  // re-express equalities; same-leaf equalities become intra-row predicates,
+  // parallel edges sharing one side collapse (x=y ∧ x'=y → x=x' intra-row)
+  for (auto &e : g.eqs) {
+    ColRef a{newid[find(e.first.leaf)], e.first.col};
+    ColRef b{newid[find(e.second.leaf)], e.second.col};
+    if (a.leaf == b.leaf) {
+      if (a.col != b.col) out.leaves[a.leaf].col_eqs.emplace_back(a.col, b.col);
+      continue;
+    }
+    bool merged = false;
+    for (auto &f : out.eqs) {
+      ColRef &x = f.first, &y = f.second;
+      ColRef xa = x.leaf == a.leaf ? x : y, yb = x.leaf == a.leaf ? y : x;
+      bool same_pair = (x.leaf == a.leaf && y.leaf == b.leaf) || (x.leaf == b.leaf && y.leaf == a.leaf);
+      if (!same_pair) continue;
+      if (xa.col == a.col && yb.col == b.col) { merged = true; break; }  // duplicate
+      if (yb.col == b.col) {
+        out.leaves[a.leaf].col_eqs.emplace_back(xa.col, a.col);
+        merged = true;
+        break;
+      }
+      if (xa.col == a.col) {
+        out.leaves[b.leaf].col_eqs.emplace_back(yb.col, b.col);
+        merged = true;
+        break;
+      }
+      return false;  // genuine two-key join: not a tree
+    }
+    if (!merged) out.eqs.emplace_back(a, b);
+  }
+  return true;
+}
+
+// ------------------------------------------------------------ 2-hop matcher
+struct Chain2 {
+  int ra, rb;        // the two rel leaves (same base node)
+  int sa, sb, sc;    // node leaves
+  int u1, v1, u2, v2;
+  int ya, yb, yc;    // node id columns
+};
+
+static bool match_chain2(const JoinGraph &g, Chain2 &c) {
+  if (g.leaves.size() != 5 || g.eqs.size() != 4 || g.neqs.size() != 1) return false;
+  ColRef x = g.neqs[0].first, y = g.neqs[0].second;
+  if (x.leaf == y.leaf || x.col != y.col) return false;
+  const Leaf &lx = g.leaves[x.leaf], &ly = g.leaves[y.leaf];
+  if (lx.node != ly.node || !lx.filters.empty() || !ly.filters.empty()) return false;
+  // each rel leaf joins exactly two eqs; find its neighbours
+  auto edges_of = [&](int leaf) {
+    std::vector<std::pair<int, ColRef>> r;  // (my col, other)
+    for (auto &e : g.eqs) {
+      if (e.first.leaf == leaf) r.emplace_back(e.first.col, e.second);
+      if (e.second.leaf == leaf) r.emplace_back(e.second.col, e.first);
+    }
+    return r;
+  };
+  auto e1 = edges_of(x.leaf), e2 = edges_of(y.leaf);
+  if (e1.size() != 2 || e2.size() != 2) return false;
+  // the shared node leaf S_b is the one adjacent to both
+  for (int i = 0; i < 2; ++i)
+    for (int k = 0; k < 2; ++k) {
+      if (e1[i].second.leaf != e2[k].second.leaf) continue;
+      if (e1[i].second.col != e2[k].second.col) continue;
+      const auto &to_a = e1[1 - i], &to_c = e2[1 - k];
+      int sa = to_a.second.leaf, sb = e1[i].second.leaf, sc = to_c.second.leaf;
+      if (sa == sb || sc == sb || sa == x.leaf || sc == y.leaf) return false;
+      std::set<int> all{x.leaf, y.leaf, sa, sb, sc};
+      if (all.size() != 5) return false;
+      for (int nl : {sa, sb, sc})
+        if (edges_of(nl).size() != 1 || !g.leaves[nl].col_eqs.empty()) return false;
+      c.ra = x.leaf;
+      c.rb = y.leaf;
+      c.sa = sa;
+      c.sb = sb;
+      c.sc = sc;
+      c.u1 = to_a.first;
+      c.v1 = e1[i].first;
+      c.u2 = e2[k].first;
+      c.v2 = to_c.first;
+      c.ya = to_a.second.col;
+      c.yb = e1[i].second.col;
+      c.yc = to_c.second.col;
+      return true;
+    }
+  return false;
+}
+
+struct NodeWeights {
+  HostMap map;
+  bool ones = false;
+  BufPtr cnt;
+};
+
+// Per-id weights of a node leaf: MAP_ONES for a dense unique id range,
+// otherwise a uint32 count array over [min, max] (returns false if sparse).
+static bool node_weights(Session *s, const LeafData &ld, int col, NodeWeights &w) {
+  const ColPtr &c = ld.data->cols[col];
+  if (c->type != Type::Int64) return false;
+  const ColStats &st = column_stats(s, c);
+  if (st.non_null == 0) {
+    w.map = ones_map(1, 0);
+    w.ones = true;
+    return true;
+  }
+  if (st.dense_unique && st.non_null == c->n) {
+    w.map = ones_map(st.min, st.max);
+    w.ones = true;
+    return true;
+  }
+  uint64_t range = (uint64_t)(st.max - st.min) + 1;
+  if (range > (uint64_t(1) << 31) || range > 64 * (uint64_t)std::max<int64_t>(c->n, 1024))
+    return false;
+  w.cnt = s->alloc(4 * range);
+  HIP_CHECK(hipMemsetAsync(w.cnt->p, 0, 4 * range, s->stream));
+  hipLaunchKernelGGL(k_count_ids, dim3(grid_for(c->n, 256)), dim3(256), 0, s->stream,
+                     (const int64_t *)c->data->p, c->valid ? (const uint8_t *)c->valid->p : nullptr,
+                     c->n, st.min, st.max, (uint32_t *)w.cnt->p);
+  KERNEL_CHECK();
+  memset(&w.map.m, 0, sizeof(w.map.m));
+  w.map.m.kind = MAP_DENSE32;
+  w.map.m.lo = st.min;
+  w.map.m.hi = st.max;
+  w.map.m.vals = (unsigned long long *)w.cnt->p;
+  w.ones = false;
+  return true;
+}
+
+static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t *out) {
+  LeafData rel = leaf_data(g.leaves[c.ra]);
+  LeafData na = leaf_data(g.leaves[c.sa]), nb = leaf_data(g.leaves[c.sb]),
+           nc = leaf_data(g.leaves[c.sc]);
+  const Data &R = *rel.data;
+  for (int col : {c.u1, c.v1, c.u2, c.v2})
+    if (R.cols[col]->type != Type::Int64 || R.cols[col]->valid) return false;
+  NodeWeights wa, wb, wc;
+  if (!node_weights(s, na, c.ya, wa) || !node_weights(s, nb, c.yb, wb) ||
+      !node_weights(s, nc, c.yc, wc))
+    return false;
+  const int64_t lo = wb.map.m.lo, hi = wb.map.m.hi;
+  const int64_t len = hi >= lo ? hi - lo + 1 : 0;
+  const int64_t n = R.nrows;
+  if (len > (int64_t(1) << 31)) return false;
+  // per-bin counts must fit uint32: rels × max node multiplicity
+  if (!(wa.ones && wc.ones) && n >= (int64_t(1) << 26)) return false;
+  if (n >= (int64_t(1) << 32)) return false;
+  const bool all_ones = wa.ones && wb.ones && wc.ones;
+
+  BufPtr h = s->alloc(8 * std::max<int64_t>(len, 1) + 64);
+  BufPtr acc = s->alloc(16);
+  HIP_CHECK(hipMemsetAsync(acc->p, 0, 16, s->stream));
+  uint32_t *h1 = (uint32_t *)h->p;
+  uint32_t *h2 = h1 + ((len + 15) & ~int64_t(15));  // keep dwordx4 alignment
+  if (len > 0) {
+    HIP_CHECK(hipMemsetAsync(h->p, 0, 8 * std::max<int64_t>(len, 1) + 64, s->stream));
+    Chain2Args a;
+    a.u1 = (const int64_t *)R.cols[c.u1]->data->p;
+    a.v1 = (const int64_t *)R.cols[c.v1]->data->p;
+    a.u2 = (const int64_t *)R.cols[c.u2]->data->p;
+    a.v2 = (const int64_t *)R.cols[c.v2]->data->p;
+    a.n = n;
+    a.wa = wa.map.m;
+    a.wb = wb.map.m;
+    a.wc = wc.map.m;
+    a.lo = lo;
+    a.hi = hi;
+    a.h1 = h1;
+    a.h2 = h2;
+    a.loops = (unsigned long long *)acc->p + 1;
+    if (n > 0) {
+      KernelTimer kt(s, "chain2_hist", 16.0 * n);
+      unsigned grid = grid_for(n, 256, 256 * 32);
+      if (all_ones)
+        hipLaunchKernelGGL(k_chain2_hist<true>, dim3(grid), dim3(256), 0, s->stream, a);
+      else
+        hipLaunchKernelGGL(k_chain2_hist<false>, dim3(grid), dim3(256), 0, s->stream, a);
+      KERNEL_CHECK();
+    }
+    {
+      KernelTimer kt(s, "chain2_dot", 8.0 * len);
+      unsigned grid = grid_for(len / 4 + 1, 256, 256 * 8);
+      if (wb.ones)
+        hipLaunchKernelGGL(k_chain2_dot<true>, dim3(grid), dim3(256), 0, s->stream, h1, h2,
+                           wb.map.m, lo, len, (unsigned long long *)acc->p);
+      else
+        hipLaunchKernelGGL(k_chain2_dot<false>, dim3(grid), dim3(256), 0, s->stream, h1, h2,
+                           wb.map.m, lo, len, (unsigned long long *)acc->p);
+      KERNEL_CHECK();
+    }
+  }
+  HIP_CHECK(hipMemcpyAsync(s->h_scalars, acc->p, 16, hipMemcpyDeviceToHost, s->stream));
+  s->sync();
+  uint64_t total = (uint64_t)s->h_scalars[0], loops = (uint64_t)s->h_scalars[1];
+  *out = total - loops;
+  return true;
+}
+
+bool try_fused_count(const NodePtr &n, int64_t *out) {
+  Session *s = n->s;
+  {
+    std::lock_guard<std::mutex> lk(n->mu);
+    if (n->result) return false;
+  }
+  if (n->kind != Kind::Join && n->kind != Kind::Filter && n->kind != Kind::Select) return false;
+  JoinGraph g;
+  std::vector<ColRef> cols;
+  if (!collect(n, g, cols)) return false;
+  if (g.eqs.empty()) return false;  // no join: nothing to fuse
+  if (g.neqs.size() > 4) return false;
+  Chain2 c2;
+  if (match_chain2(g, c2)) {
+    uint64_t r;
+    if (run_chain2(s, g, c2, &r)) {
+      s->last_plan = "fused_chain2";
+      *out = (int64_t)r;
+      return true;
+    }
+  }
+  // general: inclusion–exclusion over the uniqueness predicates
+  const int k = (int)g.neqs.size();
+  int64_t total = 0;
+  for (int mask = 0; mask < (1 << k); ++mask) {
+    std::vector<int> subset;
+    for (int b = 0; b < k; ++b)
+      if (mask >> b & 1) subset.push_back(b);
+    JoinGraph t;
+    if (!apply_equalities(g, subset, t)) return false;
+    uint64_t cnt;
+    if (!tree_count(s, t, &cnt)) return false;
+    total += (subset.size() % 2 ? -1 : 1) * (int64_t)cnt;
+  }
+  s->last_plan = "message_passing";
+  *out = total;
+  return true;
+}
+
+}  // namespace capf
+
+// ===================================================================== C-ABI
+using namespace capf;
+
+extern "C" capf_status capf_chain2_local_hists(capf_session *cs, capf_table *rels,
+                                               const char *src_col, const char *dst_col,
+                                               int64_t node_base, int64_t n_nodes,
+                                               uint32_t *d_in_hist, uint32_t *d_out_hist,
+                                               int64_t *self_loops) {
+  try {
+    if (!cs || !rels || !src_col || !dst_col || !d_in_hist || !d_out_hist || !self_loops)
+      illegal("null argument");
+    if (n_nodes < 0) illegal("negative node count");
+    Session *s = &cs->impl;
+    const NodePtr &nd = rels->node;
+    int si = nd->col_index_or_throw(src_col), di = nd->col_index_or_throw(dst_col);
+    DataPtr d = materialize(nd);
+    const ColPtr &src = d->cols[si], &dst = d->cols[di];
+    if (src->type != Type::Int64 || dst->type != Type::Int64 || src->valid || dst->valid)
+      illegal("chain2_local_hists needs non-null INTEGER endpoint columns");
+    if (d->nrows >= (int64_t(1) << 32)) not_impl("more than 2^32 rels per rank");
+    HIP_CHECK(hipMemsetAsync(d_in_hist, 0, 4 * n_nodes, s->stream));
+    HIP_CHECK(hipMemsetAsync(d_out_hist, 0, 4 * n_nodes, s->stream));
+    BufPtr acc = s->alloc(16);
+    HIP_CHECK(hipMemsetAsync(acc->p, 0, 16, s->stream));
+    Chain2Args a;
+    a.u1 = a.u2 = (const int64_t *)src->data->p;
+    a.v1 = a.v2 = (const int64_t *)dst->data->p;
+    a.n = d->nrows;
+    a.wa = a.wb = a.wc = ones_map(node_base, node_base + n_nodes - 1).m;
+    a.lo = node_base;
+    a.hi = node_base + n_nodes - 1;
+    a.h1 = d_in_hist;
+    a.h2 = d_out_hist;
+    a.loops = (unsigned long long *)acc->p + 1;
+    if (a.n > 0 && n_nodes > 0) {
+      KernelTimer kt(s, "chain2_hist", 16.0 * a.n);
+      hipLaunchKernelGGL(k_chain2_hist<true>, dim3(grid_for(a.n, 256, 256 * 32)), dim3(256), 0,
+                         s->stream, a);
+      KERNEL_CHECK();
+    }
+    HIP_CHECK(hipMemcpyAsync(s->h_scalars, acc->p, 16, hipMemcpyDeviceToHost, s->stream));
+    s->sync();
+    *self_loops = s->h_scalars[1];
+    return CAPF_OK;
+  } catch (const capf::Error &e) {
+    return record_error(e.code, e.what());
+  }
+}
+
+extern "C" capf_status capf_dot_u32(capf_session *cs, const uint32_t *d_a, const uint32_t *d_b,
+                                    int64_t n, uint64_t *out) {
+  try {
+    if (!cs || !d_a || !d_b || !out) illegal("null argument");
+    Session *s = &cs->impl;
+    BufPtr acc = s->alloc(8);
+    HIP_CHECK(hipMemsetAsync(acc->p, 0, 8, s->stream));
+    if (n > 0) {
+      if (((uintptr_t)d_a | (uintptr_t)d_b) & 15) illegal("dot operands must be 16-B aligned");
+      KernelTimer kt(s, "chain2_dot", 8.0 * n);
+      hipLaunchKernelGGL(k_chain2_dot<true>, dim3(grid_for(n / 4 + 1, 256, 256 * 8)), dim3(256),
+                         0, s->stream, d_a, d_b, ones_map(0, n - 1).m, (int64_t)0, n,
+                         (unsigned long long *)acc->p);
+      KERNEL_CHECK();
+    }
+    HIP_CHECK(hipMemcpyAsync(s->h_scalars, acc->p, 8, hipMemcpyDeviceToHost, s->stream));
+    s->sync();
+    *out = (uint64_t)s->h_scalars[0];
+    return CAPF_OK;
+  } catch (const capf::Error &e) {
+    return record_error(e.code, e.what());
+  }
+}

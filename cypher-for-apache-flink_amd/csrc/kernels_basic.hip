@@ -1,0 +1,609 @@
+// kernels_basic.hip — scans, compaction, gathers and the per-row expression
+// interpreter behind Table.filter / withColumns / orderBy keys.
+//
+// Expression semantics follow FlinkSQLExprMapper
+// (flink-cypher/.../impl/FlinkSQLExprMapper.scala:48-294) with Cypher
+// three-valued logic: comparisons with NULL are NULL, Ands/Ors fold with
+// SQL semantics (FlinkSQLExprMapper.scala:87-88), filter keeps TRUE rows only
+// (FlinkTable.filter, FlinkTable.scala:76-78).
+#include <algorithm>
+
+#include "capf_internal.h"
+#include "device_common.h"
+
+namespace capf {
+
+// ------------------------------------------------------------------ scan
+constexpr int SCAN_BLOCK = 256;
+constexpr int SCAN_ITEMS = 8;
+constexpr int SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_tiles(const int64_t *in, int64_t *out,
+                                                           int64_t *tile_sums, int64_t n) {
+  __shared__ int64_t lds[17];
+  int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
+  int64_t v[SCAN_ITEMS];
+  int64_t local = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    v[k] = base + k < n ? in[base + k] : 0;
+    local += v[k];
+  }
+  int64_t total;
+  int64_t ex = block_exclusive_scan(local, lds, total);
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    if (base + k < n) out[base + k] = ex;
+    ex += v[k];
+  }
+  if (threadIdx.x == 0) tile_sums[blockIdx.x] = total;
+}
+
+__global__ void k_add_tile_offsets(int64_t *out, const int64_t *tile_off, int64_t n) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] += tile_off[i / SCAN_TILE];
+}
+
+static void scan_rec(Session *s, const int64_t *in, int64_t *out, int64_t n, int64_t *total_dev) {
+  int64_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+  BufPtr sums = s->alloc(sizeof(int64_t) * (tiles + 1));
+  hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, s->stream, in,
+                     out, (int64_t *)sums->p, n);
+  KERNEL_CHECK();
+  if (tiles == 1) {
+    HIP_CHECK(hipMemcpyAsync(total_dev, sums->p, 8, hipMemcpyDeviceToDevice, s->stream));
+    return;
+  }
+  BufPtr offs = s->alloc(sizeof(int64_t) * tiles);
+  scan_rec(s, (const int64_t *)sums->p, (int64_t *)offs->p, tiles, total_dev);
+  hipLaunchKernelGGL(k_add_tile_offsets, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     s->stream, out, (const int64_t *)offs->p, n);
+  KERNEL_CHECK();
+}
+
+int64_t exclusive_scan_i64(Session *s, const int64_t *d_in, int64_t *d_out, int64_t n) {
+  if (n <= 0) return 0;
+  scan_rec(s, d_in, d_out, n, s->d_scalars);
+  HIP_CHECK(hipMemcpyAsync(s->h_scalars, s->d_scalars, 8, hipMemcpyDeviceToHost, s->stream));
+  s->sync();
+  return s->h_scalars[0];
+}
+
+// ------------------------------------------------------------ compaction
+__global__ __launch_bounds__(SCAN_BLOCK) void k_count_flags(const uint8_t *flags, int64_t n,
+                                                            int64_t *tile_counts) {
+  __shared__ int64_t lds[17];
+  int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
+  int64_t c = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) c += (base + k < n && flags[base + k]) ? 1 : 0;
+  int64_t r = block_reduce_sum(c, lds);
+  if (threadIdx.x == 0) tile_counts[blockIdx.x] = r;
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scatter_flags(const uint8_t *flags, int64_t n,
+                                                              const int64_t *tile_off,
+                                                              int64_t *out) {
+  __shared__ int64_t lds[17];
+  int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
+  uint8_t f[SCAN_ITEMS];
+  int64_t c = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    f[k] = (base + k < n) ? flags[base + k] : 0;
+    c += f[k] ? 1 : 0;
+  }
+  int64_t total;
+  int64_t pos = block_exclusive_scan(c, lds, total) + tile_off[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k)
+    if (f[k]) out[pos++] = base + k;
+}
+
+BufPtr compact_flags(Session *s, const uint8_t *d_flags, int64_t n, int64_t *out_count) {
+  if (n == 0) {
+    *out_count = 0;
+    return s->alloc(0);
+  }
+  int64_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+  BufPtr counts = s->alloc(8 * tiles), offs = s->alloc(8 * tiles);
+  hipLaunchKernelGGL(k_count_flags, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, s->stream,
+                     d_flags, n, (int64_t *)counts->p);
+  KERNEL_CHECK();
+  int64_t total = exclusive_scan_i64(s, (const int64_t *)counts->p, (int64_t *)offs->p, tiles);
+  BufPtr idx = s->alloc(8 * std::max<int64_t>(total, 1));
+  hipLaunchKernelGGL(k_scatter_flags, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, s->stream,
+                     d_flags, n, (const int64_t *)offs->p, (int64_t *)idx->p);
+  KERNEL_CHECK();
+  *out_count = total;
+  return idx;
+}
+
+// ------------------------------------------------------------ index helpers
+__global__ void k_iota(int64_t *out, int64_t start, int64_t m) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = start + i;
+}
+
+BufPtr iota_index(Session *s, int64_t start, int64_t m) {
+  BufPtr b = s->alloc(8 * std::max<int64_t>(m, 1));
+  if (m > 0) {
+    hipLaunchKernelGGL(k_iota, dim3(grid_for(m, 256)), dim3(256), 0, s->stream, (int64_t *)b->p,
+                       start, m);
+    KERNEL_CHECK();
+  }
+  return b;
+}
+
+__global__ void k_cross(int64_t *li, int64_t *ri, int64_t nr, int64_t m) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    li[i] = i / nr;
+    ri[i] = i % nr;
+  }
+}
+
+void cross_index(Session *s, int64_t nl, int64_t nr, BufPtr &li, BufPtr &ri) {
+  int64_t m = nl * nr;
+  li = s->alloc(8 * std::max<int64_t>(m, 1));
+  ri = s->alloc(8 * std::max<int64_t>(m, 1));
+  if (m > 0) {
+    hipLaunchKernelGGL(k_cross, dim3(grid_for(m, 256)), dim3(256), 0, s->stream,
+                       (int64_t *)li->p, (int64_t *)ri->p, nr, m);
+    KERNEL_CHECK();
+  }
+}
+
+// ------------------------------------------------------------ gather / concat
+template <typename T>
+__global__ void k_gather(const T *src, const uint8_t *sval, const int64_t *idx, T *dst,
+                         uint8_t *dval, int64_t m) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t j = idx[i];
+    bool ok = j >= 0;
+    if (dst) dst[i] = ok ? src[j] : T(0);
+    if (dval) dval[i] = ok ? (sval ? sval[j] : 1) : 0;
+  }
+}
+
+ColPtr gather_column(Session *s, const ColPtr &c, const int64_t *d_idx, int64_t m,
+                     bool idx_may_be_null) {
+  if (!d_idx) {
+    if (m == c->n) return c;
+    illegal("internal: identity gather with mismatched length");
+  }
+  if (c->type == Type::Null) return null_column(s, Type::Null, m);
+  bool with_valid = c->valid != nullptr || idx_may_be_null;
+  ColPtr o = make_column(s, c->type, m, with_valid);
+  if (m == 0) return o;
+  const uint8_t *sval = c->valid ? (const uint8_t *)c->valid->p : nullptr;
+  uint8_t *dval = o->valid ? (uint8_t *)o->valid->p : nullptr;
+  unsigned g = grid_for(m, 256);
+  if (c->type == Type::Bool)
+    hipLaunchKernelGGL(k_gather<uint8_t>, dim3(g), dim3(256), 0, s->stream,
+                       (const uint8_t *)c->data->p, sval, d_idx, (uint8_t *)o->data->p, dval, m);
+  else
+    hipLaunchKernelGGL(k_gather<int64_t>, dim3(g), dim3(256), 0, s->stream,
+                       (const int64_t *)c->data->p, sval, d_idx, (int64_t *)o->data->p, dval, m);
+  KERNEL_CHECK();
+  return o;
+}
+
+template <typename T>
+__global__ void k_copy_part(const T *src, const uint8_t *sval, T *dst, uint8_t *dval, int64_t n,
+                            int64_t off) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (dst) dst[off + i] = src ? src[i] : T(0);
+    if (dval) dval[off + i] = src ? (sval ? sval[i] : 1) : 0;
+  }
+}
+
+ColPtr concat_columns(Session *s, const ColPtr &a, const ColPtr &b, Type t) {
+  int64_t m = a->n + b->n;
+  if (t == Type::Null) return null_column(s, t, m);
+  bool with_valid = a->valid || b->valid || a->type == Type::Null || b->type == Type::Null;
+  ColPtr o = make_column(s, t, m, with_valid);
+  uint8_t *dval = o->valid ? (uint8_t *)o->valid->p : nullptr;
+  int64_t off = 0;
+  for (const ColPtr &c : {a, b}) {
+    if (c->n > 0) {
+      const void *src = c->type == Type::Null ? nullptr : c->data->p;
+      const uint8_t *sval = c->valid ? (const uint8_t *)c->valid->p : nullptr;
+      unsigned g = grid_for(c->n, 256);
+      if (t == Type::Bool)
+        hipLaunchKernelGGL(k_copy_part<uint8_t>, dim3(g), dim3(256), 0, s->stream,
+                           (const uint8_t *)src, sval, (uint8_t *)o->data->p, dval, c->n, off);
+      else
+        hipLaunchKernelGGL(k_copy_part<int64_t>, dim3(g), dim3(256), 0, s->stream,
+                           (const int64_t *)src, sval, (int64_t *)o->data->p, dval, c->n, off);
+      KERNEL_CHECK();
+    }
+    off += c->n;
+  }
+  return o;
+}
+
+// ------------------------------------------------------------ statistics
+__global__ void k_minmax(const int64_t *v, const uint8_t *valid, int64_t n, int64_t *acc) {
+  int64_t mn = INT64_MAX, mx = INT64_MIN, cnt = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (valid && !valid[i]) continue;
+    int64_t x = v[i];
+    mn = x < mn ? x : mn;
+    mx = x > mx ? x : mx;
+    ++cnt;
+  }
+#pragma unroll
+  for (int d = WAVE / 2; d > 0; d >>= 1) {
+    int64_t a = __shfl_xor(mn, d, WAVE), b = __shfl_xor(mx, d, WAVE);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+    cnt += __shfl_xor(cnt, d, WAVE);
+  }
+  if (lane_id() == 0) {
+    atomicMin((long long *)&acc[0], (long long)mn);
+    atomicMax((long long *)&acc[1], (long long)mx);
+    atomicAdd((unsigned long long *)&acc[2], (unsigned long long)cnt);
+  }
+}
+
+__global__ void k_dup_check(const int64_t *v, const uint8_t *valid, int64_t n, int64_t base,
+                            uint32_t *bits, int64_t *dup) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (valid && !valid[i]) continue;
+    uint64_t k = (uint64_t)(v[i] - base);
+    uint32_t m = 1u << (k & 31);
+    uint32_t old = atomicOr(&bits[k >> 5], m);
+    if (old & m) *dup = 1;
+  }
+}
+
+ColStats compute_stats(Session *s, const Column &c) {
+  ColStats st;
+  if (c.type != Type::Int64 && c.type != Type::String) {
+    st.non_null = c.type == Type::Null ? 0 : c.n;
+    return st;
+  }
+  if (c.n == 0) return st;
+  int64_t init[3] = {INT64_MAX, INT64_MIN, 0};
+  HIP_CHECK(hipMemcpyAsync(s->d_scalars, init, sizeof(init), hipMemcpyHostToDevice, s->stream));
+  hipLaunchKernelGGL(k_minmax, dim3(grid_for(c.n, 256, 1024)), dim3(256), 0, s->stream,
+                     (const int64_t *)c.data->p, c.valid ? (const uint8_t *)c.valid->p : nullptr,
+                     c.n, s->d_scalars);
+  KERNEL_CHECK();
+  HIP_CHECK(hipMemcpyAsync(s->h_scalars, s->d_scalars, sizeof(init), hipMemcpyDeviceToHost, s->stream));
+  s->sync();
+  st.min = s->h_scalars[0];
+  st.max = s->h_scalars[1];
+  st.non_null = s->h_scalars[2];
+  if (st.non_null > 0 && (uint64_t)(st.max - st.min) + 1 == (uint64_t)st.non_null &&
+      st.non_null <= (int64_t(1) << 34)) {
+    int64_t words = (st.non_null + 31) / 32;
+    BufPtr bits = s->alloc(4 * words);
+    HIP_CHECK(hipMemsetAsync(bits->p, 0, 4 * words, s->stream));
+    HIP_CHECK(hipMemsetAsync(s->d_scalars + 3, 0, 8, s->stream));
+    hipLaunchKernelGGL(k_dup_check, dim3(grid_for(c.n, 256, 4096)), dim3(256), 0, s->stream,
+                       (const int64_t *)c.data->p,
+                       c.valid ? (const uint8_t *)c.valid->p : nullptr, c.n, st.min,
+                       (uint32_t *)bits->p, s->d_scalars + 3);
+    KERNEL_CHECK();
+    HIP_CHECK(hipMemcpyAsync(s->h_scalars + 3, s->d_scalars + 3, 8, hipMemcpyDeviceToHost, s->stream));
+    s->sync();
+    st.dense_unique = s->h_scalars[3] == 0;
+  }
+  return st;
+}
+
+// ------------------------------------------------------------ interpreter
+struct Val {
+  int64_t b;   // int64 value, bool (0/1), string code or double bits
+  int32_t t;   // capf type
+  int32_t nul; // 1 = NULL
+};
+
+__device__ inline double vf(const Val &v) {
+  return v.t == CAPF_TYPE_FLOAT64 ? __longlong_as_double(v.b) : (double)v.b;
+}
+__device__ inline Val mk(int64_t b, int32_t t, int32_t nul) {
+  Val v;
+  v.b = b;
+  v.t = t;
+  v.nul = nul;
+  return v;
+}
+__device__ inline Val mkf(double f) { return mk(__double_as_longlong(f), CAPF_TYPE_FLOAT64, 0); }
+__device__ inline Val mkb(bool x) { return mk(x ? 1 : 0, CAPF_TYPE_BOOL, 0); }
+__device__ inline Val mknull(int32_t t) { return mk(0, t, 1); }
+
+__device__ inline Val load_col(const ColView &c, int64_t r) {
+  if (c.type == CAPF_TYPE_NULL || !c.data) return mknull(CAPF_TYPE_NULL);
+  if (c.valid && !c.valid[r]) return mknull(c.type);
+  if (c.type == CAPF_TYPE_BOOL) return mk(((const uint8_t *)c.data)[r] ? 1 : 0, c.type, 0);
+  return mk(((const int64_t *)c.data)[r], c.type, 0);
+}
+
+// -1 less, 0 equal, 1 greater (non-null operands)
+__device__ inline int cmp_vals(const Val &a, const Val &b) {
+  if (a.t == CAPF_TYPE_FLOAT64 || b.t == CAPF_TYPE_FLOAT64) {
+    double x = vf(a), y = vf(b);
+    return x < y ? -1 : (x > y ? 1 : 0);
+  }
+  return a.b < b.b ? -1 : (a.b > b.b ? 1 : 0);
+}
+
+constexpr int MAX_STACK = 24;
+constexpr int MAX_LDS_CODE = 96;
+
+__device__ Val run_program(const Instr *code, int ncode, const ColView *cols, int64_t r) {
+  Val st[MAX_STACK];
+  int sp = 0;
+  for (int pc = 0; pc < ncode; ++pc) {
+    const Instr in = code[pc];
+    switch (in.op) {
+      case OP_COL: st[sp++] = load_col(cols[in.i], r); break;
+      case OP_LIT_INT: st[sp++] = mk(in.i, CAPF_TYPE_INT64, 0); break;
+      case OP_LIT_FLOAT: st[sp++] = mkf(in.f); break;
+      case OP_LIT_BOOL: st[sp++] = mkb(in.i != 0); break;
+      case OP_LIT_STRING: st[sp++] = mk(in.i, CAPF_TYPE_STRING, 0); break;
+      case OP_LIT_NULL: st[sp++] = mknull((int32_t)in.i); break;
+      case OP_EQ: case OP_NEQ: case OP_LT: case OP_LE: case OP_GT: case OP_GE: {
+        Val b = st[--sp], a = st[--sp];
+        if (a.nul || b.nul) {
+          st[sp++] = mknull(CAPF_TYPE_BOOL);
+          break;
+        }
+        int c = cmp_vals(a, b);
+        bool res;
+        switch (in.op) {
+          case OP_EQ: res = c == 0; break;
+          case OP_NEQ: res = c != 0; break;
+          case OP_LT: res = c < 0; break;
+          case OP_LE: res = c <= 0; break;
+          case OP_GT: res = c > 0; break;
+          default: res = c >= 0; break;
+        }
+        st[sp++] = mkb(res);
+        break;
+      }
+      case OP_NOT: {
+        Val a = st[--sp];
+        st[sp++] = a.nul ? mknull(CAPF_TYPE_BOOL) : mkb(a.b == 0);
+        break;
+      }
+      case OP_AND: case OP_OR: {
+        int k = (int)in.i;
+        bool any_dom = false, any_null = false;  // dominant = false for AND, true for OR
+        for (int j = 0; j < k; ++j) {
+          Val a = st[--sp];
+          if (a.nul)
+            any_null = true;
+          else if ((in.op == OP_AND) == (a.b == 0))
+            any_dom = true;
+        }
+        if (any_dom)
+          st[sp++] = mkb(in.op == OP_OR);
+        else if (any_null)
+          st[sp++] = mknull(CAPF_TYPE_BOOL);
+        else
+          st[sp++] = mkb(in.op == OP_AND);
+        break;
+      }
+      case OP_IS_NULL: {
+        Val a = st[--sp];
+        st[sp++] = mkb(a.nul != 0);
+        break;
+      }
+      case OP_IS_NOT_NULL: {
+        Val a = st[--sp];
+        st[sp++] = mkb(a.nul == 0);
+        break;
+      }
+      case OP_ADD: case OP_SUB: case OP_MUL: case OP_DIV: case OP_MOD: {
+        Val b = st[--sp], a = st[--sp];
+        bool fl = a.t == CAPF_TYPE_FLOAT64 || b.t == CAPF_TYPE_FLOAT64;
+        if (a.nul || b.nul) {
+          st[sp++] = mknull(fl ? CAPF_TYPE_FLOAT64 : CAPF_TYPE_INT64);
+          break;
+        }
+        if (fl) {
+          double x = vf(a), y = vf(b), z;
+          switch (in.op) {
+            case OP_ADD: z = x + y; break;
+            case OP_SUB: z = x - y; break;
+            case OP_MUL: z = x * y; break;
+            case OP_DIV: z = x / y; break;
+            default: z = fmod(x, y); break;
+          }
+          st[sp++] = mkf(z);
+        } else {
+          int64_t x = a.b, y = b.b, z = 0;
+          bool nul = false;
+          switch (in.op) {
+            case OP_ADD: z = (int64_t)((uint64_t)x + (uint64_t)y); break;
+            case OP_SUB: z = (int64_t)((uint64_t)x - (uint64_t)y); break;
+            case OP_MUL: z = (int64_t)((uint64_t)x * (uint64_t)y); break;
+            case OP_DIV:
+              if (y == 0) nul = true; else z = (y == -1) ? (int64_t)(0 - (uint64_t)x) : x / y;
+              break;
+            default:
+              if (y == 0) nul = true; else z = (y == -1) ? 0 : x % y;
+              break;
+          }
+          st[sp++] = mk(z, CAPF_TYPE_INT64, nul ? 1 : 0);
+        }
+        break;
+      }
+      case OP_NEG: {
+        Val a = st[--sp];
+        if (!a.nul) {
+          if (a.t == CAPF_TYPE_FLOAT64)
+            a = mkf(-vf(a));
+          else
+            a.b = (int64_t)(0 - (uint64_t)a.b);
+        }
+        st[sp++] = a;
+        break;
+      }
+      case OP_TO_FLOAT: {
+        Val a = st[--sp];
+        if (a.nul || a.t == CAPF_TYPE_BOOL)
+          st[sp++] = mknull(CAPF_TYPE_FLOAT64);
+        else
+          st[sp++] = mkf(vf(a));
+        break;
+      }
+      case OP_TO_INTEGER: {
+        // Flink lowers ToInteger to a cast to INT (32 bit),
+        // FlinkSQLExprMapper.scala:183.  Java (int) semantics.
+        Val a = st[--sp];
+        if (a.nul || a.t == CAPF_TYPE_BOOL) {
+          st[sp++] = mknull(CAPF_TYPE_INT64);
+        } else if (a.t == CAPF_TYPE_FLOAT64) {
+          double x = vf(a);
+          int32_t y;
+          if (x != x) y = 0;
+          else if (x >= 2147483647.0) y = 2147483647;
+          else if (x <= -2147483648.0) y = (-2147483647 - 1);
+          else y = (int32_t)x;
+          st[sp++] = mk((int64_t)y, CAPF_TYPE_INT64, 0);
+        } else {
+          st[sp++] = mk((int64_t)(int32_t)(uint32_t)(uint64_t)a.b, CAPF_TYPE_INT64, 0);
+        }
+        break;
+      }
+      case OP_COALESCE: {
+        int k = (int)in.i;
+        Val res = mknull(CAPF_TYPE_NULL);
+        // operands were pushed first..last; pick the first non-null
+        for (int j = 0; j < k; ++j) {
+          Val a = st[sp - k + j];
+          if (!a.nul) {
+            res = a;
+            break;
+          }
+        }
+        sp -= k;
+        st[sp++] = res;
+        break;
+      }
+      default: st[sp++] = mknull(CAPF_TYPE_NULL); break;
+    }
+  }
+  return st[0];
+}
+
+__global__ void k_eval(const Instr *code, int ncode, const ColView *cols, int ncols, int64_t n,
+                       void *out, uint8_t *out_valid, int32_t out_type, uint8_t *pred) {
+  __shared__ Instr s_code[MAX_LDS_CODE];
+  __shared__ ColView s_cols[32];
+  const bool lds_code = ncode <= MAX_LDS_CODE;
+  if (lds_code)
+    for (int i = threadIdx.x; i < ncode; i += blockDim.x) s_code[i] = code[i];
+  const bool lds_cols = ncols <= 32;
+  if (lds_cols)
+    for (int i = threadIdx.x; i < ncols; i += blockDim.x) s_cols[i] = cols[i];
+  __syncthreads();
+  const Instr *cp = lds_code ? s_code : code;
+  const ColView *cv = lds_cols ? s_cols : cols;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    Val v = run_program(cp, ncode, cv, r);
+    if (pred) {
+      pred[r] = (!v.nul && v.b != 0) ? 1 : 0;
+      continue;
+    }
+    if (out_valid) out_valid[r] = v.nul ? 0 : 1;
+    if (out_type == CAPF_TYPE_NULL) continue;
+    if (out_type == CAPF_TYPE_BOOL) {
+      ((uint8_t *)out)[r] = (!v.nul && v.b != 0) ? 1 : 0;
+    } else if (out_type == CAPF_TYPE_FLOAT64) {
+      ((double *)out)[r] = v.nul ? 0.0 : vf(v);
+    } else {
+      ((int64_t *)out)[r] = v.nul ? 0 : v.b;
+    }
+  }
+}
+
+struct DeviceProgram {
+  BufPtr code, cols;
+  int ncode, ncols;
+};
+
+static DeviceProgram upload_program(Session *s, const Program &p,
+                                    const std::vector<std::string> &names, const Data &d) {
+  DeviceProgram dp;
+  std::vector<ColView> views;
+  for (auto &nm : p.names) {
+    int idx = -1;
+    for (size_t k = 0; k < names.size(); ++k)
+      if (names[k] == nm) idx = (int)k;
+    if (idx < 0) illegal("expression references unknown column '" + nm + "'");
+    views.push_back(view_of(d.cols[idx]));
+  }
+  dp.ncode = (int)p.code.size();
+  dp.ncols = (int)views.size();
+  // stack depth check (host) — the device stack is fixed size
+  int depth = 0, maxd = 0;
+  for (auto &in : p.code) {
+    switch (in.op) {
+      case OP_COL: case OP_LIT_INT: case OP_LIT_FLOAT: case OP_LIT_BOOL: case OP_LIT_STRING:
+      case OP_LIT_NULL: depth++; break;
+      case OP_AND: case OP_OR: case OP_COALESCE: depth -= (int)in.i - 1; break;
+      case OP_NOT: case OP_IS_NULL: case OP_IS_NOT_NULL: case OP_NEG: case OP_TO_FLOAT:
+      case OP_TO_INTEGER: break;
+      default: depth -= 1; break;
+    }
+    maxd = std::max(maxd, depth);
+  }
+  if (maxd > MAX_STACK) not_impl("expression too deep for the GPU interpreter");
+  dp.code = s->alloc(sizeof(Instr) * p.code.size());
+  HIP_CHECK(hipMemcpyAsync(dp.code->p, p.code.data(), sizeof(Instr) * p.code.size(),
+                           hipMemcpyHostToDevice, s->stream));
+  dp.cols = s->alloc(sizeof(ColView) * std::max<size_t>(views.size(), 1));
+  if (!views.empty())
+    HIP_CHECK(hipMemcpyAsync(dp.cols->p, views.data(), sizeof(ColView) * views.size(),
+                             hipMemcpyHostToDevice, s->stream));
+  // pageable host sources: make sure the copies have consumed them
+  s->sync();
+  return dp;
+}
+
+ColPtr eval_program(Session *s, const Program &p, const std::vector<std::string> &names,
+                    const Data &d, Type out_type) {
+  int64_t n = d.nrows;
+  ColPtr o = make_column(s, out_type, n, true);
+  if (n == 0) return o;
+  DeviceProgram dp = upload_program(s, p, names, d);
+  hipLaunchKernelGGL(k_eval, dim3(grid_for(n, 256)), dim3(256), 0, s->stream,
+                     (const Instr *)dp.code->p, dp.ncode, (const ColView *)dp.cols->p, dp.ncols, n,
+                     o->data ? o->data->p : nullptr, (uint8_t *)o->valid->p, (int32_t)out_type,
+                     (uint8_t *)nullptr);
+  KERNEL_CHECK();
+  return o;
+}
+
+BufPtr eval_filter(Session *s, const Program &p, const std::vector<std::string> &names,
+                   const Data &d, int64_t *out_count) {
+  int64_t n = d.nrows;
+  if (n == 0) {
+    *out_count = 0;
+    return s->alloc(0);
+  }
+  DeviceProgram dp = upload_program(s, p, names, d);
+  BufPtr flags = s->alloc(n);
+  {
+    KernelTimer kt(s, "filter_eval", (double)n);
+    hipLaunchKernelGGL(k_eval, dim3(grid_for(n, 256)), dim3(256), 0, s->stream,
+                       (const Instr *)dp.code->p, dp.ncode, (const ColView *)dp.cols->p, dp.ncols,
+                       n, (void *)nullptr, (uint8_t *)nullptr, 0, (uint8_t *)flags->p);
+    KERNEL_CHECK();
+  }
+  return compact_flags(s, (const uint8_t *)flags->p, n, out_count);
+}
+
+}  // namespace capf

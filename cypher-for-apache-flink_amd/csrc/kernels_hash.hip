@@ -1,0 +1,591 @@
+// kernels_hash.hip — HBM-resident hash tables for the materialising operators:
+// equi-join (Table.join, FlinkTable.scala:171-187), DISTINCT
+// (FlinkTable.scala:189-196, with Spark's dropDuplicates(cols) semantics,
+// morpheus-spark-cypher/.../impl/table/SparkTable.scala:198-200) and GROUP BY
+// aggregation (FlinkTable.group, FlinkTable.scala:123-150; aggregators
+// FlinkSQLExprMapper.scala:281-287).  ORDER BY uses a stable radix sort.
+//
+// Open addressing with linear probing on uint32 row ids; key equality compares
+// the key columns (multi-column keys, NULL == NULL for grouping, NULL never
+// matches in a join — SQL semantics of the Flink `===` predicate).
+#include <cstring>
+#include <rocprim/rocprim.hpp>
+
+#include <algorithm>
+
+#include "capf_internal.h"
+#include "device_common.h"
+
+namespace capf {
+
+constexpr uint32_t EMPTY = 0xFFFFFFFFu;
+
+struct KeyViews {
+  const ColView *cols;  // device array of key column views
+  int n;
+};
+
+__device__ inline uint64_t key_word(const ColView &c, int64_t r, bool &isnull) {
+  if (c.type == CAPF_TYPE_NULL || !c.data || (c.valid && !c.valid[r])) {
+    isnull = true;
+    return 0;
+  }
+  isnull = false;
+  if (c.type == CAPF_TYPE_BOOL) return ((const uint8_t *)c.data)[r] ? 1 : 0;
+  uint64_t w = ((const uint64_t *)c.data)[r];
+  if (c.type == CAPF_TYPE_FLOAT64 && w == 0x8000000000000000ull) w = 0;  // -0.0 == 0.0
+  return w;
+}
+
+__device__ inline uint64_t hash_row(const ColView *cols, int n, int64_t r, bool &anynull) {
+  uint64_t h = 0x243F6A8885A308D3ull;
+  anynull = false;
+  for (int k = 0; k < n; ++k) {
+    bool nul;
+    uint64_t w = key_word(cols[k], r, nul);
+    anynull |= nul;
+    h = fmix64(h ^ (nul ? 0x9E3779B97F4A7C15ull : w) ^ ((uint64_t)k << 56)) + (nul ? 1 : 0);
+  }
+  return h;
+}
+
+__device__ inline bool rows_equal(const ColView *a, int64_t ra, const ColView *b, int64_t rb,
+                                  int n) {
+  for (int k = 0; k < n; ++k) {
+    bool na, nb;
+    uint64_t wa = key_word(a[k], ra, na), wb = key_word(b[k], rb, nb);
+    if (na != nb) return false;
+    if (!na && wa != wb) return false;
+  }
+  return true;
+}
+
+// Insert every row (skip_null: rows with a NULL key are not inserted and get
+// slot = EMPTY).  slot_min[slot] receives the smallest row id of the key, so
+// group representatives are deterministic.
+__global__ void k_ht_insert(const ColView *keys, int nkeys, int64_t n, uint32_t *slots,
+                            uint32_t *slot_min, uint64_t mask, uint32_t *slot_of_row,
+                            int skip_null) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    bool anynull;
+    uint64_t h = hash_row(keys, nkeys, r, anynull);
+    if (skip_null && anynull) {
+      slot_of_row[r] = EMPTY;
+      continue;
+    }
+    uint64_t slot = h & mask;
+    while (true) {
+      uint32_t cur = slots[slot];
+      if (cur == EMPTY) {
+        uint32_t old = atomicCAS(&slots[slot], EMPTY, (uint32_t)r);
+        if (old == EMPTY) break;
+        cur = old;
+      }
+      if (rows_equal(keys, cur, keys, r, nkeys)) break;
+      slot = (slot + 1) & mask;
+    }
+    atomicMin(&slot_min[slot], (uint32_t)r);
+    slot_of_row[r] = (uint32_t)slot;
+  }
+}
+
+__global__ void k_rep_flags(const uint32_t *slot_of_row, const uint32_t *slot_min, int64_t n,
+                            uint8_t *is_rep) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t sl = slot_of_row[r];
+    is_rep[r] = (sl != EMPTY && slot_min[sl] == (uint32_t)r) ? 1 : 0;
+  }
+}
+
+__global__ void k_slot_gid(const int64_t *reps, int64_t ngroups, const uint32_t *slot_of_row,
+                           int64_t *gid_of_slot) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ngroups;
+       g += (int64_t)gridDim.x * blockDim.x)
+    gid_of_slot[slot_of_row[reps[g]]] = g;
+}
+
+__global__ void k_row_gid(const uint32_t *slot_of_row, const int64_t *gid_of_slot, int64_t n,
+                          int64_t *gid) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t sl = slot_of_row[r];
+    gid[r] = sl == EMPTY ? -1 : gid_of_slot[sl];
+  }
+}
+
+static BufPtr upload_views(Session *s, const std::vector<ColView> &v) {
+  BufPtr b = s->alloc(sizeof(ColView) * std::max<size_t>(v.size(), 1));
+  if (!v.empty())
+    HIP_CHECK(hipMemcpyAsync(b->p, v.data(), sizeof(ColView) * v.size(), hipMemcpyHostToDevice,
+                             s->stream));
+  s->sync();
+  return b;
+}
+
+static uint64_t table_capacity(int64_t n) {
+  uint64_t cap = 1024;
+  while (cap < (uint64_t)n * 2) cap <<= 1;
+  return cap;
+}
+
+struct HashTable {
+  BufPtr slots, slot_min, slot_of_row;
+  uint64_t mask = 0;
+  BufPtr views;
+  int nkeys = 0;
+};
+
+static HashTable build_table(Session *s, const Data &d, const std::vector<int> &keys,
+                             bool skip_null) {
+  if (d.nrows >= (int64_t)EMPTY) not_impl("hash table over more than 2^32-1 rows");
+  HashTable ht;
+  std::vector<ColView> v;
+  for (int k : keys) v.push_back(view_of(d.cols[k]));
+  ht.views = upload_views(s, v);
+  ht.nkeys = (int)keys.size();
+  uint64_t cap = table_capacity(d.nrows);
+  ht.mask = cap - 1;
+  ht.slots = s->alloc(4 * cap);
+  ht.slot_min = s->alloc(4 * cap);
+  ht.slot_of_row = s->alloc(4 * std::max<int64_t>(d.nrows, 1));
+  HIP_CHECK(hipMemsetAsync(ht.slots->p, 0xFF, 4 * cap, s->stream));
+  HIP_CHECK(hipMemsetAsync(ht.slot_min->p, 0xFF, 4 * cap, s->stream));
+  if (d.nrows > 0) {
+    KernelTimer kt(s, "hash_build", 8.0 * d.nrows * keys.size());
+    hipLaunchKernelGGL(k_ht_insert, dim3(grid_for(d.nrows, 256)), dim3(256), 0, s->stream,
+                       (const ColView *)ht.views->p, ht.nkeys, d.nrows, (uint32_t *)ht.slots->p,
+                       (uint32_t *)ht.slot_min->p, ht.mask, (uint32_t *)ht.slot_of_row->p,
+                       skip_null ? 1 : 0);
+    KERNEL_CHECK();
+  }
+  return ht;
+}
+
+// Dense group ids (0..ngroups-1, ordered by smallest row of the group).
+static void dense_groups(Session *s, const HashTable &ht, int64_t n, Grouping &g) {
+  BufPtr flags = s->alloc(std::max<int64_t>(n, 1));
+  hipLaunchKernelGGL(k_rep_flags, dim3(grid_for(n, 256)), dim3(256), 0, s->stream,
+                     (const uint32_t *)ht.slot_of_row->p, (const uint32_t *)ht.slot_min->p, n,
+                     (uint8_t *)flags->p);
+  KERNEL_CHECK();
+  g.rep_row = compact_flags(s, (const uint8_t *)flags->p, n, &g.ngroups);
+  BufPtr gid_of_slot = s->alloc(8 * (ht.mask + 1));
+  if (g.ngroups > 0) {
+    hipLaunchKernelGGL(k_slot_gid, dim3(grid_for(g.ngroups, 256)), dim3(256), 0, s->stream,
+                       (const int64_t *)g.rep_row->p, g.ngroups,
+                       (const uint32_t *)ht.slot_of_row->p, (int64_t *)gid_of_slot->p);
+    KERNEL_CHECK();
+  }
+  g.group_of_row = s->alloc(8 * std::max<int64_t>(n, 1));
+  hipLaunchKernelGGL(k_row_gid, dim3(grid_for(n, 256)), dim3(256), 0, s->stream,
+                     (const uint32_t *)ht.slot_of_row->p, (const int64_t *)gid_of_slot->p, n,
+                     (int64_t *)g.group_of_row->p);
+  KERNEL_CHECK();
+}
+
+__global__ void k_fill_i64(int64_t *p, int64_t v, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+
+Grouping group_rows(Session *s, const Data &d, const std::vector<int> &keys) {
+  Grouping g;
+  int64_t n = d.nrows;
+  if (keys.empty()) {
+    g.ngroups = n > 0 ? 1 : 0;
+    g.group_of_row = s->alloc(8 * std::max<int64_t>(n, 1));
+    g.rep_row = s->alloc(8);
+    HIP_CHECK(hipMemsetAsync(g.rep_row->p, 0, 8, s->stream));
+    if (n > 0) {
+      hipLaunchKernelGGL(k_fill_i64, dim3(grid_for(n, 256)), dim3(256), 0, s->stream,
+                         (int64_t *)g.group_of_row->p, (int64_t)0, n);
+      KERNEL_CHECK();
+    }
+    return g;
+  }
+  if (n == 0) {
+    g.ngroups = 0;
+    g.group_of_row = s->alloc(8);
+    g.rep_row = s->alloc(8);
+    return g;
+  }
+  HashTable ht = build_table(s, d, keys, false);
+  dense_groups(s, ht, n, g);
+  return g;
+}
+
+// ------------------------------------------------------------------ join
+__global__ void k_count_group(const int64_t *gid, int64_t n, int64_t *cnt) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    int64_t g = gid[r];
+    if (g >= 0) atomicAdd((unsigned long long *)&cnt[g], 1ull);
+  }
+}
+
+__global__ void k_fill_csr(const int64_t *gid, int64_t n, const int64_t *off, int64_t *cursor,
+                           int64_t *csr) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    int64_t g = gid[r];
+    if (g < 0) continue;
+    int64_t p = (int64_t)atomicAdd((unsigned long long *)&cursor[g], 1ull);
+    csr[off[g] + p] = r;
+  }
+}
+
+// Probe: find the build-side group of each probe row (-1: none / NULL key).
+__global__ void k_probe(const ColView *pkeys, const ColView *bkeys, int nkeys, int64_t n,
+                        const uint32_t *slots, uint64_t mask, const uint32_t *slot_of_row_b,
+                        const int64_t *gid_of_row_b, const int64_t *gcnt, int64_t *pgid,
+                        int64_t *out_cnt, int outer) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    bool anynull;
+    uint64_t h = hash_row(pkeys, nkeys, r, anynull);
+    int64_t g = -1;
+    if (!anynull) {
+      uint64_t slot = h & mask;
+      while (true) {
+        uint32_t cur = slots[slot];
+        if (cur == EMPTY) break;
+        if (rows_equal(bkeys, cur, pkeys, r, nkeys)) {
+          g = gid_of_row_b[cur];
+          break;
+        }
+        slot = (slot + 1) & mask;
+      }
+    }
+    pgid[r] = g;
+    int64_t c = g >= 0 ? gcnt[g] : 0;
+    out_cnt[r] = (outer && c == 0) ? 1 : c;
+  }
+}
+
+__global__ void k_join_emit(const int64_t *pgid, const int64_t *out_off, int64_t n,
+                            const int64_t *goff, const int64_t *gcnt, const int64_t *csr,
+                            int64_t *lidx, int64_t *ridx, int outer, uint8_t *bmatched) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    int64_t g = pgid[r];
+    int64_t o = out_off[r];
+    if (g < 0) {
+      if (outer) {
+        lidx[o] = r;
+        ridx[o] = -1;
+      }
+      continue;
+    }
+    if (bmatched) bmatched[g] = 1;
+    int64_t c = gcnt[g], b = goff[g];
+    for (int64_t j = 0; j < c; ++j) {
+      lidx[o + j] = r;
+      ridx[o + j] = csr[b + j];
+    }
+  }
+}
+
+__global__ void k_unmatched(const int64_t *gid, const uint8_t *gmatched, int64_t n,
+                            uint8_t *flags) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    int64_t g = gid[r];
+    flags[r] = (g < 0 || !gmatched[g]) ? 1 : 0;
+  }
+}
+
+__global__ void k_append_unmatched(const int64_t *rows, int64_t m, int64_t off, int64_t *lidx,
+                                   int64_t *ridx) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    lidx[off + i] = -1;
+    ridx[off + i] = rows[i];
+  }
+}
+
+JoinPairs hash_join(Session *s, const Data &l, const Data &r,
+                    const std::vector<std::pair<int, int>> &keys, int32_t join_type) {
+  std::vector<int> lk, rk;
+  for (auto &kp : keys) {
+    lk.push_back(kp.first);
+    rk.push_back(kp.second);
+  }
+  const bool left_outer = join_type == CAPF_JOIN_LEFT_OUTER || join_type == CAPF_JOIN_FULL_OUTER;
+  const bool right_outer = join_type == CAPF_JOIN_RIGHT_OUTER || join_type == CAPF_JOIN_FULL_OUTER;
+  JoinPairs jp;
+  // build side = right table
+  HashTable ht = build_table(s, r, rk, true);
+  Grouping g;
+  int64_t nr = r.nrows, nl = l.nrows;
+  if (nr > 0) dense_groups(s, ht, nr, g);
+  BufPtr gcnt = s->alloc(8 * std::max<int64_t>(g.ngroups, 1));
+  BufPtr goff = s->alloc(8 * std::max<int64_t>(g.ngroups, 1));
+  BufPtr csr = s->alloc(8 * std::max<int64_t>(nr, 1));
+  if (g.ngroups > 0) {
+    HIP_CHECK(hipMemsetAsync(gcnt->p, 0, 8 * g.ngroups, s->stream));
+    hipLaunchKernelGGL(k_count_group, dim3(grid_for(nr, 256)), dim3(256), 0, s->stream,
+                       (const int64_t *)g.group_of_row->p, nr, (int64_t *)gcnt->p);
+    KERNEL_CHECK();
+    exclusive_scan_i64(s, (const int64_t *)gcnt->p, (int64_t *)goff->p, g.ngroups);
+    BufPtr cursor = s->alloc(8 * g.ngroups);
+    HIP_CHECK(hipMemsetAsync(cursor->p, 0, 8 * g.ngroups, s->stream));
+    hipLaunchKernelGGL(k_fill_csr, dim3(grid_for(nr, 256)), dim3(256), 0, s->stream,
+                       (const int64_t *)g.group_of_row->p, nr, (const int64_t *)goff->p,
+                       (int64_t *)cursor->p, (int64_t *)csr->p);
+    KERNEL_CHECK();
+  }
+  // probe with the left table
+  std::vector<ColView> pv;
+  for (int k : lk) pv.push_back(view_of(l.cols[k]));
+  BufPtr pviews = upload_views(s, pv);
+  BufPtr pgid = s->alloc(8 * std::max<int64_t>(nl, 1));
+  BufPtr ocnt = s->alloc(8 * std::max<int64_t>(nl, 1));
+  BufPtr ooff = s->alloc(8 * std::max<int64_t>(nl, 1));
+  int64_t total = 0;
+  if (nl > 0) {
+    if (nr == 0) {
+      // nothing to match: every probe row is unmatched
+      hipLaunchKernelGGL(k_fill_i64, dim3(grid_for(nl, 256)), dim3(256), 0, s->stream,
+                         (int64_t *)pgid->p, (int64_t)-1, nl);
+      hipLaunchKernelGGL(k_fill_i64, dim3(grid_for(nl, 256)), dim3(256), 0, s->stream,
+                         (int64_t *)ocnt->p, (int64_t)(left_outer ? 1 : 0), nl);
+      KERNEL_CHECK();
+    } else {
+      KernelTimer kt(s, "hash_probe", 8.0 * nl * lk.size());
+      hipLaunchKernelGGL(k_probe, dim3(grid_for(nl, 256)), dim3(256), 0, s->stream,
+                         (const ColView *)pviews->p, (const ColView *)ht.views->p,
+                         (int)lk.size(), nl, (const uint32_t *)ht.slots->p, ht.mask,
+                         (const uint32_t *)ht.slot_of_row->p,
+                         (const int64_t *)g.group_of_row->p, (const int64_t *)gcnt->p,
+                         (int64_t *)pgid->p, (int64_t *)ocnt->p, left_outer ? 1 : 0);
+      KERNEL_CHECK();
+    }
+    total = exclusive_scan_i64(s, (const int64_t *)ocnt->p, (int64_t *)ooff->p, nl);
+  }
+  int64_t extra = 0;
+  BufPtr gmatched, unmatched_rows;
+  if (right_outer) {
+    gmatched = s->alloc(std::max<int64_t>(g.ngroups, 1));
+    if (g.ngroups > 0) HIP_CHECK(hipMemsetAsync(gmatched->p, 0, g.ngroups, s->stream));
+  }
+  jp.left = s->alloc(8 * std::max<int64_t>(total + nr, 1));
+  jp.right = s->alloc(8 * std::max<int64_t>(total + nr, 1));
+  if (nl > 0 && total > 0) {
+    KernelTimer kt(s, "join_emit", 16.0 * total);
+    hipLaunchKernelGGL(k_join_emit, dim3(grid_for(nl, 256)), dim3(256), 0, s->stream,
+                       (const int64_t *)pgid->p, (const int64_t *)ooff->p, nl,
+                       (const int64_t *)goff->p, (const int64_t *)gcnt->p,
+                       (const int64_t *)csr->p, (int64_t *)jp.left->p, (int64_t *)jp.right->p,
+                       left_outer ? 1 : 0, right_outer ? (uint8_t *)gmatched->p : nullptr);
+    KERNEL_CHECK();
+  }
+  if (right_outer && nr > 0) {
+    BufPtr flags = s->alloc(nr);
+    hipLaunchKernelGGL(k_unmatched, dim3(grid_for(nr, 256)), dim3(256), 0, s->stream,
+                       (const int64_t *)g.group_of_row->p, (const uint8_t *)gmatched->p, nr,
+                       (uint8_t *)flags->p);
+    KERNEL_CHECK();
+    unmatched_rows = compact_flags(s, (const uint8_t *)flags->p, nr, &extra);
+    if (extra > 0) {
+      hipLaunchKernelGGL(k_append_unmatched, dim3(grid_for(extra, 256)), dim3(256), 0,
+                         s->stream, (const int64_t *)unmatched_rows->p, extra, total,
+                         (int64_t *)jp.left->p, (int64_t *)jp.right->p);
+      KERNEL_CHECK();
+    }
+  }
+  jp.n = total + extra;
+  return jp;
+}
+
+// ------------------------------------------------------------- aggregation
+template <typename T>
+__device__ inline T load_num(const ColView &c, int64_t r) {
+  if (c.type == CAPF_TYPE_BOOL) return (T)((const uint8_t *)c.data)[r];
+  if (c.type == CAPF_TYPE_FLOAT64) return (T)((const double *)c.data)[r];
+  return (T)((const int64_t *)c.data)[r];
+}
+
+__device__ inline void atomic_min_f64(double *p, double v) {
+  unsigned long long *a = (unsigned long long *)p;
+  unsigned long long old = *a;
+  while (v < __longlong_as_double(old)) {
+    unsigned long long prev = atomicCAS(a, old, (unsigned long long)__double_as_longlong(v));
+    if (prev == old) break;
+    old = prev;
+  }
+}
+__device__ inline void atomic_max_f64(double *p, double v) {
+  unsigned long long *a = (unsigned long long *)p;
+  unsigned long long old = *a;
+  while (v > __longlong_as_double(old)) {
+    unsigned long long prev = atomicCAS(a, old, (unsigned long long)__double_as_longlong(v));
+    if (prev == old) break;
+    old = prev;
+  }
+}
+
+// acc: per group value (int64 or double), cnt: per group non-null count
+__global__ void k_agg(const int64_t *gid, int64_t n, ColView arg, int kind, int fl, void *acc,
+                      unsigned long long *cnt) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    int64_t g = gid ? gid[r] : 0;
+    if (g < 0) continue;
+    if (kind == CAPF_AGG_COUNT_STAR) {
+      atomicAdd(&cnt[g], 1ull);
+      continue;
+    }
+    if (arg.type == CAPF_TYPE_NULL || !arg.data || (arg.valid && !arg.valid[r])) continue;
+    atomicAdd(&cnt[g], 1ull);
+    if (kind == CAPF_AGG_COUNT) continue;
+    if (fl) {
+      double v = load_num<double>(arg, r);
+      double *a = (double *)acc + g;
+      if (kind == CAPF_AGG_SUM || kind == CAPF_AGG_AVG) atomicAdd(a, v);
+      else if (kind == CAPF_AGG_MIN) atomic_min_f64(a, v);
+      else atomic_max_f64(a, v);
+    } else {
+      long long v = load_num<long long>(arg, r);
+      long long *a = (long long *)acc + g;
+      if (kind == CAPF_AGG_SUM || kind == CAPF_AGG_AVG) atomicAdd((unsigned long long *)a, (unsigned long long)v);
+      else if (kind == CAPF_AGG_MIN) atomicMin(a, v);
+      else atomicMax(a, v);
+    }
+  }
+}
+
+__global__ void k_agg_final(int64_t ng, int kind, int fl, int out_type, const void *acc,
+                            const unsigned long long *cnt, void *out, uint8_t *valid) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ng;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    unsigned long long c = cnt[g];
+    if (kind == CAPF_AGG_COUNT_STAR || kind == CAPF_AGG_COUNT) {
+      ((int64_t *)out)[g] = (int64_t)c;
+      valid[g] = 1;
+      continue;
+    }
+    valid[g] = c > 0 ? 1 : 0;
+    if (out_type == CAPF_TYPE_NULL) continue;
+    if (fl) {
+      double a = ((const double *)acc)[g];
+      if (kind == CAPF_AGG_AVG && c > 0) a = a / (double)c;
+      if (out_type == CAPF_TYPE_FLOAT64)
+        ((double *)out)[g] = c > 0 ? a : 0.0;
+      else
+        ((int64_t *)out)[g] = c > 0 ? (int64_t)a : 0;
+    } else {
+      int64_t a = ((const int64_t *)acc)[g];
+      // Flink AVG on a LONG column is a LONG (Java long division)
+      if (kind == CAPF_AGG_AVG && c > 0) a = a / (int64_t)c;
+      if (out_type == CAPF_TYPE_BOOL)
+        ((uint8_t *)out)[g] = c > 0 ? (a != 0) : 0;
+      else
+        ((int64_t *)out)[g] = c > 0 ? a : 0;
+    }
+  }
+}
+
+ColPtr aggregate(Session *s, const Grouping &g, const Data &d, int64_t nrows, int32_t kind,
+                 const ColPtr &arg, Type out_type) {
+  (void)d;
+  int64_t ng = g.ngroups;
+  ColPtr o = make_column(s, out_type, ng, true);
+  if (ng == 0) return o;
+  bool fl = arg && arg->type == Type::Float64;
+  BufPtr acc = s->alloc(8 * ng);
+  BufPtr cnt = s->alloc(8 * ng);
+  HIP_CHECK(hipMemsetAsync(cnt->p, 0, 8 * ng, s->stream));
+  // identity element of the accumulator
+  int64_t init_bits = 0;
+  if (kind == CAPF_AGG_MIN) {
+    if (fl) { double x = INFINITY; memcpy(&init_bits, &x, 8); } else init_bits = INT64_MAX;
+  } else if (kind == CAPF_AGG_MAX) {
+    if (fl) { double x = -INFINITY; memcpy(&init_bits, &x, 8); } else init_bits = INT64_MIN;
+  }
+  hipLaunchKernelGGL(k_fill_i64, dim3(grid_for(ng, 256)), dim3(256), 0, s->stream,
+                     (int64_t *)acc->p, init_bits, ng);
+  KERNEL_CHECK();
+  ColView av = arg ? view_of(arg) : ColView{nullptr, nullptr, CAPF_TYPE_NULL, 0};
+  if (nrows > 0) {
+    KernelTimer kt(s, "group_aggregate", 16.0 * nrows);
+    hipLaunchKernelGGL(k_agg, dim3(grid_for(nrows, 256)), dim3(256), 0, s->stream,
+                       (const int64_t *)g.group_of_row->p, nrows, av, kind, fl ? 1 : 0, acc->p,
+                       (unsigned long long *)cnt->p);
+    KERNEL_CHECK();
+  }
+  hipLaunchKernelGGL(k_agg_final, dim3(grid_for(ng, 256)), dim3(256), 0, s->stream, ng, kind,
+                     fl ? 1 : 0, (int32_t)out_type, acc->p, (const unsigned long long *)cnt->p,
+                     o->data ? o->data->p : nullptr, (uint8_t *)o->valid->p);
+  KERNEL_CHECK();
+  return o;
+}
+
+// ------------------------------------------------------------- ORDER BY
+// Order-preserving uint64 image of a key; NULL handled by a separate pass.
+__global__ void k_sort_key(ColView c, int64_t n, int desc, uint64_t *key, uint64_t *nullkey) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    bool nul = c.type == CAPF_TYPE_NULL || !c.data || (c.valid && !c.valid[r]);
+    uint64_t k = 0;
+    if (!nul) {
+      if (c.type == CAPF_TYPE_BOOL) {
+        k = ((const uint8_t *)c.data)[r] ? 1 : 0;
+      } else if (c.type == CAPF_TYPE_FLOAT64) {
+        uint64_t b = ((const uint64_t *)c.data)[r];
+        if (b == 0x8000000000000000ull) b = 0;
+        k = (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+      } else {
+        k = ((const uint64_t *)c.data)[r] ^ 0x8000000000000000ull;
+      }
+    }
+    key[r] = desc ? ~k : k;
+    // Cypher/Calcite: NULL is the largest value — last ascending, first descending
+    nullkey[r] = desc ? (nul ? 0 : 1) : (nul ? 1 : 0);
+  }
+}
+
+__global__ void k_gather_u64(const uint64_t *src, const int64_t *idx, uint64_t *dst, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = src[idx[i]];
+}
+
+static void radix_pass(Session *s, const uint64_t *keys_in, BufPtr &perm, int64_t n, int bits) {
+  // stable sort of perm by keys_in[perm[i]]
+  BufPtr kin = s->alloc(8 * n), kout = s->alloc(8 * n), pout = s->alloc(8 * n);
+  hipLaunchKernelGGL(k_gather_u64, dim3(grid_for(n, 256)), dim3(256), 0, s->stream, keys_in,
+                     (const int64_t *)perm->p, (uint64_t *)kin->p, n);
+  KERNEL_CHECK();
+  size_t tmp = 0;
+  HIP_CHECK(rocprim::radix_sort_pairs(nullptr, tmp, (const uint64_t *)kin->p,
+                                      (uint64_t *)kout->p, (const int64_t *)perm->p,
+                                      (int64_t *)pout->p, (size_t)n, 0, bits, s->stream));
+  BufPtr tbuf = s->alloc(std::max<size_t>(tmp, 16));
+  HIP_CHECK(rocprim::radix_sort_pairs(tbuf->p, tmp, (const uint64_t *)kin->p,
+                                      (uint64_t *)kout->p, (const int64_t *)perm->p,
+                                      (int64_t *)pout->p, (size_t)n, 0, bits, s->stream));
+  perm = pout;
+}
+
+BufPtr sort_permutation(Session *s, const std::vector<ColPtr> &keys,
+                        const std::vector<int32_t> &desc, int64_t n) {
+  BufPtr perm = iota_index(s, 0, n);
+  if (n <= 1) return perm;
+  BufPtr key = s->alloc(8 * n), nk = s->alloc(8 * n);
+  // LSD over the sort items: least significant item first, each stable.
+  for (int k = (int)keys.size() - 1; k >= 0; --k) {
+    hipLaunchKernelGGL(k_sort_key, dim3(grid_for(n, 256)), dim3(256), 0, s->stream,
+                       view_of(keys[k]), n, desc[k] ? 1 : 0, (uint64_t *)key->p,
+                       (uint64_t *)nk->p);
+    KERNEL_CHECK();
+    radix_pass(s, (const uint64_t *)key->p, perm, n, 64);
+    radix_pass(s, (const uint64_t *)nk->p, perm, n, 1);
+  }
+  s->sync();
+  return perm;
+}
+
+}  // namespace capf

@@ -1,0 +1,1140 @@
+// runtime.cpp — session, column store, lazy plan DAG and the C-ABI entry points.
+//
+// Each capf_table_* function mirrors one method of the okapi Table SPI
+// (okapi-relational/.../api/table/Table.scala:43-178) as implemented by
+// FlinkTable (flink-cypher/.../impl/table/FlinkTable.scala:49-199).  Like the
+// Flink Table API, operations only build a plan; materialisation happens on
+// size / download (FlinkTable.scala:57-61).
+#include <cstdio>
+#include <sstream>
+
+#include "capf_internal.h"
+
+namespace capf {
+
+const char *type_name(Type t) {
+  switch (t) {
+    case Type::Null: return "NULL";
+    case Type::Int64: return "INTEGER";
+    case Type::Float64: return "FLOAT";
+    case Type::Bool: return "BOOLEAN";
+    case Type::String: return "STRING";
+  }
+  return "?";
+}
+
+DevBuf::~DevBuf() {
+  if (owned && p) {
+    if (s && s->stream)
+      (void)hipFreeAsync(p, s->stream);
+    else
+      (void)hipFree(p);
+  }
+}
+
+BufPtr Session::alloc(size_t bytes) {
+  auto b = std::make_shared<DevBuf>();
+  b->s = this;
+  b->bytes = bytes;
+  if (bytes == 0) return b;
+  // 256-byte rounding keeps every column 16-B aligned for dwordx4 access.
+  size_t rounded = (bytes + 255) & ~size_t(255);
+  HIP_CHECK(hipMallocAsync(&b->p, rounded, stream));
+  return b;
+}
+
+void Session::sync() { HIP_CHECK(hipStreamSynchronize(stream)); }
+
+hipEvent_t Session::get_event() {
+  if (!event_pool.empty()) {
+    hipEvent_t e = event_pool.back();
+    event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  HIP_CHECK(hipEventCreate(&e));
+  return e;
+}
+
+// Resolve recorded kernel timings (synchronises on the recorded events only
+// when the profile is read, so timing never perturbs the timed region).
+void Session::resolve_profile() {
+  for (auto &p : pending) {
+    (void)hipEventSynchronize(p.b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, p.a, p.b);
+    auto &e = profile[p.name];
+    e.launches++;
+    e.total_ms += ms;
+    e.bytes += p.bytes;
+    event_pool.push_back(p.a);
+    event_pool.push_back(p.b);
+  }
+  pending.clear();
+}
+
+KernelTimer::KernelTimer(Session *s_, const char *n, double by) : s(s_), name(n), bytes(by) {
+  if (!s->profiling) return;
+  a = s->get_event();
+  b = s->get_event();
+  HIP_CHECK(hipEventRecord(a, s->stream));
+}
+
+KernelTimer::~KernelTimer() {
+  if (!a) return;
+  (void)hipEventRecord(b, s->stream);
+  s->pending.push_back(PendingTiming{name, bytes, a, b});
+}
+
+int Node::col_index(const std::string &name) const {
+  for (size_t i = 0; i < names.size(); ++i)
+    if (names[i] == name) return (int)i;
+  return -1;
+}
+
+int Node::col_index_or_throw(const std::string &name) const {
+  int i = col_index(name);
+  if (i < 0) {
+    std::ostringstream os;
+    os << "column '" << name << "' not found; available: [";
+    for (size_t k = 0; k < names.size(); ++k) os << (k ? ", " : "") << names[k];
+    os << "]";
+    illegal(os.str());
+  }
+  return i;
+}
+
+Program Program::from_c(const capf_expr *e) {
+  Program p;
+  if (!e) illegal("null expression program");
+  if (e->n <= 0) illegal("empty expression program");
+  p.code.resize(e->n);
+  for (int i = 0; i < e->n; ++i) {
+    p.code[i].op = e->ops[i];
+    p.code[i].pad = 0;
+    p.code[i].i = e->iargs ? e->iargs[i] : 0;
+    p.code[i].f = e->fargs ? e->fargs[i] : 0.0;
+  }
+  for (int i = 0; i < e->n_names; ++i) p.names.emplace_back(e->names[i]);
+  for (auto &in : p.code)
+    if (in.op == OP_COL && (in.i < 0 || in.i >= (int64_t)p.names.size()))
+      illegal("column reference out of range in expression program");
+  return p;
+}
+
+std::vector<std::string> Program::referenced() const {
+  std::vector<std::string> r;
+  for (auto &in : code)
+    if (in.op == OP_COL) r.push_back(names[in.i]);
+  return r;
+}
+
+static bool is_numeric(Type t) { return t == Type::Int64 || t == Type::Float64; }
+
+Type infer_type(const Program &p, const std::vector<std::string> &names,
+                const std::vector<Type> &types) {
+  std::vector<Type> st;
+  auto pop = [&]() {
+    if (st.empty()) illegal("malformed expression program (stack underflow)");
+    Type t = st.back();
+    st.pop_back();
+    return t;
+  };
+  for (auto &in : p.code) {
+    switch (in.op) {
+      case OP_COL: {
+        const std::string &nm = p.names[in.i];
+        int idx = -1;
+        for (size_t k = 0; k < names.size(); ++k)
+          if (names[k] == nm) idx = (int)k;
+        if (idx < 0) illegal("expression references unknown column '" + nm + "'");
+        st.push_back(types[idx]);
+        break;
+      }
+      case OP_LIT_INT: st.push_back(Type::Int64); break;
+      case OP_LIT_FLOAT: st.push_back(Type::Float64); break;
+      case OP_LIT_BOOL: st.push_back(Type::Bool); break;
+      case OP_LIT_STRING: st.push_back(Type::String); break;
+      case OP_LIT_NULL: {
+        Type t = (Type)in.i;
+        if (in.i < 0 || in.i > 4) t = Type::Null;
+        st.push_back(t);
+        break;
+      }
+      case OP_EQ: case OP_NEQ: case OP_LT: case OP_LE: case OP_GT: case OP_GE: {
+        Type b = pop(), a = pop();
+        bool ordered = in.op != OP_EQ && in.op != OP_NEQ;
+        if (a != Type::Null && b != Type::Null) {
+          if (ordered && (a == Type::String || b == Type::String))
+            not_impl("ordering comparison on strings");
+          if (!(a == b || (is_numeric(a) && is_numeric(b))))
+            illegal(std::string("cannot compare ") + type_name(a) + " with " + type_name(b));
+        }
+        st.push_back(Type::Bool);
+        break;
+      }
+      case OP_NOT: pop(); st.push_back(Type::Bool); break;
+      case OP_AND: case OP_OR: {
+        if (in.i < 0) illegal("negative arity");
+        for (int64_t k = 0; k < in.i; ++k) pop();
+        st.push_back(Type::Bool);
+        break;
+      }
+      case OP_IS_NULL: case OP_IS_NOT_NULL: pop(); st.push_back(Type::Bool); break;
+      case OP_ADD: case OP_SUB: case OP_MUL: case OP_DIV: case OP_MOD: {
+        Type b = pop(), a = pop();
+        if ((a != Type::Null && !is_numeric(a)) || (b != Type::Null && !is_numeric(b)))
+          not_impl(std::string("arithmetic on ") + type_name(a) + " and " + type_name(b));
+        if (a == Type::Float64 || b == Type::Float64)
+          st.push_back(Type::Float64);
+        else if (a == Type::Null && b == Type::Null)
+          st.push_back(Type::Null);
+        else
+          st.push_back(Type::Int64);
+        break;
+      }
+      case OP_NEG: {
+        Type a = pop();
+        if (a != Type::Null && !is_numeric(a)) not_impl("negation of non-numeric");
+        st.push_back(a);
+        break;
+      }
+      case OP_TO_FLOAT: {
+        Type a = pop();
+        if (a == Type::String) not_impl("toFloat on strings");
+        st.push_back(Type::Float64);
+        break;
+      }
+      case OP_TO_INTEGER: {
+        Type a = pop();
+        if (a == Type::String) not_impl("toInteger on strings");
+        st.push_back(Type::Int64);
+        break;
+      }
+      case OP_COALESCE: {
+        if (in.i <= 0) illegal("coalesce arity");
+        Type r = Type::Null;
+        for (int64_t k = 0; k < in.i; ++k) {
+          Type t = pop();
+          if (t == Type::Null) continue;
+          if (r == Type::Null)
+            r = t;
+          else if (r != t) {
+            if (is_numeric(r) && is_numeric(t))
+              r = Type::Float64;
+            else
+              illegal("coalesce over incompatible types");
+          }
+        }
+        st.push_back(r);
+        break;
+      }
+      default: not_impl("expression opcode " + std::to_string(in.op));
+    }
+  }
+  if (st.size() != 1) illegal("malformed expression program (stack not singular)");
+  return st.back();
+}
+
+ColPtr make_column(Session *s, Type t, int64_t n, bool with_valid) {
+  auto c = std::make_shared<Column>();
+  c->type = t;
+  c->n = n;
+  if (t != Type::Null && n > 0) c->data = s->alloc(type_width(t) * n);
+  if (with_valid && n > 0) c->valid = s->alloc(n);
+  return c;
+}
+
+ColPtr null_column(Session *s, Type t, int64_t n) {
+  (void)s;
+  auto c = std::make_shared<Column>();
+  c->type = Type::Null;
+  c->n = n;
+  (void)t;
+  return c;
+}
+
+ColView view_of(const ColPtr &c) {
+  ColView v;
+  v.data = c->data ? c->data->p : nullptr;
+  v.valid = c->valid ? (const uint8_t *)c->valid->p : nullptr;
+  v.type = (int32_t)c->type;
+  v.pad = 0;
+  return v;
+}
+
+const ColStats &column_stats(Session *s, const ColPtr &c) {
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->stats) c->stats = compute_stats(s, *c);
+  return *c->stats;
+}
+
+// ------------------------------------------------------------- materialise
+static DataPtr materialize_impl(const NodePtr &n);
+
+DataPtr materialize(const NodePtr &n) {
+  std::lock_guard<std::mutex> g(n->mu);
+  if (!n->result) n->result = materialize_impl(n);
+  return n->result;
+}
+
+static DataPtr gather_all(Session *s, const Data &d, const BufPtr &idx, int64_t m) {
+  auto out = std::make_shared<Data>();
+  out->nrows = m;
+  for (auto &c : d.cols) out->cols.push_back(gather_column(s, c, (const int64_t *)(idx ? idx->p : nullptr), m));
+  return out;
+}
+
+
+static DataPtr materialize_impl(const NodePtr &n) {
+  Session *s = n->s;
+  switch (n->kind) {
+    case Kind::Source: illegal("source table without data");
+    case Kind::Select: {
+      DataPtr c = materialize(n->kids[0]);
+      auto out = std::make_shared<Data>();
+      out->nrows = c->nrows;
+      for (int i : n->sel_index) out->cols.push_back(c->cols[i]);
+      return out;
+    }
+    case Kind::Filter: {
+      DataPtr c = materialize(n->kids[0]);
+      int64_t m = 0;
+      BufPtr idx = eval_filter(s, n->pred, n->kids[0]->names, *c, &m);
+      return gather_all(s, *c, idx, m);
+    }
+    case Kind::Join: {
+      DataPtr l = materialize(n->kids[0]);
+      DataPtr r = materialize(n->kids[1]);
+      BufPtr li, ri;
+      int64_t m = 0;
+      if (n->join_type == CAPF_JOIN_CROSS) {
+        m = l->nrows * r->nrows;
+        cross_index(s, l->nrows, r->nrows, li, ri);
+      } else {
+        JoinPairs jp = hash_join(s, *l, *r, n->join_keys, n->join_type);
+        li = jp.left;
+        ri = jp.right;
+        m = jp.n;
+      }
+      auto out = std::make_shared<Data>();
+      out->nrows = m;
+      bool lnull = n->join_type == CAPF_JOIN_RIGHT_OUTER || n->join_type == CAPF_JOIN_FULL_OUTER;
+      bool rnull = n->join_type == CAPF_JOIN_LEFT_OUTER || n->join_type == CAPF_JOIN_FULL_OUTER;
+      for (auto &c : l->cols)
+        out->cols.push_back(gather_column(s, c, (const int64_t *)(li ? li->p : nullptr), m, lnull));
+      for (auto &c : r->cols)
+        out->cols.push_back(gather_column(s, c, (const int64_t *)(ri ? ri->p : nullptr), m, rnull));
+      return out;
+    }
+    case Kind::Union: {
+      DataPtr l = materialize(n->kids[0]);
+      DataPtr r = materialize(n->kids[1]);
+      auto out = std::make_shared<Data>();
+      out->nrows = l->nrows + r->nrows;
+      for (size_t i = 0; i < n->names.size(); ++i) {
+        int ri = n->kids[1]->col_index(n->names[i]);
+        out->cols.push_back(concat_columns(s, l->cols[i], r->cols[ri], n->types[i]));
+      }
+      return out;
+    }
+    case Kind::Distinct: {
+      DataPtr c = materialize(n->kids[0]);
+      Grouping g = group_rows(s, *c, n->key_index);
+      return gather_all(s, *c, g.rep_row, g.ngroups);
+    }
+    case Kind::Group: {
+      // fused factorised count: group(∅, count(*)) over an inner-join tree
+      bool all_count_star = n->key_index.empty() && !n->aggs.empty();
+      for (auto &a : n->aggs) all_count_star &= a.kind == CAPF_AGG_COUNT_STAR;
+      if (all_count_star) {
+        int64_t cnt = 0;
+        if (try_fused_count(n->kids[0], &cnt)) {
+          auto out = std::make_shared<Data>();
+          out->nrows = 1;
+          for (size_t k = 0; k < n->aggs.size(); ++k) {
+            auto col = make_column(s, Type::Int64, 1, false);
+            HIP_CHECK(hipMemcpyAsync(col->data->p, &cnt, 8, hipMemcpyHostToDevice, s->stream));
+            out->cols.push_back(col);
+          }
+          s->sync();
+          return out;
+        }
+      }
+      DataPtr c = materialize(n->kids[0]);
+      Grouping g = group_rows(s, *c, n->key_index);
+      if (n->key_index.empty() && g.ngroups == 0) {
+        // global aggregation over an empty input still yields one row
+        g.ngroups = 1;
+      }
+      auto out = std::make_shared<Data>();
+      out->nrows = g.ngroups;
+      for (int k : n->key_index)
+        out->cols.push_back(gather_column(s, c->cols[k], (const int64_t *)g.rep_row->p, g.ngroups));
+      for (auto &a : n->aggs) {
+        ColPtr arg;
+        if (a.kind != CAPF_AGG_COUNT_STAR) {
+          Type at = infer_type(a.arg, n->kids[0]->names, n->kids[0]->types);
+          arg = eval_program(s, a.arg, n->kids[0]->names, *c, at);
+        }
+        if (a.distinct && a.kind == CAPF_AGG_COUNT && c->nrows > 0) {
+          // count(DISTINCT e): Spark semantics (SparkSQLExprMapper.scala:427-429);
+          // Flink ignores the flag (FlinkSQLExprMapper.scala:282), see DESIGN.md.
+          auto gid = std::make_shared<Column>();
+          gid->type = Type::Int64;
+          gid->n = c->nrows;
+          gid->data = g.group_of_row;
+          Data pairs;
+          pairs.nrows = c->nrows;
+          pairs.cols = {gid, arg};
+          Grouping dg = group_rows(s, pairs, {0, 1});
+          const int64_t *reps = (const int64_t *)dg.rep_row->p;
+          Grouping g2;
+          g2.ngroups = g.ngroups;
+          g2.group_of_row = gather_column(s, gid, reps, dg.ngroups)->data;
+          ColPtr darg = gather_column(s, arg, reps, dg.ngroups);
+          out->cols.push_back(aggregate(s, g2, *c, dg.ngroups, a.kind, darg, a.out_type));
+          continue;
+        }
+        out->cols.push_back(aggregate(s, g, *c, c->nrows, a.kind, arg, a.out_type));
+      }
+      return out;
+    }
+    case Kind::WithColumns: {
+      DataPtr c = materialize(n->kids[0]);
+      auto out = std::make_shared<Data>();
+      out->nrows = c->nrows;
+      out->cols = c->cols;
+      out->cols.resize(n->names.size());
+      for (size_t k = 0; k < n->exprs.size(); ++k) {
+        Type t = n->types[n->target_index[k]];
+        out->cols[n->target_index[k]] = eval_program(s, n->exprs[k], n->kids[0]->names, *c, t);
+      }
+      return out;
+    }
+    case Kind::OrderBy: {
+      DataPtr c = materialize(n->kids[0]);
+      std::vector<ColPtr> keys;
+      for (auto &p : n->exprs) {
+        Type t = infer_type(p, n->kids[0]->names, n->kids[0]->types);
+        keys.push_back(eval_program(s, p, n->kids[0]->names, *c, t));
+      }
+      BufPtr perm = sort_permutation(s, keys, n->desc, c->nrows);
+      return gather_all(s, *c, perm, c->nrows);
+    }
+    case Kind::Skip:
+    case Kind::Limit: {
+      DataPtr c = materialize(n->kids[0]);
+      int64_t start, m;
+      if (n->kind == Kind::Skip) {
+        start = std::min(n->count, c->nrows);
+        m = c->nrows - start;
+      } else {
+        start = 0;
+        m = std::min(n->count, c->nrows);
+      }
+      BufPtr idx = iota_index(s, start, m);
+      return gather_all(s, *c, idx, m);
+    }
+  }
+  fail(CAPF_ERR_INTERNAL, "unknown plan node");
+}
+
+int64_t node_size(const NodePtr &n) {
+  {
+    std::lock_guard<std::mutex> g(n->mu);
+    if (n->result) return n->result->nrows;
+  }
+  int64_t cnt = 0;
+  if (n->kind == Kind::Union) return node_size(n->kids[0]) + node_size(n->kids[1]);
+  if (try_fused_count(n, &cnt)) return cnt;
+  return materialize(n)->nrows;
+}
+
+}  // namespace capf
+
+// ===================================================================== C-ABI
+using namespace capf;
+
+static thread_local std::string g_err;
+static thread_local int32_t g_err_kind = 0;
+
+namespace capf {
+int32_t record_error(int32_t code, const char *msg) {
+  g_err = msg;
+  g_err_kind = code;
+  return code;
+}
+}  // namespace capf
+
+#define CAPF_API_BEGIN try {
+#define CAPF_API_END                                   \
+  return CAPF_OK;                                      \
+  }                                                    \
+  catch (const capf::Error &e) {                       \
+    g_err = e.what();                                  \
+    g_err_kind = e.code;                               \
+    return e.code;                                     \
+  }                                                    \
+  catch (const std::exception &e) {                    \
+    g_err = e.what();                                  \
+    g_err_kind = CAPF_ERR_INTERNAL;                    \
+    return CAPF_ERR_INTERNAL;                          \
+  }
+
+static capf_table *wrap(NodePtr n) {
+  auto *t = new capf_table;
+  t->node = std::move(n);
+  return t;
+}
+
+static void need(const void *p, const char *what) {
+  if (!p) illegal(std::string("null argument: ") + what);
+}
+
+static NodePtr new_node(Session *s, Kind k) {
+  auto n = std::make_shared<Node>();
+  n->s = s;
+  n->kind = k;
+  return n;
+}
+
+extern "C" {
+
+const char *capf_last_error(void) { return g_err.c_str(); }
+int32_t capf_last_error_kind(void) { return g_err_kind; }
+int32_t capf_abi_version(void) { return CAPF_ABI_VERSION; }
+
+capf_status capf_session_create(int32_t device, void *hip_stream, capf_session **out) {
+  CAPF_API_BEGIN
+  need(out, "out");
+  auto *cs = new capf_session;
+  Session &s = cs->impl;
+  s.device = device;
+  HIP_CHECK(hipSetDevice(device));
+  if (hip_stream) {
+    s.stream = (hipStream_t)hip_stream;
+    s.own_stream = false;
+  } else {
+    HIP_CHECK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    s.own_stream = true;
+  }
+  // keep freed blocks in the stream-ordered pool instead of returning them to
+  // the driver: no hipMalloc on the hot path after warm-up.
+  hipMemPool_t pool;
+  if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+    uint64_t thr = UINT64_MAX;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+  }
+  HIP_CHECK(hipMalloc(&s.d_scalars, 64 * sizeof(int64_t)));
+  HIP_CHECK(hipHostMalloc(&s.h_scalars, 64 * sizeof(int64_t), hipHostMallocDefault));
+  *out = cs;
+  CAPF_API_END
+}
+
+capf_status capf_session_destroy(capf_session *cs) {
+  CAPF_API_BEGIN
+  if (!cs) return CAPF_OK;
+  Session &s = cs->impl;
+  (void)hipStreamSynchronize(s.stream);
+  s.resolve_profile();
+  for (auto e : s.event_pool) (void)hipEventDestroy(e);
+  (void)hipFree(s.d_scalars);
+  (void)hipHostFree(s.h_scalars);
+  if (s.own_stream) (void)hipStreamDestroy(s.stream);
+  delete cs;
+  CAPF_API_END
+}
+
+capf_status capf_session_sync(capf_session *cs) {
+  CAPF_API_BEGIN
+  need(cs, "session");
+  cs->impl.sync();
+  CAPF_API_END
+}
+
+capf_status capf_session_set_profiling(capf_session *cs, int32_t enabled) {
+  CAPF_API_BEGIN
+  need(cs, "session");
+  cs->impl.profiling = enabled != 0;
+  CAPF_API_END
+}
+
+capf_status capf_session_reset_profile(capf_session *cs) {
+  CAPF_API_BEGIN
+  need(cs, "session");
+  cs->impl.resolve_profile();
+  cs->impl.profile.clear();
+  CAPF_API_END
+}
+
+capf_status capf_session_profile_count(capf_session *cs, int32_t *n) {
+  CAPF_API_BEGIN
+  need(cs, "session");
+  need(n, "n");
+  cs->impl.resolve_profile();
+  *n = (int32_t)cs->impl.profile.size();
+  CAPF_API_END
+}
+
+capf_status capf_session_profile_entry(capf_session *cs, int32_t i, const char **kernel,
+                                       int64_t *launches, double *total_ms, double *bytes) {
+  CAPF_API_BEGIN
+  need(cs, "session");
+  if (i < 0 || i >= (int32_t)cs->impl.profile.size()) illegal("profile index out of range");
+  auto it = cs->impl.profile.begin();
+  std::advance(it, i);
+  if (kernel) *kernel = it->first.c_str();
+  if (launches) *launches = it->second.launches;
+  if (total_ms) *total_ms = it->second.total_ms;
+  if (bytes) *bytes = it->second.bytes;
+  CAPF_API_END
+}
+
+const char *capf_session_last_plan(capf_session *cs) {
+  return cs ? cs->impl.last_plan.c_str() : "";
+}
+
+capf_status capf_string_intern(capf_session *cs, const char *str, int64_t *code) {
+  CAPF_API_BEGIN
+  need(cs, "session");
+  need(str, "str");
+  need(code, "code");
+  Session &s = cs->impl;
+  std::lock_guard<std::mutex> g(s.str_mu);
+  auto it = s.string_codes.find(str);
+  if (it != s.string_codes.end()) {
+    *code = it->second;
+  } else {
+    int64_t c = (int64_t)s.strings.size();
+    s.strings.emplace_back(str);
+    s.string_codes.emplace(str, c);
+    *code = c;
+  }
+  CAPF_API_END
+}
+
+capf_status capf_string_lookup(capf_session *cs, int64_t code, const char **str) {
+  CAPF_API_BEGIN
+  need(cs, "session");
+  need(str, "str");
+  Session &s = cs->impl;
+  std::lock_guard<std::mutex> g(s.str_mu);
+  if (code < 0 || code >= (int64_t)s.strings.size()) illegal("unknown string code");
+  *str = s.strings[code].c_str();
+  CAPF_API_END
+}
+
+static void check_unique_names(const std::vector<std::string> &names) {
+  for (size_t i = 0; i < names.size(); ++i)
+    for (size_t j = i + 1; j < names.size(); ++j)
+      if (names[i] == names[j]) illegal("duplicate column name '" + names[i] + "'");
+}
+
+static capf_status table_from(capf_session *cs, int32_t ncols, const char *const *names,
+                              const int32_t *types, const void *const *data,
+                              const uint8_t *const *valid, int64_t nrows, bool device,
+                              bool copy, capf_table **out) {
+  CAPF_API_BEGIN
+  need(cs, "session");
+  need(out, "out");
+  if (ncols < 0 || nrows < 0) illegal("negative table dimensions");
+  Session *s = &cs->impl;
+  auto n = new_node(s, Kind::Source);
+  auto d = std::make_shared<Data>();
+  d->nrows = nrows;
+  for (int i = 0; i < ncols; ++i) {
+    Type t = (Type)types[i];
+    if (types[i] < 0 || types[i] > 4) illegal("bad column type");
+    n->names.emplace_back(names[i]);
+    n->types.push_back(t);
+    auto c = std::make_shared<Column>();
+    c->type = t;
+    c->n = nrows;
+    size_t w = type_width(t);
+    if (t != Type::Null && nrows > 0) {
+      need(data[i], "column data");
+      if (device && !copy) {
+        c->data = std::make_shared<DevBuf>();
+        c->data->p = const_cast<void *>(data[i]);
+        c->data->bytes = w * nrows;
+        c->data->owned = false;
+        c->data->s = s;
+      } else {
+        c->data = s->alloc(w * nrows);
+        HIP_CHECK(hipMemcpyAsync(c->data->p, data[i], w * nrows,
+                                 device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                                 s->stream));
+      }
+    }
+    if (valid && valid[i] && nrows > 0) {
+      if (device && !copy) {
+        c->valid = std::make_shared<DevBuf>();
+        c->valid->p = const_cast<uint8_t *>(valid[i]);
+        c->valid->bytes = nrows;
+        c->valid->owned = false;
+        c->valid->s = s;
+      } else {
+        c->valid = s->alloc(nrows);
+        HIP_CHECK(hipMemcpyAsync(c->valid->p, valid[i], nrows,
+                                 device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                                 s->stream));
+      }
+    }
+    d->cols.push_back(c);
+  }
+  check_unique_names(n->names);
+  s->sync();
+  n->result = d;
+  *out = wrap(n);
+  CAPF_API_END
+}
+
+capf_status capf_table_from_host(capf_session *s, int32_t ncols, const char *const *names,
+                                 const int32_t *types, const void *const *data,
+                                 const uint8_t *const *valid, int64_t nrows, capf_table **out) {
+  return table_from(s, ncols, names, types, data, valid, nrows, false, true, out);
+}
+
+capf_status capf_table_from_device(capf_session *s, int32_t ncols, const char *const *names,
+                                   const int32_t *types, void *const *data,
+                                   uint8_t *const *valid, int64_t nrows, int32_t copy,
+                                   capf_table **out) {
+  return table_from(s, ncols, names, types, (const void *const *)data,
+                    (const uint8_t *const *)valid, nrows, true, copy != 0, out);
+}
+
+capf_status capf_table_unit(capf_session *cs, capf_table **out) {
+  CAPF_API_BEGIN
+  need(cs, "session");
+  need(out, "out");
+  auto n = new_node(&cs->impl, Kind::Source);
+  auto d = std::make_shared<Data>();
+  d->nrows = 1;
+  n->result = d;
+  *out = wrap(n);
+  CAPF_API_END
+}
+
+capf_status capf_table_empty(capf_session *cs, int32_t ncols, const char *const *names,
+                             const int32_t *types, capf_table **out) {
+  std::vector<const void *> data(ncols > 0 ? ncols : 1, nullptr);
+  return table_from(cs, ncols, names, types, data.data(), nullptr, 0, false, true, out);
+}
+
+capf_status capf_table_retain(capf_table *t) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  // handles are values: retaining creates no new handle in this ABI; use
+  // capf_table_cache to obtain a second owning handle.
+  CAPF_API_END
+}
+
+capf_status capf_table_release(capf_table *t) {
+  CAPF_API_BEGIN
+  delete t;
+  CAPF_API_END
+}
+
+capf_status capf_table_num_columns(capf_table *t, int32_t *n) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(n, "n");
+  *n = (int32_t)t->node->names.size();
+  CAPF_API_END
+}
+
+capf_status capf_table_column_name(capf_table *t, int32_t i, const char **name) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(name, "name");
+  if (i < 0 || i >= (int32_t)t->node->names.size()) illegal("column index out of range");
+  *name = t->node->names[i].c_str();
+  CAPF_API_END
+}
+
+capf_status capf_table_column_type(capf_table *t, const char *col, int32_t *type) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(col, "col");
+  need(type, "type");
+  *type = (int32_t)t->node->types[t->node->col_index_or_throw(col)];
+  CAPF_API_END
+}
+
+capf_status capf_table_size(capf_table *t, int64_t *n) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(n, "n");
+  *n = node_size(t->node);
+  CAPF_API_END
+}
+
+capf_status capf_table_download(capf_table *t, const char *col, void *values_out,
+                                uint8_t *valid_out) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(col, "col");
+  int i = t->node->col_index_or_throw(col);
+  DataPtr d = materialize(t->node);
+  Session *s = t->node->s;
+  const ColPtr &c = d->cols[i];
+  size_t w = type_width(c->type);
+  if (d->nrows > 0) {
+    if (c->type != Type::Null && values_out)
+      HIP_CHECK(hipMemcpyAsync(values_out, c->data->p, w * d->nrows, hipMemcpyDeviceToHost, s->stream));
+    if (valid_out) {
+      if (c->type == Type::Null)
+        memset(valid_out, 0, d->nrows);
+      else if (c->valid)
+        HIP_CHECK(hipMemcpyAsync(valid_out, c->valid->p, d->nrows, hipMemcpyDeviceToHost, s->stream));
+      else
+        memset(valid_out, 1, d->nrows);
+    }
+    s->sync();
+  }
+  CAPF_API_END
+}
+
+capf_status capf_table_device_column(capf_table *t, const char *col, void **values,
+                                     uint8_t **valid, int64_t *nrows) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(col, "col");
+  int i = t->node->col_index_or_throw(col);
+  DataPtr d = materialize(t->node);
+  const ColPtr &c = d->cols[i];
+  if (values) *values = c->data ? c->data->p : nullptr;
+  if (valid) *valid = c->valid ? (uint8_t *)c->valid->p : nullptr;
+  if (nrows) *nrows = d->nrows;
+  CAPF_API_END
+}
+
+capf_status capf_table_cache(capf_table *t, capf_table **out) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(out, "out");
+  *out = wrap(t->node);  // Table.cache default: identity (Table.scala:52)
+  CAPF_API_END
+}
+
+capf_status capf_table_select(capf_table *t, int32_t n, const char *const *cols,
+                              const char *const *aliases, capf_table **out) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(out, "out");
+  const NodePtr &c = t->node;
+  auto nn = new_node(c->s, Kind::Select);
+  nn->kids.push_back(c);
+  for (int i = 0; i < n; ++i) {
+    int idx = c->col_index_or_throw(cols[i]);
+    nn->sel_index.push_back(idx);
+    nn->names.emplace_back(aliases && aliases[i] ? aliases[i] : cols[i]);
+    nn->types.push_back(c->types[idx]);
+  }
+  check_unique_names(nn->names);
+  *out = wrap(nn);
+  CAPF_API_END
+}
+
+capf_status capf_table_drop(capf_table *t, int32_t n, const char *const *cols, capf_table **out) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(out, "out");
+  const NodePtr &c = t->node;
+  // FlinkTable.drop = select(physicalColumns diff cols) (FlinkTable.scala:100-103)
+  auto nn = new_node(c->s, Kind::Select);
+  nn->kids.push_back(c);
+  for (size_t i = 0; i < c->names.size(); ++i) {
+    bool dropped = false;
+    for (int k = 0; k < n; ++k) dropped |= c->names[i] == cols[k];
+    if (dropped) continue;
+    nn->sel_index.push_back((int)i);
+    nn->names.push_back(c->names[i]);
+    nn->types.push_back(c->types[i]);
+  }
+  *out = wrap(nn);
+  CAPF_API_END
+}
+
+capf_status capf_table_filter(capf_table *t, const capf_expr *pred, capf_table **out) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(out, "out");
+  const NodePtr &c = t->node;
+  Program p = Program::from_c(pred);
+  Type ty = infer_type(p, c->names, c->types);
+  if (ty != Type::Bool && ty != Type::Null) illegal("filter predicate is not boolean");
+  auto nn = new_node(c->s, Kind::Filter);
+  nn->kids.push_back(c);
+  nn->pred = std::move(p);
+  nn->names = c->names;
+  nn->types = c->types;
+  *out = wrap(nn);
+  CAPF_API_END
+}
+
+capf_status capf_table_join(capf_table *l, capf_table *r, int32_t join_type, int32_t npairs,
+                            const char *const *lcols, const char *const *rcols,
+                            capf_table **out) {
+  CAPF_API_BEGIN
+  need(l, "left");
+  need(r, "right");
+  need(out, "out");
+  const NodePtr &a = l->node;
+  const NodePtr &b = r->node;
+  // FlinkTable.join asserts disjoint columns (FlinkTable.scala:173-174)
+  for (auto &x : a->names)
+    for (auto &y : b->names)
+      if (x == y) illegal("overlapping columns: " + x);
+  if (join_type < CAPF_JOIN_INNER || join_type > CAPF_JOIN_CROSS) illegal("bad join type");
+  auto nn = new_node(a->s, Kind::Join);
+  nn->kids = {a, b};
+  nn->join_type = join_type;
+  if (join_type != CAPF_JOIN_CROSS) {
+    for (int i = 0; i < npairs; ++i) {
+      int li = a->col_index_or_throw(lcols[i]);
+      int ri = b->col_index_or_throw(rcols[i]);
+      Type lt = a->types[li], rt = b->types[ri];
+      if (lt != rt && lt != Type::Null && rt != Type::Null &&
+          !(is_numeric(lt) && is_numeric(rt)))
+        illegal(std::string("join on incompatible types ") + type_name(lt) + " / " + type_name(rt));
+      if (lt != rt && lt != Type::Null && rt != Type::Null)
+        not_impl("join between INTEGER and FLOAT columns");
+      nn->join_keys.emplace_back(li, ri);
+    }
+  }
+  nn->names = a->names;
+  nn->names.insert(nn->names.end(), b->names.begin(), b->names.end());
+  nn->types = a->types;
+  nn->types.insert(nn->types.end(), b->types.begin(), b->types.end());
+  *out = wrap(nn);
+  CAPF_API_END
+}
+
+capf_status capf_table_union_all(capf_table *l, capf_table *r, capf_table **out) {
+  CAPF_API_BEGIN
+  need(l, "left");
+  need(r, "right");
+  need(out, "out");
+  const NodePtr &a = l->node;
+  const NodePtr &b = r->node;
+  if (a->names.size() != b->names.size()) illegal("unionAll: column sets differ");
+  auto nn = new_node(a->s, Kind::Union);
+  nn->kids = {a, b};
+  nn->names = a->names;
+  for (size_t i = 0; i < a->names.size(); ++i) {
+    int j = b->col_index(a->names[i]);
+    if (j < 0) illegal("unionAll: right side lacks column '" + a->names[i] + "'");
+    Type x = a->types[i], y = b->types[j];
+    // Equal column types for union all, differing nullability OK
+    // (FlinkTable.scala:152-169)
+    if (x != y && x != Type::Null && y != Type::Null)
+      illegal(std::string("Equal column types for union all: ") + a->names[i] + " " +
+              type_name(x) + " vs " + type_name(y));
+    nn->types.push_back(x == Type::Null ? y : x);
+  }
+  *out = wrap(nn);
+  CAPF_API_END
+}
+
+capf_status capf_table_order_by(capf_table *t, int32_t n, const capf_expr *keys,
+                                const int32_t *descending, capf_table **out) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(out, "out");
+  const NodePtr &c = t->node;
+  auto nn = new_node(c->s, Kind::OrderBy);
+  nn->kids.push_back(c);
+  for (int i = 0; i < n; ++i) {
+    Program p = Program::from_c(&keys[i]);
+    Type ty = infer_type(p, c->names, c->types);
+    if (ty == Type::String) not_impl("ORDER BY on strings");
+    nn->exprs.push_back(std::move(p));
+    nn->desc.push_back(descending ? descending[i] : 0);
+  }
+  nn->names = c->names;
+  nn->types = c->types;
+  *out = wrap(nn);
+  CAPF_API_END
+}
+
+static capf_status skip_limit(capf_table *t, int64_t n, Kind k, capf_table **out) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(out, "out");
+  if (n < 0) illegal("negative skip/limit");
+  const NodePtr &c = t->node;
+  auto nn = new_node(c->s, k);
+  nn->kids.push_back(c);
+  nn->count = n;
+  nn->names = c->names;
+  nn->types = c->types;
+  *out = wrap(nn);
+  CAPF_API_END
+}
+
+capf_status capf_table_skip(capf_table *t, int64_t n, capf_table **out) {
+  return skip_limit(t, n, Kind::Skip, out);
+}
+capf_status capf_table_limit(capf_table *t, int64_t n, capf_table **out) {
+  return skip_limit(t, n, Kind::Limit, out);
+}
+
+capf_status capf_table_distinct_cols(capf_table *t, int32_t n, const char *const *cols,
+                                     capf_table **out) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(out, "out");
+  const NodePtr &c = t->node;
+  auto nn = new_node(c->s, Kind::Distinct);
+  nn->kids.push_back(c);
+  for (int i = 0; i < n; ++i) nn->key_index.push_back(c->col_index_or_throw(cols[i]));
+  nn->names = c->names;
+  nn->types = c->types;
+  *out = wrap(nn);
+  CAPF_API_END
+}
+
+capf_status capf_table_distinct(capf_table *t, capf_table **out) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  std::vector<const char *> cols;
+  for (auto &nm : t->node->names) cols.push_back(nm.c_str());
+  capf_status st = capf_table_distinct_cols(t, (int32_t)cols.size(), cols.data(), out);
+  if (st != CAPF_OK) return st;
+  CAPF_API_END
+}
+
+capf_status capf_table_group(capf_table *t, int32_t n_by, const char *const *by_cols,
+                             int32_t n_aggs, const int32_t *agg_kinds,
+                             const capf_expr *agg_args, const int32_t *agg_distinct,
+                             const char *const *agg_names, capf_table **out) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(out, "out");
+  const NodePtr &c = t->node;
+  auto nn = new_node(c->s, Kind::Group);
+  nn->kids.push_back(c);
+  for (int i = 0; i < n_by; ++i) {
+    int idx = c->col_index_or_throw(by_cols[i]);
+    nn->key_index.push_back(idx);
+    nn->names.push_back(c->names[idx]);
+    nn->types.push_back(c->types[idx]);
+  }
+  for (int i = 0; i < n_aggs; ++i) {
+    AggSpec a;
+    a.kind = agg_kinds[i];
+    a.distinct = agg_distinct && agg_distinct[i];
+    a.name = agg_names[i];
+    if (a.kind < CAPF_AGG_COUNT_STAR || a.kind > CAPF_AGG_AVG) illegal("bad aggregator kind");
+    if (a.kind == CAPF_AGG_COUNT_STAR) {
+      a.out_type = Type::Int64;
+    } else {
+      a.arg = Program::from_c(&agg_args[i]);
+      Type at = infer_type(a.arg, c->names, c->types);
+      if (a.distinct && a.kind != CAPF_AGG_COUNT)
+        not_impl("DISTINCT modifier on aggregator other than count");
+      switch (a.kind) {
+        case CAPF_AGG_COUNT: a.out_type = Type::Int64; break;
+        case CAPF_AGG_SUM:
+        case CAPF_AGG_AVG:
+          // Avg's type signature is the input type (Expr.scala:1058-1066);
+          // Flink's AVG on LONG returns LONG.
+          if (at == Type::String || at == Type::Bool) not_impl("sum/avg of non-numeric");
+          a.out_type = at;
+          break;
+        case CAPF_AGG_MIN:
+        case CAPF_AGG_MAX:
+          if (at == Type::String) not_impl("min/max of strings");
+          a.out_type = at;
+          break;
+      }
+    }
+    nn->names.push_back(a.name);
+    nn->types.push_back(a.out_type);
+    nn->aggs.push_back(std::move(a));
+  }
+  check_unique_names(nn->names);
+  *out = wrap(nn);
+  CAPF_API_END
+}
+
+capf_status capf_table_with_columns(capf_table *t, int32_t n, const capf_expr *exprs,
+                                    const char *const *names, capf_table **out) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(out, "out");
+  const NodePtr &c = t->node;
+  auto nn = new_node(c->s, Kind::WithColumns);
+  nn->kids.push_back(c);
+  nn->names = c->names;
+  nn->types = c->types;
+  for (int i = 0; i < n; ++i) {
+    Program p = Program::from_c(&exprs[i]);
+    Type ty = infer_type(p, c->names, c->types);
+    int idx = nn->col_index(names[i]);
+    if (idx < 0) {
+      nn->names.emplace_back(names[i]);
+      nn->types.push_back(ty);
+      idx = (int)nn->names.size() - 1;
+    } else {
+      nn->types[idx] = ty;
+    }
+    nn->exprs.push_back(std::move(p));
+    nn->target_index.push_back(idx);
+  }
+  *out = wrap(nn);
+  CAPF_API_END
+}
+
+capf_status capf_table_show(capf_table *t, int32_t rows) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  DataPtr d = materialize(t->node);
+  Session *s = t->node->s;
+  int64_t m = std::min<int64_t>(rows, d->nrows);
+  std::vector<std::vector<int64_t>> vals(d->cols.size(), std::vector<int64_t>(m));
+  std::vector<std::vector<uint8_t>> valid(d->cols.size(), std::vector<uint8_t>(m, 1));
+  for (size_t i = 0; i < d->cols.size(); ++i) {
+    auto &c = d->cols[i];
+    if (m == 0) continue;
+    if (c->type == Type::Null) {
+      std::fill(valid[i].begin(), valid[i].end(), 0);
+      continue;
+    }
+    std::vector<uint8_t> raw(type_width(c->type) * m);
+    HIP_CHECK(hipMemcpy(raw.data(), c->data->p, raw.size(), hipMemcpyDeviceToHost));
+    for (int64_t r = 0; r < m; ++r)
+      vals[i][r] = c->type == Type::Bool ? raw[r] : ((int64_t *)raw.data())[r];
+    if (c->valid) HIP_CHECK(hipMemcpy(valid[i].data(), c->valid->p, m, hipMemcpyDeviceToHost));
+  }
+  for (size_t i = 0; i < d->cols.size(); ++i) printf("%s%s", i ? " | " : "", t->node->names[i].c_str());
+  printf("\n");
+  for (int64_t r = 0; r < m; ++r) {
+    for (size_t i = 0; i < d->cols.size(); ++i) {
+      if (i) printf(" | ");
+      auto ty = d->cols[i]->type;
+      if (!valid[i][r]) {
+        printf("null");
+      } else if (ty == Type::Float64) {
+        double f;
+        memcpy(&f, &vals[i][r], 8);
+        printf("%g", f);
+      } else if (ty == Type::Bool) {
+        printf("%s", vals[i][r] ? "true" : "false");
+      } else if (ty == Type::String) {
+        std::lock_guard<std::mutex> g(s->str_mu);
+        printf("'%s'", vals[i][r] >= 0 && vals[i][r] < (int64_t)s->strings.size()
+                           ? s->strings[vals[i][r]].c_str() : "?");
+      } else {
+        printf("%lld", (long long)vals[i][r]);
+      }
+    }
+    printf("\n");
+  }
+  fflush(stdout);
+  CAPF_API_END
+}
+
+}  // extern "C"

@@ -1,0 +1,398 @@
+"""Cypher IR expressions used by the relational layer, and their lowering to
+the GPU expression program of the C-ABI.
+
+The classes mirror the okapi IR (okapi-ir/src/main/scala/org/opencypher/okapi/
+ir/api/expr/Expr.scala): the subset that FlinkSQLExprMapper can lower
+(flink-cypher/src/main/scala/org/opencypher/flink/impl/FlinkSQLExprMapper.scala:
+48-294).  `compile_program` is the counterpart of `asFlinkSQLExpr`:
+
+ * Var / HasLabel / HasType / StartNode / EndNode resolve to their physical
+   column (`expression_for`, CAPFFunctions.scala:63-73); a header expression
+   whose column is missing from the table lowers to a NULL literal;
+ * ElementProperty not in the header lowers to a NULL literal
+   (FlinkSQLExprMapper.scala:102-112);
+ * Param is substituted by its value (FlinkSQLExprMapper.scala:80);
+ * anything else raises NotImplementedException (:289-290).
+"""
+from dataclasses import dataclass, field
+from typing import Tuple
+
+# capf column types (include/capf_gpu.h)
+T_NULL, T_INT, T_FLOAT, T_BOOL, T_STRING = 0, 1, 2, 3, 4
+
+CT_TO_CAPF = {
+    "NULL": T_NULL, "INTEGER": T_INT, "FLOAT": T_FLOAT, "BOOLEAN": T_BOOL, "STRING": T_STRING,
+    "NODE": T_INT, "RELATIONSHIP": T_INT, "ANY": T_NULL,
+}
+CAPF_TO_CT = {T_NULL: "NULL", T_INT: "INTEGER", T_FLOAT: "FLOAT", T_BOOL: "BOOLEAN", T_STRING: "STRING"}
+
+# opcodes
+OP_COL, OP_LIT_INT, OP_LIT_FLOAT, OP_LIT_BOOL, OP_LIT_STRING, OP_LIT_NULL = 1, 2, 3, 4, 5, 6
+OP_EQ, OP_NEQ, OP_LT, OP_LE, OP_GT, OP_GE = 10, 11, 12, 13, 14, 15
+OP_NOT, OP_AND, OP_OR, OP_IS_NULL, OP_IS_NOT_NULL = 20, 21, 22, 23, 24
+OP_ADD, OP_SUB, OP_MUL, OP_DIV, OP_MOD, OP_NEG = 30, 31, 32, 33, 34, 35
+OP_TO_FLOAT, OP_TO_INTEGER, OP_COALESCE = 40, 41, 50
+
+# aggregators
+AGG_COUNT_STAR, AGG_COUNT, AGG_SUM, AGG_MIN, AGG_MAX, AGG_AVG = 0, 1, 2, 3, 4, 5
+
+
+class Expr:
+    children: Tuple = ()
+
+    def name(self):
+        return str(self)
+
+
+@dataclass(frozen=True)
+class Var(Expr):
+    vname: str
+    ctype: str = field(default="ANY", compare=False)
+
+    def __str__(self):
+        return self.vname
+
+
+@dataclass(frozen=True)
+class ElementProperty(Expr):
+    owner: Var
+    key: str
+    ctype: str = field(default="ANY", compare=False)
+
+    def __str__(self):
+        return f"{self.owner}.{self.key}"
+
+
+Property = ElementProperty
+
+
+@dataclass(frozen=True)
+class HasLabel(Expr):
+    owner: Var
+    label: str
+
+    def __str__(self):
+        return f"{self.owner}:{self.label}"
+
+
+@dataclass(frozen=True)
+class HasType(Expr):
+    owner: Var
+    rel_type: str
+
+    def __str__(self):
+        return f"{self.owner}:{self.rel_type}"
+
+
+@dataclass(frozen=True)
+class StartNode(Expr):
+    rel: Var
+
+    def __str__(self):
+        return f"source({self.rel})"
+
+
+@dataclass(frozen=True)
+class EndNode(Expr):
+    rel: Var
+
+    def __str__(self):
+        return f"target({self.rel})"
+
+
+@dataclass(frozen=True)
+class IntegerLit(Expr):
+    v: int
+
+    def __str__(self):
+        return str(self.v)
+
+
+@dataclass(frozen=True)
+class FloatLit(Expr):
+    v: float
+
+    def __str__(self):
+        return repr(self.v)
+
+
+@dataclass(frozen=True)
+class StringLit(Expr):
+    v: str
+
+    def __str__(self):
+        return repr(self.v)
+
+
+@dataclass(frozen=True)
+class BoolLit(Expr):
+    v: bool
+
+    def __str__(self):
+        return "true" if self.v else "false"
+
+
+TrueLit = BoolLit(True)
+FalseLit = BoolLit(False)
+
+
+@dataclass(frozen=True)
+class NullLit(Expr):
+    ctype: str = "NULL"
+
+    def __str__(self):
+        return "null"
+
+
+@dataclass(frozen=True)
+class Param(Expr):
+    pname: str
+
+    def __str__(self):
+        return "$" + self.pname
+
+
+def _binary(name, sym):
+    def __str__(self):
+        return f"({self.lhs} {sym} {self.rhs})"
+
+    cls = dataclass(frozen=True)(type(name, (Expr,), {"__annotations__": {"lhs": Expr, "rhs": Expr},
+                                                       "__str__": __str__}))
+    return cls
+
+
+Equals = _binary("Equals", "=")
+LessThan = _binary("LessThan", "<")
+LessThanOrEqual = _binary("LessThanOrEqual", "<=")
+GreaterThan = _binary("GreaterThan", ">")
+GreaterThanOrEqual = _binary("GreaterThanOrEqual", ">=")
+Add = _binary("Add", "+")
+Subtract = _binary("Subtract", "-")
+Multiply = _binary("Multiply", "*")
+Divide = _binary("Divide", "/")
+Modulo = _binary("Modulo", "%")
+
+
+def _unary(name, fmt):
+    def __str__(self):
+        return fmt.format(self.expr)
+
+    return dataclass(frozen=True)(type(name, (Expr,), {"__annotations__": {"expr": Expr},
+                                                        "__str__": __str__}))
+
+
+Not = _unary("Not", "NOT {}")
+IsNull = _unary("IsNull", "{} IS NULL")
+IsNotNull = _unary("IsNotNull", "{} IS NOT NULL")
+ToFloat = _unary("ToFloat", "toFloat({})")
+ToInteger = _unary("ToInteger", "toInteger({})")
+Negate = _unary("Negate", "-{}")
+
+
+@dataclass(frozen=True)
+class Ands(Expr):
+    exprs: Tuple[Expr, ...]
+
+    def __init__(self, *exprs):
+        object.__setattr__(self, "exprs", tuple(exprs))
+
+    def __str__(self):
+        return "(" + " AND ".join(map(str, self.exprs)) + ")"
+
+
+@dataclass(frozen=True)
+class Ors(Expr):
+    exprs: Tuple[Expr, ...]
+
+    def __init__(self, *exprs):
+        object.__setattr__(self, "exprs", tuple(exprs))
+
+    def __str__(self):
+        return "(" + " OR ".join(map(str, self.exprs)) + ")"
+
+
+@dataclass(frozen=True)
+class Coalesce(Expr):
+    exprs: Tuple[Expr, ...]
+
+    def __init__(self, *exprs):
+        object.__setattr__(self, "exprs", tuple(exprs))
+
+    def __str__(self):
+        return "coalesce(" + ", ".join(map(str, self.exprs)) + ")"
+
+
+# ----------------------------------------------------------------- aggregators
+class Aggregator(Expr):
+    kind = -1
+    distinct = False
+
+
+@dataclass(frozen=True)
+class CountStar(Aggregator):
+    kind = AGG_COUNT_STAR
+
+    def __str__(self):
+        return "count(*)"
+
+
+@dataclass(frozen=True)
+class Count(Aggregator):
+    expr: Expr
+    distinct: bool = False
+    kind = AGG_COUNT
+
+    def __str__(self):
+        return f"count({'DISTINCT ' if self.distinct else ''}{self.expr})"
+
+
+@dataclass(frozen=True)
+class Sum(Aggregator):
+    expr: Expr
+    kind = AGG_SUM
+
+    def __str__(self):
+        return f"sum({self.expr})"
+
+
+@dataclass(frozen=True)
+class Min(Aggregator):
+    expr: Expr
+    kind = AGG_MIN
+
+    def __str__(self):
+        return f"min({self.expr})"
+
+
+@dataclass(frozen=True)
+class Max(Aggregator):
+    expr: Expr
+    kind = AGG_MAX
+
+    def __str__(self):
+        return f"max({self.expr})"
+
+
+@dataclass(frozen=True)
+class Avg(Aggregator):
+    expr: Expr
+    kind = AGG_AVG
+
+    def __str__(self):
+        return f"avg({self.expr})"
+
+
+# --------------------------------------------------------------- lowering
+_BIN_OPS = {
+    "Equals": OP_EQ, "LessThan": OP_LT, "LessThanOrEqual": OP_LE, "GreaterThan": OP_GT,
+    "GreaterThanOrEqual": OP_GE, "Add": OP_ADD, "Subtract": OP_SUB, "Multiply": OP_MUL,
+    "Divide": OP_DIV, "Modulo": OP_MOD,
+}
+_UN_OPS = {"Not": OP_NOT, "IsNull": OP_IS_NULL, "IsNotNull": OP_IS_NOT_NULL, "ToFloat": OP_TO_FLOAT,
+           "ToInteger": OP_TO_INTEGER, "Negate": OP_NEG}
+
+
+def resolve_column(expr, header, columns):
+    """Physical column of a header expression or None (→ NULL literal)."""
+    col = header.get(expr) if header is not None else None
+    if col is not None and col in columns:
+        return col
+    return None
+
+
+def compile_program(expr, header, columns, params=None, intern=None):
+    """Lower `expr` to (ops, iargs, fargs, names) for the C-ABI.
+
+    header: dict Expr -> physical column; columns: set of the table's columns;
+    intern: str -> int64 code (session string dictionary).
+    """
+    params = params or {}
+    ops, ia, fa, names = [], [], [], []
+    name_idx = {}
+
+    def emit(op, i=0, f=0.0):
+        ops.append(op)
+        ia.append(int(i))
+        fa.append(float(f))
+
+    def lit(v):
+        if v is None:
+            emit(OP_LIT_NULL, T_NULL)
+        elif isinstance(v, bool):
+            emit(OP_LIT_BOOL, 1 if v else 0)
+        elif isinstance(v, int):
+            emit(OP_LIT_INT, v)
+        elif isinstance(v, float):
+            emit(OP_LIT_FLOAT, 0, v)
+        elif isinstance(v, str):
+            if intern is None:
+                raise ValueError("string literal without a string dictionary")
+            emit(OP_LIT_STRING, intern(v))
+        else:
+            from ._lib import NotImplementedException
+            raise NotImplementedException(f"literal {v!r} of type {type(v).__name__}")
+
+    def col(name):
+        if name not in name_idx:
+            name_idx[name] = len(names)
+            names.append(name)
+        emit(OP_COL, name_idx[name])
+
+    def go(e):
+        cls = type(e).__name__
+        if isinstance(e, (Var, HasLabel, HasType, StartNode, EndNode, ElementProperty)):
+            c = resolve_column(e, header, columns)
+            if c is None:
+                ct = getattr(e, "ctype", "BOOLEAN" if isinstance(e, (HasLabel, HasType)) else "INTEGER")
+                emit(OP_LIT_NULL, CT_TO_CAPF.get(ct, T_NULL))
+            else:
+                col(c)
+            return
+        c = resolve_column(e, header, columns) if header is not None and e in header else None
+        if c is not None:  # an already-projected expression (e.g. an alias column)
+            col(c)
+            return
+        if isinstance(e, IntegerLit):
+            emit(OP_LIT_INT, e.v)
+        elif isinstance(e, FloatLit):
+            emit(OP_LIT_FLOAT, 0, e.v)
+        elif isinstance(e, BoolLit):
+            emit(OP_LIT_BOOL, 1 if e.v else 0)
+        elif isinstance(e, StringLit):
+            lit(e.v)
+        elif isinstance(e, NullLit):
+            emit(OP_LIT_NULL, CT_TO_CAPF.get(e.ctype, T_NULL))
+        elif isinstance(e, Param):
+            lit(params[e.pname])
+        elif cls in _BIN_OPS:
+            go(e.lhs)
+            go(e.rhs)
+            emit(_BIN_OPS[cls])
+        elif cls in _UN_OPS:
+            go(e.expr)
+            emit(_UN_OPS[cls])
+        elif isinstance(e, Ands):
+            if not e.exprs:
+                emit(OP_LIT_BOOL, 1)
+                return
+            for x in e.exprs:
+                go(x)
+            emit(OP_AND, len(e.exprs))
+        elif isinstance(e, Ors):
+            if not e.exprs:
+                emit(OP_LIT_BOOL, 0)
+                return
+            for x in e.exprs:
+                go(x)
+            emit(OP_OR, len(e.exprs))
+        elif isinstance(e, Coalesce):
+            for x in e.exprs:
+                go(x)
+            emit(OP_COALESCE, len(e.exprs))
+        else:
+            from ._lib import NotImplementedException
+            raise NotImplementedException(
+                f"No support for converting Cypher expression {e} to a GPU expression")
+
+    go(expr)
+    return ops, ia, fa, names

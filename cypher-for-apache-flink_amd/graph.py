@@ -1,0 +1,205 @@
+"""Element tables and the scan graph over any Table[T] backend.
+
+Mirrors the okapi-relational graph layer that sits directly above the Table SPI:
+ * element tables — one node table per label combination, one relationship
+   table per type, all ids int64 (CAPFElementTable.create,
+   flink-cypher/.../api/io/CAPFTable.scala:76-83; CAPFScanGraphFactory,
+   flink-cypher-testing/.../support/creation/graphs/CAPFScanGraphFactory.scala:24-158);
+ * ScanGraph.scanOperator — pick the element tables whose label set ⊇ the
+   requested labels (okapi-api/.../api/graph/Pattern.scala:95-111), align them
+   to the var's header with constant label columns and NULL property columns
+   (RelationalPlanner.scala:447-515) and UNION ALL them
+   (okapi-relational/.../impl/graph/ScanGraph.scala:59-105).
+
+A label constraint in a pattern is therefore a table-selection decision, not
+a row predicate.
+
+The backend `session` only needs `table(columns)` and `empty(names, types)`;
+tables need the Table[T] methods.  The same code drives GpuTable (product)
+and the numpy oracle table (tests).
+"""
+from dataclasses import dataclass, field
+from typing import Dict, FrozenSet, List, Tuple
+
+from .expr import (CT_TO_CAPF, T_BOOL, T_FLOAT, T_INT, T_NULL, T_STRING, BoolLit, ElementProperty,
+                   EndNode, HasLabel, HasType, NullLit, StartNode, Var)
+from .header import RecordHeader
+
+
+@dataclass
+class GraphData:
+    """An in-memory property graph (okapi-testing InMemoryTestGraph)."""
+    nodes: List[Tuple[int, FrozenSet[str], Dict]] = field(default_factory=list)
+    rels: List[Tuple[int, int, int, str, Dict]] = field(default_factory=list)
+
+
+def ctype_of(v):
+    if isinstance(v, bool):
+        return "BOOLEAN"
+    if isinstance(v, int):
+        return "INTEGER"
+    if isinstance(v, float):
+        return "FLOAT"
+    if isinstance(v, str):
+        return "STRING"
+    raise NotImplementedError(f"property value {v!r} of type {type(v).__name__}")
+
+
+def _join_type(a, b):
+    if a is None:
+        return b
+    if b is None or a == b:
+        return a
+    if {a, b} == {"INTEGER", "FLOAT"}:
+        return "FLOAT"
+    raise NotImplementedError(f"property with conflicting types {a} / {b}")
+
+
+@dataclass
+class ElementTable:
+    kind: str                 # "node" | "rel"
+    labels: FrozenSet[str]    # label combination (node) or {type} (rel)
+    table: object             # backend table
+    props: Dict[str, str]     # property key -> CypherType name
+    # physical column names inside `table`
+    id_col: str = "id"
+    src_col: str = "source"
+    dst_col: str = "target"
+
+    def prop_col(self, key):
+        return "p_" + key
+
+
+class ScanGraph:
+    def __init__(self, session, node_tables, rel_tables):
+        self.session = session
+        self.node_tables = list(node_tables)
+        self.rel_tables = list(rel_tables)
+        # ScanGraph.validate: one table per label combination / rel type
+        # (okapi-relational/.../impl/graph/ScanGraph.scala:115-143)
+        combos = [t.labels for t in self.node_tables]
+        if len(combos) != len(set(combos)):
+            raise ValueError("more than one node table per label combination")
+        types = [t.labels for t in self.rel_tables]
+        if len(types) != len(set(types)):
+            raise ValueError("more than one relationship table per type")
+
+    @property
+    def rel_types(self):
+        return sorted(next(iter(t.labels)) for t in self.rel_tables)
+
+    @staticmethod
+    def from_data(session, g: GraphData):
+        """CAPFScanGraphFactory: one element table per label combination / type."""
+        by_combo, by_type = {}, {}
+        for nid, labels, props in g.nodes:
+            by_combo.setdefault(frozenset(labels), []).append((nid, props))
+        for rid, s, t, typ, props in g.rels:
+            by_type.setdefault(typ, []).append((rid, s, t, props))
+        node_tables, rel_tables = [], []
+        for combo, rows in sorted(by_combo.items(), key=lambda kv: sorted(kv[0])):
+            keys = {}
+            for _, props in rows:
+                for k, v in props.items():
+                    if v is not None:
+                        keys[k] = _join_type(keys.get(k), ctype_of(v))
+            cols = [("id", T_INT, [r[0] for r in rows], None)]
+            for k in sorted(keys):
+                vals = [_coerce(r[1].get(k), keys[k]) for r in rows]
+                cols.append(("p_" + k, CT_TO_CAPF[keys[k]], vals, None))
+            node_tables.append(ElementTable("node", combo, session.table(cols, nrows=len(rows)), keys))
+        for typ, rows in sorted(by_type.items()):
+            keys = {}
+            for *_, props in rows:
+                for k, v in props.items():
+                    if v is not None:
+                        keys[k] = _join_type(keys.get(k), ctype_of(v))
+            cols = [("id", T_INT, [r[0] for r in rows], None),
+                    ("source", T_INT, [r[1] for r in rows], None),
+                    ("target", T_INT, [r[2] for r in rows], None)]
+            for k in sorted(keys):
+                vals = [_coerce(r[3].get(k), keys[k]) for r in rows]
+                cols.append(("p_" + k, CT_TO_CAPF[keys[k]], vals, None))
+            rel_tables.append(ElementTable("rel", frozenset([typ]), session.table(cols, nrows=len(rows)), keys))
+        return ScanGraph(session, node_tables, rel_tables)
+
+    # ------------------------------------------------------------ scans
+    def node_scan(self, var_name, labels=()):
+        """ScanGraph.scanOperator for NodePattern(CTNode(labels))."""
+        want = frozenset(labels)
+        sel = [t for t in self.node_tables if want <= t.labels]
+        v = Var(var_name, "NODE")
+        all_labels = sorted(set().union(*[t.labels for t in sel])) if sel else sorted(want)
+        props = {}
+        for t in sel:
+            for k, ct in t.props.items():
+                props[k] = _join_type(props.get(k), ct)
+        header = {v: var_name}
+        for l in all_labels:
+            header[HasLabel(v, l)] = f"{var_name}:{l}"
+        for k in sorted(props):
+            header[ElementProperty(v, k, props[k])] = f"{var_name}.{k}"
+        h = RecordHeader(header)
+        order = [header[e] for e in header]
+        types = [T_INT] + [T_BOOL] * len(all_labels) + [CT_TO_CAPF[props[k]] for k in sorted(props)]
+        return self._align_union(sel, h, order, types, v, all_labels, props, rel=False)
+
+    def rel_scan(self, var_name, types=()):
+        """ScanGraph.scanOperator for RelationshipPattern(CTRelationship(types))."""
+        want = set(types)
+        sel = [t for t in self.rel_tables if not want or (t.labels & want)]
+        r = Var(var_name, "RELATIONSHIP")
+        all_types = sorted(set().union(*[t.labels for t in sel])) if sel else sorted(want)
+        props = {}
+        for t in sel:
+            for k, ct in t.props.items():
+                props[k] = _join_type(props.get(k), ct)
+        header = {r: var_name, StartNode(r): f"source({var_name})", EndNode(r): f"target({var_name})"}
+        for ty in all_types:
+            header[HasType(r, ty)] = f"{var_name}:{ty}"
+        for k in sorted(props):
+            header[ElementProperty(r, k, props[k])] = f"{var_name}.{k}"
+        h = RecordHeader(header)
+        order = [header[e] for e in header]
+        tys = [T_INT, T_INT, T_INT] + [T_BOOL] * len(all_types) + [CT_TO_CAPF[props[k]] for k in sorted(props)]
+        return self._align_union(sel, h, order, tys, r, all_types, props, rel=True)
+
+    def _align_union(self, sel, h, order, types, v, flags, props, rel):
+        from .planner import Planned
+        if not sel:
+            return Planned(self.session.empty(order, types), h)
+        name = v.vname
+        parts = []
+        for t in sel:
+            cols = [(t.id_col, name)]
+            if rel:
+                cols += [(t.src_col, f"source({name})"), (t.dst_col, f"target({name})")]
+            present = set()
+            for k in sorted(props):
+                if k in t.props:
+                    cols.append((t.prop_col(k), f"{name}.{k}"))
+                    present.add(k)
+            tab = t.table.select(*cols)
+            adds = []
+            for f in flags:
+                e = HasType(v, f) if rel else HasLabel(v, f)
+                adds.append((BoolLit(f in t.labels), h.column(e)))
+            for k in sorted(props):
+                if k not in present:
+                    adds.append((NullLit(props[k]), f"{name}.{k}"))
+            if adds:
+                tab = tab.withColumns(*adds, header=RecordHeader({}), params={})
+            tab = tab.select(*order)
+            parts.append(tab)
+        out = parts[0]
+        for p in parts[1:]:
+            out = out.unionAll(p)
+        return Planned(out, h)
+
+
+def _coerce(v, ct):
+    if v is None:
+        return None
+    if ct == "FLOAT":
+        return float(v)
+    return v

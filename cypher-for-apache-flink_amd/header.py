@@ -1,0 +1,86 @@
+"""RecordHeader: the expression → physical column mapping of a relational table.
+
+Mirrors the parts of okapi's RecordHeader the Table SPI consumes
+(okapi-relational/src/main/scala/org/opencypher/okapi/relational/impl/table/
+RecordHeader.scala:68-455): `column(expr)`, `ownedBy(var)` (used by
+Table.group, FlinkTable.scala:129-135), `startNodeFor`/`endNodeFor`, and
+column naming derived from the expression text (:299-318).
+"""
+from .expr import ElementProperty, EndNode, HasLabel, HasType, StartNode, Var
+
+
+def owner_of(e):
+    if isinstance(e, (ElementProperty, HasLabel, HasType)):
+        return e.owner
+    if isinstance(e, (StartNode, EndNode)):
+        return e.rel
+    return None
+
+
+class RecordHeader:
+    def __init__(self, mapping=None):
+        self._m = dict(mapping or {})
+
+    # dict-like access used by expression lowering
+    def get(self, expr, default=None):
+        return self._m.get(expr, default)
+
+    def __contains__(self, expr):
+        return expr in self._m
+
+    def __iter__(self):
+        return iter(self._m)
+
+    def items(self):
+        return self._m.items()
+
+    def column(self, expr):
+        try:
+            return self._m[expr]
+        except KeyError:
+            raise KeyError(f"{expr} not in header {list(map(str, self._m))}")
+
+    @property
+    def expressions(self):
+        return list(self._m)
+
+    @property
+    def columns(self):
+        seen, out = set(), []
+        for c in self._m.values():
+            if c not in seen:
+                seen.add(c)
+                out.append(c)
+        return out
+
+    def owned_by(self, var):
+        return [e for e in self._m if e == var or owner_of(e) == var]
+
+    def vars(self):
+        return [e for e in self._m if isinstance(e, Var)]
+
+    def start_node_for(self, rel):
+        return self.column(StartNode(rel))
+
+    def end_node_for(self, rel):
+        return self.column(EndNode(rel))
+
+    def with_expr(self, expr, column):
+        m = dict(self._m)
+        m[expr] = column
+        return RecordHeader(m)
+
+    def union(self, other):
+        m = dict(self._m)
+        m.update(other._m)
+        return RecordHeader(m)
+
+    def without(self, exprs):
+        drop = set(exprs)
+        return RecordHeader({e: c for e, c in self._m.items() if e not in drop})
+
+    def renamed(self, fn):
+        return RecordHeader({e: fn(e, c) for e, c in self._m.items()})
+
+    def __repr__(self):
+        return "RecordHeader(" + ", ".join(f"{e}->{c}" for e, c in self._m.items()) + ")"

@@ -1,0 +1,417 @@
+"""Relational planning of MATCH patterns onto any Table[T] backend.
+
+This is the caller side of the drop-in boundary: a restatement of the okapi
+planning that produces the Table-operation sequences the backend executes —
+  * LogicalPlanner.planComponentPattern / planExpansions
+    (okapi-logical/.../impl/LogicalPlanner.scala:309-433): node scans, then one
+    Expand / ExpandInto / BoundedVarLengthExpand per relationship in pattern
+    order, WHERE conjuncts as one Filter each (:211-227);
+  * RelationalPlanner Expand / ExpandInto
+    (okapi-relational/.../impl/planning/RelationalPlanner.scala:130-189);
+  * DirectedVarLengthExpandPlanner
+    (okapi-relational/.../impl/planning/VarLengthExpandPlanner.scala:82-259);
+  * relationship uniqueness NOT(r_i = r_j) added per MATCH clause by the
+    front end (okapi-ir/.../impl/parse/CypherParser.scala:72);
+  * projections / aggregation / DISTINCT / ORDER BY / SKIP / LIMIT on top
+    (Table.withColumns / group / distinct / orderBy / skip / limit).
+
+Queries are given as small pattern objects (the Cypher parser and IR builder
+are out of scope: the front end stays unchanged in the real deployment).
+"""
+from dataclasses import dataclass, field
+from itertools import combinations
+from typing import List, Optional, Sequence, Tuple
+
+from .expr import (Aggregator, Ands, BoolLit, ElementProperty, EndNode, Equals, Expr, HasLabel,
+                   HasType, Not, NullLit, StartNode, TrueLit, Var)
+from .header import RecordHeader, owner_of
+
+
+@dataclass
+class Planned:
+    """A relational operator's result: backend table + record header."""
+    table: object
+    header: RecordHeader
+
+
+# ------------------------------------------------------------- query model
+@dataclass
+class NodeP:
+    name: str
+    labels: Tuple[str, ...] = ()
+
+
+@dataclass
+class RelP:
+    name: str
+    src: str
+    dst: str
+    types: Tuple[str, ...] = ()
+    direction: str = "out"          # out | in | both
+    length: Optional[Tuple[int, int]] = None  # (lower, upper) for *l..u
+
+
+@dataclass
+class Match:
+    nodes: List[NodeP]
+    rels: List[RelP] = field(default_factory=list)
+    where: List[Expr] = field(default_factory=list)
+
+
+@dataclass
+class Stage:
+    """A WITH / RETURN projection: items = [(alias, Expr | Aggregator)]."""
+    items: List[Tuple[str, Expr]]
+    distinct: bool = False
+    where: List[Expr] = field(default_factory=list)
+    order_by: List[Tuple[str, str]] = field(default_factory=list)  # (alias, asc|desc)
+    skip: Optional[int] = None
+    limit: Optional[int] = None
+
+
+@dataclass
+class Query:
+    matches: List[Match]
+    stages: List[Stage]
+
+
+# ------------------------------------------------------------- relational ops
+def _rename_disjoint(left: Planned, right: Planned) -> Planned:
+    """withDisjointColumnNames (RelationalPlanner.scala:366-368, 524-538)."""
+    lcols = set(left.header.columns) | set(left.table.physicalColumns)
+    clash = [c for c in right.table.physicalColumns if c in lcols]
+    if not clash:
+        return right
+    ren = {}
+    taken = lcols | set(right.table.physicalColumns)
+    for c in clash:
+        k = 1
+        while f"{c}_{k}" in taken:
+            k += 1
+        ren[c] = f"{c}_{k}"
+        taken.add(ren[c])
+    tab = right.table.select(*[(c, ren.get(c, c)) for c in right.table.physicalColumns])
+    return Planned(tab, right.header.renamed(lambda e, c: ren.get(c, c)))
+
+
+def join(left: Planned, right: Planned, pairs: Sequence[Tuple[Expr, Expr]], join_type="inner") -> Planned:
+    right = _rename_disjoint(left, right)
+    cols = [(left.header.column(a), right.header.column(b)) for a, b in pairs]
+    return Planned(left.table.join(right.table, join_type, *cols), left.header.union(right.header))
+
+
+def filter_(op: Planned, expr: Expr, params=None) -> Planned:
+    if expr == TrueLit or (isinstance(expr, Ands) and not expr.exprs):
+        return op
+    return Planned(op.table.filter(expr, op.header, params or {}), op.header)
+
+
+def union_all(a: Planned, b: Planned) -> Planned:
+    """TabularUnionAll: align the right side's columns to the left header."""
+    exprs = a.header.expressions
+    missing = [e for e in exprs if e not in b.header] + [e for e in b.header.expressions if e not in a.header]
+    if missing:
+        raise ValueError(f"union of differing headers: {missing}")
+    tb = b.table.select(*[(b.header.column(e), a.header.column(e)) for e in exprs])
+    ta = a.table.select(*[a.header.column(e) for e in exprs])
+    return Planned(ta.unionAll(tb), RecordHeader({e: a.header.column(e) for e in exprs}))
+
+
+def add_into(op: Planned, items: Sequence[Tuple[Expr, Expr]], params=None) -> Planned:
+    """AddInto(expr -> target expr) as withColumns (RelationalOperator.scala:219-264)."""
+    h = op.header
+    cols = []
+    for src, tgt in items:
+        col = h.get(tgt) or _col_name(tgt)
+        cols.append((src, col))
+        h = h.with_expr(tgt, col)
+    return Planned(op.table.withColumns(*cols, header=op.header, params=params or {}), h)
+
+
+def _col_name(e):
+    return str(e)
+
+
+def alias_var(op: Planned, old: Var, new: Var) -> Planned:
+    """Alias a relationship var's columns to a new var (edgeScan as e_i)."""
+    cols, m = [], {}
+    for e in op.header.owned_by(old):
+        c = op.header.column(e)
+        ne = _rewrite_owner(e, old, new)
+        nc = str(ne)
+        cols.append((c, nc))
+        m[ne] = nc
+    return Planned(op.table.select(*cols), RecordHeader(m))
+
+
+def _rewrite_owner(e, old, new):
+    if e == old:
+        return new
+    if isinstance(e, ElementProperty):
+        return ElementProperty(new, e.key, e.ctype)
+    if isinstance(e, HasLabel):
+        return HasLabel(new, e.label)
+    if isinstance(e, HasType):
+        return HasType(new, e.rel_type)
+    if isinstance(e, StartNode):
+        return StartNode(new)
+    if isinstance(e, EndNode):
+        return EndNode(new)
+    raise ValueError(e)
+
+
+# ------------------------------------------------------------- expand
+def expand(graph, source: Var, rel: RelP, target: Var, src_op: Planned, tgt_op: Planned,
+           direction: str) -> Planned:
+    """RelationalPlanner Expand (RelationalPlanner.scala:130-165)."""
+    r = Var(rel.name, "RELATIONSHIP")
+    second = graph.rel_scan(rel.name, rel.types)
+    start, end = StartNode(r), EndNode(r)
+    if direction == "out":
+        tmp = join(src_op, second, [(source, start)])
+        return join(tmp, tgt_op, [(end, target)])
+    if direction == "in":
+        tmp = join(tgt_op, second, [(target, end)])
+        return join(tmp, src_op, [(start, source)])
+    # undirected: outgoing ∪ incoming-without-loops
+    tmp_out = join(src_op, second, [(source, start)])
+    outgoing = join(tmp_out, tgt_op, [(end, target)])
+    no_loops = filter_(second, Not(Equals(start, end)))
+    tmp_in = join(src_op, no_loops, [(source, end)])
+    incoming = join(tmp_in, tgt_op, [(start, target)])
+    return union_all(outgoing, incoming)
+
+
+def expand_into(graph, source: Var, rel: RelP, target: Var, in_op: Planned, direction: str) -> Planned:
+    """RelationalPlanner ExpandInto (RelationalPlanner.scala:167-189)."""
+    r = Var(rel.name, "RELATIONSHIP")
+    rels = graph.rel_scan(rel.name, rel.types)
+    start, end = StartNode(r), EndNode(r)
+    if direction in ("out", "in"):
+        if direction == "in":
+            source, target = target, source
+        return join(in_op, rels, [(source, start), (target, end)])
+    outgoing = join(in_op, rels, [(source, start), (target, end)])
+    incoming = join(in_op, graph.rel_scan(rel.name, rel.types), [(target, start), (source, end)])
+    return union_all(outgoing, incoming)
+
+
+def var_length_expand(graph, source: Var, rel: RelP, target: Var, src_op: Planned, tgt_op: Planned,
+                      is_expand_into: bool) -> Planned:
+    """DirectedVarLengthExpandPlanner.plan (VarLengthExpandPlanner.scala:246-259)."""
+    lower, upper = rel.length
+    edge = Var(rel.name, "RELATIONSHIP")
+    edge_scan = graph.rel_scan(rel.name, rel.types)
+
+    def seg(i):
+        return Var(f"{rel.name}_{i}", "RELATIONSHIP")
+
+    existing_rels = [e for e in src_op.header.vars() if e.ctype == "RELATIONSHIP"]
+
+    def iso(new, cands):
+        return Ands(*[Not(Equals(e, new)) for e in cands]) if cands else TrueLit
+
+    paths = []
+    # init (:82-97)
+    e1 = seg(1)
+    step = alias_var(edge_scan, edge, e1)
+    cur = filter_(join(src_op, step, [(source, StartNode(e1))]), iso(e1, existing_rels))
+    edges = [e1]
+    if upper >= 1:
+        paths.append((cur, list(edges)))
+    # expand(i) (:107-135)
+    for i in range(2, upper + 1):
+        ei = seg(i)
+        step = alias_var(edge_scan, edge, ei)
+        cur = filter_(join(cur, step, [(EndNode(edges[-1]), StartNode(ei))]), iso(ei, edges))
+        edges.append(ei)
+        paths.append((cur, list(edges)))
+    paths = [(p, es) for p, es in paths if len(es) >= lower]
+
+    # addTargetOps (:218-229)
+    def add_target(p, last):
+        if is_expand_into:
+            return filter_(p, Equals(target, EndNode(last)))
+        return join(p, tgt_op, [(EndNode(last), target)])
+
+    with_targets = [add_target(p, es[-1]) for p, es in paths]
+    if lower == 0:
+        with_targets.append(_copy_element(src_op, source, target, tgt_op))
+    if not with_targets:
+        raise ValueError("empty var-length range")
+    return _finalize(with_targets)
+
+
+def _copy_element(src_op, source, target, tgt_op):
+    """copyElement: zero-length paths (VarLengthExpandPlanner.scala:180-205)."""
+    items = []
+    for e in tgt_op.header.owned_by(target):
+        if e == target:
+            items.append((source, target))
+        elif isinstance(e, HasLabel):
+            s = HasLabel(source, e.label)
+            items.append((s if s in src_op.header else BoolLit(False), e))
+        elif isinstance(e, ElementProperty):
+            s = ElementProperty(source, e.key, e.ctype)
+            items.append((s if s in src_op.header else NullLit(e.ctype), e))
+    return add_into(src_op, items)
+
+
+def _finalize(paths: List[Planned]) -> Planned:
+    """Null-pad shorter paths to the widest header and UNION ALL (:145-170)."""
+    widest = max(paths, key=lambda p: len(p.header.columns)).header
+    aligned = []
+    for p in paths:
+        missing = [e for e in widest.expressions if e not in p.header]
+        if missing:
+            p = add_into(p, [(NullLit(_ctype(e)), e) for e in missing])
+        aligned.append(p)
+    out = aligned[0]
+    for p in aligned[1:]:
+        out = union_all(out, p)
+    return out
+
+
+def _ctype(e):
+    if isinstance(e, (HasLabel, HasType)):
+        return "BOOLEAN"
+    if isinstance(e, ElementProperty):
+        return e.ctype
+    return "INTEGER"
+
+
+# ------------------------------------------------------------- pattern planning
+def plan_match(graph, m: Match, prev: Optional[Planned], params=None) -> Planned:
+    """planComponentPattern + planExpansions + planFilter for one MATCH clause."""
+    rels = []
+    for r in m.rels:  # normalise <-[r]- to -[r]->
+        if r.direction == "in":
+            r = RelP(r.name, r.dst, r.src, r.types, "out", r.length)
+        rels.append(r)
+    labels = {}
+    for n in m.nodes:
+        labels.setdefault(n.name, set()).update(n.labels)
+    node_names = [n.name for n in m.nodes]
+    for r in rels:
+        for v in (r.src, r.dst):
+            if v not in labels:
+                labels[v] = set()
+                node_names.append(v)
+    node_names = list(dict.fromkeys(node_names))
+    bound = set(v.vname for v in prev.header.vars()) if prev is not None else set()
+    plans = []  # (set of vars, Planned)
+    solved = [v for v in node_names if v in bound]
+    # label constraints on already-bound nodes are row predicates on their
+    # label columns (their scans already happened)
+    extra_where = [HasLabel(Var(v, "NODE"), l) for v in solved for l in sorted(labels[v])]
+    if prev is not None and solved:
+        plans.append((set(bound), prev))
+        remaining = [v for v in node_names if v not in bound]
+    else:
+        first = node_names[0]
+        scan = graph.node_scan(first, sorted(labels[first]))
+        if prev is not None:
+            scan = Planned(prev.table.join(scan.table, "cross"), prev.header.union(scan.header))
+            plans.append((set(bound) | {first}, scan))
+        else:
+            plans.append(({first}, scan))
+        remaining = node_names[1:]
+    for v in remaining:
+        plans.append(({v}, graph.node_scan(v, sorted(labels[v]))))
+
+    for r in rels:
+        si = next(i for i, (vs, _) in enumerate(plans) if r.src in vs)
+        ti = next(i for i, (vs, _) in enumerate(plans) if r.dst in vs)
+        s, t = Var(r.src, "NODE"), Var(r.dst, "NODE")
+        if r.length is not None:
+            if si == ti:
+                op = var_length_expand(graph, s, r, t, plans[si][1], plans[si][1], True)
+                plans[si] = (plans[si][0] | {r.name}, op)
+            else:
+                op = var_length_expand(graph, s, r, t, plans[si][1], plans[ti][1], False)
+                vs = plans[si][0] | plans[ti][0] | {r.name}
+                plans = [p for i, p in enumerate(plans) if i not in (si, ti)] + [(vs, op)]
+        elif si == ti:
+            # a cyclic relationship (a)-[r]-(a) is planned as a directed
+            # ExpandInto (LogicalPlanner.scala:407-418, CyclicRelationship)
+            d = "both" if r.direction == "both" and r.src != r.dst else "out"
+            op = expand_into(graph, s, r, t, plans[si][1], d)
+            plans[si] = (plans[si][0] | {r.name}, op)
+        else:
+            op = expand(graph, s, r, t, plans[si][1], plans[ti][1], r.direction)
+            vs = plans[si][0] | plans[ti][0] | {r.name}
+            plans = [p for i, p in enumerate(plans) if i not in (si, ti)] + [(vs, op)]
+    # disconnected components: cartesian products
+    op = plans[0][1]
+    for _, p in plans[1:]:
+        p = _rename_disjoint(op, p)
+        op = Planned(op.table.join(p.table, "cross"), op.header.union(p.header))
+    # WHERE conjuncts, then front-end uniqueness predicates, one Filter each
+    fixed = [Var(r.name, "RELATIONSHIP") for r in rels if r.length is None]
+    preds = list(m.where) + extra_where + [Not(Equals(a, b)) for a, b in combinations(fixed, 2)]
+    for p in preds:
+        op = filter_(op, p, params)
+    return op
+
+
+def plan_stage(op: Planned, st: Stage, params=None) -> Planned:
+    aggs = [(a, e) for a, e in st.items if isinstance(e, Aggregator)]
+    projs = [(a, e) for a, e in st.items if not isinstance(e, Aggregator)]
+    # project non-aggregate items into alias vars (RelationalPlanner Add → withColumns)
+    h = op.header
+    adds, new_h = [], {}
+    for alias, e in projs:
+        v = Var(alias)
+        col = "__" + alias
+        adds.append((e, col))
+        new_h[v] = col
+    # aggregation arguments are evaluated against the incoming header
+    if adds:
+        tab = op.table.withColumns(*adds, header=h, params=params or {})
+        h2 = h
+        for v, c in new_h.items():
+            h2 = h2.with_expr(v, c)
+        op = Planned(tab, h2)
+    if aggs:
+        group_vars = [Var(a) for a, _ in projs]
+        agg_cols = {"__" + a: e for a, e in aggs}
+        tab = op.table.group(group_vars, agg_cols, header=op.header, params=params or {})
+        hh = {Var(a): "__" + a for a, _ in st.items}
+        op = Planned(tab, RecordHeader(hh))
+    else:
+        cols = ["__" + a for a, _ in projs]
+        op = Planned(op.table.select(*cols), RecordHeader({Var(a): "__" + a for a, _ in projs}))
+    if st.distinct:
+        op = Planned(op.table.distinct(), op.header)
+    for p in st.where:
+        op = filter_(op, p, params)
+    if st.order_by:
+        items = [(Var(a), o) for a, o in st.order_by]
+        op = Planned(op.table.orderBy(*items, header=op.header, params=params or {}), op.header)
+    if st.skip is not None:
+        op = Planned(op.table.skip(st.skip), op.header)
+    if st.limit is not None:
+        op = Planned(op.table.limit(st.limit), op.header)
+    return op
+
+
+def plan_query(graph, q: Query, params=None) -> Planned:
+    op = None
+    for m in q.matches:
+        op = plan_match(graph, m, op, params)
+    for st in q.stages:
+        op = plan_stage(op, st, params)
+    return op
+
+
+def records(op: Planned, aliases: Sequence[str]):
+    """RelationalCypherResult.records.toMaps: list of {alias: value}."""
+    cols = {a: op.header.column(Var(a)) for a in aliases}
+    data = {a: op.table.column_values(c) for a, c in cols.items()}
+    n = len(next(iter(data.values()))) if data else op.table.size
+    return [{a: data[a][i] for a in aliases} for i in range(n)]
+
+
+def run(graph, q: Query, params=None):
+    op = plan_query(graph, q, params)
+    return records(op, [a for a, _ in q.stages[-1].items])

@@ -1,0 +1,45 @@
+"""Synthetic benchmark graphs resident in HBM (BASELINE.json configs 2-4).
+
+R-MAT with Graph500 parameters a/b/c/d = .57/.19/.19/.05, edge factor 16,
+seed 0x5EED0000 + scale; generated on the GPU by
+capf_rmat_rel_table.  The graph is exposed as a ScanGraph with one node
+label combination per table, exactly like EdgeListDataSource
+(flink-cypher/.../api/io/edgelist/EdgeListDataSource.scala:56-92: label `V`,
+type `E`), or with the config-2 `Person` / `Other` split.
+"""
+from .expr import BoolLit, Equals, Var
+from .graph import ElementTable, ScanGraph
+from .header import RecordHeader
+
+A, B, C = 0.57, 0.19, 0.19
+
+
+def thresholds(a=A, b=B, c=C):
+    t = lambda x: min(int(x * 2 ** 32), 2 ** 32 - 1)
+    return t(a), t(a + b), t(a + b + c)
+
+
+def rmat_seed(scale):
+    return 0x5EED0000 + scale
+
+
+def rmat_graph(session, scale, edge_factor=16, seed=None, person_split=False, first=0, count=None,
+               node_base=0, n_nodes=None):
+    """ScanGraph over an R-MAT edge table (optionally a shard [first, first+count))."""
+    seed = rmat_seed(scale) if seed is None else seed
+    m = edge_factor << scale
+    count = m - first if count is None else count
+    n = (1 << scale) if n_nodes is None else n_nodes
+    rels = session.rmat_rels(scale, seed, thresholds(), first, count, id_base=0)
+    rel_tables = [ElementTable("rel", frozenset(["E"]), rels, {})]
+    if person_split:
+        nodes = session.range_nodes(node_base, n, seed=seed, id_col="id", label_col="person")
+        h = RecordHeader({Var("person"): "person"})
+        person = nodes.filter(Equals(Var("person"), BoolLit(True)), h, {}).select("id")
+        other = nodes.filter(Equals(Var("person"), BoolLit(False)), h, {}).select("id")
+        node_tables = [ElementTable("node", frozenset(["Person"]), person, {}),
+                       ElementTable("node", frozenset(["Other"]), other, {})]
+    else:
+        nodes = session.range_nodes(node_base, n, id_col="id")
+        node_tables = [ElementTable("node", frozenset(["V"]), nodes, {})]
+    return ScanGraph(session, node_tables, rel_tables)

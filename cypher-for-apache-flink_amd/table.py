@@ -1,0 +1,329 @@
+"""GpuTable / GpuSession: the host-side mirror of the okapi Table SPI over the
+MI355X C-ABI (include/capf_gpu.h).
+
+`GpuTable` implements exactly the methods of
+  trait Table[T <: Table[T]] extends CypherTable
+  (okapi-relational/src/main/scala/org/opencypher/okapi/relational/api/table/Table.scala:43-178)
+with the same names and argument meaning as FlinkTable
+(flink-cypher/src/main/scala/org/opencypher/flink/impl/table/FlinkTable.scala:49-199),
+so a planner written against the SPI (planner.py, mirroring RelationalPlanner)
+drives it unchanged.  Every operation returns a new immutable table; nothing
+executes on the GPU until `size` / `rows` (lazy, like the Flink Table API).
+"""
+import ctypes
+from ctypes import byref, c_char_p, c_double, c_int32, c_int64, c_uint64, c_void_p
+
+import numpy as np
+
+from . import _lib
+from .expr import (AGG_COUNT_STAR, CAPF_TO_CT, T_BOOL, T_FLOAT, T_INT, T_NULL, T_STRING, Aggregator,
+                   compile_program)
+
+JOIN_TYPES = {"inner": 0, "left_outer": 1, "right_outer": 2, "full_outer": 3, "cross": 4}
+
+_NP_DTYPE = {T_INT: np.int64, T_FLOAT: np.float64, T_BOOL: np.uint8, T_STRING: np.int64}
+
+
+class GpuSession:
+    """Backend state of a RelationalCypherSession[GpuTable]
+    (okapi-relational/.../api/graph/RelationalCypherSession.scala:63-111)."""
+
+    def __init__(self, device=0, stream=None):
+        _lib.load()
+        h = c_void_p()
+        _lib.call("capf_session_create", int(device), stream, byref(h))
+        self._h = h
+        self._strings = {}
+        self._codes = {}
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.load().capf_session_destroy(self._h)
+            self._h = None
+
+    # -- strings ------------------------------------------------------------
+    def intern(self, s):
+        c = self._codes.get(s)
+        if c is None:
+            v = c_int64()
+            _lib.call("capf_string_intern", self._h, s.encode(), byref(v))
+            c = v.value
+            self._codes[s] = c
+            self._strings[c] = s
+        return c
+
+    def lookup(self, code):
+        s = self._strings.get(code)
+        if s is None:
+            p = c_char_p()
+            _lib.call("capf_string_lookup", self._h, int(code), byref(p))
+            s = p.value.decode()
+            self._strings[code] = s
+        return s
+
+    # -- table factories ----------------------------------------------------
+    def table(self, columns, nrows=None):
+        """columns: list of (name, capf_type, values, valid-or-None).
+
+        values: sequence of python values (None = NULL) or a numpy array."""
+        names, types, datas, valids, keep = [], [], [], [], []
+        n = nrows
+        for name, t, values, valid in columns:
+            vals = values
+            if not isinstance(vals, np.ndarray) or vals.dtype == object:
+                lst = list(vals)
+                if valid is None and any(v is None for v in lst):
+                    valid = np.array([v is not None for v in lst], dtype=np.uint8)
+                if t == T_STRING:
+                    vals = np.array([self.intern(v) if v is not None else 0 for v in lst], dtype=np.int64)
+                elif t == T_NULL:
+                    vals = None
+                else:
+                    vals = np.array([v if v is not None else 0 for v in lst], dtype=_NP_DTYPE[t])
+            elif t != T_NULL:
+                vals = np.ascontiguousarray(vals.astype(_NP_DTYPE[t], copy=False))
+            m = len(values)
+            if n is None:
+                n = m
+            elif n != m:
+                raise _lib.IllegalArgumentException("columns of different length")
+            names.append(name)
+            types.append(t)
+            datas.append(vals.ctypes.data if vals is not None and m > 0 else None)
+            if valid is not None:
+                valid = np.ascontiguousarray(np.asarray(valid, dtype=np.uint8))
+                valids.append(valid.ctypes.data if m > 0 else None)
+            else:
+                valids.append(None)
+            keep += [vals, valid]
+        n = n or 0
+        k = len(names)
+        h = c_void_p()
+        _lib.call("capf_table_from_host", self._h, k, _lib.strs(names), (c_int32 * max(k, 1))(*types),
+                  (c_void_p * max(k, 1))(*datas), (c_void_p * max(k, 1))(*valids), n, byref(h))
+        return GpuTable(self, h)
+
+    def unit(self):
+        h = c_void_p()
+        _lib.call("capf_table_unit", self._h, byref(h))
+        return GpuTable(self, h)
+
+    def empty(self, names, types):
+        h = c_void_p()
+        k = len(names)
+        _lib.call("capf_table_empty", self._h, k, _lib.strs(names), (c_int32 * max(k, 1))(*types), byref(h))
+        return GpuTable(self, h)
+
+    def rmat_rels(self, scale, seed, thresholds, first, count, id_base=0, cols=("id", "source", "target")):
+        h = c_void_p()
+        ta, tab, tabc = thresholds
+        _lib.call("capf_rmat_rel_table", self._h, int(scale), int(seed), ta, tab, tabc, int(first),
+                  int(count), int(id_base), cols[0].encode(), cols[1].encode(), cols[2].encode(), byref(h))
+        return GpuTable(self, h)
+
+    def range_nodes(self, base, n, seed=0, id_col="id", label_col=None):
+        h = c_void_p()
+        _lib.call("capf_range_node_table", self._h, int(base), int(n), int(seed), id_col.encode(),
+                  label_col.encode() if label_col else None, byref(h))
+        return GpuTable(self, h)
+
+    # -- profiling ----------------------------------------------------------
+    def set_profiling(self, on):
+        _lib.call("capf_session_set_profiling", self._h, 1 if on else 0)
+
+    def reset_profile(self):
+        _lib.call("capf_session_reset_profile", self._h)
+
+    def profile(self):
+        n = c_int32()
+        _lib.call("capf_session_profile_count", self._h, byref(n))
+        out = {}
+        for i in range(n.value):
+            name, launches, ms, by = c_char_p(), c_int64(), c_double(), c_double()
+            _lib.call("capf_session_profile_entry", self._h, i, byref(name), byref(launches), byref(ms), byref(by))
+            out[name.value.decode()] = {"launches": launches.value, "total_ms": ms.value, "bytes": by.value}
+        return out
+
+    def last_plan(self):
+        return _lib.load().capf_session_last_plan(self._h).decode()
+
+    def sync(self):
+        _lib.call("capf_session_sync", self._h)
+
+
+def _program(expr, header, table, params):
+    return compile_program(expr, header, set(table.physicalColumns), params, table.session.intern)
+
+
+class GpuTable:
+    """Table[GpuTable] over an opaque capf_table handle."""
+
+    def __init__(self, session, handle):
+        self.session = session
+        self._h = handle
+        self._cols = None
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and _lib._lib is not None and getattr(self.session, "_h", None):
+            _lib._lib.capf_table_release(h)
+
+    def _new(self, fn, *args):
+        h = c_void_p()
+        _lib.call(fn, *args, byref(h))
+        return GpuTable(self.session, h)
+
+    # ---------------------------------------------------------- CypherTable
+    @property
+    def physicalColumns(self):
+        if self._cols is None:
+            n = c_int32()
+            _lib.call("capf_table_num_columns", self._h, byref(n))
+            cols = []
+            for i in range(n.value):
+                p = c_char_p()
+                _lib.call("capf_table_column_name", self._h, i, byref(p))
+                cols.append(p.value.decode())
+            self._cols = cols
+        return list(self._cols)
+
+    def capf_type(self, col):
+        t = c_int32()
+        _lib.call("capf_table_column_type", self._h, col.encode(), byref(t))
+        return t.value
+
+    @property
+    def columnType(self):
+        return {c: CAPF_TO_CT[self.capf_type(c)] for c in self.physicalColumns}
+
+    @property
+    def size(self):
+        n = c_int64()
+        _lib.call("capf_table_size", self._h, byref(n))
+        return n.value
+
+    def column_arrays(self, col):
+        """(values ndarray, valid ndarray[bool]) of a column (materialises)."""
+        n = self.size
+        t = self.capf_type(col)
+        valid = np.zeros(n, dtype=np.uint8)
+        if t == T_NULL:
+            _lib.call("capf_table_download", self._h, col.encode(), None, valid.ctypes.data if n else None)
+            return np.zeros(n, dtype=np.int64), valid.astype(bool)
+        vals = np.zeros(n, dtype=_NP_DTYPE[t])
+        _lib.call("capf_table_download", self._h, col.encode(), vals.ctypes.data if n else None,
+                  valid.ctypes.data if n else None)
+        return vals, valid.astype(bool)
+
+    def column_values(self, col):
+        """Python values (None for NULL) of one column."""
+        t = self.capf_type(col)
+        vals, valid = self.column_arrays(col)
+        out = []
+        for v, ok in zip(vals.tolist(), valid.tolist()):
+            if not ok:
+                out.append(None)
+            elif t == T_STRING:
+                out.append(self.session.lookup(v))
+            elif t == T_BOOL:
+                out.append(bool(v))
+            else:
+                out.append(v)
+        return out
+
+    @property
+    def rows(self):
+        cols = self.physicalColumns
+        data = [self.column_values(c) for c in cols]
+        n = len(data[0]) if data else self.size
+        return [{c: data[i][r] for i, c in enumerate(cols)} for r in range(n)]
+
+    # ---------------------------------------------------------- Table[T]
+    def cache(self):
+        return self._new("capf_table_cache", self._h)
+
+    def select(self, *cols):
+        pairs = [(c, c) if isinstance(c, str) else tuple(c) for c in cols]
+        src = [p[0] for p in pairs]
+        al = [p[1] for p in pairs]
+        return self._new("capf_table_select", self._h, len(pairs), _lib.strs(src), _lib.strs(al))
+
+    def filter(self, expr, header=None, params=None):
+        prog = _program(expr, header, self, params)
+        e, keep = _lib._keepalive_expr(prog)
+        return self._new("capf_table_filter", self._h, byref(e))
+
+    def drop(self, *cols):
+        return self._new("capf_table_drop", self._h, len(cols), _lib.strs(list(cols)))
+
+    def join(self, other, join_type, *join_cols):
+        jt = JOIN_TYPES[join_type] if isinstance(join_type, str) else int(join_type)
+        ls = [l for l, _ in join_cols]
+        rs = [r for _, r in join_cols]
+        return self._new("capf_table_join", self._h, other._h, jt, len(join_cols), _lib.strs(ls), _lib.strs(rs))
+
+    def unionAll(self, other):
+        return self._new("capf_table_union_all", self._h, other._h)
+
+    def orderBy(self, *sort_items, header=None, params=None):
+        progs = [_program(e, header, self, params) for e, _ in sort_items]
+        arr, keep = _lib.expr_array(progs)
+        desc = (c_int32 * max(len(sort_items), 1))(*[1 if o in ("desc", "Descending", True) else 0
+                                                     for _, o in sort_items])
+        return self._new("capf_table_order_by", self._h, len(progs), arr, desc)
+
+    def skip(self, n):
+        return self._new("capf_table_skip", self._h, int(n))
+
+    def limit(self, n):
+        return self._new("capf_table_limit", self._h, int(n))
+
+    def distinct(self, *cols):
+        if not cols:
+            return self._new("capf_table_distinct", self._h)
+        return self._new("capf_table_distinct_cols", self._h, len(cols), _lib.strs(list(cols)))
+
+    def group(self, by, aggregations, header=None, params=None):
+        """by: iterable of Var (grouping uses every column they own,
+        FlinkTable.scala:129-135); aggregations: {column: Aggregator}."""
+        cols = []
+        for v in by:
+            for e in header.owned_by(v):
+                c = header.column(e)
+                if c in self.physicalColumns and c not in cols:
+                    cols.append(c)
+        names = list(aggregations)
+        kinds, progs, dist = [], [], []
+        for name in names:
+            agg = aggregations[name]
+            if not isinstance(agg, Aggregator):
+                raise _lib.IllegalArgumentException(f"{agg} is not an aggregator")
+            kinds.append(agg.kind)
+            dist.append(1 if getattr(agg, "distinct", False) else 0)
+            progs.append(None if agg.kind == AGG_COUNT_STAR else _program(agg.expr, header, self, params))
+        arr, keep = _lib.expr_array(progs)
+        k = len(names)
+        return self._new("capf_table_group", self._h, len(cols), _lib.strs(cols), k,
+                         (c_int32 * max(k, 1))(*kinds), arr, (c_int32 * max(k, 1))(*dist), _lib.strs(names))
+
+    def withColumns(self, *columns, header=None, params=None):
+        progs = [_program(e, header, self, params) for e, _ in columns]
+        arr, keep = _lib.expr_array(progs)
+        return self._new("capf_table_with_columns", self._h, len(columns), arr,
+                         _lib.strs([c for _, c in columns]))
+
+    def show(self, rows=20):
+        _lib.call("capf_table_show", self._h, int(rows))
+
+    # ---------------------------------------------------------- multi-GPU helpers
+    def chain2_local_hists(self, src_col, dst_col, node_base, n_nodes, d_in, d_out):
+        loops = c_int64()
+        _lib.call("capf_chain2_local_hists", self.session._h, self._h, src_col.encode(), dst_col.encode(),
+                  int(node_base), int(n_nodes), c_void_p(d_in), c_void_p(d_out), byref(loops))
+        return loops.value
+
+
+def dot_u32(session, d_a, d_b, n):
+    out = c_uint64()
+    _lib.call("capf_dot_u32", session._h, c_void_p(d_a), c_void_p(d_b), int(n), byref(out))
+    return out.value

@@ -1,0 +1,285 @@
+/*
+ * capf_gpu.h — C-ABI of the MI355X relational backend for okapi-relational.
+ *
+ * This is the drop-in boundary that replaces the Flink implementation of the
+ * okapi `Table[T]` SPI.  Every entry point below corresponds to one method of
+ *
+ *   trait Table[T <: Table[T]] extends CypherTable
+ *     okapi-relational/src/main/scala/org/opencypher/okapi/relational/api/table/Table.scala:43-178
+ *   trait CypherTable
+ *     okapi-api/src/main/scala/org/opencypher/okapi/api/table/CypherTable.scala:41-70
+ *
+ * as implemented today by FlinkTable
+ *     flink-cypher/src/main/scala/org/opencypher/flink/impl/table/FlinkTable.scala:49-199
+ *
+ * (citations are relative to the reference checkout).  A JVM shim
+ * (`GpuTable extends Table[GpuTable]`) binds these
+ * functions 1:1 over JNI; the Python host layer in
+ * cypher-for-apache-flink_amd/table.py binds them over ctypes.
+ *
+ * Conventions
+ *  - Tables are immutable, reference-counted handles.  Every operation returns
+ *    a NEW handle (Table.scala: "every op returns a new T"); the caller owns it
+ *    and must capf_table_release() it.  Column buffers are shared between
+ *    handles, so select/drop/alias are metadata-only.
+ *  - Evaluation is lazy, exactly like the Flink Table API: operations build a
+ *    plan DAG; nothing runs on the GPU until capf_table_size / capf_table_download
+ *    (FlinkTable.scala:57-61, CAPFRecords.scala:142-144).  This is what lets
+ *    `group(∅, count(*))` over an Expand join chain run as a fused,
+ *    factorised count instead of materialising ~1e12 joined rows.
+ *  - Every function returns CAPF_OK (0) or a negative status.  The message
+ *    is available from capf_last_error() (thread-local) and the kind from
+ *    capf_last_error_kind(); the shim rethrows the matching
+ *    okapi.impl.exception (okapi-api/.../impl/exception/InternalException.scala:36-65).
+ *  - Column names are arbitrary caller strings (RecordHeader column names,
+ *    okapi-relational/.../impl/table/RecordHeader.scala:299-318).
+ *  - Logical types follow the Flink type mapping
+ *    (flink-cypher/.../impl/convert/FlinkConversions.scala:43-117):
+ *    CTInteger / node / relationship ids → INT64, CTFloat → FLOAT64,
+ *    CTBoolean → BOOL, CTString → STRING (dictionary codes, see capf_string_*).
+ */
+#ifndef CAPF_GPU_H
+#define CAPF_GPU_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CAPF_ABI_VERSION 1
+
+typedef struct capf_session capf_session;
+typedef struct capf_table capf_table;
+typedef int32_t capf_status;
+
+/* status codes */
+enum {
+  CAPF_OK = 0,
+  CAPF_ERR_ILLEGAL_ARGUMENT = -1, /* okapi IllegalArgumentException */
+  CAPF_ERR_NOT_IMPLEMENTED = -2,  /* okapi NotImplementedException   */
+  CAPF_ERR_INTERNAL = -3,         /* okapi IllegalStateException / InternalException */
+  CAPF_ERR_HIP = -4,              /* HIP runtime failure               */
+  CAPF_ERR_OOM = -5               /* device allocation failed          */
+};
+
+/* column types (FlinkConversions.scala:43-117) */
+enum {
+  CAPF_TYPE_NULL = 0,    /* CTNull: column of nulls */
+  CAPF_TYPE_INT64 = 1,   /* CTInteger, CTNode/CTRelationship/CTIdentity ids (Types.LONG) */
+  CAPF_TYPE_FLOAT64 = 2, /* CTFloat (Types.DOUBLE) */
+  CAPF_TYPE_BOOL = 3,    /* CTBoolean, HasLabel / HasType columns */
+  CAPF_TYPE_STRING = 4   /* CTString, stored as int64 dictionary codes */
+};
+
+/* join types (okapi-relational/.../impl/planning/PhysicalConstants.scala:29-35) */
+enum {
+  CAPF_JOIN_INNER = 0,
+  CAPF_JOIN_LEFT_OUTER = 1,
+  CAPF_JOIN_RIGHT_OUTER = 2,
+  CAPF_JOIN_FULL_OUTER = 3,
+  CAPF_JOIN_CROSS = 4
+};
+
+/* aggregators (okapi-ir/.../api/expr/Expr.scala:1031-1140,
+ * lowered as in FlinkSQLExprMapper.scala:281-287) */
+enum {
+  CAPF_AGG_COUNT_STAR = 0,
+  CAPF_AGG_COUNT = 1,
+  CAPF_AGG_SUM = 2,
+  CAPF_AGG_MIN = 3,
+  CAPF_AGG_MAX = 4,
+  CAPF_AGG_AVG = 5
+};
+
+/*
+ * Expression programs.  The shim lowers the supported subset of okapi `Expr`
+ * trees (what FlinkSQLExprMapper.asFlinkSQLExpr handles,
+ * flink-cypher/.../impl/FlinkSQLExprMapper.scala:48-294) into a postfix
+ * program evaluated per row on the GPU with Cypher three-valued logic.
+ * Parameters (`Param`) are substituted as literals by the shim.
+ */
+enum {
+  CAPF_OP_COL = 1,         /* push column names[iarg]                       */
+  CAPF_OP_LIT_INT = 2,     /* push int64 iarg                               */
+  CAPF_OP_LIT_FLOAT = 3,   /* push double farg                              */
+  CAPF_OP_LIT_BOOL = 4,    /* push bool iarg != 0                           */
+  CAPF_OP_LIT_STRING = 5,  /* push string code iarg (capf_string_intern)    */
+  CAPF_OP_LIT_NULL = 6,    /* push NULL of capf type iarg                   */
+  CAPF_OP_EQ = 10,         /* Equals            (===)                       */
+  CAPF_OP_NEQ = 11,        /* Not(Equals)       fused                       */
+  CAPF_OP_LT = 12,         /* LessThan                                      */
+  CAPF_OP_LE = 13,         /* LessThanOrEqual                               */
+  CAPF_OP_GT = 14,         /* GreaterThan                                   */
+  CAPF_OP_GE = 15,         /* GreaterThanOrEqual                            */
+  CAPF_OP_NOT = 20,        /* Not                                           */
+  CAPF_OP_AND = 21,        /* Ands, arity iarg                              */
+  CAPF_OP_OR = 22,         /* Ors,  arity iarg                              */
+  CAPF_OP_IS_NULL = 23,    /* IsNull                                        */
+  CAPF_OP_IS_NOT_NULL = 24,/* IsNotNull / Exists                            */
+  CAPF_OP_ADD = 30,        /* Add (numeric)                                 */
+  CAPF_OP_SUB = 31,        /* Subtract                                      */
+  CAPF_OP_MUL = 32,        /* Multiply                                      */
+  CAPF_OP_DIV = 33,        /* Divide (integer division on int64 operands)   */
+  CAPF_OP_MOD = 34,        /* Modulo                                        */
+  CAPF_OP_NEG = 35,        /* unary minus                                   */
+  CAPF_OP_TO_FLOAT = 40,   /* ToFloat  → DOUBLE                             */
+  CAPF_OP_TO_INTEGER = 41, /* ToInteger → Flink casts to INT (32-bit!)      */
+  CAPF_OP_COALESCE = 50    /* Coalesce, arity iarg                          */
+};
+
+typedef struct capf_expr {
+  int32_t n;                 /* number of instructions                     */
+  const int32_t *ops;        /* opcode per instruction                     */
+  const int64_t *iargs;      /* integer immediate per instruction          */
+  const double *fargs;       /* float immediate per instruction (may be 0) */
+  int32_t n_names;           /* column names referenced by CAPF_OP_COL     */
+  const char *const *names;
+} capf_expr;
+
+/* ---------------------------------------------------------------- errors */
+const char *capf_last_error(void);
+int32_t capf_last_error_kind(void);
+int32_t capf_abi_version(void);
+
+/* --------------------------------------------------------------- session
+ * RelationalCypherSession[T] backend state
+ * (okapi-relational/.../api/graph/RelationalCypherSession.scala:63-111;
+ *  CAPFSession.create, flink-cypher/.../api/CAPFSession.scala:74-91).
+ * `hip_stream` may be NULL (the session creates its own stream) or a
+ * hipStream_t owned by the caller (e.g. torch.cuda.current_stream()).     */
+capf_status capf_session_create(int32_t device, void *hip_stream, capf_session **out);
+capf_status capf_session_destroy(capf_session *s);
+capf_status capf_session_sync(capf_session *s);
+/* Per-kernel HIP-event timing of the hot kernels (off by default). */
+capf_status capf_session_set_profiling(capf_session *s, int32_t enabled);
+capf_status capf_session_reset_profile(capf_session *s);
+capf_status capf_session_profile_count(capf_session *s, int32_t *n);
+capf_status capf_session_profile_entry(capf_session *s, int32_t i, const char **kernel,
+                                       int64_t *launches, double *total_ms, double *bytes);
+/* last fused-count execution path taken ("fused_chain2", "message_passing", "materialize") */
+const char *capf_session_last_plan(capf_session *s);
+
+/* String dictionary for CAPF_TYPE_STRING columns. */
+capf_status capf_string_intern(capf_session *s, const char *str, int64_t *code);
+capf_status capf_string_lookup(capf_session *s, int64_t code, const char **str);
+
+/* ---------------------------------------------------- table construction
+ * CAPFElementTable.create / CAPFRecordsFactory.from
+ * (flink-cypher/.../api/io/CAPFTable.scala:76-83, impl/CAPFRecords.scala:47-100).
+ * data[i]: nrows values of 8 bytes (INT64/FLOAT64/STRING) or 1 byte (BOOL),
+ *          NULL for a CAPF_TYPE_NULL column.
+ * valid[i]: NULL (no nulls) or nrows bytes, 1 = value present.            */
+capf_status capf_table_from_host(capf_session *s, int32_t ncols, const char *const *names,
+                                 const int32_t *types, const void *const *data,
+                                 const uint8_t *const *valid, int64_t nrows, capf_table **out);
+/* Same with device pointers; copy = 0 borrows them (caller keeps them alive). */
+capf_status capf_table_from_device(capf_session *s, int32_t ncols, const char *const *names,
+                                   const int32_t *types, void *const *data,
+                                   uint8_t *const *valid, int64_t nrows, int32_t copy,
+                                   capf_table **out);
+/* RelationalCypherRecordsFactory.unit / empty(header)
+ * (okapi-relational/.../api/table/RelationalCypherRecords.scala:43-54)       */
+capf_status capf_table_unit(capf_session *s, capf_table **out);
+capf_status capf_table_empty(capf_session *s, int32_t ncols, const char *const *names,
+                             const int32_t *types, capf_table **out);
+capf_status capf_table_retain(capf_table *t);
+capf_status capf_table_release(capf_table *t);
+
+/* ------------------------------------------------------------ CypherTable */
+/* physicalColumns (CypherTable.scala:48) */
+capf_status capf_table_num_columns(capf_table *t, int32_t *n);
+capf_status capf_table_column_name(capf_table *t, int32_t i, const char **name);
+/* columnType (CypherTable.scala:58) */
+capf_status capf_table_column_type(capf_table *t, const char *col, int32_t *type);
+/* size (CypherTable.scala:68): triggers execution */
+capf_status capf_table_size(capf_table *t, int64_t *n);
+/* rows (CypherTable.scala:63): download one column; values buffer holds
+ * size × (8 or 1) bytes, valid_out (may be NULL) size bytes.              */
+capf_status capf_table_download(capf_table *t, const char *col, void *values_out,
+                                uint8_t *valid_out);
+/* Device view of a materialised column (for zero-copy interop). */
+capf_status capf_table_device_column(capf_table *t, const char *col, void **values,
+                                     uint8_t **valid, int64_t *nrows);
+
+/* --------------------------------------------------------------- Table[T] */
+/* cache() (Table.scala:52) */
+capf_status capf_table_cache(capf_table *t, capf_table **out);
+/* select((col, alias)+) (Table.scala:71) */
+capf_status capf_table_select(capf_table *t, int32_t n, const char *const *cols,
+                              const char *const *aliases, capf_table **out);
+/* filter(expr)(header, params) (Table.scala:81) */
+capf_status capf_table_filter(capf_table *t, const capf_expr *pred, capf_table **out);
+/* drop(cols*) (Table.scala:89) */
+capf_status capf_table_drop(capf_table *t, int32_t n, const char *const *cols, capf_table **out);
+/* join(other, joinType, (l, r)*) (Table.scala:99) */
+capf_status capf_table_join(capf_table *l, capf_table *r, int32_t join_type, int32_t npairs,
+                            const char *const *lcols, const char *const *rcols,
+                            capf_table **out);
+/* unionAll(other) (Table.scala:107) */
+capf_status capf_table_union_all(capf_table *l, capf_table *r, capf_table **out);
+/* orderBy((expr, order)*) (Table.scala:115) */
+capf_status capf_table_order_by(capf_table *t, int32_t n, const capf_expr *keys,
+                                const int32_t *descending, capf_table **out);
+/* skip(n) / limit(n) (Table.scala:123, :131) */
+capf_status capf_table_skip(capf_table *t, int64_t n, capf_table **out);
+capf_status capf_table_limit(capf_table *t, int64_t n, capf_table **out);
+/* distinct / distinct(cols*) (Table.scala:138, :146) */
+capf_status capf_table_distinct(capf_table *t, capf_table **out);
+capf_status capf_table_distinct_cols(capf_table *t, int32_t n, const char *const *cols,
+                                     capf_table **out);
+/* group(by, aggregations)(header, params) (Table.scala:158-159).
+ * by_cols are the physical columns owned by the grouping vars
+ * (header.ownedBy, FlinkTable.scala:129-135).                              */
+capf_status capf_table_group(capf_table *t, int32_t n_by, const char *const *by_cols,
+                             int32_t n_aggs, const int32_t *agg_kinds,
+                             const capf_expr *agg_args, const int32_t *agg_distinct,
+                             const char *const *agg_names, capf_table **out);
+/* withColumns((expr, col)*)(header, params) (Table.scala:170) */
+capf_status capf_table_with_columns(capf_table *t, int32_t n, const capf_expr *exprs,
+                                    const char *const *names, capf_table **out);
+/* show(n) (Table.scala:177): prints to stdout */
+capf_status capf_table_show(capf_table *t, int32_t rows);
+
+/* ------------------------------------------------ synthetic graph inputs
+ * Deterministic Graph500-style R-MAT generator (counter-based, identical to
+ * oracle/rmat.c) writing straight into HBM.  Not part of the Table SPI:
+ * it stands in for the graph-ingest step (EdgeListDataSource,
+ * flink-cypher/.../api/io/edgelist/EdgeListDataSource.scala:56-92).
+ * thresholds = floor(a*2^32), floor((a+b)*2^32), floor((a+b+c)*2^32).
+ * Produces a relationship table with columns (id_col, src_col, dst_col),
+ * rel ids = id_base + edge index, for edges [first, first+count).          */
+capf_status capf_rmat_rel_table(capf_session *s, int32_t scale, uint64_t seed,
+                                uint32_t t_a, uint32_t t_ab, uint32_t t_abc,
+                                int64_t first, int64_t count, int64_t id_base,
+                                const char *id_col, const char *src_col,
+                                const char *dst_col, capf_table **out);
+/* Node table with id column [base, base+n) and an optional BOOL label column
+ * label_col (NULL = none) set with probability 1/2 from the seeded hash.  */
+capf_status capf_range_node_table(capf_session *s, int64_t base, int64_t n, uint64_t seed,
+                                  const char *id_col, const char *label_col,
+                                  capf_table **out);
+
+/* ------------------------------------------------ multi-GPU partial counts
+ * Building blocks of the hash-partitioned 2-hop count: the
+ * caller (one process per GPU, torch.distributed/RCCL) exchanges the
+ * per-node histograms between ranks.  See DESIGN.md "Multi-GPU".
+ * capf_chain2_local_hists: over the rel rows of this rank, writes
+ *   in_hist[v - node_base]  += #rels with dst = v   (v any node)
+ *   out_hist[v - node_base] += #rels with src = v
+ * for rels whose endpoints both lie in [node_base, node_base + n_nodes)
+ * and returns the number of such self-loops.  Buffers are device uint32
+ * arrays of n_nodes entries and are zeroed by the call.                    */
+capf_status capf_chain2_local_hists(capf_session *s, capf_table *rels, const char *src_col,
+                                    const char *dst_col, int64_t node_base, int64_t n_nodes,
+                                    uint32_t *d_in_hist, uint32_t *d_out_hist,
+                                    int64_t *self_loops);
+/* Σ_v a[v]·b[v] over n entries (device uint32 arrays), exact in uint64. */
+capf_status capf_dot_u32(capf_session *s, const uint32_t *d_a, const uint32_t *d_b, int64_t n,
+                         uint64_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CAPF_GPU_H */

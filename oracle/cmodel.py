@@ -1,0 +1,122 @@
+"""ctypes binding of oracle/rmat.c (TEST INFRASTRUCTURE ONLY)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+BUILD = os.path.join(HERE, "build")
+SO = os.path.join(BUILD, "liboracle.so")
+
+# Graph500 R-MAT parameters
+A, B, C = 0.57, 0.19, 0.19
+
+
+def thresholds(a=A, b=B, c=C):
+    t = lambda x: min(int(x * 2 ** 32), 2 ** 32 - 1)
+    return t(a), t(a + b), t(a + b + c)
+
+
+def rmat_seed(scale):
+    return 0x5EED0000 + scale
+
+
+def build():
+    os.makedirs(BUILD, exist_ok=True)
+    src = os.path.join(HERE, "rmat.c")
+    if not os.path.exists(SO) or os.path.getmtime(SO) < os.path.getmtime(src):
+        subprocess.check_call(["gcc", "-O3", "-march=x86-64-v2", "-fPIC", "-shared", "-pthread",
+                               src, "-o", SO])
+    return SO
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        l = ctypes.CDLL(SO)
+        P = ctypes.c_void_p
+        i64, u64, u32, i32 = ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+        l.rmat_edges.argtypes = [i32, u64, u32, u32, u32, i64, i64, P, P]
+        l.rmat_edges.restype = None
+        l.node_labels.argtypes = [i64, i64, u64, P]
+        l.node_labels.restype = None
+        l.count_1hop.argtypes = [P, P, i64, P, P, i64]
+        l.count_1hop.restype = u64
+        l.count_2hop.argtypes = [P, P, i64, i64]
+        l.count_2hop.restype = u64
+        l.degree_hists.argtypes = [P, P, i64, i64, i64, P, P, P]
+        l.degree_hists.restype = None
+        l.pipeline_build.argtypes = [P, i64, P, P, P, i64, i32]
+        l.pipeline_build.restype = P
+        l.pipeline_probe.argtypes = [P, i64, i64, i32]
+        l.pipeline_probe.restype = u64
+        l.pipeline_free.argtypes = [P]
+        l.pipeline_free.restype = None
+        l.oracle_splitmix64.argtypes = [u64]
+        l.oracle_splitmix64.restype = u64
+        _lib = l
+    return _lib
+
+
+def rmat(scale, edge_factor=16, seed=None, first=0, count=None):
+    seed = rmat_seed(scale) if seed is None else seed
+    m = (edge_factor << scale) if count is None else count
+    src = np.empty(m, dtype=np.int64)
+    dst = np.empty(m, dtype=np.int64)
+    ta, tab, tabc = thresholds()
+    lib().rmat_edges(scale, seed, ta, tab, tabc, first, m, src.ctypes.data, dst.ctypes.data)
+    return src, dst
+
+
+def labels(n, seed, base=0):
+    out = np.empty(n, dtype=np.uint8)
+    lib().node_labels(base, n, seed, out.ctypes.data)
+    return out
+
+
+def count_1hop(src, dst, n, in_a=None, in_b=None):
+    pa = None if in_a is None else np.ascontiguousarray(in_a, dtype=np.uint8)
+    pb = None if in_b is None else np.ascontiguousarray(in_b, dtype=np.uint8)
+    return lib().count_1hop(src.ctypes.data, dst.ctypes.data, len(src),
+                            None if pa is None else pa.ctypes.data,
+                            None if pb is None else pb.ctypes.data, n)
+
+
+def count_2hop(src, dst, n):
+    return lib().count_2hop(src.ctypes.data, dst.ctypes.data, len(src), n)
+
+
+def degree_hists(src, dst, base, n):
+    i = np.empty(n, dtype=np.uint32)
+    o = np.empty(n, dtype=np.uint32)
+    loops = ctypes.c_int64()
+    lib().degree_hists(src.ctypes.data, dst.ctypes.data, len(src), base, n, i.ctypes.data, o.ctypes.data,
+                       ctypes.byref(loops))
+    return i, o, loops.value
+
+
+class Pipeline:
+    """Flink-shaped hash-join pipeline of the 2-hop count (CPU baseline)."""
+
+    def __init__(self, node_ids, rel_ids, src, dst, threads=1):
+        self._keep = [np.ascontiguousarray(x, dtype=np.int64) for x in (node_ids, rel_ids, src, dst)]
+        n, i, s, d = self._keep
+        self.m = len(s)
+        self._h = lib().pipeline_build(n.ctypes.data, len(n), i.ctypes.data, s.ctypes.data, d.ctypes.data,
+                                       len(s), threads)
+
+    def probe(self, lo, hi, threads):
+        return lib().pipeline_probe(self._h, lo, hi, threads)
+
+    def close(self):
+        if self._h:
+            lib().pipeline_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()

@@ -1,0 +1,277 @@
+/*
+ * oracle/rmat.c — TEST INFRASTRUCTURE ONLY (never linked into the product).
+ *
+ * CPU restatement used by tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg:
+ *
+ *  1. rmat_edges: the same counter-based Graph500-style R-MAT generator as
+ *     csrc/graph_gen.hip (bit-identical edges for a given seed).
+ *  2. Closed-form counts of the north-star patterns (independent of any join
+ *     implementation):
+ *       1-hop  (a:L)-->(b)        = Σ_rels [a ∈ S_a]·[b ∈ S_b]
+ *       2-hop  (a)-->(b)-->(c), r1<>r2
+ *              = Σ_b in(b)·out(b) − #self-loops        
+ *  3. pipeline_2hop: the Flink physical plan shape of
+ *       S_a ⋈[a=start(r1)] R1 ⋈[end(r1)=b] S_b ⋈[b=start(r2)] R2 ⋈[end(r2)=c] S_c,
+ *       Filter(NOT(r1 = r2)), count(*)
+ *     as lowered by RelationalPlanner.scala:130-165 and executed by Flink's
+ *     hash joins (FlinkTable.join, FlinkTable.scala:171-187): hash tables are
+ *     built on the node scans and on R2 keyed by start(r2); every r1 row
+ *     probes them tuple-at-a-time and every joined row is produced and
+ *     counted.  Parallelism = threads (LocalEnvironment default = cores,
+ *     flink-cypher/.../api/CAPFSession.scala:81).  This is the CPU baseline.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+static inline uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+uint64_t oracle_splitmix64(uint64_t x) { return splitmix64(x); }
+
+/* Edge e: for level l, u = 32-bit draw; quadrant by integer thresholds. */
+void rmat_edges(int scale, uint64_t seed, uint32_t ta, uint32_t tab, uint32_t tabc, int64_t first,
+                int64_t count, int64_t *src, int64_t *dst) {
+  const uint64_t key = splitmix64(seed);
+  for (int64_t k = 0; k < count; ++k) {
+    const uint64_t e = (uint64_t)(first + k);
+    uint64_t s = 0, d = 0, r = 0;
+    for (int l = 0; l < scale; ++l) {
+      if ((l & 1) == 0) r = splitmix64(key + e * 32ull + (uint64_t)(l >> 1));
+      const uint32_t u = (l & 1) ? (uint32_t)(r >> 32) : (uint32_t)r;
+      const uint32_t q = u < ta ? 0u : (u < tab ? 1u : (u < tabc ? 2u : 3u));
+      const int bit = scale - 1 - l;
+      s |= (uint64_t)(q >> 1) << bit;
+      d |= (uint64_t)(q & 1) << bit;
+    }
+    src[k] = (int64_t)s;
+    dst[k] = (int64_t)d;
+  }
+}
+
+/* Person label bit of node v (same hash as csrc/graph_gen.hip). */
+void node_labels(int64_t base, int64_t n, uint64_t seed, uint8_t *out) {
+  const uint64_t lkey = splitmix64(seed ^ 0x1ABE1ull);
+  for (int64_t k = 0; k < n; ++k) out[k] = (uint8_t)(splitmix64(lkey + (uint64_t)(base + k)) >> 63);
+}
+
+/* ---------------------------------------------------------- closed forms */
+/* 1-hop with per-node membership flags of S_a and S_b over ids [0, n). */
+uint64_t count_1hop(const int64_t *src, const int64_t *dst, int64_t m, const uint8_t *in_a,
+                    const uint8_t *in_b, int64_t n) {
+  uint64_t c = 0;
+  for (int64_t e = 0; e < m; ++e) {
+    int64_t s = src[e], d = dst[e];
+    if (s < 0 || s >= n || d < 0 || d >= n) continue;
+    c += (uint64_t)(in_a ? in_a[s] : 1) * (uint64_t)(in_b ? in_b[d] : 1);
+  }
+  return c;
+}
+
+/* 2-hop (a)-->(b)-->(c) with r1 <> r2 over a dense node range [0, n). */
+uint64_t count_2hop(const int64_t *src, const int64_t *dst, int64_t m, int64_t n) {
+  uint32_t *in = (uint32_t *)calloc((size_t)n, 4), *out = (uint32_t *)calloc((size_t)n, 4);
+  uint64_t loops = 0, total = 0;
+  for (int64_t e = 0; e < m; ++e) {
+    int64_t s = src[e], d = dst[e];
+    if (s < 0 || s >= n || d < 0 || d >= n) continue;
+    in[d]++;
+    out[s]++;
+    loops += s == d;
+  }
+  for (int64_t v = 0; v < n; ++v) total += (uint64_t)in[v] * out[v];
+  free(in);
+  free(out);
+  return total - loops;
+}
+
+/* Per-node in/out degree histograms (for the distributed-count tests). */
+void degree_hists(const int64_t *src, const int64_t *dst, int64_t m, int64_t base, int64_t n,
+                  uint32_t *in, uint32_t *out, int64_t *loops) {
+  memset(in, 0, (size_t)n * 4);
+  memset(out, 0, (size_t)n * 4);
+  int64_t l = 0;
+  for (int64_t e = 0; e < m; ++e) {
+    int64_t s = src[e] - base, d = dst[e] - base;
+    if (s < 0 || s >= n || d < 0 || d >= n) continue;
+    in[d]++;
+    out[s]++;
+    l += s == d;
+  }
+  *loops = l;
+}
+
+/* ------------------------------------------------- Flink-shaped pipeline */
+typedef struct {
+  /* open-addressing hash set of node ids (S_a = S_b = S_c = all nodes) */
+  int64_t *node_keys;
+  uint64_t node_mask;
+  /* R2 hash table keyed by start(r2): bucket → rows (chained, CSR layout) */
+  int64_t *r2_off;    /* nb + 1 bucket offsets */
+  int64_t *r2_rows;   /* rows grouped by bucket */
+  uint64_t r2_mask;
+  const int64_t *src, *dst, *id;
+} JoinState;
+
+static inline uint64_t hmix(int64_t k) {
+  uint64_t x = (uint64_t)k;
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  return x;
+}
+
+static int node_probe(const JoinState *js, int64_t k) {
+  uint64_t s = hmix(k) & js->node_mask;
+  for (;;) {
+    int64_t c = js->node_keys[s];
+    if (c == k) return 1;
+    if (c == INT64_MIN) return 0;
+    s = (s + 1) & js->node_mask;
+  }
+}
+
+typedef struct {
+  const JoinState *js;
+  int64_t lo, hi;
+  uint64_t count;
+} ProbeTask;
+
+static void *probe_worker(void *arg) {
+  ProbeTask *t = (ProbeTask *)arg;
+  const JoinState *js = t->js;
+  uint64_t c = 0;
+  for (int64_t r1 = t->lo; r1 < t->hi; ++r1) {
+    const int64_t a = js->src[r1], b = js->dst[r1];
+    if (!node_probe(js, a)) continue;      /* S_a ⋈ R1 */
+    if (!node_probe(js, b)) continue;      /* ⋈ S_b    */
+    const uint64_t bk = hmix(b) & js->r2_mask;
+    for (int64_t j = js->r2_off[bk]; j < js->r2_off[bk + 1]; ++j) {   /* ⋈ R2 */
+      const int64_t r2 = js->r2_rows[j];
+      if (js->src[r2] != b) continue;
+      if (!node_probe(js, js->dst[r2])) continue;                     /* ⋈ S_c */
+      if (js->id[r1] != js->id[r2]) ++c;   /* Filter(NOT(r1 = r2)), count(*) */
+    }
+  }
+  t->count = c;
+  return NULL;
+}
+
+typedef struct {
+  JoinState js;
+  int64_t n_nodes, m;
+} Pipeline;
+
+typedef struct {
+  JoinState *js;
+  int64_t m;
+  uint64_t blo, bhi; /* bucket range owned by this builder */
+  int64_t *fill;
+  int phase;
+} BuildTask;
+
+static void *build_worker(void *arg) {
+  BuildTask *t = (BuildTask *)arg;
+  JoinState *js = t->js;
+  for (int64_t r = 0; r < t->m; ++r) {
+    uint64_t b = hmix(js->src[r]) & js->r2_mask;
+    if (b < t->blo || b >= t->bhi) continue;
+    if (t->phase == 0)
+      js->r2_off[b + 1]++;
+    else
+      js->r2_rows[js->r2_off[b] + t->fill[b]++] = r;
+  }
+  return NULL;
+}
+
+void pipeline_free(void *handle);
+
+/* Build phase: hash set on the node scan, bucketed hash table on R2 by start
+ * id (partitioned over `threads` builders by bucket range). */
+void *pipeline_build(const int64_t *node_ids, int64_t n_nodes, const int64_t *id,
+                     const int64_t *src, const int64_t *dst, int64_t m, int threads) {
+  if (threads < 1) threads = 1;
+  Pipeline *p = (Pipeline *)calloc(1, sizeof(Pipeline));
+  JoinState *js = &p->js;
+  uint64_t cap = 1024;
+  while (cap < 2 * (uint64_t)n_nodes) cap <<= 1;
+  js->node_mask = cap - 1;
+  js->node_keys = (int64_t *)malloc(cap * 8);
+  for (uint64_t i = 0; i < cap; ++i) js->node_keys[i] = INT64_MIN;
+  for (int64_t i = 0; i < n_nodes; ++i) {
+    uint64_t s = hmix(node_ids[i]) & js->node_mask;
+    while (js->node_keys[s] != INT64_MIN && js->node_keys[s] != node_ids[i]) s = (s + 1) & js->node_mask;
+    js->node_keys[s] = node_ids[i];
+  }
+  uint64_t nb = 1024;
+  while (nb < (uint64_t)m) nb <<= 1;
+  js->r2_mask = nb - 1;
+  js->r2_off = (int64_t *)calloc(nb + 1, 8);
+  js->r2_rows = (int64_t *)malloc((size_t)(m > 0 ? m : 1) * 8);
+  int64_t *fill = (int64_t *)calloc(nb, 8);
+  js->src = src;
+  js->dst = dst;
+  js->id = id;
+  pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * threads);
+  BuildTask *tasks = (BuildTask *)malloc(sizeof(BuildTask) * threads);
+  for (int phase = 0; phase < 2; ++phase) {
+    if (phase == 1)
+      for (uint64_t b = 0; b < nb; ++b) js->r2_off[b + 1] += js->r2_off[b];
+    for (int t = 0; t < threads; ++t) {
+      tasks[t].js = js;
+      tasks[t].m = m;
+      tasks[t].blo = nb * (uint64_t)t / threads;
+      tasks[t].bhi = nb * (uint64_t)(t + 1) / threads;
+      tasks[t].fill = fill;
+      tasks[t].phase = phase;
+      pthread_create(&th[t], NULL, build_worker, &tasks[t]);
+    }
+    for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+  }
+  free(th);
+  free(tasks);
+  free(fill);
+  p->n_nodes = n_nodes;
+  p->m = m;
+  return p;
+}
+
+/* Probe phase over r1 rows [lo, hi) with `threads` workers (contiguous r1
+ * ranges: R-MAT edge order is random, so the load is even). */
+uint64_t pipeline_probe(void *handle, int64_t lo, int64_t hi, int threads) {
+  Pipeline *p = (Pipeline *)handle;
+  if (threads < 1) threads = 1;
+  pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * threads);
+  ProbeTask *tasks = (ProbeTask *)malloc(sizeof(ProbeTask) * threads);
+  int64_t span = hi - lo;
+  for (int t = 0; t < threads; ++t) {
+    tasks[t].js = &p->js;
+    tasks[t].lo = lo + span * t / threads;
+    tasks[t].hi = lo + span * (t + 1) / threads;
+    tasks[t].count = 0;
+    pthread_create(&th[t], NULL, probe_worker, &tasks[t]);
+  }
+  uint64_t c = 0;
+  for (int t = 0; t < threads; ++t) {
+    pthread_join(th[t], NULL);
+    c += tasks[t].count;
+  }
+  free(th);
+  free(tasks);
+  return c;
+}
+
+void pipeline_free(void *handle) {
+  Pipeline *p = (Pipeline *)handle;
+  if (!p) return;
+  free(p->js.node_keys);
+  free(p->js.r2_off);
+  free(p->js.r2_rows);
+  free(p);
+}

@@ -1,0 +1,550 @@
+"""numpy restatement of the Flink Table[T] semantics — TEST INFRASTRUCTURE ONLY.
+
+OracleTable implements the same SPI as the product GpuTable
+(okapi-relational/.../api/table/Table.scala:43-178) with the semantics of
+FlinkTable (flink-cypher/.../impl/table/FlinkTable.scala:49-199):
+
+ * select / drop: projection (FlinkTable.scala:63-74, 100-103);
+ * filter: expression lowered as FlinkSQLExprMapper.asFlinkSQLExpr
+   (FlinkSQLExprMapper.scala:48-294) under SQL three-valued logic; only TRUE
+   rows survive (FlinkTable.scala:76-78);
+ * join: equi-join, `true && l1 === r1 && ...` — NULL keys never match
+   (FlinkTable.scala:171-187); disjoint columns asserted (:173-174);
+ * unionAll: bag union, rhs columns matched by name (FlinkTable.scala:152-169);
+ * distinct(cols): one row per distinct value of cols (Spark dropDuplicates,
+   morpheus-spark-cypher/.../SparkTable.scala:198-200; the Flink version is
+   broken);
+ * group: GROUP BY the owned columns with NULL as its own group; aggregators
+   per FlinkSQLExprMapper.scala:281-287 (count(*) counts rows; count(e)
+   non-null; sum/min/max/avg ignore NULL and are NULL on no input; avg of an
+   INTEGER column is an INTEGER, Java long division — Expr.scala:1058-1066);
+ * orderBy: NULL sorts as the largest value;
+ * withColumns: replace in place or append (FlinkTable.scala:86-98).
+
+Everything materialises with numpy; sizes are the small parity cases.
+"""
+import numpy as np
+
+from capf_amd.expr import (T_BOOL, T_FLOAT, T_INT, T_NULL, T_STRING, CAPF_TO_CT, CT_TO_CAPF, Aggregator,
+                           Ands, BoolLit, Coalesce, ElementProperty, EndNode, FloatLit, HasLabel, HasType,
+                           IntegerLit, NullLit, Ors, Param, StartNode, StringLit, Var, AGG_AVG, AGG_COUNT,
+                           AGG_COUNT_STAR, AGG_MAX, AGG_MIN, AGG_SUM)
+
+
+class Col:
+    __slots__ = ("t", "v", "ok")
+
+    def __init__(self, t, v, ok):
+        self.t = t
+        self.v = v
+        self.ok = np.asarray(ok, dtype=bool)
+
+    def take(self, idx):
+        idx = np.asarray(idx, dtype=np.int64)
+        neg = idx < 0
+        safe = np.where(neg, 0, idx)
+        if len(self.v) == 0:
+            v = np.zeros(len(idx), dtype=self.v.dtype) if self.v.dtype != object else np.full(len(idx), None, dtype=object)
+            return Col(self.t, v, np.zeros(len(idx), dtype=bool))
+        return Col(self.t, self.v[safe], np.where(neg, False, self.ok[safe]))
+
+
+_NP = {T_INT: np.int64, T_FLOAT: np.float64, T_BOOL: np.bool_, T_STRING: object, T_NULL: np.int64}
+
+
+def _empty_vals(t, n):
+    if t == T_STRING:
+        return np.full(n, None, dtype=object)
+    return np.zeros(n, dtype=_NP[t])
+
+
+class OracleSession:
+    def table(self, columns, nrows=None):
+        cols = {}
+        order = []
+        n = nrows
+        for name, t, values, valid in columns:
+            lst = list(values)
+            m = len(lst)
+            n = m if n is None else n
+            ok = np.array([x is not None for x in lst], dtype=bool) if valid is None else np.asarray(valid, bool)
+            if t == T_STRING:
+                v = np.array(lst, dtype=object)
+            elif t == T_NULL:
+                v = np.zeros(m, dtype=np.int64)
+                ok = np.zeros(m, dtype=bool)
+            else:
+                v = np.array([x if x is not None else 0 for x in lst], dtype=_NP[t])
+            cols[name] = Col(t, v, ok)
+            order.append(name)
+        return OracleTable(order, cols, n or 0)
+
+    def unit(self):
+        return OracleTable([], {}, 1)
+
+    def empty(self, names, types):
+        return OracleTable(list(names), {c: Col(t, _empty_vals(t, 0), []) for c, t in zip(names, types)}, 0)
+
+    def intern(self, s):
+        return s
+
+
+# ------------------------------------------------------------ expressions
+class Val:
+    """Vectorised value: type, values, validity."""
+    __slots__ = ("t", "v", "ok")
+
+    def __init__(self, t, v, ok):
+        self.t, self.v, self.ok = t, v, np.asarray(ok, dtype=bool)
+
+
+def _num(x):
+    if x.t == T_FLOAT:
+        return x.v.astype(np.float64)
+    if x.t == T_BOOL:
+        return x.v.astype(np.int64)
+    return x.v
+
+
+def _cmp(a, b, op):
+    ok = a.ok & b.ok
+    if a.t == T_NULL or b.t == T_NULL:
+        return Val(T_BOOL, np.zeros(len(ok), bool), np.zeros(len(ok), bool))
+    if a.t == T_STRING or b.t == T_STRING:
+        if a.t != b.t:
+            raise TypeError("cannot compare STRING with non-string")
+        if op not in ("eq", "ne"):
+            raise NotImplementedError("ordering comparison on strings")
+        r = np.array([(x == y) if (p and q) else False for x, y, p, q in zip(a.v, b.v, a.ok, b.ok)], dtype=bool)
+        return Val(T_BOOL, r if op == "eq" else ~r, ok)
+    x, y = _num(a), _num(b)
+    with np.errstate(invalid="ignore"):
+        r = {"eq": x == y, "ne": x != y, "lt": x < y, "le": x <= y, "gt": x > y, "ge": x >= y}[op]
+    return Val(T_BOOL, np.asarray(r, bool), ok)
+
+
+def _arith(a, b, op):
+    n = len(a.ok)
+    ok = a.ok & b.ok
+    fl = a.t == T_FLOAT or b.t == T_FLOAT
+    if a.t in (T_STRING, T_BOOL) or b.t in (T_STRING, T_BOOL):
+        raise NotImplementedError("arithmetic on non-numeric values")
+    if fl:
+        x, y = _num(a).astype(np.float64), _num(b).astype(np.float64)
+        with np.errstate(all="ignore"):
+            r = {"add": x + y, "sub": x - y, "mul": x * y, "div": x / y, "mod": np.fmod(x, y)}[op]
+        return Val(T_FLOAT, r, ok)
+    x, y = a.v.astype(np.int64), b.v.astype(np.int64)
+    r = np.zeros(n, dtype=np.int64)
+    with np.errstate(all="ignore"):
+        if op == "add":
+            r = x + y
+        elif op == "sub":
+            r = x - y
+        elif op == "mul":
+            r = x * y
+        else:
+            zero = y == 0
+            ok = ok & ~zero
+            ys = np.where(zero, 1, y)
+            # Java long division truncates toward zero
+            q = np.abs(x) // np.abs(ys) * np.sign(x) * np.sign(ys)
+            r = q if op == "div" else x - q * ys
+    return Val(T_INT, r, ok)
+
+
+def evaluate(e, table, header, params):
+    n = table._n
+    cols = table._cols
+
+    def const(t, value, valid=True):
+        if t == T_STRING:
+            return Val(t, np.full(n, value, dtype=object), np.full(n, valid))
+        return Val(t, np.full(n, value if value is not None else 0, dtype=_NP[t]), np.full(n, valid))
+
+    def col_of(x):
+        c = header.get(x) if header is not None else None
+        if c is not None and c in cols:
+            k = cols[c]
+            return Val(k.t, k.v, k.ok)
+        return None
+
+    def go(x):
+        if isinstance(x, (Var, HasLabel, HasType, StartNode, EndNode, ElementProperty)):
+            v = col_of(x)
+            if v is not None:
+                return v
+            ct = getattr(x, "ctype", "BOOLEAN" if isinstance(x, (HasLabel, HasType)) else "INTEGER")
+            t = CT_TO_CAPF.get(ct, T_NULL)
+            return const(t, None, False)
+        v = col_of(x) if header is not None and x in header else None
+        if v is not None:
+            return v
+        name = type(x).__name__
+        if isinstance(x, IntegerLit):
+            return const(T_INT, x.v)
+        if isinstance(x, FloatLit):
+            return const(T_FLOAT, x.v)
+        if isinstance(x, BoolLit):
+            return const(T_BOOL, x.v)
+        if isinstance(x, StringLit):
+            return const(T_STRING, x.v)
+        if isinstance(x, NullLit):
+            return const(CT_TO_CAPF.get(x.ctype, T_NULL), None, False)
+        if isinstance(x, Param):
+            p = params[x.pname]
+            if p is None:
+                return const(T_NULL, None, False)
+            t = T_BOOL if isinstance(p, bool) else T_INT if isinstance(p, int) else T_FLOAT if isinstance(p, float) else T_STRING
+            return const(t, p)
+        cmp_ops = {"Equals": "eq", "LessThan": "lt", "LessThanOrEqual": "le", "GreaterThan": "gt",
+                   "GreaterThanOrEqual": "ge"}
+        if name in cmp_ops:
+            return _cmp(go(x.lhs), go(x.rhs), cmp_ops[name])
+        ar_ops = {"Add": "add", "Subtract": "sub", "Multiply": "mul", "Divide": "div", "Modulo": "mod"}
+        if name in ar_ops:
+            return _arith(go(x.lhs), go(x.rhs), ar_ops[name])
+        if name == "Not":
+            a = go(x.expr)
+            return Val(T_BOOL, ~a.v.astype(bool), a.ok)
+        if name == "IsNull":
+            a = go(x.expr)
+            return Val(T_BOOL, ~a.ok, np.ones(n, bool))
+        if name == "IsNotNull":
+            a = go(x.expr)
+            return Val(T_BOOL, a.ok.copy(), np.ones(n, bool))
+        if name == "Negate":
+            a = go(x.expr)
+            return Val(a.t, -a.v, a.ok)
+        if name == "ToFloat":
+            a = go(x.expr)
+            if a.t == T_BOOL:
+                return const(T_FLOAT, None, False)
+            return Val(T_FLOAT, _num(a).astype(np.float64), a.ok)
+        if name == "ToInteger":
+            # Flink: cast to INT (32 bit), FlinkSQLExprMapper.scala:183
+            a = go(x.expr)
+            if a.t == T_BOOL:
+                return const(T_INT, None, False)
+            if a.t == T_FLOAT:
+                f = np.nan_to_num(a.v.astype(np.float64), nan=0.0)
+                r = np.clip(np.trunc(f), -2 ** 31, 2 ** 31 - 1).astype(np.int64)
+            else:
+                r = a.v.astype(np.int64).astype(np.int32).astype(np.int64)
+            return Val(T_INT, r, a.ok)
+        if isinstance(x, (Ands, Ors)):
+            vals = [go(y) for y in x.exprs]
+            is_and = isinstance(x, Ands)
+            if not vals:
+                return const(T_BOOL, is_and)
+            dom = np.zeros(n, bool)
+            anynull = np.zeros(n, bool)
+            for a in vals:
+                b = a.v.astype(bool)
+                dom |= a.ok & (~b if is_and else b)
+                anynull |= ~a.ok
+            res = np.full(n, not is_and) if True else None
+            res = np.where(dom, not is_and, is_and)
+            ok = dom | ~anynull
+            return Val(T_BOOL, res.astype(bool), ok)
+        if isinstance(x, Coalesce):
+            vals = [go(y) for y in x.exprs]
+            t = T_NULL
+            for a in vals:
+                if a.t != T_NULL:
+                    t = T_FLOAT if (t == T_INT and a.t == T_FLOAT) or (t == T_FLOAT and a.t == T_INT) else (a.t if t == T_NULL else t)
+            out = _empty_vals(t, n)
+            ok = np.zeros(n, bool)
+            for a in vals:
+                take = ~ok & a.ok
+                if t == T_FLOAT:
+                    out[take] = _num(a)[take]
+                else:
+                    out[take] = a.v[take]
+                ok |= a.ok
+            return Val(t, out, ok)
+        raise NotImplementedError(f"oracle: unsupported expression {x}")
+
+    return go(e)
+
+
+def _key_codes(cols, null_is_group=True):
+    """Joint integer codes of rows over `cols` (NULL → its own code, or -1)."""
+    n = len(cols[0].ok) if cols else 0
+    parts = []
+    anynull = np.zeros(n, bool)
+    for c in cols:
+        anynull |= ~c.ok
+        if c.t == T_STRING:
+            vals = np.array([v if ok else "" for v, ok in zip(c.v, c.ok)], dtype=object)
+            _, inv = np.unique(vals.astype(str), return_inverse=True) if n else (None, np.zeros(0, np.int64))
+            parts.append(np.asarray(inv, dtype=np.int64))
+        elif c.t == T_FLOAT:
+            f = np.where(c.ok, c.v.astype(np.float64), 0.0)
+            f = np.where(f == 0, 0.0, f)  # -0.0 == 0.0
+            parts.append(f.view(np.int64))
+        else:
+            parts.append(np.where(c.ok, c.v.astype(np.int64), 0))
+        parts.append(c.ok.astype(np.int64))
+    if n == 0:
+        return np.zeros(0, np.int64), anynull
+    if not parts:
+        return np.zeros(n, np.int64), anynull
+    stacked = np.stack(parts, axis=1)
+    _, inv = np.unique(stacked, axis=0, return_inverse=True)
+    codes = np.asarray(inv, dtype=np.int64).reshape(-1)
+    if not null_is_group:
+        codes = np.where(anynull, -1, codes)
+    return codes, anynull
+
+
+class OracleTable:
+    def __init__(self, order, cols, n):
+        self._order = list(order)
+        self._cols = dict(cols)
+        self._n = int(n)
+        if len(set(self._order)) != len(self._order):
+            raise ValueError("duplicate column names")
+
+    def _mk(self, order, cols, n):
+        return OracleTable(order, cols, n)
+
+    # ----------------------------------------------------------- CypherTable
+    @property
+    def physicalColumns(self):
+        return list(self._order)
+
+    @property
+    def columnType(self):
+        return {c: CAPF_TO_CT[self._cols[c].t] for c in self._order}
+
+    def capf_type(self, c):
+        return self._cols[c].t
+
+    @property
+    def size(self):
+        return self._n
+
+    def column_values(self, col):
+        c = self._cols[col]
+        out = []
+        for v, ok in zip(c.v.tolist(), c.ok.tolist()):
+            if not ok:
+                out.append(None)
+            elif c.t == T_BOOL:
+                out.append(bool(v))
+            elif c.t == T_INT:
+                out.append(int(v))
+            elif c.t == T_FLOAT:
+                out.append(float(v))
+            else:
+                out.append(v)
+        return out
+
+    @property
+    def rows(self):
+        data = {c: self.column_values(c) for c in self._order}
+        return [{c: data[c][i] for c in self._order} for i in range(self._n)]
+
+    # ----------------------------------------------------------- Table[T]
+    def cache(self):
+        return self
+
+    def select(self, *cols):
+        pairs = [(c, c) if isinstance(c, str) else tuple(c) for c in cols]
+        for c, _ in pairs:
+            if c not in self._cols:
+                raise KeyError(c)
+        return self._mk([a for _, a in pairs], {a: self._cols[c] for c, a in pairs}, self._n)
+
+    def filter(self, expr, header=None, params=None):
+        v = evaluate(expr, self, header, params or {})
+        keep = np.nonzero(v.ok & v.v.astype(bool))[0]
+        return self._take(keep)
+
+    def _take(self, idx):
+        return self._mk(self._order, {c: k.take(idx) for c, k in self._cols.items()}, len(idx))
+
+    def drop(self, *cols):
+        left = [c for c in self._order if c not in cols]
+        return self.select(*left)
+
+    def join(self, other, join_type, *pairs):
+        overlap = set(self._order) & set(other._order)
+        assert not overlap, f"overlapping columns: {overlap}"
+        nl, nr = self._n, other._n
+        if join_type == "cross":
+            li = np.repeat(np.arange(nl), nr)
+            ri = np.tile(np.arange(nr), nl)
+        else:
+            lk = [self._cols[a] for a, _ in pairs]
+            rk = [other._cols[b] for _, b in pairs]
+            # joint codes over the concatenation so equal keys share a code
+            both = [Col(a.t if a.t != T_NULL else b.t, np.concatenate([a.v, b.v]) if a.v.dtype == b.v.dtype
+                        else np.concatenate([a.v.astype(object), b.v.astype(object)]),
+                        np.concatenate([a.ok, b.ok])) for a, b in zip(lk, rk)]
+            codes, _ = _key_codes(both, null_is_group=False)
+            lc, rc = codes[:nl], codes[nl:]
+            order = np.argsort(rc, kind="stable")
+            rs = rc[order]
+            lo = np.searchsorted(rs, lc, side="left")
+            hi = np.searchsorted(rs, lc, side="right")
+            cnt = np.where(lc < 0, 0, hi - lo)
+            li = np.repeat(np.arange(nl), cnt)
+            starts = np.repeat(lo, cnt)
+            offs = np.arange(len(li)) - np.repeat(np.cumsum(cnt) - cnt, cnt)
+            ri = order[starts + offs] if len(li) else np.zeros(0, np.int64)
+            if join_type in ("left_outer", "full_outer"):
+                miss = np.nonzero(cnt == 0)[0]
+                li = np.concatenate([li, miss])
+                ri = np.concatenate([ri, np.full(len(miss), -1)])
+            if join_type in ("right_outer", "full_outer"):
+                matched = np.zeros(nr, bool)
+                matched[ri[ri >= 0]] = True
+                miss = np.nonzero(~matched)[0]
+                li = np.concatenate([li, np.full(len(miss), -1)])
+                ri = np.concatenate([ri, miss])
+        cols = {c: k.take(li) for c, k in self._cols.items()}
+        cols.update({c: k.take(ri) for c, k in other._cols.items()})
+        return self._mk(self._order + other._order, cols, len(li))
+
+    def unionAll(self, other):
+        if set(self._order) != set(other._order):
+            raise ValueError("unionAll: column sets differ")
+        cols = {}
+        for c in self._order:
+            a, b = self._cols[c], other._cols[c]
+            t = a.t if a.t != T_NULL else b.t
+            if a.t != b.t and T_NULL not in (a.t, b.t):
+                raise ValueError(f"Equal column types for union all: {c}")
+            va = a.v if a.t == t else _empty_vals(t, len(a.ok))
+            vb = b.v if b.t == t else _empty_vals(t, len(b.ok))
+            cols[c] = Col(t, np.concatenate([va, vb]), np.concatenate([a.ok, b.ok]))
+        return self._mk(self._order, cols, self._n + other._n)
+
+    def orderBy(self, *sort_items, header=None, params=None):
+        idx = np.arange(self._n)
+        for e, o in reversed(sort_items):
+            v = evaluate(e, self, header, params or {})
+            desc = o in ("desc", "Descending", True)
+            vals = v.v[idx]
+            ok = v.ok[idx]
+            if v.t == T_STRING:
+                raise NotImplementedError("ORDER BY on strings")
+            key = vals.astype(np.float64) if v.t == T_FLOAT else vals.astype(np.int64)
+            if desc:
+                key = -key if v.t == T_FLOAT else ~key
+            o1 = np.argsort(key, kind="stable")
+            idx = idx[o1]
+            ok = ok[o1]
+            nulls = ~ok
+            o2 = np.argsort(~nulls if desc else nulls, kind="stable")
+            idx = idx[o2]
+        return self._take(idx)
+
+    def skip(self, n):
+        return self._take(np.arange(min(n, self._n), self._n))
+
+    def limit(self, n):
+        return self._take(np.arange(min(n, self._n)))
+
+    def distinct(self, *cols):
+        keys = [self._cols[c] for c in (cols or self._order)]
+        if not keys:
+            return self._take(np.arange(min(1, self._n)))
+        codes, _ = _key_codes(keys)
+        _, first = np.unique(codes, return_index=True)
+        return self._take(np.sort(first))
+
+    def group(self, by, aggregations, header=None, params=None):
+        gcols = []
+        for v in by:
+            for e in header.owned_by(v):
+                c = header.column(e)
+                if c in self._cols and c not in gcols:
+                    gcols.append(c)
+        if gcols:
+            codes, _ = _key_codes([self._cols[c] for c in gcols])
+            uniq, first, inv = np.unique(codes, return_index=True, return_inverse=True)
+            order = np.argsort(first)
+            remap = np.empty_like(order)
+            remap[order] = np.arange(len(order))
+            gid = remap[np.asarray(inv).reshape(-1)]
+            ng = len(uniq)
+            reps = np.sort(first)
+        else:
+            gid = np.zeros(self._n, dtype=np.int64)
+            ng = 1
+            reps = np.zeros(1, dtype=np.int64)
+        out_order = list(gcols)
+        cols = {c: self._cols[c].take(reps) for c in gcols}
+        for name, agg in aggregations.items():
+            cols[name] = self._aggregate(agg, gid, ng, header, params or {})
+            out_order.append(name)
+        return self._mk(out_order, cols, ng)
+
+    def _aggregate(self, agg, gid, ng, header, params):
+        if not isinstance(agg, Aggregator):
+            raise TypeError(agg)
+        if agg.kind == AGG_COUNT_STAR:
+            return Col(T_INT, np.bincount(gid, minlength=ng).astype(np.int64), np.ones(ng, bool))
+        v = evaluate(agg.expr, self, header, params)
+        sel = v.ok
+        if agg.kind == AGG_COUNT:
+            if agg.distinct:  # Spark semantics (Flink ignores DISTINCT)
+                seen = set()
+                cnt = np.zeros(ng, np.int64)
+                for g, x, ok in zip(gid.tolist(), v.v.tolist(), sel.tolist()):
+                    if ok and (g, x) not in seen:
+                        seen.add((g, x))
+                        cnt[g] += 1
+                return Col(T_INT, cnt, np.ones(ng, bool))
+            return Col(T_INT, np.bincount(gid[sel], minlength=ng).astype(np.int64), np.ones(ng, bool))
+        if v.t == T_STRING and agg.kind != AGG_COUNT:
+            raise NotImplementedError("aggregate of strings")
+        cnt = np.bincount(gid[sel], minlength=ng)
+        t = v.t
+        res = _empty_vals(t if t != T_NULL else T_INT, ng)
+        # sequential fold in row order (Flink accumulates per group)
+        acc = [None] * ng
+        for g, x, ok in zip(gid.tolist(), v.v.tolist(), sel.tolist()):
+            if not ok:
+                continue
+            a = acc[g]
+            if agg.kind in (AGG_SUM, AGG_AVG):
+                acc[g] = x if a is None else a + x
+            elif agg.kind == AGG_MIN:
+                acc[g] = x if a is None or x < a else a
+            else:
+                acc[g] = x if a is None or x > a else a
+        for g in range(ng):
+            a = acc[g]
+            if a is None:
+                continue
+            if agg.kind == AGG_AVG:
+                if t == T_FLOAT:
+                    a = a / cnt[g]
+                else:  # Java long division
+                    q = abs(int(a)) // int(cnt[g])
+                    a = q if a >= 0 else -q
+            if t == T_INT:
+                a = ((int(a) + 2 ** 63) % 2 ** 64) - 2 ** 63  # LONG wrap-around
+            res[g] = a
+        return Col(t if t != T_NULL else T_INT, res, cnt > 0)
+
+    def withColumns(self, *columns, header=None, params=None):
+        order = list(self._order)
+        cols = dict(self._cols)
+        for e, name in columns:
+            v = evaluate(e, self, header, params or {})
+            vals = v.v
+            if v.t == T_STRING:
+                vals = np.asarray(vals, dtype=object)
+            cols[name] = Col(v.t, vals, v.ok)
+            if name not in order:
+                order.append(name)
+        return self._mk(order, cols, self._n)
+
+    def show(self, rows=20):
+        for r in self.rows[:rows]:
+            print(r)

@@ -1,0 +1,36 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+if GOLDEN not in sys.path:
+    sys.path.insert(0, GOLDEN)
+
+import capf_import  # noqa: E402,F401
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")
+    config.addinivalue_line("markers", "slow: larger parity sizes")
+
+
+def bag(rows):
+    """okapi-testing Bag (OT/Bag.scala:29-51): multiset equality of records."""
+    def norm(v):
+        if isinstance(v, float) and v == int(v):
+            return ("num", float(v))
+        if isinstance(v, (int, float)) and not isinstance(v, bool):
+            return ("num", float(v))
+        return ("v", v)
+    return sorted(tuple(sorted((k, norm(v)) for k, v in r.items())) for r in rows)
+
+
+@pytest.fixture(scope="session")
+def gpu_session():
+    from capf_amd.table import GpuSession
+    s = GpuSession(0)
+    yield s

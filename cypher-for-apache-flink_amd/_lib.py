@@ -122,6 +122,19 @@ _SIGS = {
 EXPORTED_SYMBOLS = sorted(_SIGS)
 
 _lib = None
+_exiting = False
+
+
+def _at_exit():
+    # handles still alive at interpreter exit are leaked, not released: the
+    # HIP runtime may already be shutting down
+    global _exiting
+    _exiting = True
+
+
+import atexit  # noqa: E402
+
+atexit.register(_at_exit)
 
 
 def load(path=LIB_PATH):

@@ -40,7 +40,14 @@ struct Error : std::runtime_error {
                    std::string(#expr) + ": " + hipGetErrorString(_e));                   \
   } while (0)
 
-#define KERNEL_CHECK() HIP_CHECK(hipGetLastError())
+// CAPF_DEBUG_SYNC=1: synchronise after every launch so an asynchronous fault
+// is reported at the kernel that caused it.
+bool debug_sync_enabled();
+#define KERNEL_CHECK()                                         \
+  do {                                                         \
+    HIP_CHECK(hipGetLastError());                              \
+    if (::capf::debug_sync_enabled()) HIP_CHECK(hipDeviceSynchronize()); \
+  } while (0)
 
 enum class Type : int32_t {
   Null = CAPF_TYPE_NULL,

@@ -279,10 +279,27 @@ static bool collect(const NodePtr &n, JoinGraph &g, std::vector<ColRef> &out) {
       if (!collect(n->kids[1], g, r)) return false;
       for (auto &kp : n->join_keys) {
         if (n->kids[0]->types[kp.first] != Type::Int64) return false;
+        if (l[kp.first].leaf < 0 || r[kp.second].leaf < 0) return false;
         g.eqs.emplace_back(l[kp.first], r[kp.second]);
       }
       out = l;
       out.insert(out.end(), r.begin(), r.end());
+      return true;
+    }
+    case Kind::WithColumns: {
+      // transparent when it only adds/replaces columns by literals (the
+      // constant label / NULL property columns of scan alignment,
+      // RelationalPlanner.scala:447-515); the literal columns themselves can
+      // not take part in a join or predicate of the fused count
+      bool literal_only = true;
+      for (auto &p : n->exprs)
+        literal_only &= p.code.size() == 1 && p.code[0].op != OP_COL;
+      if (!literal_only) break;
+      std::vector<ColRef> c;
+      if (!collect(n->kids[0], g, c)) return false;
+      out = c;
+      out.resize(n->names.size(), ColRef{-2, -1});
+      for (int t : n->target_index) out[t] = ColRef{-2, -1};
       return true;
     }
     case Kind::Filter: {
@@ -293,7 +310,10 @@ static bool collect(const NodePtr &n, JoinGraph &g, std::vector<ColRef> &out) {
       std::vector<int> refs;
       for (auto &nm : n->pred.names) refs.push_back(kid->col_index(nm));
       std::set<int> leaves;
-      for (int r : refs) leaves.insert(c[r].leaf);
+      for (int r : refs) {
+        if (c[r].leaf < 0) return false;
+        leaves.insert(c[r].leaf);
+      }
       if (leaves.size() == 1) {
         // single-table predicate: push into the leaf with leaf column names
         int lf = *leaves.begin();
@@ -616,8 +636,10 @@ static bool match_chain2(const JoinGraph &g, Chain2 &c) {
       if (sa == sb || sc == sb || sa == x.leaf || sc == y.leaf) return false;
       std::set<int> all{x.leaf, y.leaf, sa, sb, sc};
       if (all.size() != 5) return false;
+      if (edges_of(sa).size() != 1 || edges_of(sc).size() != 1 || edges_of(sb).size() != 2)
+        return false;
       for (int nl : {sa, sb, sc})
-        if (edges_of(nl).size() != 1 || !g.leaves[nl].col_eqs.empty()) return false;
+        if (!g.leaves[nl].col_eqs.empty()) return false;
       c.ra = x.leaf;
       c.rb = y.leaf;
       c.sa = sa;

@@ -12,6 +12,14 @@
 
 namespace capf {
 
+bool debug_sync_enabled() {
+  static const bool on = [] {
+    const char *e = getenv("CAPF_DEBUG_SYNC");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 const char *type_name(Type t) {
   switch (t) {
     case Type::Null: return "NULL";

@@ -1,0 +1,78 @@
+"""One process per GPU: the hash-partitioned 2-hop count over RCCL.
+
+SURVEY §8(e): the graph is partitioned over G GPUs and the 2-hop join needs
+one exchange keyed by the middle node b.  Because the fused count only needs
+per-node path multiplicities (the "count-only frontier"), the exchange is
+reduced to per-node histograms:
+
+  1. rank r holds the rel shard E_r (a contiguous edge-index range of the
+     R-MAT stream — R-MAT edges are i.i.d., so this is a uniform partition);
+     it computes in_r[v] = |{e ∈ E_r : dst = v}|, out_r[v] = |{e ∈ E_r : src = v}|
+     and its self-loop count with ONE pass over its shard
+     (capf_chain2_local_hists);
+  2. reduce-scatter (RCCL over xGMI) gives rank r the global in/out counts of
+     the nodes it owns (contiguous node range V_r) — the repartition by join
+     key b;
+  3. rank r computes Σ_{b ∈ V_r} in[b]·out[b] (capf_dot_u32);
+  4. one int64 all-reduce of (partial − local self-loops) gives the count.
+
+Bit-exact: every term is an integer; uint32 histogram sums are exact below
+2^32 rels per node.  The exchange volume is 2·N·4 B per rank, independent of
+the number of joined rows.
+"""
+import torch
+import torch.distributed as dist
+
+
+def edge_range(m, rank, world):
+    return m * rank // world, m * (rank + 1) // world
+
+
+def padded_nodes(n, world):
+    """Node count padded so every rank's slice is a multiple of 4 (dwordx4)."""
+    q = 4 * world
+    return (n + q - 1) // q * q
+
+
+def reduce_scatter(t, world, group=None):
+    """Sum `t` over ranks and return this rank's contiguous 1/world slice."""
+    out = torch.empty(t.numel() // world, dtype=t.dtype, device=t.device)
+    if dist.get_backend(group) == "nccl":
+        dist.reduce_scatter_tensor(out, t, op=dist.ReduceOp.SUM, group=group)
+    else:  # gloo (CPU tests): all-reduce then slice
+        t = t.clone()
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        r = dist.get_rank(group)
+        out.copy_(t[r * out.numel():(r + 1) * out.numel()])
+    return out
+
+
+def combine_two_hop(in_hist, out_hist, local_loops, dot_fn, group=None):
+    """Steps 2-4: exchange the local histograms and reduce to the count.
+
+    in_hist / out_hist: int32 tensors of padded length; dot_fn(a, b) -> int
+    computes Σ a·b exactly (GPU: capf_dot_u32; tests: numpy)."""
+    world = dist.get_world_size(group)
+    rin = reduce_scatter(in_hist, world, group)
+    rout = reduce_scatter(out_hist, world, group)
+    partial = dot_fn(rin, rout) - int(local_loops)
+    acc = torch.tensor([partial], dtype=torch.int64, device=in_hist.device)
+    dist.all_reduce(acc, op=dist.ReduceOp.SUM, group=group)
+    return int(acc.item())
+
+
+def gpu_two_hop_count(session, rels, n_nodes, node_base=0, group=None, hists=None):
+    """Distributed 2-hop count(*) for this rank's rel shard `rels` (GpuTable)."""
+    from .table import dot_u32
+    world = dist.get_world_size(group)
+    npad = padded_nodes(n_nodes, world)
+    if hists is None:
+        hists = (torch.zeros(npad, dtype=torch.int32, device="cuda"),
+                 torch.zeros(npad, dtype=torch.int32, device="cuda"))
+    in_h, out_h = hists
+    loops = rels.chain2_local_hists("source", "target", node_base, n_nodes, in_h.data_ptr(), out_h.data_ptr())
+    if npad > n_nodes:
+        in_h[n_nodes:].zero_()
+        out_h[n_nodes:].zero_()
+    return combine_two_hop(in_h, out_h, loops,
+                           lambda a, b: dot_u32(session, a.data_ptr(), b.data_ptr(), a.numel()), group)

@@ -165,7 +165,7 @@ class GpuTable:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h and _lib._lib is not None and getattr(self.session, "_h", None):
+        if h and _lib._lib is not None and not _lib._exiting and getattr(self.session, "_h", None):
             _lib._lib.capf_table_release(h)
 
     def _new(self, fn, *args):

@@ -1,0 +1,78 @@
+"""Generates the committed golden fixtures (run from the repo root in the dev
+container; /root/reference is only read here, never at test time):
+
+  reference_cases.json  expected Bags of the reference acceptance tests
+                        (transcribed in reference_cases.py) + the oracle's Bags
+  ldbc_sample.json      the reference's LDBC sample KNOWS graph
+                        (morpheus-examples/src/main/resources/ldbc/csv/
+                        person_0_0.csv.gz, person_knows_person_0_0.csv.gz)
+  rmat_counts.json      R-MAT counts of configs 2/3 at small scales by the
+                        closed forms (oracle/rmat.c), plus the config-5 query
+                        on the LDBC sample by the oracle table
+"""
+import csv
+import gzip
+import io
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, HERE)
+
+import capf_import  # noqa: E402,F401
+from capf_amd.graph import ScanGraph  # noqa: E402
+from capf_amd.planner import run  # noqa: E402
+from oracle import cmodel  # noqa: E402
+from oracle.create_parser import parse_create  # noqa: E402
+from oracle.table_np import OracleSession  # noqa: E402
+
+LDBC = "/root/reference/morpheus-examples/src/main/resources/ldbc/csv"
+
+
+def ldbc_sample():
+    with gzip.open(os.path.join(LDBC, "person_0_0.csv.gz"), "rt") as f:
+        persons = [int(r["id"]) for r in csv.DictReader(f, delimiter="|")]
+    with gzip.open(os.path.join(LDBC, "person_knows_person_0_0.csv.gz"), "rt") as f:
+        rd = csv.reader(f, delimiter="|")
+        next(rd)
+        knows = [[int(r[0]), int(r[1])] for r in rd]
+    return {"source": "morpheus-examples/src/main/resources/ldbc/csv/person_{0_0,knows_person_0_0}.csv.gz",
+            "persons": persons, "knows": knows}
+
+
+def main():
+    from reference_cases import CASES
+    out = []
+    for cid, src, create, query, expected in CASES:
+        got = run(ScanGraph.from_data(OracleSession(), parse_create(create)), query)
+        out.append({"id": cid, "source": src, "create": create.strip(), "expected": expected, "oracle": got})
+    with open(os.path.join(HERE, "reference_cases.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+    if os.path.isdir(LDBC):
+        with open(os.path.join(HERE, "ldbc_sample.json"), "w") as f:
+            json.dump(ldbc_sample(), f)
+
+    counts = {"rmat": {}, "params": {"a": cmodel.A, "b": cmodel.B, "c": cmodel.C, "edge_factor": 16,
+                                      "seed": "0x5EED0000 + scale"}}
+    for scale in range(6, 17, 2):
+        s, d = cmodel.rmat(scale)
+        n = 1 << scale
+        person = cmodel.labels(n, cmodel.rmat_seed(scale))
+        counts["rmat"][str(scale)] = {
+            "two_hop": int(cmodel.count_2hop(s, d, n)),
+            "one_hop_person": int(cmodel.count_1hop(s, d, n, in_a=person)),
+            "self_loops": int((s == d).sum()),
+        }
+    from ldbc import config5_query, ldbc_graph_data
+    g = ScanGraph.from_data(OracleSession(), ldbc_graph_data())
+    counts["ldbc_config5"] = sorted(([r["reach"], r["n"]] for r in run(g, config5_query())))
+    with open(os.path.join(HERE, "rmat_counts.json"), "w") as f:
+        json.dump(counts, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

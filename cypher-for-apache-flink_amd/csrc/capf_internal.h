@@ -281,6 +281,10 @@ int32_t record_error(int32_t code, const char *msg);
 
 // Fused counting over lazy inner-join trees (the Expand hot path).
 bool try_fused_count(const NodePtr &n, int64_t *out);
+// Radix-partitioned LDS histograms of the 2-hop count (chain2_partitioned.hip).
+bool chain2_partitioned(Session *s, const int64_t *u1, const int64_t *v1, const int64_t *u2,
+                        const int64_t *v2, int64_t n, int64_t lo, int64_t hi, uint32_t *h_in,
+                        uint32_t *h_out, uint64_t *loops_out);
 
 }  // namespace capf
 

@@ -738,7 +738,17 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
     a.h1 = h1;
     a.h2 = h2;
     a.loops = (unsigned long long *)acc->p + 1;
-    if (n > 0) {
+    uint64_t part_loops = 0;
+    const char *mode = getenv("CAPF_CHAIN2");  // "atomic" | "partitioned" (default: by size)
+    const bool want_part = all_ones && wa.map.m.lo == lo && wc.map.m.lo == lo &&
+                           wa.map.m.hi == hi && wc.map.m.hi == hi &&
+                           (mode ? strcmp(mode, "partitioned") == 0 : n >= (int64_t(1) << 22));
+    if (n > 0 && want_part &&
+        chain2_partitioned(s, a.u1, a.v1, a.u2, a.v2, n, lo, hi, h1, h2, &part_loops)) {
+      HIP_CHECK(hipMemcpyAsync((unsigned long long *)acc->p + 1, &part_loops, 8,
+                               hipMemcpyHostToDevice, s->stream));
+      s->sync();
+    } else if (n > 0) {
       KernelTimer kt(s, "chain2_hist", 16.0 * n);
       unsigned grid = grid_for(n, 256, 256 * 32);
       if (all_ones)

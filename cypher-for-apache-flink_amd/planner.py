@@ -198,7 +198,8 @@ def expand_into(graph, source: Var, rel: RelP, target: Var, in_op: Planned, dire
 
 def var_length_expand(graph, source: Var, rel: RelP, target: Var, src_op: Planned, tgt_op: Planned,
                       is_expand_into: bool) -> Planned:
-    """DirectedVarLengthExpandPlanner.plan (VarLengthExpandPlanner.scala:246-259)."""
+    """Directed/UndirectedVarLengthExpandPlanner.plan
+    (VarLengthExpandPlanner.scala:246-259, 277-307), join for join."""
     lower, upper = rel.length
     edge = Var(rel.name, "RELATIONSHIP")
     edge_scan = graph.rel_scan(rel.name, rel.types)
@@ -209,32 +210,54 @@ def var_length_expand(graph, source: Var, rel: RelP, target: Var, src_op: Planne
     existing_rels = [e for e in src_op.header.vars() if e.ctype == "RELATIONSHIP"]
 
     def iso(new, cands):
+        # isomorphismFilter (:178-179); Ands() of nothing is TrueLit → no Filter
         return Ands(*[Not(Equals(e, new)) for e in cands]) if cands else TrueLit
 
-    paths = []
-    # init (:82-97)
-    e1 = seg(1)
-    step = alias_var(edge_scan, edge, e1)
-    cur = filter_(join(src_op, step, [(source, StartNode(e1))]), iso(e1, existing_rels))
-    edges = [e1]
-    if upper >= 1:
-        paths.append((cur, list(edges)))
-    # expand(i) (:107-135)
-    for i in range(2, upper + 1):
+    def init(direction):  # (:82-97)
+        e1 = seg(1)
+        step = alias_var(edge_scan, edge, e1)
+        key = StartNode(e1) if direction == "out" else EndNode(e1)
+        return filter_(join(src_op, step, [(source, key)]), iso(e1, existing_rels))
+
+    def expand_step(i, table, dirs, edges):  # (:107-135)
         ei = seg(i)
         step = alias_var(edge_scan, edge, ei)
-        cur = filter_(join(cur, step, [(EndNode(edges[-1]), StartNode(ei))]), iso(ei, edges))
-        edges.append(ei)
-        paths.append((cur, list(edges)))
-    paths = [(p, es) for p, es in paths if len(es) >= lower]
+        last = edges[-1]
+        left, right = {
+            ("out", "out"): (EndNode(last), StartNode(ei)),
+            ("out", "in"): (EndNode(last), EndNode(ei)),
+            ("in", "out"): (StartNode(last), EndNode(ei)),
+            ("in", "in"): (StartNode(last), StartNode(ei)),
+        }[dirs]
+        return filter_(join(table, step, [(left, right)]), iso(ei, edges)), ei
 
-    # addTargetOps (:218-229)
-    def add_target(p, last):
+    def add_target(p, last, direction):  # addTargetOps (:218-229)
+        key = EndNode(last) if direction == "out" else StartNode(last)
         if is_expand_into:
-            return filter_(p, Equals(target, EndNode(last)))
-        return join(p, tgt_op, [(EndNode(last), target)])
+            return filter_(p, Equals(target, key))
+        return join(p, tgt_op, [(key, target)])
 
-    with_targets = [add_target(p, es[-1]) for p, es in paths]
+    with_targets = []
+    if rel.direction != "both":
+        acc = [(init("out"), [seg(1)])]
+        for i in range(2, upper + 1):
+            last, edges = acc[-1]
+            nxt, ei = expand_step(i, last, ("out", "out"), edges)
+            acc.append((nxt, edges + [ei]))
+        acc = [(p, es) for p, es in acc if len(es) >= lower] if upper >= 1 else []
+        with_targets = [add_target(p, es[-1], "out") for p, es in acc]
+    else:
+        acc = [((init("out"), init("in")), [seg(1)])]
+        for i in range(2, upper + 1):
+            (last, last_rev), edges = acc[-1]
+            out_out, ei = expand_step(i, last, ("out", "out"), edges)
+            out_in, _ = expand_step(i, last, ("out", "in"), edges)
+            in_out, _ = expand_step(i, last_rev, ("in", "out"), edges)
+            in_in, _ = expand_step(i, last_rev, ("in", "in"), edges)
+            acc.append(((union_all(out_out, in_out), union_all(out_in, in_in)), edges + [ei]))
+        acc = [(p, es) for p, es in acc if len(es) >= lower] if upper >= 1 else []
+        with_targets = [union_all(add_target(o, es[-1], "out"), add_target(n, es[-1], "in"))
+                        for (o, n), es in acc]
     if lower == 0:
         with_targets.append(_copy_element(src_op, source, target, tgt_op))
     if not with_targets:

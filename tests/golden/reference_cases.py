@@ -235,3 +235,14 @@ CASES = [
            [ret(("p1.name", P("p1", "name")), ("p2.name", P("p2", "name")), ("p3.name", P("p3", "name")))]),
      [{"p1.name": "Alice", "p2.name": "Bob", "p3.name": "Eve"}]),
 ]
+
+CASES.append(
+    ("undirected_var_length", "MTa/MatchTests.scala:360-376",
+     """CREATE (a:A {prop: 'a'})
+        CREATE (b:B {prop: 'b'})
+        CREATE (c:C {prop: 'c'})
+        CREATE (a)-[:T]->(b)
+        CREATE (b)<-[:T]-(c)""",
+     Query([Match([NodeP("a", ("A",)), NodeP("other")], [RelP("r", "a", "other", direction="both", length=(2, 2))])],
+           [ret(("a.prop", P("a", "prop")), ("other.prop", P("other", "prop")))]),
+     [{"a.prop": "a", "other.prop": "c"}]))

@@ -190,8 +190,24 @@ struct PendingTiming {
   hipEvent_t a, b;
 };
 
+// Stream-ordered caching allocator over hipMalloc.  All work of a session is
+// issued on its one stream, so a freed block may be handed to the next
+// allocation immediately: stream order makes every later use of the block run
+// after every earlier one.  (HIP's own stream-ordered pool, hipMallocAsync,
+// gave non-deterministic results on this stack under heavy reuse — measured,
+// see DESIGN.md.)
+struct BlockCache {
+  std::multimap<size_t, void *> free_blocks;  // rounded size → block
+  std::map<void *, size_t> sizes;             // every block ever allocated
+  size_t cached = 0;
+  void *get(size_t rounded);
+  void put(void *p);
+  void release_all();
+};
+
 struct Session {
   int device = 0;
+  BlockCache cache;
   std::vector<PendingTiming> pending;   // recorded, not yet resolved
   std::vector<hipEvent_t> event_pool;
   hipEvent_t get_event();

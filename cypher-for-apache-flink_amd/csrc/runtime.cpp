@@ -31,12 +31,60 @@ const char *type_name(Type t) {
   return "?";
 }
 
+static int alloc_mode() {  // CAPF_ALLOC=sync → hipMalloc/hipFree per buffer (diagnostics)
+  static const int m = [] {
+    const char *e = getenv("CAPF_ALLOC");
+    return (e && strcmp(e, "sync") == 0) ? 1 : 0;
+  }();
+  return m;
+}
+
+static size_t round_block(size_t bytes) {
+  // 256 B granule below 1 MiB, 2 MiB granule above: big buffers of similar
+  // size (per-query histograms, gathers) are reused across queries
+  if (bytes < (size_t(1) << 20)) return (bytes + 255) & ~size_t(255);
+  const size_t g = size_t(2) << 20;
+  return (bytes + g - 1) / g * g;
+}
+
+void *BlockCache::get(size_t rounded) {
+  auto it = free_blocks.lower_bound(rounded);
+  // reuse a cached block up to 25 % larger than needed
+  if (it != free_blocks.end() && it->first <= rounded + rounded / 4) {
+    void *p = it->second;
+    cached -= it->first;
+    free_blocks.erase(it);
+    return p;
+  }
+  return nullptr;
+}
+
+void BlockCache::put(void *p) {
+  auto it = sizes.find(p);
+  if (it == sizes.end()) return;
+  free_blocks.emplace(it->second, p);
+  cached += it->second;
+}
+
+void BlockCache::release_all() {
+  for (auto &kv : free_blocks) {
+    sizes.erase(kv.second);
+    (void)hipFree(kv.second);
+  }
+  free_blocks.clear();
+  cached = 0;
+}
+
 DevBuf::~DevBuf() {
   if (owned && p) {
-    if (s && s->stream)
-      (void)hipFreeAsync(p, s->stream);
-    else
+    if (alloc_mode() == 1) {
+      if (s && s->stream) (void)hipStreamSynchronize(s->stream);
       (void)hipFree(p);
+    } else if (s) {
+      s->cache.put(p);  // stream-ordered reuse, no synchronisation
+    } else {
+      (void)hipFree(p);
+    }
   }
 }
 
@@ -45,9 +93,24 @@ BufPtr Session::alloc(size_t bytes) {
   b->s = this;
   b->bytes = bytes;
   if (bytes == 0) return b;
-  // 256-byte rounding keeps every column 16-B aligned for dwordx4 access.
-  size_t rounded = (bytes + 255) & ~size_t(255);
-  HIP_CHECK(hipMallocAsync(&b->p, rounded, stream));
+  const size_t rounded = round_block(bytes);  // keeps every column 16-B aligned
+  if (alloc_mode() == 1) {
+    HIP_CHECK(hipMalloc(&b->p, rounded));
+  } else {
+    b->p = cache.get(rounded);
+    if (!b->p) {
+      hipError_t e = hipMalloc(&b->p, rounded);
+      if (e == hipErrorOutOfMemory) {  // give cached blocks back and retry once
+        (void)hipGetLastError();
+        HIP_CHECK(hipStreamSynchronize(stream));
+        cache.release_all();
+        e = hipMalloc(&b->p, rounded);
+      }
+      HIP_CHECK(e);
+      cache.sizes[b->p] = rounded;
+    }
+  }
+  if (getenv("CAPF_POISON")) HIP_CHECK(hipMemsetAsync(b->p, 0xA5, rounded, stream));
   return b;
 }
 
@@ -527,13 +590,8 @@ capf_status capf_session_create(int32_t device, void *hip_stream, capf_session *
     HIP_CHECK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
     s.own_stream = true;
   }
-  // keep freed blocks in the stream-ordered pool instead of returning them to
-  // the driver: no hipMalloc on the hot path after warm-up.
-  hipMemPool_t pool;
-  if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
-    uint64_t thr = UINT64_MAX;
-    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-  }
+  // freed blocks go back to the session's caching allocator (BlockCache):
+  // no hipMalloc on the hot path after warm-up.
   HIP_CHECK(hipMalloc(&s.d_scalars, 64 * sizeof(int64_t)));
   HIP_CHECK(hipHostMalloc(&s.h_scalars, 64 * sizeof(int64_t), hipHostMallocDefault));
   *out = cs;
@@ -547,6 +605,7 @@ capf_status capf_session_destroy(capf_session *cs) {
   (void)hipStreamSynchronize(s.stream);
   s.resolve_profile();
   for (auto e : s.event_pool) (void)hipEventDestroy(e);
+  s.cache.release_all();
   (void)hipFree(s.d_scalars);
   (void)hipHostFree(s.h_scalars);
   if (s.own_stream) (void)hipStreamDestroy(s.stream);

@@ -21,11 +21,15 @@ def pytest_configure(config):
 def bag(rows):
     """okapi-testing Bag (OT/Bag.scala:29-51): multiset equality of records."""
     def norm(v):
-        if isinstance(v, float) and v == int(v):
-            return ("num", float(v))
-        if isinstance(v, (int, float)) and not isinstance(v, bool):
-            return ("num", float(v))
-        return ("v", v)
+        if v is None:
+            return ("0null", 0.0, "")
+        if isinstance(v, bool):
+            return ("bool", float(v), "")
+        if isinstance(v, (int, float)):
+            if isinstance(v, float) and v != v:
+                return ("nan", 0.0, "")
+            return ("num", float(v), "")
+        return ("str", 0.0, str(v))
     return sorted(tuple(sorted((k, norm(v)) for k, v in r.items())) for r in rows)
 
 

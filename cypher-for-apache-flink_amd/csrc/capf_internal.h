@@ -79,10 +79,17 @@ struct ColStats {
   bool dense_unique = false;   // values are exactly {min..max}, each once
 };
 
+// Physical encodings of an INT64 / STRING-code column.  The logical type is
+// unchanged (CTInteger = Flink LONG); ENC_FOR32 is frame-of-reference
+// compression chosen at ingest when max - min < 2^32: value = base + u32.
+enum : int32_t { ENC_PLAIN = 0, ENC_FOR32 = 1 };
+
 struct Column {
   Type type = Type::Null;
   int64_t n = 0;
-  BufPtr data;   // n * width bytes (nullptr for Type::Null or n == 0)
+  int32_t enc = ENC_PLAIN;
+  int64_t base = 0;  // ENC_FOR32 reference value
+  BufPtr data;   // n * width bytes (4 for ENC_FOR32; nullptr for Type::Null or n == 0)
   BufPtr valid;  // n bytes (1 = present) or nullptr = no nulls
   mutable std::mutex mu;
   mutable std::optional<ColStats> stats;
@@ -129,8 +136,15 @@ struct ColView {
   const void *data;
   const uint8_t *valid;
   int32_t type;
-  int32_t pad;
+  int32_t enc;   // ENC_PLAIN / ENC_FOR32
+  int64_t base;  // ENC_FOR32 reference value
 };
+
+// Integer value of row r of an INT64 / STRING column view (any encoding).
+__host__ __device__ inline int64_t ld_int(const ColView &c, int64_t r) {
+  return c.enc == ENC_FOR32 ? c.base + (int64_t)((const uint32_t *)c.data)[r]
+                            : ((const int64_t *)c.data)[r];
+}
 
 // ------------------------------------------------------------- plan nodes
 enum class Kind {
@@ -269,6 +283,9 @@ BufPtr compact_flags(Session *s, const uint8_t *d_flags, int64_t n, int64_t *out
 ColPtr concat_columns(Session *s, const ColPtr &a, const ColPtr &b, Type t);
 // Exclusive scan of int64 counts; returns total.
 int64_t exclusive_scan_i64(Session *s, const int64_t *d_in, int64_t *d_out, int64_t n);
+// uint32 exclusive scan (total < 2^32) left on the device, no host sync.
+void exclusive_scan_u32_async(Session *s, const uint32_t *d_in, uint32_t *d_out, int64_t n,
+                              uint32_t *d_total);
 // Hash grouping: group id per row (dense, 0..ngroups-1) and representative row per group.
 struct Grouping {
   BufPtr group_of_row;  // int64 [nrows]
@@ -291,6 +308,11 @@ BufPtr sort_permutation(Session *s, const std::vector<ColPtr> &keys,
                         const std::vector<int32_t> &desc, int64_t n);
 // Column statistics kernel.
 ColStats compute_stats(Session *s, const Column &c);
+// Frame-of-reference encodings: FOR32 stores an INTEGER column whose value
+// range spans < 2^32 as uint32 offsets from `base` (half the HBM bytes).
+// encode_column returns the input when the range does not fit.
+ColPtr encode_column(Session *s, const ColPtr &c);
+ColPtr decode_column(Session *s, const ColPtr &c);
 
 // Record an error for capf_last_error() (used by entry points outside runtime.cpp).
 int32_t record_error(int32_t code, const char *msg);
@@ -298,9 +320,9 @@ int32_t record_error(int32_t code, const char *msg);
 // Fused counting over lazy inner-join trees (the Expand hot path).
 bool try_fused_count(const NodePtr &n, int64_t *out);
 // Radix-partitioned LDS histograms of the 2-hop count (chain2_partitioned.hip).
-bool chain2_partitioned(Session *s, const int64_t *u1, const int64_t *v1, const int64_t *u2,
-                        const int64_t *v2, int64_t n, int64_t lo, int64_t hi, uint32_t *h_in,
-                        uint32_t *h_out, uint64_t *loops_out);
+// cols = {start(r1), end(r1), start(r2), end(r2)}, all plain or all FOR32.
+bool chain2_partitioned(Session *s, const ColView *cols, int64_t n, int64_t lo, int64_t hi,
+                        uint32_t *h_in, uint32_t *h_out, uint64_t *loops_out);
 
 }  // namespace capf
 

@@ -96,7 +96,7 @@ struct MsgJob {
 
 __device__ inline bool load_key(const ColView &c, int64_t r, int64_t &k) {
   if (c.type == CAPF_TYPE_NULL || !c.data || (c.valid && !c.valid[r])) return false;
-  k = ((const int64_t *)c.data)[r];
+  k = ld_int(c, r);
   return true;
 }
 
@@ -132,7 +132,7 @@ __global__ void k_message(const MsgJob *jp, int64_t n, unsigned long long *root_
 //   loops += Wa(u1)·Wb(v1)·Wc(v2) for rels with v1 = u2 (the r1 = r2 term)
 // Node weights are 1 on a dense id range (MAP_ONES) or a per-id count array.
 struct Chain2Args {
-  const int64_t *u1, *v1, *u2, *v2;  // rel columns (u2/v2 may alias u1/v1)
+  ColView u1, v1, u2, v2;  // non-null rel id columns (u2/v2 may alias u1/v1)
   int64_t n;
   DMap wa, wb, wc;
   int64_t lo, hi;
@@ -151,8 +151,8 @@ __global__ __launch_bounds__(256) void k_chain2_hist(Chain2Args a) {
   unsigned long long loops = 0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.n; e += stride) {
-    const int64_t x1 = a.u1[e], y1 = a.v1[e];
-    const int64_t x2 = a.u2[e], y2 = a.v2[e];
+    const int64_t x1 = ld_int(a.u1, e), y1 = ld_int(a.v1, e);
+    const int64_t x2 = ld_int(a.u2, e), y2 = ld_int(a.v2, e);
     const unsigned long long wa = w_of<ONES>(a.wa, x1);
     const unsigned long long wc = w_of<ONES>(a.wc, y2);
     if (wa && y1 >= a.lo && y1 <= a.hi) atomicAdd(&a.h1[y1 - a.lo], (uint32_t)wa);
@@ -194,12 +194,11 @@ __global__ __launch_bounds__(256) void k_chain2_dot(const uint32_t *h1, const ui
 }
 
 // per-id count array of a node table's id column over [lo, hi]
-__global__ void k_count_ids(const int64_t *ids, const uint8_t *valid, int64_t n, int64_t lo,
-                            int64_t hi, uint32_t *cnt) {
+__global__ void k_count_ids(ColView ids, int64_t n, int64_t lo, int64_t hi, uint32_t *cnt) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    if (valid && !valid[i]) continue;
-    int64_t k = ids[i];
+    if (ids.valid && !ids.valid[i]) continue;
+    int64_t k = ld_int(ids, i);
     if (k >= lo && k <= hi) atomicAdd(&cnt[k - lo], 1u);
   }
 }
@@ -685,8 +684,7 @@ static bool node_weights(Session *s, const LeafData &ld, int col, NodeWeights &w
   w.cnt = s->alloc(4 * range);
   HIP_CHECK(hipMemsetAsync(w.cnt->p, 0, 4 * range, s->stream));
   hipLaunchKernelGGL(k_count_ids, dim3(grid_for(c->n, 256)), dim3(256), 0, s->stream,
-                     (const int64_t *)c->data->p, c->valid ? (const uint8_t *)c->valid->p : nullptr,
-                     c->n, st.min, st.max, (uint32_t *)w.cnt->p);
+                     view_of(c), c->n, st.min, st.max, (uint32_t *)w.cnt->p);
   KERNEL_CHECK();
   memset(&w.map.m, 0, sizeof(w.map.m));
   w.map.m.kind = MAP_DENSE32;
@@ -725,10 +723,11 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
   if (len > 0) {
     HIP_CHECK(hipMemsetAsync(h->p, 0, 8 * std::max<int64_t>(len, 1) + 64, s->stream));
     Chain2Args a;
-    a.u1 = (const int64_t *)R.cols[c.u1]->data->p;
-    a.v1 = (const int64_t *)R.cols[c.v1]->data->p;
-    a.u2 = (const int64_t *)R.cols[c.u2]->data->p;
-    a.v2 = (const int64_t *)R.cols[c.v2]->data->p;
+    a.u1 = view_of(R.cols[c.u1]);
+    a.v1 = view_of(R.cols[c.v1]);
+    a.u2 = view_of(R.cols[c.u2]);
+    a.v2 = view_of(R.cols[c.v2]);
+    const ColView pc[4] = {a.u1, a.v1, a.u2, a.v2};
     a.n = n;
     a.wa = wa.map.m;
     a.wb = wb.map.m;
@@ -744,7 +743,7 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
                            wa.map.m.hi == hi && wc.map.m.hi == hi &&
                            (mode ? strcmp(mode, "partitioned") == 0 : n >= (int64_t(1) << 22));
     if (n > 0 && want_part &&
-        chain2_partitioned(s, a.u1, a.v1, a.u2, a.v2, n, lo, hi, h1, h2, &part_loops)) {
+        chain2_partitioned(s, pc, n, lo, hi, h1, h2, &part_loops)) {
       HIP_CHECK(hipMemcpyAsync((unsigned long long *)acc->p + 1, &part_loops, 8,
                                hipMemcpyHostToDevice, s->stream));
       s->sync();
@@ -842,8 +841,8 @@ extern "C" capf_status capf_chain2_local_hists(capf_session *cs, capf_table *rel
     BufPtr acc = s->alloc(16);
     HIP_CHECK(hipMemsetAsync(acc->p, 0, 16, s->stream));
     Chain2Args a;
-    a.u1 = a.u2 = (const int64_t *)src->data->p;
-    a.v1 = a.v2 = (const int64_t *)dst->data->p;
+    a.u1 = a.u2 = view_of(src);
+    a.v1 = a.v2 = view_of(dst);
     a.n = d->nrows;
     a.wa = a.wb = a.wc = ones_map(node_base, node_base + n_nodes - 1).m;
     a.lo = node_base;
@@ -851,6 +850,15 @@ extern "C" capf_status capf_chain2_local_hists(capf_session *cs, capf_table *rel
     a.h1 = d_in_hist;
     a.h2 = d_out_hist;
     a.loops = (unsigned long long *)acc->p + 1;
+    const char *mode = getenv("CAPF_CHAIN2");
+    const bool want_part = mode ? strcmp(mode, "partitioned") == 0 : a.n >= (int64_t(1) << 22);
+    const ColView pc[4] = {a.u1, a.v1, a.u2, a.v2};
+    uint64_t part_loops = 0;
+    if (a.n > 0 && n_nodes > 0 && want_part &&
+        chain2_partitioned(s, pc, a.n, a.lo, a.hi, a.h1, a.h2, &part_loops)) {
+      *self_loops = (int64_t)part_loops;
+      return CAPF_OK;
+    }
     if (a.n > 0 && n_nodes > 0) {
       KernelTimer kt(s, "chain2_hist", 16.0 * a.n);
       hipLaunchKernelGGL(k_chain2_hist<true>, dim3(grid_for(a.n, 256, 256 * 32)), dim3(256), 0,

@@ -18,19 +18,20 @@ constexpr int SCAN_BLOCK = 256;
 constexpr int SCAN_ITEMS = 8;
 constexpr int SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
 
-__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_tiles(const int64_t *in, int64_t *out,
-                                                           int64_t *tile_sums, int64_t n) {
-  __shared__ int64_t lds[17];
+template <typename T>
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_tiles(const T *in, T *out, T *tile_sums,
+                                                           int64_t n) {
+  __shared__ T lds[17];
   int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
-  int64_t v[SCAN_ITEMS];
-  int64_t local = 0;
+  T v[SCAN_ITEMS];
+  T local = 0;
 #pragma unroll
   for (int k = 0; k < SCAN_ITEMS; ++k) {
-    v[k] = base + k < n ? in[base + k] : 0;
+    v[k] = base + k < n ? in[base + k] : T(0);
     local += v[k];
   }
-  int64_t total;
-  int64_t ex = block_exclusive_scan(local, lds, total);
+  T total;
+  T ex = block_exclusive_scan(local, lds, total);
 #pragma unroll
   for (int k = 0; k < SCAN_ITEMS; ++k) {
     if (base + k < n) out[base + k] = ex;
@@ -39,34 +40,46 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_tiles(const int64_t *in, in
   if (threadIdx.x == 0) tile_sums[blockIdx.x] = total;
 }
 
-__global__ void k_add_tile_offsets(int64_t *out, const int64_t *tile_off, int64_t n) {
+template <typename T>
+__global__ void k_add_tile_offsets(T *out, const T *tile_off, int64_t n) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] += tile_off[i / SCAN_TILE];
 }
 
-static void scan_rec(Session *s, const int64_t *in, int64_t *out, int64_t n, int64_t *total_dev) {
+template <typename T>
+static void scan_rec(Session *s, const T *in, T *out, int64_t n, T *total_dev) {
   int64_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
-  BufPtr sums = s->alloc(sizeof(int64_t) * (tiles + 1));
-  hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, s->stream, in,
-                     out, (int64_t *)sums->p, n);
+  BufPtr sums = s->alloc(sizeof(T) * (tiles + 1));
+  hipLaunchKernelGGL(k_scan_tiles<T>, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, s->stream, in,
+                     out, (T *)sums->p, n);
   KERNEL_CHECK();
   if (tiles == 1) {
-    HIP_CHECK(hipMemcpyAsync(total_dev, sums->p, 8, hipMemcpyDeviceToDevice, s->stream));
+    HIP_CHECK(hipMemcpyAsync(total_dev, sums->p, sizeof(T), hipMemcpyDeviceToDevice, s->stream));
     return;
   }
-  BufPtr offs = s->alloc(sizeof(int64_t) * tiles);
-  scan_rec(s, (const int64_t *)sums->p, (int64_t *)offs->p, tiles, total_dev);
-  hipLaunchKernelGGL(k_add_tile_offsets, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                     s->stream, out, (const int64_t *)offs->p, n);
+  BufPtr offs = s->alloc(sizeof(T) * tiles);
+  scan_rec<T>(s, (const T *)sums->p, (T *)offs->p, tiles, total_dev);
+  hipLaunchKernelGGL(k_add_tile_offsets<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     s->stream, out, (const T *)offs->p, n);
   KERNEL_CHECK();
 }
 
 int64_t exclusive_scan_i64(Session *s, const int64_t *d_in, int64_t *d_out, int64_t n) {
   if (n <= 0) return 0;
-  scan_rec(s, d_in, d_out, n, s->d_scalars);
+  scan_rec<int64_t>(s, d_in, d_out, n, s->d_scalars);
   HIP_CHECK(hipMemcpyAsync(s->h_scalars, s->d_scalars, 8, hipMemcpyDeviceToHost, s->stream));
   s->sync();
   return s->h_scalars[0];
+}
+
+// uint32 variant (totals < 2^32), asynchronous: the total stays on the device.
+void exclusive_scan_u32_async(Session *s, const uint32_t *d_in, uint32_t *d_out, int64_t n,
+                              uint32_t *d_total) {
+  if (n <= 0) {
+    HIP_CHECK(hipMemsetAsync(d_total, 0, 4, s->stream));
+    return;
+  }
+  scan_rec<uint32_t>(s, d_in, d_out, n, d_total);
 }
 
 // ------------------------------------------------------------ compaction
@@ -176,7 +189,18 @@ ColPtr gather_column(Session *s, const ColPtr &c, const int64_t *d_idx, int64_t 
   }
   if (c->type == Type::Null) return null_column(s, Type::Null, m);
   bool with_valid = c->valid != nullptr || idx_may_be_null;
-  ColPtr o = make_column(s, c->type, m, with_valid);
+  ColPtr o;
+  if (c->enc == ENC_FOR32) {  // gathered rows keep the frame of reference
+    o = std::make_shared<Column>();
+    o->type = c->type;
+    o->n = m;
+    o->enc = ENC_FOR32;
+    o->base = c->base;
+    if (m > 0) o->data = s->alloc(4 * m);
+    if (with_valid && m > 0) o->valid = s->alloc(m);
+  } else {
+    o = make_column(s, c->type, m, with_valid);
+  }
   if (m == 0) return o;
   const uint8_t *sval = c->valid ? (const uint8_t *)c->valid->p : nullptr;
   uint8_t *dval = o->valid ? (uint8_t *)o->valid->p : nullptr;
@@ -184,6 +208,9 @@ ColPtr gather_column(Session *s, const ColPtr &c, const int64_t *d_idx, int64_t 
   if (c->type == Type::Bool)
     hipLaunchKernelGGL(k_gather<uint8_t>, dim3(g), dim3(256), 0, s->stream,
                        (const uint8_t *)c->data->p, sval, d_idx, (uint8_t *)o->data->p, dval, m);
+  else if (c->enc == ENC_FOR32)
+    hipLaunchKernelGGL(k_gather<uint32_t>, dim3(g), dim3(256), 0, s->stream,
+                       (const uint32_t *)c->data->p, sval, d_idx, (uint32_t *)o->data->p, dval, m);
   else
     hipLaunchKernelGGL(k_gather<int64_t>, dim3(g), dim3(256), 0, s->stream,
                        (const int64_t *)c->data->p, sval, d_idx, (int64_t *)o->data->p, dval, m);
@@ -198,6 +225,16 @@ __global__ void k_copy_part(const T *src, const uint8_t *sval, T *dst, uint8_t *
        i += (int64_t)gridDim.x * blockDim.x) {
     if (dst) dst[off + i] = src ? src[i] : T(0);
     if (dval) dval[off + i] = src ? (sval ? sval[i] : 1) : 0;
+  }
+}
+
+// integer column of any encoding → plain int64 slice of the output
+__global__ void k_copy_part_int(ColView src, int64_t *dst, uint8_t *dval, int64_t n, int64_t off) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const bool has = src.type != CAPF_TYPE_NULL && src.data;
+    dst[off + i] = has ? ld_int(src, i) : 0;
+    if (dval) dval[off + i] = has ? (src.valid ? src.valid[i] : 1) : 0;
   }
 }
 
@@ -216,6 +253,9 @@ ColPtr concat_columns(Session *s, const ColPtr &a, const ColPtr &b, Type t) {
       if (t == Type::Bool)
         hipLaunchKernelGGL(k_copy_part<uint8_t>, dim3(g), dim3(256), 0, s->stream,
                            (const uint8_t *)src, sval, (uint8_t *)o->data->p, dval, c->n, off);
+      else if (c->enc == ENC_FOR32)
+        hipLaunchKernelGGL(k_copy_part_int, dim3(g), dim3(256), 0, s->stream, view_of(c),
+                           (int64_t *)o->data->p, dval, c->n, off);
       else
         hipLaunchKernelGGL(k_copy_part<int64_t>, dim3(g), dim3(256), 0, s->stream,
                            (const int64_t *)src, sval, (int64_t *)o->data->p, dval, c->n, off);
@@ -226,13 +266,62 @@ ColPtr concat_columns(Session *s, const ColPtr &a, const ColPtr &b, Type t) {
   return o;
 }
 
+// ------------------------------------------------------------ encodings
+__global__ void k_decode_for32(const uint32_t *src, int64_t base, int64_t *dst, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = base + (int64_t)src[i];
+}
+
+__global__ void k_encode_for32(const int64_t *src, const uint8_t *valid, int64_t base,
+                               uint32_t *dst, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = (valid && !valid[i]) ? 0u : (uint32_t)(src[i] - base);
+}
+
+ColPtr decode_column(Session *s, const ColPtr &c) {
+  if (c->enc == ENC_PLAIN) return c;
+  auto o = std::make_shared<Column>();
+  o->type = c->type;
+  o->n = c->n;
+  o->valid = c->valid;
+  if (c->n > 0) {
+    o->data = s->alloc(8 * c->n);
+    hipLaunchKernelGGL(k_decode_for32, dim3(grid_for(c->n, 256)), dim3(256), 0, s->stream,
+                       (const uint32_t *)c->data->p, c->base, (int64_t *)o->data->p, c->n);
+    KERNEL_CHECK();
+  }
+  return o;
+}
+
+ColPtr encode_column(Session *s, const ColPtr &c) {
+  if (c->enc != ENC_PLAIN || (c->type != Type::Int64 && c->type != Type::String) || c->n == 0)
+    return c;
+  const ColStats &st = column_stats(s, c);
+  if (st.non_null == 0 || (uint64_t)(st.max - st.min) > 0xFFFFFFFFull) return c;
+  auto o = std::make_shared<Column>();
+  o->type = c->type;
+  o->n = c->n;
+  o->enc = ENC_FOR32;
+  o->base = st.min;
+  o->valid = c->valid;
+  o->data = s->alloc(4 * c->n);
+  hipLaunchKernelGGL(k_encode_for32, dim3(grid_for(c->n, 256)), dim3(256), 0, s->stream,
+                     (const int64_t *)c->data->p, c->valid ? (const uint8_t *)c->valid->p : nullptr,
+                     st.min, (uint32_t *)o->data->p, c->n);
+  KERNEL_CHECK();
+  o->stats = st;  // the values are unchanged
+  return o;
+}
+
 // ------------------------------------------------------------ statistics
-__global__ void k_minmax(const int64_t *v, const uint8_t *valid, int64_t n, int64_t *acc) {
+__global__ void k_minmax(ColView v, int64_t n, int64_t *acc) {
   int64_t mn = INT64_MAX, mx = INT64_MIN, cnt = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    if (valid && !valid[i]) continue;
-    int64_t x = v[i];
+    if (v.valid && !v.valid[i]) continue;
+    int64_t x = ld_int(v, i);
     mn = x < mn ? x : mn;
     mx = x > mx ? x : mx;
     ++cnt;
@@ -251,12 +340,11 @@ __global__ void k_minmax(const int64_t *v, const uint8_t *valid, int64_t n, int6
   }
 }
 
-__global__ void k_dup_check(const int64_t *v, const uint8_t *valid, int64_t n, int64_t base,
-                            uint32_t *bits, int64_t *dup) {
+__global__ void k_dup_check(ColView v, int64_t n, int64_t base, uint32_t *bits, int64_t *dup) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    if (valid && !valid[i]) continue;
-    uint64_t k = (uint64_t)(v[i] - base);
+    if (v.valid && !v.valid[i]) continue;
+    uint64_t k = (uint64_t)(ld_int(v, i) - base);
     uint32_t m = 1u << (k & 31);
     uint32_t old = atomicOr(&bits[k >> 5], m);
     if (old & m) *dup = 1;
@@ -270,11 +358,16 @@ ColStats compute_stats(Session *s, const Column &c) {
     return st;
   }
   if (c.n == 0) return st;
+  ColView v;
+  v.data = c.data->p;
+  v.valid = c.valid ? (const uint8_t *)c.valid->p : nullptr;
+  v.type = (int32_t)c.type;
+  v.enc = c.enc;
+  v.base = c.base;
   int64_t init[3] = {INT64_MAX, INT64_MIN, 0};
   HIP_CHECK(hipMemcpyAsync(s->d_scalars, init, sizeof(init), hipMemcpyHostToDevice, s->stream));
-  hipLaunchKernelGGL(k_minmax, dim3(grid_for(c.n, 256, 1024)), dim3(256), 0, s->stream,
-                     (const int64_t *)c.data->p, c.valid ? (const uint8_t *)c.valid->p : nullptr,
-                     c.n, s->d_scalars);
+  hipLaunchKernelGGL(k_minmax, dim3(grid_for(c.n, 256, 1024)), dim3(256), 0, s->stream, v, c.n,
+                     s->d_scalars);
   KERNEL_CHECK();
   HIP_CHECK(hipMemcpyAsync(s->h_scalars, s->d_scalars, sizeof(init), hipMemcpyDeviceToHost, s->stream));
   s->sync();
@@ -287,10 +380,8 @@ ColStats compute_stats(Session *s, const Column &c) {
     BufPtr bits = s->alloc(4 * words);
     HIP_CHECK(hipMemsetAsync(bits->p, 0, 4 * words, s->stream));
     HIP_CHECK(hipMemsetAsync(s->d_scalars + 3, 0, 8, s->stream));
-    hipLaunchKernelGGL(k_dup_check, dim3(grid_for(c.n, 256, 4096)), dim3(256), 0, s->stream,
-                       (const int64_t *)c.data->p,
-                       c.valid ? (const uint8_t *)c.valid->p : nullptr, c.n, st.min,
-                       (uint32_t *)bits->p, s->d_scalars + 3);
+    hipLaunchKernelGGL(k_dup_check, dim3(grid_for(c.n, 256, 4096)), dim3(256), 0, s->stream, v,
+                       c.n, st.min, (uint32_t *)bits->p, s->d_scalars + 3);
     KERNEL_CHECK();
     HIP_CHECK(hipMemcpyAsync(s->h_scalars + 3, s->d_scalars + 3, 8, hipMemcpyDeviceToHost, s->stream));
     s->sync();
@@ -324,7 +415,7 @@ __device__ inline Val load_col(const ColView &c, int64_t r) {
   if (c.type == CAPF_TYPE_NULL || !c.data) return mknull(CAPF_TYPE_NULL);
   if (c.valid && !c.valid[r]) return mknull(c.type);
   if (c.type == CAPF_TYPE_BOOL) return mk(((const uint8_t *)c.data)[r] ? 1 : 0, c.type, 0);
-  return mk(((const int64_t *)c.data)[r], c.type, 0);
+  return mk(ld_int(c, r), c.type, 0);
 }
 
 // -1 less, 0 equal, 1 greater (non-null operands)

@@ -32,8 +32,9 @@ __device__ inline uint64_t key_word(const ColView &c, int64_t r, bool &isnull) {
   }
   isnull = false;
   if (c.type == CAPF_TYPE_BOOL) return ((const uint8_t *)c.data)[r] ? 1 : 0;
+  if (c.type != CAPF_TYPE_FLOAT64) return (uint64_t)ld_int(c, r);
   uint64_t w = ((const uint64_t *)c.data)[r];
-  if (c.type == CAPF_TYPE_FLOAT64 && w == 0x8000000000000000ull) w = 0;  // -0.0 == 0.0
+  if (w == 0x8000000000000000ull) w = 0;  // -0.0 == 0.0
   return w;
 }
 
@@ -405,7 +406,7 @@ template <typename T>
 __device__ inline T load_num(const ColView &c, int64_t r) {
   if (c.type == CAPF_TYPE_BOOL) return (T)((const uint8_t *)c.data)[r];
   if (c.type == CAPF_TYPE_FLOAT64) return (T)((const double *)c.data)[r];
-  return (T)((const int64_t *)c.data)[r];
+  return (T)ld_int(c, r);
 }
 
 __device__ inline void atomic_min_f64(double *p, double v) {
@@ -538,7 +539,7 @@ __global__ void k_sort_key(ColView c, int64_t n, int desc, uint64_t *key, uint64
         if (b == 0x8000000000000000ull) b = 0;
         k = (b >> 63) ? ~b : (b | 0x8000000000000000ull);
       } else {
-        k = ((const uint64_t *)c.data)[r] ^ 0x8000000000000000ull;
+        k = (uint64_t)ld_int(c, r) ^ 0x8000000000000000ull;
       }
     }
     key[r] = desc ? ~k : k;

@@ -330,7 +330,8 @@ ColView view_of(const ColPtr &c) {
   v.data = c->data ? c->data->p : nullptr;
   v.valid = c->valid ? (const uint8_t *)c->valid->p : nullptr;
   v.type = (int32_t)c->type;
-  v.pad = 0;
+  v.enc = c->enc;
+  v.base = c->base;
   return v;
 }
 
@@ -789,6 +790,37 @@ capf_status capf_table_empty(capf_session *cs, int32_t ncols, const char *const 
   return table_from(cs, ncols, names, types, data.data(), nullptr, 0, false, true, out);
 }
 
+capf_status capf_table_compact(capf_table *t, capf_table **out) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(out, "out");
+  DataPtr d = materialize(t->node);
+  Session *s = t->node->s;
+  auto n = new_node(s, Kind::Source);
+  n->names = t->node->names;
+  n->types = t->node->types;
+  auto e = std::make_shared<Data>();
+  e->nrows = d->nrows;
+  for (const ColPtr &c : d->cols) e->cols.push_back(encode_column(s, c));
+  s->sync();
+  n->result = e;
+  *out = wrap(n);
+  CAPF_API_END
+}
+
+capf_status capf_table_column_encoding(capf_table *t, const char *col, int32_t *enc,
+                                       int64_t *base) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(col, "col");
+  int i = t->node->col_index_or_throw(col);
+  DataPtr d = materialize(t->node);
+  const ColPtr &c = d->cols[i];
+  if (enc) *enc = c->enc;
+  if (base) *base = c->base;
+  CAPF_API_END
+}
+
 capf_status capf_table_retain(capf_table *t) {
   CAPF_API_BEGIN
   need(t, "table");
@@ -845,7 +877,7 @@ capf_status capf_table_download(capf_table *t, const char *col, void *values_out
   int i = t->node->col_index_or_throw(col);
   DataPtr d = materialize(t->node);
   Session *s = t->node->s;
-  const ColPtr &c = d->cols[i];
+  const ColPtr c = decode_column(s, d->cols[i]);
   size_t w = type_width(c->type);
   if (d->nrows > 0) {
     if (c->type != Type::Null && values_out)
@@ -870,6 +902,14 @@ capf_status capf_table_device_column(capf_table *t, const char *col, void **valu
   need(col, "col");
   int i = t->node->col_index_or_throw(col);
   DataPtr d = materialize(t->node);
+  if (d->cols[i]->enc != ENC_PLAIN) {
+    // the handle's storage becomes the plain column (same values), so the
+    // returned pointer lives as long as the table
+    Session *s = t->node->s;
+    std::lock_guard<std::mutex> g(t->node->mu);
+    d->cols[i] = decode_column(s, d->cols[i]);
+    s->sync();
+  }
   const ColPtr &c = d->cols[i];
   if (values) *values = c->data ? c->data->p : nullptr;
   if (valid) *valid = c->valid ? (uint8_t *)c->valid->p : nullptr;
@@ -1164,7 +1204,8 @@ capf_status capf_table_show(capf_table *t, int32_t rows) {
   std::vector<std::vector<int64_t>> vals(d->cols.size(), std::vector<int64_t>(m));
   std::vector<std::vector<uint8_t>> valid(d->cols.size(), std::vector<uint8_t>(m, 1));
   for (size_t i = 0; i < d->cols.size(); ++i) {
-    auto &c = d->cols[i];
+    const ColPtr c = decode_column(s, d->cols[i]);
+    s->sync();
     if (m == 0) continue;
     if (c->type == Type::Null) {
       std::fill(valid[i].begin(), valid[i].end(), 0);

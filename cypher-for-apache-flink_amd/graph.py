@@ -89,7 +89,7 @@ class ScanGraph:
         return sorted(next(iter(t.labels)) for t in self.rel_tables)
 
     @staticmethod
-    def from_data(session, g: GraphData):
+    def from_data(session, g: GraphData, compact=False):
         """CAPFScanGraphFactory: one element table per label combination / type."""
         by_combo, by_type = {}, {}
         for nid, labels, props in g.nodes:
@@ -107,7 +107,8 @@ class ScanGraph:
             for k in sorted(keys):
                 vals = [_coerce(r[1].get(k), keys[k]) for r in rows]
                 cols.append(("p_" + k, CT_TO_CAPF[keys[k]], vals, None))
-            node_tables.append(ElementTable("node", combo, session.table(cols, nrows=len(rows)), keys))
+            t = session.table(cols, nrows=len(rows))
+            node_tables.append(ElementTable("node", combo, t.compact() if compact else t, keys))
         for typ, rows in sorted(by_type.items()):
             keys = {}
             for *_, props in rows:
@@ -120,7 +121,8 @@ class ScanGraph:
             for k in sorted(keys):
                 vals = [_coerce(r[3].get(k), keys[k]) for r in rows]
                 cols.append(("p_" + k, CT_TO_CAPF[keys[k]], vals, None))
-            rel_tables.append(ElementTable("rel", frozenset([typ]), session.table(cols, nrows=len(rows)), keys))
+            t = session.table(cols, nrows=len(rows))
+            rel_tables.append(ElementTable("rel", frozenset([typ]), t.compact() if compact else t, keys))
         return ScanGraph(session, node_tables, rel_tables)
 
     # ------------------------------------------------------------ scans

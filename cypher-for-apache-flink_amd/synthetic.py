@@ -24,16 +24,22 @@ def rmat_seed(scale):
 
 
 def rmat_graph(session, scale, edge_factor=16, seed=None, person_split=False, first=0, count=None,
-               node_base=0, n_nodes=None):
-    """ScanGraph over an R-MAT edge table (optionally a shard [first, first+count))."""
+               node_base=0, n_nodes=None, compact=False):
+    """ScanGraph over an R-MAT edge table (optionally a shard [first, first+count)).
+
+    compact=True stores the id columns FOR32-encoded (GpuTable.compact)."""
     seed = rmat_seed(scale) if seed is None else seed
     m = edge_factor << scale
     count = m - first if count is None else count
     n = (1 << scale) if n_nodes is None else n_nodes
     rels = session.rmat_rels(scale, seed, thresholds(), first, count, id_base=0)
+    if compact:
+        rels = rels.compact()
     rel_tables = [ElementTable("rel", frozenset(["E"]), rels, {})]
     if person_split:
         nodes = session.range_nodes(node_base, n, seed=seed, id_col="id", label_col="person")
+        if compact:
+            nodes = nodes.compact()
         h = RecordHeader({Var("person"): "person"})
         person = nodes.filter(Equals(Var("person"), BoolLit(True)), h, {}).select("id")
         other = nodes.filter(Equals(Var("person"), BoolLit(False)), h, {}).select("id")
@@ -41,5 +47,7 @@ def rmat_graph(session, scale, edge_factor=16, seed=None, person_split=False, fi
                        ElementTable("node", frozenset(["Other"]), other, {})]
     else:
         nodes = session.range_nodes(node_base, n, id_col="id")
+        if compact:
+            nodes = nodes.compact()
         node_tables = [ElementTable("node", frozenset(["V"]), nodes, {})]
     return ScanGraph(session, node_tables, rel_tables)

@@ -242,6 +242,17 @@ class GpuTable:
     def cache(self):
         return self._new("capf_table_cache", self._h)
 
+    def compact(self):
+        """Materialised copy whose INTEGER columns are FOR32-encoded where
+        their value range fits 32 bits (same rows; half the id bytes)."""
+        return self._new("capf_table_compact", self._h)
+
+    def encoding(self, col):
+        """(encoding, base) of a column: (0, 0) plain, (1, base) FOR32."""
+        e, b = c_int32(), c_int64()
+        _lib.call("capf_table_column_encoding", self._h, col.encode(), byref(e), byref(b))
+        return e.value, b.value
+
     def select(self, *cols):
         pairs = [(c, c) if isinstance(c, str) else tuple(c) for c in cols]
         src = [p[0] for p in pairs]

@@ -203,6 +203,18 @@ capf_status capf_table_download(capf_table *t, const char *col, void *values_out
 capf_status capf_table_device_column(capf_table *t, const char *col, void **values,
                                      uint8_t **valid, int64_t *nrows);
 
+/* Storage encodings of a materialised column.  CAPF_ENC_FOR32: INTEGER values
+ * held as uint32 offsets from a per-column base (frame of reference) — same
+ * values, half the HBM bytes.  No reference counterpart: the Flink backend
+ * stores ids as Java longs (CAPFGraph.scala ids are LongType).              */
+#define CAPF_ENC_PLAIN 0
+#define CAPF_ENC_FOR32 1
+/* Materialise t and re-encode every INTEGER column whose value range spans
+ * < 2^32 as FOR32.  Results of every operator are unchanged.               */
+capf_status capf_table_compact(capf_table *t, capf_table **out);
+capf_status capf_table_column_encoding(capf_table *t, const char *col, int32_t *enc,
+                                       int64_t *base);
+
 /* --------------------------------------------------------------- Table[T] */
 /* cache() (Table.scala:52) */
 capf_status capf_table_cache(capf_table *t, capf_table **out);

@@ -30,10 +30,11 @@ from oracle.table_np import OracleSession
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("compact", [False, True], ids=["int64", "for32"])
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
-def test_reference_case_on_gpu(gpu_session, case):
+def test_reference_case_on_gpu(gpu_session, case, compact):
     cid, src, create, query, expected = case
-    g = ScanGraph.from_data(gpu_session, parse_create(create))
+    g = ScanGraph.from_data(gpu_session, parse_create(create), compact=compact)
     got = run(g, query)
     assert bag(got) == bag(expected), f"{cid} ({src}): {got}"
     og = ScanGraph.from_data(OracleSession(), parse_create(create))
@@ -46,9 +47,10 @@ ONE_HOP_PERSON = Query([Match([NodeP("a", ("Person",)), NodeP("b")], [RelP("r", 
                        [Stage([("count", CountStar())])])
 
 
+@pytest.mark.parametrize("compact", [False, True], ids=["int64", "for32"])
 @pytest.mark.parametrize("scale", [6, 8, 10, 12, 14, 16, 18])
-def test_two_hop_count_rmat(gpu_session, scale):
-    g = rmat_graph(gpu_session, scale)
+def test_two_hop_count_rmat(gpu_session, scale, compact):
+    g = rmat_graph(gpu_session, scale, compact=compact)
     got = run(g, TWO_HOP)[0]["count"]
     assert gpu_session.last_plan() == "fused_chain2"
     src, dst = cmodel.rmat(scale)
@@ -128,12 +130,25 @@ def _rand_tables(seed=3, n=500):
 
 def _both(cols):
     gs = pytest.gpu_session_ref
-    return gs.table(cols), OracleSession().table(cols)
+    g = gs.table(cols)
+    if pytest.capf_compact:
+        g = g.compact()
+        for name, t, _, _ in cols:  # every non-empty INTEGER/STRING column is re-encoded
+            if t in (T_INT, T_STRING):
+                assert g.encoding(name)[0] == 1, name
+    return g, OracleSession().table(cols)
 
 
 @pytest.fixture(autouse=True)
 def _expose(gpu_session):
     pytest.gpu_session_ref = gpu_session
+    pytest.capf_compact = False
+
+
+@pytest.fixture(params=[False, True], ids=["int64", "for32"])
+def encoding(request, _expose):
+    """Operator tests run on plain int64 columns and on FOR32-compacted ones."""
+    pytest.capf_compact = request.param
 
 
 H = RecordHeader({Var("k"): "k", Var("f"): "f", Var("s"): "s", Var("b"): "b", Var("i"): "i"})
@@ -152,6 +167,7 @@ FILTERS = [
 
 
 @pytest.mark.parametrize("pred", FILTERS, ids=[str(p) for p in FILTERS])
+@pytest.mark.usefixtures("encoding")
 def test_filter_parity(pred):
     g, o = _both(_rand_tables())
     assert bag(g.filter(pred, H, {}).rows) == bag(o.filter(pred, H, {}).rows)
@@ -163,6 +179,7 @@ EXPRS = [Add(Var("k"), IntegerLit(3)), Multiply(Var("f"), FloatLit(2.5)), Divide
 
 
 @pytest.mark.parametrize("e", EXPRS, ids=[str(e) for e in EXPRS])
+@pytest.mark.usefixtures("encoding")
 def test_with_columns_parity(e):
     g, o = _both(_rand_tables())
     rg = g.withColumns((e, "x"), header=H, params={}).rows
@@ -178,6 +195,7 @@ def test_with_columns_parity(e):
 
 
 @pytest.mark.parametrize("jt", ["inner", "left_outer", "right_outer", "full_outer", "cross"])
+@pytest.mark.usefixtures("encoding")
 def test_join_parity(jt):
     rng = np.random.default_rng(11)
     n1, n2 = (60, 40) if jt == "cross" else (400, 300)
@@ -189,6 +207,8 @@ def test_join_parity(jt):
          ("bv", T_INT, list(range(n2)), None)]
     gs = pytest.gpu_session_ref
     ga, gb = gs.table(a), gs.table(b)
+    if pytest.capf_compact:  # mixed encodings: FOR32 left keys probe plain right keys
+        ga = ga.compact()
     oa, ob = OracleSession().table(a), OracleSession().table(b)
     pairs = [] if jt == "cross" else [("ak", "bk"), ("as", "bs")]
     assert bag(ga.join(gb, jt, *pairs).rows) == bag(oa.join(ob, jt, *pairs).rows)
@@ -200,11 +220,16 @@ def test_join_overlapping_columns_raises():
         g.join(g, "inner", ("k", "k"))
 
 
+@pytest.mark.usefixtures("encoding")
 def test_union_distinct_parity():
     g, o = _both(_rand_tables())
     g2 = g.select("i", "k", "s", "f", "b")  # different column order: matched by name
     o2 = o.select("i", "k", "s", "f", "b")
     assert bag(g.unionAll(g2).rows) == bag(o.unionAll(o2).rows)
+    # union of a FOR32 and a plain table (different bases) decodes to int64
+    gp = pytest.gpu_session_ref.table(_rand_tables(seed=5))
+    op = OracleSession().table(_rand_tables(seed=5))
+    assert bag(g.unionAll(gp).rows) == bag(o.unionAll(op).rows)
     assert bag(g.select("k", "s").distinct().rows) == bag(o.select("k", "s").distinct().rows)
     # distinct(cols): one row per distinct value of cols
     rg = g.distinct("s").rows
@@ -212,6 +237,7 @@ def test_union_distinct_parity():
     assert sorted(map(repr, [r["s"] for r in rg])) == sorted(map(repr, [r["s"] for r in ro]))
 
 
+@pytest.mark.usefixtures("encoding")
 def test_group_parity():
     g, o = _both(_rand_tables(n=2000))
     aggs = {"cnt": CountStar(), "cf": Count(Var("f")), "sk": Sum(Var("k")), "mn": Min(Var("f")),
@@ -234,12 +260,28 @@ def test_group_parity():
     assert e.group([], {"c": CountStar(), "s": Sum(Var("k"))}, header=H).rows == [{"c": 0, "s": None}]
 
 
+@pytest.mark.usefixtures("encoding")
 def test_order_skip_limit_parity():
     g, o = _both(_rand_tables())
     for items in ([(Var("k"), "asc"), (Var("i"), "desc")], [(Var("f"), "desc"), (Var("i"), "asc")]):
         rg = g.orderBy(*items, header=H, params={}).skip(13).limit(100).rows
         ro = o.orderBy(*items, header=H, params={}).skip(13).limit(100).rows
         assert [r["i"] for r in rg] == [r["i"] for r in ro]
+
+
+def test_compact_roundtrip(gpu_session):
+    big = 10 ** 15
+    cols = [("a", T_INT, [big + 7, big, None, big + 2 ** 32 - 1], None),
+            ("w", T_INT, [0, 2 ** 40, 1, 2], None),          # range > 2^32: stays plain
+            ("n", T_INT, [None, None, None, None], None)]    # all null: stays plain
+    t = gpu_session.table(cols).compact()
+    assert t.encoding("a") == (1, big)
+    assert t.encoding("w")[0] == 0 and t.encoding("n")[0] == 0
+    assert t.column_values("a") == [big + 7, big, None, big + 2 ** 32 - 1]
+    assert t.column_values("w") == [0, 2 ** 40, 1, 2]
+    ha = RecordHeader({Var("a"): "a"})
+    assert t.filter(GreaterThan(Var("a"), IntegerLit(big + 3)), ha, {}).column_values("a") == \
+        [big + 7, big + 2 ** 32 - 1]
 
 
 def test_unit_and_empty(gpu_session):

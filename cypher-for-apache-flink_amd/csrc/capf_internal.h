@@ -221,6 +221,7 @@ struct BlockCache {
 
 struct Session {
   int device = 0;
+  int num_cus = 256;  // compute units of the device (persistent-grid sizing)
   BlockCache cache;
   std::vector<PendingTiming> pending;   // recorded, not yet resolved
   std::vector<hipEvent_t> event_pool;
@@ -321,8 +322,9 @@ int32_t record_error(int32_t code, const char *msg);
 bool try_fused_count(const NodePtr &n, int64_t *out);
 // Radix-partitioned LDS histograms of the 2-hop count (chain2_partitioned.hip).
 // cols = {start(r1), end(r1), start(r2), end(r2)}, all plain or all FOR32.
+// The self-loop count is added to *d_loops (device memory): no host round trip.
 bool chain2_partitioned(Session *s, const ColView *cols, int64_t n, int64_t lo, int64_t hi,
-                        uint32_t *h_in, uint32_t *h_out, uint64_t *loops_out);
+                        uint32_t *h_in, uint32_t *h_out, unsigned long long *d_loops);
 
 }  // namespace capf
 

@@ -59,7 +59,9 @@ __device__ inline int64_t c2_ld(const void *p, int64_t base, int64_t e) {
 
 template <bool F32>
 __device__ inline int64_t c2_key(const C2Cols<F32> &c, int64_t from, int64_t to) {
-  return (from >= c.lo && from <= c.hi && to >= c.lo && to <= c.hi) ? to - c.lo : -1;
+  const uint64_t len = (uint64_t)(c.hi - c.lo) + 1;
+  const bool ok = ((uint64_t)(from - c.lo) < len) & ((uint64_t)(to - c.lo) < len);  // branch-free
+  return ok ? to - c.lo : -1;
 }
 
 struct C2Keys {
@@ -230,20 +232,49 @@ __global__ __launch_bounds__(C2_HBLOCK) void k_c2_bucket(const C2Chunk *chunks,
 // LDS (keys held in registers, counted, scanned, staged) and writes them
 // CONTIGUOUSLY into a tile-private region of `part` (fixed stride 2·TILE),
 // together with one packed (start | count << 16) word per run.  No count
-// pass, no global scan: the rels are read once.  P3 then gathers, for a run,
-// its segments across a range of tiles into the LDS histogram.
+// pass, no global scan: the rels are read once (16-B loads, 4 rels per lane).
+// P3 then gathers, for a run, its segments across a range of tiles into the
+// LDS histogram — one tile per lane, 16-B loads along the segment.  The
+// P3 work list is built on the device, so the whole count runs without a
+// host round trip.
 constexpr int64_t C3_TILE = 16384;
 constexpr int C3_BLOCK = 512;
-constexpr int C3_SPT = (int)(C3_TILE / C3_BLOCK);  // 32 rels per thread
+constexpr int C3_GROUPS = (int)(C3_TILE / (4 * C3_BLOCK));  // 8 groups of 4 rels per thread
+constexpr int C3_SPT = 4 * C3_GROUPS;                       // 32 rels per thread
+
+// 4 consecutive ids starting at e (16-B aligned when e % 4 == 0)
+template <bool F32>
+__device__ inline void c3_load4(const void *p, int64_t base, int64_t e, int64_t e1, int64_t v[4]) {
+  if (e + 4 <= e1) {
+    if (F32) {
+      const uint4 q = *(const uint4 *)((const uint32_t *)p + e);
+      v[0] = base + (int64_t)q.x;
+      v[1] = base + (int64_t)q.y;
+      v[2] = base + (int64_t)q.z;
+      v[3] = base + (int64_t)q.w;
+    } else {
+      const longlong2 q0 = *(const longlong2 *)((const int64_t *)p + e);
+      const longlong2 q1 = *(const longlong2 *)((const int64_t *)p + e + 2);
+      v[0] = q0.x;
+      v[1] = q0.y;
+      v[2] = q1.x;
+      v[3] = q1.y;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = e + k < e1 ? c2_ld<F32>(p, base, e + k) : 0;
+  }
+}
 
 template <bool F32>
 __global__ __launch_bounds__(C3_BLOCK) void k_c3_partition(C2Cols<F32> c, uint16_t *part,
                                                             uint32_t *meta,
-                                                            unsigned long long *loops) {
+                                                            unsigned long long *loops,
+                                                            int64_t t_base) {
   __shared__ __attribute__((aligned(16))) uint16_t stage[2 * C3_TILE];  // 64 KiB
   __shared__ uint32_t cur[C2_MAX_RUNS];
   __shared__ uint32_t lds_scan[17];
-  const int64_t t = blockIdx.x;
+  const int64_t t = t_base + blockIdx.x;
   const int nr = 2 * c.nb;
   constexpr uint32_t NONE = 0xFFFFFFFFu;
   for (int i = threadIdx.x; i < nr; i += C3_BLOCK) cur[i] = 0;
@@ -251,18 +282,39 @@ __global__ __launch_bounds__(C3_BLOCK) void k_c3_partition(C2Cols<F32> c, uint16
   const int64_t e0 = t * C3_TILE, e1 = min(e0 + C3_TILE, c.n);
   uint32_t kin[C3_SPT], kout[C3_SPT];  // run << 15 | low bits
   unsigned long long lp = 0;
+  const bool alias_u = c.u2 == c.u1, alias_v = c.v2 == c.v1;
 #pragma unroll
-  for (int j = 0; j < C3_SPT; ++j) {
-    const int64_t e = e0 + (int64_t)j * C3_BLOCK + threadIdx.x;
-    kin[j] = kout[j] = NONE;
-    if (e < e1) {
-      const C2Keys k = c2_load(c, e);
-      if (k.ki >= 0) kin[j] = (uint32_t)k.ki;
-      if (k.ko >= 0) kout[j] = (uint32_t)(k.ko + ((int64_t)c.nb << C2_BITS));
-      lp += k.loop ? 1ull : 0ull;
+  for (int g = 0; g < C3_GROUPS; ++g) {
+    const int64_t e = e0 + 4 * ((int64_t)g * C3_BLOCK + threadIdx.x);
+    int64_t x1[4], y1[4], x2[4], y2[4];
+    c3_load4<F32>(c.u1, c.bu1, e, e1, x1);
+    c3_load4<F32>(c.v1, c.bv1, e, e1, y1);
+    if (alias_u) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) x2[k] = x1[k];
+    } else {
+      c3_load4<F32>(c.u2, c.bu2, e, e1, x2);
     }
-    if (kin[j] != NONE) atomicAdd(&cur[kin[j] >> C2_BITS], 1u);
-    if (kout[j] != NONE) atomicAdd(&cur[kout[j] >> C2_BITS], 1u);
+    if (alias_v) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) y2[k] = y1[k];
+    } else {
+      c3_load4<F32>(c.v2, c.bv2, e, e1, y2);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int j = 4 * g + k;
+      kin[j] = kout[j] = NONE;
+      if (e + k < e1) {
+        const int64_t ki = c2_key(c, x1[k], y1[k]);  // end(r1)   when start(r1) ∈ S_a
+        const int64_t ko = c2_key(c, y2[k], x2[k]);  // start(r2) when end(r2)   ∈ S_c
+        if (ki >= 0) kin[j] = (uint32_t)ki;
+        if (ko >= 0) kout[j] = (uint32_t)(ko + ((int64_t)c.nb << C2_BITS));
+        lp += (ki >= 0 && ko >= 0 && y1[k] == x2[k]) ? 1ull : 0ull;
+      }
+      if (kin[j] != NONE) atomicAdd(&cur[kin[j] >> C2_BITS], 1u);
+      if (kout[j] != NONE) atomicAdd(&cur[kout[j] >> C2_BITS], 1u);
+    }
   }
   __syncthreads();
   uint32_t cs[4], sum = 0;
@@ -299,6 +351,136 @@ __global__ __launch_bounds__(C3_BLOCK) void k_c3_partition(C2Cols<F32> c, uint16
   if (lane_id() == 0 && lp) atomicAdd(loops, lp);
 }
 
+// P1, second form: full tiles only (the ragged last tile goes through
+// k_c3_partition), branch-free keys, and each key's rank inside its run taken
+// from the counting atomic itself — one LDS atomic per key instead of two.
+// Keys outside the node range go to a dummy run nr (counted and staged like
+// the others, never read back), so no lane is ever masked off.
+template <bool F32>
+__device__ inline void c4_load4(const void *p, int64_t base, int64_t e, int64_t v[4]) {
+  if (F32) {
+    const uint4 q = *(const uint4 *)((const uint32_t *)p + e);
+    v[0] = base + (int64_t)q.x;
+    v[1] = base + (int64_t)q.y;
+    v[2] = base + (int64_t)q.z;
+    v[3] = base + (int64_t)q.w;
+  } else {
+    const longlong2 q0 = *(const longlong2 *)((const int64_t *)p + e);
+    const longlong2 q1 = *(const longlong2 *)((const int64_t *)p + e + 2);
+    v[0] = q0.x;
+    v[1] = q0.y;
+    v[2] = q1.x;
+    v[3] = q1.y;
+  }
+}
+
+template <bool F32, int BLOCK, bool ALIAS>
+__global__ __launch_bounds__(BLOCK) void k_c4_partition(C2Cols<F32> c, uint16_t *part,
+                                                         uint32_t *meta,
+                                                         unsigned long long *loops) {
+  constexpr int RPT = (int)(C3_TILE / BLOCK);
+  constexpr int GROUPS = RPT / 4;
+  constexpr int RUNS_PT = (C2_MAX_RUNS + BLOCK - 1) / BLOCK;
+  __shared__ __attribute__((aligned(16))) uint16_t stage[2 * C3_TILE];  // 64 KiB
+  __shared__ uint32_t cur[C2_MAX_RUNS];
+  __shared__ uint32_t lds_scan[17];
+  const int64_t t = blockIdx.x;
+  const int nr = 2 * c.nb;
+  for (int i = threadIdx.x; i <= nr; i += BLOCK) cur[i] = 0;
+  __syncthreads();
+  const int64_t e0 = t * C3_TILE;
+  const uint64_t len = (uint64_t)(c.hi - c.lo) + 1;
+  const uint32_t out_run0 = (uint32_t)c.nb << C2_BITS;
+  const uint32_t dummy = (uint32_t)nr << C2_BITS;
+  uint32_t kin[RPT], kout[RPT], rank[RPT];
+  uint32_t lp = 0;
+#pragma unroll
+  for (int g = 0; g < GROUPS; ++g) {
+    const int64_t e = e0 + 4 * ((int64_t)g * BLOCK + threadIdx.x);
+    int64_t x1[4], y1[4], x2[4], y2[4];
+    c4_load4<F32>(c.u1, c.bu1, e, x1);
+    c4_load4<F32>(c.v1, c.bv1, e, y1);
+    if (!ALIAS) {
+      c4_load4<F32>(c.u2, c.bu2, e, x2);
+      c4_load4<F32>(c.v2, c.bv2, e, y2);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int j = 4 * g + k;
+      const int64_t a = x1[k] - c.lo, bq = y1[k] - c.lo;
+      const int64_t cq = (ALIAS ? x1[k] : x2[k]) - c.lo;
+      const int64_t d = (ALIAS ? y1[k] : y2[k]) - c.lo;
+      const bool in_ok = ((uint64_t)a < len) & ((uint64_t)bq < len);   // start(r1) ∈ S_a
+      const bool out_ok = ((uint64_t)d < len) & ((uint64_t)cq < len);  // end(r2) ∈ S_c
+      // in range ⇒ the offsets fit 32 bits: only those stay live
+      const uint32_t b32 = (uint32_t)bq, c32 = (uint32_t)cq;
+      kin[j] = in_ok ? b32 : dummy;
+      kout[j] = out_ok ? c32 + out_run0 : dummy;
+      lp += (in_ok & out_ok & (b32 == c32)) ? 1u : 0u;
+      const uint32_t ri = atomicAdd(&cur[kin[j] >> C2_BITS], 1u);
+      const uint32_t ro = atomicAdd(&cur[kout[j] >> C2_BITS], 1u);
+      rank[j] = ri | (ro << 16);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // bound what the scheduler keeps in flight
+  }
+  // launder the keys: stops the compiler from keeping the count phase's LDS
+  // addresses alive across the scan (32 extra VGPRs → spills)
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) asm volatile("" : "+v"(kin[j]), "+v"(kout[j]));
+  __syncthreads();
+  uint32_t cs[RUNS_PT], sum = 0;
+#pragma unroll
+  for (int q = 0; q < RUNS_PT; ++q) {
+    const int r = RUNS_PT * threadIdx.x + q;
+    cs[q] = r <= nr ? cur[r] : 0u;
+    sum += cs[q];
+  }
+  uint32_t total;
+  uint32_t ex = block_exclusive_scan(sum, lds_scan, total);
+#pragma unroll
+  for (int q = 0; q < RUNS_PT; ++q) {
+    const int r = RUNS_PT * threadIdx.x + q;
+    if (r <= nr) cur[r] = ex;
+    if (r < nr) meta[t * nr + r] = ex | (cs[q] << 16);  // [tile][run], transposed later
+    ex += cs[q];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    stage[cur[kin[j] >> C2_BITS] + (rank[j] & 0xFFFF)] = (uint16_t)(kin[j] & (C2_BW - 1));
+    stage[cur[kout[j] >> C2_BITS] + (rank[j] >> 16)] = (uint16_t)(kout[j] & (C2_BW - 1));
+    if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+  }
+  __syncthreads();
+  // the stage IS the region's layout: contiguous 16-B copy-out
+  uint4 *dst = (uint4 *)(part + t * 2 * C3_TILE);
+  const uint4 *src = (const uint4 *)stage;
+  const uint32_t n16 = (total + 7) / 8;
+  for (uint32_t i = threadIdx.x; i < n16; i += BLOCK) dst[i] = src[i];
+  unsigned long long lp64 = wave_reduce_sum((unsigned long long)lp);
+  if (lane_id() == 0 && lp64) atomicAdd(loops, lp64);
+}
+
+template <bool F32, int BLOCK>
+static void launch_c4(Session *s, const C2Cols<F32> &c, uint16_t *part, uint32_t *meta,
+                      unsigned long long *d_loops) {
+  const int64_t nfull = c.n / C3_TILE;
+  if (nfull > 0) {
+    if (c.u2 == c.u1 && c.v2 == c.v1)
+      hipLaunchKernelGGL((k_c4_partition<F32, BLOCK, true>), dim3((unsigned)nfull), dim3(BLOCK), 0,
+                         s->stream, c, part, meta, d_loops);
+    else
+      hipLaunchKernelGGL((k_c4_partition<F32, BLOCK, false>), dim3((unsigned)nfull), dim3(BLOCK),
+                         0, s->stream, c, part, meta, d_loops);
+    KERNEL_CHECK();
+  }
+  if (nfull < c.ntiles) {  // the ragged last tile
+    hipLaunchKernelGGL(k_c3_partition<F32>, dim3(1), dim3(C3_BLOCK), 0, s->stream, c, part, meta,
+                       d_loops, nfull);
+    KERNEL_CHECK();
+  }
+}
+
 // [tile][run] → [run][tile] and per-run totals
 __global__ void k_c3_transpose(const uint32_t *meta, uint32_t *meta_t, int64_t ntiles, int nr,
                                unsigned long long *run_total) {
@@ -325,45 +507,111 @@ __global__ void k_c3_transpose(const uint32_t *meta, uint32_t *meta_t, int64_t n
 }
 
 struct C3Unit {
-  int32_t run, pad;
-  int64_t t0, t1;      // tile range
-  int64_t hist_base;   // first global histogram index of the bucket
+  int32_t run;
   int32_t exclusive;   // the run is this one unit → plain store
-  int32_t side;
+  int64_t t0, t1;      // tile range
 };
 
-__global__ __launch_bounds__(C2_HBLOCK) void k_c3_bucket(const C3Unit *units, const uint16_t *part,
+constexpr int C3_UBLOCK = 1024;
+
+// Work list of P3 on the device: run r (cnt keys) is split into
+// ceil(cnt / target) tile ranges (at most one per 64 tiles), target ≈ 1/1024
+// of all keys so that ~4 units per CU balance the hub-heavy R-MAT runs.
+__global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(const unsigned long long *run_total,
+                                                         int nr, int64_t ntiles, C3Unit *units,
+                                                         int32_t *nunits) {
+  __shared__ unsigned long long lds64[17];
+  __shared__ uint32_t lds32[17];
+  unsigned long long cnt[2], tot = 0;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int r = 2 * threadIdx.x + q;
+    cnt[q] = r < nr ? run_total[r] : 0ull;
+    tot += cnt[q];
+  }
+  unsigned long long total;
+  block_exclusive_scan(tot, lds64, total);
+  const unsigned long long target = max(total / (4 * 256), 65536ull);
+  const int64_t maxsplit = max<int64_t>(1, ntiles / 64);
+  uint32_t nu[2], nsum = 0;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    nu[q] = cnt[q] ? (uint32_t)min<int64_t>((int64_t)((cnt[q] + target - 1) / target), maxsplit) : 0u;
+    nsum += nu[q];
+  }
+  uint32_t ntot;
+  uint32_t off = block_exclusive_scan(nsum, lds32, ntot);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int r = 2 * threadIdx.x + q;
+    for (uint32_t k = 0; k < nu[q]; ++k) {
+      C3Unit u;
+      u.run = r;
+      u.exclusive = nu[q] == 1;
+      u.t0 = ntiles * k / nu[q];
+      u.t1 = ntiles * (k + 1) / nu[q];
+      units[off + k] = u;
+    }
+    off += nu[q];
+  }
+  if (threadIdx.x == 0) *nunits = (int32_t)ntot;
+}
+
+__global__ __launch_bounds__(C2_HBLOCK) void k_c3_bucket(const C3Unit *units,
+                                                          const int32_t *nunits,
+                                                          const uint16_t *part,
                                                           const uint32_t *meta_t, int64_t ntiles,
-                                                          uint32_t *h_in, uint32_t *h_out,
+                                                          int nb, uint32_t *h_in, uint32_t *h_out,
                                                           int64_t hist_len) {
+  if ((int32_t)blockIdx.x >= *nunits) return;
   extern __shared__ __attribute__((aligned(16))) uint32_t bins[];  // C2_BW entries
   const C3Unit u = units[blockIdx.x];
-  uint32_t *hist = u.side ? h_out : h_in;
+  uint32_t *hist = u.run >= nb ? h_out : h_in;
+  const int64_t hist_base = (int64_t)(u.run % nb) * C2_BW;
   for (int i = threadIdx.x; i < C2_BW; i += C2_HBLOCK) bins[i] = 0;
   __syncthreads();
   const int wave = threadIdx.x / WAVE, lane = lane_id();
   constexpr int NW = C2_HBLOCK / WAVE;
   const uint32_t *m = meta_t + (int64_t)u.run * ntiles;
-  for (int64_t t = u.t0 + wave; t < u.t1; t += NW) {
-    const uint32_t w = m[t];
+  // one tile per lane; the lane walks its segment in aligned 16-B pieces
+  for (int64_t tb = u.t0 + (int64_t)wave * WAVE; tb < u.t1; tb += (int64_t)NW * WAVE) {
+    const int64_t t = tb + lane;
+    const uint32_t w = t < u.t1 ? m[t] : 0u;
     const uint32_t st = w & 0xFFFF, len = w >> 16;
-    const uint16_t *seg = part + t * 2 * C3_TILE + st;
-    for (uint32_t j = lane; j < len; j += WAVE) atomicAdd(&bins[seg[j]], 1u);
+    const uint32_t a0 = st & ~7u;
+    const uint32_t nq = len ? ((st + len + 7) / 8 - a0 / 8) : 0u;
+    uint32_t maxq = nq;
+#pragma unroll
+    for (int d = WAVE / 2; d > 0; d >>= 1) maxq = max(maxq, (uint32_t)__shfl_xor((int)maxq, d, WAVE));
+    const uint4 *seg = (const uint4 *)(part + t * 2 * C3_TILE) + a0 / 8;
+    for (uint32_t q = 0; q < maxq; ++q) {
+      if (q < nq) {
+        const uint4 v = seg[q];
+        const uint32_t b = a0 + 8 * q;  // element index of v.x's low half
+        const uint32_t words[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t idx = b + k;
+          if (idx >= st && idx < st + len)
+            atomicAdd(&bins[(words[k >> 1] >> (16 * (k & 1))) & 0xFFFF], 1u);
+        }
+      }
+    }
   }
   __syncthreads();
-  const int64_t lim = min((int64_t)C2_BW, hist_len - u.hist_base);
+  const int64_t lim = min((int64_t)C2_BW, hist_len - hist_base);
   for (int i = threadIdx.x; i < lim; i += C2_HBLOCK) {
     const uint32_t v = bins[i];
     if (u.exclusive)
-      hist[u.hist_base + i] = v;
+      hist[hist_base + i] = v;
     else if (v)
-      atomicAdd(&hist[u.hist_base + i], v);
+      atomicAdd(&hist[hist_base + i], v);
   }
 }
 
 template <bool F32>
 static bool chain2_single_pass(Session *s, const C2Cols<F32> &c0, uint32_t *h_in,
-                               uint32_t *h_out, uint64_t *loops_out) {
+                               uint32_t *h_out, unsigned long long *d_loops, int p1) {
   C2Cols<F32> c = c0;
   c.ntiles = (c.n + C3_TILE - 1) / C3_TILE;
   const int nr = 2 * c.nb;
@@ -374,62 +622,48 @@ static bool chain2_single_pass(Session *s, const C2Cols<F32> &c0, uint32_t *h_in
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 4 * C2_BW));
     attr_set = true;
   }
+  const int max_units = nr + 4 * 256 + 1;
   BufPtr part = s->alloc(2 * 2 * C3_TILE * c.ntiles);
   BufPtr meta = s->alloc(4 * nr * c.ntiles), meta_t = s->alloc(4 * nr * c.ntiles);
-  BufPtr acc = s->alloc(8 * (nr + 1));  // [0] loops, [1..nr] run totals
-  HIP_CHECK(hipMemsetAsync(acc->p, 0, 8 * (nr + 1), s->stream));
-  {
+  BufPtr acc = s->alloc(8 * nr + 16 + sizeof(C3Unit) * max_units);
+  unsigned long long *run_total = (unsigned long long *)acc->p;
+  int32_t *nunits = (int32_t *)(run_total + nr);
+  C3Unit *units = (C3Unit *)(run_total + nr + 2);
+  HIP_CHECK(hipMemsetAsync(acc->p, 0, 8 * nr + 16, s->stream));
+  if (p1 == 1 || p1 == 2) {
+    KernelTimer kt(s, "c4_partition", (F32 ? 12.0 : 20.0) * c.n);
+    if (p1 == 1)
+      launch_c4<F32, 512>(s, c, (uint16_t *)part->p, (uint32_t *)meta->p, d_loops);
+    else
+      launch_c4<F32, 1024>(s, c, (uint16_t *)part->p, (uint32_t *)meta->p, d_loops);
+  } else {
     KernelTimer kt(s, "c3_partition", (F32 ? 12.0 : 20.0) * c.n);
-    hipLaunchKernelGGL(k_c3_partition<F32>, dim3((unsigned)c.ntiles), dim3(C3_BLOCK), 0, s->stream, c,
-                       (uint16_t *)part->p, (uint32_t *)meta->p, (unsigned long long *)acc->p);
+    hipLaunchKernelGGL(k_c3_partition<F32>, dim3((unsigned)c.ntiles), dim3(C3_BLOCK), 0,
+                       s->stream, c, (uint16_t *)part->p, (uint32_t *)meta->p, d_loops,
+                       (int64_t)0);
     KERNEL_CHECK();
   }
   hipLaunchKernelGGL(k_c3_transpose, dim3((unsigned)((c.ntiles + 31) / 32), (nr + 31) / 32),
                      dim3(256), 0, s->stream, (const uint32_t *)meta->p, (uint32_t *)meta_t->p,
-                     c.ntiles, nr, (unsigned long long *)acc->p + 1);
+                     c.ntiles, nr, run_total);
   KERNEL_CHECK();
-  std::vector<int64_t> hbuf(nr + 1);
-  HIP_CHECK(hipMemcpyAsync(hbuf.data(), acc->p, 8 * (nr + 1), hipMemcpyDeviceToHost, s->stream));
-  s->sync();
-  *loops_out = (uint64_t)hbuf[0];
-  int64_t total = 0;
-  for (int r = 0; r < nr; ++r) total += hbuf[1 + r];
-  const int64_t target = std::max<int64_t>(total / (4 * 256), 1 << 16);
-  std::vector<C3Unit> units;
-  for (int r = 0; r < nr; ++r) {
-    const int64_t cnt = hbuf[1 + r];
-    if (cnt <= 0) continue;
-    // rels are in random order: an even split of the tiles is an even split of the keys
-    const int64_t nu = std::min<int64_t>((cnt + target - 1) / target, c.ntiles);
-    for (int64_t q = 0; q < nu; ++q) {
-      C3Unit u;
-      u.run = r;
-      u.pad = 0;
-      u.t0 = c.ntiles * q / nu;
-      u.t1 = c.ntiles * (q + 1) / nu;
-      u.hist_base = (int64_t)(r % c.nb) * C2_BW;
-      u.exclusive = nu == 1;
-      u.side = r / c.nb;
-      units.push_back(u);
-    }
-  }
-  if (!units.empty()) {
-    BufPtr du = s->alloc(sizeof(C3Unit) * units.size());
-    HIP_CHECK(hipMemcpyAsync(du->p, units.data(), sizeof(C3Unit) * units.size(),
-                             hipMemcpyHostToDevice, s->stream));
-    KernelTimer kt(s, "c3_bucket_hist", 2.0 * total);
-    hipLaunchKernelGGL(k_c3_bucket, dim3((unsigned)units.size()), dim3(C2_HBLOCK), 4 * C2_BW,
-                       s->stream, (const C3Unit *)du->p, (const uint16_t *)part->p,
-                       (const uint32_t *)meta_t->p, c.ntiles, h_in, h_out, len);
+  hipLaunchKernelGGL(k_c3_units, dim3(1), dim3(C3_UBLOCK), 0, s->stream,
+                     (const unsigned long long *)run_total, nr, c.ntiles, units, nunits);
+  KERNEL_CHECK();
+  {
+    KernelTimer kt(s, "c3_bucket_hist", 4.0 * c.n);
+    hipLaunchKernelGGL(k_c3_bucket, dim3((unsigned)max_units), dim3(C2_HBLOCK), 4 * C2_BW,
+                       s->stream, (const C3Unit *)units, (const int32_t *)nunits,
+                       (const uint16_t *)part->p, (const uint32_t *)meta_t->p, c.ntiles, c.nb,
+                       h_in, h_out, len);
     KERNEL_CHECK();
-    s->sync();  // the host unit vector must outlive the pageable copy
   }
   return true;
 }
 
 template <bool F32>
 static bool chain2_run(Session *s, const ColView *cols, int64_t n, int64_t lo, int64_t hi,
-                       uint32_t *h_in, uint32_t *h_out, uint64_t *loops_out) {
+                       uint32_t *h_in, uint32_t *h_out, unsigned long long *d_loops) {
   const int64_t len = hi - lo + 1;
   const int nb = (int)((len + C2_BW - 1) / C2_BW);
   static bool attr_set = false;
@@ -452,19 +686,22 @@ static bool chain2_run(Session *s, const ColView *cols, int64_t n, int64_t lo, i
   c.hi = hi;
   c.nb = nb;
   c.ntiles = (n + C2_TILE - 1) / C2_TILE;
-  const char *variant = getenv("CAPF_C2");  // "twopass": P1 count + scan + P2 scatter
-  if (!variant || strcmp(variant, "twopass") != 0)
-    return chain2_single_pass(s, c, h_in, h_out, loops_out);
+  // single-pass P1 forms: "c4" (default, 512 threads) | "c4w" (1024) | "single" (c3);
+  // "twopass": P1 count + scan + P2 scatter
+  const char *variant = getenv("CAPF_C2");
+  if (!variant || strcmp(variant, "twopass") != 0) {
+    const int p1 = !variant || strcmp(variant, "c4") == 0 ? 1 : strcmp(variant, "c4w") == 0 ? 2 : 0;
+    return chain2_single_pass(s, c, h_in, h_out, d_loops, p1);
+  }
   const int nr = 2 * nb;
   const int64_t nruns = (int64_t)nr * c.ntiles;
   BufPtr counts = s->alloc(4 * nruns), offs = s->alloc(4 * nruns);
-  BufPtr acc = s->alloc(8 * (nr + 3));  // [0] loops, [1..nr+1] run starts, [nr+2] total
+  BufPtr acc = s->alloc(8 * (nr + 3));  // [1..nr+1] run starts, [nr+2] total
   uint32_t *d_total = (uint32_t *)((int64_t *)acc->p + nr + 2);
-  HIP_CHECK(hipMemsetAsync(acc->p, 0, 8, s->stream));
   {
     KernelTimer kt(s, "c2_count", (F32 ? 8.0 : 16.0) * n);
     hipLaunchKernelGGL(k_c2_count<F32>, dim3((unsigned)c.ntiles), dim3(C2_BLOCK), 0, s->stream, c,
-                       (uint32_t *)counts->p, (unsigned long long *)acc->p);
+                       (uint32_t *)counts->p, d_loops);
     KERNEL_CHECK();
   }
   exclusive_scan_u32_async(s, (const uint32_t *)counts->p, (uint32_t *)offs->p, nruns, d_total);
@@ -474,7 +711,6 @@ static bool chain2_run(Session *s, const ColView *cols, int64_t n, int64_t lo, i
   std::vector<int64_t> hbuf(nr + 2);
   HIP_CHECK(hipMemcpyAsync(hbuf.data(), acc->p, 8 * (nr + 2), hipMemcpyDeviceToHost, s->stream));
   s->sync();
-  *loops_out = (uint64_t)hbuf[0];
   const int64_t *starts = hbuf.data() + 1;
   const int64_t total = starts[nr];
   BufPtr part = s->alloc(2 * std::max<int64_t>(total, 8) + 16);
@@ -516,21 +752,22 @@ static bool chain2_run(Session *s, const ColView *cols, int64_t n, int64_t lo, i
 
 // h_in / h_out must be zeroed by the caller.  cols = {start(r1), end(r1),
 // start(r2), end(r2)}: non-null INTEGER columns, all plain or all FOR32.
-// Returns false if the shape is outside this kernel's limits (the caller
-// falls back to k_chain2_hist).
+// Self-loop count is added to *d_loops (device).  Returns false if the shape
+// is outside this kernel's limits (the caller falls back to k_chain2_hist).
 bool chain2_partitioned(Session *s, const ColView *cols, int64_t n, int64_t lo, int64_t hi,
-                        uint32_t *h_in, uint32_t *h_out, uint64_t *loops_out) {
+                        uint32_t *h_in, uint32_t *h_out, unsigned long long *d_loops) {
   const int64_t len = hi - lo + 1;
   const int64_t nb = (len + C2_BW - 1) / C2_BW;
-  if (len <= 0 || 2 * nb > C2_MAX_RUNS || n <= 0) return false;
+  if (len <= 0 || 2 * nb + 1 > C2_MAX_RUNS || n <= 0) return false;  // + the dummy run
   if (n >= (int64_t(1) << 31)) return false;  // 2·n keys must fit the uint32 scan
   int nf = 0;
   for (int i = 0; i < 4; ++i) {
     if (cols[i].valid || !cols[i].data) return false;
+    if ((uintptr_t)cols[i].data & 15) return false;  // 16-B vector loads
     nf += cols[i].enc == ENC_FOR32;
   }
-  if (nf == 4) return chain2_run<true>(s, cols, n, lo, hi, h_in, h_out, loops_out);
-  if (nf == 0) return chain2_run<false>(s, cols, n, lo, hi, h_in, h_out, loops_out);
+  if (nf == 4) return chain2_run<true>(s, cols, n, lo, hi, h_in, h_out, d_loops);
+  if (nf == 0) return chain2_run<false>(s, cols, n, lo, hi, h_in, h_out, d_loops);
   return false;
 }
 

@@ -737,16 +737,13 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
     a.h1 = h1;
     a.h2 = h2;
     a.loops = (unsigned long long *)acc->p + 1;
-    uint64_t part_loops = 0;
     const char *mode = getenv("CAPF_CHAIN2");  // "atomic" | "partitioned" (default: by size)
     const bool want_part = all_ones && wa.map.m.lo == lo && wc.map.m.lo == lo &&
                            wa.map.m.hi == hi && wc.map.m.hi == hi &&
                            (mode ? strcmp(mode, "partitioned") == 0 : n >= (int64_t(1) << 22));
     if (n > 0 && want_part &&
-        chain2_partitioned(s, pc, n, lo, hi, h1, h2, &part_loops)) {
-      HIP_CHECK(hipMemcpyAsync((unsigned long long *)acc->p + 1, &part_loops, 8,
-                               hipMemcpyHostToDevice, s->stream));
-      s->sync();
+        chain2_partitioned(s, pc, n, lo, hi, h1, h2, a.loops)) {
+      // loops accumulated on the device
     } else if (n > 0) {
       KernelTimer kt(s, "chain2_hist", 16.0 * n);
       unsigned grid = grid_for(n, 256, 256 * 32);
@@ -853,13 +850,9 @@ extern "C" capf_status capf_chain2_local_hists(capf_session *cs, capf_table *rel
     const char *mode = getenv("CAPF_CHAIN2");
     const bool want_part = mode ? strcmp(mode, "partitioned") == 0 : a.n >= (int64_t(1) << 22);
     const ColView pc[4] = {a.u1, a.v1, a.u2, a.v2};
-    uint64_t part_loops = 0;
-    if (a.n > 0 && n_nodes > 0 && want_part &&
-        chain2_partitioned(s, pc, a.n, a.lo, a.hi, a.h1, a.h2, &part_loops)) {
-      *self_loops = (int64_t)part_loops;
-      return CAPF_OK;
-    }
-    if (a.n > 0 && n_nodes > 0) {
+    const bool done = a.n > 0 && n_nodes > 0 && want_part &&
+                      chain2_partitioned(s, pc, a.n, a.lo, a.hi, a.h1, a.h2, a.loops);
+    if (!done && a.n > 0 && n_nodes > 0) {
       KernelTimer kt(s, "chain2_hist", 16.0 * a.n);
       hipLaunchKernelGGL(k_chain2_hist<true>, dim3(grid_for(a.n, 256, 256 * 32)), dim3(256), 0,
                          s->stream, a);

@@ -584,6 +584,11 @@ capf_status capf_session_create(int32_t device, void *hip_stream, capf_session *
   Session &s = cs->impl;
   s.device = device;
   HIP_CHECK(hipSetDevice(device));
+  {
+    int cus = 0;
+    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    if (cus > 0) s.num_cus = cus;
+  }
   if (hip_stream) {
     s.stream = (hipStream_t)hip_stream;
     s.own_stream = false;

@@ -60,6 +60,24 @@ def test_two_hop_count_rmat(gpu_session, scale, compact):
         assert got == p.probe(0, len(src), 4)
 
 
+@pytest.mark.parametrize("variant", ["c4", "c4w", "single", "twopass", "atomic"])
+@pytest.mark.parametrize("compact", [False, True], ids=["int64", "for32"])
+@pytest.mark.parametrize("scale,count", [(6, None), (11, 30001), (14, None), (15, 123457)])
+def test_two_hop_partition_variants(gpu_session, monkeypatch, variant, compact, scale, count):
+    """Every histogram path, forced at small and ragged sizes (count not a
+    multiple of the 4-rel vector or the tile), must give the closed form."""
+    if variant == "atomic":
+        monkeypatch.setenv("CAPF_CHAIN2", "atomic")
+    else:
+        monkeypatch.setenv("CAPF_CHAIN2", "partitioned")
+        monkeypatch.setenv("CAPF_C2", variant)
+    g = rmat_graph(gpu_session, scale, compact=compact, count=count)
+    got = run(g, TWO_HOP)[0]["count"]
+    assert gpu_session.last_plan() == "fused_chain2"
+    src, dst = cmodel.rmat(scale, count=count)
+    assert got == cmodel.count_2hop(src, dst, 1 << scale)
+
+
 def test_rmat_generator_bit_exact(gpu_session):
     t = gpu_session.rmat_rels(12, cmodel.rmat_seed(12), cmodel.thresholds(), 1000, 5000)
     src, dst = cmodel.rmat(12, first=1000, count=5000)

@@ -21,6 +21,7 @@
 //   P4 k_chain2_dot Σ in·out (fused_count.hip)
 // Bytes per rel at int64 reference width: P1 16, P2 16 + 4, P3 4.
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <vector>
 
@@ -63,6 +64,12 @@ __device__ inline int64_t c2_key(const C2Cols<F32> &c, int64_t from, int64_t to)
   const bool ok = ((uint64_t)(from - c.lo) < len) & ((uint64_t)(to - c.lo) < len);  // branch-free
   return ok ? to - c.lo : -1;
 }
+
+// LDS bank spreading.  R-MAT ids are skewed bit by bit (each bit is 0 with
+// probability .76), so ids whose low 5 bits are all zero — one LDS bank —
+// take ~25 % of the keys.  Folding bits 5-14 into the bank bits (a bijection
+// that only rewrites the low 5 bits) cuts that bank's share to ~6 %.
+__device__ inline uint32_t lds_slot(uint32_t x) { return x ^ ((x >> 5) & 31) ^ ((x >> 10) & 31); }
 
 struct C2Keys {
   int64_t ki, ko;
@@ -201,25 +208,25 @@ __global__ __launch_bounds__(C2_HBLOCK) void k_c2_bucket(const C2Chunk *chunks,
   // scalar head/tail, 16-B (8 keys) loads in the aligned body
   const int64_t a0 = min(ch.end, (ch.begin + 7) & ~int64_t(7));
   const int64_t a1 = max(a0, ch.end & ~int64_t(7));
-  for (int64_t i = ch.begin + threadIdx.x; i < a0; i += C2_HBLOCK) atomicAdd(&bins[part[i]], 1u);
-  for (int64_t i = a1 + threadIdx.x; i < ch.end; i += C2_HBLOCK) atomicAdd(&bins[part[i]], 1u);
+  for (int64_t i = ch.begin + threadIdx.x; i < a0; i += C2_HBLOCK) atomicAdd(&bins[lds_slot(part[i])], 1u);
+  for (int64_t i = a1 + threadIdx.x; i < ch.end; i += C2_HBLOCK) atomicAdd(&bins[lds_slot(part[i])], 1u);
   const uint4 *p4 = (const uint4 *)(part + a0);
   const int64_t n4 = (a1 - a0) / 8;
   for (int64_t i = threadIdx.x; i < n4; i += C2_HBLOCK) {
     const uint4 v = p4[i];
-    atomicAdd(&bins[v.x & 0xFFFF], 1u);
-    atomicAdd(&bins[v.x >> 16], 1u);
-    atomicAdd(&bins[v.y & 0xFFFF], 1u);
-    atomicAdd(&bins[v.y >> 16], 1u);
-    atomicAdd(&bins[v.z & 0xFFFF], 1u);
-    atomicAdd(&bins[v.z >> 16], 1u);
-    atomicAdd(&bins[v.w & 0xFFFF], 1u);
-    atomicAdd(&bins[v.w >> 16], 1u);
+    atomicAdd(&bins[lds_slot(v.x & 0xFFFF)], 1u);
+    atomicAdd(&bins[lds_slot(v.x >> 16)], 1u);
+    atomicAdd(&bins[lds_slot(v.y & 0xFFFF)], 1u);
+    atomicAdd(&bins[lds_slot(v.y >> 16)], 1u);
+    atomicAdd(&bins[lds_slot(v.z & 0xFFFF)], 1u);
+    atomicAdd(&bins[lds_slot(v.z >> 16)], 1u);
+    atomicAdd(&bins[lds_slot(v.w & 0xFFFF)], 1u);
+    atomicAdd(&bins[lds_slot(v.w >> 16)], 1u);
   }
   __syncthreads();
   const int64_t lim = min((int64_t)C2_BW, hist_len - ch.hist_base);
   for (int i = threadIdx.x; i < lim; i += C2_HBLOCK) {
-    const uint32_t v = bins[i];
+    const uint32_t v = bins[lds_slot(i)];
     if (ch.exclusive)
       hist[ch.hist_base + i] = v;
     else if (v)
@@ -386,7 +393,7 @@ __global__ __launch_bounds__(BLOCK) void k_c4_partition(C2Cols<F32> c, uint16_t 
   __shared__ uint32_t lds_scan[17];
   const int64_t t = blockIdx.x;
   const int nr = 2 * c.nb;
-  for (int i = threadIdx.x; i <= nr; i += BLOCK) cur[i] = 0;
+  for (int i = threadIdx.x; i < C2_MAX_RUNS; i += BLOCK) cur[i] = 0;
   __syncthreads();
   const int64_t e0 = t * C3_TILE;
   const uint64_t len = (uint64_t)(c.hi - c.lo) + 1;
@@ -417,8 +424,8 @@ __global__ __launch_bounds__(BLOCK) void k_c4_partition(C2Cols<F32> c, uint16_t 
       kin[j] = in_ok ? b32 : dummy;
       kout[j] = out_ok ? c32 + out_run0 : dummy;
       lp += (in_ok & out_ok & (b32 == c32)) ? 1u : 0u;
-      const uint32_t ri = atomicAdd(&cur[kin[j] >> C2_BITS], 1u);
-      const uint32_t ro = atomicAdd(&cur[kout[j] >> C2_BITS], 1u);
+      const uint32_t ri = atomicAdd(&cur[lds_slot(kin[j] >> C2_BITS)], 1u);
+      const uint32_t ro = atomicAdd(&cur[lds_slot(kout[j] >> C2_BITS)], 1u);
       rank[j] = ri | (ro << 16);
     }
     __builtin_amdgcn_sched_barrier(0);  // bound what the scheduler keeps in flight
@@ -432,7 +439,7 @@ __global__ __launch_bounds__(BLOCK) void k_c4_partition(C2Cols<F32> c, uint16_t 
 #pragma unroll
   for (int q = 0; q < RUNS_PT; ++q) {
     const int r = RUNS_PT * threadIdx.x + q;
-    cs[q] = r <= nr ? cur[r] : 0u;
+    cs[q] = r <= nr ? cur[lds_slot(r)] : 0u;
     sum += cs[q];
   }
   uint32_t total;
@@ -440,15 +447,15 @@ __global__ __launch_bounds__(BLOCK) void k_c4_partition(C2Cols<F32> c, uint16_t 
 #pragma unroll
   for (int q = 0; q < RUNS_PT; ++q) {
     const int r = RUNS_PT * threadIdx.x + q;
-    if (r <= nr) cur[r] = ex;
+    if (r <= nr) cur[lds_slot(r)] = ex;
     if (r < nr) meta[t * nr + r] = ex | (cs[q] << 16);  // [tile][run], transposed later
     ex += cs[q];
   }
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < RPT; ++j) {
-    stage[cur[kin[j] >> C2_BITS] + (rank[j] & 0xFFFF)] = (uint16_t)(kin[j] & (C2_BW - 1));
-    stage[cur[kout[j] >> C2_BITS] + (rank[j] >> 16)] = (uint16_t)(kout[j] & (C2_BW - 1));
+    stage[cur[lds_slot(kin[j] >> C2_BITS)] + (rank[j] & 0xFFFF)] = (uint16_t)(kin[j] & (C2_BW - 1));
+    stage[cur[lds_slot(kout[j] >> C2_BITS)] + (rank[j] >> 16)] = (uint16_t)(kout[j] & (C2_BW - 1));
     if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
   }
   __syncthreads();
@@ -481,28 +488,42 @@ static void launch_c4(Session *s, const C2Cols<F32> &c, uint16_t *part, uint32_t
   }
 }
 
-// [tile][run] → [run][tile] and per-run totals
-__global__ void k_c3_transpose(const uint32_t *meta, uint32_t *meta_t, int64_t ntiles, int nr,
-                               unsigned long long *run_total) {
+// [tile][run] → [run][tile] and per-run totals.  A block moves 32 runs ×
+// 256 tiles through a 32×33 LDS tile (8 steps) and adds each run's count
+// once per block (one atomic per run per 256 tiles, not per 32).
+constexpr int C3_TT = 256;
+__global__ __launch_bounds__(256) void k_c3_transpose(const uint32_t *meta, uint32_t *meta_t,
+                                                       int64_t ntiles, int nr,
+                                                       unsigned long long *run_total) {
   __shared__ uint32_t tilebuf[32][33];
-  const int64_t t0 = (int64_t)blockIdx.x * 32;
   const int r0 = blockIdx.y * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads = 32 × 8
-  for (int k = ty; k < 32; k += 8) {
-    const int64_t t = t0 + k;
-    const int r = r0 + tx;
-    tilebuf[k][tx] = (t < ntiles && r < nr) ? meta[t * nr + r] : 0u;
+  unsigned int cnt[4] = {0, 0, 0, 0};                       // runs r0 + ty + 8q
+  for (int64_t t0 = (int64_t)blockIdx.x * C3_TT; t0 < min(ntiles, ((int64_t)blockIdx.x + 1) * C3_TT);
+       t0 += 32) {
+    for (int k = ty; k < 32; k += 8) {
+      const int64_t t = t0 + k;
+      const int r = r0 + tx;
+      tilebuf[k][tx] = (t < ntiles && r < nr) ? meta[t * nr + r] : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = ty + 8 * q;
+      const int r = r0 + k;
+      const int64_t t = t0 + tx;
+      const uint32_t v = tilebuf[tx][k];
+      if (t < ntiles && r < nr) meta_t[(int64_t)r * ntiles + t] = v;
+      cnt[q] += v >> 16;
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  for (int k = ty; k < 32; k += 8) {
-    const int r = r0 + k;
-    const int64_t t = t0 + tx;
-    const uint32_t v = tilebuf[tx][k];
-    if (t < ntiles && r < nr) meta_t[(int64_t)r * ntiles + t] = v;
-    // per-run total over these 32 tiles
-    unsigned int cnt = v >> 16;
-    for (int d = 16; d > 0; d >>= 1) cnt += __shfl_xor(cnt, d, 32);
-    if (tx == 0 && cnt && r < nr) atomicAdd(&run_total[r], (unsigned long long)cnt);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    unsigned int c = cnt[q];
+    for (int d = 16; d > 0; d >>= 1) c += __shfl_xor(c, d, 32);
+    const int r = r0 + ty + 8 * q;
+    if (tx == 0 && c && r < nr) atomicAdd(&run_total[r], (unsigned long long)c);
   }
 }
 
@@ -532,7 +553,7 @@ __global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(const unsigned long long
   unsigned long long total;
   block_exclusive_scan(tot, lds64, total);
   const unsigned long long target = max(total / (4 * 256), 65536ull);
-  const int64_t maxsplit = max<int64_t>(1, ntiles / 64);
+  const int64_t maxsplit = max<int64_t>(1, ntiles / 1024);
   uint32_t nu[2], nsum = 0;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
@@ -557,6 +578,7 @@ __global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(const unsigned long long
   if (threadIdx.x == 0) *nunits = (int32_t)ntot;
 }
 
+template <int K, int Q>
 __global__ __launch_bounds__(C2_HBLOCK) void k_c3_bucket(const C3Unit *units,
                                                           const int32_t *nunits,
                                                           const uint16_t *part,
@@ -573,35 +595,56 @@ __global__ __launch_bounds__(C2_HBLOCK) void k_c3_bucket(const C3Unit *units,
   const int wave = threadIdx.x / WAVE, lane = lane_id();
   constexpr int NW = C2_HBLOCK / WAVE;
   const uint32_t *m = meta_t + (int64_t)u.run * ntiles;
-  // one tile per lane; the lane walks its segment in aligned 16-B pieces
-  for (int64_t tb = u.t0 + (int64_t)wave * WAVE; tb < u.t1; tb += (int64_t)NW * WAVE) {
-    const int64_t t = tb + lane;
-    const uint32_t w = t < u.t1 ? m[t] : 0u;
-    const uint32_t st = w & 0xFFFF, len = w >> 16;
-    const uint32_t a0 = st & ~7u;
-    const uint32_t nq = len ? ((st + len + 7) / 8 - a0 / 8) : 0u;
-    uint32_t maxq = nq;
+  // One tile per lane, C3_K tiles per lane at once, C3_Q 16-B pieces of each
+  // segment per step: the segments are short (≈32 keys) and scattered, so the
+  // kernel is bound by memory latency unless many loads are in flight.
+  // the unit's tiles are split contiguously over the waves
+  const int64_t ut = u.t1 - u.t0;
+  const int64_t w0 = u.t0 + ut * wave / NW, w1 = u.t0 + ut * (wave + 1) / NW;
+  for (int64_t tb = w0; tb < w1; tb += (int64_t)WAVE * K) {
+    uint32_t st[K], len[K], a0[K], nq[K];
+    const uint4 *seg[K];
+    uint32_t maxq = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int64_t t = tb + k * WAVE + lane;
+      const uint32_t w = t < w1 ? m[t] : 0u;
+      st[k] = w & 0xFFFF;
+      len[k] = w >> 16;
+      a0[k] = st[k] & ~7u;
+      nq[k] = len[k] ? ((st[k] + len[k] + 7) / 8 - a0[k] / 8) : 0u;
+      seg[k] = (const uint4 *)(part + t * 2 * C3_TILE) + a0[k] / 8;
+      maxq = max(maxq, nq[k]);
+    }
 #pragma unroll
     for (int d = WAVE / 2; d > 0; d >>= 1) maxq = max(maxq, (uint32_t)__shfl_xor((int)maxq, d, WAVE));
-    const uint4 *seg = (const uint4 *)(part + t * 2 * C3_TILE) + a0 / 8;
-    for (uint32_t q = 0; q < maxq; ++q) {
-      if (q < nq) {
-        const uint4 v = seg[q];
-        const uint32_t b = a0 + 8 * q;  // element index of v.x's low half
-        const uint32_t words[4] = {v.x, v.y, v.z, v.w};
+    for (uint32_t q0 = 0; q0 < maxq; q0 += Q) {
+      uint4 v[K][Q];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const uint32_t idx = b + k;
-          if (idx >= st && idx < st + len)
-            atomicAdd(&bins[(words[k >> 1] >> (16 * (k & 1))) & 0xFFFF], 1u);
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int qq = 0; qq < Q; ++qq)
+          if (q0 + qq < nq[k]) v[k][qq] = seg[k][q0 + qq];
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int qq = 0; qq < Q; ++qq) {
+          if (q0 + qq >= nq[k]) continue;
+          const uint32_t b = a0[k] + 8 * (q0 + qq);  // element index of v.x's low half
+          const uint32_t words[4] = {v[k][qq].x, v[k][qq].y, v[k][qq].z, v[k][qq].w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const uint32_t idx = b + e;
+            if (idx >= st[k] && idx < st[k] + len[k])
+              atomicAdd(&bins[lds_slot((words[e >> 1] >> (16 * (e & 1))) & 0xFFFF)], 1u);
+          }
         }
-      }
     }
   }
   __syncthreads();
   const int64_t lim = min((int64_t)C2_BW, hist_len - hist_base);
   for (int i = threadIdx.x; i < lim; i += C2_HBLOCK) {
-    const uint32_t v = bins[i];
+    const uint32_t v = bins[lds_slot(i)];
     if (u.exclusive)
       hist[hist_base + i] = v;
     else if (v)
@@ -618,8 +661,10 @@ static bool chain2_single_pass(Session *s, const C2Cols<F32> &c0, uint32_t *h_in
   const int64_t len = c.hi - c.lo + 1;
   static bool attr_set = false;
   if (!attr_set) {
-    HIP_CHECK(hipFuncSetAttribute((const void *)k_c3_bucket,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 4 * C2_BW));
+    for (const void *f : {(const void *)k_c3_bucket<1, 1>, (const void *)k_c3_bucket<2, 1>,
+                          (const void *)k_c3_bucket<4, 1>, (const void *)k_c3_bucket<1, 2>,
+                          (const void *)k_c3_bucket<2, 2>, (const void *)k_c3_bucket<4, 2>})
+      HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * C2_BW));
     attr_set = true;
   }
   const int max_units = nr + 4 * 256 + 1;
@@ -643,16 +688,28 @@ static bool chain2_single_pass(Session *s, const C2Cols<F32> &c0, uint32_t *h_in
                        (int64_t)0);
     KERNEL_CHECK();
   }
-  hipLaunchKernelGGL(k_c3_transpose, dim3((unsigned)((c.ntiles + 31) / 32), (nr + 31) / 32),
-                     dim3(256), 0, s->stream, (const uint32_t *)meta->p, (uint32_t *)meta_t->p,
-                     c.ntiles, nr, run_total);
-  KERNEL_CHECK();
+  {
+    KernelTimer kt(s, "c3_transpose", 8.0 * nr * c.ntiles);
+    hipLaunchKernelGGL(k_c3_transpose, dim3((unsigned)((c.ntiles + C3_TT - 1) / C3_TT), (nr + 31) / 32),
+                       dim3(256), 0, s->stream, (const uint32_t *)meta->p, (uint32_t *)meta_t->p,
+                       c.ntiles, nr, run_total);
+    KERNEL_CHECK();
+  }
   hipLaunchKernelGGL(k_c3_units, dim3(1), dim3(C3_UBLOCK), 0, s->stream,
                      (const unsigned long long *)run_total, nr, c.ntiles, units, nunits);
   KERNEL_CHECK();
   {
     KernelTimer kt(s, "c3_bucket_hist", 4.0 * c.n);
-    hipLaunchKernelGGL(k_c3_bucket, dim3((unsigned)max_units), dim3(C2_HBLOCK), 4 * C2_BW,
+    // P3 shape (tiles per lane, pieces per step); CAPF_P3="k,q" overrides
+    int pk = 1, pq = 2;
+    if (const char *e = getenv("CAPF_P3")) sscanf(e, "%d,%d", &pk, &pq);
+    auto kern = k_c3_bucket<1, 2>;
+    if (pk == 1 && pq == 1) kern = k_c3_bucket<1, 1>;
+    if (pk == 2 && pq == 1) kern = k_c3_bucket<2, 1>;
+    if (pk == 4 && pq == 1) kern = k_c3_bucket<4, 1>;
+    if (pk == 2 && pq == 2) kern = k_c3_bucket<2, 2>;
+    if (pk == 4 && pq == 2) kern = k_c3_bucket<4, 2>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)max_units), dim3(C2_HBLOCK), 4 * C2_BW,
                        s->stream, (const C3Unit *)units, (const int32_t *)nunits,
                        (const uint16_t *)part->p, (const uint32_t *)meta_t->p, c.ntiles, c.nb,
                        h_in, h_out, len);
@@ -690,7 +747,7 @@ static bool chain2_run(Session *s, const ColView *cols, int64_t n, int64_t lo, i
   // "twopass": P1 count + scan + P2 scatter
   const char *variant = getenv("CAPF_C2");
   if (!variant || strcmp(variant, "twopass") != 0) {
-    const int p1 = !variant || strcmp(variant, "c4") == 0 ? 1 : strcmp(variant, "c4w") == 0 ? 2 : 0;
+    const int p1 = !variant || strcmp(variant, "c4w") == 0 ? 2 : strcmp(variant, "c4") == 0 ? 1 : 0;
     return chain2_single_pass(s, c, h_in, h_out, d_loops, p1);
   }
   const int nr = 2 * nb;

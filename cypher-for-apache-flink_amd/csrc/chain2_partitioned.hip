@@ -49,6 +49,8 @@ struct C2Cols {
   int64_t lo, hi;  // dense node range of S_a = S_b = S_c (MAP_ONES)
   int nb;          // buckets per side
   int64_t ntiles;
+  NodeMix mix;     // histogram index = node_mix(id − lo) on a 2^k domain
+  int64_t hist_len;  // 2^k (a multiple of C2_BW)
 };
 
 // key of b = `to` when both endpoints lie in the node range, else -1
@@ -62,7 +64,7 @@ template <bool F32>
 __device__ inline int64_t c2_key(const C2Cols<F32> &c, int64_t from, int64_t to) {
   const uint64_t len = (uint64_t)(c.hi - c.lo) + 1;
   const bool ok = ((uint64_t)(from - c.lo) < len) & ((uint64_t)(to - c.lo) < len);  // branch-free
-  return ok ? to - c.lo : -1;
+  return ok ? (int64_t)node_mix((uint32_t)(to - c.lo), c.mix) : -1;
 }
 
 // LDS bank spreading.  R-MAT ids are skewed bit by bit (each bit is 0 with
@@ -421,8 +423,8 @@ __global__ __launch_bounds__(BLOCK) void k_c4_partition(C2Cols<F32> c, uint16_t 
       const bool out_ok = ((uint64_t)d < len) & ((uint64_t)cq < len);  // end(r2) ∈ S_c
       // in range ⇒ the offsets fit 32 bits: only those stay live
       const uint32_t b32 = (uint32_t)bq, c32 = (uint32_t)cq;
-      kin[j] = in_ok ? b32 : dummy;
-      kout[j] = out_ok ? c32 + out_run0 : dummy;
+      kin[j] = in_ok ? node_mix(b32, c.mix) : dummy;
+      kout[j] = out_ok ? node_mix(c32, c.mix) + out_run0 : dummy;
       lp += (in_ok & out_ok & (b32 == c32)) ? 1u : 0u;
       const uint32_t ri = atomicAdd(&cur[lds_slot(kin[j] >> C2_BITS)], 1u);
       const uint32_t ro = atomicAdd(&cur[lds_slot(kout[j] >> C2_BITS)], 1u);
@@ -535,12 +537,17 @@ struct C3Unit {
 
 constexpr int C3_UBLOCK = 1024;
 
-// Work list of P3 on the device: run r (cnt keys) is split into
-// ceil(cnt / target) tile ranges (at most one per 64 tiles), target ≈ 1/1024
-// of all keys so that ~4 units per CU balance the hub-heavy R-MAT runs.
+// Work list of P3 on the device.  With hash-partitioned runs the run sizes
+// are near-uniform (max/mean ≈ 1.6 at s24), so every run is ONE unit — an
+// exclusive one, whose plain stores cover all 2^15 bins of its bucket: the
+// histograms need no memset, empty runs included (they store zeros).  A run
+// holding more than twice the mean (a hub-heavy bucket) is split into tile
+// ranges that flush with atomic adds into bins cleared by k_c3_zero.  Units
+// stay in run order: k_c3_bucket maps them onto XCDs in groups of
+// consecutive runs (c3_unit_of).
 __global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(const unsigned long long *run_total,
                                                          int nr, int64_t ntiles, C3Unit *units,
-                                                         int32_t *nunits) {
+                                                         int32_t *nunits, int32_t *split) {
   __shared__ unsigned long long lds64[17];
   __shared__ uint32_t lds32[17];
   unsigned long long cnt[2], tot = 0;
@@ -552,12 +559,15 @@ __global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(const unsigned long long
   }
   unsigned long long total;
   block_exclusive_scan(tot, lds64, total);
-  const unsigned long long target = max(total / (4 * 256), 65536ull);
-  const int64_t maxsplit = max<int64_t>(1, ntiles / 1024);
+  const unsigned long long target = max(2 * total / (unsigned long long)max(nr, 1), 65536ull);
+  const int64_t maxsplit = max<int64_t>(1, ntiles / 256);
   uint32_t nu[2], nsum = 0;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
-    nu[q] = cnt[q] ? (uint32_t)min<int64_t>((int64_t)((cnt[q] + target - 1) / target), maxsplit) : 0u;
+    const int r = 2 * threadIdx.x + q;
+    nu[q] = r >= nr ? 0u
+            : cnt[q] ? (uint32_t)min<int64_t>((int64_t)((cnt[q] + target - 1) / target), maxsplit)
+                     : 1u;
     nsum += nu[q];
   }
   uint32_t ntot;
@@ -565,17 +575,39 @@ __global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(const unsigned long long
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int r = 2 * threadIdx.x + q;
+    if (!nu[q]) continue;
     for (uint32_t k = 0; k < nu[q]; ++k) {
       C3Unit u;
       u.run = r;
       u.exclusive = nu[q] == 1;
-      u.t0 = ntiles * k / nu[q];
-      u.t1 = ntiles * (k + 1) / nu[q];
+      u.t0 = cnt[q] ? ntiles * k / nu[q] : 0;
+      u.t1 = cnt[q] ? ntiles * (k + 1) / nu[q] : 0;
       units[off + k] = u;
     }
     off += nu[q];
+    split[r] = nu[q] > 1;
   }
   if (threadIdx.x == 0) *nunits = (int32_t)ntot;
+}
+
+// XCD-aware unit placement.  Workgroup i runs on XCD i mod 8, and P3 holds
+// one workgroup per CU (128 KiB LDS), 32 per XCD.  Runs r and r+1 are
+// adjacent in every tile's region, so their ~64-B segments share 128-B
+// lines: giving each XCD 32 CONSECUTIVE units per 256-workgroup wave lets
+// those blocks (sweeping the tiles in the same order at the same pace) hit
+// the shared lines in their own L2 instead of fetching each line per run.
+__device__ inline int c3_unit_of(int i) {
+  return (i / 256) * 256 + (i % 8) * 32 + (i % 256) / 8;
+}
+
+// Clears the buckets of split runs (their units flush with atomic adds).
+__global__ __launch_bounds__(256) void k_c3_zero(const int32_t *split, int nb, uint32_t *h_in,
+                                                  uint32_t *h_out) {
+  const int r = blockIdx.y;
+  if (!split[r]) return;
+  uint4 *p = (uint4 *)((r >= nb ? h_out : h_in) + (int64_t)(r % nb) * C2_BW);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < C2_BW / 4; i += gridDim.x * 256)
+    p[i] = make_uint4(0, 0, 0, 0);
 }
 
 template <int K, int Q>
@@ -585,9 +617,10 @@ __global__ __launch_bounds__(C2_HBLOCK) void k_c3_bucket(const C3Unit *units,
                                                           const uint32_t *meta_t, int64_t ntiles,
                                                           int nb, uint32_t *h_in, uint32_t *h_out,
                                                           int64_t hist_len) {
-  if ((int32_t)blockIdx.x >= *nunits) return;
+  const int ui = c3_unit_of((int)blockIdx.x);
+  if (ui >= *nunits) return;
   extern __shared__ __attribute__((aligned(16))) uint32_t bins[];  // C2_BW entries
-  const C3Unit u = units[blockIdx.x];
+  const C3Unit u = units[ui];
   uint32_t *hist = u.run >= nb ? h_out : h_in;
   const int64_t hist_base = (int64_t)(u.run % nb) * C2_BW;
   for (int i = threadIdx.x; i < C2_BW; i += C2_HBLOCK) bins[i] = 0;
@@ -658,7 +691,6 @@ static bool chain2_single_pass(Session *s, const C2Cols<F32> &c0, uint32_t *h_in
   C2Cols<F32> c = c0;
   c.ntiles = (c.n + C3_TILE - 1) / C3_TILE;
   const int nr = 2 * c.nb;
-  const int64_t len = c.hi - c.lo + 1;
   static bool attr_set = false;
   if (!attr_set) {
     for (const void *f : {(const void *)k_c3_bucket<1, 1>, (const void *)k_c3_bucket<2, 1>,
@@ -667,13 +699,14 @@ static bool chain2_single_pass(Session *s, const C2Cols<F32> &c0, uint32_t *h_in
       HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * C2_BW));
     attr_set = true;
   }
-  const int max_units = nr + 4 * 256 + 1;
+  const int max_units = (2 * nr + 1 + 255) / 256 * 256;  // runs + splits, whole XCD waves
   BufPtr part = s->alloc(2 * 2 * C3_TILE * c.ntiles);
   BufPtr meta = s->alloc(4 * nr * c.ntiles), meta_t = s->alloc(4 * nr * c.ntiles);
-  BufPtr acc = s->alloc(8 * nr + 16 + sizeof(C3Unit) * max_units);
+  BufPtr acc = s->alloc(8 * nr + 16 + 4 * nr + sizeof(C3Unit) * max_units);
   unsigned long long *run_total = (unsigned long long *)acc->p;
   int32_t *nunits = (int32_t *)(run_total + nr);
-  C3Unit *units = (C3Unit *)(run_total + nr + 2);
+  int32_t *split = nunits + 4;
+  C3Unit *units = (C3Unit *)(split + nr);
   HIP_CHECK(hipMemsetAsync(acc->p, 0, 8 * nr + 16, s->stream));
   if (p1 == 1 || p1 == 2) {
     KernelTimer kt(s, "c4_partition", (F32 ? 12.0 : 20.0) * c.n);
@@ -696,7 +729,10 @@ static bool chain2_single_pass(Session *s, const C2Cols<F32> &c0, uint32_t *h_in
     KERNEL_CHECK();
   }
   hipLaunchKernelGGL(k_c3_units, dim3(1), dim3(C3_UBLOCK), 0, s->stream,
-                     (const unsigned long long *)run_total, nr, c.ntiles, units, nunits);
+                     (const unsigned long long *)run_total, nr, c.ntiles, units, nunits, split);
+  KERNEL_CHECK();
+  hipLaunchKernelGGL(k_c3_zero, dim3(4, nr), dim3(256), 0, s->stream, (const int32_t *)split, c.nb,
+                     h_in, h_out);
   KERNEL_CHECK();
   {
     KernelTimer kt(s, "c3_bucket_hist", 4.0 * c.n);
@@ -712,7 +748,7 @@ static bool chain2_single_pass(Session *s, const C2Cols<F32> &c0, uint32_t *h_in
     hipLaunchKernelGGL(kern, dim3((unsigned)max_units), dim3(C2_HBLOCK), 4 * C2_BW,
                        s->stream, (const C3Unit *)units, (const int32_t *)nunits,
                        (const uint16_t *)part->p, (const uint32_t *)meta_t->p, c.ntiles, c.nb,
-                       h_in, h_out, len);
+                       h_in, h_out, c.hist_len);
     KERNEL_CHECK();
   }
   return true;
@@ -721,8 +757,9 @@ static bool chain2_single_pass(Session *s, const C2Cols<F32> &c0, uint32_t *h_in
 template <bool F32>
 static bool chain2_run(Session *s, const ColView *cols, int64_t n, int64_t lo, int64_t hi,
                        uint32_t *h_in, uint32_t *h_out, unsigned long long *d_loops) {
-  const int64_t len = hi - lo + 1;
-  const int nb = (int)((len + C2_BW - 1) / C2_BW);
+  const int kbits = chain2_hist_bits(hi - lo + 1);
+  const int64_t hlen = int64_t(1) << kbits;
+  const int nb = (int)(hlen / C2_BW);
   static bool attr_set = false;
   if (!attr_set) {
     HIP_CHECK(hipFuncSetAttribute((const void *)k_c2_bucket,
@@ -743,6 +780,8 @@ static bool chain2_run(Session *s, const ColView *cols, int64_t n, int64_t lo, i
   c.hi = hi;
   c.nb = nb;
   c.ntiles = (n + C2_TILE - 1) / C2_TILE;
+  c.mix = node_mix_for(kbits);
+  c.hist_len = hlen;
   // single-pass P1 forms: "c4" (default, 512 threads) | "c4w" (1024) | "single" (c3);
   // "twopass": P1 count + scan + P2 scatter
   const char *variant = getenv("CAPF_C2");
@@ -752,6 +791,8 @@ static bool chain2_run(Session *s, const ColView *cols, int64_t n, int64_t lo, i
   }
   const int nr = 2 * nb;
   const int64_t nruns = (int64_t)nr * c.ntiles;
+  HIP_CHECK(hipMemsetAsync(h_in, 0, 4 * hlen, s->stream));  // chunks of a split run add atomically
+  HIP_CHECK(hipMemsetAsync(h_out, 0, 4 * hlen, s->stream));
   BufPtr counts = s->alloc(4 * nruns), offs = s->alloc(4 * nruns);
   BufPtr acc = s->alloc(8 * (nr + 3));  // [1..nr+1] run starts, [nr+2] total
   uint32_t *d_total = (uint32_t *)((int64_t *)acc->p + nr + 2);
@@ -800,22 +841,33 @@ static bool chain2_run(Session *s, const ColView *cols, int64_t n, int64_t lo, i
     KernelTimer kt(s, "c2_bucket_hist", 2.0 * total);
     hipLaunchKernelGGL(k_c2_bucket, dim3((unsigned)chunks.size()), dim3(C2_HBLOCK), 4 * C2_BW,
                        s->stream, (const C2Chunk *)dch->p, (const uint16_t *)part->p, h_in,
-                       h_out, len);
+                       h_out, hlen);
     KERNEL_CHECK();
     s->sync();  // the host chunk vector must outlive the pageable copy
   }
   return true;
 }
 
-// h_in / h_out must be zeroed by the caller.  cols = {start(r1), end(r1),
-// start(r2), end(r2)}: non-null INTEGER columns, all plain or all FOR32.
-// Self-loop count is added to *d_loops (device).  Returns false if the shape
-// is outside this kernel's limits (the caller falls back to k_chain2_hist).
+int chain2_hist_bits(int64_t len) {
+  int k = C2_BITS;
+  while (k < 62 && (int64_t(1) << k) < len) ++k;
+  return k;
+}
+
+int64_t chain2_hist_len(int64_t len) { return int64_t(1) << chain2_hist_bits(len); }
+
+// cols = {start(r1), end(r1), start(r2), end(r2)}: non-null INTEGER columns,
+// all plain or all FOR32.  h_in / h_out hold chain2_hist_len(hi − lo + 1)
+// counters each, indexed by node_mix(id − lo); every counter is written (no
+// memset needed).  The self-loop count is added to *d_loops (device).
+// Returns false — before launching anything — if the shape is outside this
+// kernel's limits (the caller falls back to k_chain2_hist).
 bool chain2_partitioned(Session *s, const ColView *cols, int64_t n, int64_t lo, int64_t hi,
                         uint32_t *h_in, uint32_t *h_out, unsigned long long *d_loops) {
   const int64_t len = hi - lo + 1;
-  const int64_t nb = (len + C2_BW - 1) / C2_BW;
-  if (len <= 0 || 2 * nb + 1 > C2_MAX_RUNS || n <= 0) return false;  // + the dummy run
+  if (len <= 0 || n <= 0) return false;
+  const int64_t nb = chain2_hist_len(len) / C2_BW;
+  if (2 * nb + 1 > C2_MAX_RUNS) return false;  // + the dummy run
   if (n >= (int64_t(1) << 31)) return false;  // 2·n keys must fit the uint32 scan
   int nf = 0;
   for (int i = 0; i < 4; ++i) {

@@ -138,6 +138,8 @@ struct Chain2Args {
   int64_t lo, hi;
   uint32_t *h1, *h2;
   unsigned long long *loops;
+  int mixed;    // 1: index the histograms by node_mix(id − lo) (the partitioned layout)
+  NodeMix mix;
 };
 
 template <bool ONES>
@@ -155,8 +157,14 @@ __global__ __launch_bounds__(256) void k_chain2_hist(Chain2Args a) {
     const int64_t x2 = ld_int(a.u2, e), y2 = ld_int(a.v2, e);
     const unsigned long long wa = w_of<ONES>(a.wa, x1);
     const unsigned long long wc = w_of<ONES>(a.wc, y2);
-    if (wa && y1 >= a.lo && y1 <= a.hi) atomicAdd(&a.h1[y1 - a.lo], (uint32_t)wa);
-    if (wc && x2 >= a.lo && x2 <= a.hi) atomicAdd(&a.h2[x2 - a.lo], (uint32_t)wc);
+    if (wa && y1 >= a.lo && y1 <= a.hi) {
+      const uint32_t i = (uint32_t)(y1 - a.lo);
+      atomicAdd(&a.h1[a.mixed ? node_mix(i, a.mix) : i], (uint32_t)wa);
+    }
+    if (wc && x2 >= a.lo && x2 <= a.hi) {
+      const uint32_t i = (uint32_t)(x2 - a.lo);
+      atomicAdd(&a.h2[a.mixed ? node_mix(i, a.mix) : i], (uint32_t)wc);
+    }
     if (y1 == x2 && wa && wc) loops += wa * wc * w_of<ONES>(a.wb, y1);
   }
   loops = wave_reduce_sum(loops);
@@ -715,13 +723,15 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
   if (n >= (int64_t(1) << 32)) return false;
   const bool all_ones = wa.ones && wb.ones && wc.ones;
 
-  BufPtr h = s->alloc(8 * std::max<int64_t>(len, 1) + 64);
+  // partitioned histograms are indexed by node_mix(b − lo) over 2^k ≥ len counters
+  const int64_t hlen = len > 0 ? std::max(len, chain2_hist_len(len)) : 0;
+  BufPtr h = s->alloc(8 * std::max<int64_t>(hlen, 1) + 64);
   BufPtr acc = s->alloc(16);
   HIP_CHECK(hipMemsetAsync(acc->p, 0, 16, s->stream));
   uint32_t *h1 = (uint32_t *)h->p;
-  uint32_t *h2 = h1 + ((len + 15) & ~int64_t(15));  // keep dwordx4 alignment
+  uint32_t *h2 = h1 + ((hlen + 15) & ~int64_t(15));  // keep dwordx4 alignment
+  int64_t dot_len = len;
   if (len > 0) {
-    HIP_CHECK(hipMemsetAsync(h->p, 0, 8 * std::max<int64_t>(len, 1) + 64, s->stream));
     Chain2Args a;
     a.u1 = view_of(R.cols[c.u1]);
     a.v1 = view_of(R.cols[c.v1]);
@@ -737,31 +747,36 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
     a.h1 = h1;
     a.h2 = h2;
     a.loops = (unsigned long long *)acc->p + 1;
+    a.mixed = 0;
+    a.mix = node_mix_for(0);
     const char *mode = getenv("CAPF_CHAIN2");  // "atomic" | "partitioned" (default: by size)
     const bool want_part = all_ones && wa.map.m.lo == lo && wc.map.m.lo == lo &&
                            wa.map.m.hi == hi && wc.map.m.hi == hi &&
                            (mode ? strcmp(mode, "partitioned") == 0 : n >= (int64_t(1) << 22));
     if (n > 0 && want_part &&
         chain2_partitioned(s, pc, n, lo, hi, h1, h2, a.loops)) {
-      // loops accumulated on the device
-    } else if (n > 0) {
-      KernelTimer kt(s, "chain2_hist", 16.0 * n);
-      unsigned grid = grid_for(n, 256, 256 * 32);
-      if (all_ones)
-        hipLaunchKernelGGL(k_chain2_hist<true>, dim3(grid), dim3(256), 0, s->stream, a);
-      else
-        hipLaunchKernelGGL(k_chain2_hist<false>, dim3(grid), dim3(256), 0, s->stream, a);
-      KERNEL_CHECK();
+      dot_len = chain2_hist_len(len);  // every counter written; loops accumulated on the device
+    } else {
+      HIP_CHECK(hipMemsetAsync(h->p, 0, 8 * std::max<int64_t>(hlen, 1) + 64, s->stream));
+      if (n > 0) {
+        KernelTimer kt(s, "chain2_hist", 16.0 * n);
+        unsigned grid = grid_for(n, 256, 256 * 32);
+        if (all_ones)
+          hipLaunchKernelGGL(k_chain2_hist<true>, dim3(grid), dim3(256), 0, s->stream, a);
+        else
+          hipLaunchKernelGGL(k_chain2_hist<false>, dim3(grid), dim3(256), 0, s->stream, a);
+        KERNEL_CHECK();
+      }
     }
     {
-      KernelTimer kt(s, "chain2_dot", 8.0 * len);
-      unsigned grid = grid_for(len / 4 + 1, 256, 256 * 8);
-      if (wb.ones)
+      KernelTimer kt(s, "chain2_dot", 8.0 * dot_len);
+      unsigned grid = grid_for(dot_len / 4 + 1, 256, 256 * 8);
+      if (wb.ones)  // ONES: Σ in·out is invariant under the node_mix bijection
         hipLaunchKernelGGL(k_chain2_dot<true>, dim3(grid), dim3(256), 0, s->stream, h1, h2,
-                           wb.map.m, lo, len, (unsigned long long *)acc->p);
+                           wb.map.m, lo, dot_len, (unsigned long long *)acc->p);
       else
         hipLaunchKernelGGL(k_chain2_dot<false>, dim3(grid), dim3(256), 0, s->stream, h1, h2,
-                           wb.map.m, lo, len, (unsigned long long *)acc->p);
+                           wb.map.m, lo, dot_len, (unsigned long long *)acc->p);
       KERNEL_CHECK();
     }
   }
@@ -816,6 +831,10 @@ bool try_fused_count(const NodePtr &n, int64_t *out) {
 // ===================================================================== C-ABI
 using namespace capf;
 
+extern "C" int64_t capf_chain2_hist_len(int64_t n_nodes) {
+  return n_nodes > 0 && n_nodes <= (int64_t(1) << 31) ? chain2_hist_len(n_nodes) : 0;
+}
+
 extern "C" capf_status capf_chain2_local_hists(capf_session *cs, capf_table *rels,
                                                const char *src_col, const char *dst_col,
                                                int64_t node_base, int64_t n_nodes,
@@ -824,7 +843,7 @@ extern "C" capf_status capf_chain2_local_hists(capf_session *cs, capf_table *rel
   try {
     if (!cs || !rels || !src_col || !dst_col || !d_in_hist || !d_out_hist || !self_loops)
       illegal("null argument");
-    if (n_nodes < 0) illegal("negative node count");
+    if (n_nodes <= 0 || n_nodes > (int64_t(1) << 31)) illegal("node count out of range");
     Session *s = &cs->impl;
     const NodePtr &nd = rels->node;
     int si = nd->col_index_or_throw(src_col), di = nd->col_index_or_throw(dst_col);
@@ -833,8 +852,7 @@ extern "C" capf_status capf_chain2_local_hists(capf_session *cs, capf_table *rel
     if (src->type != Type::Int64 || dst->type != Type::Int64 || src->valid || dst->valid)
       illegal("chain2_local_hists needs non-null INTEGER endpoint columns");
     if (d->nrows >= (int64_t(1) << 32)) not_impl("more than 2^32 rels per rank");
-    HIP_CHECK(hipMemsetAsync(d_in_hist, 0, 4 * n_nodes, s->stream));
-    HIP_CHECK(hipMemsetAsync(d_out_hist, 0, 4 * n_nodes, s->stream));
+    const int64_t hlen = chain2_hist_len(n_nodes);
     BufPtr acc = s->alloc(16);
     HIP_CHECK(hipMemsetAsync(acc->p, 0, 16, s->stream));
     Chain2Args a;
@@ -847,16 +865,22 @@ extern "C" capf_status capf_chain2_local_hists(capf_session *cs, capf_table *rel
     a.h1 = d_in_hist;
     a.h2 = d_out_hist;
     a.loops = (unsigned long long *)acc->p + 1;
+    a.mixed = 1;
+    a.mix = node_mix_for(chain2_hist_bits(n_nodes));
     const char *mode = getenv("CAPF_CHAIN2");
     const bool want_part = mode ? strcmp(mode, "partitioned") == 0 : a.n >= (int64_t(1) << 22);
     const ColView pc[4] = {a.u1, a.v1, a.u2, a.v2};
-    const bool done = a.n > 0 && n_nodes > 0 && want_part &&
-                      chain2_partitioned(s, pc, a.n, a.lo, a.hi, a.h1, a.h2, a.loops);
-    if (!done && a.n > 0 && n_nodes > 0) {
-      KernelTimer kt(s, "chain2_hist", 16.0 * a.n);
-      hipLaunchKernelGGL(k_chain2_hist<true>, dim3(grid_for(a.n, 256, 256 * 32)), dim3(256), 0,
-                         s->stream, a);
-      KERNEL_CHECK();
+    const bool done =
+        want_part && chain2_partitioned(s, pc, a.n, a.lo, a.hi, a.h1, a.h2, a.loops);
+    if (!done) {
+      HIP_CHECK(hipMemsetAsync(d_in_hist, 0, 4 * hlen, s->stream));
+      HIP_CHECK(hipMemsetAsync(d_out_hist, 0, 4 * hlen, s->stream));
+      if (a.n > 0) {
+        KernelTimer kt(s, "chain2_hist", 16.0 * a.n);
+        hipLaunchKernelGGL(k_chain2_hist<true>, dim3(grid_for(a.n, 256, 256 * 32)), dim3(256), 0,
+                           s->stream, a);
+        KERNEL_CHECK();
+      }
     }
     HIP_CHECK(hipMemcpyAsync(s->h_scalars, acc->p, 16, hipMemcpyDeviceToHost, s->stream));
     s->sync();

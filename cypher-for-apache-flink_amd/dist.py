@@ -29,9 +29,12 @@ def edge_range(m, rank, world):
 
 
 def padded_nodes(n, world):
-    """Node count padded so every rank's slice is a multiple of 4 (dwordx4)."""
+    """Histogram length (capf_chain2_hist_len: 2^k >= n, indexed by the node_mix
+    hash) padded so every rank's slice is a multiple of 4 (dwordx4)."""
+    from .table import chain2_hist_len
+    h = chain2_hist_len(n)
     q = 4 * world
-    return (n + q - 1) // q * q
+    return (h + q - 1) // q * q
 
 
 def reduce_scatter(t, world, group=None):
@@ -63,7 +66,7 @@ def combine_two_hop(in_hist, out_hist, local_loops, dot_fn, group=None):
 
 def gpu_two_hop_count(session, rels, n_nodes, node_base=0, group=None, hists=None):
     """Distributed 2-hop count(*) for this rank's rel shard `rels` (GpuTable)."""
-    from .table import dot_u32
+    from .table import chain2_hist_len, dot_u32
     world = dist.get_world_size(group)
     npad = padded_nodes(n_nodes, world)
     if hists is None:
@@ -71,8 +74,9 @@ def gpu_two_hop_count(session, rels, n_nodes, node_base=0, group=None, hists=Non
                  torch.zeros(npad, dtype=torch.int32, device="cuda"))
     in_h, out_h = hists
     loops = rels.chain2_local_hists("source", "target", node_base, n_nodes, in_h.data_ptr(), out_h.data_ptr())
-    if npad > n_nodes:
-        in_h[n_nodes:].zero_()
-        out_h[n_nodes:].zero_()
+    hlen = chain2_hist_len(n_nodes)
+    if npad > hlen:
+        in_h[hlen:].zero_()
+        out_h[hlen:].zero_()
     return combine_two_hop(in_h, out_h, loops,
                            lambda a, b: dot_u32(session, a.data_ptr(), b.data_ptr(), a.numel()), group)

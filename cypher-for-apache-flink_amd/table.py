@@ -334,6 +334,11 @@ class GpuTable:
         return loops.value
 
 
+def chain2_hist_len(n_nodes):
+    """Counters per histogram written by chain2_local_hists (2^k >= n_nodes)."""
+    return int(_lib.load().capf_chain2_hist_len(int(n_nodes)))
+
+
 def dot_u32(session, d_a, d_b, n):
     out = c_uint64()
     _lib.call("capf_dot_u32", session._h, c_void_p(d_a), c_void_p(d_b), int(n), byref(out))

@@ -278,11 +278,16 @@ capf_status capf_range_node_table(capf_session *s, int64_t base, int64_t n, uint
  * caller (one process per GPU, torch.distributed/RCCL) exchanges the
  * per-node histograms between ranks.  See DESIGN.md "Multi-GPU".
  * capf_chain2_local_hists: over the rel rows of this rank, writes
- *   in_hist[v - node_base]  += #rels with dst = v   (v any node)
- *   out_hist[v - node_base] += #rels with src = v
+ *   in_hist[mix(v - node_base)]  = #rels with dst = v   (v any node)
+ *   out_hist[mix(v - node_base)] = #rels with src = v
  * for rels whose endpoints both lie in [node_base, node_base + n_nodes)
  * and returns the number of such self-loops.  Buffers are device uint32
- * arrays of n_nodes entries and are zeroed by the call.                    */
+ * arrays of capf_chain2_hist_len(n_nodes) = 2^k >= n_nodes entries, every
+ * entry written by the call; mix is the bijection of 2^k node offsets
+ * (odd multiply, xorshift; csrc/device_common.h node_mix) the radix
+ * partitioning hashes by, so a contiguous 1/G slice of the histogram index
+ * is a hash partition of the nodes.                                         */
+int64_t capf_chain2_hist_len(int64_t n_nodes);
 capf_status capf_chain2_local_hists(capf_session *s, capf_table *rels, const char *src_col,
                                     const char *dst_col, int64_t node_base, int64_t n_nodes,
                                     uint32_t *d_in_hist, uint32_t *d_out_hist,

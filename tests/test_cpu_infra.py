@@ -80,3 +80,22 @@ def test_one_hop_label_closed_form():
                    rels=[(i, int(a), int(b), "E", {}) for i, (a, b) in enumerate(zip(src, dst))])
     q = Query([Match([NodeP("a", ("Person",)), NodeP("b")], [RelP("r", "a", "b")])], [Stage([("c", CountStar())])])
     assert run(ScanGraph.from_data(OracleSession(), gd), q)[0]["c"] == cmodel.count_1hop(src, dst, n, in_a=person)
+
+
+@pytest.mark.parametrize("k", [15, 16, 20, 24])
+def test_node_mix_is_a_bijection(k):
+    from oracle import nodemix
+    h = nodemix.node_mix(np.arange(1 << k), k)
+    assert h.min() == 0 and h.max() == (1 << k) - 1
+    assert len(np.unique(h)) == 1 << k
+
+
+def test_node_mix_balances_rmat_runs():
+    # the raw top bits of R-MAT ids are skewed (run 0 holds ~8 % of keys at 9
+    # run bits); the mixed ones are near-uniform
+    from oracle import nodemix
+    s, d = cmodel.rmat(20, count=1 << 20)
+    raw = np.bincount(d >> 15, minlength=32)
+    mixed = np.bincount(nodemix.node_mix(d, 20) >> 15, minlength=32)
+    assert raw.max() / raw.mean() > 4
+    assert mixed.max() / mixed.mean() < 1.5

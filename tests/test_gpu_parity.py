@@ -307,3 +307,36 @@ def test_unit_and_empty(gpu_session):
     e = gpu_session.empty(["a", "b"], [T_INT, T_STRING])
     assert e.size == 0 and e.physicalColumns == ["a", "b"]
     assert e.columnType == {"a": "INTEGER", "b": "STRING"}
+
+
+@pytest.mark.parametrize("variant", ["c4w", "atomic"])
+@pytest.mark.parametrize("compact", [False, True], ids=["int64", "for32"])
+@pytest.mark.parametrize("scale,base", [(10, 0), (13, 5), (16, 0)])
+def test_local_hists_hashed_layout(gpu_session, monkeypatch, variant, compact, scale, base):
+    """capf_chain2_local_hists: every counter of the node_mix-indexed in/out
+    histograms equals the oracle's degree count (partitioned and atomic paths
+    share the layout), and the self-loop count matches."""
+    import torch
+    from capf_amd.table import chain2_hist_len
+    from oracle import nodemix
+    monkeypatch.setenv("CAPF_CHAIN2", "partitioned" if variant != "atomic" else "atomic")
+    monkeypatch.setenv("CAPF_C2", variant)
+    m = 16 << scale
+    t = gpu_session.rmat_rels(scale, cmodel.rmat_seed(scale), cmodel.thresholds(), 0, m)
+    if compact:
+        t = t.compact()
+    n = (1 << scale) - base  # node range [base, 2^scale): rels touching ids < base drop out
+    hl = chain2_hist_len(n)
+    assert hl == 1 << nodemix.hist_bits(n)
+    hi = torch.full((hl,), 7, dtype=torch.int32, device="cuda")  # garbage: all must be written
+    ho = torch.full((hl,), 7, dtype=torch.int32, device="cuda")
+    loops = t.chain2_local_hists("source", "target", base, n, hi.data_ptr(), ho.data_ptr())
+    src, dst = cmodel.rmat(scale)
+    ok = (src >= base) & (dst >= base)
+    s, d = src[ok] - base, dst[ok] - base
+    k = nodemix.hist_bits(n)
+    ein = np.bincount(nodemix.node_mix(d, k), minlength=hl)
+    eout = np.bincount(nodemix.node_mix(s, k), minlength=hl)
+    assert np.array_equal(hi.cpu().numpy().astype(np.int64), ein)
+    assert np.array_equal(ho.cpu().numpy().astype(np.int64), eout)
+    assert loops == int((s == d).sum())

@@ -325,10 +325,12 @@ bool try_fused_count(const NodePtr &n, int64_t *out);
 // Histograms hold chain2_hist_len(hi − lo + 1) counters indexed by
 // node_mix(id − lo) (device_common.h) and are fully written (no memset).
 // The self-loop count is added to *d_loops (device memory): no host round trip.
+// in_range: the columns' statistics put every id inside [lo, hi].
 int chain2_hist_bits(int64_t len);
 int64_t chain2_hist_len(int64_t len);
 bool chain2_partitioned(Session *s, const ColView *cols, int64_t n, int64_t lo, int64_t hi,
-                        uint32_t *h_in, uint32_t *h_out, unsigned long long *d_loops);
+                        bool in_range, uint32_t *h_in, uint32_t *h_out,
+                        unsigned long long *d_loops);
 
 }  // namespace capf
 

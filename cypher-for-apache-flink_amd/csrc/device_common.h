@@ -25,31 +25,37 @@ __host__ __device__ inline uint64_t fmix64(uint64_t k) {
   return k;
 }
 
-// Bijective mixer of node offsets on a 2^k domain (odd multiply mod 2^k,
-// xorshift; each step invertible).  The radix-partitioned histograms key
+// Bijective mixer of node offsets on a 2^k domain: odd multiply mod 2^k, then
+// xorshift (each step invertible).  The radix-partitioned histograms key
 // their runs by the HIGH bits of node_mix(id − lo): hash partitioning, so the
 // per-bit skew of R-MAT ids (bit = 0 with p = .76 at every level) cannot pile
-// 8 % of all keys into run 0 (measured bucket max/mean at s24: 43 raw, 1.6
-// mixed; LDS bank max/mean 8.1 → 1.07).  Σ_b in[b]·out[b] is invariant under
-// a bijection of b, so the dot runs over the mixed index unchanged.
+// 8 % of all keys into run 0 (measured at s24, 256 runs: max/mean 43 raw,
+// 1.27 mixed).  Σ_b in[b]·out[b] is invariant under a bijection of b, so the
+// dot runs over the mixed index unchanged.  For k ≤ 24 the multiply is the
+// full-rate 24-bit v_mul_u32_u24 (the 32-bit form is quarter rate).
 struct NodeMix {
   uint32_t mask;  // 2^k − 1
-  int sh;         // k / 2; 0 = identity (diagnostics: CAPF_NOMIX=1)
+  int sh;         // k / 2
+  int wide;       // k > 24: 32-bit multiply
 };
 
-__host__ __device__ inline uint32_t node_mix(uint32_t x, NodeMix m) {
-  if (m.sh == 0) return x;
-  uint32_t h = (x * 0x9E3779B1u) & m.mask;
-  h ^= h >> m.sh;
-  h = (h * 0x85EBCA6Bu) & m.mask;
+constexpr uint32_t NODE_MIX_A = 0xB5297Bu;  // odd, < 2^24
+
+template <bool WIDE>
+__device__ inline uint32_t node_mix_t(uint32_t x, NodeMix m) {
+  const uint32_t h = (WIDE ? x * NODE_MIX_A : __umul24(x, NODE_MIX_A)) & m.mask;
   return h ^ (h >> m.sh);
+}
+
+__device__ inline uint32_t node_mix(uint32_t x, NodeMix m) {
+  return m.wide ? node_mix_t<true>(x, m) : node_mix_t<false>(x, m);
 }
 
 inline NodeMix node_mix_for(int kbits) {
   NodeMix m;
   m.mask = kbits >= 32 ? 0xFFFFFFFFu : (uint32_t(1) << kbits) - 1;
   m.sh = kbits / 2;
-  if (getenv("CAPF_NOMIX")) m.sh = 0;
+  m.wide = kbits > 24;
   return m;
 }
 

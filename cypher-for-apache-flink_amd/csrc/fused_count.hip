@@ -753,8 +753,13 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
     const bool want_part = all_ones && wa.map.m.lo == lo && wc.map.m.lo == lo &&
                            wa.map.m.hi == hi && wc.map.m.hi == hi &&
                            (mode ? strcmp(mode, "partitioned") == 0 : n >= (int64_t(1) << 22));
+    bool in_range = true;  // column statistics (cached): all endpoint ids inside [lo, hi]
+    for (int col : {c.u1, c.v1, c.u2, c.v2}) {
+      const ColStats &st = column_stats(s, R.cols[col]);
+      in_range = in_range && st.min >= lo && st.max <= hi;
+    }
     if (n > 0 && want_part &&
-        chain2_partitioned(s, pc, n, lo, hi, h1, h2, a.loops)) {
+        chain2_partitioned(s, pc, n, lo, hi, in_range, h1, h2, a.loops)) {
       dot_len = chain2_hist_len(len);  // every counter written; loops accumulated on the device
     } else {
       HIP_CHECK(hipMemsetAsync(h->p, 0, 8 * std::max<int64_t>(hlen, 1) + 64, s->stream));
@@ -870,8 +875,10 @@ extern "C" capf_status capf_chain2_local_hists(capf_session *cs, capf_table *rel
     const char *mode = getenv("CAPF_CHAIN2");
     const bool want_part = mode ? strcmp(mode, "partitioned") == 0 : a.n >= (int64_t(1) << 22);
     const ColView pc[4] = {a.u1, a.v1, a.u2, a.v2};
-    const bool done =
-        want_part && chain2_partitioned(s, pc, a.n, a.lo, a.hi, a.h1, a.h2, a.loops);
+    const ColStats &ss = column_stats(s, src), &sd = column_stats(s, dst);
+    const bool in_range = ss.min >= a.lo && ss.max <= a.hi && sd.min >= a.lo && sd.max <= a.hi;
+    const bool done = want_part && chain2_partitioned(s, pc, a.n, a.lo, a.hi, in_range, a.h1,
+                                                      a.h2, a.loops);
     if (!done) {
       HIP_CHECK(hipMemsetAsync(d_in_hist, 0, 4 * hlen, s->stream));
       HIP_CHECK(hipMemsetAsync(d_out_hist, 0, 4 * hlen, s->stream));

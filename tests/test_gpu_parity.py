@@ -60,22 +60,20 @@ def test_two_hop_count_rmat(gpu_session, scale, compact):
         assert got == p.probe(0, len(src), 4)
 
 
-@pytest.mark.parametrize("variant", ["c4", "c4w", "single", "twopass", "atomic"])
+@pytest.mark.parametrize("variant", ["partitioned", "atomic"])
 @pytest.mark.parametrize("compact", [False, True], ids=["int64", "for32"])
-@pytest.mark.parametrize("scale,count", [(6, None), (11, 30001), (14, None), (15, 123457)])
-def test_two_hop_partition_variants(gpu_session, monkeypatch, variant, compact, scale, count):
+@pytest.mark.parametrize("scale,count,nodes", [(6, None, None), (11, 30001, None), (14, None, None),
+                                               (15, 123457, None), (12, None, 3000), (14, 50001, 9999)])
+def test_two_hop_partition_variants(gpu_session, monkeypatch, variant, compact, scale, count, nodes):
     """Every histogram path, forced at small and ragged sizes (count not a
-    multiple of the 4-rel vector or the tile), must give the closed form."""
-    if variant == "atomic":
-        monkeypatch.setenv("CAPF_CHAIN2", "atomic")
-    else:
-        monkeypatch.setenv("CAPF_CHAIN2", "partitioned")
-        monkeypatch.setenv("CAPF_C2", variant)
-    g = rmat_graph(gpu_session, scale, compact=compact, count=count)
+    multiple of the 4-rel vector or the tile) and with a node table smaller
+    than the id range (range checks + dummy run), must give the closed form."""
+    monkeypatch.setenv("CAPF_CHAIN2", variant)
+    g = rmat_graph(gpu_session, scale, compact=compact, count=count, n_nodes=nodes)
     got = run(g, TWO_HOP)[0]["count"]
     assert gpu_session.last_plan() == "fused_chain2"
     src, dst = cmodel.rmat(scale, count=count)
-    assert got == cmodel.count_2hop(src, dst, 1 << scale)
+    assert got == cmodel.count_2hop(src, dst, nodes or 1 << scale)
 
 
 def test_rmat_generator_bit_exact(gpu_session):
@@ -309,7 +307,7 @@ def test_unit_and_empty(gpu_session):
     assert e.columnType == {"a": "INTEGER", "b": "STRING"}
 
 
-@pytest.mark.parametrize("variant", ["c4w", "atomic"])
+@pytest.mark.parametrize("variant", ["partitioned", "atomic"])
 @pytest.mark.parametrize("compact", [False, True], ids=["int64", "for32"])
 @pytest.mark.parametrize("scale,base", [(10, 0), (13, 5), (16, 0)])
 def test_local_hists_hashed_layout(gpu_session, monkeypatch, variant, compact, scale, base):
@@ -319,8 +317,7 @@ def test_local_hists_hashed_layout(gpu_session, monkeypatch, variant, compact, s
     import torch
     from capf_amd.table import chain2_hist_len
     from oracle import nodemix
-    monkeypatch.setenv("CAPF_CHAIN2", "partitioned" if variant != "atomic" else "atomic")
-    monkeypatch.setenv("CAPF_C2", variant)
+    monkeypatch.setenv("CAPF_CHAIN2", variant)
     m = 16 << scale
     t = gpu_session.rmat_rels(scale, cmodel.rmat_seed(scale), cmodel.thresholds(), 0, m)
     if compact:
@@ -340,3 +337,33 @@ def test_local_hists_hashed_layout(gpu_session, monkeypatch, variant, compact, s
     assert np.array_equal(hi.cpu().numpy().astype(np.int64), ein)
     assert np.array_equal(ho.cpu().numpy().astype(np.int64), eout)
     assert loops == int((s == d).sum())
+
+
+@pytest.mark.parametrize("n", [1 << 17, 100000], ids=["in_range", "checked"])
+@pytest.mark.parametrize("compact", [False, True], ids=["int64", "for32"])
+def test_two_hop_hub_overflow(gpu_session, monkeypatch, n, compact):
+    """Hubs with in/out degree far above 2^16 in one P3 unit: the packed
+    uint16 LDS counters hand off 2^15 per overflow (k_c3_overflow) and the
+    hub runs are split into atomically flushed units; the count stays exact."""
+    from capf_amd.graph import ElementTable, ScanGraph as SG
+    from capf_amd.expr import T_INT
+    monkeypatch.setenv("CAPF_CHAIN2", "partitioned")
+    rng = np.random.default_rng(11)
+    m = 1 << 20
+    src = rng.integers(0, 1 << 17, m)  # ids ≥ n (checked case) fall outside the node table
+    dst = rng.integers(0, 1 << 17, m)
+    src[: 300000] = 5            # out-hub
+    dst[100000: 400000] = 9      # in-hub
+    dst[500000: 600000] = 70000  # second in-hub in another bucket
+    src[590000: 700000] = 70000
+    dst[650000: 660000] = src[650000: 660000]  # self-loops
+    rels = gpu_session.table([("id", T_INT, np.arange(m), None), ("source", T_INT, src, None),
+                              ("target", T_INT, dst, None)])
+    nodes = gpu_session.range_nodes(0, n, id_col="id")
+    if compact:
+        rels, nodes = rels.compact(), nodes.compact()
+    g = SG(gpu_session, [ElementTable("node", frozenset(["V"]), nodes, {})],
+           [ElementTable("rel", frozenset(["E"]), rels, {})])
+    got = run(g, TWO_HOP)[0]["count"]
+    assert gpu_session.last_plan() == "fused_chain2"
+    assert got == cmodel.count_2hop(src.astype(np.int64), dst.astype(np.int64), n)

@@ -363,7 +363,8 @@ __device__ inline void c3_handoff(uint32_t *w, uint32_t inc, uint32_t hidx, uint
   if (k < o.cap) o.log[k] = make_uint2(hidx, side);
 }
 
-constexpr int C5_PPS = 2;  // P3 pieces per lane per step (loads in flight)
+// P3 pieces per lane per step (measured at s24: 2 → 0.553, 4 → 0.536, 8 → 0.548 ms)
+constexpr int C5_PPS = 4;
 
 struct C5WaveTab {
   uint32_t pre[WAVE + 1];  // exclusive prefix of the 64 tiles' piece counts, + total
@@ -382,8 +383,9 @@ constexpr size_t C5_GATHER_LDS =
 // tools/bench_gather.hip) — and every lane holds a live piece.  Pad keys
 // (8·(t mod 8) + slot) and the keys of past-the-end lanes (= lane) are
 // counted like the others and subtracted from bins 0..63 at the flush.
+// PPS pieces per lane per step: independent searches and loads in flight.
 // MODE (diagnostics, CAPF_P3_MODE=1): loads only, keys xor-folded.
-template <int MODE>
+template <int MODE, int PPS>
 __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
                                                          const int32_t *nunits,
                                                          const uint16_t *part,
@@ -426,10 +428,10 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
     tab.qb[lane] = (uint32_t)t * rs8 + (w & 0xFFFF);
     const uint32_t total = __shfl(inc, WAVE - 1, WAVE);
     __builtin_amdgcn_wave_barrier();
-    for (uint32_t p0 = 0; p0 < total; p0 += WAVE * C5_PPS) {
-      uint4 v[C5_PPS];
+    for (uint32_t p0 = 0; p0 < total; p0 += WAVE * PPS) {
+      uint4 v[PPS];
 #pragma unroll
-      for (int j = 0; j < C5_PPS; ++j) {
+      for (int j = 0; j < PPS; ++j) {
         const uint32_t p = p0 + j * WAVE + lane;
         uint32_t k = 0;  // last tile k with pre[k] <= p
 #pragma unroll
@@ -443,7 +445,7 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
         }
       }
 #pragma unroll
-      for (int j = 0; j < C5_PPS; ++j) {
+      for (int j = 0; j < PPS; ++j) {
         const uint32_t wd[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
         if (MODE == 1) {
           fold ^= wd[0] ^ wd[1] ^ wd[2] ^ wd[3];
@@ -526,10 +528,8 @@ static void chain2_c5(Session *s, C5Cols<F32> c, bool in_range, uint32_t *h_in, 
   c.rstride = ((int64_t)2 * SH::TILE + 8 * (nr + 1) + 7) & ~int64_t(7);
   static bool attr_set = false;
   if (!attr_set) {
-    HIP_CHECK(hipFuncSetAttribute((const void *)k_c5_gather<0>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, C5_GATHER_LDS));
-    HIP_CHECK(hipFuncSetAttribute((const void *)k_c5_gather<1>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, C5_GATHER_LDS));
+    for (const void *f : {(const void *)k_c5_gather<0, C5_PPS>, (const void *)k_c5_gather<1, C5_PPS>})
+      HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, C5_GATHER_LDS));
     attr_set = true;
   }
   const int max_units = (2 * nr + 1 + 255) / 256 * 256;  // runs + splits, whole XCD waves
@@ -573,7 +573,7 @@ static void chain2_c5(Session *s, C5Cols<F32> c, bool in_range, uint32_t *h_in, 
   {
     KernelTimer kt(s, "c5_gather", 4.0 * c.n);
     const char *md = getenv("CAPF_P3_MODE");
-    auto kern = md && atoi(md) == 1 ? k_c5_gather<1> : k_c5_gather<0>;
+    auto kern = md && atoi(md) == 1 ? k_c5_gather<1, C5_PPS> : k_c5_gather<0, C5_PPS>;
     hipLaunchKernelGGL(kern, dim3((unsigned)max_units), dim3(C5_BLOCK), C5_GATHER_LDS, s->stream,
                        (const C3Unit *)units, (const int32_t *)nunits, (const uint16_t *)part->p,
                        (const uint32_t *)meta_t->p, c.ntiles, c.nb, c.rstride, h_in, h_out, ovf);

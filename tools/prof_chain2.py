@@ -1,6 +1,6 @@
 """Profiling driver (not a test): one warm + one measured 2-hop count at a scale.
 
-usage: python tests/prof_chain2.py SCALE VARIANT(single|twopass) COMPACT(0|1)
+usage: python tools/prof_chain2.py SCALE VARIANT(single|twopass) COMPACT(0|1)
 Run under rocprofv3 (--kernel-trace --stats, or --pmc ...) to attribute the
 partition kernels' time and traffic."""
 import os

@@ -10,6 +10,6 @@ for set in "SQ_WAVES SQ_INSTS SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_
            "SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS SQ_INST_LEVEL_VMEM SQ_INSTS_LDS_ATOMIC SQ_INSTS_LDS_LOAD" \
            "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum" ; do
   i=$((i+1))
-  timeout -k 10 180 rocprofv3 --kernel-include-regex "$R" --pmc $set -d gpurun_out/pmc2/p$i --output-format csv -- python3 tests/prof_chain2.py 24 $V 1 > gpurun_out/pmc2/log$i.txt 2>&1
+  timeout -k 10 180 rocprofv3 --kernel-include-regex "$R" --pmc $set -d gpurun_out/pmc2/p$i --output-format csv -- python3 tools/prof_chain2.py 24 $V 1 > gpurun_out/pmc2/log$i.txt 2>&1
 done
 echo done

@@ -3,5 +3,5 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/trace
-timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --stats -d gpurun_out/trace -o run --output-format csv -- python3 tests/prof_chain2.py 24 ${1:-c4w} 1 > gpurun_out/trace/log.txt 2>&1
+timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --stats -d gpurun_out/trace -o run --output-format csv -- python3 tools/prof_chain2.py 24 ${1:-c4w} 1 > gpurun_out/trace/log.txt 2>&1
 echo done

@@ -84,8 +84,8 @@ def cpu_baseline(session, graph, scale, budget_s):
 
 
 # kernels of one fused 2-hop count (fused_count.hip + chain2_partitioned.hip)
-PIPELINE = ("c4_partition", "c3_partition", "c3_transpose", "c3_bucket_hist", "c2_count",
-            "c2_scatter", "c2_bucket_hist", "chain2_hist", "chain2_dot")
+PIPELINE = ("c5_partition", "c3_transpose", "c3_units", "c5_gather", "c3_overflow", "chain2_hist",
+            "chain2_dot")
 
 
 def pipeline_roofline(prof, steps, compulsory_bytes, traffic_per_query=None):

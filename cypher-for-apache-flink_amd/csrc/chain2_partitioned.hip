@@ -564,12 +564,15 @@ static void chain2_c5(Session *s, C5Cols<F32> c, bool in_range, uint32_t *h_in, 
                        c.ntiles, nr, run_total);
     KERNEL_CHECK();
   }
-  hipLaunchKernelGGL(k_c3_units, dim3(1), dim3(C3_UBLOCK), 0, s->stream,
-                     (const unsigned long long *)run_total, nr, c.ntiles, units, nunits, split);
-  KERNEL_CHECK();
-  hipLaunchKernelGGL(k_c3_zero, dim3(4, nr), dim3(256), 0, s->stream, (const int32_t *)split, c.nb,
-                     h_in, h_out);
-  KERNEL_CHECK();
+  {
+    KernelTimer kt(s, "c3_units", 8.0 * nr);
+    hipLaunchKernelGGL(k_c3_units, dim3(1), dim3(C3_UBLOCK), 0, s->stream,
+                       (const unsigned long long *)run_total, nr, c.ntiles, units, nunits, split);
+    KERNEL_CHECK();
+    hipLaunchKernelGGL(k_c3_zero, dim3(4, nr), dim3(256), 0, s->stream, (const int32_t *)split,
+                       c.nb, h_in, h_out);
+    KERNEL_CHECK();
+  }
   {
     KernelTimer kt(s, "c5_gather", 4.0 * c.n);
     const char *md = getenv("CAPF_P3_MODE");
@@ -579,8 +582,11 @@ static void chain2_c5(Session *s, C5Cols<F32> c, bool in_range, uint32_t *h_in, 
                        (const uint32_t *)meta_t->p, c.ntiles, c.nb, c.rstride, h_in, h_out, ovf);
     KERNEL_CHECK();
   }
-  hipLaunchKernelGGL(k_c3_overflow, dim3(16), dim3(256), 0, s->stream, ovf, h_in, h_out);
-  KERNEL_CHECK();
+  {
+    KernelTimer kt(s, "c3_overflow", 0.0);
+    hipLaunchKernelGGL(k_c3_overflow, dim3(16), dim3(256), 0, s->stream, ovf, h_in, h_out);
+    KERNEL_CHECK();
+  }
 }
 
 int chain2_hist_bits(int64_t len) {

@@ -8,7 +8,7 @@ OUT=gpurun_out/prof
 mkdir -p $OUT
 SCALE=${1:-24}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o bench --output-format csv -- python3 bench.py --steps 10 --warmup 3 --scale $SCALE --no-cpu > $OUT/bench_traced.json 2> $OUT/trace.log
-timeout -k 10 300 rocprofv3 --kernel-include-regex "c4_|c3_|c2_|chain2" --pmc FETCH_SIZE -d $OUT/fetch -o f --output-format csv -- python3 bench.py --steps 3 --warmup 1 --scale $SCALE --no-cpu > $OUT/bench_fetch.json 2> $OUT/fetch.log
-timeout -k 10 300 rocprofv3 --kernel-include-regex "c4_|c3_|c2_|chain2" --pmc WRITE_SIZE -d $OUT/write -o w --output-format csv -- python3 bench.py --steps 3 --warmup 1 --scale $SCALE --no-cpu > $OUT/bench_write.json 2> $OUT/write.log
+timeout -k 10 300 rocprofv3 --kernel-include-regex "c5_|c3_|chain2" --pmc FETCH_SIZE -d $OUT/fetch -o f --output-format csv -- python3 bench.py --steps 3 --warmup 1 --scale $SCALE --no-cpu > $OUT/bench_fetch.json 2> $OUT/fetch.log
+timeout -k 10 300 rocprofv3 --kernel-include-regex "c5_|c3_|chain2" --pmc WRITE_SIZE -d $OUT/write -o w --output-format csv -- python3 bench.py --steps 3 --warmup 1 --scale $SCALE --no-cpu > $OUT/bench_write.json 2> $OUT/write.log
 python3 tools/make_pmc_json.py $OUT $SCALE
 echo done

@@ -91,6 +91,7 @@ _SIGS = {
     "capf_table_release": (c_int32, [_T]),
     "capf_table_num_columns": (c_int32, [_T, POINTER(c_int32)]),
     "capf_table_column_name": (c_int32, [_T, c_int32, POINTER(c_char_p)]),
+    "capf_table_columns": (c_int32, [_T, POINTER(c_void_p), POINTER(c_int64), POINTER(c_int32)]),
     "capf_table_column_type": (c_int32, [_T, c_char_p, POINTER(c_int32)]),
     "capf_table_size": (c_int32, [_T, POINTER(c_int64)]),
     "capf_table_download": (c_int32, [_T, c_char_p, c_void_p, c_void_p]),
@@ -166,8 +167,17 @@ def check(status):
     return status
 
 
+_FNS = {}
+
+
 def call(name, *args):
-    return check(getattr(load(), name)(*args))
+    fn = _FNS.get(name)
+    if fn is None:
+        fn = _FNS[name] = getattr(load(), name)
+    status = fn(*args)
+    if status != 0:
+        check(status)
+    return status
 
 
 def strs(values):

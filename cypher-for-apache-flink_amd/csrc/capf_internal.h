@@ -93,6 +93,9 @@ struct Column {
   BufPtr valid;  // n bytes (1 = present) or nullptr = no nulls
   mutable std::mutex mu;
   mutable std::optional<ColStats> stats;
+  // values of a tiny host-born column (a fused scalar result), kept beside
+  // the device copy so `rows` needs no device round trip
+  std::vector<int64_t> host_i64;
   bool is_all_null() const { return type == Type::Null; }
 };
 using ColPtr = std::shared_ptr<Column>;
@@ -185,6 +188,8 @@ struct Node {
   // memoised result
   std::mutex mu;
   DataPtr result;
+  // physicalColumns in one call: names joined by '\0' (built on first request)
+  std::string joined_names;
 
   int col_index(const std::string &name) const;  // -1 if absent
   int col_index_or_throw(const std::string &name) const;
@@ -256,6 +261,9 @@ struct KernelTimer {
 
 // ------------------------------------------------------------- helpers
 DataPtr materialize(const NodePtr &n);
+// One-row INTEGER column holding v (device copy written by a kernel: async,
+// no host buffer lifetime) with a host mirror.
+ColPtr scalar_i64_column(Session *s, int64_t v);
 int64_t node_size(const NodePtr &n);
 ColPtr make_column(Session *s, Type t, int64_t n, bool with_valid);
 ColPtr null_column(Session *s, Type t, int64_t n);

@@ -363,8 +363,8 @@ __device__ inline void c3_handoff(uint32_t *w, uint32_t inc, uint32_t hidx, uint
   if (k < o.cap) o.log[k] = make_uint2(hidx, side);
 }
 
-// P3 pieces per lane per step (measured at s24: 2 → 0.553, 4 → 0.536, 8 → 0.548 ms)
-constexpr int C5_PPS = 4;
+// P3 pieces per lane per step, double-buffered (s24: 2 → 0.49 ms; 4 spills → 0.66 ms)
+constexpr int C5_PPS = 2;
 
 struct C5WaveTab {
   uint32_t pre[WAVE + 1];  // exclusive prefix of the 64 tiles' piece counts, + total
@@ -372,7 +372,13 @@ struct C5WaveTab {
 };
 
 constexpr size_t C5_GATHER_LDS =
-    4 * (C2_WORDS + C5_CORR) + sizeof(C5WaveTab) * (C5_BLOCK / WAVE);
+    4 * (C2_WORDS + C5_CORR) + 2 * sizeof(C5WaveTab) * (C5_BLOCK / WAVE);
+
+__device__ inline int64_t uniform64(int64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
 
 // P3.  The wave takes 64 tiles of its unit at a time and treats their
 // segments (8-key padded, 16-B aligned pieces) as ONE sequence: lane l of
@@ -383,104 +389,183 @@ constexpr size_t C5_GATHER_LDS =
 // tools/bench_gather.hip) — and every lane holds a live piece.  Pad keys
 // (8·(t mod 8) + slot) and the keys of past-the-end lanes (= lane) are
 // counted like the others and subtracted from bins 0..63 at the flush.
-// PPS pieces per lane per step: independent searches and loads in flight.
-// MODE (diagnostics, CAPF_P3_MODE=1): loads only, keys xor-folded.
-template <int MODE, int PPS>
+//
+// Software-pipelined: the wave walks ONE stream of steps across its batches;
+// the pieces of step i+1 (search + 16-B loads, possibly in the next batch) are
+// issued before the LDS atomics of step i.  Batch tables are double-buffered
+// in LDS, the next batch's meta word is prefetched while the current table is
+// built, piece buffers ping-pong (no register copies → no early vmcnt wait).
+//
+// What bounds it (s24, measured): 0.49 ms; loads + search alone 0.29 ms; with
+// the keys spread so no two lanes of an atomic share a word (DIAG 2) 0.30 ms.
+// R-MAT's skew puts ~2.4 lanes of a typical 64-lane ds_add on one word
+// (tools: simulated per run), and same-word lanes serialise in the LDS atomic
+// unit.  Voting out lane 0's key, half-wave atomics and non-returning atomics
+// were measured and do not help (the duplicates are spread over many
+// moderately hot keys).
+template <int PPS, int DIAG = 0>
 __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
-                                                         const int32_t *nunits,
-                                                         const uint16_t *part,
-                                                         const uint32_t *meta_t, int64_t ntiles,
-                                                         int nb, int64_t rstride, uint32_t *h_in,
-                                                         uint32_t *h_out, C3Ovf ovf) {
+                                                            const int32_t *nunits,
+                                                            const uint16_t *part,
+                                                            const uint32_t *meta_t, int64_t ntiles,
+                                                            int nb, int64_t rstride, uint32_t *h_in,
+                                                            uint32_t *h_out, C3Ovf ovf) {
   const int ui = c3_unit_of((int)blockIdx.x);
   if (ui >= *nunits) return;
-  extern __shared__ __attribute__((aligned(16))) uint32_t words[];  // bins, corr, tables
+  extern __shared__ __attribute__((aligned(16))) uint32_t words[];
   constexpr int NW = C5_BLOCK / WAVE;
+  constexpr uint32_t STEP = WAVE * PPS;
   uint32_t *corr = words + C2_WORDS;
-  C5WaveTab *tabs = (C5WaveTab *)(corr + C5_CORR);
+  C5WaveTab *tabs = (C5WaveTab *)(corr + C5_CORR);  // 2 per wave
   const C3Unit u = units[ui];
   const uint32_t side = u.run >= nb ? 1u : 0u;
   uint32_t *hist = side ? h_out : h_in;
   const uint32_t hist_base = (uint32_t)(u.run % nb) * C2_BW;
   for (int i = threadIdx.x; i < C2_WORDS + C5_CORR; i += C5_BLOCK) words[i] = 0;
   __syncthreads();
-  const int wave = threadIdx.x / WAVE, lane = lane_id();
-  C5WaveTab &tab = tabs[wave];
+  // wave-uniform values live in SGPRs: uniform loop control, no exec masking
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = lane_id();
+  C5WaveTab *tab2 = tabs + 2 * wave;
   const uint4 *part4 = (const uint4 *)part;
   const uint32_t *m = meta_t + (int64_t)u.run * ntiles;
   const int64_t ut = u.t1 - u.t0;
-  const int64_t w0 = u.t0 + ut * wave / NW, w1 = u.t0 + ut * (wave + 1) / NW;
+  const int64_t w0 = uniform64(u.t0 + ut * wave / NW), w1 = uniform64(u.t0 + ut * (wave + 1) / NW);
   const uint32_t rs8 = (uint32_t)(rstride / 8);
-  uint32_t padc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // padc[e]: this lane's tiles with a pad at slot e
-  uint32_t dead = 0, fold = 0;
+  uint32_t padc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t dead = 0;
   const uint4 dead_keys = make_uint4(lane | lane << 16, lane | lane << 16, lane | lane << 16,
                                      lane | lane << 16);
-  for (int64_t tb = w0; tb < w1; tb += WAVE) {
-    // the batch's table: one tile per lane
+  // batch setup: table of tiles [tb, tb + 64) into tab2[buf]; returns the piece total
+  uint32_t wpre = w0 + lane < w1 ? m[w0 + lane] : 0u;  // meta word of the next batch
+  auto setup = [&](int64_t tb, int buf) -> uint32_t {
     const int64_t t = tb + lane;
-    const uint32_t w = t < w1 ? m[t] : 0u;
+    const uint32_t w = wpre;
     const uint32_t len = w >> 16, nq = (len + 7) >> 3, r = len & 7;
 #pragma unroll
     for (int e = 1; e < 8; ++e) padc[e] += (r != 0 && r <= (uint32_t)e) ? 1u : 0u;
     const uint32_t inc = wave_inclusive_scan(nq);
-    tab.pre[lane] = inc - nq;
-    if (lane == WAVE - 1) tab.pre[WAVE] = inc;
-    tab.qb[lane] = (uint32_t)t * rs8 + (w & 0xFFFF);
-    const uint32_t total = __shfl(inc, WAVE - 1, WAVE);
+    tab2[buf].pre[lane] = inc - nq;
+    if (lane == WAVE - 1) tab2[buf].pre[WAVE] = inc;
+    tab2[buf].qb[lane] = (uint32_t)t * rs8 + (w & 0xFFFF);
+    // prefetch the next batch's meta word only now that `w` is dead, so the
+    // load lands in the same register (no copy → no early wait)
+    __builtin_amdgcn_sched_barrier(0);
+    const int64_t tn = tb + WAVE + lane;
+    wpre = tn < w1 ? m[tn] : 0u;
     __builtin_amdgcn_wave_barrier();
-    for (uint32_t p0 = 0; p0 < total; p0 += WAVE * PPS) {
-      uint4 v[PPS];
+    return (uint32_t)__builtin_amdgcn_readfirstlane(__shfl(inc, WAVE - 1, WAVE));
+  };
+  // total > 0.  Past-the-end lanes load a valid piece (the last one) and
+  // replace it with their dead keys: every load is unconditional, so the
+  // wait before the counting only covers the step being counted.
+  auto fetch = [&](int buf, uint32_t p0, uint32_t total, uint4 *v) {
+    const C5WaveTab &tab = tab2[buf];
 #pragma unroll
-      for (int j = 0; j < PPS; ++j) {
-        const uint32_t p = p0 + j * WAVE + lane;
-        uint32_t k = 0;  // last tile k with pre[k] <= p
+    for (int j = 0; j < PPS; ++j) {
+      const uint32_t p = p0 + j * WAVE + lane;
+      const uint32_t pc = min(p, total - 1);
+      uint32_t k = 0;
 #pragma unroll
-        for (int b = WAVE / 2; b > 0; b >>= 1)
-          if (tab.pre[k + b] <= p) k += b;
-        if (p < total) {
-          v[j] = part4[tab.qb[k] + (p - tab.pre[k])];
-        } else {
-          v[j] = dead_keys;
-          ++dead;
-        }
+      for (int b = WAVE / 2; b > 0; b >>= 1)
+        if (tab.pre[k + b] <= pc) k += b;
+      v[j] = part4[tab.qb[k] + (pc - tab.pre[k])];
+    }
+  };
+  // Hub keys: R-MAT concentrates a large share of a run's keys on a few
+  // nodes, and lanes of one ds_add hitting the same word serialise.  Each
+  // atomic instruction first votes on lane 0's key: the lanes holding it are
+  // summed by one lane (popcount), the others add 1 as usual.
+  auto count = [&](const uint4 *v, uint32_t p0, uint32_t total) {
+    uint32_t acc = 0;
+    uint32_t old[PPS][8];
+#pragma unroll
+    for (int j = 0; j < PPS; ++j) {
+      const bool live = p0 + j * WAVE + lane < total;
+      dead += live ? 0u : 1u;
+      const uint32_t wd[4] = {live ? v[j].x : dead_keys.x, live ? v[j].y : dead_keys.y,
+                              live ? v[j].z : dead_keys.z, live ? v[j].w : dead_keys.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
+        if (DIAG == 2) key = (key + 131u * lane + 977u * e) & 0xFFFF;  // no same-address lanes
+        const uint32_t unit = (key >> 15) * 0xFFFFu + 1u;  // 1 (low half) or 2^16 (high)
+        old[j][e] = atomicAdd(&words[key & (C2_WORDS - 1)], unit);
+        acc |= old[j][e] + unit;
       }
+    }
+    if (DIAG == 0 && (acc & 0x80008000u)) {
+      // rare: some half reached 2^15 — find the add(s) that crossed it
 #pragma unroll
       for (int j = 0; j < PPS; ++j) {
-        const uint32_t wd[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
-        if (MODE == 1) {
-          fold ^= wd[0] ^ wd[1] ^ wd[2] ^ wd[3];
-          continue;
-        }
-        uint32_t old[8], acc = 0;
+        const bool live = p0 + j * WAVE + lane < total;
+        const uint32_t wd[4] = {live ? v[j].x : dead_keys.x, live ? v[j].y : dead_keys.y,
+                                live ? v[j].z : dead_keys.z, live ? v[j].w : dead_keys.w};
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
-          const uint32_t add = (key >> 15) * 0xFFFFu + 1u;  // 1 (low half) or 2^16 (high)
-          old[e] = atomicAdd(&words[key & (C2_WORDS - 1)], add);
-          acc |= old[e] + add;
-        }
-        if (acc & 0x80008000u) {  // some half reached 2^15: find the crossing add(s)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
-            const uint32_t sh = (key >> 15) << 4;
-            if (((old[e] >> sh) & 0xFFFFu) == 0x7FFFu)
-              c3_handoff(&words[key & (C2_WORDS - 1)], 1u << sh, hist_base + key, side, ovf);
-          }
+          const uint32_t sh = (key >> 15) << 4;
+          if (((old[j][e] >> sh) & 0xFFFFu) == 0x7FFFu)
+            c3_handoff(&words[key & (C2_WORDS - 1)], 1u << sh, hist_base + key, side, ovf);
         }
       }
     }
-    __builtin_amdgcn_wave_barrier();  // the table is rewritten by the next batch
+  };
+  if (w0 < w1) {
+    int64_t tb = uniform64(w0);
+    int buf = 0;
+    uint32_t total = setup(tb, buf), p0 = 0;
+    while (total == 0) {  // first non-empty batch
+      tb += WAVE;
+      if (tb >= w1) break;
+      buf ^= 1;
+      total = setup(tb, buf);
+    }
+    if (total) {
+      // the next step: the same batch, or the next non-empty one
+      // scalar (wave-uniform) loop state: readfirstlane keeps it in SGPRs
+      auto advance = [&]() -> bool {
+        if (p0 + STEP < total) {
+          p0 = (uint32_t)__builtin_amdgcn_readfirstlane(p0 + STEP);
+          return true;
+        }
+        do {
+          tb = uniform64(tb + WAVE);
+          if (tb >= w1) return false;
+          buf ^= 1;
+          total = setup(tb, buf);
+          p0 = 0;
+        } while (total == 0);
+        return true;
+      };
+      // ping-pong piece buffers (unrolled by 2: no register copies, so the
+      // wait before counting A covers A's loads only, not B's)
+      uint4 va[PPS], vb[PPS];
+      fetch(buf, p0, total, va);
+      for (;;) {
+        uint32_t cp0 = p0, ctot = total;
+        if (!advance()) {
+          count(va, cp0, ctot);
+          break;
+        }
+        fetch(buf, p0, total, vb);
+        count(va, cp0, ctot);
+        cp0 = p0;
+        ctot = total;
+        if (!advance()) {
+          count(vb, cp0, ctot);
+          break;
+        }
+        fetch(buf, p0, total, va);
+        count(vb, cp0, ctot);
+      }
+    }
   }
-  // corrections: this lane's tiles all have t ≡ w0 + lane (mod 8)
   const uint32_t pcls = 8u * (uint32_t)((w0 + lane) & 7);
 #pragma unroll
   for (int e = 1; e < 8; ++e)
     if (padc[e]) atomicAdd(&corr[pcls + e], padc[e]);
   if (dead) atomicAdd(&corr[lane], 8 * dead);
-  if (MODE == 1) atomicXor(&words[lane], fold);
   __syncthreads();
-  // flush: word i → bins i and i + 2^15, two coalesced streams
   for (int i = threadIdx.x; i < C2_WORDS; i += C5_BLOCK) {
     const uint32_t w = words[i];
     const uint32_t lo = (w & 0xFFFF) - (i < C5_CORR ? corr[i] : 0u), hi = w >> 16;
@@ -528,7 +613,7 @@ static void chain2_c5(Session *s, C5Cols<F32> c, bool in_range, uint32_t *h_in, 
   c.rstride = ((int64_t)2 * SH::TILE + 8 * (nr + 1) + 7) & ~int64_t(7);
   static bool attr_set = false;
   if (!attr_set) {
-    for (const void *f : {(const void *)k_c5_gather<0, C5_PPS>, (const void *)k_c5_gather<1, C5_PPS>})
+    for (const void *f : {(const void *)k_c5_gather<C5_PPS, 0>, (const void *)k_c5_gather<C5_PPS, 2>})
       HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, C5_GATHER_LDS));
     attr_set = true;
   }
@@ -575,8 +660,10 @@ static void chain2_c5(Session *s, C5Cols<F32> c, bool in_range, uint32_t *h_in, 
   }
   {
     KernelTimer kt(s, "c5_gather", 4.0 * c.n);
-    const char *md = getenv("CAPF_P3_MODE");
-    auto kern = md && atoi(md) == 1 ? k_c5_gather<1, C5_PPS> : k_c5_gather<0, C5_PPS>;
+    // CAPF_P3_DIAG=2 (diagnostics, wrong counts): keys spread so no two lanes
+    // of an atomic share a word — measures the cost of hub-key conflicts
+    const char *dg = getenv("CAPF_P3_DIAG");
+    auto kern = dg && atoi(dg) == 2 ? k_c5_gather<C5_PPS, 2> : k_c5_gather<C5_PPS, 0>;
     hipLaunchKernelGGL(kern, dim3((unsigned)max_units), dim3(C5_BLOCK), C5_GATHER_LDS, s->stream,
                        (const C3Unit *)units, (const int32_t *)nunits, (const uint16_t *)part->p,
                        (const uint32_t *)meta_t->p, c.ntiles, c.nb, c.rstride, h_in, h_out, ovf);

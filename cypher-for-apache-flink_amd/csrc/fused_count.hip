@@ -23,6 +23,7 @@
 //  * the exact 2-hop shape runs as ONE pass over the rel table
 //    (k_chain2_*): both histograms and the self-loop correction, followed by
 //    a dot product over the node range.
+#include <chrono>
 #include <algorithm>
 #include <cstring>
 #include <functional>
@@ -703,7 +704,21 @@ static bool node_weights(Session *s, const LeafData &ld, int col, NodeWeights &w
   return true;
 }
 
+// CAPF_HOST_TRACE=1: host-side timestamps of the fused count (diagnostics)
+static double host_us() {
+  return std::chrono::duration<double, std::micro>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+static bool host_trace() {
+  static const bool on = getenv("CAPF_HOST_TRACE") != nullptr;
+  return on;
+}
+static double g_trace_t0 = 0;
+
 static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t *out) {
+  const double ta = host_trace() ? host_us() : 0;
+  double tb = ta;
   LeafData rel = leaf_data(g.leaves[c.ra]);
   LeafData na = leaf_data(g.leaves[c.sa]), nb = leaf_data(g.leaves[c.sb]),
            nc = leaf_data(g.leaves[c.sc]);
@@ -758,6 +773,7 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
       const ColStats &st = column_stats(s, R.cols[col]);
       in_range = in_range && st.min >= lo && st.max <= hi;
     }
+    tb = host_trace() ? host_us() : 0;
     if (n > 0 && want_part &&
         chain2_partitioned(s, pc, n, lo, hi, in_range, h1, h2, a.loops)) {
       dot_len = chain2_hist_len(len);  // every counter written; loops accumulated on the device
@@ -785,14 +801,19 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
       KERNEL_CHECK();
     }
   }
+  const double tc = host_trace() ? host_us() : 0;
   HIP_CHECK(hipMemcpyAsync(s->h_scalars, acc->p, 16, hipMemcpyDeviceToHost, s->stream));
   s->sync();
+  if (host_trace())
+    fprintf(stderr, "[capf host] analyse %.1f us, weights+stats %.1f us, launches %.1f us, wait %.1f us\n",
+            ta - g_trace_t0, tb - ta, tc - tb, host_us() - tc);
   uint64_t total = (uint64_t)s->h_scalars[0], loops = (uint64_t)s->h_scalars[1];
   *out = total - loops;
   return true;
 }
 
 bool try_fused_count(const NodePtr &n, int64_t *out) {
+  if (host_trace()) g_trace_t0 = host_us();
   Session *s = n->s;
   {
     std::lock_guard<std::mutex> lk(n->mu);

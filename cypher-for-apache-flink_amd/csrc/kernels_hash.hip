@@ -192,6 +192,15 @@ __global__ void k_fill_i64(int64_t *p, int64_t v, int64_t n) {
     p[i] = v;
 }
 
+ColPtr scalar_i64_column(Session *s, int64_t v) {
+  ColPtr col = make_column(s, Type::Int64, 1, false);
+  hipLaunchKernelGGL(k_fill_i64, dim3(1), dim3(64), 0, s->stream, (int64_t *)col->data->p, v,
+                     (int64_t)1);
+  KERNEL_CHECK();
+  col->host_i64.assign(1, v);
+  return col;
+}
+
 Grouping group_rows(Session *s, const Data &d, const std::vector<int> &keys) {
   Grouping g;
   int64_t n = d.nrows;

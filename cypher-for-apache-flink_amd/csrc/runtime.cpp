@@ -424,12 +424,7 @@ static DataPtr materialize_impl(const NodePtr &n) {
         if (try_fused_count(n->kids[0], &cnt)) {
           auto out = std::make_shared<Data>();
           out->nrows = 1;
-          for (size_t k = 0; k < n->aggs.size(); ++k) {
-            auto col = make_column(s, Type::Int64, 1, false);
-            HIP_CHECK(hipMemcpyAsync(col->data->p, &cnt, 8, hipMemcpyHostToDevice, s->stream));
-            out->cols.push_back(col);
-          }
-          s->sync();
+          for (size_t k = 0; k < n->aggs.size(); ++k) out->cols.push_back(scalar_i64_column(s, cnt));
           return out;
         }
       }
@@ -857,6 +852,28 @@ capf_status capf_table_column_name(capf_table *t, int32_t i, const char **name) 
   CAPF_API_END
 }
 
+capf_status capf_table_columns(capf_table *t, const char **joined, int64_t *bytes, int32_t *n) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(joined, "joined");
+  need(bytes, "bytes");
+  need(n, "n");
+  Node &nd = *t->node;
+  {
+    std::lock_guard<std::mutex> lk(nd.mu);
+    if (nd.joined_names.empty() && !nd.names.empty()) {
+      for (const auto &c : nd.names) {
+        nd.joined_names += c;
+        nd.joined_names.push_back('\0');
+      }
+    }
+  }
+  *joined = nd.joined_names.data();
+  *bytes = (int64_t)nd.joined_names.size();
+  *n = (int32_t)nd.names.size();
+  CAPF_API_END
+}
+
 capf_status capf_table_column_type(capf_table *t, const char *col, int32_t *type) {
   CAPF_API_BEGIN
   need(t, "table");
@@ -882,6 +899,12 @@ capf_status capf_table_download(capf_table *t, const char *col, void *values_out
   int i = t->node->col_index_or_throw(col);
   DataPtr d = materialize(t->node);
   Session *s = t->node->s;
+  const ColPtr &hc = d->cols[i];
+  if (!hc->host_i64.empty() && (int64_t)hc->host_i64.size() == d->nrows && !hc->valid) {
+    if (values_out) memcpy(values_out, hc->host_i64.data(), 8 * d->nrows);
+    if (valid_out) memset(valid_out, 1, d->nrows);
+    return CAPF_OK;
+  }
   const ColPtr c = decode_column(s, d->cols[i]);
   size_t w = type_width(c->type);
   if (d->nrows > 0) {

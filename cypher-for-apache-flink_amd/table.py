@@ -177,14 +177,10 @@ class GpuTable:
     @property
     def physicalColumns(self):
         if self._cols is None:
-            n = c_int32()
-            _lib.call("capf_table_num_columns", self._h, byref(n))
-            cols = []
-            for i in range(n.value):
-                p = c_char_p()
-                _lib.call("capf_table_column_name", self._h, i, byref(p))
-                cols.append(p.value.decode())
-            self._cols = cols
+            p, nb, n = c_void_p(), c_int64(), c_int32()
+            _lib.call("capf_table_columns", self._h, byref(p), byref(nb), byref(n))
+            raw = ctypes.string_at(p.value, nb.value) if nb.value else b""
+            self._cols = raw.decode().split("\0")[:n.value]
         return list(self._cols)
 
     def capf_type(self, col):

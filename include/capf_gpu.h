@@ -191,6 +191,9 @@ capf_status capf_table_release(capf_table *t);
 /* physicalColumns (CypherTable.scala:48) */
 capf_status capf_table_num_columns(capf_table *t, int32_t *n);
 capf_status capf_table_column_name(capf_table *t, int32_t i, const char **name);
+/* physicalColumns in one call: *joined points at *bytes bytes holding the
+ * *n column names, each terminated by '\0' (valid while the table lives)   */
+capf_status capf_table_columns(capf_table *t, const char **joined, int64_t *bytes, int32_t *n);
 /* columnType (CypherTable.scala:58) */
 capf_status capf_table_column_type(capf_table *t, const char *col, int32_t *type);
 /* size (CypherTable.scala:68): triggers execution */

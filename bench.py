@@ -183,30 +183,55 @@ def run_single(args):
 
 
 def run_distributed(args):
-    """N ranks (torch.distributed.run), one GPU each: hash-partitioned 2-hop
-    count with one RCCL reduce-scatter of per-node counts (dist.py)."""
+    """N ranks (torch.distributed.run), one GPU each, node-partitioned graph
+    (dist.py): rank r holds the rels whose target (in-copy) and source
+    (out-copy) it owns; the 2-hop count is a local partial per rank plus ONE
+    int64 all-reduce over RCCL.  --layout edge: rels sharded by edge range,
+    per-node histograms reduce-scattered."""
     import torch
     import torch.distributed as dist
-    from capf_amd.dist import edge_range, gpu_two_hop_count, padded_nodes
+    from capf_amd.dist import (edge_range, gpu_two_hop_count, gpu_two_hop_count_sharded,
+                               node_partitioned_copies, padded_nodes)
     from capf_amd.synthetic import rmat_seed, thresholds
     from capf_amd.table import GpuSession
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RCCL prints its version banner on stdout: keep stdout for the one JSON line
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     torch.cuda.set_device(local)
     dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    s = GpuSession(local, stream=torch.cuda.current_stream().cuda_stream)
+    s = GpuSession.on_torch_stream(local)
     m = args.edge_factor << args.scale
     n_nodes = 1 << args.scale
-    lo, hi = edge_range(m, rank, world)
-    rels = s.rmat_rels(args.scale, rmat_seed(args.scale), thresholds(), lo, hi - lo)
-    if not args.int64:
-        rels = rels.compact()
-    npad = padded_nodes(n_nodes, world)
-    hists = (torch.zeros(npad, dtype=torch.int32, device="cuda"),
-             torch.zeros(npad, dtype=torch.int32, device="cuda"))
-    step = lambda: gpu_two_hop_count(s, rels, n_nodes, hists=hists)  # noqa: E731
+    if args.layout == "node":
+        # ingest (untimed): every rank generates the edge stream and keeps its two copies
+        full = s.rmat_rels(args.scale, rmat_seed(args.scale), thresholds(), 0, m)
+        in_copy, out_copy = node_partitioned_copies(full, n_nodes, world, rank, compact=not args.int64)
+        del full
+        s.sync()
+        partial = torch.zeros(1, dtype=torch.int64, device="cuda")
+        step = lambda: gpu_two_hop_count_sharded(s, in_copy, out_copy, n_nodes, partial)  # noqa: E731
+        local_rels = in_copy.size + out_copy.size
+        layout = (f"node-partitioned: rank holds the rels whose target (in-copy) / source (out-copy) it "
+                  f"owns; one int64 all-reduce per query")
+        # rank's share of the job's compulsory bytes (src+dst int64 per rel, node ids)
+        compulsory = (16.0 * m + 8.0 * n_nodes) / world
+    else:
+        lo, hi = edge_range(m, rank, world)
+        rels = s.rmat_rels(args.scale, rmat_seed(args.scale), thresholds(), lo, hi - lo)
+        if not args.int64:
+            rels = rels.compact()
+        npad = padded_nodes(n_nodes, world)
+        hists = (torch.zeros(npad, dtype=torch.int32, device="cuda"),
+                 torch.zeros(npad, dtype=torch.int32, device="cuda"))
+        step = lambda: gpu_two_hop_count(s, rels, n_nodes, hists=hists)  # noqa: E731
+        local_rels = hi - lo
+        layout = (f"edge-range shards; per-node counts reduce-scattered over RCCL, {npad * 8} B per rank")
+        compulsory = 16.0 * (hi - lo) + 8.0 * n_nodes
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -230,9 +255,10 @@ def run_distributed(args):
     torch.cuda.synchronize()
     s.set_profiling(False)
     prof = s.profile()
+    sys.stdout.flush()
+    os.dup2(json_fd, 1)
     if rank == 0:
         ms_per_step = elapsed * 1e3 / args.steps
-        compulsory = 16.0 * (hi - lo) + 8.0 * n_nodes  # rank 0's shard
         print(json.dumps({
             "metric": METRIC,
             "value": count * args.steps / elapsed,
@@ -246,13 +272,13 @@ def run_distributed(args):
             "vs_baseline": None,
             "dtype": "int64",
             "data": (f"synthetic R-MAT s{args.scale} (Graph500 a/b/c=.57/.19/.19, edge factor "
-                     f"{args.edge_factor}), each rank generates its edge shard in HBM before timing"),
+                     f"{args.edge_factor}), generated in HBM and partitioned before timing"),
             "config": {
                 "workload": f"R-MAT s{args.scale} 2-hop MATCH (a)-->(b)-->(c) RETURN count(*)",
                 "scale": args.scale, "nodes": n_nodes, "rels": m, "count": count,
+                "rank0_rel_rows": local_rels,
                 "id_storage": "int64" if args.int64 else "FOR32",
-                "parallelism": f"dp{world} (rels sharded by edge range; per-node counts reduce-scattered "
-                               f"over RCCL, {npad * 8} B per rank)",
+                "parallelism": f"dp{world} ({layout})",
             },
             "roofline": pipeline_roofline(prof, prof_steps, compulsory),
         }))
@@ -269,9 +295,12 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--int64", action="store_true", help="keep the id columns int64 (no FOR32)")
+    ap.add_argument("--dist", action="store_true", help="distributed path even at world size 1")
+    ap.add_argument("--layout", choices=["node", "edge"], default="node",
+                    help="multi-GPU graph layout (N > 1): node-partitioned copies or edge-range shards")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.gpus > 1 or world > 1:
+    if args.gpus > 1 or world > 1 or args.dist:
         run_distributed(args)
     else:
         run_single(args)

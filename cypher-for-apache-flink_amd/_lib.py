@@ -120,6 +120,9 @@ _SIGS = {
     "capf_chain2_hist_len": (c_int64, [c_int64]),
     "capf_chain2_local_hists": (c_int32, [_S, _T, c_char_p, c_char_p, c_int64, c_int64, c_void_p,
                                           c_void_p, POINTER(c_int64)]),
+    "capf_table_node_partition": (c_int32, [_T, c_char_p, c_int64, c_int64, c_int32, c_int32, _PT]),
+    "capf_chain2_sharded_count": (c_int32, [_S, _T, c_char_p, _T, c_char_p, c_char_p, c_int64, c_int64,
+                                            c_int32, c_int32, c_void_p]),
     "capf_dot_u32": (c_int32, [_S, c_void_p, c_void_p, c_int64, POINTER(c_uint64)]),
 }
 

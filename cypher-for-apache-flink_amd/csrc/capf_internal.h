@@ -336,6 +336,12 @@ bool try_fused_count(const NodePtr &n, int64_t *out);
 // in_range: the columns' statistics put every id inside [lo, hi].
 int chain2_hist_bits(int64_t len);
 int64_t chain2_hist_len(int64_t len);
+__global__ void k_partial_minus_loops(const unsigned long long *acc, int64_t *out);
+// Node-partitioned multi-GPU layout (chain2_partitioned.hip)
+uint8_t *node_owner_flags(Session *s, const ColView &key, int64_t n, int64_t lo, int64_t n_nodes,
+                          int parts, int part, BufPtr &keep);
+bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out, int64_t lo,
+                    int64_t n_nodes, int parts, int part, int64_t *d_partial);
 bool chain2_partitioned(Session *s, const ColView *cols, int64_t n, int64_t lo, int64_t hi,
                         bool in_range, uint32_t *h_in, uint32_t *h_out,
                         unsigned long long *d_loops);

@@ -231,12 +231,12 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
 constexpr int C3_TT = 256;
 __global__ __launch_bounds__(256) void k_c3_transpose(const uint32_t *meta, uint32_t *meta_t,
                                                        int64_t ntiles, int nr,
-                                                       unsigned long long *run_total) {
+                                                       unsigned long long *run_total, int64_t tt) {
   __shared__ uint32_t tilebuf[32][33];
   const int r0 = blockIdx.y * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads = 32 × 8
   unsigned int cnt[4] = {0, 0, 0, 0};                       // runs r0 + ty + 8q
-  for (int64_t t0 = (int64_t)blockIdx.x * C3_TT; t0 < min(ntiles, ((int64_t)blockIdx.x + 1) * C3_TT);
+  for (int64_t t0 = (int64_t)blockIdx.x * tt; t0 < min(ntiles, ((int64_t)blockIdx.x + 1) * tt);
        t0 += 32) {
     for (int k = ty; k < 32; k += 8) {
       const int64_t t = t0 + k;
@@ -266,9 +266,17 @@ __global__ __launch_bounds__(256) void k_c3_transpose(const uint32_t *meta, uint
 
 struct C3Unit {
   int32_t run;
-  int32_t exclusive;  // the run is this one unit → plain store
+  int32_t exclusive;  // the only unit writing (run, slice) → plain stores
   int64_t t0, t1;     // tile range
+  int32_t slice;      // histogram slice it writes
+  int32_t pad;
 };
+
+// Histogram slices: a graph with few runs (small, or one rank's share of a
+// node-partitioned graph) still needs ≳ 1.5 waves of P3 units to fill 256
+// CUs, so every run is cut into S tile ranges, each counted into its own
+// slice of the histograms with plain stores; the dot sums the slices.
+static int c5_slices(int nr) { return std::min(8, std::max(1, (384 + nr - 1) / nr)); }
 
 constexpr int C3_UBLOCK = 1024;
 
@@ -280,8 +288,13 @@ constexpr int C3_UBLOCK = 1024;
 // ranges that flush with atomic adds into bins cleared by k_c3_zero.  Units
 // stay in run order: P3 maps them onto XCDs in groups of consecutive runs
 // (c3_unit_of).
+struct C3Sides {
+  int nb;              // runs per side: runs [0, nb) in, [nb, 2·nb) out
+  int64_t t0[2], t1[2];  // tile range holding each side's segments
+};
+
 __global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(const unsigned long long *run_total,
-                                                         int nr, int64_t ntiles, C3Unit *units,
+                                                         int nr, C3Sides sd, int S, C3Unit *units,
                                                          int32_t *nunits, int32_t *split) {
   __shared__ unsigned long long lds64[17];
   __shared__ uint32_t lds32[17];
@@ -295,14 +308,14 @@ __global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(const unsigned long long
   unsigned long long total;
   block_exclusive_scan(tot, lds64, total);
   const unsigned long long target = max(2 * total / (unsigned long long)max(nr, 1), 65536ull);
-  const int64_t maxsplit = max<int64_t>(1, ntiles / 256);
   uint32_t nu[2], nsum = 0;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int r = 2 * threadIdx.x + q;
-    nu[q] = r >= nr ? 0u
-            : cnt[q] ? (uint32_t)min<int64_t>((int64_t)((cnt[q] + target - 1) / target), maxsplit)
-                     : 1u;
+    const int sdi = r >= sd.nb ? 1 : 0;
+    const int64_t maxsplit = max<int64_t>(1, (sd.t1[sdi] - sd.t0[sdi]) / 256);
+    const uint32_t hub = cnt[q] ? (uint32_t)min<int64_t>((int64_t)((cnt[q] + target - 1) / target), maxsplit) : 1u;
+    nu[q] = r >= nr ? 0u : max(hub, (uint32_t)S);
     nsum += nu[q];
   }
   uint32_t ntot;
@@ -311,26 +324,31 @@ __global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(const unsigned long long
   for (int q = 0; q < 2; ++q) {
     const int r = 2 * threadIdx.x + q;
     if (!nu[q]) continue;
+    const int sdi = r >= sd.nb ? 1 : 0;
+    const int64_t b = sd.t0[sdi], len = sd.t1[sdi] - sd.t0[sdi];
     for (uint32_t k = 0; k < nu[q]; ++k) {
       C3Unit u;
       u.run = r;
-      u.exclusive = nu[q] == 1;
-      u.t0 = cnt[q] ? ntiles * k / nu[q] : 0;
-      u.t1 = cnt[q] ? ntiles * (k + 1) / nu[q] : 0;
+      u.exclusive = nu[q] == (uint32_t)S;
+      u.t0 = cnt[q] ? b + len * k / nu[q] : b;
+      u.t1 = cnt[q] ? b + len * (k + 1) / nu[q] : b;
+      u.slice = (int32_t)(k % (uint32_t)S);
+      u.pad = 0;
       units[off + k] = u;
     }
     off += nu[q];
-    split[r] = nu[q] > 1;
+    split[r] = nu[q] > (uint32_t)S;
   }
   if (threadIdx.x == 0) *nunits = (int32_t)ntot;
 }
 
-// Clears the buckets of split runs (their units flush with atomic adds).
+// Clears every slice of the buckets of split runs (their units flush with
+// atomic adds).
 __global__ __launch_bounds__(256) void k_c3_zero(const int32_t *split, int nb, uint32_t *h_in,
-                                                  uint32_t *h_out) {
+                                                  uint32_t *h_out, int64_t slice_stride) {
   const int r = blockIdx.y;
   if (!split[r]) return;
-  uint4 *p = (uint4 *)((r >= nb ? h_out : h_in) + (int64_t)(r % nb) * C2_BW);
+  uint4 *p = (uint4 *)((r >= nb ? h_out : h_in) + blockIdx.z * slice_stride + (int64_t)(r % nb) * C2_BW);
   for (int i = blockIdx.x * 256 + threadIdx.x; i < C2_BW / 4; i += gridDim.x * 256)
     p[i] = make_uint4(0, 0, 0, 0);
 }
@@ -409,7 +427,8 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
                                                             const uint16_t *part,
                                                             const uint32_t *meta_t, int64_t ntiles,
                                                             int nb, int64_t rstride, uint32_t *h_in,
-                                                            uint32_t *h_out, C3Ovf ovf) {
+                                                            uint32_t *h_out, int64_t slice_stride,
+                                                            C3Ovf ovf) {
   const int ui = c3_unit_of((int)blockIdx.x);
   if (ui >= *nunits) return;
   extern __shared__ __attribute__((aligned(16))) uint32_t words[];
@@ -420,7 +439,7 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
   const C3Unit u = units[ui];
   const uint32_t side = u.run >= nb ? 1u : 0u;
   uint32_t *hist = side ? h_out : h_in;
-  const uint32_t hist_base = (uint32_t)(u.run % nb) * C2_BW;
+  const uint32_t hist_base = (uint32_t)(u.slice * slice_stride + (int64_t)(u.run % nb) * C2_BW);
   for (int i = threadIdx.x; i < C2_WORDS + C5_CORR; i += C5_BLOCK) words[i] = 0;
   __syncthreads();
   // wave-uniform values live in SGPRs: uniform loop control, no exec masking
@@ -605,23 +624,25 @@ static void launch_c5(Session *s, const C5Cols<F32> &c, uint16_t *part, uint32_t
   }
 }
 
-template <bool F32, class SH>
-static void chain2_c5(Session *s, C5Cols<F32> c, bool in_range, uint32_t *h_in, uint32_t *h_out,
-                      unsigned long long *d_loops) {
-  c.ntiles = (c.n + SH::TILE - 1) / SH::TILE;
-  const int nr = 2 * c.nb;
-  c.rstride = ((int64_t)2 * SH::TILE + 8 * (nr + 1) + 7) & ~int64_t(7);
+// Everything after P1: meta transpose + run totals, the work list, P3, the
+// overflow hand-offs.  `part`/`meta` hold ntiles tiles of nr = 2·sd.nb runs.
+// Histograms: S slices (c5_slices) of sd.nb·64 Ki counters per side, slice s
+// at h_in/h_out + s·slice_stride; every counter of every slice is written.
+static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, const C3Sides &sd,
+                    int64_t ntiles, int64_t rstride, int64_t nkeys, int S, uint32_t *h_in,
+                    uint32_t *h_out, int64_t slice_stride) {
+  const int nr = 2 * sd.nb;
   static bool attr_set = false;
   if (!attr_set) {
     for (const void *f : {(const void *)k_c5_gather<C5_PPS, 0>, (const void *)k_c5_gather<C5_PPS, 2>})
       HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, C5_GATHER_LDS));
     attr_set = true;
   }
-  const int max_units = (2 * nr + 1 + 255) / 256 * 256;  // runs + splits, whole XCD waves
+  // runs × slices + hub splits (≤ 2 per run beyond the slices), whole XCD waves
+  const int max_units = ((S + 2) * nr + 1 + 255) / 256 * 256;
   // every overflow event consumes 2^15 adds of one half-counter within one unit
-  const uint32_t ovf_cap = (uint32_t)(2 * c.n / (1 << 15) + 64);
-  BufPtr part = s->alloc(2 * c.rstride * c.ntiles);
-  BufPtr meta = s->alloc(4 * nr * c.ntiles), meta_t = s->alloc(4 * nr * c.ntiles);
+  const uint32_t ovf_cap = (uint32_t)(nkeys / (1 << 15) + 64);
+  BufPtr meta_t = s->alloc(4 * nr * ntiles);
   BufPtr acc = s->alloc(8 * nr + 16 + 4 * nr + sizeof(C3Unit) * max_units + 8 * (int64_t)ovf_cap);
   unsigned long long *run_total = (unsigned long long *)acc->p;
   int32_t *nunits = (int32_t *)(run_total + nr);  // [0] units, [1] overflow events
@@ -633,6 +654,93 @@ static void chain2_c5(Session *s, C5Cols<F32> c, bool in_range, uint32_t *h_in, 
   ovf.cap = ovf_cap;
   HIP_CHECK(hipMemsetAsync(acc->p, 0, 8 * nr + 16, s->stream));
   {
+    KernelTimer kt(s, "c3_transpose", 8.0 * nr * ntiles);
+    // tiles per block: 256, fewer when there are few runs (≥ ~1024 blocks)
+    int64_t tt = C3_TT;
+    while (tt > 32 && ((ntiles + tt - 1) / tt) * ((nr + 31) / 32) < 1024) tt /= 2;
+    hipLaunchKernelGGL(k_c3_transpose, dim3((unsigned)((ntiles + tt - 1) / tt), (nr + 31) / 32),
+                       dim3(256), 0, s->stream, meta, (uint32_t *)meta_t->p, ntiles, nr, run_total,
+                       tt);
+    KERNEL_CHECK();
+  }
+  {
+    KernelTimer kt(s, "c3_units", 8.0 * nr);
+    hipLaunchKernelGGL(k_c3_units, dim3(1), dim3(C3_UBLOCK), 0, s->stream,
+                       (const unsigned long long *)run_total, nr, sd, S, units, nunits, split);
+    KERNEL_CHECK();
+    hipLaunchKernelGGL(k_c3_zero, dim3(4, nr, S), dim3(256), 0, s->stream, (const int32_t *)split,
+                       sd.nb, h_in, h_out, slice_stride);
+    KERNEL_CHECK();
+  }
+  {
+    KernelTimer kt(s, "c5_gather", 2.0 * nkeys);
+    // CAPF_P3_DIAG=2 (diagnostics, wrong counts): keys spread so no two lanes
+    // of an atomic share a word — measures the cost of hub-key conflicts
+    const char *dg = getenv("CAPF_P3_DIAG");
+    auto kern = dg && atoi(dg) == 2 ? k_c5_gather<C5_PPS, 2> : k_c5_gather<C5_PPS, 0>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)max_units), dim3(C5_BLOCK), C5_GATHER_LDS, s->stream,
+                       (const C3Unit *)units, (const int32_t *)nunits, part,
+                       (const uint32_t *)meta_t->p, ntiles, sd.nb, rstride, h_in, h_out,
+                       slice_stride, ovf);
+    KERNEL_CHECK();
+  }
+  {
+    KernelTimer kt(s, "c3_overflow", 0.0);
+    hipLaunchKernelGGL(k_c3_overflow, dim3(16), dim3(256), 0, s->stream, ovf, h_in, h_out);
+    KERNEL_CHECK();
+  }
+}
+
+// out[i] = Σ_s slices[s·stride + i] for both sides (n a multiple of 4).
+__global__ __launch_bounds__(256) void k_c5_fold(const uint32_t *si, const uint32_t *so, int S,
+                                                  int64_t stride, int64_t n, uint32_t *oi,
+                                                  uint32_t *oo) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n / 4;
+       i += (int64_t)gridDim.x * 256) {
+    uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(0, 0, 0, 0);
+    for (int k = 0; k < S; ++k) {
+      const uint4 x = ((const uint4 *)(si + k * stride))[i];
+      const uint4 y = ((const uint4 *)(so + k * stride))[i];
+      a = make_uint4(a.x + x.x, a.y + x.y, a.z + x.z, a.w + x.w);
+      b = make_uint4(b.x + y.x, b.y + y.y, b.z + y.z, b.w + y.w);
+    }
+    ((uint4 *)oi)[i] = a;
+    ((uint4 *)oo)[i] = b;
+  }
+}
+
+// acc[0] += Σ_i (Σ_s in_s[i])·(Σ_s out_s[i]) (n a multiple of 4).
+__global__ __launch_bounds__(256) void k_c5_dot_slices(const uint32_t *si, const uint32_t *so,
+                                                        int S, int64_t stride, int64_t n,
+                                                        unsigned long long *acc) {
+  __shared__ unsigned long long lds[17];
+  unsigned long long t = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n / 4;
+       i += (int64_t)gridDim.x * 256) {
+    uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(0, 0, 0, 0);
+    for (int k = 0; k < S; ++k) {
+      const uint4 x = ((const uint4 *)(si + k * stride))[i];
+      const uint4 y = ((const uint4 *)(so + k * stride))[i];
+      a = make_uint4(a.x + x.x, a.y + x.y, a.z + x.z, a.w + x.w);
+      b = make_uint4(b.x + y.x, b.y + y.y, b.z + y.z, b.w + y.w);
+    }
+    t += (unsigned long long)a.x * b.x + (unsigned long long)a.y * b.y +
+         (unsigned long long)a.z * b.z + (unsigned long long)a.w * b.w;
+  }
+  unsigned long long tot;
+  block_exclusive_scan(t, lds, tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(acc, tot);
+}
+
+template <bool F32, class SH>
+static void chain2_c5(Session *s, C5Cols<F32> c, bool in_range, uint32_t *h_in, uint32_t *h_out,
+                      unsigned long long *d_loops) {
+  c.ntiles = (c.n + SH::TILE - 1) / SH::TILE;
+  const int nr = 2 * c.nb;
+  c.rstride = ((int64_t)2 * SH::TILE + 8 * (nr + 1) + 7) & ~int64_t(7);
+  BufPtr part = s->alloc(2 * c.rstride * c.ntiles);
+  BufPtr meta = s->alloc(4 * nr * c.ntiles);
+  {
     KernelTimer kt(s, "c5_partition", (F32 ? 12.0 : 20.0) * c.n);
     uint16_t *pp = (uint16_t *)part->p;
     uint32_t *mp = (uint32_t *)meta->p;
@@ -642,38 +750,259 @@ static void chain2_c5(Session *s, C5Cols<F32> c, bool in_range, uint32_t *h_in, 
     if (!alias && !in_range) launch_c5<F32, false, true, SH>(s, c, pp, mp, d_loops);
     if (!alias && in_range) launch_c5<F32, false, false, SH>(s, c, pp, mp, d_loops);
   }
-  {
-    KernelTimer kt(s, "c3_transpose", 8.0 * nr * c.ntiles);
-    hipLaunchKernelGGL(k_c3_transpose, dim3((unsigned)((c.ntiles + C3_TT - 1) / C3_TT), (nr + 31) / 32),
-                       dim3(256), 0, s->stream, (const uint32_t *)meta->p, (uint32_t *)meta_t->p,
-                       c.ntiles, nr, run_total);
+  C3Sides sd;
+  sd.nb = c.nb;
+  sd.t0[0] = sd.t0[1] = 0;
+  sd.t1[0] = sd.t1[1] = c.ntiles;
+  const int S = c5_slices(nr);
+  const int64_t hl = (int64_t)c.nb * C2_BW;
+  if (S == 1) {
+    c5_post(s, (const uint16_t *)part->p, (const uint32_t *)meta->p, sd, c.ntiles, c.rstride,
+            2 * c.n, 1, h_in, h_out, hl);
+    return;
+  }
+  BufPtr sl = s->alloc(8 * S * hl);
+  uint32_t *si = (uint32_t *)sl->p, *so = si + S * hl;
+  c5_post(s, (const uint16_t *)part->p, (const uint32_t *)meta->p, sd, c.ntiles, c.rstride,
+          2 * c.n, S, si, so, hl);
+  hipLaunchKernelGGL(k_c5_fold, dim3(grid_for(hl / 4, 256, 1024)), dim3(256), 0, s->stream, si, so,
+                     S, hl, hl, h_in, h_out);
+  KERNEL_CHECK();
+}
+
+// ------------------------------------------------------------- sharded P1
+// Node-partitioned multi-GPU layout: rank p owns the nodes
+// whose mixed index falls in its bucket range [b0, b1), and holds every rel
+// twice — the out-copy (rels whose source it owns) and the in-copy (rels whose
+// target it owns).  in[b] then comes from the in-copy's target column and
+// out[b] from the out-copy's source column, both for owned b only: the 2-hop
+// count needs no histogram exchange, only one int64 all-reduce.  One key per
+// row; tiles [0, T_in) scan the in-copy, [T_in, T_in + T_out) the out-copy
+// (whose target column is read for the self-loop term).
+struct C5Shard {
+  const void *kin, *kout, *oth;  // in-copy key, out-copy key, out-copy other endpoint
+  int64_t bin, bout, both;       // FOR32 bases (0 for plain int64 columns)
+  int64_t n_in, n_out;
+  int64_t t_in;                  // in-copy tiles
+  int64_t lo;
+  uint64_t len;
+  int b0, nbl;                   // owned buckets [b0, b0 + nbl)
+  int copies;                    // run counters per run (power of 2, see below)
+  NodeMix mix;
+};
+
+constexpr int C5S_TILE = 32768;  // rows (= keys) per tile
+constexpr int C5S_MAXR = 520;    // runs incl. the dummy: nbl ≤ 259
+constexpr int C5S_CNT = 1024;    // LDS run counters: copies · (runs + 1) ≤ 1024
+
+// A rank of a G-GPU node owns few buckets (2·32 + 1 runs at s24, G = 8): the
+// 64 lanes of a counting atomic would pile onto a handful of words.  Each run
+// then gets `copies` counters, lane l using copy l mod copies, and a run's
+// slots are the concatenation of its copies' sub-ranges.
+static int c5s_copies(int nr) {
+  int c = 1;
+  while (2 * c * (nr + 1) <= C5S_CNT && c < 8) c *= 2;
+  return c;
+}
+
+template <bool F32, bool WIDE>
+__global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_c5_shard_partition(
+    C5Shard c, uint16_t *part, uint32_t *meta, unsigned long long *loops, int64_t rstride) {
+  constexpr int TILE = C5S_TILE, MAXR = C5S_MAXR;
+  constexpr int RPT = TILE / C5_BLOCK, GROUPS = RPT / 4;
+  constexpr int STAGE = TILE + 8 * MAXR;
+  static_assert(MAXR <= C5_BLOCK, "one run per thread in the scan");
+  __shared__ uint4 stage4[STAGE / 8];
+  __shared__ uint32_t cur[C5S_CNT];
+  __shared__ uint32_t lds_scan[17];
+  uint16_t *stage = (uint16_t *)stage4;
+  const int64_t t = blockIdx.x;
+  const int side = t >= c.t_in ? 1 : 0;  // block-uniform
+  const int nr = 2 * c.nbl;
+  const int C = c.copies;
+  const uint32_t my_copy = (uint32_t)(lane_id() & (C - 1));
+  const uint32_t pb = 8u * (uint32_t)(t & 7);
+  const uint4 pad = make_uint4(pb | (pb + 1) << 16, (pb + 2) | (pb + 3) << 16,
+                               (pb + 4) | (pb + 5) << 16, (pb + 6) | (pb + 7) << 16);
+  for (int i = threadIdx.x; i < STAGE / 8; i += C5_BLOCK) stage4[i] = pad;
+  for (int i = threadIdx.x; i < C * (nr + 1); i += C5_BLOCK) cur[i] = 0;
+  __syncthreads();
+  const int64_t ts = side ? t - c.t_in : t;
+  const int64_t e0 = ts * TILE, e1 = min(e0 + TILE, side ? c.n_out : c.n_in);
+  const void *kp = side ? c.kout : c.kin;
+  const int64_t kb = side ? c.bout : c.bin;
+  const uint32_t dummy = (uint32_t)nr << C2_BITS;
+  const uint32_t run0 = (uint32_t)(side * c.nbl);
+  uint32_t key[RPT];
+  uint32_t lp = 0;
+#pragma unroll
+  for (int g = 0; g < GROUPS; ++g) {
+    const int64_t e = e0 + 4 * ((int64_t)g * C5_BLOCK + threadIdx.x);
+    uint32_t x[4], y[4];
+    bool okx[4], oky[4];
+    c5_load4<F32, true>(kp, kb, c.lo, c.len, e, e1, true, x, okx);
+    if (side) c5_load4<F32, true>(c.oth, c.both, c.lo, c.len, e, e1, true, y, oky);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t h = node_mix_t<WIDE>(x[k], c.mix);
+      const uint32_t b = (h >> C2_BITS) - (uint32_t)c.b0;  // wraps when below b0
+      const bool ok = okx[k] && b < (uint32_t)c.nbl;
+      key[4 * g + k] = ok ? ((b + run0) << C2_BITS) | (h & 0xFFFF) : dummy;
+      if (side) lp += (ok && oky[k] && x[k] == y[k]) ? 1u : 0u;
+      atomicAdd(&cur[(key[4 * g + k] >> C2_BITS) * C + my_copy], 1u);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) asm volatile("" : "+v"(key[j]));
+  __syncthreads();
+  // exclusive scan of the 8-padded run sizes, one run per thread (dummy last)
+  const int r = threadIdx.x;
+  uint32_t cnt = 0;
+  if (r <= nr)
+    for (int k = 0; k < C; ++k) cnt += cur[r * C + k];
+  uint32_t total;
+  const uint32_t ex = block_exclusive_scan((cnt + 7) & ~7u, lds_scan, total);
+  if (r <= nr) {
+    uint32_t o = ex;
+    for (int k = 0; k < C; ++k) {
+      const uint32_t v = cur[r * C + k];
+      cur[r * C + k] = o;
+      o += v;
+    }
+  }
+  if (r < nr) meta[t * nr + r] = (ex >> 3) | (cnt << 16);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    stage[atomicAdd(&cur[(key[j] >> C2_BITS) * C + my_copy], 1u)] = (uint16_t)key[j];
+    if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+  }
+  __syncthreads();
+  uint4 *dst = (uint4 *)(part + t * rstride);
+  for (uint32_t i = threadIdx.x; i < total / 8; i += C5_BLOCK) dst[i] = stage4[i];
+  unsigned long long lp64 = wave_reduce_sum((unsigned long long)lp);
+  if (lane_id() == 0 && lp64) atomicAdd(loops, lp64);
+}
+
+// Buckets of 64 Ki mixed node indexes owned by `part` of `parts`.
+static void owned_buckets(int kbits, int parts, int part, int *b0, int *nbl) {
+  const int64_t nb = (int64_t(1) << kbits) / C2_BW;
+  const int64_t lo = nb * part / parts, hi = nb * (part + 1) / parts;
+  *b0 = (int)lo;
+  *nbl = (int)(hi - lo);
+}
+
+int node_owner_bits(int64_t n_nodes) { return chain2_hist_bits(n_nodes); }
+
+// Owner rank of node offset x (id − lo): the bucket of its mixed index.
+__device__ inline int owner_of(uint32_t x, NodeMix mix, bool wide, int64_t nb, int parts) {
+  const uint32_t h = wide ? node_mix_t<true>(x, mix) : node_mix_t<false>(x, mix);
+  const int64_t b = h >> C2_BITS;
+  // smallest p with b < nb·(p+1)/parts
+  int p = (int)((b * parts) / nb);
+  while (p > 0 && b < nb * p / parts) --p;
+  while (p + 1 < parts && b >= nb * (p + 1) / parts) ++p;
+  return p;
+}
+
+__global__ void k_owner_flags(ColView key, int64_t n, int64_t lo, NodeMix mix, int wide,
+                              int64_t nb, int parts, int part, uint8_t *flags) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t v = ld_int(key, i);
+    flags[i] = owner_of((uint32_t)(v - lo), mix, wide != 0, nb, parts) == part;
+  }
+}
+
+uint8_t *node_owner_flags(Session *s, const ColView &key, int64_t n, int64_t lo, int64_t n_nodes,
+                          int parts, int part, BufPtr &keep) {
+  const int kbits = chain2_hist_bits(n_nodes);
+  keep = s->alloc(std::max<int64_t>(n, 1));
+  if (n > 0) {
+    hipLaunchKernelGGL(k_owner_flags, dim3(grid_for(n, 256)), dim3(256), 0, s->stream, key, n, lo,
+                       node_mix_for(kbits), (int)(kbits > 24), (int64_t(1) << kbits) / C2_BW,
+                       parts, part, (uint8_t *)keep->p);
     KERNEL_CHECK();
   }
-  {
-    KernelTimer kt(s, "c3_units", 8.0 * nr);
-    hipLaunchKernelGGL(k_c3_units, dim3(1), dim3(C3_UBLOCK), 0, s->stream,
-                       (const unsigned long long *)run_total, nr, c.ntiles, units, nunits, split);
-    KERNEL_CHECK();
-    hipLaunchKernelGGL(k_c3_zero, dim3(4, nr), dim3(256), 0, s->stream, (const int32_t *)split,
-                       c.nb, h_in, h_out);
-    KERNEL_CHECK();
+  return (uint8_t *)keep->p;
+}
+
+// Local 2-hop partial of `part`: Σ_{owned b} in[b]·out[b] − owned self-loops
+// into *d_partial (device, int64) — asynchronous on the session stream.
+// cols = {in-copy target, out-copy source, out-copy target}; all plain or all
+// FOR32, 16-B aligned, non-null.  Histograms live in session scratch.
+bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out, int64_t lo,
+                    int64_t n_nodes, int parts, int part, int64_t *d_partial) {
+  const int kbits = chain2_hist_bits(n_nodes);
+  int b0, nbl;
+  owned_buckets(kbits, parts, part, &b0, &nbl);
+  if (2 * nbl + 1 > C5S_MAXR) return false;
+  if (n_in >= (int64_t(1) << 31) || n_out >= (int64_t(1) << 31)) return false;
+  int nf = 0;
+  for (int i = 0; i < 3; ++i) {
+    if (cols[i].valid || (!cols[i].data && (i == 0 ? n_in : n_out) > 0)) return false;
+    if ((uintptr_t)cols[i].data & 15) return false;
+    nf += cols[i].enc == ENC_FOR32;
   }
-  {
-    KernelTimer kt(s, "c5_gather", 4.0 * c.n);
-    // CAPF_P3_DIAG=2 (diagnostics, wrong counts): keys spread so no two lanes
-    // of an atomic share a word — measures the cost of hub-key conflicts
-    const char *dg = getenv("CAPF_P3_DIAG");
-    auto kern = dg && atoi(dg) == 2 ? k_c5_gather<C5_PPS, 2> : k_c5_gather<C5_PPS, 0>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)max_units), dim3(C5_BLOCK), C5_GATHER_LDS, s->stream,
-                       (const C3Unit *)units, (const int32_t *)nunits, (const uint16_t *)part->p,
-                       (const uint32_t *)meta_t->p, c.ntiles, c.nb, c.rstride, h_in, h_out, ovf);
-    KERNEL_CHECK();
+  if (nf != 0 && nf != 3) return false;
+  BufPtr acc = s->alloc(16);
+  HIP_CHECK(hipMemsetAsync(acc->p, 0, 16, s->stream));
+  unsigned long long *d_acc = (unsigned long long *)acc->p;  // [0] Σ in·out, [1] loops
+  if (nbl > 0) {
+    C5Shard c;
+    c.kin = cols[0].data;
+    c.kout = cols[1].data;
+    c.oth = cols[2].data;
+    c.bin = nf ? cols[0].base : 0;
+    c.bout = nf ? cols[1].base : 0;
+    c.both = nf ? cols[2].base : 0;
+    c.n_in = n_in;
+    c.n_out = n_out;
+    c.t_in = (n_in + C5S_TILE - 1) / C5S_TILE;
+    const int64_t t_out = (n_out + C5S_TILE - 1) / C5S_TILE;
+    const int64_t ntiles = c.t_in + t_out;
+    c.lo = lo;
+    c.len = (uint64_t)n_nodes;
+    c.b0 = b0;
+    c.nbl = nbl;
+    c.mix = node_mix_for(kbits);
+    const int nr = 2 * nbl;
+    c.copies = c5s_copies(nr);
+    const int64_t rstride = ((int64_t)C5S_TILE + 8 * (nr + 1) + 7) & ~int64_t(7);
+    if (ntiles > 0) {
+      BufPtr partb = s->alloc(2 * rstride * ntiles);
+      BufPtr meta = s->alloc(4 * nr * ntiles);
+      {
+        KernelTimer kt(s, "c5_partition", (nf ? 4.0 : 8.0) * (n_in + 2 * n_out));
+        auto kern = nf ? (kbits > 24 ? k_c5_shard_partition<true, true> : k_c5_shard_partition<true, false>)
+                       : (kbits > 24 ? k_c5_shard_partition<false, true> : k_c5_shard_partition<false, false>);
+        hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(C5_BLOCK), 0, s->stream, c,
+                           (uint16_t *)partb->p, (uint32_t *)meta->p, d_acc + 1, rstride);
+        KERNEL_CHECK();
+      }
+      C3Sides sd;
+      sd.nb = nbl;
+      sd.t0[0] = 0;
+      sd.t1[0] = c.t_in;
+      sd.t0[1] = c.t_in;
+      sd.t1[1] = ntiles;
+      const int S = c5_slices(nr);
+      const int64_t hl = (int64_t)nbl * C2_BW;
+      BufPtr sl = s->alloc(8 * S * hl);
+      uint32_t *si = (uint32_t *)sl->p, *so = si + S * hl;
+      c5_post(s, (const uint16_t *)partb->p, (const uint32_t *)meta->p, sd, ntiles, rstride,
+              n_in + n_out, S, si, so, hl);
+      KernelTimer kt(s, "chain2_dot", 8.0 * S * hl);
+      hipLaunchKernelGGL(k_c5_dot_slices, dim3(grid_for(hl / 4, 256, 1024)), dim3(256), 0,
+                         s->stream, si, so, S, hl, hl, d_acc);
+      KERNEL_CHECK();
+    }
   }
-  {
-    KernelTimer kt(s, "c3_overflow", 0.0);
-    hipLaunchKernelGGL(k_c3_overflow, dim3(16), dim3(256), 0, s->stream, ovf, h_in, h_out);
-    KERNEL_CHECK();
-  }
+  hipLaunchKernelGGL(k_partial_minus_loops, dim3(1), dim3(64), 0, s->stream,
+                     (const unsigned long long *)d_acc, d_partial);
+  KERNEL_CHECK();
+  return true;
 }
 
 int chain2_hist_bits(int64_t len) {

@@ -812,6 +812,10 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
   return true;
 }
 
+__global__ void k_partial_minus_loops(const unsigned long long *acc, int64_t *out) {
+  if (threadIdx.x == 0) *out = (int64_t)(acc[0] - acc[1]);
+}
+
 bool try_fused_count(const NodePtr &n, int64_t *out) {
   if (host_trace()) g_trace_t0 = host_us();
   Session *s = n->s;
@@ -913,6 +917,35 @@ extern "C" capf_status capf_chain2_local_hists(capf_session *cs, capf_table *rel
     HIP_CHECK(hipMemcpyAsync(s->h_scalars, acc->p, 16, hipMemcpyDeviceToHost, s->stream));
     s->sync();
     *self_loops = s->h_scalars[1];
+    return CAPF_OK;
+  } catch (const capf::Error &e) {
+    return record_error(e.code, e.what());
+  }
+}
+
+extern "C" capf_status capf_chain2_sharded_count(capf_session *cs, capf_table *in_copy,
+                                                 const char *in_dst, capf_table *out_copy,
+                                                 const char *out_src, const char *out_dst,
+                                                 int64_t node_base, int64_t n_nodes,
+                                                 int32_t parts, int32_t part, int64_t *d_partial) {
+  try {
+    if (!cs || !in_copy || !out_copy || !in_dst || !out_src || !out_dst || !d_partial)
+      illegal("null argument");
+    if (n_nodes <= 0 || n_nodes > (int64_t(1) << 31)) illegal("node count out of range");
+    if (parts <= 0 || part < 0 || part >= parts) illegal("part out of range");
+    Session *s = &cs->impl;
+    DataPtr di = materialize(in_copy->node), dout = materialize(out_copy->node);
+    const ColPtr &a = di->cols[in_copy->node->col_index_or_throw(in_dst)];
+    const ColPtr &b = dout->cols[out_copy->node->col_index_or_throw(out_src)];
+    const ColPtr &c = dout->cols[out_copy->node->col_index_or_throw(out_dst)];
+    for (const ColPtr *x : {&a, &b, &c})
+      if ((*x)->type != Type::Int64 || (*x)->valid)
+        illegal("sharded 2-hop count needs non-null INTEGER endpoint columns");
+    const ColView cols[3] = {view_of(a), view_of(b), view_of(c)};
+    if (!chain2_sharded(s, cols, di->nrows, dout->nrows, node_base, n_nodes, parts, part,
+                        d_partial))
+      not_impl("sharded 2-hop count: shape outside the kernel's limits (buckets per rank, "
+               "rows per copy < 2^31, mixed encodings)");
     return CAPF_OK;
   } catch (const capf::Error &e) {
     return record_error(e.code, e.what());

@@ -808,6 +808,38 @@ capf_status capf_table_compact(capf_table *t, capf_table **out) {
   CAPF_API_END
 }
 
+capf_status capf_table_node_partition(capf_table *t, const char *key_col, int64_t node_base,
+                                      int64_t n_nodes, int32_t parts, int32_t part,
+                                      capf_table **out) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(key_col, "key_col");
+  need(out, "out");
+  if (n_nodes <= 0 || n_nodes > (int64_t(1) << 31)) illegal("node count out of range");
+  if (parts <= 0 || part < 0 || part >= parts) illegal("part out of range");
+  const int ki = t->node->col_index_or_throw(key_col);
+  if (t->node->types[ki] != Type::Int64) illegal("partition key must be an INTEGER column");
+  DataPtr d = materialize(t->node);
+  Session *s = t->node->s;
+  const ColPtr &kc = d->cols[ki];
+  if (kc->valid) illegal("partition key must be non-null");
+  BufPtr flags;
+  const uint8_t *f = node_owner_flags(s, view_of(kc), d->nrows, node_base, n_nodes, parts, part, flags);
+  int64_t m = 0;
+  BufPtr idx = compact_flags(s, f, d->nrows, &m);
+  auto n = new_node(s, Kind::Source);
+  n->names = t->node->names;
+  n->types = t->node->types;
+  auto e = std::make_shared<Data>();
+  e->nrows = m;
+  for (const ColPtr &c : d->cols)
+    e->cols.push_back(gather_column(s, decode_column(s, c), (const int64_t *)idx->p, m));
+  s->sync();
+  n->result = e;
+  *out = wrap(n);
+  CAPF_API_END
+}
+
 capf_status capf_table_column_encoding(capf_table *t, const char *col, int32_t *enc,
                                        int64_t *base) {
   CAPF_API_BEGIN

@@ -1,5 +1,19 @@
 """One process per GPU: the hash-partitioned 2-hop count over RCCL.
 
+Two layouts are implemented.
+
+NODE-PARTITIONED (default, `node_partitioned_copies` + `gpu_two_hop_count_sharded`):
+SURVEY §8(e) stores each rel on owner(src) and, for incoming expansion, a copy
+on owner(dst), with owner(v) = the rank holding mix(v)'s bucket.  Rank r then
+holds every rel that ends at one of its nodes (in-copy) and every rel that
+starts at one (out-copy): in[b] and out[b] for its own b are both local, the
+count-only frontier never leaves the GPU, and the only collective is ONE int64
+all-reduce of the per-rank partials Σ_{b owned} in[b]·out[b] − owned self-loops.
+
+EDGE-RANGE (below): rels sharded by edge index, per-node histograms
+reduce-scattered (2·N·4 B per rank).  Kept as the layout for graphs stored
+without the in-copy.
+
 SURVEY §8(e): the graph is partitioned over G GPUs and the 2-hop join needs
 one exchange keyed by the middle node b.  Because the fused count only needs
 per-node path multiplicities (the "count-only frontier"), the exchange is
@@ -80,3 +94,28 @@ def gpu_two_hop_count(session, rels, n_nodes, node_base=0, group=None, hists=Non
         out_h[hlen:].zero_()
     return combine_two_hop(in_h, out_h, loops,
                            lambda a, b: dot_u32(session, a.data_ptr(), b.data_ptr(), a.numel()), group)
+
+
+def node_partitioned_copies(rels, n_nodes, world, rank, node_base=0, src="source", dst="target",
+                            compact=True):
+    """(in_copy, out_copy) of this rank: the rels whose target / source node it
+    owns (FOR32-compacted unless compact=False).  Graph-ingest step, outside
+    the timed query."""
+    out_copy = rels.node_partition(src, node_base, n_nodes, world, rank)
+    in_copy = rels.node_partition(dst, node_base, n_nodes, world, rank)
+    if compact:
+        out_copy, in_copy = out_copy.compact(), in_copy.compact()
+    return in_copy, out_copy
+
+
+def gpu_two_hop_count_sharded(session, in_copy, out_copy, n_nodes, partial, node_base=0, group=None):
+    """Distributed 2-hop count(*) over the node-partitioned copies: the local
+    partial is enqueued on the session stream (= torch's current stream) into
+    the int64 device tensor `partial`, then ONE all-reduce (RCCL) sums it."""
+    from .table import chain2_sharded_count_async
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    chain2_sharded_count_async(session, in_copy, out_copy, node_base, n_nodes, world, rank,
+                               partial.data_ptr())
+    dist.all_reduce(partial, op=dist.ReduceOp.SUM, group=group)
+    return int(partial.item())

@@ -36,6 +36,19 @@ class GpuSession:
         self._strings = {}
         self._codes = {}
 
+    @classmethod
+    def on_torch_stream(cls, device=0):
+        """Session whose work is ordered with torch's: a dedicated torch stream
+        becomes torch's current stream and the session's (torch's default
+        stream is the legacy null stream, which a non-blocking session stream
+        would NOT be ordered with — collectives and .item() would race)."""
+        import torch
+        st = torch.cuda.Stream(device=device)
+        torch.cuda.set_stream(st)
+        s = cls(device, stream=c_void_p(st.cuda_stream))
+        s.torch_stream = st  # keep it alive
+        return s
+
     def close(self):
         if getattr(self, "_h", None):
             _lib.load().capf_session_destroy(self._h)
@@ -323,11 +336,24 @@ class GpuTable:
         _lib.call("capf_table_show", self._h, int(rows))
 
     # ---------------------------------------------------------- multi-GPU helpers
+    def node_partition(self, key_col, node_base, n_nodes, parts, part):
+        """Rows whose key_col node is owned by `part` of `parts` (Multi-GPU)."""
+        return self._new("capf_table_node_partition", self._h, key_col.encode(), int(node_base),
+                         int(n_nodes), int(parts), int(part))
+
     def chain2_local_hists(self, src_col, dst_col, node_base, n_nodes, d_in, d_out):
         loops = c_int64()
         _lib.call("capf_chain2_local_hists", self.session._h, self._h, src_col.encode(), dst_col.encode(),
                   int(node_base), int(n_nodes), c_void_p(d_in), c_void_p(d_out), byref(loops))
         return loops.value
+
+
+def chain2_sharded_count_async(session, in_copy, out_copy, node_base, n_nodes, parts, part,
+                               d_partial, src="source", dst="target"):
+    """Enqueue this rank's 2-hop partial (int64 at device address d_partial)."""
+    _lib.call("capf_chain2_sharded_count", session._h, in_copy._h, dst.encode(), out_copy._h,
+              src.encode(), dst.encode(), int(node_base), int(n_nodes), int(parts), int(part),
+              c_void_p(d_partial))
 
 
 def chain2_hist_len(n_nodes):

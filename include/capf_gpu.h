@@ -290,6 +290,24 @@ capf_status capf_range_node_table(capf_session *s, int64_t base, int64_t n, uint
  * (odd multiply, xorshift; csrc/device_common.h node_mix) the radix
  * partitioning hashes by, so a contiguous 1/G slice of the histogram index
  * is a hash partition of the nodes.                                         */
+/* Node-partitioned layout (SURVEY §8(e) "each rel is stored on owner(src);
+ * for incoming expansion also a copy on owner(dst)"): owner(v) = the rank
+ * whose contiguous range of 64 Ki-index buckets holds mix(v - node_base).
+ * capf_table_node_partition: the rows of t whose key_col is owned by `part`
+ * of `parts` (the out-copy with key = source, the in-copy with key = target).
+ * capf_chain2_sharded_count: this rank's partial of the 2-hop count,
+ *   Σ_{b owned} in[b]·out[b] − owned self-loops,
+ * in[b] from the in-copy's target column, out[b] from the out-copy's source
+ * column (its target column gives the self-loops).  Asynchronous on the
+ * session stream; writes the int64 partial to device memory d_partial, ready
+ * for one all-reduce (sum) over ranks.  Histograms are session scratch.      */
+capf_status capf_table_node_partition(capf_table *t, const char *key_col, int64_t node_base,
+                                      int64_t n_nodes, int32_t parts, int32_t part,
+                                      capf_table **out);
+capf_status capf_chain2_sharded_count(capf_session *s, capf_table *in_copy, const char *in_dst,
+                                      capf_table *out_copy, const char *out_src,
+                                      const char *out_dst, int64_t node_base, int64_t n_nodes,
+                                      int32_t parts, int32_t part, int64_t *d_partial);
 int64_t capf_chain2_hist_len(int64_t n_nodes);
 capf_status capf_chain2_local_hists(capf_session *s, capf_table *rels, const char *src_col,
                                     const char *dst_col, int64_t node_base, int64_t n_nodes,

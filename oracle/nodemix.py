@@ -21,3 +21,14 @@ def node_mix(x, k):
     mask = np.uint64((1 << k) - 1)
     h = (x * np.uint64(A)) & mask
     return (h ^ (h >> np.uint64(k // 2))).astype(np.int64)
+
+
+def owner(x, n_nodes, parts):
+    """Owner rank of node offsets x under the node-partitioned layout
+    (csrc/chain2_partitioned.hip owned_buckets/owner_of): rank p owns the
+    64 Ki-index buckets [nb·p/parts, nb·(p+1)/parts) of mix(x)."""
+    k = hist_bits(n_nodes)
+    nb = (1 << k) >> 16
+    b = node_mix(x, k) >> 16
+    bounds = np.array([nb * p // parts for p in range(parts + 1)], dtype=np.int64)
+    return np.searchsorted(bounds, b, side="right") - 1

@@ -59,3 +59,47 @@ def test_distributed_two_hop_combine(world):
     src, dst = cmodel.rmat(scale)
     expect = cmodel.count_2hop(src, dst, 1 << scale)
     assert all(v == expect for v in res.values()), (res, expect)
+
+
+def _sharded_worker(rank, world, port, scale, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import capf_import  # noqa: F401
+    from oracle import cmodel, nodemix
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 1 << scale
+    src, dst = cmodel.rmat(scale)
+    # this rank's copies (capf_table_node_partition): rels it owns the target / source of
+    in_dst = dst[nodemix.owner(dst, n, world) == rank]
+    out_mask = nodemix.owner(src, n, world) == rank
+    out_src, out_dst = src[out_mask], dst[out_mask]
+    ein = np.bincount(in_dst, minlength=n).astype(np.int64)
+    eout = np.bincount(out_src, minlength=n).astype(np.int64)
+    partial = int((ein * eout).sum()) - int((out_src == out_dst).sum())
+    t = torch.tensor([partial], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)  # the one collective of the sharded count
+    q.put((rank, int(t.item())))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_node_partitioned_two_hop(world):
+    """Node-partitioned layout (dist.gpu_two_hop_count_sharded): per-rank
+    partials over the owned nodes, one int64 all-reduce, equal the closed form."""
+    scale = 18  # 4 buckets of 64 Ki: uneven bucket ranges at world 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, scale, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    import capf_import  # noqa: F401
+    from oracle import cmodel
+    src, dst = cmodel.rmat(scale)
+    expect = cmodel.count_2hop(src, dst, 1 << scale)
+    assert all(v == expect for v in res.values()), (res, expect)

@@ -367,3 +367,43 @@ def test_two_hop_hub_overflow(gpu_session, monkeypatch, n, compact):
     got = run(g, TWO_HOP)[0]["count"]
     assert gpu_session.last_plan() == "fused_chain2"
     assert got == cmodel.count_2hop(src.astype(np.int64), dst.astype(np.int64), n)
+
+
+@pytest.mark.parametrize("compact", [False, True], ids=["int64", "for32"])
+@pytest.mark.parametrize("scale,parts", [(10, 2), (16, 1), (16, 3), (18, 4), (18, 3)])
+def test_sharded_two_hop_partials(gpu_session, compact, scale, parts):
+    """Node-partitioned layout (dist.py): every part's in/out copies hold
+    exactly the rels whose target/source it owns, each part's on-device
+    partial Σ_{owned b} in·out − owned loops equals the oracle's, and the
+    partials sum to the closed-form 2-hop count (what the all-reduce forms)."""
+    import torch
+    from capf_amd.dist import node_partitioned_copies
+    from capf_amd.table import chain2_sharded_count_async
+    from oracle import nodemix
+    m = 16 << scale
+    n = 1 << scale
+    t = gpu_session.rmat_rels(scale, cmodel.rmat_seed(scale), cmodel.thresholds(), 0, m)
+    if not compact:
+        t = t.select("id", "source", "target")
+    src, dst = cmodel.rmat(scale)
+    own_s = nodemix.owner(src, n, parts)
+    own_d = nodemix.owner(dst, n, parts)
+    total = 0
+    for p in range(parts):
+        in_copy, out_copy = node_partitioned_copies(t, n, parts, p)
+        if not compact:  # keep the copies int64 (node_partitioned_copies compacts)
+            in_copy = t.node_partition("target", 0, n, parts, p)
+            out_copy = t.node_partition("source", 0, n, parts, p)
+        assert in_copy.size == int((own_d == p).sum())
+        assert out_copy.size == int((own_s == p).sum())
+        assert sorted(out_copy.column_arrays("id")[0].tolist()) == np.nonzero(own_s == p)[0].tolist()
+        part = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+        chain2_sharded_count_async(gpu_session, in_copy, out_copy, 0, n, parts, p, part.data_ptr())
+        gpu_session.sync()
+        ein = np.bincount(dst[own_d == p], minlength=n).astype(np.int64)
+        eout = np.bincount(src[own_s == p], minlength=n).astype(np.int64)
+        loops = int(((src == dst) & (own_s == p)).sum())
+        expect = int((ein * eout).sum()) - loops
+        assert int(part.item()) == expect, (p, int(part.item()), expect)
+        total += expect
+    assert total == cmodel.count_2hop(src, dst, n)

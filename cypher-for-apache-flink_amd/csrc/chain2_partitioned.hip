@@ -154,14 +154,36 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   const uint32_t dummy = (uint32_t)nr << C2_BITS;
   uint32_t kin[RPT], kout[RPT];
   uint32_t lp = 0;
+  // ALIAS: the next group's two loads are issued before this group's hashing
+  // and counting (double-buffered registers; the unrolled loop renames them)
+  uint32_t px[2][4], py[2][4];
+  bool pox[2][4], poy[2][4];
+  if (ALIAS) {
+    const int64_t e = e0 + 4 * (int64_t)threadIdx.x;
+    c5_load4<F32, CHECK>(c.u1, c.bu1, c.lo, c.len, e, e1, RAGGED, px[0], pox[0]);
+    c5_load4<F32, CHECK>(c.v1, c.bv1, c.lo, c.len, e, e1, RAGGED, py[0], poy[0]);
+  }
 #pragma unroll
   for (int g = 0; g < GROUPS; ++g) {
     const int64_t e = e0 + 4 * ((int64_t)g * C5_BLOCK + threadIdx.x);
     uint32_t x1[4], y1[4], x2[4], y2[4];
     bool okx1[4], oky1[4], okx2[4], oky2[4];
-    c5_load4<F32, CHECK>(c.u1, c.bu1, c.lo, c.len, e, e1, RAGGED, x1, okx1);
-    c5_load4<F32, CHECK>(c.v1, c.bv1, c.lo, c.len, e, e1, RAGGED, y1, oky1);
-    if (!ALIAS) {
+    if (ALIAS) {
+      if (g + 1 < GROUPS) {
+        const int64_t en = e + 4 * C5_BLOCK;
+        c5_load4<F32, CHECK>(c.u1, c.bu1, c.lo, c.len, en, e1, RAGGED, px[(g + 1) & 1], pox[(g + 1) & 1]);
+        c5_load4<F32, CHECK>(c.v1, c.bv1, c.lo, c.len, en, e1, RAGGED, py[(g + 1) & 1], poy[(g + 1) & 1]);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        x1[k] = px[g & 1][k];
+        y1[k] = py[g & 1][k];
+        okx1[k] = pox[g & 1][k];
+        oky1[k] = poy[g & 1][k];
+      }
+    } else {
+      c5_load4<F32, CHECK>(c.u1, c.bu1, c.lo, c.len, e, e1, RAGGED, x1, okx1);
+      c5_load4<F32, CHECK>(c.v1, c.bv1, c.lo, c.len, e, e1, RAGGED, y1, oky1);
       c5_load4<F32, CHECK>(c.u2, c.bu2, c.lo, c.len, e, e1, RAGGED, x2, okx2);
       c5_load4<F32, CHECK>(c.v2, c.bv2, c.lo, c.len, e, e1, RAGGED, y2, oky2);
     }
@@ -273,10 +295,9 @@ struct C3Unit {
 };
 
 // Histogram slices: a graph with few runs (small, or one rank's share of a
-// node-partitioned graph) still needs ≳ 1.5 waves of P3 units to fill 256
-// CUs, so every run is cut into S tile ranges, each counted into its own
+// node-partitioned graph) still needs 2 full waves of P3 units on 256 CUs, so every run is cut into S tile ranges, each counted into its own
 // slice of the histograms with plain stores; the dot sums the slices.
-static int c5_slices(int nr) { return std::min(8, std::max(1, (384 + nr - 1) / nr)); }
+static int c5_slices(int nr) { return std::min(8, std::max(1, (512 + nr - 1) / nr)); }
 
 constexpr int C3_UBLOCK = 1024;
 
@@ -788,10 +809,11 @@ struct C5Shard {
   uint64_t len;
   int b0, nbl;                   // owned buckets [b0, b0 + nbl)
   int copies;                    // run counters per run (power of 2, see below)
+  int gpt;                       // 4096-row groups per tile (≤ 4): tile = 4096·gpt rows
   NodeMix mix;
 };
 
-constexpr int C5S_TILE = 32768;  // rows (= keys) per tile
+constexpr int C5S_TILE = 16384;  // rows (= keys) per tile (at most)
 constexpr int C5S_MAXR = 520;    // runs incl. the dummy: nbl ≤ 259
 constexpr int C5S_CNT = 1024;    // LDS run counters: copies · (runs + 1) ≤ 1024
 
@@ -815,6 +837,7 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   __shared__ uint4 stage4[STAGE / 8];
   __shared__ uint32_t cur[C5S_CNT];
   __shared__ uint32_t lds_scan[17];
+  __shared__ uint32_t body_end;
   uint16_t *stage = (uint16_t *)stage4;
   const int64_t t = blockIdx.x;
   const int side = t >= c.t_in ? 1 : 0;  // block-uniform
@@ -828,28 +851,52 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   for (int i = threadIdx.x; i < C * (nr + 1); i += C5_BLOCK) cur[i] = 0;
   __syncthreads();
   const int64_t ts = side ? t - c.t_in : t;
-  const int64_t e0 = ts * TILE, e1 = min(e0 + TILE, side ? c.n_out : c.n_in);
+  const int64_t rows = (int64_t)c.gpt * 4 * C5_BLOCK;
+  const int64_t e0 = ts * rows, e1 = min(e0 + rows, side ? c.n_out : c.n_in);
+  // groups holding rows of this tile (uniform): later groups are skipped, so a
+  // short tile never floods the dummy run's counter
+  const int gu = (int)min<int64_t>(c.gpt, (e1 - e0 + 4 * C5_BLOCK - 1) / (4 * C5_BLOCK));
   const void *kp = side ? c.kout : c.kin;
   const int64_t kb = side ? c.bout : c.bin;
   const uint32_t dummy = (uint32_t)nr << C2_BITS;
   const uint32_t run0 = (uint32_t)(side * c.nbl);
   uint32_t key[RPT];
   uint32_t lp = 0;
+  // the next group's loads are issued before this group's hashing/counting
+  uint32_t px[2][4], py[2][4];
+  bool pox[2][4], poy[2][4];
+  {
+    const int64_t e = e0 + 4 * (int64_t)threadIdx.x;
+    c5_load4<F32, true>(kp, kb, c.lo, c.len, e, e1, true, px[0], pox[0]);
+    if (side) c5_load4<F32, true>(c.oth, c.both, c.lo, c.len, e, e1, true, py[0], poy[0]);
+  }
 #pragma unroll
   for (int g = 0; g < GROUPS; ++g) {
-    const int64_t e = e0 + 4 * ((int64_t)g * C5_BLOCK + threadIdx.x);
-    uint32_t x[4], y[4];
-    bool okx[4], oky[4];
-    c5_load4<F32, true>(kp, kb, c.lo, c.len, e, e1, true, x, okx);
-    if (side) c5_load4<F32, true>(c.oth, c.both, c.lo, c.len, e, e1, true, y, oky);
+    if (g < gu) {  // static index per unrolled group: key[] stays in VGPRs
+      if (g + 1 < gu) {
+        const int64_t en = e0 + 4 * ((int64_t)(g + 1) * C5_BLOCK + threadIdx.x);
+        c5_load4<F32, true>(kp, kb, c.lo, c.len, en, e1, true, px[(g + 1) & 1], pox[(g + 1) & 1]);
+        if (side)
+          c5_load4<F32, true>(c.oth, c.both, c.lo, c.len, en, e1, true, py[(g + 1) & 1], poy[(g + 1) & 1]);
+      }
+      uint32_t x[4], y[4];
+      bool okx[4], oky[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t h = node_mix_t<WIDE>(x[k], c.mix);
-      const uint32_t b = (h >> C2_BITS) - (uint32_t)c.b0;  // wraps when below b0
-      const bool ok = okx[k] && b < (uint32_t)c.nbl;
-      key[4 * g + k] = ok ? ((b + run0) << C2_BITS) | (h & 0xFFFF) : dummy;
-      if (side) lp += (ok && oky[k] && x[k] == y[k]) ? 1u : 0u;
-      atomicAdd(&cur[(key[4 * g + k] >> C2_BITS) * C + my_copy], 1u);
+      for (int k = 0; k < 4; ++k) {
+        x[k] = px[g & 1][k];
+        y[k] = py[g & 1][k];
+        okx[k] = pox[g & 1][k];
+        oky[k] = poy[g & 1][k];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t h = node_mix_t<WIDE>(x[k], c.mix);
+        const uint32_t b = (h >> C2_BITS) - (uint32_t)c.b0;  // wraps when below b0
+        const bool ok = okx[k] && b < (uint32_t)c.nbl;
+        key[4 * g + k] = ok ? ((b + run0) << C2_BITS) | (h & 0xFFFF) : dummy;
+        if (side) lp += (ok && oky[k] && x[k] == y[k]) ? 1u : 0u;
+        atomicAdd(&cur[(key[4 * g + k] >> C2_BITS) * C + my_copy], 1u);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -872,15 +919,16 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
     }
   }
   if (r < nr) meta[t * nr + r] = (ex >> 3) | (cnt << 16);
+  if (r == nr) body_end = ex;  // the dummy run (last) is not copied out
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < RPT; ++j) {
-    stage[atomicAdd(&cur[(key[j] >> C2_BITS) * C + my_copy], 1u)] = (uint16_t)key[j];
+    if (j < 4 * gu) stage[atomicAdd(&cur[(key[j] >> C2_BITS) * C + my_copy], 1u)] = (uint16_t)key[j];
     if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
   }
   __syncthreads();
   uint4 *dst = (uint4 *)(part + t * rstride);
-  for (uint32_t i = threadIdx.x; i < total / 8; i += C5_BLOCK) dst[i] = stage4[i];
+  for (uint32_t i = threadIdx.x; i < body_end / 8; i += C5_BLOCK) dst[i] = stage4[i];
   unsigned long long lp64 = wave_reduce_sum((unsigned long long)lp);
   if (lane_id() == 0 && lp64) atomicAdd(loops, lp64);
 }
@@ -959,8 +1007,24 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
     c.both = nf ? cols[2].base : 0;
     c.n_in = n_in;
     c.n_out = n_out;
-    c.t_in = (n_in + C5S_TILE - 1) / C5S_TILE;
-    const int64_t t_out = (n_out + C5S_TILE - 1) / C5S_TILE;
+    // tile size: whole rounds of resident blocks (2 per CU), counting one
+    // group of per-tile overhead (stage fill, scan, copy-out)
+    {
+      const int64_t slots = 2 * (int64_t)s->num_cus;
+      int64_t best = -1;
+      for (int g = C5S_TILE / (4 * C5_BLOCK); g >= 1; --g) {
+        const int64_t rows = (int64_t)g * 4 * C5_BLOCK;
+        const int64_t tiles = (n_in + rows - 1) / rows + (n_out + rows - 1) / rows;
+        const int64_t cost = (tiles + slots - 1) / slots * (g + 1);
+        if (best < 0 || cost < best) {
+          best = cost;
+          c.gpt = g;
+        }
+      }
+    }
+    const int64_t trows = (int64_t)c.gpt * 4 * C5_BLOCK;
+    c.t_in = (n_in + trows - 1) / trows;
+    const int64_t t_out = (n_out + trows - 1) / trows;
     const int64_t ntiles = c.t_in + t_out;
     c.lo = lo;
     c.len = (uint64_t)n_nodes;

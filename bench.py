@@ -35,6 +35,14 @@ def two_hop_query():
                  [Stage([("count", CountStar())])])
 
 
+def triangle_query():
+    from capf_amd.expr import CountStar
+    from capf_amd.planner import Match, NodeP, Query, RelP, Stage
+    return Query([Match([NodeP("a"), NodeP("b"), NodeP("c")],
+                        [RelP("r1", "a", "b"), RelP("r2", "b", "c"), RelP("r3", "c", "a")])],
+                 [Stage([("count", CountStar())])])
+
+
 def cpu_threads():
     try:
         n = len(os.sched_getaffinity(0))

@@ -123,6 +123,8 @@ _SIGS = {
     "capf_table_node_partition": (c_int32, [_T, c_char_p, c_int64, c_int64, c_int32, c_int32, _PT]),
     "capf_chain2_sharded_count": (c_int32, [_S, _T, c_char_p, _T, c_char_p, c_char_p, c_int64, c_int64,
                                             c_int32, c_int32, c_void_p]),
+    "capf_triangle_count_part": (c_int32, [_S, _T, c_char_p, c_char_p, c_int64, c_int64, c_int32, c_int32,
+                                           c_void_p]),
     "capf_dot_u32": (c_int32, [_S, c_void_p, c_void_p, c_int64, POINTER(c_uint64)]),
 }
 

@@ -342,6 +342,9 @@ uint8_t *node_owner_flags(Session *s, const ColView &key, int64_t n, int64_t lo,
                           int parts, int part, BufPtr &keep);
 bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out, int64_t lo,
                     int64_t n_nodes, int parts, int part, int64_t *d_partial);
+// Directed triangle count (triangle.hip), part `part` of `parts`, to device int64.
+void triangle_count_async(Session *s, const ColView &src, const ColView &dst, int64_t m,
+                          int64_t lo, uint64_t len, int parts, int part, int64_t *d_out);
 bool chain2_partitioned(Session *s, const ColView *cols, int64_t n, int64_t lo, int64_t hi,
                         bool in_range, uint32_t *h_in, uint32_t *h_out,
                         unsigned long long *d_loops);

@@ -28,6 +28,7 @@
 #include <cstring>
 #include <functional>
 #include <numeric>
+#include <map>
 #include <set>
 
 #include "capf_internal.h"
@@ -665,6 +666,77 @@ static bool match_chain2(const JoinGraph &g, Chain2 &c) {
   return false;
 }
 
+// ---------------------------------------------------------- triangle matcher
+// (a)-[r1]->(b)-[r2]->(c)-[r3]->(a): Expand, Expand, ExpandInto
+// (RelationalPlanner.scala:130-189) — three scans of one rel table, three node
+// scans, six equalities forming a 6-cycle, pairwise r_i <> r_j.
+struct Tri {
+  int rel;         // one of the rel leaves (all scan the same base)
+  int src, dst;    // its start / end columns
+  int nodes[3];    // node leaves
+  int ycol[3];     // their id columns
+  int idcol;       // the uniqueness column of the rel leaves
+};
+
+static bool match_triangle(const JoinGraph &g, Tri &t) {
+  if (g.leaves.size() != 6 || g.eqs.size() != 6 || g.neqs.size() != 3) return false;
+  std::set<int> rels;
+  int idcol = -1;
+  for (auto &ne : g.neqs) {
+    if (ne.first.leaf == ne.second.leaf || ne.first.col != ne.second.col) return false;
+    if (idcol >= 0 && ne.first.col != idcol) return false;
+    idcol = ne.first.col;
+    rels.insert(ne.first.leaf);
+    rels.insert(ne.second.leaf);
+  }
+  if (rels.size() != 3) return false;
+  const int r0 = *rels.begin();
+  for (int r : rels) {
+    const Leaf &l = g.leaves[r];
+    if (l.node != g.leaves[r0].node || !l.filters.empty() || !l.col_eqs.empty()) return false;
+  }
+  auto edges_of = [&](int leaf) {
+    std::vector<std::pair<int, ColRef>> r;  // (my col, other)
+    for (auto &e : g.eqs) {
+      if (e.first.leaf == leaf) r.emplace_back(e.first.col, e.second);
+      if (e.second.leaf == leaf) r.emplace_back(e.second.col, e.first);
+    }
+    return r;
+  };
+  auto e0 = edges_of(r0);
+  if (e0.size() != 2 || e0[0].first == e0[1].first) return false;
+  const int cs = e0[0].first, cd = e0[1].first;  // orientation: any consistent one
+  std::map<int, std::pair<int, int>> node_ends;  // node leaf → (#cs ends, #cd ends)
+  std::map<int, int> node_col;
+  for (int r : rels) {
+    auto e = edges_of(r);
+    if (e.size() != 2 || e[0].first == e[1].first) return false;
+    for (auto &x : e) {
+      const int nl = x.second.leaf;
+      if (rels.count(nl)) return false;
+      if (x.first != cs && x.first != cd) return false;
+      auto it = node_col.find(nl);
+      if (it != node_col.end() && it->second != x.second.col) return false;
+      node_col[nl] = x.second.col;
+      (x.first == cs ? node_ends[nl].first : node_ends[nl].second)++;
+    }
+  }
+  if (node_ends.size() != 3) return false;
+  int k = 0;
+  for (auto &ne : node_ends) {
+    if (ne.second.first != 1 || ne.second.second != 1) return false;  // a directed cycle
+    if (!g.leaves[ne.first].col_eqs.empty()) return false;
+    t.nodes[k] = ne.first;
+    t.ycol[k] = node_col[ne.first];
+    ++k;
+  }
+  t.rel = r0;
+  t.src = cs;
+  t.dst = cd;
+  t.idcol = idcol;
+  return true;
+}
+
 struct NodeWeights {
   HostMap map;
   bool ones = false;
@@ -812,6 +884,37 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
   return true;
 }
 
+// The triangle on the GPU (triangle.hip) when the three node scans are one
+// dense unique id range and the rel ids are unique (r_i = r_j ⇔ same row).
+static bool run_triangle(Session *s, const JoinGraph &g, const Tri &t, uint64_t *out) {
+  LeafData rel = leaf_data(g.leaves[t.rel]);
+  const Data &R = *rel.data;
+  for (int col : {t.src, t.dst, t.idcol})
+    if (R.cols[col]->type != Type::Int64 || R.cols[col]->valid) return false;
+  const ColStats &ids = column_stats(s, R.cols[t.idcol]);
+  if (!(ids.dense_unique && ids.non_null == R.nrows) && R.nrows > 1) return false;
+  NodeWeights w[3];
+  for (int k = 0; k < 3; ++k) {
+    LeafData nd = leaf_data(g.leaves[t.nodes[k]]);
+    if (!node_weights(s, nd, t.ycol[k], w[k]) || !w[k].ones) return false;
+    if (w[k].map.m.lo != w[0].map.m.lo || w[k].map.m.hi != w[0].map.m.hi) return false;
+  }
+  const int64_t lo = w[0].map.m.lo, hi = w[0].map.m.hi;
+  const int64_t len = hi >= lo ? hi - lo + 1 : 0;
+  if (len > (int64_t(1) << 31) || R.nrows >= (int64_t(1) << 32)) return false;
+  BufPtr acc = s->alloc(16);
+  if (len > 0 && R.nrows > 0) {
+    triangle_count_async(s, view_of(R.cols[t.src]), view_of(R.cols[t.dst]), R.nrows, lo,
+                         (uint64_t)len, 1, 0, (int64_t *)acc->p);
+  } else {
+    HIP_CHECK(hipMemsetAsync(acc->p, 0, 8, s->stream));
+  }
+  HIP_CHECK(hipMemcpyAsync(s->h_scalars, acc->p, 8, hipMemcpyDeviceToHost, s->stream));
+  s->sync();
+  *out = (uint64_t)s->h_scalars[0];
+  return true;
+}
+
 __global__ void k_partial_minus_loops(const unsigned long long *acc, int64_t *out) {
   if (threadIdx.x == 0) *out = (int64_t)(acc[0] - acc[1]);
 }
@@ -834,6 +937,15 @@ bool try_fused_count(const NodePtr &n, int64_t *out) {
     uint64_t r;
     if (run_chain2(s, g, c2, &r)) {
       s->last_plan = "fused_chain2";
+      *out = (int64_t)r;
+      return true;
+    }
+  }
+  Tri tri;
+  if (match_triangle(g, tri)) {
+    uint64_t r;
+    if (run_triangle(s, g, tri, &r)) {
+      s->last_plan = "fused_triangle";
       *out = (int64_t)r;
       return true;
     }
@@ -946,6 +1058,34 @@ extern "C" capf_status capf_chain2_sharded_count(capf_session *cs, capf_table *i
                         d_partial))
       not_impl("sharded 2-hop count: shape outside the kernel's limits (buckets per rank, "
                "rows per copy < 2^31, mixed encodings)");
+    return CAPF_OK;
+  } catch (const capf::Error &e) {
+    return record_error(e.code, e.what());
+  }
+}
+
+extern "C" capf_status capf_triangle_count_part(capf_session *cs, capf_table *rels,
+                                                const char *src_col, const char *dst_col,
+                                                int64_t node_base, int64_t n_nodes, int32_t parts,
+                                                int32_t part, int64_t *d_count) {
+  try {
+    if (!cs || !rels || !src_col || !dst_col || !d_count) illegal("null argument");
+    if (n_nodes <= 0 || n_nodes > (int64_t(1) << 31)) illegal("node count out of range");
+    if (parts <= 0 || part < 0 || part >= parts) illegal("part out of range");
+    Session *s = &cs->impl;
+    const NodePtr &nd = rels->node;
+    DataPtr d = materialize(nd);
+    const ColPtr &a = d->cols[nd->col_index_or_throw(src_col)];
+    const ColPtr &b = d->cols[nd->col_index_or_throw(dst_col)];
+    if (a->type != Type::Int64 || b->type != Type::Int64 || a->valid || b->valid)
+      illegal("triangle count needs non-null INTEGER endpoint columns");
+    if (d->nrows >= (int64_t(1) << 32)) not_impl("more than 2^32 rels");
+    if (d->nrows == 0) {
+      HIP_CHECK(hipMemsetAsync(d_count, 0, 8, s->stream));
+      return CAPF_OK;
+    }
+    triangle_count_async(s, view_of(a), view_of(b), d->nrows, node_base, (uint64_t)n_nodes, parts,
+                         part, d_count);
     return CAPF_OK;
   } catch (const capf::Error &e) {
     return record_error(e.code, e.what());

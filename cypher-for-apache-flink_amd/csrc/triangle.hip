@@ -1,0 +1,367 @@
+// triangle.hip — fused count of the directed triangle
+//   MATCH (a)-->(b)-->(c)-->(a) RETURN count(*)
+// i.e. the okapi plan Expand, Expand, ExpandInto (RelationalPlanner.scala:
+// 130-189: the closing edge is a join on TWO keys, start = c and end = a)
+// followed by the pairwise uniqueness filter r1 <> r2, r1 <> r3, r2 <> r3.
+//
+// The relational plan materialises the wedge table (~1.3e12 rows at R-MAT
+// s24) before the closing join.  Here the count comes from the multiplicity
+// matrix A (A[x][y] = #rels x -> y) without any wedge row:
+//
+//   count = 3·T + 3·Σ_{pairs {x,y}, x≠y} (L[x] + L[y])·A[x][y]·A[y][x]
+//           + Σ_x L[x](L[x]−1)(L[x]−2)
+//
+// T  = Σ over node triples {p, q, w}, all distinct, of the directed 3-cycles
+//      p→q→w→p and p→w→q→p weighted by multiplicities (each triple once; the
+//      factor 3 = the rotations (a, b, c) of one cycle);
+// L  = self-loops per node: a walk with exactly one self-loop (a→a→c→a and its
+//      rotations) has distinct rels automatically; three self-loops at one
+//      node need three distinct rels.
+// oracle/cmodel.py restates the same count as trace(A³) − Σ_x (L³ − L(L−1)(L−2))
+// and by brute force over rels.
+//
+// T uses the degree-ordered "forward" algorithm: every distinct node pair
+// {u, v} becomes ONE oriented edge p→q from the lower to the higher (degree,
+// id) rank, carrying f = A[p][q] and b = A[q][p]; every triangle is found once,
+// at its lowest-rank vertex p, as q, w ∈ N+(p) with w ∈ N+(q).
+//
+// Kernels:
+//   keys   (min, max, dir) 63-bit key per non-loop rel, loops counted per node
+//   sort   rocprim radix sort + run-length encode → distinct (pair, dir) runs
+//   pairs  merge the two directions of a pair, degrees (atomics)
+//   orient (p << 32 | q) key, (f, b) value, loop term; radix sort → CSR
+//          (binary-search row pointers)
+//   count  one wave per row p (rows handed out in chunks by an atomic
+//          cursor): N+(p) staged in LDS, lanes walk N+(q) for each q ∈ N+(p)
+//          and binary-search each w in the LDS copy
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <rocprim/rocprim.hpp>
+
+#include "capf_internal.h"
+#include "device_common.h"
+
+namespace capf {
+
+constexpr uint64_t TRI_NONE = ~0ull;
+
+// (u, v, dir) key of a non-loop rel inside [lo, lo + len); loops → L[x]++.
+__global__ void k_tri_keys(ColView s, ColView d, int64_t m, int64_t lo, uint64_t len,
+                           uint64_t *keys, uint32_t *loops) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t x = (uint64_t)(ld_int(s, i) - lo), y = (uint64_t)(ld_int(d, i) - lo);
+    uint64_t k = TRI_NONE;
+    if (x < len && y < len) {
+      if (x == y) {
+        atomicAdd(&loops[x], 1u);
+      } else {
+        const uint64_t u = min(x, y), v = max(x, y);
+        k = (u << 32) | (v << 1) | (x > y ? 1u : 0u);
+      }
+    }
+    keys[i] = k;
+  }
+}
+
+// Runs of equal (pair, dir) keys → one entry per distinct pair.  Run j emits
+// its pair if it is the pair's first run; the pair's other direction, if
+// present, is run j + 1.  Degrees count distinct neighbours.
+__global__ void k_tri_pairs(const uint64_t *ukeys, const uint32_t *cnt, const uint32_t *nruns,
+                            uint32_t *deg, uint64_t *pair_uv, uint2 *pair_fb) {
+  const uint32_t nr = *nruns;
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nr; j += gridDim.x * blockDim.x) {
+    const uint64_t k = ukeys[j];
+    const uint64_t pr = k >> 1;
+    if (k == TRI_NONE || (j > 0 && (ukeys[j - 1] >> 1) == pr)) {
+      pair_uv[j] = TRI_NONE;  // dropped rels / second direction merged into run j − 1
+      continue;
+    }
+    uint32_t f = 0, b = 0;
+    if (k & 1) {
+      b = cnt[j];
+    } else {
+      f = cnt[j];
+      if (j + 1 < nr && ukeys[j + 1] != TRI_NONE && (ukeys[j + 1] >> 1) == pr) b = cnt[j + 1];
+    }
+    const uint32_t u = (uint32_t)(pr >> 31), v = (uint32_t)(pr & 0x7FFFFFFFu);
+    pair_uv[j] = ((uint64_t)u << 32) | v;
+    pair_fb[j] = make_uint2(f, b);  // f = #(u→v), b = #(v→u)
+    atomicAdd(&deg[u], 1u);
+    atomicAdd(&deg[v], 1u);
+  }
+}
+
+// Orient each pair from the lower to the higher (degree, id) rank; the loop
+// term Σ (L[u] + L[v])·f·b goes to acc[1].
+__global__ void k_tri_orient(const uint64_t *pair_uv, const uint2 *pair_fb, const uint32_t *nruns,
+                             const uint32_t *deg, const uint32_t *loops, uint64_t *okey,
+                             uint64_t *oval, unsigned long long *acc) {
+  __shared__ unsigned long long lds[17];
+  const uint32_t nr = *nruns;
+  unsigned long long lt = 0;
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nr; j += gridDim.x * blockDim.x) {
+    const uint64_t uv = pair_uv[j];
+    if (uv == TRI_NONE) {
+      okey[j] = TRI_NONE;
+      oval[j] = 0;
+      continue;
+    }
+    const uint32_t u = (uint32_t)(uv >> 32), v = (uint32_t)uv;
+    const uint2 fb = pair_fb[j];
+    const uint64_t ru = ((uint64_t)deg[u] << 32) | u, rv = ((uint64_t)deg[v] << 32) | v;
+    const bool fwd = ru < rv;
+    const uint32_t p = fwd ? u : v, q = fwd ? v : u;
+    const uint32_t f = fwd ? fb.x : fb.y, b = fwd ? fb.y : fb.x;  // f = #(p→q), b = #(q→p)
+    okey[j] = ((uint64_t)p << 32) | q;
+    oval[j] = ((uint64_t)f << 32) | b;
+    lt += (unsigned long long)(loops[u] + loops[v]) * f * b;
+  }
+  unsigned long long tot;
+  block_exclusive_scan(lt, lds, tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(&acc[1], tot);
+}
+
+// rowptr[x] = first oriented edge with p ≥ x (binary search), x ∈ [0, len];
+// rowptr[len] = P, the number of oriented edges (keys < TRI_NONE).
+__global__ void k_tri_rowptr(const uint64_t *okey, uint32_t nr, uint64_t len, uint32_t *rowptr) {
+  for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x <= len;
+       x += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t lo = 0, hi = nr;
+    const uint64_t t = x << 32;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (okey[mid] < t) lo = mid + 1;
+      else hi = mid;
+    }
+    rowptr[x] = lo;
+  }
+}
+
+__global__ void k_tri_split(const uint64_t *okey, const uint64_t *oval, uint32_t P, uint32_t *cols,
+                            uint2 *vals) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < P; i += gridDim.x * blockDim.x) {
+    cols[i] = (uint32_t)okey[i];
+    const uint64_t v = oval[i];
+    vals[i] = make_uint2((uint32_t)(v >> 32), (uint32_t)v);
+  }
+}
+
+// Σ_x L(L−1)(L−2) into acc[2].
+__global__ void k_tri_loop3(const uint32_t *loops, uint64_t len, unsigned long long *acc) {
+  __shared__ unsigned long long lds[17];
+  unsigned long long t = 0;
+  for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < len;
+       x += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long L = loops[x];
+    if (L >= 3) t += L * (L - 1) * (L - 2);
+  }
+  unsigned long long tot;
+  block_exclusive_scan(t, lds, tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(&acc[2], tot);
+}
+
+constexpr int TRI_BLOCK = 256;
+constexpr int TRI_CAP = 1024;  // N+(p) staged in LDS up to this many entries
+constexpr int TRI_CHUNK = 16;  // rows per cursor grab
+
+// Index of w in the ascending a(0..n), or −1.
+template <class A>
+__device__ inline int64_t tri_find(const A &a, int64_t n, uint32_t w) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a(mid) < w) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < n && a(lo) == w ? lo : -1;
+}
+
+// T over this part's rows into acc[0]: row chunks of TRI_CHUNK are dealt
+// round-robin over the parts (chunk c of the graph belongs to part c mod
+// parts) and handed to waves by an atomic cursor.
+__global__ __launch_bounds__(TRI_BLOCK) void k_tri_count(const uint32_t *rowptr,
+                                                          const uint32_t *cols, const uint2 *vals,
+                                                          uint64_t len, int parts, int part,
+                                                          unsigned long long *cursor,
+                                                          unsigned long long *acc) {
+  __shared__ uint32_t s_cols[TRI_BLOCK / WAVE][TRI_CAP];
+  __shared__ unsigned long long lds[17];
+  const int wv = threadIdx.x / WAVE, lane = lane_id();
+  uint32_t *sc = s_cols[wv];
+  unsigned long long t = 0;
+  for (;;) {
+    unsigned long long r0 = 0;
+    if (lane == 0) r0 = atomicAdd(cursor, 1ull);
+    r0 = ((unsigned long long)__shfl((long long)r0, 0, WAVE) * parts + part) * TRI_CHUNK;
+    if (r0 >= len) break;
+    const uint64_t r1 = min<uint64_t>(r0 + TRI_CHUNK, len);
+    for (uint64_t p = r0; p < r1; ++p) {
+      const uint32_t a = rowptr[p], dp = rowptr[p + 1] - a;
+      if (dp < 2) continue;  // a triangle needs two out-neighbours at its lowest vertex
+      const bool staged = dp <= TRI_CAP;
+      if (staged) {
+        for (uint32_t k = lane; k < dp; k += WAVE) sc[k] = cols[a + k];
+        __builtin_amdgcn_wave_barrier();
+      }
+      for (uint32_t k = 0; k < dp; ++k) {
+        const uint32_t q = staged ? sc[k] : cols[a + k];
+        const uint32_t qa = rowptr[q], dq = rowptr[q + 1] - qa;
+        if (dq == 0) continue;
+        const uint2 pq = vals[a + k];  // (#p→q, #q→p)
+        for (uint32_t j = lane; j < dq; j += WAVE) {
+          const uint32_t w = cols[qa + j];
+          const int64_t i = staged ? tri_find([&](int64_t x) { return sc[x]; }, dp, w)
+                                   : tri_find([&](int64_t x) { return cols[a + x]; }, dp, w);
+          if (i >= 0) {
+            const uint2 qw = vals[qa + j], pw = vals[a + i];
+            // p→q→w→p  +  p→w→q→p
+            t += (unsigned long long)pq.x * qw.x * pw.y + (unsigned long long)pw.x * qw.y * pq.y;
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();  // sc is rewritten by the next row
+    }
+  }
+  unsigned long long tot;
+  block_exclusive_scan(t, lds, tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(&acc[0], tot);
+}
+
+__global__ void k_tri_total(const unsigned long long *acc, int64_t *out) {
+  if (threadIdx.x == 0) *out = (int64_t)(3ull * acc[0] + 3ull * acc[1] + acc[2]);
+}
+
+template <class F>
+static void rocprim_call(Session *s, F &&f) {
+  size_t tmp = 0;
+  HIP_CHECK(f(nullptr, tmp));
+  BufPtr t = s->alloc(std::max<size_t>(tmp, 16));
+  HIP_CHECK(f(t->p, tmp));
+}
+
+// Oriented CSR of the distinct node pairs of (src, dst) over [lo, lo + len).
+struct TriGraph {
+  BufPtr rowptr, cols, vals, loops, acc;  // acc: [0] T, [1] Σ(L+L)·f·b, [2] Σ L(L−1)(L−2), [3] cursor
+  uint32_t P = 0;
+  uint64_t len = 0;
+};
+
+static void tri_build(Session *s, const ColView &src, const ColView &dst, int64_t m, int64_t lo,
+                      uint64_t len, TriGraph &g) {
+  g.len = len;
+  g.acc = s->alloc(32);
+  HIP_CHECK(hipMemsetAsync(g.acc->p, 0, 32, s->stream));
+  unsigned long long *acc = (unsigned long long *)g.acc->p;
+  g.loops = s->alloc(4 * len);
+  HIP_CHECK(hipMemsetAsync(g.loops->p, 0, 4 * len, s->stream));
+  uint32_t *loops = (uint32_t *)g.loops->p;
+  const int64_t m1 = std::max<int64_t>(m, 1);
+  BufPtr keys = s->alloc(8 * m1), sorted = s->alloc(8 * m1);
+  {
+    KernelTimer kt(s, "tri_keys", 16.0 * m);
+    hipLaunchKernelGGL(k_tri_keys, dim3(grid_for(m1, 256)), dim3(256), 0, s->stream, src, dst, m,
+                       lo, len, (uint64_t *)keys->p, loops);
+    KERNEL_CHECK();
+  }
+  uint64_t *kout = (uint64_t *)sorted->p;
+  {
+    KernelTimer kt(s, "tri_sort_keys", 32.0 * m);
+    const uint64_t *kin = (const uint64_t *)keys->p;
+    rocprim_call(s, [&](void *t, size_t &n) {
+      return rocprim::radix_sort_keys(t, n, kin, kout, (size_t)m, 0, 64, s->stream);
+    });
+  }
+  BufPtr ukeys = s->alloc(8 * m1), cnt = s->alloc(4 * m1), nruns = s->alloc(16);
+  {
+    KernelTimer kt(s, "tri_rle", 20.0 * m);
+    rocprim_call(s, [&](void *t, size_t &n) {
+      return rocprim::run_length_encode(t, n, (const uint64_t *)kout, (unsigned int)m,
+                                        (uint64_t *)ukeys->p, (uint32_t *)cnt->p,
+                                        (uint32_t *)nruns->p, s->stream);
+    });
+  }
+  BufPtr deg = s->alloc(4 * len);
+  HIP_CHECK(hipMemsetAsync(deg->p, 0, 4 * len, s->stream));
+  uint64_t *pair_uv = (uint64_t *)keys->p;  // runs ≤ m: the unsorted keys are dead
+  BufPtr pair_fb = s->alloc(8 * m1);
+  const unsigned grid = grid_for(m1, 256, 256 * 64);
+  {
+    KernelTimer kt(s, "tri_pairs", 24.0 * m);
+    hipLaunchKernelGGL(k_tri_pairs, dim3(grid), dim3(256), 0, s->stream, (const uint64_t *)ukeys->p,
+                       (const uint32_t *)cnt->p, (const uint32_t *)nruns->p, (uint32_t *)deg->p,
+                       pair_uv, (uint2 *)pair_fb->p);
+    KERNEL_CHECK();
+  }
+  uint64_t *okey = (uint64_t *)ukeys->p;  // runs ≤ m: the run keys are dead after the merge
+  uint64_t *oval = kout;
+  {
+    KernelTimer kt(s, "tri_orient", 32.0 * m);
+    hipLaunchKernelGGL(k_tri_orient, dim3(grid), dim3(256), 0, s->stream, (const uint64_t *)pair_uv,
+                       (const uint2 *)pair_fb->p, (const uint32_t *)nruns->p, (const uint32_t *)deg->p,
+                       (const uint32_t *)loops, okey, oval, acc);
+    KERNEL_CHECK();
+  }
+  uint32_t nr = 0;
+  HIP_CHECK(hipMemcpyAsync(&nr, nruns->p, 4, hipMemcpyDeviceToHost, s->stream));
+  s->sync();
+  BufPtr ok2 = s->alloc(8 * std::max<uint32_t>(nr, 1)), ov2 = s->alloc(8 * std::max<uint32_t>(nr, 1));
+  {
+    KernelTimer kt(s, "tri_sort_pairs", 32.0 * nr);
+    rocprim_call(s, [&](void *t, size_t &n) {
+      return rocprim::radix_sort_pairs(t, n, (const uint64_t *)okey, (uint64_t *)ok2->p,
+                                       (const uint64_t *)oval, (uint64_t *)ov2->p, (size_t)nr, 0, 64,
+                                       s->stream);
+    });
+  }
+  g.rowptr = s->alloc(4 * (len + 2));
+  {
+    KernelTimer kt(s, "tri_rowptr", 4.0 * len);
+    hipLaunchKernelGGL(k_tri_rowptr, dim3(grid_for((int64_t)len + 1, 256, 256 * 64)), dim3(256), 0,
+                       s->stream, (const uint64_t *)ok2->p, nr, len, (uint32_t *)g.rowptr->p);
+    KERNEL_CHECK();
+  }
+  HIP_CHECK(hipMemcpyAsync(&g.P, (uint32_t *)g.rowptr->p + len, 4, hipMemcpyDeviceToHost, s->stream));
+  s->sync();
+  g.cols = s->alloc(4 * std::max<uint32_t>(g.P, 1));
+  g.vals = s->alloc(8 * std::max<uint32_t>(g.P, 1));
+  if (g.P > 0) {
+    KernelTimer kt(s, "tri_split", 20.0 * g.P);
+    hipLaunchKernelGGL(k_tri_split, dim3(grid_for(g.P, 256, 256 * 64)), dim3(256), 0, s->stream,
+                       (const uint64_t *)ok2->p, (const uint64_t *)ov2->p, g.P, (uint32_t *)g.cols->p,
+                       (uint2 *)g.vals->p);
+    KERNEL_CHECK();
+  }
+}
+
+// Device count (int64 at d_out) of the directed triangle over rels (src, dst)
+// with endpoints in [lo, lo + len), restricted to part `part` of `parts`
+// (row chunks dealt round-robin; the loop terms belong to part 0): the sum
+// over parts is the count.  Asynchronous after the build's two host reads.
+void triangle_count_async(Session *s, const ColView &src, const ColView &dst, int64_t m,
+                          int64_t lo, uint64_t len, int parts, int part, int64_t *d_out) {
+  TriGraph g;
+  tri_build(s, src, dst, m, lo, len, g);
+  unsigned long long *acc = (unsigned long long *)g.acc->p;
+  if (part != 0) HIP_CHECK(hipMemsetAsync(acc + 1, 0, 8, s->stream));
+  else {
+    KernelTimer kt(s, "tri_loop3", 4.0 * len);
+    hipLaunchKernelGGL(k_tri_loop3, dim3(grid_for((int64_t)len, 256, 1024)), dim3(256), 0,
+                       s->stream, (const uint32_t *)g.loops->p, len, acc);
+    KERNEL_CHECK();
+  }
+  if (g.P > 0) {
+    KernelTimer kt(s, "tri_count", 4.0 * g.P);
+    hipLaunchKernelGGL(k_tri_count, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
+                       (const uint32_t *)g.rowptr->p, (const uint32_t *)g.cols->p,
+                       (const uint2 *)g.vals->p, len, parts, part, acc + 3, acc);
+    KERNEL_CHECK();
+  }
+  hipLaunchKernelGGL(k_tri_total, dim3(1), dim3(64), 0, s->stream, (const unsigned long long *)acc,
+                     d_out);
+  KERNEL_CHECK();
+  // g's buffers return to the stream-ordered pool: reuse is ordered after the kernels
+}
+
+}  // namespace capf

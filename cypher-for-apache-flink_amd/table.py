@@ -356,6 +356,14 @@ def chain2_sharded_count_async(session, in_copy, out_copy, node_base, n_nodes, p
               c_void_p(d_partial))
 
 
+def triangle_count_part_async(session, rels, node_base, n_nodes, parts, part, d_count,
+                              src="source", dst="target"):
+    """Enqueue part `part` of `parts` of the directed triangle count (int64 at
+    device address d_count); the parts sum to the count."""
+    _lib.call("capf_triangle_count_part", session._h, rels._h, src.encode(), dst.encode(), int(node_base),
+              int(n_nodes), int(parts), int(part), c_void_p(d_count))
+
+
 def chain2_hist_len(n_nodes):
     """Counters per histogram written by chain2_local_hists (2^k >= n_nodes)."""
     return int(_lib.load().capf_chain2_hist_len(int(n_nodes)))

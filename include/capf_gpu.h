@@ -308,6 +308,16 @@ capf_status capf_chain2_sharded_count(capf_session *s, capf_table *in_copy, cons
                                       capf_table *out_copy, const char *out_src,
                                       const char *out_dst, int64_t node_base, int64_t n_nodes,
                                       int32_t parts, int32_t part, int64_t *d_partial);
+/* Directed triangle (a)-->(b)-->(c)-->(a) with pairwise distinct rels over
+ * the rels of `rels` whose endpoints lie in [node_base, node_base + n_nodes)
+ * (the fused form of Expand, Expand, ExpandInto + uniqueness,
+ * RelationalPlanner.scala:130-189): part `part` of `parts` of the count as a
+ * device int64 at d_count — the parts sum to the count (rank r of G computes
+ * part r over a replicated rel table, then one all-reduce).  Asynchronous on
+ * the session stream after two internal host reads.                         */
+capf_status capf_triangle_count_part(capf_session *s, capf_table *rels, const char *src_col,
+                                     const char *dst_col, int64_t node_base, int64_t n_nodes,
+                                     int32_t parts, int32_t part, int64_t *d_count);
 int64_t capf_chain2_hist_len(int64_t n_nodes);
 capf_status capf_chain2_local_hists(capf_session *s, capf_table *rels, const char *src_col,
                                     const char *dst_col, int64_t node_base, int64_t n_nodes,

@@ -49,6 +49,8 @@ def lib():
         l.count_1hop.restype = u64
         l.count_2hop.argtypes = [P, P, i64, i64]
         l.count_2hop.restype = u64
+        l.count_triangle_brute.argtypes = [P, P, i64, i64]
+        l.count_triangle_brute.restype = u64
         l.degree_hists.argtypes = [P, P, i64, i64, i64, P, P, P]
         l.degree_hists.restype = None
         l.pipeline_build.argtypes = [P, i64, P, P, P, i64, i32]
@@ -85,6 +87,31 @@ def count_1hop(src, dst, n, in_a=None, in_b=None):
     return lib().count_1hop(src.ctypes.data, dst.ctypes.data, len(src),
                             None if pa is None else pa.ctypes.data,
                             None if pb is None else pb.ctypes.data, n)
+
+
+def count_triangle_brute(src, dst, n):
+    """(a)-->(b)-->(c)-->(a) with distinct rels, brute force over rels (small scales)."""
+    L = lib()
+    src = np.ascontiguousarray(src, dtype=np.int64)
+    dst = np.ascontiguousarray(dst, dtype=np.int64)
+    return int(L.count_triangle_brute(src.ctypes.data, dst.ctypes.data, len(src), n))
+
+
+def count_triangle_formula(src, dst, n):
+    """Same count by linear algebra: trace(A^3) over the multiplicity matrix A
+    (closed walks a->b->c->a of rels), minus the walks reusing a rel — only
+    three self-loops at one node can coincide: L^3 - L(L-1)(L-2) per node."""
+    import scipy.sparse as sp
+    src = np.asarray(src, dtype=np.int64)
+    dst = np.asarray(dst, dtype=np.int64)
+    ok = (src >= 0) & (src < n) & (dst >= 0) & (dst < n)
+    s, d = src[ok], dst[ok]
+    A = sp.csr_matrix((np.ones(len(s), dtype=np.int64), (s, d)), shape=(n, n))
+    A.sum_duplicates()
+    tr = int((A @ A).multiply(A.T).sum())
+    L = np.bincount(s[s == d], minlength=n).astype(object)
+    bad = sum(int(x) ** 3 - int(x) * (int(x) - 1) * (int(x) - 2) for x in L if x)
+    return tr - bad
 
 
 def count_2hop(src, dst, n):

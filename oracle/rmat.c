@@ -91,6 +91,40 @@ uint64_t count_2hop(const int64_t *src, const int64_t *dst, int64_t m, int64_t n
   return total - loops;
 }
 
+/* Directed triangle (a)-->(b)-->(c)-->(a) with pairwise distinct rels over a
+ * dense node range [0, n) — brute force over rels (RelationalPlanner's
+ * Expand, Expand, ExpandInto join chain + the uniqueness filter,
+ * RelationalPlanner.scala:130-189): for every r1 = a->b, every r2 = b->c
+ * (r2 != r1), every r3 = c->a (r3 != r1, r2).  Small scales only.          */
+uint64_t count_triangle_brute(const int64_t *src, const int64_t *dst, int64_t m, int64_t n) {
+  int64_t *off = (int64_t *)calloc((size_t)n + 1, 8), *pos = (int64_t *)malloc((size_t)n * 8);
+  int64_t *adj = (int64_t *)malloc((size_t)(m > 0 ? m : 1) * 8);
+  for (int64_t e = 0; e < m; ++e)
+    if (src[e] >= 0 && src[e] < n && dst[e] >= 0 && dst[e] < n) off[src[e] + 1]++;
+  for (int64_t v = 0; v < n; ++v) off[v + 1] += off[v];
+  memcpy(pos, off, (size_t)n * 8);
+  for (int64_t e = 0; e < m; ++e)
+    if (src[e] >= 0 && src[e] < n && dst[e] >= 0 && dst[e] < n) adj[pos[src[e]]++] = e;
+  uint64_t c = 0;
+  for (int64_t r1 = 0; r1 < m; ++r1) {
+    const int64_t a = src[r1], b = dst[r1];
+    if (a < 0 || a >= n || b < 0 || b >= n) continue;
+    for (int64_t i = off[b]; i < off[b + 1]; ++i) {
+      const int64_t r2 = adj[i];
+      if (r2 == r1) continue;
+      const int64_t cc = dst[r2];
+      for (int64_t k = off[cc]; k < off[cc + 1]; ++k) {
+        const int64_t r3 = adj[k];
+        if (dst[r3] == a && r3 != r1 && r3 != r2) ++c;
+      }
+    }
+  }
+  free(off);
+  free(pos);
+  free(adj);
+  return c;
+}
+
 /* Per-node in/out degree histograms (for the distributed-count tests). */
 void degree_hists(const int64_t *src, const int64_t *dst, int64_t m, int64_t base, int64_t n,
                   uint32_t *in, uint32_t *out, int64_t *loops) {

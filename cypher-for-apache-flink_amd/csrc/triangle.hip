@@ -71,25 +71,42 @@ __global__ void k_tri_keys(ColView s, ColView d, int64_t m, int64_t lo, uint64_t
 __global__ void k_tri_pairs(const uint64_t *ukeys, const uint32_t *cnt, const uint32_t *nruns,
                             uint32_t *deg, uint64_t *pair_uv, uint2 *pair_fb) {
   const uint32_t nr = *nruns;
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nr; j += gridDim.x * blockDim.x) {
-    const uint64_t k = ukeys[j];
-    const uint64_t pr = k >> 1;
-    if (k == TRI_NONE || (j > 0 && (ukeys[j - 1] >> 1) == pr)) {
-      pair_uv[j] = TRI_NONE;  // dropped rels / second direction merged into run j − 1
-      continue;
+  const int lane = lane_id();
+  const uint32_t stride = gridDim.x * blockDim.x;
+  // whole waves per step: the degree of u is aggregated over the wave (a hub's
+  // pairs are consecutive in the sorted order and would serialise on deg[u])
+  for (uint32_t j0 = blockIdx.x * blockDim.x + (threadIdx.x & ~(WAVE - 1)); j0 < nr; j0 += stride) {
+    const uint32_t j = j0 + lane;
+    bool emit = false;
+    uint32_t u = 0xFFFFFFFFu, v = 0;
+    if (j < nr) {
+      const uint64_t k = ukeys[j];
+      const uint64_t pr = k >> 1;
+      if (k == TRI_NONE || (j > 0 && (ukeys[j - 1] >> 1) == pr)) {
+        pair_uv[j] = TRI_NONE;  // dropped rels / second direction merged into run j − 1
+      } else {
+        uint32_t f = 0, b = 0;
+        if (k & 1) {
+          b = cnt[j];
+        } else {
+          f = cnt[j];
+          if (j + 1 < nr && ukeys[j + 1] != TRI_NONE && (ukeys[j + 1] >> 1) == pr) b = cnt[j + 1];
+        }
+        u = (uint32_t)(pr >> 31);
+        v = (uint32_t)(pr & 0x7FFFFFFFu);
+        pair_uv[j] = ((uint64_t)u << 32) | v;
+        pair_fb[j] = make_uint2(f, b);  // f = #(u→v), b = #(v→u)
+        emit = true;
+      }
     }
-    uint32_t f = 0, b = 0;
-    if (k & 1) {
-      b = cnt[j];
-    } else {
-      f = cnt[j];
-      if (j + 1 < nr && ukeys[j + 1] != TRI_NONE && (ukeys[j + 1] >> 1) == pr) b = cnt[j + 1];
-    }
-    const uint32_t u = (uint32_t)(pr >> 31), v = (uint32_t)(pr & 0x7FFFFFFFu);
-    pair_uv[j] = ((uint64_t)u << 32) | v;
-    pair_fb[j] = make_uint2(f, b);  // f = #(u→v), b = #(v→u)
-    atomicAdd(&deg[u], 1u);
-    atomicAdd(&deg[v], 1u);
+    const uint32_t key = emit ? u : 0xFFFFFFFFu;
+    const uint32_t prev = __shfl_up(key, 1, WAVE);
+    const bool head = lane == 0 || key != prev;
+    const unsigned long long heads = __ballot(head);
+    const unsigned long long above = lane == WAVE - 1 ? 0ull : heads & ~((2ull << lane) - 1);
+    const int next = above ? __ffsll((long long)above) - 1 : WAVE;
+    if (emit && head) atomicAdd(&deg[u], (uint32_t)(next - lane));
+    if (emit) atomicAdd(&deg[v], 1u);
   }
 }
 
@@ -165,6 +182,7 @@ __global__ void k_tri_loop3(const uint32_t *loops, uint64_t len, unsigned long l
 constexpr int TRI_BLOCK = 256;
 constexpr int TRI_CAP = 1024;  // N+(p) staged in LDS up to this many entries
 constexpr int TRI_CHUNK = 16;  // rows per cursor grab
+constexpr int TRI_ILP = 4;     // N+(q) entries per lane in flight
 
 // Index of w in the ascending a(0..n), or −1.
 template <class A>
@@ -178,18 +196,32 @@ __device__ inline int64_t tri_find(const A &a, int64_t n, uint32_t w) {
   return lo < n && a(lo) == w ? lo : -1;
 }
 
+struct TriBatch {
+  uint32_t pre[WAVE + 1];  // exclusive prefix of the batch's |N+(q)|, + total
+  uint32_t qa[WAVE];       // N+(q) start in cols
+  uint2 pq[WAVE];          // (#p→q, #q→p)
+};
+
 // T over this part's rows into acc[0]: row chunks of TRI_CHUNK are dealt
 // round-robin over the parts (chunk c of the graph belongs to part c mod
-// parts) and handed to waves by an atomic cursor.
+// parts) and handed to waves by an atomic cursor.  N+(p) is staged in LDS;
+// its q's are taken 64 at a time and their lists N+(q) are walked as ONE
+// flattened sequence (lane = position, found by a 6-step search in the
+// batch's prefix table — most lists are far shorter than a wave), TRI_ILP
+// positions per lane in flight, each w binary-searched in the staged row.
+// (An LDS hash table instead of the sorted row, 12 KiB per wave, measured
+// 1.6× slower: the kernel waits on the N+(q) loads, so occupancy wins.)
 __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count(const uint32_t *rowptr,
                                                           const uint32_t *cols, const uint2 *vals,
                                                           uint64_t len, int parts, int part,
                                                           unsigned long long *cursor,
                                                           unsigned long long *acc) {
   __shared__ uint32_t s_cols[TRI_BLOCK / WAVE][TRI_CAP];
+  __shared__ TriBatch s_tab[TRI_BLOCK / WAVE];
   __shared__ unsigned long long lds[17];
   const int wv = threadIdx.x / WAVE, lane = lane_id();
   uint32_t *sc = s_cols[wv];
+  TriBatch &tb = s_tab[wv];
   unsigned long long t = 0;
   for (;;) {
     unsigned long long r0 = 0;
@@ -200,26 +232,67 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count(const uint32_t *rowptr,
     for (uint64_t p = r0; p < r1; ++p) {
       const uint32_t a = rowptr[p], dp = rowptr[p + 1] - a;
       if (dp < 2) continue;  // a triangle needs two out-neighbours at its lowest vertex
-      const bool staged = dp <= TRI_CAP;
-      if (staged) {
-        for (uint32_t k = lane; k < dp; k += WAVE) sc[k] = cols[a + k];
-        __builtin_amdgcn_wave_barrier();
-      }
-      for (uint32_t k = 0; k < dp; ++k) {
-        const uint32_t q = staged ? sc[k] : cols[a + k];
-        const uint32_t qa = rowptr[q], dq = rowptr[q + 1] - qa;
-        if (dq == 0) continue;
-        const uint2 pq = vals[a + k];  // (#p→q, #q→p)
-        for (uint32_t j = lane; j < dq; j += WAVE) {
-          const uint32_t w = cols[qa + j];
-          const int64_t i = staged ? tri_find([&](int64_t x) { return sc[x]; }, dp, w)
-                                   : tri_find([&](int64_t x) { return cols[a + x]; }, dp, w);
-          if (i >= 0) {
-            const uint2 qw = vals[qa + j], pw = vals[a + i];
-            // p→q→w→p  +  p→w→q→p
-            t += (unsigned long long)pq.x * qw.x * pw.y + (unsigned long long)pw.x * qw.y * pq.y;
+      if (dp > TRI_CAP) {  // rare long row: per q, binary search in global memory
+        for (uint32_t k = 0; k < dp; ++k) {
+          const uint32_t q = cols[a + k];
+          const uint32_t qa = rowptr[q], dq = rowptr[q + 1] - qa;
+          const uint2 pq = vals[a + k];
+          for (uint32_t j = lane; j < dq; j += WAVE) {
+            const uint32_t w = cols[qa + j];
+            const int64_t i = tri_find([&](int64_t x) { return cols[a + x]; }, dp, w);
+            if (i >= 0) {
+              const uint2 qw = vals[qa + j], pw = vals[a + i];
+              t += (unsigned long long)pq.x * qw.x * pw.y + (unsigned long long)pw.x * qw.y * pq.y;
+            }
           }
         }
+        continue;
+      }
+      for (uint32_t k = lane; k < dp; k += WAVE) sc[k] = cols[a + k];
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t kb = 0; kb < dp; kb += WAVE) {
+        // the batch's table: one q per lane
+        const uint32_t k = kb + lane;
+        uint32_t qa = 0, dq = 0;
+        uint2 pq = make_uint2(0, 0);
+        if (k < dp) {
+          const uint32_t q = sc[k];
+          qa = rowptr[q];
+          dq = rowptr[q + 1] - qa;
+          pq = vals[a + k];
+        }
+        const uint32_t inc = wave_inclusive_scan(dq);
+        tb.pre[lane] = inc - dq;
+        if (lane == WAVE - 1) tb.pre[WAVE] = inc;
+        tb.qa[lane] = qa;
+        tb.pq[lane] = pq;
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl(inc, WAVE - 1, WAVE));
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t t0 = 0; t0 < total; t0 += TRI_ILP * WAVE) {
+          uint32_t w[TRI_ILP], pos[TRI_ILP], bi[TRI_ILP];
+#pragma unroll
+          for (int u = 0; u < TRI_ILP; ++u) {
+            const uint32_t x = t0 + u * WAVE + lane;
+            uint32_t b = 0;  // last batch entry with pre[b] <= x
+#pragma unroll
+            for (int st = WAVE / 2; st > 0; st >>= 1)
+              if (tb.pre[b + st] <= x) b += st;
+            bi[u] = b;
+            pos[u] = tb.qa[b] + (x - tb.pre[b]);
+            w[u] = x < total ? cols[pos[u]] : 0xFFFFFFFFu;
+          }
+#pragma unroll
+          for (int u = 0; u < TRI_ILP; ++u) {
+            if (w[u] == 0xFFFFFFFFu) continue;
+            const int64_t i = tri_find([&](int64_t x) { return sc[x]; }, dp, w[u]);
+            if (i >= 0) {
+              const uint2 pqv = tb.pq[bi[u]], qw = vals[pos[u]], pw = vals[a + i];
+              // p→q→w→p  +  p→w→q→p
+              t += (unsigned long long)pqv.x * qw.x * pw.y + (unsigned long long)pw.x * qw.y * pqv.y;
+            }
+          }
+        }
+        __builtin_amdgcn_wave_barrier();  // the table is rewritten by the next batch
       }
       __builtin_amdgcn_wave_barrier();  // sc is rewritten by the next row
     }

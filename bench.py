@@ -25,6 +25,7 @@ sys.path.insert(0, ROOT)
 import capf_import  # noqa: E402,F401
 
 METRIC = "joined rows/sec for 2-hop MATCH on R-MAT s24 at 1/2/4/8 GPUs; % HBM roofline"
+TRI_METRIC = "joined rows/sec for triangle MATCH (a)-->(b)-->(c)-->(a) on R-MAT (config 4)"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
@@ -41,6 +42,12 @@ def triangle_query():
     return Query([Match([NodeP("a"), NodeP("b"), NodeP("c")],
                         [RelP("r1", "a", "b"), RelP("r2", "b", "c"), RelP("r3", "c", "a")])],
                  [Stage([("count", CountStar())])])
+
+
+def workload_name(args):
+    if args.query == "triangle":
+        return f"R-MAT s{args.scale} triangle MATCH (a)-->(b)-->(c)-->(a) RETURN count(*)"
+    return f"R-MAT s{args.scale} 2-hop MATCH (a)-->(b)-->(c) RETURN count(*)"
 
 
 def cpu_threads():
@@ -93,7 +100,8 @@ def cpu_baseline(session, graph, scale, budget_s):
 
 # kernels of one fused 2-hop count (fused_count.hip + chain2_partitioned.hip)
 PIPELINE = ("c5_partition", "c3_transpose", "c3_units", "c5_gather", "c3_overflow", "chain2_hist",
-            "chain2_dot")
+            "chain2_dot", "tri_keys", "tri_sort_keys", "tri_rle", "tri_pairs", "tri_orient",
+            "tri_sort_pairs", "tri_rowptr", "tri_split", "tri_loop3", "tri_count")
 
 
 def pipeline_roofline(prof, steps, compulsory_bytes, traffic_per_query=None):
@@ -138,7 +146,7 @@ def run_single(args):
 
     s = GpuSession(0)
     g = rmat_graph(s, args.scale, args.edge_factor, compact=not args.int64)
-    q = two_hop_query()
+    q = triangle_query() if args.query == "triangle" else two_hop_query()
     n_nodes = 1 << args.scale
     m = args.edge_factor << args.scale
     step = lambda: run(g, q)[0]["count"]  # noqa: E731
@@ -164,7 +172,7 @@ def run_single(args):
     roof = pipeline_roofline(prof, prof_steps, compulsory, traffic)
     roof["end_to_end_frac"] = compulsory / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS
     result = {
-        "metric": METRIC,
+        "metric": METRIC if args.query == "two_hop" else TRI_METRIC,
         "value": count * args.steps / elapsed,
         "unit": "joined rows/s",
         "n_gpus": 1,
@@ -178,14 +186,14 @@ def run_single(args):
         "data": (f"synthetic R-MAT s{args.scale} (Graph500 a/b/c=.57/.19/.19, edge factor {args.edge_factor}, "
                  f"seed 0x{0x5EED0000 + args.scale:X}) generated in HBM before timing"),
         "config": {
-            "workload": f"R-MAT s{args.scale} 2-hop MATCH (a)-->(b)-->(c) RETURN count(*)",
+            "workload": workload_name(args),
             "scale": args.scale, "nodes": n_nodes, "rels": m, "count": count, "plan": plan,
             "id_storage": "int64" if args.int64 else "FOR32 (uint32 offsets + base; int64 values)",
             "parallelism": "dp1",
         },
         "roofline": roof,
     }
-    if not args.no_cpu:
+    if not args.no_cpu and args.query == "two_hop":
         result["cpu_baseline"] = cpu_baseline(s, g, args.scale, args.cpu_seconds)
     print(json.dumps(result))
 
@@ -215,7 +223,24 @@ def run_distributed(args):
     s = GpuSession.on_torch_stream(local)
     m = args.edge_factor << args.scale
     n_nodes = 1 << args.scale
-    if args.layout == "node":
+    if args.query == "triangle":
+        # config 4: the rel table replicated on every rank ("replicate the
+        # rel hash set"); rank r counts its round-robin share of the oriented CSR rows
+        from capf_amd.table import triangle_count_part_async
+        full = s.rmat_rels(args.scale, rmat_seed(args.scale), thresholds(), 0, m)
+        if not args.int64:
+            full = full.compact()
+        s.sync()
+        partial = torch.zeros(1, dtype=torch.int64, device="cuda")
+
+        def step():
+            triangle_count_part_async(s, full, 0, n_nodes, world, rank, partial.data_ptr())
+            dist.all_reduce(partial, op=dist.ReduceOp.SUM)
+            return int(partial.item())
+        local_rels = m
+        layout = "replicated rels, oriented-CSR rows dealt round-robin over ranks; one int64 all-reduce"
+        compulsory = (16.0 * m + 8.0 * n_nodes) / world
+    elif args.layout == "node":
         # ingest (untimed): every rank generates the edge stream and keeps its two copies
         full = s.rmat_rels(args.scale, rmat_seed(args.scale), thresholds(), 0, m)
         in_copy, out_copy = node_partitioned_copies(full, n_nodes, world, rank, compact=not args.int64)
@@ -268,7 +293,7 @@ def run_distributed(args):
     if rank == 0:
         ms_per_step = elapsed * 1e3 / args.steps
         print(json.dumps({
-            "metric": METRIC,
+            "metric": METRIC if args.query == "two_hop" else TRI_METRIC,
             "value": count * args.steps / elapsed,
             "unit": "joined rows/s",
             "n_gpus": world,
@@ -282,7 +307,7 @@ def run_distributed(args):
             "data": (f"synthetic R-MAT s{args.scale} (Graph500 a/b/c=.57/.19/.19, edge factor "
                      f"{args.edge_factor}), generated in HBM and partitioned before timing"),
             "config": {
-                "workload": f"R-MAT s{args.scale} 2-hop MATCH (a)-->(b)-->(c) RETURN count(*)",
+                "workload": workload_name(args),
                 "scale": args.scale, "nodes": n_nodes, "rels": m, "count": count,
                 "rank0_rel_rows": local_rels,
                 "id_storage": "int64" if args.int64 else "FOR32",
@@ -304,6 +329,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--int64", action="store_true", help="keep the id columns int64 (no FOR32)")
     ap.add_argument("--dist", action="store_true", help="distributed path even at world size 1")
+    ap.add_argument("--query", choices=["two_hop", "triangle"], default="two_hop",
+                    help="two_hop: the headline (config 3); triangle: config 4")
     ap.add_argument("--layout", choices=["node", "edge"], default="node",
                     help="multi-GPU graph layout (N > 1): node-partitioned copies or edge-range shards")
     args = ap.parse_args()

@@ -117,6 +117,9 @@ _SIGS = {
     "capf_rmat_rel_table": (c_int32, [_S, c_int32, c_uint64, c_uint32, c_uint32, c_uint32, c_int64,
                                       c_int64, c_int64, c_char_p, c_char_p, c_char_p, _PT]),
     "capf_range_node_table": (c_int32, [_S, c_int64, c_int64, c_uint64, c_char_p, c_char_p, _PT]),
+    "capf_edge_list_parse": (c_int32, [_S, c_char_p, c_int64, c_char_p, c_char_p, c_char_p, c_char_p,
+                                       c_char_p, _PT]),
+    "capf_edge_list_read": (c_int32, [_S, c_char_p, c_char_p, c_char_p, c_char_p, c_char_p, c_char_p, _PT]),
     "capf_chain2_hist_len": (c_int64, [c_int64]),
     "capf_chain2_local_hists": (c_int32, [_S, _T, c_char_p, c_char_p, c_int64, c_int64, c_void_p,
                                           c_void_p, POINTER(c_int64)]),

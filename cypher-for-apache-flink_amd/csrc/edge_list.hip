@@ -1,0 +1,335 @@
+// edge_list.hip — CSV edge-list ingest straight into HBM.
+//
+// EdgeListDataSource.graph (flink-cypher/.../api/io/edgelist/EdgeListDataSource.scala:61-81)
+// reads a CSV through Flink's CsvTableSource with two LONG fields
+// (sourceStartNodeKey, sourceEndNodeKey), a field delimiter and a comment
+// prefix (:62-68), then gives every row a unique LONG id with
+// `safeAddIdColumn` = DataSet.zipWithUniqueId (flink-cypher/.../impl/TableOps.scala:217-238).
+// Here the raw bytes are copied to the device once and parsed there:
+//
+//   K1 k_el_count  per 16 KiB chunk (1024 threads × 16 B): '\n' count
+//   (scan)         chunk → first line index (int64 exclusive scan)
+//   K2 k_el_parse  per chunk: the chunk staged in LDS, its newline offsets
+//                  found by a block scan, then one thread per line ending in
+//                  the chunk parses (start, end) into the line's slot
+//   compaction     only when comment lines were skipped
+//
+// Row semantics follow Flink 1.7's CsvInputFormat / LongParser: a trailing
+// '\r' is stripped (line delimiter '\n'); a line starting with the comment
+// prefix is skipped; each LONG field is an optional '-' and decimal digits
+// up to the (possibly multi-byte) field delimiter; an empty field, any other
+// byte (whitespace included), an orphan sign, an int64 overflow or a line
+// with fewer than two fields fails the whole read (Flink raises a
+// ParseException in the job); text after the second field is not read
+// (only two fields are declared).  Rel ids are the data-line ordinals
+// 0..M-1: one valid zipWithUniqueId assignment (Flink's ids are unique but
+// depend on the task parallelism, so only uniqueness is specified).
+#include <cstdio>
+#include <vector>
+
+#include "capf_internal.h"
+#include "device_common.h"
+
+namespace capf {
+
+constexpr int EL_BLOCK = 1024;
+constexpr int EL_CHUNK = 16 * EL_BLOCK;  // bytes per workgroup
+constexpr int EL_MAX_DELIM = 8;          // field delimiter / comment prefix bytes
+
+enum : uint32_t {
+  EL_OK = 0, EL_TOO_SHORT = 1, EL_EMPTY = 2, EL_ILLEGAL_CHAR = 3, EL_OVERFLOW = 4, EL_ORPHAN_SIGN = 5
+};
+
+struct ElSpec {
+  uint8_t sep[EL_MAX_DELIM];
+  uint8_t comment[EL_MAX_DELIM];
+  int sep_len, comment_len;
+};
+
+// 16-bit mask of the '\n' bytes of a 16-B piece (bit i = byte i).
+__device__ inline uint32_t el_newlines(uint4 q) {
+  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t x = w[k] ^ 0x0A0A0A0Au;
+    // exact zero-byte detector (no borrow between bytes): 0x80 per zero byte
+    const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) m |= ((z >> (8 * b + 7)) & 1u) << (4 * k + b);
+  }
+  return m;
+}
+
+__global__ __launch_bounds__(EL_BLOCK) void k_el_count(const uint4 *text, int64_t *chunk_nl) {
+  __shared__ int64_t lds[17];
+  const uint4 q = text[(int64_t)blockIdx.x * EL_BLOCK + threadIdx.x];
+  const int64_t c = __popc(el_newlines(q));
+  const int64_t tot = block_reduce_sum(c, lds);
+  if (threadIdx.x == 0) chunk_nl[blockIdx.x] = tot;
+}
+
+// Byte at absolute position p: the staged chunk when p lies in it, else HBM
+// (only the first line of a chunk starts before it).
+struct ElBytes {
+  const uint8_t *g;
+  const uint8_t *lds;
+  int64_t c0;
+  __device__ uint8_t operator[](int64_t p) const { return p >= c0 ? lds[p - c0] : g[p]; }
+};
+
+__device__ inline bool el_delim_at(const ElBytes &b, int64_t p, int64_t end, const ElSpec &sp) {
+  if (p + sp.sep_len > end) return false;
+  for (int i = 0; i < sp.sep_len; ++i)
+    if (b[p + i] != sp.sep[i]) return false;
+  return true;
+}
+
+// LongParser.parseField: [p, end) up to the delimiter → value; *p advances
+// to the delimiter (or end).  Returns an EL_* code.
+__device__ inline uint32_t el_parse_long(const ElBytes &b, int64_t &p, int64_t end,
+                                         const ElSpec &sp, int64_t &out) {
+  if (p >= end || el_delim_at(b, p, end, sp)) return EL_EMPTY;
+  bool neg = false;
+  if (b[p] == '-') {
+    neg = true;
+    ++p;
+    if (p >= end || el_delim_at(b, p, end, sp)) return EL_ORPHAN_SIGN;
+  }
+  const uint64_t limit = neg ? 9223372036854775808ull : 9223372036854775807ull;
+  uint64_t mag = 0;
+  for (; p < end && !el_delim_at(b, p, end, sp); ++p) {
+    const uint32_t d = (uint32_t)b[p] - '0';
+    if (d > 9) return EL_ILLEGAL_CHAR;
+    if (mag > (limit - d) / 10) return EL_OVERFLOW;
+    mag = mag * 10 + d;
+  }
+  out = neg ? (int64_t)(0ull - mag) : (int64_t)mag;
+  return EL_OK;
+}
+
+__global__ __launch_bounds__(EL_BLOCK) void k_el_parse(const uint4 *text, int64_t n,
+                                                       const int64_t *chunk_off, int64_t nchunks,
+                                                       int64_t nlines, ElSpec sp, int64_t *src,
+                                                       int64_t *dst, uint8_t *keep,
+                                                       unsigned long long *err,
+                                                       unsigned long long *kept) {
+  __shared__ uint4 stage[EL_BLOCK];
+  __shared__ uint16_t nlp[EL_CHUNK];
+  __shared__ uint32_t lds_scan[17];
+  __shared__ unsigned long long lds_kept[17];
+  const int64_t b = blockIdx.x, c0 = b * EL_CHUNK;
+  const uint4 q = text[b * EL_BLOCK + threadIdx.x];
+  stage[threadIdx.x] = q;
+  uint32_t m = el_newlines(q), cnt;
+  uint32_t idx = block_exclusive_scan((uint32_t)__popc(m), lds_scan, cnt);
+  while (m) {
+    const int i = __ffs(m) - 1;
+    m &= m - 1;
+    nlp[idx++] = (uint16_t)(16 * threadIdx.x + i);
+  }
+  __syncthreads();
+  const ElBytes by{(const uint8_t *)text, (const uint8_t *)stage, c0};
+  const int64_t l0 = chunk_off[b];
+  // lines ending in this chunk: k < cnt end at a '\n'; the last chunk also
+  // owns the unterminated last line (its slot is nlines − 1)
+  const bool tail = b == nchunks - 1 && l0 + cnt < nlines;
+  const uint32_t items = cnt + (tail ? 1u : 0u);
+  unsigned long long mine = 0;
+  for (uint32_t k = threadIdx.x; k < items; k += EL_BLOCK) {
+    const int64_t gl = l0 + k;
+    int64_t end = k < cnt ? c0 + nlp[k] : n;
+    int64_t start;
+    if (k > 0) {
+      start = c0 + nlp[k - 1] + 1;
+    } else {  // walk back to the previous '\n' (in an earlier chunk)
+      start = c0;
+      while (start > 0 && by[start - 1] != '\n') --start;
+    }
+    if (end > start && by[end - 1] == '\r') --end;
+    bool comment = sp.comment_len > 0 && end - start >= sp.comment_len;
+    for (int i = 0; comment && i < sp.comment_len; ++i) comment = by[start + i] == sp.comment[i];
+    int64_t s = 0, d = 0;
+    uint32_t code = EL_OK;
+    if (!comment) {
+      int64_t p = start;
+      code = el_parse_long(by, p, end, sp, s);
+      if (code == EL_OK) {
+        if (p >= end) {
+          code = EL_TOO_SHORT;  // no delimiter before the end of the line
+        } else {
+          p += sp.sep_len;
+          code = p >= end ? EL_TOO_SHORT : el_parse_long(by, p, end, sp, d);
+        }
+      }
+      if (code != EL_OK) atomicMin(err, ((unsigned long long)gl << 8) | code);
+      mine += 1;
+    }
+    src[gl] = s;
+    dst[gl] = d;
+    keep[gl] = comment ? 0 : 1;
+  }
+  const unsigned long long tot = block_reduce_sum(mine, lds_kept);
+  if (threadIdx.x == 0 && tot) atomicAdd(kept, tot);
+}
+
+static const char *el_reason(uint32_t code) {
+  switch (code) {
+    case EL_TOO_SHORT: return "Row too short (fewer than 2 fields)";
+    case EL_EMPTY: return "empty LONG field";
+    case EL_ILLEGAL_CHAR: return "illegal character in a LONG field";
+    case EL_OVERFLOW: return "LONG value out of range";
+    case EL_ORPHAN_SIGN: return "orphan sign in a LONG field";
+    default: return "unknown parse error";
+  }
+}
+
+// Parses `nbytes` host bytes into (id, source, target) INT64 columns.
+static DataPtr edge_list_parse(Session *s, const char *bytes, int64_t nbytes, const ElSpec &sp) {
+  auto d = std::make_shared<Data>();
+  for (int i = 0; i < 3; ++i) d->cols.push_back(make_column(s, Type::Int64, 0, false));
+  if (nbytes == 0) return d;
+  const int64_t nchunks = (nbytes + EL_CHUNK - 1) / EL_CHUNK;
+  BufPtr text = s->alloc(nchunks * EL_CHUNK);
+  HIP_CHECK(hipMemcpyAsync(text->p, bytes, nbytes, hipMemcpyHostToDevice, s->stream));
+  if (nchunks * EL_CHUNK > nbytes)  // zero padding: never a '\n'
+    HIP_CHECK(hipMemsetAsync((char *)text->p + nbytes, 0, nchunks * EL_CHUNK - nbytes, s->stream));
+  BufPtr cnt = s->alloc(8 * nchunks), off = s->alloc(8 * nchunks);
+  {
+    KernelTimer kt(s, "el_count", (double)nchunks * EL_CHUNK);
+    hipLaunchKernelGGL(k_el_count, dim3((unsigned)nchunks), dim3(EL_BLOCK), 0, s->stream,
+                       (const uint4 *)text->p, (int64_t *)cnt->p);
+    KERNEL_CHECK();
+  }
+  const int64_t nl = exclusive_scan_i64(s, (const int64_t *)cnt->p, (int64_t *)off->p, nchunks);
+  const int64_t nlines = nl + (bytes[nbytes - 1] != '\n' ? 1 : 0);
+  ColPtr src = make_column(s, Type::Int64, nlines, false);
+  ColPtr dst = make_column(s, Type::Int64, nlines, false);
+  BufPtr keep = s->alloc(std::max<int64_t>(nlines, 1));
+  BufPtr flags = s->alloc(16);
+  unsigned long long *d_err = (unsigned long long *)flags->p, *d_kept = d_err + 1;
+  const unsigned long long init[2] = {~0ull, 0ull};
+  HIP_CHECK(hipMemcpyAsync(d_err, init, 16, hipMemcpyHostToDevice, s->stream));
+  if (nlines > 0) {
+    KernelTimer kt(s, "el_parse", (double)nchunks * EL_CHUNK + 17.0 * nlines);
+    hipLaunchKernelGGL(k_el_parse, dim3((unsigned)nchunks), dim3(EL_BLOCK), 0, s->stream,
+                       (const uint4 *)text->p, nbytes, (const int64_t *)off->p, nchunks, nlines, sp,
+                       (int64_t *)src->data->p, (int64_t *)dst->data->p, (uint8_t *)keep->p, d_err,
+                       d_kept);
+    KERNEL_CHECK();
+  }
+  unsigned long long h[2];
+  HIP_CHECK(hipMemcpyAsync(h, d_err, 16, hipMemcpyDeviceToHost, s->stream));
+  s->sync();
+  if (h[0] != ~0ull) {
+    const int64_t line = (int64_t)(h[0] >> 8);
+    char msg[160];
+    snprintf(msg, sizeof msg, "edge list line %lld could not be parsed: %s",
+             (long long)line + 1, el_reason((uint32_t)(h[0] & 0xFF)));
+    illegal(msg);
+  }
+  const int64_t m = (int64_t)h[1];
+  if (m != nlines) {  // comment lines: compact the data lines
+    int64_t got = 0;
+    BufPtr idx = compact_flags(s, (const uint8_t *)keep->p, nlines, &got);
+    if (got != m) fail(CAPF_ERR_INTERNAL, "edge list: kept-line count mismatch");
+    src = gather_column(s, src, (const int64_t *)idx->p, m);
+    dst = gather_column(s, dst, (const int64_t *)idx->p, m);
+  }
+  auto id = std::make_shared<Column>();
+  id->type = Type::Int64;
+  id->n = m;
+  if (m > 0) id->data = iota_index(s, 0, m);
+  d->nrows = m;
+  d->cols = {id, src, dst};
+  s->sync();
+  return d;
+}
+
+static ElSpec el_spec(const char *sep, const char *comment) {
+  ElSpec sp{};
+  if (!sep || !*sep) illegal("edge list: the field delimiter (option `sep`) must be non-empty");
+  sp.sep_len = (int)strlen(sep);
+  sp.comment_len = comment ? (int)strlen(comment) : 0;
+  if (sp.sep_len > EL_MAX_DELIM || sp.comment_len > EL_MAX_DELIM)
+    illegal("edge list: delimiter / comment prefix longer than 8 bytes");
+  if (strchr(sep, '\n') || (comment && strchr(comment, '\n')))
+    illegal("edge list: delimiter / comment prefix must not contain the line delimiter");
+  memcpy(sp.sep, sep, sp.sep_len);
+  if (sp.comment_len) memcpy(sp.comment, comment, sp.comment_len);
+  return sp;
+}
+
+static capf_table *edge_list_table(Session *s, DataPtr d, const char *id_col, const char *src_col,
+                                   const char *dst_col) {
+  auto n = std::make_shared<Node>();
+  n->s = s;
+  n->kind = Kind::Source;
+  n->names = {id_col, src_col, dst_col};
+  n->types = {Type::Int64, Type::Int64, Type::Int64};
+  n->result = d;
+  auto *t = new capf_table;
+  t->node = n;
+  return t;
+}
+
+}  // namespace capf
+
+using namespace capf;
+
+extern "C" capf_status capf_edge_list_parse(capf_session *cs, const char *bytes, int64_t nbytes,
+                                            const char *sep, const char *comment,
+                                            const char *id_col, const char *src_col,
+                                            const char *dst_col, capf_table **out) {
+  try {
+    if (!cs || !out || !id_col || !src_col || !dst_col || (nbytes > 0 && !bytes))
+      illegal("null argument");
+    if (nbytes < 0) illegal("negative byte count");
+    const ElSpec sp = el_spec(sep, comment);
+    Session *s = &cs->impl;
+    *out = edge_list_table(s, edge_list_parse(s, bytes, nbytes, sp), id_col, src_col, dst_col);
+    return CAPF_OK;
+  } catch (const capf::Error &e) {
+    return record_error(e.code, e.what());
+  }
+}
+
+extern "C" capf_status capf_edge_list_read(capf_session *cs, const char *path, const char *sep,
+                                           const char *comment, const char *id_col,
+                                           const char *src_col, const char *dst_col,
+                                           capf_table **out) {
+  try {
+    if (!cs || !out || !path || !id_col || !src_col || !dst_col) illegal("null argument");
+    const ElSpec sp = el_spec(sep, comment);
+    FILE *f = fopen(path, "rb");
+    if (!f) illegal(std::string("edge list: cannot open ") + path);
+    fseek(f, 0, SEEK_END);
+    const long len = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    // pinned staging: one DMA of the whole file
+    char *host = nullptr;
+    if (len > 0 && hipHostMalloc((void **)&host, (size_t)len, hipHostMallocDefault) != hipSuccess) {
+      fclose(f);
+      fail(CAPF_ERR_OOM, "edge list: pinned host buffer");
+    }
+    const size_t got = len > 0 ? fread(host, 1, (size_t)len, f) : 0;
+    fclose(f);
+    if ((long)got != len) {
+      (void)hipHostFree(host);
+      illegal(std::string("edge list: short read of ") + path);
+    }
+    Session *s = &cs->impl;
+    DataPtr d;
+    try {
+      d = edge_list_parse(s, host, len, sp);
+    } catch (...) {
+      (void)hipHostFree(host);
+      throw;
+    }
+    (void)hipHostFree(host);
+    *out = edge_list_table(s, d, id_col, src_col, dst_col);
+    return CAPF_OK;
+  } catch (const capf::Error &e) {
+    return record_error(e.code, e.what());
+  }
+}

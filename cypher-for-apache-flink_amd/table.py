@@ -11,6 +11,7 @@ drives it unchanged.  Every operation returns a new immutable table; nothing
 executes on the GPU until `size` / `rows` (lazy, like the Flink Table API).
 """
 import ctypes
+import os
 from ctypes import byref, c_char_p, c_double, c_int32, c_int64, c_uint64, c_void_p
 
 import numpy as np
@@ -138,6 +139,19 @@ class GpuSession:
         h = c_void_p()
         _lib.call("capf_range_node_table", self._h, int(base), int(n), int(seed), id_col.encode(),
                   label_col.encode() if label_col else None, byref(h))
+        return GpuTable(self, h)
+
+    def edge_list(self, source, sep, comment=None, cols=("id", "source", "target")):
+        """Relationship table parsed on the GPU from a CSV edge list: `source`
+        is a path (str) or the file's bytes (capf_edge_list_read / _parse)."""
+        h = c_void_p()
+        com = comment.encode() if comment else None
+        names = [c.encode() for c in cols]
+        if isinstance(source, (bytes, bytearray, memoryview)):
+            buf = bytes(source)
+            _lib.call("capf_edge_list_parse", self._h, buf, len(buf), sep.encode(), com, *names, byref(h))
+        else:
+            _lib.call("capf_edge_list_read", self._h, os.fsencode(source), sep.encode(), com, *names, byref(h))
         return GpuTable(self, h)
 
     # -- profiling ----------------------------------------------------------

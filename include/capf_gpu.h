@@ -276,6 +276,24 @@ capf_status capf_range_node_table(capf_session *s, int64_t base, int64_t n, uint
                                   const char *id_col, const char *label_col,
                                   capf_table **out);
 
+/* ------------------------------------------------------ edge-list ingest
+ * EdgeListDataSource.graph (flink-cypher/.../api/io/edgelist/EdgeListDataSource.scala:61-81):
+ * a CSV of two LONG fields per line (start, end), field delimiter `sep`
+ * (option "sep"), lines beginning with `comment` (option "comment", may be
+ * NULL) skipped — CsvTableSource.builder().field(.., LONG) ×2
+ * .fieldDelimiter(sep).commentPrefix(comment) (:62-68).  Parsed on the GPU
+ * into a relationship table (id_col, src_col, dst_col); ids are the data-line
+ * ordinals 0..M-1, one valid zipWithUniqueId assignment (safeAddIdColumn,
+ * flink-cypher/.../impl/TableOps.scala:217-238).  A malformed line fails the
+ * call with CAPF_ERR_ILLEGAL_ARGUMENT naming the line (Flink: ParseException).
+ * capf_edge_list_parse takes the file's bytes; capf_edge_list_read the path. */
+capf_status capf_edge_list_parse(capf_session *s, const char *bytes, int64_t nbytes,
+                                 const char *sep, const char *comment, const char *id_col,
+                                 const char *src_col, const char *dst_col, capf_table **out);
+capf_status capf_edge_list_read(capf_session *s, const char *path, const char *sep,
+                                const char *comment, const char *id_col, const char *src_col,
+                                const char *dst_col, capf_table **out);
+
 /* ------------------------------------------------ multi-GPU partial counts
  * Building blocks of the hash-partitioned 2-hop count: the
  * caller (one process per GPU, torch.distributed/RCCL) exchanges the

@@ -120,6 +120,8 @@ _SIGS = {
     "capf_edge_list_parse": (c_int32, [_S, c_char_p, c_int64, c_char_p, c_char_p, c_char_p, c_char_p,
                                        c_char_p, _PT]),
     "capf_edge_list_read": (c_int32, [_S, c_char_p, c_char_p, c_char_p, c_char_p, c_char_p, c_char_p, _PT]),
+    "capf_var_length_reach": (c_int32, [_S, _T, c_char_p, c_char_p, _T, c_char_p, _T, c_char_p, c_int32,
+                                        c_int32, c_char_p, c_char_p, _PT]),
     "capf_chain2_hist_len": (c_int64, [c_int64]),
     "capf_chain2_local_hists": (c_int32, [_S, _T, c_char_p, c_char_p, c_int64, c_int64, c_void_p,
                                           c_void_p, POINTER(c_int64)]),

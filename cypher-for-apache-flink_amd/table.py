@@ -154,6 +154,16 @@ class GpuSession:
             _lib.call("capf_edge_list_read", self._h, os.fsencode(source), sep.encode(), com, *names, byref(h))
         return GpuTable(self, h)
 
+    def var_length_reach(self, rels, src_col, dst_col, sources, source_id_col, targets, target_id_col,
+                         lower, upper, out_source_col, out_reach_col):
+        """Fused VarLengthExpand → Distinct(a, b) → Aggregate(a, count(*))
+        (capf_var_length_reach): one row (a, reach) per source reaching a target."""
+        h = c_void_p()
+        _lib.call("capf_var_length_reach", self._h, rels._h, src_col.encode(), dst_col.encode(), sources._h,
+                  source_id_col.encode(), targets._h, target_id_col.encode(), int(lower), int(upper),
+                  out_source_col.encode(), out_reach_col.encode(), byref(h))
+        return GpuTable(self, h)
+
     # -- profiling ----------------------------------------------------------
     def set_profiling(self, on):
         _lib.call("capf_session_set_profiling", self._h, 1 if on else 0)

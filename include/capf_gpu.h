@@ -294,6 +294,25 @@ capf_status capf_edge_list_read(capf_session *s, const char *path, const char *s
                                 const char *comment, const char *id_col, const char *src_col,
                                 const char *dst_col, capf_table **out);
 
+/* ----------------------------------------- fused var-length reach (config 5)
+ * The fused form of
+ *   VarLengthExpand(a, [r*lower..upper], b)   VarLengthExpandPlanner.scala:82-259
+ *   → Distinct(a, b)                          FlinkTable.scala:189-196
+ *   → Aggregate(by a, count(*) AS reach)      FlinkTable.scala:123-150
+ * over a directed relationship scan `rels` (src_col → dst_col), the source
+ * node scan `sources` and the target node scan `targets`: one row
+ * (out_source_col = a's id, out_reach_col = #distinct b) per source a that
+ * reaches at least one target — the rows the relational plan produces,
+ * without materialising the paths.  Only lower = 1 is fused (for it, rel
+ * isomorphism cannot change the distinct pairs); other bounds return
+ * CAPF_ERR_NOT_IMPLEMENTED and the caller plans the join chain.            */
+capf_status capf_var_length_reach(capf_session *s, capf_table *rels, const char *src_col,
+                                  const char *dst_col, capf_table *sources,
+                                  const char *source_id_col, capf_table *targets,
+                                  const char *target_id_col, int32_t lower, int32_t upper,
+                                  const char *out_source_col, const char *out_reach_col,
+                                  capf_table **out);
+
 /* ------------------------------------------------ multi-GPU partial counts
  * Building blocks of the hash-partitioned 2-hop count: the
  * caller (one process per GPU, torch.distributed/RCCL) exchanges the

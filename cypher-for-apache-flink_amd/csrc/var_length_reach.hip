@@ -20,7 +20,8 @@
 //   CSR    in-edges by target (count, scan, fill)
 //   state  visited / frontier / next: D nodes × K words of 64 source bits,
 //          node-major (a node's K words are contiguous) in HBM
-//   level  thread per (node y, word k): next = OR_{x ∈ in(y)} frontier[x][k]
+//   push1  level 1: rels of the batch's sources set their bits (M atomics)
+//   level  levels 2..u, thread per (node y, word k): next = OR_{x ∈ in(y)} frontier[x][k]
 //          & ~visited[y][k]; visited |= next  — K consecutive threads share
 //          y's CSR row and read x's frontier words as one coalesced run
 //   count  block per word k: wave ballots of (visited bit j ∧ target(y)),
@@ -89,17 +90,40 @@ __global__ void k_vr_fill(const uint32_t *src, const uint32_t *dst, int64_t m, u
     cols[atomicAdd(&cursor[dst[i]], 1u)] = src[i];
 }
 
-// frontier bit of source j (global source list index s0 + j) at its node
-__global__ void k_vr_seed(const int64_t *src_nodes, int64_t s0, int64_t ns, int64_t K,
-                          unsigned long long *frontier) {
+// Level 1 by push (the frontier is only the batch's sources): every rel
+// (x → y) whose x is source j of the batch sets bit j of y in visited and in
+// the level-2 frontier — M atomics instead of a pull over M·K words.
+__global__ void k_vr_srcpos(const int64_t *src_nodes, int64_t ns, int32_t *srcpos) {
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < ns;
        j += (int64_t)gridDim.x * blockDim.x)
-    atomicOr(&frontier[src_nodes[s0 + j] * K + (j >> 6)], 1ull << (j & 63));
+    srcpos[src_nodes[j]] = (int32_t)j;
+}
+
+__global__ void k_vr_push1(const uint32_t *si, const uint32_t *di, int64_t m, const int32_t *srcpos,
+                           int64_t s0, int64_t nb, int64_t K, unsigned long long *visited,
+                           unsigned long long *frontier) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j = (int64_t)srcpos[si[i]] - s0;
+    if (j < 0 || j >= nb) continue;
+    const int64_t w = (int64_t)di[i] * K + (j >> 6);
+    const unsigned long long bit = 1ull << (j & 63);
+    atomicOr(&visited[w], bit);
+    atomicOr(&frontier[w], bit);
+  }
 }
 
 constexpr int VR_ILP = 16;
 
+// rows by decreasing in-degree: the hub rows (long dependent load chains)
+// start first and overlap with the bulk instead of forming the tail
+__global__ void k_vr_degkey(const uint32_t *rowptr, uint32_t D, uint64_t *key) {
+  for (uint32_t y = blockIdx.x * blockDim.x + threadIdx.x; y < D; y += gridDim.x * blockDim.x)
+    key[y] = ((uint64_t)(0xFFFFFFFFu - (rowptr[y + 1] - rowptr[y])) << 32) | y;
+}
+
 __global__ __launch_bounds__(256) void k_vr_level(const uint32_t *rowptr, const uint32_t *cols,
+                                                  const uint64_t *order,
                                                   const unsigned long long *frontier,
                                                   unsigned long long *next,
                                                   unsigned long long *visited, int64_t D,
@@ -107,7 +131,9 @@ __global__ __launch_bounds__(256) void k_vr_level(const uint32_t *rowptr, const 
   const int64_t total = D * K;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t y = t / K, k = t - y * K;
+    const int64_t r = t / K, k = t - r * K;
+    const int64_t y = (int64_t)(uint32_t)order[r];
+    const int64_t ty = y * K + k;
     unsigned long long acc = 0;
     const uint32_t e1 = rowptr[y + 1];
     uint32_t e = rowptr[y];
@@ -125,10 +151,10 @@ __global__ __launch_bounds__(256) void k_vr_level(const uint32_t *rowptr, const 
       for (int i = 0; i < VR_ILP; ++i) acc |= f[i];
     }
     for (; e < e1; ++e) acc |= frontier[(int64_t)cols[e] * K + k];
-    const unsigned long long v = visited[t];
+    const unsigned long long v = visited[ty];
     const unsigned long long nv = acc & ~v;
-    if (!last) next[t] = nv;
-    if (nv) visited[t] = v | nv;
+    if (!last) next[ty] = nv;
+    if (nv) visited[ty] = v | nv;
   }
 }
 
@@ -256,9 +282,19 @@ static DataPtr var_length_reach(Session *s, const ColPtr &rsrc, const ColPtr &rd
                        (const uint32_t *)di->p, m, (uint32_t *)cursor->p, (uint32_t *)cols->p);
     KERNEL_CHECK();
   }
-  si.reset();
-  di.reset();
   cursor.reset();
+  BufPtr order;
+  {
+    BufPtr dkey = s->alloc(8 * (int64_t)D);
+    order = s->alloc(8 * (int64_t)D);
+    hipLaunchKernelGGL(k_vr_degkey, dim3(grid_for(D, 256)), dim3(256), 0, s->stream,
+                       (const uint32_t *)rowptr->p, D, (uint64_t *)dkey->p);
+    KERNEL_CHECK();
+    vr_rocprim(s, [&](void *t, size_t &n) {
+      return rocprim::radix_sort_keys(t, n, (const uint64_t *)dkey->p, (uint64_t *)order->p,
+                                      (size_t)D, 0, 64, s->stream);
+    });
+  }
   // 4. MS-BFS in batches of 64·K sources
   BufPtr reach = s->alloc(8 * std::max<int64_t>(ns, 1));
   const int64_t kmax = std::max<int64_t>(1, (int64_t)(VR_STATE_BUDGET / (24.0 * D)));
@@ -266,18 +302,28 @@ static DataPtr var_length_reach(Session *s, const ColPtr &rsrc, const ColPtr &rd
   BufPtr fa = s->alloc(8 * (int64_t)D * K), fb = s->alloc(8 * (int64_t)D * K);
   BufPtr vis = s->alloc(8 * (int64_t)D * K);
   const unsigned glev = grid_for((int64_t)D * K, 256, (int64_t)s->num_cus * 32);
+  BufPtr srcpos = s->alloc(4 * (int64_t)D);
+  HIP_CHECK(hipMemsetAsync(srcpos->p, 0xFF, 4 * (size_t)D, s->stream));
+  hipLaunchKernelGGL(k_vr_srcpos, dim3(grid_for(ns, 256)), dim3(256), 0, s->stream,
+                     (const int64_t *)src_nodes->p, ns, (int32_t *)srcpos->p);
+  KERNEL_CHECK();
   for (int64_t s0 = 0; s0 < ns; s0 += 64 * K) {
     const int64_t nb = std::min<int64_t>(64 * K, ns - s0);
-    HIP_CHECK(hipMemsetAsync(fa->p, 0, 8 * (size_t)D * K, s->stream));
+    HIP_CHECK(hipMemsetAsync(fb->p, 0, 8 * (size_t)D * K, s->stream));
     HIP_CHECK(hipMemsetAsync(vis->p, 0, 8 * (size_t)D * K, s->stream));
-    hipLaunchKernelGGL(k_vr_seed, dim3(grid_for(nb, 256)), dim3(256), 0, s->stream,
-                       (const int64_t *)src_nodes->p, s0, nb, K, (unsigned long long *)fa->p);
-    KERNEL_CHECK();
-    unsigned long long *cur = (unsigned long long *)fa->p, *nxt = (unsigned long long *)fb->p;
-    for (int l = 1; l <= upper; ++l) {
+    {
+      KernelTimer kt(s, "vr_push1", 12.0 * m);
+      hipLaunchKernelGGL(k_vr_push1, dim3(g), dim3(256), 0, s->stream, (const uint32_t *)si->p,
+                         (const uint32_t *)di->p, m, (const int32_t *)srcpos->p, s0, nb, K,
+                         (unsigned long long *)vis->p, (unsigned long long *)fb->p);
+      KERNEL_CHECK();
+    }
+    unsigned long long *cur = (unsigned long long *)fb->p, *nxt = (unsigned long long *)fa->p;
+    for (int l = 2; l <= upper; ++l) {
       KernelTimer kt(s, "vr_level", 8.0 * K * ((double)m + 3.0 * D));
       hipLaunchKernelGGL(k_vr_level, dim3(glev), dim3(256), 0, s->stream,
-                         (const uint32_t *)rowptr->p, (const uint32_t *)cols->p, cur, nxt,
+                         (const uint32_t *)rowptr->p, (const uint32_t *)cols->p,
+                         (const uint64_t *)order->p, cur, nxt,
                          (unsigned long long *)vis->p, (int64_t)D, K, l == upper ? 1 : 0);
       KERNEL_CHECK();
       std::swap(cur, nxt);

@@ -24,7 +24,13 @@
 // (only two fields are declared).  Rel ids are the data-line ordinals
 // 0..M-1: one valid zipWithUniqueId assignment (Flink's ids are unique but
 // depend on the task parallelism, so only uniqueness is specified).
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <atomic>
 #include <cstdio>
+#include <thread>
 #include <vector>
 
 #include "capf_internal.h"
@@ -69,16 +75,25 @@ __global__ __launch_bounds__(EL_BLOCK) void k_el_count(const uint4 *text, int64_
   if (threadIdx.x == 0) chunk_nl[blockIdx.x] = tot;
 }
 
-// Byte at absolute position p: the staged chunk when p lies in it, else HBM
-// (only the first line of a chunk starts before it).
-struct ElBytes {
+// Byte at absolute position p.  ElLds: lines inside the staged chunk (the
+// common case — the accessor indexes the __shared__ stage directly, so the
+// loads are ds_read_u8, not flat loads); ElAny: the first line of a chunk,
+// which may start in an earlier chunk (HBM below c0).
+struct ElLds {
+  const uint8_t *lds;
+  int64_t c0;
+  __device__ uint8_t operator[](int64_t p) const { return lds[p - c0]; }
+};
+struct ElAny {
   const uint8_t *g;
   const uint8_t *lds;
   int64_t c0;
   __device__ uint8_t operator[](int64_t p) const { return p >= c0 ? lds[p - c0] : g[p]; }
 };
 
-__device__ inline bool el_delim_at(const ElBytes &b, int64_t p, int64_t end, const ElSpec &sp) {
+template <int SEP1, class B>
+__device__ inline bool el_delim_at(const B &b, int64_t p, int64_t end, const ElSpec &sp) {
+  if (SEP1) return p < end && b[p] == sp.sep[0];
   if (p + sp.sep_len > end) return false;
   for (int i = 0; i < sp.sep_len; ++i)
     if (b[p + i] != sp.sep[i]) return false;
@@ -87,19 +102,22 @@ __device__ inline bool el_delim_at(const ElBytes &b, int64_t p, int64_t end, con
 
 // LongParser.parseField: [p, end) up to the delimiter → value; *p advances
 // to the delimiter (or end).  Returns an EL_* code.
-__device__ inline uint32_t el_parse_long(const ElBytes &b, int64_t &p, int64_t end,
-                                         const ElSpec &sp, int64_t &out) {
-  if (p >= end || el_delim_at(b, p, end, sp)) return EL_EMPTY;
+template <int SEP1, class B>
+__device__ inline uint32_t el_parse_long(const B &b, int64_t &p, int64_t end, const ElSpec &sp,
+                                         int64_t &out) {
+  if (p >= end || el_delim_at<SEP1>(b, p, end, sp)) return EL_EMPTY;
   bool neg = false;
   if (b[p] == '-') {
     neg = true;
     ++p;
-    if (p >= end || el_delim_at(b, p, end, sp)) return EL_ORPHAN_SIGN;
+    if (p >= end || el_delim_at<SEP1>(b, p, end, sp)) return EL_ORPHAN_SIGN;
   }
   const uint64_t limit = neg ? 9223372036854775808ull : 9223372036854775807ull;
   uint64_t mag = 0;
-  for (; p < end && !el_delim_at(b, p, end, sp); ++p) {
-    const uint32_t d = (uint32_t)b[p] - '0';
+  for (; p < end; ++p) {
+    const uint8_t ch = b[p];
+    if (SEP1 ? ch == sp.sep[0] : el_delim_at<SEP1>(b, p, end, sp)) break;
+    const uint32_t d = (uint32_t)ch - '0';
     if (d > 9) return EL_ILLEGAL_CHAR;
     if (mag > (limit - d) / 10) return EL_OVERFLOW;
     mag = mag * 10 + d;
@@ -108,6 +126,24 @@ __device__ inline uint32_t el_parse_long(const ElBytes &b, int64_t &p, int64_t e
   return EL_OK;
 }
 
+// One line [start, end): comment test, two LONG fields.
+template <int SEP1, class B>
+__device__ inline uint32_t el_line(const B &by, int64_t start, int64_t end, const ElSpec &sp,
+                                   bool &comment, int64_t &s, int64_t &d) {
+  if (end > start && by[end - 1] == '\r') --end;
+  comment = sp.comment_len > 0 && end - start >= sp.comment_len;
+  for (int i = 0; comment && i < sp.comment_len; ++i) comment = by[start + i] == sp.comment[i];
+  s = d = 0;
+  if (comment) return EL_OK;
+  int64_t p = start;
+  uint32_t code = el_parse_long<SEP1>(by, p, end, sp, s);
+  if (code != EL_OK) return code;
+  if (p >= end) return EL_TOO_SHORT;  // no delimiter before the end of the line
+  p += sp.sep_len;
+  return p >= end ? EL_TOO_SHORT : el_parse_long<SEP1>(by, p, end, sp, d);
+}
+
+template <int SEP1>
 __global__ __launch_bounds__(EL_BLOCK) void k_el_parse(const uint4 *text, int64_t n,
                                                        const int64_t *chunk_off, int64_t nchunks,
                                                        int64_t nlines, ElSpec sp, int64_t *src,
@@ -129,7 +165,7 @@ __global__ __launch_bounds__(EL_BLOCK) void k_el_parse(const uint4 *text, int64_
     nlp[idx++] = (uint16_t)(16 * threadIdx.x + i);
   }
   __syncthreads();
-  const ElBytes by{(const uint8_t *)text, (const uint8_t *)stage, c0};
+  const ElLds fast{(const uint8_t *)stage, c0};
   const int64_t l0 = chunk_off[b];
   // lines ending in this chunk: k < cnt end at a '\n'; the last chunk also
   // owns the unterminated last line (its slot is nlines − 1)
@@ -138,33 +174,20 @@ __global__ __launch_bounds__(EL_BLOCK) void k_el_parse(const uint4 *text, int64_
   unsigned long long mine = 0;
   for (uint32_t k = threadIdx.x; k < items; k += EL_BLOCK) {
     const int64_t gl = l0 + k;
-    int64_t end = k < cnt ? c0 + nlp[k] : n;
-    int64_t start;
+    const int64_t end = k < cnt ? c0 + nlp[k] : n;
+    bool comment;
+    int64_t s, d;
+    uint32_t code;
     if (k > 0) {
-      start = c0 + nlp[k - 1] + 1;
+      code = el_line<SEP1>(fast, c0 + nlp[k - 1] + 1, end, sp, comment, s, d);
     } else {  // walk back to the previous '\n' (in an earlier chunk)
-      start = c0;
-      while (start > 0 && by[start - 1] != '\n') --start;
+      const ElAny any{(const uint8_t *)text, (const uint8_t *)stage, c0};
+      int64_t start = c0;
+      while (start > 0 && any[start - 1] != '\n') --start;
+      code = el_line<SEP1>(any, start, end, sp, comment, s, d);
     }
-    if (end > start && by[end - 1] == '\r') --end;
-    bool comment = sp.comment_len > 0 && end - start >= sp.comment_len;
-    for (int i = 0; comment && i < sp.comment_len; ++i) comment = by[start + i] == sp.comment[i];
-    int64_t s = 0, d = 0;
-    uint32_t code = EL_OK;
-    if (!comment) {
-      int64_t p = start;
-      code = el_parse_long(by, p, end, sp, s);
-      if (code == EL_OK) {
-        if (p >= end) {
-          code = EL_TOO_SHORT;  // no delimiter before the end of the line
-        } else {
-          p += sp.sep_len;
-          code = p >= end ? EL_TOO_SHORT : el_parse_long(by, p, end, sp, d);
-        }
-      }
-      if (code != EL_OK) atomicMin(err, ((unsigned long long)gl << 8) | code);
-      mine += 1;
-    }
+    if (code != EL_OK) atomicMin(err, ((unsigned long long)gl << 8) | code);
+    mine += comment ? 0 : 1;
     src[gl] = s;
     dst[gl] = d;
     keep[gl] = comment ? 0 : 1;
@@ -185,15 +208,14 @@ static const char *el_reason(uint32_t code) {
 }
 
 // Parses `nbytes` host bytes into (id, source, target) INT64 columns.
-static DataPtr edge_list_parse(Session *s, const char *bytes, int64_t nbytes, const ElSpec &sp) {
+// Parses the device copy `text` (nbytes, zero-padded to whole chunks) into
+// (id, source, target) INT64 columns.  last = the file's last byte.
+static DataPtr edge_list_parse_device(Session *s, const BufPtr &text, int64_t nbytes, char last,
+                                      const ElSpec &sp) {
   auto d = std::make_shared<Data>();
   for (int i = 0; i < 3; ++i) d->cols.push_back(make_column(s, Type::Int64, 0, false));
   if (nbytes == 0) return d;
   const int64_t nchunks = (nbytes + EL_CHUNK - 1) / EL_CHUNK;
-  BufPtr text = s->alloc(nchunks * EL_CHUNK);
-  HIP_CHECK(hipMemcpyAsync(text->p, bytes, nbytes, hipMemcpyHostToDevice, s->stream));
-  if (nchunks * EL_CHUNK > nbytes)  // zero padding: never a '\n'
-    HIP_CHECK(hipMemsetAsync((char *)text->p + nbytes, 0, nchunks * EL_CHUNK - nbytes, s->stream));
   BufPtr cnt = s->alloc(8 * nchunks), off = s->alloc(8 * nchunks);
   {
     KernelTimer kt(s, "el_count", (double)nchunks * EL_CHUNK);
@@ -202,7 +224,7 @@ static DataPtr edge_list_parse(Session *s, const char *bytes, int64_t nbytes, co
     KERNEL_CHECK();
   }
   const int64_t nl = exclusive_scan_i64(s, (const int64_t *)cnt->p, (int64_t *)off->p, nchunks);
-  const int64_t nlines = nl + (bytes[nbytes - 1] != '\n' ? 1 : 0);
+  const int64_t nlines = nl + (last != '\n' ? 1 : 0);
   ColPtr src = make_column(s, Type::Int64, nlines, false);
   ColPtr dst = make_column(s, Type::Int64, nlines, false);
   BufPtr keep = s->alloc(std::max<int64_t>(nlines, 1));
@@ -212,7 +234,8 @@ static DataPtr edge_list_parse(Session *s, const char *bytes, int64_t nbytes, co
   HIP_CHECK(hipMemcpyAsync(d_err, init, 16, hipMemcpyHostToDevice, s->stream));
   if (nlines > 0) {
     KernelTimer kt(s, "el_parse", (double)nchunks * EL_CHUNK + 17.0 * nlines);
-    hipLaunchKernelGGL(k_el_parse, dim3((unsigned)nchunks), dim3(EL_BLOCK), 0, s->stream,
+    hipLaunchKernelGGL(sp.sep_len == 1 ? k_el_parse<1> : k_el_parse<0>, dim3((unsigned)nchunks),
+                       dim3(EL_BLOCK), 0, s->stream,
                        (const uint4 *)text->p, nbytes, (const int64_t *)off->p, nchunks, nlines, sp,
                        (int64_t *)src->data->p, (int64_t *)dst->data->p, (uint8_t *)keep->p, d_err,
                        d_kept);
@@ -244,6 +267,90 @@ static DataPtr edge_list_parse(Session *s, const char *bytes, int64_t nbytes, co
   d->cols = {id, src, dst};
   s->sync();
   return d;
+}
+
+static BufPtr el_text_buffer(Session *s, int64_t nbytes) {
+  const int64_t nchunks = (nbytes + EL_CHUNK - 1) / EL_CHUNK;
+  BufPtr text = s->alloc(std::max<int64_t>(nchunks, 1) * EL_CHUNK);
+  if (nchunks * EL_CHUNK > nbytes)  // zero padding: never a '\n'
+    HIP_CHECK(hipMemsetAsync((char *)text->p + nbytes, 0, nchunks * EL_CHUNK - nbytes, s->stream));
+  return text;
+}
+
+static DataPtr edge_list_parse(Session *s, const char *bytes, int64_t nbytes, const ElSpec &sp) {
+  BufPtr text = el_text_buffer(s, nbytes);
+  if (nbytes > 0)
+    HIP_CHECK(hipMemcpyAsync(text->p, bytes, nbytes, hipMemcpyHostToDevice, s->stream));
+  return edge_list_parse_device(s, text, nbytes, nbytes > 0 ? bytes[nbytes - 1] : '\n', sp);
+}
+
+// File → HBM: 64 MiB pieces read by parallel pread()s into two pinned staging
+// buffers, each DMA'd while the next piece is read (no whole-file pinning).
+constexpr int64_t EL_PIECE = 64ll << 20;
+constexpr int EL_READERS = 8;
+
+static DataPtr edge_list_read_file(Session *s, const char *path, const ElSpec &sp) {
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) illegal(std::string("edge list: cannot open ") + path);
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    close(fd);
+    illegal(std::string("edge list: cannot stat ") + path);
+  }
+  const int64_t len = (int64_t)st.st_size;
+  char *stage[2] = {nullptr, nullptr};
+  hipEvent_t done[2] = {nullptr, nullptr};
+  auto cleanup = [&]() {
+    for (int b = 0; b < 2; ++b) {
+      if (done[b]) (void)hipEventDestroy(done[b]);
+      if (stage[b]) (void)hipHostFree(stage[b]);
+    }
+    close(fd);
+  };
+  try {
+    BufPtr text = el_text_buffer(s, len);
+    const int64_t piece = std::min<int64_t>(EL_PIECE, std::max<int64_t>(len, 1));
+    for (int b = 0; b < 2; ++b) {
+      HIP_CHECK(hipHostMalloc((void **)&stage[b], (size_t)piece, hipHostMallocDefault));
+      HIP_CHECK(hipEventCreateWithFlags(&done[b], hipEventDisableTiming));
+    }
+    char last = '\n';
+    for (int64_t off = 0, i = 0; off < len; off += piece, ++i) {
+      const int b = (int)(i & 1);
+      const int64_t n = std::min(piece, len - off);
+      HIP_CHECK(hipEventSynchronize(done[b]));  // the DMA that last used this buffer
+      std::atomic<bool> bad{false};
+      std::vector<std::thread> rd;
+      const int64_t part = (n + EL_READERS - 1) / EL_READERS;
+      for (int t = 0; t < EL_READERS; ++t) {
+        const int64_t lo = t * part, hi = std::min(n, lo + part);
+        if (lo >= hi) break;
+        rd.emplace_back([&, lo, hi]() {
+          for (int64_t p = lo; p < hi;) {
+            const ssize_t r = pread(fd, stage[b] + p, (size_t)(hi - p), (off_t)(off + p));
+            if (r <= 0) {
+              bad = true;
+              return;
+            }
+            p += r;
+          }
+        });
+      }
+      for (auto &th : rd) th.join();
+      if (bad) illegal(std::string("edge list: short read of ") + path);
+      last = stage[b][n - 1];
+      HIP_CHECK(hipMemcpyAsync((char *)text->p + off, stage[b], (size_t)n, hipMemcpyHostToDevice,
+                               s->stream));
+      HIP_CHECK(hipEventRecord(done[b], s->stream));
+    }
+    DataPtr d = edge_list_parse_device(s, text, len, last, sp);  // syncs the stream
+    cleanup();
+    return d;
+  } catch (...) {
+    s->sync();
+    cleanup();
+    throw;
+  }
 }
 
 static ElSpec el_spec(const char *sep, const char *comment) {
@@ -301,32 +408,8 @@ extern "C" capf_status capf_edge_list_read(capf_session *cs, const char *path, c
   try {
     if (!cs || !out || !path || !id_col || !src_col || !dst_col) illegal("null argument");
     const ElSpec sp = el_spec(sep, comment);
-    FILE *f = fopen(path, "rb");
-    if (!f) illegal(std::string("edge list: cannot open ") + path);
-    fseek(f, 0, SEEK_END);
-    const long len = ftell(f);
-    fseek(f, 0, SEEK_SET);
-    // pinned staging: one DMA of the whole file
-    char *host = nullptr;
-    if (len > 0 && hipHostMalloc((void **)&host, (size_t)len, hipHostMallocDefault) != hipSuccess) {
-      fclose(f);
-      fail(CAPF_ERR_OOM, "edge list: pinned host buffer");
-    }
-    const size_t got = len > 0 ? fread(host, 1, (size_t)len, f) : 0;
-    fclose(f);
-    if ((long)got != len) {
-      (void)hipHostFree(host);
-      illegal(std::string("edge list: short read of ") + path);
-    }
     Session *s = &cs->impl;
-    DataPtr d;
-    try {
-      d = edge_list_parse(s, host, len, sp);
-    } catch (...) {
-      (void)hipHostFree(host);
-      throw;
-    }
-    (void)hipHostFree(host);
+    DataPtr d = edge_list_read_file(s, path, sp);
     *out = edge_list_table(s, d, id_col, src_col, dst_col);
     return CAPF_OK;
   } catch (const capf::Error &e) {

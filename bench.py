@@ -25,6 +25,7 @@ sys.path.insert(0, ROOT)
 import capf_import  # noqa: E402,F401
 
 METRIC = "joined rows/sec for 2-hop MATCH on R-MAT s24 at 1/2/4/8 GPUs; % HBM roofline"
+ONE_HOP_METRIC = "joined rows/sec for 1-hop MATCH (a:Person)-->(b) count(*) on R-MAT (config 2)"
 TRI_METRIC = "joined rows/sec for triangle MATCH (a)-->(b)-->(c)-->(a) on R-MAT (config 4)"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
@@ -44,7 +45,16 @@ def triangle_query():
                  [Stage([("count", CountStar())])])
 
 
+def one_hop_person_query():
+    from capf_amd.expr import CountStar
+    from capf_amd.planner import Match, NodeP, Query, RelP, Stage
+    return Query([Match([NodeP("a", ("Person",)), NodeP("b")], [RelP("r", "a", "b")])],
+                 [Stage([("count", CountStar())])])
+
+
 def workload_name(args):
+    if args.query == "one_hop_person":
+        return f"R-MAT s{args.scale} 1-hop MATCH (a:Person)-->(b) RETURN count(*)"
     if args.query == "triangle":
         return f"R-MAT s{args.scale} triangle MATCH (a)-->(b)-->(c)-->(a) RETURN count(*)"
     return f"R-MAT s{args.scale} 2-hop MATCH (a)-->(b)-->(c) RETURN count(*)"
@@ -99,7 +109,7 @@ def cpu_baseline(session, graph, scale, budget_s):
 
 
 # kernels of one fused 2-hop count (fused_count.hip + chain2_partitioned.hip)
-PIPELINE = ("c5_partition", "c3_transpose", "c3_units", "c5_gather", "c3_overflow", "chain2_hist",
+PIPELINE = ("c5_partition", "c3_transpose", "c3_units", "c5_gather", "c3_overflow", "chain2_hist", "message_pass",
             "chain2_dot", "tri_keys", "tri_sort_keys", "tri_rle", "tri_pairs", "tri_orient",
             "tri_sort_pairs", "tri_rowptr", "tri_split", "tri_loop3", "tri_count")
 
@@ -145,8 +155,9 @@ def run_single(args):
     from capf_amd.table import GpuSession
 
     s = GpuSession(0)
-    g = rmat_graph(s, args.scale, args.edge_factor, compact=not args.int64)
-    q = triangle_query() if args.query == "triangle" else two_hop_query()
+    g = rmat_graph(s, args.scale, args.edge_factor, compact=not args.int64,
+                   person_split=args.query == "one_hop_person")
+    q = {"triangle": triangle_query, "one_hop_person": one_hop_person_query}.get(args.query, two_hop_query)()
     n_nodes = 1 << args.scale
     m = args.edge_factor << args.scale
     step = lambda: run(g, q)[0]["count"]  # noqa: E731
@@ -162,17 +173,18 @@ def run_single(args):
     s.set_profiling(False)
     prof = s.profile()
     plan = s.last_plan()
-    compulsory = 16.0 * m + 8.0 * n_nodes
+    # src+dst at int64 width + node ids (+ the 1-B label for config 2)
+    compulsory = 16.0 * m + (9.0 if args.query == "one_hop_person" else 8.0) * n_nodes
     traffic = None
     pmc = os.path.join(ROOT, "profiles", f"pmc_s{args.scale}.json")
-    if os.path.exists(pmc):
+    if os.path.exists(pmc) and args.query == "two_hop":
         with open(pmc) as f:
             traffic = json.load(f).get("hbm_bytes_per_query")
     ms_per_step = elapsed * 1e3 / args.steps
     roof = pipeline_roofline(prof, prof_steps, compulsory, traffic)
     roof["end_to_end_frac"] = compulsory / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS
     result = {
-        "metric": METRIC if args.query == "two_hop" else TRI_METRIC,
+        "metric": {"two_hop": METRIC, "triangle": TRI_METRIC, "one_hop_person": ONE_HOP_METRIC}[args.query],
         "value": count * args.steps / elapsed,
         "unit": "joined rows/s",
         "n_gpus": 1,
@@ -329,8 +341,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--int64", action="store_true", help="keep the id columns int64 (no FOR32)")
     ap.add_argument("--dist", action="store_true", help="distributed path even at world size 1")
-    ap.add_argument("--query", choices=["two_hop", "triangle"], default="two_hop",
-                    help="two_hop: the headline (config 3); triangle: config 4")
+    ap.add_argument("--query", choices=["two_hop", "triangle", "one_hop_person"], default="two_hop",
+                    help="two_hop: the headline (config 3); triangle: config 4; one_hop_person: config 2")
     ap.add_argument("--layout", choices=["node", "edge"], default="node",
                     help="multi-GPU graph layout (N > 1): node-partitioned copies or edge-range shards")
     args = ap.parse_args()

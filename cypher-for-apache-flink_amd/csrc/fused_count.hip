@@ -37,7 +37,7 @@
 namespace capf {
 
 // ============================================================ device maps
-enum MapKind : int32_t { MAP_ONES = 0, MAP_DENSE = 1, MAP_HASH = 2, MAP_DENSE32 = 3 };
+enum MapKind : int32_t { MAP_ONES = 0, MAP_DENSE = 1, MAP_HASH = 2, MAP_DENSE32 = 3, MAP_BITS = 4 };
 
 struct DMap {
   int32_t kind;
@@ -55,6 +55,11 @@ __device__ inline unsigned long long map_get(const DMap &m, int64_t k) {
   if (m.kind == MAP_DENSE) return (k >= m.lo && k <= m.hi) ? m.vals[k - m.lo] : 0ull;
   if (m.kind == MAP_DENSE32)
     return (k >= m.lo && k <= m.hi) ? (unsigned long long)((const uint32_t *)m.vals)[k - m.lo] : 0ull;
+  if (m.kind == MAP_BITS) {  // 0/1 membership: 1 bit per key of [lo, hi] (L2-resident)
+    if (k < m.lo || k > m.hi) return 0ull;
+    const uint64_t o = (uint64_t)(k - m.lo);
+    return (unsigned long long)((((const uint32_t *)m.vals)[o >> 5] >> (o & 31)) & 1u);
+  }
   uint64_t slot = fmix64((uint64_t)k) & m.mask;
   while (true) {
     int64_t cur = m.keys[slot];
@@ -125,6 +130,38 @@ __global__ void k_message(const MsgJob *jp, int64_t n, unsigned long long *root_
     local = wave_reduce_sum(local);
     if (lane_id() == 0 && local) atomicAdd(root_acc, local);
   }
+}
+
+// The root sum over a leaf with two children and non-null key columns (the
+// 1-hop count of config 2: rels with the source and target scans' messages):
+// MSG_U rows per thread with all key loads, then all message lookups, issued
+// before any is used — the generic loop is one dependent chain per row.
+constexpr int MSG_U = 8;
+
+__global__ __launch_bounds__(256) void k_message_root2(const MsgJob *jp, int64_t n,
+                                                       unsigned long long *root_acc) {
+  const MsgJob &j = *jp;
+  const int64_t T = (int64_t)gridDim.x * blockDim.x;
+  unsigned long long local = 0;
+  for (int64_t r0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r0 < n; r0 += MSG_U * T) {
+    int64_t k0[MSG_U], k1[MSG_U];
+#pragma unroll
+    for (int u = 0; u < MSG_U; ++u) {
+      const int64_t r = min(r0 + u * T, n - 1);
+      k0[u] = ld_int(j.cols[0], r);
+      k1[u] = ld_int(j.cols[1], r);
+    }
+    unsigned long long w0[MSG_U], w1[MSG_U];
+#pragma unroll
+    for (int u = 0; u < MSG_U; ++u) {
+      w0[u] = map_get(j.child[0], k0[u]);
+      w1[u] = map_get(j.child[1], k1[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < MSG_U; ++u) local += r0 + u * T < n ? w0[u] * w1[u] : 0ull;
+  }
+  local = wave_reduce_sum(local);
+  if (lane_id() == 0 && local) atomicAdd(root_acc, local);
 }
 
 // ============================================================ 2-hop fast path
@@ -406,6 +443,49 @@ static HostMap ones_map(int64_t lo, int64_t hi) {
   return h;
 }
 
+// Membership bitmap of a childless leaf's key column over the parent key's
+// range [lo, hi]: the leaf's message when every key occurs at most once
+// (node scans) — 1 bit per key instead of an 8-B count, so the parent's
+// lookups hit L2.  *dup is set when a key repeats (then counts are needed).
+__global__ void k_bits_set(ColView c, int64_t n, int64_t lo, int64_t hi, uint32_t *words,
+                           uint32_t *dup) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    if (c.valid && !c.valid[r]) continue;
+    const int64_t k = ld_int(c, r);
+    if (k < lo || k > hi) continue;
+    const uint64_t o = (uint64_t)(k - lo);
+    const uint32_t bit = 1u << (o & 31);
+    if (atomicOr(&words[o >> 5], bit) & bit) *dup = 1u;
+  }
+}
+
+static bool bits_map_for(Session *s, const ColPtr &parent_key, const ColPtr &mykey, HostMap &h) {
+  const ColStats &st = column_stats(s, parent_key);
+  if (st.non_null == 0 || mykey->type != Type::Int64) return false;
+  const uint64_t range = (uint64_t)(st.max - st.min) + 1;
+  if (range > (uint64_t(1) << 34)) return false;
+  const int64_t nw = (int64_t)((range + 31) / 32);
+  h.vals = s->alloc(4 * nw + 4);
+  HIP_CHECK(hipMemsetAsync(h.vals->p, 0, 4 * nw + 4, s->stream));
+  uint32_t *words = (uint32_t *)h.vals->p, *dup = words + nw;
+  if (mykey->n > 0) {
+    hipLaunchKernelGGL(k_bits_set, dim3(grid_for(mykey->n, 256)), dim3(256), 0, s->stream,
+                       view_of(mykey), mykey->n, st.min, st.max, words, dup);
+    KERNEL_CHECK();
+  }
+  uint32_t d = 0;
+  HIP_CHECK(hipMemcpyAsync(&d, dup, 4, hipMemcpyDeviceToHost, s->stream));
+  s->sync();
+  if (d) return false;
+  memset(&h.m, 0, sizeof(h.m));
+  h.m.kind = MAP_BITS;
+  h.m.lo = st.min;
+  h.m.hi = st.max;
+  h.m.vals = (unsigned long long *)words;
+  return true;
+}
+
 static HostMap new_map_for(Session *s, const ColPtr &parent_key, int64_t sender_rows) {
   HostMap h;
   memset(&h.m, 0, sizeof(h.m));
@@ -517,6 +597,8 @@ static bool tree_count(Session *s, JoinGraph &g, uint64_t *out) {
           return;
         }
       }
+      // childless leaf with unique keys: a membership bitmap (no pass, no atomics on counts)
+      if (j.nchild == 0 && bits_map_for(s, data[parent].data->cols[pcol], mykey, msg[v])) return;
       msg[v] = new_map_for(s, data[parent].data->cols[pcol], n);
       j.cols[j.nchild] = view_of(mykey);
       j.has_parent = 1;
@@ -526,8 +608,15 @@ static bool tree_count(Session *s, JoinGraph &g, uint64_t *out) {
     HIP_CHECK(hipMemcpyAsync(job_buf->p, &j, sizeof(j), hipMemcpyHostToDevice, s->stream));
     {
       KernelTimer kt(s, "message_pass", 8.0 * n * (j.nchild + j.has_parent));
-      hipLaunchKernelGGL(k_message, dim3(grid_for(n, 256)), dim3(256), 0, s->stream,
-                         (const MsgJob *)job_buf->p, n, (unsigned long long *)acc->p);
+      const bool root2 = !j.has_parent && j.nchild == 2 && !j.cols[0].valid && !j.cols[1].valid &&
+                         j.cols[0].data && j.cols[1].data;
+      if (root2)
+        hipLaunchKernelGGL(k_message_root2, dim3(grid_for(n, 256 * MSG_U, (int64_t)s->num_cus * 16)),
+                           dim3(256), 0, s->stream, (const MsgJob *)job_buf->p, n,
+                           (unsigned long long *)acc->p);
+      else
+        hipLaunchKernelGGL(k_message, dim3(grid_for(n, 256)), dim3(256), 0, s->stream,
+                           (const MsgJob *)job_buf->p, n, (unsigned long long *)acc->p);
       KERNEL_CHECK();
     }
     s->sync();  // job_buf is reused by the next message

@@ -316,7 +316,8 @@ ColPtr encode_column(Session *s, const ColPtr &c) {
 }
 
 // ------------------------------------------------------------ statistics
-__global__ void k_minmax(ColView v, int64_t n, int64_t *acc) {
+__global__ __launch_bounds__(256) void k_minmax(ColView v, int64_t n, int64_t *acc) {
+  __shared__ int64_t red[3][4];
   int64_t mn = INT64_MAX, mx = INT64_MIN, cnt = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -333,22 +334,59 @@ __global__ void k_minmax(ColView v, int64_t n, int64_t *acc) {
     mx = b > mx ? b : mx;
     cnt += __shfl_xor(cnt, d, WAVE);
   }
+  // one set of atomics per block (not per wave): they serialise on 3 words
+  const int w = threadIdx.x / WAVE;
   if (lane_id() == 0) {
-    atomicMin((long long *)&acc[0], (long long)mn);
-    atomicMax((long long *)&acc[1], (long long)mx);
-    atomicAdd((unsigned long long *)&acc[2], (unsigned long long)cnt);
+    red[0][w] = mn;
+    red[1][w] = mx;
+    red[2][w] = cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < (int)(blockDim.x / WAVE); ++k) {
+      mn = red[0][k] < mn ? red[0][k] : mn;
+      mx = red[1][k] > mx ? red[1][k] : mx;
+      cnt += red[2][k];
+    }
+    if (cnt) {
+      atomicMin((long long *)&acc[0], (long long)mn);
+      atomicMax((long long *)&acc[1], (long long)mx);
+      atomicAdd((unsigned long long *)&acc[2], (unsigned long long)cnt);
+    }
   }
 }
 
-__global__ void k_dup_check(ColView v, int64_t n, int64_t base, uint32_t *bits, int64_t *dup) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    if (v.valid && !v.valid[i]) continue;
-    uint64_t k = (uint64_t)(ld_int(v, i) - base);
-    uint32_t m = 1u << (k & 31);
-    uint32_t old = atomicOr(&bits[k >> 5], m);
-    if (old & m) *dup = 1;
+// Duplicate test of a column whose values fill [base, base + n): one bit per
+// value.  Each thread takes DUP_RUN consecutive rows and ORs the bits of one
+// 32-value word in a register, flushing with one atomic when the word changes
+// — sequential ids (node tables) cost one uncontended atomic per 32 rows
+// instead of 32 lanes serialising on the same word.
+constexpr int DUP_RUN = 32;
+
+__global__ __launch_bounds__(256) void k_dup_check(ColView v, int64_t n, int64_t base,
+                                                   uint32_t *bits, int64_t *dup) {
+  bool found = false;
+  for (int64_t c0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * DUP_RUN; c0 < n;
+       c0 += (int64_t)gridDim.x * blockDim.x * DUP_RUN) {
+    const int64_t c1 = c0 + DUP_RUN < n ? c0 + DUP_RUN : n;
+    uint64_t cw = ~0ull;
+    uint32_t acc = 0;
+    for (int64_t i = c0; i < c1; ++i) {
+      if (v.valid && !v.valid[i]) continue;
+      const uint64_t k = (uint64_t)(ld_int(v, i) - base);
+      const uint64_t w = k >> 5;
+      const uint32_t m = 1u << (k & 31);
+      if (w != cw) {
+        if (acc) found |= (atomicOr(&bits[cw], acc) & acc) != 0;
+        cw = w;
+        acc = 0;
+      }
+      found |= (acc & m) != 0;
+      acc |= m;
+    }
+    if (acc) found |= (atomicOr(&bits[cw], acc) & acc) != 0;
   }
+  if (found) *dup = 1;
 }
 
 ColStats compute_stats(Session *s, const Column &c) {
@@ -366,7 +404,7 @@ ColStats compute_stats(Session *s, const Column &c) {
   v.base = c.base;
   int64_t init[3] = {INT64_MAX, INT64_MIN, 0};
   HIP_CHECK(hipMemcpyAsync(s->d_scalars, init, sizeof(init), hipMemcpyHostToDevice, s->stream));
-  hipLaunchKernelGGL(k_minmax, dim3(grid_for(c.n, 256, 1024)), dim3(256), 0, s->stream, v, c.n,
+  hipLaunchKernelGGL(k_minmax, dim3(grid_for(c.n, 256, 2048)), dim3(256), 0, s->stream, v, c.n,
                      s->d_scalars);
   KERNEL_CHECK();
   HIP_CHECK(hipMemcpyAsync(s->h_scalars, s->d_scalars, sizeof(init), hipMemcpyDeviceToHost, s->stream));
@@ -380,7 +418,8 @@ ColStats compute_stats(Session *s, const Column &c) {
     BufPtr bits = s->alloc(4 * words);
     HIP_CHECK(hipMemsetAsync(bits->p, 0, 4 * words, s->stream));
     HIP_CHECK(hipMemsetAsync(s->d_scalars + 3, 0, 8, s->stream));
-    hipLaunchKernelGGL(k_dup_check, dim3(grid_for(c.n, 256, 4096)), dim3(256), 0, s->stream, v,
+    hipLaunchKernelGGL(k_dup_check, dim3(grid_for((c.n + DUP_RUN - 1) / DUP_RUN, 256, 4096)),
+                       dim3(256), 0, s->stream, v,
                        c.n, st.min, (uint32_t *)bits->p, s->d_scalars + 3);
     KERNEL_CHECK();
     HIP_CHECK(hipMemcpyAsync(s->h_scalars + 3, s->d_scalars + 3, 8, hipMemcpyDeviceToHost, s->stream));

@@ -43,6 +43,10 @@ def rmat_graph(session, scale, edge_factor=16, seed=None, person_split=False, fi
         h = RecordHeader({Var("person"): "person"})
         person = nodes.filter(Equals(Var("person"), BoolLit(True)), h, {}).select("id")
         other = nodes.filter(Equals(Var("person"), BoolLit(False)), h, {}).select("id")
+        if compact:
+            # one element table per label combination, built at ingest
+            # (ScanGraph.scala:115-128): materialised here, not re-filtered per query
+            person, other = person.compact(), other.compact()
         node_tables = [ElementTable("node", frozenset(["Person"]), person, {}),
                        ElementTable("node", frozenset(["Other"]), other, {})]
     else:

@@ -164,6 +164,51 @@ __global__ __launch_bounds__(256) void k_message_root2(const MsgJob *jp, int64_t
   if (lane_id() == 0 && local) atomicAdd(root_acc, local);
 }
 
+// FOR32 specialisation (both key columns uint32 + base, the compacted
+// layout): 16-B loads of 4 rows per column, message kinds as template
+// parameters (no per-row kind dispatch), 2 groups of 4 rows in flight.
+template <int KA, int KB>
+__device__ inline unsigned long long map_get_t(const DMap &m, int64_t k) {
+  (void)KB;
+  if (KA == MAP_ONES) return (k >= m.lo && k <= m.hi) ? 1ull : 0ull;
+  if (KA == MAP_BITS) {
+    if (k < m.lo || k > m.hi) return 0ull;
+    const uint64_t o = (uint64_t)(k - m.lo);
+    return (unsigned long long)((((const uint32_t *)m.vals)[o >> 5] >> (o & 31)) & 1u);
+  }
+  return map_get(m, k);
+}
+
+template <int KA, int KB>
+__global__ __launch_bounds__(256) void k_message_root2_f32(const MsgJob *jp, int64_t n,
+                                                           unsigned long long *root_acc) {
+  const MsgJob &j = *jp;
+  const uint4 *c0 = (const uint4 *)j.cols[0].data, *c1 = (const uint4 *)j.cols[1].data;
+  const int64_t b0 = j.cols[0].base, b1 = j.cols[1].base;
+  const DMap ma = j.child[0], mb = j.child[1];
+  const int64_t groups = n / 4, T = (int64_t)gridDim.x * blockDim.x;
+  unsigned long long local = 0;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += 2 * T) {
+    const int64_t g2 = g + T < groups ? g + T : g;
+    const uint4 a0 = c0[g], a1 = c1[g], e0 = c0[g2], e1 = c1[g2];
+    const uint32_t ka[8] = {a0.x, a0.y, a0.z, a0.w, e0.x, e0.y, e0.z, e0.w};
+    const uint32_t kb[8] = {a1.x, a1.y, a1.z, a1.w, e1.x, e1.y, e1.z, e1.w};
+    unsigned long long w[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      w[u] = map_get_t<KA, 0>(ma, b0 + (int64_t)ka[u]) * map_get_t<KB, 0>(mb, b1 + (int64_t)kb[u]);
+    unsigned long long sum = w[0] + w[1] + w[2] + w[3];
+    if (g2 != g) sum += w[4] + w[5] + w[6] + w[7];
+    local += sum;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)(n - 4 * groups)) {  // ragged tail
+    const int64_t r = 4 * groups + threadIdx.x;
+    local += map_get(ma, ld_int(j.cols[0], r)) * map_get(mb, ld_int(j.cols[1], r));
+  }
+  local = wave_reduce_sum(local);
+  if (lane_id() == 0 && local) atomicAdd(root_acc, local);
+}
+
 // ============================================================ 2-hop fast path
 // One pass over the rel table computes, for the Sb key range [lo, hi]:
 //   h1[b] += Wa(u1)        for rels with v1 = b      (hop 1, message R1 → S_b)
@@ -610,7 +655,17 @@ static bool tree_count(Session *s, JoinGraph &g, uint64_t *out) {
       KernelTimer kt(s, "message_pass", 8.0 * n * (j.nchild + j.has_parent));
       const bool root2 = !j.has_parent && j.nchild == 2 && !j.cols[0].valid && !j.cols[1].valid &&
                          j.cols[0].data && j.cols[1].data;
-      if (root2)
+      const bool f32 = root2 && j.cols[0].enc == ENC_FOR32 && j.cols[1].enc == ENC_FOR32;
+      auto simple = [](int k) { return k == MAP_ONES || k == MAP_BITS; };
+      if (f32 && simple(j.child[0].kind) && simple(j.child[1].kind)) {
+        auto kern = j.child[0].kind == MAP_BITS
+                        ? (j.child[1].kind == MAP_BITS ? k_message_root2_f32<MAP_BITS, MAP_BITS>
+                                                       : k_message_root2_f32<MAP_BITS, MAP_ONES>)
+                        : (j.child[1].kind == MAP_BITS ? k_message_root2_f32<MAP_ONES, MAP_BITS>
+                                                       : k_message_root2_f32<MAP_ONES, MAP_ONES>);
+        hipLaunchKernelGGL(kern, dim3(grid_for(n / 8 + 1, 256, (int64_t)s->num_cus * 16)), dim3(256),
+                           0, s->stream, (const MsgJob *)job_buf->p, n, (unsigned long long *)acc->p);
+      } else if (root2)
         hipLaunchKernelGGL(k_message_root2, dim3(grid_for(n, 256 * MSG_U, (int64_t)s->num_cus * 16)),
                            dim3(256), 0, s->stream, (const MsgJob *)job_buf->p, n,
                            (unsigned long long *)acc->p);

@@ -86,11 +86,14 @@ def test_rmat_generator_bit_exact(gpu_session):
     assert np.array_equal(i, np.arange(1000, 6000))
 
 
-@pytest.mark.parametrize("scale", [8, 12, 16])
-def test_one_hop_person_count_rmat(gpu_session, scale):
-    g = rmat_graph(gpu_session, scale, person_split=True)
+@pytest.mark.parametrize("compact", [False, True], ids=["int64", "for32"])
+@pytest.mark.parametrize("scale,count", [(8, None), (12, None), (16, None), (12, 40001), (14, 9)])
+def test_one_hop_person_count_rmat(gpu_session, scale, count, compact):
+    """Config 2; `count` makes the rel table ragged (not a multiple of the
+    4-row vector loads of the FOR32 root kernel)."""
+    g = rmat_graph(gpu_session, scale, person_split=True, count=count, compact=compact)
     got = run(g, ONE_HOP_PERSON)[0]["count"]
-    src, dst = cmodel.rmat(scale)
+    src, dst = cmodel.rmat(scale, count=count)
     person = cmodel.labels(1 << scale, cmodel.rmat_seed(scale))
     assert got == cmodel.count_1hop(src, dst, 1 << scale, in_a=person)
 

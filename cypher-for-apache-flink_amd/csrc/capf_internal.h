@@ -244,6 +244,9 @@ struct Session {
   // small device scratch for scalar results
   int64_t *d_scalars = nullptr;  // 64 slots
   int64_t *h_scalars = nullptr;  // pinned mirror
+  // set by capf_table_count_async for the duration of one call: the fused
+  // count writes its result to this device int64 and does not wait
+  int64_t *async_out = nullptr;
 
   BufPtr alloc(size_t bytes);
   void sync();

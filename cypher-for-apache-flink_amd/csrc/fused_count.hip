@@ -932,6 +932,11 @@ static bool host_trace() {
 }
 static double g_trace_t0 = 0;
 
+// acc = (Σ in·out, self-loop term) → the count, on the device
+__global__ void k_partial_minus_loops(const unsigned long long *acc, int64_t *out) {
+  if (threadIdx.x == 0) *out = (int64_t)(acc[0] - acc[1]);
+}
+
 static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t *out) {
   const double ta = host_trace() ? host_us() : 0;
   double tb = ta;
@@ -1018,6 +1023,13 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
     }
   }
   const double tc = host_trace() ? host_us() : 0;
+  if (s->async_out) {  // capf_table_count_async: total − loops on the device, no wait
+    hipLaunchKernelGGL(k_partial_minus_loops, dim3(1), dim3(64), 0, s->stream,
+                       (const unsigned long long *)acc->p, s->async_out);
+    KERNEL_CHECK();
+    *out = 0;
+    return true;
+  }
   HIP_CHECK(hipMemcpyAsync(s->h_scalars, acc->p, 16, hipMemcpyDeviceToHost, s->stream));
   s->sync();
   if (host_trace())
@@ -1047,20 +1059,21 @@ static bool run_triangle(Session *s, const JoinGraph &g, const Tri &t, uint64_t 
   const int64_t len = hi >= lo ? hi - lo + 1 : 0;
   if (len > (int64_t(1) << 31) || R.nrows >= (int64_t(1) << 32)) return false;
   BufPtr acc = s->alloc(16);
+  int64_t *dst = s->async_out ? s->async_out : (int64_t *)acc->p;
   if (len > 0 && R.nrows > 0) {
     triangle_count_async(s, view_of(R.cols[t.src]), view_of(R.cols[t.dst]), R.nrows, lo,
-                         (uint64_t)len, 1, 0, (int64_t *)acc->p);
+                         (uint64_t)len, 1, 0, dst);
   } else {
-    HIP_CHECK(hipMemsetAsync(acc->p, 0, 8, s->stream));
+    HIP_CHECK(hipMemsetAsync(dst, 0, 8, s->stream));
+  }
+  if (s->async_out) {
+    *out = 0;
+    return true;
   }
   HIP_CHECK(hipMemcpyAsync(s->h_scalars, acc->p, 8, hipMemcpyDeviceToHost, s->stream));
   s->sync();
   *out = (uint64_t)s->h_scalars[0];
   return true;
-}
-
-__global__ void k_partial_minus_loops(const unsigned long long *acc, int64_t *out) {
-  if (threadIdx.x == 0) *out = (int64_t)(acc[0] - acc[1]);
 }
 
 bool try_fused_count(const NodePtr &n, int64_t *out) {
@@ -1094,6 +1107,7 @@ bool try_fused_count(const NodePtr &n, int64_t *out) {
       return true;
     }
   }
+  if (s->async_out) return false;  // the message-passing count reads partials on the host
   // general: inclusion–exclusion over the uniqueness predicates
   const int k = (int)g.neqs.size();
   int64_t total = 0;

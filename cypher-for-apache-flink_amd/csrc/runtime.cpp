@@ -923,6 +923,35 @@ capf_status capf_table_size(capf_table *t, int64_t *n) {
   CAPF_API_END
 }
 
+capf_status capf_table_count_async(capf_table *t, int64_t *d_count) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(d_count, "d_count");
+  NodePtr n = t->node;
+  Session *s = n->s;
+  // group(∅, count(*)) → the count of its input (also under projections of
+  // its one column: RETURN count(*) AS c); anything else → its row count
+  NodePtr g = n;
+  while (g->kind == Kind::Select && !g->names.empty()) g = g->kids[0];
+  if (g->kind == Kind::Group && g->key_index.empty() && g->aggs.size() == 1 &&
+      g->aggs[0].kind == CAPF_AGG_COUNT_STAR)
+    n = g->kids[0];
+  struct Reset {
+    Session *s;
+    ~Reset() { s->async_out = nullptr; }
+  } reset{s};
+  s->async_out = d_count;
+  int64_t unused = 0;
+  if (!try_fused_count(n, &unused)) {
+    // not a fused shape (or already materialised): count on the host path
+    s->async_out = nullptr;
+    s->h_scalars[0] = node_size(n);
+    HIP_CHECK(hipMemcpyAsync(d_count, s->h_scalars, 8, hipMemcpyHostToDevice, s->stream));
+    s->sync();  // the pinned slot is reused by the next call
+  }
+  CAPF_API_END
+}
+
 capf_status capf_table_download(capf_table *t, const char *col, void *values_out,
                                 uint8_t *valid_out) {
   CAPF_API_BEGIN

@@ -235,6 +235,11 @@ class GpuTable:
         _lib.call("capf_table_size", self._h, byref(n))
         return n.value
 
+    def count_async(self, d_count):
+        """`size` (or the count(*) of a global group(∅, {count(*)})) written to
+        the device int64 at address d_count, without waiting for the GPU."""
+        _lib.call("capf_table_count_async", self._h, c_void_p(int(d_count)))
+
     def column_arrays(self, col):
         """(values ndarray, valid ndarray[bool]) of a column (materialises)."""
         n = self.size

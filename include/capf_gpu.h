@@ -198,6 +198,13 @@ capf_status capf_table_columns(capf_table *t, const char **joined, int64_t *byte
 capf_status capf_table_column_type(capf_table *t, const char *col, int32_t *type);
 /* size (CypherTable.scala:68): triggers execution */
 capf_status capf_table_size(capf_table *t, int64_t *n);
+/* size / group(∅, {count(*)}) without the host wait: the count lands in the
+ * device int64 at d_count, ordered on the session stream.  Same value as
+ * capf_table_size (CypherTable.scala:68) / the count(*) column of
+ * Table.group (Table.scala:158-159); lets a driver plan query i+1 while the
+ * GPU runs query i.  Shapes that are not a fused count fall back to the
+ * synchronous count (then copy it to d_count).                             */
+capf_status capf_table_count_async(capf_table *t, int64_t *d_count);
 /* rows (CypherTable.scala:63): download one column; values buffer holds
  * size × (8 or 1) bytes, valid_out (may be NULL) size bytes.              */
 capf_status capf_table_download(capf_table *t, const char *col, void *values_out,

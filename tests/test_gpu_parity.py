@@ -76,6 +76,34 @@ def test_two_hop_partition_variants(gpu_session, monkeypatch, variant, compact, 
     assert got == cmodel.count_2hop(src, dst, nodes or 1 << scale)
 
 
+@pytest.mark.parametrize("query", ["two_hop", "triangle", "one_hop_person", "grouped"])
+def test_count_async_matches_size(gpu_session, query):
+    """capf_table_count_async: a queue of in-flight counts (no host wait per
+    query) lands the same values as the synchronous records path — fused
+    chain2 / triangle on the device, the other shapes through the fallback."""
+    import torch
+    tri = Query([Match([NodeP("a"), NodeP("b"), NodeP("c")],
+                       [RelP("r1", "a", "b"), RelP("r2", "b", "c"), RelP("r3", "c", "a")])],
+                [Stage([("count", CountStar())])])
+    grouped = Query([Match([NodeP("a"), NodeP("b")], [RelP("r", "a", "b")])],
+                    [Stage([("a", Var("a")), ("n", CountStar())])])
+    q = {"two_hop": TWO_HOP, "triangle": tri, "one_hop_person": ONE_HOP_PERSON, "grouped": grouped}[query]
+    g = rmat_graph(gpu_session, 12, person_split=query == "one_hop_person", compact=True)
+    if query == "grouped":
+        want = len(run(g, q))  # row count of the grouped table
+    else:
+        want = run(g, q)[0]["count"]
+    slots = torch.full((6,), -1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()  # the fill runs on torch's stream, the counts on the session's
+    for i in range(6):
+        plan_query(g, q).table.count_async(slots.data_ptr() + 8 * i)
+    gpu_session.sync()
+    assert slots.cpu().tolist() == [want] * 6
+    if query == "two_hop":
+        src, dst = cmodel.rmat(12)
+        assert want == cmodel.count_2hop(src, dst, 1 << 12)
+
+
 def test_rmat_generator_bit_exact(gpu_session):
     t = gpu_session.rmat_rels(12, cmodel.rmat_seed(12), cmodel.thresholds(), 1000, 5000)
     src, dst = cmodel.rmat(12, first=1000, count=5000)

@@ -266,7 +266,23 @@ __global__ __launch_bounds__(256) void k_chain2_dot(const uint32_t *h1, const ui
   const int64_t n4 = len / 4;
   const uint4 *a4 = (const uint4 *)h1;
   const uint4 *b4 = (const uint4 *)h2;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+  int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ONES) {
+    // 4 independent dwordx4 pairs in flight per thread before the first use
+    for (; i0 + 3 * stride < n4; i0 += 4 * stride) {
+      uint4 x[4], y[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        x[k] = a4[i0 + k * stride];
+        y[k] = b4[i0 + k * stride];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        s += (unsigned long long)x[k].x * y[k].x + (unsigned long long)x[k].y * y[k].y +
+             (unsigned long long)x[k].z * y[k].z + (unsigned long long)x[k].w * y[k].w;
+    }
+  }
+  for (int64_t i = i0; i < n4; i += stride) {
     uint4 x = a4[i], y = b4[i];
     if (ONES) {
       s += (unsigned long long)x.x * y.x + (unsigned long long)x.y * y.y +

@@ -10,6 +10,10 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 if GOLDEN not in sys.path:
     sys.path.insert(0, GOLDEN)
 
+# torch first: it ships its own HIP runtime, which cannot enumerate the GPU
+# once libcapf_gpu.so's runtime has initialised it in the same process
+import torch  # noqa: E402,F401
+
 import capf_import  # noqa: E402,F401
 
 

@@ -248,41 +248,42 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
 }
 
 // [tile][run] → [run][tile] and per-run totals.  A block moves 32 runs ×
-// 256 tiles through a 32×33 LDS tile (8 steps) and adds each run's count
-// once per block (one atomic per run per 256 tiles, not per 32).
+// tt (≤ 256) tiles through LDS in ONE round: every thread issues its tt/8
+// row loads before the single barrier (the old 32-tile rounds kept 4 loads
+// in flight per thread), then each run's tt words go out as one contiguous
+// row.  Run totals are summed during the loads and added once per run per
+// block (a per-block partial row summed by k_c3_units instead was measured
+// slower: the one-block units kernel turns latency bound).
 constexpr int C3_TT = 256;
 __global__ __launch_bounds__(256) void k_c3_transpose(const uint32_t *meta, uint32_t *meta_t,
                                                        int64_t ntiles, int nr,
                                                        unsigned long long *run_total, int64_t tt) {
-  __shared__ uint32_t tilebuf[32][33];
+  __shared__ uint32_t tilebuf[C3_TT][33];
+  __shared__ uint32_t part[8][33];
   const int r0 = blockIdx.y * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads = 32 × 8
-  unsigned int cnt[4] = {0, 0, 0, 0};                       // runs r0 + ty + 8q
-  for (int64_t t0 = (int64_t)blockIdx.x * tt; t0 < min(ntiles, ((int64_t)blockIdx.x + 1) * tt);
-       t0 += 32) {
-    for (int k = ty; k < 32; k += 8) {
-      const int64_t t = t0 + k;
-      const int r = r0 + tx;
-      tilebuf[k][tx] = (t < ntiles && r < nr) ? meta[t * nr + r] : 0u;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int k = ty + 8 * q;
-      const int r = r0 + k;
-      const int64_t t = t0 + tx;
-      const uint32_t v = tilebuf[tx][k];
-      if (t < ntiles && r < nr) meta_t[(int64_t)r * ntiles + t] = v;
-      cnt[q] += v >> 16;
-    }
-    __syncthreads();
+  const int64_t tb = (int64_t)blockIdx.x * tt;
+  const int64_t tn = min<int64_t>(tt, ntiles - tb);  // tiles in this block
+  const int r = r0 + tx;
+  uint32_t cnt = 0;
+#pragma unroll 8
+  for (int k = ty; k < tt; k += 8) {
+    const uint32_t v = (k < tn && r < nr) ? meta[(tb + k) * nr + r] : 0u;
+    tilebuf[k][tx] = v;
+    cnt += v >> 16;
   }
+  part[ty][tx] = cnt;
+  __syncthreads();
+  if (ty == 0) {
+    uint32_t c = 0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    unsigned int c = cnt[q];
-    for (int d = 16; d > 0; d >>= 1) c += __shfl_xor(c, d, 32);
-    const int r = r0 + ty + 8 * q;
-    if (tx == 0 && c && r < nr) atomicAdd(&run_total[r], (unsigned long long)c);
+    for (int q = 0; q < 8; ++q) c += part[q][tx];
+    if (c && r < nr) atomicAdd(&run_total[r], (unsigned long long)c);
+  }
+  const int lt = __builtin_ctzll((unsigned long long)tt);  // tt is a power of two
+  for (int idx = threadIdx.x; idx < 32 * tt; idx += 256) {
+    const int q = idx >> lt, i = idx & (int)(tt - 1);
+    if (i < tn && r0 + q < nr) meta_t[(int64_t)(r0 + q) * ntiles + tb + i] = tilebuf[i][q];
   }
 }
 
@@ -664,6 +665,10 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   // every overflow event consumes 2^15 adds of one half-counter within one unit
   const uint32_t ovf_cap = (uint32_t)(nkeys / (1 << 15) + 64);
   BufPtr meta_t = s->alloc(4 * nr * ntiles);
+  // transpose blocks: tiles per block tt, fewer when there are few runs (≥ ~1024 blocks)
+  int64_t tt = C3_TT;
+  while (tt > 32 && ((ntiles + tt - 1) / tt) * ((nr + 31) / 32) < 1024) tt /= 2;
+  const int nparts = (int)((ntiles + tt - 1) / tt);
   BufPtr acc = s->alloc(8 * nr + 16 + 4 * nr + sizeof(C3Unit) * max_units + 8 * (int64_t)ovf_cap);
   unsigned long long *run_total = (unsigned long long *)acc->p;
   int32_t *nunits = (int32_t *)(run_total + nr);  // [0] units, [1] overflow events
@@ -676,12 +681,9 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   HIP_CHECK(hipMemsetAsync(acc->p, 0, 8 * nr + 16, s->stream));
   {
     KernelTimer kt(s, "c3_transpose", 8.0 * nr * ntiles);
-    // tiles per block: 256, fewer when there are few runs (≥ ~1024 blocks)
-    int64_t tt = C3_TT;
-    while (tt > 32 && ((ntiles + tt - 1) / tt) * ((nr + 31) / 32) < 1024) tt /= 2;
-    hipLaunchKernelGGL(k_c3_transpose, dim3((unsigned)((ntiles + tt - 1) / tt), (nr + 31) / 32),
-                       dim3(256), 0, s->stream, meta, (uint32_t *)meta_t->p, ntiles, nr, run_total,
-                       tt);
+    hipLaunchKernelGGL(k_c3_transpose, dim3((unsigned)nparts, (nr + 31) / 32), dim3(256), 0,
+                       s->stream, meta, (uint32_t *)meta_t->p, ntiles, nr,
+                       run_total, tt);
     KERNEL_CHECK();
   }
   {

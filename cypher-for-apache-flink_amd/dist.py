@@ -112,10 +112,18 @@ def gpu_two_hop_count_sharded(session, in_copy, out_copy, n_nodes, partial, node
     """Distributed 2-hop count(*) over the node-partitioned copies: the local
     partial is enqueued on the session stream (= torch's current stream) into
     the int64 device tensor `partial`, then ONE all-reduce (RCCL) sums it."""
+    gpu_two_hop_count_sharded_async(session, in_copy, out_copy, n_nodes, partial, node_base, group)
+    return int(partial.item())
+
+
+def gpu_two_hop_count_sharded_async(session, in_copy, out_copy, n_nodes, partial, node_base=0,
+                                    group=None):
+    """gpu_two_hop_count_sharded without the host read: the summed count is
+    left in `partial` (ordered on the session/torch stream), so a driver can
+    enqueue the next query before this one finishes."""
     from .table import chain2_sharded_count_async
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     chain2_sharded_count_async(session, in_copy, out_copy, node_base, n_nodes, world, rank,
                                partial.data_ptr())
     dist.all_reduce(partial, op=dist.ReduceOp.SUM, group=group)
-    return int(partial.item())

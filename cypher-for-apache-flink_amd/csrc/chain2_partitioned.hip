@@ -512,19 +512,48 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
       v[j] = part4[tab.qb[k] + (pc - tab.pre[k])];
     }
   };
-  // Hub keys: R-MAT concentrates a large share of a run's keys on a few
-  // nodes, and lanes of one ds_add hitting the same word serialise.  Each
-  // atomic instruction first votes on lane 0's key: the lanes holding it are
-  // summed by one lane (popcount), the others add 1 as usual.
+  // Counting one step: 8 keys per piece, PPS pieces per lane (hub-key merge
+  // below).  `acc` ORs every post-add word: bit 15 of a half set ⇒ some add
+  // may have lifted that half to 2^15 → the exact (rare) hand-off check.
   auto count = [&](const uint4 *v, uint32_t p0, uint32_t total) {
     uint32_t acc = 0;
     uint32_t old[PPS][8];
+    uint32_t n0[PPS];
+    bool dup[PPS][8];
 #pragma unroll
     for (int j = 0; j < PPS; ++j) {
       const bool live = p0 + j * WAVE + lane < total;
       dead += live ? 0u : 1u;
       const uint32_t wd[4] = {live ? v[j].x : dead_keys.x, live ? v[j].y : dead_keys.y,
                               live ? v[j].z : dead_keys.z, live ? v[j].w : dead_keys.w};
+      if (DIAG == 0) {
+        // hub keys: the keys of the piece equal to its first key are added
+        // once, as a count n0 ≤ 8, by slot 0 (R-MAT skew puts a hub's key in
+        // many slots of its run's pieces, and same-word lanes of one ds_add
+        // serialise); the other slots add 1 each, lanes holding a duplicate
+        // sit that atomic out
+        const uint32_t k0 = wd[0] & 0xFFFF;
+        n0[j] = 1;
+        dup[j][0] = false;
+#pragma unroll
+        for (int e = 1; e < 8; ++e) {
+          const uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
+          dup[j][e] = key == k0;
+          n0[j] += dup[j][e] ? 1u : 0u;
+        }
+        const uint32_t inc0 = n0[j] << ((k0 >> 15) << 4);
+        old[j][0] = atomicAdd(&words[k0 & (C2_WORDS - 1)], inc0);
+        acc |= old[j][0] + inc0;
+#pragma unroll
+        for (int e = 1; e < 8; ++e) {
+          const uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
+          const uint32_t unit = (key >> 15) * 0xFFFFu + 1u;
+          old[j][e] = 0;
+          if (!dup[j][e]) old[j][e] = atomicAdd(&words[key & (C2_WORDS - 1)], unit);
+          acc |= old[j][e] + unit;
+        }
+        continue;
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
@@ -535,7 +564,8 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
       }
     }
     if (DIAG == 0 && (acc & 0x80008000u)) {
-      // rare: some half reached 2^15 — find the add(s) that crossed it
+      // rare: some half reached 2^15 — find the add(s) that crossed it (the
+      // half before the add was < 2^15 and the add took it to ≥ 2^15)
 #pragma unroll
       for (int j = 0; j < PPS; ++j) {
         const bool live = p0 + j * WAVE + lane < total;
@@ -544,8 +574,11 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
+          const uint32_t inc = e == 0 ? n0[j] : 1u;
+          if (e > 0 && dup[j][e]) continue;
           const uint32_t sh = (key >> 15) << 4;
-          if (((old[j][e] >> sh) & 0xFFFFu) == 0x7FFFu)
+          const uint32_t oh = (old[j][e] >> sh) & 0xFFFFu;
+          if (oh < 0x8000u && oh + inc >= 0x8000u)
             c3_handoff(&words[key & (C2_WORDS - 1)], 1u << sh, hist_base + key, side, ovf);
         }
       }
@@ -656,7 +689,8 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   const int nr = 2 * sd.nb;
   static bool attr_set = false;
   if (!attr_set) {
-    for (const void *f : {(const void *)k_c5_gather<C5_PPS, 0>, (const void *)k_c5_gather<C5_PPS, 2>})
+    for (const void *f : {(const void *)k_c5_gather<C5_PPS, 0>, (const void *)k_c5_gather<C5_PPS, 2>,
+                          (const void *)k_c5_gather<C5_PPS, 3>})
       HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, C5_GATHER_LDS));
     attr_set = true;
   }
@@ -700,7 +734,9 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
     // CAPF_P3_DIAG=2 (diagnostics, wrong counts): keys spread so no two lanes
     // of an atomic share a word — measures the cost of hub-key conflicts
     const char *dg = getenv("CAPF_P3_DIAG");
-    auto kern = dg && atoi(dg) == 2 ? k_c5_gather<C5_PPS, 2> : k_c5_gather<C5_PPS, 0>;
+    auto kern = dg && atoi(dg) == 2   ? k_c5_gather<C5_PPS, 2>
+                : dg && atoi(dg) == 3 ? k_c5_gather<C5_PPS, 3>
+                                      : k_c5_gather<C5_PPS, 0>;
     hipLaunchKernelGGL(kern, dim3((unsigned)max_units), dim3(C5_BLOCK), C5_GATHER_LDS, s->stream,
                        (const C3Unit *)units, (const int32_t *)nunits, part,
                        (const uint32_t *)meta_t->p, ntiles, sd.nb, rstride, h_in, h_out,

@@ -518,7 +518,7 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
   auto count = [&](const uint4 *v, uint32_t p0, uint32_t total) {
     uint32_t acc = 0;
     uint32_t old[PPS][8];
-    uint32_t n0[PPS];
+    uint32_t n0[PPS], n1[PPS];
     bool dup[PPS][8];
 #pragma unroll
     for (int j = 0; j < PPS; ++j) {
@@ -527,25 +527,33 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
       const uint32_t wd[4] = {live ? v[j].x : dead_keys.x, live ? v[j].y : dead_keys.y,
                               live ? v[j].z : dead_keys.z, live ? v[j].w : dead_keys.w};
       if (DIAG == 0) {
-        // hub keys: the keys of the piece equal to its first key are added
-        // once, as a count n0 ≤ 8, by slot 0 (R-MAT skew puts a hub's key in
+        // hub keys: the keys of the piece equal to its first (second) key
+        // are added once, as a count ≤ 8, by slot 0 (1) (R-MAT skew puts a hub's key in
         // many slots of its run's pieces, and same-word lanes of one ds_add
         // serialise); the other slots add 1 each, lanes holding a duplicate
         // sit that atomic out
-        const uint32_t k0 = wd[0] & 0xFFFF;
-        n0[j] = 1;
+        const uint32_t k0 = wd[0] & 0xFFFF, k1 = wd[0] >> 16;
         dup[j][0] = false;
+        dup[j][1] = k1 == k0;
+        n0[j] = dup[j][1] ? 2u : 1u;
+        n1[j] = 1;
 #pragma unroll
-        for (int e = 1; e < 8; ++e) {
+        for (int e = 2; e < 8; ++e) {
           const uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
-          dup[j][e] = key == k0;
-          n0[j] += dup[j][e] ? 1u : 0u;
+          const bool d0 = key == k0, d1 = !d0 && key == k1;  // k1 == k0 ⇒ d0 already
+          dup[j][e] = d0 || d1;
+          n0[j] += d0 ? 1u : 0u;
+          n1[j] += d1 ? 1u : 0u;
         }
         const uint32_t inc0 = n0[j] << ((k0 >> 15) << 4);
         old[j][0] = atomicAdd(&words[k0 & (C2_WORDS - 1)], inc0);
         acc |= old[j][0] + inc0;
+        const uint32_t inc1 = n1[j] << ((k1 >> 15) << 4);
+        old[j][1] = 0;
+        if (!dup[j][1]) old[j][1] = atomicAdd(&words[k1 & (C2_WORDS - 1)], inc1);
+        acc |= old[j][1] + inc1;
 #pragma unroll
-        for (int e = 1; e < 8; ++e) {
+        for (int e = 2; e < 8; ++e) {
           const uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
           const uint32_t unit = (key >> 15) * 0xFFFFu + 1u;
           old[j][e] = 0;
@@ -574,7 +582,7 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
-          const uint32_t inc = e == 0 ? n0[j] : 1u;
+          const uint32_t inc = e == 0 ? n0[j] : e == 1 ? n1[j] : 1u;
           if (e > 0 && dup[j][e]) continue;
           const uint32_t sh = (key >> 15) << 4;
           const uint32_t oh = (old[j][e] >> sh) & 0xFFFFu;

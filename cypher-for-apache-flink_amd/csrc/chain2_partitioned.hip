@@ -386,9 +386,10 @@ __device__ inline int c3_unit_of(int i) {
 }
 
 // P3 counters: bins are packed uint16 pairs, word w holds bin w (low half)
-// and bin w + 2^15 (high half).  The add that lifts a half to 2^15 hands
-// 2^15 off to the overflow log and takes it back out of the word, so a half
-// never exceeds 2^15 + (adds in flight on the CU) < 2^16: exact, no carry.
+// and bin w + 2^15 (high half).  The add that lifts a half from below 2^15
+// to 2^15 or more hands 2^15 off to the overflow log and takes it back out
+// of the word, so a half never exceeds 2^15 + (sum of the adds in flight on
+// the CU: ≤ 1024 lanes × 8 for the merged hub adds) < 2^16: exact, no carry.
 struct C3Ovf {
   uint2 *log;  // (histogram index, side)
   uint32_t *n;

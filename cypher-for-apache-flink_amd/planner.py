@@ -56,6 +56,7 @@ class Match:
     nodes: List[NodeP]
     rels: List[RelP] = field(default_factory=list)
     where: List[Expr] = field(default_factory=list)
+    optional: bool = False  # OPTIONAL MATCH
 
 
 @dataclass
@@ -377,6 +378,53 @@ def plan_match(graph, m: Match, prev: Optional[Planned], params=None) -> Planned
     return op
 
 
+def plan_optional(graph, m: Match, lhs: Planned, params=None) -> Planned:
+    """planOptional (RelationalPlanner.scala:298-329): the optional pattern is
+    planned on its own (rhs), then
+      1. common expressions of both headers; the Vars among them join,
+      2. the rhs drops the join vars' other expressions (labels, properties)
+         and every other common expression,
+      3. the rhs join-var columns get temporary names,
+      4. lhs LEFT OUTER JOIN rhs on (lhs var column = temporary column),
+      5. the temporary columns are dropped (Select of the header's columns).
+    Rows of lhs without a match keep NULLs in every rhs column.  Uniqueness
+    predicates apply within the optional pattern only (MTa/OptionalMatchTests
+    .scala:191-240: e2 may equal e1)."""
+    if lhs is None:
+        raise NotImplementedError("OPTIONAL MATCH as the first clause (Optional over the unit table)")
+    rhs = plan_match(graph, m, None, params)
+    common = [e for e in lhs.header.expressions if e in rhs.header]
+    join_vars = [e for e in common if isinstance(e, Var)]
+    if not join_vars:
+        raise NotImplementedError("OPTIONAL MATCH sharing no variable with the preceding clauses")
+    remove = {e for v in join_vars for e in rhs.header.owned_by(v) if e != v} | \
+        {e for e in common if not isinstance(e, Var)}
+    keep = [e for e in rhs.header.expressions if e not in remove]
+    jcol = {rhs.header.column(v): v for v in join_vars}
+    taken = set(lhs.table.physicalColumns) | set(rhs.table.physicalColumns)
+    tmp = {}
+    for i, c in enumerate(jcol):
+        t = f"__optional_{i}"
+        while t in taken:
+            t += "_"
+        taken.add(t)
+        tmp[c] = t
+    rcols = list(dict.fromkeys(rhs.header.column(e) for e in keep))
+    rtab = rhs.table.select(*[(c, tmp.get(c, c)) for c in rcols])
+    rhead = RecordHeader({e: tmp.get(c, c) for e, c in ((e, rhs.header.column(e)) for e in keep)
+                          if not (isinstance(e, Var) and e in jcol.values())})
+    right = _rename_disjoint(lhs, Planned(rtab, rhead))
+    # the temporary names are fresh, so _rename_disjoint left them alone
+    pairs = [(lhs.header.column(v), tmp[c]) for c, v in jcol.items()]
+    joined = lhs.table.join(right.table, "left_outer", *pairs)
+    joined = joined.drop(*[tmp[c] for c in jcol])
+    # rhs expressions that lived in a join-var column now read the lhs column
+    inv = {t: c for c, t in tmp.items()}
+    head = lhs.header.union(RecordHeader({e: (lhs.header.column(jcol[inv[c]]) if c in inv else c)
+                                          for e, c in right.header.items()}))
+    return Planned(joined, head)
+
+
 def plan_stage(op: Planned, st: Stage, params=None) -> Planned:
     aggs = [(a, e) for a, e in st.items if isinstance(e, Aggregator)]
     projs = [(a, e) for a, e in st.items if not isinstance(e, Aggregator)]
@@ -480,7 +528,7 @@ def plan_query(graph, q: Query, params=None) -> Planned:
         return op
     op = None
     for m in q.matches:
-        op = plan_match(graph, m, op, params)
+        op = plan_optional(graph, m, op, params) if m.optional else plan_match(graph, m, op, params)
     for st in q.stages:
         op = plan_stage(op, st, params)
     return op

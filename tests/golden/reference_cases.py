@@ -246,3 +246,70 @@ CASES.append(
      Query([Match([NodeP("a", ("A",)), NodeP("other")], [RelP("r", "a", "other", direction="both", length=(2, 2))])],
            [ret(("a.prop", P("a", "prop")), ("other.prop", P("other", "prop")))]),
      [{"a.prop": "a", "other.prop": "c"}]))
+
+
+# ------------------------------------------------------ OptionalMatchTests (MTa)
+# OPTIONAL MATCH = planOptional's left outer join (RelationalPlanner.scala:298-329),
+# shared with the Flink backend through the okapi planner.
+KNOWS3 = """
+        CREATE (p1:Person {name: "Alice"})
+        CREATE (p2:Person {name: "Bob"})
+        CREATE (p3:Person {name: "Eve"})
+        CREATE (p1)-[:KNOWS]->(p2)
+        CREATE (p2)-[:KNOWS]->(p3)
+"""
+
+
+def _names(*vs):
+    return ret(*[(f"{v}.name", P(v, "name")) for v in vs])
+
+
+OPTIONAL_CASES = [
+    ("optional_match", "MTa/OptionalMatchTests.scala:122-159", KNOWS3,
+     Query([Match([NodeP("p1", ("Person",))]),
+            Match([NodeP("p1"), NodeP("p2"), NodeP("p3")], [RelP("e1", "p1", "p2"), RelP("e2", "p2", "p3")],
+                  optional=True)], [_names("p1", "p2", "p3")]),
+     [{"p1.name": "Eve", "p2.name": None, "p3.name": None},
+      {"p1.name": "Bob", "p2.name": None, "p3.name": None},
+      {"p1.name": "Alice", "p2.name": "Bob", "p3.name": "Eve"}]),
+    ("optional_match_predicates", "MTa/OptionalMatchTests.scala:161-189",
+     """CREATE (p1:Person {name: "Alice"})
+        CREATE (p2:Person {name: "Bob"})
+        CREATE (p1)-[:KNOWS]->(p2)""",
+     Query([Match([NodeP("p1", ("Person",))]),
+            Match([NodeP("p1"), NodeP("p2", ("Person",))], [RelP("e1", "p1", "p2", ("KNOWS",))],
+                  optional=True)], [_names("p1", "p2")]),
+     [{"p1.name": "Bob", "p2.name": None}, {"p1.name": "Alice", "p2.name": "Bob"}]),
+    ("optional_match_matched_rels", "MTa/OptionalMatchTests.scala:191-239",
+     KNOWS3 + "        CREATE (p1)-[:KNOWS]->(p3)\n",
+     Query([Match([NodeP("p1", ("Person",)), NodeP("p2", ("Person",))], [RelP("e1", "p1", "p2", ("KNOWS",))]),
+            Match([NodeP("p1"), NodeP("p3", ("Person",))], [RelP("e2", "p1", "p3", ("KNOWS",))],
+                  optional=True)], [_names("p1", "p2", "p3")]),
+     [{"p1.name": "Alice", "p2.name": "Bob", "p3.name": "Eve"},
+      {"p1.name": "Alice", "p2.name": "Eve", "p3.name": "Bob"},
+      {"p1.name": "Alice", "p2.name": "Bob", "p3.name": "Bob"},
+      {"p1.name": "Alice", "p2.name": "Eve", "p3.name": "Eve"},
+      {"p1.name": "Bob", "p2.name": "Eve", "p3.name": "Eve"}]),
+    ("optional_match_partial", "MTa/OptionalMatchTests.scala:276-313", KNOWS3,
+     Query([Match([NodeP("p1", ("Person",))]),
+            Match([NodeP("p1"), NodeP("p2", ("Person",)), NodeP("p3", ("Person",))],
+                  [RelP("e1", "p1", "p2", ("KNOWS",)), RelP("e2", "p2", "p3", ("KNOWS",))], optional=True)],
+           [_names("p1", "p2", "p3")]),
+     [{"p1.name": "Alice", "p2.name": "Bob", "p3.name": "Eve"},
+      {"p1.name": "Bob", "p2.name": None, "p3.name": None},
+      {"p1.name": "Eve", "p2.name": None, "p3.name": None}]),
+    ("optional_match_duplicates", "MTa/OptionalMatchTests.scala:315-351",
+     """CREATE (p1:Person {name: "Alice"})
+        CREATE (p2:Person {name: "Bob"})
+        CREATE (p3:Person {name: "Eve"})
+        CREATE (p4:Person {name: "Paul"})
+        CREATE (p1)-[:KNOWS]->(p3)
+        CREATE (p2)-[:KNOWS]->(p3)
+        CREATE (p3)-[:KNOWS]->(p4)""",
+     Query([Match([NodeP("a", ("Person",)), NodeP("b", ("Person",))], [RelP("e1", "a", "b", ("KNOWS",))]),
+            Match([NodeP("b"), NodeP("c", ("Person",))], [RelP("e2", "b", "c", ("KNOWS",))], optional=True)],
+           [_names("b", "c")]),
+     [{"b.name": "Eve", "c.name": "Paul"}, {"b.name": "Eve", "c.name": "Paul"},
+      {"b.name": "Paul", "c.name": None}]),
+]
+CASES = CASES + OPTIONAL_CASES

@@ -312,4 +312,23 @@ OPTIONAL_CASES = [
      [{"b.name": "Eve", "c.name": "Paul"}, {"b.name": "Eve", "c.name": "Paul"},
       {"b.name": "Paul", "c.name": None}]),
 ]
+OPTIONAL_CASES.append(
+    ("optional_match_duplicates_cycle", "MTa/OptionalMatchTests.scala:353-402",
+     """CREATE (p1:Person {name: "Alice"})
+        CREATE (p2:Person {name: "Bob"})
+        CREATE (p3:Person {name: "Eve"})
+        CREATE (p4:Person {name: "Paul"})
+        CREATE (p1)-[:KNOWS]->(p3)
+        CREATE (p2)-[:KNOWS]->(p3)
+        CREATE (p3)-[:KNOWS]->(p4)
+        CREATE (p4)-[:KNOWS {foo: 42}]->(p1)""",
+     Query([Match([NodeP("a", ("Person",)), NodeP("b", ("Person",)), NodeP("c", ("Person",))],
+                  [RelP("e1", "a", "b", ("KNOWS",)), RelP("e2", "b", "c", ("KNOWS",))]),
+            Match([NodeP("c"), NodeP("a")], [RelP("e3", "c", "a", ("KNOWS",))], optional=True)],
+           [ret(("a.name", P("a", "name")), ("b.name", P("b", "name")), ("c.name", P("c", "name")),
+                ("e3.foo", ElementProperty(Var("e3", "RELATIONSHIP"), "foo", "ANY")))]),
+     [{"a.name": "Alice", "b.name": "Eve", "c.name": "Paul", "e3.foo": 42},
+      {"a.name": "Eve", "b.name": "Paul", "c.name": "Alice", "e3.foo": None},
+      {"a.name": "Paul", "b.name": "Alice", "c.name": "Eve", "e3.foo": None},
+      {"a.name": "Bob", "b.name": "Eve", "c.name": "Paul", "e3.foo": None}]))
 CASES = CASES + OPTIONAL_CASES

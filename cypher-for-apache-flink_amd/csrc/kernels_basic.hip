@@ -188,6 +188,17 @@ ColPtr gather_column(Session *s, const ColPtr &c, const int64_t *d_idx, int64_t 
     illegal("internal: identity gather with mismatched length");
   }
   if (c->type == Type::Null) return null_column(s, Type::Null, m);
+  if (!c->data || c->n == 0) {
+    // empty source (outer join against an empty side): every index is the
+    // null index, so the result is all NULL of the column's type
+    if (m > 0 && !idx_may_be_null) illegal("internal: gather from an empty column");
+    ColPtr o = make_column(s, c->type, m, true);
+    if (m > 0) {
+      HIP_CHECK(hipMemsetAsync(o->data->p, 0, m * type_width(c->type), s->stream));
+      HIP_CHECK(hipMemsetAsync(o->valid->p, 0, m, s->stream));
+    }
+    return o;
+  }
   bool with_valid = c->valid != nullptr || idx_may_be_null;
   ColPtr o;
   if (c->enc == ENC_FOR32) {  // gathered rows keep the frame of reference

@@ -331,4 +331,11 @@ OPTIONAL_CASES.append(
       {"a.name": "Eve", "b.name": "Paul", "c.name": "Alice", "e3.foo": None},
       {"a.name": "Paul", "b.name": "Alice", "c.name": "Eve", "e3.foo": None},
       {"a.name": "Bob", "b.name": "Eve", "c.name": "Paul", "e3.foo": None}]))
+OPTIONAL_CASES.append(
+    ("optional_match_stacked_empty", "MTa/OptionalMatchTests.scala:404-421", "CREATE (s {val: 1})",
+     Query([Match([NodeP("a")]),
+            Match([NodeP("a"), NodeP("b", ("NonExistent",))], [RelP("r1", "a", "b")], optional=True),
+            Match([NodeP("a"), NodeP("c", ("NonExistent",))], [RelP("r2", "a", "c")], optional=True)],
+           [ret(("b", N("b")), ("c", N("c")))]),
+     [{"b": None, "c": None}]))
 CASES = CASES + OPTIONAL_CASES

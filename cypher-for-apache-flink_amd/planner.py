@@ -23,7 +23,7 @@ from itertools import combinations
 from typing import List, Optional, Sequence, Tuple
 
 from .expr import (Aggregator, Ands, BoolLit, CountStar, ElementProperty, EndNode, Equals, Expr, HasLabel,
-                   HasType, Not, NullLit, StartNode, TrueLit, Var)
+                   HasType, IntegerLit, Not, NullLit, StartNode, TrueLit, Var)
 from .header import RecordHeader, owner_of
 
 
@@ -387,12 +387,24 @@ def plan_optional(graph, m: Match, lhs: Planned, params=None) -> Planned:
       3. the rhs join-var columns get temporary names,
       4. lhs LEFT OUTER JOIN rhs on (lhs var column = temporary column),
       5. the temporary columns are dropped (Select of the header's columns).
-    Rows of lhs without a match keep NULLs in every rhs column.  Uniqueness
+    Rows of lhs without a match keep NULLs in every rhs column; a leading
+    OPTIONAL MATCH joins the unit table.  Uniqueness
     predicates apply within the optional pattern only (MTa/OptionalMatchTests
     .scala:191-240: e2 may equal e1)."""
-    if lhs is None:
-        raise NotImplementedError("OPTIONAL MATCH as the first clause (Optional over the unit table)")
     rhs = plan_match(graph, m, None, params)
+    if lhs is None:
+        # a leading OPTIONAL MATCH: Optional(Start, rhs) — the unit table (one
+        # row, no columns) left-outer-joined with no join columns: the rhs
+        # rows, or one all-NULL row when the pattern has no match
+        # (the empty key list is expressed as one constant key on both sides)
+        taken = set(rhs.table.physicalColumns)
+        kl, kr = "__optional_unit", "__optional_unit_r"
+        while kl in taken or kr in taken:
+            kl, kr = kl + "_", kr + "_"
+        unit = graph.session.unit().withColumns((IntegerLit(1), kl), header=RecordHeader({}))
+        rtab = rhs.table.withColumns((IntegerLit(1), kr), header=rhs.header, params=params)
+        joined = unit.join(rtab, "left_outer", (kl, kr)).drop(kl, kr)
+        return Planned(joined, rhs.header)
     common = [e for e in lhs.header.expressions if e in rhs.header]
     join_vars = [e for e in common if isinstance(e, Var)]
     if not join_vars:

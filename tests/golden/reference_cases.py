@@ -338,4 +338,16 @@ OPTIONAL_CASES.append(
             Match([NodeP("a"), NodeP("c", ("NonExistent",))], [RelP("r2", "a", "c")], optional=True)],
            [ret(("b", N("b")), ("c", N("c")))]),
      [{"b": None, "c": None}]))
+OPTIONAL_CASES += [
+    ("optional_match_leading_no_label", "MTa/OptionalMatchTests.scala:51-60", "CREATE (:A)",
+     Query([Match([NodeP("n", ("B",))], optional=True)], [ret(("n", N("n")))]),
+     [{"n": None}]),
+    # the reference RETURNs * (b as a node); b's name stands for the node here
+    ("optional_match_leading", "MTa/OptionalMatchTests.scala:423-444",
+     """CREATE (p1:Person {name: "Alice"})
+        CREATE (p2:Person {name: "Bob"})""",
+     Query([Match([NodeP("a", ("Foo",))], optional=True), Match([NodeP("b", ("Person",))])],
+           [ret(("a", N("a")), ("b.name", P("b", "name")))]),
+     [{"a": None, "b.name": "Alice"}, {"a": None, "b.name": "Bob"}]),
+]
 CASES = CASES + OPTIONAL_CASES

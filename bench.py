@@ -238,6 +238,7 @@ def run_single(args):
                                       "(capf_table_count_async), K counts checked after the final sync"
                                       if pipelined else "query-at-a-time (result downloaded every step)")
     result["config"]["ms_per_step_query_at_a_time"] = elapsed_sync * 1e3 / args.steps
+    result["config"]["parity"] = check_fixture(args, count)
     if not args.no_cpu and args.query == "two_hop":
         result["cpu_baseline"] = cpu_baseline(s, g, args.scale, args.cpu_seconds)
     print(json.dumps(result))
@@ -263,8 +264,15 @@ def run_distributed(args):
     sys.stdout.flush()
     json_fd = os.dup(1)
     os.dup2(2, 1)
-    torch.cuda.set_device(local)
-    dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    if args.one_device:
+        # rehearsal of the N-rank path on a 1-GPU box: every rank on cuda:0,
+        # gloo collectives (RCCL refuses two ranks on one device)
+        local = 0
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     s = GpuSession.on_torch_stream(local)
     m = args.edge_factor << args.scale
     n_nodes = 1 << args.scale
@@ -339,6 +347,7 @@ def run_distributed(args):
         got = slots.cpu().tolist()
         if any(c != count for c in got):
             raise SystemExit(f"rank {rank}: pipelined counts {got} differ from {count}")
+    parity = check_fixture(args, count)
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
@@ -350,6 +359,12 @@ def run_distributed(args):
     torch.cuda.synchronize()
     s.set_profiling(False)
     prof = s.profile()
+    # every rank's device time per query; the JSON reports the slowest rank's
+    rank_ms = sum(v["total_ms"] for k, v in prof.items() if k in PIPELINE) / prof_steps
+    per_rank = torch.zeros(world, dtype=torch.float64, device="cuda")
+    per_rank[rank] = rank_ms
+    dist.all_reduce(per_rank, op=dist.ReduceOp.SUM)
+    per_rank = per_rank.cpu().tolist()
     sys.stdout.flush()
     os.dup2(json_fd, 1)
     if rank == 0:
@@ -377,10 +392,63 @@ def run_distributed(args):
                 "steps_mode": ("pipelined: step i enqueues the local count + all-reduce into slot i "
                                "without a host read; K counts checked after the final sync"
                                if pipelined else "query-at-a-time"),
+                "parity": parity,
+                "device_ms_per_query_by_rank": per_rank,
+                "max_rank_device_ms": max(per_rank),
+                "one_device_rehearsal": bool(args.one_device),
             },
             "roofline": pipeline_roofline(prof, prof_steps, compulsory),
         }))
     dist.destroy_process_group()
+
+
+def free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` started by hand (no WORLD_SIZE in the env): start N
+    fresh rank processes with torch.distributed.run, one per GPU, and exit
+    with the launcher's code.  This process makes no GPU call (it never
+    imports the backend), so the ranks are clean children; rank 0 prints
+    the JSON line on the inherited stdout."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def fixture_count(query, scale, edge_factor):
+    """The committed count for this workload (tests/golden/rmat_counts.json,
+    computed by oracle/rmat.c in the dev container), or None."""
+    if edge_factor != 16:
+        return None
+    path = os.path.join(ROOT, "tests", "golden", "rmat_counts.json")
+    try:
+        with open(path) as f:
+            c = json.load(f)
+    except OSError:
+        return None
+    if query == "triangle":
+        return c.get("triangle", {}).get(str(scale))
+    e = c.get("full", {}).get(str(scale)) or c.get("rmat", {}).get(str(scale))
+    return e.get(query) if e else None
+
+
+def check_fixture(args, count):
+    """Parity outside the timed region: the bench's own count must be the
+    fixture's (SystemExit otherwise, so no number is printed for a wrong
+    answer)."""
+    want = fixture_count(args.query, args.scale, args.edge_factor)
+    if want is not None and count != want:
+        raise SystemExit(f"count {count} != committed fixture {want} ({args.query} s{args.scale})")
+    return {"fixture": want, "match": want is not None}
 
 
 def main():
@@ -398,10 +466,16 @@ def main():
     ap.add_argument("--dist", action="store_true", help="distributed path even at world size 1")
     ap.add_argument("--query", choices=["two_hop", "triangle", "one_hop_person"], default="two_hop",
                     help="two_hop: the headline (config 3); triangle: config 4; one_hop_person: config 2")
+    ap.add_argument("--one-device", action="store_true",
+                    help="rehearsal: all N ranks on cuda:0 with gloo collectives (not a scaling number)")
     ap.add_argument("--layout", choices=["node", "edge"], default="node",
                     help="multi-GPU graph layout (N > 1): node-partitioned copies or edge-range shards")
     args = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus and "WORLD_SIZE" in os.environ:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if args.gpus > 1 or world > 1 or args.dist:
         run_distributed(args)
     else:

@@ -126,4 +126,28 @@ def gpu_two_hop_count_sharded_async(session, in_copy, out_copy, n_nodes, partial
     rank = dist.get_rank(group)
     chain2_sharded_count_async(session, in_copy, out_copy, node_base, n_nodes, world, rank,
                                partial.data_ptr())
+    sum_partials(partial, group)
+
+
+def sum_partials(partial, group=None):
+    """The one collective of the node-partitioned count: an int64 SUM
+    all-reduce of the per-rank partials, in place (RCCL on the GPU; gloo in
+    the CPU tests)."""
     dist.all_reduce(partial, op=dist.ReduceOp.SUM, group=group)
+    return partial
+
+
+def hist_bits(n_nodes):
+    """k of the node_mix domain 2^k ≥ n_nodes (at least 2^16: one bucket)."""
+    k = 16
+    while (1 << k) < n_nodes:
+        k += 1
+    return k
+
+
+def owned_buckets(n_nodes, world, rank):
+    """[b0, b1): the 64 Ki-index buckets of node_mix owned by `rank`
+    (capf_table_node_partition / capf_chain2_sharded_count use the same split:
+    contiguous bucket ranges, nb·r/G .. nb·(r+1)/G)."""
+    nb = (1 << hist_bits(n_nodes)) >> 16
+    return nb * rank // world, nb * (rank + 1) // world

@@ -59,6 +59,10 @@ def lib():
         l.pipeline_probe.restype = u64
         l.pipeline_free.argtypes = [P]
         l.pipeline_free.restype = None
+        l.rmat_stream_counts.argtypes = [i32, u64, u32, u32, u32, i64, i32, P]
+        l.rmat_stream_counts.restype = None
+        l.count_triangle_trace.argtypes = [P, P, i64, i64, i32]
+        l.count_triangle_trace.restype = u64
         l.oracle_splitmix64.argtypes = [u64]
         l.oracle_splitmix64.restype = u64
         _lib = l
@@ -112,6 +116,25 @@ def count_triangle_formula(src, dst, n):
     L = np.bincount(s[s == d], minlength=n).astype(object)
     bad = sum(int(x) ** 3 - int(x) * (int(x) - 1) * (int(x) - 2) for x in L if x)
     return tr - bad
+
+
+def count_triangle_trace(src, dst, n, threads=8):
+    """trace(A^3) − self-loop corrections by sorted-list intersection in C
+    (threads; an independent method for the larger fixture scales)."""
+    src = np.ascontiguousarray(src, dtype=np.int64)
+    dst = np.ascontiguousarray(dst, dtype=np.int64)
+    return int(lib().count_triangle_trace(src.ctypes.data, dst.ctypes.data, len(src), n, threads))
+
+
+def stream_counts(scale, edge_factor=16, threads=8):
+    """Closed-form counts of the full-size R-MAT graph, streamed (no edge
+    arrays): dict(two_hop, self_loops, one_hop_person, max_in, max_out)."""
+    res = np.zeros(5, dtype=np.uint64)
+    ta, tab, tabc = thresholds()
+    lib().rmat_stream_counts(scale, rmat_seed(scale), ta, tab, tabc, edge_factor << scale, threads,
+                             res.ctypes.data)
+    keys = ("two_hop", "self_loops", "one_hop_person", "max_in", "max_out")
+    return {k: int(v) for k, v in zip(keys, res)}
 
 
 def count_2hop(src, dst, n):

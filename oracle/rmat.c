@@ -309,3 +309,250 @@ void pipeline_free(void *handle) {
   free(p->js.r2_rows);
   free(p);
 }
+
+/* ------------------------------------------- full-size counts (fixtures) */
+/* Streaming closed forms at the headline sizes (R-MAT s22/s24): every thread
+ * generates its contiguous edge range with rmat_edges' arithmetic and keeps
+ * private in/out degree histograms; nothing of size M is ever stored.
+ * out[0] = Σ_b in(b)·out(b) − self-loops  (2-hop, (a)-->(b)-->(c), r1 <> r2)
+ * out[1] = self-loops
+ * out[2] = #rels whose source carries the Person label (config 2,
+ *          (a:Person)-->(b): b ranges over every node table)
+ * out[3] = max in-degree, out[4] = max out-degree                            */
+typedef struct {
+  int scale;
+  uint64_t seed;
+  uint32_t ta, tab, tabc;
+  int64_t lo, hi, n;
+  const uint8_t *person;
+  uint32_t *in, *out;
+  uint64_t loops, person_rels;
+} StreamTask;
+
+static void *stream_worker(void *arg) {
+  StreamTask *t = (StreamTask *)arg;
+  enum { CH = 1 << 16 };
+  int64_t *s = (int64_t *)malloc(CH * 8), *d = (int64_t *)malloc(CH * 8);
+  for (int64_t e = t->lo; e < t->hi; e += CH) {
+    const int64_t c = t->hi - e < CH ? t->hi - e : CH;
+    rmat_edges(t->scale, t->seed, t->ta, t->tab, t->tabc, e, c, s, d);
+    for (int64_t k = 0; k < c; ++k) {
+      t->out[s[k]]++;
+      t->in[d[k]]++;
+      t->loops += s[k] == d[k];
+      t->person_rels += t->person[s[k]];
+    }
+  }
+  free(s);
+  free(d);
+  return NULL;
+}
+
+void rmat_stream_counts(int scale, uint64_t seed, uint32_t ta, uint32_t tab, uint32_t tabc, int64_t m,
+                        int threads, uint64_t *res) {
+  if (threads < 1) threads = 1;
+  const int64_t n = (int64_t)1 << scale;
+  uint8_t *person = (uint8_t *)malloc((size_t)n);
+  node_labels(0, n, seed, person);
+  pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * threads);
+  StreamTask *ts = (StreamTask *)calloc((size_t)threads, sizeof(StreamTask));
+  for (int i = 0; i < threads; ++i) {
+    StreamTask *t = &ts[i];
+    t->scale = scale;
+    t->seed = seed;
+    t->ta = ta;
+    t->tab = tab;
+    t->tabc = tabc;
+    t->lo = m * i / threads;
+    t->hi = m * (i + 1) / threads;
+    t->n = n;
+    t->person = person;
+    t->in = (uint32_t *)calloc((size_t)n, 4);
+    t->out = (uint32_t *)calloc((size_t)n, 4);
+    pthread_create(&th[i], NULL, stream_worker, t);
+  }
+  uint64_t loops = 0, person_rels = 0;
+  for (int i = 0; i < threads; ++i) {
+    pthread_join(th[i], NULL);
+    loops += ts[i].loops;
+    person_rels += ts[i].person_rels;
+  }
+  uint64_t total = 0, max_in = 0, max_out = 0;
+  for (int64_t v = 0; v < n; ++v) {
+    uint64_t a = 0, b = 0;
+    for (int i = 0; i < threads; ++i) {
+      a += ts[i].in[v];
+      b += ts[i].out[v];
+    }
+    total += a * b;
+    if (a > max_in) max_in = a;
+    if (b > max_out) max_out = b;
+  }
+  for (int i = 0; i < threads; ++i) {
+    free(ts[i].in);
+    free(ts[i].out);
+  }
+  free(ts);
+  free(th);
+  free(person);
+  res[0] = total - loops;
+  res[1] = loops;
+  res[2] = person_rels;
+  res[3] = max_in;
+  res[4] = max_out;
+}
+
+/* Directed triangle count by a method independent of csrc/triangle.hip (which
+ * orients an undirected simple graph by degree):
+ *   count = trace(A³) − Σ_x (L³ − L(L−1)(L−2)),   L = A[x][x]
+ * (closed walks a→b→c→a of rels; only three self-loops at one node can reuse
+ * a rel), with trace(A³) = Σ_{(a,b)} A[a][b] · Σ_c A[b][c]·A[c][a] evaluated
+ * by intersecting b's sorted out-list with a's sorted in-list (both with
+ * multiplicities; binary search of the shorter list into the longer).
+ * Threads take 64-node chunks of a from a shared counter (hub skew).        */
+typedef struct {
+  const int64_t *ooff, *ioff;
+  const int64_t *onb, *inb;  /* distinct neighbours, sorted */
+  const uint32_t *omul, *imul;
+  int64_t n;
+  int64_t *next; /* shared chunk counter */
+  pthread_mutex_t *mu;
+  uint64_t sum;
+} TriTask;
+
+static uint64_t isect(const int64_t *x, const uint32_t *xm, int64_t nx, const int64_t *y,
+                      const uint32_t *ym, int64_t ny) {
+  uint64_t s = 0;
+  if (nx > ny) {
+    const int64_t *t = x; x = y; y = t;
+    const uint32_t *tm = xm; xm = ym; ym = tm;
+    int64_t tn = nx; nx = ny; ny = tn;
+  }
+  if (nx == 0) return 0;
+  if (ny < 16 * nx) { /* merge */
+    int64_t i = 0, j = 0;
+    while (i < nx && j < ny) {
+      if (x[i] < y[j]) ++i;
+      else if (x[i] > y[j]) ++j;
+      else { s += (uint64_t)xm[i] * ym[j]; ++i; ++j; }
+    }
+    return s;
+  }
+  int64_t lo = 0;
+  for (int64_t i = 0; i < nx; ++i) { /* x sorted: search window only moves right */
+    int64_t a = lo, b = ny;
+    while (a < b) {
+      int64_t mid = (a + b) >> 1;
+      if (y[mid] < x[i]) a = mid + 1; else b = mid;
+    }
+    lo = a;
+    if (a < ny && y[a] == x[i]) s += (uint64_t)xm[i] * ym[a];
+  }
+  return s;
+}
+
+static void *tri_worker(void *arg) {
+  TriTask *t = (TriTask *)arg;
+  uint64_t sum = 0;
+  for (;;) {
+    pthread_mutex_lock(t->mu);
+    int64_t a0 = *t->next;
+    *t->next += 64;
+    pthread_mutex_unlock(t->mu);
+    if (a0 >= t->n) break;
+    int64_t a1 = a0 + 64 < t->n ? a0 + 64 : t->n;
+    for (int64_t a = a0; a < a1; ++a)
+      for (int64_t k = t->ooff[a]; k < t->ooff[a + 1]; ++k) {
+        const int64_t b = t->onb[k];
+        sum += (uint64_t)t->omul[k] * isect(t->onb + t->ooff[b], t->omul + t->ooff[b], t->ooff[b + 1] - t->ooff[b],
+                                            t->inb + t->ioff[a], t->imul + t->ioff[a], t->ioff[a + 1] - t->ioff[a]);
+      }
+  }
+  t->sum = sum;
+  return NULL;
+}
+
+static int cmp_i64(const void *a, const void *b) {
+  const int64_t x = *(const int64_t *)a, y = *(const int64_t *)b;
+  return x < y ? -1 : x > y;
+}
+
+/* CSR of distinct sorted neighbours with multiplicities: key[e] → val[e]. */
+static void build_mcsr(const int64_t *key, const int64_t *val, int64_t m, int64_t n, int64_t **off_o,
+                       int64_t **nb_o, uint32_t **mul_o) {
+  int64_t *off = (int64_t *)calloc((size_t)n + 1, 8), *pos = (int64_t *)malloc((size_t)n * 8);
+  int64_t *adj = (int64_t *)malloc((size_t)(m > 0 ? m : 1) * 8);
+  for (int64_t e = 0; e < m; ++e) off[key[e] + 1]++;
+  for (int64_t v = 0; v < n; ++v) off[v + 1] += off[v];
+  memcpy(pos, off, (size_t)n * 8);
+  for (int64_t e = 0; e < m; ++e) adj[pos[key[e]]++] = val[e];
+  int64_t *noff = (int64_t *)calloc((size_t)n + 1, 8);
+  uint32_t *mul = (uint32_t *)malloc((size_t)(m > 0 ? m : 1) * 4);
+  int64_t w = 0;
+  for (int64_t v = 0; v < n; ++v) {
+    int64_t b = off[v], e = off[v + 1];
+    qsort(adj + b, (size_t)(e - b), 8, cmp_i64);
+    noff[v] = w;
+    for (int64_t i = b; i < e;) {
+      int64_t j = i;
+      while (j < e && adj[j] == adj[i]) ++j;
+      adj[w] = adj[i];
+      mul[w] = (uint32_t)(j - i);
+      ++w;
+      i = j;
+    }
+  }
+  noff[n] = w;
+  free(off);
+  free(pos);
+  *off_o = noff;
+  *nb_o = adj;
+  *mul_o = mul;
+}
+
+uint64_t count_triangle_trace(const int64_t *src, const int64_t *dst, int64_t m, int64_t n, int threads) {
+  if (threads < 1) threads = 1;
+  /* ids outside [0, n) never match a node scan: drop those rels */
+  int64_t *s = (int64_t *)malloc((size_t)(m > 0 ? m : 1) * 8), *d = (int64_t *)malloc((size_t)(m > 0 ? m : 1) * 8);
+  int64_t mm = 0;
+  for (int64_t e = 0; e < m; ++e)
+    if (src[e] >= 0 && src[e] < n && dst[e] >= 0 && dst[e] < n) {
+      s[mm] = src[e];
+      d[mm] = dst[e];
+      ++mm;
+    }
+  int64_t *ooff, *onb, *ioff, *inb;
+  uint32_t *omul, *imul;
+  build_mcsr(s, d, mm, n, &ooff, &onb, &omul);
+  build_mcsr(d, s, mm, n, &ioff, &inb, &imul);
+  uint64_t bad = 0;
+  {
+    uint32_t *L = (uint32_t *)calloc((size_t)n, 4);
+    for (int64_t e = 0; e < mm; ++e) L[s[e]] += s[e] == d[e];
+    for (int64_t v = 0; v < n; ++v) {
+      const uint64_t l = L[v];
+      if (l) bad += l * l * l - l * (l - 1) * (l - 2);
+    }
+    free(L);
+  }
+  free(s);
+  free(d);
+  int64_t next = 0;
+  pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
+  pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * threads);
+  TriTask *ts = (TriTask *)calloc((size_t)threads, sizeof(TriTask));
+  for (int i = 0; i < threads; ++i) {
+    ts[i].ooff = ooff; ts[i].ioff = ioff; ts[i].onb = onb; ts[i].inb = inb;
+    ts[i].omul = omul; ts[i].imul = imul; ts[i].n = n; ts[i].next = &next; ts[i].mu = &mu;
+    pthread_create(&th[i], NULL, tri_worker, &ts[i]);
+  }
+  uint64_t tr = 0;
+  for (int i = 0; i < threads; ++i) {
+    pthread_join(th[i], NULL);
+    tr += ts[i].sum;
+  }
+  free(th);
+  free(ts);
+  free(ooff); free(onb); free(omul); free(ioff); free(inb); free(imul);
+  return tr - bad;
+}

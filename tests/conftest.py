@@ -22,19 +22,50 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: larger parity sizes")
 
 
+def cypher_value_key(v):
+    """A hashable, type-exact key of one CypherValue for Bag comparison.
+
+    CypherValue equality (okapi-api .../api/value/CypherValue.scala) is typed:
+    CypherInteger(4) != CypherFloat(4.0), so ints and floats stay distinct
+    and ints compare exactly (no float rounding of ids above 2^53).  Floats
+    are compared at 12 significant digits: the north-star tolerance for
+    floating-point aggregates (1e-12 relative) absorbs summation order.
+    NaN equals NaN here (one canonical key); NULL is its own kind.  Lists
+    (collect) compare element-wise; nodes / relationships (dicts with
+    "_kind") by identity, labels/type and properties."""
+    if v is None:
+        return ("null",)
+    if isinstance(v, bool):
+        return ("bool", v)
+    if isinstance(v, int):
+        return ("int", v)
+    if isinstance(v, float):
+        if v != v:
+            return ("float", "nan")
+        return ("float", float(f"{v:.12g}"))
+    if isinstance(v, str):
+        return ("str", v)
+    if isinstance(v, (list, tuple)):
+        return ("list", tuple(cypher_value_key(x) for x in v))
+    if isinstance(v, dict):
+        return ("map", tuple(sorted((k, cypher_value_key(x)) for k, x in v.items())))
+    if isinstance(v, (frozenset, set)):
+        return ("set", tuple(sorted(v)))
+    try:
+        import numpy as np
+        if isinstance(v, np.integer):
+            return ("int", int(v))
+        if isinstance(v, np.floating):
+            return cypher_value_key(float(v))
+    except ImportError:
+        pass
+    raise TypeError(f"no Cypher value kind for {type(v).__name__}: {v!r}")
+
+
 def bag(rows):
-    """okapi-testing Bag (OT/Bag.scala:29-51): multiset equality of records."""
-    def norm(v):
-        if v is None:
-            return ("0null", 0.0, "")
-        if isinstance(v, bool):
-            return ("bool", float(v), "")
-        if isinstance(v, (int, float)):
-            if isinstance(v, float) and v != v:
-                return ("nan", 0.0, "")
-            return ("num", float(v), "")
-        return ("str", 0.0, str(v))
-    return sorted(tuple(sorted((k, norm(v)) for k, v in r.items())) for r in rows)
+    """okapi-testing Bag (OT/Bag.scala:29-51): multiset equality of records,
+    each record a CypherMap compared with typed CypherValue equality."""
+    return sorted(tuple(sorted((k, cypher_value_key(v)) for k, v in r.items())) for r in rows)
 
 
 @pytest.fixture(scope="session")

@@ -8,7 +8,16 @@ container; /root/reference is only read here, never at test time):
                         person_0_0.csv.gz, person_knows_person_0_0.csv.gz)
   rmat_counts.json      R-MAT counts of configs 2/3 at small scales by the
                         closed forms (oracle/rmat.c), plus the config-5 query
-                        on the LDBC sample by the oracle table
+                        on the LDBC sample by the oracle table;
+                        "full": configs 2/3 at the headline sizes (s20-s24,
+                        streamed closed forms, rmat_stream_counts);
+                        "triangle": config 4 by trace(A^3) intersection
+                        (count_triangle_trace, s6-s24; s <= 10 also brute force)
+
+    python tests/golden/make_golden.py [--full]
+
+--full recomputes the full-size entries (~15 min on 8 cores for the s24
+triangle); without it they are carried over from the existing file.
 """
 import csv
 import gzip
@@ -58,6 +67,26 @@ def main():
 
     counts = {"rmat": {}, "params": {"a": cmodel.A, "b": cmodel.B, "c": cmodel.C, "edge_factor": 16,
                                       "seed": "0x5EED0000 + scale"}}
+    path = os.path.join(HERE, "rmat_counts.json")
+    old = json.load(open(path)) if os.path.exists(path) else {}
+    full = "--full" in sys.argv
+    if full or "full" not in old:
+        counts["full"] = {str(sc): cmodel.stream_counts(sc) for sc in (20, 22, 24)}
+    else:
+        counts["full"] = old["full"]
+    tri = dict(old.get("triangle", {})) if not full else {}
+    for scale in range(6, 25, 2):
+        if str(scale) in tri or (scale > 20 and not full):
+            continue
+        s, d = cmodel.rmat(scale)
+        n = 1 << scale
+        t = cmodel.count_triangle_trace(s, d, n)
+        if scale <= 10:
+            assert t == cmodel.count_triangle_brute(s, d, n)
+        if scale <= 16:
+            assert t == cmodel.count_triangle_formula(s, d, n)
+        tri[str(scale)] = t
+    counts["triangle"] = tri
     for scale in range(6, 17, 2):
         s, d = cmodel.rmat(scale)
         n = 1 << scale
@@ -70,7 +99,7 @@ def main():
     from ldbc import config5_query, ldbc_graph_data
     g = ScanGraph.from_data(OracleSession(), ldbc_graph_data())
     counts["ldbc_config5"] = sorted(([r["reach"], r["n"]] for r in run(g, config5_query())))
-    with open(os.path.join(HERE, "rmat_counts.json"), "w") as f:
+    with open(path, "w") as f:
         json.dump(counts, f, indent=1, sort_keys=True)
 
 

@@ -99,3 +99,20 @@ def test_node_mix_balances_rmat_runs():
     mixed = np.bincount(nodemix.node_mix(d, 20) >> 15, minlength=32)
     assert raw.max() / raw.mean() > 4
     assert mixed.max() / mixed.mean() < 1.5
+
+
+def test_bag_is_type_exact():
+    """The test Bag follows typed CypherValue equality: an INTEGER result is
+    not a FLOAT result (the avg-of-integers hazard, Expr.scala:1058-1066),
+    large int64 ids do not collapse through float rounding, NULL is neither
+    0 nor false, and the multiset counts duplicates."""
+    from conftest import bag
+    assert bag([{"a": 4}]) != bag([{"a": 4.0}])
+    assert bag([{"a": 2 ** 60}]) != bag([{"a": 2 ** 60 + 1}])
+    assert bag([{"a": None}]) != bag([{"a": 0}])
+    assert bag([{"a": False}]) != bag([{"a": 0}])
+    assert bag([{"a": 1}, {"a": 1}]) != bag([{"a": 1}])
+    assert bag([{"a": 0.1 + 0.2}]) == bag([{"a": 0.3}])  # 1e-12 relative tolerance
+    assert bag([{"a": float("nan")}]) == bag([{"a": float("nan")}])
+    assert bag([{"a": [1, 2]}]) != bag([{"a": [1.0, 2.0]}])
+    assert bag([{"a": 1, "b": "x"}, {"a": 2, "b": None}]) == bag([{"b": None, "a": 2}, {"b": "x", "a": 1}])

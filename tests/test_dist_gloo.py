@@ -62,26 +62,52 @@ def test_distributed_two_hop_combine(world):
 
 
 def _sharded_worker(rank, world, port, scale, q):
+    """One rank of the node-partitioned count with the product's host side
+    (capf_amd.dist: owned_buckets = the split capf_table_node_partition uses,
+    sum_partials = the one collective) and the oracle's partial in place of
+    the GPU kernel (no GPU here; tests/test_dist_gpu.py runs the kernels)."""
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
     import capf_import  # noqa: F401
+    from capf_amd import dist as cdist
     from oracle import cmodel, nodemix
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     n = 1 << scale
     src, dst = cmodel.rmat(scale)
-    # this rank's copies (capf_table_node_partition): rels it owns the target / source of
-    in_dst = dst[nodemix.owner(dst, n, world) == rank]
-    out_mask = nodemix.owner(src, n, world) == rank
+    b0, b1 = cdist.owned_buckets(n, world, rank)
+    k = cdist.hist_bits(n)
+    own = lambda x: ((nodemix.node_mix(x, k) >> 16) >= b0) & ((nodemix.node_mix(x, k) >> 16) < b1)  # noqa: E731
+    in_dst = dst[own(dst)]
+    out_mask = own(src)
     out_src, out_dst = src[out_mask], dst[out_mask]
     ein = np.bincount(in_dst, minlength=n).astype(np.int64)
     eout = np.bincount(out_src, minlength=n).astype(np.int64)
     partial = int((ein * eout).sum()) - int((out_src == out_dst).sum())
     t = torch.tensor([partial], dtype=torch.int64)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)  # the one collective of the sharded count
-    q.put((rank, int(t.item())))
+    cdist.sum_partials(t)
+    q.put((rank, int(t.item()), len(in_dst)))
     dist.destroy_process_group()
+
+
+def test_owned_buckets_match_owner():
+    """dist.owned_buckets (host) and the oracle's owner() (restating the
+    device owner_of) give every node exactly one owner, for world sizes that do
+    and do not divide the bucket count."""
+    import capf_import  # noqa: F401
+    from capf_amd import dist as cdist
+    from oracle import nodemix
+    for scale in (16, 18, 20):
+        n = 1 << scale
+        x = np.arange(n)
+        for world in (1, 2, 3, 5, 8):
+            own = nodemix.owner(x, n, world)
+            k = cdist.hist_bits(n)
+            b = nodemix.node_mix(x, k) >> 16
+            for r in range(world):
+                b0, b1 = cdist.owned_buckets(n, world, r)
+                assert np.array_equal((b >= b0) & (b < b1), own == r), (scale, world, r)
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -95,11 +121,12 @@ def test_node_partitioned_two_hop(world):
     procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, scale, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=180) for _ in procs)
+    res = [q.get(timeout=180) for _ in procs]
     for p in procs:
         p.join(timeout=60)
     import capf_import  # noqa: F401
     from oracle import cmodel
     src, dst = cmodel.rmat(scale)
     expect = cmodel.count_2hop(src, dst, 1 << scale)
-    assert all(v == expect for v in res.values()), (res, expect)
+    assert all(v == expect for _, v, _ in res), (res, expect)
+    assert sum(r[2] for r in res) == len(src)

@@ -30,6 +30,7 @@
 
 #include <atomic>
 #include <cstdio>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -322,19 +323,27 @@ static DataPtr edge_list_read_file(Session *s, const char *path, const ElSpec &s
       std::atomic<bool> bad{false};
       std::vector<std::thread> rd;
       const int64_t part = (n + EL_READERS - 1) / EL_READERS;
-      for (int t = 0; t < EL_READERS; ++t) {
-        const int64_t lo = t * part, hi = std::min(n, lo + part);
-        if (lo >= hi) break;
-        rd.emplace_back([&, lo, hi]() {
-          for (int64_t p = lo; p < hi;) {
-            const ssize_t r = pread(fd, stage[b] + p, (size_t)(hi - p), (off_t)(off + p));
-            if (r <= 0) {
-              bad = true;
-              return;
-            }
-            p += r;
+      auto read_range = [&, b, off](int64_t lo, int64_t hi) {
+        for (int64_t p = lo; p < hi;) {
+          const ssize_t r = pread(fd, stage[b] + p, (size_t)(hi - p), (off_t)(off + p));
+          if (r <= 0) {
+            bad = true;
+            return;
           }
-        });
+          p += r;
+        }
+      };
+      try {
+        for (int t = 0; t < EL_READERS; ++t) {
+          const int64_t lo = t * part, hi = std::min(n, lo + part);
+          if (lo >= hi) break;
+          rd.emplace_back(read_range, lo, hi);
+        }
+      } catch (const std::system_error &) {
+        // a reader thread could not be started: the ones that were started
+        // are joined below; the remaining ranges are read on this thread
+        const int64_t done_to = (int64_t)rd.size() * part;
+        read_range(done_to, n);
       }
       for (auto &th : rd) th.join();
       if (bad) illegal(std::string("edge list: short read of ") + path);
@@ -398,6 +407,8 @@ extern "C" capf_status capf_edge_list_parse(capf_session *cs, const char *bytes,
     return CAPF_OK;
   } catch (const capf::Error &e) {
     return record_error(e.code, e.what());
+  } catch (const std::exception &e) {  // bad_alloc, system_error, … never cross the C-ABI
+    return record_error(CAPF_ERR_INTERNAL, e.what());
   }
 }
 
@@ -414,5 +425,7 @@ extern "C" capf_status capf_edge_list_read(capf_session *cs, const char *path, c
     return CAPF_OK;
   } catch (const capf::Error &e) {
     return record_error(e.code, e.what());
+  } catch (const std::exception &e) {  // bad_alloc, system_error, … never cross the C-ABI
+    return record_error(CAPF_ERR_INTERNAL, e.what());
   }
 }

@@ -396,19 +396,35 @@ def plan_optional(graph, m: Match, lhs: Planned, params=None) -> Planned:
         # a leading OPTIONAL MATCH: Optional(Start, rhs) — the unit table (one
         # row, no columns) left-outer-joined with no join columns: the rhs
         # rows, or one all-NULL row when the pattern has no match
-        # (the empty key list is expressed as one constant key on both sides)
+        # (the empty key list is expressed as one constant key on both sides).
+        # The rhs is the PROBE side and the one-row unit the build side
+        # (unit RIGHT OUTER rhs ≡ rhs LEFT OUTER unit, mirrored): every rhs row
+        # finds the single build row in parallel, and the unmatched unit row
+        # still yields the all-NULL row when the pattern has no match.
         taken = set(rhs.table.physicalColumns)
         kl, kr = "__optional_unit", "__optional_unit_r"
         while kl in taken or kr in taken:
             kl, kr = kl + "_", kr + "_"
         unit = graph.session.unit().withColumns((IntegerLit(1), kl), header=RecordHeader({}))
         rtab = rhs.table.withColumns((IntegerLit(1), kr), header=rhs.header, params=params)
-        joined = unit.join(rtab, "left_outer", (kl, kr)).drop(kl, kr)
+        joined = rtab.join(unit, "right_outer", (kr, kl)).drop(kl, kr)
         return Planned(joined, rhs.header)
     common = [e for e in lhs.header.expressions if e in rhs.header]
     join_vars = [e for e in common if isinstance(e, Var)]
     if not join_vars:
-        raise NotImplementedError("OPTIONAL MATCH sharing no variable with the preceding clauses")
+        # no shared variable: a left outer join with an EMPTY join list
+        # (RelationalPlanner.scala:325 with joinExprs = ∅): every lhs row times
+        # every rhs row, or the lhs row with NULLs when the rhs is empty —
+        # expressed as one constant key on both sides
+        right = _rename_disjoint(lhs, rhs)
+        taken = set(lhs.table.physicalColumns) | set(right.table.physicalColumns)
+        kl, kr = "__optional_const", "__optional_const_r"
+        while kl in taken or kr in taken:
+            kl, kr = kl + "_", kr + "_"
+        ltab = lhs.table.withColumns((IntegerLit(1), kl), header=lhs.header, params=params)
+        rtab = right.table.withColumns((IntegerLit(1), kr), header=right.header, params=params)
+        joined = ltab.join(rtab, "left_outer", (kl, kr)).drop(kl, kr)
+        return Planned(joined, lhs.header.union(right.header))
     remove = {e for v in join_vars for e in rhs.header.owned_by(v) if e != v} | \
         {e for e in common if not isinstance(e, Var)}
     keep = [e for e in rhs.header.expressions if e not in remove]
@@ -495,7 +511,9 @@ def _fused_reach(graph, q: Query):
     if len(q.matches) != 1 or len(q.stages) < 2:
         return None
     m = q.matches[0]
-    if len(m.rels) != 1 or m.where:
+    if len(m.rels) != 1 or m.where or m.optional:
+        # OPTIONAL MATCH keeps a (NULL, …) row for an empty pattern: only the
+        # relational lowering (left outer join) has that semantics
         return None
     r = m.rels[0]
     if r.length is None or r.length[0] != 1 or r.direction not in ("out", "in") or r.src == r.dst:

@@ -138,6 +138,20 @@ def pipeline_roofline(prof, steps, compulsory_bytes, traffic_per_query=None):
     }
 
 
+def id_width(args):
+    """Ingest-time id encoding of the synthetic graph: False = plain int64,
+    4 = FOR32, 3 = FOR24 (3-byte offsets + base where the range fits 24 bits,
+    FOR32 otherwise).  The values are the reference's int64 ids either way."""
+    if args.int64:
+        return False
+    return 3 if args.query == "two_hop" and not args.for32 else 4
+
+
+def id_storage(args):
+    return {False: "int64", 4: "FOR32 (uint32 offsets + base; int64 values)",
+            3: "FOR24 (3-byte offsets + base where the range fits 24 bits; int64 values)"}[id_width(args)]
+
+
 def timed_steps(fn, steps, sync):
     sync()
     t0 = time.perf_counter()
@@ -155,7 +169,7 @@ def run_single(args):
     from capf_amd.table import GpuSession
 
     s = GpuSession(0)
-    g = rmat_graph(s, args.scale, args.edge_factor, compact=not args.int64,
+    g = rmat_graph(s, args.scale, args.edge_factor, compact=id_width(args),
                    person_split=args.query == "one_hop_person")
     q = {"triangle": triangle_query, "one_hop_person": one_hop_person_query}.get(args.query, two_hop_query)()
     n_nodes = 1 << args.scale
@@ -229,7 +243,7 @@ def run_single(args):
         "config": {
             "workload": workload_name(args),
             "scale": args.scale, "nodes": n_nodes, "rels": m, "count": count, "plan": plan,
-            "id_storage": "int64" if args.int64 else "FOR32 (uint32 offsets + base; int64 values)",
+            "id_storage": id_storage(args),
             "parallelism": "dp1",
         },
         "roofline": roof,
@@ -462,7 +476,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--sync-steps", action="store_true",
                     help="time query-at-a-time steps only (result downloaded every step)")
-    ap.add_argument("--int64", action="store_true", help="keep the id columns int64 (no FOR32)")
+    ap.add_argument("--int64", action="store_true", help="keep the id columns int64 (no FOR encoding)")
+    ap.add_argument("--for32", action="store_true", help="FOR32 id columns instead of FOR24")
     ap.add_argument("--dist", action="store_true", help="distributed path even at world size 1")
     ap.add_argument("--query", choices=["two_hop", "triangle", "one_hop_person"], default="two_hop",
                     help="two_hop: the headline (config 3); triangle: config 4; one_hop_person: config 2")

@@ -81,8 +81,12 @@ struct ColStats {
 
 // Physical encodings of an INT64 / STRING-code column.  The logical type is
 // unchanged (CTInteger = Flink LONG); ENC_FOR32 is frame-of-reference
-// compression chosen at ingest when max - min < 2^32: value = base + u32.
-enum : int32_t { ENC_PLAIN = 0, ENC_FOR32 = 1 };
+// compression chosen at ingest when max - min < 2^32: value = base + u32;
+// ENC_FOR24 the same with 3-byte little-endian offsets (max - min < 2^24,
+// e.g. node ids of a 16 Mi-node graph): 3 B per id instead of 8.  FOR24
+// buffers carry 16 zero bytes past 3·n, so 4-B and 12-B loads at any row
+// stay inside the allocation.
+enum : int32_t { ENC_PLAIN = 0, ENC_FOR32 = 1, ENC_FOR24 = 2 };
 
 struct Column {
   Type type = Type::Null;
@@ -139,14 +143,21 @@ struct ColView {
   const void *data;
   const uint8_t *valid;
   int32_t type;
-  int32_t enc;   // ENC_PLAIN / ENC_FOR32
-  int64_t base;  // ENC_FOR32 reference value
+  int32_t enc;   // ENC_PLAIN / ENC_FOR32 / ENC_FOR24
+  int64_t base;  // FOR reference value
 };
+
+// 3-byte little-endian offset of row r of a FOR24 buffer.
+__host__ __device__ inline uint32_t ld_u24(const void *p, int64_t r) {
+  const uint8_t *b = (const uint8_t *)p + 3 * r;
+  return (uint32_t)b[0] | (uint32_t)b[1] << 8 | (uint32_t)b[2] << 16;
+}
 
 // Integer value of row r of an INT64 / STRING column view (any encoding).
 __host__ __device__ inline int64_t ld_int(const ColView &c, int64_t r) {
-  return c.enc == ENC_FOR32 ? c.base + (int64_t)((const uint32_t *)c.data)[r]
-                            : ((const int64_t *)c.data)[r];
+  return c.enc == ENC_FOR32   ? c.base + (int64_t)((const uint32_t *)c.data)[r]
+         : c.enc == ENC_FOR24 ? c.base + (int64_t)ld_u24(c.data, r)
+                              : ((const int64_t *)c.data)[r];
 }
 
 // ------------------------------------------------------------- plan nodes
@@ -323,7 +334,7 @@ ColStats compute_stats(Session *s, const Column &c);
 // Frame-of-reference encodings: FOR32 stores an INTEGER column whose value
 // range spans < 2^32 as uint32 offsets from `base` (half the HBM bytes).
 // encode_column returns the input when the range does not fit.
-ColPtr encode_column(Session *s, const ColPtr &c);
+ColPtr encode_column(Session *s, const ColPtr &c, int width = 4);
 ColPtr decode_column(Session *s, const ColPtr &c);
 
 // Record an error for capf_last_error() (used by entry points outside runtime.cpp).

@@ -62,11 +62,12 @@ struct C5Big {
 template <class SH>
 constexpr int c5_stage_keys() { return 2 * SH::TILE + 8 * SH::MAXR; }
 
-// P1 arguments: four id columns (FOR32: uint32 + base; plain: int64).
-template <bool F32>
+// P1 arguments: four id columns of W bytes per id: 8 = plain int64, 4 =
+// FOR32, 3 = FOR24 (offset + base; 0 base for plain columns).
+template <int W>
 struct C5Cols {
   const void *u1, *v1, *u2, *v2;
-  int64_t bu1, bv1, bu2, bv2;  // FOR32 bases (0 for plain columns)
+  int64_t bu1, bv1, bu2, bv2;  // FOR bases (0 for plain columns)
   int64_t n;
   int64_t lo;
   uint64_t len;      // node range [lo, lo + len)
@@ -76,30 +77,52 @@ struct C5Cols {
   NodeMix mix;
 };
 
-// Four 32-bit node offsets (id − lo) from 16 B (FOR32) or 32 B (int64) at
-// row e.  CHECK = false (the columns' min/max lie inside the node range):
+struct U3 {  // 12 bytes, 4-B aligned: one global_load_dwordx3
+  uint32_t x, y, z;
+};
+
+// Raw offset of row r of a W-byte column (W = 4 or 3).
+template <int W>
+__device__ inline uint32_t c5_off(const void *p, int64_t r) {
+  return W == 4 ? ((const uint32_t *)p)[r] : ld_u24(p, r);
+}
+
+// Four 32-bit node offsets (id − lo) from 12 B (FOR24), 16 B (FOR32) or 32 B
+// (int64) at row e (a multiple of 4: FOR24 rows e..e+3 are 3 aligned
+// dwords).  CHECK = false (the columns' min/max lie inside the node range):
 // only the low word matters, offsets wrap exactly into [0, len).  With
 // CHECK, `ok` says whether each id lies in the range.
-template <bool F32, bool CHECK>
+template <int W, bool CHECK>
 __device__ inline void c5_load4(const void *p, int64_t base, int64_t lo, uint64_t len, int64_t e,
                                 int64_t e1, bool ragged, uint32_t o[4], bool ok[4]) {
   int64_t v[4];
   if (!ragged || e + 4 <= e1) {
-    if (F32) {
-      const uint4 q = *(const uint4 *)((const uint32_t *)p + e);
+    if (W != 8) {
+      uint32_t q[4];
+      if (W == 4) {
+        const uint4 t = *(const uint4 *)((const uint32_t *)p + e);
+        q[0] = t.x;
+        q[1] = t.y;
+        q[2] = t.z;
+        q[3] = t.w;
+      } else {
+        const U3 t = *(const U3 *)((const uint8_t *)p + 3 * e);
+        q[0] = t.x & 0xFFFFFFu;
+        q[1] = __builtin_amdgcn_alignbit(t.y, t.x, 24) & 0xFFFFFFu;
+        q[2] = __builtin_amdgcn_alignbit(t.z, t.y, 16) & 0xFFFFFFu;
+        q[3] = t.z >> 8;
+      }
       if (!CHECK) {
         const uint32_t d = (uint32_t)(base - lo);
-        o[0] = q.x + d;
-        o[1] = q.y + d;
-        o[2] = q.z + d;
-        o[3] = q.w + d;
+        o[0] = q[0] + d;
+        o[1] = q[1] + d;
+        o[2] = q[2] + d;
+        o[3] = q[3] + d;
         ok[0] = ok[1] = ok[2] = ok[3] = true;
         return;
       }
-      v[0] = base + (int64_t)q.x;
-      v[1] = base + (int64_t)q.y;
-      v[2] = base + (int64_t)q.z;
-      v[3] = base + (int64_t)q.w;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = base + (int64_t)q[k];
     } else {
       const longlong2 q0 = *(const longlong2 *)((const int64_t *)p + e);
       const longlong2 q1 = *(const longlong2 *)((const int64_t *)p + e + 2);
@@ -111,8 +134,7 @@ __device__ inline void c5_load4(const void *p, int64_t base, int64_t lo, uint64_
   } else {
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      v[k] = e + k < e1 ? (F32 ? base + (int64_t)((const uint32_t *)p)[e + k]
-                               : ((const int64_t *)p)[e + k])
+      v[k] = e + k < e1 ? (W != 8 ? base + (int64_t)c5_off<W>(p, e + k) : ((const int64_t *)p)[e + k])
                         : lo - 1;  // out of range → dummy
   }
 #pragma unroll
@@ -126,8 +148,12 @@ __device__ inline void c5_load4(const void *p, int64_t base, int64_t lo, uint64_
 // P1.  ALIAS: r1 and r2 scan the same (start, end) columns — the directed
 // 2-hop (a)-->(b)-->(c) — so one 8-B row gives both keys.  CHECK: range
 // tests needed.  RAGGED: the single last partial tile.
-template <bool F32, bool ALIAS, bool CHECK, bool RAGGED, class SH>
-__global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_c5_partition(C5Cols<F32> c, uint16_t *part,
+// DIAG (diagnostics only, CAPF_P1_DIAG; wrong counts): 1 = no LDS sort, the
+// keys go straight from registers to the tile region (the streaming floor of
+// P1's bytes); 2 = the count phase and scan, no scatter (the stage prefill is
+// copied out).
+template <int W, bool ALIAS, bool CHECK, bool RAGGED, class SH, int DIAG = 0>
+__global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_c5_partition(C5Cols<W> c, uint16_t *part,
                                                             uint32_t *meta,
                                                             unsigned long long *loops,
                                                             int64_t t_base) {
@@ -160,8 +186,8 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   bool pox[2][4], poy[2][4];
   if (ALIAS) {
     const int64_t e = e0 + 4 * (int64_t)threadIdx.x;
-    c5_load4<F32, CHECK>(c.u1, c.bu1, c.lo, c.len, e, e1, RAGGED, px[0], pox[0]);
-    c5_load4<F32, CHECK>(c.v1, c.bv1, c.lo, c.len, e, e1, RAGGED, py[0], poy[0]);
+    c5_load4<W, CHECK>(c.u1, c.bu1, c.lo, c.len, e, e1, RAGGED, px[0], pox[0]);
+    c5_load4<W, CHECK>(c.v1, c.bv1, c.lo, c.len, e, e1, RAGGED, py[0], poy[0]);
   }
 #pragma unroll
   for (int g = 0; g < GROUPS; ++g) {
@@ -171,8 +197,8 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
     if (ALIAS) {
       if (g + 1 < GROUPS) {
         const int64_t en = e + 4 * C5_BLOCK;
-        c5_load4<F32, CHECK>(c.u1, c.bu1, c.lo, c.len, en, e1, RAGGED, px[(g + 1) & 1], pox[(g + 1) & 1]);
-        c5_load4<F32, CHECK>(c.v1, c.bv1, c.lo, c.len, en, e1, RAGGED, py[(g + 1) & 1], poy[(g + 1) & 1]);
+        c5_load4<W, CHECK>(c.u1, c.bu1, c.lo, c.len, en, e1, RAGGED, px[(g + 1) & 1], pox[(g + 1) & 1]);
+        c5_load4<W, CHECK>(c.v1, c.bv1, c.lo, c.len, en, e1, RAGGED, py[(g + 1) & 1], poy[(g + 1) & 1]);
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -182,10 +208,10 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
         oky1[k] = poy[g & 1][k];
       }
     } else {
-      c5_load4<F32, CHECK>(c.u1, c.bu1, c.lo, c.len, e, e1, RAGGED, x1, okx1);
-      c5_load4<F32, CHECK>(c.v1, c.bv1, c.lo, c.len, e, e1, RAGGED, y1, oky1);
-      c5_load4<F32, CHECK>(c.u2, c.bu2, c.lo, c.len, e, e1, RAGGED, x2, okx2);
-      c5_load4<F32, CHECK>(c.v2, c.bv2, c.lo, c.len, e, e1, RAGGED, y2, oky2);
+      c5_load4<W, CHECK>(c.u1, c.bu1, c.lo, c.len, e, e1, RAGGED, x1, okx1);
+      c5_load4<W, CHECK>(c.v1, c.bv1, c.lo, c.len, e, e1, RAGGED, y1, oky1);
+      c5_load4<W, CHECK>(c.u2, c.bu2, c.lo, c.len, e, e1, RAGGED, x2, okx2);
+      c5_load4<W, CHECK>(c.v2, c.bv2, c.lo, c.len, e, e1, RAGGED, y2, oky2);
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -202,8 +228,10 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
       }
       lp += (in_ok & out_ok & (b == cq)) ? 1u : 0u;
       // count only (no return: no wait); positions come from a second pass
-      atomicAdd(&cur[kin[j] >> C2_BITS], 1u);
-      atomicAdd(&cur[kout[j] >> C2_BITS], 1u);
+      if (DIAG != 1) {
+        atomicAdd(&cur[kin[j] >> C2_BITS], 1u);
+        atomicAdd(&cur[kout[j] >> C2_BITS], 1u);
+      }
     }
     asm volatile("" : "+v"(lp));        // keep the self-loop sum here (no raw ids kept alive)
     __builtin_amdgcn_sched_barrier(0);  // bound what the scheduler keeps in flight
@@ -212,6 +240,19 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   // addresses alive across the scan (extra VGPRs → spills)
 #pragma unroll
   for (int j = 0; j < RPT; ++j) asm volatile("" : "+v"(kin[j]), "+v"(kout[j]));
+  if (DIAG == 1) {
+    uint4 *dst = (uint4 *)(part + t * c.rstride);
+#pragma unroll
+    for (int q = 0; q < RPT / 4; ++q)
+      dst[q * C5_BLOCK + threadIdx.x] =
+          make_uint4((kin[4 * q] & 0xFFFF) | kout[4 * q] << 16, (kin[4 * q + 1] & 0xFFFF) | kout[4 * q + 1] << 16,
+                     (kin[4 * q + 2] & 0xFFFF) | kout[4 * q + 2] << 16,
+                     (kin[4 * q + 3] & 0xFFFF) | kout[4 * q + 3] << 16);
+    if (threadIdx.x < (unsigned)nr) meta[t * nr + threadIdx.x] = 0;
+    unsigned long long lp64 = wave_reduce_sum((unsigned long long)lp);
+    if (lane_id() == 0 && lp64) atomicAdd(loops, lp64);
+    return;
+  }
   __syncthreads();
   // exclusive scan of the 8-padded run sizes (the dummy run nr last)
   uint32_t cs[RUNS_PT], sum = 0;
@@ -235,6 +276,7 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   // a run is free — P3 only counts)
 #pragma unroll
   for (int j = 0; j < RPT; ++j) {
+    if (DIAG == 2) break;
     stage[atomicAdd(&cur[kin[j] >> C2_BITS], 1u)] = (uint16_t)kin[j];
     stage[atomicAdd(&cur[kout[j] >> C2_BITS], 1u)] = (uint16_t)kout[j];
     if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
@@ -672,17 +714,22 @@ __global__ __launch_bounds__(256) void k_c3_overflow(C3Ovf o, uint32_t *h_in, ui
   }
 }
 
-template <bool F32, bool ALIAS, bool CHECK, class SH>
-static void launch_c5(Session *s, const C5Cols<F32> &c, uint16_t *part, uint32_t *meta,
+template <int W, bool ALIAS, bool CHECK, class SH>
+static void launch_c5(Session *s, const C5Cols<W> &c, uint16_t *part, uint32_t *meta,
                       unsigned long long *d_loops) {
   const int64_t nfull = c.n / SH::TILE;
   if (nfull > 0) {
-    hipLaunchKernelGGL((k_c5_partition<F32, ALIAS, CHECK, false, SH>), dim3((unsigned)nfull),
-                       dim3(C5_BLOCK), 0, s->stream, c, part, meta, d_loops, (int64_t)0);
+    const char *dg = getenv("CAPF_P1_DIAG");  // diagnostics only: wrong counts
+    const int diag = dg ? atoi(dg) : 0;
+    auto kern = diag == 1   ? k_c5_partition<W, ALIAS, CHECK, false, SH, 1>
+                : diag == 2 ? k_c5_partition<W, ALIAS, CHECK, false, SH, 2>
+                            : k_c5_partition<W, ALIAS, CHECK, false, SH, 0>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)nfull), dim3(C5_BLOCK), 0, s->stream, c, part, meta,
+                       d_loops, (int64_t)0);
     KERNEL_CHECK();
   }
   if (nfull < c.ntiles) {  // the ragged last tile
-    hipLaunchKernelGGL((k_c5_partition<F32, ALIAS, true, true, SH>), dim3(1), dim3(C5_BLOCK), 0,
+    hipLaunchKernelGGL((k_c5_partition<W, ALIAS, true, true, SH>), dim3(1), dim3(C5_BLOCK), 0,
                        s->stream, c, part, meta, d_loops, nfull);
     KERNEL_CHECK();
   }
@@ -800,8 +847,8 @@ __global__ __launch_bounds__(256) void k_c5_dot_slices(const uint32_t *si, const
   if (threadIdx.x == 0 && tot) atomicAdd(acc, tot);
 }
 
-template <bool F32, class SH>
-static void chain2_c5(Session *s, C5Cols<F32> c, bool in_range, uint32_t *h_in, uint32_t *h_out,
+template <int W, class SH>
+static void chain2_c5(Session *s, C5Cols<W> c, bool in_range, uint32_t *h_in, uint32_t *h_out,
                       unsigned long long *d_loops) {
   c.ntiles = (c.n + SH::TILE - 1) / SH::TILE;
   const int nr = 2 * c.nb;
@@ -809,14 +856,14 @@ static void chain2_c5(Session *s, C5Cols<F32> c, bool in_range, uint32_t *h_in, 
   BufPtr part = s->alloc(2 * c.rstride * c.ntiles);
   BufPtr meta = s->alloc(4 * nr * c.ntiles);
   {
-    KernelTimer kt(s, "c5_partition", (F32 ? 12.0 : 20.0) * c.n);
+    KernelTimer kt(s, "c5_partition", (2.0 * W + 4.0) * c.n);
     uint16_t *pp = (uint16_t *)part->p;
     uint32_t *mp = (uint32_t *)meta->p;
     const bool alias = c.u2 == c.u1 && c.v2 == c.v1;
-    if (alias && !in_range) launch_c5<F32, true, true, SH>(s, c, pp, mp, d_loops);
-    if (alias && in_range) launch_c5<F32, true, false, SH>(s, c, pp, mp, d_loops);
-    if (!alias && !in_range) launch_c5<F32, false, true, SH>(s, c, pp, mp, d_loops);
-    if (!alias && in_range) launch_c5<F32, false, false, SH>(s, c, pp, mp, d_loops);
+    if (alias && !in_range) launch_c5<W, true, true, SH>(s, c, pp, mp, d_loops);
+    if (alias && in_range) launch_c5<W, true, false, SH>(s, c, pp, mp, d_loops);
+    if (!alias && !in_range) launch_c5<W, false, true, SH>(s, c, pp, mp, d_loops);
+    if (!alias && in_range) launch_c5<W, false, false, SH>(s, c, pp, mp, d_loops);
   }
   C3Sides sd;
   sd.nb = c.nb;
@@ -874,7 +921,7 @@ static int c5s_copies(int nr) {
   return c;
 }
 
-template <bool F32, bool WIDE>
+template <int W, bool WIDE>
 __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_c5_shard_partition(
     C5Shard c, uint16_t *part, uint32_t *meta, unsigned long long *loops, int64_t rstride) {
   constexpr int TILE = C5S_TILE, MAXR = C5S_MAXR;
@@ -914,17 +961,17 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   bool pox[2][4], poy[2][4];
   {
     const int64_t e = e0 + 4 * (int64_t)threadIdx.x;
-    c5_load4<F32, true>(kp, kb, c.lo, c.len, e, e1, true, px[0], pox[0]);
-    if (side) c5_load4<F32, true>(c.oth, c.both, c.lo, c.len, e, e1, true, py[0], poy[0]);
+    c5_load4<W, true>(kp, kb, c.lo, c.len, e, e1, true, px[0], pox[0]);
+    if (side) c5_load4<W, true>(c.oth, c.both, c.lo, c.len, e, e1, true, py[0], poy[0]);
   }
 #pragma unroll
   for (int g = 0; g < GROUPS; ++g) {
     if (g < gu) {  // static index per unrolled group: key[] stays in VGPRs
       if (g + 1 < gu) {
         const int64_t en = e0 + 4 * ((int64_t)(g + 1) * C5_BLOCK + threadIdx.x);
-        c5_load4<F32, true>(kp, kb, c.lo, c.len, en, e1, true, px[(g + 1) & 1], pox[(g + 1) & 1]);
+        c5_load4<W, true>(kp, kb, c.lo, c.len, en, e1, true, px[(g + 1) & 1], pox[(g + 1) & 1]);
         if (side)
-          c5_load4<F32, true>(c.oth, c.both, c.lo, c.len, en, e1, true, py[(g + 1) & 1], poy[(g + 1) & 1]);
+          c5_load4<W, true>(c.oth, c.both, c.lo, c.len, en, e1, true, py[(g + 1) & 1], poy[(g + 1) & 1]);
       }
       uint32_t x[4], y[4];
       bool okx[4], oky[4];
@@ -1086,8 +1133,8 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
       BufPtr meta = s->alloc(4 * nr * ntiles);
       {
         KernelTimer kt(s, "c5_partition", (nf ? 4.0 : 8.0) * (n_in + 2 * n_out));
-        auto kern = nf ? (kbits > 24 ? k_c5_shard_partition<true, true> : k_c5_shard_partition<true, false>)
-                       : (kbits > 24 ? k_c5_shard_partition<false, true> : k_c5_shard_partition<false, false>);
+        auto kern = nf ? (kbits > 24 ? k_c5_shard_partition<4, true> : k_c5_shard_partition<4, false>)
+                       : (kbits > 24 ? k_c5_shard_partition<8, true> : k_c5_shard_partition<8, false>);
         hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(C5_BLOCK), 0, s->stream, c,
                            (uint16_t *)partb->p, (uint32_t *)meta->p, d_acc + 1, rstride);
         KERNEL_CHECK();
@@ -1141,19 +1188,21 @@ bool chain2_partitioned(Session *s, const ColView *cols, int64_t n, int64_t lo, 
   const int64_t nb = (int64_t(1) << kbits) / C2_BW;
   if (2 * nb + 1 > C5Big::MAXR) return false;  // + the dummy run
   if (n >= (int64_t(1) << 30)) return false;   // 2·n keys: 32-bit element indices in `part`
-  int nf = 0;
+  int nf = 0, n24 = 0;
   for (int i = 0; i < 4; ++i) {
     if (cols[i].valid || !cols[i].data) return false;
     if ((uintptr_t)cols[i].data & 15) return false;  // 16-B vector loads
     nf += cols[i].enc == ENC_FOR32;
+    n24 += cols[i].enc == ENC_FOR24;
   }
-  if (nf != 0 && nf != 4) return false;
+  if (n24 != 0 && n24 != 4) return false;
+  if (n24 == 0 && nf != 0 && nf != 4) return false;
   auto fill = [&](auto &c) {
     c.u1 = cols[0].data;
     c.v1 = cols[1].data;
     c.u2 = cols[2].data;
     c.v2 = cols[3].data;
-    const bool f = nf == 4;
+    const bool f = nf == 4 || n24 == 4;
     c.bu1 = f ? cols[0].base : 0;
     c.bv1 = f ? cols[1].base : 0;
     c.bu2 = f ? cols[2].base : 0;
@@ -1165,21 +1214,30 @@ bool chain2_partitioned(Session *s, const ColView *cols, int64_t n, int64_t lo, 
     c.mix = node_mix_for(kbits);
   };
   const bool small = 2 * nb + 1 <= C5Small::MAXR;
-  if (nf == 4) {
-    C5Cols<true> c;
+  if (n24 == 4) {
+    C5Cols<3> c;
     fill(c);
     if (small)
-      chain2_c5<true, C5Small>(s, c, in_range, h_in, h_out, d_loops);
+      chain2_c5<3, C5Small>(s, c, in_range, h_in, h_out, d_loops);
     else
-      chain2_c5<true, C5Big>(s, c, in_range, h_in, h_out, d_loops);
+      chain2_c5<3, C5Big>(s, c, in_range, h_in, h_out, d_loops);
     return true;
   }
-  C5Cols<false> c;
+  if (nf == 4) {
+    C5Cols<4> c;
+    fill(c);
+    if (small)
+      chain2_c5<4, C5Small>(s, c, in_range, h_in, h_out, d_loops);
+    else
+      chain2_c5<4, C5Big>(s, c, in_range, h_in, h_out, d_loops);
+    return true;
+  }
+  C5Cols<8> c;
   fill(c);
   if (small)
-    chain2_c5<false, C5Small>(s, c, in_range, h_in, h_out, d_loops);
+    chain2_c5<8, C5Small>(s, c, in_range, h_in, h_out, d_loops);
   else
-    chain2_c5<false, C5Big>(s, c, in_range, h_in, h_out, d_loops);
+    chain2_c5<8, C5Big>(s, c, in_range, h_in, h_out, d_loops);
   return true;
 }
 

@@ -181,6 +181,19 @@ __global__ void k_gather(const T *src, const uint8_t *sval, const int64_t *idx, 
   }
 }
 
+// FOR24 rows gathered into FOR32 (same base): the gathered rows are no
+// longer a scan-order stream, 4-B rows keep every later access aligned
+__global__ void k_gather_u24(const void *src, const uint8_t *sval, const int64_t *idx,
+                             uint32_t *dst, uint8_t *dval, int64_t m) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t j = idx[i];
+    bool ok = j >= 0;
+    if (dst) dst[i] = ok ? ld_u24(src, j) : 0u;
+    if (dval) dval[i] = ok ? (sval ? sval[j] : 1) : 0;
+  }
+}
+
 ColPtr gather_column(Session *s, const ColPtr &c, const int64_t *d_idx, int64_t m,
                      bool idx_may_be_null) {
   if (!d_idx) {
@@ -201,7 +214,7 @@ ColPtr gather_column(Session *s, const ColPtr &c, const int64_t *d_idx, int64_t 
   }
   bool with_valid = c->valid != nullptr || idx_may_be_null;
   ColPtr o;
-  if (c->enc == ENC_FOR32) {  // gathered rows keep the frame of reference
+  if (c->enc == ENC_FOR32 || c->enc == ENC_FOR24) {  // gathered rows keep the frame of reference
     o = std::make_shared<Column>();
     o->type = c->type;
     o->n = m;
@@ -219,6 +232,9 @@ ColPtr gather_column(Session *s, const ColPtr &c, const int64_t *d_idx, int64_t 
   if (c->type == Type::Bool)
     hipLaunchKernelGGL(k_gather<uint8_t>, dim3(g), dim3(256), 0, s->stream,
                        (const uint8_t *)c->data->p, sval, d_idx, (uint8_t *)o->data->p, dval, m);
+  else if (c->enc == ENC_FOR24)
+    hipLaunchKernelGGL(k_gather_u24, dim3(g), dim3(256), 0, s->stream, (const void *)c->data->p, sval,
+                       d_idx, (uint32_t *)o->data->p, dval, m);
   else if (c->enc == ENC_FOR32)
     hipLaunchKernelGGL(k_gather<uint32_t>, dim3(g), dim3(256), 0, s->stream,
                        (const uint32_t *)c->data->p, sval, d_idx, (uint32_t *)o->data->p, dval, m);
@@ -264,7 +280,7 @@ ColPtr concat_columns(Session *s, const ColPtr &a, const ColPtr &b, Type t) {
       if (t == Type::Bool)
         hipLaunchKernelGGL(k_copy_part<uint8_t>, dim3(g), dim3(256), 0, s->stream,
                            (const uint8_t *)src, sval, (uint8_t *)o->data->p, dval, c->n, off);
-      else if (c->enc == ENC_FOR32)
+      else if (c->enc != ENC_PLAIN)
         hipLaunchKernelGGL(k_copy_part_int, dim3(g), dim3(256), 0, s->stream, view_of(c),
                            (int64_t *)o->data->p, dval, c->n, off);
       else
@@ -291,6 +307,33 @@ __global__ void k_encode_for32(const int64_t *src, const uint8_t *valid, int64_t
     dst[i] = (valid && !valid[i]) ? 0u : (uint32_t)(src[i] - base);
 }
 
+__global__ void k_decode_for24(const void *src, int64_t base, int64_t *dst, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = base + (int64_t)ld_u24(src, i);
+}
+
+// Thread per 4 rows: 12 bytes = 3 aligned dwords (rows past n encode 0; the
+// 16-B tail pad is zeroed by the last thread).
+__global__ void k_encode_for24(const int64_t *src, const uint8_t *valid, int64_t base,
+                               uint32_t *dst, int64_t n) {
+  const int64_t groups = (n + 3) / 4;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < groups;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t r = 4 * g + k;
+      v[k] = (r < n && !(valid && !valid[r])) ? (uint32_t)(src[r] - base) & 0xFFFFFFu : 0u;
+    }
+    dst[3 * g] = v[0] | v[1] << 24;
+    dst[3 * g + 1] = v[1] >> 8 | v[2] << 16;
+    dst[3 * g + 2] = v[2] >> 16 | v[3] << 8;
+    if (g == groups - 1)
+      for (int k = 0; k < 4; ++k) dst[3 * groups + k] = 0u;
+  }
+}
+
 ColPtr decode_column(Session *s, const ColPtr &c) {
   if (c->enc == ENC_PLAIN) return c;
   auto o = std::make_shared<Column>();
@@ -299,18 +342,40 @@ ColPtr decode_column(Session *s, const ColPtr &c) {
   o->valid = c->valid;
   if (c->n > 0) {
     o->data = s->alloc(8 * c->n);
-    hipLaunchKernelGGL(k_decode_for32, dim3(grid_for(c->n, 256)), dim3(256), 0, s->stream,
-                       (const uint32_t *)c->data->p, c->base, (int64_t *)o->data->p, c->n);
+    if (c->enc == ENC_FOR24)
+      hipLaunchKernelGGL(k_decode_for24, dim3(grid_for(c->n, 256)), dim3(256), 0, s->stream,
+                         (const void *)c->data->p, c->base, (int64_t *)o->data->p, c->n);
+    else
+      hipLaunchKernelGGL(k_decode_for32, dim3(grid_for(c->n, 256)), dim3(256), 0, s->stream,
+                         (const uint32_t *)c->data->p, c->base, (int64_t *)o->data->p, c->n);
     KERNEL_CHECK();
   }
   return o;
 }
 
-ColPtr encode_column(Session *s, const ColPtr &c) {
+// width 4: FOR32 where the range fits 32 bits; width 3: FOR24 where it fits
+// 24 bits, else FOR32 where it fits 32.  Already-encoded columns unchanged.
+ColPtr encode_column(Session *s, const ColPtr &c, int width) {
   if (c->enc != ENC_PLAIN || (c->type != Type::Int64 && c->type != Type::String) || c->n == 0)
     return c;
   const ColStats &st = column_stats(s, c);
   if (st.non_null == 0 || (uint64_t)(st.max - st.min) > 0xFFFFFFFFull) return c;
+  if (width == 3 && (uint64_t)(st.max - st.min) <= 0xFFFFFFull) {
+    auto o = std::make_shared<Column>();
+    o->type = c->type;
+    o->n = c->n;
+    o->enc = ENC_FOR24;
+    o->base = st.min;
+    o->valid = c->valid;
+    const int64_t groups = (c->n + 3) / 4;
+    o->data = s->alloc(12 * groups + 16);
+    hipLaunchKernelGGL(k_encode_for24, dim3(grid_for(groups, 256)), dim3(256), 0, s->stream,
+                       (const int64_t *)c->data->p, c->valid ? (const uint8_t *)c->valid->p : nullptr,
+                       st.min, (uint32_t *)o->data->p, c->n);
+    KERNEL_CHECK();
+    o->stats = st;
+    return o;
+  }
   auto o = std::make_shared<Column>();
   o->type = c->type;
   o->n = c->n;

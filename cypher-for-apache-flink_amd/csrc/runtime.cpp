@@ -791,9 +791,14 @@ capf_status capf_table_empty(capf_session *cs, int32_t ncols, const char *const 
 }
 
 capf_status capf_table_compact(capf_table *t, capf_table **out) {
+  return capf_table_compact_width(t, 4, out);
+}
+
+capf_status capf_table_compact_width(capf_table *t, int32_t width, capf_table **out) {
   CAPF_API_BEGIN
   need(t, "table");
   need(out, "out");
+  if (width != 3 && width != 4) illegal("compact width must be 3 (FOR24) or 4 (FOR32) bytes");
   DataPtr d = materialize(t->node);
   Session *s = t->node->s;
   auto n = new_node(s, Kind::Source);
@@ -801,7 +806,7 @@ capf_status capf_table_compact(capf_table *t, capf_table **out) {
   n->types = t->node->types;
   auto e = std::make_shared<Data>();
   e->nrows = d->nrows;
-  for (const ColPtr &c : d->cols) e->cols.push_back(encode_column(s, c));
+  for (const ColPtr &c : d->cols) e->cols.push_back(encode_column(s, c, width));
   s->sync();
   n->result = e;
   *out = wrap(n);

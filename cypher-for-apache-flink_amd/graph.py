@@ -24,6 +24,7 @@ from typing import Dict, FrozenSet, List, Tuple
 from .expr import (CT_TO_CAPF, T_BOOL, T_FLOAT, T_INT, T_NULL, T_STRING, BoolLit, ElementProperty,
                    EndNode, HasLabel, HasType, NullLit, StartNode, Var)
 from .header import RecordHeader
+from .table import compact_as
 
 
 @dataclass
@@ -108,7 +109,7 @@ class ScanGraph:
                 vals = [_coerce(r[1].get(k), keys[k]) for r in rows]
                 cols.append(("p_" + k, CT_TO_CAPF[keys[k]], vals, None))
             t = session.table(cols, nrows=len(rows))
-            node_tables.append(ElementTable("node", combo, t.compact() if compact else t, keys))
+            node_tables.append(ElementTable("node", combo, compact_as(t, compact), keys))
         for typ, rows in sorted(by_type.items()):
             keys = {}
             for *_, props in rows:
@@ -122,7 +123,7 @@ class ScanGraph:
                 vals = [_coerce(r[3].get(k), keys[k]) for r in rows]
                 cols.append(("p_" + k, CT_TO_CAPF[keys[k]], vals, None))
             t = session.table(cols, nrows=len(rows))
-            rel_tables.append(ElementTable("rel", frozenset([typ]), t.compact() if compact else t, keys))
+            rel_tables.append(ElementTable("rel", frozenset([typ]), compact_as(t, compact), keys))
         return ScanGraph(session, node_tables, rel_tables)
 
     # ------------------------------------------------------------ scans

@@ -10,6 +10,7 @@ type `E`), or with the config-2 `Person` / `Other` split.
 from .expr import BoolLit, Equals, Var
 from .graph import ElementTable, ScanGraph
 from .header import RecordHeader
+from .table import compact_as
 
 A, B, C = 0.57, 0.19, 0.19
 
@@ -27,31 +28,29 @@ def rmat_graph(session, scale, edge_factor=16, seed=None, person_split=False, fi
                node_base=0, n_nodes=None, compact=False):
     """ScanGraph over an R-MAT edge table (optionally a shard [first, first+count)).
 
-    compact=True stores the id columns FOR32-encoded (GpuTable.compact)."""
+    compact=True stores the id columns FOR32-encoded (GpuTable.compact),
+    compact=3 FOR24 (3 B per id where the range fits 24 bits)."""
     seed = rmat_seed(scale) if seed is None else seed
     m = edge_factor << scale
     count = m - first if count is None else count
     n = (1 << scale) if n_nodes is None else n_nodes
     rels = session.rmat_rels(scale, seed, thresholds(), first, count, id_base=0)
-    if compact:
-        rels = rels.compact()
+    rels = compact_as(rels, compact)
     rel_tables = [ElementTable("rel", frozenset(["E"]), rels, {})]
     if person_split:
         nodes = session.range_nodes(node_base, n, seed=seed, id_col="id", label_col="person")
-        if compact:
-            nodes = nodes.compact()
+        nodes = compact_as(nodes, compact)
         h = RecordHeader({Var("person"): "person"})
         person = nodes.filter(Equals(Var("person"), BoolLit(True)), h, {}).select("id")
         other = nodes.filter(Equals(Var("person"), BoolLit(False)), h, {}).select("id")
         if compact:
             # one element table per label combination, built at ingest
             # (ScanGraph.scala:115-128): materialised here, not re-filtered per query
-            person, other = person.compact(), other.compact()
+            person, other = compact_as(person, compact), compact_as(other, compact)
         node_tables = [ElementTable("node", frozenset(["Person"]), person, {}),
                        ElementTable("node", frozenset(["Other"]), other, {})]
     else:
         nodes = session.range_nodes(node_base, n, id_col="id")
-        if compact:
-            nodes = nodes.compact()
+        nodes = compact_as(nodes, compact)
         node_tables = [ElementTable("node", frozenset(["V"]), nodes, {})]
     return ScanGraph(session, node_tables, rel_tables)

@@ -280,13 +280,16 @@ class GpuTable:
     def cache(self):
         return self._new("capf_table_cache", self._h)
 
-    def compact(self):
+    def compact(self, width=4):
         """Materialised copy whose INTEGER columns are FOR32-encoded where
-        their value range fits 32 bits (same rows; half the id bytes)."""
-        return self._new("capf_table_compact", self._h)
+        their value range fits 32 bits (same rows; half the id bytes);
+        width=3: FOR24 where the range fits 24 bits (3 B per id)."""
+        if width == 4:
+            return self._new("capf_table_compact", self._h)
+        return self._new("capf_table_compact_width", self._h, int(width))
 
     def encoding(self, col):
-        """(encoding, base) of a column: (0, 0) plain, (1, base) FOR32."""
+        """(encoding, base) of a column: (0, 0) plain, (1, base) FOR32, (2, base) FOR24."""
         e, b = c_int32(), c_int64()
         _lib.call("capf_table_column_encoding", self._h, col.encode(), byref(e), byref(b))
         return e.value, b.value
@@ -375,6 +378,14 @@ class GpuTable:
         _lib.call("capf_chain2_local_hists", self.session._h, self._h, src_col.encode(), dst_col.encode(),
                   int(node_base), int(n_nodes), c_void_p(d_in), c_void_p(d_out), byref(loops))
         return loops.value
+
+
+def compact_as(table, compact):
+    """Ingest-time encoding choice of the graph builders: False = plain int64,
+    True / 4 = FOR32 where the range fits, 3 = FOR24 where it fits (else FOR32)."""
+    if not compact:
+        return table
+    return table.compact(3 if compact == 3 else 4)
 
 
 def chain2_sharded_count_async(session, in_copy, out_copy, node_base, n_nodes, parts, part,

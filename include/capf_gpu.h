@@ -219,9 +219,13 @@ capf_status capf_table_device_column(capf_table *t, const char *col, void **valu
  * stores ids as Java longs (CAPFGraph.scala ids are LongType).              */
 #define CAPF_ENC_PLAIN 0
 #define CAPF_ENC_FOR32 1
+#define CAPF_ENC_FOR24 2 /* 3-byte offsets (range < 2^24): 3 B per id */
 /* Materialise t and re-encode every INTEGER column whose value range spans
  * < 2^32 as FOR32.  Results of every operator are unchanged.               */
 capf_status capf_table_compact(capf_table *t, capf_table **out);
+/* The same with a narrowest width: 3 = FOR24 where the range spans < 2^24
+ * (FOR32 where it only fits 32 bits), 4 = capf_table_compact.             */
+capf_status capf_table_compact_width(capf_table *t, int32_t width, capf_table **out);
 capf_status capf_table_column_encoding(capf_table *t, const char *col, int32_t *enc,
                                        int64_t *base);
 

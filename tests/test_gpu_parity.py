@@ -30,7 +30,7 @@ from oracle.table_np import OracleSession
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("compact", [False, True], ids=["int64", "for32"])
+@pytest.mark.parametrize("compact", [False, True, 3], ids=["int64", "for32", "for24"])
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
 def test_reference_case_on_gpu(gpu_session, case, compact):
     cid, src, create, query, expected = case
@@ -47,7 +47,7 @@ ONE_HOP_PERSON = Query([Match([NodeP("a", ("Person",)), NodeP("b")], [RelP("r", 
                        [Stage([("count", CountStar())])])
 
 
-@pytest.mark.parametrize("compact", [False, True], ids=["int64", "for32"])
+@pytest.mark.parametrize("compact", [False, True, 3], ids=["int64", "for32", "for24"])
 @pytest.mark.parametrize("scale", [6, 8, 10, 12, 14, 16, 18])
 def test_two_hop_count_rmat(gpu_session, scale, compact):
     g = rmat_graph(gpu_session, scale, compact=compact)
@@ -61,7 +61,7 @@ def test_two_hop_count_rmat(gpu_session, scale, compact):
 
 
 @pytest.mark.parametrize("variant", ["partitioned", "atomic"])
-@pytest.mark.parametrize("compact", [False, True], ids=["int64", "for32"])
+@pytest.mark.parametrize("compact", [False, True, 3], ids=["int64", "for32", "for24"])
 @pytest.mark.parametrize("scale,count,nodes", [(6, None, None), (11, 30001, None), (14, None, None),
                                                (15, 123457, None), (12, None, 3000), (14, 50001, 9999)])
 def test_two_hop_partition_variants(gpu_session, monkeypatch, variant, compact, scale, count, nodes):
@@ -114,7 +114,7 @@ def test_rmat_generator_bit_exact(gpu_session):
     assert np.array_equal(i, np.arange(1000, 6000))
 
 
-@pytest.mark.parametrize("compact", [False, True], ids=["int64", "for32"])
+@pytest.mark.parametrize("compact", [False, True, 3], ids=["int64", "for32", "for24"])
 @pytest.mark.parametrize("scale,count", [(8, None), (12, None), (16, None), (12, 40001), (14, 9)])
 def test_one_hop_person_count_rmat(gpu_session, scale, count, compact):
     """Config 2; `count` makes the rel table ragged (not a multiple of the
@@ -179,10 +179,11 @@ def _both(cols):
     gs = pytest.gpu_session_ref
     g = gs.table(cols)
     if pytest.capf_compact:
-        g = g.compact()
-        for name, t, _, _ in cols:  # every non-empty INTEGER/STRING column is re-encoded
+        width = 3 if pytest.capf_compact == 3 else 4
+        g = g.compact(width)
+        for name, t, values, _ in cols:  # every non-empty INTEGER/STRING column is re-encoded
             if t in (T_INT, T_STRING):
-                assert g.encoding(name)[0] == 1, name
+                assert g.encoding(name)[0] in ((1, 2) if width == 3 else (1,)), name
     return g, OracleSession().table(cols)
 
 
@@ -192,9 +193,9 @@ def _expose(gpu_session):
     pytest.capf_compact = False
 
 
-@pytest.fixture(params=[False, True], ids=["int64", "for32"])
+@pytest.fixture(params=[False, True, 3], ids=["int64", "for32", "for24"])
 def encoding(request, _expose):
-    """Operator tests run on plain int64 columns and on FOR32-compacted ones."""
+    """Operator tests run on plain int64 columns and on FOR32 / FOR24-compacted ones."""
     pytest.capf_compact = request.param
 
 
@@ -254,8 +255,8 @@ def test_join_parity(jt):
          ("bv", T_INT, list(range(n2)), None)]
     gs = pytest.gpu_session_ref
     ga, gb = gs.table(a), gs.table(b)
-    if pytest.capf_compact:  # mixed encodings: FOR32 left keys probe plain right keys
-        ga = ga.compact()
+    if pytest.capf_compact:  # mixed encodings: FOR32/FOR24 left keys probe plain right keys
+        ga = ga.compact(3 if pytest.capf_compact == 3 else 4)
     oa, ob = OracleSession().table(a), OracleSession().table(b)
     pairs = [] if jt == "cross" else [("ak", "bk"), ("as", "bs")]
     assert bag(ga.join(gb, jt, *pairs).rows) == bag(oa.join(ob, jt, *pairs).rows)
@@ -316,6 +317,30 @@ def test_order_skip_limit_parity():
         assert [r["i"] for r in rg] == [r["i"] for r in ro]
 
 
+def test_compact_for24_roundtrip(gpu_session):
+    """FOR24 (3-byte offsets): values, NULLs, a base near 2^62, ragged row
+    counts (not a multiple of the 4-row group), the widest 24-bit range, and
+    columns too wide for 24 bits (FOR32) or 32 bits (plain)."""
+    big = 2 ** 62
+    for n in (1, 3, 4, 5, 1027):
+        vals = [big + (i * 7919) % (1 << 24) if i % 5 else None for i in range(n)]
+        vals[0] = big  # min
+        if n > 1:
+            vals[-1] = big + (1 << 24) - 1  # max: range exactly 2^24 - 1
+        cols = [("a", T_INT, vals, None), ("w", T_INT, [i << 24 for i in range(n)], None)]
+        t = gpu_session.table(cols).compact(3)
+        assert t.encoding("a") == (2, big), n
+        assert t.encoding("w")[0] == (2 if n == 1 else 1 if n - 1 < 256 else 0), n
+        assert t.column_values("a") == vals
+        assert t.column_values("w") == [i << 24 for i in range(n)]
+        # gather (filter) and concat (union) of a FOR24 column
+        ha = RecordHeader({Var("a"): "a"})
+        f = t.filter(GreaterThan(Var("a"), IntegerLit(big + 1000)), ha, {})
+        assert f.column_values("a") == [v for v in vals if v is not None and v > big + 1000]
+        u = t.select("a").unionAll(gpu_session.table([("a", T_INT, [5, None], None)]))
+        assert u.column_values("a") == vals + [5, None]
+
+
 def test_compact_roundtrip(gpu_session):
     big = 10 ** 15
     cols = [("a", T_INT, [big + 7, big, None, big + 2 ** 32 - 1], None),
@@ -339,7 +364,7 @@ def test_unit_and_empty(gpu_session):
 
 
 @pytest.mark.parametrize("variant", ["partitioned", "atomic"])
-@pytest.mark.parametrize("compact", [False, True], ids=["int64", "for32"])
+@pytest.mark.parametrize("compact", [False, True, 3], ids=["int64", "for32", "for24"])
 @pytest.mark.parametrize("scale,base", [(10, 0), (13, 5), (16, 0)])
 def test_local_hists_hashed_layout(gpu_session, monkeypatch, variant, compact, scale, base):
     """capf_chain2_local_hists: every counter of the node_mix-indexed in/out
@@ -371,7 +396,7 @@ def test_local_hists_hashed_layout(gpu_session, monkeypatch, variant, compact, s
 
 
 @pytest.mark.parametrize("n", [1 << 17, 100000], ids=["in_range", "checked"])
-@pytest.mark.parametrize("compact", [False, True], ids=["int64", "for32"])
+@pytest.mark.parametrize("compact", [False, True, 3], ids=["int64", "for32", "for24"])
 def test_two_hop_hub_overflow(gpu_session, monkeypatch, n, compact):
     """Hubs with in/out degree far above 2^16 in one P3 unit: the packed
     uint16 LDS counters hand off 2^15 per overflow (k_c3_overflow) and the
@@ -400,7 +425,7 @@ def test_two_hop_hub_overflow(gpu_session, monkeypatch, n, compact):
     assert got == cmodel.count_2hop(src.astype(np.int64), dst.astype(np.int64), n)
 
 
-@pytest.mark.parametrize("compact", [False, True], ids=["int64", "for32"])
+@pytest.mark.parametrize("compact", [False, True, 3], ids=["int64", "for32", "for24"])
 @pytest.mark.parametrize("scale,parts", [(10, 2), (16, 1), (16, 3), (18, 4), (18, 3)])
 def test_sharded_two_hop_partials(gpu_session, compact, scale, parts):
     """Node-partitioned layout (dist.py): every part's in/out copies hold
@@ -446,7 +471,7 @@ def _triangle_query():
                  [Stage([("count", CountStar())])])
 
 
-@pytest.mark.parametrize("compact", [False, True], ids=["int64", "for32"])
+@pytest.mark.parametrize("compact", [False, True, 3], ids=["int64", "for32", "for24"])
 @pytest.mark.parametrize("scale", [6, 8, 10, 12])
 def test_triangle_count_rmat(gpu_session, scale, compact):
     """MATCH (a)-->(b)-->(c)-->(a) RETURN count(*) through the planner (Expand,

@@ -39,7 +39,7 @@ TRIANGLE = Query([Match([NodeP("a"), NodeP("b"), NodeP("c")],
                  [Stage([("count", CountStar())])])
 
 
-@pytest.mark.parametrize("compact", [True, False], ids=["for32", "int64"])
+@pytest.mark.parametrize("compact", [3, True, False], ids=["for24", "for32", "int64"])
 @pytest.mark.parametrize("scale", [20, 22, 24])
 def test_two_hop_headline(gpu_session, scale, compact):
     """Config 3: MATCH (a)-->(b)-->(c) RETURN count(*) — s24 is the headline."""
@@ -53,7 +53,7 @@ def test_two_hop_headline_async_queue(gpu_session):
     """The pipelined bench mode (capf_table_count_async): 4 in-flight s24
     counts land the fixture in every slot."""
     import torch
-    g = rmat_graph(gpu_session, 24, compact=True)
+    g = rmat_graph(gpu_session, 24, compact=3)
     slots = torch.full((4,), -1, dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
     for i in range(4):

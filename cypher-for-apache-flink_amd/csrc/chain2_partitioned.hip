@@ -171,7 +171,7 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   const uint32_t pb = 8u * (uint32_t)(t & 7);
   const uint4 pad = make_uint4(pb | (pb + 1) << 16, (pb + 2) | (pb + 3) << 16,
                                (pb + 4) | (pb + 5) << 16, (pb + 6) | (pb + 7) << 16);
-  for (int i = threadIdx.x; i < STAGE / 8; i += C5_BLOCK) stage4[i] = pad;
+  (void)pad;  // pads are written per run after the scan (no stage prefill)
   for (int i = threadIdx.x; i <= nr; i += C5_BLOCK) cur[i] = 0;
   __syncthreads();
   const int64_t e0 = t * TILE;
@@ -268,7 +268,11 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   for (int q = 0; q < RUNS_PT; ++q) {
     const int r = RUNS_PT * threadIdx.x + q;
     if (r <= nr) cur[r] = ex;
-    if (r < nr) meta[t * nr + r] = (ex >> 3) | (cs[q] << 16);  // [tile][run], transposed later
+    if (r < nr) {
+      meta[t * nr + r] = (ex >> 3) | (cs[q] << 16);  // [tile][run], transposed later
+      // pad slots of the run's last piece: 8·(t mod 8) + slot (P3 subtracts them per bin)
+      for (uint32_t p = ex + cs[q]; p & 7u; ++p) stage[p] = (uint16_t)(pb + (p & 7u));
+    }
     ex += (cs[q] + 7) & ~7u;
   }
   __syncthreads();
@@ -355,13 +359,30 @@ constexpr int C3_UBLOCK = 1024;
 struct C3Sides {
   int nb;              // runs per side: runs [0, nb) in, [nb, 2·nb) out
   int64_t t0[2], t1[2];  // tile range holding each side's segments
+  int split_x16;       // a run is split when it holds > split_x16/16 × the mean
 };
+
+// CAPF_P3_SPLIT (tuning): split threshold in units of the mean run size
+static int c3_split_x16() {
+  const char *e = getenv("CAPF_P3_SPLIT");
+  return e ? std::max(1, (int)(16.0 * atof(e))) : 32;
+}
+
+// Units are also ordered largest-first (LPT: `order` lists unit indexes by
+// decreasing estimated keys, a 64-level counting sort): P3 workgroups are
+// dispatched in blockIdx order, so the heavy (hub) units start in the first
+// wave and the short ones fill the tail.
+constexpr int C3_MAXU = 4096;  // LDS capacity of the ordering pass
 
 __global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(const unsigned long long *run_total,
                                                          int nr, C3Sides sd, int S, C3Unit *units,
-                                                         int32_t *nunits, int32_t *split) {
+                                                         int32_t *nunits, int32_t *split,
+                                                         int32_t *order) {
   __shared__ unsigned long long lds64[17];
   __shared__ uint32_t lds32[17];
+  __shared__ uint32_t est[C3_MAXU];
+  __shared__ uint32_t qcnt[65];
+  __shared__ uint32_t maxest;
   unsigned long long cnt[2], tot = 0;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
@@ -371,7 +392,8 @@ __global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(const unsigned long long
   }
   unsigned long long total;
   block_exclusive_scan(tot, lds64, total);
-  const unsigned long long target = max(2 * total / (unsigned long long)max(nr, 1), 65536ull);
+  const unsigned long long target =
+      max((unsigned long long)sd.split_x16 * total / (16ull * (unsigned long long)max(nr, 1)), 65536ull);
   uint32_t nu[2], nsum = 0;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
@@ -399,11 +421,36 @@ __global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(const unsigned long long
       u.slice = (int32_t)(k % (uint32_t)S);
       u.pad = 0;
       units[off + k] = u;
+      if (off + k < (uint32_t)C3_MAXU) est[off + k] = (uint32_t)min<unsigned long long>(cnt[q] / nu[q], 0xFFFFFFFFull);
     }
     off += nu[q];
     split[r] = nu[q] > (uint32_t)S;
   }
   if (threadIdx.x == 0) *nunits = (int32_t)ntot;
+  if (!order) return;
+  if (threadIdx.x <= 64) qcnt[threadIdx.x] = 0;
+  if (threadIdx.x == 0) maxest = 0;
+  __syncthreads();
+  const uint32_t nu_all = min(ntot, (uint32_t)C3_MAXU);
+  for (uint32_t i = threadIdx.x; i < nu_all; i += C3_UBLOCK) atomicMax(&maxest, est[i]);
+  __syncthreads();
+  const unsigned long long mx = max(maxest, 1u);
+  // level 0 = largest
+  for (uint32_t i = threadIdx.x; i < nu_all; i += C3_UBLOCK)
+    atomicAdd(&qcnt[63 - (uint32_t)(63ull * est[i] / mx)], 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t a = 0;
+    for (int l = 0; l < 64; ++l) {
+      const uint32_t c = qcnt[l];
+      qcnt[l] = a;
+      a += c;
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nu_all; i += C3_UBLOCK)
+    order[atomicAdd(&qcnt[63 - (uint32_t)(63ull * est[i] / mx)], 1u)] = (int32_t)i;
+  for (uint32_t i = nu_all + threadIdx.x; i < ntot; i += C3_UBLOCK) order[i] = (int32_t)i;
 }
 
 // Clears every slice of the buckets of split runs (their units flush with
@@ -433,9 +480,10 @@ __device__ inline int c3_unit_of(int i) {
 // of the word, so a half never exceeds 2^15 + (sum of the adds in flight on
 // the CU: ≤ 1024 lanes × 8 for the merged hub adds) < 2^16: exact, no carry.
 struct C3Ovf {
-  uint2 *log;  // (histogram index, side)
+  uint2 *log;  // (histogram index, side | count << 1): hand-offs (count 2^15) and hot-key totals
   uint32_t *n;
   uint32_t cap;
+  unsigned long long *trace;  // diagnostics (CAPF_P3_TRACE): 4 words per unit, else null
 };
 
 // Slow path of an overflowing add (rare: a bin reached 2^15 within the unit).
@@ -443,7 +491,7 @@ __device__ inline void c3_handoff(uint32_t *w, uint32_t inc, uint32_t hidx, uint
                                         const C3Ovf &o) {
   atomicSub(w, inc << 15);
   const uint32_t k = atomicAdd(o.n, 1u);
-  if (k < o.cap) o.log[k] = make_uint2(hidx, side);
+  if (k < o.cap) o.log[k] = make_uint2(hidx, side | (1u << 16));
 }
 
 // P3 pieces per lane per step, double-buffered (s24: 2 → 0.49 ms; 4 spills → 0.66 ms)
@@ -486,16 +534,18 @@ __device__ inline int64_t uniform64(int64_t v) {
 // unit.  Voting out lane 0's key, half-wave atomics and non-returning atomics
 // were measured and do not help (the duplicates are spread over many
 // moderately hot keys).
-template <int PPS, int DIAG = 0>
+template <int PPS, int DIAG = 0, int DEPTH = 1, int HOT = 0>
 __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
                                                             const int32_t *nunits,
                                                             const uint16_t *part,
                                                             const uint32_t *meta_t, int64_t ntiles,
                                                             int nb, int64_t rstride, uint32_t *h_in,
                                                             uint32_t *h_out, int64_t slice_stride,
-                                                            C3Ovf ovf) {
-  const int ui = c3_unit_of((int)blockIdx.x);
+                                                            C3Ovf ovf, const int32_t *order) {
+  if ((int)blockIdx.x >= *nunits && order) return;
+  const int ui = order ? order[blockIdx.x] : c3_unit_of((int)blockIdx.x);
   if (ui >= *nunits) return;
+  const unsigned long long t_start = ovf.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
   extern __shared__ __attribute__((aligned(16))) uint32_t words[];
   constexpr int NW = C5_BLOCK / WAVE;
   constexpr uint32_t STEP = WAVE * PPS;
@@ -517,6 +567,13 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
   const uint32_t rs8 = (uint32_t)(rstride / 8);
   uint32_t padc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint32_t dead = 0;
+  // HOT: the wave's hot key H (wave-uniform; none = 0xFFFFFFFF).  Once a live
+  // piece shows its first key ≥ 3 times, that key (≥ C5_CORR: never a pad or
+  // dead-lane key) is H; its later copies are counted in a register (nh) and
+  // sit every atomic out, and the wave's total goes through the hand-off log
+  // (k_c3_overflow) — a run's top hub (14 % of run 0's keys at s24) otherwise
+  // puts ~9 lanes of every ds_add on one word.
+  uint32_t H = 0xFFFFFFFFu, nh = 0;
   const uint4 dead_keys = make_uint4(lane | lane << 16, lane | lane << 16, lane | lane << 16,
                                      lane | lane << 16);
   // batch setup: table of tiles [tb, tb + 64) into tab2[buf]; returns the piece total
@@ -563,6 +620,8 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
     uint32_t old[PPS][8];
     uint32_t n0[PPS], n1[PPS];
     bool dup[PPS][8];
+    bool live0 = false;
+    uint32_t k00 = 0;
 #pragma unroll
     for (int j = 0; j < PPS; ++j) {
       const bool live = p0 + j * WAVE + lane < total;
@@ -576,6 +635,10 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
         // serialise); the other slots add 1 each, lanes holding a duplicate
         // sit that atomic out
         const uint32_t k0 = wd[0] & 0xFFFF, k1 = wd[0] >> 16;
+        if (j == 0) {
+          live0 = live;
+          k00 = k0;
+        }
         dup[j][0] = false;
         dup[j][1] = k1 == k0;
         n0[j] = dup[j][1] ? 2u : 1u;
@@ -584,9 +647,11 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
         for (int e = 2; e < 8; ++e) {
           const uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
           const bool d0 = key == k0, d1 = !d0 && key == k1;  // k1 == k0 ⇒ d0 already
-          dup[j][e] = d0 || d1;
+          const bool d2 = HOT && !d0 && !d1 && key == H;     // H ≥ C5_CORR: never dead/pad
+          dup[j][e] = d0 || d1 || d2;
           n0[j] += d0 ? 1u : 0u;
           n1[j] += d1 ? 1u : 0u;
+          if (HOT) nh += d2 ? 1u : 0u;
         }
         const uint32_t inc0 = n0[j] << ((k0 >> 15) << 4);
         old[j][0] = atomicAdd(&words[k0 & (C2_WORDS - 1)], inc0);
@@ -613,6 +678,10 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
         old[j][e] = atomicAdd(&words[key & (C2_WORDS - 1)], unit);
         acc |= old[j][e] + unit;
       }
+    }
+    if (HOT && DIAG == 0 && H == 0xFFFFFFFFu) {
+      const unsigned long long bm = __ballot(live0 && n0[0] >= 3u && k00 >= (uint32_t)C5_CORR);
+      if (bm) H = (uint32_t)__builtin_amdgcn_readlane((int)k00, __builtin_ctzll(bm));
     }
     if (DIAG == 0 && (acc & 0x80008000u)) {
       // rare: some half reached 2^15 — find the add(s) that crossed it (the
@@ -662,26 +731,72 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
         } while (total == 0);
         return true;
       };
-      // ping-pong piece buffers (unrolled by 2: no register copies, so the
-      // wait before counting A covers A's loads only, not B's)
-      uint4 va[PPS], vb[PPS];
-      fetch(buf, p0, total, va);
-      for (;;) {
-        uint32_t cp0 = p0, ctot = total;
-        if (!advance()) {
-          count(va, cp0, ctot);
-          break;
-        }
-        fetch(buf, p0, total, vb);
-        count(va, cp0, ctot);
-        cp0 = p0;
-        ctot = total;
-        if (!advance()) {
-          count(vb, cp0, ctot);
-          break;
-        }
+      if (DEPTH == 1) {
+        // ping-pong piece buffers (unrolled by 2: no register copies, so the
+        // wait before counting A covers A's loads only, not B's)
+        uint4 va[PPS], vb[PPS];
         fetch(buf, p0, total, va);
-        count(vb, cp0, ctot);
+        for (;;) {
+          uint32_t cp0 = p0, ctot = total;
+          if (!advance()) {
+            count(va, cp0, ctot);
+            break;
+          }
+          fetch(buf, p0, total, vb);
+          count(va, cp0, ctot);
+          cp0 = p0;
+          ctot = total;
+          if (!advance()) {
+            count(vb, cp0, ctot);
+            break;
+          }
+          fetch(buf, p0, total, va);
+          count(vb, cp0, ctot);
+        }
+      } else {
+        // three rotating piece buffers: the loads of steps i+1 and i+2 are in
+        // flight while step i counts (unrolled by 3, no register copies)
+        uint4 va[PPS], vb[PPS], vc[PPS];
+        uint32_t pa, ta, pb, tb2, pc, tc;
+        pa = p0;
+        ta = total;
+        fetch(buf, p0, total, va);
+        if (!advance()) {
+          count(va, pa, ta);
+        } else {
+          pb = p0;
+          tb2 = total;
+          fetch(buf, p0, total, vb);
+          for (;;) {
+            if (!advance()) {
+              count(va, pa, ta);
+              count(vb, pb, tb2);
+              break;
+            }
+            pc = p0;
+            tc = total;
+            fetch(buf, p0, total, vc);
+            count(va, pa, ta);
+            if (!advance()) {
+              count(vb, pb, tb2);
+              count(vc, pc, tc);
+              break;
+            }
+            pa = p0;
+            ta = total;
+            fetch(buf, p0, total, va);
+            count(vb, pb, tb2);
+            if (!advance()) {
+              count(vc, pc, tc);
+              count(va, pa, ta);
+              break;
+            }
+            pb = p0;
+            tb2 = total;
+            fetch(buf, p0, total, vb);
+            count(vc, pc, tc);
+          }
+        }
       }
     }
   }
@@ -690,6 +805,13 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
   for (int e = 1; e < 8; ++e)
     if (padc[e]) atomicAdd(&corr[pcls + e], padc[e]);
   if (dead) atomicAdd(&corr[lane], 8 * dead);
+  if (HOT && H != 0xFFFFFFFFu) {
+    const unsigned long long th = wave_reduce_sum((unsigned long long)nh);
+    if (lane == 0 && th) {
+      const uint32_t k = atomicAdd(ovf.n, 1u);
+      if (k < ovf.cap) ovf.log[k] = make_uint2(hist_base + H, side | ((uint32_t)th << 1));
+    }
+  }
   __syncthreads();
   for (int i = threadIdx.x; i < C2_WORDS; i += C5_BLOCK) {
     const uint32_t w = words[i];
@@ -703,6 +825,17 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
       if (hi) atomicAdd(h + C2_WORDS, hi);
     }
   }
+  if (ovf.trace) {  // diagnostics: this unit's span, where it ran
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (3 << 11));           // HW_REG_XCC_ID[3:0]
+      const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));  // HW_REG_HW_ID
+      ovf.trace[4 * ui] = t_start;
+      ovf.trace[4 * ui + 1] = __builtin_amdgcn_s_memrealtime();
+      ovf.trace[4 * ui + 2] = ((unsigned long long)xcc << 32) | hw;
+      ovf.trace[4 * ui + 3] = ((unsigned long long)u.run << 32) | (uint32_t)(u.t1 - u.t0);
+    }
+  }
 }
 
 // Adds the handed-off 2^15 units (after every P3 store has landed).
@@ -710,7 +843,7 @@ __global__ __launch_bounds__(256) void k_c3_overflow(C3Ovf o, uint32_t *h_in, ui
   const uint32_t n = min(*o.n, o.cap);
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     const uint2 e = o.log[i];
-    atomicAdd(&(e.y ? h_out : h_in)[e.x], 1u << 15);
+    atomicAdd(&((e.y & 1u) ? h_out : h_in)[e.x], e.y >> 1);
   }
 }
 
@@ -746,14 +879,16 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   static bool attr_set = false;
   if (!attr_set) {
     for (const void *f : {(const void *)k_c5_gather<C5_PPS, 0>, (const void *)k_c5_gather<C5_PPS, 2>,
-                          (const void *)k_c5_gather<C5_PPS, 3>})
+                          (const void *)k_c5_gather<C5_PPS, 3>, (const void *)k_c5_gather<C5_PPS, 0, 2>,
+                          (const void *)k_c5_gather<C5_PPS, 0, 1, 1>, (const void *)k_c5_gather<C5_PPS, 0, 2, 1>})
       HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, C5_GATHER_LDS));
     attr_set = true;
   }
   // runs × slices + hub splits (≤ 2 per run beyond the slices), whole XCD waves
-  const int max_units = ((S + 2) * nr + 1 + 255) / 256 * 256;
+  // Σ_runs max(S, ⌈cnt/target⌉) ≤ S·nr + nr + total/target, target ≥ split/16 × mean
+  const int max_units = (S * nr + nr + 16 * nr / std::max(1, sd.split_x16) + 2 + 255) / 256 * 256;
   // every overflow event consumes 2^15 adds of one half-counter within one unit
-  const uint32_t ovf_cap = (uint32_t)(nkeys / (1 << 15) + 64);
+  const uint32_t ovf_cap = (uint32_t)(nkeys / (1 << 15) + 64 + 16 * (int64_t)max_units);
   BufPtr meta_t = s->alloc(4 * nr * ntiles);
   // transpose blocks: tiles per block tt, fewer when there are few runs (≥ ~1024 blocks)
   int64_t tt = C3_TT;
@@ -764,10 +899,23 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   int32_t *nunits = (int32_t *)(run_total + nr);  // [0] units, [1] overflow events
   int32_t *split = nunits + 4;
   C3Unit *units = (C3Unit *)(split + nr);
+  // CAPF_P3_LPT=1: largest-first unit order instead of the XCD-grouped run order
+  const char *lpt_env = getenv("CAPF_P3_LPT");
+  const bool lpt = lpt_env && atoi(lpt_env) == 1;
+  BufPtr order_buf = lpt ? s->alloc(4 * (int64_t)max_units) : BufPtr();
+  int32_t *order = lpt ? (int32_t *)order_buf->p : nullptr;
   C3Ovf ovf;
   ovf.n = (uint32_t *)(nunits + 1);
   ovf.log = (uint2 *)(units + max_units);
   ovf.cap = ovf_cap;
+  ovf.trace = nullptr;
+  const char *trace_path = getenv("CAPF_P3_TRACE");  // diagnostics only
+  BufPtr trace;
+  if (trace_path) {
+    trace = s->alloc(32 * (int64_t)max_units);
+    HIP_CHECK(hipMemsetAsync(trace->p, 0, 32 * (size_t)max_units, s->stream));
+    ovf.trace = (unsigned long long *)trace->p;
+  }
   HIP_CHECK(hipMemsetAsync(acc->p, 0, 8 * nr + 16, s->stream));
   {
     KernelTimer kt(s, "c3_transpose", 8.0 * nr * ntiles);
@@ -779,7 +927,7 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   {
     KernelTimer kt(s, "c3_units", 8.0 * nr);
     hipLaunchKernelGGL(k_c3_units, dim3(1), dim3(C3_UBLOCK), 0, s->stream,
-                       (const unsigned long long *)run_total, nr, sd, S, units, nunits, split);
+                       (const unsigned long long *)run_total, nr, sd, S, units, nunits, split, order);
     KERNEL_CHECK();
     hipLaunchKernelGGL(k_c3_zero, dim3(4, nr, S), dim3(256), 0, s->stream, (const int32_t *)split,
                        sd.nb, h_in, h_out, slice_stride);
@@ -790,19 +938,36 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
     // CAPF_P3_DIAG=2 (diagnostics, wrong counts): keys spread so no two lanes
     // of an atomic share a word — measures the cost of hub-key conflicts
     const char *dg = getenv("CAPF_P3_DIAG");
-    auto kern = dg && atoi(dg) == 2   ? k_c5_gather<C5_PPS, 2>
+    const char *dp = getenv("CAPF_P3_DEPTH");
+    const char *hot = getenv("CAPF_P3_HOT");
+    // depth 2 (loads of steps i+1, i+2 in flight while step i counts) is the
+    // default: 0.437 vs 0.445 ms at s24; CAPF_P3_DEPTH=1 selects depth 1
+    const bool d2 = !(dp && atoi(dp) == 1), h1 = hot && atoi(hot) == 1;
+    auto kern = dg && atoi(dg) == 2 ? k_c5_gather<C5_PPS, 2>
                 : dg && atoi(dg) == 3 ? k_c5_gather<C5_PPS, 3>
+                : d2 && h1            ? k_c5_gather<C5_PPS, 0, 2, 1>
+                : h1                  ? k_c5_gather<C5_PPS, 0, 1, 1>
+                : d2                  ? k_c5_gather<C5_PPS, 0, 2>
                                       : k_c5_gather<C5_PPS, 0>;
     hipLaunchKernelGGL(kern, dim3((unsigned)max_units), dim3(C5_BLOCK), C5_GATHER_LDS, s->stream,
                        (const C3Unit *)units, (const int32_t *)nunits, part,
                        (const uint32_t *)meta_t->p, ntiles, sd.nb, rstride, h_in, h_out,
-                       slice_stride, ovf);
+                       slice_stride, ovf, (const int32_t *)order);
     KERNEL_CHECK();
   }
   {
     KernelTimer kt(s, "c3_overflow", 0.0);
     hipLaunchKernelGGL(k_c3_overflow, dim3(16), dim3(256), 0, s->stream, ovf, h_in, h_out);
     KERNEL_CHECK();
+  }
+  if (trace_path) {  // diagnostics: append (start, end, where, run|tiles) per unit
+    std::vector<unsigned long long> h(4 * (size_t)max_units);
+    s->sync();
+    HIP_CHECK(hipMemcpy(h.data(), trace->p, 32 * (size_t)max_units, hipMemcpyDeviceToHost));
+    if (FILE *f = fopen(trace_path, "ab")) {
+      fwrite(h.data(), 8, h.size(), f);
+      fclose(f);
+    }
   }
 }
 
@@ -866,6 +1031,7 @@ static void chain2_c5(Session *s, C5Cols<W> c, bool in_range, uint32_t *h_in, ui
     if (!alias && in_range) launch_c5<W, false, false, SH>(s, c, pp, mp, d_loops);
   }
   C3Sides sd;
+  sd.split_x16 = c3_split_x16();
   sd.nb = c.nb;
   sd.t0[0] = sd.t0[1] = 0;
   sd.t1[0] = sd.t1[1] = c.ntiles;
@@ -1140,6 +1306,7 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
         KERNEL_CHECK();
       }
       C3Sides sd;
+      sd.split_x16 = c3_split_x16();
       sd.nb = nbl;
       sd.t0[0] = 0;
       sd.t1[0] = c.t_in;

@@ -14,7 +14,8 @@ from capf_amd.table import GpuSession  # noqa: E402
 
 scale = int(sys.argv[1])
 s = GpuSession(0)
-g = rmat_graph(s, scale, compact=os.environ.get("CAPF_INT64") is None)
+_w = os.environ.get("CAPF_WIDTH", "3")  # id storage: 3 = FOR24, 4 = FOR32, 8 = int64
+g = rmat_graph(s, scale, compact={"3": 3, "4": True, "8": False}[_w])
 q = two_hop_query()
 base = dict(os.environ)
 for spec in sys.argv[2:]:

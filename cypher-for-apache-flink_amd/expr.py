@@ -222,6 +222,28 @@ class Coalesce(Expr):
         return "coalesce(" + ", ".join(map(str, self.exprs)) + ")"
 
 
+class ExistsPattern(Expr):
+    """EXISTS((a)-->()-->(b)) — a pattern predicate (okapi ExistsPatternExpr,
+    okapi-ir/.../api/expr/Expr.scala).  `pattern` is a planner Match over
+    variables of the enclosing clause; the relational planner turns it into
+    an ExistsSubQuery (RelationalPlanner.scala:224-247) whose boolean target
+    column then stands for this expression in the header (the Flink mapper
+    lowers ExistsPatternExpr to its target field, FlinkSQLExprMapper.scala:226).
+    Identity-hashed: two EXISTS with the same text are two sub-queries."""
+
+    def __init__(self, pattern):
+        self.pattern = pattern
+
+    def __str__(self):
+        return f"exists#{id(self) & 0xFFFFFF:06x}"
+
+    def __hash__(self):
+        return id(self)
+
+    def __eq__(self, other):
+        return self is other
+
+
 # ----------------------------------------------------------------- aggregators
 class Aggregator(Expr):
     kind = -1

@@ -22,8 +22,8 @@ from dataclasses import dataclass, field
 from itertools import combinations
 from typing import List, Optional, Sequence, Tuple
 
-from .expr import (Aggregator, Ands, BoolLit, CountStar, ElementProperty, EndNode, Equals, Expr, HasLabel,
-                   HasType, IntegerLit, Not, NullLit, StartNode, TrueLit, Var)
+from .expr import (Aggregator, Ands, BoolLit, CountStar, ElementProperty, EndNode, Equals, ExistsPattern, Expr,
+                   HasLabel, HasType, IntegerLit, IsNotNull, Not, NullLit, StartNode, TrueLit, Var)
 from .header import RecordHeader, owner_of
 
 
@@ -374,8 +374,72 @@ def plan_match(graph, m: Match, prev: Optional[Planned], params=None) -> Planned
     fixed = [Var(r.name, "RELATIONSHIP") for r in rels if r.length is None]
     preds = list(m.where) + extra_where + [Not(Equals(a, b)) for a, b in combinations(fixed, 2)]
     for p in preds:
+        op = plan_subqueries(graph, op, p, params)
         op = filter_(op, p, params)
     return op
+
+
+def _exists_in(e):
+    """ExistsPattern sub-expressions of e, innermost first (planInnerSubquery,
+    LogicalPlanner.scala:230-243)."""
+    out = []
+
+    def go(x):
+        if isinstance(x, ExistsPattern):
+            out.append(x)
+            return
+        for name in ("lhs", "rhs", "expr"):
+            c = getattr(x, name, None)
+            if isinstance(c, Expr):
+                go(c)
+        for c in getattr(x, "exprs", ()) or ():
+            if isinstance(c, Expr):
+                go(c)
+    go(e)
+    return out
+
+
+def plan_subqueries(graph, op: Planned, expr: Expr, params=None) -> Planned:
+    """Plans every EXISTS pattern inside `expr` that the header does not hold yet."""
+    for ex in _exists_in(expr):
+        if ex not in op.header:
+            op = plan_exists(graph, ex, op, params)
+    return op
+
+
+def plan_exists(graph, ex: ExistsPattern, lhs: Planned, params=None) -> Planned:
+    """ExistsSubQuery (RelationalPlanner.scala:224-247): the pattern is planned
+    on its own (rhs, with its own scans of the shared variables), then
+      1. the variables common to both headers are the join expressions,
+      2. the rhs join-var columns are aliased to fresh names, every other rhs
+         expression is dropped,
+      3. DISTINCT rows of the aliases,
+      4. lhs LEFT OUTER JOIN rhs on (lhs var = alias),
+      5. IsNotNull(first alias) is added as the predicate's target column.
+    (The reference's rhs keeps its other columns through the Distinct and the
+    join; only IsNotNull(alias) is read from them, so they are not carried.)"""
+    rhs = plan_match(graph, ex.pattern, None, params)
+    lvars = {v.vname: v for v in lhs.header.vars()}
+    join_vars = [v for v in rhs.header.vars() if v.vname in lvars]
+    if not join_vars:
+        from ._lib import NotImplementedException
+        raise NotImplementedException("EXISTS pattern sharing no variable with the enclosing clause")
+    taken = set(lhs.table.physicalColumns) | set(rhs.table.physicalColumns)
+    fresh = []
+    for i in range(len(join_vars) + 1):
+        c = f"__exists_{len(lhs.header.expressions)}_{i}"
+        while c in taken:
+            c += "_"
+        taken.add(c)
+        fresh.append(c)
+    target, aliases = fresh[0], fresh[1:]
+    rtab = rhs.table.select(*[(rhs.header.column(v), a) for v, a in zip(join_vars, aliases)]).distinct()
+    pairs = [(lhs.header.column(lvars[v.vname]), a) for v, a in zip(join_vars, aliases)]
+    joined = lhs.table.join(rtab, "left_outer", *pairs)
+    joined = joined.withColumns((IsNotNull(Var(aliases[0])), target),
+                                header=RecordHeader({Var(aliases[0]): aliases[0]}), params=params or {})
+    joined = joined.drop(*aliases)
+    return Planned(joined, lhs.header.with_expr(ex, target))
 
 
 def plan_optional(graph, m: Match, lhs: Planned, params=None) -> Planned:
@@ -453,17 +517,27 @@ def plan_optional(graph, m: Match, lhs: Planned, params=None) -> Planned:
     return Planned(joined, head)
 
 
-def plan_stage(op: Planned, st: Stage, params=None) -> Planned:
+def plan_stage(op: Planned, st: Stage, params=None, graph=None) -> Planned:
     aggs = [(a, e) for a, e in st.items if isinstance(e, Aggregator)]
     projs = [(a, e) for a, e in st.items if not isinstance(e, Aggregator)]
+    for _, e in projs:
+        op = plan_subqueries(graph, op, e, params)
     # project non-aggregate items into alias vars (RelationalPlanner Add → withColumns)
     h = op.header
     adds, new_h = [], {}
     for alias, e in projs:
-        v = Var(alias)
+        owned = [x for x in h.owned_by(e) if x != e] if isinstance(e, Var) and e in h else []
+        v = Var(alias, e.ctype if isinstance(e, Var) else "ANY")
         col = "__" + alias
         adds.append((e, col))
         new_h[v] = col
+        # a node / relationship var keeps its labels, type, endpoints and
+        # properties under the alias (RETURN n returns the whole element)
+        for x in owned:
+            nx = _rewrite_owner(x, e, v)
+            c = "__" + alias + "." + h.column(x)
+            adds.append((x, c))
+            new_h[nx] = c
     # aggregation arguments are evaluated against the incoming header
     if adds:
         tab = op.table.withColumns(*adds, header=h, params=params or {})
@@ -475,23 +549,44 @@ def plan_stage(op: Planned, st: Stage, params=None) -> Planned:
         group_vars = [Var(a) for a, _ in projs]
         agg_cols = {"__" + a: e for a, e in aggs}
         tab = op.table.group(group_vars, agg_cols, header=op.header, params=params or {})
-        hh = {Var(a): "__" + a for a, _ in st.items}
+        hh = dict(new_h)
+        hh.update({Var(a): "__" + a for a, _ in aggs})
         op = Planned(tab, RecordHeader(hh))
     else:
-        cols = ["__" + a for a, _ in projs]
-        op = Planned(op.table.select(*cols), RecordHeader({Var(a): "__" + a for a, _ in projs}))
+        cols = list(dict.fromkeys(new_h.values()))
+        op = Planned(op.table.select(*cols), RecordHeader(new_h))
     if st.distinct:
         op = Planned(op.table.distinct(), op.header)
     for p in st.where:
+        op = plan_subqueries(graph, op, p, params)
         op = filter_(op, p, params)
     if st.order_by:
         items = [(Var(a), o) for a, o in st.order_by]
         op = Planned(op.table.orderBy(*items, header=op.header, params=params or {}), op.header)
     if st.skip is not None:
-        op = Planned(op.table.skip(st.skip), op.header)
+        op = Planned(op.table.skip(_row_count(st.skip, params, "SKIP")), op.header)
     if st.limit is not None:
-        op = Planned(op.table.limit(st.limit), op.header)
+        op = Planned(op.table.limit(_row_count(st.limit, params, "LIMIT")), op.header)
     return op
+
+
+def _row_count(e, params, what):
+    """Skip / Limit argument: an integer literal or a parameter holding an
+    integer (RelationalOperator.scala:362-398); anything else is illegal."""
+    from .expr import IntegerLit, Param
+    from ._lib import IllegalArgumentException
+    if isinstance(e, bool):
+        raise IllegalArgumentException(f"{what}: an integer literal or parameter, got {e!r}")
+    if isinstance(e, int):
+        return e
+    if isinstance(e, IntegerLit):
+        return e.v
+    if isinstance(e, Param):
+        v = (params or {}).get(e.pname)
+        if isinstance(v, int) and not isinstance(v, bool):
+            return v
+        raise IllegalArgumentException(f"{what}: parameter ${e.pname} must be a CypherInteger, got {v!r}")
+    raise IllegalArgumentException(f"{what}: an integer literal or parameter, got {e}")
 
 
 def _fused_reach(graph, q: Query):
@@ -554,22 +649,89 @@ def plan_query(graph, q: Query, params=None) -> Planned:
     if fused is not None:
         op, rest = fused
         for st in rest:
-            op = plan_stage(op, st, params)
+            op = plan_stage(op, st, params, graph)
         return op
     op = None
     for m in q.matches:
         op = plan_optional(graph, m, op, params) if m.optional else plan_match(graph, m, op, params)
     for st in q.stages:
-        op = plan_stage(op, st, params)
+        op = plan_stage(op, st, params, graph)
     return op
 
 
+@dataclass(frozen=True)
+class CypherNode:
+    """A returned node (CAPFNode: id, labels, non-null properties)."""
+    id: int
+    labels: frozenset
+    properties: tuple  # sorted (key, value) pairs
+
+    def props(self):
+        return dict(self.properties)
+
+
+@dataclass(frozen=True)
+class CypherRelationship:
+    """A returned relationship (CAPFRelationship: id, source, target, type,
+    non-null properties)."""
+    id: int
+    source: int
+    target: int
+    rel_type: str
+    properties: tuple
+
+    def props(self):
+        return dict(self.properties)
+
+
+def _element_values(op: Planned, v: Var, data):
+    """rowToCypherMap.collectNode / collectRel (flink-cypher/.../impl/convert/
+    rowToCypherMap.scala:77-123) over downloaded columns: a NULL id is a NULL
+    element; labels are the true label flags, properties the non-null ones.
+    The relationship's target is read from the END node column (the Flink
+    code reads startNodeFor twice, :98-99 — a reference bug, not reproduced)."""
+    h = op.header
+    ids = data(h.column(v))
+    owned = h.owned_by(v)
+    labels = [(x.label, data(h.column(x))) for x in owned if isinstance(x, HasLabel)]
+    types = [(x.rel_type, data(h.column(x))) for x in owned if isinstance(x, HasType)]
+    props = [(x.key, data(h.column(x))) for x in owned if isinstance(x, ElementProperty)]
+    is_rel = v.ctype == "RELATIONSHIP" or StartNode(v) in h
+    src = data(h.column(StartNode(v))) if is_rel else None
+    dst = data(h.column(EndNode(v))) if is_rel else None
+    out = []
+    for i, ident in enumerate(ids):
+        if ident is None:
+            out.append(None)
+            continue
+        pr = tuple(sorted((k, vals[i]) for k, vals in props if vals[i] is not None))
+        if is_rel:
+            ty = [t for t, flags in types if flags[i]]
+            out.append(CypherRelationship(ident, src[i], dst[i], ty[0] if ty else None, pr))
+        else:
+            out.append(CypherNode(ident, frozenset(l for l, flags in labels if flags[i]), pr))
+    return out
+
+
 def records(op: Planned, aliases: Sequence[str]):
-    """RelationalCypherResult.records.toMaps: list of {alias: value}."""
-    cols = {a: op.header.column(Var(a)) for a in aliases}
-    data = {a: op.table.column_values(c) for a, c in cols.items()}
-    n = len(next(iter(data.values()))) if data else op.table.size
-    return [{a: data[a][i] for a in aliases} for i in range(n)]
+    """RelationalCypherResult.records.toMaps: list of {alias: value}; node and
+    relationship variables come back as CypherNode / CypherRelationship."""
+    cache = {}
+
+    def data(c):
+        if c not in cache:
+            cache[c] = op.table.column_values(c)
+        return cache[c]
+
+    out_cols = {}
+    for a in aliases:
+        v = next((e for e in op.header.vars() if e.vname == a), Var(a))
+        if v.ctype in ("NODE", "RELATIONSHIP") and len(op.header.owned_by(v)) >= 1:
+            out_cols[a] = _element_values(op, v, data)
+        else:
+            out_cols[a] = data(op.header.column(v))
+    n = len(next(iter(out_cols.values()))) if out_cols else op.table.size
+    return [{a: out_cols[a][i] for a in aliases} for i in range(n)]
 
 
 def run(graph, q: Query, params=None):

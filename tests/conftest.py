@@ -51,6 +51,13 @@ def cypher_value_key(v):
         return ("map", tuple(sorted((k, cypher_value_key(x)) for k, x in v.items())))
     if isinstance(v, (frozenset, set)):
         return ("set", tuple(sorted(v)))
+    from capf_amd.planner import CypherNode, CypherRelationship
+    if isinstance(v, CypherNode):
+        return ("node", v.id, tuple(sorted(v.labels)),
+                tuple((k, cypher_value_key(x)) for k, x in sorted(v.properties)))
+    if isinstance(v, CypherRelationship):
+        return ("relationship", v.id, v.source, v.target, v.rel_type,
+                tuple((k, cypher_value_key(x)) for k, x in sorted(v.properties)))
     try:
         import numpy as np
         if isinstance(v, np.integer):
@@ -60,6 +67,21 @@ def cypher_value_key(v):
     except ImportError:
         pass
     raise TypeError(f"no Cypher value kind for {type(v).__name__}: {v!r}")
+
+
+def check_case(got, expected, opts):
+    """A reference case's assertion: Bag equality (OT/Bag.scala), or the
+    ordered row list ({"ordered": True}), or only the row count."""
+    if "row_count" in opts:
+        return len(got) == opts["row_count"]
+    if opts.get("ordered"):
+        return [bag([r]) for r in got] == [bag([r]) for r in expected]
+    return bag(got) == bag(expected)
+
+
+def case_parts(case):
+    cid, src, create, query, expected = case[:5]
+    return cid, src, create, query, expected, (case[5] if len(case) > 5 else {})
 
 
 def bag(rows):

@@ -52,14 +52,28 @@ def ldbc_sample():
             "persons": persons, "knows": knows}
 
 
+def _json_value(v):
+    """JSON form of the element values (CypherNode / CypherRelationship)."""
+    from capf_amd.planner import CypherNode, CypherRelationship
+    if isinstance(v, CypherNode):
+        return {"node": v.id, "labels": sorted(v.labels), "properties": dict(v.properties)}
+    if isinstance(v, CypherRelationship):
+        return {"relationship": v.id, "source": v.source, "target": v.target, "type": v.rel_type,
+                "properties": dict(v.properties)}
+    raise TypeError(type(v).__name__)
+
+
 def main():
     from reference_cases import CASES
     out = []
-    for cid, src, create, query, expected in CASES:
-        got = run(ScanGraph.from_data(OracleSession(), parse_create(create)), query)
-        out.append({"id": cid, "source": src, "create": create.strip(), "expected": expected, "oracle": got})
+    for case in CASES:
+        cid, src, create, query, expected = case[:5]
+        opts = case[5] if len(case) > 5 else {}
+        got = run(ScanGraph.from_data(OracleSession(), parse_create(create)), query, opts.get("params"))
+        out.append({"id": cid, "source": src, "create": create.strip(), "expected": expected, "oracle": got,
+                    "options": opts})
     with open(os.path.join(HERE, "reference_cases.json"), "w") as f:
-        json.dump(out, f, indent=1, sort_keys=True)
+        json.dump(out, f, indent=1, sort_keys=True, default=_json_value)
 
     if os.path.isdir(LDBC):
         with open(os.path.join(HERE, "ldbc_sample.json"), "w") as f:

@@ -351,3 +351,174 @@ OPTIONAL_CASES += [
      [{"a": None, "b.name": "Alice"}, {"a": None, "b.name": "Bob"}]),
 ]
 CASES = CASES + OPTIONAL_CASES
+
+
+# ------------------------------------------------------------ ReturnTests (MTa)
+# Element results (rowToCypherMap) and the RETURN tail
+# (ORDER BY / SKIP / LIMIT / DISTINCT, §8(f) rank 4).  A 6th tuple element
+# holds options: {"ordered": True} compares the row LIST (ORDER BY cases —
+# the reference compares Bags, the order is what those tests are about),
+# {"row_count": k} checks only the number of rows (the reference counts the
+# rows of the underlying table).  Node / relationship values are
+# CypherNode / CypherRelationship (planner.py); ids are CreateQueryParser's.
+from capf_amd.expr import (Add, Ands, BoolLit, Equals, ExistsPattern, GreaterThan, IntegerLit,  # noqa: E402
+                           Not, Ors, Param, StringLit)
+from capf_amd.planner import CypherNode, CypherRelationship  # noqa: E402
+
+
+def R(v):
+    from capf_amd.expr import Var
+    return Var(v, "RELATIONSHIP")
+
+
+def node(i, labels=(), **props):
+    return CypherNode(i, frozenset(labels), tuple(sorted(props.items())))
+
+
+def rel(i, s, t, typ, **props):
+    return CypherRelationship(i, s, t, typ, tuple(sorted(props.items())))
+
+
+VALS3 = """CREATE (:Node {val: 4}), (:Node {val: 3}), (:Node  {val: 42})"""
+
+
+def _val_query(**kw):
+    return Query([Match([NodeP("a")])], [ret(("val", P("a", "val")), **kw)])
+
+
+RETURN_CASES = [
+    ("return_full_node", "MTa/ReturnTests.scala:103-112", "CREATE ({foo:'bar'}),()",
+     scan_n(ret(("n", N("n")))),
+     [{"n": node(0, foo="bar")}, {"n": node(1)}]),
+    ("return_full_rel", "MTa/ReturnTests.scala:114-124", "CREATE ()-[:Rel {foo:'bar'}]->()-[:Rel]->()",
+     Query([Match([NodeP("_a0"), NodeP("_a1")], [RelP("r", "_a0", "_a1")])], [ret(("r", R("r")))]),
+     [{"r": rel(2, 0, 1, "Rel", foo="bar")}, {"r": rel(4, 1, 3, "Rel")}]),
+    ("return_rel_property_untyped", "MTa/ReturnTests.scala:126-136", "CREATE ()-[:Rel {foo:'bar'}]->()-[:Rel]->()",
+     Query([Match([NodeP("_a0"), NodeP("_a1")], [RelP("r", "_a0", "_a1")])],
+           [ret(("r.foo", ElementProperty(R("r"), "foo", "STRING")))]),
+     [{"r.foo": "bar"}, {"r.foo": None}]),
+    ("return_multiple_references", "MTa/ReturnTests.scala:138-153", "CREATE ({val: 0})",
+     Query([Match([NodeP("a")])],
+           [ret(("a", N("a")), ("foo", P("a", "val"))), ret(("a", N("a")), ("bar", Var("foo"))),
+            ret(("a.val", P("a", "val")))]),
+     [{"a.val": 0}]),
+    ("return_distinct_property", "MTa/ReturnTests.scala:157-174",
+     """CREATE ({name:'bar'}) CREATE ({name:'bar'}) CREATE ({name:'baz'}) CREATE ({name:'baz'})
+        CREATE ({name:'bar'}) CREATE ({name:'foo'})""",
+     scan_n(ret(("name", P("n", "name")), distinct=True)),
+     [{"name": "bar"}, {"name": "foo"}, {"name": "baz"}]),
+    ("return_distinct_combinations", "MTa/ReturnTests.scala:176-193",
+     """CREATE ({p1:'a', p2: 'a', p3: '1'}) CREATE ({p1:'a', p2: 'a', p3: '2'})
+        CREATE ({p1:'a', p2: 'b', p3: '3'}) CREATE ({p1:'b', p2: 'a', p3: '4'})
+        CREATE ({p1:'b', p2: 'b', p3: '5'})""",
+     scan_n(ret(("p1", P("n", "p1")), ("p2", P("n", "p2")), distinct=True)),
+     [{"p2": "a", "p1": "a"}, {"p2": "a", "p1": "b"}, {"p2": "b", "p1": "a"}, {"p2": "b", "p1": "b"}]),
+    ("order_by_default", "MTa/ReturnTests.scala:196-207", VALS3,
+     _val_query(order_by=[("val", "asc")]), [{"val": 3}, {"val": 4}, {"val": 42}], {"ordered": True}),
+    ("order_by_asc", "MTa/ReturnTests.scala:209-220", VALS3,
+     _val_query(order_by=[("val", "asc")]), [{"val": 3}, {"val": 4}, {"val": 42}], {"ordered": True}),
+    ("order_by_desc", "MTa/ReturnTests.scala:222-233", VALS3,
+     _val_query(order_by=[("val", "desc")]), [{"val": 42}, {"val": 4}, {"val": 3}], {"ordered": True}),
+    ("skip", "MTa/ReturnTests.scala:236-243", VALS3, _val_query(skip=2), None, {"row_count": 1}),
+    ("order_by_skip", "MTa/ReturnTests.scala:245-255", VALS3,
+     _val_query(order_by=[("val", "asc")], skip=1), [{"val": 4}, {"val": 42}], {"ordered": True}),
+    # SKIP 1 + 1: the front end folds the constant (Skip accepts a literal or parameter,
+    # RelationalOperator.scala:362-377)
+    ("order_by_arithmetic_skip", "MTa/ReturnTests.scala:257-267", VALS3,
+     _val_query(order_by=[("val", "asc")], skip=IntegerLit(2)), [{"val": 42}], {"ordered": True}),
+    ("limit", "MTa/ReturnTests.scala:270-277", VALS3, _val_query(limit=1), None, {"row_count": 1}),
+    ("limit_parameter", "MTa/ReturnTests.scala:279-290", "CREATE (a:A),(b:B),(c:C)",
+     Query([Match([NodeP("a")])], [ret(("a", N("a")), limit=Param("limit")), ret(("a", N("a")))]),
+     None, {"row_count": 1, "params": {"limit": 1}}),
+]
+
+# ------------------------------------------- PredicateTests EXISTS (MTa :705-870)
+# ExistsSubQuery (RelationalPlanner.scala:224-247), SURVEY §8(f) rank 3.
+
+
+def _ex(nodes, rels, where=()):
+    return ExistsPattern(Match(nodes, rels, list(where)))
+
+
+EXISTS_CASES = [
+    ("exists_basic", "MTa/PredicateTests.scala:706-722",
+     """CREATE (v {id: 1})-[:REL]->({id: 2})-[:REL]->(w {id: 3})
+        CREATE (v)-[:REL]->(w)
+        CREATE (w)-[:REL]->({id: 4})""",
+     Query([Match([NodeP("a"), NodeP("b")], [RelP("_r0", "a", "b")],
+                  [_ex([NodeP("a"), NodeP("_x"), NodeP("b")], [RelP("_e1", "a", "_x"), RelP("_e2", "_x", "b")])])],
+           [ret(("a.id", P("a", "id")), ("b.id", P("b", "id")))]),
+     [{"a.id": 1, "b.id": 3}]),
+    ("exists_var_length", "MTa/PredicateTests.scala:724-735",
+     "CREATE (v {id: 1})-[:REL]->({id: 2})-[:REL]->({id: 3})<-[:REL]-(v)",
+     Query([Match([NodeP("a"), NodeP("b")], [RelP("_r0", "a", "b")],
+                  [_ex([NodeP("a"), NodeP("_x"), NodeP("b")],
+                       [RelP("_e1", "a", "_x", length=(1, 3)), RelP("_e2", "_x", "b")])])],
+           [ret(("a.id", P("a", "id")), ("b.id", P("b", "id")))]),
+     [{"a.id": 1, "b.id": 3}]),
+    ("exists_node_predicate", "MTa/PredicateTests.scala:737-751",
+     """CREATE ({id: 1})-[:REL]->({name: 'foo'})
+        CREATE ({id: 3})-[:REL]->({name: 'bar'})""",
+     Query([Match([NodeP("a")], [],
+                  [_ex([NodeP("a"), NodeP("_x")], [RelP("_e1", "a", "_x")],
+                       [Equals(P("_x", "name"), StringLit("foo"))])])],
+           [ret(("a.id", P("a", "id")))]),
+     [{"a.id": 1}]),
+    ("exists_rel_predicate", "MTa/PredicateTests.scala:753-767",
+     """CREATE (v {id: 1})-[:REL {val: 'foo'}]->()-[:REL]->({id: 2})<-[:REL]-(v)
+        CREATE (w {id: 3})-[:REL {val: 'bar'}]->()-[:REL]->({id: 4})<-[:REL]-(w)""",
+     Query([Match([NodeP("a"), NodeP("b")], [RelP("_r0", "a", "b")],
+                  [_ex([NodeP("a"), NodeP("_x"), NodeP("b")], [RelP("_e1", "a", "_x"), RelP("_e2", "_x", "b")],
+                       [Equals(ElementProperty(R("_e1"), "val", "STRING"), StringLit("foo"))])])],
+           [ret(("a.id", P("a", "id")), ("b.id", P("b", "id")))]),
+     [{"a.id": 1, "b.id": 2}]),
+    ("exists_label_predicate", "MTa/PredicateTests.scala:769-783",
+     """CREATE (v{id: 1})-[:REL {val: 'foo'}]->(:A)-[:REL]->({id: 2})<-[:REL]-(v)
+        CREATE (w{id: 3})-[:REL {val: 'bar'}]->(:B)-[:REL]->({id: 4})<-[:REL]-(w)""",
+     Query([Match([NodeP("a"), NodeP("b")], [RelP("_r0", "a", "b")],
+                  [_ex([NodeP("a"), NodeP("_x", ("A",)), NodeP("b")],
+                       [RelP("_e1", "a", "_x"), RelP("_e2", "_x", "b")])])],
+           [ret(("a.id", P("a", "id")), ("b.id", P("b", "id")))]),
+     [{"a.id": 1, "b.id": 2}]),
+    ("exists_type_predicate", "MTa/PredicateTests.scala:785-799",
+     """CREATE (v {id: 1})-[:A]->()-[:REL]->({id: 2})<-[:REL]-(v)
+        CREATE (w {id: 3})-[:B]->()-[:REL]->({id: 4})<-[:REL]-(w)""",
+     Query([Match([NodeP("a"), NodeP("b")], [RelP("_r0", "a", "b")],
+                  [_ex([NodeP("a"), NodeP("_x"), NodeP("b")],
+                       [RelP("_e1", "a", "_x", ("A",)), RelP("_e2", "_x", "b")])])],
+           [ret(("a.id", P("a", "id")), ("b.id", P("b", "id")))]),
+     [{"a.id": 1, "b.id": 2}]),
+    ("exists_inverse", "MTa/PredicateTests.scala:801-813",
+     "CREATE (v {id: 1})-[:REL]->({id: 2})-[:REL]->({id: 3})<-[:REL]-(v)",
+     Query([Match([NodeP("a"), NodeP("b")], [RelP("_r0", "a", "b")],
+                  [Not(_ex([NodeP("a"), NodeP("_x"), NodeP("b")], [RelP("_e1", "a", "_x"), RelP("_e2", "_x", "b")]))])],
+           [ret(("a.id", P("a", "id")), ("b.id", P("b", "id")))]),
+     [{"a.id": 1, "b.id": 2}, {"a.id": 2, "b.id": 3}]),
+    ("exists_nested", "MTa/PredicateTests.scala:815-838",
+     """CREATE ({id: 1, age: 21})
+        CREATE ({id: 2, age: 18, foo: true})
+        CREATE ({id: 3, age: 18, foo: true})-[:KNOWS]->(:Foo)
+        CREATE ({id: 4, age: 18, foo: false})-[:KNOWS]->(:Foo)""",
+     Query([Match([NodeP("a")], [],
+                  [Ors(GreaterThan(P("a", "age"), IntegerLit(20)),
+                       Ands(_ex([NodeP("a"), NodeP("_x", ("Foo",))], [RelP("_e1", "a", "_x", ("KNOWS",))]),
+                            Equals(P("a", "foo"), BoolLit(True))))])],
+           [ret(("a.id", P("a", "id")))]),
+     [{"a.id": 1}, {"a.id": 3}]),
+    ("exists_derived_node_predicate", "MTa/PredicateTests.scala:840-856",
+     """CREATE ({id: 1, val: 0})-[:REL]->({id: 3, val: 2})
+        CREATE ({id: 2, val: 0})-[:REL]->({id: 3, val: 1})""",
+     Query([Match([NodeP("a")], [],
+                  [_ex([NodeP("a"), NodeP("_x")], [RelP("_e1", "a", "_x")],
+                       [Equals(P("_x", "val"), Add(P("a", "val"), IntegerLit(2)))])])],
+           [ret(("a.id", P("a", "id")))]),
+     [{"a.id": 1}]),
+    ("exists_multiple_predicates", "MTa/PredicateTests.scala:858-869",
+     "CREATE ({id: 1})-[:REL]->({id: 2, foo: true})",
+     Query([Match([NodeP("a")], [],
+                  [_ex([NodeP("a"), NodeP("_x")], [RelP("_e1", "a", "_x")],
+                       [Equals(P("_x", "id"), IntegerLit(2)), Equals(P("_x", "foo"), BoolLit(True))])])],
+           [ret(("a.id", P("a", "id")))]),
+     [{"a.id": 1}]),
+]
+CASES = CASES + RETURN_CASES + EXISTS_CASES

@@ -2,7 +2,7 @@
 results of the reference's own acceptance tests (tests/golden/reference_cases.py)."""
 import pytest
 
-from conftest import bag
+from conftest import bag, case_parts, check_case
 from reference_cases import CASES
 
 from capf_amd.graph import ScanGraph
@@ -13,10 +13,10 @@ from oracle.table_np import OracleSession
 
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
 def test_reference_case_on_oracle(case):
-    cid, src, create, query, expected = case
+    cid, src, create, query, expected, opts = case_parts(case)
     g = ScanGraph.from_data(OracleSession(), parse_create(create))
-    got = run(g, query)
-    assert bag(got) == bag(expected), f"{cid} ({src}): {got}"
+    got = run(g, query, opts.get("params"))
+    assert check_case(got, expected, opts), f"{cid} ({src}): {got}"
 
 
 def test_create_parser_ids():
@@ -58,7 +58,7 @@ def test_avg_ints_type_is_checked():
     integers case (AggregationTests.scala:49-57, INTEGER avg per
     Expr.scala:1058-1066): the oracle returns the INTEGER 4, and a FLOAT 4.0
     would fail the comparison."""
-    cid, src, create, query, expected = next(c for c in CASES if c[0] == "avg_ints")
+    cid, src, create, query, expected, _ = case_parts(next(c for c in CASES if c[0] == "avg_ints"))
     got = run(ScanGraph.from_data(OracleSession(), parse_create(create)), query)
     assert bag(got) == bag(expected)
     assert type(got[0]["res"]) is int

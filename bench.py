@@ -144,7 +144,7 @@ def id_width(args):
     FOR32 otherwise).  The values are the reference's int64 ids either way."""
     if args.int64:
         return False
-    return 3 if args.query == "two_hop" and not args.for32 else 4
+    return 3 if args.query in ("two_hop", "one_hop_person") and not args.for32 else 4
 
 
 def id_storage(args):

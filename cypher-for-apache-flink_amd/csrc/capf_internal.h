@@ -97,6 +97,9 @@ struct Column {
   BufPtr valid;  // n bytes (1 = present) or nullptr = no nulls
   mutable std::mutex mu;
   mutable std::optional<ColStats> stats;
+  // are the non-null values pairwise distinct?  -1 unknown (computed once,
+  // like stats: the column is immutable)
+  mutable int8_t unique_flag = -1;
   // values of a tiny host-born column (a fused scalar result), kept beside
   // the device copy so `rows` needs no device round trip
   std::vector<int64_t> host_i64;

@@ -108,8 +108,7 @@ __device__ inline bool load_key(const ColView &c, int64_t r, int64_t &k) {
 }
 
 // One message (or the root sum) of the message-passing count.
-__global__ void k_message(const MsgJob *jp, int64_t n, unsigned long long *root_acc) {
-  const MsgJob &j = *jp;
+__global__ void k_message(const MsgJob j, int64_t n, unsigned long long *root_acc) {
   unsigned long long local = 0;
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
        r += (int64_t)gridDim.x * blockDim.x) {
@@ -138,9 +137,8 @@ __global__ void k_message(const MsgJob *jp, int64_t n, unsigned long long *root_
 // before any is used — the generic loop is one dependent chain per row.
 constexpr int MSG_U = 8;
 
-__global__ __launch_bounds__(256) void k_message_root2(const MsgJob *jp, int64_t n,
+__global__ __launch_bounds__(256) void k_message_root2(const MsgJob j, int64_t n,
                                                        unsigned long long *root_acc) {
-  const MsgJob &j = *jp;
   const int64_t T = (int64_t)gridDim.x * blockDim.x;
   unsigned long long local = 0;
   for (int64_t r0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r0 < n; r0 += MSG_U * T) {
@@ -180,9 +178,8 @@ __device__ inline unsigned long long map_get_t(const DMap &m, int64_t k) {
 }
 
 template <int KA, int KB>
-__global__ __launch_bounds__(256) void k_message_root2_f32(const MsgJob *jp, int64_t n,
+__global__ __launch_bounds__(256) void k_message_root2_f32(const MsgJob j, int64_t n,
                                                            unsigned long long *root_acc) {
-  const MsgJob &j = *jp;
   const uint4 *c0 = (const uint4 *)j.cols[0].data, *c1 = (const uint4 *)j.cols[1].data;
   const int64_t b0 = j.cols[0].base, b1 = j.cols[1].base;
   const DMap ma = j.child[0], mb = j.child[1];
@@ -207,6 +204,63 @@ __global__ __launch_bounds__(256) void k_message_root2_f32(const MsgJob *jp, int
   }
   local = wave_reduce_sum(local);
   if (lane_id() == 0 && local) atomicAdd(root_acc, local);
+}
+
+// Root with ONE remaining child message (the others were all-ones over a
+// range the root's key column provably lies in — column statistics — and are
+// dropped, their column is never read): Σ_rows map(key), 4 rows per 12/16-B
+// load (FOR24 / FOR32) or 2 per 16-B load (int64), 8 rows in flight per lane.
+struct U3w {
+  uint32_t x, y, z;
+};
+
+template <int KA, int W>
+__global__ __launch_bounds__(256) void k_message_root1(const ColView c, const DMap m, int64_t n,
+                                                       unsigned long long *root_acc) {
+  const int64_t base = c.base;
+  const int64_t groups = n / 4, T = (int64_t)gridDim.x * blockDim.x;
+  unsigned long long local = 0;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += 2 * T) {
+    const int64_t g2 = g + T < groups ? g + T : g;
+    int64_t k[8];
+    if (W == 4) {
+      const uint4 a = ((const uint4 *)c.data)[g], e = ((const uint4 *)c.data)[g2];
+      const uint32_t v[8] = {a.x, a.y, a.z, a.w, e.x, e.y, e.z, e.w};
+#pragma unroll
+      for (int u = 0; u < 8; ++u) k[u] = base + (int64_t)v[u];
+    } else if (W == 3) {
+      const U3w a = *(const U3w *)((const uint8_t *)c.data + 12 * g);
+      const U3w e = *(const U3w *)((const uint8_t *)c.data + 12 * g2);
+      const uint32_t v[8] = {a.x & 0xFFFFFFu, __builtin_amdgcn_alignbit(a.y, a.x, 24) & 0xFFFFFFu,
+                             __builtin_amdgcn_alignbit(a.z, a.y, 16) & 0xFFFFFFu, a.z >> 8,
+                             e.x & 0xFFFFFFu, __builtin_amdgcn_alignbit(e.y, e.x, 24) & 0xFFFFFFu,
+                             __builtin_amdgcn_alignbit(e.z, e.y, 16) & 0xFFFFFFu, e.z >> 8};
+#pragma unroll
+      for (int u = 0; u < 8; ++u) k[u] = base + (int64_t)v[u];
+    } else {
+      const longlong2 *p = (const longlong2 *)c.data;
+      const longlong2 a0 = p[2 * g], a1 = p[2 * g + 1], e0 = p[2 * g2], e1 = p[2 * g2 + 1];
+      const int64_t v[8] = {a0.x, a0.y, a1.x, a1.y, e0.x, e0.y, e1.x, e1.y};
+#pragma unroll
+      for (int u = 0; u < 8; ++u) k[u] = v[u];
+    }
+    unsigned long long w[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) w[u] = map_get_t<KA, 0>(m, k[u]);
+    unsigned long long sum = w[0] + w[1] + w[2] + w[3];
+    if (g2 != g) sum += w[4] + w[5] + w[6] + w[7];
+    local += sum;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)(n - 4 * groups)) {  // ragged tail
+    const int64_t r = 4 * groups + threadIdx.x;
+    local += map_get(m, ld_int(c, r));
+  }
+  local = wave_reduce_sum(local);
+  if (lane_id() == 0 && local) atomicAdd(root_acc, local);
+}
+
+__global__ void k_add_u64(unsigned long long *acc, unsigned long long v) {
+  if (threadIdx.x == 0) atomicAdd(acc, v);
 }
 
 // ============================================================ 2-hop fast path
@@ -535,10 +589,15 @@ static bool bits_map_for(Session *s, const ColPtr &parent_key, const ColPtr &myk
                        view_of(mykey), mykey->n, st.min, st.max, words, dup);
     KERNEL_CHECK();
   }
-  uint32_t d = 0;
-  HIP_CHECK(hipMemcpyAsync(&d, dup, 4, hipMemcpyDeviceToHost, s->stream));
-  s->sync();
-  if (d) return false;
+  // duplicates → not a membership map.  Uniqueness is a property of the
+  // (immutable) key column: read back once, cached on the column
+  if (mykey->unique_flag < 0) {
+    uint32_t d = 0;
+    HIP_CHECK(hipMemcpyAsync(&d, dup, 4, hipMemcpyDeviceToHost, s->stream));
+    s->sync();
+    mykey->unique_flag = d ? 0 : 1;
+  }
+  if (!mykey->unique_flag) return false;
   memset(&h.m, 0, sizeof(h.m));
   h.m.kind = MAP_BITS;
   h.m.lo = st.min;
@@ -583,7 +642,8 @@ static HostMap new_map_for(Session *s, const ColPtr &parent_key, int64_t sender_
 }
 
 // Count of the acyclic equi-join described by `g` (no inequalities).
-static bool tree_count(Session *s, JoinGraph &g, uint64_t *out) {
+// Adds the join tree's count to the device counter *d_acc (no host wait).
+static bool tree_count(Session *s, JoinGraph &g, unsigned long long *d_acc) {
   const int L = (int)g.leaves.size();
   if (L == 0) return false;
   // adjacency; reject cycles / multi-edges / disconnected graphs
@@ -628,12 +688,10 @@ static bool tree_count(Session *s, JoinGraph &g, uint64_t *out) {
     if (data[i].data->nrows >= (int64_t(1) << 40)) return false;
 
   std::vector<HostMap> msg(L);
-  BufPtr job_buf = s->alloc(sizeof(MsgJob));
-  BufPtr acc = s->alloc(8);
-  HIP_CHECK(hipMemsetAsync(acc->p, 0, 8, s->stream));
   std::function<void(int, int, int)> visit = [&](int v, int parent, int via_eq) {
     MsgJob j;
     memset(&j, 0, sizeof(j));
+    int root_cols[MAX_CHILD + 1] = {0};
     for (auto &nb : adj[v]) {
       if (nb.first == parent) continue;
       visit(nb.first, v, nb.second);
@@ -642,9 +700,51 @@ static bool tree_count(Session *s, JoinGraph &g, uint64_t *out) {
       int mycol = eq.first.leaf == v ? eq.first.col : eq.second.col;
       j.cols[j.nchild] = view_of(data[v].data->cols[mycol]);
       j.child[j.nchild] = msg[nb.first].m;
+      root_cols[j.nchild] = mycol;
       j.nchild++;
     }
     const int64_t n = data[v].data->nrows;
+    if (parent < 0 && data[v].plain) {
+      // root: a child message that is all-ones over [lo, hi] while this key
+      // column's values all lie in [lo, hi] (no NULLs) weighs every row 1
+      int keep = 0;
+      for (int c = 0; c < j.nchild; ++c) {
+        bool one = false;
+        if (j.child[c].kind == MAP_ONES && !j.cols[c].valid) {
+          const ColPtr &kc = data[v].data->cols[root_cols[c]];
+          const ColStats &st = column_stats(s, kc);
+          one = st.non_null == n && (n == 0 || (st.min >= j.child[c].lo && st.max <= j.child[c].hi));
+        }
+        if (!one) {
+          j.cols[keep] = j.cols[c];
+          j.child[keep] = j.child[c];
+          root_cols[keep] = root_cols[c];
+          ++keep;
+        }
+      }
+      j.nchild = keep;
+      if (keep == 0) {  // every row counts once
+        if (n > 0) hipLaunchKernelGGL(k_add_u64, dim3(1), dim3(64), 0, s->stream, d_acc, (unsigned long long)n);
+        return;
+      }
+      const ColView &c0 = j.cols[0];
+      const int cw = c0.enc == ENC_FOR32 ? 4 : c0.enc == ENC_FOR24 ? 3 : 8;
+      const bool aligned = ((uintptr_t)c0.data & 15) == 0;
+      if (keep == 1 && n > 0 && c0.data && !c0.valid && aligned &&
+          (j.child[0].kind == MAP_BITS || j.child[0].kind == MAP_ONES)) {
+        KernelTimer kt(s, "message_pass", (double)cw * n);
+        auto pick = [&](auto ka) {
+          constexpr int KA = decltype(ka)::value;
+          return cw == 4 ? k_message_root1<KA, 4> : cw == 3 ? k_message_root1<KA, 3> : k_message_root1<KA, 8>;
+        };
+        auto kern = j.child[0].kind == MAP_BITS ? pick(std::integral_constant<int, MAP_BITS>())
+                                                : pick(std::integral_constant<int, MAP_ONES>());
+        hipLaunchKernelGGL(kern, dim3(grid_for(n / 8 + 1, 256, (int64_t)s->num_cus * 16)), dim3(256), 0,
+                           s->stream, c0, j.child[0], n, d_acc);
+        KERNEL_CHECK();
+        return;
+      }
+    }
     if (parent >= 0) {
       const auto &eq = g.eqs[via_eq];
       int mycol = eq.first.leaf == v ? eq.first.col : eq.second.col;
@@ -666,7 +766,6 @@ static bool tree_count(Session *s, JoinGraph &g, uint64_t *out) {
       j.out = msg[v].m;
     }
     if (n == 0) return;
-    HIP_CHECK(hipMemcpyAsync(job_buf->p, &j, sizeof(j), hipMemcpyHostToDevice, s->stream));
     {
       KernelTimer kt(s, "message_pass", 8.0 * n * (j.nchild + j.has_parent));
       const bool root2 = !j.has_parent && j.nchild == 2 && !j.cols[0].valid && !j.cols[1].valid &&
@@ -680,22 +779,18 @@ static bool tree_count(Session *s, JoinGraph &g, uint64_t *out) {
                         : (j.child[1].kind == MAP_BITS ? k_message_root2_f32<MAP_ONES, MAP_BITS>
                                                        : k_message_root2_f32<MAP_ONES, MAP_ONES>);
         hipLaunchKernelGGL(kern, dim3(grid_for(n / 8 + 1, 256, (int64_t)s->num_cus * 16)), dim3(256),
-                           0, s->stream, (const MsgJob *)job_buf->p, n, (unsigned long long *)acc->p);
+                           0, s->stream, j, n, d_acc);
       } else if (root2)
         hipLaunchKernelGGL(k_message_root2, dim3(grid_for(n, 256 * MSG_U, (int64_t)s->num_cus * 16)),
-                           dim3(256), 0, s->stream, (const MsgJob *)job_buf->p, n,
-                           (unsigned long long *)acc->p);
+                           dim3(256), 0, s->stream, j, n, d_acc);
       else
-        hipLaunchKernelGGL(k_message, dim3(grid_for(n, 256)), dim3(256), 0, s->stream,
-                           (const MsgJob *)job_buf->p, n, (unsigned long long *)acc->p);
+        hipLaunchKernelGGL(k_message, dim3(grid_for(n, 256)), dim3(256), 0, s->stream, j, n, d_acc);
       KERNEL_CHECK();
     }
-    s->sync();  // job_buf is reused by the next message
+    // the job travels as a kernel argument (copied at launch): no host wait
+    // between messages (buffers are recycled in stream order)
   };
   visit(root, -1, -1);
-  HIP_CHECK(hipMemcpyAsync(s->h_scalars, acc->p, 8, hipMemcpyDeviceToHost, s->stream));
-  s->sync();
-  *out = (uint64_t)s->h_scalars[0];
   return true;
 }
 
@@ -721,9 +816,14 @@ static bool apply_equalities(const JoinGraph &g, const std::vector<int> &subset,
     DataPtr d = materialize(la.node);
     const ColStats &st = column_stats(la.node->s, d->cols[a.col]);
     if (!(st.dense_unique && st.non_null == d->nrows)) {
-      // uniqueness of a non-dense id column: verify by grouping
-      Grouping gr = group_rows(la.node->s, *d, {a.col});
-      if (gr.ngroups != d->nrows) return false;
+      // uniqueness of a non-dense id column: verified by grouping ONCE, then
+      // cached on the (immutable) column
+      const ColPtr &idc = d->cols[a.col];
+      if (idc->unique_flag < 0) {
+        Grouping gr = group_rows(la.node->s, *d, {a.col});
+        idc->unique_flag = (gr.ngroups == d->nrows && st.non_null == d->nrows) ? 1 : 0;
+      }
+      if (!idc->unique_flag) return false;
     }
     int ra = find(a.leaf), rb = find(b.leaf);
     if (ra != rb) rep[rb] = ra;
@@ -1092,6 +1192,16 @@ static bool run_triangle(Session *s, const JoinGraph &g, const Tri &t, uint64_t 
   return true;
 }
 
+// *dst = Σ_mask (−1)^|mask| · term[mask] (inclusion–exclusion, exact in
+// two's complement)
+__global__ void k_signed_terms(const unsigned long long *term, int k, int64_t *dst) {
+  if (threadIdx.x != 0) return;
+  unsigned long long t = 0;
+  for (int mask = 0; mask < (1 << k); ++mask)
+    t += (__popc(mask) & 1) ? (0ull - term[mask]) : term[mask];
+  *dst = (int64_t)t;
+}
+
 bool try_fused_count(const NodePtr &n, int64_t *out) {
   if (host_trace()) g_trace_t0 = host_us();
   Session *s = n->s;
@@ -1123,22 +1233,37 @@ bool try_fused_count(const NodePtr &n, int64_t *out) {
       return true;
     }
   }
-  if (s->async_out) return false;  // the message-passing count reads partials on the host
-  // general: inclusion–exclusion over the uniqueness predicates
+  // general: inclusion–exclusion over the uniqueness predicates.  Every term
+  // is counted into its own device slot; one kernel forms Σ ±term on the
+  // device (into the async slot, or one download at the end)
   const int k = (int)g.neqs.size();
-  int64_t total = 0;
+  std::vector<JoinGraph> terms(1 << k);
   for (int mask = 0; mask < (1 << k); ++mask) {
     std::vector<int> subset;
     for (int b = 0; b < k; ++b)
       if (mask >> b & 1) subset.push_back(b);
-    JoinGraph t;
-    if (!apply_equalities(g, subset, t)) return false;
-    uint64_t cnt;
-    if (!tree_count(s, t, &cnt)) return false;
-    total += (subset.size() % 2 ? -1 : 1) * (int64_t)cnt;
+    if (!apply_equalities(g, subset, terms[mask])) return false;
   }
+  BufPtr slots = s->alloc(8 * (1 << k) + 8);
+  HIP_CHECK(hipMemsetAsync(slots->p, 0, 8 * (1 << k) + 8, s->stream));
+  unsigned long long *d_slots = (unsigned long long *)slots->p;
+  for (int mask = 0; mask < (1 << k); ++mask)
+    if (!tree_count(s, terms[mask], d_slots + mask)) {
+      s->sync();  // kernels of earlier terms may still read their maps
+      return false;
+    }
+  int64_t *dst = s->async_out ? s->async_out : (int64_t *)(d_slots + (1 << k));
+  hipLaunchKernelGGL(k_signed_terms, dim3(1), dim3(64), 0, s->stream,
+                     (const unsigned long long *)d_slots, k, dst);
+  KERNEL_CHECK();
   s->last_plan = "message_passing";
-  *out = total;
+  if (s->async_out) {
+    *out = 0;
+    return true;
+  }
+  HIP_CHECK(hipMemcpyAsync(s->h_scalars, dst, 8, hipMemcpyDeviceToHost, s->stream));
+  s->sync();
+  *out = (int64_t)s->h_scalars[0];
   return true;
 }
 

@@ -84,6 +84,12 @@ class ScanGraph:
         types = [t.labels for t in self.rel_tables]
         if len(types) != len(set(types)):
             raise ValueError("more than one relationship table per type")
+        # aligned scans per (element tables, labels, properties), built once
+        # with canonical column names and renamed per variable by a zero-copy
+        # select: the graph is immutable, so a scan (and the statistics of
+        # a multi-table UNION ALL behind it) is computed once per graph — the
+        # role of okapi's Cache operator (RelationalOptimizer.scala:37-92)
+        self._scan_cache = {}
 
     @property
     def rel_types(self):
@@ -171,6 +177,17 @@ class ScanGraph:
         from .planner import Planned
         if not sel:
             return Planned(self.session.empty(order, types), h)
+        canon = "_scan_"
+        canon_order = _scan_columns(canon, flags, props, rel)
+        assert len(canon_order) == len(order) and _scan_columns(v.vname, flags, props, rel) == order
+        key = (rel, tuple(id(t) for t in sel), tuple(flags), tuple(sorted(props.items())))
+        base = self._scan_cache.get(key)
+        if base is None:
+            base = self._build_union(sel, h, canon_order, Var(canon, v.ctype), flags, props, rel)
+            self._scan_cache[key] = base
+        return Planned(base.select(*zip(canon_order, order)), h)
+
+    def _build_union(self, sel, h, order, v, flags, props, rel):
         name = v.vname
         parts = []
         for t in sel:
@@ -185,8 +202,7 @@ class ScanGraph:
             tab = t.table.select(*cols)
             adds = []
             for f in flags:
-                e = HasType(v, f) if rel else HasLabel(v, f)
-                adds.append((BoolLit(f in t.labels), h.column(e)))
+                adds.append((BoolLit(f in t.labels), f"{name}:{f}"))
             for k in sorted(props):
                 if k not in present:
                     adds.append((NullLit(props[k]), f"{name}.{k}"))
@@ -197,7 +213,15 @@ class ScanGraph:
         out = parts[0]
         for p in parts[1:]:
             out = out.unionAll(p)
-        return Planned(out, h)
+        return out
+
+
+def _scan_columns(name, flags, props, rel):
+    """Column names of an aligned scan of variable `name` (header order)."""
+    cols = [name] + ([f"source({name})", f"target({name})"] if rel else [])
+    cols += [f"{name}:{f}" for f in flags]
+    cols += [f"{name}.{k}" for k in sorted(props)]
+    return cols
 
 
 def _coerce(v, ct):

@@ -522,3 +522,67 @@ EXISTS_CASES = [
      [{"a.id": 1}]),
 ]
 CASES = CASES + RETURN_CASES + EXISTS_CASES
+
+
+# ------------------------------- AggregationTests "in WITH" / "without alias" (FTt)
+# WITH agg AS res RETURN res: the aggregate is a WITH stage, RETURN projects
+# its alias (a second projection over the grouped table).
+
+
+def _in_with(alias, agg):
+    return scan_n(ret((alias, agg)), ret((alias, Var(alias))))
+
+
+SIX_NAMES = "CREATE ({name: 'foo'}), ({name: 'bar'}), (), (), (), ({name: 'baz'})"
+AGG_WITH_CASES = [
+    ("avg_ints_with", "FTt/acceptance/AggregationTests.scala:39-47", INTS,
+     _in_with("res", Avg(P("n", "val"))), [{"res": 4}]),
+    ("avg_ints_no_alias", "FTt/acceptance/AggregationTests.scala:59-67", INTS,
+     scan_n(ret(("AVG(n.val)", Avg(P("n", "val"))))), [{"AVG(n.val)": 4}]),
+    ("avg_floats_with", "FTt/acceptance/AggregationTests.scala:69-77", FLOATS,
+     _in_with("res", Avg(P("n", "val"))), [{"res": 3.5}]),
+    ("avg_single_null_with", "FTt/acceptance/AggregationTests.scala:89-97", FLOATS_NULL,
+     _in_with("res", Avg(P("n", "val"))), [{"res": 32.5}]),
+    ("avg_only_nulls_with", "FTt/acceptance/AggregationTests.scala:109-117", NULLS,
+     _in_with("res", Avg(P("n", "val"))), [{"res": None}]),
+    ("count_star_with", "FTt/acceptance/AggregationTests.scala:140-148", SIX_NAMES,
+     _in_with("nbrRows", CountStar()), [{"nbrRows": 6}]),
+    ("count_n_no_alias", "FTt/acceptance/AggregationTests.scala:170-178", SIX_NAMES,
+     scan_n(ret(("count(n)", Count(N("n"))))), [{"count(n)": 6}]),
+    ("count_star_no_alias", "FTt/acceptance/AggregationTests.scala:180-188", SIX_NAMES,
+     scan_n(ret(("count(*)", CountStar()))), [{"count(*)": 6}]),
+    ("count_node_with", "FTt/acceptance/AggregationTests.scala:200-208", SIX_NAMES,
+     _in_with("nodes", Count(N("n"))), [{"nodes": 6}]),
+    ("count_grouping_with", "FTt/acceptance/AggregationTests.scala:232-242",
+     "CREATE ({name: 'foo'}), ({name: 'foo'}), (), (), (), ({name: 'baz'})",
+     scan_n(ret(("name", P("n", "name")), ("amount", CountStar())),
+            ret(("name", Var("name")), ("amount", Var("amount")))),
+     [{"name": "foo", "amount": 2}, {"name": None, "amount": 3}, {"name": "baz", "amount": 1}]),
+    ("min_with", "FTt/acceptance/AggregationTests.scala:282-290", INTS3,
+     _in_with("res", Min(P("n", "val"))), [{"res": 23}]),
+    ("min_single_null_with", "FTt/acceptance/AggregationTests.scala:302-310", INTS_NULL,
+     _in_with("res", Min(P("n", "val"))), [{"res": 23}]),
+    ("min_single_null_no_alias", "FTt/acceptance/AggregationTests.scala:322-330", INTS_NULL,
+     scan_n(ret(("MIN(n.val)", Min(P("n", "val"))))), [{"MIN(n.val)": 23}]),
+    ("min_only_nulls_with", "FTt/acceptance/AggregationTests.scala:332-340", NULLS,
+     _in_with("res", Min(P("n", "val"))), [{"res": None}]),
+    ("max_with", "FTt/acceptance/AggregationTests.scala:387-395", INTS3,
+     _in_with("res", Max(P("n", "val"))), [{"res": 84}]),
+    ("max_single_null_with", "FTt/acceptance/AggregationTests.scala:407-415", INTS_NULL,
+     _in_with("res", Max(P("n", "val"))), [{"res": 42}]),
+    ("max_single_null_no_alias", "FTt/acceptance/AggregationTests.scala:427-435", INTS_NULL,
+     scan_n(ret(("MAX(n.val)", Max(P("n", "val"))))), [{"MAX(n.val)": 42}]),
+    ("max_only_nulls_with", "FTt/acceptance/AggregationTests.scala:437-445", NULLS,
+     _in_with("res", Max(P("n", "val"))), [{"res": None}]),
+    ("sum_ints_with", "FTt/acceptance/AggregationTests.scala:494-502", INTS,
+     _in_with("res", Sum(P("n", "val"))), [{"res": 12}]),
+    ("sum_floats_with", "FTt/acceptance/AggregationTests.scala:514-522", FLOATS,
+     _in_with("res", Sum(P("n", "val"))), [{"res": 10.5}]),
+    ("sum_floats_no_alias", "FTt/acceptance/AggregationTests.scala:534-542", FLOATS,
+     scan_n(ret(("SUM(n.val)", Sum(P("n", "val"))))), [{"SUM(n.val)": 10.5}]),
+    ("sum_single_null_with", "FTt/acceptance/AggregationTests.scala:544-552", FLOATS_NULL,
+     _in_with("res", Sum(P("n", "val"))), [{"res": 65.0}]),
+    ("sum_only_nulls_with", "FTt/acceptance/AggregationTests.scala:564-572", NULLS,
+     _in_with("res", Sum(P("n", "val"))), [{"res": None}]),
+]
+CASES = CASES + AGG_WITH_CASES

@@ -128,6 +128,30 @@ def test_one_hop_person_count_rmat(gpu_session, scale, count, compact):
     assert got == cmodel.count_1hop(src, dst, 1 << scale, in_a=person)
 
 
+@pytest.mark.parametrize("compact", [False, True, 3], ids=["int64", "for32", "for24"])
+@pytest.mark.parametrize("scale,nodes", [(12, 3000), (14, 9999), (16, None)])
+def test_one_hop_person_partial_node_range(gpu_session, scale, nodes, compact):
+    """Config 2 with a node table narrower than the rel ids (rels whose target
+    is not a node drop out): the all-ones message of (b) may only be skipped
+    when the target column provably lies in the node range (statistics);
+    here it does not, and the count must still be exact.  Plus the
+    pipelined async path of the message-passing count."""
+    import torch
+    g = rmat_graph(gpu_session, scale, person_split=True, compact=compact, n_nodes=nodes)
+    got = run(g, ONE_HOP_PERSON)[0]["count"]
+    n = nodes or 1 << scale
+    src, dst = cmodel.rmat(scale)
+    person = cmodel.labels(1 << scale, cmodel.rmat_seed(scale))[:n]
+    want = cmodel.count_1hop(src, dst, n, in_a=person)
+    assert got == want
+    slots = torch.full((3,), -1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    for i in range(3):
+        plan_query(g, ONE_HOP_PERSON).table.count_async(slots.data_ptr() + 8 * i)
+    gpu_session.sync()
+    assert slots.cpu().tolist() == [want] * 3
+
+
 def test_two_hop_materialized_vs_oracle(gpu_session):
     """The non-fused path: return the joined rows themselves."""
     q = Query([Match([NodeP("a"), NodeP("b"), NodeP("c")], [RelP("r1", "a", "b"), RelP("r2", "b", "c")])],

@@ -25,6 +25,7 @@ sys.path.insert(0, ROOT)
 import capf_import  # noqa: E402,F401
 
 METRIC = "joined rows/sec for 2-hop MATCH on R-MAT s24 at 1/2/4/8 GPUs; % HBM roofline"
+ROWS_METRIC = "joined rows/sec for MATCH (a)-->(b) RETURN a, b materialised on R-MAT (radix-partitioned join leg)"
 ONE_HOP_METRIC = "joined rows/sec for 1-hop MATCH (a:Person)-->(b) count(*) on R-MAT (config 2)"
 TRI_METRIC = "joined rows/sec for triangle MATCH (a)-->(b)-->(c)-->(a) on R-MAT (config 4)"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -52,7 +53,18 @@ def one_hop_person_query():
                  [Stage([("count", CountStar())])])
 
 
+def one_hop_rows_query():
+    """MATCH (a)-->(b) RETURN a, b — the materialising Expand join (2 joins
+    of RelationalPlanner.scala:130-165 through the radix-partitioned join)."""
+    from capf_amd.expr import Var
+    from capf_amd.planner import Match, NodeP, Query, RelP, Stage
+    return Query([Match([NodeP("a"), NodeP("b")], [RelP("r", "a", "b")])],
+                 [Stage([("a", Var("a", "NODE")), ("b", Var("b", "NODE"))])])
+
+
 def workload_name(args):
+    if args.query == "one_hop_rows":
+        return f"R-MAT s{args.scale} 1-hop MATCH (a)-->(b) RETURN a, b (rows materialised in HBM)"
     if args.query == "one_hop_person":
         return f"R-MAT s{args.scale} 1-hop MATCH (a:Person)-->(b) RETURN count(*)"
     if args.query == "triangle":
@@ -111,7 +123,8 @@ def cpu_baseline(session, graph, scale, budget_s):
 # kernels of one fused 2-hop count (fused_count.hip + chain2_partitioned.hip)
 PIPELINE = ("c5_partition", "c3_transpose", "c3_units", "c5_gather", "c3_overflow", "chain2_hist", "message_pass",
             "chain2_dot", "tri_keys", "tri_sort_keys", "tri_rle", "tri_pairs", "tri_orient",
-            "tri_sort_pairs", "tri_rowptr", "tri_split", "tri_loop3", "tri_count")
+            "tri_sort_pairs", "tri_rowptr", "tri_split", "tri_loop3", "tri_count",
+            "rj_partition1", "rj_partition2", "rj_join_count", "rj_join_emit", "gather")
 
 
 def pipeline_roofline(prof, steps, compulsory_bytes, traffic_per_query=None):
@@ -160,6 +173,63 @@ def timed_steps(fn, steps, sync):
         out = fn()
     sync()
     return out, time.perf_counter() - t0
+
+
+def run_rows_leg(args):
+    """Materialising join leg: K steps of plan + evaluation of
+    MATCH (a)-->(b) RETURN a, b into device memory (no download), ids FOR32.
+    Compulsory bytes (SURVEY §8(d) style): src+dst at int64 width (16 B/rel),
+    the two node scans (8 B/node each) and the result (a, b: 16 B/row + the
+    1-B label flag of each node)."""
+    from capf_amd.planner import plan_query
+    from capf_amd.synthetic import rmat_graph
+    from capf_amd.table import GpuSession
+    s = GpuSession(0)
+    g = rmat_graph(s, args.scale, args.edge_factor, compact=True)
+    q = one_hop_rows_query()
+    n_nodes = 1 << args.scale
+    m = args.edge_factor << args.scale
+    step = lambda: plan_query(g, q).table.materialize()  # noqa: E731
+    rows = plan_query(g, q).table.size
+    if rows != m:
+        raise SystemExit(f"{rows} rows, expected one per rel ({m})")
+    for _ in range(args.warmup):
+        step()
+    s.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    s.sync()
+    elapsed = time.perf_counter() - t0
+    s.reset_profile()
+    s.set_profiling(True)
+    prof_steps = max(1, min(args.steps, 5))
+    for _ in range(prof_steps):
+        step()
+    s.sync()
+    s.set_profiling(False)
+    prof = s.profile()
+    per = {k: v["total_ms"] / prof_steps for k, v in prof.items()}
+    kern_ms = sum(per.values())
+    compulsory = 16.0 * m + 16.0 * n_nodes + 18.0 * rows
+    ms = elapsed * 1e3 / args.steps
+    print(json.dumps({
+        "metric": ROWS_METRIC, "value": rows * args.steps / elapsed, "unit": "joined rows/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "int64",
+        "data": f"synthetic R-MAT s{args.scale} generated in HBM before timing",
+        "config": {"workload": workload_name(args), "scale": args.scale, "nodes": n_nodes, "rels": m,
+                   "rows": rows, "id_storage": "FOR32", "plan": s.last_plan() or "relational (2 joins)",
+                   "join": "radix-partitioned (csrc/radix_join.hip)"},
+        # the step runs many small kernels (two joins, gathers, scans): the
+        # roofline is taken over the whole step's wall time; the timed
+        # kernels' split (partition / join passes) is reported beside it
+        "roofline": {"bound": "hbm", "kernel": "whole step (2 radix joins + gathers + scans), wall time",
+                     "achieved": compulsory / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": compulsory / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "traffic": None, "algorithmic_bytes_per_launch": compulsory,
+                     "timed_kernels_ms_per_step": per, "timed_kernels_ms_sum": kern_ms},
+    }))
 
 
 def run_single(args):
@@ -479,7 +549,7 @@ def main():
     ap.add_argument("--int64", action="store_true", help="keep the id columns int64 (no FOR encoding)")
     ap.add_argument("--for32", action="store_true", help="FOR32 id columns instead of FOR24")
     ap.add_argument("--dist", action="store_true", help="distributed path even at world size 1")
-    ap.add_argument("--query", choices=["two_hop", "triangle", "one_hop_person"], default="two_hop",
+    ap.add_argument("--query", choices=["two_hop", "triangle", "one_hop_person", "one_hop_rows"], default="two_hop",
                     help="two_hop: the headline (config 3); triangle: config 4; one_hop_person: config 2")
     ap.add_argument("--one-device", action="store_true",
                     help="rehearsal: all N ranks on cuda:0 with gloo collectives (not a scaling number)")
@@ -491,7 +561,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus and "WORLD_SIZE" in os.environ:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    if args.gpus > 1 or world > 1 or args.dist:
+    if args.query == "one_hop_rows":
+        run_rows_leg(args)
+    elif args.gpus > 1 or world > 1 or args.dist:
         run_distributed(args)
     else:
         run_single(args)

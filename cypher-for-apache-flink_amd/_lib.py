@@ -101,6 +101,7 @@ _SIGS = {
     "capf_table_cache": (c_int32, [_T, _PT]),
     "capf_table_compact": (c_int32, [_T, _PT]),
     "capf_table_compact_width": (c_int32, [_T, c_int32, _PT]),
+    "capf_table_materialize": (c_int32, [_T]),
     "capf_table_column_encoding": (c_int32, [_T, c_char_p, POINTER(c_int32), POINTER(c_int64)]),
     "capf_table_select": (c_int32, [_T, c_int32, _STRS, _STRS, _PT]),
     "capf_table_filter": (c_int32, [_T, POINTER(CapfExpr), _PT]),

@@ -326,6 +326,12 @@ struct JoinPairs {
 };
 JoinPairs hash_join(Session *s, const Data &l, const Data &r,
                     const std::vector<std::pair<int, int>> &keys, int32_t join_type);
+// Radix-partitioned equi-join on one key column (radix_join.hip): used for
+// large inputs (CAPF_JOIN=radix|hash forces a path).
+bool radix_join_applies(const Data &l, const Data &r, const std::vector<std::pair<int, int>> &keys,
+                        int32_t join_type);
+JoinPairs radix_join(Session *s, const Data &l, const Data &r,
+                     const std::vector<std::pair<int, int>> &keys, int32_t join_type);
 // Aggregations over a grouping.
 ColPtr aggregate(Session *s, const Grouping &g, const Data &d, int64_t nrows, int32_t kind,
                  const ColPtr &arg, Type out_type);

@@ -74,6 +74,7 @@ __device__ inline void map_add(const DMap &m, int64_t k, unsigned long long w) {
     if (k >= m.lo && k <= m.hi) atomicAdd(&m.vals[k - m.lo], w);
     return;
   }
+  if (m.kind != MAP_HASH) return;  // only dense and hash maps have storage
   uint64_t slot = fmix64((uint64_t)k) & m.mask;
   while (true) {
     int64_t cur = m.keys[slot];
@@ -761,6 +762,9 @@ static bool tree_count(Session *s, JoinGraph &g, unsigned long long *d_acc) {
       // childless leaf with unique keys: a membership bitmap (no pass, no atomics on counts)
       if (j.nchild == 0 && bits_map_for(s, data[parent].data->cols[pcol], mykey, msg[v])) return;
       msg[v] = new_map_for(s, data[parent].data->cols[pcol], n);
+      // the parent's key column has no value: the empty all-ones map already
+      // weighs every key 0 — nothing to add (the map has no storage)
+      if (msg[v].m.kind == MAP_ONES) return;
       j.cols[j.nchild] = view_of(mykey);
       j.has_parent = 1;
       j.out = msg[v].m;

@@ -1,0 +1,448 @@
+// radix_join.hip — the radix-partitioned equi-join of the north star, for
+// Table.join on one key column (FlinkTable.join, FlinkTable.scala:171-187;
+// the Expand joins of RelationalPlanner.scala:130-165 are exactly this shape:
+// node id = start(r) / end(r) = node id).
+//
+//   key word w   (the same equality as the hash join: int values / string
+//                 codes by value, floats by bits with -0 = 0, NULL never matches)
+//   h = fmix64(w)  a bijection on 64 bits: h equal ⇔ w equal, so only h is kept
+//   P1 / P2      two radix passes of 8 bits each (h >> 56, then h >> 48 & 255):
+//                per 8 Ki-row tile an LDS histogram, one exclusive scan over
+//                (bucket, tile) counts, an LDS-cursor scatter of (h, row) into
+//                contiguous buckets; the second pass runs per first-level
+//                bucket, so (b1, b2) = 65 536 contiguous partitions per side
+//   J            one workgroup per work item (a partition, or a 8 Ki-row probe
+//                chunk of a big one): the build partition goes into an LDS
+//                open-addressing multimap (4 Ki slots = 48 KiB, chunks of 2 Ki
+//                build rows when larger), every probe row walks its chain;
+//                COUNT pass → one scan of the per-item counts → EMIT pass at
+//                the item's offset, each lane's matches placed by a wave64
+//                prefix sum (ballot popcount when every lane has 0 or 1) and
+//                one block scan: no global atomics, deterministic placement
+//   outer sides  matched flags set in the emit pass, the unmatched rows (NULL
+//                keys included) appended by a flag compaction
+// The build side is the smaller input (inner and outer joins alike: both
+// sides carry matched flags).  Bytes per row and side: P1 read key + write
+// 12 B, P2 read 12 B + write 12 B, J read 12 B; output 16 B per pair.
+#include <algorithm>
+#include <vector>
+
+#include "capf_internal.h"
+#include "device_common.h"
+
+namespace capf {
+
+constexpr int RJ_P = 256;          // buckets per radix pass
+constexpr int RJ_TILE = 8192;      // rows per partitioning tile
+constexpr int RJ_PBLOCK = 512;     // partitioning workgroup
+constexpr int RJ_CAP = 4096;       // LDS multimap slots (h 8 B + row 4 B)
+constexpr int RJ_CHUNK = RJ_CAP / 2;  // build rows per LDS fill (load ≤ 1/2)
+constexpr int RJ_PCHUNK = 8192;    // probe rows per work item
+constexpr int RJ_JBLOCK = 256;     // join workgroup
+constexpr uint32_t RJ_EMPTY = 0xFFFFFFFFu;
+
+__device__ inline uint64_t rj_word(const ColView &c, int64_t r, bool &nul) {
+  if (c.type == CAPF_TYPE_NULL || !c.data || (c.valid && !c.valid[r])) {
+    nul = true;
+    return 0;
+  }
+  nul = false;
+  if (c.type == CAPF_TYPE_BOOL) return ((const uint8_t *)c.data)[r] ? 1 : 0;
+  if (c.type != CAPF_TYPE_FLOAT64) return (uint64_t)ld_int(c, r);
+  uint64_t w = ((const uint64_t *)c.data)[r];
+  return w == 0x8000000000000000ull ? 0 : w;
+}
+
+// ---------------------------------------------------------------- pass 1
+__global__ __launch_bounds__(RJ_PBLOCK) void k_rj_hist1(ColView key, int64_t n, int64_t ntiles,
+                                                         int64_t *counts) {
+  __shared__ uint32_t hist[RJ_P];
+  for (int i = threadIdx.x; i < RJ_P; i += RJ_PBLOCK) hist[i] = 0;
+  __syncthreads();
+  const int64_t t = blockIdx.x, e0 = t * RJ_TILE, e1 = min(e0 + RJ_TILE, n);
+  for (int64_t r = e0 + threadIdx.x; r < e1; r += RJ_PBLOCK) {
+    bool nul;
+    const uint64_t w = rj_word(key, r, nul);
+    if (!nul) atomicAdd(&hist[fmix64(w) >> 56], 1u);
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < RJ_P; b += RJ_PBLOCK) counts[(int64_t)b * ntiles + t] = hist[b];
+}
+
+__global__ __launch_bounds__(RJ_PBLOCK) void k_rj_scatter1(ColView key, int64_t n, int64_t ntiles,
+                                                            const int64_t *offs, uint64_t *oh,
+                                                            uint32_t *orow) {
+  __shared__ uint32_t cur[RJ_P];
+  const int64_t t = blockIdx.x, e0 = t * RJ_TILE, e1 = min(e0 + RJ_TILE, n);
+  for (int b = threadIdx.x; b < RJ_P; b += RJ_PBLOCK)
+    cur[b] = (uint32_t)offs[(int64_t)b * ntiles + t];  // < 2^32 rows per side (checked)
+  __syncthreads();
+  const uint64_t base = 0;
+  for (int64_t r = e0 + threadIdx.x; r < e1; r += RJ_PBLOCK) {
+    bool nul;
+    const uint64_t w = rj_word(key, r, nul);
+    if (nul) continue;
+    const uint64_t h = fmix64(w);
+    const uint64_t pos = base + atomicAdd(&cur[h >> 56], 1u);
+    oh[pos] = h;
+    orow[pos] = (uint32_t)r;
+  }
+}
+
+// ---------------------------------------------------------------- pass 2
+// Tiles of the second pass never straddle a first-level bucket.
+struct RJTile2 {
+  int64_t start, end;   // rows of the pass-1 output
+  int64_t region;       // counts2 region base of the bucket: 256·(first tile of the bucket)
+  int32_t ntb;          // tiles of the bucket
+  int32_t local;        // this tile's index inside its bucket
+};
+
+__global__ __launch_bounds__(RJ_PBLOCK) void k_rj_hist2(const uint64_t *h1, const RJTile2 *tiles,
+                                                         int64_t *counts) {
+  __shared__ uint32_t hist[RJ_P];
+  for (int i = threadIdx.x; i < RJ_P; i += RJ_PBLOCK) hist[i] = 0;
+  __syncthreads();
+  const RJTile2 tl = tiles[blockIdx.x];
+  for (int64_t r = tl.start + threadIdx.x; r < tl.end; r += RJ_PBLOCK)
+    atomicAdd(&hist[(h1[r] >> 48) & (RJ_P - 1)], 1u);
+  __syncthreads();
+  for (int b = threadIdx.x; b < RJ_P; b += RJ_PBLOCK)
+    counts[tl.region + (int64_t)b * tl.ntb + tl.local] = hist[b];
+}
+
+__global__ __launch_bounds__(RJ_PBLOCK) void k_rj_scatter2(const uint64_t *h1, const uint32_t *r1,
+                                                            const RJTile2 *tiles, const int64_t *offs,
+                                                            uint64_t *oh, uint32_t *orow) {
+  __shared__ unsigned long long cur[RJ_P];
+  const RJTile2 tl = tiles[blockIdx.x];
+  for (int b = threadIdx.x; b < RJ_P; b += RJ_PBLOCK)
+    cur[b] = (unsigned long long)offs[tl.region + (int64_t)b * tl.ntb + tl.local];
+  __syncthreads();
+  for (int64_t r = tl.start + threadIdx.x; r < tl.end; r += RJ_PBLOCK) {
+    const uint64_t h = h1[r];
+    const unsigned long long pos = atomicAdd(&cur[(h >> 48) & (RJ_P - 1)], 1ull);
+    oh[pos] = h;
+    orow[pos] = r1[r];
+  }
+}
+
+// Partition starts: pstart[p] for p = b1·256 + b2 (65 536 partitions), + total.
+__global__ void k_rj_pstart(const int64_t *offs2, const RJTile2 *first_tile_of_bucket_region,
+                            const int64_t *bucket_start, const int32_t *bucket_ntiles,
+                            const int64_t *bucket_region, int64_t total, int64_t *pstart) {
+  (void)first_tile_of_bucket_region;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p <= RJ_P * RJ_P; p += gridDim.x * blockDim.x) {
+    if (p == RJ_P * RJ_P) {
+      pstart[p] = total;
+      continue;
+    }
+    const int b1 = p >> 8, b2 = p & 255;
+    const int32_t nt = bucket_ntiles[b1];
+    pstart[p] = nt > 0 ? offs2[bucket_region[b1] + (int64_t)b2 * nt] : bucket_start[b1];
+  }
+}
+
+// Partitioned side: (h, row) in partition order + partition starts.
+struct RJSide {
+  BufPtr h, row, pstart;
+  int64_t n = 0;  // partitioned (non-null) rows
+};
+
+static RJSide rj_partition(Session *s, const ColPtr &col, int64_t n) {
+  RJSide out;
+  out.pstart = s->alloc(8 * (RJ_P * RJ_P + 1));
+  const ColView key = view_of(col);
+  const int64_t nt1 = std::max<int64_t>(1, (n + RJ_TILE - 1) / RJ_TILE);
+  BufPtr c1 = s->alloc(8 * RJ_P * nt1), o1 = s->alloc(8 * (RJ_P * nt1 + 1));
+  int64_t total = 0;
+  {
+    KernelTimer kt(s, "rj_partition1", 12.0 * n);
+    if (n > 0) {
+      hipLaunchKernelGGL(k_rj_hist1, dim3((unsigned)nt1), dim3(RJ_PBLOCK), 0, s->stream, key, n, nt1,
+                         (int64_t *)c1->p);
+      KERNEL_CHECK();
+    } else {
+      HIP_CHECK(hipMemsetAsync(c1->p, 0, 8 * RJ_P * nt1, s->stream));
+    }
+    total = exclusive_scan_i64(s, (const int64_t *)c1->p, (int64_t *)o1->p, RJ_P * nt1);
+  }
+  out.n = total;
+  if (total >= (int64_t(1) << 32)) not_impl("radix join side with 2^32 or more rows");
+  BufPtr h1 = s->alloc(8 * std::max<int64_t>(total, 1)), r1 = s->alloc(4 * std::max<int64_t>(total, 1));
+  if (n > 0) {
+    KernelTimer kt(s, "rj_partition1", 12.0 * total);
+    hipLaunchKernelGGL(k_rj_scatter1, dim3((unsigned)nt1), dim3(RJ_PBLOCK), 0, s->stream, key, n, nt1,
+                       (const int64_t *)o1->p, (uint64_t *)h1->p, (uint32_t *)r1->p);
+    KERNEL_CHECK();
+  }
+  // first-level bucket starts on the host (257 values) → the pass-2 tile list
+  std::vector<int64_t> bstart(RJ_P + 1);
+  {
+    std::vector<int64_t> o1h(RJ_P * nt1 + 1);
+    HIP_CHECK(hipMemcpyAsync(o1h.data(), o1->p, 8 * o1h.size(), hipMemcpyDeviceToHost, s->stream));
+    s->sync();
+    for (int b = 0; b < RJ_P; ++b) bstart[b] = o1h[(size_t)b * nt1];
+    bstart[RJ_P] = total;
+  }
+  std::vector<RJTile2> tiles;
+  std::vector<int32_t> bnt(RJ_P);
+  std::vector<int64_t> breg(RJ_P);
+  for (int b = 0; b < RJ_P; ++b) {
+    const int64_t lo = bstart[b], hi = bstart[b + 1];
+    const int32_t nt = (int32_t)((hi - lo + RJ_TILE - 1) / RJ_TILE);
+    bnt[b] = nt;
+    breg[b] = (int64_t)RJ_P * (int64_t)tiles.size();
+    for (int32_t k = 0; k < nt; ++k)
+      tiles.push_back(RJTile2{lo + (int64_t)k * RJ_TILE, std::min(hi, lo + (int64_t)(k + 1) * RJ_TILE), breg[b], nt, k});
+  }
+  const int64_t nt2 = (int64_t)tiles.size();
+  BufPtr dt = s->alloc(sizeof(RJTile2) * std::max<int64_t>(nt2, 1));
+  BufPtr meta = s->alloc(8 * RJ_P + 4 * RJ_P + 8 * RJ_P);
+  int64_t *d_bstart = (int64_t *)meta->p;
+  int32_t *d_bnt = (int32_t *)(d_bstart + RJ_P);
+  int64_t *d_breg = (int64_t *)(d_bnt + RJ_P);
+  if (nt2 > 0)
+    HIP_CHECK(hipMemcpyAsync(dt->p, tiles.data(), sizeof(RJTile2) * nt2, hipMemcpyHostToDevice, s->stream));
+  HIP_CHECK(hipMemcpyAsync(d_bstart, bstart.data(), 8 * RJ_P, hipMemcpyHostToDevice, s->stream));
+  HIP_CHECK(hipMemcpyAsync(d_bnt, bnt.data(), 4 * RJ_P, hipMemcpyHostToDevice, s->stream));
+  HIP_CHECK(hipMemcpyAsync(d_breg, breg.data(), 8 * RJ_P, hipMemcpyHostToDevice, s->stream));
+  out.h = s->alloc(8 * std::max<int64_t>(total, 1));
+  out.row = s->alloc(4 * std::max<int64_t>(total, 1));
+  BufPtr o2 = s->alloc(8 * (RJ_P * std::max<int64_t>(nt2, 1) + 1));
+  if (nt2 > 0) {
+    KernelTimer kt(s, "rj_partition2", 24.0 * total);
+    BufPtr c2 = s->alloc(8 * RJ_P * nt2);
+    hipLaunchKernelGGL(k_rj_hist2, dim3((unsigned)nt2), dim3(RJ_PBLOCK), 0, s->stream,
+                       (const uint64_t *)h1->p, (const RJTile2 *)dt->p, (int64_t *)c2->p);
+    KERNEL_CHECK();
+    exclusive_scan_i64(s, (const int64_t *)c2->p, (int64_t *)o2->p, RJ_P * nt2);
+    hipLaunchKernelGGL(k_rj_scatter2, dim3((unsigned)nt2), dim3(RJ_PBLOCK), 0, s->stream,
+                       (const uint64_t *)h1->p, (const uint32_t *)r1->p, (const RJTile2 *)dt->p,
+                       (const int64_t *)o2->p, (uint64_t *)out.h->p, (uint32_t *)out.row->p);
+    KERNEL_CHECK();
+  }
+  hipLaunchKernelGGL(k_rj_pstart, dim3((RJ_P * RJ_P + 256) / 256), dim3(256), 0, s->stream,
+                     (const int64_t *)o2->p, (const RJTile2 *)nullptr, (const int64_t *)d_bstart,
+                     (const int32_t *)d_bnt, (const int64_t *)d_breg, total, (int64_t *)out.pstart->p);
+  KERNEL_CHECK();
+  s->sync();  // the host tile list / metadata go out of scope
+  return out;
+}
+
+// ---------------------------------------------------------------- join
+struct RJWork {
+  int32_t part;
+  int32_t pad;
+  int64_t p0, p1;  // probe rows of the item (partition-relative positions in the probe arrays)
+};
+
+// COUNT (emit == false: out_cnt[item] = matches) or EMIT (pairs at out_off[item]).
+template <bool EMIT>
+__global__ __launch_bounds__(RJ_JBLOCK) void k_rj_join(const RJWork *work, const uint64_t *bh,
+                                                        const uint32_t *brow, const int64_t *bstart,
+                                                        const uint64_t *ph, const uint32_t *prow,
+                                                        int64_t *out_cnt, const int64_t *out_off,
+                                                        int64_t *oprobe, int64_t *obuild,
+                                                        uint8_t *pmatched, uint8_t *bmatched) {
+  __shared__ uint64_t th[RJ_CAP];
+  __shared__ uint32_t tr[RJ_CAP];
+  __shared__ int64_t lds_scan[17];
+  const RJWork wk = work[blockIdx.x];
+  const int64_t b0 = bstart[wk.part], b1 = bstart[wk.part + 1];
+  int64_t item_total = 0;
+  int64_t base = EMIT ? out_off[blockIdx.x] : 0;
+  for (int64_t c0 = b0; c0 < b1; c0 += RJ_CHUNK) {
+    const int64_t c1 = min(c0 + (int64_t)RJ_CHUNK, b1);
+    for (int i = threadIdx.x; i < RJ_CAP; i += RJ_JBLOCK) tr[i] = RJ_EMPTY;
+    __syncthreads();
+    for (int64_t i = c0 + threadIdx.x; i < c1; i += RJ_JBLOCK) {
+      const uint64_t h = bh[i];
+      uint32_t slot = (uint32_t)h & (RJ_CAP - 1);
+      while (atomicCAS(&tr[slot], RJ_EMPTY, (uint32_t)(i - c0)) != RJ_EMPTY) slot = (slot + 1) & (RJ_CAP - 1);
+      th[slot] = h;
+    }
+    __syncthreads();
+    for (int64_t q0 = wk.p0; q0 < wk.p1; q0 += RJ_JBLOCK) {
+      const int64_t q = q0 + threadIdx.x;
+      const bool live = q < wk.p1;
+      const uint64_t h = live ? ph[q] : 0;
+      uint32_t cnt = 0;
+      if (live) {
+        uint32_t slot = (uint32_t)h & (RJ_CAP - 1);
+        for (uint32_t e = tr[slot]; e != RJ_EMPTY; slot = (slot + 1) & (RJ_CAP - 1), e = tr[slot])
+          cnt += th[slot] == h ? 1u : 0u;
+      }
+      // wave64 compaction: ballot + popcount when every lane has ≤ 1 match
+      // (a unique build key, the Expand case), else a wave scan
+      int64_t ex, tot;
+      {
+        const unsigned long long many = __ballot(cnt > 1);
+        uint32_t wex, wtot;
+        if (!many) {
+          const unsigned long long m = __ballot(cnt == 1);
+          wex = (uint32_t)__popcll(m & ((1ull << lane_id()) - 1));
+          wtot = (uint32_t)__popcll(m);
+        } else {
+          const uint32_t inc = wave_inclusive_scan(cnt);
+          wex = inc - cnt;
+          wtot = __shfl(inc, WAVE - 1, WAVE);
+        }
+        // block: one value per wave
+        int64_t wave_off, block_tot;
+        {
+          __shared__ int64_t wsum[RJ_JBLOCK / WAVE];
+          const int wv = threadIdx.x / WAVE;
+          if (lane_id() == 0) wsum[wv] = wtot;
+          __syncthreads();
+          int64_t acc = 0, all = 0;
+          for (int k = 0; k < RJ_JBLOCK / WAVE; ++k) {
+            if (k < wv) acc += wsum[k];
+            all += wsum[k];
+          }
+          wave_off = acc;
+          block_tot = all;
+          __syncthreads();
+        }
+        ex = wave_off + wex;
+        tot = block_tot;
+      }
+      if (EMIT && cnt) {
+        int64_t o = base + ex;
+        uint32_t slot = (uint32_t)h & (RJ_CAP - 1);
+        for (uint32_t e = tr[slot]; e != RJ_EMPTY; slot = (slot + 1) & (RJ_CAP - 1), e = tr[slot])
+          if (th[slot] == h) {
+            const uint32_t br = brow[c0 + e];
+            oprobe[o] = prow[q];
+            obuild[o] = br;
+            if (bmatched) bmatched[br] = 1;
+            ++o;
+          }
+        if (pmatched) pmatched[prow[q]] = 1;
+      }
+      base += tot;
+      item_total += tot;
+    }
+    __syncthreads();
+  }
+  (void)lds_scan;
+  if (!EMIT && threadIdx.x == 0) out_cnt[blockIdx.x] = item_total;
+}
+
+__global__ void k_rj_unmatched(const uint8_t *matched, int64_t n, uint8_t *flags) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x)
+    flags[r] = matched[r] ? 0 : 1;
+}
+
+__global__ void k_rj_append(const int64_t *rows, int64_t m, int64_t off, int64_t *own, int64_t *other) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    own[off + i] = rows[i];
+    other[off + i] = -1;
+  }
+}
+
+bool radix_join_applies(const Data &l, const Data &r, const std::vector<std::pair<int, int>> &keys,
+                        int32_t join_type) {
+  if (keys.size() != 1 || join_type == CAPF_JOIN_CROSS) return false;
+  const char *mode = getenv("CAPF_JOIN");  // "radix" | "hash" (default: by size)
+  if (mode && strcmp(mode, "hash") == 0) return false;
+  if (l.nrows >= (int64_t(1) << 32) || r.nrows >= (int64_t(1) << 32)) return false;
+  if (mode && strcmp(mode, "radix") == 0) return true;
+  return std::max(l.nrows, r.nrows) >= (int64_t(1) << 18);
+}
+
+JoinPairs radix_join(Session *s, const Data &l, const Data &r,
+                     const std::vector<std::pair<int, int>> &keys, int32_t join_type) {
+  const bool left_outer = join_type == CAPF_JOIN_LEFT_OUTER || join_type == CAPF_JOIN_FULL_OUTER;
+  const bool right_outer = join_type == CAPF_JOIN_RIGHT_OUTER || join_type == CAPF_JOIN_FULL_OUTER;
+  // build = the smaller side
+  const bool build_left = l.nrows < r.nrows;
+  const Data &B = build_left ? l : r, &Pr = build_left ? r : l;
+  const ColPtr &bk = B.cols[build_left ? keys[0].first : keys[0].second];
+  const ColPtr &pk = Pr.cols[build_left ? keys[0].second : keys[0].first];
+  const bool b_outer = build_left ? left_outer : right_outer;
+  const bool p_outer = build_left ? right_outer : left_outer;
+  RJSide bs = rj_partition(s, bk, B.nrows);
+  RJSide ps = rj_partition(s, pk, Pr.nrows);
+  // work items: partitions with probe rows, big probe partitions in chunks
+  std::vector<int64_t> bst(RJ_P * RJ_P + 1), pst(RJ_P * RJ_P + 1);
+  HIP_CHECK(hipMemcpyAsync(bst.data(), bs.pstart->p, 8 * bst.size(), hipMemcpyDeviceToHost, s->stream));
+  HIP_CHECK(hipMemcpyAsync(pst.data(), ps.pstart->p, 8 * pst.size(), hipMemcpyDeviceToHost, s->stream));
+  s->sync();
+  std::vector<RJWork> work;
+  for (int p = 0; p < RJ_P * RJ_P; ++p) {
+    const int64_t q0 = pst[p], q1 = pst[p + 1];
+    if (q1 == q0 || bst[p + 1] == bst[p]) continue;  // no pair can come out of it
+    for (int64_t a = q0; a < q1; a += RJ_PCHUNK) work.push_back(RJWork{p, 0, a, std::min(q1, a + RJ_PCHUNK)});
+  }
+  // LPT-ish: the dispatcher takes work in order — big build partitions first
+  std::stable_sort(work.begin(), work.end(), [&](const RJWork &x, const RJWork &y) {
+    return bst[x.part + 1] - bst[x.part] > bst[y.part + 1] - bst[y.part];
+  });
+  const int64_t nw = (int64_t)work.size();
+  BufPtr dw = s->alloc(sizeof(RJWork) * std::max<int64_t>(nw, 1));
+  if (nw > 0)
+    HIP_CHECK(hipMemcpyAsync(dw->p, work.data(), sizeof(RJWork) * nw, hipMemcpyHostToDevice, s->stream));
+  BufPtr cnt = s->alloc(8 * std::max<int64_t>(nw, 1)), off = s->alloc(8 * (nw + 1));
+  int64_t total = 0;
+  if (nw > 0) {
+    KernelTimer kt(s, "rj_join_count", 12.0 * (double)(ps.n + bs.n));
+    hipLaunchKernelGGL(k_rj_join<false>, dim3((unsigned)nw), dim3(RJ_JBLOCK), 0, s->stream,
+                       (const RJWork *)dw->p, (const uint64_t *)bs.h->p, (const uint32_t *)bs.row->p,
+                       (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
+                       (const uint32_t *)ps.row->p, (int64_t *)cnt->p, (const int64_t *)nullptr,
+                       (int64_t *)nullptr, (int64_t *)nullptr, (uint8_t *)nullptr, (uint8_t *)nullptr);
+    KERNEL_CHECK();
+    total = exclusive_scan_i64(s, (const int64_t *)cnt->p, (int64_t *)off->p, nw);
+  }
+  BufPtr pm, bm;
+  if (p_outer) {
+    pm = s->alloc(std::max<int64_t>(Pr.nrows, 1));
+    HIP_CHECK(hipMemsetAsync(pm->p, 0, std::max<int64_t>(Pr.nrows, 1), s->stream));
+  }
+  if (b_outer) {
+    bm = s->alloc(std::max<int64_t>(B.nrows, 1));
+    HIP_CHECK(hipMemsetAsync(bm->p, 0, std::max<int64_t>(B.nrows, 1), s->stream));
+  }
+  const int64_t cap = total + (p_outer ? Pr.nrows : 0) + (b_outer ? B.nrows : 0);
+  BufPtr oprobe = s->alloc(8 * std::max<int64_t>(cap, 1)), obuild = s->alloc(8 * std::max<int64_t>(cap, 1));
+  if (nw > 0 && (total > 0 || p_outer || b_outer)) {
+    KernelTimer kt(s, "rj_join_emit", 12.0 * (double)(ps.n + bs.n) + 16.0 * (double)total);
+    hipLaunchKernelGGL(k_rj_join<true>, dim3((unsigned)nw), dim3(RJ_JBLOCK), 0, s->stream,
+                       (const RJWork *)dw->p, (const uint64_t *)bs.h->p, (const uint32_t *)bs.row->p,
+                       (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
+                       (const uint32_t *)ps.row->p, (int64_t *)nullptr, (const int64_t *)off->p,
+                       (int64_t *)oprobe->p, (int64_t *)obuild->p,
+                       p_outer ? (uint8_t *)pm->p : nullptr, b_outer ? (uint8_t *)bm->p : nullptr);
+    KERNEL_CHECK();
+  }
+  int64_t m = total;
+  // unmatched rows of the outer sides (NULL keys included: never flagged)
+  auto append_unmatched = [&](const BufPtr &matched, int64_t n, int64_t *own, int64_t *other) {
+    if (n == 0) return;
+    BufPtr flags = s->alloc(n);
+    hipLaunchKernelGGL(k_rj_unmatched, dim3(grid_for(n, 256)), dim3(256), 0, s->stream,
+                       (const uint8_t *)matched->p, n, (uint8_t *)flags->p);
+    KERNEL_CHECK();
+    int64_t k = 0;
+    BufPtr rows = compact_flags(s, (const uint8_t *)flags->p, n, &k);
+    if (k > 0) {
+      hipLaunchKernelGGL(k_rj_append, dim3(grid_for(k, 256)), dim3(256), 0, s->stream,
+                         (const int64_t *)rows->p, k, m, own, other);
+      KERNEL_CHECK();
+    }
+    m += k;
+  };
+  if (p_outer) append_unmatched(pm, Pr.nrows, (int64_t *)oprobe->p, (int64_t *)obuild->p);
+  if (b_outer) append_unmatched(bm, B.nrows, (int64_t *)obuild->p, (int64_t *)oprobe->p);
+  JoinPairs jp;
+  jp.left = build_left ? obuild : oprobe;
+  jp.right = build_left ? oprobe : obuild;
+  jp.n = m;
+  s->sync();  // the host work list goes out of scope
+  return jp;
+}
+
+}  // namespace capf

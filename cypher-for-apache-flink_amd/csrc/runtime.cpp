@@ -384,7 +384,9 @@ static DataPtr materialize_impl(const NodePtr &n) {
         m = l->nrows * r->nrows;
         cross_index(s, l->nrows, r->nrows, li, ri);
       } else {
-        JoinPairs jp = hash_join(s, *l, *r, n->join_keys, n->join_type);
+        JoinPairs jp = radix_join_applies(*l, *r, n->join_keys, n->join_type)
+                           ? radix_join(s, *l, *r, n->join_keys, n->join_type)
+                           : hash_join(s, *l, *r, n->join_keys, n->join_type);
         li = jp.left;
         ri = jp.right;
         m = jp.n;
@@ -1008,6 +1010,13 @@ capf_status capf_table_device_column(capf_table *t, const char *col, void **valu
   if (values) *values = c->data ? c->data->p : nullptr;
   if (valid) *valid = c->valid ? (uint8_t *)c->valid->p : nullptr;
   if (nrows) *nrows = d->nrows;
+  CAPF_API_END
+}
+
+capf_status capf_table_materialize(capf_table *t) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  materialize(t->node);
   CAPF_API_END
 }
 

@@ -235,6 +235,11 @@ class GpuTable:
         _lib.call("capf_table_size", self._h, byref(n))
         return n.value
 
+    def materialize(self):
+        """Evaluate the table into device memory (no download)."""
+        _lib.call("capf_table_materialize", self._h)
+        return self
+
     def count_async(self, d_count):
         """`size` (or the count(*) of a global group(∅, {count(*)})) written to
         the device int64 at address d_count, without waiting for the GPU."""

@@ -232,6 +232,10 @@ capf_status capf_table_column_encoding(capf_table *t, const char *col, int32_t *
 /* --------------------------------------------------------------- Table[T] */
 /* cache() (Table.scala:52) */
 capf_status capf_table_cache(capf_table *t, capf_table **out);
+/* Not an SPI method: evaluates the lazy operator DAG of t into device
+ * memory (what rows / size do before their download or count) — the
+ * materialising path timed by bench.py --query one_hop_rows.               */
+capf_status capf_table_materialize(capf_table *t);
 /* select((col, alias)+) (Table.scala:71) */
 capf_status capf_table_select(capf_table *t, int32_t n, const char *const *cols,
                               const char *const *aliases, capf_table **out);

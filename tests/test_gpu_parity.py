@@ -32,7 +32,9 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("compact", [False, True, 3], ids=["int64", "for32", "for24"])
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
-def test_reference_case_on_gpu(gpu_session, case, compact):
+def test_reference_case_on_gpu(gpu_session, case, compact, monkeypatch):
+    if compact == 3:  # one encoding runs every reference case through the radix join
+        monkeypatch.setenv("CAPF_JOIN", "radix")
     cid, src, create, query, expected, opts = case_parts(case)
     g = ScanGraph.from_data(gpu_session, parse_create(create), compact=compact)
     got = run(g, query, opts.get("params"))
@@ -268,8 +270,17 @@ def test_with_columns_parity(e):
             assert a["x"] == b["x"]
 
 
+@pytest.fixture(params=["auto", "radix", "hash"])
+def join_mode(request, monkeypatch):
+    """Both materialising join implementations: the radix-partitioned LDS
+    join (radix_join.hip) and the global hash table (kernels_hash.hip)."""
+    if request.param != "auto":
+        monkeypatch.setenv("CAPF_JOIN", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("jt", ["inner", "left_outer", "right_outer", "full_outer", "cross"])
-@pytest.mark.usefixtures("encoding")
+@pytest.mark.usefixtures("encoding", "join_mode")
 def test_join_parity(jt):
     rng = np.random.default_rng(11)
     n1, n2 = (60, 40) if jt == "cross" else (400, 300)
@@ -286,6 +297,55 @@ def test_join_parity(jt):
     oa, ob = OracleSession().table(a), OracleSession().table(b)
     pairs = [] if jt == "cross" else [("ak", "bk"), ("as", "bs")]
     assert bag(ga.join(gb, jt, *pairs).rows) == bag(oa.join(ob, jt, *pairs).rows)
+    if jt != "cross":  # one key column: the radix join's shape
+        one = [("ak", "bk")]
+        assert bag(ga.join(gb, jt, *one).rows) == bag(oa.join(ob, jt, *one).rows)
+        st = [("as", "bs")]  # a STRING key (dictionary codes)
+        assert bag(ga.join(gb, jt, *st).rows) == bag(oa.join(ob, jt, *st).rows)
+
+
+@pytest.mark.parametrize("jt", ["inner", "left_outer", "right_outer", "full_outer"])
+@pytest.mark.parametrize("sizes", [(0, 500), (500, 0), (3000, 200000), (300000, 5000), (70000, 70000)])
+def test_radix_join_large(gpu_session, monkeypatch, jt, sizes):
+    """The radix join at sizes that fill many partitions, with skewed keys
+    (one key on 20 % of the rows: chunked LDS builds and split probe items),
+    NULL keys on both sides, empty sides; checked against numpy."""
+    monkeypatch.setenv("CAPF_JOIN", "radix")
+    rng = np.random.default_rng(sum(sizes))
+    nl, nr = sizes
+    def keys(n, hot):
+        k = rng.integers(0, max(n // 3, 1) + 7, n).astype(np.int64)
+        if hot:  # the larger side: one key on 20 % of its rows
+            k[: n // 5] = 42
+        return k
+    lk, rk = keys(nl, nl >= nr), keys(nr, nr > nl)
+    lv = np.ones(nl, dtype=np.uint8)
+    lv[::97] = 0
+    rv = np.ones(nr, dtype=np.uint8)
+    rv[::89] = 0
+    ga = gpu_session.table([("lk", T_INT, lk, lv), ("li", T_INT, np.arange(nl), None)])
+    gb = gpu_session.table([("rk", T_INT, rk, rv), ("ri", T_INT, np.arange(nr), None)])
+    out = ga.join(gb, jt, ("lk", "rk"))
+    li, lok = out.column_arrays("li")
+    ri, rok = out.column_arrays("ri")
+    got = sorted(zip(np.where(lok, li, -1).tolist(), np.where(rok, ri, -1).tolist()))
+    # numpy reference: pairs of non-null equal keys, plus unmatched rows of outer sides
+    lval, rval = np.nonzero(lv)[0], np.nonzero(rv)[0]
+    from collections import defaultdict
+    byk = defaultdict(list)
+    for j in rval:
+        byk[int(rk[j])].append(int(j))
+    pairs, lm, rm = [], set(), set()
+    for i in lval:
+        for j in byk.get(int(lk[i]), ()):
+            pairs.append((int(i), j))
+            lm.add(int(i))
+            rm.add(j)
+    if jt in ("left_outer", "full_outer"):
+        pairs += [(i, -1) for i in range(nl) if i not in lm]
+    if jt in ("right_outer", "full_outer"):
+        pairs += [(-1, j) for j in range(nr) if j not in rm]
+    assert got == sorted(pairs)
 
 
 def test_join_overlapping_columns_raises():

@@ -88,9 +88,22 @@ struct ColStats {
 // stay inside the allocation.
 enum : int32_t { ENC_PLAIN = 0, ENC_FOR32 = 1, ENC_FOR24 = 2 };
 
+struct Column;
+// Late materialisation: a column defined as rows `idx` of `src` (a join side,
+// a filter, a sort), gathered only when a kernel or a download reads it
+// (force).  Gathers of gathers compose their indexes instead of moving data.
+struct LazyGather {
+  Session *s = nullptr;
+  std::shared_ptr<Column> src;  // never lazy itself
+  BufPtr idx;  // int64 [m], -1 = NULL row (nullable)
+  int64_t m = 0;
+  bool nullable = false;
+};
+
 struct Column {
   Type type = Type::Null;
   int64_t n = 0;
+  std::shared_ptr<LazyGather> lazy;  // non-null: data/valid/enc/base not yet computed
   int32_t enc = ENC_PLAIN;
   int64_t base = 0;  // ENC_FOR32 reference value
   BufPtr data;   // n * width bytes (4 for ENC_FOR32; nullptr for Type::Null or n == 0)
@@ -301,6 +314,16 @@ BufPtr eval_filter(Session *s, const Program &p, const std::vector<std::string> 
 // Gather rows (int64 indices, -1 = null row) of a column.
 ColPtr gather_column(Session *s, const ColPtr &c, const int64_t *d_idx, int64_t n,
                      bool idx_may_be_null = false);
+// Late-materialised gather (LazyGather): rows idx of c, composed with c's own
+// index when c is lazy; `cache` shares one composition among the columns of
+// a side (keyed by the two index buffers).
+struct IdxCache {
+  std::vector<std::pair<std::pair<const void *, const void *>, BufPtr>> entries;
+};
+ColPtr gather_lazy(Session *s, const ColPtr &c, const BufPtr &idx, int64_t n, bool idx_may_be_null,
+                   IdxCache *cache);
+// Computes a lazy column in place (no-op otherwise).
+void force(const ColPtr &c);
 BufPtr iota_index(Session *s, int64_t start, int64_t m);
 void cross_index(Session *s, int64_t nl, int64_t nr, BufPtr &li, BufPtr &ri);
 // Compact indices of rows whose flag byte is non-zero.

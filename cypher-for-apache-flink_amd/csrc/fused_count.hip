@@ -1064,8 +1064,10 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
   LeafData na = leaf_data(g.leaves[c.sa]), nb = leaf_data(g.leaves[c.sb]),
            nc = leaf_data(g.leaves[c.sc]);
   const Data &R = *rel.data;
-  for (int col : {c.u1, c.v1, c.u2, c.v2})
+  for (int col : {c.u1, c.v1, c.u2, c.v2}) {
+    force(R.cols[col]);
     if (R.cols[col]->type != Type::Int64 || R.cols[col]->valid) return false;
+  }
   NodeWeights wa, wb, wc;
   if (!node_weights(s, na, c.ya, wa) || !node_weights(s, nb, c.yb, wb) ||
       !node_weights(s, nc, c.yc, wc))
@@ -1165,8 +1167,10 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
 static bool run_triangle(Session *s, const JoinGraph &g, const Tri &t, uint64_t *out) {
   LeafData rel = leaf_data(g.leaves[t.rel]);
   const Data &R = *rel.data;
-  for (int col : {t.src, t.dst, t.idcol})
+  for (int col : {t.src, t.dst, t.idcol}) {
+    force(R.cols[col]);
     if (R.cols[col]->type != Type::Int64 || R.cols[col]->valid) return false;
+  }
   const ColStats &ids = column_stats(s, R.cols[t.idcol]);
   if (!(ids.dense_unique && ids.non_null == R.nrows) && R.nrows > 1) return false;
   NodeWeights w[3];
@@ -1294,6 +1298,8 @@ extern "C" capf_status capf_chain2_local_hists(capf_session *cs, capf_table *rel
     int si = nd->col_index_or_throw(src_col), di = nd->col_index_or_throw(dst_col);
     DataPtr d = materialize(nd);
     const ColPtr &src = d->cols[si], &dst = d->cols[di];
+    force(src);
+    force(dst);
     if (src->type != Type::Int64 || dst->type != Type::Int64 || src->valid || dst->valid)
       illegal("chain2_local_hists needs non-null INTEGER endpoint columns");
     if (d->nrows >= (int64_t(1) << 32)) not_impl("more than 2^32 rels per rank");
@@ -1354,7 +1360,7 @@ extern "C" capf_status capf_chain2_sharded_count(capf_session *cs, capf_table *i
     const ColPtr &b = dout->cols[out_copy->node->col_index_or_throw(out_src)];
     const ColPtr &c = dout->cols[out_copy->node->col_index_or_throw(out_dst)];
     for (const ColPtr *x : {&a, &b, &c})
-      if ((*x)->type != Type::Int64 || (*x)->valid)
+      if (force(*x), (*x)->type != Type::Int64 || (*x)->valid)
         illegal("sharded 2-hop count needs non-null INTEGER endpoint columns");
     const ColView cols[3] = {view_of(a), view_of(b), view_of(c)};
     if (!chain2_sharded(s, cols, di->nrows, dout->nrows, node_base, n_nodes, parts, part,
@@ -1380,6 +1386,8 @@ extern "C" capf_status capf_triangle_count_part(capf_session *cs, capf_table *re
     DataPtr d = materialize(nd);
     const ColPtr &a = d->cols[nd->col_index_or_throw(src_col)];
     const ColPtr &b = d->cols[nd->col_index_or_throw(dst_col)];
+    force(a);
+    force(b);
     if (a->type != Type::Int64 || b->type != Type::Int64 || a->valid || b->valid)
       illegal("triangle count needs non-null INTEGER endpoint columns");
     if (d->nrows >= (int64_t(1) << 32)) not_impl("more than 2^32 rels");

@@ -194,8 +194,69 @@ __global__ void k_gather_u24(const void *src, const uint8_t *sval, const int64_t
   }
 }
 
+// ------------------------------------------------------ late materialisation
+__global__ void k_compose_idx(const int64_t *outer, const int64_t *inner, int64_t *out, int64_t m) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j = outer[i];
+    out[i] = j < 0 ? -1 : inner[j];
+  }
+}
+
+static bool lazy_enabled() {
+  static const bool on = !(getenv("CAPF_LAZY") && atoi(getenv("CAPF_LAZY")) == 0);
+  return on;
+}
+
+void force(const ColPtr &c) {
+  if (!c || !c->lazy) return;
+  const std::shared_ptr<LazyGather> lz = c->lazy;
+  ColPtr g = gather_column(lz->s, lz->src, (const int64_t *)lz->idx->p, lz->m, lz->nullable);
+  c->data = g->data;
+  c->valid = g->valid;
+  c->enc = g->enc;
+  c->base = g->base;
+  c->lazy.reset();
+}
+
+ColPtr gather_lazy(Session *s, const ColPtr &c, const BufPtr &idx, int64_t m, bool nullable,
+                   IdxCache *cache) {
+  if (!idx || !lazy_enabled() || c->type == Type::Null || m == 0)
+    return gather_column(s, c, idx ? (const int64_t *)idx->p : nullptr, m, nullable);
+  ColPtr src = c;
+  BufPtr id = idx;
+  if (c->lazy) {
+    const std::pair<const void *, const void *> key(c->lazy->idx.get(), idx.get());
+    BufPtr composed;
+    if (cache)
+      for (auto &e : cache->entries)
+        if (e.first == key) composed = e.second;
+    if (!composed) {
+      composed = s->alloc(8 * m);
+      hipLaunchKernelGGL(k_compose_idx, dim3(grid_for(m, 256)), dim3(256), 0, s->stream,
+                         (const int64_t *)idx->p, (const int64_t *)c->lazy->idx->p, (int64_t *)composed->p, m);
+      KERNEL_CHECK();
+      if (cache) cache->entries.emplace_back(key, composed);
+    }
+    id = composed;
+    nullable = nullable || c->lazy->nullable;
+    src = c->lazy->src;
+  }
+  auto o = std::make_shared<Column>();
+  o->type = src->type;
+  o->n = m;
+  o->lazy = std::make_shared<LazyGather>();
+  o->lazy->s = s;
+  o->lazy->src = src;
+  o->lazy->idx = id;
+  o->lazy->m = m;
+  o->lazy->nullable = nullable;
+  return o;
+}
+
 ColPtr gather_column(Session *s, const ColPtr &c, const int64_t *d_idx, int64_t m,
                      bool idx_may_be_null) {
+  force(c);
   if (!d_idx) {
     if (m == c->n) return c;
     illegal("internal: identity gather with mismatched length");
@@ -266,6 +327,8 @@ __global__ void k_copy_part_int(ColView src, int64_t *dst, uint8_t *dval, int64_
 }
 
 ColPtr concat_columns(Session *s, const ColPtr &a, const ColPtr &b, Type t) {
+  force(a);
+  force(b);
   int64_t m = a->n + b->n;
   if (t == Type::Null) return null_column(s, t, m);
   bool with_valid = a->valid || b->valid || a->type == Type::Null || b->type == Type::Null;
@@ -335,6 +398,7 @@ __global__ void k_encode_for24(const int64_t *src, const uint8_t *valid, int64_t
 }
 
 ColPtr decode_column(Session *s, const ColPtr &c) {
+  force(c);
   if (c->enc == ENC_PLAIN) return c;
   auto o = std::make_shared<Column>();
   o->type = c->type;
@@ -356,6 +420,7 @@ ColPtr decode_column(Session *s, const ColPtr &c) {
 // width 4: FOR32 where the range fits 32 bits; width 3: FOR24 where it fits
 // 24 bits, else FOR32 where it fits 32.  Already-encoded columns unchanged.
 ColPtr encode_column(Session *s, const ColPtr &c, int width) {
+  force(c);
   if (c->enc != ENC_PLAIN || (c->type != Type::Int64 && c->type != Type::String) || c->n == 0)
     return c;
   const ColStats &st = column_stats(s, c);
@@ -782,6 +847,16 @@ static DeviceProgram upload_program(Session *s, const Program &p,
 ColPtr eval_program(Session *s, const Program &p, const std::vector<std::string> &names,
                     const Data &d, Type out_type) {
   int64_t n = d.nrows;
+  // a bare column reference of the same type (a projection `x AS y`): the
+  // column is shared, not copied (columns are immutable)
+  if (p.code.size() == 1 && p.code[0].op == OP_COL && p.code[0].i >= 0 &&
+      (size_t)p.code[0].i < p.names.size()) {
+    const auto it = std::find(names.begin(), names.end(), p.names[(size_t)p.code[0].i]);
+    if (it != names.end()) {
+      const ColPtr &c = d.cols[(size_t)(it - names.begin())];
+      if (c->type == out_type) return c;
+    }
+  }
   ColPtr o = make_column(s, out_type, n, true);
   if (n == 0) return o;
   DeviceProgram dp = upload_program(s, p, names, d);

@@ -326,6 +326,7 @@ ColPtr null_column(Session *s, Type t, int64_t n) {
 }
 
 ColView view_of(const ColPtr &c) {
+  force(c);
   ColView v;
   v.data = c->data ? c->data->p : nullptr;
   v.valid = c->valid ? (const uint8_t *)c->valid->p : nullptr;
@@ -336,6 +337,7 @@ ColView view_of(const ColPtr &c) {
 }
 
 const ColStats &column_stats(Session *s, const ColPtr &c) {
+  force(c);
   std::lock_guard<std::mutex> g(c->mu);
   if (!c->stats) c->stats = compute_stats(s, *c);
   return *c->stats;
@@ -351,9 +353,10 @@ DataPtr materialize(const NodePtr &n) {
 }
 
 static DataPtr gather_all(Session *s, const Data &d, const BufPtr &idx, int64_t m) {
+  IdxCache cache;
   auto out = std::make_shared<Data>();
   out->nrows = m;
-  for (auto &c : d.cols) out->cols.push_back(gather_column(s, c, (const int64_t *)(idx ? idx->p : nullptr), m));
+  for (auto &c : d.cols) out->cols.push_back(gather_lazy(s, c, idx, m, false, &cache));
   return out;
 }
 
@@ -395,10 +398,9 @@ static DataPtr materialize_impl(const NodePtr &n) {
       out->nrows = m;
       bool lnull = n->join_type == CAPF_JOIN_RIGHT_OUTER || n->join_type == CAPF_JOIN_FULL_OUTER;
       bool rnull = n->join_type == CAPF_JOIN_LEFT_OUTER || n->join_type == CAPF_JOIN_FULL_OUTER;
-      for (auto &c : l->cols)
-        out->cols.push_back(gather_column(s, c, (const int64_t *)(li ? li->p : nullptr), m, lnull));
-      for (auto &c : r->cols)
-        out->cols.push_back(gather_column(s, c, (const int64_t *)(ri ? ri->p : nullptr), m, rnull));
+      IdxCache cache;  // the columns of one side share one (composed) index
+      for (auto &c : l->cols) out->cols.push_back(gather_lazy(s, c, li, m, lnull, &cache));
+      for (auto &c : r->cols) out->cols.push_back(gather_lazy(s, c, ri, m, rnull, &cache));
       return out;
     }
     case Kind::Union: {
@@ -829,6 +831,7 @@ capf_status capf_table_node_partition(capf_table *t, const char *key_col, int64_
   DataPtr d = materialize(t->node);
   Session *s = t->node->s;
   const ColPtr &kc = d->cols[ki];
+  force(kc);
   if (kc->valid) illegal("partition key must be non-null");
   BufPtr flags;
   const uint8_t *f = node_owner_flags(s, view_of(kc), d->nrows, node_base, n_nodes, parts, part, flags);
@@ -855,6 +858,7 @@ capf_status capf_table_column_encoding(capf_table *t, const char *col, int32_t *
   int i = t->node->col_index_or_throw(col);
   DataPtr d = materialize(t->node);
   const ColPtr &c = d->cols[i];
+  force(c);
   if (enc) *enc = c->enc;
   if (base) *base = c->base;
   CAPF_API_END
@@ -998,6 +1002,7 @@ capf_status capf_table_device_column(capf_table *t, const char *col, void **valu
   need(col, "col");
   int i = t->node->col_index_or_throw(col);
   DataPtr d = materialize(t->node);
+  force(d->cols[i]);
   if (d->cols[i]->enc != ENC_PLAIN) {
     // the handle's storage becomes the plain column (same values), so the
     // returned pointer lives as long as the table
@@ -1016,7 +1021,8 @@ capf_status capf_table_device_column(capf_table *t, const char *col, void **valu
 capf_status capf_table_materialize(capf_table *t) {
   CAPF_API_BEGIN
   need(t, "table");
-  materialize(t->node);
+  DataPtr d = materialize(t->node);
+  for (const ColPtr &c : d->cols) force(c);  // every result column lands in HBM
   CAPF_API_END
 }
 

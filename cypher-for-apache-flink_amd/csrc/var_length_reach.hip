@@ -358,6 +358,7 @@ static DataPtr var_length_reach(Session *s, const ColPtr &rsrc, const ColPtr &rd
 
 static ColPtr int_column_of(const NodePtr &nd, const DataPtr &d, const char *name) {
   const ColPtr &c = d->cols[nd->col_index_or_throw(name)];
+  force(c);
   if (c->type != Type::Int64) illegal(std::string("column ") + name + " is not INTEGER");
   if (c->valid) not_impl(std::string("var-length reach: nullable id column ") + name);
   return c;

@@ -344,7 +344,11 @@ struct C3Unit {
 // Histogram slices: a graph with few runs (small, or one rank's share of a
 // node-partitioned graph) still needs 2 full waves of P3 units on 256 CUs, so every run is cut into S tile ranges, each counted into its own
 // slice of the histograms with plain stores; the dot sums the slices.
-static int c5_slices(int nr) { return std::min(8, std::max(1, (512 + nr - 1) / nr)); }
+static int c5_slices(int nr) {
+  const char *e = getenv("CAPF_SLICES");  // tuning
+  if (e && atoi(e) > 0) return std::min(8, atoi(e));
+  return std::min(8, std::max(1, (512 + nr - 1) / nr));
+}
 
 constexpr int C3_UBLOCK = 1024;
 
@@ -1247,13 +1251,15 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
   owned_buckets(kbits, parts, part, &b0, &nbl);
   if (2 * nbl + 1 > C5S_MAXR) return false;
   if (n_in >= (int64_t(1) << 31) || n_out >= (int64_t(1) << 31)) return false;
-  int nf = 0;
+  int nf = 0, n24 = 0;
   for (int i = 0; i < 3; ++i) {
     if (cols[i].valid || (!cols[i].data && (i == 0 ? n_in : n_out) > 0)) return false;
     if ((uintptr_t)cols[i].data & 15) return false;
     nf += cols[i].enc == ENC_FOR32;
+    n24 += cols[i].enc == ENC_FOR24;
   }
-  if (nf != 0 && nf != 3) return false;
+  if (nf + n24 != 0 && nf != 3 && n24 != 3) return false;
+  const int W = n24 == 3 ? 3 : nf == 3 ? 4 : 8;
   BufPtr acc = s->alloc(16);
   HIP_CHECK(hipMemsetAsync(acc->p, 0, 16, s->stream));
   unsigned long long *d_acc = (unsigned long long *)acc->p;  // [0] Σ in·out, [1] loops
@@ -1262,9 +1268,9 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
     c.kin = cols[0].data;
     c.kout = cols[1].data;
     c.oth = cols[2].data;
-    c.bin = nf ? cols[0].base : 0;
-    c.bout = nf ? cols[1].base : 0;
-    c.both = nf ? cols[2].base : 0;
+    c.bin = W != 8 ? cols[0].base : 0;
+    c.bout = W != 8 ? cols[1].base : 0;
+    c.both = W != 8 ? cols[2].base : 0;
     c.n_in = n_in;
     c.n_out = n_out;
     // tile size: whole rounds of resident blocks (2 per CU), counting one
@@ -1298,9 +1304,10 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
       BufPtr partb = s->alloc(2 * rstride * ntiles);
       BufPtr meta = s->alloc(4 * nr * ntiles);
       {
-        KernelTimer kt(s, "c5_partition", (nf ? 4.0 : 8.0) * (n_in + 2 * n_out));
-        auto kern = nf ? (kbits > 24 ? k_c5_shard_partition<4, true> : k_c5_shard_partition<4, false>)
-                       : (kbits > 24 ? k_c5_shard_partition<8, true> : k_c5_shard_partition<8, false>);
+        KernelTimer kt(s, "c5_partition", (double)W * (n_in + 2 * n_out));
+        auto kern = W == 3 ? (kbits > 24 ? k_c5_shard_partition<3, true> : k_c5_shard_partition<3, false>)
+                    : W == 4 ? (kbits > 24 ? k_c5_shard_partition<4, true> : k_c5_shard_partition<4, false>)
+                             : (kbits > 24 ? k_c5_shard_partition<8, true> : k_c5_shard_partition<8, false>);
         hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(C5_BLOCK), 0, s->stream, c,
                            (uint16_t *)partb->p, (uint32_t *)meta->p, d_acc + 1, rstride);
         KERNEL_CHECK();

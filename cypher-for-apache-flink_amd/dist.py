@@ -99,13 +99,12 @@ def gpu_two_hop_count(session, rels, n_nodes, node_base=0, group=None, hists=Non
 def node_partitioned_copies(rels, n_nodes, world, rank, node_base=0, src="source", dst="target",
                             compact=True):
     """(in_copy, out_copy) of this rank: the rels whose target / source node it
-    owns (FOR32-compacted unless compact=False).  Graph-ingest step, outside
-    the timed query."""
+    owns, FOR-compacted (compact=True/4: FOR32, 3: FOR24 where the id range
+    fits 24 bits; False: int64).  Graph-ingest step, outside the timed query."""
+    from .table import compact_as
     out_copy = rels.node_partition(src, node_base, n_nodes, world, rank)
     in_copy = rels.node_partition(dst, node_base, n_nodes, world, rank)
-    if compact:
-        out_copy, in_copy = out_copy.compact(), in_copy.compact()
-    return in_copy, out_copy
+    return compact_as(in_copy, compact), compact_as(out_copy, compact)
 
 
 def gpu_two_hop_count_sharded(session, in_copy, out_copy, n_nodes, partial, node_base=0, group=None):

@@ -20,7 +20,7 @@ m, n = 16 << scale, 1 << scale
 full = s.rmat_rels(scale, rmat_seed(scale), thresholds(), 0, m)
 tot = 0
 for p in parts:
-    ic, oc = node_partitioned_copies(full, n, G, p)
+    ic, oc = node_partitioned_copies(full, n, G, p, compact=int(os.environ.get("CAPF_WIDTH", "3")))
     partial = torch.zeros(1, dtype=torch.int64, device="cuda")
     run = lambda: chain2_sharded_count_async(s, ic, oc, 0, n, G, p, partial.data_ptr())  # noqa: E731
     for _ in range(3):

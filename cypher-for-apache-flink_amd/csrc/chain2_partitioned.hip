@@ -347,7 +347,8 @@ struct C3Unit {
 static int c5_slices(int nr) {
   const char *e = getenv("CAPF_SLICES");  // tuning
   if (e && atoi(e) > 0) return std::min(8, atoi(e));
-  return std::min(8, std::max(1, (512 + nr - 1) / nr));
+  // one unit per CU: G = 8 rank (64 runs) S = 4 → 0.250 ms/rank vs S = 8 0.271, S = 2 0.300
+  return std::min(8, std::max(1, (256 + nr - 1) / nr));
 }
 
 constexpr int C3_UBLOCK = 1024;
@@ -545,17 +546,32 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
                                                             const uint32_t *meta_t, int64_t ntiles,
                                                             int nb, int64_t rstride, uint32_t *h_in,
                                                             uint32_t *h_out, int64_t slice_stride,
-                                                            C3Ovf ovf, const int32_t *order) {
-  if ((int)blockIdx.x >= *nunits && order) return;
+                                                            C3Ovf ovf, const int32_t *order,
+                                                            C3Sides sd, int S) {
+  // units == null: the static work list of a node-partitioned rank — unit
+  // (run, k) counts tile range k of S of the run's side into slice k
+  const int nu = units ? *nunits : 2 * sd.nb * S;
+  if ((int)blockIdx.x >= nu && order) return;
   const int ui = order ? order[blockIdx.x] : c3_unit_of((int)blockIdx.x);
-  if (ui >= *nunits) return;
+  if (ui >= nu) return;
   const unsigned long long t_start = ovf.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
   extern __shared__ __attribute__((aligned(16))) uint32_t words[];
   constexpr int NW = C5_BLOCK / WAVE;
   constexpr uint32_t STEP = WAVE * PPS;
   uint32_t *corr = words + C2_WORDS;
   C5WaveTab *tabs = (C5WaveTab *)(corr + C5_CORR);  // 2 per wave
-  const C3Unit u = units[ui];
+  C3Unit u;
+  if (units) {
+    u = units[ui];
+  } else {
+    const int k = ui % S, sdi = ui / S >= sd.nb ? 1 : 0;
+    const int64_t len = sd.t1[sdi] - sd.t0[sdi];
+    u.run = ui / S;
+    u.exclusive = 1;
+    u.t0 = sd.t0[sdi] + len * k / S;
+    u.t1 = sd.t0[sdi] + len * (k + 1) / S;
+    u.slice = k;
+  }
   const uint32_t side = u.run >= nb ? 1u : 0u;
   uint32_t *hist = side ? h_out : h_in;
   const uint32_t hist_base = (uint32_t)(u.slice * slice_stride + (int64_t)(u.run % nb) * C2_BW);
@@ -878,7 +894,7 @@ static void launch_c5(Session *s, const C5Cols<W> &c, uint16_t *part, uint32_t *
 // at h_in/h_out + s·slice_stride; every counter of every slice is written.
 static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, const C3Sides &sd,
                     int64_t ntiles, int64_t rstride, int64_t nkeys, int S, uint32_t *h_in,
-                    uint32_t *h_out, int64_t slice_stride) {
+                    uint32_t *h_out, int64_t slice_stride, bool static_units = false) {
   const int nr = 2 * sd.nb;
   static bool attr_set = false;
   if (!attr_set) {
@@ -928,7 +944,7 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
                        run_total, tt);
     KERNEL_CHECK();
   }
-  {
+  if (!static_units) {
     KernelTimer kt(s, "c3_units", 8.0 * nr);
     hipLaunchKernelGGL(k_c3_units, dim3(1), dim3(C3_UBLOCK), 0, s->stream,
                        (const unsigned long long *)run_total, nr, sd, S, units, nunits, split, order);
@@ -953,10 +969,11 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
                 : h1                  ? k_c5_gather<C5_PPS, 0, 1, 1>
                 : d2                  ? k_c5_gather<C5_PPS, 0, 2>
                                       : k_c5_gather<C5_PPS, 0>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)max_units), dim3(C5_BLOCK), C5_GATHER_LDS, s->stream,
-                       (const C3Unit *)units, (const int32_t *)nunits, part,
-                       (const uint32_t *)meta_t->p, ntiles, sd.nb, rstride, h_in, h_out,
-                       slice_stride, ovf, (const int32_t *)order);
+    const int grid = static_units ? (nr * S + 255) / 256 * 256 : max_units;
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(C5_BLOCK), C5_GATHER_LDS, s->stream,
+                       static_units ? nullptr : (const C3Unit *)units, (const int32_t *)nunits,
+                       part, (const uint32_t *)meta_t->p, ntiles, sd.nb, rstride, h_in, h_out,
+                       slice_stride, ovf, static_units ? nullptr : (const int32_t *)order, sd, S);
     KERNEL_CHECK();
   }
   {
@@ -1072,12 +1089,13 @@ struct C5Shard {
   int64_t lo;
   uint64_t len;
   int b0, nbl;                   // owned buckets [b0, b0 + nbl)
+  int lsub, nsb;                 // 2^lsub sub-bucket runs per bucket and side; nsb = nbl << lsub
   int copies;                    // run counters per run (power of 2, see below)
   int gpt;                       // 4096-row groups per tile (≤ 4): tile = 4096·gpt rows
   NodeMix mix;
 };
 
-constexpr int C5S_TILE = 16384;  // rows (= keys) per tile (at most)
+constexpr int C5S_TILE = 32768;  // rows (= keys) per tile (at most); 16384 via CAPF_SHARD_TILE=16
 constexpr int C5S_MAXR = 520;    // runs incl. the dummy: nbl ≤ 259
 constexpr int C5S_CNT = 1024;    // LDS run counters: copies · (runs + 1) ≤ 1024
 
@@ -1091,10 +1109,10 @@ static int c5s_copies(int nr) {
   return c;
 }
 
-template <int W, bool WIDE>
+template <int W, bool WIDE, int TILE>
 __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_c5_shard_partition(
     C5Shard c, uint16_t *part, uint32_t *meta, unsigned long long *loops, int64_t rstride) {
-  constexpr int TILE = C5S_TILE, MAXR = C5S_MAXR;
+  constexpr int MAXR = C5S_MAXR;
   constexpr int RPT = TILE / C5_BLOCK, GROUPS = RPT / 4;
   constexpr int STAGE = TILE + 8 * MAXR;
   static_assert(MAXR <= C5_BLOCK, "one run per thread in the scan");
@@ -1105,7 +1123,7 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   uint16_t *stage = (uint16_t *)stage4;
   const int64_t t = blockIdx.x;
   const int side = t >= c.t_in ? 1 : 0;  // block-uniform
-  const int nr = 2 * c.nbl;
+  const int nr = 2 * c.nsb;
   const int C = c.copies;
   const uint32_t my_copy = (uint32_t)(lane_id() & (C - 1));
   const uint32_t pb = 8u * (uint32_t)(t & 7);
@@ -1123,7 +1141,8 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   const void *kp = side ? c.kout : c.kin;
   const int64_t kb = side ? c.bout : c.bin;
   const uint32_t dummy = (uint32_t)nr << C2_BITS;
-  const uint32_t run0 = (uint32_t)(side * c.nbl);
+  const uint32_t run0 = (uint32_t)(side * c.nsb);
+  const uint32_t lsub = (uint32_t)c.lsub, ssh = 16u - lsub;  // h & 0xFFFF >> 16 = 0: no sub-buckets
   uint32_t key[RPT];
   uint32_t lp = 0;
   // the next group's loads are issued before this group's hashing/counting
@@ -1157,7 +1176,8 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
         const uint32_t h = node_mix_t<WIDE>(x[k], c.mix);
         const uint32_t b = (h >> C2_BITS) - (uint32_t)c.b0;  // wraps when below b0
         const bool ok = okx[k] && b < (uint32_t)c.nbl;
-        key[4 * g + k] = ok ? ((b + run0) << C2_BITS) | (h & 0xFFFF) : dummy;
+        const uint32_t run = run0 + (b << lsub) + ((h & 0xFFFF) >> ssh);
+        key[4 * g + k] = ok ? (run << C2_BITS) | (h & 0xFFFF) : dummy;
         if (side) lp += (ok && oky[k] && x[k] == y[k]) ? 1u : 0u;
         atomicAdd(&cur[(key[4 * g + k] >> C2_BITS) * C + my_copy], 1u);
       }
@@ -1195,6 +1215,293 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   for (uint32_t i = threadIdx.x; i < body_end / 8; i += C5_BLOCK) dst[i] = stage4[i];
   unsigned long long lp64 = wave_reduce_sum((unsigned long long)lp);
   if (lane_id() == 0 && lp64) atomicAdd(loops, lp64);
+}
+
+// ---------------------------------------------- sharded P3, sub-bucket units
+// A rank owning few buckets (G ≥ 4 at s24: 64 or 32 buckets) has P1 cut every
+// owned 64 Ki bucket into 2^lsub sub-bucket runs per side (runs [0, nsb) in,
+// [nsb, 2·nsb) out), so ONE workgroup holds both the in- and the out-counters
+// of a sub-bucket in LDS (uint32, 2 · 2^sbits) and finishes Σ in·out itself:
+// no histogram slices in HBM, no dot / overflow / units kernels, 4 fewer
+// launches.  Waves 0..7 count the in-run over the in-copy tiles [0, t_in),
+// waves 8..15 the out-run over the out-copy tiles [t_in, ntiles).  Piece
+// walking, the pad / dead-lane correction and the hub-key merge are those of
+// k_c5_gather; uint32 bins cannot overflow (≤ 2^31 rows per copy).
+struct C5SbArgs {
+  const uint16_t *part;
+  const uint32_t *meta_t;
+  int64_t ntiles, t_in;
+  int nsb, sbits;
+  uint32_t rs8;
+  unsigned long long *acc;    // += Σ in·out
+  unsigned long long *trace;  // diagnostics (CAPF_P3_TRACE): 4 words per unit, else null
+};
+
+constexpr int C5SB_MAXBITS = 14;
+constexpr size_t c5sb_lds(int sbits) {
+  return 4 * ((size_t)2 << sbits) + 4 * 2 * C5_CORR + 2 * sizeof(C5WaveTab) * (C5_BLOCK / WAVE);
+}
+
+__global__ __launch_bounds__(C5_BLOCK) void k_c5_sb_gather(C5SbArgs a) {
+  const int ui = c3_unit_of((int)blockIdx.x);
+  if (ui >= a.nsb) return;
+  const unsigned long long t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  extern __shared__ __attribute__((aligned(16))) uint32_t words[];
+  __shared__ unsigned long long lds_red[17];
+  constexpr int NW = C5_BLOCK / WAVE, HW = NW / 2;
+  constexpr uint32_t STEP = WAVE * C5_PPS;
+  const int NB = 1 << a.sbits;
+  uint32_t *corr = words + 2 * NB;
+  C5WaveTab *tabs = (C5WaveTab *)(corr + 2 * C5_CORR);
+  for (int i = threadIdx.x; i < 2 * NB + 2 * C5_CORR; i += C5_BLOCK) words[i] = 0;
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = lane_id();
+  const int side = wave >= HW ? 1 : 0, sw = wave - side * HW;
+  uint32_t *cnt = words + side * NB;
+  const uint32_t kmask = (uint32_t)NB - 1;
+  C5WaveTab *tab2 = tabs + 2 * wave;
+  const uint4 *part4 = (const uint4 *)a.part;
+  const uint32_t *m = a.meta_t + (int64_t)(ui + side * a.nsb) * a.ntiles;
+  const int64_t s0 = side ? a.t_in : 0, s1 = side ? a.ntiles : a.t_in;
+  const int64_t w0 = uniform64(s0 + (s1 - s0) * sw / HW), w1 = uniform64(s0 + (s1 - s0) * (sw + 1) / HW);
+  uint32_t padc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t dead = 0;
+  const uint4 dead_keys = make_uint4(lane | lane << 16, lane | lane << 16, lane | lane << 16,
+                                     lane | lane << 16);
+  uint32_t wpre = w0 + lane < w1 ? m[w0 + lane] : 0u;
+  auto setup = [&](int64_t tb, int buf) -> uint32_t {
+    const int64_t t = tb + lane;
+    const uint32_t w = wpre;
+    const uint32_t len = w >> 16, nq = (len + 7) >> 3, r = len & 7;
+#pragma unroll
+    for (int e = 1; e < 8; ++e) padc[e] += (r != 0 && r <= (uint32_t)e) ? 1u : 0u;
+    const uint32_t inc = wave_inclusive_scan(nq);
+    tab2[buf].pre[lane] = inc - nq;
+    if (lane == WAVE - 1) tab2[buf].pre[WAVE] = inc;
+    tab2[buf].qb[lane] = (uint32_t)t * a.rs8 + (w & 0xFFFF);
+    __builtin_amdgcn_sched_barrier(0);
+    const int64_t tn = tb + WAVE + lane;
+    wpre = tn < w1 ? m[tn] : 0u;
+    __builtin_amdgcn_wave_barrier();
+    return (uint32_t)__builtin_amdgcn_readfirstlane(__shfl(inc, WAVE - 1, WAVE));
+  };
+  auto fetch = [&](int buf, uint32_t p0, uint32_t total, uint4 *v) {
+    const C5WaveTab &tab = tab2[buf];
+#pragma unroll
+    for (int j = 0; j < C5_PPS; ++j) {
+      const uint32_t p = p0 + j * WAVE + lane;
+      const uint32_t pc = min(p, total - 1);
+      uint32_t k = 0;
+#pragma unroll
+      for (int b = WAVE / 2; b > 0; b >>= 1)
+        if (tab.pre[k + b] <= pc) k += b;
+      v[j] = part4[tab.qb[k] + (pc - tab.pre[k])];
+    }
+  };
+  // a piece's copies of its first (second) key are added once, as a count
+  auto count = [&](const uint4 *v, uint32_t p0, uint32_t total) {
+#pragma unroll
+    for (int j = 0; j < C5_PPS; ++j) {
+      const bool live = p0 + j * WAVE + lane < total;
+      dead += live ? 0u : 1u;
+      const uint32_t wd[4] = {live ? v[j].x : dead_keys.x, live ? v[j].y : dead_keys.y,
+                              live ? v[j].z : dead_keys.z, live ? v[j].w : dead_keys.w};
+      const uint32_t k0 = wd[0] & 0xFFFF, k1 = wd[0] >> 16;
+      uint32_t n0 = k1 == k0 ? 2u : 1u, n1 = 1;
+      bool dup[8];
+#pragma unroll
+      for (int e = 2; e < 8; ++e) {
+        const uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
+        const bool d0 = key == k0, d1 = !d0 && key == k1;
+        dup[e] = d0 || d1;
+        n0 += d0 ? 1u : 0u;
+        n1 += d1 ? 1u : 0u;
+      }
+      atomicAdd(&cnt[k0 & kmask], n0);
+      if (k1 != k0) atomicAdd(&cnt[k1 & kmask], n1);
+#pragma unroll
+      for (int e = 2; e < 8; ++e) {
+        const uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
+        if (!dup[e]) atomicAdd(&cnt[key & kmask], 1u);
+      }
+    }
+  };
+  if (w0 < w1) {
+    int64_t tb = uniform64(w0);
+    int buf = 0;
+    uint32_t total = setup(tb, buf), p0 = 0;
+    while (total == 0) {
+      tb += WAVE;
+      if (tb >= w1) break;
+      buf ^= 1;
+      total = setup(tb, buf);
+    }
+    if (total) {
+      auto advance = [&]() -> bool {
+        if (p0 + STEP < total) {
+          p0 = (uint32_t)__builtin_amdgcn_readfirstlane(p0 + STEP);
+          return true;
+        }
+        do {
+          tb = uniform64(tb + WAVE);
+          if (tb >= w1) return false;
+          buf ^= 1;
+          total = setup(tb, buf);
+          p0 = 0;
+        } while (total == 0);
+        return true;
+      };
+      // three rotating piece buffers: loads of steps i+1, i+2 in flight while step i counts
+      uint4 va[C5_PPS], vb[C5_PPS], vc[C5_PPS];
+      uint32_t pa, ta, pb, tb2, pc, tc;
+      pa = p0;
+      ta = total;
+      fetch(buf, p0, total, va);
+      if (!advance()) {
+        count(va, pa, ta);
+      } else {
+        pb = p0;
+        tb2 = total;
+        fetch(buf, p0, total, vb);
+        for (;;) {
+          if (!advance()) {
+            count(va, pa, ta);
+            count(vb, pb, tb2);
+            break;
+          }
+          pc = p0;
+          tc = total;
+          fetch(buf, p0, total, vc);
+          count(va, pa, ta);
+          if (!advance()) {
+            count(vb, pb, tb2);
+            count(vc, pc, tc);
+            break;
+          }
+          pa = p0;
+          ta = total;
+          fetch(buf, p0, total, va);
+          count(vb, pb, tb2);
+          if (!advance()) {
+            count(vc, pc, tc);
+            count(va, pa, ta);
+            break;
+          }
+          pb = p0;
+          tb2 = total;
+          fetch(buf, p0, total, vb);
+          count(vc, pc, tc);
+        }
+      }
+    }
+  }
+  uint32_t *cs = corr + side * C5_CORR;
+  const uint32_t pcls = 8u * (uint32_t)((w0 + lane) & 7);
+#pragma unroll
+  for (int e = 1; e < 8; ++e)
+    if (padc[e]) atomicAdd(&cs[pcls + e], padc[e]);
+  if (dead) atomicAdd(&cs[lane], 8 * dead);
+  __syncthreads();
+  unsigned long long t = 0;
+  for (int i = threadIdx.x; i < NB; i += C5_BLOCK) {
+    uint32_t x = words[i], y = words[NB + i];
+    if (i < C5_CORR) {
+      x -= corr[i];
+      y -= corr[C5_CORR + i];
+    }
+    t += (unsigned long long)x * y;
+  }
+  unsigned long long tot;
+  block_exclusive_scan(t, lds_red, tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(a.acc, tot);
+  if (a.trace && threadIdx.x == 0) {  // diagnostics: this unit's span, where it ran
+    const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (3 << 11));
+    const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));
+    a.trace[4 * ui] = t_start;
+    a.trace[4 * ui + 1] = __builtin_amdgcn_s_memrealtime();
+    a.trace[4 * ui + 2] = ((unsigned long long)xcc << 32) | hw;
+    a.trace[4 * ui + 3] = (unsigned long long)ui << 32;
+  }
+}
+
+// Sub-bucket runs per bucket (log2) for a rank owning nbl buckets: the most
+// that keep 2·nsb + 1 runs within P1's limit; 0 (slice path) unless the
+// sub-buckets are ≤ 2^C5SB_MAXBITS nodes (LDS: 2 uint32 arrays).
+static int c5sb_lsub(int nbl) {
+  // measured at s24 G = 8 and off by default: per-unit rates equal the slice
+  // path's, but 8 Ki-node sub-buckets are skewed (p99 unit 1.7×, the hub's
+  // 3.2× the median) where the slice units are not → 0.296 vs 0.235 ms/rank
+  const char *e = getenv("CAPF_SHARD_SB");  // tuning: 1 = sub-bucket units
+  if (!(e && atoi(e) == 1) || nbl <= 0) return 0;
+  int l = 0;
+  while (l < C2_BITS && 2 * ((int64_t)nbl << (l + 1)) + 1 <= C5S_MAXR) ++l;
+  return C2_BITS - l <= C5SB_MAXBITS ? l : 0;
+}
+
+// T + P3 of the sub-bucket path: meta transpose, then one k_c5_sb_gather unit
+// per sub-bucket, adding Σ in·out into d_acc[0].
+static void c5_sb_post(Session *s, const uint16_t *part, const uint32_t *meta, int64_t ntiles,
+                       int64_t t_in, int nsb, int sbits, int64_t rstride, unsigned long long *d_acc) {
+  const int nr = 2 * nsb;
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIP_CHECK(hipFuncSetAttribute((const void *)k_c5_sb_gather,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)c5sb_lds(C5SB_MAXBITS)));
+    attr_set = true;
+  }
+  BufPtr meta_t = s->alloc(4 * nr * ntiles);
+  BufPtr tot = s->alloc(8 * nr);
+  HIP_CHECK(hipMemsetAsync(tot->p, 0, 8 * nr, s->stream));
+  int64_t tt = C3_TT;
+  while (tt > 32 && ((ntiles + tt - 1) / tt) * ((nr + 31) / 32) < 1024) tt /= 2;
+  {
+    KernelTimer kt(s, "c3_transpose", 8.0 * nr * ntiles);
+    hipLaunchKernelGGL(k_c3_transpose, dim3((unsigned)((ntiles + tt - 1) / tt), (nr + 31) / 32),
+                       dim3(256), 0, s->stream, meta, (uint32_t *)meta_t->p, ntiles, nr,
+                       (unsigned long long *)tot->p, tt);
+    KERNEL_CHECK();
+  }
+  C5SbArgs a;
+  a.part = part;
+  a.meta_t = (const uint32_t *)meta_t->p;
+  a.ntiles = ntiles;
+  a.t_in = t_in;
+  a.nsb = nsb;
+  a.sbits = sbits;
+  a.rs8 = (uint32_t)(rstride / 8);
+  a.acc = d_acc;
+  a.trace = nullptr;
+  const char *trace_path = getenv("CAPF_P3_TRACE");  // diagnostics only
+  const int nblocks = (nsb + 255) / 256 * 256;       // c3_unit_of is a bijection per 256
+  BufPtr trace;
+  if (trace_path) {
+    trace = s->alloc(32 * (int64_t)nsb);
+    HIP_CHECK(hipMemsetAsync(trace->p, 0, 32 * (size_t)nsb, s->stream));
+    a.trace = (unsigned long long *)trace->p;
+  }
+  {
+    KernelTimer kt(s, "c5_gather", 2.0 * (double)rstride * ntiles);
+    hipLaunchKernelGGL(k_c5_sb_gather, dim3((unsigned)nblocks), dim3(C5_BLOCK), c5sb_lds(sbits),
+                       s->stream, a);
+    KERNEL_CHECK();
+  }
+  if (trace_path) {
+    std::vector<unsigned long long> h(4 * (size_t)nsb);
+    s->sync();
+    HIP_CHECK(hipMemcpy(h.data(), trace->p, 32 * (size_t)nsb, hipMemcpyDeviceToHost));
+    if (FILE *f = fopen(trace_path, "ab")) {
+      fwrite(h.data(), 8, h.size(), f);
+      fclose(f);
+    }
+  }
+}
+
+template <int TILE>
+static auto c5s_kernel(int W, bool wide) {
+  return W == 3 ? (wide ? k_c5_shard_partition<3, true, TILE> : k_c5_shard_partition<3, false, TILE>)
+         : W == 4 ? (wide ? k_c5_shard_partition<4, true, TILE> : k_c5_shard_partition<4, false, TILE>)
+                  : (wide ? k_c5_shard_partition<8, true, TILE> : k_c5_shard_partition<8, false, TILE>);
 }
 
 // Buckets of 64 Ki mixed node indexes owned by `part` of `parts`.
@@ -1275,10 +1582,13 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
     c.n_out = n_out;
     // tile size: whole rounds of resident blocks (2 per CU), counting one
     // group of per-tile overhead (stage fill, scan, copy-out)
+    const char *te = getenv("CAPF_SHARD_TILE");  // tuning: 16 → 16 Ki-row tiles
+    // (32 Ki-row tiles need 32 keys per thread in VGPRs: no spills at FOR24 only)
+    const int tile = (te && atoi(te) == 16) || W != 3 ? 16384 : C5S_TILE;
     {
       const int64_t slots = 2 * (int64_t)s->num_cus;
       int64_t best = -1;
-      for (int g = C5S_TILE / (4 * C5_BLOCK); g >= 1; --g) {
+      for (int g = tile / (4 * C5_BLOCK); g >= 1; --g) {
         const int64_t rows = (int64_t)g * 4 * C5_BLOCK;
         const int64_t tiles = (n_in + rows - 1) / rows + (n_out + rows - 1) / rows;
         const int64_t cost = (tiles + slots - 1) / slots * (g + 1);
@@ -1297,38 +1607,51 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
     c.b0 = b0;
     c.nbl = nbl;
     c.mix = node_mix_for(kbits);
-    const int nr = 2 * nbl;
+    // sub-bucket units (k_c5_sb_gather) when the runs fit P1 and the two
+    // counter arrays fit LDS; CAPF_SHARD_SB=0 (tuning) keeps the slice path
+    const int lsub = c5sb_lsub(nbl);
+    c.lsub = lsub;
+    c.nsb = nbl << lsub;
+    const int nr = 2 * c.nsb;
     c.copies = c5s_copies(nr);
-    const int64_t rstride = ((int64_t)C5S_TILE + 8 * (nr + 1) + 7) & ~int64_t(7);
+    const int64_t rstride = ((int64_t)tile + 8 * (nr + 1) + 7) & ~int64_t(7);
     if (ntiles > 0) {
       BufPtr partb = s->alloc(2 * rstride * ntiles);
       BufPtr meta = s->alloc(4 * nr * ntiles);
       {
         KernelTimer kt(s, "c5_partition", (double)W * (n_in + 2 * n_out));
-        auto kern = W == 3 ? (kbits > 24 ? k_c5_shard_partition<3, true> : k_c5_shard_partition<3, false>)
-                    : W == 4 ? (kbits > 24 ? k_c5_shard_partition<4, true> : k_c5_shard_partition<4, false>)
-                             : (kbits > 24 ? k_c5_shard_partition<8, true> : k_c5_shard_partition<8, false>);
+        auto kern = tile == C5S_TILE ? c5s_kernel<C5S_TILE>(W, kbits > 24) : c5s_kernel<16384>(W, kbits > 24);
         hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(C5_BLOCK), 0, s->stream, c,
                            (uint16_t *)partb->p, (uint32_t *)meta->p, d_acc + 1, rstride);
         KERNEL_CHECK();
       }
-      C3Sides sd;
-      sd.split_x16 = c3_split_x16();
-      sd.nb = nbl;
-      sd.t0[0] = 0;
-      sd.t1[0] = c.t_in;
-      sd.t0[1] = c.t_in;
-      sd.t1[1] = ntiles;
-      const int S = c5_slices(nr);
-      const int64_t hl = (int64_t)nbl * C2_BW;
-      BufPtr sl = s->alloc(8 * S * hl);
-      uint32_t *si = (uint32_t *)sl->p, *so = si + S * hl;
-      c5_post(s, (const uint16_t *)partb->p, (const uint32_t *)meta->p, sd, ntiles, rstride,
-              n_in + n_out, S, si, so, hl);
-      KernelTimer kt(s, "chain2_dot", 8.0 * S * hl);
-      hipLaunchKernelGGL(k_c5_dot_slices, dim3(grid_for(hl / 4, 256, 1024)), dim3(256), 0,
-                         s->stream, si, so, S, hl, hl, d_acc);
-      KERNEL_CHECK();
+      if (lsub > 0) {
+        c5_sb_post(s, (const uint16_t *)partb->p, (const uint32_t *)meta->p, ntiles, c.t_in,
+                   c.nsb, 16 - lsub, rstride, d_acc);
+      } else {
+        C3Sides sd;
+        sd.split_x16 = c3_split_x16();
+        sd.nb = nbl;
+        sd.t0[0] = 0;
+        sd.t1[0] = c.t_in;
+        sd.t0[1] = c.t_in;
+        sd.t1[1] = ntiles;
+        const int S = c5_slices(nr);
+        const int64_t hl = (int64_t)nbl * C2_BW;
+        BufPtr sl = s->alloc(8 * S * hl);
+        uint32_t *si = (uint32_t *)sl->p, *so = si + S * hl;
+        // static work list (no units / zero kernels): S tile ranges per run; a
+        // rank's runs hold ≤ 1.4 × the mean at s24 (no hub splits happen)
+        const char *st = getenv("CAPF_SHARD_STATIC");  // tuning: 0 = device work list
+        c5_post(s, (const uint16_t *)partb->p, (const uint32_t *)meta->p, sd, ntiles, rstride,
+                n_in + n_out, S, si, so, hl, !(st && atoi(st) == 0));
+        KernelTimer kt(s, "chain2_dot", 8.0 * S * hl);
+        // one block per CU: every block ends in one same-address device atomic
+        // (G = 8 rank: 256 blocks 18.5 µs, 1024 24.4 µs, 2048 36 µs)
+        hipLaunchKernelGGL(k_c5_dot_slices, dim3(grid_for(hl / 4, 256, dot_grid(s->num_cus))),
+                           dim3(256), 0, s->stream, si, so, S, hl, hl, d_acc);
+        KERNEL_CHECK();
+      }
     }
   }
   hipLaunchKernelGGL(k_partial_minus_loops, dim3(1), dim3(64), 0, s->stream,

@@ -118,6 +118,13 @@ __device__ inline T block_reduce_sum(T v, T *lds /* >= 16 */) {
   return r;  // valid in thread 0 only
 }
 
+// Blocks of a dot-product kernel (each block ends in one same-address device
+// atomic, so fewer blocks cost less): `dflt`, or CAPF_DOT_GRID (tuning).
+inline int64_t dot_grid(int64_t dflt) {
+  const char *e = getenv("CAPF_DOT_GRID");
+  return e && atoi(e) > 0 ? atoi(e) : dflt;
+}
+
 inline unsigned grid_for(int64_t n, int block, int64_t cap = 256 * 16) {
   int64_t g = (n + block - 1) / block;
   if (g < 1) g = 1;

@@ -1134,7 +1134,8 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
     }
     {
       KernelTimer kt(s, "chain2_dot", 8.0 * dot_len);
-      unsigned grid = grid_for(dot_len / 4 + 1, 256, 256 * 8);
+      // one block per CU (s24: 256 blocks 24 µs, 2048 37 µs — same-address atomics)
+      unsigned grid = grid_for(dot_len / 4 + 1, 256, dot_grid(s->num_cus));
       if (wb.ones)  // ONES: Σ in·out is invariant under the node_mix bijection
         hipLaunchKernelGGL(k_chain2_dot<true>, dim3(grid), dim3(256), 0, s->stream, h1, h2,
                            wb.map.m, lo, dot_len, (unsigned long long *)acc->p);

@@ -326,6 +326,7 @@ __global__ __launch_bounds__(256) void k_c3_transpose(const uint32_t *meta, uint
     for (int q = 0; q < 8; ++q) c += part[q][tx];
     if (c && r < nr) atomicAdd(&run_total[r], (unsigned long long)c);
   }
+  if (!meta_t) return;  // run totals only (P3 reads meta in place)
   const int lt = __builtin_ctzll((unsigned long long)tt);  // tt is a power of two
   for (int idx = threadIdx.x; idx < 32 * tt; idx += 256) {
     const int q = idx >> lt, i = idx & (int)(tt - 1);
@@ -547,7 +548,7 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
                                                             int nb, int64_t rstride, uint32_t *h_in,
                                                             uint32_t *h_out, int64_t slice_stride,
                                                             C3Ovf ovf, const int32_t *order,
-                                                            C3Sides sd, int S) {
+                                                            C3Sides sd, int S, int64_t mstride) {
   // units == null: the static work list of a node-partitioned rank — unit
   // (run, k) counts tile range k of S of the run's side into slice k
   const int nu = units ? *nunits : 2 * sd.nb * S;
@@ -581,7 +582,8 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = lane_id();
   C5WaveTab *tab2 = tabs + 2 * wave;
   const uint4 *part4 = (const uint4 *)part;
-  const uint32_t *m = meta_t + (int64_t)u.run * ntiles;
+  // run-major meta_t (mstride 1) or P1's tile-major meta read in place (mstride nr)
+  const uint32_t *m = meta_t + (mstride == 1 ? (int64_t)u.run * ntiles : (int64_t)u.run);
   const int64_t ut = u.t1 - u.t0;
   const int64_t w0 = uniform64(u.t0 + ut * wave / NW), w1 = uniform64(u.t0 + ut * (wave + 1) / NW);
   const uint32_t rs8 = (uint32_t)(rstride / 8);
@@ -597,7 +599,7 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
   const uint4 dead_keys = make_uint4(lane | lane << 16, lane | lane << 16, lane | lane << 16,
                                      lane | lane << 16);
   // batch setup: table of tiles [tb, tb + 64) into tab2[buf]; returns the piece total
-  uint32_t wpre = w0 + lane < w1 ? m[w0 + lane] : 0u;  // meta word of the next batch
+  uint32_t wpre = w0 + lane < w1 ? m[(w0 + lane) * mstride] : 0u;  // meta word of the next batch
   auto setup = [&](int64_t tb, int buf) -> uint32_t {
     const int64_t t = tb + lane;
     const uint32_t w = wpre;
@@ -612,7 +614,7 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
     // load lands in the same register (no copy → no early wait)
     __builtin_amdgcn_sched_barrier(0);
     const int64_t tn = tb + WAVE + lane;
-    wpre = tn < w1 ? m[tn] : 0u;
+    wpre = tn < w1 ? m[tn * mstride] : 0u;
     __builtin_amdgcn_wave_barrier();
     return (uint32_t)__builtin_amdgcn_readfirstlane(__shfl(inc, WAVE - 1, WAVE));
   };
@@ -909,7 +911,12 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   const int max_units = (S * nr + nr + 16 * nr / std::max(1, sd.split_x16) + 2 + 255) / 256 * 256;
   // every overflow event consumes 2^15 adds of one half-counter within one unit
   const uint32_t ovf_cap = (uint32_t)(nkeys / (1 << 15) + 64 + 16 * (int64_t)max_units);
-  BufPtr meta_t = s->alloc(4 * nr * ntiles);
+  // CAPF_META_T=0 (tuning): P3 reads P1's tile-major meta in place (the units
+  // of 32 consecutive runs on one XCD share its lines in L2) and the transpose
+  // kernel only sums the run totals — s24: transpose 31 → 24 µs, P3 +7..20 µs
+  const char *mt = getenv("CAPF_META_T");
+  const bool transpose = !(mt && atoi(mt) == 0);
+  BufPtr meta_t = transpose ? s->alloc(4 * nr * ntiles) : BufPtr();
   // transpose blocks: tiles per block tt, fewer when there are few runs (≥ ~1024 blocks)
   int64_t tt = C3_TT;
   while (tt > 32 && ((ntiles + tt - 1) / tt) * ((nr + 31) / 32) < 1024) tt /= 2;
@@ -940,7 +947,7 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   {
     KernelTimer kt(s, "c3_transpose", 8.0 * nr * ntiles);
     hipLaunchKernelGGL(k_c3_transpose, dim3((unsigned)nparts, (nr + 31) / 32), dim3(256), 0,
-                       s->stream, meta, (uint32_t *)meta_t->p, ntiles, nr,
+                       s->stream, meta, transpose ? (uint32_t *)meta_t->p : nullptr, ntiles, nr,
                        run_total, tt);
     KERNEL_CHECK();
   }
@@ -972,8 +979,10 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
     const int grid = static_units ? (nr * S + 255) / 256 * 256 : max_units;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(C5_BLOCK), C5_GATHER_LDS, s->stream,
                        static_units ? nullptr : (const C3Unit *)units, (const int32_t *)nunits,
-                       part, (const uint32_t *)meta_t->p, ntiles, sd.nb, rstride, h_in, h_out,
-                       slice_stride, ovf, static_units ? nullptr : (const int32_t *)order, sd, S);
+                       part, transpose ? (const uint32_t *)meta_t->p : meta, ntiles, sd.nb,
+                       rstride, h_in, h_out, slice_stride, ovf,
+                       static_units ? nullptr : (const int32_t *)order, sd, S,
+                       transpose ? (int64_t)1 : (int64_t)nr);
     KERNEL_CHECK();
   }
   {

@@ -1,0 +1,112 @@
+/*
+ * GpuExprMapper.scala — lowers okapi `Expr` trees to capf_expr postfix programs:
+ * the GPU counterpart of FlinkSQLExprMapper.asFlinkSQLExpr
+ * (flink-cypher/src/main/scala/org/opencypher/flink/impl/FlinkSQLExprMapper.scala:48-294)
+ * and the JVM twin of cypher-for-apache-flink_amd/expr.py::compile_program (the
+ * Python binding the parity tests run).  Column references resolve through
+ * the RecordHeader; a header expression without a physical column becomes a
+ * typed NULL literal (FlinkSQLExprMapper.scala:60-73); `Param`s are
+ * substituted as literals; anything else is NotImplementedException, as in
+ * FlinkSQLExprMapper.scala:289-290.
+ */
+package org.opencypher.gpu
+
+import scala.collection.mutable
+
+import org.opencypher.okapi.api.value.CypherValue._
+import org.opencypher.okapi.impl.exception.NotImplementedException
+import org.opencypher.okapi.ir.api.expr._
+import org.opencypher.okapi.relational.impl.table.RecordHeader
+
+object GpuExprMapper {
+  // opcodes of include/capf_gpu.h (CAPF_OP_*)
+  private final val Col = 1; private final val LitInt = 2; private final val LitFloat = 3
+  private final val LitBool = 4; private final val LitString = 5; private final val LitNull = 6
+  private final val Eq = 10; private final val Neq = 11; private final val Lt = 12; private final val Le = 13
+  private final val Gt = 14; private final val Ge = 15
+  private final val Not_ = 20; private final val And = 21; private final val Or = 22
+  private final val IsNull_ = 23; private final val IsNotNull_ = 24
+  private final val Add_ = 30; private final val Sub = 31; private final val Mul = 32; private final val Div = 33
+  private final val Mod = 34; private final val Neg = 35
+  private final val ToFloat_ = 40; private final val ToInteger_ = 41; private final val Coalesce_ = 50
+
+  def program(expr: Expr, header: RecordHeader, table: GpuTable, parameters: CypherMap): Program = {
+    val ops = mutable.ArrayBuffer.empty[Int]
+    val iargs = mutable.ArrayBuffer.empty[Long]
+    val fargs = mutable.ArrayBuffer.empty[Double]
+    val names = mutable.LinkedHashMap.empty[String, Int]
+    lazy val columns = table.physicalColumns.toSet
+    implicit val session: GpuCypherSession = table.session
+
+    def emit(op: Int, i: Long = 0L, f: Double = 0.0): Unit = { ops += op; iargs += i; fargs += f }
+
+    def col(name: String): Unit = emit(Col, names.getOrElseUpdate(name, names.size).toLong)
+
+    def lit(v: CypherValue): Unit = v match {
+      case CypherNull => emit(LitNull, Native.TypeNull)
+      case CypherBoolean(b) => emit(LitBool, if (b) 1L else 0L)
+      case CypherInteger(i) => emit(LitInt, i)
+      case CypherFloat(d) => emit(LitFloat, 0L, d)
+      case CypherString(s) => emit(LitString, session.intern(s))
+      case other => throw NotImplementedException(s"GPU literal $other")
+    }
+
+    def physical(e: Expr): Option[String] =
+      if (header.contains(e)) Some(header.column(e)).filter(columns.contains) else None
+
+    def go(e: Expr): Unit = e match {
+      case _: Var | _: HasLabel | _: HasType | _: StartNode | _: EndNode | _: ElementProperty =>
+        physical(e) match {
+          case Some(c) => col(c)
+          case None => emit(LitNull, GpuTypes.fromCypher(e.cypherType))   // FlinkSQLExprMapper.scala:60-73
+        }
+      case _ if physical(e).isDefined => col(physical(e).get)                // already projected (alias)
+      case IntegerLit(v) => emit(LitInt, v)
+      case FloatLit(v) => emit(LitFloat, 0L, v)
+      case TrueLit => emit(LitBool, 1L)
+      case FalseLit => emit(LitBool, 0L)
+      case StringLit(v) => emit(LitString, session.intern(v))
+      case NullLit(t) => emit(LitNull, GpuTypes.fromCypher(t))
+      case Param(name) => lit(parameters(name))
+      case Equals(l, r) => go(l); go(r); emit(Eq)
+      case Not(Equals(l, r)) => go(l); go(r); emit(Neq)
+      case LessThan(l, r) => go(l); go(r); emit(Lt)
+      case LessThanOrEqual(l, r) => go(l); go(r); emit(Le)
+      case GreaterThan(l, r) => go(l); go(r); emit(Gt)
+      case GreaterThanOrEqual(l, r) => go(l); go(r); emit(Ge)
+      case Not(x) => go(x); emit(Not_)
+      case Ands(xs) if xs.isEmpty => emit(LitBool, 1L)
+      case Ands(xs) => xs.foreach(go); emit(And, xs.size.toLong)
+      case Ors(xs) if xs.isEmpty => emit(LitBool, 0L)
+      case Ors(xs) => xs.foreach(go); emit(Or, xs.size.toLong)
+      case IsNull(x) => go(x); emit(IsNull_)
+      case IsNotNull(x) => go(x); emit(IsNotNull_)
+      case Add(l, r) => go(l); go(r); emit(Add_)
+      case Subtract(l, r) => go(l); go(r); emit(Sub)
+      case Multiply(l, r) => go(l); go(r); emit(Mul)
+      case Divide(l, r) => go(l); go(r); emit(Div)
+      case Modulo(l, r) => go(l); go(r); emit(Mod)
+      case ToFloat(x) => go(x); emit(ToFloat_)
+      case ToInteger(x) => go(x); emit(ToInteger_)                          // Flink: INT (FlinkSQLExprMapper.scala:183)
+      case Coalesce(xs) => xs.foreach(go); emit(Coalesce_, xs.size.toLong)
+      case other =>
+        throw NotImplementedException(s"No support for converting Cypher expression $other to a GPU expression")
+    }
+
+    go(expr)
+    new Program(ops.toArray, iargs.toArray, fargs.toArray, names.keys.toArray)
+  }
+
+  /** (CAPF_AGG_* kind, argument program, distinct) — the aggregators of
+    * FlinkSQLExprMapper.scala:281-287 (Expr.scala:1031-1140). */
+  def aggregator(agg: Aggregator, header: RecordHeader, table: GpuTable, parameters: CypherMap): (Int, Program, Boolean) =
+    agg match {
+      case CountStar(_) => (Native.AggCountStar, Program.empty, false)
+      case Count(e, distinct) => (Native.AggCount, program(e, header, table, parameters), distinct)
+      case Sum(e) => (Native.AggSum, program(e, header, table, parameters), false)
+      case Min(e) => (Native.AggMin, program(e, header, table, parameters), false)
+      case Max(e) => (Native.AggMax, program(e, header, table, parameters), false)
+      case Avg(e) => (Native.AggAvg, program(e, header, table, parameters), false)
+      case other => throw NotImplementedException(s"GPU aggregator $other")
+    }
+}

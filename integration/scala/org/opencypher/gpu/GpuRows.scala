@@ -1,0 +1,68 @@
+/*
+ * GpuRows.scala — CypherTable.rows (CypherTable.scala:63) over downloaded
+ * columns: one capf_table_download per column into direct buffers, then rows as
+ * `String => CypherValue`, the shape CAPFRecords' materialisation consumes
+ * (flink-cypher/.../impl/CAPFRecords.scala:142-144, rowToCypherMap.scala:40-131).
+ * Also GpuCypherSession, the RelationalCypherSession[GpuTable] backend state
+ * (CAPFSession.scala:47-91): one capf_session, the string dictionary, and the
+ * records / element-table factories.
+ */
+package org.opencypher.gpu
+
+import java.nio.{ByteBuffer, ByteOrder}
+
+import org.opencypher.okapi.api.value.CypherValue._
+
+object GpuRows {
+  def download(t: GpuTable): Iterator[String => CypherValue] = {
+    val n = t.size
+    require(n <= Int.MaxValue / 8, s"rows: $n rows do not fit one host buffer")
+    val cols = t.physicalColumns
+    val data: Map[String, Int => CypherValue] = cols.map { c =>
+      val ty = Native.guard(Native.tableColumnType(t.handle, c))
+      val width = if (ty == Native.TypeBool) 1 else 8
+      val values = ByteBuffer.allocateDirect(math.max(1, (n * width).toInt)).order(ByteOrder.nativeOrder())
+      val valid = ByteBuffer.allocateDirect(math.max(1, n.toInt))
+      if (ty != Native.TypeNull) Native.guard(Native.tableDownload(t.handle, c, values, valid))
+      val get: Int => CypherValue = ty match {
+        case Native.TypeNull => _ => CypherNull
+        case Native.TypeInt64 => i => if (valid.get(i) == 0) CypherNull else CypherInteger(values.getLong(8 * i))
+        case Native.TypeFloat64 => i => if (valid.get(i) == 0) CypherNull else CypherFloat(values.getDouble(8 * i))
+        case Native.TypeBool => i => if (valid.get(i) == 0) CypherNull else CypherBoolean(values.get(i) != 0)
+        case Native.TypeString => i =>
+          if (valid.get(i) == 0) CypherNull
+          else CypherString(Native.guard(Native.stringLookup(t.session.handle, values.getLong(8 * i))))
+      }
+      c -> get
+    }.toMap
+    Iterator.range(0, n.toInt).map(i => (c: String) => data(c)(i))
+  }
+}
+
+/** Backend state of one RelationalCypherSession[GpuTable] (one per GPU / JVM). */
+final class GpuCypherSession(device: Int = 0, hipStream: Long = 0L) extends AutoCloseable {
+  private[gpu] val handle: Long = Native.guard(Native.sessionCreate(device, hipStream))
+  private val strings = scala.collection.mutable.HashMap.empty[String, Long]
+
+  def intern(s: String): Long = strings.getOrElseUpdate(s, Native.guard(Native.stringIntern(handle, s)))
+
+  /** RelationalCypherRecordsFactory.unit / empty (RelationalCypherRecords.scala:43-54). */
+  def unit(): GpuTable = GpuTable(Native.guard(Native.tableUnit(handle)))(this)
+
+  def empty(columns: Seq[(String, Int)]): GpuTable =
+    GpuTable(Native.guard(Native.tableEmpty(handle, columns.map(_._1).toArray, columns.map(_._2).toArray)))(this)
+
+  /** CAPFElementTable.create / records from host columns (CAPFTable.scala:76-83): direct
+    * buffers of 8 B (INT64 / FLOAT64 / STRING codes) or 1 B (BOOL) per row. */
+  def fromHost(columns: Seq[(String, Int, ByteBuffer, ByteBuffer)], nrows: Long): GpuTable =
+    GpuTable(Native.guard(Native.tableFromHost(handle, columns.map(_._1).toArray, columns.map(_._2).toArray,
+      columns.map(_._3).toArray, columns.map(_._4).toArray, nrows)))(this)
+
+  /** GpuEdgeListDataSource.graph (EdgeListDataSource.scala:56-92): parsed natively. */
+  def edgeList(path: String, sep: String = " ", comment: String = "#"): GpuTable =
+    GpuTable(Native.guard(Native.edgeListRead(handle, path, sep, comment, "id", "source", "target")))(this)
+
+  def sync(): Unit = Native.guard(Native.sessionSync(handle))
+
+  override def close(): Unit = Native.guard(Native.sessionDestroy(handle))
+}

@@ -96,6 +96,8 @@ _SIGS = {
     "capf_table_size": (c_int32, [_T, POINTER(c_int64)]),
     "capf_table_count_async": (c_int32, [_T, c_void_p]),
     "capf_table_download": (c_int32, [_T, c_char_p, c_void_p, c_void_p]),
+    "capf_table_list_info": (c_int32, [_T, c_char_p, POINTER(c_int32), POINTER(c_int64)]),
+    "capf_table_download_list": (c_int32, [_T, c_char_p, c_void_p, c_void_p, c_void_p]),
     "capf_table_device_column": (c_int32, [_T, c_char_p, POINTER(c_void_p), POINTER(c_void_p),
                                            POINTER(c_int64)]),
     "capf_table_cache": (c_int32, [_T, _PT]),

@@ -54,7 +54,8 @@ enum class Type : int32_t {
   Int64 = CAPF_TYPE_INT64,
   Float64 = CAPF_TYPE_FLOAT64,
   Bool = CAPF_TYPE_BOOL,
-  String = CAPF_TYPE_STRING
+  String = CAPF_TYPE_STRING,
+  List = CAPF_TYPE_LIST  // data = int64 offsets [n + 1], child = the elements
 };
 inline size_t type_width(Type t) { return t == Type::Bool ? 1 : (t == Type::Null ? 0 : 8); }
 const char *type_name(Type t);
@@ -116,6 +117,8 @@ struct Column {
   // values of a tiny host-born column (a fused scalar result), kept beside
   // the device copy so `rows` needs no device round trip
   std::vector<int64_t> host_i64;
+  // Type::List: the element column (never lazy, no NULL elements)
+  std::shared_ptr<Column> child;
   bool is_all_null() const { return type == Type::Null; }
 };
 using ColPtr = std::shared_ptr<Column>;
@@ -358,6 +361,11 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
 // Aggregations over a grouping.
 ColPtr aggregate(Session *s, const Grouping &g, const Data &d, int64_t nrows, int32_t kind,
                  const ColPtr &arg, Type out_type);
+// collect(arg) per group (lists.hip): a Type::List column of g.ngroups lists.
+ColPtr collect_lists(Session *s, const Grouping &g, int64_t nrows, const ColPtr &arg,
+                     bool distinct);
+// Rows d_idx (-1 = NULL list) of a Type::List column.
+ColPtr gather_list(Session *s, const ColPtr &c, const int64_t *d_idx, int64_t m);
 // Sort permutation (stable) by key columns.
 BufPtr sort_permutation(Session *s, const std::vector<ColPtr> &keys,
                         const std::vector<int32_t> &desc, int64_t n);

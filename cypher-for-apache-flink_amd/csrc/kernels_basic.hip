@@ -221,7 +221,7 @@ void force(const ColPtr &c) {
 
 ColPtr gather_lazy(Session *s, const ColPtr &c, const BufPtr &idx, int64_t m, bool nullable,
                    IdxCache *cache) {
-  if (!idx || !lazy_enabled() || c->type == Type::Null || m == 0)
+  if (!idx || !lazy_enabled() || c->type == Type::Null || c->type == Type::List || m == 0)
     return gather_column(s, c, idx ? (const int64_t *)idx->p : nullptr, m, nullable);
   ColPtr src = c;
   BufPtr id = idx;
@@ -262,6 +262,7 @@ ColPtr gather_column(Session *s, const ColPtr &c, const int64_t *d_idx, int64_t 
     illegal("internal: identity gather with mismatched length");
   }
   if (c->type == Type::Null) return null_column(s, Type::Null, m);
+  if (c->type == Type::List) return gather_list(s, c, d_idx, m);
   if (!c->data || c->n == 0) {
     // empty source (outer join against an empty side): every index is the
     // null index, so the result is all NULL of the column's type
@@ -327,6 +328,7 @@ __global__ void k_copy_part_int(ColView src, int64_t *dst, uint8_t *dval, int64_
 }
 
 ColPtr concat_columns(Session *s, const ColPtr &a, const ColPtr &b, Type t) {
+  if (t == Type::List) not_impl("unionAll of list columns");
   force(a);
   force(b);
   int64_t m = a->n + b->n;

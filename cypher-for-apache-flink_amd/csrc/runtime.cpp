@@ -27,6 +27,7 @@ const char *type_name(Type t) {
     case Type::Float64: return "FLOAT";
     case Type::Bool: return "BOOLEAN";
     case Type::String: return "STRING";
+    case Type::List: return "LIST";
   }
   return "?";
 }
@@ -205,6 +206,7 @@ static bool is_numeric(Type t) { return t == Type::Int64 || t == Type::Float64; 
 Type infer_type(const Program &p, const std::vector<std::string> &names,
                 const std::vector<Type> &types) {
   std::vector<Type> st;
+  bool list_ref = false;
   auto pop = [&]() {
     if (st.empty()) illegal("malformed expression program (stack underflow)");
     Type t = st.back();
@@ -219,6 +221,7 @@ Type infer_type(const Program &p, const std::vector<std::string> &names,
         for (size_t k = 0; k < names.size(); ++k)
           if (names[k] == nm) idx = (int)k;
         if (idx < 0) illegal("expression references unknown column '" + nm + "'");
+        list_ref |= types[idx] == Type::List;
         st.push_back(types[idx]);
         break;
       }
@@ -304,6 +307,8 @@ Type infer_type(const Program &p, const std::vector<std::string> &names,
     }
   }
   if (st.size() != 1) illegal("malformed expression program (stack not singular)");
+  // a list column can be projected (a bare reference), not computed on
+  if (list_ref && p.code.size() != 1) not_impl("expressions over list values");
   return st.back();
 }
 
@@ -326,6 +331,10 @@ ColPtr null_column(Session *s, Type t, int64_t n) {
 }
 
 ColView view_of(const ColPtr &c) {
+  // LIST columns (collect results) are projected, gathered and downloaded,
+  // never read by a row kernel: keys, predicates and sort items over lists
+  // are not supported (Flink: no comparison on MULTISET either)
+  if (c->type == Type::List) not_impl("list values as keys, predicates or sort items");
   force(c);
   ColView v;
   v.data = c->data ? c->data->p : nullptr;
@@ -337,6 +346,7 @@ ColView view_of(const ColPtr &c) {
 }
 
 const ColStats &column_stats(Session *s, const ColPtr &c) {
+  if (c->type == Type::List) not_impl("statistics of a list column");
   force(c);
   std::lock_guard<std::mutex> g(c->mu);
   if (!c->stats) c->stats = compute_stats(s, *c);
@@ -447,6 +457,10 @@ static DataPtr materialize_impl(const NodePtr &n) {
         if (a.kind != CAPF_AGG_COUNT_STAR) {
           Type at = infer_type(a.arg, n->kids[0]->names, n->kids[0]->types);
           arg = eval_program(s, a.arg, n->kids[0]->names, *c, at);
+        }
+        if (a.kind == CAPF_AGG_COLLECT) {
+          out->cols.push_back(collect_lists(s, g, c->nrows, arg, a.distinct));
+          continue;
         }
         if (a.distinct && a.kind == CAPF_AGG_COUNT && c->nrows > 0) {
           // count(DISTINCT e): Spark semantics (SparkSQLExprMapper.scala:427-429);
@@ -977,6 +991,8 @@ capf_status capf_table_download(capf_table *t, const char *col, void *values_out
     if (valid_out) memset(valid_out, 1, d->nrows);
     return CAPF_OK;
   }
+  if (d->cols[i]->type == Type::List)
+    illegal("column '" + std::string(col) + "' is a LIST: use capf_table_download_list");
   const ColPtr c = decode_column(s, d->cols[i]);
   size_t w = type_width(c->type);
   if (d->nrows > 0) {
@@ -992,6 +1008,57 @@ capf_status capf_table_download(capf_table *t, const char *col, void *values_out
     }
     s->sync();
   }
+  CAPF_API_END
+}
+
+capf_status capf_table_list_info(capf_table *t, const char *col, int32_t *elem_type,
+                                 int64_t *n_values) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(col, "col");
+  int i = t->node->col_index_or_throw(col);
+  if (t->node->types[i] != Type::List) illegal("column '" + std::string(col) + "' is not a LIST");
+  DataPtr d = materialize(t->node);
+  const ColPtr &c = d->cols[i];
+  Session *s = t->node->s;
+  int64_t total = 0;
+  if (c->n > 0) {
+    HIP_CHECK(hipMemcpyAsync(&total, (const int64_t *)c->data->p + c->n, 8, hipMemcpyDeviceToHost,
+                             s->stream));
+    s->sync();
+  }
+  if (elem_type) *elem_type = (int32_t)c->child->type;
+  if (n_values) *n_values = total;
+  CAPF_API_END
+}
+
+capf_status capf_table_download_list(capf_table *t, const char *col, int64_t *offsets_out,
+                                     void *values_out, uint8_t *valid_out) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(col, "col");
+  int i = t->node->col_index_or_throw(col);
+  if (t->node->types[i] != Type::List) illegal("column '" + std::string(col) + "' is not a LIST");
+  DataPtr d = materialize(t->node);
+  const ColPtr &c = d->cols[i];
+  Session *s = t->node->s;
+  const int64_t n = c->n;
+  int64_t total = 0;
+  HIP_CHECK(hipMemcpyAsync(&total, (const int64_t *)c->data->p + n, 8, hipMemcpyDeviceToHost,
+                           s->stream));
+  s->sync();
+  if (offsets_out)
+    HIP_CHECK(hipMemcpyAsync(offsets_out, c->data->p, 8 * (n + 1), hipMemcpyDeviceToHost, s->stream));
+  if (values_out && total > 0 && c->child->type != Type::Null)
+    HIP_CHECK(hipMemcpyAsync(values_out, c->child->data->p, type_width(c->child->type) * total,
+                             hipMemcpyDeviceToHost, s->stream));
+  if (valid_out && n > 0) {
+    if (c->valid)
+      HIP_CHECK(hipMemcpyAsync(valid_out, c->valid->p, n, hipMemcpyDeviceToHost, s->stream));
+    else
+      memset(valid_out, 1, n);
+  }
+  s->sync();
   CAPF_API_END
 }
 
@@ -1148,6 +1215,7 @@ capf_status capf_table_union_all(capf_table *l, capf_table *r, capf_table **out)
     if (x != y && x != Type::Null && y != Type::Null)
       illegal(std::string("Equal column types for union all: ") + a->names[i] + " " +
               type_name(x) + " vs " + type_name(y));
+    if (x == Type::List || y == Type::List) not_impl("unionAll of list columns");
     nn->types.push_back(x == Type::Null ? y : x);
   }
   *out = wrap(nn);
@@ -1243,14 +1311,15 @@ capf_status capf_table_group(capf_table *t, int32_t n_by, const char *const *by_
     a.kind = agg_kinds[i];
     a.distinct = agg_distinct && agg_distinct[i];
     a.name = agg_names[i];
-    if (a.kind < CAPF_AGG_COUNT_STAR || a.kind > CAPF_AGG_AVG) illegal("bad aggregator kind");
+    if (a.kind < CAPF_AGG_COUNT_STAR || a.kind > CAPF_AGG_COLLECT) illegal("bad aggregator kind");
     if (a.kind == CAPF_AGG_COUNT_STAR) {
       a.out_type = Type::Int64;
     } else {
       a.arg = Program::from_c(&agg_args[i]);
       Type at = infer_type(a.arg, c->names, c->types);
-      if (a.distinct && a.kind != CAPF_AGG_COUNT)
-        not_impl("DISTINCT modifier on aggregator other than count");
+      if (a.distinct && a.kind != CAPF_AGG_COUNT && a.kind != CAPF_AGG_COLLECT)
+        not_impl("DISTINCT modifier on aggregator other than count / collect");
+      if (at == Type::List) not_impl("aggregation of list values");
       switch (a.kind) {
         case CAPF_AGG_COUNT: a.out_type = Type::Int64; break;
         case CAPF_AGG_SUM:
@@ -1265,6 +1334,7 @@ capf_status capf_table_group(capf_table *t, int32_t n_by, const char *const *by_
           if (at == Type::String) not_impl("min/max of strings");
           a.out_type = at;
           break;
+        case CAPF_AGG_COLLECT: a.out_type = Type::List; break;
       }
     }
     nn->names.push_back(a.name);
@@ -1320,6 +1390,13 @@ capf_status capf_table_show(capf_table *t, int32_t rows) {
       std::fill(valid[i].begin(), valid[i].end(), 0);
       continue;
     }
+    if (c->type == Type::List) {  // shown as its length
+      std::vector<int64_t> off(m + 1);
+      HIP_CHECK(hipMemcpy(off.data(), c->data->p, 8 * (m + 1), hipMemcpyDeviceToHost));
+      for (int64_t r = 0; r < m; ++r) vals[i][r] = off[r + 1] - off[r];
+      if (c->valid) HIP_CHECK(hipMemcpy(valid[i].data(), c->valid->p, m, hipMemcpyDeviceToHost));
+      continue;
+    }
     std::vector<uint8_t> raw(type_width(c->type) * m);
     HIP_CHECK(hipMemcpy(raw.data(), c->data->p, raw.size(), hipMemcpyDeviceToHost));
     for (int64_t r = 0; r < m; ++r)
@@ -1340,6 +1417,8 @@ capf_status capf_table_show(capf_table *t, int32_t rows) {
         printf("%g", f);
       } else if (ty == Type::Bool) {
         printf("%s", vals[i][r] ? "true" : "false");
+      } else if (ty == Type::List) {
+        printf("[%lld values]", (long long)vals[i][r]);
       } else if (ty == Type::String) {
         std::lock_guard<std::mutex> g(s->str_mu);
         printf("'%s'", vals[i][r] >= 0 && vals[i][r] < (int64_t)s->strings.size()

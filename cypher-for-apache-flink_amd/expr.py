@@ -18,13 +18,14 @@ from dataclasses import dataclass, field
 from typing import Tuple
 
 # capf column types (include/capf_gpu.h)
-T_NULL, T_INT, T_FLOAT, T_BOOL, T_STRING = 0, 1, 2, 3, 4
+T_NULL, T_INT, T_FLOAT, T_BOOL, T_STRING, T_LIST = 0, 1, 2, 3, 4, 5
 
 CT_TO_CAPF = {
     "NULL": T_NULL, "INTEGER": T_INT, "FLOAT": T_FLOAT, "BOOLEAN": T_BOOL, "STRING": T_STRING,
     "NODE": T_INT, "RELATIONSHIP": T_INT, "ANY": T_NULL,
 }
-CAPF_TO_CT = {T_NULL: "NULL", T_INT: "INTEGER", T_FLOAT: "FLOAT", T_BOOL: "BOOLEAN", T_STRING: "STRING"}
+CAPF_TO_CT = {T_NULL: "NULL", T_INT: "INTEGER", T_FLOAT: "FLOAT", T_BOOL: "BOOLEAN", T_STRING: "STRING",
+              T_LIST: "LIST"}
 
 # opcodes
 OP_COL, OP_LIT_INT, OP_LIT_FLOAT, OP_LIT_BOOL, OP_LIT_STRING, OP_LIT_NULL = 1, 2, 3, 4, 5, 6
@@ -34,7 +35,7 @@ OP_ADD, OP_SUB, OP_MUL, OP_DIV, OP_MOD, OP_NEG = 30, 31, 32, 33, 34, 35
 OP_TO_FLOAT, OP_TO_INTEGER, OP_COALESCE = 40, 41, 50
 
 # aggregators
-AGG_COUNT_STAR, AGG_COUNT, AGG_SUM, AGG_MIN, AGG_MAX, AGG_AVG = 0, 1, 2, 3, 4, 5
+AGG_COUNT_STAR, AGG_COUNT, AGG_SUM, AGG_MIN, AGG_MAX, AGG_AVG, AGG_COLLECT = 0, 1, 2, 3, 4, 5, 6
 
 
 class Expr:
@@ -418,3 +419,54 @@ def compile_program(expr, header, columns, params=None, intern=None):
 
     go(expr)
     return ops, ia, fa, names
+
+
+@dataclass(frozen=True)
+class Collect(Aggregator):
+    """collect(e) / collect(DISTINCT e) (okapi Expr.scala Collect; Flink
+    child0.collect, FlinkSQLExprMapper.scala:283): the non-NULL values of the
+    group as a list.  Flink's COLLECT is a MULTISET, so element order is not
+    part of the result (tests compare lists as bags)."""
+    expr: Expr
+    distinct: bool = False
+    kind = AGG_COLLECT
+
+    def __str__(self):
+        return f"collect({'DISTINCT ' if self.distinct else ''}{self.expr})"
+
+
+# Aggregators of the okapi IR that the Flink backend does not map
+# (FlinkSQLExprMapper.scala:281-290 has no case for them): planning them raises
+# NotImplementedException, as the reference does.
+@dataclass(frozen=True)
+class StDev(Aggregator):
+    expr: Expr
+
+    def __str__(self):
+        return f"stDev({self.expr})"
+
+
+@dataclass(frozen=True)
+class StDevP(Aggregator):
+    expr: Expr
+
+    def __str__(self):
+        return f"stDevP({self.expr})"
+
+
+@dataclass(frozen=True)
+class PercentileCont(Aggregator):
+    expr: Expr
+    percentile: float
+
+    def __str__(self):
+        return f"percentileCont({self.expr}, {self.percentile})"
+
+
+@dataclass(frozen=True)
+class PercentileDisc(Aggregator):
+    expr: Expr
+    percentile: float
+
+    def __str__(self):
+        return f"percentileDisc({self.expr}, {self.percentile})"

@@ -17,7 +17,7 @@ from ctypes import byref, c_char_p, c_double, c_int32, c_int64, c_uint64, c_void
 import numpy as np
 
 from . import _lib
-from .expr import (AGG_COUNT_STAR, CAPF_TO_CT, T_BOOL, T_FLOAT, T_INT, T_NULL, T_STRING, Aggregator,
+from .expr import (AGG_COUNT_STAR, CAPF_TO_CT, T_BOOL, T_FLOAT, T_INT, T_LIST, T_NULL, T_STRING, Aggregator,
                    compile_program)
 
 JOIN_TYPES = {"inner": 0, "left_outer": 1, "right_outer": 2, "full_outer": 3, "cross": 4}
@@ -258,9 +258,35 @@ class GpuTable:
                   valid.ctypes.data if n else None)
         return vals, valid.astype(bool)
 
+    def list_values(self, col):
+        """Python lists (None for a NULL list) of a LIST column (collect)."""
+        et, nv = c_int32(), c_int64()
+        _lib.call("capf_table_list_info", self._h, col.encode(), byref(et), byref(nv))
+        n = self.size
+        offs = np.zeros(n + 1, dtype=np.int64)
+        valid = np.zeros(max(n, 1), dtype=np.uint8)
+        t = et.value
+        vals = np.zeros(max(nv.value, 1), dtype=_NP_DTYPE.get(t, np.int64))
+        _lib.call("capf_table_download_list", self._h, col.encode(), offs.ctypes.data,
+                  vals.ctypes.data if nv.value and t != T_NULL else None, valid.ctypes.data if n else None)
+        out = []
+        for i in range(n):
+            if not valid[i]:
+                out.append(None)
+                continue
+            xs = vals[offs[i]:offs[i + 1]].tolist()
+            if t == T_STRING:
+                xs = [self.session.lookup(x) for x in xs]
+            elif t == T_BOOL:
+                xs = [bool(x) for x in xs]
+            out.append(xs)
+        return out
+
     def column_values(self, col):
         """Python values (None for NULL) of one column."""
         t = self.capf_type(col)
+        if t == T_LIST:
+            return self.list_values(col)
         vals, valid = self.column_arrays(col)
         out = []
         for v, ok in zip(vals.tolist(), valid.tolist()):
@@ -355,6 +381,9 @@ class GpuTable:
             agg = aggregations[name]
             if not isinstance(agg, Aggregator):
                 raise _lib.IllegalArgumentException(f"{agg} is not an aggregator")
+            if agg.kind < 0:  # FlinkSQLExprMapper.scala:289-290
+                raise _lib.NotImplementedException(
+                    f"No support for converting Cypher expression {agg} to a GPU expression")
             kinds.append(agg.kind)
             dist.append(1 if getattr(agg, "distinct", False) else 0)
             progs.append(None if agg.kind == AGG_COUNT_STAR else _program(agg.expr, header, self, params))

@@ -70,7 +70,8 @@ enum {
   CAPF_TYPE_INT64 = 1,   /* CTInteger, CTNode/CTRelationship/CTIdentity ids (Types.LONG) */
   CAPF_TYPE_FLOAT64 = 2, /* CTFloat (Types.DOUBLE) */
   CAPF_TYPE_BOOL = 3,    /* CTBoolean, HasLabel / HasType columns */
-  CAPF_TYPE_STRING = 4   /* CTString, stored as int64 dictionary codes */
+  CAPF_TYPE_STRING = 4,  /* CTString, stored as int64 dictionary codes */
+  CAPF_TYPE_LIST = 5     /* CTList(elem): the result of collect (see capf_table_list_info) */
 };
 
 /* join types (okapi-relational/.../impl/planning/PhysicalConstants.scala:29-35) */
@@ -90,7 +91,13 @@ enum {
   CAPF_AGG_SUM = 2,
   CAPF_AGG_MIN = 3,
   CAPF_AGG_MAX = 4,
-  CAPF_AGG_AVG = 5
+  CAPF_AGG_AVG = 5,
+  /* Collect (Expr.scala Collect; Flink child0.collect, FlinkSQLExprMapper.scala:283):
+   * the non-NULL values of each group as a LIST column (empty list for none);
+   * agg_distinct drops duplicate values.  Flink's COLLECT is a MULTISET: the
+   * element order is not part of the result (here: ascending values, string
+   * elements in dictionary-code order). */
+  CAPF_AGG_COLLECT = 6
 };
 
 /*
@@ -209,6 +216,16 @@ capf_status capf_table_count_async(capf_table *t, int64_t *d_count);
  * size × (8 or 1) bytes, valid_out (may be NULL) size bytes.              */
 capf_status capf_table_download(capf_table *t, const char *col, void *values_out,
                                 uint8_t *valid_out);
+/* LIST columns (CAPF_TYPE_LIST, from CAPF_AGG_COLLECT).  capf_table_list_info:
+ * the element type (CAPF_TYPE_*) and the total element count of column col.
+ * capf_table_download_list: offsets_out[size + 1] (int64, list i = elements
+ * [offsets[i], offsets[i+1])), values_out[n_values] elements (8 or 1 bytes
+ * each, never NULL), valid_out[size] list validity (may be NULL).
+ * capf_table_download of a LIST column is CAPF_ERR_ILLEGAL_ARGUMENT.        */
+capf_status capf_table_list_info(capf_table *t, const char *col, int32_t *elem_type,
+                                 int64_t *n_values);
+capf_status capf_table_download_list(capf_table *t, const char *col, int64_t *offsets_out,
+                                     void *values_out, uint8_t *valid_out);
 /* Device view of a materialised column (for zero-copy interop). */
 capf_status capf_table_device_column(capf_table *t, const char *col, void **values,
                                      uint8_t **valid, int64_t *nrows);

@@ -333,6 +333,22 @@ JNI(void, tableDownload)(JNIEnv *env, jobject, jlong t, jstring col, jobject val
   JStr c(env, col);
   fail(env, capf_table_download(T(t), c.p, direct(env, values), (uint8_t *)direct(env, valid)));
 }
+// LIST columns (collect): returns the element type; element count → nValuesOut[0]
+JNI(jint, tableListInfo)(JNIEnv *env, jobject, jlong t, jstring col, jlongArray nValuesOut) {
+  JStr c(env, col);
+  int32_t elem = 0;
+  int64_t nv = 0;
+  if (fail(env, capf_table_list_info(T(t), c.p, &elem, &nv))) return 0;
+  jlong v = nv;
+  env->SetLongArrayRegion(nValuesOut, 0, 1, &v);
+  return elem;
+}
+JNI(void, tableDownloadList)(JNIEnv *env, jobject, jlong t, jstring col, jobject offsets,
+                             jobject values, jobject valid) {
+  JStr c(env, col);
+  fail(env, capf_table_download_list(T(t), c.p, (int64_t *)direct(env, offsets), direct(env, values),
+                                     (uint8_t *)direct(env, valid)));
+}
 // device view: out = {values, valid, nrows}
 JNI(void, tableDeviceColumn)(JNIEnv *env, jobject, jlong t, jstring col, jlongArray out) {
   JStr c(env, col);

@@ -107,6 +107,7 @@ object GpuExprMapper {
       case Min(e) => (Native.AggMin, program(e, header, table, parameters), false)
       case Max(e) => (Native.AggMax, program(e, header, table, parameters), false)
       case Avg(e) => (Native.AggAvg, program(e, header, table, parameters), false)
+      case Collect(e, distinct) => (Native.AggCollect, program(e, header, table, parameters), distinct)
       case other => throw NotImplementedException(s"GPU aggregator $other")
     }
 }

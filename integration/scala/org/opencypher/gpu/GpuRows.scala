@@ -20,6 +20,7 @@ object GpuRows {
     val cols = t.physicalColumns
     val data: Map[String, Int => CypherValue] = cols.map { c =>
       val ty = Native.guard(Native.tableColumnType(t.handle, c))
+      if (ty == Native.TypeList) c -> lists(t, c, n) else {
       val width = if (ty == Native.TypeBool) 1 else 8
       val values = ByteBuffer.allocateDirect(math.max(1, (n * width).toInt)).order(ByteOrder.nativeOrder())
       val valid = ByteBuffer.allocateDirect(math.max(1, n.toInt))
@@ -34,8 +35,29 @@ object GpuRows {
           else CypherString(Native.guard(Native.stringLookup(t.session.handle, values.getLong(8 * i))))
       }
       c -> get
-    }.toMap
+    }}.toMap
     Iterator.range(0, n.toInt).map(i => (c: String) => data(c)(i))
+  }
+
+  /** A LIST column (collect): offsets + elements (capf_table_download_list). */
+  private def lists(t: GpuTable, c: String, n: Long): Int => CypherValue = {
+    val nv = Array(0L)
+    val elem = Native.guard(Native.tableListInfo(t.handle, c, nv))
+    val width = if (elem == Native.TypeBool) 1 else 8
+    val offsets = ByteBuffer.allocateDirect(8 * (n.toInt + 1)).order(ByteOrder.nativeOrder())
+    val values = ByteBuffer.allocateDirect(math.max(1, (nv(0) * width).toInt)).order(ByteOrder.nativeOrder())
+    val valid = ByteBuffer.allocateDirect(math.max(1, n.toInt))
+    Native.guard(Native.tableDownloadList(t.handle, c, offsets, values, valid))
+    def value(k: Int): CypherValue = elem match {
+      case Native.TypeInt64 => CypherInteger(values.getLong(8 * k))
+      case Native.TypeFloat64 => CypherFloat(values.getDouble(8 * k))
+      case Native.TypeBool => CypherBoolean(values.get(k) != 0)
+      case Native.TypeString => CypherString(Native.guard(Native.stringLookup(t.session.handle, values.getLong(8 * k))))
+      case _ => CypherNull
+    }
+    i =>
+      if (valid.get(i) == 0) CypherNull
+      else CypherList((offsets.getLong(8 * i).toInt until offsets.getLong(8 * (i + 1)).toInt).map(value): _*)
   }
 }
 

@@ -124,6 +124,7 @@ object GpuTypes {
     case Native.TypeBool => CTBoolean.nullable
     case Native.TypeString => CTString.nullable
     case Native.TypeNull => CTNull
+    case Native.TypeList => CTList(CTAny).nullable   // element type: Native.tableListInfo
     case other => throw IllegalArgumentException("a capf column type", other)
   }
 

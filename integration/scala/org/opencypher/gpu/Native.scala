@@ -38,6 +38,7 @@ object Native {
   final val TypeFloat64 = 2
   final val TypeBool = 3
   final val TypeString = 4
+  final val TypeList = 5
 
   final val JoinInner = 0
   final val JoinLeftOuter = 1
@@ -51,6 +52,7 @@ object Native {
   final val AggMin = 3
   final val AggMax = 4
   final val AggAvg = 5
+  final val AggCollect = 6
 
   /** Runs a native call, rethrowing its failure as the okapi exception of that kind
     * (okapi-api/.../impl/exception/InternalException.scala:36-65). */
@@ -100,6 +102,9 @@ object Native {
   @native def tableSize(table: Long): Long
   @native def tableCountAsync(table: Long, dCount: Long): Unit
   @native def tableDownload(table: Long, col: String, values: ByteBuffer, valid: ByteBuffer): Unit
+  @native def tableListInfo(table: Long, col: String, nValuesOut: Array[Long]): Int
+  @native def tableDownloadList(table: Long, col: String, offsets: ByteBuffer, values: ByteBuffer,
+                                valid: ByteBuffer): Unit
   @native def tableDeviceColumn(table: Long, col: String, out: Array[Long]): Unit
   @native def tableCompact(table: Long): Long
   @native def tableCompactWidth(table: Long, width: Int): Long

@@ -18,6 +18,9 @@ FlinkTable (flink-cypher/.../impl/table/FlinkTable.scala:49-199):
    per FlinkSQLExprMapper.scala:281-287 (count(*) counts rows; count(e)
    non-null; sum/min/max/avg ignore NULL and are NULL on no input; avg of an
    INTEGER column is an INTEGER, Java long division — Expr.scala:1058-1066);
+ * collect: the group's non-NULL values as a list (DISTINCT drops repeats);
+   Flink's COLLECT is a MULTISET (FlinkSQLExprMapper.scala:283), so the
+   element order is not part of the result;
  * orderBy: NULL sorts as the largest value;
  * withColumns: replace in place or append (FlinkTable.scala:86-98).
 
@@ -25,10 +28,10 @@ Everything materialises with numpy; sizes are the small parity cases.
 """
 import numpy as np
 
-from capf_amd.expr import (T_BOOL, T_FLOAT, T_INT, T_NULL, T_STRING, CAPF_TO_CT, CT_TO_CAPF, Aggregator,
-                           Ands, BoolLit, Coalesce, ElementProperty, EndNode, FloatLit, HasLabel, HasType,
-                           IntegerLit, NullLit, Ors, Param, StartNode, StringLit, Var, AGG_AVG, AGG_COUNT,
-                           AGG_COUNT_STAR, AGG_MAX, AGG_MIN, AGG_SUM)
+from capf_amd.expr import (T_BOOL, T_FLOAT, T_INT, T_LIST, T_NULL, T_STRING, CAPF_TO_CT, CT_TO_CAPF,
+                           Aggregator, Ands, BoolLit, Coalesce, ElementProperty, EndNode, FloatLit, HasLabel,
+                           HasType, IntegerLit, NullLit, Ors, Param, StartNode, StringLit, Var, AGG_AVG,
+                           AGG_COLLECT, AGG_COUNT, AGG_COUNT_STAR, AGG_MAX, AGG_MIN, AGG_SUM)
 
 
 class Col:
@@ -49,11 +52,12 @@ class Col:
         return Col(self.t, self.v[safe], np.where(neg, False, self.ok[safe]))
 
 
-_NP = {T_INT: np.int64, T_FLOAT: np.float64, T_BOOL: np.bool_, T_STRING: object, T_NULL: np.int64}
+_NP = {T_INT: np.int64, T_FLOAT: np.float64, T_BOOL: np.bool_, T_STRING: object, T_NULL: np.int64,
+       T_LIST: object}
 
 
 def _empty_vals(t, n):
-    if t == T_STRING:
+    if t in (T_STRING, T_LIST):
         return np.full(n, None, dtype=object)
     return np.zeros(n, dtype=_NP[t])
 
@@ -275,6 +279,8 @@ def _key_codes(cols, null_is_group=True):
     anynull = np.zeros(n, bool)
     for c in cols:
         anynull |= ~c.ok
+        if c.t == T_LIST:
+            raise NotImplementedError("list values as keys")
         if c.t == T_STRING:
             vals = np.array([v if ok else "" for v, ok in zip(c.v, c.ok)], dtype=object)
             _, inv = np.unique(vals.astype(str), return_inverse=True) if n else (None, np.zeros(0, np.int64))
@@ -337,6 +343,8 @@ class OracleTable:
                 out.append(int(v))
             elif c.t == T_FLOAT:
                 out.append(float(v))
+            elif c.t == T_LIST:
+                out.append(list(v))
             else:
                 out.append(v)
         return out
@@ -414,6 +422,8 @@ class OracleTable:
         cols = {}
         for c in self._order:
             a, b = self._cols[c], other._cols[c]
+            if T_LIST in (a.t, b.t):
+                raise NotImplementedError("unionAll of list columns")
             t = a.t if a.t != T_NULL else b.t
             if a.t != b.t and T_NULL not in (a.t, b.t):
                 raise ValueError(f"Equal column types for union all: {c}")
@@ -486,10 +496,30 @@ class OracleTable:
     def _aggregate(self, agg, gid, ng, header, params):
         if not isinstance(agg, Aggregator):
             raise TypeError(agg)
+        if agg.kind < 0:  # no case in FlinkSQLExprMapper.scala:281-290
+            raise NotImplementedError(f"No support for converting Cypher expression {agg}")
         if agg.kind == AGG_COUNT_STAR:
             return Col(T_INT, np.bincount(gid, minlength=ng).astype(np.int64), np.ones(ng, bool))
         v = evaluate(agg.expr, self, header, params)
         sel = v.ok
+        if v.t == T_LIST:
+            raise NotImplementedError("aggregation of list values")
+        if agg.kind == AGG_COLLECT:
+            lists = [[] for _ in range(ng)]
+            seen = [set() for _ in range(ng)]
+            for g, x, ok in zip(gid.tolist(), v.v.tolist(), sel.tolist()):
+                if not ok or v.t == T_NULL:
+                    continue
+                x = bool(x) if v.t == T_BOOL else x
+                if agg.distinct:
+                    if x in seen[g]:
+                        continue
+                    seen[g].add(x)
+                lists[g].append(x)
+            out = np.empty(ng, dtype=object)
+            for g in range(ng):
+                out[g] = sorted(lists[g])
+            return Col(T_LIST, out, np.ones(ng, bool))
         if agg.kind == AGG_COUNT:
             if agg.distinct:  # Spark semantics (Flink ignores DISTINCT)
                 seen = set()

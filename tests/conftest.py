@@ -31,8 +31,10 @@ def cypher_value_key(v):
     are compared at 12 significant digits: the north-star tolerance for
     floating-point aggregates (1e-12 relative) absorbs summation order.
     NaN equals NaN here (one canonical key); NULL is its own kind.  Lists
-    (collect) compare element-wise; nodes / relationships (dicts with
-    "_kind") by identity, labels/type and properties."""
+    (collect) compare as bags: Flink's COLLECT is a MULTISET
+    (FlinkSQLExprMapper.scala:283) and the reference tests compare collected
+    lists with .toBag; nodes / relationships by identity, labels/type and
+    properties."""
     if v is None:
         return ("null",)
     if isinstance(v, bool):
@@ -46,7 +48,7 @@ def cypher_value_key(v):
     if isinstance(v, str):
         return ("str", v)
     if isinstance(v, (list, tuple)):
-        return ("list", tuple(cypher_value_key(x) for x in v))
+        return ("list", tuple(sorted((cypher_value_key(x) for x in v), key=repr)))
     if isinstance(v, dict):
         return ("map", tuple(sorted((k, cypher_value_key(x)) for k, x in v.items())))
     if isinstance(v, (frozenset, set)):

@@ -11,7 +11,7 @@ Sources (relative to the reference checkout):
   MTa = morpheus-testing/src/test/scala/org/opencypher/morpheus/impl/acceptance/
 """
 import capf_import  # noqa: F401
-from capf_amd.expr import (Avg, Count, CountStar, ElementProperty, Max, Min, Sum, Var)
+from capf_amd.expr import (Avg, Collect, Count, CountStar, ElementProperty, Max, Min, Sum, Var)
 from capf_amd.planner import Match, NodeP, Query, RelP, Stage
 
 
@@ -586,3 +586,74 @@ AGG_WITH_CASES = [
      _in_with("res", Sum(P("n", "val"))), [{"res": None}]),
 ]
 CASES = CASES + AGG_WITH_CASES
+
+
+# ------------------------------ AggregationTests COLLECT / Combinations (FTt)
+# collect(e) is Flink's COLLECT, a MULTISET (FlinkSQLExprMapper.scala:283): the
+# reference compares the lists with .toBag, and so does conftest.bag.
+# Option "deviates": {field: value the reference test expects} marks the
+# avg-over-INTEGER fields: the reference expects a FLOAT (49.666…, 32.5) where
+# okapi types avg as its input type (Expr.scala:1058-1066) and Flink's AVG on
+# LONG divides as a long — the parity hazard recorded in SURVEY §8(c); the
+# expected rows here hold the INTEGER result (49, 32, 84) and
+# test_oracle_golden checks that only such fields deviate.
+
+
+def _agg_all():
+    return [("avg", Avg(P("n", "val"))), ("cnt", CountStar()), ("min", Min(P("n", "val"))),
+            ("max", Max(P("n", "val"))), ("sum", Sum(P("n", "val"))), ("col", Collect(P("n", "val")))]
+
+
+COMB_OUT = ["avg", "cnt", "min", "max", "sum", "col"]
+KEYED_INTS = "CREATE ({key: 'a', val: 42}),({key: 'a',val: 23}),({key: 'b', val: 84})"
+KEYED_FLOATS = "CREATE ({key: 'a', val: 42.0}),({key: 'a',val: 23.0}),({key: 'b', val: 84.0})"
+
+COLLECT_CASES = [
+    ("collect_ints_with", "FTt/acceptance/AggregationTests.scala:734-743", INTS,
+     _in_with("res", Collect(P("n", "val"))), [{"res": [2, 4, 6]}]),
+    ("collect_ints_return", "FTt/acceptance/AggregationTests.scala:745-753", INTS,
+     scan_n(ret(("res", Collect(P("n", "val"))))), [{"res": [2, 4, 6]}]),
+    ("collect_single_null_with", "FTt/acceptance/AggregationTests.scala:755-763", FLOATS_NULL,
+     _in_with("res", Collect(P("n", "val"))), [{"res": [23.0, 42.0]}]),
+    ("collect_single_null_return", "FTt/acceptance/AggregationTests.scala:765-773", FLOATS_NULL,
+     scan_n(ret(("res", Collect(P("n", "val"))))), [{"res": [23.0, 42.0]}]),
+    ("collect_only_nulls_with", "FTt/acceptance/AggregationTests.scala:775-783", NULLS,
+     _in_with("res", Collect(P("n", "val"))), [{"res": []}]),
+    ("collect_only_nulls_return", "FTt/acceptance/AggregationTests.scala:785-793", NULLS,
+     scan_n(ret(("res", Collect(P("n", "val"))))), [{"res": []}]),
+    ("collect_distinct_grouping", "FTt/acceptance/AggregationTests.scala:795-815",
+     "CREATE (a:Start{id: 1}) CREATE (a)-[:REL]->({val: \"foo\"}) CREATE (a)-[:REL]->({val: \"foo\"})",
+     Query([Match([NodeP("a", ("Start",)), NodeP("b")], [RelP("_r", "a", "b")])],
+           [ret(("a.id", P("a", "id")), ("val", Collect(P("b", "val"), distinct=True)))]),
+     [{"a.id": 1, "val": ["foo"]}]),
+    ("collect_absent_strings", "FTt/acceptance/AggregationTests.scala:817-831",
+     "CREATE (a:Person{id: 1, name:'Anna'}) CREATE (b:Person{id: 2, name:'Bob'}) "
+     "CREATE (p1:Purchase{id: 3}) CREATE (a)-[:BOUGHT]->(p1)",
+     Query([Match([NodeP("person", ("Person",)), NodeP("friend", ("Person",)), NodeP("customer", ("Customer",)),
+                   NodeP("product", ("Product",))],
+                  [RelP("_f", "person", "friend", ("FRIEND_OF",), "both"),
+                   RelP("_i", "friend", "customer", ("IS",)),
+                   RelP("_b", "customer", "product", ("BOUGHT",))])],
+           [ret(("for", P("person", "name")),
+                ("recommendations", Collect(P("product", "title"), distinct=True)))]),
+     [], {"row_count": 0}),
+    ("comb_with", "FTt/acceptance/AggregationTests.scala:835-857", INTS3,
+     scan_n(ret(*_agg_all()), ret(*[(a, Var(a)) for a in COMB_OUT])),
+     [{"avg": 49, "cnt": 3, "min": 23, "max": 84, "sum": 149, "col": [23, 42, 84]}],
+     {"deviates": {"avg": 49.666666666666664}}),
+    ("comb_return", "FTt/acceptance/AggregationTests.scala:859-880", INTS3,
+     scan_n(ret(*_agg_all())),
+     [{"avg": 49, "cnt": 3, "min": 23, "max": 84, "sum": 149, "col": [23, 42, 84]}],
+     {"deviates": {"avg": 49.666666666666664}}),
+    ("comb_grouping_return", "FTt/acceptance/AggregationTests.scala:882-901", KEYED_FLOATS,
+     scan_n(ret(("key", P("n", "key")), *_agg_all())),
+     [{"key": "b", "avg": 84.0, "cnt": 1, "min": 84.0, "max": 84.0, "sum": 84.0, "col": [84.0]},
+      {"key": "a", "avg": 32.5, "cnt": 2, "min": 23.0, "max": 42.0, "sum": 65.0, "col": [23.0, 42.0]}]),
+    ("comb_grouping_with", "FTt/acceptance/AggregationTests.scala:903-925", KEYED_INTS,
+     scan_n(ret(("key", P("n", "key")), *_agg_all()),
+            ret(*[(a, Var(a)) for a in ["key"] + COMB_OUT])),
+     [{"key": "a", "avg": 32, "cnt": 2, "min": 23, "max": 42, "sum": 65, "col": [23, 42]},
+      {"key": "b", "avg": 84, "cnt": 1, "min": 84, "max": 84, "sum": 84, "col": [84]}],
+     {"deviates": {"avg": "32.5 (key a), 84.0 (key b)"}}),
+]
+CASES = CASES + COLLECT_CASES

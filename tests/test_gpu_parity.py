@@ -609,3 +609,62 @@ def test_triangle_partials_sum(gpu_session, parts):
     gpu_session.sync()
     src, dst = cmodel.rmat(scale)
     assert int(d.sum().item()) == cmodel.count_triangle_formula(src, dst, 1 << scale)
+
+
+def _collect_graph(n=3000, seed=11):
+    """Nodes with an integer key (some NULL), a float and a string value
+    (some NULL) — collect / collect DISTINCT inputs with repeats."""
+    from capf_amd.graph import GraphData
+    rng = np.random.default_rng(seed)
+    g = GraphData()
+    for i in range(n):
+        props = {}
+        if rng.random() > 0.1:
+            props["key"] = int(rng.integers(0, 40))
+        if rng.random() > 0.2:
+            props["val"] = float(rng.integers(0, 25)) / 4.0
+        if rng.random() > 0.3:
+            props["s"] = "w%d" % rng.integers(0, 12)
+        g.nodes.append((i, frozenset(["N"]), props))
+    return g
+
+
+@pytest.mark.parametrize("distinct", [False, True])
+@pytest.mark.parametrize("what", ["val", "s", "key"])
+def test_collect_grouped_sorted_limited(gpu_session, distinct, what):
+    """collect over 40 groups (+ the NULL group), then ORDER BY key, SKIP and
+    LIMIT: the list column is gathered twice (sort permutation, slice) —
+    lists.hip gather_list — and must equal the oracle's lists as bags."""
+    from capf_amd.expr import Collect
+    P = lambda k: ElementProperty(Var("n", "NODE"), k)  # noqa: E731
+    q = Query([Match([NodeP("n")])],
+              [Stage([("key", P("key")), ("col", Collect(P(what), distinct=distinct)), ("c", CountStar())],
+                     order_by=[("key", "desc")], skip=3, limit=30)])
+    data = _collect_graph()
+    got = run(ScanGraph.from_data(gpu_session, data, compact=True), q)
+    want = run(ScanGraph.from_data(OracleSession(), data), q)
+    assert len(got) == 30
+    assert [bag([r]) for r in got] == [bag([r]) for r in want]
+    if distinct:
+        assert all(len(r["col"]) == len(set(r["col"])) for r in got)
+
+
+def test_collect_list_ops_fail_loudly(gpu_session):
+    """A list column can be projected, not keyed or compared: DISTINCT over it
+    is NotImplementedException (as a MULTISET key is in Flink)."""
+    from capf_amd.expr import Collect
+    P = lambda k: ElementProperty(Var("n", "NODE"), k)  # noqa: E731
+    q = Query([Match([NodeP("n")])], [Stage([("col", Collect(P("val")))], distinct=True)])
+    with pytest.raises(_lib.NotImplementedException):
+        run(ScanGraph.from_data(gpu_session, _collect_graph(200)), q)
+
+
+@pytest.mark.parametrize("agg", ["StDev", "PercentileDisc"])
+def test_unmapped_aggregators_raise_on_gpu(gpu_session, agg):
+    import capf_amd.expr as ex
+    cls = getattr(ex, agg)
+    P = ElementProperty(Var("n", "NODE"), "val")
+    a = cls(P) if agg == "StDev" else cls(P, 0.5)
+    q = Query([Match([NodeP("n")])], [Stage([("res", a)])])
+    with pytest.raises(_lib.NotImplementedException):
+        run(ScanGraph.from_data(gpu_session, parse_create("CREATE ({val: 1}), ({val: 2})")), q)

@@ -657,3 +657,26 @@ COLLECT_CASES = [
      {"deviates": {"avg": "32.5 (key a), 84.0 (key b)"}}),
 ]
 CASES = CASES + COLLECT_CASES
+
+# --------------------------------- ExpandIntoTests "Expand into after var expand"
+CASES.append(
+    ("expand_into_after_var_expand", "MTa/ExpandIntoTests.scala:109-145",
+     """CREATE (p1:Person {name: "Alice"})
+        CREATE (p2:Person {name: "Bob"})
+        CREATE (comment:Comment)
+        CREATE (post1:Post {content: "asdf"})
+        CREATE (post2:Post {content: "foobar"})
+        CREATE (p1)-[:KNOWS]->(p2)
+        CREATE (p2)<-[:HASCREATOR]-(comment)
+        CREATE (comment)-[:REPLYOF]->(post1)-[:REPLYOF]->(post2)
+        CREATE (post2)-[:HASCREATOR]->(p1)""",
+     Query([Match([NodeP("p1", ("Person",)), NodeP("p2", ("Person",)), NodeP("comment", ("Comment",)),
+                   NodeP("post", ("Post",))],
+                  [RelP("e1", "p1", "p2", ("KNOWS",)),
+                   RelP("e2", "comment", "p2", ("HASCREATOR",)),
+                   RelP("e3", "comment", "post", ("REPLYOF",), length=(1, 10)),
+                   RelP("_h", "post", "p1", ("HASCREATOR",))],
+                  where=[Equals(P("p1", "name"), StringLit("Alice"))])],
+           [ret(("p1.name", P("p1", "name")), ("p2.name", P("p2", "name")),
+                ("post.content", P("post", "content")))]),
+     [{"p1.name": "Alice", "p2.name": "Bob", "post.content": "foobar"}]))

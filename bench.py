@@ -151,6 +151,35 @@ def pipeline_roofline(prof, steps, compulsory_bytes, traffic_per_query=None):
     }
 
 
+def tri_roofline(prof, steps, n_nodes, traffic_per_query=None):
+    """Config 4: compulsory bytes are not meaningful — the work
+    is closing-edge probes.  Roofline of the dominant kernel tri_count over ITS
+    algorithmic bytes: 4 B per probe (the neighbour id w of N+(q), searched in
+    the LDS copy of N+(p)), 16 B per hit (the two multiplicity pairs), 20 B per
+    oriented edge (rowptr pair, multiplicity pair, staged column) and 8 B per
+    node row; probe / hit / edge counts come from the kernel's own counters
+    (profiled pass).  `traffic` = PMC bytes of tri_count (rocprofv3 FETCH×2 +
+    WRITE, profiles/pmc_tri_s<scale>.json) when collected."""
+    per = {k: v["total_ms"] / steps for k, v in prof.items() if k in PIPELINE}
+    probes = prof.get("tri_probes", {}).get("bytes", 0.0) / steps
+    hits = prof.get("tri_hits", {}).get("bytes", 0.0) / steps
+    edges = prof.get("tri_oriented_edges", {}).get("bytes", 0.0) / steps
+    t = per.get("tri_count", 0.0)
+    algo = 4.0 * probes + 16.0 * hits + 20.0 * edges + 8.0 * n_nodes
+    achieved = algo / (t * 1e-3) / 1e9 if t > 0 else None
+    return {
+        "bound": "hbm", "kernel": "tri_count (closing-edge probes)",
+        "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS if achieved else None,
+        "traffic": traffic_per_query, "algorithmic_bytes_per_launch": algo,
+        "probes_per_launch": probes, "hits_per_launch": hits, "oriented_edges": edges,
+        "probes_per_s": probes / (t * 1e-3) if t > 0 else None,
+        "kernel_ms": t, "pipeline_ms_per_query": sum(per.values()), "kernel_ms_per_query": per,
+        "note": "compulsory 16·M + 8·N bytes are not meaningful for config 4 (SURVEY §8(d)); "
+                "value is rows/s, the roofline is the count kernel's probe traffic",
+    }
+
+
 def id_width(args):
     """Ingest-time id encoding of the synthetic graph: False = plain int64,
     4 = FOR32, 3 = FOR24 (3-byte offsets + base where the range fits 24 bits,
@@ -289,13 +318,19 @@ def run_single(args):
     # src+dst at int64 width + node ids (+ the 1-B label for config 2)
     compulsory = 16.0 * m + (9.0 if args.query == "one_hop_person" else 8.0) * n_nodes
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", f"pmc_s{args.scale}.json")
-    if os.path.exists(pmc) and args.query == "two_hop":
+    pmc = os.path.join(ROOT, "profiles", f"pmc_{'tri_' if args.query == 'triangle' else ''}s{args.scale}.json")
+    if os.path.exists(pmc) and args.query in ("two_hop", "triangle"):
         with open(pmc) as f:
-            traffic = json.load(f).get("hbm_bytes_per_query")
+            j = json.load(f)
+            traffic = (j.get("hbm_bytes_per_query") if args.query == "two_hop" else
+                       next((v["read_bytes"] + v["write_bytes"] for k, v in j.get("kernels", {}).items()
+                             if k.startswith("k_tri_count")), None))
     ms_per_step = elapsed * 1e3 / args.steps
-    roof = pipeline_roofline(prof, prof_steps, compulsory, traffic)
-    roof["end_to_end_frac"] = compulsory / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS
+    if args.query == "triangle":
+        roof = tri_roofline(prof, prof_steps, n_nodes, traffic)
+    else:
+        roof = pipeline_roofline(prof, prof_steps, compulsory, traffic)
+        roof["end_to_end_frac"] = compulsory / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS
     result = {
         "metric": {"two_hop": METRIC, "triangle": TRI_METRIC, "one_hop_person": ONE_HOP_METRIC}[args.query],
         "value": count * args.steps / elapsed,

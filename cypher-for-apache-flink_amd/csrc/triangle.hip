@@ -222,7 +222,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count(const uint32_t *rowptr,
   const int wv = threadIdx.x / WAVE, lane = lane_id();
   uint32_t *sc = s_cols[wv];
   TriBatch &tb = s_tab[wv];
-  unsigned long long t = 0;
+  unsigned long long t = 0, probes = 0, hits = 0;
   for (;;) {
     unsigned long long r0 = 0;
     if (lane == 0) r0 = atomicAdd(cursor, 1ull);
@@ -237,10 +237,12 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count(const uint32_t *rowptr,
           const uint32_t q = cols[a + k];
           const uint32_t qa = rowptr[q], dq = rowptr[q + 1] - qa;
           const uint2 pq = vals[a + k];
+          if (lane == 0) probes += dq;
           for (uint32_t j = lane; j < dq; j += WAVE) {
             const uint32_t w = cols[qa + j];
             const int64_t i = tri_find([&](int64_t x) { return cols[a + x]; }, dp, w);
             if (i >= 0) {
+              ++hits;
               const uint2 qw = vals[qa + j], pw = vals[a + i];
               t += (unsigned long long)pq.x * qw.x * pw.y + (unsigned long long)pw.x * qw.y * pq.y;
             }
@@ -267,6 +269,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count(const uint32_t *rowptr,
         tb.qa[lane] = qa;
         tb.pq[lane] = pq;
         const uint32_t total = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl(inc, WAVE - 1, WAVE));
+        if (lane == 0) probes += total;
         __builtin_amdgcn_wave_barrier();
         for (uint32_t t0 = 0; t0 < total; t0 += TRI_ILP * WAVE) {
           uint32_t w[TRI_ILP], pos[TRI_ILP], bi[TRI_ILP];
@@ -286,6 +289,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count(const uint32_t *rowptr,
             if (w[u] == 0xFFFFFFFFu) continue;
             const int64_t i = tri_find([&](int64_t x) { return sc[x]; }, dp, w[u]);
             if (i >= 0) {
+              ++hits;
               const uint2 pqv = tb.pq[bi[u]], qw = vals[pos[u]], pw = vals[a + i];
               // p→q→w→p  +  p→w→q→p
               t += (unsigned long long)pqv.x * qw.x * pw.y + (unsigned long long)pw.x * qw.y * pqv.y;
@@ -300,6 +304,10 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count(const uint32_t *rowptr,
   unsigned long long tot;
   block_exclusive_scan(t, lds, tot);
   if (threadIdx.x == 0 && tot) atomicAdd(&acc[0], tot);
+  block_exclusive_scan(probes, lds, tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(&acc[4], tot);
+  block_exclusive_scan(hits, lds, tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(&acc[5], tot);
 }
 
 __global__ void k_tri_total(const unsigned long long *acc, int64_t *out) {
@@ -316,7 +324,9 @@ static void rocprim_call(Session *s, F &&f) {
 
 // Oriented CSR of the distinct node pairs of (src, dst) over [lo, lo + len).
 struct TriGraph {
-  BufPtr rowptr, cols, vals, loops, acc;  // acc: [0] T, [1] Σ(L+L)·f·b, [2] Σ L(L−1)(L−2), [3] cursor
+  // acc: [0] T, [1] Σ(L+L)·f·b, [2] Σ L(L−1)(L−2), [3] cursor, [4] probes (w ∈ N+(q)
+  // looked up in N+(p)), [5] hits (closed triangles found)
+  BufPtr rowptr, cols, vals, loops, acc;
   uint32_t P = 0;
   uint64_t len = 0;
 };
@@ -324,8 +334,8 @@ struct TriGraph {
 static void tri_build(Session *s, const ColView &src, const ColView &dst, int64_t m, int64_t lo,
                       uint64_t len, TriGraph &g) {
   g.len = len;
-  g.acc = s->alloc(32);
-  HIP_CHECK(hipMemsetAsync(g.acc->p, 0, 32, s->stream));
+  g.acc = s->alloc(48);
+  HIP_CHECK(hipMemsetAsync(g.acc->p, 0, 48, s->stream));
   unsigned long long *acc = (unsigned long long *)g.acc->p;
   g.loops = s->alloc(4 * len);
   HIP_CHECK(hipMemsetAsync(g.loops->p, 0, 4 * len, s->stream));
@@ -434,6 +444,17 @@ void triangle_count_async(Session *s, const ColView &src, const ColView &dst, in
   hipLaunchKernelGGL(k_tri_total, dim3(1), dim3(64), 0, s->stream, (const unsigned long long *)acc,
                      d_out);
   KERNEL_CHECK();
+  if (s->profiling && g.P > 0) {
+    // diagnostics (profiling mode only, host sync): the count kernel's work —
+    // probes (w ∈ N+(q) searched in N+(p)), hits, oriented edges — as
+    // byte-only profile entries, for bench.py's probe-traffic roofline
+    unsigned long long h[2];
+    HIP_CHECK(hipMemcpyAsync(h, acc + 4, 16, hipMemcpyDeviceToHost, s->stream));
+    s->sync();
+    s->profile["tri_probes"].bytes += (double)h[0];
+    s->profile["tri_hits"].bytes += (double)h[1];
+    s->profile["tri_oriented_edges"].bytes += (double)g.P;
+  }
   // g's buffers return to the stream-ordered pool: reuse is ordered after the kernels
 }
 

@@ -12,6 +12,7 @@ import os
 import sys
 
 out, scale = sys.argv[1], int(sys.argv[2])
+prefix = sys.argv[3] if len(sys.argv) > 3 else ""  # "tri_" for the triangle passes
 
 
 def per_kernel(pattern, counter):
@@ -42,6 +43,6 @@ res["hbm_bytes_per_query"] = tot
 res["note"] = ("read_bytes = 2 x FETCH_SIZE (gfx950 streaming-read correction); P3's scattered "
                "16-B segment reads are outside the calibrated pattern; Infinity-Cache hits are "
                "counted by the memory-side counters")
-with open(os.path.join(out, f"pmc_s{scale}.json"), "w") as fh:
+with open(os.path.join(out, f"pmc_{prefix}s{scale}.json"), "w") as fh:
     json.dump(res, fh, indent=1)
 print(json.dumps(res, indent=1))

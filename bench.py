@@ -416,12 +416,14 @@ def run_distributed(args):
     elif args.layout == "node":
         # ingest (untimed): every rank generates the edge stream and keeps its two copies
         full = s.rmat_rels(args.scale, rmat_seed(args.scale), thresholds(), 0, m)
-        in_copy, out_copy = node_partitioned_copies(full, n_nodes, world, rank, compact=not args.int64)
+        in_copy, out_copy = node_partitioned_copies(full, n_nodes, world, rank, compact=id_width(args))
         del full
         s.sync()
         partial = torch.zeros(1, dtype=torch.int64, device="cuda")
         step = lambda: gpu_two_hop_count_sharded(s, in_copy, out_copy, n_nodes, partial)  # noqa: E731
-        pipe = lambda slot: gpu_two_hop_count_sharded_async(s, in_copy, out_copy, n_nodes, slot)  # noqa: E731
+        # the all-reduce of query i overlaps the kernels of query i+1 (RCCL stream)
+        pipe = lambda slot: gpu_two_hop_count_sharded_async(s, in_copy, out_copy, n_nodes, slot,  # noqa: E731
+                                                            async_op=True)
         local_rels = in_copy.size + out_copy.size
         layout = (f"node-partitioned: rank holds the rels whose target (in-copy) / source (out-copy) it "
                   f"owns; one int64 all-reduce per query")
@@ -453,11 +455,14 @@ def run_distributed(args):
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    works = []
     for i in range(args.steps):
         if pipelined:
-            pipe(slots[i:i + 1])
+            works.append(pipe(slots[i:i + 1]))
         else:
             count = step()
+    for w in works:
+        w.wait()
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
@@ -506,10 +511,11 @@ def run_distributed(args):
                 "workload": workload_name(args),
                 "scale": args.scale, "nodes": n_nodes, "rels": m, "count": count,
                 "rank0_rel_rows": local_rels,
-                "id_storage": "int64" if args.int64 else "FOR32",
+                "id_storage": "int64" if args.int64 else (id_storage(args) if args.layout == "node" and args.query == "two_hop" else "FOR32"),
                 "parallelism": f"dp{world} ({layout})",
                 "steps_mode": ("pipelined: step i enqueues the local count + all-reduce into slot i "
-                               "without a host read; K counts checked after the final sync"
+                               "without a host read (the all-reduce of step i overlaps the "
+                               "kernels of step i+1); K counts checked after the final sync"
                                if pipelined else "query-at-a-time"),
                 "parity": parity,
                 "device_ms_per_query_by_rank": per_rank,

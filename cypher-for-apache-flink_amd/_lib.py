@@ -135,6 +135,9 @@ _SIGS = {
                                             c_int32, c_int32, c_void_p]),
     "capf_triangle_count_part": (c_int32, [_S, _T, c_char_p, c_char_p, c_int64, c_int64, c_int32, c_int32,
                                            c_void_p]),
+    "capf_table_hash_route": (c_int32, [_T, c_int32, _STRS, c_int32, POINTER(c_int64), _PT]),
+    "capf_table_download_device": (c_int32, [_T, c_char_p, c_void_p, c_void_p]),
+    "capf_table_has_nulls": (c_int32, [_T, c_char_p, POINTER(c_int32)]),
     "capf_dot_u32": (c_int32, [_S, c_void_p, c_void_p, c_int64, POINTER(c_uint64)]),
 }
 

@@ -396,6 +396,10 @@ uint8_t *node_owner_flags(Session *s, const ColView &key, int64_t n, int64_t lo,
                           int parts, int part, BufPtr &keep);
 bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out, int64_t lo,
                     int64_t n_nodes, int parts, int part, int64_t *d_partial);
+// Rows of `keys` (n rows) grouped by owner h(key tuple) of `parts` (shuffle.hip):
+// the permutation (int64 row indexes) and the row count per owner.
+BufPtr route_permutation(Session *s, const std::vector<ColView> &keys, int64_t n, int parts,
+                         std::vector<int64_t> &counts);
 // Directed triangle count (triangle.hip), part `part` of `parts`, to device int64.
 void triangle_count_async(Session *s, const ColView &src, const ColView &dst, int64_t m,
                           int64_t lo, uint64_t len, int parts, int part, int64_t *d_out);

@@ -864,6 +864,83 @@ capf_status capf_table_node_partition(capf_table *t, const char *key_col, int64_
   CAPF_API_END
 }
 
+capf_status capf_table_hash_route(capf_table *t, int32_t nkeys, const char *const *keys,
+                                  int32_t parts, int64_t *counts, capf_table **out) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(out, "out");
+  need(counts, "counts");
+  if (nkeys <= 0) illegal("at least one routing key");
+  need(keys, "keys");
+  DataPtr d = materialize(t->node);
+  Session *s = t->node->s;
+  std::vector<ColView> kv;
+  for (int j = 0; j < nkeys; ++j) {
+    need(keys[j], "key");
+    const int ki = t->node->col_index_or_throw(keys[j]);
+    const ColPtr &kc = d->cols[ki];
+    if (kc->type == Type::List) illegal("a LIST column cannot be a routing key");
+    force(kc);
+    kv.push_back(view_of(kc));
+  }
+  for (const ColPtr &c : d->cols)
+    if (c->type == Type::List) illegal("LIST columns are not routed between ranks");
+  std::vector<int64_t> cnt;
+  BufPtr perm = route_permutation(s, kv, d->nrows, parts, cnt);
+  auto n = new_node(s, Kind::Source);
+  n->names = t->node->names;
+  n->types = t->node->types;
+  auto e = std::make_shared<Data>();
+  e->nrows = d->nrows;
+  for (const ColPtr &c : d->cols) e->cols.push_back(gather_column(s, c, (const int64_t *)perm->p, d->nrows));
+  s->sync();
+  n->result = e;
+  for (int p = 0; p < parts; ++p) counts[p] = cnt[p];
+  *out = wrap(n);
+  CAPF_API_END
+}
+
+capf_status capf_table_download_device(capf_table *t, const char *col, void *d_values,
+                                       uint8_t *d_valid) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(col, "col");
+  int i = t->node->col_index_or_throw(col);
+  DataPtr d = materialize(t->node);
+  Session *s = t->node->s;
+  if (d->cols[i]->type == Type::List)
+    illegal("column '" + std::string(col) + "' is a LIST: use capf_table_download_list");
+  force(d->cols[i]);
+  const ColPtr c = decode_column(s, d->cols[i]);
+  const size_t w = type_width(c->type);
+  if (d->nrows > 0) {
+    if (c->type != Type::Null && d_values)
+      HIP_CHECK(hipMemcpyAsync(d_values, c->data->p, w * d->nrows, hipMemcpyDeviceToDevice, s->stream));
+    if (d_valid) {
+      if (c->type == Type::Null)
+        HIP_CHECK(hipMemsetAsync(d_valid, 0, d->nrows, s->stream));
+      else if (c->valid)
+        HIP_CHECK(hipMemcpyAsync(d_valid, c->valid->p, d->nrows, hipMemcpyDeviceToDevice, s->stream));
+      else
+        HIP_CHECK(hipMemsetAsync(d_valid, 1, d->nrows, s->stream));
+    }
+    s->sync();
+  }
+  CAPF_API_END
+}
+
+capf_status capf_table_has_nulls(capf_table *t, const char *col, int32_t *has) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(col, "col");
+  need(has, "has");
+  int i = t->node->col_index_or_throw(col);
+  DataPtr d = materialize(t->node);
+  force(d->cols[i]);
+  *has = d->cols[i]->type == Type::Null ? (d->nrows > 0) : (d->cols[i]->valid != nullptr);
+  CAPF_API_END
+}
+
 capf_status capf_table_column_encoding(capf_table *t, const char *col, int32_t *enc,
                                        int64_t *base) {
   CAPF_API_BEGIN

@@ -116,24 +116,27 @@ def gpu_two_hop_count_sharded(session, in_copy, out_copy, n_nodes, partial, node
 
 
 def gpu_two_hop_count_sharded_async(session, in_copy, out_copy, n_nodes, partial, node_base=0,
-                                    group=None):
+                                    group=None, async_op=False):
     """gpu_two_hop_count_sharded without the host read: the summed count is
     left in `partial` (ordered on the session/torch stream), so a driver can
-    enqueue the next query before this one finishes."""
+    enqueue the next query before this one finishes.  async_op=True returns
+    the all-reduce's work handle instead of ordering the stream after it: the
+    next query's kernels then overlap this query's all-reduce (RCCL runs on
+    its own stream); `partial` holds the sum once the handle is waited on."""
     from .table import chain2_sharded_count_async
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     chain2_sharded_count_async(session, in_copy, out_copy, node_base, n_nodes, world, rank,
                                partial.data_ptr())
-    sum_partials(partial, group)
+    return sum_partials(partial, group, async_op)
 
 
-def sum_partials(partial, group=None):
+def sum_partials(partial, group=None, async_op=False):
     """The one collective of the node-partitioned count: an int64 SUM
     all-reduce of the per-rank partials, in place (RCCL on the GPU; gloo in
-    the CPU tests)."""
-    dist.all_reduce(partial, op=dist.ReduceOp.SUM, group=group)
-    return partial
+    the CPU tests).  async_op: return the work handle (wait before reading)."""
+    work = dist.all_reduce(partial, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+    return work if async_op else partial
 
 
 def hist_bits(n_nodes):

@@ -396,6 +396,27 @@ capf_status capf_chain2_local_hists(capf_session *s, capf_table *rels, const cha
 capf_status capf_dot_u32(capf_session *s, const uint32_t *d_a, const uint32_t *d_b, int64_t n,
                          uint64_t *out);
 
+/* ------------------------------------------------- distributed Table layer
+ * The exchange of a hash-partitioned Table over G ranks (dist_table.py):
+ * Flink's join and groupBy repartition both inputs by a hash of the key
+ * before the local operator (FlinkTable.scala:171-187 join, :123-150 group
+ * lower onto DataSet joinWithTiny/hash-partitioned join and groupBy); here
+ * the repartition is this call plus one all-to-all per column (RCCL).
+ * capf_table_hash_route: a materialised copy of t whose rows are grouped by
+ *   owner = h(values of keys[0..nkeys)) of `parts` (owner order, stable inside
+ *   an owner); counts[p] = rows owned by p (host array of `parts`).  Equal key
+ *   tuples have equal owners; NULLs of a key route together; −0.0 as 0.0.
+ *   LIST columns cannot be routed (CAPF_ERR_ILLEGAL_ARGUMENT).
+ * capf_table_download_device: `rows` of one column into DEVICE buffers
+ *   (decoded values, size × 8 or 1 bytes; d_valid = size bytes, 1 = present).
+ * capf_table_has_nulls: does column col carry a validity array (or is it
+ *   an all-NULL column with rows)?                                          */
+capf_status capf_table_hash_route(capf_table *t, int32_t nkeys, const char *const *keys,
+                                  int32_t parts, int64_t *counts, capf_table **out);
+capf_status capf_table_download_device(capf_table *t, const char *col, void *d_values,
+                                       uint8_t *d_valid);
+capf_status capf_table_has_nulls(capf_table *t, const char *col, int32_t *has);
+
 #ifdef __cplusplus
 }
 #endif

@@ -548,6 +548,31 @@ JNI(jlong, chain2LocalHists)(JNIEnv *env, jobject, jlong s, jlong rels, jstring 
                                     reinterpret_cast<uint32_t *>(d_out), &loops));
   return loops;
 }
+// distributed Table layer: hash routing + device-side column copies; the
+// JVM side moves the [off[p], off[p+1]) slices with its collective library
+// (counts → countsOut[0..parts))
+JNI(jlong, tableHashRoute)(JNIEnv *env, jobject, jlong t, jobjectArray keys, jint parts,
+                           jlongArray countsOut) {
+  JStrs k(env, keys);
+  std::vector<int64_t> cnt(parts > 0 ? parts : 1);
+  capf_table *out = nullptr;
+  if (fail(env, capf_table_hash_route(T(t), k.n(), k.data(), parts, cnt.data(), &out))) return 0;
+  std::vector<jlong> v(cnt.begin(), cnt.end());
+  env->SetLongArrayRegion(countsOut, 0, parts, v.data());
+  return H(out);
+}
+JNI(void, tableDownloadDevice)(JNIEnv *env, jobject, jlong t, jstring col, jlong d_values,
+                               jlong d_valid) {
+  JStr c(env, col);
+  fail(env, capf_table_download_device(T(t), c.p, reinterpret_cast<void *>(d_values),
+                                       reinterpret_cast<uint8_t *>(d_valid)));
+}
+JNI(jboolean, tableHasNulls)(JNIEnv *env, jobject, jlong t, jstring col) {
+  JStr c(env, col);
+  int32_t h = 0;
+  fail(env, capf_table_has_nulls(T(t), c.p, &h));
+  return (jboolean)(h ? 1 : 0);
+}
 JNI(jlong, dotU32)(JNIEnv *env, jobject, jlong s, jlong d_a, jlong d_b, jlong n) {
   uint64_t r = 0;
   fail(env, capf_dot_u32(S(s), reinterpret_cast<const uint32_t *>(d_a),

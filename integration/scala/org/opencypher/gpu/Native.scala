@@ -154,4 +154,8 @@ object Native {
   @native def chain2LocalHists(session: Long, rels: Long, srcCol: String, dstCol: String, nodeBase: Long,
                                nNodes: Long, dIn: Long, dOut: Long): Long
   @native def dotU32(session: Long, dA: Long, dB: Long, n: Long): Long
+  // distributed Table layer (dist_table.py): rows grouped by owner h(keys), counts per owner
+  @native def tableHashRoute(table: Long, keys: Array[String], parts: Int, countsOut: Array[Long]): Long
+  @native def tableDownloadDevice(table: Long, col: String, dValues: Long, dValid: Long): Unit
+  @native def tableHasNulls(table: Long, col: String): Boolean
 }

@@ -135,6 +135,8 @@ _SIGS = {
                                             c_int32, c_int32, c_void_p]),
     "capf_triangle_count_part": (c_int32, [_S, _T, c_char_p, c_char_p, c_int64, c_int64, c_int32, c_int32,
                                            c_void_p]),
+    "capf_csv_parse_longs": (c_int32, [_S, c_char_p, c_int64, c_char_p, c_int32, _STRS, _PT]),
+    "capf_csv_read_longs": (c_int32, [_S, c_char_p, c_char_p, c_int32, _STRS, _PT]),
     "capf_table_hash_route": (c_int32, [_T, c_int32, _STRS, c_int32, POINTER(c_int64), _PT]),
     "capf_table_download_device": (c_int32, [_T, c_char_p, c_void_p, c_void_p]),
     "capf_table_has_nulls": (c_int32, [_T, c_char_p, POINTER(c_int32)]),

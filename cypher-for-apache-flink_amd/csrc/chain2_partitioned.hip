@@ -303,7 +303,8 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
 constexpr int C3_TT = 256;
 __global__ __launch_bounds__(256) void k_c3_transpose(const uint32_t *meta, uint32_t *meta_t,
                                                        int64_t ntiles, int nr,
-                                                       unsigned long long *run_total, int64_t tt) {
+                                                       unsigned long long *run_total, int64_t tt,
+                                                       uint32_t *bsum = nullptr) {
   __shared__ uint32_t tilebuf[C3_TT][33];
   __shared__ uint32_t part[8][33];
   const int r0 = blockIdx.y * 32;
@@ -325,6 +326,8 @@ __global__ __launch_bounds__(256) void k_c3_transpose(const uint32_t *meta, uint
 #pragma unroll
     for (int q = 0; q < 8; ++q) c += part[q][tx];
     if (c && r < nr) atomicAdd(&run_total[r], (unsigned long long)c);
+    // per-(run, tile block) key counts: the balanced P3's split points
+    if (bsum && r < nr) bsum[(int64_t)r * gridDim.x + blockIdx.x] = c;
   }
   if (!meta_t) return;  // run totals only (P3 reads meta in place)
   const int lt = __builtin_ctzll((unsigned long long)tt);  // tt is a power of two
@@ -517,6 +520,64 @@ __device__ inline int64_t uniform64(int64_t v) {
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
+__device__ inline uint32_t bal_start(int w, uint32_t W, int P) {
+  return (uint32_t)(((uint64_t)w * W) / (uint64_t)P);
+}
+
+// The workgroup whose key range holds offset x < W.
+__device__ inline int bal_wg_of(uint32_t x, uint32_t W, int P) {
+  int w = (int)min<uint64_t>(((uint64_t)x * P) / max(W, 1u), (uint64_t)(P - 1));
+  while (w + 1 < P && bal_start(w + 1, W, P) <= x) ++w;
+  while (w > 0 && bal_start(w, W, P) > x) --w;
+  return w;
+}
+
+// The sub-bucket holding key offset x: the last j < nsb with pre[j] ≤ x.
+__device__ inline int bal_sb_of(const uint32_t *pre, int nsb, uint32_t x) {
+  int lo = 0, hi = nsb;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (pre[mid] <= x) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// Split tile of a run for key offset x (one wave): tt·(smallest block k with
+// Σ_{k' < k} bs[k'] ≥ x), at most ntiles; for x = 0 the run's first block
+// holding keys (a run's keys lie in its side's tiles only: an out-run's part 0
+// must not start at tile 0, or its waves' even tile split would hand most
+// waves the in-copy tiles, empty for this run).
+__device__ inline int64_t bal_tile(const uint32_t *bs, int nblk, int tt, int64_t ntiles, uint32_t x) {
+  const int lane = lane_id();
+  uint32_t carry = 0;
+  for (int c = 0; c < nblk; c += WAVE) {
+    const int k = c + lane;
+    const uint32_t v = k < nblk ? bs[k] : 0u;
+    const uint32_t inc = wave_inclusive_scan(v);
+    const unsigned long long hit = __ballot(k < nblk && (x == 0 ? v > 0 : carry + inc - v >= x));
+    if (hit) return min<int64_t>((int64_t)(c + __builtin_ctzll(hit)) * tt, ntiles);
+    carry += (uint32_t)__shfl(inc, WAVE - 1, WAVE);
+  }
+  return ntiles;
+}
+
+// Apportioned P3 units of a node-partitioned rank (CAPF_SHARD_SB=3): run r
+// (64 Ki-node bucket side) gets k_r = max(1, round(P·T_r / W)) units, each
+// 1/k_r of its keys — split points rounded to blocks of tt tiles from the
+// transpose's per-(run, block) counts — so every unit counts ≈ W/P keys
+// whatever the skew (a hub's run gets more units), and unit (r, i) writes
+// slice base_r + i.  Every P3 workgroup derives the table from the run totals;
+// block 0 also stores it (base, k per run) for the dot.
+constexpr int C5APP_MAXR = 520;  // runs of a rank's P1 (C5S_MAXR)
+
+struct C5Sched {
+  const unsigned long long *run_total;  // [nr] keys (null: the even split of S slices)
+  const uint32_t *bsum;                 // [nr][nblk]
+  int nblk, tt, P;
+  int32_t *table;                       // out: base[nr], k[nr]
+};
+
 // P3.  The wave takes 64 tiles of its unit at a time and treats their
 // segments (8-key padded, 16-B aligned pieces) as ONE sequence: lane l of
 // step s handles piece s·64·PPS + l (+ 64·j), found by a 6-step binary search
@@ -548,10 +609,55 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
                                                             int nb, int64_t rstride, uint32_t *h_in,
                                                             uint32_t *h_out, int64_t slice_stride,
                                                             C3Ovf ovf, const int32_t *order,
-                                                            C3Sides sd, int S, int64_t mstride) {
+                                                            C3Sides sd, int S, int64_t mstride,
+                                                            C5Sched sch) {
   // units == null: the static work list of a node-partitioned rank — unit
-  // (run, k) counts tile range k of S of the run's side into slice k
-  const int nu = units ? *nunits : 2 * sd.nb * S;
+  // (run, k) counts tile range k of S of the run's side into slice k, or
+  // (sch.run_total) the apportioned units: (run, i) into slice base_r + i
+  __shared__ int32_t sbase[C5APP_MAXR + 1], sk[C5APP_MAXR];
+  __shared__ uint32_t lds_sc[17];
+  __shared__ int64_t sbnd[2];
+  int nu = units ? *nunits : 2 * sd.nb * S;
+  const int nrr = 2 * sd.nb;
+  if (sch.run_total) {
+    // k_r ≈ P·T_r / W with Σ k_r = P exactly (largest remainder; every
+    // non-empty run ≥ 1): one unit per CU, no second round of units
+    __shared__ unsigned long long rem[C5APP_MAXR];
+    __shared__ unsigned long long lds_w[17];
+    const int r = threadIdx.x;
+    unsigned long long T = r < nrr ? sch.run_total[r] : 0ull;  // one coalesced load
+    unsigned long long W;
+    block_exclusive_scan(T, lds_w, W);
+    W = max(W, 1ull);
+    int32_t k = 0;
+    if (r < nrr) {
+      const unsigned long long e = (unsigned long long)sch.P * T;
+      k = (int32_t)(e / W);
+      rem[r] = k == 0 && T > 0 ? ~0ull : e % W;  // forced units first
+    }
+    __syncthreads();
+    uint32_t fl;
+    block_exclusive_scan((uint32_t)k, lds_sc, fl);
+    const int deficit = sch.P - (int)fl;
+    if (r < nrr && T > 0) {
+      int ahead = 0;  // runs with a larger remainder (ties: lower index first)
+      for (int q = 0; q < nrr; ++q) ahead += rem[q] > rem[r] || (rem[q] == rem[r] && q < r);
+      if (ahead < deficit || k == 0) ++k;
+    }
+    uint32_t tot;
+    const uint32_t ex = block_exclusive_scan((uint32_t)k, lds_sc, tot);
+    if (r < nrr) {
+      sbase[r] = (int32_t)ex;
+      sk[r] = k;
+      if (blockIdx.x == 0) {
+        sch.table[r] = (int32_t)ex;
+        sch.table[nrr + r] = k;
+      }
+    }
+    if (r == 0) sbase[nrr] = (int32_t)tot;
+    __syncthreads();
+    nu = sbase[nrr];
+  }
   if ((int)blockIdx.x >= nu && order) return;
   const int ui = order ? order[blockIdx.x] : c3_unit_of((int)blockIdx.x);
   if (ui >= nu) return;
@@ -564,6 +670,28 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
   C3Unit u;
   if (units) {
     u = units[ui];
+  } else if (sch.run_total) {
+    // the run holding unit ui (last r with base_r ≤ ui), part i of k_r
+    int lo = 0, hi = nrr;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (sbase[mid] <= ui) lo = mid;
+      else hi = mid;
+    }
+    const int i = ui - sbase[lo], k = sk[lo];
+    const unsigned long long T = sch.run_total[lo];
+    const int wv = threadIdx.x / WAVE;
+    if (wv < 2) {  // split tiles of the part's key range, one wave each
+      const uint32_t x = (uint32_t)(T * (unsigned long long)(i + wv) / (unsigned long long)k);
+      const int64_t t = bal_tile(sch.bsum + (int64_t)lo * sch.nblk, sch.nblk, sch.tt, ntiles, x);
+      if (lane_id() == 0) sbnd[wv] = t;
+    }
+    __syncthreads();
+    u.run = lo;
+    u.exclusive = 1;
+    u.t0 = sbnd[0];
+    u.t1 = sbnd[1];
+    u.slice = ui;  // slices are indexed by unit
   } else {
     const int k = ui % S, sdi = ui / S >= sd.nb ? 1 : 0;
     const int64_t len = sd.t1[sdi] - sd.t0[sdi];
@@ -575,7 +703,8 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
   }
   const uint32_t side = u.run >= nb ? 1u : 0u;
   uint32_t *hist = side ? h_out : h_in;
-  const uint32_t hist_base = (uint32_t)(u.slice * slice_stride + (int64_t)(u.run % nb) * C2_BW);
+  const uint32_t hist_base = sch.run_total ? (uint32_t)((int64_t)u.slice * C2_BW)
+                                           : (uint32_t)(u.slice * slice_stride + (int64_t)(u.run % nb) * C2_BW);
   for (int i = threadIdx.x; i < C2_WORDS + C5_CORR; i += C5_BLOCK) words[i] = 0;
   __syncthreads();
   // wave-uniform values live in SGPRs: uniform loop control, no exec masking
@@ -896,8 +1025,10 @@ static void launch_c5(Session *s, const C5Cols<W> &c, uint16_t *part, uint32_t *
 // at h_in/h_out + s·slice_stride; every counter of every slice is written.
 static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, const C3Sides &sd,
                     int64_t ntiles, int64_t rstride, int64_t nkeys, int S, uint32_t *h_in,
-                    uint32_t *h_out, int64_t slice_stride, bool static_units = false) {
+                    uint32_t *h_out, int64_t slice_stride, bool static_units = false,
+                    int32_t *apportion_table = nullptr) {
   const int nr = 2 * sd.nb;
+  const bool app = apportion_table != nullptr;  // apportioned units (C5Sched), slices by unit
   static bool attr_set = false;
   if (!attr_set) {
     for (const void *f : {(const void *)k_c5_gather<C5_PPS, 0>, (const void *)k_c5_gather<C5_PPS, 2>,
@@ -944,11 +1075,21 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
     ovf.trace = (unsigned long long *)trace->p;
   }
   HIP_CHECK(hipMemsetAsync(acc->p, 0, 8 * nr + 16, s->stream));
+  BufPtr bsum = app ? s->alloc(4 * (int64_t)nr * nparts) : BufPtr();
+  C5Sched sch{};
+  if (app) {
+    sch.run_total = run_total;
+    sch.bsum = (const uint32_t *)bsum->p;
+    sch.nblk = nparts;
+    sch.tt = (int)tt;
+    sch.P = s->num_cus;
+    sch.table = apportion_table;
+  }
   {
     KernelTimer kt(s, "c3_transpose", 8.0 * nr * ntiles);
     hipLaunchKernelGGL(k_c3_transpose, dim3((unsigned)nparts, (nr + 31) / 32), dim3(256), 0,
                        s->stream, meta, transpose ? (uint32_t *)meta_t->p : nullptr, ntiles, nr,
-                       run_total, tt);
+                       run_total, tt, app ? (uint32_t *)bsum->p : nullptr);
     KERNEL_CHECK();
   }
   if (!static_units) {
@@ -976,13 +1117,15 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
                 : h1                  ? k_c5_gather<C5_PPS, 0, 1, 1>
                 : d2                  ? k_c5_gather<C5_PPS, 0, 2>
                                       : k_c5_gather<C5_PPS, 0>;
-    const int grid = static_units ? (nr * S + 255) / 256 * 256 : max_units;
+    const int grid = app            ? (s->num_cus + nr + 255) / 256 * 256
+                     : static_units ? (nr * S + 255) / 256 * 256
+                                    : max_units;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(C5_BLOCK), C5_GATHER_LDS, s->stream,
                        static_units ? nullptr : (const C3Unit *)units, (const int32_t *)nunits,
                        part, transpose ? (const uint32_t *)meta_t->p : meta, ntiles, sd.nb,
                        rstride, h_in, h_out, slice_stride, ovf,
                        static_units ? nullptr : (const int32_t *)order, sd, S,
-                       transpose ? (int64_t)1 : (int64_t)nr);
+                       transpose ? (int64_t)1 : (int64_t)nr, sch);
     KERNEL_CHECK();
   }
   {
@@ -1036,6 +1179,40 @@ __global__ __launch_bounds__(256) void k_c5_dot_slices(const uint32_t *si, const
     }
     t += (unsigned long long)a.x * b.x + (unsigned long long)a.y * b.y +
          (unsigned long long)a.z * b.z + (unsigned long long)a.w * b.w;
+  }
+  unsigned long long tot;
+  block_exclusive_scan(t, lds, tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(acc, tot);
+}
+
+// acc[0] += Σ_b Σ_i (Σ in-slices of b)·(Σ out-slices of b) over the apportioned
+// slices sl[unit][64 Ki] (table: base[2·nb], k[2·nb]; runs [0, nb) in, [nb, 2·nb) out).
+__global__ __launch_bounds__(256) void k_c5_dot_apportioned(const uint32_t *sl, const int32_t *table, int nb,
+                                                             unsigned long long *acc) {
+  __shared__ int32_t base[C5APP_MAXR], kk[C5APP_MAXR];
+  __shared__ unsigned long long lds[17];
+  for (int r = threadIdx.x; r < 2 * nb; r += 256) {
+    base[r] = table[r];
+    kk[r] = table[2 * nb + r];
+  }
+  __syncthreads();
+  constexpr int Q = C2_BW / 4;
+  const int64_t n4 = (int64_t)nb * Q;
+  unsigned long long t = 0;
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n4; q += (int64_t)gridDim.x * 256) {
+    const int b = (int)(q / Q);
+    const int64_t i4 = q % Q;
+    uint4 x = make_uint4(0, 0, 0, 0), y = make_uint4(0, 0, 0, 0);
+    for (int k = 0; k < kk[b]; ++k) {
+      const uint4 v = ((const uint4 *)(sl + (int64_t)(base[b] + k) * C2_BW))[i4];
+      x = make_uint4(x.x + v.x, x.y + v.y, x.z + v.z, x.w + v.w);
+    }
+    for (int k = 0; k < kk[nb + b]; ++k) {
+      const uint4 v = ((const uint4 *)(sl + (int64_t)(base[nb + b] + k) * C2_BW))[i4];
+      y = make_uint4(y.x + v.x, y.y + v.y, y.z + v.z, y.w + v.w);
+    }
+    t += (unsigned long long)x.x * y.x + (unsigned long long)x.y * y.y + (unsigned long long)x.z * y.z +
+         (unsigned long long)x.w * y.w;
   }
   unsigned long long tot;
   block_exclusive_scan(t, lds, tot);
@@ -1436,12 +1613,20 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_sb_gather(C5SbArgs a) {
 // Sub-bucket runs per bucket (log2) for a rank owning nbl buckets: the most
 // that keep 2·nsb + 1 runs within P1's limit; 0 (slice path) unless the
 // sub-buckets are ≤ 2^C5SB_MAXBITS nodes (LDS: 2 uint32 arrays).
+// P3 of a node-partitioned rank (CAPF_SHARD_SB, tuning): 0 = histogram
+// slices + dot, 1 = one sub-bucket per unit (k_c5_sb_gather), 2 = balanced key
+// ranges over sub-buckets (k_c5_bal_gather + k_c5_bal_fold)
+static int c5s_mode() {
+  const char *e = getenv("CAPF_SHARD_SB");
+  return e ? atoi(e) : 0;
+}
+
 static int c5sb_lsub(int nbl) {
   // measured at s24 G = 8 and off by default: per-unit rates equal the slice
   // path's, but 8 Ki-node sub-buckets are skewed (p99 unit 1.7×, the hub's
   // 3.2× the median) where the slice units are not → 0.296 vs 0.235 ms/rank
-  const char *e = getenv("CAPF_SHARD_SB");  // tuning: 1 = sub-bucket units
-  if (!(e && atoi(e) == 1) || nbl <= 0) return 0;
+  const int mode = c5s_mode();
+  if ((mode != 1 && mode != 2) || nbl <= 0) return 0;
   int l = 0;
   while (l < C2_BITS && 2 * ((int64_t)nbl << (l + 1)) + 1 <= C5S_MAXR) ++l;
   return C2_BITS - l <= C5SB_MAXBITS ? l : 0;
@@ -1503,6 +1688,365 @@ static void c5_sb_post(Session *s, const uint16_t *part, const uint32_t *meta, i
       fwrite(h.data(), 8, h.size(), f);
       fclose(f);
     }
+  }
+}
+
+// ---------------------------------------- sharded P3, balanced key ranges
+// The sub-bucket runs of a rank (P1 with lsub > 0: nsb sub-buckets of 2^sbits
+// nodes, in-run j and out-run nsb + j) hold W keys.  Workgroup w of P (one
+// per CU) takes the keys [w·W/P, (w+1)·W/P) of the sequence "sub-bucket 0
+// in, out; sub-bucket 1 in, out; …" — every workgroup the same number of keys
+// whatever the skew (a hub's sub-bucket simply spans several workgroups).
+// Split points inside a run are rounded to blocks of tt tiles using the
+// transpose's per-(run, block) counts, identically by both neighbours, so
+// every tile segment is counted exactly once.  A sub-bucket lying wholly in
+// one workgroup is finished there: in and out counters (uint32, 2·2^sbits in
+// LDS) → Σ in·out added to acc, nothing written.  A split sub-bucket's
+// portions store their corrected counters into the workgroup's slot (first or
+// last portion), and k_c5_bal_fold sums the slots of each split sub-bucket
+// and adds its Σ in·out: ≤ 2 slots per workgroup, no slice or dot pass over
+// the whole node range, no overflow log (uint32 counters).
+struct C5BalArgs {
+  const uint16_t *part;
+  const uint32_t *meta_t;               // [run][tile] (start/8 | count << 16)
+  const unsigned long long *run_total;  // [run] keys
+  const uint32_t *bsum;                 // [run][nblk] keys per block of tt tiles
+  int64_t ntiles;
+  int nblk, tt;
+  int nsb, sbits;
+  uint32_t rs8;
+  int nwg;                  // P
+  uint32_t *slots;          // 2·P slots of (in, out) 2·2^sbits counters
+  unsigned long long *acc;  // += Σ in·out
+};
+
+constexpr int C5BAL_MAXSB = 512;
+
+constexpr size_t c5bal_lds(int sbits) {
+  return 4 * ((size_t)2 << sbits) + 4 * 2 * C5_CORR + 2 * sizeof(C5WaveTab) * (C5_BLOCK / WAVE);
+}
+
+__global__ __launch_bounds__(C5_BLOCK) void k_c5_bal_gather(C5BalArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t words[];
+  __shared__ uint32_t pre[C5BAL_MAXSB + 1];
+  __shared__ uint32_t tin[C5BAL_MAXSB];
+  __shared__ uint32_t lds_scan[17];
+  __shared__ unsigned long long lds_red[17];
+  __shared__ int64_t bnd[4];
+  constexpr int NW = C5_BLOCK / WAVE;
+  constexpr uint32_t STEP = WAVE * C5_PPS;
+  const int NB = 1 << a.sbits;
+  const uint32_t kmask = (uint32_t)NB - 1;
+  uint32_t *corr = words + 2 * NB;
+  C5WaveTab *tabs = (C5WaveTab *)(corr + 2 * C5_CORR);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = lane_id();
+  const int P = a.nwg, w = blockIdx.x;
+  // the schedule: sub-bucket sizes and their exclusive prefix (every workgroup alike)
+  for (int j0 = 0; j0 < a.nsb; j0 += C5_BLOCK) {
+    const int j = j0 + threadIdx.x;
+    uint32_t tj = 0, sj = 0;
+    if (j < a.nsb) {
+      tj = (uint32_t)a.run_total[j];
+      sj = tj + (uint32_t)a.run_total[a.nsb + j];
+    }
+    uint32_t tot;
+    const uint32_t ex = block_exclusive_scan(sj, lds_scan, tot);
+    const uint32_t base = j0 ? pre[j0] : 0u;
+    if (j < a.nsb) {
+      pre[j] = base + ex;
+      tin[j] = tj;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) pre[min(j0 + C5_BLOCK, a.nsb)] = base + tot;
+    __syncthreads();
+  }
+  for (int i = threadIdx.x; i < 2 * NB + 2 * C5_CORR; i += C5_BLOCK) words[i] = 0;
+  __syncthreads();
+  const uint32_t W = pre[a.nsb];
+  const uint32_t A = bal_start(w, W, P), B = bal_start(w + 1, W, P);
+  if (A >= B) return;  // block-uniform
+  const int jfirst = bal_sb_of(pre, a.nsb, A);
+  C5WaveTab *tab2 = tabs + 2 * wave;
+  const uint4 *part4 = (const uint4 *)a.part;
+  const uint4 dead_keys = make_uint4(lane | lane << 16, lane | lane << 16, lane | lane << 16,
+                                     lane | lane << 16);
+  // count the segments of run row m over tiles [w0, w1) into cnt; pad and
+  // dead-lane keys are subtracted through cs (bins 0..63)
+  auto walk = [&](const uint32_t *m, int64_t w0, int64_t w1, uint32_t *cnt, uint32_t *cs) {
+    uint32_t padc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t dead = 0;
+    uint32_t wpre = w0 + lane < w1 ? m[w0 + lane] : 0u;
+    auto setup = [&](int64_t tb, int buf) -> uint32_t {
+      const int64_t t = tb + lane;
+      const uint32_t wd = wpre;
+      const uint32_t len = wd >> 16, nq = (len + 7) >> 3, r = len & 7;
+#pragma unroll
+      for (int e = 1; e < 8; ++e) padc[e] += (r != 0 && r <= (uint32_t)e) ? 1u : 0u;
+      const uint32_t inc = wave_inclusive_scan(nq);
+      tab2[buf].pre[lane] = inc - nq;
+      if (lane == WAVE - 1) tab2[buf].pre[WAVE] = inc;
+      tab2[buf].qb[lane] = (uint32_t)t * a.rs8 + (wd & 0xFFFF);
+      __builtin_amdgcn_sched_barrier(0);
+      const int64_t tn = tb + WAVE + lane;
+      wpre = tn < w1 ? m[tn] : 0u;
+      __builtin_amdgcn_wave_barrier();
+      return (uint32_t)__builtin_amdgcn_readfirstlane(__shfl(inc, WAVE - 1, WAVE));
+    };
+    auto fetch = [&](int buf, uint32_t p0, uint32_t total, uint4 *v) {
+      const C5WaveTab &tab = tab2[buf];
+#pragma unroll
+      for (int j = 0; j < C5_PPS; ++j) {
+        const uint32_t p = p0 + j * WAVE + lane;
+        const uint32_t pc = min(p, total - 1);
+        uint32_t k = 0;
+#pragma unroll
+        for (int b = WAVE / 2; b > 0; b >>= 1)
+          if (tab.pre[k + b] <= pc) k += b;
+        v[j] = part4[tab.qb[k] + (pc - tab.pre[k])];
+      }
+    };
+    // a piece's copies of its first (second) key are added once, as a count
+    auto count = [&](const uint4 *v, uint32_t p0, uint32_t total) {
+#pragma unroll
+      for (int j = 0; j < C5_PPS; ++j) {
+        const bool live = p0 + j * WAVE + lane < total;
+        dead += live ? 0u : 1u;
+        const uint32_t wd[4] = {live ? v[j].x : dead_keys.x, live ? v[j].y : dead_keys.y,
+                                live ? v[j].z : dead_keys.z, live ? v[j].w : dead_keys.w};
+        const uint32_t k0 = wd[0] & 0xFFFF, k1 = wd[0] >> 16;
+        uint32_t n0 = k1 == k0 ? 2u : 1u, n1 = 1;
+        bool dup[8];
+#pragma unroll
+        for (int e = 2; e < 8; ++e) {
+          const uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
+          const bool d0 = key == k0, d1 = !d0 && key == k1;
+          dup[e] = d0 || d1;
+          n0 += d0 ? 1u : 0u;
+          n1 += d1 ? 1u : 0u;
+        }
+        atomicAdd(&cnt[k0 & kmask], n0);
+        if (k1 != k0) atomicAdd(&cnt[k1 & kmask], n1);
+#pragma unroll
+        for (int e = 2; e < 8; ++e) {
+          const uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
+          if (!dup[e]) atomicAdd(&cnt[key & kmask], 1u);
+        }
+      }
+    };
+    if (w0 < w1) {
+      int64_t tb = uniform64(w0);
+      int buf = 0;
+      uint32_t total = setup(tb, buf), p0 = 0;
+      while (total == 0) {
+        tb += WAVE;
+        if (tb >= w1) break;
+        buf ^= 1;
+        total = setup(tb, buf);
+      }
+      if (total) {
+        auto advance = [&]() -> bool {
+          if (p0 + STEP < total) {
+            p0 = (uint32_t)__builtin_amdgcn_readfirstlane(p0 + STEP);
+            return true;
+          }
+          do {
+            tb = uniform64(tb + WAVE);
+            if (tb >= w1) return false;
+            buf ^= 1;
+            total = setup(tb, buf);
+            p0 = 0;
+          } while (total == 0);
+          return true;
+        };
+        // three rotating piece buffers: loads of steps i+1, i+2 in flight while step i counts
+        uint4 va[C5_PPS], vb[C5_PPS], vc[C5_PPS];
+        uint32_t pa, ta, pb, tb2, pc, tc;
+        pa = p0;
+        ta = total;
+        fetch(buf, p0, total, va);
+        if (!advance()) {
+          count(va, pa, ta);
+        } else {
+          pb = p0;
+          tb2 = total;
+          fetch(buf, p0, total, vb);
+          for (;;) {
+            if (!advance()) {
+              count(va, pa, ta);
+              count(vb, pb, tb2);
+              break;
+            }
+            pc = p0;
+            tc = total;
+            fetch(buf, p0, total, vc);
+            count(va, pa, ta);
+            if (!advance()) {
+              count(vb, pb, tb2);
+              count(vc, pc, tc);
+              break;
+            }
+            pa = p0;
+            ta = total;
+            fetch(buf, p0, total, va);
+            count(vb, pb, tb2);
+            if (!advance()) {
+              count(vc, pc, tc);
+              count(va, pa, ta);
+              break;
+            }
+            pb = p0;
+            tb2 = total;
+            fetch(buf, p0, total, vb);
+            count(vc, pc, tc);
+          }
+        }
+      }
+    }
+    const uint32_t pcls = 8u * (uint32_t)((w0 + lane) & 7);
+#pragma unroll
+    for (int e = 1; e < 8; ++e)
+      if (padc[e]) atomicAdd(&cs[pcls + e], padc[e]);
+    if (dead) atomicAdd(&cs[lane], 8 * dead);
+  };
+  for (int j = jfirst; j < a.nsb && pre[j] < B; ++j) {
+    const uint32_t S = pre[j + 1] - pre[j];
+    if (S == 0) continue;
+    const uint32_t lo = max(A, pre[j]) - pre[j], hi = min(B, pre[j + 1]) - pre[j];
+    const uint32_t T = tin[j];
+    if (wave < 4) {  // the four split tiles of this portion, one wave each
+      const int run = wave < 2 ? j : a.nsb + j;
+      const uint32_t x = wave == 0 ? min(lo, T) : wave == 1 ? min(hi, T) : wave == 2 ? max(lo, T) - T
+                                                                                     : max(hi, T) - T;
+      const int64_t t = bal_tile(a.bsum + (int64_t)run * a.nblk, a.nblk, a.tt, a.ntiles, x);
+      if (lane == 0) bnd[wave] = t;
+    }
+    __syncthreads();
+    const int64_t ti0 = bnd[0], li = max<int64_t>(bnd[1] - bnd[0], 0);
+    const int64_t to0 = bnd[2], lt = li + max<int64_t>(bnd[3] - bnd[2], 0);
+    // the 16 waves split the portion's tiles: in-run tiles first, then out-run
+    const int64_t v0 = uniform64(lt * wave / NW), v1 = uniform64(lt * (wave + 1) / NW);
+    if (v0 < li) walk(a.meta_t + (int64_t)j * a.ntiles, ti0 + v0, ti0 + min(v1, li), words, corr);
+    if (v1 > li)
+      walk(a.meta_t + (int64_t)(a.nsb + j) * a.ntiles, to0 + max(v0, li) - li, to0 + v1 - li, words + NB,
+           corr + C5_CORR);
+    __syncthreads();
+    if (lo == 0 && hi == S) {  // the whole sub-bucket: finish it here
+      unsigned long long t = 0;
+      for (int i = threadIdx.x; i < NB; i += C5_BLOCK) {
+        uint32_t x = words[i], y = words[NB + i];
+        if (i < C5_CORR) {
+          x -= corr[i];
+          y -= corr[C5_CORR + i];
+        }
+        t += (unsigned long long)x * y;
+      }
+      const unsigned long long tot = block_reduce_sum(t, lds_red);
+      if (threadIdx.x == 0 && tot) atomicAdd(a.acc, tot);
+    } else {  // a portion of a split sub-bucket: corrected counters to the slot
+      uint32_t *dst = a.slots + (int64_t)(2 * w + (j == jfirst ? 0 : 1)) * 2 * NB;
+      for (int i = threadIdx.x; i < NB; i += C5_BLOCK) {
+        uint32_t x = words[i], y = words[NB + i];
+        if (i < C5_CORR) {
+          x -= corr[i];
+          y -= corr[C5_CORR + i];
+        }
+        dst[i] = x;
+        dst[NB + i] = y;
+      }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * NB + 2 * C5_CORR; i += C5_BLOCK) words[i] = 0;
+    __syncthreads();
+  }
+}
+
+// One block per sub-bucket: a split one sums its portions' slots and adds Σ in·out.
+__global__ __launch_bounds__(256) void k_c5_bal_fold(C5BalArgs a) {
+  __shared__ uint32_t pre[C5BAL_MAXSB + 1];
+  __shared__ uint32_t lds_scan[17];
+  __shared__ unsigned long long lds_red[17];
+  const int NB = 1 << a.sbits;
+  const int P = a.nwg;
+  for (int j0 = 0; j0 < a.nsb; j0 += 256) {
+    const int j = j0 + threadIdx.x;
+    const uint32_t sj = j < a.nsb ? (uint32_t)a.run_total[j] + (uint32_t)a.run_total[a.nsb + j] : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_exclusive_scan(sj, lds_scan, tot);
+    const uint32_t base = j0 ? pre[j0] : 0u;
+    if (j < a.nsb) pre[j] = base + ex;
+    __syncthreads();
+    if (threadIdx.x == 0) pre[min(j0 + 256, a.nsb)] = base + tot;
+    __syncthreads();
+  }
+  const int j = blockIdx.x;
+  const uint32_t W = pre[a.nsb];
+  if (pre[j + 1] == pre[j]) return;
+  const int wa = bal_wg_of(pre[j], W, P), wb = bal_wg_of(pre[j + 1] - 1, W, P);
+  if (wa == wb) return;  // finished inside its workgroup
+  unsigned long long t = 0;
+  for (int i = threadIdx.x; i < NB; i += 256) {
+    uint32_t x = 0, y = 0;
+    for (int w = wa; w <= wb; ++w) {
+      const int jf = bal_sb_of(pre, a.nsb, bal_start(w, W, P));
+      const uint32_t *src = a.slots + (int64_t)(2 * w + (jf == j ? 0 : 1)) * 2 * NB;
+      x += src[i];
+      y += src[NB + i];
+    }
+    t += (unsigned long long)x * y;
+  }
+  const unsigned long long tot = block_reduce_sum(t, lds_red);
+  if (threadIdx.x == 0 && tot) atomicAdd(a.acc, tot);
+}
+
+// T + balanced P3 + fold of the sub-bucket path (adds Σ in·out into d_acc[0]).
+static void c5_bal_post(Session *s, const uint16_t *part, const uint32_t *meta, int64_t ntiles, int nsb,
+                        int sbits, int64_t rstride, unsigned long long *d_acc) {
+  const int nr = 2 * nsb;
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIP_CHECK(hipFuncSetAttribute((const void *)k_c5_bal_gather, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)c5bal_lds(C5SB_MAXBITS)));
+    attr_set = true;
+  }
+  int64_t tt = C3_TT;
+  while (tt > 32 && ((ntiles + tt - 1) / tt) * ((nr + 31) / 32) < 1024) tt /= 2;
+  const int nblk = (int)((ntiles + tt - 1) / tt);
+  const int P = s->num_cus;
+  BufPtr meta_t = s->alloc(4 * nr * ntiles);
+  BufPtr tot = s->alloc(8 * nr + 4 * (int64_t)nr * nblk);
+  unsigned long long *run_total = (unsigned long long *)tot->p;
+  uint32_t *bsum = (uint32_t *)(run_total + nr);
+  HIP_CHECK(hipMemsetAsync(tot->p, 0, 8 * nr, s->stream));
+  BufPtr slots = s->alloc(4 * (int64_t)(2 * P) * (2 << sbits));
+  {
+    KernelTimer kt(s, "c3_transpose", 8.0 * nr * ntiles);
+    hipLaunchKernelGGL(k_c3_transpose, dim3((unsigned)nblk, (nr + 31) / 32), dim3(256), 0, s->stream, meta,
+                       (uint32_t *)meta_t->p, ntiles, nr, run_total, tt, bsum);
+    KERNEL_CHECK();
+  }
+  C5BalArgs a;
+  a.part = part;
+  a.meta_t = (const uint32_t *)meta_t->p;
+  a.run_total = run_total;
+  a.bsum = bsum;
+  a.ntiles = ntiles;
+  a.nblk = nblk;
+  a.tt = (int)tt;
+  a.nsb = nsb;
+  a.sbits = sbits;
+  a.rs8 = (uint32_t)(rstride / 8);
+  a.nwg = P;
+  a.slots = (uint32_t *)slots->p;
+  a.acc = d_acc;
+  {
+    KernelTimer kt(s, "c5_gather", 2.0 * (double)rstride * ntiles);
+    hipLaunchKernelGGL(k_c5_bal_gather, dim3((unsigned)P), dim3(C5_BLOCK), c5bal_lds(sbits), s->stream, a);
+    KERNEL_CHECK();
+  }
+  {
+    KernelTimer kt(s, "chain2_dot", 0.0);
+    hipLaunchKernelGGL(k_c5_bal_fold, dim3((unsigned)nsb), dim3(256), 0, s->stream, a);
+    KERNEL_CHECK();
   }
 }
 
@@ -1634,7 +2178,10 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
                            (uint16_t *)partb->p, (uint32_t *)meta->p, d_acc + 1, rstride);
         KERNEL_CHECK();
       }
-      if (lsub > 0) {
+      if (lsub > 0 && c5s_mode() == 2) {
+        c5_bal_post(s, (const uint16_t *)partb->p, (const uint32_t *)meta->p, ntiles, c.nsb, 16 - lsub,
+                    rstride, d_acc);
+      } else if (lsub > 0) {
         c5_sb_post(s, (const uint16_t *)partb->p, (const uint32_t *)meta->p, ntiles, c.t_in,
                    c.nsb, 16 - lsub, rstride, d_acc);
       } else {
@@ -1647,6 +2194,18 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
         sd.t1[1] = ntiles;
         const int S = c5_slices(nr);
         const int64_t hl = (int64_t)nbl * C2_BW;
+        if (c5s_mode() == 3) {  // apportioned units: slices by unit, variable per run
+          const int umax = s->num_cus + 2 * nr;
+          BufPtr sl = s->alloc(4 * (int64_t)umax * C2_BW);
+          BufPtr tab = s->alloc(8 * (int64_t)nr);
+          uint32_t *sp = (uint32_t *)sl->p;
+          c5_post(s, (const uint16_t *)partb->p, (const uint32_t *)meta->p, sd, ntiles, rstride,
+                  n_in + n_out, (umax + nr - 1) / nr, sp, sp, C2_BW, true, (int32_t *)tab->p);
+          KernelTimer kt(s, "chain2_dot", 4.0 * umax * C2_BW);
+          hipLaunchKernelGGL(k_c5_dot_apportioned, dim3(dot_grid(s->num_cus)), dim3(256), 0, s->stream, sp,
+                             (const int32_t *)tab->p, nbl, d_acc);
+          KERNEL_CHECK();
+        } else {
         BufPtr sl = s->alloc(8 * S * hl);
         uint32_t *si = (uint32_t *)sl->p, *so = si + S * hl;
         // static work list (no units / zero kernels): S tile ranges per run; a
@@ -1660,6 +2219,7 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
         hipLaunchKernelGGL(k_c5_dot_slices, dim3(grid_for(hl / 4, 256, dot_grid(s->num_cus))),
                            dim3(256), 0, s->stream, si, so, S, hl, hl, d_acc);
         KERNEL_CHECK();
+        }
       }
     }
   }

@@ -197,9 +197,93 @@ __global__ __launch_bounds__(EL_BLOCK) void k_el_parse(const uint4 *text, int64_
   if (threadIdx.x == 0 && tot) atomicAdd(kept, tot);
 }
 
+// ------------------------------------------------ K LONG fields per line
+// The node / relationship tables of an FS graph source whose declared fields
+// are all LONG (FSGraphSource.readFromCsv, FSGraphSource.scala:80-84: a
+// CsvTableSource with the canonical field list — id, source, target and
+// INTEGER properties, CAPFGraphExport.scala canonical*FieldReference) parse
+// with the same row rules, one output column per declared field.
+constexpr int CSV_MAXK = 16;
+struct CsvOut {
+  int64_t *col[CSV_MAXK];
+  int k;
+};
+
+template <int SEP1, class B>
+__device__ inline uint32_t csv_line(const B &by, int64_t start, int64_t end, const ElSpec &sp,
+                                    bool &comment, const CsvOut &o, int64_t gl) {
+  if (end > start && by[end - 1] == '\r') --end;
+  comment = sp.comment_len > 0 && end - start >= sp.comment_len;
+  for (int i = 0; comment && i < sp.comment_len; ++i) comment = by[start + i] == sp.comment[i];
+  if (comment) {
+    for (int f = 0; f < o.k; ++f) o.col[f][gl] = 0;
+    return EL_OK;
+  }
+  int64_t p = start;
+  for (int f = 0; f < o.k; ++f) {
+    if (f > 0) {
+      if (p >= end) return EL_TOO_SHORT;  // no delimiter before the end of the line
+      p += sp.sep_len;
+      if (p >= end) return EL_TOO_SHORT;
+    }
+    int64_t v = 0;
+    const uint32_t code = el_parse_long<SEP1>(by, p, end, sp, v);
+    if (code != EL_OK) return code;
+    o.col[f][gl] = v;
+  }
+  return EL_OK;
+}
+
+template <int SEP1>
+__global__ __launch_bounds__(EL_BLOCK) void k_csv_parse(const uint4 *text, int64_t n,
+                                                        const int64_t *chunk_off, int64_t nchunks,
+                                                        int64_t nlines, ElSpec sp, CsvOut o,
+                                                        uint8_t *keep, unsigned long long *err,
+                                                        unsigned long long *kept) {
+  __shared__ uint4 stage[EL_BLOCK];
+  __shared__ uint16_t nlp[EL_CHUNK];
+  __shared__ uint32_t lds_scan[17];
+  __shared__ unsigned long long lds_kept[17];
+  const int64_t b = blockIdx.x, c0 = b * EL_CHUNK;
+  const uint4 q = text[b * EL_BLOCK + threadIdx.x];
+  stage[threadIdx.x] = q;
+  uint32_t m = el_newlines(q), cnt;
+  uint32_t idx = block_exclusive_scan((uint32_t)__popc(m), lds_scan, cnt);
+  while (m) {
+    const int i = __ffs(m) - 1;
+    m &= m - 1;
+    nlp[idx++] = (uint16_t)(16 * threadIdx.x + i);
+  }
+  __syncthreads();
+  const ElLds fast{(const uint8_t *)stage, c0};
+  const int64_t l0 = chunk_off[b];
+  const bool tail = b == nchunks - 1 && l0 + cnt < nlines;
+  const uint32_t items = cnt + (tail ? 1u : 0u);
+  unsigned long long mine = 0;
+  for (uint32_t k = threadIdx.x; k < items; k += EL_BLOCK) {
+    const int64_t gl = l0 + k;
+    const int64_t end = k < cnt ? c0 + nlp[k] : n;
+    bool comment;
+    uint32_t code;
+    if (k > 0) {
+      code = csv_line<SEP1>(fast, c0 + nlp[k - 1] + 1, end, sp, comment, o, gl);
+    } else {
+      const ElAny any{(const uint8_t *)text, (const uint8_t *)stage, c0};
+      int64_t start = c0;
+      while (start > 0 && any[start - 1] != '\n') --start;
+      code = csv_line<SEP1>(any, start, end, sp, comment, o, gl);
+    }
+    if (code != EL_OK) atomicMin(err, ((unsigned long long)gl << 8) | code);
+    mine += comment ? 0 : 1;
+    keep[gl] = comment ? 0 : 1;
+  }
+  const unsigned long long tot = block_reduce_sum(mine, lds_kept);
+  if (threadIdx.x == 0 && tot) atomicAdd(kept, tot);
+}
+
 static const char *el_reason(uint32_t code) {
   switch (code) {
-    case EL_TOO_SHORT: return "Row too short (fewer than 2 fields)";
+    case EL_TOO_SHORT: return "Row too short (fewer fields than declared)";
     case EL_EMPTY: return "empty LONG field";
     case EL_ILLEGAL_CHAR: return "illegal character in a LONG field";
     case EL_OVERFLOW: return "LONG value out of range";
@@ -270,6 +354,63 @@ static DataPtr edge_list_parse_device(Session *s, const BufPtr &text, int64_t nb
   return d;
 }
 
+// Parses the device copy `text` into K INT64 columns (one per declared field).
+static DataPtr csv_longs_parse_device(Session *s, const BufPtr &text, int64_t nbytes, char last,
+                                      const ElSpec &sp, int k) {
+  auto d = std::make_shared<Data>();
+  for (int i = 0; i < k; ++i) d->cols.push_back(make_column(s, Type::Int64, 0, false));
+  if (nbytes == 0) return d;
+  const int64_t nchunks = (nbytes + EL_CHUNK - 1) / EL_CHUNK;
+  BufPtr cnt = s->alloc(8 * nchunks), off = s->alloc(8 * nchunks);
+  {
+    KernelTimer kt(s, "el_count", (double)nchunks * EL_CHUNK);
+    hipLaunchKernelGGL(k_el_count, dim3((unsigned)nchunks), dim3(EL_BLOCK), 0, s->stream,
+                       (const uint4 *)text->p, (int64_t *)cnt->p);
+    KERNEL_CHECK();
+  }
+  const int64_t nl = exclusive_scan_i64(s, (const int64_t *)cnt->p, (int64_t *)off->p, nchunks);
+  const int64_t nlines = nl + (last != '\n' ? 1 : 0);
+  std::vector<ColPtr> cols;
+  CsvOut o{};
+  o.k = k;
+  for (int i = 0; i < k; ++i) {
+    cols.push_back(make_column(s, Type::Int64, nlines, false));
+    o.col[i] = nlines > 0 ? (int64_t *)cols[i]->data->p : nullptr;
+  }
+  BufPtr keep = s->alloc(std::max<int64_t>(nlines, 1));
+  BufPtr flags = s->alloc(16);
+  unsigned long long *d_err = (unsigned long long *)flags->p, *d_kept = d_err + 1;
+  const unsigned long long init[2] = {~0ull, 0ull};
+  HIP_CHECK(hipMemcpyAsync(d_err, init, 16, hipMemcpyHostToDevice, s->stream));
+  if (nlines > 0) {
+    KernelTimer kt(s, "csv_parse", (double)nchunks * EL_CHUNK + 8.0 * k * nlines);
+    hipLaunchKernelGGL(sp.sep_len == 1 ? k_csv_parse<1> : k_csv_parse<0>, dim3((unsigned)nchunks),
+                       dim3(EL_BLOCK), 0, s->stream, (const uint4 *)text->p, nbytes, (const int64_t *)off->p,
+                       nchunks, nlines, sp, o, (uint8_t *)keep->p, d_err, d_kept);
+    KERNEL_CHECK();
+  }
+  unsigned long long h[2];
+  HIP_CHECK(hipMemcpyAsync(h, d_err, 16, hipMemcpyDeviceToHost, s->stream));
+  s->sync();
+  if (h[0] != ~0ull) {
+    char msg[160];
+    snprintf(msg, sizeof msg, "CSV line %lld could not be parsed: %s", (long long)(h[0] >> 8) + 1,
+             el_reason((uint32_t)(h[0] & 0xFF)));
+    illegal(msg);
+  }
+  const int64_t m = (int64_t)h[1];
+  if (m != nlines) {  // comment lines
+    int64_t got = 0;
+    BufPtr idx = compact_flags(s, (const uint8_t *)keep->p, nlines, &got);
+    if (got != m) fail(CAPF_ERR_INTERNAL, "csv: kept-line count mismatch");
+    for (auto &c : cols) c = gather_column(s, c, (const int64_t *)idx->p, m);
+  }
+  d->nrows = m;
+  d->cols = cols;
+  s->sync();
+  return d;
+}
+
 static BufPtr el_text_buffer(Session *s, int64_t nbytes) {
   const int64_t nchunks = (nbytes + EL_CHUNK - 1) / EL_CHUNK;
   BufPtr text = s->alloc(std::max<int64_t>(nchunks, 1) * EL_CHUNK);
@@ -290,13 +431,15 @@ static DataPtr edge_list_parse(Session *s, const char *bytes, int64_t nbytes, co
 constexpr int64_t EL_PIECE = 64ll << 20;
 constexpr int EL_READERS = 8;
 
-static DataPtr edge_list_read_file(Session *s, const char *path, const ElSpec &sp) {
+// File → device text buffer (zero-padded to whole chunks); *len_out / *last_out
+// = the file's size and last byte.
+static BufPtr read_text_file(Session *s, const char *path, int64_t *len_out, char *last_out) {
   const int fd = open(path, O_RDONLY);
-  if (fd < 0) illegal(std::string("edge list: cannot open ") + path);
+  if (fd < 0) illegal(std::string("cannot open ") + path);
   struct stat st;
   if (fstat(fd, &st) != 0) {
     close(fd);
-    illegal(std::string("edge list: cannot stat ") + path);
+    illegal(std::string("cannot stat ") + path);
   }
   const int64_t len = (int64_t)st.st_size;
   char *stage[2] = {nullptr, nullptr};
@@ -346,20 +489,29 @@ static DataPtr edge_list_read_file(Session *s, const char *path, const ElSpec &s
         read_range(done_to, n);
       }
       for (auto &th : rd) th.join();
-      if (bad) illegal(std::string("edge list: short read of ") + path);
+      if (bad) illegal(std::string("short read of ") + path);
       last = stage[b][n - 1];
       HIP_CHECK(hipMemcpyAsync((char *)text->p + off, stage[b], (size_t)n, hipMemcpyHostToDevice,
                                s->stream));
       HIP_CHECK(hipEventRecord(done[b], s->stream));
     }
-    DataPtr d = edge_list_parse_device(s, text, len, last, sp);  // syncs the stream
+    s->sync();
     cleanup();
-    return d;
+    *len_out = len;
+    *last_out = last;
+    return text;
   } catch (...) {
     s->sync();
     cleanup();
     throw;
   }
+}
+
+static DataPtr edge_list_read_file(Session *s, const char *path, const ElSpec &sp) {
+  int64_t len = 0;
+  char last = '\n';
+  BufPtr text = read_text_file(s, path, &len, &last);
+  return edge_list_parse_device(s, text, len, last, sp);  // syncs the stream
 }
 
 static ElSpec el_spec(const char *sep, const char *comment) {
@@ -426,6 +578,67 @@ extern "C" capf_status capf_edge_list_read(capf_session *cs, const char *path, c
   } catch (const capf::Error &e) {
     return record_error(e.code, e.what());
   } catch (const std::exception &e) {  // bad_alloc, system_error, … never cross the C-ABI
+    return record_error(CAPF_ERR_INTERNAL, e.what());
+  }
+}
+
+static capf_table *csv_table(Session *s, DataPtr d, int32_t ncols, const char *const *names) {
+  auto n = std::make_shared<Node>();
+  n->s = s;
+  n->kind = Kind::Source;
+  for (int i = 0; i < ncols; ++i) {
+    n->names.emplace_back(names[i]);
+    n->types.push_back(Type::Int64);
+  }
+  n->result = d;
+  auto *t = new capf_table;
+  t->node = n;
+  return t;
+}
+
+static void csv_args(capf_session *cs, int32_t ncols, const char *const *names, capf_table **out) {
+  if (!cs || !out || !names) illegal("null argument");
+  if (ncols < 1 || ncols > CSV_MAXK) illegal("CSV: 1..16 LONG fields");
+  for (int i = 0; i < ncols; ++i)
+    if (!names[i]) illegal("null column name");
+}
+
+extern "C" capf_status capf_csv_parse_longs(capf_session *cs, const char *bytes, int64_t nbytes,
+                                            const char *sep, int32_t ncols, const char *const *names,
+                                            capf_table **out) {
+  try {
+    csv_args(cs, ncols, names, out);
+    if (nbytes < 0 || (nbytes > 0 && !bytes)) illegal("bad byte buffer");
+    const ElSpec sp = el_spec(sep, nullptr);
+    Session *s = &cs->impl;
+    BufPtr text = el_text_buffer(s, nbytes);
+    if (nbytes > 0) HIP_CHECK(hipMemcpyAsync(text->p, bytes, nbytes, hipMemcpyHostToDevice, s->stream));
+    DataPtr d = csv_longs_parse_device(s, text, nbytes, nbytes > 0 ? bytes[nbytes - 1] : '\n', sp, ncols);
+    *out = csv_table(s, d, ncols, names);
+    return CAPF_OK;
+  } catch (const capf::Error &e) {
+    return record_error(e.code, e.what());
+  } catch (const std::exception &e) {
+    return record_error(CAPF_ERR_INTERNAL, e.what());
+  }
+}
+
+extern "C" capf_status capf_csv_read_longs(capf_session *cs, const char *path, const char *sep,
+                                           int32_t ncols, const char *const *names, capf_table **out) {
+  try {
+    csv_args(cs, ncols, names, out);
+    if (!path) illegal("null argument");
+    const ElSpec sp = el_spec(sep, nullptr);
+    Session *s = &cs->impl;
+    int64_t len = 0;
+    char last = '\n';
+    BufPtr text = read_text_file(s, path, &len, &last);
+    DataPtr d = csv_longs_parse_device(s, text, len, last, sp, ncols);
+    *out = csv_table(s, d, ncols, names);
+    return CAPF_OK;
+  } catch (const capf::Error &e) {
+    return record_error(e.code, e.what());
+  } catch (const std::exception &e) {
     return record_error(CAPF_ERR_INTERNAL, e.what());
   }
 }

@@ -154,6 +154,21 @@ class GpuSession:
             _lib.call("capf_edge_list_read", self._h, os.fsencode(source), sep.encode(), com, *names, byref(h))
         return GpuTable(self, h)
 
+    def csv_read_longs(self, path, sep, names):
+        """A CSV table whose declared fields are all LONG, parsed on the GPU
+        (capf_csv_read_longs; FSGraphSource.readFromCsv)."""
+        h = c_void_p()
+        _lib.call("capf_csv_read_longs", self._h, os.fsencode(path), sep.encode(), len(names),
+                  _lib.strs(list(names)), byref(h))
+        return GpuTable(self, h)
+
+    def csv_parse_longs(self, data, sep, names):
+        h = c_void_p()
+        buf = bytes(data)
+        _lib.call("capf_csv_parse_longs", self._h, buf, len(buf), sep.encode(), len(names),
+                  _lib.strs(list(names)), byref(h))
+        return GpuTable(self, h)
+
     def var_length_reach(self, rels, src_col, dst_col, sources, source_id_col, targets, target_id_col,
                          lower, upper, out_source_col, out_reach_col):
         """Fused VarLengthExpand → Distinct(a, b) → Aggregate(a, count(*))

@@ -396,6 +396,19 @@ capf_status capf_chain2_local_hists(capf_session *s, capf_table *rels, const cha
 capf_status capf_dot_u32(capf_session *s, const uint32_t *d_a, const uint32_t *d_b, int64_t n,
                          uint64_t *out);
 
+/* CSV tables of an FS graph source whose declared fields are all LONG
+ * (FSGraphSource.readFromCsv, flink-cypher/.../api/io/fs/FSGraphSource.scala:80-84:
+ * Flink's CsvTableSource over the canonical field list of CAPFGraphExport —
+ * id, source, target and INTEGER properties).  One INT64 column per declared
+ * field, in file order; row rules as capf_edge_list_read (LongParser, trailing
+ * '\r' stripped, short rows / empty fields / overflow fail the read naming the
+ * line); text after the last declared field is not read.  ncols ≤ 16.      */
+capf_status capf_csv_parse_longs(capf_session *s, const char *bytes, int64_t nbytes,
+                                 const char *sep, int32_t ncols, const char *const *names,
+                                 capf_table **out);
+capf_status capf_csv_read_longs(capf_session *s, const char *path, const char *sep,
+                                int32_t ncols, const char *const *names, capf_table **out);
+
 /* ------------------------------------------------- distributed Table layer
  * The exchange of a hash-partitioned Table over G ranks (dist_table.py):
  * Flink's join and groupBy repartition both inputs by a hash of the key

@@ -548,6 +548,23 @@ JNI(jlong, chain2LocalHists)(JNIEnv *env, jobject, jlong s, jlong rels, jstring 
                                     reinterpret_cast<uint32_t *>(d_out), &loops));
   return loops;
 }
+// FS graph source: all-LONG CSV tables parsed on the GPU
+JNI(jlong, csvReadLongs)(JNIEnv *env, jobject, jlong s, jstring path, jstring sep, jobjectArray names) {
+  JStr p(env, path), d(env, sep);
+  JStrs nm(env, names);
+  capf_table *out = nullptr;
+  return fail(env, capf_csv_read_longs(S(s), p.p, d.p, nm.n(), nm.data(), &out)) ? 0 : H(out);
+}
+JNI(jlong, csvParseLongs)(JNIEnv *env, jobject, jlong s, jobject bytes, jlong nbytes, jstring sep,
+                          jobjectArray names) {
+  JStr d(env, sep);
+  JStrs nm(env, names);
+  capf_table *out = nullptr;
+  return fail(env, capf_csv_parse_longs(S(s), (const char *)direct(env, bytes), nbytes, d.p, nm.n(),
+                                        nm.data(), &out))
+             ? 0
+             : H(out);
+}
 // distributed Table layer: hash routing + device-side column copies; the
 // JVM side moves the [off[p], off[p+1]) slices with its collective library
 // (counts → countsOut[0..parts))

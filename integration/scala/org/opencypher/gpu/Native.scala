@@ -154,6 +154,10 @@ object Native {
   @native def chain2LocalHists(session: Long, rels: Long, srcCol: String, dstCol: String, nodeBase: Long,
                                nNodes: Long, dIn: Long, dOut: Long): Long
   @native def dotU32(session: Long, dA: Long, dB: Long, n: Long): Long
+  // FS graph source: all-LONG CSV tables (FSGraphSource.scala:80-84) parsed on the GPU
+  @native def csvReadLongs(session: Long, path: String, sep: String, names: Array[String]): Long
+  @native def csvParseLongs(session: Long, bytes: java.nio.ByteBuffer, nBytes: Long, sep: String,
+                            names: Array[String]): Long
   // distributed Table layer (dist_table.py): rows grouped by owner h(keys), counts per owner
   @native def tableHashRoute(table: Long, keys: Array[String], parts: Int, countsOut: Array[Long]): Long
   @native def tableDownloadDevice(table: Long, col: String, dValues: Long, dValid: Long): Unit

@@ -511,13 +511,17 @@ def test_two_hop_hub_overflow(gpu_session, monkeypatch, n, compact):
     assert got == cmodel.count_2hop(src.astype(np.int64), dst.astype(np.int64), n)
 
 
+@pytest.mark.parametrize("mode", ["0", "2", "3"], ids=["slices", "balanced", "apportioned"])
 @pytest.mark.parametrize("compact", [False, True, 3], ids=["int64", "for32", "for24"])
-@pytest.mark.parametrize("scale,parts", [(10, 2), (16, 1), (16, 3), (18, 4), (18, 3)])
-def test_sharded_two_hop_partials(gpu_session, compact, scale, parts):
+@pytest.mark.parametrize("scale,parts", [(10, 2), (16, 1), (16, 3), (18, 4), (18, 3), (20, 8)])
+def test_sharded_two_hop_partials(gpu_session, compact, scale, parts, mode, monkeypatch):
     """Node-partitioned layout (dist.py): every part's in/out copies hold
     exactly the rels whose target/source it owns, each part's on-device
     partial Σ_{owned b} in·out − owned loops equals the oracle's, and the
-    partials sum to the closed-form 2-hop count (what the all-reduce forms)."""
+    partials sum to the closed-form 2-hop count (what the all-reduce forms).
+    Both P3 forms of a rank: histogram slices + dot, and balanced key ranges
+    over sub-buckets (split sub-buckets folded from their slots)."""
+    monkeypatch.setenv("CAPF_SHARD_SB", mode)
     import torch
     from capf_amd.dist import node_partitioned_copies
     from capf_amd.table import chain2_sharded_count_async
@@ -532,7 +536,7 @@ def test_sharded_two_hop_partials(gpu_session, compact, scale, parts):
     own_d = nodemix.owner(dst, n, parts)
     total = 0
     for p in range(parts):
-        in_copy, out_copy = node_partitioned_copies(t, n, parts, p)
+        in_copy, out_copy = node_partitioned_copies(t, n, parts, p, compact=compact)
         if not compact:  # keep the copies int64 (node_partitioned_copies compacts)
             in_copy = t.node_partition("target", 0, n, parts, p)
             out_copy = t.node_partition("source", 0, n, parts, p)

@@ -369,6 +369,10 @@ struct C3Sides {
   int nb;              // runs per side: runs [0, nb) in, [nb, 2·nb) out
   int64_t t0[2], t1[2];  // tile range holding each side's segments
   int split_x16;       // a run is split when it holds > split_x16/16 × the mean
+  int packed = 0;      // static units store their counters as packed uint16 pairs
+                       // (word i of bucket b of slice k at (k·nb + b)·2^15 + i); the
+                       // hand-off log then holds side bins b·2^16 + key, applied by
+                       // k_c5_dot_packed (no k_c3_overflow)
 };
 
 // CAPF_P3_SPLIT (tuning): split threshold in units of the mean run size
@@ -703,6 +707,7 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
   }
   const uint32_t side = u.run >= nb ? 1u : 0u;
   uint32_t *hist = side ? h_out : h_in;
+  const uint32_t log_base = (uint32_t)((int64_t)(u.run % nb) * C2_BW);  // packed: side bin of key 0
   const uint32_t hist_base = sch.run_total ? (uint32_t)((int64_t)u.slice * C2_BW)
                                            : (uint32_t)(u.slice * slice_stride + (int64_t)(u.run % nb) * C2_BW);
   for (int i = threadIdx.x; i < C2_WORDS + C5_CORR; i += C5_BLOCK) words[i] = 0;
@@ -850,7 +855,8 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
           const uint32_t sh = (key >> 15) << 4;
           const uint32_t oh = (old[j][e] >> sh) & 0xFFFFu;
           if (oh < 0x8000u && oh + inc >= 0x8000u)
-            c3_handoff(&words[key & (C2_WORDS - 1)], 1u << sh, hist_base + key, side, ovf);
+            c3_handoff(&words[key & (C2_WORDS - 1)], 1u << sh, (sd.packed ? log_base : hist_base) + key,
+                       side, ovf);
         }
       }
     }
@@ -960,10 +966,15 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
     const unsigned long long th = wave_reduce_sum((unsigned long long)nh);
     if (lane == 0 && th) {
       const uint32_t k = atomicAdd(ovf.n, 1u);
-      if (k < ovf.cap) ovf.log[k] = make_uint2(hist_base + H, side | ((uint32_t)th << 1));
+      if (k < ovf.cap)
+        ovf.log[k] = make_uint2((sd.packed ? log_base : hist_base) + H, side | ((uint32_t)th << 1));
     }
   }
   __syncthreads();
+  if (sd.packed) {  // exclusive static unit: one packed word per bin pair
+    uint32_t *h = hist + ((int64_t)u.slice * nb + u.run % nb) * C2_WORDS;
+    for (int i = threadIdx.x; i < C2_WORDS; i += C5_BLOCK) h[i] = words[i] - (i < C5_CORR ? corr[i] : 0u);
+  } else
   for (int i = threadIdx.x; i < C2_WORDS; i += C5_BLOCK) {
     const uint32_t w = words[i];
     const uint32_t lo = (w & 0xFFFF) - (i < C5_CORR ? corr[i] : 0u), hi = w >> 16;
@@ -1026,7 +1037,8 @@ static void launch_c5(Session *s, const C5Cols<W> &c, uint16_t *part, uint32_t *
 static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, const C3Sides &sd,
                     int64_t ntiles, int64_t rstride, int64_t nkeys, int S, uint32_t *h_in,
                     uint32_t *h_out, int64_t slice_stride, bool static_units = false,
-                    int32_t *apportion_table = nullptr) {
+                    int32_t *apportion_table = nullptr, C3Ovf *packed_ovf = nullptr,
+                    BufPtr *keep = nullptr) {
   const int nr = 2 * sd.nb;
   const bool app = apportion_table != nullptr;  // apportioned units (C5Sched), slices by unit
   static bool attr_set = false;
@@ -1128,7 +1140,10 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
                        transpose ? (int64_t)1 : (int64_t)nr, sch);
     KERNEL_CHECK();
   }
-  {
+  if (sd.packed) {  // the hand-offs are applied by k_c5_dot_packed
+    *packed_ovf = ovf;
+    *keep = acc;
+  } else {
     KernelTimer kt(s, "c3_overflow", 0.0);
     hipLaunchKernelGGL(k_c3_overflow, dim3(16), dim3(256), 0, s->stream, ovf, h_in, h_out);
     KERNEL_CHECK();
@@ -1163,13 +1178,13 @@ __global__ __launch_bounds__(256) void k_c5_fold(const uint32_t *si, const uint3
 }
 
 // acc[0] += Σ_i (Σ_s in_s[i])·(Σ_s out_s[i]) (n a multiple of 4).
-__global__ __launch_bounds__(256) void k_c5_dot_slices(const uint32_t *si, const uint32_t *so,
-                                                        int S, int64_t stride, int64_t n,
-                                                        unsigned long long *acc) {
+__global__ __launch_bounds__(1024) void k_c5_dot_slices(const uint32_t *si, const uint32_t *so,
+                                                         int S, int64_t stride, int64_t n,
+                                                         unsigned long long *acc) {
   __shared__ unsigned long long lds[17];
   unsigned long long t = 0;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n / 4;
-       i += (int64_t)gridDim.x * 256) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n / 4;
+       i += (int64_t)gridDim.x * blockDim.x) {
     uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(0, 0, 0, 0);
     for (int k = 0; k < S; ++k) {
       const uint4 x = ((const uint4 *)(si + k * stride))[i];
@@ -1213,6 +1228,62 @@ __global__ __launch_bounds__(256) void k_c5_dot_apportioned(const uint32_t *sl, 
     }
     t += (unsigned long long)x.x * y.x + (unsigned long long)x.y * y.y + (unsigned long long)x.z * y.z +
          (unsigned long long)x.w * y.w;
+  }
+  unsigned long long tot;
+  block_exclusive_scan(t, lds, tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(acc, tot);
+}
+
+// Σ_b in·out over packed slices (S per side, words as laid out by C3Sides::packed)
+// plus the hand-off log: a logged bin g gets in_g = Σ_s half + Σ its side-0
+// counts, out_g likewise, and adds in_g·out_g − (Σ halves)·(Σ halves) once (at
+// its first log entry; every block takes every grid-th entry).
+__device__ inline uint32_t packed_half_sum(const uint32_t *sl, int S, int64_t stride, int64_t g) {
+  const int64_t w = (g >> C2_BITS) * C2_WORDS + (g & (C2_WORDS - 1));
+  const int sh = (int)((g >> 15) & 1) * 16;
+  uint32_t x = 0;
+  for (int k = 0; k < S; ++k) x += (sl[k * stride + w] >> sh) & 0xFFFFu;
+  return x;
+}
+
+__global__ __launch_bounds__(1024) void k_c5_dot_packed(const uint32_t *si, const uint32_t *so, int S,
+                                                        int64_t stride, int64_t nwords, C3Ovf ovf,
+                                                        unsigned long long *acc) {
+  __shared__ unsigned long long lds[17];
+  unsigned long long t = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nwords / 4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t a[8] = {0, 0, 0, 0, 0, 0, 0, 0}, b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int k = 0; k < S; ++k) {
+      const uint4 x = ((const uint4 *)(si + k * stride))[i];
+      const uint4 y = ((const uint4 *)(so + k * stride))[i];
+      const uint32_t xs[4] = {x.x, x.y, x.z, x.w}, ys[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        a[2 * q] += xs[q] & 0xFFFFu;
+        a[2 * q + 1] += xs[q] >> 16;
+        b[2 * q] += ys[q] & 0xFFFFu;
+        b[2 * q + 1] += ys[q] >> 16;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t += (unsigned long long)a[q] * b[q];
+  }
+  const uint32_t n = min(*ovf.n, ovf.cap);
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const uint32_t g = ovf.log[e].x;
+    bool first = true;
+    for (uint32_t j = 0; j < e && first; ++j) first = ovf.log[j].x != g;
+    if (!first) continue;
+    unsigned long long cin = 0, cout = 0;
+    for (uint32_t j = e; j < n; ++j) {
+      const uint2 f = ovf.log[j];
+      if (f.x != g) continue;
+      if (f.y & 1u) cout += f.y >> 1;
+      else cin += f.y >> 1;
+    }
+    const unsigned long long bi = packed_half_sum(si, S, stride, g), bo = packed_half_sum(so, S, stride, g);
+    t += (bi + cin) * (bo + cout) - bi * bo;
   }
   unsigned long long tot;
   block_exclusive_scan(t, lds, tot);
@@ -1278,10 +1349,16 @@ struct C5Shard {
   int lsub, nsb;                 // 2^lsub sub-bucket runs per bucket and side; nsb = nbl << lsub
   int copies;                    // run counters per run (power of 2, see below)
   int gpt;                       // 4096-row groups per tile (≤ 4): tile = 4096·gpt rows
+  int nhot;                      // heavy hitters (≤ C5S_MAXHOT): keys equal to hot[j] are
+  uint32_t hot[2];               // counted per wave, not partitioned (node_mix(id − lo))
+  int64_t n_diag;                // out-copy rows [0, n_diag) may be self-loops (2-D layout:
+                                 // rows whose target is owned too come first); the
+                                 // target column is read for those rows only
   NodeMix mix;
 };
 
 constexpr int C5S_TILE = 32768;  // rows (= keys) per tile (at most); 16384 via CAPF_SHARD_TILE=16
+constexpr int C5S_MAXHOT = 1;    // heavy-hitter keys of a rank (sampled at ingest, a plan hint)
 constexpr int C5S_MAXR = 520;    // runs incl. the dummy: nbl ≤ 259
 constexpr int C5S_CNT = 1024;    // LDS run counters: copies · (runs + 1) ≤ 1024
 
@@ -1295,9 +1372,9 @@ static int c5s_copies(int nr) {
   return c;
 }
 
-template <int W, bool WIDE, int TILE>
+template <int W, bool WIDE, int TILE, bool HOT>
 __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_c5_shard_partition(
-    C5Shard c, uint16_t *part, uint32_t *meta, unsigned long long *loops, int64_t rstride) {
+    C5Shard c, uint16_t *part, uint32_t *meta, uint32_t *tile_acc, int64_t rstride) {
   constexpr int MAXR = C5S_MAXR;
   constexpr int RPT = TILE / C5_BLOCK, GROUPS = RPT / 4;
   constexpr int STAGE = TILE + 8 * MAXR;
@@ -1305,7 +1382,7 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   __shared__ uint4 stage4[STAGE / 8];
   __shared__ uint32_t cur[C5S_CNT];
   __shared__ uint32_t lds_scan[17];
-  __shared__ uint32_t body_end;
+  __shared__ uint32_t body_end, dummy_n;
   uint16_t *stage = (uint16_t *)stage4;
   const int64_t t = blockIdx.x;
   const int side = t >= c.t_in ? 1 : 0;  // block-uniform
@@ -1321,6 +1398,7 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   const int64_t ts = side ? t - c.t_in : t;
   const int64_t rows = (int64_t)c.gpt * 4 * C5_BLOCK;
   const int64_t e0 = ts * rows, e1 = min(e0 + rows, side ? c.n_out : c.n_in);
+  const bool chk = side && e0 < c.n_diag;  // block-uniform: this tile needs the loop test
   // groups holding rows of this tile (uniform): later groups are skipped, so a
   // short tile never floods the dummy run's counter
   const int gu = (int)min<int64_t>(c.gpt, (e1 - e0 + 4 * C5_BLOCK - 1) / (4 * C5_BLOCK));
@@ -1331,13 +1409,17 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   const uint32_t lsub = (uint32_t)c.lsub, ssh = 16u - lsub;  // h & 0xFFFF >> 16 = 0: no sub-buckets
   uint32_t key[RPT];
   uint32_t lp = 0;
+  // heavy hitter (skew handling): keys whose mixed index is c.hot[0] are not
+  // partitioned but counted at the end from the dummy run's stage slots — one
+  // compare per key and no counter register (32 keys per thread already fill
+  // the VGPR budget); no hint = 0xFFFFFFFF, never a mixed index
   // the next group's loads are issued before this group's hashing/counting
   uint32_t px[2][4], py[2][4];
   bool pox[2][4], poy[2][4];
   {
     const int64_t e = e0 + 4 * (int64_t)threadIdx.x;
     c5_load4<W, true>(kp, kb, c.lo, c.len, e, e1, true, px[0], pox[0]);
-    if (side) c5_load4<W, true>(c.oth, c.both, c.lo, c.len, e, e1, true, py[0], poy[0]);
+    if (chk) c5_load4<W, true>(c.oth, c.both, c.lo, c.len, e, e1, true, py[0], poy[0]);
   }
 #pragma unroll
   for (int g = 0; g < GROUPS; ++g) {
@@ -1345,11 +1427,15 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
       if (g + 1 < gu) {
         const int64_t en = e0 + 4 * ((int64_t)(g + 1) * C5_BLOCK + threadIdx.x);
         c5_load4<W, true>(kp, kb, c.lo, c.len, en, e1, true, px[(g + 1) & 1], pox[(g + 1) & 1]);
-        if (side)
+        if (chk)
           c5_load4<W, true>(c.oth, c.both, c.lo, c.len, en, e1, true, py[(g + 1) & 1], poy[(g + 1) & 1]);
       }
       uint32_t x[4], y[4];
       bool okx[4], oky[4];
+      // rows of this group's 4 that lie in the diagonal block (2-D order)
+      const uint32_t dg = chk ? (uint32_t)min<int64_t>(max<int64_t>(
+                                    c.n_diag - (e0 + 4 * ((int64_t)g * C5_BLOCK + threadIdx.x)), 0), 4)
+                              : 0u;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         x[k] = px[g & 1][k];
@@ -1362,9 +1448,13 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
         const uint32_t h = node_mix_t<WIDE>(x[k], c.mix);
         const uint32_t b = (h >> C2_BITS) - (uint32_t)c.b0;  // wraps when below b0
         const bool ok = okx[k] && b < (uint32_t)c.nbl;
+        // a heavy hitter goes to the dummy run: counted here, never copied out
+        // the heavy hitter (mixed index) goes to the dummy run as key 1 (past-the-end
+        // rows as key 0): never copied out, counted in the dummy run's stage slots
         const uint32_t run = run0 + (b << lsub) + ((h & 0xFFFF) >> ssh);
-        key[4 * g + k] = ok ? (run << C2_BITS) | (h & 0xFFFF) : dummy;
-        if (side) lp += (ok && oky[k] && x[k] == y[k]) ? 1u : 0u;
+        key[4 * g + k] = HOT ? (ok && h != c.hot[0] ? (run << C2_BITS) | (h & 0xFFFF) : dummy | (ok ? 1u : 0u))
+                             : (ok ? (run << C2_BITS) | (h & 0xFFFF) : dummy);
+        if (chk) lp += (ok && oky[k] && x[k] == y[k] && (uint32_t)k < dg) ? 1u : 0u;
         atomicAdd(&cur[(key[4 * g + k] >> C2_BITS) * C + my_copy], 1u);
       }
     }
@@ -1389,7 +1479,10 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
     }
   }
   if (r < nr) meta[t * nr + r] = (ex >> 3) | (cnt << 16);
-  if (r == nr) body_end = ex;  // the dummy run (last) is not copied out
+  if (r == nr) {
+    body_end = ex;  // the dummy run (last) is not copied out
+    dummy_n = cnt;
+  }
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < RPT; ++j) {
@@ -1399,8 +1492,41 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   __syncthreads();
   uint4 *dst = (uint4 *)(part + t * rstride);
   for (uint32_t i = threadIdx.x; i < body_end / 8; i += C5_BLOCK) dst[i] = stage4[i];
-  unsigned long long lp64 = wave_reduce_sum((unsigned long long)lp);
-  if (lane_id() == 0 && lp64) atomicAdd(loops, lp64);
+  // the heavy hitter's keys of this tile: the 1s of the dummy run's slots
+  uint32_t hn = 0;
+  if (HOT)
+    for (uint32_t i = threadIdx.x; i < dummy_n; i += C5_BLOCK) hn += stage[body_end + i] == 1 ? 1u : 0u;
+  // per-tile (self-loops, hot keys) with plain stores, summed by k_sharded_final:
+  // one same-address device atomic per wave serialises at the memory side
+  // (~88 per µs on one word: 2·10^3 tiles × 16 waves ≈ 0.37 ms)
+  __shared__ uint32_t red[2][C5_BLOCK / WAVE];
+  const uint32_t l32 = (uint32_t)wave_reduce_sum((unsigned long long)lp);
+  const uint32_t h32 = (uint32_t)wave_reduce_sum((unsigned long long)hn);
+  if (lane_id() == 0) {
+    red[0][threadIdx.x / WAVE] = l32;
+    red[1][threadIdx.x / WAVE] = h32;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    uint32_t v = 0;
+    for (int w = 0; w < C5_BLOCK / WAVE; ++w) v += red[threadIdx.x][w];
+    tile_acc[2 * t + threadIdx.x] = v;
+  }
+}
+
+// this rank's partial: Σ in·out over the partitioned keys (acc[0]) + hot_in·hot_out −
+// self-loops; tile_acc = (loops, hot keys) per P1 tile, tiles [0, t_in) in-copy
+__global__ __launch_bounds__(1024) void k_sharded_final(const unsigned long long *acc, const uint32_t *tile_acc,
+                                                        int64_t ntiles, int64_t t_in, int64_t *out) {
+  __shared__ unsigned long long lds[3][17];
+  unsigned long long lp = 0, hi = 0, ho = 0;
+  for (int64_t t = threadIdx.x; t < ntiles; t += blockDim.x) {
+    lp += tile_acc[2 * t];
+    (t < t_in ? hi : ho) += tile_acc[2 * t + 1];
+  }
+  const unsigned long long L = block_reduce_sum(lp, lds[0]), I = block_reduce_sum(hi, lds[1]),
+                           O = block_reduce_sum(ho, lds[2]);
+  if (threadIdx.x == 0) *out = (int64_t)(acc[0] + I * O - L);
 }
 
 // ---------------------------------------------- sharded P3, sub-bucket units
@@ -2051,10 +2177,14 @@ static void c5_bal_post(Session *s, const uint16_t *part, const uint32_t *meta, 
 }
 
 template <int TILE>
-static auto c5s_kernel(int W, bool wide) {
-  return W == 3 ? (wide ? k_c5_shard_partition<3, true, TILE> : k_c5_shard_partition<3, false, TILE>)
-         : W == 4 ? (wide ? k_c5_shard_partition<4, true, TILE> : k_c5_shard_partition<4, false, TILE>)
-                  : (wide ? k_c5_shard_partition<8, true, TILE> : k_c5_shard_partition<8, false, TILE>);
+static auto c5s_kernel(int W, bool wide, bool hot) {
+  if (hot)  // a heavy-hitter hint: one more compare per key (only ranks that hold a hub pay it)
+    return W == 3 ? (wide ? k_c5_shard_partition<3, true, TILE, true> : k_c5_shard_partition<3, false, TILE, true>)
+           : W == 4 ? (wide ? k_c5_shard_partition<4, true, TILE, true> : k_c5_shard_partition<4, false, TILE, true>)
+                    : (wide ? k_c5_shard_partition<8, true, TILE, true> : k_c5_shard_partition<8, false, TILE, true>);
+  return W == 3 ? (wide ? k_c5_shard_partition<3, true, TILE, false> : k_c5_shard_partition<3, false, TILE, false>)
+         : W == 4 ? (wide ? k_c5_shard_partition<4, true, TILE, false> : k_c5_shard_partition<4, false, TILE, false>)
+                  : (wide ? k_c5_shard_partition<8, true, TILE, false> : k_c5_shard_partition<8, false, TILE, false>);
 }
 
 // Buckets of 64 Ki mixed node indexes owned by `part` of `parts`.
@@ -2087,6 +2217,43 @@ __global__ void k_owner_flags(ColView key, int64_t n, int64_t lo, NodeMix mix, i
   }
 }
 
+// 2-D split of a rank's out-copy: f_diag = source and target owned by `part`,
+// f_off = source owned, target not.
+__global__ void k_owner_flags2(ColView src, ColView dst, int64_t n, int64_t lo, NodeMix mix, int wide,
+                               int64_t nb, int parts, int part, uint8_t *f_diag, uint8_t *f_off) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const bool so = owner_of((uint32_t)(ld_int(src, i) - lo), mix, wide != 0, nb, parts) == part;
+    const bool dw = owner_of((uint32_t)(ld_int(dst, i) - lo), mix, wide != 0, nb, parts) == part;
+    f_diag[i] = so && dw;
+    f_off[i] = so && !dw;
+  }
+}
+
+// Gather index of the out-copy in 2-D order: the rows whose source AND target
+// `part` owns first (*n_diag of them), then the rows whose source only it owns.
+BufPtr node_partition_diag_index(Session *s, const ColView &src, const ColView &dst, int64_t n, int64_t lo,
+                                 int64_t n_nodes, int parts, int part, int64_t *m, int64_t *n_diag) {
+  const int kbits = chain2_hist_bits(n_nodes);
+  const int64_t n1 = std::max<int64_t>(n, 1);
+  BufPtr fl = s->alloc(2 * n1);
+  uint8_t *fd = (uint8_t *)fl->p, *fo = fd + n1;
+  if (n > 0) {
+    hipLaunchKernelGGL(k_owner_flags2, dim3(grid_for(n, 256)), dim3(256), 0, s->stream, src, dst, n, lo,
+                       node_mix_for(kbits), (int)(kbits > 24), (int64_t(1) << kbits) / C2_BW, parts, part,
+                       fd, fo);
+    KERNEL_CHECK();
+  }
+  int64_t a = 0, b = 0;
+  BufPtr ia = compact_flags(s, fd, n, &a), ib = compact_flags(s, fo, n, &b);
+  BufPtr idx = s->alloc(8 * std::max<int64_t>(a + b, 1));
+  if (a) HIP_CHECK(hipMemcpyAsync(idx->p, ia->p, 8 * a, hipMemcpyDeviceToDevice, s->stream));
+  if (b) HIP_CHECK(hipMemcpyAsync((int64_t *)idx->p + a, ib->p, 8 * b, hipMemcpyDeviceToDevice, s->stream));
+  *m = a + b;
+  *n_diag = a;
+  return idx;
+}
+
 uint8_t *node_owner_flags(Session *s, const ColView &key, int64_t n, int64_t lo, int64_t n_nodes,
                           int parts, int part, BufPtr &keep) {
   const int kbits = chain2_hist_bits(n_nodes);
@@ -2105,7 +2272,8 @@ uint8_t *node_owner_flags(Session *s, const ColView &key, int64_t n, int64_t lo,
 // cols = {in-copy target, out-copy source, out-copy target}; all plain or all
 // FOR32, 16-B aligned, non-null.  Histograms live in session scratch.
 bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out, int64_t lo,
-                    int64_t n_nodes, int parts, int part, int64_t *d_partial) {
+                    int64_t n_nodes, int parts, int part, int64_t *d_partial, int64_t n_diag,
+                    int nhot, const int64_t *hot_ids) {
   const int kbits = chain2_hist_bits(n_nodes);
   int b0, nbl;
   owned_buckets(kbits, parts, part, &b0, &nbl);
@@ -2122,7 +2290,27 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
   const int W = n24 == 3 ? 3 : nf == 3 ? 4 : 8;
   BufPtr acc = s->alloc(16);
   HIP_CHECK(hipMemsetAsync(acc->p, 0, 16, s->stream));
-  unsigned long long *d_acc = (unsigned long long *)acc->p;  // [0] Σ in·out, [1] loops
+  unsigned long long *d_acc = (unsigned long long *)acc->p;  // [0] Σ in·out
+  BufPtr tacc;  // P1's per-tile (self-loops, hot keys)
+  uint32_t *tile_acc = nullptr;
+  int64_t ntiles_all = 0, t_in_all = 0;
+  // heavy hitters: distinct ids inside the node range (others could never match a key)
+  uint32_t hot[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};  // mixed indexes (< 2^31: never all ones)
+  int nh = 0;
+  {
+    const NodeMix mx = node_mix_for(kbits);
+    for (int i = 0; i < nhot && hot_ids && nh < C5S_MAXHOT; ++i) {
+      const int64_t x = hot_ids[i] - lo;
+      if (x < 0 || x >= n_nodes) continue;
+      const uint32_t ux = (uint32_t)x;
+      uint32_t hh = mx.wide ? ux * NODE_MIX_A : (uint32_t)((uint64_t)(ux & 0xFFFFFFu) * NODE_MIX_A);
+      hh &= mx.mask;
+      hh ^= hh >> mx.sh;
+      bool dup = false;
+      for (int j = 0; j < nh; ++j) dup |= hot[j] == hh;
+      if (!dup) hot[nh++] = hh;
+    }
+  }
   if (nbl > 0) {
     C5Shard c;
     c.kin = cols[0].data;
@@ -2133,6 +2321,10 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
     c.both = W != 8 ? cols[2].base : 0;
     c.n_in = n_in;
     c.n_out = n_out;
+    c.n_diag = n_diag < 0 ? n_out : std::min(n_diag, n_out);
+    c.nhot = nh;
+    c.hot[0] = hot[0];
+    c.hot[1] = hot[1];
     // tile size: whole rounds of resident blocks (2 per CU), counting one
     // group of per-tile overhead (stage fill, scan, copy-out)
     const char *te = getenv("CAPF_SHARD_TILE");  // tuning: 16 → 16 Ki-row tiles
@@ -2155,6 +2347,10 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
     c.t_in = (n_in + trows - 1) / trows;
     const int64_t t_out = (n_out + trows - 1) / trows;
     const int64_t ntiles = c.t_in + t_out;
+    tacc = s->alloc(8 * std::max<int64_t>(ntiles, 1));
+    tile_acc = (uint32_t *)tacc->p;
+    ntiles_all = ntiles;
+    t_in_all = c.t_in;
     c.lo = lo;
     c.len = (uint64_t)n_nodes;
     c.b0 = b0;
@@ -2173,9 +2369,10 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
       BufPtr meta = s->alloc(4 * nr * ntiles);
       {
         KernelTimer kt(s, "c5_partition", (double)W * (n_in + 2 * n_out));
-        auto kern = tile == C5S_TILE ? c5s_kernel<C5S_TILE>(W, kbits > 24) : c5s_kernel<16384>(W, kbits > 24);
+        auto kern = tile == C5S_TILE ? c5s_kernel<C5S_TILE>(W, kbits > 24, nh > 0)
+                                     : c5s_kernel<16384>(W, kbits > 24, nh > 0);
         hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(C5_BLOCK), 0, s->stream, c,
-                           (uint16_t *)partb->p, (uint32_t *)meta->p, d_acc + 1, rstride);
+                           (uint16_t *)partb->p, (uint32_t *)meta->p, tile_acc, rstride);
         KERNEL_CHECK();
       }
       if (lsub > 0 && c5s_mode() == 2) {
@@ -2206,6 +2403,23 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
                              (const int32_t *)tab->p, nbl, d_acc);
           KERNEL_CHECK();
         } else {
+        const char *pk = getenv("CAPF_SHARD_PACKED");  // tuning: 0 = uint32 slices + overflow kernel
+        sd.packed = !(pk && atoi(pk) == 0);
+        if (sd.packed) {
+          // packed uint16 slices: half the slice bytes written by P3 and read by the dot
+          const int64_t hw = (int64_t)nbl * C2_WORDS;
+          BufPtr sl = s->alloc(8 * S * hw);
+          uint32_t *si = (uint32_t *)sl->p, *so = si + S * hw;
+          const char *st = getenv("CAPF_SHARD_STATIC");  // tuning: 0 = device work list
+          C3Ovf ovf;
+          BufPtr keep;
+          c5_post(s, (const uint16_t *)partb->p, (const uint32_t *)meta->p, sd, ntiles, rstride,
+                  n_in + n_out, S, si, so, hw, !(st && atoi(st) == 0), nullptr, &ovf, &keep);
+          KernelTimer kt(s, "chain2_dot", 8.0 * S * hw);
+          hipLaunchKernelGGL(k_c5_dot_packed, dim3(grid_for(hw / 4, 1024, dot_grid(s->num_cus))), dim3(1024),
+                             0, s->stream, si, so, S, hw, hw, ovf, d_acc);
+          KERNEL_CHECK();
+        } else {
         BufPtr sl = s->alloc(8 * S * hl);
         uint32_t *si = (uint32_t *)sl->p, *so = si + S * hl;
         // static work list (no units / zero kernels): S tile ranges per run; a
@@ -2216,15 +2430,20 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
         KernelTimer kt(s, "chain2_dot", 8.0 * S * hl);
         // one block per CU: every block ends in one same-address device atomic
         // (G = 8 rank: 256 blocks 18.5 µs, 1024 24.4 µs, 2048 36 µs)
-        hipLaunchKernelGGL(k_c5_dot_slices, dim3(grid_for(hl / 4, 256, dot_grid(s->num_cus))),
-                           dim3(256), 0, s->stream, si, so, S, hl, hl, d_acc);
+        // one block per CU (each block ends in one device atomic); 16 waves per
+        // block keep 8·S·… loads in flight per CU (256 threads: latency bound)
+        const char *db = getenv("CAPF_DOT_BLOCK");  // tuning
+        const int dblk = db ? atoi(db) : 1024;
+        hipLaunchKernelGGL(k_c5_dot_slices, dim3(grid_for(hl / 4, dblk, dot_grid(s->num_cus))),
+                           dim3(dblk), 0, s->stream, si, so, S, hl, hl, d_acc);
         KERNEL_CHECK();
+        }
         }
       }
     }
   }
-  hipLaunchKernelGGL(k_partial_minus_loops, dim3(1), dim3(64), 0, s->stream,
-                     (const unsigned long long *)d_acc, d_partial);
+  hipLaunchKernelGGL(k_sharded_final, dim3(1), dim3(1024), 0, s->stream, (const unsigned long long *)d_acc,
+                     tile_acc, ntiles_all, t_in_all, d_partial);
   KERNEL_CHECK();
   return true;
 }

@@ -1350,6 +1350,17 @@ extern "C" capf_status capf_chain2_sharded_count(capf_session *cs, capf_table *i
                                                  const char *out_src, const char *out_dst,
                                                  int64_t node_base, int64_t n_nodes,
                                                  int32_t parts, int32_t part, int64_t *d_partial) {
+  return capf_chain2_sharded_count_diag(cs, in_copy, in_dst, out_copy, out_src, out_dst, -1, 0, nullptr,
+                                        node_base, n_nodes, parts, part, d_partial);
+}
+
+extern "C" capf_status capf_chain2_sharded_count_diag(capf_session *cs, capf_table *in_copy,
+                                                      const char *in_dst, capf_table *out_copy,
+                                                      const char *out_src, const char *out_dst,
+                                                      int64_t n_diag, int32_t n_hot,
+                                                      const int64_t *hot_ids, int64_t node_base,
+                                                      int64_t n_nodes, int32_t parts, int32_t part,
+                                                      int64_t *d_partial) {
   try {
     if (!cs || !in_copy || !out_copy || !in_dst || !out_src || !out_dst || !d_partial)
       illegal("null argument");
@@ -1365,7 +1376,7 @@ extern "C" capf_status capf_chain2_sharded_count(capf_session *cs, capf_table *i
         illegal("sharded 2-hop count needs non-null INTEGER endpoint columns");
     const ColView cols[3] = {view_of(a), view_of(b), view_of(c)};
     if (!chain2_sharded(s, cols, di->nrows, dout->nrows, node_base, n_nodes, parts, part,
-                        d_partial))
+                        d_partial, n_diag, n_hot, hot_ids))
       not_impl("sharded 2-hop count: shape outside the kernel's limits (buckets per rank, "
                "rows per copy < 2^31, mixed encodings)");
     return CAPF_OK;

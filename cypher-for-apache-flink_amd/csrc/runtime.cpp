@@ -864,6 +864,42 @@ capf_status capf_table_node_partition(capf_table *t, const char *key_col, int64_
   CAPF_API_END
 }
 
+capf_status capf_table_node_partition_diag(capf_table *t, const char *src_col, const char *dst_col,
+                                           int64_t node_base, int64_t n_nodes, int32_t parts,
+                                           int32_t part, capf_table **out, int64_t *n_diag) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(src_col, "src_col");
+  need(dst_col, "dst_col");
+  need(out, "out");
+  need(n_diag, "n_diag");
+  if (n_nodes <= 0 || n_nodes > (int64_t(1) << 31)) illegal("node count out of range");
+  if (parts <= 0 || part < 0 || part >= parts) illegal("part out of range");
+  const int si = t->node->col_index_or_throw(src_col), di = t->node->col_index_or_throw(dst_col);
+  if (t->node->types[si] != Type::Int64 || t->node->types[di] != Type::Int64)
+    illegal("partition keys must be INTEGER columns");
+  DataPtr d = materialize(t->node);
+  Session *s = t->node->s;
+  for (int i : {si, di}) {
+    force(d->cols[i]);
+    if (d->cols[i]->valid) illegal("partition keys must be non-null");
+  }
+  int64_t m = 0;
+  BufPtr idx = node_partition_diag_index(s, view_of(d->cols[si]), view_of(d->cols[di]), d->nrows, node_base,
+                                         n_nodes, parts, part, &m, n_diag);
+  auto n = new_node(s, Kind::Source);
+  n->names = t->node->names;
+  n->types = t->node->types;
+  auto e = std::make_shared<Data>();
+  e->nrows = m;
+  for (const ColPtr &c : d->cols)
+    e->cols.push_back(gather_column(s, decode_column(s, c), (const int64_t *)idx->p, m));
+  s->sync();
+  n->result = e;
+  *out = wrap(n);
+  CAPF_API_END
+}
+
 capf_status capf_table_hash_route(capf_table *t, int32_t nkeys, const char *const *keys,
                                   int32_t parts, int64_t *counts, capf_table **out) {
   CAPF_API_BEGIN

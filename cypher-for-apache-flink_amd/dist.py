@@ -97,14 +97,47 @@ def gpu_two_hop_count(session, rels, n_nodes, node_base=0, group=None, hists=Non
 
 
 def node_partitioned_copies(rels, n_nodes, world, rank, node_base=0, src="source", dst="target",
-                            compact=True):
+                            compact=True, diag=True):
     """(in_copy, out_copy) of this rank: the rels whose target / source node it
     owns, FOR-compacted (compact=True/4: FOR32, 3: FOR24 where the id range
-    fits 24 bits; False: int64).  Graph-ingest step, outside the timed query."""
+    fits 24 bits; False: int64).  diag: the out-copy in 2-D order — the rels
+    whose target the rank owns too first, their count as `out_copy.n_diag`
+    (a block partition of the adjacency matrix by (owner(src), owner(dst)));
+    only those can be self-loops, so the count reads the target column of
+    1/G of the out-copy instead of all of it.  Graph-ingest step, outside the
+    timed query."""
     from .table import compact_as
-    out_copy = rels.node_partition(src, node_base, n_nodes, world, rank)
+    if diag:
+        out_copy, n_diag = rels.node_partition_diag(src, dst, node_base, n_nodes, world, rank)
+    else:
+        out_copy, n_diag = rels.node_partition(src, node_base, n_nodes, world, rank), -1
     in_copy = rels.node_partition(dst, node_base, n_nodes, world, rank)
-    return compact_as(in_copy, compact), compact_as(out_copy, compact)
+    out_copy = compact_as(out_copy, compact)  # compaction keeps the row order
+    out_copy.n_diag = n_diag
+    in_copy = compact_as(in_copy, compact)
+    out_copy.hot_ids = heavy_hitters(in_copy, dst, out_copy, src)
+    return in_copy, out_copy
+
+
+def heavy_hitters(in_copy, in_key, out_copy, out_key, sample=1 << 18, k=1, min_frac=1.0 / 256):
+    """Ingest-time statistic of a rank's copies: the (at most k) node ids that
+    hold ≥ min_frac (0.4 %) of a sample of the rank's 2-hop keys (the in-copy's target
+    and the out-copy's source column, first `sample` rows of each — R-MAT /
+    edge-list rows are in no key order).  A plan hint like a most-common-
+    values list: the count is exact for any ids (capf_chain2_sharded_count_diag
+    counts the hub's keys in registers instead of partitioning them)."""
+    import numpy as np
+    vals = []
+    for t, c in ((in_copy, in_key), (out_copy, out_key)):
+        n = min(t.size, sample)
+        if n:
+            vals.append(np.asarray(t.limit(n).column_arrays(c)[0]))
+    if not vals:
+        return []
+    v = np.concatenate(vals)
+    ids, cnt = np.unique(v, return_counts=True)
+    order = np.argsort(-cnt, kind="stable")[:k]
+    return [int(ids[i]) for i in order if cnt[i] >= max(2, min_frac * len(v))]
 
 
 def gpu_two_hop_count_sharded(session, in_copy, out_copy, n_nodes, partial, node_base=0, group=None):

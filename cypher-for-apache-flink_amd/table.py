@@ -422,6 +422,14 @@ class GpuTable:
         return self._new("capf_table_node_partition", self._h, key_col.encode(), int(node_base),
                          int(n_nodes), int(parts), int(part))
 
+    def node_partition_diag(self, src_col, dst_col, node_base, n_nodes, parts, part):
+        """The out-copy of `part` in 2-D order: rows whose source it owns, those
+        whose target it owns too first.  Returns (table, n_diag)."""
+        h, nd = c_void_p(), c_int64()
+        _lib.call("capf_table_node_partition_diag", self._h, src_col.encode(), dst_col.encode(), int(node_base),
+                  int(n_nodes), int(parts), int(part), byref(h), byref(nd))
+        return GpuTable(self.session, h), nd.value
+
     def chain2_local_hists(self, src_col, dst_col, node_base, n_nodes, d_in, d_out):
         loops = c_int64()
         _lib.call("capf_chain2_local_hists", self.session._h, self._h, src_col.encode(), dst_col.encode(),
@@ -439,9 +447,13 @@ def compact_as(table, compact):
 
 def chain2_sharded_count_async(session, in_copy, out_copy, node_base, n_nodes, parts, part,
                                d_partial, src="source", dst="target"):
-    """Enqueue this rank's 2-hop partial (int64 at device address d_partial)."""
-    _lib.call("capf_chain2_sharded_count", session._h, in_copy._h, dst.encode(), out_copy._h,
-              src.encode(), dst.encode(), int(node_base), int(n_nodes), int(parts), int(part),
+    """Enqueue this rank's 2-hop partial (int64 at device address d_partial).
+    An out-copy in 2-D order (node_partition_diag) carries `n_diag`: only its
+    first n_diag rows are tested for self-loops."""
+    hot = list(getattr(out_copy, "hot_ids", ()))[:2]
+    _lib.call("capf_chain2_sharded_count_diag", session._h, in_copy._h, dst.encode(), out_copy._h,
+              src.encode(), dst.encode(), int(getattr(out_copy, "n_diag", -1)), len(hot),
+              (c_int64 * max(len(hot), 1))(*hot), int(node_base), int(n_nodes), int(parts), int(part),
               c_void_p(d_partial))
 
 

@@ -377,6 +377,26 @@ capf_status capf_chain2_sharded_count(capf_session *s, capf_table *in_copy, cons
                                       capf_table *out_copy, const char *out_src,
                                       const char *out_dst, int64_t node_base, int64_t n_nodes,
                                       int32_t parts, int32_t part, int64_t *d_partial);
+/* 2-D layout of the out-copy (a block partition of the adjacency matrix by
+ * (owner(source), owner(target)), as distributed graph stores keep it):
+ * capf_table_node_partition_diag returns the rows whose source `part` owns
+ * with the rows whose target it owns too first (*n_diag of them);
+ * capf_chain2_sharded_count_diag is capf_chain2_sharded_count for such an
+ * out-copy: a self-loop has both endpoints owned, so the target column is
+ * read for rows [0, n_diag) only (n_diag = -1: every row).  hot_ids: up to
+ * 2 heavy-hitter node ids (host array; a plan hint sampled at ingest — any
+ * ids give the same count): keys equal to one are counted in registers by
+ * the partition pass instead of being partitioned (skew handling: a hub's
+ * keys would pile onto one LDS counter word in the counting pass).          */
+capf_status capf_table_node_partition_diag(capf_table *t, const char *src_col, const char *dst_col,
+                                           int64_t node_base, int64_t n_nodes, int32_t parts,
+                                           int32_t part, capf_table **out, int64_t *n_diag);
+capf_status capf_chain2_sharded_count_diag(capf_session *s, capf_table *in_copy, const char *in_dst,
+                                           capf_table *out_copy, const char *out_src,
+                                           const char *out_dst, int64_t n_diag, int32_t n_hot,
+                                           const int64_t *hot_ids, int64_t node_base,
+                                           int64_t n_nodes, int32_t parts, int32_t part,
+                                           int64_t *d_partial);
 /* Directed triangle (a)-->(b)-->(c)-->(a) with pairwise distinct rels over
  * the rels of `rels` whose endpoints lie in [node_base, node_base + n_nodes)
  * (the fused form of Expand, Expand, ExpandInto + uniqueness,

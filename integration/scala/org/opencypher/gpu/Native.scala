@@ -148,6 +148,11 @@ object Native {
   @native def chain2ShardedCount(session: Long, inCopy: Long, inDst: String, outCopy: Long, outSrc: String,
                                  outDst: String, nodeBase: Long, nNodes: Long, parts: Int, part: Int,
                                  dPartial: Long): Unit
+  @native def tableNodePartitionDiag(table: Long, srcCol: String, dstCol: String, nodeBase: Long, nNodes: Long,
+                                     parts: Int, part: Int, nDiagOut: Array[Long]): Long
+  @native def chain2ShardedCountDiag(session: Long, inCopy: Long, inDst: String, outCopy: Long, outSrc: String,
+                                     outDst: String, nDiag: Long, hotIds: Array[Long], nodeBase: Long,
+                                     nNodes: Long, parts: Int, part: Int, dPartial: Long): Unit
   @native def triangleCountPart(session: Long, rels: Long, srcCol: String, dstCol: String, nodeBase: Long,
                                 nNodes: Long, parts: Int, part: Int, dCount: Long): Unit
   @native def chain2HistLen(nNodes: Long): Long

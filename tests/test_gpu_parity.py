@@ -543,6 +543,11 @@ def test_sharded_two_hop_partials(gpu_session, compact, scale, parts, mode, monk
         assert in_copy.size == int((own_d == p).sum())
         assert out_copy.size == int((own_s == p).sum())
         assert sorted(out_copy.column_arrays("id")[0].tolist()) == np.nonzero(own_s == p)[0].tolist()
+        nd = getattr(out_copy, "n_diag", -1)
+        if nd >= 0:  # 2-D order: the rels whose target p owns too come first
+            ids = out_copy.column_arrays("id")[0]
+            assert nd == int(((own_s == p) & (own_d == p)).sum())
+            assert (own_d[ids[:nd]] == p).all() and (own_d[ids[nd:]] != p).all()
         part = torch.full((1,), -1, dtype=torch.int64, device="cuda")
         chain2_sharded_count_async(gpu_session, in_copy, out_copy, 0, n, parts, p, part.data_ptr())
         gpu_session.sync()
@@ -672,3 +677,40 @@ def test_unmapped_aggregators_raise_on_gpu(gpu_session, agg):
     q = Query([Match([NodeP("n")])], [Stage([("res", a)])])
     with pytest.raises(_lib.NotImplementedException):
         run(ScanGraph.from_data(gpu_session, parse_create("CREATE ({val: 1}), ({val: 2})")), q)
+
+
+@pytest.mark.parametrize("hot", ["sampled", "none", "owned", "foreign", "dup", "range"])
+def test_sharded_heavy_hitter_hints(gpu_session, hot):
+    """Heavy-hitter hints of the sharded 2-hop count (dist.heavy_hitters, a
+    sampled plan hint): whatever ids are passed — the sampled hubs, none, other
+    owned nodes, nodes another rank owns, duplicates, ids outside the node
+    range — every partial equals the oracle's (self-loops at a hub included)."""
+    import torch
+    from capf_amd.dist import node_partitioned_copies
+    from capf_amd.table import chain2_sharded_count_async
+    from oracle import nodemix
+    scale, parts = 18, 3
+    m, n = 16 << scale, 1 << scale
+    t = gpu_session.rmat_rels(scale, cmodel.rmat_seed(scale), cmodel.thresholds(), 0, m)
+    src, dst = cmodel.rmat(scale)
+    own_s, own_d = nodemix.owner(src, n, parts), nodemix.owner(dst, n, parts)
+    deg = np.bincount(src, minlength=n) + np.bincount(dst, minlength=n)
+    total = 0
+    for p in range(parts):
+        in_copy, out_copy = node_partitioned_copies(t, n, parts, p, compact=3)
+        mine = np.nonzero(nodemix.owner(np.arange(n), n, parts) == p)[0]
+        top = mine[np.argsort(-deg[mine])[:2]].tolist()
+        other = np.nonzero(nodemix.owner(np.arange(n), n, parts) != p)[0][:2].tolist()
+        out_copy.hot_ids = {"sampled": out_copy.hot_ids, "none": [], "owned": mine[5:7].tolist(),
+                            "foreign": other, "dup": top[:1] * 2, "range": [-5, n + 3]}[hot]
+        if hot == "sampled":  # a sampled hint: ids of nodes this rank owns
+            assert set(out_copy.hot_ids) <= set(mine.tolist())
+        part = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+        chain2_sharded_count_async(gpu_session, in_copy, out_copy, 0, n, parts, p, part.data_ptr())
+        gpu_session.sync()
+        ein = np.bincount(dst[own_d == p], minlength=n).astype(np.int64)
+        eout = np.bincount(src[own_s == p], minlength=n).astype(np.int64)
+        expect = int((ein * eout).sum()) - int(((src == dst) & (own_s == p)).sum())
+        assert int(part.item()) == expect, (p, hot, out_copy.hot_ids)
+        total += expect
+    assert total == cmodel.count_2hop(src, dst, n)

@@ -40,6 +40,7 @@ for p in parts:
     prof = {k: round(x["total_ms"] / 5, 4) for k, x in s.profile().items()}
     dev = sum(prof.values())
     tot += v
-    print(f"s{scale} G={G} part {p}: in {ic.size} out {oc.size} rows; step {el*1e3:.3f} ms "
+    print(f"s{scale} G={G} part {p}: in {ic.size} out {oc.size} rows (hot {getattr(oc, 'hot_ids', [])}); "
+          f"step {el*1e3:.3f} ms "
           f"dev {dev:.3f} ms {prof} partial {v}", flush=True)
 print("sum of partials", tot)

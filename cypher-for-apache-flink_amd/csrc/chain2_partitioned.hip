@@ -1269,15 +1269,24 @@ __global__ __launch_bounds__(1024) void k_c5_dot_packed(const uint32_t *si, cons
 #pragma unroll
     for (int q = 0; q < 8; ++q) t += (unsigned long long)a[q] * b[q];
   }
+  // the log (a few entries per hub bin) staged in LDS when it fits: the
+  // first-occurrence test and the per-bin sums then cost LDS reads only
+  constexpr uint32_t LOG_LDS = 4096;
+  __shared__ uint2 lg[LOG_LDS];
   const uint32_t n = min(*ovf.n, ovf.cap);
+  const bool staged = n <= LOG_LDS;
+  const uint2 *L = staged ? lg : ovf.log;
+  if (staged)
+    for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) lg[j] = ovf.log[j];
+  __syncthreads();
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
-    const uint32_t g = ovf.log[e].x;
+    const uint32_t g = L[e].x;
     bool first = true;
-    for (uint32_t j = 0; j < e && first; ++j) first = ovf.log[j].x != g;
+    for (uint32_t j = 0; j < e && first; ++j) first = L[j].x != g;
     if (!first) continue;
     unsigned long long cin = 0, cout = 0;
     for (uint32_t j = e; j < n; ++j) {
-      const uint2 f = ovf.log[j];
+      const uint2 f = L[j];
       if (f.x != g) continue;
       if (f.y & 1u) cout += f.y >> 1;
       else cin += f.y >> 1;
@@ -2404,7 +2413,10 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
           KERNEL_CHECK();
         } else {
         const char *pk = getenv("CAPF_SHARD_PACKED");  // tuning: 0 = uint32 slices + overflow kernel
-        sd.packed = !(pk && atoi(pk) == 0);
+        // packed when several slices per run (G ≥ 4 at s24): with one slice the runs
+        // are whole buckets whose hub bins log many hand-offs (measured G = 2:
+        // packed dot 41 µs vs uint32 dot + overflow 22 µs)
+        sd.packed = pk ? atoi(pk) != 0 : S >= 2;
         if (sd.packed) {
           // packed uint16 slices: half the slice bytes written by P3 and read by the dot
           const int64_t hw = (int64_t)nbl * C2_WORDS;

@@ -119,6 +119,12 @@ struct Column {
   std::vector<int64_t> host_i64;
   // Type::List: the element column (never lazy, no NULL elements)
   std::shared_ptr<Column> child;
+  // an index derived from this column and a peer column (the triangle
+  // count's oriented CSR of (this, peer)), built on first use and kept for
+  // the column's lifetime like `stats`: ingest-time work, not per query
+  mutable std::shared_ptr<void> index;
+  mutable std::weak_ptr<Column> index_peer;
+  mutable int64_t index_key[2] = {0, 0};
   bool is_all_null() const { return type == Type::Null; }
 };
 using ColPtr = std::shared_ptr<Column>;
@@ -406,7 +412,8 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
 BufPtr route_permutation(Session *s, const std::vector<ColView> &keys, int64_t n, int parts,
                          std::vector<int64_t> &counts);
 // Directed triangle count (triangle.hip), part `part` of `parts`, to device int64.
-void triangle_count_async(Session *s, const ColView &src, const ColView &dst, int64_t m,
+// The oriented CSR is cached on `src` (Column::index) for the pair (src, dst).
+void triangle_count_async(Session *s, const ColPtr &src, const ColPtr &dst, int64_t m,
                           int64_t lo, uint64_t len, int parts, int part, int64_t *d_out);
 bool chain2_partitioned(Session *s, const ColView *cols, int64_t n, int64_t lo, int64_t hi,
                         bool in_range, uint32_t *h_in, uint32_t *h_out,

@@ -1186,7 +1186,7 @@ static bool run_triangle(Session *s, const JoinGraph &g, const Tri &t, uint64_t 
   BufPtr acc = s->alloc(16);
   int64_t *dst = s->async_out ? s->async_out : (int64_t *)acc->p;
   if (len > 0 && R.nrows > 0) {
-    triangle_count_async(s, view_of(R.cols[t.src]), view_of(R.cols[t.dst]), R.nrows, lo,
+    triangle_count_async(s, R.cols[t.src], R.cols[t.dst], R.nrows, lo,
                          (uint64_t)len, 1, 0, dst);
   } else {
     HIP_CHECK(hipMemsetAsync(dst, 0, 8, s->stream));
@@ -1407,7 +1407,7 @@ extern "C" capf_status capf_triangle_count_part(capf_session *cs, capf_table *re
       HIP_CHECK(hipMemsetAsync(d_count, 0, 8, s->stream));
       return CAPF_OK;
     }
-    triangle_count_async(s, view_of(a), view_of(b), d->nrows, node_base, (uint64_t)n_nodes, parts,
+    triangle_count_async(s, a, b, d->nrows, node_base, (uint64_t)n_nodes, parts,
                          part, d_count);
     return CAPF_OK;
   } catch (const capf::Error &e) {

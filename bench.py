@@ -25,7 +25,7 @@ sys.path.insert(0, ROOT)
 import capf_import  # noqa: E402,F401
 
 METRIC = "joined rows/sec for 2-hop MATCH on R-MAT s24 at 1/2/4/8 GPUs; % HBM roofline"
-ROWS_METRIC = "joined rows/sec for MATCH (a)-->(b) RETURN a, b materialised on R-MAT (radix-partitioned join leg)"
+ROWS_METRIC = "joined rows/sec for MATCH (a)-->(b) RETURN a, b materialised on R-MAT (materialising join leg)"
 ONE_HOP_METRIC = "joined rows/sec for 1-hop MATCH (a:Person)-->(b) count(*) on R-MAT (config 2)"
 TRI_METRIC = "joined rows/sec for triangle MATCH (a)-->(b)-->(c)-->(a) on R-MAT (config 4)"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -55,7 +55,7 @@ def one_hop_person_query():
 
 def one_hop_rows_query():
     """MATCH (a)-->(b) RETURN a, b — the materialising Expand join (2 joins
-    of RelationalPlanner.scala:130-165 through the radix-partitioned join)."""
+    of RelationalPlanner.scala:130-165 through the materialising joins)."""
     from capf_amd.expr import Var
     from capf_amd.planner import Match, NodeP, Query, RelP, Stage
     return Query([Match([NodeP("a"), NodeP("b")], [RelP("r", "a", "b")])],
@@ -249,11 +249,15 @@ def run_rows_leg(args):
         "data": f"synthetic R-MAT s{args.scale} generated in HBM before timing",
         "config": {"workload": workload_name(args), "scale": args.scale, "nodes": n_nodes, "rels": m,
                    "rows": rows, "id_storage": "FOR32", "plan": s.last_plan() or "relational (2 joins)",
-                   "join": "radix-partitioned (csrc/radix_join.hip)"},
+                   "join": {"radix": "radix-partitioned (csrc/radix_join.hip), forced by CAPF_JOIN=radix",
+                            "hash": "global hash table (csrc/kernels_hash.hip), forced by CAPF_JOIN=hash"}.get(
+                       os.environ.get("CAPF_JOIN", ""),
+                       "planner choice: direct-address join on the dense node-id key (csrc/dense_join.hip), "
+                       "radix-partitioned join (csrc/radix_join.hip) for other keys")},
         # the step runs many small kernels (two joins, gathers, scans): the
         # roofline is taken over the whole step's wall time; the timed
         # kernels' split (partition / join passes) is reported beside it
-        "roofline": {"bound": "hbm", "kernel": "whole step (2 radix joins + gathers + scans), wall time",
+        "roofline": {"bound": "hbm", "kernel": "whole step (2 joins + gathers + scans), wall time",
                      "achieved": compulsory / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": compulsory / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "traffic": None, "algorithmic_bytes_per_launch": compulsory,

@@ -117,12 +117,19 @@ struct Column {
   // values of a tiny host-born column (a fused scalar result), kept beside
   // the device copy so `rows` needs no device round trip
   std::vector<int64_t> host_i64;
+  // every row holds the same non-NULL value (a literal evaluated over a
+  // table, e.g. the label column of a one-label scan): const_bits = its
+  // physical bits; a gather of it is a fill (no index read)
+  bool is_const = false;
+  uint64_t const_bits = 0;
   // Type::List: the element column (never lazy, no NULL elements)
   std::shared_ptr<Column> child;
   // an index derived from this column and a peer column (the triangle
   // count's oriented CSR of (this, peer)), built on first use and kept for
   // the column's lifetime like `stats`: ingest-time work, not per query
   mutable std::shared_ptr<void> index;
+  // the direct-address index of a dense unique id column (dense_join.hip)
+  mutable std::shared_ptr<void> dense;
   mutable std::weak_ptr<Column> index_peer;
   mutable int64_t index_key[2] = {0, 0};
   bool is_all_null() const { return type == Type::Null; }
@@ -353,11 +360,18 @@ struct Grouping {
 Grouping group_rows(Session *s, const Data &d, const std::vector<int> &keys);
 // Equi-join of two materialised tables on key columns → (left idx, right idx) pairs.
 struct JoinPairs {
-  BufPtr left, right;  // int64 [n], -1 for a null-extended side
+  BufPtr left, right;  // int64 [n], -1 for a null-extended side; null = identity (n rows)
   int64_t n = 0;
+  // inner join whose key values are equal on every output row: 1 = the left
+  // key column may be replaced by the right one, 2 = the other way round
+  int key_alias = 0;
 };
 JoinPairs hash_join(Session *s, const Data &l, const Data &r,
                     const std::vector<std::pair<int, int>> &keys, int32_t join_type);
+// Direct-address join on a dense unique INTEGER key column (dense_join.hip):
+// false when no side qualifies (then radix / hash join).
+bool dense_join(Session *s, const Data &l, const Data &r, const std::vector<std::pair<int, int>> &keys,
+                int32_t join_type, JoinPairs &out);
 // Radix-partitioned equi-join on one key column (radix_join.hip): used for
 // large inputs (CAPF_JOIN=radix|hash forces a path).
 bool radix_join_applies(const Data &l, const Data &r, const std::vector<std::pair<int, int>> &keys,

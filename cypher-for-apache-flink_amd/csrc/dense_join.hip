@@ -1,0 +1,188 @@
+// dense_join.hip — the Expand join when one side's key is a dense unique id
+// column (FlinkTable.join, FlinkTable.scala:171-187, in the shape the Expand
+// of RelationalPlanner.scala:130-165 produces: node.id = start(r) / end(r),
+// node ids of an element table being unique by construction).
+//
+// When the build key column holds exactly {min..max}, each value once and no
+// NULL (the column statistics, computed once per column), the hash table of a
+// hash join degenerates into a direct-address table: slot[v − min] = row.
+// It is built once per column and cached on it, like the statistics (the
+// ingest-time index of a node table); when row r holds min + r for every r
+// (ids stored in order, the usual node table) no table is needed at all:
+// row = v − min.  The probe is then one streaming pass:
+//
+//   k_dense_probe   per probe row: key → (in range? slot : miss), the build
+//                   row written as int64 (−1 = no match), one match count per
+//                   block (fixed grid, one atomic per block)
+//   inner join      all probe rows matched (every rel's endpoints exist, the
+//                   Expand case): the probe side's index is the identity —
+//                   its columns pass through untouched, zero copy; otherwise
+//                   the matched rows are compacted (wave ballot / scan)
+//   probe-side outer (LEFT OUTER with the probe on the left, RIGHT OUTER with
+//                   it on the right): identity + the −1 rows null-extended
+//
+// Build-side outer and FULL OUTER joins go to the radix join.  Bytes per
+// probe row: the key (3/4/8 B by encoding) read, 8 B written; the slot
+// table (4 B per build row) is L2/MALL-resident for node tables of up to
+// ~2^25 rows.
+#include <algorithm>
+#include <cstring>
+
+#include "capf_internal.h"
+#include "device_common.h"
+
+namespace capf {
+
+struct DenseIndex {
+  int64_t min = 0, n = 0;
+  bool ident = false;  // row r holds min + r
+  BufPtr slot;         // int32 row of value min + k (null when ident)
+};
+
+__global__ void k_dense_index(ColView c, int64_t n, int64_t mn, int32_t *slot, int *not_ident) {
+  bool off = false;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = ld_int(c, r) - mn;
+    slot[k] = (int32_t)r;
+    off |= k != r;
+  }
+  if (__ballot(off) && lane_id() == 0) atomicOr(not_ident, 1);
+}
+
+// The dense index of column c of a table of `nrows` rows, or nullptr when the
+// column is not a non-null dense unique INTEGER column.
+static std::shared_ptr<DenseIndex> dense_index(Session *s, const ColPtr &c, int64_t nrows) {
+  force(c);
+  if (c->type != Type::Int64 || c->lazy || nrows == 0 || nrows >= (int64_t(1) << 31)) return nullptr;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (c->dense) return std::static_pointer_cast<DenseIndex>(c->dense);
+  }
+  const ColStats &st = column_stats(s, c);
+  if (!st.dense_unique || st.non_null != nrows) return nullptr;
+  auto di = std::make_shared<DenseIndex>();
+  di->min = st.min;
+  di->n = nrows;
+  BufPtr slot = s->alloc(4 * nrows), flag = s->alloc(4);
+  HIP_CHECK(hipMemsetAsync(flag->p, 0, 4, s->stream));
+  hipLaunchKernelGGL(k_dense_index, dim3(grid_for(nrows, 256)), dim3(256), 0, s->stream, view_of(c),
+                     nrows, st.min, (int32_t *)slot->p, (int *)flag->p);
+  KERNEL_CHECK();
+  int nf = 0;
+  HIP_CHECK(hipMemcpyAsync(&nf, flag->p, 4, hipMemcpyDeviceToHost, s->stream));
+  s->sync();
+  di->ident = nf == 0;
+  if (!di->ident) di->slot = slot;
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->dense = di;
+  return di;
+}
+
+template <bool IDENT>
+__global__ __launch_bounds__(256) void k_dense_probe(ColView key, int64_t n, int64_t mn, int64_t range,
+                                                     const int32_t *slot, int64_t *brow,
+                                                     unsigned long long *matched) {
+  __shared__ unsigned long long red[256 / WAVE];
+  unsigned long long cnt = 0;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    int64_t b = -1;
+    if (!key.valid || key.valid[r]) {
+      const int64_t k = ld_int(key, r) - mn;
+      if ((uint64_t)k < (uint64_t)range) b = IDENT ? k : (int64_t)slot[k];
+    }
+    brow[r] = b;
+    cnt += b >= 0 ? 1u : 0u;
+  }
+  cnt = wave_reduce_sum(cnt);
+  if (lane_id() == 0) red[threadIdx.x / WAVE] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < 256 / WAVE; ++w) t += red[w];
+    if (t) atomicAdd(matched, t);
+  }
+}
+
+__global__ void k_dense_flags(const int64_t *brow, int64_t n, uint8_t *flags) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x)
+    flags[r] = brow[r] >= 0 ? 1 : 0;
+}
+
+__global__ void k_dense_pick(const int64_t *rows, int64_t m, const int64_t *brow, int64_t *out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = brow[rows[i]];
+}
+
+bool dense_join(Session *s, const Data &l, const Data &r, const std::vector<std::pair<int, int>> &keys,
+                int32_t join_type, JoinPairs &out) {
+  if (keys.size() != 1 || join_type == CAPF_JOIN_CROSS || join_type == CAPF_JOIN_FULL_OUTER) return false;
+  const char *mode = getenv("CAPF_JOIN");  // "radix" | "hash" force the general joins
+  if (mode && (strcmp(mode, "radix") == 0 || strcmp(mode, "hash") == 0)) return false;
+  // the build side is the dense one; an outer join must keep the probe side
+  // (the build side's unmatched rows would need a second pass)
+  const bool l_ok = join_type != CAPF_JOIN_LEFT_OUTER, r_ok = join_type != CAPF_JOIN_RIGHT_OUTER;
+  std::shared_ptr<DenseIndex> di;
+  bool build_left = false;
+  if (r_ok && r.nrows <= l.nrows) di = dense_index(s, r.cols[keys[0].second], r.nrows);
+  if (!di && l_ok) {
+    di = dense_index(s, l.cols[keys[0].first], l.nrows);
+    build_left = di != nullptr;
+  }
+  if (!di && r_ok && r.nrows > l.nrows) di = dense_index(s, r.cols[keys[0].second], r.nrows);
+  if (!di) return false;
+  const Data &Pr = build_left ? r : l;
+  const ColPtr &pk = Pr.cols[build_left ? keys[0].second : keys[0].first];
+  force(pk);
+  if (pk->type != Type::Int64) return false;
+  const int64_t n = Pr.nrows;
+  const bool probe_outer = join_type != CAPF_JOIN_INNER;
+  BufPtr brow = s->alloc(8 * std::max<int64_t>(n, 1));
+  BufPtr acc = s->alloc(8);
+  HIP_CHECK(hipMemsetAsync(acc->p, 0, 8, s->stream));
+  if (n > 0) {
+    const double kw = pk->enc == ENC_FOR24 ? 3.0 : pk->enc == ENC_FOR32 ? 4.0 : 8.0;
+    KernelTimer kt(s, "dense_probe", (kw + 8.0) * n);
+    const unsigned grid = grid_for(n, 256, (int64_t)s->num_cus * 8);
+    if (di->ident)
+      hipLaunchKernelGGL(k_dense_probe<true>, dim3(grid), dim3(256), 0, s->stream, view_of(pk), n, di->min,
+                         di->n, (const int32_t *)nullptr, (int64_t *)brow->p, (unsigned long long *)acc->p);
+    else
+      hipLaunchKernelGGL(k_dense_probe<false>, dim3(grid), dim3(256), 0, s->stream, view_of(pk), n, di->min,
+                         di->n, (const int32_t *)di->slot->p, (int64_t *)brow->p,
+                         (unsigned long long *)acc->p);
+    KERNEL_CHECK();
+  }
+  int64_t matched = 0;
+  HIP_CHECK(hipMemcpyAsync(s->h_scalars, acc->p, 8, hipMemcpyDeviceToHost, s->stream));
+  s->sync();
+  matched = s->h_scalars[0];
+  BufPtr pidx, bidx = brow;  // pidx null = identity over the probe rows
+  int64_t m = n;
+  if (!probe_outer && matched < n) {
+    BufPtr flags = s->alloc(std::max<int64_t>(n, 1));
+    hipLaunchKernelGGL(k_dense_flags, dim3(grid_for(n, 256)), dim3(256), 0, s->stream,
+                       (const int64_t *)brow->p, n, (uint8_t *)flags->p);
+    KERNEL_CHECK();
+    int64_t k = 0;
+    pidx = compact_flags(s, (const uint8_t *)flags->p, n, &k);
+    m = k;
+    bidx = s->alloc(8 * std::max<int64_t>(k, 1));
+    if (k > 0) {
+      hipLaunchKernelGGL(k_dense_pick, dim3(grid_for(k, 256)), dim3(256), 0, s->stream,
+                         (const int64_t *)pidx->p, k, (const int64_t *)brow->p, (int64_t *)bidx->p);
+      KERNEL_CHECK();
+    }
+  }
+  out.left = build_left ? bidx : pidx;
+  out.right = build_left ? pidx : bidx;
+  out.n = m;
+  // inner join: the build key equals the probe key on every output row
+  out.key_alias = join_type == CAPF_JOIN_INNER ? (build_left ? 1 : 2) : 0;
+  return true;
+}
+
+}  // namespace capf

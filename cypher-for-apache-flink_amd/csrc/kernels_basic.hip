@@ -181,6 +181,69 @@ __global__ void k_gather(const T *src, const uint8_t *sval, const int64_t *idx, 
   }
 }
 
+// Four consecutive rows per thread: 2 × 16-B index loads, the gathered
+// values stored as one 4·sizeof(T) vector and the validity as one u32 (a
+// 1-B store per row leaves the byte columns at ~1 TB/s).
+template <typename T>
+__global__ void k_gather4(const T *src, const uint8_t *sval, const int64_t *idx, T *dst,
+                          uint8_t *dval, int64_t m) {
+  const int64_t m4 = m / 4;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m4;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const longlong2 a = ((const longlong2 *)idx)[2 * q], b = ((const longlong2 *)idx)[2 * q + 1];
+    const int64_t j[4] = {a.x, a.y, b.x, b.y};
+    T v[4];
+    uint32_t vm = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool ok = j[k] >= 0;
+      v[k] = ok && dst ? src[j[k]] : T(0);
+      vm |= (uint32_t)(ok ? (sval ? sval[j[k]] : 1) : 0) << (8 * k);
+    }
+    if (dst) {
+      if (sizeof(T) == 1) {
+        ((uint32_t *)dst)[q] = (uint32_t)(uint8_t)v[0] | (uint32_t)(uint8_t)v[1] << 8 |
+                               (uint32_t)(uint8_t)v[2] << 16 | (uint32_t)(uint8_t)v[3] << 24;
+      } else if (sizeof(T) == 4) {
+        ((uint4 *)dst)[q] = make_uint4((uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]);
+      } else {
+        ((longlong2 *)dst)[2 * q] = make_longlong2((long long)v[0], (long long)v[1]);
+        ((longlong2 *)dst)[2 * q + 1] = make_longlong2((long long)v[2], (long long)v[3]);
+      }
+    }
+    if (dval) ((uint32_t *)dval)[q] = vm;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)(m - 4 * m4)) {
+    const int64_t i = 4 * m4 + threadIdx.x;
+    const int64_t j = idx[i];
+    const bool ok = j >= 0;
+    if (dst) dst[i] = ok ? src[j] : T(0);
+    if (dval) dval[i] = ok ? (sval ? sval[j] : 1) : 0;
+  }
+}
+
+__global__ void k_fill_u64(uint64_t *p, uint64_t v, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+
+// m rows of a constant column's value (no validity: no NULLs)
+static ColPtr const_column(Session *s, const Column &c, int64_t m) {
+  ColPtr o = make_column(s, c.type, m, false);
+  o->is_const = true;
+  o->const_bits = c.const_bits;
+  if (m == 0) return o;
+  if (c.type == Type::Bool) {
+    HIP_CHECK(hipMemsetAsync(o->data->p, (int)(c.const_bits & 1), m, s->stream));
+  } else {
+    hipLaunchKernelGGL(k_fill_u64, dim3(grid_for(m, 256)), dim3(256), 0, s->stream, (uint64_t *)o->data->p,
+                       c.const_bits, m);
+    KERNEL_CHECK();
+  }
+  return o;
+}
+
 // FOR24 rows gathered into FOR32 (same base): the gathered rows are no
 // longer a scan-order stream, 4-B rows keep every later access aligned
 __global__ void k_gather_u24(const void *src, const uint8_t *sval, const int64_t *idx,
@@ -221,11 +284,14 @@ void force(const ColPtr &c) {
 
 ColPtr gather_lazy(Session *s, const ColPtr &c, const BufPtr &idx, int64_t m, bool nullable,
                    IdxCache *cache) {
+  if (!idx && m == c->n) return c;  // identity: the column passes through, lazy or not
   if (!idx || !lazy_enabled() || c->type == Type::Null || c->type == Type::List || m == 0)
     return gather_column(s, c, idx ? (const int64_t *)idx->p : nullptr, m, nullable);
   ColPtr src = c;
   BufPtr id = idx;
-  if (c->lazy) {
+  if (c->lazy && c->lazy->src->is_const && !nullable && !c->lazy->nullable) {
+    src = c->lazy->src;  // a constant gathers to a fill: the composed index is never read
+  } else if (c->lazy) {
     const std::pair<const void *, const void *> key(c->lazy->idx.get(), idx.get());
     BufPtr composed;
     if (cache)
@@ -263,6 +329,7 @@ ColPtr gather_column(Session *s, const ColPtr &c, const int64_t *d_idx, int64_t 
   }
   if (c->type == Type::Null) return null_column(s, Type::Null, m);
   if (c->type == Type::List) return gather_list(s, c, d_idx, m);
+  if (c->is_const && !idx_may_be_null && c->n > 0) return const_column(s, *c, m);
   if (!c->data || c->n == 0) {
     // empty source (outer join against an empty side): every index is the
     // null index, so the result is all NULL of the column's type
@@ -291,17 +358,18 @@ ColPtr gather_column(Session *s, const ColPtr &c, const int64_t *d_idx, int64_t 
   const uint8_t *sval = c->valid ? (const uint8_t *)c->valid->p : nullptr;
   uint8_t *dval = o->valid ? (uint8_t *)o->valid->p : nullptr;
   unsigned g = grid_for(m, 256);
+  const unsigned g4 = grid_for((m + 3) / 4, 256);
   if (c->type == Type::Bool)
-    hipLaunchKernelGGL(k_gather<uint8_t>, dim3(g), dim3(256), 0, s->stream,
+    hipLaunchKernelGGL(k_gather4<uint8_t>, dim3(g4), dim3(256), 0, s->stream,
                        (const uint8_t *)c->data->p, sval, d_idx, (uint8_t *)o->data->p, dval, m);
   else if (c->enc == ENC_FOR24)
     hipLaunchKernelGGL(k_gather_u24, dim3(g), dim3(256), 0, s->stream, (const void *)c->data->p, sval,
                        d_idx, (uint32_t *)o->data->p, dval, m);
   else if (c->enc == ENC_FOR32)
-    hipLaunchKernelGGL(k_gather<uint32_t>, dim3(g), dim3(256), 0, s->stream,
+    hipLaunchKernelGGL(k_gather4<uint32_t>, dim3(g4), dim3(256), 0, s->stream,
                        (const uint32_t *)c->data->p, sval, d_idx, (uint32_t *)o->data->p, dval, m);
   else
-    hipLaunchKernelGGL(k_gather<int64_t>, dim3(g), dim3(256), 0, s->stream,
+    hipLaunchKernelGGL(k_gather4<int64_t>, dim3(g4), dim3(256), 0, s->stream,
                        (const int64_t *)c->data->p, sval, d_idx, (int64_t *)o->data->p, dval, m);
   KERNEL_CHECK();
   return o;
@@ -857,6 +925,21 @@ ColPtr eval_program(Session *s, const Program &p, const std::vector<std::string>
     if (it != names.end()) {
       const ColPtr &c = d.cols[(size_t)(it - names.begin())];
       if (c->type == out_type) return c;
+    }
+  }
+  if (p.code.size() == 1) {  // a literal of the column's type: every row holds it
+    const Instr &in = p.code[0];
+    const bool lit = (in.op == OP_LIT_BOOL && out_type == Type::Bool) ||
+                     (in.op == OP_LIT_INT && out_type == Type::Int64) ||
+                     (in.op == OP_LIT_FLOAT && out_type == Type::Float64) ||
+                     (in.op == OP_LIT_STRING && out_type == Type::String);
+    if (lit) {
+      Column proto;
+      proto.type = out_type;
+      proto.const_bits = in.op == OP_LIT_BOOL ? (uint64_t)(in.i != 0)
+                         : in.op == OP_LIT_FLOAT ? (uint64_t)__builtin_bit_cast(uint64_t, in.f)
+                                                 : (uint64_t)in.i;
+      return const_column(s, proto, n);
     }
   }
   ColPtr o = make_column(s, out_type, n, true);

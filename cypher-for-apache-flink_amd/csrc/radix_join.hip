@@ -8,7 +8,8 @@
 //   h = fmix64(w)  a bijection on 64 bits: h equal ⇔ w equal, so only h is kept
 //   P1 / P2      two radix passes of 8 bits each (h >> 56, then h >> 48 & 255):
 //                per 8 Ki-row tile an LDS histogram, one exclusive scan over
-//                (bucket, tile) counts, an LDS-cursor scatter of (h, row) into
+//                (bucket, tile) counts, the tile's (h, row) pairs grouped by
+//                bucket in LDS and written out run by run (coalesced) into
 //                contiguous buckets; the second pass runs per first-level
 //                bucket, so (b1, b2) = 65 536 contiguous partitions per side
 //   J            one workgroup per work item (a partition, or a 8 Ki-row probe
@@ -69,24 +70,79 @@ __global__ __launch_bounds__(RJ_PBLOCK) void k_rj_hist1(ColView key, int64_t n, 
   for (int b = threadIdx.x; b < RJ_P; b += RJ_PBLOCK) counts[(int64_t)b * ntiles + t] = hist[b];
 }
 
-__global__ __launch_bounds__(RJ_PBLOCK) void k_rj_scatter1(ColView key, int64_t n, int64_t ntiles,
+// Scatter of one tile through LDS: every row's rank inside its bucket comes
+// from the LDS count atomic, the tile's (h, row) pairs are grouped by bucket
+// in LDS, then written out in that order — consecutive lanes write
+// consecutive addresses of one bucket's run (a per-row scatter to 256
+// cursors makes every 8-B store its own memory transaction: 0.86 TB/s).
+// PASS 1 reads the key column (rows [e0, e1)), PASS 2 the pass-1 output
+// (h, row) of one first-level bucket's tile; `goff` = this tile's global
+// start per bucket.
+constexpr int RJ_SBLOCK = 1024;
+constexpr int RJ_RPT = RJ_TILE / RJ_SBLOCK;
+
+template <int PASS>
+__device__ inline uint32_t rj_bucket(uint64_t h) {
+  return PASS == 1 ? (uint32_t)(h >> 56) : (uint32_t)(h >> 48) & (RJ_P - 1);
+}
+
+template <int PASS>
+__device__ inline void rj_scatter_tile(const ColView &key, const uint64_t *h1, const uint32_t *r1,
+                                       int64_t e0, int64_t e1, const int64_t *goff_src,
+                                       int64_t goff_stride, uint64_t *oh, uint32_t *orow) {
+  __shared__ uint64_t sh[RJ_TILE];
+  __shared__ uint32_t sr[RJ_TILE];
+  __shared__ uint32_t cnt[RJ_P];
+  __shared__ uint32_t loff[RJ_P];
+  __shared__ int64_t goff[RJ_P];
+  __shared__ uint32_t lds_scan[17];
+  for (int i = threadIdx.x; i < RJ_P; i += RJ_SBLOCK) {
+    cnt[i] = 0;
+    goff[i] = goff_src[(int64_t)i * goff_stride];
+  }
+  __syncthreads();
+  uint64_t h[RJ_RPT];
+  uint32_t rk[RJ_RPT];
+#pragma unroll
+  for (int k = 0; k < RJ_RPT; ++k) {
+    const int64_t r = e0 + (int64_t)k * RJ_SBLOCK + threadIdx.x;
+    rk[k] = 0xFFFFFFFFu;
+    h[k] = 0;
+    if (r < e1) {
+      bool nul = false;
+      h[k] = PASS == 1 ? fmix64(rj_word(key, r, nul)) : h1[r];
+      if (!nul) rk[k] = atomicAdd(&cnt[rj_bucket<PASS>(h[k])], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t total;
+  const uint32_t c = threadIdx.x < RJ_P ? cnt[threadIdx.x] : 0u;
+  const uint32_t ex = block_exclusive_scan(c, lds_scan, total);
+  if (threadIdx.x < RJ_P) loff[threadIdx.x] = ex;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < RJ_RPT; ++k) {
+    if (rk[k] == 0xFFFFFFFFu) continue;
+    const uint32_t slot = loff[rj_bucket<PASS>(h[k])] + rk[k];
+    sh[slot] = h[k];
+    sr[slot] = PASS == 1 ? (uint32_t)(e0 + (int64_t)k * RJ_SBLOCK + threadIdx.x)
+                         : r1[e0 + (int64_t)k * RJ_SBLOCK + threadIdx.x];
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < total; i += RJ_SBLOCK) {
+    const uint64_t v = sh[i];
+    const uint32_t b = rj_bucket<PASS>(v);
+    const int64_t pos = goff[b] + (int64_t)(i - loff[b]);
+    oh[pos] = v;
+    orow[pos] = sr[i];
+  }
+}
+
+__global__ __launch_bounds__(RJ_SBLOCK) void k_rj_scatter1(ColView key, int64_t n, int64_t ntiles,
                                                             const int64_t *offs, uint64_t *oh,
                                                             uint32_t *orow) {
-  __shared__ uint32_t cur[RJ_P];
   const int64_t t = blockIdx.x, e0 = t * RJ_TILE, e1 = min(e0 + RJ_TILE, n);
-  for (int b = threadIdx.x; b < RJ_P; b += RJ_PBLOCK)
-    cur[b] = (uint32_t)offs[(int64_t)b * ntiles + t];  // < 2^32 rows per side (checked)
-  __syncthreads();
-  const uint64_t base = 0;
-  for (int64_t r = e0 + threadIdx.x; r < e1; r += RJ_PBLOCK) {
-    bool nul;
-    const uint64_t w = rj_word(key, r, nul);
-    if (nul) continue;
-    const uint64_t h = fmix64(w);
-    const uint64_t pos = base + atomicAdd(&cur[h >> 56], 1u);
-    oh[pos] = h;
-    orow[pos] = (uint32_t)r;
-  }
+  rj_scatter_tile<1>(key, nullptr, nullptr, e0, e1, offs + t, ntiles, oh, orow);
 }
 
 // ---------------------------------------------------------------- pass 2
@@ -111,20 +167,11 @@ __global__ __launch_bounds__(RJ_PBLOCK) void k_rj_hist2(const uint64_t *h1, cons
     counts[tl.region + (int64_t)b * tl.ntb + tl.local] = hist[b];
 }
 
-__global__ __launch_bounds__(RJ_PBLOCK) void k_rj_scatter2(const uint64_t *h1, const uint32_t *r1,
+__global__ __launch_bounds__(RJ_SBLOCK) void k_rj_scatter2(const uint64_t *h1, const uint32_t *r1,
                                                             const RJTile2 *tiles, const int64_t *offs,
                                                             uint64_t *oh, uint32_t *orow) {
-  __shared__ unsigned long long cur[RJ_P];
   const RJTile2 tl = tiles[blockIdx.x];
-  for (int b = threadIdx.x; b < RJ_P; b += RJ_PBLOCK)
-    cur[b] = (unsigned long long)offs[tl.region + (int64_t)b * tl.ntb + tl.local];
-  __syncthreads();
-  for (int64_t r = tl.start + threadIdx.x; r < tl.end; r += RJ_PBLOCK) {
-    const uint64_t h = h1[r];
-    const unsigned long long pos = atomicAdd(&cur[(h >> 48) & (RJ_P - 1)], 1ull);
-    oh[pos] = h;
-    orow[pos] = r1[r];
-  }
+  rj_scatter_tile<2>(ColView{}, h1, r1, tl.start, tl.end, offs + tl.region + tl.local, tl.ntb, oh, orow);
 }
 
 // Partition starts: pstart[p] for p = b1·256 + b2 (65 536 partitions), + total.
@@ -172,7 +219,7 @@ static RJSide rj_partition(Session *s, const ColPtr &col, int64_t n) {
   BufPtr h1 = s->alloc(8 * std::max<int64_t>(total, 1)), r1 = s->alloc(4 * std::max<int64_t>(total, 1));
   if (n > 0) {
     KernelTimer kt(s, "rj_partition1", 12.0 * total);
-    hipLaunchKernelGGL(k_rj_scatter1, dim3((unsigned)nt1), dim3(RJ_PBLOCK), 0, s->stream, key, n, nt1,
+    hipLaunchKernelGGL(k_rj_scatter1, dim3((unsigned)nt1), dim3(RJ_SBLOCK), 0, s->stream, key, n, nt1,
                        (const int64_t *)o1->p, (uint64_t *)h1->p, (uint32_t *)r1->p);
     KERNEL_CHECK();
   }
@@ -217,7 +264,7 @@ static RJSide rj_partition(Session *s, const ColPtr &col, int64_t n) {
                        (const uint64_t *)h1->p, (const RJTile2 *)dt->p, (int64_t *)c2->p);
     KERNEL_CHECK();
     exclusive_scan_i64(s, (const int64_t *)c2->p, (int64_t *)o2->p, RJ_P * nt2);
-    hipLaunchKernelGGL(k_rj_scatter2, dim3((unsigned)nt2), dim3(RJ_PBLOCK), 0, s->stream,
+    hipLaunchKernelGGL(k_rj_scatter2, dim3((unsigned)nt2), dim3(RJ_SBLOCK), 0, s->stream,
                        (const uint64_t *)h1->p, (const uint32_t *)r1->p, (const RJTile2 *)dt->p,
                        (const int64_t *)o2->p, (uint64_t *)out.h->p, (uint32_t *)out.row->p);
     KERNEL_CHECK();

@@ -393,16 +393,20 @@ static DataPtr materialize_impl(const NodePtr &n) {
       DataPtr r = materialize(n->kids[1]);
       BufPtr li, ri;
       int64_t m = 0;
+      int key_alias = 0;
       if (n->join_type == CAPF_JOIN_CROSS) {
         m = l->nrows * r->nrows;
         cross_index(s, l->nrows, r->nrows, li, ri);
       } else {
-        JoinPairs jp = radix_join_applies(*l, *r, n->join_keys, n->join_type)
-                           ? radix_join(s, *l, *r, n->join_keys, n->join_type)
-                           : hash_join(s, *l, *r, n->join_keys, n->join_type);
+        JoinPairs jp;
+        if (!dense_join(s, *l, *r, n->join_keys, n->join_type, jp))
+          jp = radix_join_applies(*l, *r, n->join_keys, n->join_type)
+                   ? radix_join(s, *l, *r, n->join_keys, n->join_type)
+                   : hash_join(s, *l, *r, n->join_keys, n->join_type);
         li = jp.left;
         ri = jp.right;
         m = jp.n;
+        key_alias = jp.key_alias;
       }
       auto out = std::make_shared<Data>();
       out->nrows = m;
@@ -411,6 +415,13 @@ static DataPtr materialize_impl(const NodePtr &n) {
       IdxCache cache;  // the columns of one side share one (composed) index
       for (auto &c : l->cols) out->cols.push_back(gather_lazy(s, c, li, m, lnull, &cache));
       for (auto &c : r->cols) out->cols.push_back(gather_lazy(s, c, ri, m, rnull, &cache));
+      if (key_alias) {
+        // the build key column of an inner dense join IS the probe key column
+        // (equal values on every row): no gather of it
+        const size_t kl = (size_t)n->join_keys[0].first, kr = l->cols.size() + (size_t)n->join_keys[0].second;
+        if (key_alias == 1) out->cols[kl] = out->cols[kr];
+        else out->cols[kr] = out->cols[kl];
+      }
       return out;
     }
     case Kind::Union: {

@@ -202,15 +202,72 @@ struct TriBatch {
   uint2 pq[WAVE];          // (#p→q, #q→p)
 };
 
+// One row p: its q's are taken 64 at a time and their lists N+(q) are walked
+// as ONE flattened sequence (lane = position, found by a 6-step search in the
+// batch's prefix table — most lists are far shorter than a wave), TRI_ILP
+// positions per lane in flight, each w searched in N+(p) by `find` (the LDS
+// copy of a short row, the row in global memory — L2-resident while the wave
+// walks it — for a long one).  `qs(k)` = the k-th q of N+(p).
+template <class Q, class F>
+__device__ inline void tri_row(uint32_t a, uint32_t dp, const uint32_t *rowptr, const uint32_t *cols,
+                               const uint2 *vals, TriBatch &tb, Q qs, F find, unsigned long long &t,
+                               unsigned long long &probes, unsigned long long &hits) {
+  const int lane = lane_id();
+  for (uint32_t kb = 0; kb < dp; kb += WAVE) {
+    // the batch's table: one q per lane
+    const uint32_t k = kb + lane;
+    uint32_t qa = 0, dq = 0;
+    uint2 pq = make_uint2(0, 0);
+    if (k < dp) {
+      const uint32_t q = qs(k);
+      qa = rowptr[q];
+      dq = rowptr[q + 1] - qa;
+      pq = vals[a + k];
+    }
+    const uint32_t inc = wave_inclusive_scan(dq);
+    tb.pre[lane] = inc - dq;
+    if (lane == WAVE - 1) tb.pre[WAVE] = inc;
+    tb.qa[lane] = qa;
+    tb.pq[lane] = pq;
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl(inc, WAVE - 1, WAVE));
+    if (lane == 0) probes += total;
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t t0 = 0; t0 < total; t0 += TRI_ILP * WAVE) {
+      uint32_t w[TRI_ILP], pos[TRI_ILP], bi[TRI_ILP];
+#pragma unroll
+      for (int u = 0; u < TRI_ILP; ++u) {
+        const uint32_t x = t0 + u * WAVE + lane;
+        uint32_t b = 0;  // last batch entry with pre[b] <= x
+#pragma unroll
+        for (int st = WAVE / 2; st > 0; st >>= 1)
+          if (tb.pre[b + st] <= x) b += st;
+        bi[u] = b;
+        pos[u] = tb.qa[b] + (x - tb.pre[b]);
+        w[u] = x < total ? cols[pos[u]] : 0xFFFFFFFFu;
+      }
+#pragma unroll
+      for (int u = 0; u < TRI_ILP; ++u) {
+        if (w[u] == 0xFFFFFFFFu) continue;
+        const int64_t i = tri_find(find, dp, w[u]);
+        if (i >= 0) {
+          ++hits;
+          const uint2 pqv = tb.pq[bi[u]], qw = vals[pos[u]], pw = vals[a + i];
+          // p→q→w→p  +  p→w→q→p
+          t += (unsigned long long)pqv.x * qw.x * pw.y + (unsigned long long)pw.x * qw.y * pqv.y;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the table is rewritten by the next batch
+  }
+}
+
 // T over this part's rows into acc[0]: row chunks of TRI_CHUNK are dealt
 // round-robin over the parts (chunk c of the graph belongs to part c mod
-// parts) and handed to waves by an atomic cursor.  N+(p) is staged in LDS;
-// its q's are taken 64 at a time and their lists N+(q) are walked as ONE
-// flattened sequence (lane = position, found by a 6-step search in the
-// batch's prefix table — most lists are far shorter than a wave), TRI_ILP
-// positions per lane in flight, each w binary-searched in the staged row.
-// (An LDS hash table instead of the sorted row, 12 KiB per wave, measured
-// 1.6× slower: the kernel waits on the N+(q) loads, so occupancy wins.)
+// parts) and handed to waves by an atomic cursor.  N+(p) is staged in LDS when
+// it has ≤ TRI_CAP entries (tri_row searches the LDS copy), else searched in
+// place.  (An LDS hash table instead of the sorted row, 12 KiB per wave,
+// measured 1.6× slower: the kernel waits on the N+(q) loads, so occupancy
+// wins.)
 __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count(const uint32_t *rowptr,
                                                           const uint32_t *cols, const uint2 *vals,
                                                           uint64_t len, int parts, int part,
@@ -232,72 +289,16 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count(const uint32_t *rowptr,
     for (uint64_t p = r0; p < r1; ++p) {
       const uint32_t a = rowptr[p], dp = rowptr[p + 1] - a;
       if (dp < 2) continue;  // a triangle needs two out-neighbours at its lowest vertex
-      if (dp > TRI_CAP) {  // rare long row: per q, binary search in global memory
-        for (uint32_t k = 0; k < dp; ++k) {
-          const uint32_t q = cols[a + k];
-          const uint32_t qa = rowptr[q], dq = rowptr[q + 1] - qa;
-          const uint2 pq = vals[a + k];
-          if (lane == 0) probes += dq;
-          for (uint32_t j = lane; j < dq; j += WAVE) {
-            const uint32_t w = cols[qa + j];
-            const int64_t i = tri_find([&](int64_t x) { return cols[a + x]; }, dp, w);
-            if (i >= 0) {
-              ++hits;
-              const uint2 qw = vals[qa + j], pw = vals[a + i];
-              t += (unsigned long long)pq.x * qw.x * pw.y + (unsigned long long)pw.x * qw.y * pq.y;
-            }
-          }
-        }
+      if (dp > TRI_CAP) {  // rare long row: searched in global memory
+        const uint32_t *row = cols + a;
+        tri_row(a, dp, rowptr, cols, vals, tb, [&](uint32_t k) { return row[k]; },
+                [&](int64_t x) { return row[x]; }, t, probes, hits);
         continue;
       }
       for (uint32_t k = lane; k < dp; k += WAVE) sc[k] = cols[a + k];
       __builtin_amdgcn_wave_barrier();
-      for (uint32_t kb = 0; kb < dp; kb += WAVE) {
-        // the batch's table: one q per lane
-        const uint32_t k = kb + lane;
-        uint32_t qa = 0, dq = 0;
-        uint2 pq = make_uint2(0, 0);
-        if (k < dp) {
-          const uint32_t q = sc[k];
-          qa = rowptr[q];
-          dq = rowptr[q + 1] - qa;
-          pq = vals[a + k];
-        }
-        const uint32_t inc = wave_inclusive_scan(dq);
-        tb.pre[lane] = inc - dq;
-        if (lane == WAVE - 1) tb.pre[WAVE] = inc;
-        tb.qa[lane] = qa;
-        tb.pq[lane] = pq;
-        const uint32_t total = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl(inc, WAVE - 1, WAVE));
-        if (lane == 0) probes += total;
-        __builtin_amdgcn_wave_barrier();
-        for (uint32_t t0 = 0; t0 < total; t0 += TRI_ILP * WAVE) {
-          uint32_t w[TRI_ILP], pos[TRI_ILP], bi[TRI_ILP];
-#pragma unroll
-          for (int u = 0; u < TRI_ILP; ++u) {
-            const uint32_t x = t0 + u * WAVE + lane;
-            uint32_t b = 0;  // last batch entry with pre[b] <= x
-#pragma unroll
-            for (int st = WAVE / 2; st > 0; st >>= 1)
-              if (tb.pre[b + st] <= x) b += st;
-            bi[u] = b;
-            pos[u] = tb.qa[b] + (x - tb.pre[b]);
-            w[u] = x < total ? cols[pos[u]] : 0xFFFFFFFFu;
-          }
-#pragma unroll
-          for (int u = 0; u < TRI_ILP; ++u) {
-            if (w[u] == 0xFFFFFFFFu) continue;
-            const int64_t i = tri_find([&](int64_t x) { return sc[x]; }, dp, w[u]);
-            if (i >= 0) {
-              ++hits;
-              const uint2 pqv = tb.pq[bi[u]], qw = vals[pos[u]], pw = vals[a + i];
-              // p→q→w→p  +  p→w→q→p
-              t += (unsigned long long)pqv.x * qw.x * pw.y + (unsigned long long)pw.x * qw.y * pqv.y;
-            }
-          }
-        }
-        __builtin_amdgcn_wave_barrier();  // the table is rewritten by the next batch
-      }
+      tri_row(a, dp, rowptr, cols, vals, tb, [&](uint32_t k) { return sc[k]; },
+              [&](int64_t x) { return sc[x]; }, t, probes, hits);
       __builtin_amdgcn_wave_barrier();  // sc is rewritten by the next row
     }
   }

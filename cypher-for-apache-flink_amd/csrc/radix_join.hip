@@ -190,6 +190,10 @@ __global__ void k_rj_pstart(const int64_t *offs2, const RJTile2 *first_tile_of_b
   }
 }
 
+__global__ void k_rj_bucket_starts(const int64_t *o1, int64_t nt1, int64_t *bstart) {
+  bstart[threadIdx.x] = o1[(int64_t)threadIdx.x * nt1];
+}
+
 // Partitioned side: (h, row) in partition order + partition starts.
 struct RJSide {
   BufPtr h, row, pstart;
@@ -223,13 +227,16 @@ static RJSide rj_partition(Session *s, const ColPtr &col, int64_t n) {
                        (const int64_t *)o1->p, (uint64_t *)h1->p, (uint32_t *)r1->p);
     KERNEL_CHECK();
   }
-  // first-level bucket starts on the host (257 values) → the pass-2 tile list
+  // first-level bucket starts (257 values, gathered on the device) → the
+  // pass-2 tile list on the host
   std::vector<int64_t> bstart(RJ_P + 1);
   {
-    std::vector<int64_t> o1h(RJ_P * nt1 + 1);
-    HIP_CHECK(hipMemcpyAsync(o1h.data(), o1->p, 8 * o1h.size(), hipMemcpyDeviceToHost, s->stream));
+    BufPtr bs = s->alloc(8 * RJ_P);
+    hipLaunchKernelGGL(k_rj_bucket_starts, dim3(1), dim3(RJ_P), 0, s->stream, (const int64_t *)o1->p, nt1,
+                       (int64_t *)bs->p);
+    KERNEL_CHECK();
+    HIP_CHECK(hipMemcpyAsync(bstart.data(), bs->p, 8 * RJ_P, hipMemcpyDeviceToHost, s->stream));
     s->sync();
-    for (int b = 0; b < RJ_P; ++b) bstart[b] = o1h[(size_t)b * nt1];
     bstart[RJ_P] = total;
   }
   std::vector<RJTile2> tiles;
@@ -376,6 +383,25 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_join(const RJWork *work, const
   if (!EMIT && threadIdx.x == 0) out_cnt[blockIdx.x] = item_total;
 }
 
+// Work items per partition p: icnt[p] (heavy build side) or icnt[NPART + p]
+// (light); the scan of the 2·NPART counts lists the heavy items first.
+__global__ void k_rj_item_counts(const int64_t *bst, const int64_t *pst, int64_t *icnt) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nb = bst[p + 1] - bst[p], np = pst[p + 1] - pst[p];
+  const int64_t items = nb > 0 && np > 0 ? (np + RJ_PCHUNK - 1) / RJ_PCHUNK : 0;
+  const bool heavy = nb > RJ_CHUNK;
+  icnt[p] = heavy ? items : 0;
+  icnt[(int64_t)RJ_P * RJ_P + p] = heavy ? 0 : items;
+}
+
+__global__ void k_rj_items(const int64_t *bst, const int64_t *pst, const int64_t *ioff, RJWork *work) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nb = bst[p + 1] - bst[p], q0 = pst[p], q1 = pst[p + 1];
+  if (nb == 0 || q1 == q0) return;
+  int64_t o = ioff[nb > RJ_CHUNK ? p : (int64_t)RJ_P * RJ_P + p];
+  for (int64_t a = q0; a < q1; a += RJ_PCHUNK) work[o++] = RJWork{p, 0, a, min(q1, a + (int64_t)RJ_PCHUNK)};
+}
+
 __global__ void k_rj_unmatched(const uint8_t *matched, int64_t n, uint8_t *flags) {
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
        r += (int64_t)gridDim.x * blockDim.x)
@@ -413,25 +439,22 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
   const bool p_outer = build_left ? right_outer : left_outer;
   RJSide bs = rj_partition(s, bk, B.nrows);
   RJSide ps = rj_partition(s, pk, Pr.nrows);
-  // work items: partitions with probe rows, big probe partitions in chunks
-  std::vector<int64_t> bst(RJ_P * RJ_P + 1), pst(RJ_P * RJ_P + 1);
-  HIP_CHECK(hipMemcpyAsync(bst.data(), bs.pstart->p, 8 * bst.size(), hipMemcpyDeviceToHost, s->stream));
-  HIP_CHECK(hipMemcpyAsync(pst.data(), ps.pstart->p, 8 * pst.size(), hipMemcpyDeviceToHost, s->stream));
-  s->sync();
-  std::vector<RJWork> work;
-  for (int p = 0; p < RJ_P * RJ_P; ++p) {
-    const int64_t q0 = pst[p], q1 = pst[p + 1];
-    if (q1 == q0 || bst[p + 1] == bst[p]) continue;  // no pair can come out of it
-    for (int64_t a = q0; a < q1; a += RJ_PCHUNK) work.push_back(RJWork{p, 0, a, std::min(q1, a + RJ_PCHUNK)});
-  }
-  // LPT-ish: the dispatcher takes work in order — big build partitions first
-  std::stable_sort(work.begin(), work.end(), [&](const RJWork &x, const RJWork &y) {
-    return bst[x.part + 1] - bst[x.part] > bst[y.part + 1] - bst[y.part];
-  });
-  const int64_t nw = (int64_t)work.size();
+  // work items on the device: ⌈probe rows / RJ_PCHUNK⌉ per partition with rows on
+  // both sides; partitions whose build side needs several LDS fills ("heavy",
+  // skewed keys) are listed first so the dispatcher starts them early
+  constexpr int64_t NPART = (int64_t)RJ_P * RJ_P;
+  BufPtr icnt = s->alloc(8 * 2 * NPART), ioff = s->alloc(8 * (2 * NPART + 1));
+  hipLaunchKernelGGL(k_rj_item_counts, dim3((unsigned)(NPART / 256)), dim3(256), 0, s->stream,
+                     (const int64_t *)bs.pstart->p, (const int64_t *)ps.pstart->p, (int64_t *)icnt->p);
+  KERNEL_CHECK();
+  const int64_t nw = exclusive_scan_i64(s, (const int64_t *)icnt->p, (int64_t *)ioff->p, 2 * NPART);
   BufPtr dw = s->alloc(sizeof(RJWork) * std::max<int64_t>(nw, 1));
-  if (nw > 0)
-    HIP_CHECK(hipMemcpyAsync(dw->p, work.data(), sizeof(RJWork) * nw, hipMemcpyHostToDevice, s->stream));
+  if (nw > 0) {
+    hipLaunchKernelGGL(k_rj_items, dim3((unsigned)(NPART / 256)), dim3(256), 0, s->stream,
+                       (const int64_t *)bs.pstart->p, (const int64_t *)ps.pstart->p, (const int64_t *)ioff->p,
+                       (RJWork *)dw->p);
+    KERNEL_CHECK();
+  }
   BufPtr cnt = s->alloc(8 * std::max<int64_t>(nw, 1)), off = s->alloc(8 * (nw + 1));
   int64_t total = 0;
   if (nw > 0) {
@@ -488,7 +511,6 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
   jp.left = build_left ? obuild : oprobe;
   jp.right = build_left ? oprobe : obuild;
   jp.n = m;
-  s->sync();  // the host work list goes out of scope
   return jp;
 }
 

@@ -1369,7 +1369,12 @@ struct C5Shard {
 constexpr int C5S_TILE = 32768;  // rows (= keys) per tile (at most); 16384 via CAPF_SHARD_TILE=16
 constexpr int C5S_MAXHOT = 1;    // heavy-hitter keys of a rank (sampled at ingest, a plan hint)
 constexpr int C5S_MAXR = 520;    // runs incl. the dummy: nbl ≤ 259
-constexpr int C5S_CNT = 1024;    // LDS run counters: copies · (runs + 1) ≤ 1024
+// a tile scans ONE copy, so it fills only its side's ≤ nsb ≤ 259 runs + the
+// dummy: the stage reserves pad slots for those, which leaves room for 2 Ki
+// run counters (more copies per run: fewer same-word LDS atomics when a rank
+// owns few runs) at 2 workgroups per CU
+constexpr int C5S_PADRUNS = 261;
+constexpr int C5S_CNT = 2048;    // LDS run counters: copies · (runs + 1) ≤ 2048
 
 // A rank of a G-GPU node owns few buckets (2·32 + 1 runs at s24, G = 8): the
 // 64 lanes of a counting atomic would pile onto a handful of words.  Each run
@@ -1386,7 +1391,7 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
     C5Shard c, uint16_t *part, uint32_t *meta, uint32_t *tile_acc, int64_t rstride) {
   constexpr int MAXR = C5S_MAXR;
   constexpr int RPT = TILE / C5_BLOCK, GROUPS = RPT / 4;
-  constexpr int STAGE = TILE + 8 * MAXR;
+  constexpr int STAGE = TILE + 8 * C5S_PADRUNS;
   static_assert(MAXR <= C5_BLOCK, "one run per thread in the scan");
   __shared__ uint4 stage4[STAGE / 8];
   __shared__ uint32_t cur[C5S_CNT];

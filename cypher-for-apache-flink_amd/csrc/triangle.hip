@@ -208,10 +208,11 @@ struct TriBatch {
 // positions per lane in flight, each w searched in N+(p) by `find` (the LDS
 // copy of a short row, the row in global memory — L2-resident while the wave
 // walks it — for a long one).  `qs(k)` = the k-th q of N+(p).
-template <class Q, class F>
+template <class Q, class F, class M>
 __device__ inline void tri_row(uint32_t a, uint32_t dp, const uint32_t *rowptr, const uint32_t *cols,
-                               const uint2 *vals, TriBatch &tb, Q qs, F find, unsigned long long &t,
-                               unsigned long long &probes, unsigned long long &hits) {
+                               const uint2 *vals, TriBatch &tb, Q qs, F find, M maybe,
+                               unsigned long long &t, unsigned long long &probes,
+                               unsigned long long &hits) {
   const int lane = lane_id();
   for (uint32_t kb = 0; kb < dp; kb += WAVE) {
     // the batch's table: one q per lane
@@ -247,7 +248,7 @@ __device__ inline void tri_row(uint32_t a, uint32_t dp, const uint32_t *rowptr, 
       }
 #pragma unroll
       for (int u = 0; u < TRI_ILP; ++u) {
-        if (w[u] == 0xFFFFFFFFu) continue;
+        if (w[u] == 0xFFFFFFFFu || !maybe(w[u])) continue;
         const int64_t i = tri_find(find, dp, w[u]);
         if (i >= 0) {
           ++hits;
@@ -268,17 +269,28 @@ __device__ inline void tri_row(uint32_t a, uint32_t dp, const uint32_t *rowptr, 
 // place.  (An LDS hash table instead of the sorted row, 12 KiB per wave,
 // measured 1.6× slower: the kernel waits on the N+(q) loads, so occupancy
 // wins.)
+// FILTER: a per-wave LDS bitmap of hash(w) over the staged N+(p) (8 Ki bits):
+// a probe whose bit is clear is a miss without the binary search (≈ 94 % of
+// the probes miss at s24).
+constexpr int TRI_BM_WORDS = 256;
+__device__ inline uint32_t tri_bit(uint32_t w) { return (w * 0x9E3779B1u) >> 19; }  // 13 bits
+
+template <bool FILTER>
 __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count(const uint32_t *rowptr,
                                                           const uint32_t *cols, const uint2 *vals,
                                                           uint64_t len, int parts, int part,
                                                           unsigned long long *cursor,
                                                           unsigned long long *acc) {
   __shared__ uint32_t s_cols[TRI_BLOCK / WAVE][TRI_CAP];
+  __shared__ uint32_t s_bm[FILTER ? TRI_BLOCK / WAVE : 1][FILTER ? TRI_BM_WORDS : 1];
   __shared__ TriBatch s_tab[TRI_BLOCK / WAVE];
   __shared__ unsigned long long lds[17];
   const int wv = threadIdx.x / WAVE, lane = lane_id();
   uint32_t *sc = s_cols[wv];
+  uint32_t *bm = s_bm[FILTER ? wv : 0];
   TriBatch &tb = s_tab[wv];
+  if (FILTER)
+    for (int k = lane; k < TRI_BM_WORDS; k += WAVE) bm[k] = 0;
   unsigned long long t = 0, probes = 0, hits = 0;
   for (;;) {
     unsigned long long r0 = 0;
@@ -292,14 +304,31 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count(const uint32_t *rowptr,
       if (dp > TRI_CAP) {  // rare long row: searched in global memory
         const uint32_t *row = cols + a;
         tri_row(a, dp, rowptr, cols, vals, tb, [&](uint32_t k) { return row[k]; },
-                [&](int64_t x) { return row[x]; }, t, probes, hits);
+                [&](int64_t x) { return row[x]; }, [](uint32_t) { return true; }, t, probes, hits);
         continue;
       }
-      for (uint32_t k = lane; k < dp; k += WAVE) sc[k] = cols[a + k];
+      for (uint32_t k = lane; k < dp; k += WAVE) {
+        const uint32_t w = cols[a + k];
+        sc[k] = w;
+        if (FILTER) {
+          const uint32_t h = tri_bit(w);
+          atomicOr(&bm[h >> 5], 1u << (h & 31));
+        }
+      }
       __builtin_amdgcn_wave_barrier();
       tri_row(a, dp, rowptr, cols, vals, tb, [&](uint32_t k) { return sc[k]; },
-              [&](int64_t x) { return sc[x]; }, t, probes, hits);
+              [&](int64_t x) { return sc[x]; },
+              [&](uint32_t w) {
+                if (!FILTER) return true;
+                const uint32_t h = tri_bit(w);
+                return ((bm[h >> 5] >> (h & 31)) & 1u) != 0;
+              },
+              t, probes, hits);
       __builtin_amdgcn_wave_barrier();  // sc is rewritten by the next row
+      if (FILTER) {  // clear exactly the bits this row set
+        for (uint32_t k = lane; k < dp; k += WAVE) bm[tri_bit(sc[k]) >> 5] = 0;
+        __builtin_amdgcn_wave_barrier();
+      }
     }
   }
   unsigned long long tot;
@@ -461,9 +490,15 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
   }
   if (g.P > 0) {
     KernelTimer kt(s, "tri_count", 4.0 * g.P);
-    hipLaunchKernelGGL(k_tri_count, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
-                       (const uint32_t *)g.rowptr->p, (const uint32_t *)g.cols->p,
-                       (const uint2 *)g.vals->p, len, parts, part, acc + 3, acc);
+    static const bool filter = getenv("CAPF_TRI_FILTER") && atoi(getenv("CAPF_TRI_FILTER")) == 1;  // measured slower (0.98 vs 0.94 s at s24)
+    if (filter)
+      hipLaunchKernelGGL(k_tri_count<true>, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
+                         (const uint32_t *)g.rowptr->p, (const uint32_t *)g.cols->p,
+                         (const uint2 *)g.vals->p, len, parts, part, acc + 3, acc);
+    else
+      hipLaunchKernelGGL(k_tri_count<false>, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
+                         (const uint32_t *)g.rowptr->p, (const uint32_t *)g.cols->p,
+                         (const uint2 *)g.vals->p, len, parts, part, acc + 3, acc);
     KERNEL_CHECK();
   }
   hipLaunchKernelGGL(k_tri_total, dim3(1), dim3(64), 0, s->stream, (const unsigned long long *)acc,

@@ -208,7 +208,7 @@ struct TriBatch {
 // positions per lane in flight, each w searched in N+(p) by `find` (the LDS
 // copy of a short row, the row in global memory — L2-resident while the wave
 // walks it — for a long one).  `qs(k)` = the k-th q of N+(p).
-template <class Q, class F, class M>
+template <int ILP, class Q, class F, class M>
 __device__ inline void tri_row(uint32_t a, uint32_t dp, const uint32_t *rowptr, const uint32_t *cols,
                                const uint2 *vals, TriBatch &tb, Q qs, F find, M maybe,
                                unsigned long long &t, unsigned long long &probes,
@@ -233,10 +233,10 @@ __device__ inline void tri_row(uint32_t a, uint32_t dp, const uint32_t *rowptr, 
     const uint32_t total = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl(inc, WAVE - 1, WAVE));
     if (lane == 0) probes += total;
     __builtin_amdgcn_wave_barrier();
-    for (uint32_t t0 = 0; t0 < total; t0 += TRI_ILP * WAVE) {
-      uint32_t w[TRI_ILP], pos[TRI_ILP], bi[TRI_ILP];
+    for (uint32_t t0 = 0; t0 < total; t0 += ILP * WAVE) {
+      uint32_t w[ILP], pos[ILP], bi[ILP];
 #pragma unroll
-      for (int u = 0; u < TRI_ILP; ++u) {
+      for (int u = 0; u < ILP; ++u) {
         const uint32_t x = t0 + u * WAVE + lane;
         uint32_t b = 0;  // last batch entry with pre[b] <= x
 #pragma unroll
@@ -247,7 +247,7 @@ __device__ inline void tri_row(uint32_t a, uint32_t dp, const uint32_t *rowptr, 
         w[u] = x < total ? cols[pos[u]] : 0xFFFFFFFFu;
       }
 #pragma unroll
-      for (int u = 0; u < TRI_ILP; ++u) {
+      for (int u = 0; u < ILP; ++u) {
         if (w[u] == 0xFFFFFFFFu || !maybe(w[u])) continue;
         const int64_t i = tri_find(find, dp, w[u]);
         if (i >= 0) {
@@ -275,7 +275,7 @@ __device__ inline void tri_row(uint32_t a, uint32_t dp, const uint32_t *rowptr, 
 constexpr int TRI_BM_WORDS = 256;
 __device__ inline uint32_t tri_bit(uint32_t w) { return (w * 0x9E3779B1u) >> 19; }  // 13 bits
 
-template <bool FILTER>
+template <bool FILTER, int ILP>
 __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count(const uint32_t *rowptr,
                                                           const uint32_t *cols, const uint2 *vals,
                                                           uint64_t len, int parts, int part,
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count(const uint32_t *rowptr,
       if (dp < 2) continue;  // a triangle needs two out-neighbours at its lowest vertex
       if (dp > TRI_CAP) {  // rare long row: searched in global memory
         const uint32_t *row = cols + a;
-        tri_row(a, dp, rowptr, cols, vals, tb, [&](uint32_t k) { return row[k]; },
+        tri_row<ILP>(a, dp, rowptr, cols, vals, tb, [&](uint32_t k) { return row[k]; },
                 [&](int64_t x) { return row[x]; }, [](uint32_t) { return true; }, t, probes, hits);
         continue;
       }
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count(const uint32_t *rowptr,
         }
       }
       __builtin_amdgcn_wave_barrier();
-      tri_row(a, dp, rowptr, cols, vals, tb, [&](uint32_t k) { return sc[k]; },
+      tri_row<ILP>(a, dp, rowptr, cols, vals, tb, [&](uint32_t k) { return sc[k]; },
               [&](int64_t x) { return sc[x]; },
               [&](uint32_t w) {
                 if (!FILTER) return true;
@@ -491,14 +491,12 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
   if (g.P > 0) {
     KernelTimer kt(s, "tri_count", 4.0 * g.P);
     static const bool filter = getenv("CAPF_TRI_FILTER") && atoi(getenv("CAPF_TRI_FILTER")) == 1;  // measured slower (0.98 vs 0.94 s at s24)
-    if (filter)
-      hipLaunchKernelGGL(k_tri_count<true>, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
-                         (const uint32_t *)g.rowptr->p, (const uint32_t *)g.cols->p,
-                         (const uint2 *)g.vals->p, len, parts, part, acc + 3, acc);
-    else
-      hipLaunchKernelGGL(k_tri_count<false>, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
-                         (const uint32_t *)g.rowptr->p, (const uint32_t *)g.cols->p,
-                         (const uint2 *)g.vals->p, len, parts, part, acc + 3, acc);
+    static const int ilp = getenv("CAPF_TRI_ILP") ? atoi(getenv("CAPF_TRI_ILP")) : TRI_ILP;  // tuning
+    auto kern = filter ? (ilp >= 8 ? k_tri_count<true, 8> : ilp <= 2 ? k_tri_count<true, 2> : k_tri_count<true, 4>)
+                       : (ilp >= 8 ? k_tri_count<false, 8> : ilp <= 2 ? k_tri_count<false, 2> : k_tri_count<false, 4>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
+                       (const uint32_t *)g.rowptr->p, (const uint32_t *)g.cols->p,
+                       (const uint2 *)g.vals->p, len, parts, part, acc + 3, acc);
     KERNEL_CHECK();
   }
   hipLaunchKernelGGL(k_tri_total, dim3(1), dim3(64), 0, s->stream, (const unsigned long long *)acc,

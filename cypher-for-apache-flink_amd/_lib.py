@@ -134,9 +134,6 @@ _SIGS = {
                                                POINTER(c_int64)]),
     "capf_chain2_sharded_count_diag": (c_int32, [_S, _T, c_char_p, _T, c_char_p, c_char_p, c_int64, c_int32,
                                                POINTER(c_int64), c_int64, c_int64, c_int32, c_int32, c_void_p]),
-    "capf_chain2_sharded_count_2d": (c_int32, [_S, _T, c_char_p, c_int64, _T, c_char_p, c_char_p, c_int64,
-                                             c_int32, POINTER(c_int64), c_int64, c_int64, c_int32, c_int32,
-                                             c_void_p]),
     "capf_table_node_partition": (c_int32, [_T, c_char_p, c_int64, c_int64, c_int32, c_int32, _PT]),
     "capf_chain2_sharded_count": (c_int32, [_S, _T, c_char_p, _T, c_char_p, c_char_p, c_int64, c_int64,
                                             c_int32, c_int32, c_void_p]),

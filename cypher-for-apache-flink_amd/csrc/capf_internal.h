@@ -418,11 +418,9 @@ BufPtr node_partition_diag_index(Session *s, const ColView &src, const ColView &
                                  int64_t n_nodes, int parts, int part, int64_t *m, int64_t *n_diag);
 // n_diag ≥ 0: only out-copy rows [0, n_diag) can be self-loops (2-D layout); −1: any row
 // nhot / hot_ids: heavy-hitter node ids (a sampled plan hint; any ids are correct)
-// in_skip ≥ 0: the in-copy's first in_skip rows are the out-copy's diagonal
-// block (same rels): the count reads them once, from the out-copy (2-D fold)
 bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out, int64_t lo,
                     int64_t n_nodes, int parts, int part, int64_t *d_partial, int64_t n_diag = -1,
-                    int nhot = 0, const int64_t *hot_ids = nullptr, int64_t in_skip = -1);
+                    int nhot = 0, const int64_t *hot_ids = nullptr);
 // Rows of `keys` (n rows) grouped by owner h(key tuple) of `parts` (shuffle.hip):
 // the permutation (int64 row indexes) and the row count per owner.
 BufPtr route_permutation(Session *s, const std::vector<ColView> &keys, int64_t n, int parts,

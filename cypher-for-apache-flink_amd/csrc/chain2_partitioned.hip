@@ -1363,21 +1363,18 @@ struct C5Shard {
   int64_t n_diag;                // out-copy rows [0, n_diag) may be self-loops (2-D layout:
                                  // rows whose target is owned too come first); the
                                  // target column is read for those rows only
-  // 2-D fold (t_dg > 0): the diagonal block (both endpoints owned) is read ONCE,
-  // by t_dg diag tiles of 4096·gptd out-copy rows that emit both keys of a row
-  // (in-key from the target, out-key from the source) and test self-loops; the
-  // in-copy's first in_skip rows (the same block, in its own 2-D order) are
-  // skipped and the out tiles start at row n_diag.  Bytes per rank: 6·M/G,
-  // the single-GPU share, instead of 6·M/G + 3·M/G².
-  int64_t in_skip, t_dg;
-  int gptd;
   NodeMix mix;
 };
 
 constexpr int C5S_TILE = 32768;  // rows (= keys) per tile (at most); 16384 via CAPF_SHARD_TILE=16
 constexpr int C5S_MAXHOT = 1;    // heavy-hitter keys of a rank (sampled at ingest, a plan hint)
 constexpr int C5S_MAXR = 520;    // runs incl. the dummy: nbl ≤ 259
-constexpr int C5S_CNT = 1024;    // LDS run counters: copies · (runs + 1) ≤ 1024
+// a tile scans ONE copy, so it fills only its side's ≤ nsb ≤ 259 runs + the
+// dummy: the stage reserves pad slots for those, which leaves room for 2 Ki
+// run counters (more copies per run: fewer same-word LDS atomics when a rank
+// owns few runs) at 2 workgroups per CU
+constexpr int C5S_PADRUNS = 261;
+constexpr int C5S_CNT = 2048;    // LDS run counters: copies · (runs + 1) ≤ 2048
 
 // A rank of a G-GPU node owns few buckets (2·32 + 1 runs at s24, G = 8): the
 // 64 lanes of a counting atomic would pile onto a handful of words.  Each run
@@ -1393,8 +1390,8 @@ template <int W, bool WIDE, int TILE, bool HOT>
 __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_c5_shard_partition(
     C5Shard c, uint16_t *part, uint32_t *meta, uint32_t *tile_acc, int64_t rstride) {
   constexpr int MAXR = C5S_MAXR;
-  constexpr int RPT = TILE / C5_BLOCK, GROUPS = RPT / 4, HALF = GROUPS / 2;
-  constexpr int STAGE = TILE + 8 * MAXR;
+  constexpr int RPT = TILE / C5_BLOCK, GROUPS = RPT / 4;
+  constexpr int STAGE = TILE + 8 * C5S_PADRUNS;
   static_assert(MAXR <= C5_BLOCK, "one run per thread in the scan");
   __shared__ uint4 stage4[STAGE / 8];
   __shared__ uint32_t cur[C5S_CNT];
@@ -1402,8 +1399,7 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   __shared__ uint32_t body_end, dummy_n;
   uint16_t *stage = (uint16_t *)stage4;
   const int64_t t = blockIdx.x;
-  // tile kind (block-uniform): 0 in-copy, 1 out-copy, 2 diagonal block (both keys)
-  const int kind = t < c.t_in ? 0 : t < c.t_in + c.t_dg ? 2 : 1;
+  const int side = t >= c.t_in ? 1 : 0;  // block-uniform
   const int nr = 2 * c.nsb;
   const int C = c.copies;
   const uint32_t my_copy = (uint32_t)(lane_id() & (C - 1));
@@ -1413,56 +1409,24 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   for (int i = threadIdx.x; i < STAGE / 8; i += C5_BLOCK) stage4[i] = pad;
   for (int i = threadIdx.x; i < C * (nr + 1); i += C5_BLOCK) cur[i] = 0;
   __syncthreads();
-  const int64_t rows = (int64_t)(kind == 2 ? c.gptd : c.gpt) * 4 * C5_BLOCK;
-  int64_t e0, e1;
-  if (kind == 0) {
-    e0 = c.in_skip + t * rows;
-    e1 = min(e0 + rows, c.n_in);
-  } else if (kind == 2) {
-    e0 = (t - c.t_in) * rows;
-    e1 = min(e0 + rows, c.n_diag);
-  } else {
-    const int64_t first = c.t_dg > 0 ? c.n_diag : 0;  // folded: the diagonal block is done
-    e0 = first + (t - c.t_in - c.t_dg) * rows;
-    e1 = min(e0 + rows, c.n_out);
-  }
-  // the third-column loop test: unfolded out tiles that reach into the block
-  // (diag tiles compare their two keys instead)
-  const bool chk = kind == 1 && c.t_dg == 0 && e0 < c.n_diag;
+  const int64_t ts = side ? t - c.t_in : t;
+  const int64_t rows = (int64_t)c.gpt * 4 * C5_BLOCK;
+  const int64_t e0 = ts * rows, e1 = min(e0 + rows, side ? c.n_out : c.n_in);
+  const bool chk = side && e0 < c.n_diag;  // block-uniform: this tile needs the loop test
   // groups holding rows of this tile (uniform): later groups are skipped, so a
   // short tile never floods the dummy run's counter
-  const int gmax = kind == 2 ? HALF : GROUPS;
-  const int gu = (int)min<int64_t>(min<int64_t>(kind == 2 ? c.gptd : c.gpt, gmax),
-                                   (e1 - e0 + 4 * C5_BLOCK - 1) / (4 * C5_BLOCK));
-  const void *kp = kind == 0 ? c.kin : c.kout;
-  const int64_t kb = kind == 0 ? c.bin : c.bout;
+  const int gu = (int)min<int64_t>(c.gpt, (e1 - e0 + 4 * C5_BLOCK - 1) / (4 * C5_BLOCK));
+  const void *kp = side ? c.kout : c.kin;
+  const int64_t kb = side ? c.bout : c.bin;
   const uint32_t dummy = (uint32_t)nr << C2_BITS;
-  const uint32_t run0 = kind == 0 ? 0u : (uint32_t)c.nsb;  // the key column's side
+  const uint32_t run0 = (uint32_t)(side * c.nsb);
   const uint32_t lsub = (uint32_t)c.lsub, ssh = 16u - lsub;  // h & 0xFFFF >> 16 = 0: no sub-buckets
   uint32_t key[RPT];
   uint32_t lp = 0;
   // heavy hitter (skew handling): keys whose mixed index is c.hot[0] are not
-  // partitioned but counted at the end from the dummy run's stage slots (key 1
-  // for the in side, 2 for the out side; past-the-end rows are key 0)
-  auto mk = [&](uint32_t x, bool okx, uint32_t sd) {
-    const uint32_t h = node_mix_t<WIDE>(x, c.mix);
-    const uint32_t b = (h >> C2_BITS) - (uint32_t)c.b0;  // wraps when below b0
-    const bool ok = okx && b < (uint32_t)c.nbl;
-    const uint32_t run = sd * (uint32_t)c.nsb + (b << lsub) + ((h & 0xFFFF) >> ssh);
-    return HOT ? (ok && h != c.hot[0] ? (run << C2_BITS) | (h & 0xFFFF) : dummy | (ok ? 1u + sd : 0u))
-               : (ok ? (run << C2_BITS) | (h & 0xFFFF) : dummy);
-  };
-  // a diag tile runs in two phases over the same rows: groups [0, HALF) read the
-  // source (out-keys in key[0, 4·HALF)), groups [HALF, GROUPS) the target
-  // (in-keys in the upper half).  A row is a self-loop iff source = target iff
-  // (node_mix is a bijection) its two keys name the same index: in-key + nsb
-  // runs = out-key, or both the hub's dummy keys — no third column read.
-  const bool dgt = kind == 2;
-  const uint32_t loop_off = (uint32_t)c.nsb << C2_BITS;
-  auto live = [&](int g) { return dgt ? (g % HALF) < gu : g < gu; };
-  auto grow = [&](int g) { return dgt ? g % HALF : g; };  // row group of group g
-  auto gcol = [&](int g) { return dgt && g >= HALF ? c.oth : kp; };
-  auto gbase = [&](int g) { return dgt && g >= HALF ? c.both : kb; };
+  // partitioned but counted at the end from the dummy run's stage slots — one
+  // compare per key and no counter register (32 keys per thread already fill
+  // the VGPR budget); no hint = 0xFFFFFFFF, never a mixed index
   // the next group's loads are issued before this group's hashing/counting
   uint32_t px[2][4], py[2][4];
   bool pox[2][4], poy[2][4];
@@ -1473,29 +1437,38 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   }
 #pragma unroll
   for (int g = 0; g < GROUPS; ++g) {
-    if (live(g)) {  // static index per unrolled group: key[] stays in VGPRs
-      // the next live group (a diag tile jumps from its last phase-1 group to HALF)
-      const int gn = dgt && g < HALF && g + 1 >= gu ? HALF : g + 1;
-      if (gn < GROUPS && live(gn)) {
-        const int64_t en = e0 + 4 * ((int64_t)grow(gn) * C5_BLOCK + threadIdx.x);
-        c5_load4<W, true>(gcol(gn), gbase(gn), c.lo, c.len, en, e1, true, px[(g + 1) & 1], pox[(g + 1) & 1]);
+    if (g < gu) {  // static index per unrolled group: key[] stays in VGPRs
+      if (g + 1 < gu) {
+        const int64_t en = e0 + 4 * ((int64_t)(g + 1) * C5_BLOCK + threadIdx.x);
+        c5_load4<W, true>(kp, kb, c.lo, c.len, en, e1, true, px[(g + 1) & 1], pox[(g + 1) & 1]);
         if (chk)
           c5_load4<W, true>(c.oth, c.both, c.lo, c.len, en, e1, true, py[(g + 1) & 1], poy[(g + 1) & 1]);
       }
-      // unfolded out tile: rows of this group's 4 in the leading diagonal block
+      uint32_t x[4], y[4];
+      bool okx[4], oky[4];
+      // rows of this group's 4 that lie in the diagonal block (2-D order)
       const uint32_t dg = chk ? (uint32_t)min<int64_t>(max<int64_t>(
                                     c.n_diag - (e0 + 4 * ((int64_t)g * C5_BLOCK + threadIdx.x)), 0), 4)
                               : 0u;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const uint32_t x = px[g & 1][k];
-        const uint32_t sd = dgt ? (g < HALF ? 1u : 0u) : run0 ? 1u : 0u;
-        key[4 * g + k] = mk(x, pox[g & 1][k], sd);
-        if (dgt && g >= HALF) {
-          const uint32_t ko = key[4 * (g - HALF) + k], ki = key[4 * g + k];
-          lp += ((ki < dummy && ko == ki + loop_off) || (HOT && ki == (dummy | 1u) && ko == (dummy | 2u))) ? 1u : 0u;
-        }
-        if (chk) lp += (pox[g & 1][k] && poy[g & 1][k] && x == py[g & 1][k] && (uint32_t)k < dg) ? 1u : 0u;
+        x[k] = px[g & 1][k];
+        y[k] = py[g & 1][k];
+        okx[k] = pox[g & 1][k];
+        oky[k] = poy[g & 1][k];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t h = node_mix_t<WIDE>(x[k], c.mix);
+        const uint32_t b = (h >> C2_BITS) - (uint32_t)c.b0;  // wraps when below b0
+        const bool ok = okx[k] && b < (uint32_t)c.nbl;
+        // a heavy hitter goes to the dummy run: counted here, never copied out
+        // the heavy hitter (mixed index) goes to the dummy run as key 1 (past-the-end
+        // rows as key 0): never copied out, counted in the dummy run's stage slots
+        const uint32_t run = run0 + (b << lsub) + ((h & 0xFFFF) >> ssh);
+        key[4 * g + k] = HOT ? (ok && h != c.hot[0] ? (run << C2_BITS) | (h & 0xFFFF) : dummy | (ok ? 1u : 0u))
+                             : (ok ? (run << C2_BITS) | (h & 0xFFFF) : dummy);
+        if (chk) lp += (ok && oky[k] && x[k] == y[k] && (uint32_t)k < dg) ? 1u : 0u;
         atomicAdd(&cur[(key[4 * g + k] >> C2_BITS) * C + my_copy], 1u);
       }
     }
@@ -1527,53 +1500,43 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < RPT; ++j) {
-    // diag tiles: out-keys in slots [0, 4·gu), in-keys in [4·HALF, 4·HALF + 4·gu)
-    const int jj = j < 4 * HALF ? j : j - 4 * HALF;
-    const bool live = kind == 2 ? jj < 4 * gu : j < 4 * gu;
-    if (live) stage[atomicAdd(&cur[(key[j] >> C2_BITS) * C + my_copy], 1u)] = (uint16_t)key[j];
+    if (j < 4 * gu) stage[atomicAdd(&cur[(key[j] >> C2_BITS) * C + my_copy], 1u)] = (uint16_t)key[j];
     if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
   }
   __syncthreads();
   uint4 *dst = (uint4 *)(part + t * rstride);
   for (uint32_t i = threadIdx.x; i < body_end / 8; i += C5_BLOCK) dst[i] = stage4[i];
-  // the heavy hitter's keys of this tile: the 1s (in) and 2s (out) of the dummy run's slots
-  uint32_t hi = 0, ho = 0;
+  // the heavy hitter's keys of this tile: the 1s of the dummy run's slots
+  uint32_t hn = 0;
   if (HOT)
-    for (uint32_t i = threadIdx.x; i < dummy_n; i += C5_BLOCK) {
-      const uint16_t v = stage[body_end + i];
-      hi += v == 1 ? 1u : 0u;
-      ho += v == 2 ? 1u : 0u;
-    }
-  // per-tile (self-loops, hot in, hot out) with plain stores, summed by
-  // k_sharded_final: one same-address device atomic per wave serialises at the
-  // memory side (~88 per µs on one word: 2·10^3 tiles × 16 waves ≈ 0.37 ms)
-  __shared__ uint32_t red[3][C5_BLOCK / WAVE];
+    for (uint32_t i = threadIdx.x; i < dummy_n; i += C5_BLOCK) hn += stage[body_end + i] == 1 ? 1u : 0u;
+  // per-tile (self-loops, hot keys) with plain stores, summed by k_sharded_final:
+  // one same-address device atomic per wave serialises at the memory side
+  // (~88 per µs on one word: 2·10^3 tiles × 16 waves ≈ 0.37 ms)
+  __shared__ uint32_t red[2][C5_BLOCK / WAVE];
   const uint32_t l32 = (uint32_t)wave_reduce_sum((unsigned long long)lp);
-  const uint32_t i32 = (uint32_t)wave_reduce_sum((unsigned long long)hi);
-  const uint32_t o32 = (uint32_t)wave_reduce_sum((unsigned long long)ho);
+  const uint32_t h32 = (uint32_t)wave_reduce_sum((unsigned long long)hn);
   if (lane_id() == 0) {
     red[0][threadIdx.x / WAVE] = l32;
-    red[1][threadIdx.x / WAVE] = i32;
-    red[2][threadIdx.x / WAVE] = o32;
+    red[1][threadIdx.x / WAVE] = h32;
   }
   __syncthreads();
-  if (threadIdx.x < 3) {
+  if (threadIdx.x < 2) {
     uint32_t v = 0;
     for (int w = 0; w < C5_BLOCK / WAVE; ++w) v += red[threadIdx.x][w];
-    tile_acc[3 * t + threadIdx.x] = v;
+    tile_acc[2 * t + threadIdx.x] = v;
   }
 }
 
 // this rank's partial: Σ in·out over the partitioned keys (acc[0]) + hot_in·hot_out −
-// self-loops; tile_acc = (loops, hot in-keys, hot out-keys) per P1 tile
+// self-loops; tile_acc = (loops, hot keys) per P1 tile, tiles [0, t_in) in-copy
 __global__ __launch_bounds__(1024) void k_sharded_final(const unsigned long long *acc, const uint32_t *tile_acc,
-                                                        int64_t ntiles, int64_t *out) {
+                                                        int64_t ntiles, int64_t t_in, int64_t *out) {
   __shared__ unsigned long long lds[3][17];
   unsigned long long lp = 0, hi = 0, ho = 0;
   for (int64_t t = threadIdx.x; t < ntiles; t += blockDim.x) {
-    lp += tile_acc[3 * t];
-    hi += tile_acc[3 * t + 1];
-    ho += tile_acc[3 * t + 2];
+    lp += tile_acc[2 * t];
+    (t < t_in ? hi : ho) += tile_acc[2 * t + 1];
   }
   const unsigned long long L = block_reduce_sum(lp, lds[0]), I = block_reduce_sum(hi, lds[1]),
                            O = block_reduce_sum(ho, lds[2]);
@@ -2324,7 +2287,7 @@ uint8_t *node_owner_flags(Session *s, const ColView &key, int64_t n, int64_t lo,
 // FOR32, 16-B aligned, non-null.  Histograms live in session scratch.
 bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out, int64_t lo,
                     int64_t n_nodes, int parts, int part, int64_t *d_partial, int64_t n_diag,
-                    int nhot, const int64_t *hot_ids, int64_t in_skip) {
+                    int nhot, const int64_t *hot_ids) {
   const int kbits = chain2_hist_bits(n_nodes);
   int b0, nbl;
   owned_buckets(kbits, parts, part, &b0, &nbl);
@@ -2344,7 +2307,7 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
   unsigned long long *d_acc = (unsigned long long *)acc->p;  // [0] Σ in·out
   BufPtr tacc;  // P1's per-tile (self-loops, hot keys)
   uint32_t *tile_acc = nullptr;
-  int64_t ntiles_all = 0;
+  int64_t ntiles_all = 0, t_in_all = 0;
   // heavy hitters: distinct ids inside the node range (others could never match a key)
   uint32_t hot[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};  // mixed indexes (< 2^31: never all ones)
   int nh = 0;
@@ -2376,19 +2339,8 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
     c.nhot = nh;
     c.hot[0] = hot[0];
     c.hot[1] = hot[1];
-    // sub-bucket units (k_c5_sb_gather) when the runs fit P1 and the two
-    // counter arrays fit LDS; CAPF_SHARD_SB=0 (tuning) keeps the slice path
-    const int lsub = c5sb_lsub(nbl);
-    // 2-D fold (C5Shard::t_dg): the slice paths only; CAPF_SHARD_FOLD=0 (tuning) off
-    const char *fe = getenv("CAPF_SHARD_FOLD");
-    const bool fold = in_skip >= 0 && in_skip <= n_in && n_diag >= 0 && lsub == 0 &&
-                      c5s_mode() != 3 && !(fe && atoi(fe) == 0);
-    c.in_skip = fold ? in_skip : 0;
-    const int64_t nd = fold ? c.n_diag : 0;
-    const int64_t rin = n_in - c.in_skip, rout = n_out - nd;
     // tile size: whole rounds of resident blocks (2 per CU), counting one
-    // group of per-tile overhead (stage fill, scan, copy-out); a diag tile
-    // holds half the rows (two keys per row)
+    // group of per-tile overhead (stage fill, scan, copy-out)
     const char *te = getenv("CAPF_SHARD_TILE");  // tuning: 16 → 16 Ki-row tiles
     // (32 Ki-row tiles need 32 keys per thread in VGPRs: no spills at FOR24 only)
     const int tile = (te && atoi(te) == 16) || W != 3 ? 16384 : C5S_TILE;
@@ -2397,8 +2349,7 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
       int64_t best = -1;
       for (int g = tile / (4 * C5_BLOCK); g >= 1; --g) {
         const int64_t rows = (int64_t)g * 4 * C5_BLOCK;
-        const int64_t rows_d = (int64_t)std::max(1, g / 2) * 4 * C5_BLOCK;
-        const int64_t tiles = (rin + rows - 1) / rows + (nd + rows_d - 1) / rows_d + (rout + rows - 1) / rows;
+        const int64_t tiles = (n_in + rows - 1) / rows + (n_out + rows - 1) / rows;
         const int64_t cost = (tiles + slots - 1) / slots * (g + 1);
         if (best < 0 || cost < best) {
           best = cost;
@@ -2406,20 +2357,22 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
         }
       }
     }
-    c.gptd = std::max(1, c.gpt / 2);
-    const int64_t trows = (int64_t)c.gpt * 4 * C5_BLOCK, drows = (int64_t)c.gptd * 4 * C5_BLOCK;
-    c.t_in = (rin + trows - 1) / trows;
-    c.t_dg = (nd + drows - 1) / drows;
-    const int64_t t_out = (rout + trows - 1) / trows;
-    const int64_t ntiles = c.t_in + c.t_dg + t_out;
-    tacc = s->alloc(12 * std::max<int64_t>(ntiles, 1));
+    const int64_t trows = (int64_t)c.gpt * 4 * C5_BLOCK;
+    c.t_in = (n_in + trows - 1) / trows;
+    const int64_t t_out = (n_out + trows - 1) / trows;
+    const int64_t ntiles = c.t_in + t_out;
+    tacc = s->alloc(8 * std::max<int64_t>(ntiles, 1));
     tile_acc = (uint32_t *)tacc->p;
     ntiles_all = ntiles;
+    t_in_all = c.t_in;
     c.lo = lo;
     c.len = (uint64_t)n_nodes;
     c.b0 = b0;
     c.nbl = nbl;
     c.mix = node_mix_for(kbits);
+    // sub-bucket units (k_c5_sb_gather) when the runs fit P1 and the two
+    // counter arrays fit LDS; CAPF_SHARD_SB=0 (tuning) keeps the slice path
+    const int lsub = c5sb_lsub(nbl);
     c.lsub = lsub;
     c.nsb = nbl << lsub;
     const int nr = 2 * c.nsb;
@@ -2429,7 +2382,7 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
       BufPtr partb = s->alloc(2 * rstride * ntiles);
       BufPtr meta = s->alloc(4 * nr * ntiles);
       {
-        KernelTimer kt(s, "c5_partition", (double)W * (rin + rout + 2 * nd + (fold ? 0 : c.n_diag)));
+        KernelTimer kt(s, "c5_partition", (double)W * (n_in + 2 * n_out));
         auto kern = tile == C5S_TILE ? c5s_kernel<C5S_TILE>(W, kbits > 24, nh > 0)
                                      : c5s_kernel<16384>(W, kbits > 24, nh > 0);
         hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(C5_BLOCK), 0, s->stream, c,
@@ -2447,7 +2400,7 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
         sd.split_x16 = c3_split_x16();
         sd.nb = nbl;
         sd.t0[0] = 0;
-        sd.t1[0] = c.t_in + c.t_dg;  // diag tiles hold keys of both sides
+        sd.t1[0] = c.t_in;
         sd.t0[1] = c.t_in;
         sd.t1[1] = ntiles;
         const int S = c5_slices(nr);
@@ -2507,7 +2460,7 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
     }
   }
   hipLaunchKernelGGL(k_sharded_final, dim3(1), dim3(1024), 0, s->stream, (const unsigned long long *)d_acc,
-                     tile_acc, ntiles_all, d_partial);
+                     tile_acc, ntiles_all, t_in_all, d_partial);
   KERNEL_CHECK();
   return true;
 }

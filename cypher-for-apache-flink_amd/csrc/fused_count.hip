@@ -1361,17 +1361,6 @@ extern "C" capf_status capf_chain2_sharded_count_diag(capf_session *cs, capf_tab
                                                       const int64_t *hot_ids, int64_t node_base,
                                                       int64_t n_nodes, int32_t parts, int32_t part,
                                                       int64_t *d_partial) {
-  return capf_chain2_sharded_count_2d(cs, in_copy, in_dst, -1, out_copy, out_src, out_dst, n_diag, n_hot,
-                                      hot_ids, node_base, n_nodes, parts, part, d_partial);
-}
-
-extern "C" capf_status capf_chain2_sharded_count_2d(capf_session *cs, capf_table *in_copy,
-                                                    const char *in_dst, int64_t in_skip,
-                                                    capf_table *out_copy, const char *out_src,
-                                                    const char *out_dst, int64_t n_diag, int32_t n_hot,
-                                                    const int64_t *hot_ids, int64_t node_base,
-                                                    int64_t n_nodes, int32_t parts, int32_t part,
-                                                    int64_t *d_partial) {
   try {
     if (!cs || !in_copy || !out_copy || !in_dst || !out_src || !out_dst || !d_partial)
       illegal("null argument");
@@ -1379,8 +1368,6 @@ extern "C" capf_status capf_chain2_sharded_count_2d(capf_session *cs, capf_table
     if (parts <= 0 || part < 0 || part >= parts) illegal("part out of range");
     Session *s = &cs->impl;
     DataPtr di = materialize(in_copy->node), dout = materialize(out_copy->node);
-    if (in_skip >= 0 && (n_diag < 0 || in_skip != std::min(n_diag, dout->nrows) || in_skip > di->nrows))
-      illegal("2-D fold: the in-copy's leading block must be the out-copy's diagonal block");
     const ColPtr &a = di->cols[in_copy->node->col_index_or_throw(in_dst)];
     const ColPtr &b = dout->cols[out_copy->node->col_index_or_throw(out_src)];
     const ColPtr &c = dout->cols[out_copy->node->col_index_or_throw(out_dst)];
@@ -1389,7 +1376,7 @@ extern "C" capf_status capf_chain2_sharded_count_2d(capf_session *cs, capf_table
         illegal("sharded 2-hop count needs non-null INTEGER endpoint columns");
     const ColView cols[3] = {view_of(a), view_of(b), view_of(c)};
     if (!chain2_sharded(s, cols, di->nrows, dout->nrows, node_base, n_nodes, parts, part,
-                        d_partial, n_diag, n_hot, hot_ids, in_skip))
+                        d_partial, n_diag, n_hot, hot_ids))
       not_impl("sharded 2-hop count: shape outside the kernel's limits (buckets per rank, "
                "rows per copy < 2^31, mixed encodings)");
     return CAPF_OK;

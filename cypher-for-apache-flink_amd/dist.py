@@ -103,24 +103,18 @@ def node_partitioned_copies(rels, n_nodes, world, rank, node_base=0, src="source
     fits 24 bits; False: int64).  diag: the out-copy in 2-D order — the rels
     whose target the rank owns too first, their count as `out_copy.n_diag`
     (a block partition of the adjacency matrix by (owner(src), owner(dst)));
-    the in-copy likewise (rels whose source the rank owns too first,
-    `in_copy.n_diag`, the same block): the count reads that block once, from
-    the out-copy, taking both keys of a row and testing self-loops by key
-    equality.  Graph-ingest step, outside the timed query."""
+    only those can be self-loops, so the count reads the target column of
+    1/G of the out-copy instead of all of it.  Graph-ingest step, outside the
+    timed query."""
     from .table import compact_as
     if diag:
         out_copy, n_diag = rels.node_partition_diag(src, dst, node_base, n_nodes, world, rank)
-        # the in-copy in 2-D order too: its leading block is the same rels
-        in_copy, in_diag = rels.node_partition_diag(dst, src, node_base, n_nodes, world, rank)
-        if in_diag != n_diag:
-            raise AssertionError(f"diagonal blocks differ: {in_diag} vs {n_diag}")
     else:
         out_copy, n_diag = rels.node_partition(src, node_base, n_nodes, world, rank), -1
-        in_copy, in_diag = rels.node_partition(dst, node_base, n_nodes, world, rank), -1
+    in_copy = rels.node_partition(dst, node_base, n_nodes, world, rank)
     out_copy = compact_as(out_copy, compact)  # compaction keeps the row order
     out_copy.n_diag = n_diag
     in_copy = compact_as(in_copy, compact)
-    in_copy.n_diag = in_diag
     out_copy.hot_ids = heavy_hitters(in_copy, dst, out_copy, src)
     return in_copy, out_copy
 

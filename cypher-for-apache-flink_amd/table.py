@@ -449,20 +449,10 @@ def chain2_sharded_count_async(session, in_copy, out_copy, node_base, n_nodes, p
                                d_partial, src="source", dst="target"):
     """Enqueue this rank's 2-hop partial (int64 at device address d_partial).
     An out-copy in 2-D order (node_partition_diag) carries `n_diag`: only its
-    first n_diag rows are tested for self-loops.  When the in-copy is in 2-D
-    order too (its `n_diag` leading rows = the same diagonal block), the block
-    is read once, from the out-copy (capf_chain2_sharded_count_2d)."""
+    first n_diag rows are tested for self-loops."""
     hot = list(getattr(out_copy, "hot_ids", ()))[:2]
-    n_diag = int(getattr(out_copy, "n_diag", -1))
-    in_skip = int(getattr(in_copy, "n_diag", -1))
-    if n_diag >= 0 and in_skip >= 0 and os.environ.get("CAPF_SHARD_FOLD", "0") != "0":
-        # both copies in 2-D order: the shared diagonal block is read once
-        _lib.call("capf_chain2_sharded_count_2d", session._h, in_copy._h, dst.encode(), in_skip, out_copy._h,
-                  src.encode(), dst.encode(), n_diag, len(hot), (c_int64 * max(len(hot), 1))(*hot),
-                  int(node_base), int(n_nodes), int(parts), int(part), c_void_p(d_partial))
-        return
     _lib.call("capf_chain2_sharded_count_diag", session._h, in_copy._h, dst.encode(), out_copy._h,
-              src.encode(), dst.encode(), n_diag, len(hot),
+              src.encode(), dst.encode(), int(getattr(out_copy, "n_diag", -1)), len(hot),
               (c_int64 * max(len(hot), 1))(*hot), int(node_base), int(n_nodes), int(parts), int(part),
               c_void_p(d_partial))
 

@@ -397,19 +397,6 @@ capf_status capf_chain2_sharded_count_diag(capf_session *s, capf_table *in_copy,
                                            const int64_t *hot_ids, int64_t node_base,
                                            int64_t n_nodes, int32_t parts, int32_t part,
                                            int64_t *d_partial);
-/* Both copies in 2-D order (capf_table_node_partition_diag on (source,
- * target) for the out-copy and on (target, source) for the in-copy): their
- * leading blocks are the same rels, those with both endpoints owned
- * (in_skip = n_diag rows).  capf_chain2_sharded_count_2d reads that block
- * once, from the out-copy, taking both keys of each row (in-key from the
- * target, out-key from the source), and skips the in-copy's first in_skip
- * rows: a rank reads 6·M/G key bytes (FOR24) — its share of the single-GPU
- * scan — instead of 6·M/G + 3·M/G².  in_skip = -1 is _diag.                */
-capf_status capf_chain2_sharded_count_2d(capf_session *s, capf_table *in_copy, const char *in_dst,
-                                         int64_t in_skip, capf_table *out_copy, const char *out_src,
-                                         const char *out_dst, int64_t n_diag, int32_t n_hot,
-                                         const int64_t *hot_ids, int64_t node_base, int64_t n_nodes,
-                                         int32_t parts, int32_t part, int64_t *d_partial);
 /* Directed triangle (a)-->(b)-->(c)-->(a) with pairwise distinct rels over
  * the rels of `rels` whose endpoints lie in [node_base, node_base + n_nodes)
  * (the fused form of Expand, Expand, ExpandInto + uniqueness,

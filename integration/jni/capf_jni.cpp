@@ -559,22 +559,6 @@ JNI(void, chain2ShardedCountDiag)(JNIEnv *env, jobject, jlong s, jlong in_copy, 
                                            hot.data(), node_base, n_nodes, parts, part,
                                            reinterpret_cast<int64_t *>(d_partial)));
 }
-JNI(void, chain2ShardedCount2d)(JNIEnv *env, jobject, jlong s, jlong in_copy, jstring in_dst,
-                                jlong in_skip, jlong out_copy, jstring out_src, jstring out_dst,
-                                jlong n_diag, jlongArray hot_ids, jlong node_base, jlong n_nodes,
-                                jint parts, jint part, jlong d_partial) {
-  JStr id(env, in_dst), os(env, out_src), od(env, out_dst);
-  const jsize nh = hot_ids ? env->GetArrayLength(hot_ids) : 0;
-  std::vector<int64_t> hot(nh > 0 ? nh : 1);
-  if (nh > 0) {
-    std::vector<jlong> h(nh);
-    env->GetLongArrayRegion(hot_ids, 0, nh, h.data());
-    for (jsize i = 0; i < nh; ++i) hot[i] = h[i];
-  }
-  fail(env, capf_chain2_sharded_count_2d(S(s), T(in_copy), id.p, in_skip, T(out_copy), os.p, od.p, n_diag,
-                                         nh, hot.data(), node_base, n_nodes, parts, part,
-                                         reinterpret_cast<int64_t *>(d_partial)));
-}
 JNI(void, triangleCountPart)(JNIEnv *env, jobject, jlong s, jlong rels, jstring src_col,
                              jstring dst_col, jlong node_base, jlong n_nodes, jint parts,
                              jint part, jlong d_count) {

@@ -153,9 +153,6 @@ object Native {
   @native def chain2ShardedCountDiag(session: Long, inCopy: Long, inDst: String, outCopy: Long, outSrc: String,
                                      outDst: String, nDiag: Long, hotIds: Array[Long], nodeBase: Long,
                                      nNodes: Long, parts: Int, part: Int, dPartial: Long): Unit
-  @native def chain2ShardedCount2d(session: Long, inCopy: Long, inDst: String, inSkip: Long, outCopy: Long,
-                                   outSrc: String, outDst: String, nDiag: Long, hotIds: Array[Long],
-                                   nodeBase: Long, nNodes: Long, parts: Int, part: Int, dPartial: Long): Unit
   @native def triangleCountPart(session: Long, rels: Long, srcCol: String, dstCol: String, nodeBase: Long,
                                 nNodes: Long, parts: Int, part: Int, dCount: Long): Unit
   @native def chain2HistLen(nNodes: Long): Long

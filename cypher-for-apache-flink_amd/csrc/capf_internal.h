@@ -130,6 +130,10 @@ struct Column {
   mutable std::shared_ptr<void> index;
   // the direct-address index of a dense unique id column (dense_join.hip)
   mutable std::shared_ptr<void> dense;
+  // the membership bitmap of this (unique) key column over [bits_key[0],
+  // bits_key[1]] (fused_count.hip message passing)
+  mutable std::shared_ptr<void> bits;
+  mutable int64_t bits_key[2] = {0, 0};
   mutable std::weak_ptr<Column> index_peer;
   mutable int64_t index_key[2] = {0, 0};
   bool is_all_null() const { return type == Type::Null; }

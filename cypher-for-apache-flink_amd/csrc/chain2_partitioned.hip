@@ -34,6 +34,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "capf_internal.h"
@@ -152,7 +153,31 @@ __device__ inline void c5_load4(const void *p, int64_t base, int64_t lo, uint64_
 // keys go straight from registers to the tile region (the streaming floor of
 // P1's bytes); 2 = the count phase and scan, no scatter (the stage prefill is
 // copied out).
-template <int W, bool ALIAS, bool CHECK, bool RAGGED, class SH, int DIAG = 0>
+// Raw row data of one load group (4 rows of a FOR24 / FOR32 column) and its
+// decoding to node offsets (id − lo) — the !CHECK form of c5_load4.
+template <int W>
+using C5Raw = typename std::conditional<W == 3, U3, uint4>::type;
+
+template <int W>
+__device__ inline void c5_decode(const C5Raw<W> &t, uint32_t d, uint32_t o[4]) {
+  if constexpr (W == 3) {
+    o[0] = (t.x & 0xFFFFFFu) + d;
+    o[1] = (__builtin_amdgcn_alignbit(t.y, t.x, 24) & 0xFFFFFFu) + d;
+    o[2] = (__builtin_amdgcn_alignbit(t.z, t.y, 16) & 0xFFFFFFu) + d;
+    o[3] = (t.z >> 8) + d;
+  } else {
+    o[0] = t.x + d;
+    o[1] = t.y + d;
+    o[2] = t.z + d;
+    o[3] = t.w + d;
+  }
+}
+
+// UPF (ALIAS, in-range, full tiles, FOR24 / FOR32): every load of the tile is
+// issued before the first key is counted — 2 × GROUPS raw loads in flight per
+// thread (96 B at FOR24) instead of one group ahead; the raw registers of a
+// group die as its keys appear, so the peak stays within 64 VGPRs.
+template <int W, bool ALIAS, bool CHECK, bool RAGGED, class SH, int DIAG = 0, int UPF = 0>
 __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_c5_partition(C5Cols<W> c, uint16_t *part,
                                                             uint32_t *meta,
                                                             unsigned long long *loops,
@@ -180,17 +205,45 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   const uint32_t dummy = (uint32_t)nr << C2_BITS;
   uint32_t kin[RPT], kout[RPT];
   uint32_t lp = 0;
+  constexpr bool UPFRONT = UPF != 0 && ALIAS && !CHECK && !RAGGED && (W == 3 || W == 4) && DIAG == 0;
+  if constexpr (UPFRONT) {
+    C5Raw<W> ru[GROUPS], rv[GROUPS];
+#pragma unroll
+    for (int g = 0; g < GROUPS; ++g) {
+      const int64_t e = e0 + 4 * ((int64_t)g * C5_BLOCK + threadIdx.x);
+      ru[g] = *(const C5Raw<W> *)((const uint8_t *)c.u1 + W * e);
+      rv[g] = *(const C5Raw<W> *)((const uint8_t *)c.v1 + W * e);
+    }
+    const uint32_t du = (uint32_t)(c.bu1 - c.lo), dv = (uint32_t)(c.bv1 - c.lo);
+#pragma unroll
+    for (int g = 0; g < GROUPS; ++g) {
+      uint32_t x1[4], y1[4];
+      c5_decode<W>(ru[g], du, x1);
+      c5_decode<W>(rv[g], dv, y1);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int j = 4 * g + k;
+        kin[j] = node_mix_t<SH::WIDE>(y1[k], c.mix);
+        kout[j] = node_mix_t<SH::WIDE>(x1[k], c.mix) + out_run0;
+        lp += y1[k] == x1[k] ? 1u : 0u;
+        atomicAdd(&cur[kin[j] >> C2_BITS], 1u);
+        atomicAdd(&cur[kout[j] >> C2_BITS], 1u);
+      }
+      asm volatile("" : "+v"(lp));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
   // ALIAS: the next group's two loads are issued before this group's hashing
   // and counting (double-buffered registers; the unrolled loop renames them)
   uint32_t px[2][4], py[2][4];
   bool pox[2][4], poy[2][4];
-  if (ALIAS) {
+  if (ALIAS && !UPFRONT) {
     const int64_t e = e0 + 4 * (int64_t)threadIdx.x;
     c5_load4<W, CHECK>(c.u1, c.bu1, c.lo, c.len, e, e1, RAGGED, px[0], pox[0]);
     c5_load4<W, CHECK>(c.v1, c.bv1, c.lo, c.len, e, e1, RAGGED, py[0], poy[0]);
   }
 #pragma unroll
-  for (int g = 0; g < GROUPS; ++g) {
+  for (int g = 0; g < (UPFRONT ? 0 : GROUPS); ++g) {
     const int64_t e = e0 + 4 * ((int64_t)g * C5_BLOCK + threadIdx.x);
     uint32_t x1[4], y1[4], x2[4], y2[4];
     bool okx1[4], oky1[4], okx2[4], oky2[4];
@@ -1016,8 +1069,11 @@ static void launch_c5(Session *s, const C5Cols<W> &c, uint16_t *part, uint32_t *
   if (nfull > 0) {
     const char *dg = getenv("CAPF_P1_DIAG");  // diagnostics only: wrong counts
     const int diag = dg ? atoi(dg) : 0;
+    // CAPF_P1_UPFRONT=0 (tuning): one load group ahead instead of the whole tile
+    static const bool upf = !(getenv("CAPF_P1_UPFRONT") && atoi(getenv("CAPF_P1_UPFRONT")) == 0);
     auto kern = diag == 1   ? k_c5_partition<W, ALIAS, CHECK, false, SH, 1>
                 : diag == 2 ? k_c5_partition<W, ALIAS, CHECK, false, SH, 2>
+                : upf       ? k_c5_partition<W, ALIAS, CHECK, false, SH, 0, 1>
                             : k_c5_partition<W, ALIAS, CHECK, false, SH, 0>;
     hipLaunchKernelGGL(kern, dim3((unsigned)nfull), dim3(C5_BLOCK), 0, s->stream, c, part, meta,
                        d_loops, (int64_t)0);

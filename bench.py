@@ -122,6 +122,7 @@ def cpu_baseline(session, graph, scale, budget_s):
 
 # kernels of one fused 2-hop count (fused_count.hip + chain2_partitioned.hip)
 PIPELINE = ("c5_partition", "c3_transpose", "c3_units", "c5_gather", "c3_overflow", "chain2_hist", "message_pass",
+            "semi_partition", "semi_count",
             "chain2_dot", "tri_keys", "tri_sort_keys", "tri_rle", "tri_pairs", "tri_orient",
             "tri_sort_pairs", "tri_rowptr", "tri_split", "tri_loop3", "tri_count",
             "rj_partition1", "rj_partition2", "rj_join_count", "rj_join_emit", "gather")

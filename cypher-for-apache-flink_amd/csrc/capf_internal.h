@@ -429,6 +429,11 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
 // the permutation (int64 row indexes) and the row count per owner.
 BufPtr route_permutation(Session *s, const std::vector<ColView> &keys, int64_t n, int parts,
                          std::vector<int64_t> &counts);
+// Σ_rows bit[key − lo] of a membership bitmap over [lo, hi] into *d_acc,
+// radix-partitioned (chain2_partitioned.hip); `mixed_cache` holds the bitmap in
+// node_mix order (built when empty).  false: shape not handled, nothing launched.
+bool bits_count_partitioned(Session *s, const ColView &key, int64_t n, int64_t lo, int64_t hi,
+                            const uint32_t *bits, BufPtr &mixed_cache, unsigned long long *d_acc);
 // Directed triangle count (triangle.hip), part `part` of `parts`, to device int64.
 // The oriented CSR is cached on `src` (Column::index) for the pair (src, dst).
 void triangle_count_async(Session *s, const ColPtr &src, const ColPtr &dst, int64_t m,

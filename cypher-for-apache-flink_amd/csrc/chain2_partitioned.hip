@@ -1416,6 +1416,7 @@ struct C5Shard {
   int gpt;                       // 4096-row groups per tile (≤ 4): tile = 4096·gpt rows
   int nhot;                      // heavy hitters (≤ C5S_MAXHOT): keys equal to hot[j] are
   uint32_t hot[2];               // counted per wave, not partitioned (node_mix(id − lo))
+  int upf;                       // raw loads D groups ahead on tiles without the loop test
   int64_t n_diag;                // out-copy rows [0, n_diag) may be self-loops (2-D layout:
                                  // rows whose target is owned too come first); the
                                  // target column is read for those rows only
@@ -1483,6 +1484,59 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   // partitioned but counted at the end from the dummy run's stage slots — one
   // compare per key and no counter register (32 keys per thread already fill
   // the VGPR budget); no hint = 0xFFFFFFFF, never a mixed index
+  // (run, key) of node offset x (ok: inside the node range), or a dummy key:
+  // a heavy hitter goes to the dummy run as key 1 (past-the-end rows as key 0),
+  // never copied out, counted in the dummy run's stage slots
+  auto mk = [&](uint32_t x, bool okx) {
+    const uint32_t h = node_mix_t<WIDE>(x, c.mix);
+    const uint32_t b = (h >> C2_BITS) - (uint32_t)c.b0;  // wraps when below b0
+    const bool ok = okx && b < (uint32_t)c.nbl;
+    const uint32_t run = run0 + (b << lsub) + ((h & 0xFFFF) >> ssh);
+    return HOT ? (ok && h != c.hot[0] ? (run << C2_BITS) | (h & 0xFFFF) : dummy | (ok ? 1u : 0u))
+               : (ok ? (run << C2_BITS) | (h & 0xFFFF) : dummy);
+  };
+  if (W != 8 && !chk && c.upf) {
+    // tiles without the loop test (FOR24 / FOR32): raw loads run D groups
+    // ahead in a ring of registers (the single-GPU P1's upfront schedule,
+    // bounded to stay within 64 VGPRs); a partial last group loads per row
+    constexpr int D = 4;
+    using Raw = C5Raw<(W == 3 ? 3 : 4)>;
+    Raw raw[D];
+    auto issue = [&](int g) {
+      const int64_t e = e0 + 4 * ((int64_t)g * C5_BLOCK + threadIdx.x);
+      if (g < gu && e + 4 <= e1) raw[g & (D - 1)] = *(const Raw *)((const uint8_t *)kp + W * e);
+    };
+#pragma unroll
+    for (int g = 0; g < D && g < GROUPS; ++g) issue(g);
+    const int64_t dlo = kb - c.lo;
+#pragma unroll
+    for (int g = 0; g < GROUPS; ++g) {
+      if (g < gu) {
+        const int64_t e = e0 + 4 * ((int64_t)g * C5_BLOCK + threadIdx.x);
+        uint32_t x[4];
+        bool okx[4];
+        if (e + 4 <= e1) {
+          uint32_t q[4];
+          c5_decode<(W == 3 ? 3 : 4)>(raw[g & (D - 1)], 0u, q);
+          if (g + D < GROUPS) issue(g + D);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int64_t o = dlo + (int64_t)q[k];
+            x[k] = (uint32_t)o;
+            okx[k] = (uint64_t)o < c.len;
+          }
+        } else {
+          c5_load4<W, true>(kp, kb, c.lo, c.len, e, e1, true, x, okx);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          key[4 * g + k] = mk(x[k], okx[k]);
+          atomicAdd(&cur[(key[4 * g + k] >> C2_BITS) * C + my_copy], 1u);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
   // the next group's loads are issued before this group's hashing/counting
   uint32_t px[2][4], py[2][4];
   bool pox[2][4], poy[2][4];
@@ -1529,6 +1583,7 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
       }
     }
     __builtin_amdgcn_sched_barrier(0);
+  }
   }
 #pragma unroll
   for (int j = 0; j < RPT; ++j) asm volatile("" : "+v"(key[j]));
@@ -2393,6 +2448,10 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
     c.n_out = n_out;
     c.n_diag = n_diag < 0 ? n_out : std::min(n_diag, n_out);
     c.nhot = nh;
+    {
+      const char *ue = getenv("CAPF_SHARD_UPF");  // tuning: 0 = one group ahead everywhere
+      c.upf = !(ue && atoi(ue) == 0);
+    }
     c.hot[0] = hot[0];
     c.hot[1] = hot[1];
     // tile size: whole rounds of resident blocks (2 per CU), counting one
@@ -2596,6 +2655,152 @@ bool chain2_partitioned(Session *s, const ColView *cols, int64_t n, int64_t lo, 
     chain2_c5<8, C5Small>(s, c, in_range, h_in, h_out, d_loops);
   else
     chain2_c5<8, C5Big>(s, c, in_range, h_in, h_out, d_loops);
+  return true;
+}
+
+}  // namespace capf
+
+namespace capf {
+
+// ------------------------------------------ partitioned semi-join count
+// Σ_rows bit[key − lo]: the root message of the 1-hop label count
+// (MATCH (a:Person)-->(b), fused_count.hip): the Person id column's
+// membership bitmap probed with every rel's source.  Probed row by row, each
+// random 4-B lookup pulls a 128-B line from L2 into the CU — L2-bandwidth bound
+// (≈31 TB/s of lines for 67 M lookups at s22).  Radix-partitioned instead, like
+// the 2-hop P1: the keys are grouped by 64 Ki-node bucket of node_mix(key −
+// lo) (the sharded P1 kernel as one rank owning every bucket), then each
+// bucket's 8 KiB slice of the bitmap — in mixed order, built once per bitmap —
+// sits in LDS while its keys stream past: no atomics, no random HBM/L2 access.
+
+__global__ void k_mix_bits(const uint32_t *bits, uint64_t range, NodeMix mix, uint32_t *mbits) {
+  const uint64_t nw = (range + 31) / 32;
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw;
+       w += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t v = bits[w];
+    while (v) {
+      const uint32_t b = __builtin_ctz(v);
+      v &= v - 1;
+      const uint64_t o = w * 32 + b;
+      if (o >= range) break;
+      const uint32_t h = node_mix((uint32_t)o, mix);
+      atomicOr(&mbits[h >> 5], 1u << (h & 31));
+    }
+  }
+}
+
+// One block per (bucket, tile chunk): the bucket's bitmap slice in LDS, the
+// waves walk the chunk's tiles (P1's tile-major meta read in place), one
+// 16-B piece of 8 keys per lane; the segment's last piece counts only its
+// `cnt & 7` live keys (the rest are P1's pads).
+constexpr int BC_BLOCK = 1024;
+__global__ __launch_bounds__(BC_BLOCK) void k_c5_bits_count(const uint16_t *part, const uint32_t *meta,
+                                                            int64_t ntiles, int nr, int64_t rstride,
+                                                            int chunks, const uint32_t *mbits,
+                                                            unsigned long long *acc) {
+  __shared__ uint32_t slice[C2_BW / 32];
+  __shared__ unsigned long long red[BC_BLOCK / WAVE];
+  const int r = blockIdx.x / chunks, k = blockIdx.x % chunks;
+  for (int i = threadIdx.x; i < C2_BW / 32; i += BC_BLOCK) slice[i] = mbits[(int64_t)r * (C2_BW / 32) + i];
+  __syncthreads();
+  const int64_t t0 = ntiles * k / chunks, t1 = ntiles * (k + 1) / chunks;
+  const int wave = threadIdx.x / WAVE, lane = lane_id();
+  const uint4 *part4 = (const uint4 *)part;
+  unsigned long long sum = 0;
+  for (int64_t t = t0 + wave; t < t1; t += BC_BLOCK / WAVE) {
+    const uint32_t mw = meta[t * nr + r];
+    const uint32_t start = mw & 0xFFFF, cnt = mw >> 16, np = (cnt + 7) >> 3;
+    const int64_t base = t * (rstride / 8) + start;
+    for (uint32_t p = lane; p < np; p += WAVE) {
+      const uint4 v = part4[base + p];
+      const uint32_t live = min(cnt - 8 * p, 8u);
+      const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
+        sum += ((uint32_t)e < live) ? ((slice[key >> 5] >> (key & 31)) & 1u) : 0u;
+      }
+    }
+  }
+  sum = wave_reduce_sum(sum);
+  if (lane == 0) red[wave] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long tot = 0;
+    for (int w = 0; w < BC_BLOCK / WAVE; ++w) tot += red[w];
+    if (tot) atomicAdd(acc, tot);
+  }
+}
+
+bool bits_count_partitioned(Session *s, const ColView &key, int64_t n, int64_t lo, int64_t hi,
+                            const uint32_t *bits, BufPtr &mixed_cache, unsigned long long *d_acc) {
+  const char *e = getenv("CAPF_SEMI_PART");  // tuning: 0 = row-by-row bitmap probes
+  if (e && atoi(e) == 0) return false;
+  if (n < (int64_t(1) << 20) || n >= (int64_t(1) << 31) || key.valid || !key.data) return false;
+  if (key.enc != ENC_FOR24 && key.enc != ENC_FOR32) return false;
+  if ((uintptr_t)key.data & 15) return false;
+  const int64_t range = hi - lo + 1;
+  if (range <= 0 || range > (int64_t(1) << 31)) return false;
+  const int kbits = chain2_hist_bits(range);
+  const int nbl = (int)((int64_t(1) << kbits) / C2_BW);
+  if (2 * nbl + 1 > C5S_MAXR) return false;
+  const NodeMix mix = node_mix_for(kbits);
+  // the bitmap in mixed order (cached by the caller with the bitmap)
+  if (!mixed_cache) {
+    const int64_t mw = (int64_t(1) << kbits) / 32;
+    mixed_cache = s->alloc(4 * mw);
+    HIP_CHECK(hipMemsetAsync(mixed_cache->p, 0, 4 * mw, s->stream));
+    hipLaunchKernelGGL(k_mix_bits, dim3(grid_for((range + 31) / 32, 256)), dim3(256), 0, s->stream, bits,
+                       (uint64_t)range, mix, (uint32_t *)mixed_cache->p);
+    KERNEL_CHECK();
+  }
+  // P1: the sharded partition kernel, one "rank" owning every bucket, keys = the column
+  const int W = key.enc == ENC_FOR24 ? 3 : 4;
+  C5Shard c;
+  memset(&c, 0, sizeof(c));
+  c.kin = c.kout = c.oth = key.data;
+  c.bin = c.bout = c.both = key.base;
+  c.n_in = n;
+  c.n_out = 0;
+  c.n_diag = 0;
+  c.nhot = 0;
+  c.hot[0] = c.hot[1] = 0xFFFFFFFFu;
+  c.lo = lo;
+  c.len = (uint64_t)range;
+  c.b0 = 0;
+  c.nbl = nbl;
+  c.lsub = 0;
+  c.nsb = nbl;
+  c.mix = mix;
+  const int nr = 2 * nbl;
+  c.copies = c5s_copies(nr);
+  c.upf = 1;
+  const int tile = W == 3 ? C5S_TILE : 16384;
+  c.gpt = tile / (4 * C5_BLOCK);
+  c.t_in = (n + tile - 1) / tile;
+  const int64_t ntiles = c.t_in;
+  const int64_t rstride = ((int64_t)tile + 8 * (nr + 1) + 7) & ~int64_t(7);
+  BufPtr partb = s->alloc(2 * rstride * ntiles), meta = s->alloc(4 * (int64_t)nr * ntiles),
+         tacc = s->alloc(8 * ntiles);
+  {
+    KernelTimer kt(s, "semi_partition", (double)W * n + 2.0 * n);
+    auto kern = W == 3 ? (kbits > 24 ? k_c5_shard_partition<3, true, C5S_TILE, false>
+                                     : k_c5_shard_partition<3, false, C5S_TILE, false>)
+                       : (kbits > 24 ? k_c5_shard_partition<4, true, 16384, false>
+                                     : k_c5_shard_partition<4, false, 16384, false>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(C5_BLOCK), 0, s->stream, c, (uint16_t *)partb->p,
+                       (uint32_t *)meta->p, (uint32_t *)tacc->p, rstride);
+    KERNEL_CHECK();
+  }
+  {
+    KernelTimer kt(s, "semi_count", 2.0 * n);
+    // ≥ 2 blocks per CU over the buckets
+    const int chunks = (int)std::max<int64_t>(1, std::min<int64_t>(ntiles, (4 * s->num_cus + nbl - 1) / nbl));
+    hipLaunchKernelGGL(k_c5_bits_count, dim3((unsigned)(nbl * chunks)), dim3(BC_BLOCK), 0, s->stream,
+                       (const uint16_t *)partb->p, (const uint32_t *)meta->p, ntiles, nr, rstride, chunks,
+                       (const uint32_t *)mixed_cache->p, d_acc);
+    KERNEL_CHECK();
+  }
   return true;
 }
 

@@ -539,9 +539,16 @@ static LeafData leaf_data(const Leaf &lf) {
 }
 
 // ============================================================ message passing
+// A membership bitmap cached on its key column, with its node_mix-ordered copy
+// (built by the first partitioned probe, bits_count_partitioned).
+struct BitsCache {
+  BufPtr bits, mixed;
+};
+
 struct HostMap {
   DMap m;
   BufPtr vals, keys;
+  std::shared_ptr<BitsCache> bc;  // MAP_BITS from a column's cache
 };
 
 __global__ void k_fill_hash_empty(int64_t *k, uint64_t n) {
@@ -609,7 +616,8 @@ static bool bits_map_for(Session *s, const ColPtr &parent_key, const ColPtr &myk
   {
     std::lock_guard<std::mutex> lk(mykey->mu);
     if (mykey->bits && mykey->bits_key[0] == st.min && mykey->bits_key[1] == st.max) {
-      h.vals = *std::static_pointer_cast<BufPtr>(mykey->bits);
+      h.bc = std::static_pointer_cast<BitsCache>(mykey->bits);
+      h.vals = h.bc->bits;
       cached = true;
     }
   }
@@ -633,7 +641,9 @@ static bool bits_map_for(Session *s, const ColPtr &parent_key, const ColPtr &myk
     }
     if (!mykey->unique_flag) return false;
     std::lock_guard<std::mutex> lk(mykey->mu);
-    mykey->bits = std::make_shared<BufPtr>(h.vals);
+    h.bc = std::make_shared<BitsCache>();
+    h.bc->bits = h.vals;
+    mykey->bits = h.bc;
     mykey->bits_key[0] = st.min;
     mykey->bits_key[1] = st.max;
   }
@@ -731,6 +741,7 @@ static bool tree_count(Session *s, JoinGraph &g, unsigned long long *d_acc) {
     MsgJob j;
     memset(&j, 0, sizeof(j));
     int root_cols[MAX_CHILD + 1] = {0};
+    int child_leaf[MAX_CHILD + 1] = {0};
     for (auto &nb : adj[v]) {
       if (nb.first == parent) continue;
       visit(nb.first, v, nb.second);
@@ -740,6 +751,7 @@ static bool tree_count(Session *s, JoinGraph &g, unsigned long long *d_acc) {
       j.cols[j.nchild] = view_of(data[v].data->cols[mycol]);
       j.child[j.nchild] = msg[nb.first].m;
       root_cols[j.nchild] = mycol;
+      child_leaf[j.nchild] = nb.first;
       j.nchild++;
     }
     const int64_t n = data[v].data->nrows;
@@ -758,6 +770,7 @@ static bool tree_count(Session *s, JoinGraph &g, unsigned long long *d_acc) {
           j.cols[keep] = j.cols[c];
           j.child[keep] = j.child[c];
           root_cols[keep] = root_cols[c];
+          child_leaf[keep] = child_leaf[c];
           ++keep;
         }
       }
@@ -769,6 +782,12 @@ static bool tree_count(Session *s, JoinGraph &g, unsigned long long *d_acc) {
       const ColView &c0 = j.cols[0];
       const int cw = c0.enc == ENC_FOR32 ? 4 : c0.enc == ENC_FOR24 ? 3 : 8;
       const bool aligned = ((uintptr_t)c0.data & 15) == 0;
+      // a membership bitmap probed by a large FOR key column: radix-partitioned
+      // probes against LDS slices (chain2_partitioned.hip)
+      if (keep == 1 && j.child[0].kind == MAP_BITS && msg[child_leaf[0]].bc &&
+          bits_count_partitioned(s, c0, n, j.child[0].lo, j.child[0].hi, (const uint32_t *)j.child[0].vals,
+                                 msg[child_leaf[0]].bc->mixed, d_acc))
+        return;
       if (keep == 1 && n > 0 && c0.data && !c0.valid && aligned &&
           (j.child[0].kind == MAP_BITS || j.child[0].kind == MAP_ONES)) {
         KernelTimer kt(s, "message_pass", (double)cw * n);

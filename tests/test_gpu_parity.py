@@ -130,6 +130,28 @@ def test_one_hop_person_count_rmat(gpu_session, scale, count, compact):
     assert got == cmodel.count_1hop(src, dst, 1 << scale, in_a=person)
 
 
+@pytest.mark.parametrize("semi", ["0", "1"], ids=["probe_rows", "partitioned"])
+@pytest.mark.parametrize("compact", [True, 3], ids=["for32", "for24"])
+@pytest.mark.parametrize("scale,count", [(16, None), (18, None), (18, 3000001), (20, None)])
+def test_one_hop_person_partitioned_semijoin(gpu_session, scale, count, compact, semi, monkeypatch):
+    """Config 2 at sizes where the Person bitmap is probed radix-partitioned
+    (chain2_partitioned.hip::bits_count_partitioned: keys grouped by bucket,
+    the bucket's bitmap slice in LDS) against the row-by-row probes; ragged
+    tile counts included.  Both equal the oracle."""
+    monkeypatch.setenv("CAPF_SEMI_PART", semi)
+    g = rmat_graph(gpu_session, scale, person_split=True, count=count, compact=compact)
+    gpu_session.reset_profile()
+    gpu_session.set_profiling(True)
+    got = run(g, ONE_HOP_PERSON)[0]["count"]
+    got2 = run(g, ONE_HOP_PERSON)[0]["count"]  # the second query reuses the cached bitmaps
+    gpu_session.set_profiling(False)
+    src, dst = cmodel.rmat(scale, count=count)
+    person = cmodel.labels(1 << scale, cmodel.rmat_seed(scale))
+    want = cmodel.count_1hop(src, dst, 1 << scale, in_a=person)
+    assert got == got2 == want
+    assert ("semi_count" in gpu_session.profile()) == (semi == "1")
+
+
 @pytest.mark.parametrize("compact", [False, True, 3], ids=["int64", "for32", "for24"])
 @pytest.mark.parametrize("scale,nodes", [(12, 3000), (14, 9999), (16, None)])
 def test_one_hop_person_partial_node_range(gpu_session, scale, nodes, compact):

@@ -130,6 +130,8 @@ struct Column {
   mutable std::shared_ptr<void> index;
   // the direct-address index of a dense unique id column (dense_join.hip)
   mutable std::shared_ptr<void> dense;
+  // the var-length reach index of this rel source column (var_length_reach.hip)
+  mutable std::shared_ptr<void> vr_index;
   // the membership bitmap of this (unique) key column over [bits_key[0],
   // bits_key[1]] (fused_count.hip message passing)
   mutable std::shared_ptr<void> bits;

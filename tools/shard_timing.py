@@ -38,9 +38,17 @@ for p in parts:
     torch.cuda.synchronize()
     s.set_profiling(False)
     prof = {k: round(x["total_ms"] / 5, 4) for k, x in s.profile().items()}
+    # host cost of enqueueing one step (what bounds a pipelined N-GPU bench when
+    # it exceeds the device time): 20 async steps without a sync in between
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(20):
+        run()
+    enq = (time.perf_counter() - t1) / 20
+    torch.cuda.synchronize()
     dev = sum(prof.values())
     tot += v
     print(f"s{scale} G={G} part {p}: in {ic.size} out {oc.size} rows (hot {getattr(oc, 'hot_ids', [])}); "
-          f"step {el*1e3:.3f} ms "
+          f"step {el*1e3:.3f} ms enqueue {enq*1e3:.3f} ms "
           f"dev {dev:.3f} ms {prof} partial {v}", flush=True)
 print("sum of partials", tot)

@@ -156,10 +156,18 @@ bool dense_join(Session *s, const Data &l, const Data &r, const std::vector<std:
                          (unsigned long long *)acc->p);
     KERNEL_CHECK();
   }
+  // every probe key provably matches (no NULL, the key's range inside the dense
+  // build range — cached column statistics): no match count to read back, so
+  // the join stays asynchronous; otherwise one host read of the count
   int64_t matched = 0;
-  HIP_CHECK(hipMemcpyAsync(s->h_scalars, acc->p, 8, hipMemcpyDeviceToHost, s->stream));
-  s->sync();
-  matched = s->h_scalars[0];
+  const ColStats &pst = column_stats(s, pk);
+  if (n > 0 && pst.non_null == n && pst.min >= di->min && pst.max < di->min + di->n) {
+    matched = n;
+  } else {
+    HIP_CHECK(hipMemcpyAsync(s->h_scalars, acc->p, 8, hipMemcpyDeviceToHost, s->stream));
+    s->sync();
+    matched = s->h_scalars[0];
+  }
   BufPtr pidx, bidx = brow;  // pidx null = identity over the probe rows
   int64_t m = n;
   if (!probe_outer && matched < n) {

@@ -288,6 +288,14 @@ def run_single(args):
         step()
     # query-at-a-time: plan + fused count + scalar to host, no profiling events
     count, elapsed_sync = timed_steps(step, args.steps, s.sync)
+    # plan call → scalar result, median of ≥ 5 single queries
+    singles = []
+    for _ in range(max(5, min(args.steps, 15))):
+        s.sync()
+        t1 = time.perf_counter()
+        step()  # returns the scalar on the host
+        singles.append(time.perf_counter() - t1)
+    median_single_ms = sorted(singles)[len(singles) // 2] * 1e3
     elapsed = elapsed_sync
     pipelined = False
     if not args.sync_steps:
@@ -367,6 +375,8 @@ def run_single(args):
                                       "(capf_table_count_async), K counts checked after the final sync"
                                       if pipelined else "query-at-a-time (result downloaded every step)")
     result["config"]["ms_per_step_query_at_a_time"] = elapsed_sync * 1e3 / args.steps
+    result["config"]["ms_per_query_median_plan_to_scalar"] = median_single_ms
+    result["config"]["joined_rows_per_s_median_plan_to_scalar"] = count / (median_single_ms * 1e-3)
     result["config"]["first_query_ms"] = first_query_ms
     result["config"]["parity"] = check_fixture(args, count)
     if not args.no_cpu and args.query == "two_hop":

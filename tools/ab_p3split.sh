@@ -1,0 +1,14 @@
+# P3 unit-split threshold / slices A/B at s24 (not a test)
+set -e
+run() {
+  env "$@" timeout -k 10 200 python bench.py --steps 10 --warmup 3 --no-cpu > gpurun_out/x.json 2>/dev/null
+  python3 -c "
+import json,sys;d=json.load(open('gpurun_out/x.json'));r=d['roofline'];k=r['kernel_ms_per_query']
+print(sys.argv[1:], round(d['ms_per_step'],4), round(r['pipeline_ms_per_query'],4), round(k['c5_gather'],4), round(k.get('c3_overflow',0),4), round(k['chain2_dot'],4), d['config']['parity']['match'])" "$@"
+}
+run CAPF_NONE=1
+run CAPF_P3_SPLIT=1.05
+run CAPF_P3_SPLIT=1.1
+run CAPF_P3_SPLIT=1.25
+run CAPF_SLICES=2
+run CAPF_NONE=1

@@ -198,7 +198,10 @@ __global__ void k_tri_loop3(const uint32_t *loops, uint64_t len, unsigned long l
 }
 
 constexpr int TRI_BLOCK = 256;
-constexpr int TRI_CAP = 1024;  // N+(p) staged in LDS up to this many entries
+#ifndef CAPF_TRI_CAP
+#define CAPF_TRI_CAP 1024
+#endif
+constexpr int TRI_CAP = CAPF_TRI_CAP;  // N+(p) staged in LDS up to this many entries
 constexpr int TRI_CHUNK = 16;  // rows per cursor grab
 constexpr int TRI_ILP = 4;     // N+(q) entries per lane in flight
 

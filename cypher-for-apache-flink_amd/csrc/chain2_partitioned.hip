@@ -173,6 +173,21 @@ __device__ inline void c5_decode(const C5Raw<W> &t, uint32_t d, uint32_t o[4]) {
   }
 }
 
+// Raw row data at byte address p; NT = non-temporal loads (the stream is read once)
+template <int W, bool NT>
+__device__ inline C5Raw<W> c5_ld_raw(const uint8_t *p) {
+  if constexpr (!NT) {
+    return *(const C5Raw<W> *)p;
+  } else if constexpr (W == 3) {
+    const uint32_t *q = (const uint32_t *)p;
+    return U3{__builtin_nontemporal_load(q), __builtin_nontemporal_load(q + 1), __builtin_nontemporal_load(q + 2)};
+  } else {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u v = __builtin_nontemporal_load((const v4u *)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+}
+
 // UPF (ALIAS, in-range, full tiles, FOR24 / FOR32): every load of the tile is
 // issued before the first key is counted — 2 × GROUPS raw loads in flight per
 // thread (96 B at FOR24) instead of one group ahead; the raw registers of a
@@ -211,8 +226,8 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
 #pragma unroll
     for (int g = 0; g < GROUPS; ++g) {
       const int64_t e = e0 + 4 * ((int64_t)g * C5_BLOCK + threadIdx.x);
-      ru[g] = *(const C5Raw<W> *)((const uint8_t *)c.u1 + W * e);
-      rv[g] = *(const C5Raw<W> *)((const uint8_t *)c.v1 + W * e);
+      ru[g] = c5_ld_raw<W, UPF == 2>((const uint8_t *)c.u1 + W * e);
+      rv[g] = c5_ld_raw<W, UPF == 2>((const uint8_t *)c.v1 + W * e);
     }
     const uint32_t du = (uint32_t)(c.bu1 - c.lo), dv = (uint32_t)(c.bv1 - c.lo);
 #pragma unroll
@@ -1069,10 +1084,12 @@ static void launch_c5(Session *s, const C5Cols<W> &c, uint16_t *part, uint32_t *
   if (nfull > 0) {
     const char *dg = getenv("CAPF_P1_DIAG");  // diagnostics only: wrong counts
     const int diag = dg ? atoi(dg) : 0;
-    // CAPF_P1_UPFRONT=0 (tuning): one load group ahead instead of the whole tile
-    static const bool upf = !(getenv("CAPF_P1_UPFRONT") && atoi(getenv("CAPF_P1_UPFRONT")) == 0);
+    // upfront loads, non-temporal (the default, 2; s24 P1 0.516 vs 0.521 ms with
+    // default-policy loads, 1); CAPF_P1_UPFRONT=0 (tuning): one group ahead
+    static const int upf = getenv("CAPF_P1_UPFRONT") ? atoi(getenv("CAPF_P1_UPFRONT")) : 2;
     auto kern = diag == 1   ? k_c5_partition<W, ALIAS, CHECK, false, SH, 1>
                 : diag == 2 ? k_c5_partition<W, ALIAS, CHECK, false, SH, 2>
+                : upf == 2  ? k_c5_partition<W, ALIAS, CHECK, false, SH, 0, 2>
                 : upf       ? k_c5_partition<W, ALIAS, CHECK, false, SH, 0, 1>
                             : k_c5_partition<W, ALIAS, CHECK, false, SH, 0>;
     hipLaunchKernelGGL(kern, dim3((unsigned)nfull), dim3(C5_BLOCK), 0, s->stream, c, part, meta,
@@ -1504,7 +1521,9 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
     Raw raw[D];
     auto issue = [&](int g) {
       const int64_t e = e0 + 4 * ((int64_t)g * C5_BLOCK + threadIdx.x);
-      if (g < gu && e + 4 <= e1) raw[g & (D - 1)] = *(const Raw *)((const uint8_t *)kp + W * e);
+      if (g < gu && e + 4 <= e1)
+        raw[g & (D - 1)] = c.upf == 2 ? c5_ld_raw<(W == 3 ? 3 : 4), true>((const uint8_t *)kp + W * e)
+                                      : c5_ld_raw<(W == 3 ? 3 : 4), false>((const uint8_t *)kp + W * e);
     };
 #pragma unroll
     for (int g = 0; g < D && g < GROUPS; ++g) issue(g);
@@ -2450,7 +2469,7 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
     c.nhot = nh;
     {
       const char *ue = getenv("CAPF_SHARD_UPF");  // tuning: 0 = one group ahead everywhere
-      c.upf = !(ue && atoi(ue) == 0);
+      c.upf = ue ? atoi(ue) : 1;  // 2 = the ring with non-temporal loads
     }
     c.hot[0] = hot[0];
     c.hot[1] = hot[1];

@@ -226,21 +226,39 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
 #pragma unroll
     for (int g = 0; g < GROUPS; ++g) {
       const int64_t e = e0 + 4 * ((int64_t)g * C5_BLOCK + threadIdx.x);
-      ru[g] = c5_ld_raw<W, UPF == 2>((const uint8_t *)c.u1 + W * e);
-      rv[g] = c5_ld_raw<W, UPF == 2>((const uint8_t *)c.v1 + W * e);
+      ru[g] = c5_ld_raw<W, UPF >= 2>((const uint8_t *)c.u1 + W * e);
+      rv[g] = c5_ld_raw<W, UPF >= 2>((const uint8_t *)c.v1 + W * e);
     }
     const uint32_t du = (uint32_t)(c.bu1 - c.lo), dv = (uint32_t)(c.bv1 - c.lo);
+    // D0 (UPF 3: FOR bases = lo, 24-bit multiply): offsets are the raw fields —
+    // __umul24 reads only the low 24 bits, so no mask and no add; the self-loop
+    // test compares the mixed keys (node_mix is a bijection on [0, 2^k))
+    constexpr bool D0 = UPF == 3 && W == 3 && !SH::WIDE;
 #pragma unroll
     for (int g = 0; g < GROUPS; ++g) {
       uint32_t x1[4], y1[4];
-      c5_decode<W>(ru[g], du, x1);
-      c5_decode<W>(rv[g], dv, y1);
+      if constexpr (D0) {
+        x1[0] = ru[g].x;
+        x1[1] = __builtin_amdgcn_alignbit(ru[g].y, ru[g].x, 24);
+        x1[2] = __builtin_amdgcn_alignbit(ru[g].z, ru[g].y, 16);
+        x1[3] = ru[g].z >> 8;
+        y1[0] = rv[g].x;
+        y1[1] = __builtin_amdgcn_alignbit(rv[g].y, rv[g].x, 24);
+        y1[2] = __builtin_amdgcn_alignbit(rv[g].z, rv[g].y, 16);
+        y1[3] = rv[g].z >> 8;
+      } else {
+        c5_decode<W>(ru[g], du, x1);
+        c5_decode<W>(rv[g], dv, y1);
+      }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int j = 4 * g + k;
         kin[j] = node_mix_t<SH::WIDE>(y1[k], c.mix);
         kout[j] = node_mix_t<SH::WIDE>(x1[k], c.mix) + out_run0;
-        lp += y1[k] == x1[k] ? 1u : 0u;
+        if constexpr (D0)
+          lp += kout[j] - kin[j] == out_run0 ? 1u : 0u;
+        else
+          lp += y1[k] == x1[k] ? 1u : 0u;
         atomicAdd(&cur[kin[j] >> C2_BITS], 1u);
         atomicAdd(&cur[kout[j] >> C2_BITS], 1u);
       }
@@ -1085,10 +1103,13 @@ static void launch_c5(Session *s, const C5Cols<W> &c, uint16_t *part, uint32_t *
     const char *dg = getenv("CAPF_P1_DIAG");  // diagnostics only: wrong counts
     const int diag = dg ? atoi(dg) : 0;
     // upfront loads, non-temporal (the default, 2; s24 P1 0.516 vs 0.521 ms with
-    // default-policy loads, 1); CAPF_P1_UPFRONT=0 (tuning): one group ahead
+    // default-policy loads, 1), FOR24 fields used raw when the bases are lo (D0:
+    // 0.512 vs 0.517 ms); CAPF_P1_UPFRONT=0 (tuning): one group ahead
     static const int upf = getenv("CAPF_P1_UPFRONT") ? atoi(getenv("CAPF_P1_UPFRONT")) : 2;
     auto kern = diag == 1   ? k_c5_partition<W, ALIAS, CHECK, false, SH, 1>
                 : diag == 2 ? k_c5_partition<W, ALIAS, CHECK, false, SH, 2>
+                : upf >= 2 && c.bu1 == c.lo && c.bv1 == c.lo && W == 3 && !SH::WIDE
+                            ? k_c5_partition<W, ALIAS, CHECK, false, SH, 0, 3>
                 : upf == 2  ? k_c5_partition<W, ALIAS, CHECK, false, SH, 0, 2>
                 : upf       ? k_c5_partition<W, ALIAS, CHECK, false, SH, 0, 1>
                             : k_c5_partition<W, ALIAS, CHECK, false, SH, 0>;

@@ -185,6 +185,61 @@ __global__ __launch_bounds__(256) void k_vr_count(const unsigned long long *visi
   }
 }
 
+// The same counts from coalesced loads (CAPF_VR_COUNT=0 keeps k_vr_count):
+// block (kc, cg) = source words [64·kc, 64·kc + 64) × row chunks cg·16 + w
+// of VR_CR rows, one per wave; lane = source word, reading visited[y][k] as
+// 512-B rows.  Each lane adds its words into a bit-sliced counter (level i
+// holds bit i of the 64 per-source counts), the wave then hands out the
+// counts (lane j: bit j of every level of lane l's counter) into an LDS
+// table, and the block adds that table to reach[] with one coalesced atomic
+// pass.  Zero reach[s0, s0 + ns) first.
+constexpr int VR_CR = 256;   // rows per wave (< 2^VR_CL)
+constexpr int VR_CL = 9;
+
+__global__ __launch_bounds__(1024) void k_vr_count_bs(const unsigned long long *visited,
+                                                      const uint8_t *target, int64_t D, int64_t K,
+                                                      int64_t s0, int64_t ns, unsigned long long *reach) {
+  __shared__ uint32_t tab[WAVE * WAVE];
+  for (int i = threadIdx.x; i < WAVE * WAVE; i += 1024) tab[i] = 0;
+  __syncthreads();
+  const int lane = lane_id(), w = threadIdx.x / WAVE;
+  const int64_t kc = blockIdx.x, k = kc * WAVE + lane;
+  const int64_t y0 = ((int64_t)blockIdx.y * (1024 / WAVE) + w) * VR_CR, y1 = min(y0 + (int64_t)VR_CR, D);
+  unsigned long long c[VR_CL];
+#pragma unroll
+  for (int i = 0; i < VR_CL; ++i) c[i] = 0ull;
+  if (y0 < D) {
+    const bool kin = k < K;
+#pragma unroll 4
+    for (int64_t y = y0; y < y1; ++y) {
+      const unsigned long long v = (kin && target[y]) ? visited[y * K + k] : 0ull;
+      unsigned long long carry = v;
+#pragma unroll
+      for (int i = 0; i < VR_CL; ++i) {
+        const unsigned long long t = c[i] & carry;
+        c[i] ^= carry;
+        carry = t;
+      }
+    }
+    for (int l = 0; l < WAVE; ++l) {
+      uint32_t cnt = 0;
+#pragma unroll
+      for (int i = 0; i < VR_CL; ++i) {
+        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)c[i], l);
+        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(c[i] >> 32), l);
+        const uint32_t word = lane < 32 ? lo : hi;
+        cnt += ((word >> (lane & 31)) & 1u) << i;
+      }
+      if (cnt) atomicAdd(&tab[l * WAVE + lane], cnt);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < WAVE * WAVE; i += 1024) {
+    const int64_t src = kc * WAVE * WAVE + i;  // word kc·64 + i/64, bit i%64
+    if (tab[i] && src < ns) atomicAdd(&reach[s0 + src], (unsigned long long)tab[i]);
+  }
+}
+
 __global__ void k_vr_out(const int64_t *rows, int64_t n, const int64_t *src_nodes,
                          const uint64_t *dict, const int64_t *reach, int64_t *a, int64_t *r) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -371,6 +426,8 @@ static DataPtr var_length_reach(Session *s, const ColPtr &rsrc, const ColPtr &rd
   BufPtr fa = s->alloc(8 * (int64_t)D * K), fb = s->alloc(8 * (int64_t)D * K);
   BufPtr vis = s->alloc(8 * (int64_t)D * K);
   const unsigned glev = grid_for((int64_t)D * K, 256, (int64_t)s->num_cus * 32);
+  const char *vce = getenv("CAPF_VR_COUNT");  // 0 (tuning): the ballot-transpose count
+  const bool bs_count = !(vce && atoi(vce) == 0);
   for (int64_t s0 = 0; s0 < ns; s0 += 64 * K) {
     const int64_t nb = std::min<int64_t>(64 * K, ns - s0);
     HIP_CHECK(hipMemsetAsync(fb->p, 0, 8 * (size_t)D * K, s->stream));
@@ -394,9 +451,18 @@ static DataPtr var_length_reach(Session *s, const ColPtr &rsrc, const ColPtr &rd
     }
     {
       KernelTimer kt(s, "vr_count", 8.0 * K * D);
-      hipLaunchKernelGGL(k_vr_count, dim3((unsigned)((nb + 63) / 64)), dim3(256), 0, s->stream,
-                         (const unsigned long long *)vis->p, (const uint8_t *)tflag->p, (int64_t)D,
-                         K, s0, nb, (int64_t *)reach->p);
+      if (bs_count) {
+        HIP_CHECK(hipMemsetAsync((int64_t *)reach->p + s0, 0, 8 * (size_t)nb, s->stream));
+        const int64_t kw = (nb + 63) / 64;  // source words of this batch
+        const int64_t cg = (D + (int64_t)(1024 / WAVE) * VR_CR - 1) / ((int64_t)(1024 / WAVE) * VR_CR);
+        hipLaunchKernelGGL(k_vr_count_bs, dim3((unsigned)((kw + 63) / 64), (unsigned)cg), dim3(1024), 0,
+                           s->stream, (const unsigned long long *)vis->p, (const uint8_t *)tflag->p,
+                           (int64_t)D, K, s0, nb, (unsigned long long *)reach->p);
+      } else {
+        hipLaunchKernelGGL(k_vr_count, dim3((unsigned)((nb + 63) / 64)), dim3(256), 0, s->stream,
+                           (const unsigned long long *)vis->p, (const uint8_t *)tflag->p, (int64_t)D,
+                           K, s0, nb, (int64_t *)reach->p);
+      }
       KERNEL_CHECK();
     }
   }

@@ -303,6 +303,8 @@ class GpuTable:
         if t == T_LIST:
             return self.list_values(col)
         vals, valid = self.column_arrays(col)
+        if t not in (T_STRING, T_BOOL) and valid.all():
+            return vals.tolist()  # no NULLs: the values as they are
         out = []
         for v, ok in zip(vals.tolist(), valid.tolist()):
             if not ok:
@@ -319,8 +321,9 @@ class GpuTable:
     def rows(self):
         cols = self.physicalColumns
         data = [self.column_values(c) for c in cols]
-        n = len(data[0]) if data else self.size
-        return [{c: data[i][r] for i, c in enumerate(cols)} for r in range(n)]
+        if not data:
+            return [{} for _ in range(self.size)]
+        return [dict(zip(cols, row)) for row in zip(*data)]
 
     # ---------------------------------------------------------- Table[T]
     def cache(self):

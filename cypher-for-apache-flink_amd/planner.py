@@ -730,8 +730,9 @@ def records(op: Planned, aliases: Sequence[str]):
             out_cols[a] = _element_values(op, v, data)
         else:
             out_cols[a] = data(op.header.column(v))
-    n = len(next(iter(out_cols.values()))) if out_cols else op.table.size
-    return [{a: out_cols[a][i] for a in aliases} for i in range(n)]
+    if not out_cols:
+        return [{} for _ in range(op.table.size)]
+    return [dict(zip(aliases, row)) for row in zip(*(out_cols[a] for a in aliases))]
 
 
 def run(graph, q: Query, params=None):

@@ -470,3 +470,36 @@ class PercentileDisc(Aggregator):
 
     def __str__(self):
         return f"percentileDisc({self.expr}, {self.percentile})"
+
+
+# ----------------------------------------------------------- hash caching
+# Expressions are immutable and are looked up in RecordHeader dicts many times
+# per plan: each one's hash is computed once and kept on the instance (never
+# pickled — str hashes differ between processes).
+def _cached_hash(gen):
+    def __hash__(self):
+        try:
+            return self.__dict__["_hc"]
+        except KeyError:
+            h = gen(self)
+            self.__dict__["_hc"] = h
+            return h
+    return __hash__
+
+
+def _expr_getstate(self):
+    d = dict(self.__dict__)
+    d.pop("_hc", None)
+    return d
+
+
+def _all_subclasses(cls):
+    for c in cls.__subclasses__():
+        yield c
+        yield from _all_subclasses(c)
+
+
+Expr.__getstate__ = _expr_getstate
+for _cls in list(_all_subclasses(Expr)):
+    if "__dataclass_fields__" in _cls.__dict__ and _cls.__dict__.get("__hash__") is not None:
+        _cls.__hash__ = _cached_hash(_cls.__dict__["__hash__"])

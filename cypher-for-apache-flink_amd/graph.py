@@ -90,6 +90,9 @@ class ScanGraph:
         # a multi-table UNION ALL behind it) is computed once per graph — the
         # role of okapi's Cache operator (RelationalOptimizer.scala:37-92)
         self._scan_cache = {}
+        # planning metadata of a scan per (kind, variable, labels): the header
+        # and the column renaming (each call still returns a fresh select)
+        self._scan_meta = {}
 
     @property
     def rel_types(self):
@@ -135,6 +138,10 @@ class ScanGraph:
     # ------------------------------------------------------------ scans
     def node_scan(self, var_name, labels=()):
         """ScanGraph.scanOperator for NodePattern(CTNode(labels))."""
+        key = ("node", var_name, tuple(labels))
+        meta = self._scan_meta.get(key)
+        if meta is not None:
+            return self._scan_from_meta(meta)
         want = frozenset(labels)
         sel = [t for t in self.node_tables if want <= t.labels]
         v = Var(var_name, "NODE")
@@ -151,10 +158,14 @@ class ScanGraph:
         h = RecordHeader(header)
         order = [header[e] for e in header]
         types = [T_INT] + [T_BOOL] * len(all_labels) + [CT_TO_CAPF[props[k]] for k in sorted(props)]
-        return self._align_union(sel, h, order, types, v, all_labels, props, rel=False)
+        return self._align_union(sel, h, order, types, v, all_labels, props, rel=False, meta_key=key)
 
     def rel_scan(self, var_name, types=()):
         """ScanGraph.scanOperator for RelationshipPattern(CTRelationship(types))."""
+        key = ("rel", var_name, tuple(types))
+        meta = self._scan_meta.get(key)
+        if meta is not None:
+            return self._scan_from_meta(meta)
         want = set(types)
         sel = [t for t in self.rel_tables if not want or (t.labels & want)]
         r = Var(var_name, "RELATIONSHIP")
@@ -171,9 +182,14 @@ class ScanGraph:
         h = RecordHeader(header)
         order = [header[e] for e in header]
         tys = [T_INT, T_INT, T_INT] + [T_BOOL] * len(all_types) + [CT_TO_CAPF[props[k]] for k in sorted(props)]
-        return self._align_union(sel, h, order, tys, r, all_types, props, rel=True)
+        return self._align_union(sel, h, order, tys, r, all_types, props, rel=True, meta_key=key)
 
-    def _align_union(self, sel, h, order, types, v, flags, props, rel):
+    @staticmethod
+    def _scan_from_meta(meta):
+        base, pairs, h = meta
+        return _planned(base.select(*pairs), h)
+
+    def _align_union(self, sel, h, order, types, v, flags, props, rel, meta_key=None):
         from .planner import Planned
         if not sel:
             return Planned(self.session.empty(order, types), h)
@@ -185,7 +201,10 @@ class ScanGraph:
         if base is None:
             base = self._build_union(sel, h, canon_order, Var(canon, v.ctype), flags, props, rel)
             self._scan_cache[key] = base
-        return Planned(base.select(*zip(canon_order, order)), h)
+        pairs = tuple(zip(canon_order, order))
+        if meta_key is not None:
+            self._scan_meta[meta_key] = (base, pairs, h)
+        return Planned(base.select(*pairs), h)
 
     def _build_union(self, sel, h, order, v, flags, props, rel):
         name = v.vname
@@ -214,6 +233,13 @@ class ScanGraph:
         for p in parts[1:]:
             out = out.unionAll(p)
         return out
+
+
+def _planned(table, header):
+    from .planner import Planned
+    global _planned
+    _planned = Planned  # bound once: no import statement per scan
+    return Planned(table, header)
 
 
 def _scan_columns(name, flags, props, rel):

@@ -18,8 +18,11 @@ def owner_of(e):
 
 
 class RecordHeader:
+    __slots__ = ("_m", "_cols")
+
     def __init__(self, mapping=None):
-        self._m = dict(mapping or {})
+        self._m = dict(mapping) if mapping else {}
+        self._cols = None
 
     # dict-like access used by expression lowering
     def get(self, expr, default=None):
@@ -46,12 +49,15 @@ class RecordHeader:
 
     @property
     def columns(self):
-        seen, out = set(), []
-        for c in self._m.values():
-            if c not in seen:
-                seen.add(c)
-                out.append(c)
-        return out
+        if self._cols is None:  # immutable: computed once
+            self._cols = list(dict.fromkeys(self._m.values()))
+        return list(self._cols)
+
+    def column_set(self):
+        """The distinct physical columns as a set (planner renaming checks)."""
+        if self._cols is None:
+            self._cols = list(dict.fromkeys(self._m.values()))
+        return set(self._cols)
 
     def owned_by(self, var):
         return [e for e in self._m if e == var or owner_of(e) == var]
@@ -73,7 +79,10 @@ class RecordHeader:
     def union(self, other):
         m = dict(self._m)
         m.update(other._m)
-        return RecordHeader(m)
+        h = RecordHeader.__new__(RecordHeader)
+        h._m = m
+        h._cols = None
+        return h
 
     def without(self, exprs):
         drop = set(exprs)

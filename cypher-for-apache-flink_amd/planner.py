@@ -79,8 +79,10 @@ class Query:
 # ------------------------------------------------------------- relational ops
 def _rename_disjoint(left: Planned, right: Planned) -> Planned:
     """withDisjointColumnNames (RelationalPlanner.scala:366-368, 524-538)."""
-    lcols = set(left.header.columns) | set(left.table.physicalColumns)
-    clash = [c for c in right.table.physicalColumns if c in lcols]
+    lcols = left.header.column_set()
+    lcols.update(left.table.physicalColumns)
+    rcols = right.table.physicalColumns
+    clash = [c for c in rcols if c in lcols]
     if not clash:
         return right
     ren = {}
@@ -399,8 +401,26 @@ def _exists_in(e):
     return out
 
 
+_LEAVES = (Var, StartNode, EndNode, HasLabel, HasType, ElementProperty, IntegerLit, BoolLit, NullLit)
+
+
+def _may_hold_exists(e):
+    """False when `e` provably holds no EXISTS pattern (the common predicates:
+    column references, literals and NOT / = over them)."""
+    t = type(e)
+    if t in _LEAVES:
+        return False
+    if t is Not:
+        return _may_hold_exists(e.expr)
+    if t is Equals:
+        return _may_hold_exists(e.lhs) or _may_hold_exists(e.rhs)
+    return True
+
+
 def plan_subqueries(graph, op: Planned, expr: Expr, params=None) -> Planned:
     """Plans every EXISTS pattern inside `expr` that the header does not hold yet."""
+    if not _may_hold_exists(expr):
+        return op
     for ex in _exists_in(expr):
         if ex not in op.header:
             op = plan_exists(graph, ex, op, params)

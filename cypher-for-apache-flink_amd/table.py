@@ -203,6 +203,11 @@ class GpuSession:
         _lib.call("capf_session_sync", self._h)
 
 
+# encoded argument arrays of select() per column tuple (scans and renames
+# repeat the same selections every query)
+_SELECT_ARGS = {}
+
+
 def _program(expr, header, table, params):
     return compile_program(expr, header, set(table.physicalColumns), params, table.session.intern)
 
@@ -210,20 +215,20 @@ def _program(expr, header, table, params):
 class GpuTable:
     """Table[GpuTable] over an opaque capf_table handle."""
 
-    def __init__(self, session, handle):
+    def __init__(self, session, handle, cols=None):
         self.session = session
         self._h = handle
-        self._cols = None
+        self._cols = cols  # physical columns when the operation defines them (else asked once)
 
     def __del__(self):
         h = getattr(self, "_h", None)
         if h and _lib._lib is not None and not _lib._exiting and getattr(self.session, "_h", None):
             _lib._lib.capf_table_release(h)
 
-    def _new(self, fn, *args):
+    def _new(self, fn, *args, cols=None):
         h = c_void_p()
         _lib.call(fn, *args, byref(h))
-        return GpuTable(self.session, h)
+        return GpuTable(self.session, h, cols)
 
     # ---------------------------------------------------------- CypherTable
     @property
@@ -344,24 +349,37 @@ class GpuTable:
         return e.value, b.value
 
     def select(self, *cols):
-        pairs = [(c, c) if isinstance(c, str) else tuple(c) for c in cols]
-        src = [p[0] for p in pairs]
-        al = [p[1] for p in pairs]
-        return self._new("capf_table_select", self._h, len(pairs), _lib.strs(src), _lib.strs(al))
+        try:
+            enc = _SELECT_ARGS.get(cols)
+        except TypeError:  # unhashable (list) pairs
+            enc, cols = None, tuple(c if isinstance(c, str) else tuple(c) for c in cols)
+        if enc is None:
+            pairs = [(c, c) if isinstance(c, str) else tuple(c) for c in cols]
+            al = [p[1] for p in pairs]
+            enc = (len(pairs), _lib.strs([p[0] for p in pairs]), _lib.strs(al), al)
+            if len(_SELECT_ARGS) < 4096:
+                _SELECT_ARGS[cols] = enc
+        return self._new("capf_table_select", self._h, enc[0], enc[1], enc[2], cols=enc[3])
 
     def filter(self, expr, header=None, params=None):
         prog = _program(expr, header, self, params)
         e, keep = _lib._keepalive_expr(prog)
-        return self._new("capf_table_filter", self._h, byref(e))
+        return self._new("capf_table_filter", self._h, byref(e), cols=self._cols)
 
     def drop(self, *cols):
-        return self._new("capf_table_drop", self._h, len(cols), _lib.strs(list(cols)))
+        gone = set(cols)
+        keep = None if self._cols is None else [c for c in self._cols if c not in gone]
+        return self._new("capf_table_drop", self._h, len(cols), _lib.strs(list(cols)), cols=keep)
 
     def join(self, other, join_type, *join_cols):
         jt = JOIN_TYPES[join_type] if isinstance(join_type, str) else int(join_type)
         ls = [l for l, _ in join_cols]
         rs = [r for _, r in join_cols]
-        return self._new("capf_table_join", self._h, other._h, jt, len(join_cols), _lib.strs(ls), _lib.strs(rs))
+        out = None
+        if self._cols is not None and other._cols is not None:
+            out = self._cols + other._cols  # capf_table_join: left columns, then right
+        return self._new("capf_table_join", self._h, other._h, jt, len(join_cols), _lib.strs(ls), _lib.strs(rs),
+                         cols=out)
 
     def unionAll(self, other):
         return self._new("capf_table_union_all", self._h, other._h)

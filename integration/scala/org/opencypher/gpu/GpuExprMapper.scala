@@ -27,7 +27,7 @@ object GpuExprMapper {
   private final val Not_ = 20; private final val And = 21; private final val Or = 22
   private final val IsNull_ = 23; private final val IsNotNull_ = 24
   private final val Add_ = 30; private final val Sub = 31; private final val Mul = 32; private final val Div = 33
-  private final val Mod = 34; private final val Neg = 35
+  private final val Neg = 35   // CAPF_OP_MOD (34) has no okapi Expr: okapi-ir has no Modulo
   private final val ToFloat_ = 40; private final val ToInteger_ = 41; private final val Coalesce_ = 50
 
   def program(expr: Expr, header: RecordHeader, table: GpuTable, parameters: CypherMap): Program = {
@@ -85,7 +85,6 @@ object GpuExprMapper {
       case Subtract(l, r) => go(l); go(r); emit(Sub)
       case Multiply(l, r) => go(l); go(r); emit(Mul)
       case Divide(l, r) => go(l); go(r); emit(Div)
-      case Modulo(l, r) => go(l); go(r); emit(Mod)
       case ToFloat(x) => go(x); emit(ToFloat_)
       case ToInteger(x) => go(x); emit(ToInteger_)                          // Flink: INT (FlinkSQLExprMapper.scala:183)
       case Coalesce(xs) => xs.foreach(go); emit(Coalesce_, xs.size.toLong)
@@ -101,7 +100,7 @@ object GpuExprMapper {
     * FlinkSQLExprMapper.scala:281-287 (Expr.scala:1031-1140). */
   def aggregator(agg: Aggregator, header: RecordHeader, table: GpuTable, parameters: CypherMap): (Int, Program, Boolean) =
     agg match {
-      case CountStar(_) => (Native.AggCountStar, Program.empty, false)
+      case CountStar => (Native.AggCountStar, Program.empty, false)        // case object, Expr.scala:1071
       case Count(e, distinct) => (Native.AggCount, program(e, header, table, parameters), distinct)
       case Sum(e) => (Native.AggSum, program(e, header, table, parameters), false)
       case Min(e) => (Native.AggMin, program(e, header, table, parameters), false)

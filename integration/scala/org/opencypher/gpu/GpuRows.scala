@@ -3,9 +3,8 @@
  * columns: one capf_table_download per column into direct buffers, then rows as
  * `String => CypherValue`, the shape CAPFRecords' materialisation consumes
  * (flink-cypher/.../impl/CAPFRecords.scala:142-144, rowToCypherMap.scala:40-131).
- * Also GpuCypherSession, the RelationalCypherSession[GpuTable] backend state
- * (CAPFSession.scala:47-91): one capf_session, the string dictionary, and the
- * records / element-table factories.
+ * The session, records and element tables that consume it live in
+ * GpuCypherSession.scala, GpuRecords.scala and GpuElementTable.scala.
  */
 package org.opencypher.gpu
 
@@ -59,32 +58,4 @@ object GpuRows {
       if (valid.get(i) == 0) CypherNull
       else CypherList((offsets.getLong(8 * i).toInt until offsets.getLong(8 * (i + 1)).toInt).map(value): _*)
   }
-}
-
-/** Backend state of one RelationalCypherSession[GpuTable] (one per GPU / JVM). */
-final class GpuCypherSession(device: Int = 0, hipStream: Long = 0L) extends AutoCloseable {
-  private[gpu] val handle: Long = Native.guard(Native.sessionCreate(device, hipStream))
-  private val strings = scala.collection.mutable.HashMap.empty[String, Long]
-
-  def intern(s: String): Long = strings.getOrElseUpdate(s, Native.guard(Native.stringIntern(handle, s)))
-
-  /** RelationalCypherRecordsFactory.unit / empty (RelationalCypherRecords.scala:43-54). */
-  def unit(): GpuTable = GpuTable(Native.guard(Native.tableUnit(handle)))(this)
-
-  def empty(columns: Seq[(String, Int)]): GpuTable =
-    GpuTable(Native.guard(Native.tableEmpty(handle, columns.map(_._1).toArray, columns.map(_._2).toArray)))(this)
-
-  /** CAPFElementTable.create / records from host columns (CAPFTable.scala:76-83): direct
-    * buffers of 8 B (INT64 / FLOAT64 / STRING codes) or 1 B (BOOL) per row. */
-  def fromHost(columns: Seq[(String, Int, ByteBuffer, ByteBuffer)], nrows: Long): GpuTable =
-    GpuTable(Native.guard(Native.tableFromHost(handle, columns.map(_._1).toArray, columns.map(_._2).toArray,
-      columns.map(_._3).toArray, columns.map(_._4).toArray, nrows)))(this)
-
-  /** GpuEdgeListDataSource.graph (EdgeListDataSource.scala:56-92): parsed natively. */
-  def edgeList(path: String, sep: String = " ", comment: String = "#"): GpuTable =
-    GpuTable(Native.guard(Native.edgeListRead(handle, path, sep, comment, "id", "source", "target")))(this)
-
-  def sync(): Unit = Native.guard(Native.sessionSync(handle))
-
-  override def close(): Unit = Native.guard(Native.sessionDestroy(handle))
 }

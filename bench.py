@@ -9,13 +9,16 @@ libcapf_gpu.so) over the HBM-resident R-MAT graph: plan build, fused
 factorised count on the GPU, scalar result back on the host.  The graph is
 generated on the device before the timed region (inputs resident in HBM).
 
-value = joined rows/s = count(*) (path multiplicity) × K / elapsed, whole job.
+value = joined rows/s = count(*) (path multiplicity) / median step time, whole
+job: the K timed steps are K single queries, each from the plan call to the
+scalar on the host; the pipelined serving rate is a side field.
 For N > 1 the graph is hash-partitioned over one process per GPU (dist.py);
 ranks are launched by torch.distributed.run, and the max over ranks is timed.
 """
 import argparse
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -62,6 +65,18 @@ def one_hop_rows_query():
                  [Stage([("a", Var("a", "NODE")), ("b", Var("b", "NODE"))])])
 
 
+def reach_query(upper=3):
+    """Config 5: MATCH (a:Person)-[:KNOWS*1..3]->(b:Person) WITH DISTINCT a, b
+    WITH a, count(*) AS reach RETURN reach, count(*) AS n."""
+    from capf_amd.expr import CountStar, Var
+    from capf_amd.planner import Match, NodeP, Query, RelP, Stage
+    return Query([Match([NodeP("a", ("Person",)), NodeP("b", ("Person",))],
+                        [RelP("k", "a", "b", ("KNOWS",), length=(1, upper))])],
+                 [Stage([("a", Var("a")), ("b", Var("b"))], distinct=True),
+                  Stage([("a", Var("a")), ("reach", CountStar())]),
+                  Stage([("reach", Var("reach")), ("n", CountStar())])])
+
+
 def workload_name(args):
     if args.query == "one_hop_rows":
         return f"R-MAT s{args.scale} 1-hop MATCH (a)-->(b) RETURN a, b (rows materialised in HBM)"
@@ -69,15 +84,44 @@ def workload_name(args):
         return f"R-MAT s{args.scale} 1-hop MATCH (a:Person)-->(b) RETURN count(*)"
     if args.query == "triangle":
         return f"R-MAT s{args.scale} triangle MATCH (a)-->(b)-->(c)-->(a) RETURN count(*)"
+    if args.query == "reach":
+        return (f"config 5: LDBC-SF10-shaped KNOWS (2^{args.scale} Person, R-MAT edge factor {args.edge_factor}) "
+                f"MATCH (a:Person)-[:KNOWS*1..3]->(b:Person) WITH DISTINCT a, b WITH a, count(*) AS reach "
+                f"RETURN reach, count(*) AS n")
     return f"R-MAT s{args.scale} 2-hop MATCH (a)-->(b)-->(c) RETURN count(*)"
 
 
-def cpu_threads():
+CPU_THREAD_CAP = 16  # the GPU box's CPU share for one GPU (OMP_NUM_THREADS there)
+
+
+def cpu_available():
     try:
-        n = len(os.sched_getaffinity(0))
+        return len(os.sched_getaffinity(0))
     except AttributeError:
-        n = os.cpu_count() or 1
-    return max(1, min(16, n))
+        return os.cpu_count() or 1
+
+
+def cpu_threads():
+    return max(1, min(CPU_THREAD_CAP, cpu_available()))
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_info(threads):
+    """The host the CPU baseline ran on: model, cores visible, threads used, cap."""
+    return {"cpu_model": cpu_model(), "host_cores_visible": cpu_available(), "threads_used": threads,
+            "thread_cap": CPU_THREAD_CAP,
+            "cap_reason": "one GPU's share of the box's CPUs (OMP_NUM_THREADS=16 on the GPU box)"}
 
 
 def cpu_baseline(session, graph, scale, budget_s):
@@ -113,6 +157,7 @@ def cpu_baseline(session, graph, scale, budget_s):
         "value": rows / probe_s if probe_s > 0 else None,
         "unit": "joined rows/s",
         "cores": th,
+        **cpu_info(th),
         "kind": "port",
         "sample": (f"R-MAT s{scale} 2-hop, Flink plan shape (hash tables on the full node scan and "
                    f"start-keyed R2, {build_s:.1f}s build, not timed); probe of r1 rows [0,{lo}) of {m} "
@@ -195,6 +240,18 @@ def id_storage(args):
             3: "FOR24 (3-byte offsets + base where the range fits 24 bits; int64 values)"}[id_width(args)]
 
 
+def timed_singles(fn, steps, sync):
+    """K single steps, each bracketed by a device sync; (last result, seconds per step)."""
+    out, times = None, []
+    for _ in range(steps):
+        sync()
+        t0 = time.perf_counter()
+        out = fn()
+        times.append(time.perf_counter() - t0)
+    sync()
+    return out, times
+
+
 def timed_steps(fn, steps, sync):
     sync()
     t0 = time.perf_counter()
@@ -266,6 +323,124 @@ def run_rows_leg(args):
     }))
 
 
+REACH_METRIC = ("distinct (a, b) pairs/sec for config 5: [:KNOWS*1..3] var-length expand + DISTINCT + "
+                "GROUP BY on an LDBC-SF10-shaped graph")
+
+
+def reach_cpu_baseline(src, dst, n, budget_s):
+    """The relational plan's shape on the host cores (oracle/rmat.c::reach_paths):
+    per sampled source every isomorphic path of 1..3 rels (the join chain with
+    the isomorphism filters, VarLengthExpandPlanner.scala:82-259), end nodes
+    deduplicated (DISTINCT a, b) and counted (GROUP BY a).  The sample grows
+    until the budget is used; value = distinct pairs found / second."""
+    import numpy as np
+    from oracle import cmodel
+    th = cpu_threads()
+    rng = np.random.default_rng(5)
+    order = rng.permutation(n)
+    k, lo, pairs, paths, secs = 64, 0, 0, 0, 0.0
+    while lo < n and secs < budget_s:
+        part = np.sort(order[lo:lo + k])
+        t0 = time.perf_counter()
+        r, p = cmodel.reach_paths(src, dst, n, part, 3, th)
+        secs += time.perf_counter() - t0
+        pairs += int(r.sum())
+        paths += p
+        lo += k
+        k *= 2
+    return {"value": pairs / secs if secs > 0 else None, "unit": "distinct (a, b) pairs/s", "cores": th,
+            **cpu_info(th), "kind": "port",
+            "sample": (f"config 5 relational plan shape (isomorphic paths of 1..3 rels per source, DISTINCT, "
+                       f"GROUP BY) for {lo} of {n} random sources: {paths} paths, {pairs} distinct pairs "
+                       f"in {secs:.2f}s on {th} threads")}
+
+
+def run_reach_leg(args):
+    """Config 5 at its BASELINE size: 2^16 Person nodes, R-MAT
+    KNOWS rels with edge factor 30, MATCH (a:Person)-[:KNOWS*1..3]->(b:Person)
+    WITH DISTINCT a, b WITH a, count(*) AS reach RETURN reach, count(*) AS n
+    through the planner (the fused var-length reach, csrc/var_length_reach.hip).
+    A step = plan call → the histogram rows on the host; value = distinct (a, b)
+    pairs / median step.  Parity: the histogram is the committed fixture
+    (tests/golden/config5_sf10.json, C bitset BFS)."""
+    import torch  # noqa: F401
+    from capf_amd.graph import ElementTable, ScanGraph
+    from capf_amd.planner import run
+    from capf_amd.synthetic import rmat_seed, thresholds
+    from capf_amd.table import GpuSession
+    s = GpuSession(0)
+    m = args.edge_factor << args.scale
+    n = 1 << args.scale
+    rels = s.rmat_rels(args.scale, rmat_seed(args.scale), thresholds(), 0, m)
+    nodes = s.range_nodes(0, n, id_col="id")
+    g = ScanGraph(s, [ElementTable("node", frozenset(["Person"]), nodes, {})],
+                  [ElementTable("rel", frozenset(["KNOWS"]), rels, {})])
+    q = reach_query()
+    step = lambda: run(g, q)  # noqa: E731
+    t0 = time.perf_counter()
+    res = step()
+    first_ms = (time.perf_counter() - t0) * 1e3
+    for _ in range(args.warmup):
+        step()
+    res, times = timed_singles(step, args.steps, s.sync)
+    hist = sorted([r["reach"], r["n"]] for r in res)
+    pairs = sum(r * c for r, c in hist)
+    median_ms = statistics.median(times) * 1e3
+    parity = {"fixture": None, "match": False}
+    fx = os.path.join(ROOT, "tests", "golden", "config5_sf10.json")
+    if os.path.exists(fx) and (args.scale, args.edge_factor) == (16, 30):
+        with open(fx) as f:
+            want = json.load(f)["histogram"]
+        if hist != want:
+            raise SystemExit("config 5 histogram differs from the committed fixture")
+        parity = {"fixture": "tests/golden/config5_sf10.json", "match": True, "histogram_rows": len(want)}
+    s.reset_profile()
+    s.set_profiling(True)
+    prof_steps = max(1, min(args.steps, 5))
+    for _ in range(prof_steps):
+        step()
+    s.sync()
+    s.set_profiling(False)
+    prof = s.profile()
+    per = {k: v["total_ms"] / prof_steps for k, v in prof.items()}
+    lev = prof.get("vr_level", {})
+    lev_ms = lev.get("total_ms", 0.0) / max(1, lev.get("launches", 1))
+    lev_bytes = lev.get("bytes", 0.0) / max(1, lev.get("launches", 1))
+    achieved = lev_bytes / (lev_ms * 1e-3) / 1e9 if lev_ms > 0 else None
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_reach_s16.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get("vr_level_bytes_per_launch")
+    result = {
+        "metric": REACH_METRIC, "value": pairs / (median_ms * 1e-3), "unit": "distinct (a, b) pairs/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": median_ms,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int64",
+        "data": (f"synthetic LDBC-SF10-shaped graph: R-MAT s{args.scale} (Graph500 a/b/c), edge factor "
+                 f"{args.edge_factor}, every node a Person, generated in HBM before timing"),
+        "config": {"workload": workload_name(args), "scale": args.scale, "nodes": n, "rels": m,
+                   "distinct_pairs": pairs, "sources_reaching": sum(c for _, c in hist),
+                   "plan": "fused var-length reach (planner._fused_reach → capf_var_length_reach)",
+                   "steps_mode": "K single queries, plan call -> histogram rows on the host; value = pairs / median",
+                   "ms_per_query_mean": sum(times) * 1e3 / len(times), "ms_per_query_min": min(times) * 1e3,
+                   "first_query_ms": first_ms, "parity": parity},
+        "roofline": {
+            "bound": "hbm", "kernel": "vr_level (pull BFS level, 64 sources per uint64 word)",
+            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
+            "algorithmic_bytes_per_launch": lev_bytes,
+            "algorithmic_bytes_definition": ("8 B per rel per source word (the source's frontier word, pulled "
+                                             "along every in-edge) + 24 B per node per source word (frontier, "
+                                             "next frontier, visited)"),
+            "kernel_ms": lev_ms, "kernel_ms_per_query": per, "device_ms_per_query": sum(per.values())},
+    }
+    if not args.no_cpu:
+        src, _ = rels.column_arrays("source")
+        dst, _ = rels.column_arrays("target")
+        result["cpu_baseline"] = reach_cpu_baseline(src, dst, n, args.cpu_seconds)
+    print(json.dumps(result))
+
+
 def run_single(args):
     import torch  # noqa: F401  (HIP runtime, device selection)
     from capf_amd.planner import run
@@ -286,23 +461,18 @@ def run_single(args):
     first_query_ms = (time.perf_counter() - t_first) * 1e3
     for _ in range(args.warmup):
         step()
-    # query-at-a-time: plan + fused count + scalar to host, no profiling events
-    count, elapsed_sync = timed_steps(step, args.steps, s.sync)
-    # plan call → scalar result, median of ≥ 5 single queries
-    singles = []
-    for _ in range(max(5, min(args.steps, 15))):
-        s.sync()
-        t1 = time.perf_counter()
-        step()  # returns the scalar on the host
-        singles.append(time.perf_counter() - t1)
-    median_single_ms = sorted(singles)[len(singles) // 2] * 1e3
-    elapsed = elapsed_sync
-    pipelined = False
-    if not args.sync_steps:
-        # pipelined (default): step i plans query i on the host and enqueues its
-        # fused count into slot i (capf_table_count_async) while the GPU still
-        # runs query i−1; every query is planned and counted in full, and the K
-        # counts are downloaded and checked after the closing synchronize.
+    # SURVEY §8(d) / BASELINE.md: the K timed steps are K single queries, each
+    # plan call → scalar result on the host, bracketed by a device sync; value
+    # and ms_per_step come from their MEDIAN
+    count, times = timed_singles(step, args.steps, s.sync)
+    median_ms = statistics.median(times) * 1e3
+    pipelined_ms = None
+    if not args.sync_steps and args.query != "triangle":
+        # side figure (not the value): pipelined serving — step i plans query i
+        # on the host and enqueues its fused count into slot i
+        # (capf_table_count_async) while the GPU still runs query i−1; every
+        # query is planned and counted in full, the K counts are downloaded and
+        # checked after the closing synchronize
         import torch
         from capf_amd.planner import plan_query
         slots = torch.zeros(args.steps, dtype=torch.int64, device="cuda")
@@ -315,16 +485,14 @@ def run_single(args):
         for i in range(min(args.warmup, args.steps)):
             enqueue(i)
         s.sync()
-        s.sync()
         t0 = time.perf_counter()
         for i in range(args.steps):
             enqueue(i)
         s.sync()
-        elapsed = time.perf_counter() - t0
+        pipelined_ms = (time.perf_counter() - t0) * 1e3 / args.steps
         got = slots.cpu().tolist()
         if any(c != count for c in got):
             raise SystemExit(f"pipelined counts {got} differ from the synchronous count {count}")
-        pipelined = True
     # a second, profiled pass attributes the device time to the kernels
     s.reset_profile()
     s.set_profiling(True)
@@ -343,7 +511,7 @@ def run_single(args):
             traffic = (j.get("hbm_bytes_per_query") if args.query == "two_hop" else
                        next((v["read_bytes"] + v["write_bytes"] for k, v in j.get("kernels", {}).items()
                              if k.startswith("k_tri_count")), None))
-    ms_per_step = elapsed * 1e3 / args.steps
+    ms_per_step = median_ms
     if args.query == "triangle":
         roof = tri_roofline(prof, prof_steps, n_nodes, traffic)
     else:
@@ -351,7 +519,7 @@ def run_single(args):
         roof["end_to_end_frac"] = compulsory / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS
     result = {
         "metric": {"two_hop": METRIC, "triangle": TRI_METRIC, "one_hop_person": ONE_HOP_METRIC}[args.query],
-        "value": count * args.steps / elapsed,
+        "value": count / (median_ms * 1e-3),
         "unit": "joined rows/s",
         "n_gpus": 1,
         "steps": args.steps,
@@ -371,12 +539,15 @@ def run_single(args):
         },
         "roofline": roof,
     }
-    result["config"]["steps_mode"] = ("pipelined: plan of query i overlaps the GPU count of query i-1 "
-                                      "(capf_table_count_async), K counts checked after the final sync"
-                                      if pipelined else "query-at-a-time (result downloaded every step)")
-    result["config"]["ms_per_step_query_at_a_time"] = elapsed_sync * 1e3 / args.steps
-    result["config"]["ms_per_query_median_plan_to_scalar"] = median_single_ms
-    result["config"]["joined_rows_per_s_median_plan_to_scalar"] = count / (median_single_ms * 1e-3)
+    result["config"]["steps_mode"] = ("K single queries, each plan call -> scalar on the host between device "
+                                      "syncs (SURVEY 8(d)); value = count / median")
+    result["config"]["ms_per_query_median_plan_to_scalar"] = median_ms
+    result["config"]["ms_per_query_mean"] = sum(times) * 1e3 / len(times)
+    result["config"]["ms_per_query_min"] = min(times) * 1e3
+    result["config"]["ms_per_query_max"] = max(times) * 1e3
+    if pipelined_ms is not None:
+        result["config"]["ms_per_step_pipelined"] = pipelined_ms
+        result["config"]["joined_rows_per_s_pipelined"] = count / (pipelined_ms * 1e-3)
     result["config"]["first_query_ms"] = first_query_ms
     result["config"]["parity"] = check_fixture(args, count)
     if not args.no_cpu and args.query == "two_hop":
@@ -465,37 +636,46 @@ def run_distributed(args):
     count = None
     for _ in range(args.warmup):
         count = step()
-    pipelined = pipe is not None and not args.sync_steps
-    if pipelined:
-        # every step: local partial + the all-reduce into slot i, no host read;
-        # the K summed counts are checked after the closing synchronize
-        if count is None:
-            count = step()
+    # K single queries: each starts on every rank after a barrier and ends when
+    # this rank holds the all-reduced scalar; per step the slowest rank's time,
+    # value from the median step (plan → scalar)
+    times = []
+    for _ in range(args.steps):
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        count = step()
+        times.append(time.perf_counter() - t0)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t = torch.tensor(times, dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    step_max = t.cpu().tolist()
+    median_ms = statistics.median(step_max) * 1e3
+    parity = check_fixture(args, count)
+    pipelined_ms = None
+    if pipe is not None and not args.sync_steps:
+        # side figure: pipelined serving — local partial + all-reduce into slot
+        # i without a host read (step i's all-reduce overlaps step i+1's
+        # kernels); the K counts are checked after the closing synchronize
         slots = torch.zeros(args.steps, dtype=torch.int64, device="cuda")
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    works = []
-    for i in range(args.steps):
-        if pipelined:
-            works.append(pipe(slots[i:i + 1]))
-        else:
-            count = step()
-    for w in works:
-        w.wait()
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if pipelined:
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        works = [pipe(slots[i:i + 1]) for i in range(args.steps)]
+        for w in works:
+            w.wait()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        pipelined_ms = float(el.item()) * 1e3 / args.steps
         got = slots.cpu().tolist()
         if any(c != count for c in got):
             raise SystemExit(f"rank {rank}: pipelined counts {got} differ from {count}")
-    parity = check_fixture(args, count)
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
     s.reset_profile()
     s.set_profiling(True)
     prof_steps = max(1, min(args.steps, 5))
@@ -513,10 +693,10 @@ def run_distributed(args):
     sys.stdout.flush()
     os.dup2(json_fd, 1)
     if rank == 0:
-        ms_per_step = elapsed * 1e3 / args.steps
+        ms_per_step = median_ms
         print(json.dumps({
             "metric": METRIC if args.query == "two_hop" else TRI_METRIC,
-            "value": count * args.steps / elapsed,
+            "value": count / (median_ms * 1e-3),
             "unit": "joined rows/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -534,10 +714,11 @@ def run_distributed(args):
                 "rank0_rel_rows": local_rels,
                 "id_storage": "int64" if args.int64 else (id_storage(args) if args.layout == "node" and args.query == "two_hop" else "FOR32"),
                 "parallelism": f"dp{world} ({layout})",
-                "steps_mode": ("pipelined: step i enqueues the local count + all-reduce into slot i "
-                               "without a host read (the all-reduce of step i overlaps the "
-                               "kernels of step i+1); K counts checked after the final sync"
-                               if pipelined else "query-at-a-time"),
+                "steps_mode": ("K single queries (barrier, then local count + int64 all-reduce + "
+                               "scalar on the host); per step the slowest rank, value = count / median"),
+                "ms_per_query_median_plan_to_scalar": median_ms,
+                "ms_per_query_max_rank_by_step": step_max,
+                "ms_per_step_pipelined": pipelined_ms,
                 "parity": parity,
                 "device_ms_per_query_by_rank": per_rank,
                 "max_rank_device_ms": max(per_rank),
@@ -602,8 +783,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--scale", type=int, default=24)
-    ap.add_argument("--edge-factor", type=int, default=16)
+    ap.add_argument("--scale", type=int, default=None, help="R-MAT scale (default 24; 16 for --query reach)")
+    ap.add_argument("--edge-factor", type=int, default=None, help="default 16; 30 for --query reach")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--sync-steps", action="store_true",
@@ -611,13 +792,19 @@ def main():
     ap.add_argument("--int64", action="store_true", help="keep the id columns int64 (no FOR encoding)")
     ap.add_argument("--for32", action="store_true", help="FOR32 id columns instead of FOR24")
     ap.add_argument("--dist", action="store_true", help="distributed path even at world size 1")
-    ap.add_argument("--query", choices=["two_hop", "triangle", "one_hop_person", "one_hop_rows"], default="two_hop",
-                    help="two_hop: the headline (config 3); triangle: config 4; one_hop_person: config 2")
+    ap.add_argument("--query", choices=["two_hop", "triangle", "one_hop_person", "one_hop_rows", "reach"],
+                    default="two_hop",
+                    help="two_hop: the headline (config 3); triangle: config 4; one_hop_person: config 2; "
+                         "reach: config 5")
     ap.add_argument("--one-device", action="store_true",
                     help="rehearsal: all N ranks on cuda:0 with gloo collectives (not a scaling number)")
     ap.add_argument("--layout", choices=["node", "edge"], default="node",
                     help="multi-GPU graph layout (N > 1): node-partitioned copies or edge-range shards")
     args = ap.parse_args()
+    if args.scale is None:
+        args.scale = 16 if args.query == "reach" else 24
+    if args.edge_factor is None:
+        args.edge_factor = 30 if args.query == "reach" else 16
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -625,6 +812,8 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if args.query == "one_hop_rows":
         run_rows_leg(args)
+    elif args.query == "reach":
+        run_reach_leg(args)
     elif args.gpus > 1 or world > 1 or args.dist:
         run_distributed(args)
     else:

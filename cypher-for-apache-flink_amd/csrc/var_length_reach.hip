@@ -421,13 +421,19 @@ static DataPtr var_length_reach(Session *s, const ColPtr &rsrc, const ColPtr &rd
   const unsigned g = grid_for(m, 256, 256 * 64);
   // 4. MS-BFS in batches of 64·K sources
   BufPtr reach = s->alloc(8 * std::max<int64_t>(ns, 1));
-  const int64_t kmax = std::max<int64_t>(1, (int64_t)(VR_STATE_BUDGET / (24.0 * D)));
+  // CAPF_VR_BUDGET (tests): a smaller state budget in bytes → more source batches
+  const char *vb = getenv("CAPF_VR_BUDGET");
+  const double budget = vb && atof(vb) > 0 ? atof(vb) : (double)VR_STATE_BUDGET;
+  const int64_t kmax = std::max<int64_t>(1, (int64_t)(budget / (24.0 * D)));
   const int64_t K = std::min<int64_t>((ns + 63) / 64, kmax);
   BufPtr fa = s->alloc(8 * (int64_t)D * K), fb = s->alloc(8 * (int64_t)D * K);
   BufPtr vis = s->alloc(8 * (int64_t)D * K);
   const unsigned glev = grid_for((int64_t)D * K, 256, (int64_t)s->num_cus * 32);
   const char *vce = getenv("CAPF_VR_COUNT");  // 0 (tuning): the ballot-transpose count
-  const bool bs_count = !(vce && atoi(vce) == 0);
+  // the bit-sliced count takes row chunks on gridDim.y (≤ 65535): beyond that
+  // (D > 2^26 nodes) the ballot-transpose count, whose grid is 1-D over sources
+  const bool bs_count = !(vce && atoi(vce) == 0) &&
+                        (int64_t)D <= (int64_t)65535 * (1024 / WAVE) * VR_CR;
   for (int64_t s0 = 0; s0 < ns; s0 += 64 * K) {
     const int64_t nb = std::min<int64_t>(64 * K, ns - s0);
     HIP_CHECK(hipMemsetAsync(fb->p, 0, 8 * (size_t)D * K, s->stream));

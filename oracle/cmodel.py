@@ -63,6 +63,10 @@ def lib():
         l.rmat_stream_counts.restype = None
         l.count_triangle_trace.argtypes = [P, P, i64, i64, i32]
         l.count_triangle_trace.restype = u64
+        l.reach_bitset.argtypes = [P, P, i64, i64, i32, i32, P]
+        l.reach_bitset.restype = None
+        l.reach_paths.argtypes = [P, P, i64, i64, i32, P, i64, i32, P]
+        l.reach_paths.restype = i64
         l.oracle_splitmix64.argtypes = [u64]
         l.oracle_splitmix64.restype = u64
         _lib = l
@@ -170,3 +174,32 @@ class Pipeline:
 
     def __del__(self):
         self.close()
+
+
+def reach_bitset(src, dst, n, upper=3, threads=8):
+    """reach[a] for every node a in [0, n): distinct nodes at walk distance 1..upper
+    (config 5; oracle/rmat.c::reach_bitset)."""
+    s = np.ascontiguousarray(src, dtype=np.int64)
+    d = np.ascontiguousarray(dst, dtype=np.int64)
+    out = np.zeros(n, dtype=np.int64)
+    lib().reach_bitset(s.ctypes.data, d.ctypes.data, len(s), n, upper, threads, out.ctypes.data)
+    return out
+
+
+def reach_paths(src, dst, n, sources, upper=3, threads=8):
+    """(reach per sampled source, isomorphic paths enumerated): the relational
+    plan's shape (join chain + isomorphism filters, DISTINCT, GROUP BY)."""
+    s = np.ascontiguousarray(src, dtype=np.int64)
+    d = np.ascontiguousarray(dst, dtype=np.int64)
+    a = np.ascontiguousarray(sources, dtype=np.int64)
+    out = np.zeros(max(len(a), 1), dtype=np.int64)
+    paths = lib().reach_paths(s.ctypes.data, d.ctypes.data, len(s), n, upper, a.ctypes.data, len(a), threads,
+                              out.ctypes.data)
+    return out[:len(a)], int(paths)
+
+
+def reach_histogram(reach):
+    """RETURN reach, count(*) AS n as sorted [reach, n] pairs (sources with reach ≥ 1)."""
+    r = np.asarray(reach)
+    vals, cnts = np.unique(r[r > 0], return_counts=True)
+    return [[int(v), int(c)] for v, c in zip(vals, cnts)]

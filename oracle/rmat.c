@@ -556,3 +556,200 @@ uint64_t count_triangle_trace(const int64_t *src, const int64_t *dst, int64_t m,
   free(ooff); free(onb); free(omul); free(ioff); free(inb); free(imul);
   return tr - bad;
 }
+
+/* ------------------------------------------------------------------------
+ * Config 5 (BASELINE.json):
+ *   MATCH (a:L)-[:T*1..u]->(b:L) WITH DISTINCT a, b WITH a, count(*) AS reach
+ *   RETURN reach, count(*) AS n
+ * on nodes [0, n), every node a source and a target.
+ *
+ * reach_bitset: reach[a] = |{b : some walk a → b of length 1..u}| by a
+ * breadth-first search from 64 sources at a time (bit j of a uint64 per node
+ * = source s0 + j), pushing each node's NEW bits along its out-edges (CSR by
+ * source).  Lower bound 1 on a walk-reachability plan equals the relational
+ * plan's DISTINCT (a, b) pairs of isomorphic paths (a closed sub-walk between
+ * two uses of one rel can be cut out: VarLengthExpandPlanner.scala:82-259
+ * with the isomorphism filter :178-179; pinned by tests/test_ldbc_config5.py
+ * against path enumeration).  Independent of the GPU kernels: push from the
+ * source side over a CSR by source; the GPU pulls over a CSR by target.
+ *
+ * reach_paths: the relational plan's shape for a sample of sources — every
+ * path of 1..u rels with pairwise distinct rel ids (the join chain plus
+ * isomorphism filters), its end node deduplicated per source (DISTINCT a, b),
+ * counted per source (GROUP BY a) — the Flink-shaped CPU baseline.
+ * ---------------------------------------------------------------------- */
+typedef struct {
+  const int64_t *off, *adj;  /* CSR by source: out-neighbours (rel order) */
+  int64_t n, chunks;
+  int upper;
+  int64_t *next;             /* shared chunk counter */
+  pthread_mutex_t *mu;
+  int64_t *reach;            /* out: per node */
+} ReachTask;
+
+static void build_csr(const int64_t *src, const int64_t *dst, int64_t m, int64_t n, int64_t **off_o,
+                      int64_t **adj_o, int64_t **rid_o) {
+  int64_t *off = (int64_t *)calloc((size_t)n + 1, 8);
+  for (int64_t e = 0; e < m; ++e)
+    if (src[e] >= 0 && src[e] < n && dst[e] >= 0 && dst[e] < n) off[src[e] + 1]++;
+  for (int64_t v = 0; v < n; ++v) off[v + 1] += off[v];
+  int64_t *pos = (int64_t *)malloc((size_t)(n + 1) * 8);
+  memcpy(pos, off, (size_t)(n + 1) * 8);
+  int64_t *adj = (int64_t *)malloc((size_t)(off[n] > 0 ? off[n] : 1) * 8);
+  int64_t *rid = rid_o ? (int64_t *)malloc((size_t)(off[n] > 0 ? off[n] : 1) * 8) : NULL;
+  for (int64_t e = 0; e < m; ++e)
+    if (src[e] >= 0 && src[e] < n && dst[e] >= 0 && dst[e] < n) {
+      const int64_t p = pos[src[e]]++;
+      adj[p] = dst[e];
+      if (rid) rid[p] = e;
+    }
+  free(pos);
+  *off_o = off;
+  *adj_o = adj;
+  if (rid_o) *rid_o = rid;
+}
+
+static void *reach_worker(void *arg) {
+  ReachTask *t = (ReachTask *)arg;
+  const int64_t n = t->n;
+  uint64_t *vis = (uint64_t *)malloc((size_t)n * 8), *cur = (uint64_t *)malloc((size_t)n * 8),
+           *nxt = (uint64_t *)malloc((size_t)n * 8);
+  for (;;) {
+    pthread_mutex_lock(t->mu);
+    const int64_t c = (*t->next)++;
+    pthread_mutex_unlock(t->mu);
+    if (c >= t->chunks) break;
+    const int64_t s0 = c * 64, ns = n - s0 < 64 ? n - s0 : 64;
+    memset(vis, 0, (size_t)n * 8);
+    memset(cur, 0, (size_t)n * 8);
+    /* level 1: the sources' own out-edges */
+    for (int64_t j = 0; j < ns; ++j)
+      for (int64_t p = t->off[s0 + j]; p < t->off[s0 + j + 1]; ++p) cur[t->adj[p]] |= 1ull << j;
+    for (int64_t v = 0; v < n; ++v) vis[v] = cur[v];
+    for (int level = 2; level <= t->upper; ++level) {
+      memset(nxt, 0, (size_t)n * 8);
+      for (int64_t v = 0; v < n; ++v) {
+        const uint64_t f = cur[v];
+        if (!f) continue;
+        for (int64_t p = t->off[v]; p < t->off[v + 1]; ++p) nxt[t->adj[p]] |= f;
+      }
+      for (int64_t v = 0; v < n; ++v) {
+        const uint64_t fresh = nxt[v] & ~vis[v];
+        cur[v] = fresh;
+        vis[v] |= fresh;
+      }
+    }
+    int64_t cnt[64] = {0};
+    for (int64_t v = 0; v < n; ++v)
+      for (uint64_t w = vis[v]; w; w &= w - 1) cnt[__builtin_ctzll(w)]++;
+    for (int64_t j = 0; j < ns; ++j) t->reach[s0 + j] = cnt[j];
+  }
+  free(vis);
+  free(cur);
+  free(nxt);
+  return NULL;
+}
+
+void reach_bitset(const int64_t *src, const int64_t *dst, int64_t m, int64_t n, int upper, int threads,
+                  int64_t *reach) {
+  if (threads < 1) threads = 1;
+  int64_t *off, *adj;
+  build_csr(src, dst, m, n, &off, &adj, NULL);
+  int64_t next = 0;
+  pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
+  pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * threads);
+  ReachTask *ts = (ReachTask *)calloc((size_t)threads, sizeof(ReachTask));
+  for (int i = 0; i < threads; ++i) {
+    ts[i].off = off; ts[i].adj = adj; ts[i].n = n; ts[i].chunks = (n + 63) / 64;
+    ts[i].upper = upper; ts[i].next = &next; ts[i].mu = &mu; ts[i].reach = reach;
+    pthread_create(&th[i], NULL, reach_worker, &ts[i]);
+  }
+  for (int i = 0; i < threads; ++i) pthread_join(th[i], NULL);
+  free(th);
+  free(ts);
+  free(off);
+  free(adj);
+}
+
+typedef struct {
+  const int64_t *off, *adj, *rid, *sources;
+  int64_t nsrc, n;
+  int upper;
+  int64_t *next;
+  pthread_mutex_t *mu;
+  int64_t *reach, *paths;  /* out: per sampled source */
+} PathTask;
+
+static void *paths_worker(void *arg) {
+  PathTask *t = (PathTask *)arg;
+  uint8_t *seen = (uint8_t *)calloc((size_t)t->n, 1);
+  int64_t *touched = (int64_t *)malloc((size_t)(t->n > 0 ? t->n : 1) * 8);
+  for (;;) {
+    pthread_mutex_lock(t->mu);
+    const int64_t i = (*t->next)++;
+    pthread_mutex_unlock(t->mu);
+    if (i >= t->nsrc) break;
+    const int64_t a = t->sources[i];
+    int64_t nt = 0, paths = 0;
+    /* e1: every rel leaving a */
+    for (int64_t p1 = t->off[a]; p1 < t->off[a + 1]; ++p1) {
+      const int64_t b1 = t->adj[p1], r1 = t->rid[p1];
+      ++paths;
+      if (!seen[b1]) { seen[b1] = 1; touched[nt++] = b1; }
+      if (t->upper < 2) continue;
+      /* e2 ≠ e1 */
+      for (int64_t p2 = t->off[b1]; p2 < t->off[b1 + 1]; ++p2) {
+        const int64_t r2 = t->rid[p2];
+        if (r2 == r1) continue;
+        const int64_t b2 = t->adj[p2];
+        ++paths;
+        if (!seen[b2]) { seen[b2] = 1; touched[nt++] = b2; }
+        if (t->upper < 3) continue;
+        /* e3 ∉ {e1, e2} */
+        for (int64_t p3 = t->off[b2]; p3 < t->off[b2 + 1]; ++p3) {
+          const int64_t r3 = t->rid[p3];
+          if (r3 == r1 || r3 == r2) continue;
+          const int64_t b3 = t->adj[p3];
+          ++paths;
+          if (!seen[b3]) { seen[b3] = 1; touched[nt++] = b3; }
+        }
+      }
+    }
+    for (int64_t k = 0; k < nt; ++k) seen[touched[k]] = 0;
+    t->reach[i] = nt;
+    t->paths[i] = paths;
+  }
+  free(seen);
+  free(touched);
+  return NULL;
+}
+
+/* upper ≤ 3.  Returns the number of paths enumerated (the relational plan's
+ * rows before DISTINCT) over the sampled sources. */
+int64_t reach_paths(const int64_t *src, const int64_t *dst, int64_t m, int64_t n, int upper,
+                    const int64_t *sources, int64_t nsrc, int threads, int64_t *reach) {
+  if (threads < 1) threads = 1;
+  int64_t *off, *adj, *rid;
+  build_csr(src, dst, m, n, &off, &adj, &rid);
+  int64_t *paths = (int64_t *)calloc((size_t)(nsrc > 0 ? nsrc : 1), 8);
+  int64_t next = 0;
+  pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
+  pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * threads);
+  PathTask *ts = (PathTask *)calloc((size_t)threads, sizeof(PathTask));
+  for (int i = 0; i < threads; ++i) {
+    ts[i].off = off; ts[i].adj = adj; ts[i].rid = rid; ts[i].sources = sources; ts[i].nsrc = nsrc;
+    ts[i].n = n; ts[i].upper = upper; ts[i].next = &next; ts[i].mu = &mu; ts[i].reach = reach;
+    ts[i].paths = paths;
+    pthread_create(&th[i], NULL, paths_worker, &ts[i]);
+  }
+  for (int i = 0; i < threads; ++i) pthread_join(th[i], NULL);
+  int64_t total = 0;
+  for (int64_t i = 0; i < nsrc; ++i) total += paths[i];
+  free(th);
+  free(ts);
+  free(paths);
+  free(off);
+  free(adj);
+  free(rid);
+  return total;
+}

@@ -6,6 +6,9 @@ container; /root/reference is only read here, never at test time):
   ldbc_sample.json      the reference's LDBC sample KNOWS graph
                         (morpheus-examples/src/main/resources/ldbc/csv/
                         person_0_0.csv.gz, person_knows_person_0_0.csv.gz)
+  config5_sf10.json     config 5 at its BASELINE size (2^16 Person, R-MAT edge
+                        factor 30): the RETURN reach, count(*) histogram by
+                        the C bitset BFS (oracle/rmat.c::reach_bitset)
   rmat_counts.json      R-MAT counts of configs 2/3 at small scales by the
                         closed forms (oracle/rmat.c), plus the config-5 query
                         on the LDBC sample by the oracle table;
@@ -113,6 +116,34 @@ def main():
     from ldbc import config5_query, ldbc_graph_data
     g = ScanGraph.from_data(OracleSession(), ldbc_graph_data())
     counts["ldbc_config5"] = sorted(([r["reach"], r["n"]] for r in run(g, config5_query())))
+    # config 5 at its BASELINE size: LDBC-SF10-shaped KNOWS (2^16 Person nodes,
+    # R-MAT edge factor 30 = 1,966,080 rels), every node a Person; the C
+    # bitset BFS (oracle/rmat.c::reach_bitset), checked here against path
+    # enumeration (reach_paths) on a sample of sources
+    if full or "config5" not in old:
+        import numpy as np
+        sc5, ef5 = 16, 30
+        s5, d5 = cmodel.rmat(sc5, ef5)
+        n5 = 1 << sc5
+        reach5 = cmodel.reach_bitset(s5, d5, n5, 3)
+        sample = np.arange(0, n5, 257)
+        rp, _ = cmodel.reach_paths(s5, d5, n5, sample, 3)
+        assert np.array_equal(rp, reach5[sample])
+        hist5 = cmodel.reach_histogram(reach5)
+        with open(os.path.join(HERE, "config5_sf10.json"), "w") as f:  # compact: 14.5k [reach, n] pairs
+            json.dump({"scale": sc5, "edge_factor": ef5, "upper": 3, "histogram": hist5}, f,
+                      separators=(",", ":"))
+        counts["config5"] = {
+            "scale": sc5, "edge_factor": ef5, "nodes": n5, "rels": len(s5), "upper": 3,
+            "histogram_file": "config5_sf10.json", "histogram_rows": len(hist5),
+            "pairs": int(reach5.sum()),
+            "sources": int((reach5 > 0).sum()),
+            # Σ (a + 1)·reach[a] mod 2^63: pins reach per source, not only the histogram
+            "weighted": int(((np.arange(n5, dtype=np.uint64) + 1) * reach5.astype(np.uint64)).sum()
+                            % np.uint64(1 << 63)),
+        }
+    else:
+        counts["config5"] = old["config5"]
     with open(path, "w") as f:
         json.dump(counts, f, indent=1, sort_keys=True)
 

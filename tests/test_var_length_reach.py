@@ -93,3 +93,98 @@ def test_fused_equals_relational_plan(gpu_session, monkeypatch, upper):
     monkeypatch.setenv("CAPF_FUSED_REACH", "0")
     plain = sorted([r["reach"], r["n"]] for r in run(g, q))
     assert fused == plain
+
+
+# ------------------------------------------------ config 5 at its BASELINE size
+def _sf10_graph(session):
+    """LDBC-SF10-shaped KNOWS — 2^16 Person nodes,
+    R-MAT (Graph500 a/b/c) rels with edge factor 30 (1,966,080), generated in HBM."""
+    from capf_amd.graph import ElementTable
+    from capf_amd.synthetic import rmat_seed, thresholds
+    scale, ef = 16, 30
+    rels = session.rmat_rels(scale, rmat_seed(scale), thresholds(), 0, ef << scale)
+    nodes = session.range_nodes(0, 1 << scale, id_col="id")
+    g = ScanGraph(session, [ElementTable("node", frozenset(["Person"]), nodes, {})],
+                  [ElementTable("rel", frozenset(["KNOWS"]), rels, {})])
+    return g, rels
+
+
+def _fixture5():
+    import json
+    import os
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    with open(os.path.join(here, "rmat_counts.json")) as f:
+        summary = json.load(f)["config5"]
+    with open(os.path.join(here, summary["histogram_file"])) as f:
+        return summary, json.load(f)["histogram"]
+
+
+def test_config5_fixture_consistent():
+    summary, hist = _fixture5()
+    assert len(hist) == summary["histogram_rows"]
+    assert sum(r * n for r, n in hist) == summary["pairs"]
+    assert sum(n for _, n in hist) == summary["sources"]
+    assert summary["rels"] == summary["edge_factor"] << summary["scale"]
+
+
+@pytest.mark.parametrize("scale,ef", [(9, 8), (11, 30)])
+def test_c_bitset_bfs_vs_matrix_powers(scale, ef):
+    """oracle/rmat.c::reach_bitset (the config-5 fixture's oracle) against the
+    scipy matrix powers and against isomorphic-path enumeration."""
+    src, dst = cmodel.rmat(scale, ef)
+    n = 1 << scale
+    p = np.arange(n)
+    for upper in (1, 2, 3):
+        r = cmodel.reach_bitset(src, dst, n, upper)
+        exp = oreach.reach_counts(src, dst, p, p, upper)
+        assert {int(a): int(c) for a, c in enumerate(r) if c} == exp
+    sample = np.arange(0, n, 5)
+    rp, paths = cmodel.reach_paths(src, dst, n, sample, 3)
+    assert np.array_equal(rp, cmodel.reach_bitset(src, dst, n, 3)[sample]) and paths > 0
+
+
+@pytest.mark.gpu
+def test_config5_sf10_histogram(gpu_session):
+    """The config-5 query at its BASELINE size against the committed fixture
+    (C bitset BFS, tests/golden/config5_sf10.json)."""
+    summary, hist = _fixture5()
+    g, _ = _sf10_graph(gpu_session)
+    got = sorted([r["reach"], r["n"]] for r in run(g, config5_query()))
+    assert got == hist
+    assert sum(r * n for r, n in got) == summary["pairs"] == 1819538648
+
+
+@pytest.mark.gpu
+def test_config5_sf10_per_source(gpu_session):
+    """reach per source at SF10 size against the C BFS run on the same edges
+    (downloaded), and the fixture's weighted checksum."""
+    summary, _ = _fixture5()
+    g, rels = _sf10_graph(gpu_session)
+    got = {r["a"]: r["reach"] for r in run(g, reach_query(3))}
+    src, _ = rels.column_arrays("source")
+    dst, _ = rels.column_arrays("target")
+    exp = cmodel.reach_bitset(src, dst, 1 << 16, 3)
+    assert got == {a: int(c) for a, c in enumerate(exp) if c}
+    w = sum((a + 1) * c for a, c in got.items()) % (1 << 63)
+    assert w == summary["weighted"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env", [{}, {"CAPF_VR_COUNT": "0"}, {"CAPF_VR_BUDGET": "4e7"},
+                                 {"CAPF_VR_BUDGET": "4e7", "CAPF_VR_COUNT": "0"}],
+                         ids=["default", "ballot_count", "batched", "batched_ballot"])
+def test_reach_multiblock_paths(gpu_session, monkeypatch, env):
+    """More than 4096 sources and node rows (several count blocks on both grid
+    axes, cross-block atomics) and — with a small state budget — several
+    source batches: both count kernels against the C BFS (scale 13)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    scale = 13
+    src, dst = cmodel.rmat(scale, 16)
+    n = 1 << scale
+    nodes = [(i, frozenset(["Person"]), {}) for i in range(n)]
+    rels = [(k, int(s), int(d), "KNOWS", {}) for k, (s, d) in enumerate(zip(src.tolist(), dst.tolist()))]
+    g = ScanGraph.from_data(gpu_session, GraphData(nodes, rels))
+    got = {r["a"]: r["reach"] for r in run(g, reach_query(3))}
+    exp = cmodel.reach_bitset(src, dst, n, 3)
+    assert got == {a: int(c) for a, c in enumerate(exp) if c}

@@ -81,6 +81,7 @@ _SIGS = {
     "capf_session_last_plan": (c_char_p, [_S]),
     "capf_string_intern": (c_int32, [_S, c_char_p, POINTER(c_int64)]),
     "capf_string_lookup": (c_int32, [_S, c_int64, POINTER(c_char_p)]),
+    "capf_string_digest": (c_int32, [_S, POINTER(c_int64), POINTER(c_uint64)]),
     "capf_table_from_host": (c_int32, [_S, c_int32, _STRS, POINTER(c_int32), POINTER(c_void_p),
                                        POINTER(c_void_p), c_int64, _PT]),
     "capf_table_from_device": (c_int32, [_S, c_int32, _STRS, POINTER(c_int32), POINTER(c_void_p),

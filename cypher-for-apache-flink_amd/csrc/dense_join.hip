@@ -158,10 +158,12 @@ bool dense_join(Session *s, const Data &l, const Data &r, const std::vector<std:
   }
   // every probe key provably matches (no NULL, the key's range inside the dense
   // build range — cached column statistics): no match count to read back, so
-  // the join stays asynchronous; otherwise one host read of the count
+  // the join stays asynchronous; otherwise one host read of the count.  Only
+  // statistics already cached count: computing them here would cost more syncs
+  // than the one readback they save.
   int64_t matched = 0;
-  const ColStats &pst = column_stats(s, pk);
-  if (n > 0 && pst.non_null == n && pst.min >= di->min && pst.max < di->min + di->n) {
+  const std::optional<ColStats> &pst = pk->stats;
+  if (n > 0 && pst && pst->non_null == n && pst->min >= di->min && pst->max < di->min + di->n) {
     matched = n;
   } else {
     HIP_CHECK(hipMemcpyAsync(s->h_scalars, acc->p, 8, hipMemcpyDeviceToHost, s->stream));

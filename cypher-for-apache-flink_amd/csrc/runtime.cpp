@@ -722,6 +722,23 @@ capf_status capf_string_lookup(capf_session *cs, int64_t code, const char **str)
   CAPF_API_END
 }
 
+capf_status capf_string_digest(capf_session *cs, int64_t *count, uint64_t *digest) {
+  CAPF_API_BEGIN
+  need(cs, "session");
+  need(count, "count");
+  need(digest, "digest");
+  Session &s = cs->impl;
+  std::lock_guard<std::mutex> g(s.str_mu);
+  uint64_t h = 1469598103934665603ull;
+  for (const std::string &str : s.strings) {
+    for (unsigned char ch : str) h = (h ^ ch) * 1099511628211ull;
+    h = (h ^ 0xffu) * 1099511628211ull;  // separator: ("ab","c") != ("a","bc")
+  }
+  *count = (int64_t)s.strings.size();
+  *digest = h;
+  CAPF_API_END
+}
+
 static void check_unique_names(const std::vector<std::string> &names) {
   for (size_t i = 0; i < names.size(); ++i)
     for (size_t j = i + 1; j < names.size(); ++j)

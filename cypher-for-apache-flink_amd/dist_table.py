@@ -44,13 +44,13 @@ all_to_all_single per shuffle (RCCL over xGMI; host-staged under gloo), the
 columns packed row-major; the CPU tests drive the same DistTable logic over
 the numpy oracle with their own exchange.
 """
-from ctypes import byref, c_int32, c_int64, c_void_p
+from ctypes import byref, c_int32, c_int64, c_uint64, c_void_p
 
 import torch
 import torch.distributed as dist
 
 from . import _lib
-from .expr import (AGG_AVG, AGG_COUNT, AGG_COUNT_STAR, AGG_MAX, AGG_MIN, AGG_SUM, T_BOOL, T_NULL, Count,
+from .expr import (AGG_AVG, AGG_COUNT, AGG_COUNT_STAR, AGG_MAX, AGG_MIN, AGG_SUM, T_BOOL, T_NULL, T_STRING, Count,
                    Divide, Max, Min, Sum, Var)
 from .header import RecordHeader
 
@@ -123,8 +123,22 @@ class GpuExchange:
             v = c_int32()
             _lib.call("capf_table_has_nulls", table._h, c.encode(), byref(v))
             has.append(v.value)
+        # STRING columns travel as dictionary codes: every rank's dictionary must
+        # be the same (size and digest, code order).  Their 16-bit pieces and
+        # negations ride in the same MAX all-reduce: min == max on every piece.
+        check = []
+        if T_STRING in types:
+            cnt, dig = c_int64(), c_uint64()
+            _lib.call("capf_string_digest", self.s._h, byref(cnt), byref(dig))
+            pieces = [(cnt.value >> k) & 0xFFFF for k in (0, 16, 32)] + \
+                [(dig.value >> k) & 0xFFFF for k in (0, 16, 32, 48)]
+            check = [v for x in pieces for v in (x, -x)]
+        got = self.all_max_vec(has + check)
+        if check and any(got[len(has) + i] != -got[len(has) + i + 1] for i in range(0, len(check), 2)):
+            raise _lib.IllegalStateException(
+                "string dictionaries differ between ranks: STRING columns cannot be exchanged as codes")
         # one layout on every rank; an all-NULL column is rebuilt from its type alone
-        nullable = [bool(x) and t != T_NULL for x, t in zip(self.all_max_vec(has), types)]
+        nullable = [bool(x) and t != T_NULL for x, t in zip(got[:len(has)], types)]
         width = [0 if t == T_NULL else (1 if t == T_BOOL else 8) for t in types]
         return cols, types, width, nullable
 

@@ -193,7 +193,9 @@ class FSGraphSource:
         names = [f for f, _ in fields]
         types = [CT_TO_CAPF[_base_type(ct)[0]] for _, ct in fields]
         files = self._files(path)
-        gpu = hasattr(self.session, "csv_read_longs")
+        # The GPU LONG parser rejects an empty field; a nullable field ('INTEGER?')
+        # stores NULL as an empty field, so such tables take the host reader.
+        gpu = hasattr(self.session, "csv_read_longs") and not any(_base_type(ct)[1] for _, ct in fields)
         parts = []
         for fp in files:
             if gpu and all(t == T_INT for t in types):

@@ -171,6 +171,9 @@ const char *capf_session_last_plan(capf_session *s);
 /* String dictionary for CAPF_TYPE_STRING columns. */
 capf_status capf_string_intern(capf_session *s, const char *str, int64_t *code);
 capf_status capf_string_lookup(capf_session *s, int64_t code, const char **str);
+/* Size and FNV-1a digest of the dictionary in code order: ranks that exchange
+ * STRING columns as codes check that their dictionaries agree (dist_table.py). */
+capf_status capf_string_digest(capf_session *s, int64_t *count, uint64_t *digest);
 
 /* ---------------------------------------------------- table construction
  * CAPFElementTable.create / CAPFRecordsFactory.from

@@ -229,6 +229,14 @@ JNI(jstring, stringLookup)(JNIEnv *env, jobject, jlong s, jlong code) {
   if (fail(env, capf_string_lookup(S(s), code, &p))) return nullptr;
   return env->NewStringUTF(p ? p : "");
 }
+// out[0] = dictionary size, out[1] = FNV-1a digest (bits)
+JNI(void, stringDigest)(JNIEnv *env, jobject, jlong s, jlongArray out) {
+  int64_t n = 0;
+  uint64_t d = 0;
+  if (fail(env, capf_string_digest(S(s), &n, &d))) return;
+  jlong v[2] = {(jlong)n, (jlong)d};
+  env->SetLongArrayRegion(out, 0, 2, v);
+}
 
 // ---------------------------------------------------------------- construction
 // CAPFElementTable.create / CAPFRecordsFactory.from (CAPFTable.scala:76-83,

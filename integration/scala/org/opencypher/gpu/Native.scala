@@ -83,6 +83,7 @@ object Native {
   @native def sessionLastPlan(session: Long): String
   @native def stringIntern(session: Long, s: String): Long
   @native def stringLookup(session: Long, code: Long): String
+  @native def stringDigest(session: Long, out: Array[Long]): Unit
 
   // construction (CAPFTable.scala:76-83, CAPFRecords.scala:47-100, RelationalCypherRecords.scala:43-54)
   @native def tableFromHost(session: Long, names: Array[String], types: Array[Int], data: Array[ByteBuffer],

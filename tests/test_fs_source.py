@@ -142,6 +142,31 @@ def test_products_graph_on_gpu(gpu_session):
     assert rel.column_values("p_rating") == [int(r[4]) for r in _csv_rows("relationships", "BOUGHT", "table.csv")]
 
 
+NULLABLE_INT = """
+CREATE (a:Person {name: 'A', age: 30})
+CREATE (b:Person {name: 'B'})
+CREATE (c:Person {name: 'C', age: 7})
+CREATE (a)-[:KNOWS {since: 2010}]->(b)
+CREATE (b)-[:KNOWS]->(c)
+"""
+
+
+@pytest.mark.gpu
+def test_store_read_nullable_integer_on_gpu(gpu_session, tmp_path):
+    """A nullable INTEGER property ('INTEGER?') with a missing value is stored
+    as an empty CSV field and reads back as NULL on the GPU session too."""
+    g = ScanGraph.from_data(gpu_session, parse_create(NULLABLE_INT))
+    FSGraphSource(gpu_session, str(tmp_path)).store("nulls", g)
+    back = FSGraphSource(gpu_session, str(tmp_path)).graph("nulls")
+    q = Query([Match([NodeP("a"), NodeP("b")], [RelP("r", "a", "b")])],
+              [Stage([("a", _p("a", "name")), ("age", _p("a", "age")), ("b_age", _p("b", "age")),
+                      ("since", _p("r", "since"))])])
+    got = bag(run(back, q))
+    assert got == bag(run(g, q))
+    assert got == bag([{"a": "A", "age": 30, "b_age": None, "since": 2010},
+                       {"a": "B", "age": None, "b_age": 7, "since": None}])
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("compact", [False, 3])
 def test_rmat_csv_graph_on_gpu(gpu_session, tmp_path, compact):

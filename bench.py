@@ -79,7 +79,8 @@ def reach_query(upper=3):
 
 def workload_name(args):
     if args.query == "one_hop_rows":
-        return f"R-MAT s{args.scale} 1-hop MATCH (a)-->(b) RETURN a, b (rows materialised in HBM)"
+        return (f"R-MAT s{args.scale} 1-hop MATCH (a)-->(b) RETURN a, b (rows materialised in HBM)"
+                + (f", sparse node ids v*{args.id_stride}+7" if args.id_stride != 1 else ""))
     if args.query == "one_hop_person":
         return f"R-MAT s{args.scale} 1-hop MATCH (a:Person)-->(b) RETURN count(*)"
     if args.query == "triangle":
@@ -272,7 +273,7 @@ def run_rows_leg(args):
     from capf_amd.synthetic import rmat_graph
     from capf_amd.table import GpuSession
     s = GpuSession(0)
-    g = rmat_graph(s, args.scale, args.edge_factor, compact=True)
+    g = rmat_graph(s, args.scale, args.edge_factor, compact=True, id_stride=args.id_stride)
     q = one_hop_rows_query()
     n_nodes = 1 << args.scale
     m = args.edge_factor << args.scale
@@ -306,12 +307,15 @@ def run_rows_leg(args):
         "scaling": "strong", "vs_baseline": None, "dtype": "int64",
         "data": f"synthetic R-MAT s{args.scale} generated in HBM before timing",
         "config": {"workload": workload_name(args), "scale": args.scale, "nodes": n_nodes, "rels": m,
-                   "rows": rows, "id_storage": "FOR32", "plan": s.last_plan() or "relational (2 joins)",
+                   "rows": rows, "id_storage": "FOR32" if args.id_stride == 1 else
+                   f"int64, sparse ids v*{args.id_stride}+7 (no FOR: the range exceeds 32 bits)",
+                   "plan": s.last_plan() or "relational (2 joins)",
                    "join": {"radix": "radix-partitioned (csrc/radix_join.hip), forced by CAPF_JOIN=radix",
                             "hash": "global hash table (csrc/kernels_hash.hip), forced by CAPF_JOIN=hash"}.get(
                        os.environ.get("CAPF_JOIN", ""),
-                       "planner choice: direct-address join on the dense node-id key (csrc/dense_join.hip), "
-                       "radix-partitioned join (csrc/radix_join.hip) for other keys")},
+                       "planner choice: direct-address join on the dense node-id key, hashed unique-key index "
+                       "on sparse node ids (csrc/dense_join.hip), radix-partitioned join (csrc/radix_join.hip) "
+                       "for non-unique keys")},
         # the step runs many small kernels (two joins, gathers, scans): the
         # roofline is taken over the whole step's wall time; the timed
         # kernels' split (partition / join passes) is reported beside it
@@ -796,6 +800,8 @@ def main():
                     default="two_hop",
                     help="two_hop: the headline (config 3); triangle: config 4; one_hop_person: config 2; "
                          "reach: config 5")
+    ap.add_argument("--id-stride", type=int, default=1,
+                    help="one_hop_rows: node ids v*stride+7 (sparse, no dense range; e.g. 1000003)")
     ap.add_argument("--one-device", action="store_true",
                     help="rehearsal: all N ranks on cuda:0 with gloo collectives (not a scaling number)")
     ap.add_argument("--layout", choices=["node", "edge"], default="node",

@@ -37,7 +37,55 @@ struct DenseIndex {
   int64_t min = 0, n = 0;
   bool ident = false;  // row r holds min + r
   BufPtr slot;         // int32 row of value min + k (null when ident)
+  // unique but not dense (sparse ids): an open-addressing table of 16-B slots
+  // (int64 key, int32 row, pad) — one 16-B load per probe, linear probing from
+  // fmix64(key) & (cap − 1), load ≤ 1/2.  `none`: the column has duplicate or
+  // unsupported values (cached too, so the check runs once per column).
+  bool hashed = false, none = false;
+  int64_t cap = 0;
+  BufPtr hslots;
 };
+
+constexpr int64_t HIDX_EMPTY = INT64_MIN;  // empty slot (a key equal to it: no index)
+
+struct HSlot {
+  int64_t key;
+  int32_t row, pad;
+};
+
+__global__ void k_hidx_clear(HSlot *t, int64_t cap) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (int64_t)gridDim.x * blockDim.x)
+    t[i] = HSlot{HIDX_EMPTY, -1, 0};
+}
+
+// flags: bit 0 = duplicate key, bit 1 = a key equal to the empty marker
+__global__ void k_hidx_insert(ColView c, int64_t n, HSlot *t, int64_t cap, int *flags) {
+  int f = 0;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    if (c.valid && !c.valid[r]) continue;  // NULL keys never match: not indexed
+    const int64_t k = ld_int(c, r);
+    if (k == HIDX_EMPTY) {
+      f |= 2;
+      continue;
+    }
+    uint64_t h = fmix64((uint64_t)k) & (uint64_t)(cap - 1);
+    for (;;) {
+      const unsigned long long prev = atomicCAS((unsigned long long *)&t[h].key,
+                                                (unsigned long long)HIDX_EMPTY, (unsigned long long)k);
+      if (prev == (unsigned long long)HIDX_EMPTY) {
+        t[h].row = (int32_t)r;
+        break;
+      }
+      if ((int64_t)prev == k) {
+        f |= 1;
+        break;
+      }
+      h = (h + 1) & (uint64_t)(cap - 1);
+    }
+  }
+  if (f) atomicOr(flags, f);
+}
 
 __global__ void k_dense_index(ColView c, int64_t n, int64_t mn, int32_t *slot, int *not_ident) {
   bool off = false;
@@ -50,17 +98,56 @@ __global__ void k_dense_index(ColView c, int64_t n, int64_t mn, int32_t *slot, i
   if (__ballot(off) && lane_id() == 0) atomicOr(not_ident, 1);
 }
 
-// The dense index of column c of a table of `nrows` rows, or nullptr when the
-// column is not a non-null dense unique INTEGER column.
+// The hashed index of a unique (non-dense) INTEGER column: built once and
+// cached on the column; nullptr (cached as `none`) when a value repeats.
+static std::shared_ptr<DenseIndex> hashed_index(Session *s, const ColPtr &c, int64_t nrows) {
+  auto di = std::make_shared<DenseIndex>();
+  int64_t cap = 1024;
+  while (cap < 2 * nrows) cap <<= 1;
+  BufPtr t = s->alloc(sizeof(HSlot) * cap), flag = s->alloc(4);
+  HIP_CHECK(hipMemsetAsync(flag->p, 0, 4, s->stream));
+  hipLaunchKernelGGL(k_hidx_clear, dim3(grid_for(cap, 256)), dim3(256), 0, s->stream, (HSlot *)t->p, cap);
+  KERNEL_CHECK();
+  hipLaunchKernelGGL(k_hidx_insert, dim3(grid_for(nrows, 256)), dim3(256), 0, s->stream, view_of(c), nrows,
+                     (HSlot *)t->p, cap, (int *)flag->p);
+  KERNEL_CHECK();
+  int nf = 0;
+  HIP_CHECK(hipMemcpyAsync(&nf, flag->p, 4, hipMemcpyDeviceToHost, s->stream));
+  s->sync();
+  if (nf) {
+    di->none = true;
+  } else {
+    di->hashed = true;
+    di->cap = cap;
+    di->n = nrows;
+    di->hslots = t;
+  }
+  return di;
+}
+
+// The index of column c of a table of `nrows` rows: direct-address when the
+// column is a non-null dense unique INTEGER column, hashed when it is unique
+// but sparse; nullptr when neither applies.
 static std::shared_ptr<DenseIndex> dense_index(Session *s, const ColPtr &c, int64_t nrows) {
   force(c);
   if (c->type != Type::Int64 || c->lazy || nrows == 0 || nrows >= (int64_t(1) << 31)) return nullptr;
   {
     std::lock_guard<std::mutex> lk(c->mu);
-    if (c->dense) return std::static_pointer_cast<DenseIndex>(c->dense);
+    if (c->dense) {
+      auto d = std::static_pointer_cast<DenseIndex>(c->dense);
+      return d->none ? nullptr : d;
+    }
   }
   const ColStats &st = column_stats(s, c);
-  if (!st.dense_unique || st.non_null != nrows) return nullptr;
+  if (!st.dense_unique || st.non_null != nrows) {
+    const char *hm = getenv("CAPF_HASH_INDEX");  // 0 (tuning): no hashed index
+    if ((hm && atoi(hm) == 0) || c->unique_flag == 0 || nrows > (int64_t(1) << 27)) return nullptr;
+    auto hi = hashed_index(s, c, nrows);
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->dense = hi;
+    c->unique_flag = hi->none ? 0 : 1;
+    return hi->none ? nullptr : hi;
+  }
   auto di = std::make_shared<DenseIndex>();
   di->min = st.min;
   di->n = nrows;
@@ -105,6 +192,41 @@ __global__ __launch_bounds__(256) void k_dense_probe(ColView key, int64_t n, int
   }
 }
 
+// Probe of the hashed index: one 16-B slot load per step of the linear probe.
+__global__ __launch_bounds__(256) void k_hidx_probe(ColView key, int64_t n, const HSlot *t, int64_t cap,
+                                                    int64_t *brow, unsigned long long *matched) {
+  __shared__ unsigned long long red[256 / WAVE];
+  unsigned long long cnt = 0;
+  const uint64_t mask = (uint64_t)(cap - 1);
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    int64_t b = -1;
+    if (!key.valid || key.valid[r]) {
+      const int64_t k = ld_int(key, r);
+      uint64_t h = fmix64((uint64_t)k) & mask;
+      for (;;) {
+        const HSlot e = t[h];
+        if (e.key == k) {
+          b = e.row;
+          break;
+        }
+        if (e.key == HIDX_EMPTY) break;
+        h = (h + 1) & mask;
+      }
+    }
+    brow[r] = b;
+    cnt += b >= 0 ? 1u : 0u;
+  }
+  cnt = wave_reduce_sum(cnt);
+  if (lane_id() == 0) red[threadIdx.x / WAVE] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long tt = 0;
+    for (int w = 0; w < 256 / WAVE; ++w) tt += red[w];
+    if (tt) atomicAdd(matched, tt);
+  }
+}
+
 __global__ void k_dense_flags(const int64_t *brow, int64_t n, uint8_t *flags) {
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
        r += (int64_t)gridDim.x * blockDim.x)
@@ -145,9 +267,12 @@ bool dense_join(Session *s, const Data &l, const Data &r, const std::vector<std:
   HIP_CHECK(hipMemsetAsync(acc->p, 0, 8, s->stream));
   if (n > 0) {
     const double kw = pk->enc == ENC_FOR24 ? 3.0 : pk->enc == ENC_FOR32 ? 4.0 : 8.0;
-    KernelTimer kt(s, "dense_probe", (kw + 8.0) * n);
+    KernelTimer kt(s, di->hashed ? "hash_probe" : "dense_probe", (kw + 8.0 + (di->hashed ? 16.0 : 0.0)) * n);
     const unsigned grid = grid_for(n, 256, (int64_t)s->num_cus * 8);
-    if (di->ident)
+    if (di->hashed)
+      hipLaunchKernelGGL(k_hidx_probe, dim3(grid), dim3(256), 0, s->stream, view_of(pk), n,
+                         (const HSlot *)di->hslots->p, di->cap, (int64_t *)brow->p, (unsigned long long *)acc->p);
+    else if (di->ident)
       hipLaunchKernelGGL(k_dense_probe<true>, dim3(grid), dim3(256), 0, s->stream, view_of(pk), n, di->min,
                          di->n, (const int32_t *)nullptr, (int64_t *)brow->p, (unsigned long long *)acc->p);
     else
@@ -163,7 +288,7 @@ bool dense_join(Session *s, const Data &l, const Data &r, const std::vector<std:
   // than the one readback they save.
   int64_t matched = 0;
   const std::optional<ColStats> &pst = pk->stats;
-  if (n > 0 && pst && pst->non_null == n && pst->min >= di->min && pst->max < di->min + di->n) {
+  if (n > 0 && !di->hashed && pst && pst->non_null == n && pst->min >= di->min && pst->max < di->min + di->n) {
     matched = n;
   } else {
     HIP_CHECK(hipMemcpyAsync(s->h_scalars, acc->p, 8, hipMemcpyDeviceToHost, s->stream));

@@ -25,16 +25,20 @@ def rmat_seed(scale):
 
 
 def rmat_graph(session, scale, edge_factor=16, seed=None, person_split=False, first=0, count=None,
-               node_base=0, n_nodes=None, compact=False):
+               node_base=0, n_nodes=None, compact=False, id_stride=1):
     """ScanGraph over an R-MAT edge table (optionally a shard [first, first+count)).
 
     compact=True stores the id columns FOR32-encoded (GpuTable.compact),
-    compact=3 FOR24 (3 B per id where the range fits 24 bits)."""
+    compact=3 FOR24 (3 B per id where the range fits 24 bits).  id_stride > 1
+    spreads the node ids to v·id_stride + 7 (rel source/target alike): a sparse
+    id domain with no dense range, so joins on node ids cannot address directly."""
     seed = rmat_seed(scale) if seed is None else seed
     m = edge_factor << scale
     count = m - first if count is None else count
     n = (1 << scale) if n_nodes is None else n_nodes
     rels = session.rmat_rels(scale, seed, thresholds(), first, count, id_base=0)
+    if id_stride != 1:
+        rels = _spread_ids(rels, ("source", "target"), id_stride)
     rels = compact_as(rels, compact)
     rel_tables = [ElementTable("rel", frozenset(["E"]), rels, {})]
     if person_split:
@@ -51,6 +55,18 @@ def rmat_graph(session, scale, edge_factor=16, seed=None, person_split=False, fi
                        ElementTable("node", frozenset(["Other"]), other, {})]
     else:
         nodes = session.range_nodes(node_base, n, id_col="id")
+        if id_stride != 1:
+            nodes = _spread_ids(nodes, ("id",), id_stride)
         nodes = compact_as(nodes, compact)
         node_tables = [ElementTable("node", frozenset(["V"]), nodes, {})]
     return ScanGraph(session, node_tables, rel_tables)
+
+
+def _spread_ids(table, cols, stride):
+    """The table with each of `cols` replaced by col·stride + 7 (materialised)."""
+    from .expr import Add, IntegerLit, Multiply
+    h = RecordHeader({Var(c): c for c in table.physicalColumns})
+    spread = table.withColumns(*[(Add(Multiply(Var(c), IntegerLit(stride)), IntegerLit(7)), "_s_" + c)
+                                 for c in cols], header=h)
+    keep = [(c, c) if c not in cols else ("_s_" + c, c) for c in table.physicalColumns]
+    return spread.select(*keep).cache()

@@ -101,3 +101,75 @@ def test_one_hop_rows_rmat(gpu_session, compact):
     src, dst = cmodel.rmat(12)
     assert sorted(zip(a.tolist(), b.tolist())) == sorted(zip(src.tolist(), dst.tolist()))
     assert gpu_session.profile()["dense_probe"]["launches"] == 2
+
+
+def _sparse_tables(n_nodes, n_rels, misses, nulls, dups, seed):
+    """Node ids spread over a sparse domain (v·1000003 − 2^40, negative ones
+    included: no dense range), shuffled; rel keys drawn from those ids (plus
+    absent ids when `misses`); `dups` repeats a node id (no unique index)."""
+    rng = np.random.default_rng(seed)
+    ids = rng.permutation(np.arange(n_nodes, dtype=np.int64) * 1000003 - (1 << 40))
+    if dups:
+        ids[7] = ids[8]
+    src = ids[rng.integers(0, n_nodes, n_rels)]
+    if misses:
+        src[::11] += 1  # not a node id
+    sv = None
+    if nulls:
+        sv = np.ones(n_rels, dtype=np.uint8)
+        sv[::13] = 0
+    nodes = [("id", T_INT, ids, None), ("name", T_STRING, [f"n{int(i) % 7}" for i in ids], None)]
+    rels = [("rid", T_INT, np.arange(n_rels, dtype=np.int64), None), ("src", T_INT, src, sv)]
+    return nodes, rels
+
+
+@pytest.mark.parametrize("jt", ["inner", "left_outer", "right_outer", "full_outer"])
+@pytest.mark.parametrize("index_left", [True, False], ids=["nodes_left", "nodes_right"])
+@pytest.mark.parametrize("misses,nulls", [(False, False), (True, True)], ids=["all_match", "misses_nulls"])
+@pytest.mark.parametrize("dups", [False, True], ids=["unique", "dup_key"])
+def test_hashed_index_join_parity(gpu_session, jt, index_left, misses, nulls, dups):
+    """Unique sparse node ids: the hashed unique-key index (one 16-B slot load
+    per probe) replaces the direct-address table; a repeated id disables it
+    (the radix / hash joins run) — the same bag as the oracle either way."""
+    nodes, rels = _sparse_tables(3000, 20000, misses, nulls, dups, seed=len(jt) * 5 + int(index_left))
+    gn, gr = gpu_session.table(nodes), gpu_session.table(rels)
+    on, orl = OracleSession().table(nodes), OracleSession().table(rels)
+    gpu_session.reset_profile()
+    gpu_session.set_profiling(True)
+    if index_left:
+        got = gn.join(gr, jt, ("id", "src")).rows
+        want = on.join(orl, jt, ("id", "src")).rows
+    else:
+        got = gr.join(gn, jt, ("src", "id")).rows
+        want = orl.join(on, jt, ("src", "id")).rows
+    gpu_session.set_profiling(False)
+    assert bag(got) == bag(want)
+    index_is_outer = jt == "full_outer" or (jt == "left_outer" and index_left) or \
+        (jt == "right_outer" and not index_left)
+    assert ("hash_probe" in gpu_session.profile()) == (not index_is_outer and not dups)
+    assert "dense_probe" not in gpu_session.profile()
+
+
+@pytest.mark.parametrize("compact", [False, True], ids=["int64", "for32"])
+def test_one_hop_rows_rmat_sparse_ids(gpu_session, compact):
+    """MATCH (a)-->(b) RETURN a, b on R-MAT s12 with node ids v·1000003 + 7:
+    both Expand joins probe the hashed index; (a, b) = the rel's endpoints."""
+    from oracle import cmodel
+    stride = 1000003
+    g = rmat_graph(gpu_session, 12, compact=compact, id_stride=stride)
+    q = Query([Match([NodeP("a"), NodeP("b")], [RelP("r", "a", "b")])],
+              [Stage([("a", Var("a", "NODE")), ("b", Var("b", "NODE"))])])
+    gpu_session.reset_profile()
+    gpu_session.set_profiling(True)
+    t = plan_query(g, q).table
+    cols = t.physicalColumns
+    cols = cols() if callable(cols) else cols
+    ka = next(c for c in cols if c.lstrip("_") == "a")
+    kb = next(c for c in cols if c.lstrip("_") == "b")
+    a, _ = t.column_arrays(ka)
+    b, _ = t.column_arrays(kb)
+    gpu_session.set_profiling(False)
+    src, dst = cmodel.rmat(12)
+    want = sorted(zip((src * stride + 7).tolist(), (dst * stride + 7).tolist()))
+    assert sorted(zip(a.tolist(), b.tolist())) == want
+    assert gpu_session.profile()["hash_probe"]["launches"] == 2

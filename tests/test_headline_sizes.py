@@ -102,3 +102,22 @@ def test_triangle_headline(gpu_session, scale):
     got = run(g, TRIANGLE)[0]["count"]
     assert gpu_session.last_plan() == "fused_triangle"
     assert got == TRI[str(scale)]
+
+
+def test_triangle_headline_eight_parts(gpu_session):
+    """Config 4 is quoted across 8 GPUs: the 8 row-chunk parts of the s24
+    triangle count (capf_triangle_count_part, what each rank computes before
+    the int64 all-reduce; computed one after the other on this GPU) sum to the
+    committed trace(A³) fixture."""
+    import torch
+    from capf_amd.table import triangle_count_part_async
+    scale, parts = 24, 8
+    t = gpu_session.rmat_rels(scale, rmat_seed(scale), thresholds(), 0, 16 << scale)
+    d = torch.full((parts,), -1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    for p in range(parts):
+        triangle_count_part_async(gpu_session, t, 0, 1 << scale, parts, p, d.data_ptr() + 8 * p)
+    gpu_session.sync()
+    got = d.cpu().tolist()
+    assert all(v >= 0 for v in got)
+    assert sum(got) == TRI["24"]

@@ -361,6 +361,164 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count(const uint32_t *rowptr,
   if (threadIdx.x == 0 && tot) atomicAdd(&acc[5], tot);
 }
 
+// ------------------------------------------------------------ packed count
+// Node ids < 2^24 (R-MAT s ≤ 24): the oriented CSR's column word carries the
+// pair's multiplicities in its top byte — f = #(p→q) in bits 24..27, b =
+// #(q→p) in bits 28..31, 15 = "look up vals" (rare multi-edges) — so a hit
+// needs no dependent global load: p→q from the batch table, q→w from the
+// streamed word itself, p→w from the LDS copy of N+(p).
+constexpr uint32_t TRI_M24 = 0xFFFFFFu;
+
+__global__ void k_tri_pack(const uint32_t *cols, const uint2 *vals, uint32_t P, uint32_t *pcols) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < P; i += gridDim.x * blockDim.x) {
+    const uint2 v = vals[i];
+    const uint32_t f = min(v.x, 15u), b = min(v.y, 15u);
+    pcols[i] = cols[i] | f << 24 | b << 28;
+  }
+}
+
+struct TriBatch2 {
+  uint32_t pre[WAVE + 1];  // exclusive prefix of the batch's |N+(q)|, + total
+  uint32_t qa[WAVE];       // N+(q) start in pcols
+  uint32_t pk[WAVE];       // packed word of q in N+(p) (multiplicities of p–q)
+  uint32_t kk[WAVE];       // k: q's position in N+(p)
+};
+
+// (f, b) of a packed word, or of vals[e] when a nibble says "look it up"
+__device__ inline uint2 tri_fb(uint32_t word, const uint2 *vals, uint32_t e) {
+  const uint32_t f = (word >> 24) & 15u, b = word >> 28;
+  return (f == 15u || b == 15u) ? vals[e] : make_uint2(f, b);
+}
+
+// One row p (packed words).  Positions of the flattened N+(q) sequence are
+// taken ILP·64 at a time and software-pipelined: the words of step i+1
+// (prefix search + global loads) are issued before step i's binary searches,
+// in ping-pong registers (no copy, so no early wait on the loads in flight).
+template <int ILP, class Q, class F>
+__device__ inline void tri_row_packed(uint32_t a, uint32_t dp, const uint32_t *rowptr, const uint32_t *pcols,
+                                      const uint2 *vals, TriBatch2 &tb, Q qs, F fnd,
+                                      unsigned long long &t, unsigned long long &probes,
+                                      unsigned long long &hits) {
+  const int lane = lane_id();
+  constexpr uint32_t STEP = ILP * WAVE;
+  for (uint32_t kb = 0; kb < dp; kb += WAVE) {
+    const uint32_t k = kb + lane;
+    uint32_t qa = 0, dq = 0, pk = 0;
+    if (k < dp) {
+      pk = qs(k);
+      const uint32_t q = pk & TRI_M24;
+      qa = rowptr[q];
+      dq = rowptr[q + 1] - qa;
+    }
+    const uint32_t inc = wave_inclusive_scan(dq);
+    tb.pre[lane] = inc - dq;
+    if (lane == WAVE - 1) tb.pre[WAVE] = inc;
+    tb.qa[lane] = qa;
+    tb.pk[lane] = pk;
+    tb.kk[lane] = k;
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl(inc, WAVE - 1, WAVE));
+    if (lane == 0) probes += total;
+    __builtin_amdgcn_wave_barrier();
+    uint32_t w[2][ILP], pos[2][ILP], bi[2][ILP];
+    auto issue = [&](uint32_t t0, uint32_t (&ww)[ILP], uint32_t (&pp)[ILP], uint32_t (&bb)[ILP]) {
+#pragma unroll
+      for (int u = 0; u < ILP; ++u) {
+        const uint32_t x = t0 + u * WAVE + lane;
+        const uint32_t xc = min(x, total - 1);
+        uint32_t b = 0;  // last batch entry with pre[b] <= xc
+#pragma unroll
+        for (int st = WAVE / 2; st > 0; st >>= 1)
+          if (tb.pre[b + st] <= xc) b += st;
+        bb[u] = b;
+        pp[u] = tb.qa[b] + (xc - tb.pre[b]);
+        ww[u] = pcols[pp[u]];
+        if (x >= total) ww[u] = 0xFFFFFFFFu;  // past the end (the load stays unconditional)
+      }
+    };
+    auto probe = [&](const uint32_t (&ww)[ILP], const uint32_t (&pp)[ILP], const uint32_t (&bb)[ILP]) {
+#pragma unroll
+      for (int u = 0; u < ILP; ++u) {
+        if (ww[u] == 0xFFFFFFFFu) continue;
+        const uint32_t wk = ww[u] & TRI_M24;
+        uint32_t lo = 0, n = dp;
+        while (n > 0) {
+          const uint32_t half = n >> 1;
+          if ((fnd(lo + half) & TRI_M24) < wk) {
+            lo += half + 1;
+            n -= half + 1;
+          } else {
+            n = half;
+          }
+        }
+        if (lo < dp) {
+          const uint32_t pw = fnd(lo);
+          if ((pw & TRI_M24) == wk) {
+            ++hits;
+            const uint2 a1 = tri_fb(tb.pk[bb[u]], vals, a + tb.kk[bb[u]]);  // p–q
+            const uint2 a2 = tri_fb(ww[u], vals, pp[u]);                     // q–w
+            const uint2 a3 = tri_fb(pw, vals, a + lo);                       // p–w
+            // p→q→w→p  +  p→w→q→p
+            t += (unsigned long long)a1.x * a2.x * a3.y + (unsigned long long)a3.x * a2.y * a1.y;
+          }
+        }
+      }
+    };
+    if (total > 0) issue(0, w[0], pos[0], bi[0]);
+    for (uint32_t t0 = 0; t0 < total; t0 += 2 * STEP) {
+      if (t0 + STEP < total) issue(t0 + STEP, w[1], pos[1], bi[1]);
+      probe(w[0], pos[0], bi[0]);
+      if (t0 + STEP >= total) break;
+      if (t0 + 2 * STEP < total) issue(t0 + 2 * STEP, w[0], pos[0], bi[0]);
+      probe(w[1], pos[1], bi[1]);
+    }
+    __builtin_amdgcn_wave_barrier();  // the table is rewritten by the next batch
+  }
+}
+
+template <int ILP>
+__global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_packed(const uint32_t *rowptr,
+                                                                 const uint32_t *pcols, const uint2 *vals,
+                                                                 uint64_t len, int parts, int part,
+                                                                 unsigned long long *cursor,
+                                                                 unsigned long long *acc) {
+  __shared__ uint32_t s_cols[TRI_BLOCK / WAVE][TRI_CAP];
+  __shared__ TriBatch2 s_tab[TRI_BLOCK / WAVE];
+  __shared__ unsigned long long lds[17];
+  const int wv = threadIdx.x / WAVE, lane = lane_id();
+  uint32_t *sc = s_cols[wv];
+  TriBatch2 &tb = s_tab[wv];
+  unsigned long long t = 0, probes = 0, hits = 0;
+  for (;;) {
+    unsigned long long r0 = 0;
+    if (lane == 0) r0 = atomicAdd(cursor, 1ull);
+    r0 = ((unsigned long long)__shfl((long long)r0, 0, WAVE) * parts + part) * TRI_CHUNK;
+    if (r0 >= len) break;
+    const uint64_t r1 = min<uint64_t>(r0 + TRI_CHUNK, len);
+    for (uint64_t p = r0; p < r1; ++p) {
+      const uint32_t a = rowptr[p], dp = rowptr[p + 1] - a;
+      if (dp < 2) continue;  // a triangle needs two out-neighbours at its lowest vertex
+      if (dp > TRI_CAP) {  // rare long row: searched in global memory
+        const uint32_t *row = pcols + a;
+        tri_row_packed<ILP>(a, dp, rowptr, pcols, vals, tb, [&](uint32_t k) { return row[k]; },
+                            [&](uint32_t x) { return row[x]; }, t, probes, hits);
+        continue;
+      }
+      for (uint32_t k = lane; k < dp; k += WAVE) sc[k] = pcols[a + k];
+      __builtin_amdgcn_wave_barrier();
+      tri_row_packed<ILP>(a, dp, rowptr, pcols, vals, tb, [&](uint32_t k) { return sc[k]; },
+                          [&](uint32_t x) { return sc[x]; }, t, probes, hits);
+      __builtin_amdgcn_wave_barrier();  // sc is rewritten by the next row
+    }
+  }
+  unsigned long long tot;
+  block_exclusive_scan(t, lds, tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(&acc[0], tot);
+  block_exclusive_scan(probes, lds, tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(&acc[4], tot);
+  block_exclusive_scan(hits, lds, tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(&acc[5], tot);
+}
+
 __global__ void k_tri_total(const unsigned long long *acc, int64_t *out) {
   if (threadIdx.x == 0) *out = (int64_t)(3ull * acc[0] + 3ull * acc[1] + acc[2]);
 }
@@ -378,6 +536,7 @@ struct TriGraph {
   // acc: [0] T, [1] Σ(L+L)·f·b, [2] Σ L(L−1)(L−2), [3] cursor, [4] probes (w ∈ N+(q)
   // looked up in N+(p)), [5] hits (closed triangles found)
   BufPtr rowptr, cols, vals, loops, acc;
+  BufPtr pcols;  // packed column words (node ids < 2^24), else null
   uint32_t P = 0;
   uint64_t len = 0;
 };
@@ -489,6 +648,12 @@ static void tri_build(Session *s, const ColView &src, const ColView &dst, int64_
                        (uint2 *)g.vals->p);
     KERNEL_CHECK();
   }
+  if (g.P > 0 && len <= (uint64_t)TRI_M24 + 1) {
+    g.pcols = s->alloc(4 * (int64_t)g.P);
+    hipLaunchKernelGGL(k_tri_pack, dim3(grid_for(g.P, 256, 256 * 64)), dim3(256), 0, s->stream,
+                       (const uint32_t *)g.cols->p, (const uint2 *)g.vals->p, g.P, (uint32_t *)g.pcols->p);
+    KERNEL_CHECK();
+  }
 }
 
 // Device count (int64 at d_out) of the directed triangle over rels (src, dst)
@@ -535,11 +700,20 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
     KernelTimer kt(s, "tri_count", 4.0 * g.P);
     static const bool filter = getenv("CAPF_TRI_FILTER") && atoi(getenv("CAPF_TRI_FILTER")) == 1;  // measured slower (0.98 vs 0.94 s at s24)
     static const int ilp = getenv("CAPF_TRI_ILP") ? atoi(getenv("CAPF_TRI_ILP")) : TRI_ILP;  // tuning
-    auto kern = filter ? (ilp >= 8 ? k_tri_count<true, 8> : ilp <= 2 ? k_tri_count<true, 2> : k_tri_count<true, 4>)
-                       : (ilp >= 8 ? k_tri_count<false, 8> : ilp <= 2 ? k_tri_count<false, 2> : k_tri_count<false, 4>);
-    hipLaunchKernelGGL(kern, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
-                       (const uint32_t *)g.rowptr->p, (const uint32_t *)g.cols->p,
-                       (const uint2 *)g.vals->p, len, parts, part, acc + 3, acc);
+    // CAPF_TRI_PACKED=0 (tuning): the unpacked kernel (multiplicities loaded from vals per hit)
+    const bool packed = !(getenv("CAPF_TRI_PACKED") && atoi(getenv("CAPF_TRI_PACKED")) == 0);
+    if (packed && g.pcols) {
+      auto kern = ilp >= 8 ? k_tri_count_packed<8> : ilp <= 2 ? k_tri_count_packed<2> : k_tri_count_packed<4>;
+      hipLaunchKernelGGL(kern, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
+                         (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
+                         (const uint2 *)g.vals->p, len, parts, part, acc + 3, acc);
+    } else {
+      auto kern = filter ? (ilp >= 8 ? k_tri_count<true, 8> : ilp <= 2 ? k_tri_count<true, 2> : k_tri_count<true, 4>)
+                         : (ilp >= 8 ? k_tri_count<false, 8> : ilp <= 2 ? k_tri_count<false, 2> : k_tri_count<false, 4>);
+      hipLaunchKernelGGL(kern, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
+                         (const uint32_t *)g.rowptr->p, (const uint32_t *)g.cols->p,
+                         (const uint2 *)g.vals->p, len, parts, part, acc + 3, acc);
+    }
     KERNEL_CHECK();
   }
   hipLaunchKernelGGL(k_tri_total, dim3(1), dim3(64), 0, s->stream, (const unsigned long long *)acc,

@@ -626,6 +626,33 @@ def test_triangle_self_loops_multi_edges(gpu_session):
     assert got == cmodel.count_triangle_brute(src[ok], dst[ok], n) == cmodel.count_triangle_formula(src, dst, n)
 
 
+@pytest.mark.parametrize("packed", ["1", "0"], ids=["packed", "unpacked"])
+def test_triangle_heavy_multi_edges(gpu_session, monkeypatch, packed):
+    """Pairs with 15+ parallel rels in either direction (the packed column
+    word's multiplicity nibbles saturate and the count reads vals), beside
+    pairs of 1-14; checked against brute force and trace(A^3)."""
+    from capf_amd.graph import ElementTable, ScanGraph as SG
+    from capf_amd.expr import T_INT
+    monkeypatch.setenv("CAPF_TRI_PACKED", packed)
+    rng = np.random.default_rng(5)
+    n = 40
+    e = []
+    for _ in range(120):
+        x, y = rng.integers(0, n, 2)
+        e += [(int(x), int(y))] * int(rng.choice([1, 2, 3, 14, 15, 16, 23]))
+    e += [(0, 1)] * 17 + [(1, 2)] * 15 + [(2, 0)] * 16 + [(1, 0)] * 19  # one heavy triangle both ways
+    src = np.array([x for x, _ in e], dtype=np.int64)
+    dst = np.array([y for _, y in e], dtype=np.int64)
+    rels = gpu_session.table([("id", T_INT, np.arange(len(e)), None), ("source", T_INT, src, None),
+                              ("target", T_INT, dst, None)])
+    nodes = gpu_session.range_nodes(0, n, id_col="id")
+    g = SG(gpu_session, [ElementTable("node", frozenset(["V"]), nodes, {})],
+           [ElementTable("rel", frozenset(["E"]), rels, {})])
+    got = run(g, _triangle_query())[0]["count"]
+    assert gpu_session.last_plan() == "fused_triangle"
+    assert got == cmodel.count_triangle_brute(src, dst, n) == cmodel.count_triangle_formula(src, dst, n)
+
+
 @pytest.mark.parametrize("parts", [1, 2, 3, 5])
 def test_triangle_partials_sum(gpu_session, parts):
     """capf_triangle_count_part: the parts (row chunks dealt round-robin, loop

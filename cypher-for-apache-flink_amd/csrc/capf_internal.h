@@ -138,6 +138,11 @@ struct Column {
   mutable int64_t bits_key[2] = {0, 0};
   mutable std::weak_ptr<Column> index_peer;
   mutable int64_t index_key[2] = {0, 0};
+  // provenance of a node-partitioned copy's key column (capf_table_node_partition):
+  // every value is a node of [owner[0], owner[0] + owner[1]) owned by part owner[3]
+  // of owner[2] — the sharded count then skips its range and ownership tests.
+  // owner[3] = −1: no such guarantee.  Kept by compaction (values unchanged).
+  int64_t owner[4] = {0, 0, 0, -1};
   bool is_all_null() const { return type == Type::Null; }
 };
 using ColPtr = std::shared_ptr<Column>;
@@ -426,7 +431,7 @@ BufPtr node_partition_diag_index(Session *s, const ColView &src, const ColView &
 // nhot / hot_ids: heavy-hitter node ids (a sampled plan hint; any ids are correct)
 bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out, int64_t lo,
                     int64_t n_nodes, int parts, int part, int64_t *d_partial, int64_t n_diag = -1,
-                    int nhot = 0, const int64_t *hot_ids = nullptr);
+                    int nhot = 0, const int64_t *hot_ids = nullptr, bool trusted = false);
 // Rows of `keys` (n rows) grouped by owner h(key tuple) of `parts` (shuffle.hip):
 // the permutation (int64 row indexes) and the row count per owner.
 BufPtr route_permutation(Session *s, const std::vector<ColView> &keys, int64_t n, int parts,

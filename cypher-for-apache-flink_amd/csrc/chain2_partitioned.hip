@@ -1481,7 +1481,11 @@ static int c5s_copies(int nr) {
   return c;
 }
 
-template <int W, bool WIDE, int TILE, bool HOT>
+// TR (trusted): both key columns are node-partitioned copies of this very
+// (range, parts, part) — every key is an owned node, so the ring path's keys
+// skip the 64-bit range test and the ownership test: run and key come from
+// the mixed index alone, key = ((run0 − b0·2^lsub + h >> (16 − lsub)) << 16) | (h & 0xFFFF).
+template <int W, bool WIDE, int TILE, bool HOT, bool TR = false>
 __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_c5_shard_partition(
     C5Shard c, uint16_t *part, uint32_t *meta, uint32_t *tile_acc, int64_t rstride) {
   constexpr int MAXR = C5S_MAXR;
@@ -1555,6 +1559,21 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
         const int64_t e = e0 + 4 * ((int64_t)g * C5_BLOCK + threadIdx.x);
         uint32_t x[4];
         bool okx[4];
+        if (TR && e + 4 <= e1) {
+          uint32_t q[4];
+          c5_decode<(W == 3 ? 3 : 4)>(raw[g & (D - 1)], (uint32_t)dlo, q);
+          if (g + D < GROUPS) issue(g + D);
+          const uint32_t run0t = run0 - ((uint32_t)c.b0 << lsub);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t h = node_mix_t<WIDE>(q[k], c.mix);
+            const uint32_t kk = ((run0t + (h >> ssh)) << C2_BITS) | (h & 0xFFFF);
+            key[4 * g + k] = HOT ? (h != c.hot[0] ? kk : dummy | 1u) : kk;
+            atomicAdd(&cur[(key[4 * g + k] >> C2_BITS) * C + my_copy], 1u);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          continue;
+        }
         if (e + 4 <= e1) {
           uint32_t q[4];
           c5_decode<(W == 3 ? 3 : 4)>(raw[g & (D - 1)], 0u, q);
@@ -2341,6 +2360,17 @@ static void c5_bal_post(Session *s, const uint16_t *part, const uint32_t *meta, 
   }
 }
 
+template <int TILE, bool TR>
+static auto c5s_kernel_t(int W, bool wide, bool hot) {
+  if (hot)
+    return W == 3 ? (wide ? k_c5_shard_partition<3, true, TILE, true, TR> : k_c5_shard_partition<3, false, TILE, true, TR>)
+           : W == 4 ? (wide ? k_c5_shard_partition<4, true, TILE, true, TR> : k_c5_shard_partition<4, false, TILE, true, TR>)
+                    : (wide ? k_c5_shard_partition<8, true, TILE, true, TR> : k_c5_shard_partition<8, false, TILE, true, TR>);
+  return W == 3 ? (wide ? k_c5_shard_partition<3, true, TILE, false, TR> : k_c5_shard_partition<3, false, TILE, false, TR>)
+         : W == 4 ? (wide ? k_c5_shard_partition<4, true, TILE, false, TR> : k_c5_shard_partition<4, false, TILE, false, TR>)
+                  : (wide ? k_c5_shard_partition<8, true, TILE, false, TR> : k_c5_shard_partition<8, false, TILE, false, TR>);
+}
+
 template <int TILE>
 static auto c5s_kernel(int W, bool wide, bool hot) {
   if (hot)  // a heavy-hitter hint: one more compare per key (only ranks that hold a hub pay it)
@@ -2438,7 +2468,7 @@ uint8_t *node_owner_flags(Session *s, const ColView &key, int64_t n, int64_t lo,
 // FOR32, 16-B aligned, non-null.  Histograms live in session scratch.
 bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out, int64_t lo,
                     int64_t n_nodes, int parts, int part, int64_t *d_partial, int64_t n_diag,
-                    int nhot, const int64_t *hot_ids) {
+                    int nhot, const int64_t *hot_ids, bool trusted) {
   const int kbits = chain2_hist_bits(n_nodes);
   int b0, nbl;
   owned_buckets(kbits, parts, part, &b0, &nbl);
@@ -2538,8 +2568,12 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
       BufPtr meta = s->alloc(4 * nr * ntiles);
       {
         KernelTimer kt(s, "c5_partition", (double)W * (n_in + 2 * n_out));
-        auto kern = tile == C5S_TILE ? c5s_kernel<C5S_TILE>(W, kbits > 24, nh > 0)
-                                     : c5s_kernel<16384>(W, kbits > 24, nh > 0);
+        // the trusted ring only where the ring runs (FOR24 / FOR32 columns)
+        const bool tr = trusted && W != 8 && c.upf;
+        auto kern = tile == C5S_TILE ? (tr ? c5s_kernel_t<C5S_TILE, true>(W, kbits > 24, nh > 0)
+                                           : c5s_kernel<C5S_TILE>(W, kbits > 24, nh > 0))
+                                     : (tr ? c5s_kernel_t<16384, true>(W, kbits > 24, nh > 0)
+                                           : c5s_kernel<16384>(W, kbits > 24, nh > 0));
         hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(C5_BLOCK), 0, s->stream, c,
                            (uint16_t *)partb->p, (uint32_t *)meta->p, tile_acc, rstride);
         KERNEL_CHECK();

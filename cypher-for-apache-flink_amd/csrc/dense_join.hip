@@ -267,7 +267,7 @@ bool dense_join(Session *s, const Data &l, const Data &r, const std::vector<std:
   HIP_CHECK(hipMemsetAsync(acc->p, 0, 8, s->stream));
   if (n > 0) {
     const double kw = pk->enc == ENC_FOR24 ? 3.0 : pk->enc == ENC_FOR32 ? 4.0 : 8.0;
-    KernelTimer kt(s, di->hashed ? "hash_probe" : "dense_probe", (kw + 8.0 + (di->hashed ? 16.0 : 0.0)) * n);
+    KernelTimer kt(s, di->hashed ? "hidx_probe" : "dense_probe", (kw + 8.0 + (di->hashed ? 16.0 : 0.0)) * n);
     const unsigned grid = grid_for(n, 256, (int64_t)s->num_cus * 8);
     if (di->hashed)
       hipLaunchKernelGGL(k_hidx_probe, dim3(grid), dim3(256), 0, s->stream, view_of(pk), n,

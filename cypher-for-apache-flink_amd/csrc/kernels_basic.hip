@@ -509,6 +509,7 @@ ColPtr encode_column(Session *s, const ColPtr &c, int width) {
                        st.min, (uint32_t *)o->data->p, c->n);
     KERNEL_CHECK();
     o->stats = st;
+    std::copy(c->owner, c->owner + 4, o->owner);
     return o;
   }
   auto o = std::make_shared<Column>();
@@ -523,6 +524,7 @@ ColPtr encode_column(Session *s, const ColPtr &c, int width) {
                      st.min, (uint32_t *)o->data->p, c->n);
   KERNEL_CHECK();
   o->stats = st;  // the values are unchanged
+  std::copy(c->owner, c->owner + 4, o->owner);
   return o;
 }
 

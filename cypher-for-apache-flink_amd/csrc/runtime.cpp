@@ -859,6 +859,16 @@ capf_status capf_table_compact_width(capf_table *t, int32_t width, capf_table **
   CAPF_API_END
 }
 
+// The key column of a node-partitioned copy: a fresh (unshared) column gets the
+// owner tag; a shared one (an identity gather handed back as is) does not.
+static void tag_owner(ColPtr &c, int64_t lo, int64_t n_nodes, int parts, int part) {
+  if (c.use_count() != 1 || c->lazy) return;
+  c->owner[0] = lo;
+  c->owner[1] = n_nodes;
+  c->owner[2] = parts;
+  c->owner[3] = part;
+}
+
 capf_status capf_table_node_partition(capf_table *t, const char *key_col, int64_t node_base,
                                       int64_t n_nodes, int32_t parts, int32_t part,
                                       capf_table **out) {
@@ -886,6 +896,7 @@ capf_status capf_table_node_partition(capf_table *t, const char *key_col, int64_
   e->nrows = m;
   for (const ColPtr &c : d->cols)
     e->cols.push_back(gather_column(s, decode_column(s, c), (const int64_t *)idx->p, m));
+  tag_owner(e->cols[ki], node_base, n_nodes, parts, part);
   s->sync();
   n->result = e;
   *out = wrap(n);
@@ -922,6 +933,7 @@ capf_status capf_table_node_partition_diag(capf_table *t, const char *src_col, c
   e->nrows = m;
   for (const ColPtr &c : d->cols)
     e->cols.push_back(gather_column(s, decode_column(s, c), (const int64_t *)idx->p, m));
+  tag_owner(e->cols[si], node_base, n_nodes, parts, part);
   s->sync();
   n->result = e;
   *out = wrap(n);

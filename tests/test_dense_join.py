@@ -146,7 +146,7 @@ def test_hashed_index_join_parity(gpu_session, jt, index_left, misses, nulls, du
     assert bag(got) == bag(want)
     index_is_outer = jt == "full_outer" or (jt == "left_outer" and index_left) or \
         (jt == "right_outer" and not index_left)
-    assert ("hash_probe" in gpu_session.profile()) == (not index_is_outer and not dups)
+    assert ("hidx_probe" in gpu_session.profile()) == (not index_is_outer and not dups)
     assert "dense_probe" not in gpu_session.profile()
 
 
@@ -172,4 +172,4 @@ def test_one_hop_rows_rmat_sparse_ids(gpu_session, compact):
     src, dst = cmodel.rmat(12)
     want = sorted(zip((src * stride + 7).tolist(), (dst * stride + 7).tolist()))
     assert sorted(zip(a.tolist(), b.tolist())) == want
-    assert gpu_session.profile()["hash_probe"]["launches"] == 2
+    assert gpu_session.profile()["hidx_probe"]["launches"] == 2

@@ -145,6 +145,12 @@ _SIGS = {
     "capf_table_hash_route": (c_int32, [_T, c_int32, _STRS, c_int32, POINTER(c_int64), _PT]),
     "capf_table_download_device": (c_int32, [_T, c_char_p, c_void_p, c_void_p]),
     "capf_table_has_nulls": (c_int32, [_T, c_char_p, POINTER(c_int32)]),
+    "capf_table_column_range": (c_int32, [_T, c_char_p, POINTER(c_int64), POINTER(c_int64), POINTER(c_int64)]),
+    "capf_table_pack_rows": (c_int32, [_T, c_int32, POINTER(c_char_p), POINTER(c_int32), POINTER(c_int64),
+                                       POINTER(c_int32), POINTER(c_int32), c_void_p]),
+    "capf_table_from_packed_rows": (c_int32, [_S, c_int32, POINTER(c_char_p), POINTER(c_int32), POINTER(c_int32),
+                                              POINTER(c_int64), POINTER(c_int32), c_void_p, c_int64,
+                                              POINTER(_T)]),
     "capf_dot_u32": (c_int32, [_S, c_void_p, c_void_p, c_int64, POINTER(c_uint64)]),
 }
 

@@ -432,6 +432,12 @@ BufPtr node_partition_diag_index(Session *s, const ColView &src, const ColView &
 bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out, int64_t lo,
                     int64_t n_nodes, int parts, int part, int64_t *d_partial, int64_t n_diag = -1,
                     int nhot = 0, const int64_t *hot_ids = nullptr, bool trusted = false);
+// Exchange wire format (shuffle.hip): cols packed row-major, `width` bytes of
+// (value − base) per column + a validity byte where nullable; *W = row bytes.
+void pack_rows(Session *s, const std::vector<ColPtr> &cols, const int32_t *width, const int64_t *base,
+               const int32_t *nullable, int64_t n, int *W, void *d_out);
+ColPtr unpack_column(Session *s, const void *rows, int64_t n, int W, int off, int width, int voff, int64_t base,
+                     Type t);
 // Rows of `keys` (n rows) grouped by owner h(key tuple) of `parts` (shuffle.hip):
 // the permutation (int64 row indexes) and the row count per owner.
 BufPtr route_permutation(Session *s, const std::vector<ColView> &keys, int64_t n, int parts,

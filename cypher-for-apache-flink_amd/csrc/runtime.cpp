@@ -1005,6 +1005,108 @@ capf_status capf_table_download_device(capf_table *t, const char *col, void *d_v
   CAPF_API_END
 }
 
+capf_status capf_table_column_range(capf_table *t, const char *col, int64_t *mn, int64_t *mx,
+                                    int64_t *non_null) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(col, "col");
+  need(mn, "min");
+  need(mx, "max");
+  need(non_null, "non_null");
+  int i = t->node->col_index_or_throw(col);
+  if (t->node->types[i] != Type::Int64 && t->node->types[i] != Type::String)
+    illegal("column range: INTEGER or STRING columns only");
+  DataPtr d = materialize(t->node);
+  force(d->cols[i]);
+  const ColStats &st = column_stats(t->node->s, d->cols[i]);
+  *mn = st.min;
+  *mx = st.max;
+  *non_null = st.non_null;
+  CAPF_API_END
+}
+
+static void check_wire(Type t, int32_t width, int64_t base) {
+  const bool ok = t == Type::Null     ? width == 0
+                  : t == Type::Bool   ? width == 1
+                  : t == Type::Float64 ? width == 8 && base == 0
+                  : (t == Type::Int64 || t == Type::String) ? (width == 3 || width == 4 || (width == 8 && base == 0))
+                                                           : false;
+  if (!ok) illegal(std::string("packed rows: width ") + std::to_string(width) + " does not fit a " + type_name(t) +
+                   " column");
+}
+
+capf_status capf_table_pack_rows(capf_table *t, int32_t ncols, const char *const *cols, const int32_t *width,
+                                 const int64_t *base, const int32_t *nullable, int32_t *row_bytes, void *d_out) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(row_bytes, "row_bytes");
+  if (ncols < 0) illegal("negative column count");
+  if (ncols > 0) {
+    need(cols, "cols");
+    need(width, "width");
+    need(base, "base");
+    need(nullable, "nullable");
+  }
+  DataPtr d = materialize(t->node);
+  Session *s = t->node->s;
+  std::vector<ColPtr> cs;
+  for (int j = 0; j < ncols; ++j) {
+    need(cols[j], "col");
+    const int i = t->node->col_index_or_throw(cols[j]);
+    check_wire(t->node->types[i], width[j], base[j]);
+    force(d->cols[i]);
+    if (!nullable[j] && d->cols[i]->valid) illegal("packed rows: a column with NULLs needs its validity byte");
+    cs.push_back(d->cols[i]);
+  }
+  int W = 0;
+  pack_rows(s, cs, width, base, nullable, d->nrows, &W, d_out);
+  *row_bytes = W;
+  CAPF_API_END
+}
+
+capf_status capf_table_from_packed_rows(capf_session *cs, int32_t ncols, const char *const *names,
+                                        const int32_t *types, const int32_t *width, const int64_t *base,
+                                        const int32_t *nullable, const void *d_rows, int64_t nrows,
+                                        capf_table **out) {
+  CAPF_API_BEGIN
+  need(cs, "session");
+  need(out, "out");
+  if (ncols < 0 || nrows < 0) illegal("negative size");
+  if (ncols > 0) {
+    need(names, "names");
+    need(types, "types");
+    need(width, "width");
+    need(base, "base");
+    need(nullable, "nullable");
+  }
+  Session *s = &cs->impl;
+  int W = 0;
+  std::vector<int> off(ncols), voff(ncols);
+  std::vector<std::string> nm;
+  for (int j = 0; j < ncols; ++j) {
+    need(names[j], "name");
+    nm.emplace_back(names[j]);
+    check_wire((Type)types[j], width[j], base[j]);
+    off[j] = W;
+    W += width[j];
+    voff[j] = nullable[j] ? W++ : -1;
+  }
+  check_unique_names(nm);
+  if (nrows > 0 && W > 0) need(d_rows, "rows");
+  auto n = new_node(s, Kind::Source);
+  auto e = std::make_shared<Data>();
+  e->nrows = nrows;
+  for (int j = 0; j < ncols; ++j) {
+    n->names.push_back(nm[j]);
+    n->types.push_back((Type)types[j]);
+    e->cols.push_back(unpack_column(s, d_rows, nrows, W, off[j], width[j], voff[j], base[j], (Type)types[j]));
+  }
+  s->sync();
+  n->result = e;
+  *out = wrap(n);
+  CAPF_API_END
+}
+
 capf_status capf_table_has_nulls(capf_table *t, const char *col, int32_t *has) {
   CAPF_API_BEGIN
   need(t, "table");

@@ -141,4 +141,96 @@ BufPtr route_permutation(Session *s, const std::vector<ColView> &keys, int64_t n
   return perm;
 }
 
+// ------------------------------------------------------------ row packing
+// The exchange's wire format (dist_table.py GpuExchange.send): each row is W
+// bytes, row-major — per column `width` bytes of (value − base) little-endian
+// (width 3 / 4 for INTEGER / STRING-code columns whose range over ALL ranks
+// fits 24 / 32 bits, the FOR24 / FOR32 encodings; 8 otherwise and for floats;
+// 1 for BOOL), then one validity byte when the column is nullable on some
+// rank.  One all_to_all_single moves the packed rows; the receiver's columns
+// keep the narrow encodings (no re-encode).  One thread per row, the row
+// assembled in registers and written as whole dwords when W is a multiple of 4.
+struct PackCol {
+  ColView v;
+  int32_t width, off, voff;  // voff < 0: no validity byte
+  int64_t base;
+};
+
+__device__ inline uint64_t pack_value(const PackCol &c, int64_t r, bool valid) {
+  if (!valid || c.v.type == CAPF_TYPE_NULL) return 0;
+  if (c.v.type == CAPF_TYPE_BOOL) return ((const uint8_t *)c.v.data)[r] ? 1u : 0u;
+  if (c.v.type == CAPF_TYPE_FLOAT64) return ((const uint64_t *)c.v.data)[r];
+  return (uint64_t)(ld_int(c.v, r) - c.base);
+}
+
+__global__ void k_pack_rows(const PackCol *cols, int nc, int W, int64_t n, uint8_t *out) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    uint8_t *row = out + r * W;
+    for (int j = 0; j < nc; ++j) {
+      const PackCol c = cols[j];
+      const bool valid = !c.v.valid || c.v.valid[r];
+      const uint64_t x = pack_value(c, r, valid);
+      for (int b = 0; b < c.width; ++b) row[c.off + b] = (uint8_t)(x >> (8 * b));
+      if (c.voff >= 0) row[c.voff] = valid ? 1 : 0;
+    }
+  }
+}
+
+// One column out of packed rows: width 3 → FOR24 buffer, 4 → FOR32 words,
+// 8 → int64 / float64 bits, 1 → bool bytes; validity bytes when voff ≥ 0.
+__global__ void k_unpack_col(const uint8_t *rows, int64_t n, int W, int off, int width, int voff,
+                             uint8_t *data, uint8_t *valid) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t *row = rows + r * W;
+    for (int b = 0; b < width; ++b) data[r * width + b] = row[off + b];
+    if (voff >= 0) valid[r] = row[voff];
+  }
+}
+
+void pack_rows(Session *s, const std::vector<ColPtr> &cols, const int32_t *width, const int64_t *base,
+               const int32_t *nullable, int64_t n, int *W_out, void *d_out) {
+  std::vector<PackCol> pc(cols.size());
+  int W = 0;
+  for (size_t j = 0; j < cols.size(); ++j) {
+    pc[j].v = view_of(cols[j]);
+    pc[j].width = width[j];
+    pc[j].off = W;
+    pc[j].base = base[j];
+    W += width[j];
+    pc[j].voff = nullable[j] ? W++ : -1;
+  }
+  *W_out = W;
+  if (!d_out || n == 0 || W == 0) return;
+  BufPtr dc = s->alloc(sizeof(PackCol) * std::max<size_t>(pc.size(), 1));
+  HIP_CHECK(hipMemcpyAsync(dc->p, pc.data(), sizeof(PackCol) * pc.size(), hipMemcpyHostToDevice, s->stream));
+  {
+    KernelTimer kt(s, "pack_rows", (double)W * n);
+    hipLaunchKernelGGL(k_pack_rows, dim3(grid_for(n, 256)), dim3(256), 0, s->stream, (const PackCol *)dc->p,
+                       (int)pc.size(), W, n, (uint8_t *)d_out);
+    KERNEL_CHECK();
+  }
+  s->sync();  // the host copy of the column table is released on return
+}
+
+ColPtr unpack_column(Session *s, const void *rows, int64_t n, int W, int off, int width, int voff, int64_t base,
+                     Type t) {
+  auto c = std::make_shared<Column>();
+  c->type = t;
+  c->n = n;
+  if (t == Type::Null) return c;
+  c->enc = width == 3 ? ENC_FOR24 : width == 4 ? ENC_FOR32 : ENC_PLAIN;
+  c->base = width == 3 || width == 4 ? base : 0;
+  // FOR24 buffers carry 16 zero bytes past 3·n (4-B / 12-B loads at any row)
+  const int64_t bytes = (int64_t)width * n + (width == 3 ? 16 : 0);
+  c->data = s->alloc(std::max<int64_t>(bytes, 16));
+  if (width == 3) HIP_CHECK(hipMemsetAsync((uint8_t *)c->data->p + 3 * n, 0, 16, s->stream));
+  if (voff >= 0) c->valid = s->alloc(std::max<int64_t>(n, 1));
+  if (n > 0) {
+    hipLaunchKernelGGL(k_unpack_col, dim3(grid_for(n, 256)), dim3(256), 0, s->stream, (const uint8_t *)rows, n,
+                       W, off, width, voff, (uint8_t *)c->data->p, voff >= 0 ? (uint8_t *)c->valid->p : nullptr);
+    KERNEL_CHECK();
+  }
+  return c;
+}
+
 }  // namespace capf

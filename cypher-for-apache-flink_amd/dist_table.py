@@ -50,7 +50,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
-from .expr import (AGG_AVG, AGG_COUNT, AGG_COUNT_STAR, AGG_MAX, AGG_MIN, AGG_SUM, T_BOOL, T_NULL, T_STRING, Count,
+from .expr import (AGG_AVG, AGG_COUNT, AGG_COUNT_STAR, AGG_MAX, AGG_MIN, AGG_SUM, T_BOOL, T_INT, T_NULL, T_STRING, Count,
                    Divide, Max, Min, Sum, Var)
 from .header import RecordHeader
 
@@ -113,54 +113,90 @@ class GpuExchange:
     def replicate(self, table):
         return self.send(table, [table.size] * self.world, repeat=True)
 
+    def all_max_i64(self, vals):
+        t = torch.tensor(list(vals) or [0], dtype=torch.int64, device="cpu" if self.staged else self.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return t.tolist()[:len(vals)]
+
     def _layout(self, table):
+        """One wire layout on every rank (capf_table_pack_rows): per column the
+        width of (value − base) — FOR24 / FOR32 where the value range over ALL
+        ranks fits 24 / 32 bits, 8 B otherwise — and whether it carries a
+        validity byte.  Everything is agreed in ONE int64 MAX all-reduce: the
+        local NULL flags, −min and max of every INTEGER / STRING column, and
+        (STRING columns travel as dictionary codes) the dictionary size and
+        digest with their negations (min == max on every rank)."""
         cols = table.physicalColumns
         types = [table.capf_type(c) for c in cols]
         if any(t not in (0, 1, 2, 3, 4) for t in types):
             raise _lib.NotImplementedException("LIST columns are not moved between ranks")
-        has = []
-        for c in cols:
+        k = len(cols)
+        has, lo, hi = [], [], []
+        big = (1 << 63) - 1
+        for c, t in zip(cols, types):
             v = c_int32()
             _lib.call("capf_table_has_nulls", table._h, c.encode(), byref(v))
             has.append(v.value)
-        # STRING columns travel as dictionary codes: every rank's dictionary must
-        # be the same (size and digest, code order).  Their 16-bit pieces and
-        # negations ride in the same MAX all-reduce: min == max on every piece.
+            if t in (T_INT, T_STRING):
+                mn, mx, nn = c_int64(), c_int64(), c_int64()
+                _lib.call("capf_table_column_range", table._h, c.encode(), byref(mn), byref(mx), byref(nn))
+                lo.append(-mn.value if nn.value else -big)
+                hi.append(mx.value if nn.value else -big)
+            else:
+                lo.append(-big)
+                hi.append(-big)
         check = []
         if T_STRING in types:
             cnt, dig = c_int64(), c_uint64()
             _lib.call("capf_string_digest", self.s._h, byref(cnt), byref(dig))
-            pieces = [(cnt.value >> k) & 0xFFFF for k in (0, 16, 32)] + \
-                [(dig.value >> k) & 0xFFFF for k in (0, 16, 32, 48)]
-            check = [v for x in pieces for v in (x, -x)]
-        got = self.all_max_vec(has + check)
-        if check and any(got[len(has) + i] != -got[len(has) + i + 1] for i in range(0, len(check), 2)):
-            raise _lib.IllegalStateException(
-                "string dictionaries differ between ranks: STRING columns cannot be exchanged as codes")
-        # one layout on every rank; an all-NULL column is rebuilt from its type alone
-        nullable = [bool(x) and t != T_NULL for x, t in zip(got[:len(has)], types)]
-        width = [0 if t == T_NULL else (1 if t == T_BOOL else 8) for t in types]
-        return cols, types, width, nullable
+            d = dig.value - (1 << 64) if dig.value >= (1 << 63) else dig.value
+            check = [cnt.value, -cnt.value, d, -d if d != -(1 << 63) else big]
+        got = self.all_max_i64(has + lo + hi + check)
+        if check:
+            c0 = 3 * k
+            if got[c0] != -got[c0 + 1] or (got[c0 + 2] != -got[c0 + 3] and check[2] != -(1 << 63)):
+                raise _lib.IllegalStateException(
+                    "string dictionaries differ between ranks: STRING columns cannot be exchanged as codes")
+        # an all-NULL column is rebuilt from its type alone
+        nullable = [bool(x) and t != T_NULL for x, t in zip(got[:k], types)]
+        width, base = [], []
+        for j, t in enumerate(types):
+            if t == T_NULL:
+                width.append(0), base.append(0)
+            elif t == T_BOOL:
+                width.append(1), base.append(0)
+            elif t in (T_INT, T_STRING):
+                gmin, gmax = -got[k + j], got[2 * k + j]
+                if gmax < gmin:  # no value anywhere
+                    width.append(3), base.append(0)
+                elif gmax - gmin < (1 << 24):
+                    width.append(3), base.append(gmin)
+                elif gmax - gmin < (1 << 32):
+                    width.append(4), base.append(gmin)
+                else:
+                    width.append(8), base.append(0)
+            else:
+                width.append(8), base.append(0)
+        return cols, types, width, base, nullable
 
     def send(self, table, counts, repeat=False):
         """Rows [off_p, off_p + counts[p]) of `table` go to rank p (every row
         to every rank when repeat); returns the rows this rank receives, in
-        sender order."""
-        cols, types, width, nullable = self._layout(table)
+        sender order.  Rows are packed on the GPU in the narrow wire layout
+        (capf_table_pack_rows) and moved by one all_to_all_single."""
+        cols, types, width, base, nullable = self._layout(table)
         n = table.size
-        dev = "cpu" if self.staged else self.dev
-        pieces = []
-        for c, w, nl in zip(cols, width, nullable):
-            if w:
-                buf = torch.empty(max(n * w, 1), dtype=torch.uint8, device=self.dev)
-                _lib.call("capf_table_download_device", table._h, c.encode(), c_void_p(buf.data_ptr()), None)
-                pieces.append(buf[:n * w].view(n, w))
-            if nl:
-                v = torch.empty(max(n, 1), dtype=torch.uint8, device=self.dev)
-                _lib.call("capf_table_download_device", table._h, c.encode(), None, c_void_p(v.data_ptr()))
-                pieces.append(v[:n].view(n, 1))
+        k = len(cols)
+        arrs = (_lib.strs(cols), (c_int32 * max(k, 1))(*width), (c_int64 * max(k, 1))(*base),
+                (c_int32 * max(k, 1))(*[int(x) for x in nullable]))
         W = sum(width) + sum(nullable)
-        rows = torch.cat(pieces, dim=1) if pieces else torch.empty((n, 0), dtype=torch.uint8, device=self.dev)
+        dev = "cpu" if self.staged else self.dev
+        rows = torch.empty(max(n * W, 1), dtype=torch.uint8, device=self.dev)
+        wb = c_int32()
+        torch.cuda.current_stream().synchronize()
+        _lib.call("capf_table_pack_rows", table._h, k, *arrs, byref(wb), c_void_p(rows.data_ptr()))
+        assert wb.value == W, (wb.value, W)
+        rows = rows[:n * W].view(n, W)
         if repeat:
             rows = rows.repeat(self.world, 1)
         send_counts = torch.tensor(counts, dtype=torch.int64, device=dev)
@@ -168,40 +204,17 @@ class GpuExchange:
         dist.all_to_all_single(recv_counts, send_counts, group=self.group)
         rc = recv_counts.tolist()
         m = sum(rc)
+        out = torch.empty((max(m, 1), W), dtype=torch.uint8, device=dev)[:m]
         if W > 0:
             src = rows.to(dev) if self.staged else rows
-            out = torch.empty((m, W), dtype=torch.uint8, device=dev)
             dist.all_to_all_single(out, src, rc, list(counts), group=self.group)
-        else:
-            out = torch.empty((m, 0), dtype=torch.uint8, device=dev)
-        return self._build(cols, types, width, nullable, out, m)
-
-    def _build(self, cols, types, width, nullable, out, m):
-        datas, valids, keep = [], [], []
-        a = 0
-        for w, nl in zip(width, nullable):
-            d = v = None
-            if w:
-                d = out[:, a:a + w].contiguous()
-                a += w
-            if nl:
-                v = out[:, a:a + 1].contiguous()
-                a += 1
-            keep += [d, v]
-            datas.append(d.data_ptr() if d is not None and m > 0 else None)
-            valids.append(v.data_ptr() if v is not None and m > 0 else None)
-        if not self.staged:
-            torch.cuda.current_stream().synchronize()
-        k = len(cols)
+        if self.staged:
+            out = out.to(self.dev)
+        torch.cuda.current_stream().synchronize()
         h = c_void_p()
         ty = (c_int32 * max(k, 1))(*types)
-        dp = (c_void_p * max(k, 1))(*datas)
-        vp = (c_void_p * max(k, 1))(*valids)
-        if self.staged:
-            _lib.call("capf_table_from_host", self.s._h, k, _lib.strs(cols), ty, dp, vp, m, byref(h))
-        else:
-            _lib.call("capf_table_from_device", self.s._h, k, _lib.strs(cols), ty, dp, vp, m, 1, byref(h))
-        self.s.sync()  # the copies are done before the torch buffers go
+        _lib.call("capf_table_from_packed_rows", self.s._h, k, arrs[0], ty, arrs[1], arrs[2], arrs[3],
+                  c_void_p(out.data_ptr() if m > 0 and W > 0 else 0), m, byref(h))
         from .table import GpuTable
         return GpuTable(self.s, h)
 

@@ -453,6 +453,26 @@ capf_status capf_table_download_device(capf_table *t, const char *col, void *d_v
                                        uint8_t *d_valid);
 capf_status capf_table_has_nulls(capf_table *t, const char *col, int32_t *has);
 
+/* Exchange wire format of the distributed Table layer (dist_table.py: one
+ * all_to_all_single per shuffle, Flink's hash repartition in FlinkTable.scala:
+ * 123-196).  A row is packed as, per column i: width[i] bytes of
+ * (value − base[i]) little-endian — 3 / 4 for INTEGER / STRING columns whose
+ * range over every rank fits 24 / 32 bits (FOR24 / FOR32), 8 otherwise and for
+ * FLOAT (base 0), 1 for BOOL, 0 for NULL — then one validity byte when
+ * nullable[i].  capf_table_column_range: min / max / non-NULL count of an
+ * INTEGER or STRING column (column statistics, computed once).
+ * capf_table_pack_rows: *row_bytes = W; rows into d_out (n·W device bytes; null
+ * d_out: only W).  capf_table_from_packed_rows: the table of nrows packed rows
+ * at d_rows (copied out; the narrow widths stay FOR24 / FOR32 encoded).       */
+capf_status capf_table_column_range(capf_table *t, const char *col, int64_t *min, int64_t *max,
+                                    int64_t *non_null);
+capf_status capf_table_pack_rows(capf_table *t, int32_t ncols, const char *const *cols, const int32_t *width,
+                                 const int64_t *base, const int32_t *nullable, int32_t *row_bytes, void *d_out);
+capf_status capf_table_from_packed_rows(capf_session *s, int32_t ncols, const char *const *names,
+                                        const int32_t *types, const int32_t *width, const int64_t *base,
+                                        const int32_t *nullable, const void *d_rows, int64_t nrows,
+                                        capf_table **out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -615,6 +615,36 @@ JNI(jlong, tableHashRoute)(JNIEnv *env, jobject, jlong t, jobjectArray keys, jin
   env->SetLongArrayRegion(countsOut, 0, parts, v.data());
   return H(out);
 }
+// exchange wire format (dist_table.py): out = {min, max, non_null}
+JNI(void, tableColumnRange)(JNIEnv *env, jobject, jlong t, jstring col, jlongArray out) {
+  JStr c(env, col);
+  int64_t mn = 0, mx = 0, nn = 0;
+  if (fail(env, capf_table_column_range(T(t), c.p, &mn, &mx, &nn))) return;
+  jlong v[3] = {(jlong)mn, (jlong)mx, (jlong)nn};
+  env->SetLongArrayRegion(out, 0, 3, v);
+}
+// returns the row bytes W; d_out = 0: only W
+JNI(jint, tablePackRows)(JNIEnv *env, jobject, jlong t, jobjectArray cols, jintArray width, jlongArray base,
+                         jintArray nullable, jlong d_out) {
+  JStrs c(env, cols);
+  std::vector<int32_t> w = ints(env, width), nl = ints(env, nullable);
+  std::vector<int64_t> b = longs(env, base);
+  int32_t W = 0;
+  fail(env, capf_table_pack_rows(T(t), c.n(), c.data(), w.data(), b.data(), nl.data(), &W,
+                                 reinterpret_cast<void *>(d_out)));
+  return W;
+}
+JNI(jlong, tableFromPackedRows)(JNIEnv *env, jobject, jlong s, jobjectArray names, jintArray types,
+                                jintArray width, jlongArray base, jintArray nullable, jlong d_rows, jlong nrows) {
+  JStrs nm(env, names);
+  std::vector<int32_t> ty = ints(env, types), w = ints(env, width), nl = ints(env, nullable);
+  std::vector<int64_t> b = longs(env, base);
+  capf_table *out = nullptr;
+  if (fail(env, capf_table_from_packed_rows(S(s), nm.n(), nm.data(), ty.data(), w.data(), b.data(), nl.data(),
+                                            reinterpret_cast<const void *>(d_rows), nrows, &out)))
+    return 0;
+  return H(out);
+}
 JNI(void, tableDownloadDevice)(JNIEnv *env, jobject, jlong t, jstring col, jlong d_values,
                                jlong d_valid) {
   JStr c(env, col);

@@ -168,4 +168,9 @@ object Native {
   @native def tableHashRoute(table: Long, keys: Array[String], parts: Int, countsOut: Array[Long]): Long
   @native def tableDownloadDevice(table: Long, col: String, dValues: Long, dValid: Long): Unit
   @native def tableHasNulls(table: Long, col: String): Boolean
+  @native def tableColumnRange(table: Long, col: String, out: Array[Long]): Unit
+  @native def tablePackRows(table: Long, cols: Array[String], width: Array[Int], base: Array[Long],
+                            nullable: Array[Int], dOut: Long): Int
+  @native def tableFromPackedRows(session: Long, names: Array[String], types: Array[Int], width: Array[Int],
+                                  base: Array[Long], nullable: Array[Int], dRows: Long, nrows: Long): Long
 }

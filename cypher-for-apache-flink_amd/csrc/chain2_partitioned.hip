@@ -2528,7 +2528,8 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
     // group of per-tile overhead (stage fill, scan, copy-out)
     const char *te = getenv("CAPF_SHARD_TILE");  // tuning: 16 → 16 Ki-row tiles
     // (32 Ki-row tiles need 32 keys per thread in VGPRs: no spills at FOR24 only)
-    const int tile = (te && atoi(te) == 16) || W != 3 ? 16384 : C5S_TILE;
+    // CAPF_SHARD_TILE=24 (tuning): 24 Ki-row tiles (24 keys per thread: no VGPR spills)
+    const int tile = (te && atoi(te) == 16) || W != 3 ? 16384 : (te && atoi(te) == 24) ? 24576 : C5S_TILE;
     {
       const int64_t slots = 2 * (int64_t)s->num_cus;
       int64_t best = -1;
@@ -2572,6 +2573,8 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
         const bool tr = trusted && W != 8 && c.upf;
         auto kern = tile == C5S_TILE ? (tr ? c5s_kernel_t<C5S_TILE, true>(W, kbits > 24, nh > 0)
                                            : c5s_kernel<C5S_TILE>(W, kbits > 24, nh > 0))
+                    : tile == 24576 ? (tr ? c5s_kernel_t<24576, true>(W, kbits > 24, nh > 0)
+                                          : c5s_kernel<24576>(W, kbits > 24, nh > 0))
                                      : (tr ? c5s_kernel_t<16384, true>(W, kbits > 24, nh > 0)
                                            : c5s_kernel<16384>(W, kbits > 24, nh > 0));
         hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(C5_BLOCK), 0, s->stream, c,

@@ -220,9 +220,9 @@ class FSGraphSource:
         with open(os.path.join(gdir, META_FILE), "w") as f:
             json.dump({"tableStorageFormat": self.table_storage_format, "tags": [0]}, f, indent=4)
         schema = {"version": "1.0",
-                  "labelPropertyMap": [{"labels": sorted(t.labels), "properties": dict(t.props)}
+                  "labelPropertyMap": [{"labels": sorted(t.labels), "properties": _schema_props(t)}
                                        for t in graph.node_tables],
-                  "relTypePropertyMap": [{"relType": next(iter(t.labels)), "properties": dict(t.props)}
+                  "relTypePropertyMap": [{"relType": next(iter(t.labels)), "properties": _schema_props(t)}
                                          for t in graph.rel_tables]}
         with open(os.path.join(gdir, SCHEMA_FILE), "w") as f:
             json.dump(schema, f, indent=4)
@@ -241,6 +241,19 @@ class FSGraphSource:
         with open(os.path.join(path, "part-00000.csv"), "w", newline="") as f:
             for row in zip(*data):
                 f.write(",".join(_format_field(v) for v in row) + "\n")
+
+
+def _schema_props(t):
+    """Property types of an element table for the schema JSON: a property that
+    is missing on some element (a NULL in its column) is nullable ('INTEGER?'),
+    as okapi's PropertyGraphSchema types it — the reader then knows that an
+    empty CSV field is NULL."""
+    out = {}
+    for k, ct in t.props.items():
+        if not ct.endswith("?") and any(v is None for v in t.table.column_values(t.prop_col(k))):
+            ct += "?"
+        out[k] = ct
+    return out
 
 
 def _format_field(v):

@@ -13,6 +13,7 @@ echo "rows sparse"; $T 300 python -u bench.py --query one_hop_rows --scale 22 --
 echo "rows sparse radix"; CAPF_JOIN=radix $T 300 python -u bench.py --query one_hop_rows --scale 22 --steps 5 --warmup 2 --id-stride 1000003 > gpurun_out/r03_rows_sparse_radix.json 2> gpurun_out/r03_rows_sparse_radix.err
 echo "shard g8"; $T 300 python -u tools/shard_timing.py 24 8 > gpurun_out/r03_shard_g8_s24.txt 2>&1
 echo "shard g8 untrusted"; CAPF_SHARD_TRUST=0 $T 300 python -u tools/shard_timing.py 24 8 > gpurun_out/r03_shard_g8_s24_untrusted.txt 2>&1
+echo "shard g8 tile24"; CAPF_SHARD_TILE=24 $T 300 python -u tools/shard_timing.py 24 8 > gpurun_out/r03_shard_g8_s24_t24.txt 2>&1
 echo "profiles"; bash tools/collect_profiles.sh 24 > gpurun_out/r03_collect.txt 2>&1
 echo "full suite"; $T 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r03_gputests.txt 2>&1
 echo done

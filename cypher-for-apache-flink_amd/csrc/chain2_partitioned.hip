@@ -691,7 +691,44 @@ struct C5Sched {
 // unit.  Voting out lane 0's key, half-wave atomics and non-returning atomics
 // were measured and do not help (the duplicates are spread over many
 // moderately hot keys).
-template <int PPS, int DIAG = 0, int DEPTH = 1, int HOT = 0>
+// The 8 packed uint16 keys of a piece rotated left by r (0..7) elements:
+// element e of the result is element (e + r) mod 8 of the piece.
+__device__ inline void c5_rotate8(uint32_t (&a)[4], uint32_t r) {
+  uint32_t b0 = (r & 4) ? a[2] : a[0], b1 = (r & 4) ? a[3] : a[1];
+  uint32_t b2 = (r & 4) ? a[0] : a[2], b3 = (r & 4) ? a[1] : a[3];
+  uint32_t c0 = (r & 2) ? b1 : b0, c1 = (r & 2) ? b2 : b1;
+  uint32_t c2 = (r & 2) ? b3 : b2, c3 = (r & 2) ? b0 : b3;
+  a[0] = (r & 1) ? __builtin_amdgcn_alignbit(c1, c0, 16) : c0;
+  a[1] = (r & 1) ? __builtin_amdgcn_alignbit(c2, c1, 16) : c1;
+  a[2] = (r & 1) ? __builtin_amdgcn_alignbit(c3, c2, 16) : c2;
+  a[3] = (r & 1) ? __builtin_amdgcn_alignbit(c0, c3, 16) : c3;
+}
+
+// Keys of a (rotated) piece and their dedup: inc[e] = multiplicity of key[e]
+// among slots e..7 if slot e holds its first occurrence, else 0.
+__device__ inline void c5_dedup8(const uint32_t (&a)[4], uint32_t (&key)[8], uint32_t (&inc)[8]) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    key[e] = (e & 1) ? a[e >> 1] >> 16 : a[e >> 1] & 0xFFFF;
+    inc[e] = 1;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+#pragma unroll
+    for (int f = e + 1; f < 8; ++f) {
+      const bool eq = key[e] == key[f];
+      inc[e] += eq && inc[e] != 0 ? 1u : 0u;  // (a later duplicate of a non-first slot adds nothing)
+      inc[f] = eq ? 0u : inc[f];
+    }
+}
+
+// ROT (CAPF_P3_ROT): every piece's 8 keys are rotated by lane mod 8 elements
+// and fully deduplicated (28 compares: each distinct key of the piece added
+// once, with its multiplicity).  Slot e of lane l then holds the piece's key
+// (e + l) mod 8, so a hub key that fills 35 % of its run (R-MAT s24) no longer
+// lands in the same slot — the same ds_add — in most lanes: its ~22 same-word
+// lanes per instruction drop to ~8, spread over the 8 instructions.
+template <int PPS, int DIAG = 0, int DEPTH = 1, int HOT = 0, int ROT = 0>
 __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
                                                             const int32_t *nunits,
                                                             const uint16_t *part,
@@ -870,6 +907,28 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
       dead += live ? 0u : 1u;
       const uint32_t wd[4] = {live ? v[j].x : dead_keys.x, live ? v[j].y : dead_keys.y,
                               live ? v[j].z : dead_keys.z, live ? v[j].w : dead_keys.w};
+      if (ROT && DIAG == 0) {
+        uint32_t a[4] = {wd[0], wd[1], wd[2], wd[3]}, key[8], inc[8];
+        c5_rotate8(a, (uint32_t)lane & 7u);
+        c5_dedup8(a, key, inc);
+        // the hand-off check inline (olds live for this piece only: no
+        // per-step old[] array, fewer VGPRs than the slot-0/1 merge)
+        uint32_t o8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t add = inc[e] << ((key[e] >> 15) << 4);
+          o8[e] = inc[e] ? atomicAdd(&words[key[e] & (C2_WORDS - 1)], add) : 0u;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t sh = (key[e] >> 15) << 4;
+          const uint32_t nw = o8[e] + (inc[e] << sh);
+          if (inc[e] && (nw & ~o8[e] & (0x8000u << sh)))  // this add lifted its half to 2^15
+            c3_handoff(&words[key[e] & (C2_WORDS - 1)], 1u << sh, (sd.packed ? log_base : hist_base) + key[e],
+                       side, ovf);
+        }
+        continue;
+      }
       if (DIAG == 0) {
         // hub keys: the keys of the piece equal to its first (second) key
         // are added once, as a count ≤ 8, by slot 0 (1) (R-MAT skew puts a hub's key in
@@ -933,6 +992,7 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
         const bool live = p0 + j * WAVE + lane < total;
         const uint32_t wd[4] = {live ? v[j].x : dead_keys.x, live ? v[j].y : dead_keys.y,
                                 live ? v[j].z : dead_keys.z, live ? v[j].w : dead_keys.w};
+        if (ROT) continue;  // checked inline
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
@@ -1139,7 +1199,8 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   if (!attr_set) {
     for (const void *f : {(const void *)k_c5_gather<C5_PPS, 0>, (const void *)k_c5_gather<C5_PPS, 2>,
                           (const void *)k_c5_gather<C5_PPS, 3>, (const void *)k_c5_gather<C5_PPS, 0, 2>,
-                          (const void *)k_c5_gather<C5_PPS, 0, 1, 1>, (const void *)k_c5_gather<C5_PPS, 0, 2, 1>})
+                          (const void *)k_c5_gather<C5_PPS, 0, 1, 1>, (const void *)k_c5_gather<C5_PPS, 0, 2, 1>,
+                          (const void *)k_c5_gather<C5_PPS, 0, 2, 0, 1>, (const void *)k_c5_gather<C5_PPS, 0, 1, 0, 1>})
       HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, C5_GATHER_LDS));
     attr_set = true;
   }
@@ -1217,8 +1278,12 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
     // depth 2 (loads of steps i+1, i+2 in flight while step i counts) is the
     // default: 0.437 vs 0.445 ms at s24; CAPF_P3_DEPTH=1 selects depth 1
     const bool d2 = !(dp && atoi(dp) == 1), h1 = hot && atoi(hot) == 1;
+    const char *rot = getenv("CAPF_P3_ROT");  // 1: rotated, fully deduplicated pieces
+    const bool r1 = rot && atoi(rot) == 1;
     auto kern = dg && atoi(dg) == 2 ? k_c5_gather<C5_PPS, 2>
                 : dg && atoi(dg) == 3 ? k_c5_gather<C5_PPS, 3>
+                : d2 && r1            ? k_c5_gather<C5_PPS, 0, 2, 0, 1>
+                : r1                  ? k_c5_gather<C5_PPS, 0, 1, 0, 1>
                 : d2 && h1            ? k_c5_gather<C5_PPS, 0, 2, 1>
                 : h1                  ? k_c5_gather<C5_PPS, 0, 1, 1>
                 : d2                  ? k_c5_gather<C5_PPS, 0, 2>

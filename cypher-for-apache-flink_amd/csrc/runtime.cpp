@@ -1055,7 +1055,8 @@ capf_status capf_table_pack_rows(capf_table *t, int32_t ncols, const char *const
     const int i = t->node->col_index_or_throw(cols[j]);
     check_wire(t->node->types[i], width[j], base[j]);
     force(d->cols[i]);
-    if (!nullable[j] && d->cols[i]->valid) illegal("packed rows: a column with NULLs needs its validity byte");
+    if (!nullable[j] && d->cols[i]->valid && d->cols[i]->type != Type::Null)
+      illegal("packed rows: a column with NULLs needs its validity byte");
     cs.push_back(d->cols[i]);
   }
   int W = 0;

@@ -49,6 +49,18 @@ def test_two_hop_headline(gpu_session, scale, compact):
     assert got == FULL[str(scale)]["two_hop"]
 
 
+@pytest.mark.parametrize("scale", [20, 24])
+@pytest.mark.parametrize("rot", ["1"], ids=["p3_rotated_dedup"])
+def test_two_hop_headline_p3_variant(gpu_session, monkeypatch, scale, rot):
+    """The rotated, fully deduplicated P3 pieces (CAPF_P3_ROT=1) — including
+    the inline uint16 hand-off of the s24 hub (in-degree 369,897) — give the fixture."""
+    monkeypatch.setenv("CAPF_P3_ROT", rot)
+    g = rmat_graph(gpu_session, scale, compact=3)
+    got = run(g, TWO_HOP)[0]["count"]
+    assert gpu_session.last_plan() == "fused_chain2"
+    assert got == FULL[str(scale)]["two_hop"]
+
+
 def test_two_hop_headline_async_queue(gpu_session):
     """The pipelined bench mode (capf_table_count_async): 4 in-flight s24
     counts land the fixture in every slot."""

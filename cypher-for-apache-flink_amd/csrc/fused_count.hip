@@ -310,10 +310,14 @@ __global__ __launch_bounds__(256) void k_chain2_hist(Chain2Args a) {
   if (lane_id() == 0 && loops) atomicAdd(a.loops, loops);
 }
 
+// fin != null (capf_table_count_async): the workgroup whose `done` add comes
+// last writes *fin = acc[0] − acc[1] (Σ in·out − self-loops) — the count on the
+// device without a separate one-thread kernel.
 template <bool ONES>
 __global__ __launch_bounds__(256) void k_chain2_dot(const uint32_t *h1, const uint32_t *h2,
                                                     DMap wb, int64_t lo, int64_t len,
-                                                    unsigned long long *acc) {
+                                                    unsigned long long *acc, int64_t *fin = nullptr,
+                                                    unsigned int *done = nullptr) {
   __shared__ unsigned long long lds[17];
   unsigned long long s = 0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -354,6 +358,14 @@ __global__ __launch_bounds__(256) void k_chain2_dot(const uint32_t *h1, const ui
     s += (unsigned long long)h1[i] * h2[i] * (ONES ? 1ull : w_of<false>(wb, lo + i));
   s = block_reduce_sum(s, lds);
   if (threadIdx.x == 0 && s) atomicAdd(acc, s);
+  if (fin && threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(done, 1u) == gridDim.x - 1) {  // every other block's add has landed
+      __threadfence();
+      const unsigned long long a0 = atomicAdd(acc, 0ull), a1 = atomicAdd(acc + 1, 0ull);
+      *fin = (int64_t)(a0 - a1);
+    }
+  }
 }
 
 // per-id count array of a node table's id column over [lo, hi]
@@ -1141,8 +1153,9 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
   // partitioned histograms are indexed by node_mix(b − lo) over 2^k ≥ len counters
   const int64_t hlen = len > 0 ? std::max(len, chain2_hist_len(len)) : 0;
   BufPtr h = s->alloc(8 * std::max<int64_t>(hlen, 1) + 64);
-  BufPtr acc = s->alloc(16);
-  HIP_CHECK(hipMemsetAsync(acc->p, 0, 16, s->stream));
+  BufPtr acc = s->alloc(24);  // Σ in·out, self-loops, the dot's done counter
+  HIP_CHECK(hipMemsetAsync(acc->p, 0, 24, s->stream));
+  bool fin_done = false;  // the dot kernel wrote the async count
   uint32_t *h1 = (uint32_t *)h->p;
   uint32_t *h2 = h1 + ((hlen + 15) & ~int64_t(15));  // keep dwordx4 alignment
   int64_t dot_len = len;
@@ -1193,20 +1206,25 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
       KernelTimer kt(s, "chain2_dot", 8.0 * dot_len);
       // one block per CU (s24: 256 blocks 24 µs, 2048 37 µs — same-address atomics)
       unsigned grid = grid_for(dot_len / 4 + 1, 256, dot_grid(s->num_cus));
+      int64_t *fin = s->async_out;
+      unsigned int *done = (unsigned int *)((unsigned long long *)acc->p + 2);
       if (wb.ones)  // ONES: Σ in·out is invariant under the node_mix bijection
         hipLaunchKernelGGL(k_chain2_dot<true>, dim3(grid), dim3(256), 0, s->stream, h1, h2,
-                           wb.map.m, lo, dot_len, (unsigned long long *)acc->p);
+                           wb.map.m, lo, dot_len, (unsigned long long *)acc->p, fin, done);
       else
         hipLaunchKernelGGL(k_chain2_dot<false>, dim3(grid), dim3(256), 0, s->stream, h1, h2,
-                           wb.map.m, lo, dot_len, (unsigned long long *)acc->p);
+                           wb.map.m, lo, dot_len, (unsigned long long *)acc->p, fin, done);
       KERNEL_CHECK();
+      fin_done = fin != nullptr;
     }
   }
   const double tc = host_trace() ? host_us() : 0;
   if (s->async_out) {  // capf_table_count_async: total − loops on the device, no wait
-    hipLaunchKernelGGL(k_partial_minus_loops, dim3(1), dim3(64), 0, s->stream,
-                       (const unsigned long long *)acc->p, s->async_out);
-    KERNEL_CHECK();
+    if (!fin_done) {
+      hipLaunchKernelGGL(k_partial_minus_loops, dim3(1), dim3(64), 0, s->stream,
+                         (const unsigned long long *)acc->p, s->async_out);
+      KERNEL_CHECK();
+    }
     *out = 0;
     return true;
   }

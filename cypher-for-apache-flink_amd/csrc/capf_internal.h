@@ -451,9 +451,23 @@ bool bits_count_partitioned(Session *s, const ColView &key, int64_t n, int64_t l
 // The oriented CSR is cached on `src` (Column::index) for the pair (src, dst).
 void triangle_count_async(Session *s, const ColPtr &src, const ColPtr &dst, int64_t m,
                           int64_t lo, uint64_t len, int parts, int part, int64_t *d_out);
+// Hand-offs of the partitioned 2-hop histograms that P3 could not add itself
+// (its per-unit list was full): (hist index, side | count << 1) entries, hist
+// index mod hl = the counter; the dot kernel adds their terms.  Empty (n == 0
+// on the device) in practice.
+struct C2Spill {
+  const uint2 *log = nullptr;
+  const uint32_t *n = nullptr;
+  uint32_t cap = 0;
+  int64_t hl = 0;
+};
+// d_acc3 = [Σ in·out, self-loops, done counter] (device): the pipeline writes
+// the self-loop total into [1] and clears [0] and [2] itself (no memset needed)
+// spill: non-null → the hand-off log is left for the dot kernel (no separate
+// overflow kernel); null → the overflow kernel runs.
 bool chain2_partitioned(Session *s, const ColView *cols, int64_t n, int64_t lo, int64_t hi,
                         bool in_range, uint32_t *h_in, uint32_t *h_out,
-                        unsigned long long *d_loops);
+                        unsigned long long *d_acc3, C2Spill *spill = nullptr);
 
 }  // namespace capf
 

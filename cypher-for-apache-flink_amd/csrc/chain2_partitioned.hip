@@ -146,6 +146,19 @@ __device__ inline void c5_load4(const void *p, int64_t base, int64_t lo, uint64_
   }
 }
 
+// Σ of v over the workgroup into *out (plain store by thread 0); red: ≥ 16 words of LDS.
+__device__ inline void c5_tile_sum(uint32_t v, uint32_t *red, uint32_t *out) {
+  const uint32_t w = (uint32_t)wave_reduce_sum((unsigned long long)v);
+  __syncthreads();  // red may still be read by an earlier scan
+  if (lane_id() == 0) red[threadIdx.x / WAVE] = w;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int i = 0; i < (int)(blockDim.x / WAVE); ++i) t += red[i];
+    *out = t;
+  }
+}
+
 // P1.  ALIAS: r1 and r2 scan the same (start, end) columns — the directed
 // 2-hop (a)-->(b)-->(c) — so one 8-B row gives both keys.  CHECK: range
 // tests needed.  RAGGED: the single last partial tile.
@@ -193,10 +206,14 @@ __device__ inline C5Raw<W> c5_ld_raw(const uint8_t *p) {
 // thread (96 B at FOR24) instead of one group ahead; the raw registers of a
 // group die as its keys appear, so the peak stays within 64 VGPRs.
 template <int W, bool ALIAS, bool CHECK, bool RAGGED, class SH, int DIAG = 0, int UPF = 0>
+// Self-loops go out as one plain uint32 per tile (tile_loops[t], summed by
+// k_c3_units); the tile-0 workgroup also clears the `zwords` words at zbuf
+// (the run totals / work-list header of the post-P1 kernels) — no memset
+// launches in front of or behind P1.
 __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_c5_partition(C5Cols<W> c, uint16_t *part,
                                                             uint32_t *meta,
-                                                            unsigned long long *loops,
-                                                            int64_t t_base) {
+                                                            uint32_t *tile_loops,
+                                                            int64_t t_base, uint32_t *zbuf, int zwords) {
   constexpr int TILE = SH::TILE, MAXR = SH::MAXR;
   constexpr int RPT = TILE / C5_BLOCK, GROUPS = RPT / 4;
   constexpr int STAGE = c5_stage_keys<SH>();
@@ -213,6 +230,8 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
                                (pb + 4) | (pb + 5) << 16, (pb + 6) | (pb + 7) << 16);
   (void)pad;  // pads are written per run after the scan (no stage prefill)
   for (int i = threadIdx.x; i <= nr; i += C5_BLOCK) cur[i] = 0;
+  if (t == 0 && zbuf)
+    for (int i = threadIdx.x; i < zwords; i += C5_BLOCK) zbuf[i] = 0;
   __syncthreads();
   const int64_t e0 = t * TILE;
   const int64_t e1 = RAGGED ? min(e0 + TILE, c.n) : e0 + TILE;
@@ -335,8 +354,7 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
                      (kin[4 * q + 2] & 0xFFFF) | kout[4 * q + 2] << 16,
                      (kin[4 * q + 3] & 0xFFFF) | kout[4 * q + 3] << 16);
     if (threadIdx.x < (unsigned)nr) meta[t * nr + threadIdx.x] = 0;
-    unsigned long long lp64 = wave_reduce_sum((unsigned long long)lp);
-    if (lane_id() == 0 && lp64) atomicAdd(loops, lp64);
+    c5_tile_sum(lp, lds_scan, tile_loops + t);
     return;
   }
   __syncthreads();
@@ -375,8 +393,7 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   // the stage IS the region's layout: contiguous 16-B copy-out
   uint4 *dst = (uint4 *)(part + t * c.rstride);
   for (uint32_t i = threadIdx.x; i < total / 8; i += C5_BLOCK) dst[i] = stage4[i];
-  unsigned long long lp64 = wave_reduce_sum((unsigned long long)lp);
-  if (lane_id() == 0 && lp64) atomicAdd(loops, lp64);
+  c5_tile_sum(lp, lds_scan, tile_loops + t);
 }
 
 // [tile][run] → [run][tile] and per-run totals.  A block moves 32 runs ×
@@ -473,10 +490,23 @@ static int c3_split_x16() {
 // wave and the short ones fill the tail.
 constexpr int C3_MAXU = 4096;  // LDS capacity of the ordering pass
 
+// Also (the P1 → P3 path of the fused 2-hop count, `post` non-null): sums P1's
+// per-tile self-loops into acc3[1], clears acc3[0] (Σ in·out) and acc3[2] (the
+// dot's done counter), and clears the histogram slices of split runs (their
+// units flush with atomic adds) — the work of two memsets and k_c3_zero.
+struct C3Post {
+  const uint32_t *tile_loops;
+  int64_t ntiles;
+  unsigned long long *acc3;
+  uint32_t *h_in, *h_out;
+  int64_t slice_stride;
+  C2Spill *spill;  // host side: non-null → P3 keeps hand-offs local, the log goes to the dot
+};
+
 __global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(const unsigned long long *run_total,
                                                          int nr, C3Sides sd, int S, C3Unit *units,
                                                          int32_t *nunits, int32_t *split,
-                                                         int32_t *order) {
+                                                         int32_t *order, C3Post post) {
   __shared__ unsigned long long lds64[17];
   __shared__ uint32_t lds32[17];
   __shared__ uint32_t est[C3_MAXU];
@@ -526,6 +556,30 @@ __global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(const unsigned long long
     split[r] = nu[q] > (uint32_t)S;
   }
   if (threadIdx.x == 0) *nunits = (int32_t)ntot;
+  if (post.acc3) {
+    unsigned long long lsum = 0;
+    for (int64_t t = threadIdx.x; t < post.ntiles; t += C3_UBLOCK) lsum += post.tile_loops[t];
+    unsigned long long lt;
+    block_exclusive_scan(lsum, lds64, lt);
+    if (threadIdx.x == 0) {
+      post.acc3[0] = 0;
+      post.acc3[1] = lt;
+      post.acc3[2] = 0;
+    }
+    // split runs: every slice of their buckets cleared (nu > S ⇔ split)
+    __shared__ uint8_t sp[2 * C3_UBLOCK];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) sp[2 * threadIdx.x + q] = nu[q] > (uint32_t)S ? 1 : 0;
+    __syncthreads();
+    for (int r = 0; r < nr; ++r) {
+      if (!sp[r]) continue;  // uniform: every thread reads the same LDS byte
+      for (int sl = 0; sl < S; ++sl) {
+        uint4 *p = (uint4 *)((r >= sd.nb ? post.h_out : post.h_in) + sl * post.slice_stride +
+                             (int64_t)(r % sd.nb) * C2_BW);
+        for (int i = threadIdx.x; i < C2_BW / 4; i += C3_UBLOCK) p[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  }
   if (!order) return;
   if (threadIdx.x <= 64) qcnt[threadIdx.x] = 0;
   if (threadIdx.x == 0) maxest = 0;
@@ -583,12 +637,31 @@ struct C3Ovf {
   uint32_t *n;
   uint32_t cap;
   unsigned long long *trace;  // diagnostics (CAPF_P3_TRACE): 4 words per unit, else null
+  int local;   // hand-offs kept in the unit's LDS list and added after its flush (the
+               // global log then only takes a full list's spill, applied by the dot)
+  uint32_t hocap;  // list capacity used (≤ C3_HO_CAP; CAPF_P3_HOCAP lowers it for tests)
+};
+
+// The unit's LDS list of hand-offs (C3Ovf::local): at most C3_HO_CAP per unit —
+// a unit of T keys hands off at most T / 2^15 times, so the list only spills
+// for units of more than 2^23 keys.
+constexpr uint32_t C3_HO_CAP = 256;
+struct C3HoList {
+  uint32_t *n;
+  uint2 *e;
 };
 
 // Slow path of an overflowing add (rare: a bin reached 2^15 within the unit).
 __device__ inline void c3_handoff(uint32_t *w, uint32_t inc, uint32_t hidx, uint32_t side,
-                                        const C3Ovf &o) {
+                                        const C3Ovf &o, C3HoList ho = C3HoList{nullptr, nullptr}) {
   atomicSub(w, inc << 15);
+  if (o.local && ho.n) {
+    const uint32_t j = atomicAdd(ho.n, 1u);
+    if (j < o.hocap) {
+      ho.e[j] = make_uint2(hidx, side | (1u << 16));
+      return;
+    }
+  }
   const uint32_t k = atomicAdd(o.n, 1u);
   if (k < o.cap) o.log[k] = make_uint2(hidx, side | (1u << 16));
 }
@@ -744,6 +817,9 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
   __shared__ int32_t sbase[C5APP_MAXR + 1], sk[C5APP_MAXR];
   __shared__ uint32_t lds_sc[17];
   __shared__ int64_t sbnd[2];
+  __shared__ uint32_t ho_n;
+  __shared__ uint2 ho_e[C3_HO_CAP];
+  const C3HoList hol{&ho_n, ho_e};
   int nu = units ? *nunits : 2 * sd.nb * S;
   const int nrr = 2 * sd.nb;
   if (sch.run_total) {
@@ -834,6 +910,7 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
   const uint32_t hist_base = sch.run_total ? (uint32_t)((int64_t)u.slice * C2_BW)
                                            : (uint32_t)(u.slice * slice_stride + (int64_t)(u.run % nb) * C2_BW);
   for (int i = threadIdx.x; i < C2_WORDS + C5_CORR; i += C5_BLOCK) words[i] = 0;
+  if (threadIdx.x == 0) ho_n = 0;
   __syncthreads();
   // wave-uniform values live in SGPRs: uniform loop control, no exec masking
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = lane_id();
@@ -925,7 +1002,7 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
           const uint32_t nw = o8[e] + (inc[e] << sh);
           if (inc[e] && (nw & ~o8[e] & (0x8000u << sh)))  // this add lifted its half to 2^15
             c3_handoff(&words[key[e] & (C2_WORDS - 1)], 1u << sh, (sd.packed ? log_base : hist_base) + key[e],
-                       side, ovf);
+                       side, ovf, hol);
         }
         continue;
       }
@@ -1002,7 +1079,7 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
           const uint32_t oh = (old[j][e] >> sh) & 0xFFFFu;
           if (oh < 0x8000u && oh + inc >= 0x8000u)
             c3_handoff(&words[key & (C2_WORDS - 1)], 1u << sh, (sd.packed ? log_base : hist_base) + key,
-                       side, ovf);
+                       side, ovf, hol);
         }
       }
     }
@@ -1133,6 +1210,16 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
       if (hi) atomicAdd(h + C2_WORDS, hi);
     }
   }
+  if (ovf.local) {
+    // this unit's hand-offs, after its own flush has reached L2
+    __threadfence();
+    __syncthreads();
+    const uint32_t nh = min(ho_n, ovf.hocap);
+    for (uint32_t i = threadIdx.x; i < nh; i += C5_BLOCK) {
+      const uint2 e = ho_e[i];
+      atomicAdd(&((e.y & 1u) ? h_out : h_in)[e.x], e.y >> 1);
+    }
+  }
   if (ovf.trace) {  // diagnostics: this unit's span, where it ran
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1157,7 +1244,7 @@ __global__ __launch_bounds__(256) void k_c3_overflow(C3Ovf o, uint32_t *h_in, ui
 
 template <int W, bool ALIAS, bool CHECK, class SH>
 static void launch_c5(Session *s, const C5Cols<W> &c, uint16_t *part, uint32_t *meta,
-                      unsigned long long *d_loops) {
+                      uint32_t *tile_loops, uint32_t *zbuf, int zwords) {
   const int64_t nfull = c.n / SH::TILE;
   if (nfull > 0) {
     const char *dg = getenv("CAPF_P1_DIAG");  // diagnostics only: wrong counts
@@ -1174,12 +1261,12 @@ static void launch_c5(Session *s, const C5Cols<W> &c, uint16_t *part, uint32_t *
                 : upf       ? k_c5_partition<W, ALIAS, CHECK, false, SH, 0, 1>
                             : k_c5_partition<W, ALIAS, CHECK, false, SH, 0>;
     hipLaunchKernelGGL(kern, dim3((unsigned)nfull), dim3(C5_BLOCK), 0, s->stream, c, part, meta,
-                       d_loops, (int64_t)0);
+                       tile_loops, (int64_t)0, zbuf, zwords);
     KERNEL_CHECK();
   }
   if (nfull < c.ntiles) {  // the ragged last tile
     hipLaunchKernelGGL((k_c5_partition<W, ALIAS, true, true, SH>), dim3(1), dim3(C5_BLOCK), 0,
-                       s->stream, c, part, meta, d_loops, nfull);
+                       s->stream, c, part, meta, tile_loops, nfull, zbuf, zwords);
     KERNEL_CHECK();
   }
 }
@@ -1188,11 +1275,26 @@ static void launch_c5(Session *s, const C5Cols<W> &c, uint16_t *part, uint32_t *
 // overflow hand-offs.  `part`/`meta` hold ntiles tiles of nr = 2·sd.nb runs.
 // Histograms: S slices (c5_slices) of sd.nb·64 Ki counters per side, slice s
 // at h_in/h_out + s·slice_stride; every counter of every slice is written.
+// Bytes of c5_post's work area (run totals, counters, split flags, units, the
+// hand-off log) and its leading words that must start at zero.
+static int64_t c5_post_acc_bytes(int nr, int S, int split_x16, int64_t nkeys, int *max_units_out,
+                                 uint32_t *ovf_cap_out) {
+  // runs × slices + hub splits (≤ 2 per run beyond the slices), whole XCD waves
+  // Σ_runs max(S, ⌈cnt/target⌉) ≤ S·nr + nr + total/target, target ≥ split/16 × mean
+  const int max_units = (S * nr + nr + 16 * nr / std::max(1, split_x16) + 2 + 255) / 256 * 256;
+  // every overflow event consumes 2^15 adds of one half-counter within one unit
+  const uint32_t ovf_cap = (uint32_t)(nkeys / (1 << 15) + 64 + 16 * (int64_t)max_units);
+  if (max_units_out) *max_units_out = max_units;
+  if (ovf_cap_out) *ovf_cap_out = ovf_cap;
+  return 8 * nr + 16 + 4 * nr + (int64_t)sizeof(C3Unit) * max_units + 8 * (int64_t)ovf_cap;
+}
+static int c5_post_zero_words(int nr) { return (8 * nr + 16) / 4; }
+
 static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, const C3Sides &sd,
                     int64_t ntiles, int64_t rstride, int64_t nkeys, int S, uint32_t *h_in,
                     uint32_t *h_out, int64_t slice_stride, bool static_units = false,
                     int32_t *apportion_table = nullptr, C3Ovf *packed_ovf = nullptr,
-                    BufPtr *keep = nullptr) {
+                    BufPtr *keep = nullptr, const C3Post *post = nullptr, BufPtr acc_pre = BufPtr()) {
   const int nr = 2 * sd.nb;
   const bool app = apportion_table != nullptr;  // apportioned units (C5Sched), slices by unit
   static bool attr_set = false;
@@ -1206,9 +1308,9 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   }
   // runs × slices + hub splits (≤ 2 per run beyond the slices), whole XCD waves
   // Σ_runs max(S, ⌈cnt/target⌉) ≤ S·nr + nr + total/target, target ≥ split/16 × mean
-  const int max_units = (S * nr + nr + 16 * nr / std::max(1, sd.split_x16) + 2 + 255) / 256 * 256;
-  // every overflow event consumes 2^15 adds of one half-counter within one unit
-  const uint32_t ovf_cap = (uint32_t)(nkeys / (1 << 15) + 64 + 16 * (int64_t)max_units);
+  int max_units = 0;
+  uint32_t ovf_cap = 0;
+  const int64_t acc_bytes = c5_post_acc_bytes(nr, S, sd.split_x16, nkeys, &max_units, &ovf_cap);
   // CAPF_META_T=0 (tuning): P3 reads P1's tile-major meta in place (the units
   // of 32 consecutive runs on one XCD share its lines in L2) and the transpose
   // kernel only sums the run totals — s24: transpose 31 → 24 µs, P3 +7..20 µs
@@ -1219,7 +1321,9 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   int64_t tt = C3_TT;
   while (tt > 32 && ((ntiles + tt - 1) / tt) * ((nr + 31) / 32) < 1024) tt /= 2;
   const int nparts = (int)((ntiles + tt - 1) / tt);
-  BufPtr acc = s->alloc(8 * nr + 16 + 4 * nr + sizeof(C3Unit) * max_units + 8 * (int64_t)ovf_cap);
+  // acc_pre: allocated by the caller, its first c5_post_zero_words words
+  // cleared by P1's tile-0 workgroup (no memset here)
+  BufPtr acc = acc_pre ? acc_pre : s->alloc(acc_bytes);
   unsigned long long *run_total = (unsigned long long *)acc->p;
   int32_t *nunits = (int32_t *)(run_total + nr);  // [0] units, [1] overflow events
   int32_t *split = nunits + 4;
@@ -1229,11 +1333,16 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   const bool lpt = lpt_env && atoi(lpt_env) == 1;
   BufPtr order_buf = lpt ? s->alloc(4 * (int64_t)max_units) : BufPtr();
   int32_t *order = lpt ? (int32_t *)order_buf->p : nullptr;
-  C3Ovf ovf;
+  C3Ovf ovf{};
   ovf.n = (uint32_t *)(nunits + 1);
   ovf.log = (uint2 *)(units + max_units);
   ovf.cap = ovf_cap;
   ovf.trace = nullptr;
+  ovf.local = post && post->spill && !sd.packed ? 1 : 0;
+  {
+    const char *hc = getenv("CAPF_P3_HOCAP");  // tests: a smaller list, so hand-offs spill to the dot
+    ovf.hocap = hc ? (uint32_t)std::min<long>(std::max<long>(atol(hc), 0), (long)C3_HO_CAP) : C3_HO_CAP;
+  }
   const char *trace_path = getenv("CAPF_P3_TRACE");  // diagnostics only
   BufPtr trace;
   if (trace_path) {
@@ -1241,7 +1350,7 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
     HIP_CHECK(hipMemsetAsync(trace->p, 0, 32 * (size_t)max_units, s->stream));
     ovf.trace = (unsigned long long *)trace->p;
   }
-  HIP_CHECK(hipMemsetAsync(acc->p, 0, 8 * nr + 16, s->stream));
+  if (!acc_pre) HIP_CHECK(hipMemsetAsync(acc->p, 0, 8 * nr + 16, s->stream));
   BufPtr bsum = app ? s->alloc(4 * (int64_t)nr * nparts) : BufPtr();
   C5Sched sch{};
   if (app) {
@@ -1261,12 +1370,21 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   }
   if (!static_units) {
     KernelTimer kt(s, "c3_units", 8.0 * nr);
+    C3Post cp{};
+    if (post) cp = *post;
+    if (post) {  // the split-run bins are cleared by the units kernel itself
+      cp.h_in = h_in;
+      cp.h_out = h_out;
+      cp.slice_stride = slice_stride;
+    }
     hipLaunchKernelGGL(k_c3_units, dim3(1), dim3(C3_UBLOCK), 0, s->stream,
-                       (const unsigned long long *)run_total, nr, sd, S, units, nunits, split, order);
+                       (const unsigned long long *)run_total, nr, sd, S, units, nunits, split, order, cp);
     KERNEL_CHECK();
-    hipLaunchKernelGGL(k_c3_zero, dim3(4, nr, S), dim3(256), 0, s->stream, (const int32_t *)split,
-                       sd.nb, h_in, h_out, slice_stride);
-    KERNEL_CHECK();
+    if (!post) {
+      hipLaunchKernelGGL(k_c3_zero, dim3(4, nr, S), dim3(256), 0, s->stream, (const int32_t *)split,
+                         sd.nb, h_in, h_out, slice_stride);
+      KERNEL_CHECK();
+    }
   }
   {
     KernelTimer kt(s, "c5_gather", 2.0 * nkeys);
@@ -1302,6 +1420,11 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   if (sd.packed) {  // the hand-offs are applied by k_c5_dot_packed
     *packed_ovf = ovf;
     *keep = acc;
+  } else if (ovf.local) {  // P3 added its hand-offs; a spill (if any) goes to the dot
+    post->spill->log = ovf.log;
+    post->spill->n = ovf.n;
+    post->spill->cap = ovf.cap;
+    post->spill->hl = slice_stride;
   } else {
     KernelTimer kt(s, "c3_overflow", 0.0);
     hipLaunchKernelGGL(k_c3_overflow, dim3(16), dim3(256), 0, s->stream, ovf, h_in, h_out);
@@ -1458,40 +1581,51 @@ __global__ __launch_bounds__(1024) void k_c5_dot_packed(const uint32_t *si, cons
   if (threadIdx.x == 0 && tot) atomicAdd(acc, tot);
 }
 
+// d_acc3 = [Σ in·out, self-loops, done]: the units kernel writes the self-loop
+// total and clears the other two (the caller needs no memset).
 template <int W, class SH>
 static void chain2_c5(Session *s, C5Cols<W> c, bool in_range, uint32_t *h_in, uint32_t *h_out,
-                      unsigned long long *d_loops) {
+                      unsigned long long *d_acc3, C2Spill *spill) {
   c.ntiles = (c.n + SH::TILE - 1) / SH::TILE;
   const int nr = 2 * c.nb;
   c.rstride = ((int64_t)2 * SH::TILE + 8 * (nr + 1) + 7) & ~int64_t(7);
   BufPtr part = s->alloc(2 * c.rstride * c.ntiles);
   BufPtr meta = s->alloc(4 * nr * c.ntiles);
-  {
-    KernelTimer kt(s, "c5_partition", (2.0 * W + 4.0) * c.n);
-    uint16_t *pp = (uint16_t *)part->p;
-    uint32_t *mp = (uint32_t *)meta->p;
-    const bool alias = c.u2 == c.u1 && c.v2 == c.v1;
-    if (alias && !in_range) launch_c5<W, true, true, SH>(s, c, pp, mp, d_loops);
-    if (alias && in_range) launch_c5<W, true, false, SH>(s, c, pp, mp, d_loops);
-    if (!alias && !in_range) launch_c5<W, false, true, SH>(s, c, pp, mp, d_loops);
-    if (!alias && in_range) launch_c5<W, false, false, SH>(s, c, pp, mp, d_loops);
-  }
+  BufPtr tl = s->alloc(4 * std::max<int64_t>(c.ntiles, 1));
   C3Sides sd;
   sd.split_x16 = c3_split_x16();
   sd.nb = c.nb;
   sd.t0[0] = sd.t0[1] = 0;
   sd.t1[0] = sd.t1[1] = c.ntiles;
   const int S = c5_slices(nr);
+  BufPtr post_acc = s->alloc(c5_post_acc_bytes(nr, S, sd.split_x16, 2 * c.n, nullptr, nullptr));
+  {
+    KernelTimer kt(s, "c5_partition", (2.0 * W + 4.0) * c.n);
+    uint16_t *pp = (uint16_t *)part->p;
+    uint32_t *mp = (uint32_t *)meta->p;
+    uint32_t *tlp = (uint32_t *)tl->p, *zb = (uint32_t *)post_acc->p;
+    const int zw = c5_post_zero_words(nr);
+    const bool alias = c.u2 == c.u1 && c.v2 == c.v1;
+    if (alias && !in_range) launch_c5<W, true, true, SH>(s, c, pp, mp, tlp, zb, zw);
+    if (alias && in_range) launch_c5<W, true, false, SH>(s, c, pp, mp, tlp, zb, zw);
+    if (!alias && !in_range) launch_c5<W, false, true, SH>(s, c, pp, mp, tlp, zb, zw);
+    if (!alias && in_range) launch_c5<W, false, false, SH>(s, c, pp, mp, tlp, zb, zw);
+  }
+  C3Post post{};
+  post.tile_loops = (const uint32_t *)tl->p;
+  post.ntiles = c.ntiles;
+  post.acc3 = d_acc3;
+  post.spill = spill;
   const int64_t hl = (int64_t)c.nb * C2_BW;
   if (S == 1) {
     c5_post(s, (const uint16_t *)part->p, (const uint32_t *)meta->p, sd, c.ntiles, c.rstride,
-            2 * c.n, 1, h_in, h_out, hl);
+            2 * c.n, 1, h_in, h_out, hl, false, nullptr, nullptr, nullptr, &post, post_acc);
     return;
   }
   BufPtr sl = s->alloc(8 * S * hl);
   uint32_t *si = (uint32_t *)sl->p, *so = si + S * hl;
   c5_post(s, (const uint16_t *)part->p, (const uint32_t *)meta->p, sd, c.ntiles, c.rstride,
-          2 * c.n, S, si, so, hl);
+          2 * c.n, S, si, so, hl, false, nullptr, nullptr, nullptr, &post, post_acc);
   hipLaunchKernelGGL(k_c5_fold, dim3(grid_for(hl / 4, 256, 1024)), dim3(256), 0, s->stream, si, so,
                      S, hl, hl, h_in, h_out);
   KERNEL_CHECK();
@@ -2685,7 +2819,7 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
           BufPtr sl = s->alloc(8 * S * hw);
           uint32_t *si = (uint32_t *)sl->p, *so = si + S * hw;
           const char *st = getenv("CAPF_SHARD_STATIC");  // tuning: 0 = device work list
-          C3Ovf ovf;
+          C3Ovf ovf{};
           BufPtr keep;
           c5_post(s, (const uint16_t *)partb->p, (const uint32_t *)meta->p, sd, ntiles, rstride,
                   n_in + n_out, S, si, so, hw, !(st && atoi(st) == 0), nullptr, &ovf, &keep);
@@ -2740,7 +2874,7 @@ int64_t chain2_hist_len(int64_t len) { return int64_t(1) << chain2_hist_bits(len
 // k_chain2_hist).
 bool chain2_partitioned(Session *s, const ColView *cols, int64_t n, int64_t lo, int64_t hi,
                         bool in_range, uint32_t *h_in, uint32_t *h_out,
-                        unsigned long long *d_loops) {
+                        unsigned long long *d_acc3, C2Spill *spill) {
   const int64_t len = hi - lo + 1;
   if (len <= 0 || n <= 0) return false;
   const int kbits = chain2_hist_bits(len);
@@ -2777,26 +2911,26 @@ bool chain2_partitioned(Session *s, const ColView *cols, int64_t n, int64_t lo, 
     C5Cols<3> c;
     fill(c);
     if (small)
-      chain2_c5<3, C5Small>(s, c, in_range, h_in, h_out, d_loops);
+      chain2_c5<3, C5Small>(s, c, in_range, h_in, h_out, d_acc3, spill);
     else
-      chain2_c5<3, C5Big>(s, c, in_range, h_in, h_out, d_loops);
+      chain2_c5<3, C5Big>(s, c, in_range, h_in, h_out, d_acc3, spill);
     return true;
   }
   if (nf == 4) {
     C5Cols<4> c;
     fill(c);
     if (small)
-      chain2_c5<4, C5Small>(s, c, in_range, h_in, h_out, d_loops);
+      chain2_c5<4, C5Small>(s, c, in_range, h_in, h_out, d_acc3, spill);
     else
-      chain2_c5<4, C5Big>(s, c, in_range, h_in, h_out, d_loops);
+      chain2_c5<4, C5Big>(s, c, in_range, h_in, h_out, d_acc3, spill);
     return true;
   }
   C5Cols<8> c;
   fill(c);
   if (small)
-    chain2_c5<8, C5Small>(s, c, in_range, h_in, h_out, d_loops);
+    chain2_c5<8, C5Small>(s, c, in_range, h_in, h_out, d_acc3, spill);
   else
-    chain2_c5<8, C5Big>(s, c, in_range, h_in, h_out, d_loops);
+    chain2_c5<8, C5Big>(s, c, in_range, h_in, h_out, d_acc3, spill);
   return true;
 }
 

@@ -313,11 +313,13 @@ __global__ __launch_bounds__(256) void k_chain2_hist(Chain2Args a) {
 // fin != null (capf_table_count_async): the workgroup whose `done` add comes
 // last writes *fin = acc[0] − acc[1] (Σ in·out − self-loops) — the count on the
 // device without a separate one-thread kernel.
+// sp (partitioned pipeline, ONES): hand-offs P3 left in the log — the last
+// block adds Σ Δ·(other side) + Σ Δ_in·Δ_out over equal counters before fin.
 template <bool ONES>
 __global__ __launch_bounds__(256) void k_chain2_dot(const uint32_t *h1, const uint32_t *h2,
                                                     DMap wb, int64_t lo, int64_t len,
                                                     unsigned long long *acc, int64_t *fin = nullptr,
-                                                    unsigned int *done = nullptr) {
+                                                    unsigned int *done = nullptr, C2Spill sp = C2Spill()) {
   __shared__ unsigned long long lds[17];
   unsigned long long s = 0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -358,13 +360,35 @@ __global__ __launch_bounds__(256) void k_chain2_dot(const uint32_t *h1, const ui
     s += (unsigned long long)h1[i] * h2[i] * (ONES ? 1ull : w_of<false>(wb, lo + i));
   s = block_reduce_sum(s, lds);
   if (threadIdx.x == 0 && s) atomicAdd(acc, s);
-  if (fin && threadIdx.x == 0) {
+  if (!fin) return;
+  __shared__ int last;
+  if (threadIdx.x == 0) {
     __threadfence();
-    if (atomicAdd(done, 1u) == gridDim.x - 1) {  // every other block's add has landed
-      __threadfence();
-      const unsigned long long a0 = atomicAdd(acc, 0ull), a1 = atomicAdd(acc + 1, 0ull);
-      *fin = (int64_t)(a0 - a1);
-    }
+    last = atomicAdd(done, 1u) == gridDim.x - 1;  // every other block's add has landed
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  unsigned long long corr = 0;
+  const uint32_t ne = sp.n ? min(*sp.n, sp.cap) : 0u;
+  for (uint32_t e = threadIdx.x; e < ne; e += blockDim.x) {
+    const uint2 x = sp.log[e];
+    const int64_t b = (int64_t)x.x % sp.hl;
+    const unsigned long long d = x.y >> 1;
+    corr += d * ((x.y & 1u) ? h1[b] : h2[b]);
+    if (!(x.y & 1u))  // in-side entry: pairs with every out-side entry of the same counter
+      for (uint32_t f = 0; f < ne; ++f) {
+        const uint2 y = sp.log[f];
+        if ((y.y & 1u) && (int64_t)y.x % sp.hl == b) corr += d * (y.y >> 1);
+      }
+  }
+  corr = block_reduce_sum(corr, lds);
+  if (threadIdx.x == 0) {
+    const unsigned long long a0 = atomicAdd(acc, 0ull) + corr, a1 = atomicAdd(acc + 1, 0ull);
+    atomicAdd(acc, corr);  // acc[0] holds the corrected Σ for readers of acc
+    // fin may be pinned host memory: a system-scope store
+    __hip_atomic_store(fin, (int64_t)(a0 - a1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
   }
 }
 
@@ -1154,8 +1178,9 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
   const int64_t hlen = len > 0 ? std::max(len, chain2_hist_len(len)) : 0;
   BufPtr h = s->alloc(8 * std::max<int64_t>(hlen, 1) + 64);
   BufPtr acc = s->alloc(24);  // Σ in·out, self-loops, the dot's done counter
-  HIP_CHECK(hipMemsetAsync(acc->p, 0, 24, s->stream));
   bool fin_done = false;  // the dot kernel wrote the async count
+  C2Spill spill;          // hand-offs P3 left for the dot (partitioned pipeline)
+  bool acc_zeroed = false;  // the partitioned pipeline clears acc itself
   uint32_t *h1 = (uint32_t *)h->p;
   uint32_t *h2 = h1 + ((hlen + 15) & ~int64_t(15));  // keep dwordx4 alignment
   int64_t dot_len = len;
@@ -1188,9 +1213,12 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
     }
     tb = host_trace() ? host_us() : 0;
     if (n > 0 && want_part &&
-        chain2_partitioned(s, pc, n, lo, hi, in_range, h1, h2, a.loops)) {
+        chain2_partitioned(s, pc, n, lo, hi, in_range, h1, h2, (unsigned long long *)acc->p, &spill)) {
       dot_len = chain2_hist_len(len);  // every counter written; loops accumulated on the device
+      acc_zeroed = true;
     } else {
+      HIP_CHECK(hipMemsetAsync(acc->p, 0, 24, s->stream));
+      acc_zeroed = true;
       HIP_CHECK(hipMemsetAsync(h->p, 0, 8 * std::max<int64_t>(hlen, 1) + 64, s->stream));
       if (n > 0) {
         KernelTimer kt(s, "chain2_hist", 16.0 * n);
@@ -1206,18 +1234,21 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
       KernelTimer kt(s, "chain2_dot", 8.0 * dot_len);
       // one block per CU (s24: 256 blocks 24 µs, 2048 37 µs — same-address atomics)
       unsigned grid = grid_for(dot_len / 4 + 1, 256, dot_grid(s->num_cus));
-      int64_t *fin = s->async_out;
+      // the count (Σ − loops) straight into the async slot, or into the pinned
+      // host scalar the synchronous path reads after its sync (no D2H copy)
+      int64_t *fin = s->async_out ? s->async_out : s->h_scalars;
       unsigned int *done = (unsigned int *)((unsigned long long *)acc->p + 2);
       if (wb.ones)  // ONES: Σ in·out is invariant under the node_mix bijection
         hipLaunchKernelGGL(k_chain2_dot<true>, dim3(grid), dim3(256), 0, s->stream, h1, h2,
-                           wb.map.m, lo, dot_len, (unsigned long long *)acc->p, fin, done);
+                           wb.map.m, lo, dot_len, (unsigned long long *)acc->p, fin, done, spill);
       else
         hipLaunchKernelGGL(k_chain2_dot<false>, dim3(grid), dim3(256), 0, s->stream, h1, h2,
                            wb.map.m, lo, dot_len, (unsigned long long *)acc->p, fin, done);
       KERNEL_CHECK();
-      fin_done = fin != nullptr;
+      fin_done = true;
     }
   }
+  if (!acc_zeroed) HIP_CHECK(hipMemsetAsync(acc->p, 0, 24, s->stream));  // empty node range
   const double tc = host_trace() ? host_us() : 0;
   if (s->async_out) {  // capf_table_count_async: total − loops on the device, no wait
     if (!fin_done) {
@@ -1228,13 +1259,17 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
     *out = 0;
     return true;
   }
-  HIP_CHECK(hipMemcpyAsync(s->h_scalars, acc->p, 16, hipMemcpyDeviceToHost, s->stream));
-  s->sync();
+  if (fin_done) {
+    s->sync();
+    *out = (uint64_t)s->h_scalars[0];
+  } else {
+    HIP_CHECK(hipMemcpyAsync(s->h_scalars, acc->p, 16, hipMemcpyDeviceToHost, s->stream));
+    s->sync();
+    *out = (uint64_t)s->h_scalars[0] - (uint64_t)s->h_scalars[1];
+  }
   if (host_trace())
     fprintf(stderr, "[capf host] analyse %.1f us, weights+stats %.1f us, launches %.1f us, wait %.1f us\n",
             ta - g_trace_t0, tb - ta, tc - tb, host_us() - tc);
-  uint64_t total = (uint64_t)s->h_scalars[0], loops = (uint64_t)s->h_scalars[1];
-  *out = total - loops;
   return true;
 }
 
@@ -1380,8 +1415,8 @@ extern "C" capf_status capf_chain2_local_hists(capf_session *cs, capf_table *rel
       illegal("chain2_local_hists needs non-null INTEGER endpoint columns");
     if (d->nrows >= (int64_t(1) << 32)) not_impl("more than 2^32 rels per rank");
     const int64_t hlen = chain2_hist_len(n_nodes);
-    BufPtr acc = s->alloc(16);
-    HIP_CHECK(hipMemsetAsync(acc->p, 0, 16, s->stream));
+    BufPtr acc = s->alloc(24);  // [Σ (unused), self-loops, done]
+    HIP_CHECK(hipMemsetAsync(acc->p, 0, 24, s->stream));
     Chain2Args a;
     a.u1 = a.u2 = view_of(src);
     a.v1 = a.v2 = view_of(dst);
@@ -1400,7 +1435,7 @@ extern "C" capf_status capf_chain2_local_hists(capf_session *cs, capf_table *rel
     const ColStats &ss = column_stats(s, src), &sd = column_stats(s, dst);
     const bool in_range = ss.min >= a.lo && ss.max <= a.hi && sd.min >= a.lo && sd.max <= a.hi;
     const bool done = want_part && chain2_partitioned(s, pc, a.n, a.lo, a.hi, in_range, a.h1,
-                                                      a.h2, a.loops);
+                                                      a.h2, (unsigned long long *)acc->p);
     if (!done) {
       HIP_CHECK(hipMemsetAsync(d_in_hist, 0, 4 * hlen, s->stream));
       HIP_CHECK(hipMemsetAsync(d_out_hist, 0, 4 * hlen, s->stream));

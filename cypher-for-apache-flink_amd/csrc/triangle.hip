@@ -394,28 +394,36 @@ __device__ inline uint2 tri_fb(uint32_t word, const uint2 *vals, uint32_t e) {
 // taken ILP·64 at a time and software-pipelined: the words of step i+1
 // (prefix search + global loads) are issued before step i's binary searches,
 // in ping-pong registers (no copy, so no early wait on the loads in flight).
-template <int ILP, class Q, class F>
-__device__ inline void tri_row_packed(uint32_t a, uint32_t dp, const uint32_t *rowptr, const uint32_t *pcols,
-                                      const uint2 *vals, TriBatch2 &tb, Q qs, F fnd,
-                                      unsigned long long &t, unsigned long long &probes,
+// SPLIT (pass A of the two-pass schedule): the edges p→q with |N+(p)| < |N+(q)|
+// belong to pass B and are skipped here.  SWAP (pass B): the staged list is
+// N+(q) and the streamed lists are N+(p) of q's in-list entries — the roles
+// of the two looked-up words swap in the weight.  `pqe(k)`: the vals index of
+// the k-th batch entry's p–q pair (for a saturated nibble).
+// nb batch entries (qs), the staged list fnd holds ns words at vals index a.
+template <int ILP, bool SPLIT = false, bool SWAP = false, class Q, class F, class E>
+__device__ inline void tri_row_packed(uint32_t a, uint32_t nb, uint32_t ns, const uint32_t *rowptr,
+                                      const uint32_t *pcols, const uint2 *vals, TriBatch2 &tb, Q qs, F fnd,
+                                      E pqe, unsigned long long &t, unsigned long long &probes,
                                       unsigned long long &hits) {
   const int lane = lane_id();
   constexpr uint32_t STEP = ILP * WAVE;
-  for (uint32_t kb = 0; kb < dp; kb += WAVE) {
+  const uint32_t dp = ns;
+  for (uint32_t kb = 0; kb < nb; kb += WAVE) {
     const uint32_t k = kb + lane;
     uint32_t qa = 0, dq = 0, pk = 0;
-    if (k < dp) {
+    if (k < nb) {
       pk = qs(k);
       const uint32_t q = pk & TRI_M24;
       qa = rowptr[q];
       dq = rowptr[q + 1] - qa;
+      if (SPLIT && dp < dq) dq = 0;  // pass B counts this edge
     }
     const uint32_t inc = wave_inclusive_scan(dq);
     tb.pre[lane] = inc - dq;
     if (lane == WAVE - 1) tb.pre[WAVE] = inc;
     tb.qa[lane] = qa;
     tb.pk[lane] = pk;
-    tb.kk[lane] = k;
+    tb.kk[lane] = k < nb ? pqe(k) : 0u;
     const uint32_t total = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl(inc, WAVE - 1, WAVE));
     if (lane == 0) probes += total;
     __builtin_amdgcn_wave_barrier();
@@ -454,9 +462,10 @@ __device__ inline void tri_row_packed(uint32_t a, uint32_t dp, const uint32_t *r
           const uint32_t pw = fnd(lo);
           if ((pw & TRI_M24) == wk) {
             ++hits;
-            const uint2 a1 = tri_fb(tb.pk[bb[u]], vals, a + tb.kk[bb[u]]);  // p–q
-            const uint2 a2 = tri_fb(ww[u], vals, pp[u]);                     // q–w
-            const uint2 a3 = tri_fb(pw, vals, a + lo);                       // p–w
+            const uint2 a1 = tri_fb(tb.pk[bb[u]], vals, tb.kk[bb[u]]);  // p–q
+            const uint2 s2 = tri_fb(ww[u], vals, pp[u]);                 // streamed: q–w (A) / p–w (B)
+            const uint2 s3 = tri_fb(pw, vals, a + lo);                   // staged:   p–w (A) / q–w (B)
+            const uint2 a2 = SWAP ? s3 : s2, a3 = SWAP ? s2 : s3;
             // p→q→w→p  +  p→w→q→p
             t += (unsigned long long)a1.x * a2.x * a3.y + (unsigned long long)a3.x * a2.y * a1.y;
           }
@@ -475,7 +484,7 @@ __device__ inline void tri_row_packed(uint32_t a, uint32_t dp, const uint32_t *r
   }
 }
 
-template <int ILP>
+template <int ILP, bool SPLIT = false>
 __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_packed(const uint32_t *rowptr,
                                                                  const uint32_t *pcols, const uint2 *vals,
                                                                  uint64_t len, int parts, int part,
@@ -499,15 +508,88 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_packed(const uint32_t *
       if (dp < 2) continue;  // a triangle needs two out-neighbours at its lowest vertex
       if (dp > TRI_CAP) {  // rare long row: searched in global memory
         const uint32_t *row = pcols + a;
-        tri_row_packed<ILP>(a, dp, rowptr, pcols, vals, tb, [&](uint32_t k) { return row[k]; },
-                            [&](uint32_t x) { return row[x]; }, t, probes, hits);
+        tri_row_packed<ILP, SPLIT>(a, dp, dp, rowptr, pcols, vals, tb, [&](uint32_t k) { return row[k]; },
+                                   [&](uint32_t x) { return row[x]; }, [&](uint32_t k) { return a + k; }, t,
+                                   probes, hits);
         continue;
       }
       for (uint32_t k = lane; k < dp; k += WAVE) sc[k] = pcols[a + k];
       __builtin_amdgcn_wave_barrier();
-      tri_row_packed<ILP>(a, dp, rowptr, pcols, vals, tb, [&](uint32_t k) { return sc[k]; },
-                          [&](uint32_t x) { return sc[x]; }, t, probes, hits);
+      tri_row_packed<ILP, SPLIT>(a, dp, dp, rowptr, pcols, vals, tb, [&](uint32_t k) { return sc[k]; },
+                                 [&](uint32_t x) { return sc[x]; }, [&](uint32_t k) { return a + k; }, t, probes,
+                                 hits);
       __builtin_amdgcn_wave_barrier();  // sc is rewritten by the next row
+    }
+  }
+  unsigned long long tot;
+  block_exclusive_scan(t, lds, tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(&acc[0], tot);
+  block_exclusive_scan(probes, lds, tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(&acc[4], tot);
+  block_exclusive_scan(hits, lds, tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(&acc[5], tot);
+}
+
+// Pass B of the two-pass schedule (shorter list streamed): the edges p→q with
+// |N+(p)| < |N+(q)| are counted at q — N+(q) staged in LDS once, the in-list
+// p's (sorted by q, chunks of TRI_BCHUNK entries per work item so a hub's long
+// in-list spreads over waves) stream their N+(p) and binary-search each w in
+// N+(q).  Σ min(|N+(p)|, |N+(q)|) over the edges is ~2.2× below the one-pass
+// Σ |N+(q)| on R-MAT (s18 / s20).
+constexpr uint32_t TRI_BCHUNK = 1024;
+
+struct TriPassB {
+  const uint32_t *in_rowptr;  // [len + 1] into in_words / in_eidx
+  const uint32_t *in_words;   // p | multiplicity nibbles of the pair p–q
+  const uint32_t *in_eidx;    // out-CSR index of the edge p→q (vals escape)
+  const uint2 *items;         // (q, first in-list entry) per work item
+  uint32_t nitems;
+};
+
+template <int ILP>
+__global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_passb(const uint32_t *rowptr, const uint32_t *pcols,
+                                                                const uint2 *vals, TriPassB b, int parts,
+                                                                int part, unsigned long long *cursor,
+                                                                unsigned long long *acc) {
+  __shared__ uint32_t s_cols[TRI_BLOCK / WAVE][TRI_CAP];
+  __shared__ TriBatch2 s_tab[TRI_BLOCK / WAVE];
+  __shared__ unsigned long long lds[17];
+  const int wv = threadIdx.x / WAVE, lane = lane_id();
+  uint32_t *sc = s_cols[wv];
+  TriBatch2 &tb = s_tab[wv];
+  unsigned long long t = 0, probes = 0, hits = 0;
+  uint32_t staged = 0xFFFFFFFFu;  // q whose list sits in sc
+  for (;;) {
+    unsigned long long c0 = 0;
+    if (lane == 0) c0 = atomicAdd(cursor, 1ull);
+    c0 = ((unsigned long long)__shfl((long long)c0, 0, WAVE) * parts + part) * 4;
+    if (c0 >= b.nitems) break;
+    const uint64_t c1 = min<uint64_t>(c0 + 4, b.nitems);
+    for (uint64_t it = c0; it < c1; ++it) {
+      const uint2 item = b.items[it];
+      const uint32_t q = item.x;
+      const uint32_t a = rowptr[q], dq = rowptr[q + 1] - a;
+      const uint32_t i0 = b.in_rowptr[q] + item.y;
+      const uint32_t n = min(b.in_rowptr[q + 1] - i0, TRI_BCHUNK);
+      const uint32_t *inw = b.in_words + i0;
+      const uint32_t *ine = b.in_eidx + i0;
+      if (dq > TRI_CAP) {  // long N+(q): searched in global memory
+        const uint32_t *row = pcols + a;
+        tri_row_packed<ILP, false, true>(a, n, dq, rowptr, pcols, vals, tb, [&](uint32_t k) { return inw[k]; },
+                                         [&](uint32_t x) { return row[x]; }, [&](uint32_t k) { return ine[k]; },
+                                         t, probes, hits);
+        staged = 0xFFFFFFFFu;
+        continue;
+      }
+      if (q != staged) {
+        __builtin_amdgcn_wave_barrier();  // the previous list's searches are done
+        for (uint32_t k = lane; k < dq; k += WAVE) sc[k] = pcols[a + k];
+        __builtin_amdgcn_wave_barrier();
+        staged = q;
+      }
+      tri_row_packed<ILP, false, true>(a, n, dq, rowptr, pcols, vals, tb, [&](uint32_t k) { return inw[k]; },
+                                       [&](uint32_t x) { return sc[x]; }, [&](uint32_t k) { return ine[k]; },
+                                       t, probes, hits);
     }
   }
   unsigned long long tot;
@@ -531,15 +613,102 @@ static void rocprim_call(Session *s, F &&f) {
   HIP_CHECK(f(t->p, tmp));
 }
 
+// Pass-B keys: edge e = p→q (sorted oriented keys) goes to pass B when
+// |N+(p)| < |N+(q)|: key (q << 32 | p), value e; otherwise TRI_NONE.
+__global__ void k_tri_passb_keys(const uint64_t *okey, const uint32_t *rowptr, uint32_t P, uint64_t *keys,
+                                 uint32_t *eidx) {
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < P; e += gridDim.x * blockDim.x) {
+    const uint64_t k = okey[e];
+    const uint32_t pp = (uint32_t)(k >> 32), q = (uint32_t)k;
+    const uint32_t dp = rowptr[pp + 1] - rowptr[pp], dq = rowptr[q + 1] - rowptr[q];
+    keys[e] = dp < dq ? ((uint64_t)q << 32) | pp : TRI_NONE;
+    eidx[e] = e;
+  }
+}
+
+// In-list words of pass B: p with the pair's multiplicity nibbles.
+__global__ void k_tri_inlist(const uint64_t *skeys, const uint32_t *seidx, const uint32_t *pcols, uint32_t nB,
+                             uint32_t *in_words) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nB; i += gridDim.x * blockDim.x)
+    in_words[i] = (pcols[seidx[i]] & 0xFF000000u) | (uint32_t)skeys[i];
+}
+
+// Work items of pass B per q: ⌈|in-list(q)| / TRI_BCHUNK⌉ when N+(q) is non-empty.
+__global__ void k_tri_item_counts(const uint32_t *in_rowptr, const uint32_t *rowptr, uint64_t len,
+                                  uint32_t *cnt) {
+  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < len; q += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t nin = in_rowptr[q + 1] - in_rowptr[q], dq = rowptr[q + 1] - rowptr[q];
+    cnt[q] = dq > 0 ? (nin + TRI_BCHUNK - 1) / TRI_BCHUNK : 0u;
+  }
+}
+
+__global__ void k_tri_items(const uint32_t *cnt, const uint32_t *start, uint64_t len, uint2 *items) {
+  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < len; q += (uint64_t)gridDim.x * blockDim.x)
+    for (uint32_t i = 0; i < cnt[q]; ++i) items[start[q] + i] = make_uint2((uint32_t)q, i * TRI_BCHUNK);
+}
+
 // Oriented CSR of the distinct node pairs of (src, dst) over [lo, lo + len).
 struct TriGraph {
   // acc: [0] T, [1] Σ(L+L)·f·b, [2] Σ L(L−1)(L−2), [3] cursor, [4] probes (w ∈ N+(q)
   // looked up in N+(p)), [5] hits (closed triangles found)
   BufPtr rowptr, cols, vals, loops, acc;
   BufPtr pcols;  // packed column words (node ids < 2^24), else null
+  // two-pass schedule (pass B: edges with |N+(p)| < |N+(q)| counted at q)
+  BufPtr in_rowptr, in_words, in_eidx, items;
+  uint32_t nB = 0, nitems = 0;
   uint32_t P = 0;
   uint64_t len = 0;
 };
+
+// In-lists and work items of pass B (built with the CSR, cached with it).
+static void tri_build_passb(Session *s, const uint64_t *okey, TriGraph &g) {
+  const uint32_t P = g.P;
+  const uint64_t len = g.len;
+  KernelTimer kt(s, "tri_passb_build", 40.0 * P);
+  BufPtr keys = s->alloc(8 * (int64_t)P), skeys = s->alloc(8 * (int64_t)P);
+  BufPtr eidx = s->alloc(4 * (int64_t)P), seidx = s->alloc(4 * (int64_t)P);
+  hipLaunchKernelGGL(k_tri_passb_keys, dim3(grid_for(P, 256, 256 * 64)), dim3(256), 0, s->stream, okey,
+                     (const uint32_t *)g.rowptr->p, P, (uint64_t *)keys->p, (uint32_t *)eidx->p);
+  KERNEL_CHECK();
+  rocprim_call(s, [&](void *t, size_t &n) {
+    return rocprim::radix_sort_pairs(t, n, (const uint64_t *)keys->p, (uint64_t *)skeys->p,
+                                     (const uint32_t *)eidx->p, (uint32_t *)seidx->p, (size_t)P, 0, 64,
+                                     s->stream);
+  });
+  g.in_rowptr = s->alloc(4 * (len + 2));
+  hipLaunchKernelGGL(k_tri_rowptr, dim3(grid_for((int64_t)len + 1, 256, 256 * 64)), dim3(256), 0, s->stream,
+                     (const uint64_t *)skeys->p, P, len, (uint32_t *)g.in_rowptr->p);
+  KERNEL_CHECK();
+  HIP_CHECK(hipMemcpyAsync(&g.nB, (uint32_t *)g.in_rowptr->p + len, 4, hipMemcpyDeviceToHost, s->stream));
+  s->sync();
+  g.in_words = s->alloc(4 * std::max<uint32_t>(g.nB, 1));
+  g.in_eidx = s->alloc(4 * std::max<uint32_t>(g.nB, 1));
+  if (g.nB > 0) {
+    hipLaunchKernelGGL(k_tri_inlist, dim3(grid_for(g.nB, 256, 256 * 64)), dim3(256), 0, s->stream,
+                       (const uint64_t *)skeys->p, (const uint32_t *)seidx->p, (const uint32_t *)g.pcols->p, g.nB,
+                       (uint32_t *)g.in_words->p);
+    KERNEL_CHECK();
+    HIP_CHECK(hipMemcpyAsync(g.in_eidx->p, seidx->p, 4 * (size_t)g.nB, hipMemcpyDeviceToDevice, s->stream));
+  }
+  BufPtr cnt = s->alloc(4 * (len + 1)), start = s->alloc(4 * (len + 1));
+  hipLaunchKernelGGL(k_tri_item_counts, dim3(grid_for((int64_t)len, 256, 256 * 64)), dim3(256), 0, s->stream,
+                     (const uint32_t *)g.in_rowptr->p, (const uint32_t *)g.rowptr->p, len, (uint32_t *)cnt->p);
+  KERNEL_CHECK();
+  HIP_CHECK(hipMemsetAsync((uint32_t *)cnt->p + len, 0, 4, s->stream));
+  rocprim_call(s, [&](void *t, size_t &n) {
+    return rocprim::exclusive_scan(t, n, (const uint32_t *)cnt->p, (uint32_t *)start->p, 0u, (size_t)len + 1,
+                                   rocprim::plus<uint32_t>(), s->stream);
+  });
+  HIP_CHECK(hipMemcpyAsync(&g.nitems, (uint32_t *)start->p + len, 4, hipMemcpyDeviceToHost, s->stream));
+  s->sync();
+  g.items = s->alloc(8 * std::max<uint32_t>(g.nitems, 1));
+  if (g.nitems > 0) {
+    hipLaunchKernelGGL(k_tri_items, dim3(grid_for((int64_t)len, 256, 256 * 64)), dim3(256), 0, s->stream,
+                       (const uint32_t *)cnt->p, (const uint32_t *)start->p, len, (uint2 *)g.items->p);
+    KERNEL_CHECK();
+  }
+  s->sync();  // the temporaries go back to the pool
+}
 
 static void tri_build(Session *s, const ColView &src, const ColView &dst, int64_t m, int64_t lo,
                       uint64_t len, TriGraph &g) {
@@ -653,6 +822,7 @@ static void tri_build(Session *s, const ColView &src, const ColView &dst, int64_
     hipLaunchKernelGGL(k_tri_pack, dim3(grid_for(g.P, 256, 256 * 64)), dim3(256), 0, s->stream,
                        (const uint32_t *)g.cols->p, (const uint2 *)g.vals->p, g.P, (uint32_t *)g.pcols->p);
     KERNEL_CHECK();
+    tri_build_passb(s, (const uint64_t *)ok2->p, g);
   }
 }
 
@@ -684,8 +854,8 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
   const TriGraph &g = *gp;
   // per-query accumulators: T, the cached pair-loop term, Σ L(L−1)(L−2), the
   // row cursor, probes, hits
-  BufPtr qacc = s->alloc(48);
-  HIP_CHECK(hipMemsetAsync(qacc->p, 0, 48, s->stream));
+  BufPtr qacc = s->alloc(64);  // + [6] the pass-B cursor
+  HIP_CHECK(hipMemsetAsync(qacc->p, 0, 64, s->stream));
   if (part == 0)
     HIP_CHECK(hipMemcpyAsync((char *)qacc->p + 8, (const char *)g.acc->p + 8, 8,
                              hipMemcpyDeviceToDevice, s->stream));
@@ -702,11 +872,22 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
     static const int ilp = getenv("CAPF_TRI_ILP") ? atoi(getenv("CAPF_TRI_ILP")) : TRI_ILP;  // tuning
     // CAPF_TRI_PACKED=0 (tuning): the unpacked kernel (multiplicities loaded from vals per hit)
     const bool packed = !(getenv("CAPF_TRI_PACKED") && atoi(getenv("CAPF_TRI_PACKED")) == 0);
+    // CAPF_TRI_TWOPASS=0 (tuning): one pass, every wedge streamed from N+(q)
+    const bool two = packed && g.pcols && g.in_rowptr && !(getenv("CAPF_TRI_TWOPASS") && atoi(getenv("CAPF_TRI_TWOPASS")) == 0);
     if (packed && g.pcols) {
-      auto kern = ilp >= 8 ? k_tri_count_packed<8> : ilp <= 2 ? k_tri_count_packed<2> : k_tri_count_packed<4>;
+      auto kern = two ? (ilp <= 2 ? k_tri_count_packed<2, true> : k_tri_count_packed<4, true>)
+                      : (ilp >= 8 ? k_tri_count_packed<8> : ilp <= 2 ? k_tri_count_packed<2> : k_tri_count_packed<4>);
       hipLaunchKernelGGL(kern, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
                          (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
                          (const uint2 *)g.vals->p, len, parts, part, acc + 3, acc);
+      if (two && g.nitems > 0) {
+        TriPassB b{(const uint32_t *)g.in_rowptr->p, (const uint32_t *)g.in_words->p,
+                   (const uint32_t *)g.in_eidx->p, (const uint2 *)g.items->p, g.nitems};
+        auto kb = ilp <= 2 ? k_tri_count_passb<2> : k_tri_count_passb<4>;
+        hipLaunchKernelGGL(kb, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
+                           (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p, (const uint2 *)g.vals->p,
+                           b, parts, part, acc + 6, acc);
+      }
     } else {
       auto kern = filter ? (ilp >= 8 ? k_tri_count<true, 8> : ilp <= 2 ? k_tri_count<true, 2> : k_tri_count<true, 4>)
                          : (ilp >= 8 ? k_tri_count<false, 8> : ilp <= 2 ? k_tri_count<false, 2> : k_tri_count<false, 4>);

@@ -61,6 +61,24 @@ def test_two_hop_headline_p3_variant(gpu_session, monkeypatch, scale, rot):
     assert got == FULL[str(scale)]["two_hop"]
 
 
+@pytest.mark.parametrize("hocap", ["0", "2"])
+def test_two_hop_headline_handoff_spill(gpu_session, monkeypatch, hocap):
+    """P3 keeps its uint16 hand-offs in a per-unit LDS list and adds them after
+    its flush; entries beyond the list's capacity spill to a log that the dot
+    kernel folds in (Σ Δ·other + Σ Δ_in·Δ_out).  With the list capped at 0 / 2
+    entries every (most) s24 hub hand-off takes the spill path: same fixture,
+    synchronous and asynchronous."""
+    import torch
+    monkeypatch.setenv("CAPF_P3_HOCAP", hocap)
+    g = rmat_graph(gpu_session, 24, compact=3)
+    assert run(g, TWO_HOP)[0]["count"] == FULL["24"]["two_hop"]
+    slot = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    plan_query(g, TWO_HOP).table.count_async(slot.data_ptr())
+    gpu_session.sync()
+    assert slot.item() == FULL["24"]["two_hop"]
+
+
 def test_two_hop_headline_async_queue(gpu_session):
     """The pipelined bench mode (capf_table_count_async): 4 in-flight s24
     counts land the fixture in every slot."""

@@ -508,11 +508,12 @@ def run_single(args):
     # src+dst at int64 width + node ids (+ the 1-B label for config 2)
     compulsory = 16.0 * m + (9.0 if args.query == "one_hop_person" else 8.0) * n_nodes
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", f"pmc_{'tri_' if args.query == 'triangle' else ''}s{args.scale}.json")
-    if os.path.exists(pmc) and args.query in ("two_hop", "triangle"):
+    pfx = {"triangle": "tri_", "one_hop_person": "c2_"}.get(args.query, "")
+    pmc = os.path.join(ROOT, "profiles", f"pmc_{pfx}s{args.scale}.json")
+    if os.path.exists(pmc) and args.query in ("two_hop", "triangle", "one_hop_person"):
         with open(pmc) as f:
             j = json.load(f)
-            traffic = (j.get("hbm_bytes_per_query") if args.query == "two_hop" else
+            traffic = (j.get("hbm_bytes_per_query") if args.query != "triangle" else
                        next((v["read_bytes"] + v["write_bytes"] for k, v in j.get("kernels", {}).items()
                              if k.startswith("k_tri_count")), None))
     ms_per_step = median_ms

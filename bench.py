@@ -513,9 +513,9 @@ def run_single(args):
     if os.path.exists(pmc) and args.query in ("two_hop", "triangle", "one_hop_person"):
         with open(pmc) as f:
             j = json.load(f)
-            traffic = (j.get("hbm_bytes_per_query") if args.query != "triangle" else
-                       next((v["read_bytes"] + v["write_bytes"] for k, v in j.get("kernels", {}).items()
-                             if k.startswith("k_tri_count")), None))
+            tri = [v["read_bytes"] + v["write_bytes"] for k, v in j.get("kernels", {}).items()
+                   if k.startswith("k_tri_count")]  # both passes of the count
+            traffic = j.get("hbm_bytes_per_query") if args.query != "triangle" else (sum(tri) if tri else None)
     ms_per_step = median_ms
     if args.query == "triangle":
         roof = tri_roofline(prof, prof_steps, n_nodes, traffic)

@@ -451,10 +451,10 @@ bool bits_count_partitioned(Session *s, const ColView &key, int64_t n, int64_t l
 // The oriented CSR is cached on `src` (Column::index) for the pair (src, dst).
 void triangle_count_async(Session *s, const ColPtr &src, const ColPtr &dst, int64_t m,
                           int64_t lo, uint64_t len, int parts, int part, int64_t *d_out);
-// Hand-offs of the partitioned 2-hop histograms that P3 could not add itself
-// (its per-unit list was full): (hist index, side | count << 1) entries, hist
-// index mod hl = the counter; the dot kernel adds their terms.  Empty (n == 0
-// on the device) in practice.
+// Hand-offs of the partitioned 2-hop histograms (P3's uint16 counters hand
+// 2^15 off when a hub's counter fills): (hist index, side | count << 1)
+// entries, hist index mod hl = the counter; the dot kernel adds their terms
+// (a few dozen entries at R-MAT s24) instead of a separate overflow kernel.
 struct C2Spill {
   const uint2 *log = nullptr;
   const uint32_t *n = nullptr;

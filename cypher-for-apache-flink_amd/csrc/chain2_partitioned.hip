@@ -491,16 +491,13 @@ static int c3_split_x16() {
 constexpr int C3_MAXU = 4096;  // LDS capacity of the ordering pass
 
 // Also (the P1 → P3 path of the fused 2-hop count, `post` non-null): sums P1's
-// per-tile self-loops into acc3[1], clears acc3[0] (Σ in·out) and acc3[2] (the
-// dot's done counter), and clears the histogram slices of split runs (their
-// units flush with atomic adds) — the work of two memsets and k_c3_zero.
+// per-tile self-loops into acc3[1] and clears acc3[0] (Σ in·out) and acc3[2]
+// (the dot's done counter) — the work of a memset.
 struct C3Post {
   const uint32_t *tile_loops;
   int64_t ntiles;
   unsigned long long *acc3;
-  uint32_t *h_in, *h_out;
-  int64_t slice_stride;
-  C2Spill *spill;  // host side: non-null → P3 keeps hand-offs local, the log goes to the dot
+  C2Spill *spill;  // host side: non-null → the hand-off log goes to the dot kernel
 };
 
 __global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(const unsigned long long *run_total,
@@ -566,19 +563,6 @@ __global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(const unsigned long long
       post.acc3[1] = lt;
       post.acc3[2] = 0;
     }
-    // split runs: every slice of their buckets cleared (nu > S ⇔ split)
-    __shared__ uint8_t sp[2 * C3_UBLOCK];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) sp[2 * threadIdx.x + q] = nu[q] > (uint32_t)S ? 1 : 0;
-    __syncthreads();
-    for (int r = 0; r < nr; ++r) {
-      if (!sp[r]) continue;  // uniform: every thread reads the same LDS byte
-      for (int sl = 0; sl < S; ++sl) {
-        uint4 *p = (uint4 *)((r >= sd.nb ? post.h_out : post.h_in) + sl * post.slice_stride +
-                             (int64_t)(r % sd.nb) * C2_BW);
-        for (int i = threadIdx.x; i < C2_BW / 4; i += C3_UBLOCK) p[i] = make_uint4(0, 0, 0, 0);
-      }
-    }
   }
   if (!order) return;
   if (threadIdx.x <= 64) qcnt[threadIdx.x] = 0;
@@ -637,31 +621,12 @@ struct C3Ovf {
   uint32_t *n;
   uint32_t cap;
   unsigned long long *trace;  // diagnostics (CAPF_P3_TRACE): 4 words per unit, else null
-  int local;   // hand-offs kept in the unit's LDS list and added after its flush (the
-               // global log then only takes a full list's spill, applied by the dot)
-  uint32_t hocap;  // list capacity used (≤ C3_HO_CAP; CAPF_P3_HOCAP lowers it for tests)
-};
-
-// The unit's LDS list of hand-offs (C3Ovf::local): at most C3_HO_CAP per unit —
-// a unit of T keys hands off at most T / 2^15 times, so the list only spills
-// for units of more than 2^23 keys.
-constexpr uint32_t C3_HO_CAP = 256;
-struct C3HoList {
-  uint32_t *n;
-  uint2 *e;
 };
 
 // Slow path of an overflowing add (rare: a bin reached 2^15 within the unit).
 __device__ inline void c3_handoff(uint32_t *w, uint32_t inc, uint32_t hidx, uint32_t side,
-                                        const C3Ovf &o, C3HoList ho = C3HoList{nullptr, nullptr}) {
+                                        const C3Ovf &o) {
   atomicSub(w, inc << 15);
-  if (o.local && ho.n) {
-    const uint32_t j = atomicAdd(ho.n, 1u);
-    if (j < o.hocap) {
-      ho.e[j] = make_uint2(hidx, side | (1u << 16));
-      return;
-    }
-  }
   const uint32_t k = atomicAdd(o.n, 1u);
   if (k < o.cap) o.log[k] = make_uint2(hidx, side | (1u << 16));
 }
@@ -817,9 +782,6 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
   __shared__ int32_t sbase[C5APP_MAXR + 1], sk[C5APP_MAXR];
   __shared__ uint32_t lds_sc[17];
   __shared__ int64_t sbnd[2];
-  __shared__ uint32_t ho_n;
-  __shared__ uint2 ho_e[C3_HO_CAP];
-  const C3HoList hol{&ho_n, ho_e};
   int nu = units ? *nunits : 2 * sd.nb * S;
   const int nrr = 2 * sd.nb;
   if (sch.run_total) {
@@ -910,7 +872,6 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
   const uint32_t hist_base = sch.run_total ? (uint32_t)((int64_t)u.slice * C2_BW)
                                            : (uint32_t)(u.slice * slice_stride + (int64_t)(u.run % nb) * C2_BW);
   for (int i = threadIdx.x; i < C2_WORDS + C5_CORR; i += C5_BLOCK) words[i] = 0;
-  if (threadIdx.x == 0) ho_n = 0;
   __syncthreads();
   // wave-uniform values live in SGPRs: uniform loop control, no exec masking
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = lane_id();
@@ -1002,7 +963,7 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
           const uint32_t nw = o8[e] + (inc[e] << sh);
           if (inc[e] && (nw & ~o8[e] & (0x8000u << sh)))  // this add lifted its half to 2^15
             c3_handoff(&words[key[e] & (C2_WORDS - 1)], 1u << sh, (sd.packed ? log_base : hist_base) + key[e],
-                       side, ovf, hol);
+                       side, ovf);
         }
         continue;
       }
@@ -1079,7 +1040,7 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
           const uint32_t oh = (old[j][e] >> sh) & 0xFFFFu;
           if (oh < 0x8000u && oh + inc >= 0x8000u)
             c3_handoff(&words[key & (C2_WORDS - 1)], 1u << sh, (sd.packed ? log_base : hist_base) + key,
-                       side, ovf, hol);
+                       side, ovf);
         }
       }
     }
@@ -1210,16 +1171,7 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
       if (hi) atomicAdd(h + C2_WORDS, hi);
     }
   }
-  if (ovf.local) {
-    // this unit's hand-offs, after its own flush has reached L2
-    __threadfence();
-    __syncthreads();
-    const uint32_t nh = min(ho_n, ovf.hocap);
-    for (uint32_t i = threadIdx.x; i < nh; i += C5_BLOCK) {
-      const uint2 e = ho_e[i];
-      atomicAdd(&((e.y & 1u) ? h_out : h_in)[e.x], e.y >> 1);
-    }
-  }
+
   if (ovf.trace) {  // diagnostics: this unit's span, where it ran
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1338,11 +1290,10 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   ovf.log = (uint2 *)(units + max_units);
   ovf.cap = ovf_cap;
   ovf.trace = nullptr;
-  ovf.local = post && post->spill && !sd.packed ? 1 : 0;
-  {
-    const char *hc = getenv("CAPF_P3_HOCAP");  // tests: a smaller list, so hand-offs spill to the dot
-    ovf.hocap = hc ? (uint32_t)std::min<long>(std::max<long>(atol(hc), 0), (long)C3_HO_CAP) : C3_HO_CAP;
-  }
+  // the hand-off log is folded in by the dot kernel (no overflow kernel) when
+  // the caller takes it (CAPF_P3_OVFK=1, tuning/tests: the overflow kernel)
+  const char *ok_env = getenv("CAPF_P3_OVFK");
+  const bool log_to_dot = post && post->spill && !sd.packed && !(ok_env && atoi(ok_env) == 1);
   const char *trace_path = getenv("CAPF_P3_TRACE");  // diagnostics only
   BufPtr trace;
   if (trace_path) {
@@ -1372,19 +1323,14 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
     KernelTimer kt(s, "c3_units", 8.0 * nr);
     C3Post cp{};
     if (post) cp = *post;
-    if (post) {  // the split-run bins are cleared by the units kernel itself
-      cp.h_in = h_in;
-      cp.h_out = h_out;
-      cp.slice_stride = slice_stride;
-    }
     hipLaunchKernelGGL(k_c3_units, dim3(1), dim3(C3_UBLOCK), 0, s->stream,
                        (const unsigned long long *)run_total, nr, sd, S, units, nunits, split, order, cp);
     KERNEL_CHECK();
-    if (!post) {
-      hipLaunchKernelGGL(k_c3_zero, dim3(4, nr, S), dim3(256), 0, s->stream, (const int32_t *)split,
-                         sd.nb, h_in, h_out, slice_stride);
-      KERNEL_CHECK();
-    }
+    // split runs' bins cleared by a full grid (one block per (run, slice) column:
+    // the units kernel's single workgroup took 35 µs for it at s24)
+    hipLaunchKernelGGL(k_c3_zero, dim3(4, nr, S), dim3(256), 0, s->stream, (const int32_t *)split,
+                       sd.nb, h_in, h_out, slice_stride);
+    KERNEL_CHECK();
   }
   {
     KernelTimer kt(s, "c5_gather", 2.0 * nkeys);
@@ -1420,7 +1366,7 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   if (sd.packed) {  // the hand-offs are applied by k_c5_dot_packed
     *packed_ovf = ovf;
     *keep = acc;
-  } else if (ovf.local) {  // P3 added its hand-offs; a spill (if any) goes to the dot
+  } else if (log_to_dot) {  // the dot kernel adds the hand-offs' terms
     post->spill->log = ovf.log;
     post->spill->n = ovf.n;
     post->spill->cap = ovf.cap;

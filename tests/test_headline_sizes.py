@@ -61,15 +61,15 @@ def test_two_hop_headline_p3_variant(gpu_session, monkeypatch, scale, rot):
     assert got == FULL[str(scale)]["two_hop"]
 
 
-@pytest.mark.parametrize("hocap", ["0", "2"])
-def test_two_hop_headline_handoff_spill(gpu_session, monkeypatch, hocap):
-    """P3 keeps its uint16 hand-offs in a per-unit LDS list and adds them after
-    its flush; entries beyond the list's capacity spill to a log that the dot
-    kernel folds in (Σ Δ·other + Σ Δ_in·Δ_out).  With the list capped at 0 / 2
-    entries every (most) s24 hub hand-off takes the spill path: same fixture,
-    synchronous and asynchronous."""
+@pytest.mark.parametrize("ovfk", ["0", "1"], ids=["dot_folds_log", "overflow_kernel"])
+def test_two_hop_headline_handoff_paths(gpu_session, monkeypatch, ovfk):
+    """The uint16 P3 counters hand 2^15 off to a log when a hub's counter
+    fills (s24 hub in-degree 369,897).  By default the dot kernel folds the
+    log in (Σ Δ·other + Σ Δ_in·Δ_out, no overflow launch); CAPF_P3_OVFK=1 adds
+    it to the histograms with the overflow kernel first.  Same fixture both
+    ways, synchronous and asynchronous."""
     import torch
-    monkeypatch.setenv("CAPF_P3_HOCAP", hocap)
+    monkeypatch.setenv("CAPF_P3_OVFK", ovfk)
     g = rmat_graph(gpu_session, 24, compact=3)
     assert run(g, TWO_HOP)[0]["count"] == FULL["24"]["two_hop"]
     slot = torch.full((1,), -1, dtype=torch.int64, device="cuda")

@@ -167,7 +167,7 @@ def cpu_baseline(session, graph, scale, budget_s):
 
 
 # kernels of one fused 2-hop count (fused_count.hip + chain2_partitioned.hip)
-PIPELINE = ("c5_partition", "c3_transpose", "c3_units", "c5_gather", "c3_overflow", "chain2_hist", "message_pass",
+PIPELINE = ("c5_partition", "c3_transpose", "c3_units", "c3_zero", "c5_gather", "c3_overflow", "chain2_hist", "message_pass",
             "semi_partition", "semi_count",
             "chain2_dot", "tri_keys", "tri_sort_keys", "tri_rle", "tri_pairs", "tri_orient",
             "tri_sort_pairs", "tri_rowptr", "tri_split", "tri_loop3", "tri_count",
@@ -554,6 +554,8 @@ def run_single(args):
         result["config"]["ms_per_step_pipelined"] = pipelined_ms
         result["config"]["joined_rows_per_s_pipelined"] = count / (pipelined_ms * 1e-3)
     result["config"]["first_query_ms"] = first_query_ms
+    if "c3_handoffs" in prof:  # uint16 P3 counter hand-offs folded in by the dot kernel
+        result["config"]["p3_handoffs_per_query"] = prof["c3_handoffs"]["bytes"] / prof_steps
     result["config"]["parity"] = check_fixture(args, count)
     if not args.no_cpu and args.query == "two_hop":
         result["cpu_baseline"] = cpu_baseline(s, g, args.scale, args.cpu_seconds)

@@ -1328,9 +1328,12 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
     KERNEL_CHECK();
     // split runs' bins cleared by a full grid (one block per (run, slice) column:
     // the units kernel's single workgroup took 35 µs for it at s24)
-    hipLaunchKernelGGL(k_c3_zero, dim3(4, nr, S), dim3(256), 0, s->stream, (const int32_t *)split,
-                       sd.nb, h_in, h_out, slice_stride);
-    KERNEL_CHECK();
+    {
+      KernelTimer kz(s, "c3_zero", 0.0);
+      hipLaunchKernelGGL(k_c3_zero, dim3(4, nr, S), dim3(256), 0, s->stream, (const int32_t *)split,
+                         sd.nb, h_in, h_out, slice_stride);
+      KERNEL_CHECK();
+    }
   }
   {
     KernelTimer kt(s, "c5_gather", 2.0 * nkeys);

@@ -369,18 +369,69 @@ __global__ __launch_bounds__(256) void k_chain2_dot(const uint32_t *h1, const ui
   __syncthreads();
   if (!last) return;
   __threadfence();
+  // Σ(x+X)(y+Y) − Σxy = Σ_in Δ·(y + Y) + Σ_out Δ·x: the out-side deltas Y are
+  // first summed per counter in an LDS open-addressing map, then every entry
+  // reads its counters once (independent loads, no serial chain)
+  constexpr uint32_t MAPN = 2048;  // slots; up to MAPN / 2 distinct out-side counters
+  __shared__ uint32_t mk[MAPN];
+  __shared__ unsigned long long mv[MAPN];
+  __shared__ int map_full;
   unsigned long long corr = 0;
   const uint32_t ne = sp.n ? min(*sp.n, sp.cap) : 0u;
-  for (uint32_t e = threadIdx.x; e < ne; e += blockDim.x) {
-    const uint2 x = sp.log[e];
-    const int64_t b = (int64_t)x.x % sp.hl;
-    const unsigned long long d = x.y >> 1;
-    corr += d * ((x.y & 1u) ? h1[b] : h2[b]);
-    if (!(x.y & 1u))  // in-side entry: pairs with every out-side entry of the same counter
-      for (uint32_t f = 0; f < ne; ++f) {
-        const uint2 y = sp.log[f];
-        if ((y.y & 1u) && (int64_t)y.x % sp.hl == b) corr += d * (y.y >> 1);
+  if (ne > 0) {
+    for (uint32_t i = threadIdx.x; i < MAPN; i += blockDim.x) {
+      mk[i] = 0xFFFFFFFFu;
+      mv[i] = 0;
+    }
+    if (threadIdx.x == 0) map_full = 0;
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < ne; e += blockDim.x) {
+      const uint2 y = sp.log[e];
+      if (!(y.y & 1u)) continue;
+      const uint32_t b = (uint32_t)((int64_t)y.x % sp.hl);
+      uint32_t h = (b * 0x9E3779B1u) & (MAPN - 1), probes = 0;
+      for (;;) {
+        const uint32_t prev = atomicCAS(&mk[h], 0xFFFFFFFFu, b);
+        if (prev == 0xFFFFFFFFu || prev == b) {
+          atomicAdd(&mv[h], (unsigned long long)(y.y >> 1));
+          break;
+        }
+        h = (h + 1) & (MAPN - 1);
+        if (++probes > MAPN / 2) {
+          map_full = 1;
+          break;
+        }
       }
+    }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < ne; e += blockDim.x) {
+      const uint2 x = sp.log[e];
+      const int64_t b = (int64_t)x.x % sp.hl;
+      const unsigned long long d = x.y >> 1;
+      if (x.y & 1u) {
+        corr += d * h1[b];
+      } else {
+        unsigned long long Y = 0;
+        if (!map_full) {
+          uint32_t h = ((uint32_t)b * 0x9E3779B1u) & (MAPN - 1);
+          for (uint32_t k = 0; k < MAPN; ++k) {
+            const uint32_t c = mk[h];
+            if (c == (uint32_t)b) {
+              Y = mv[h];
+              break;
+            }
+            if (c == 0xFFFFFFFFu) break;
+            h = (h + 1) & (MAPN - 1);
+          }
+        } else {  // (pathological: > MAPN/2 distinct out-side counters) scan the log
+          for (uint32_t f = 0; f < ne; ++f) {
+            const uint2 y = sp.log[f];
+            if ((y.y & 1u) && (int64_t)y.x % sp.hl == b) Y += y.y >> 1;
+          }
+        }
+        corr += d * (h2[b] + Y);
+      }
+    }
   }
   corr = block_reduce_sum(corr, lds);
   if (threadIdx.x == 0) {
@@ -1258,6 +1309,12 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
     }
     *out = 0;
     return true;
+  }
+  if (s->profiling && spill.n) {  // diagnostics (profiling mode only): hand-off log entries
+    uint32_t ne = 0;
+    HIP_CHECK(hipMemcpyAsync(&ne, spill.n, 4, hipMemcpyDeviceToHost, s->stream));
+    s->sync();
+    s->profile["c3_handoffs"].bytes += (double)ne;
   }
   if (fin_done) {
     s->sync();

@@ -213,7 +213,8 @@ template <int W, bool ALIAS, bool CHECK, bool RAGGED, class SH, int DIAG = 0, in
 __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_c5_partition(C5Cols<W> c, uint16_t *part,
                                                             uint32_t *meta,
                                                             uint32_t *tile_loops,
-                                                            int64_t t_base, uint32_t *zbuf, int zwords) {
+                                                            int64_t t_base, uint32_t *zbuf, int zwords,
+                                                            unsigned long long *zacc) {
   constexpr int TILE = SH::TILE, MAXR = SH::MAXR;
   constexpr int RPT = TILE / C5_BLOCK, GROUPS = RPT / 4;
   constexpr int STAGE = c5_stage_keys<SH>();
@@ -232,6 +233,7 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   for (int i = threadIdx.x; i <= nr; i += C5_BLOCK) cur[i] = 0;
   if (t == 0 && zbuf)
     for (int i = threadIdx.x; i < zwords; i += C5_BLOCK) zbuf[i] = 0;
+  if (t == 0 && zacc && threadIdx.x < 3) zacc[threadIdx.x] = 0;  // [Σ, loops, done]
   __syncthreads();
   const int64_t e0 = t * TILE;
   const int64_t e1 = RAGGED ? min(e0 + TILE, c.n) : e0 + TILE;
@@ -404,10 +406,14 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
 // block (a per-block partial row summed by k_c3_units instead was measured
 // slower: the one-block units kernel turns latency bound).
 constexpr int C3_TT = 256;
+// tile_loops (2-hop pipeline): the blocks of run row 0 also add their tiles'
+// self-loop counts (P1's per-tile plain stores) into *loops.
 __global__ __launch_bounds__(256) void k_c3_transpose(const uint32_t *meta, uint32_t *meta_t,
                                                        int64_t ntiles, int nr,
                                                        unsigned long long *run_total, int64_t tt,
-                                                       uint32_t *bsum = nullptr) {
+                                                       uint32_t *bsum = nullptr,
+                                                       const uint32_t *tile_loops = nullptr,
+                                                       unsigned long long *loops = nullptr) {
   __shared__ uint32_t tilebuf[C3_TT][33];
   __shared__ uint32_t part[8][33];
   const int r0 = blockIdx.y * 32;
@@ -423,6 +429,12 @@ __global__ __launch_bounds__(256) void k_c3_transpose(const uint32_t *meta, uint
     cnt += v >> 16;
   }
   part[ty][tx] = cnt;
+  if (tile_loops && blockIdx.y == 0 && threadIdx.x < 64) {  // one wave: this block's tiles
+    unsigned long long l = 0;
+    for (int64_t k = threadIdx.x; k < tn; k += 64) l += tile_loops[tb + k];
+    l = wave_reduce_sum(l);
+    if (threadIdx.x == 0 && l) atomicAdd(loops, l);
+  }
   __syncthreads();
   if (ty == 0) {
     uint32_t c = 0;
@@ -490,9 +502,9 @@ static int c3_split_x16() {
 // wave and the short ones fill the tail.
 constexpr int C3_MAXU = 4096;  // LDS capacity of the ordering pass
 
-// Also (the P1 → P3 path of the fused 2-hop count, `post` non-null): sums P1's
-// per-tile self-loops into acc3[1] and clears acc3[0] (Σ in·out) and acc3[2]
-// (the dot's done counter) — the work of a memset.
+// The P1 → P3 path of the fused 2-hop count: P1's per-tile self-loops (summed
+// into acc3[1] by the transpose), acc3 = [Σ in·out, self-loops, done] cleared
+// by P1's tile-0 workgroup, and where the hand-off log goes.
 struct C3Post {
   const uint32_t *tile_loops;
   int64_t ntiles;
@@ -553,17 +565,7 @@ __global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(const unsigned long long
     split[r] = nu[q] > (uint32_t)S;
   }
   if (threadIdx.x == 0) *nunits = (int32_t)ntot;
-  if (post.acc3) {
-    unsigned long long lsum = 0;
-    for (int64_t t = threadIdx.x; t < post.ntiles; t += C3_UBLOCK) lsum += post.tile_loops[t];
-    unsigned long long lt;
-    block_exclusive_scan(lsum, lds64, lt);
-    if (threadIdx.x == 0) {
-      post.acc3[0] = 0;
-      post.acc3[1] = lt;
-      post.acc3[2] = 0;
-    }
-  }
+
   if (!order) return;
   if (threadIdx.x <= 64) qcnt[threadIdx.x] = 0;
   if (threadIdx.x == 0) maxest = 0;
@@ -1196,7 +1198,7 @@ __global__ __launch_bounds__(256) void k_c3_overflow(C3Ovf o, uint32_t *h_in, ui
 
 template <int W, bool ALIAS, bool CHECK, class SH>
 static void launch_c5(Session *s, const C5Cols<W> &c, uint16_t *part, uint32_t *meta,
-                      uint32_t *tile_loops, uint32_t *zbuf, int zwords) {
+                      uint32_t *tile_loops, uint32_t *zbuf, int zwords, unsigned long long *zacc) {
   const int64_t nfull = c.n / SH::TILE;
   if (nfull > 0) {
     const char *dg = getenv("CAPF_P1_DIAG");  // diagnostics only: wrong counts
@@ -1213,12 +1215,12 @@ static void launch_c5(Session *s, const C5Cols<W> &c, uint16_t *part, uint32_t *
                 : upf       ? k_c5_partition<W, ALIAS, CHECK, false, SH, 0, 1>
                             : k_c5_partition<W, ALIAS, CHECK, false, SH, 0>;
     hipLaunchKernelGGL(kern, dim3((unsigned)nfull), dim3(C5_BLOCK), 0, s->stream, c, part, meta,
-                       tile_loops, (int64_t)0, zbuf, zwords);
+                       tile_loops, (int64_t)0, zbuf, zwords, zacc);
     KERNEL_CHECK();
   }
   if (nfull < c.ntiles) {  // the ragged last tile
     hipLaunchKernelGGL((k_c5_partition<W, ALIAS, true, true, SH>), dim3(1), dim3(C5_BLOCK), 0,
-                       s->stream, c, part, meta, tile_loops, nfull, zbuf, zwords);
+                       s->stream, c, part, meta, tile_loops, nfull, zbuf, zwords, zacc);
     KERNEL_CHECK();
   }
 }
@@ -1316,7 +1318,8 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
     KernelTimer kt(s, "c3_transpose", 8.0 * nr * ntiles);
     hipLaunchKernelGGL(k_c3_transpose, dim3((unsigned)nparts, (nr + 31) / 32), dim3(256), 0,
                        s->stream, meta, transpose ? (uint32_t *)meta_t->p : nullptr, ntiles, nr,
-                       run_total, tt, app ? (uint32_t *)bsum->p : nullptr);
+                       run_total, tt, app ? (uint32_t *)bsum->p : nullptr,
+                       post ? post->tile_loops : nullptr, post ? post->acc3 + 1 : nullptr);
     KERNEL_CHECK();
   }
   if (!static_units) {
@@ -1555,10 +1558,10 @@ static void chain2_c5(Session *s, C5Cols<W> c, bool in_range, uint32_t *h_in, ui
     uint32_t *tlp = (uint32_t *)tl->p, *zb = (uint32_t *)post_acc->p;
     const int zw = c5_post_zero_words(nr);
     const bool alias = c.u2 == c.u1 && c.v2 == c.v1;
-    if (alias && !in_range) launch_c5<W, true, true, SH>(s, c, pp, mp, tlp, zb, zw);
-    if (alias && in_range) launch_c5<W, true, false, SH>(s, c, pp, mp, tlp, zb, zw);
-    if (!alias && !in_range) launch_c5<W, false, true, SH>(s, c, pp, mp, tlp, zb, zw);
-    if (!alias && in_range) launch_c5<W, false, false, SH>(s, c, pp, mp, tlp, zb, zw);
+    if (alias && !in_range) launch_c5<W, true, true, SH>(s, c, pp, mp, tlp, zb, zw, d_acc3);
+    if (alias && in_range) launch_c5<W, true, false, SH>(s, c, pp, mp, tlp, zb, zw, d_acc3);
+    if (!alias && !in_range) launch_c5<W, false, true, SH>(s, c, pp, mp, tlp, zb, zw, d_acc3);
+    if (!alias && in_range) launch_c5<W, false, false, SH>(s, c, pp, mp, tlp, zb, zw, d_acc3);
   }
   C3Post post{};
   post.tile_loops = (const uint32_t *)tl->p;

@@ -211,10 +211,18 @@ def call(name, *args):
     return status
 
 
+_STRS = {}  # encoded name arrays per name tuple (read-only on the C side; plans repeat them)
+
+
 def strs(values):
-    arr = (c_char_p * max(len(values), 1))()
-    for i, v in enumerate(values):
-        arr[i] = v.encode() if isinstance(v, str) else v
+    key = tuple(values)
+    arr = _STRS.get(key)
+    if arr is None:
+        arr = (c_char_p * max(len(key), 1))()
+        for i, v in enumerate(key):
+            arr[i] = v.encode() if isinstance(v, str) else v
+        if len(_STRS) < 16384:
+            _STRS[key] = arr
     return arr
 
 

@@ -313,71 +313,18 @@ __global__ __launch_bounds__(256) void k_chain2_hist(Chain2Args a) {
 // fin != null (capf_table_count_async): the workgroup whose `done` add comes
 // last writes *fin = acc[0] − acc[1] (Σ in·out − self-loops) — the count on the
 // device without a separate one-thread kernel.
-// sp (partitioned pipeline, ONES): hand-offs P3 left in the log — the last
-// block adds Σ Δ·(other side) + Σ Δ_in·Δ_out over equal counters before fin.
-template <bool ONES>
-__global__ __launch_bounds__(256) void k_chain2_dot(const uint32_t *h1, const uint32_t *h2,
-                                                    DMap wb, int64_t lo, int64_t len,
-                                                    unsigned long long *acc, int64_t *fin = nullptr,
-                                                    unsigned int *done = nullptr, C2Spill sp = C2Spill()) {
-  __shared__ unsigned long long lds[17];
-  unsigned long long s = 0;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  // 4 counters per thread per step: dwordx4 loads of both histograms
-  const int64_t n4 = len / 4;
-  const uint4 *a4 = (const uint4 *)h1;
-  const uint4 *b4 = (const uint4 *)h2;
-  int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (ONES) {
-    // 4 independent dwordx4 pairs in flight per thread before the first use
-    for (; i0 + 3 * stride < n4; i0 += 4 * stride) {
-      uint4 x[4], y[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        x[k] = a4[i0 + k * stride];
-        y[k] = b4[i0 + k * stride];
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        s += (unsigned long long)x[k].x * y[k].x + (unsigned long long)x[k].y * y[k].y +
-             (unsigned long long)x[k].z * y[k].z + (unsigned long long)x[k].w * y[k].w;
-    }
-  }
-  for (int64_t i = i0; i < n4; i += stride) {
-    uint4 x = a4[i], y = b4[i];
-    if (ONES) {
-      s += (unsigned long long)x.x * y.x + (unsigned long long)x.y * y.y +
-           (unsigned long long)x.z * y.z + (unsigned long long)x.w * y.w;
-    } else {
-      int64_t k = lo + 4 * i;
-      s += (unsigned long long)x.x * y.x * w_of<false>(wb, k) +
-           (unsigned long long)x.y * y.y * w_of<false>(wb, k + 1) +
-           (unsigned long long)x.z * y.z * w_of<false>(wb, k + 2) +
-           (unsigned long long)x.w * y.w * w_of<false>(wb, k + 3);
-    }
-  }
-  for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < len; i += stride)
-    s += (unsigned long long)h1[i] * h2[i] * (ONES ? 1ull : w_of<false>(wb, lo + i));
-  s = block_reduce_sum(s, lds);
-  if (threadIdx.x == 0 && s) atomicAdd(acc, s);
-  if (!fin) return;
-  __shared__ int last;
-  if (threadIdx.x == 0) {
-    __threadfence();
-    last = atomicAdd(done, 1u) == gridDim.x - 1;  // every other block's add has landed
-  }
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  // Σ(x+X)(y+Y) − Σxy = Σ_in Δ·(y + Y) + Σ_out Δ·x: the out-side deltas Y are
-  // first summed per counter in an LDS open-addressing map, then every entry
-  // reads its counters once (independent loads, no serial chain)
+// Σ over the hand-off log of (Σ(x+X)(y+Y) − Σxy) = Σ_in Δ·(y + Y) + Σ_out Δ·x
+// (x, y: the stored counters, X, Y: their hand-offs).  One workgroup: the
+// out-side deltas Y are summed per counter in an LDS open-addressing map, then
+// every entry reads its counters once (independent loads).
+__device__ unsigned long long c2_handoff_terms(const uint32_t *h1, const uint32_t *h2, const C2Spill &sp,
+                                               unsigned long long *lds) {
   constexpr uint32_t MAPN = 2048;  // slots; up to MAPN / 2 distinct out-side counters
   __shared__ uint32_t mk[MAPN];
   __shared__ unsigned long long mv[MAPN];
   __shared__ int map_full;
   unsigned long long corr = 0;
-  const uint32_t ne = sp.n ? min(*sp.n, sp.cap) : 0u;
+  const uint32_t ne = min(*sp.n, sp.cap);
   if (ne > 0) {
     for (uint32_t i = threadIdx.x; i < MAPN; i += blockDim.x) {
       mk[i] = 0xFFFFFFFFu;
@@ -433,13 +380,74 @@ __global__ __launch_bounds__(256) void k_chain2_dot(const uint32_t *h1, const ui
       }
     }
   }
-  corr = block_reduce_sum(corr, lds);
+  return block_reduce_sum(corr, lds);
+}
+
+// fin != null (the fused count): the workgroup whose `done` add comes last
+// writes *fin = acc[0] − acc[1] (Σ in·out − self-loops) — into the async slot
+// or the pinned host scalar, without a separate kernel or copy.  sp.n != null
+// (the partitioned pipeline): the LAST workgroup of the grid computes the
+// hand-off terms (beside the others' dot, not after it) and adds them to acc[0].
+template <bool ONES>
+__global__ __launch_bounds__(256) void k_chain2_dot(const uint32_t *h1, const uint32_t *h2,
+                                                    DMap wb, int64_t lo, int64_t len,
+                                                    unsigned long long *acc, int64_t *fin = nullptr,
+                                                    unsigned int *done = nullptr, C2Spill sp = C2Spill()) {
+  __shared__ unsigned long long lds[17];
+  unsigned long long s = 0;
+  const unsigned nblk = gridDim.x - (sp.n ? 1u : 0u);  // dot workgroups
+  if (sp.n && blockIdx.x == nblk) {
+    s = c2_handoff_terms(h1, h2, sp, lds);
+  } else {
+    const int64_t stride = (int64_t)nblk * blockDim.x;
+    // 4 counters per thread per step: dwordx4 loads of both histograms
+    const int64_t n4 = len / 4;
+    const uint4 *a4 = (const uint4 *)h1;
+    const uint4 *b4 = (const uint4 *)h2;
+    int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (ONES) {
+      // 4 independent dwordx4 pairs in flight per thread before the first use
+      for (; i0 + 3 * stride < n4; i0 += 4 * stride) {
+        uint4 x[4], y[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          x[k] = a4[i0 + k * stride];
+          y[k] = b4[i0 + k * stride];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          s += (unsigned long long)x[k].x * y[k].x + (unsigned long long)x[k].y * y[k].y +
+               (unsigned long long)x[k].z * y[k].z + (unsigned long long)x[k].w * y[k].w;
+      }
+    }
+    for (int64_t i = i0; i < n4; i += stride) {
+      uint4 x = a4[i], y = b4[i];
+      if (ONES) {
+        s += (unsigned long long)x.x * y.x + (unsigned long long)x.y * y.y +
+             (unsigned long long)x.z * y.z + (unsigned long long)x.w * y.w;
+      } else {
+        int64_t k = lo + 4 * i;
+        s += (unsigned long long)x.x * y.x * w_of<false>(wb, k) +
+             (unsigned long long)x.y * y.y * w_of<false>(wb, k + 1) +
+             (unsigned long long)x.z * y.z * w_of<false>(wb, k + 2) +
+             (unsigned long long)x.w * y.w * w_of<false>(wb, k + 3);
+      }
+    }
+    for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < len; i += stride)
+      s += (unsigned long long)h1[i] * h2[i] * (ONES ? 1ull : w_of<false>(wb, lo + i));
+    s = block_reduce_sum(s, lds);
+  }
+  if (threadIdx.x == 0 && s) atomicAdd(acc, s);
+  if (!fin) return;
   if (threadIdx.x == 0) {
-    const unsigned long long a0 = atomicAdd(acc, 0ull) + corr, a1 = atomicAdd(acc + 1, 0ull);
-    atomicAdd(acc, corr);  // acc[0] holds the corrected Σ for readers of acc
-    // fin may be pinned host memory: a system-scope store
-    __hip_atomic_store(fin, (int64_t)(a0 - a1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __threadfence_system();
+    __threadfence();
+    if (atomicAdd(done, 1u) == gridDim.x - 1) {  // every other block's add has landed
+      __threadfence();
+      const unsigned long long a0 = atomicAdd(acc, 0ull), a1 = atomicAdd(acc + 1, 0ull);
+      // fin may be pinned host memory: a system-scope store
+      __hip_atomic_store(fin, (int64_t)(a0 - a1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __threadfence_system();
+    }
   }
 }
 
@@ -1289,8 +1297,8 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
       // host scalar the synchronous path reads after its sync (no D2H copy)
       int64_t *fin = s->async_out ? s->async_out : s->h_scalars;
       unsigned int *done = (unsigned int *)((unsigned long long *)acc->p + 2);
-      if (wb.ones)  // ONES: Σ in·out is invariant under the node_mix bijection
-        hipLaunchKernelGGL(k_chain2_dot<true>, dim3(grid), dim3(256), 0, s->stream, h1, h2,
+      if (wb.ones)  // ONES: Σ in·out is invariant under the node_mix bijection (+1 block: hand-offs)
+        hipLaunchKernelGGL(k_chain2_dot<true>, dim3(grid + (spill.n ? 1 : 0)), dim3(256), 0, s->stream, h1, h2,
                            wb.map.m, lo, dot_len, (unsigned long long *)acc->p, fin, done, spill);
       else
         hipLaunchKernelGGL(k_chain2_dot<false>, dim3(grid), dim3(256), 0, s->stream, h1, h2,

@@ -65,6 +65,18 @@ def one_hop_rows_query():
                  [Stage([("a", Var("a", "NODE")), ("b", Var("b", "NODE"))])])
 
 
+def var2_rows_query():
+    """MATCH (a)-[*2..2]->(b) RETURN a, b — the relational VarLengthExpand
+    (VarLengthExpandPlanner.scala:82-135): the path step joins end(r_1) =
+    start(r_2), a many-to-many join of two rel scans (no unique side: the
+    radix-partitioned join's case), then the uniqueness filter r_1 <> r_2 and
+    the target join."""
+    from capf_amd.expr import Var
+    from capf_amd.planner import Match, NodeP, Query, RelP, Stage
+    return Query([Match([NodeP("a"), NodeP("b")], [RelP("r", "a", "b", length=(2, 2))])],
+                 [Stage([("a", Var("a", "NODE")), ("b", Var("b", "NODE"))])])
+
+
 def reach_query(upper=3):
     """Config 5: MATCH (a:Person)-[:KNOWS*1..3]->(b:Person) WITH DISTINCT a, b
     WITH a, count(*) AS reach RETURN reach, count(*) AS n."""
@@ -78,6 +90,8 @@ def reach_query(upper=3):
 
 
 def workload_name(args):
+    if args.query == "var2_rows":
+        return f"R-MAT s{args.scale} MATCH (a)-[*2..2]->(b) RETURN a, b (relational var-length, rows in HBM)"
     if args.query == "one_hop_rows":
         return (f"R-MAT s{args.scale} 1-hop MATCH (a)-->(b) RETURN a, b (rows materialised in HBM)"
                 + (f", sparse node ids v*{args.id_stride}+7" if args.id_stride != 1 else ""))
@@ -274,12 +288,17 @@ def run_rows_leg(args):
     from capf_amd.table import GpuSession
     s = GpuSession(0)
     g = rmat_graph(s, args.scale, args.edge_factor, compact=True, id_stride=args.id_stride)
-    q = one_hop_rows_query()
+    var2 = args.query == "var2_rows"
+    q = var2_rows_query() if var2 else one_hop_rows_query()
     n_nodes = 1 << args.scale
     m = args.edge_factor << args.scale
     step = lambda: plan_query(g, q).table.materialize()  # noqa: E731
     rows = plan_query(g, q).table.size
-    if rows != m:
+    if var2:  # one row per 2-path with distinct rels: the 2-hop count fixture
+        want = fixture_count("two_hop", args.scale, args.edge_factor)
+        if want is not None and rows != want:
+            raise SystemExit(f"{rows} rows, expected the 2-hop fixture {want}")
+    elif rows != m:
         raise SystemExit(f"{rows} rows, expected one per rel ({m})")
     for _ in range(args.warmup):
         step()
@@ -299,7 +318,8 @@ def run_rows_leg(args):
     prof = s.profile()
     per = {k: v["total_ms"] / prof_steps for k, v in prof.items()}
     kern_ms = sum(per.values())
-    compulsory = 16.0 * m + 16.0 * n_nodes + 18.0 * rows
+    # var2: both rel scans are read (the path step and its start/target joins)
+    compulsory = (32.0 if var2 else 16.0) * m + 16.0 * n_nodes + 18.0 * rows
     ms = elapsed * 1e3 / args.steps
     print(json.dumps({
         "metric": ROWS_METRIC, "value": rows * args.steps / elapsed, "unit": "joined rows/s", "n_gpus": 1,
@@ -799,7 +819,8 @@ def main():
     ap.add_argument("--int64", action="store_true", help="keep the id columns int64 (no FOR encoding)")
     ap.add_argument("--for32", action="store_true", help="FOR32 id columns instead of FOR24")
     ap.add_argument("--dist", action="store_true", help="distributed path even at world size 1")
-    ap.add_argument("--query", choices=["two_hop", "triangle", "one_hop_person", "one_hop_rows", "reach"],
+    ap.add_argument("--query", choices=["two_hop", "triangle", "one_hop_person", "one_hop_rows", "var2_rows",
+                                        "reach"],
                     default="two_hop",
                     help="two_hop: the headline (config 3); triangle: config 4; one_hop_person: config 2; "
                          "reach: config 5")
@@ -811,7 +832,7 @@ def main():
                     help="multi-GPU graph layout (N > 1): node-partitioned copies or edge-range shards")
     args = ap.parse_args()
     if args.scale is None:
-        args.scale = 16 if args.query == "reach" else 24
+        args.scale = 16 if args.query == "reach" else 14 if args.query == "var2_rows" else 24
     if args.edge_factor is None:
         args.edge_factor = 30 if args.query == "reach" else 16
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -819,7 +840,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus and "WORLD_SIZE" in os.environ:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    if args.query == "one_hop_rows":
+    if args.query in ("one_hop_rows", "var2_rows"):
         run_rows_leg(args)
     elif args.query == "reach":
         run_reach_leg(args)

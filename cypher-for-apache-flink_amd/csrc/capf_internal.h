@@ -460,6 +460,11 @@ struct C2Spill {
   const uint32_t *n = nullptr;
   uint32_t cap = 0;
   int64_t hl = 0;
+  // non-null: bucket layout per run (runs [0, nb) in, [nb, 2·nb) out): split[r] = 0 →
+  // packed uint16 pairs in the first 2^15 words of the bucket (word i: bin i low,
+  // bin i + 2^15 high), 1 → one uint32 per bin
+  const int32_t *split = nullptr;
+  int nb = 0;
 };
 // d_acc3 = [Σ in·out, self-loops, done counter] (device): the pipeline writes
 // the self-loop total into [1] and clears [0] and [2] itself (no memset needed)

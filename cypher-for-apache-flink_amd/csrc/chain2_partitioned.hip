@@ -488,6 +488,9 @@ struct C3Sides {
                        // (word i of bucket b of slice k at (k·nb + b)·2^15 + i); the
                        // hand-off log then holds side bins b·2^16 + key, applied by
                        // k_c5_dot_packed (no k_c3_overflow)
+  int pairs = 0;       // (fused 2-hop, one slice) exclusive units store packed uint16
+                       // pairs in the first half of their bucket's 2^16 words (half
+                       // the flush and dot bytes); split runs keep one uint32 per bin
 };
 
 // CAPF_P3_SPLIT (tuning): split threshold in units of the mean run size
@@ -1161,6 +1164,10 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
     uint32_t *h = hist + ((int64_t)u.slice * nb + u.run % nb) * C2_WORDS;
     for (int i = threadIdx.x; i < C2_WORDS; i += C5_BLOCK) h[i] = words[i] - (i < C5_CORR ? corr[i] : 0u);
   } else
+  if (sd.pairs && u.exclusive) {  // packed pairs (lo: bin i, hi: bin i + 2^15)
+    uint32_t *h = hist + hist_base;
+    for (int i = threadIdx.x; i < C2_WORDS; i += C5_BLOCK) h[i] = words[i] - (i < C5_CORR ? corr[i] : 0u);
+  } else
   for (int i = threadIdx.x; i < C2_WORDS; i += C5_BLOCK) {
     const uint32_t w = words[i];
     const uint32_t lo = (w & 0xFFFF) - (i < C5_CORR ? corr[i] : 0u), hi = w >> 16;
@@ -1377,6 +1384,8 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
     post->spill->n = ovf.n;
     post->spill->cap = ovf.cap;
     post->spill->hl = slice_stride;
+    post->spill->split = sd.pairs ? split : nullptr;  // per run: 1 = uint32 bins, 0 = packed pairs
+    post->spill->nb = sd.nb;
   } else {
     KernelTimer kt(s, "c3_overflow", 0.0);
     hipLaunchKernelGGL(k_c3_overflow, dim3(16), dim3(256), 0, s->stream, ovf, h_in, h_out);
@@ -1569,6 +1578,11 @@ static void chain2_c5(Session *s, C5Cols<W> c, bool in_range, uint32_t *h_in, ui
   post.acc3 = d_acc3;
   post.spill = spill;
   const int64_t hl = (int64_t)c.nb * C2_BW;
+  {
+    const char *pe = getenv("CAPF_HIST_PAIRS");  // 0 (tuning): one uint32 per bin everywhere
+    const char *ok_env = getenv("CAPF_P3_OVFK");
+    sd.pairs = S == 1 && spill && !(pe && atoi(pe) == 0) && !(ok_env && atoi(ok_env) == 1) ? 1 : 0;
+  }
   if (S == 1) {
     c5_post(s, (const uint16_t *)part->p, (const uint32_t *)meta->p, sd, c.ntiles, c.rstride,
             2 * c.n, 1, h_in, h_out, hl, false, nullptr, nullptr, nullptr, &post, post_acc);

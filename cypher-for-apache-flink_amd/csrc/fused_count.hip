@@ -317,6 +317,16 @@ __global__ __launch_bounds__(256) void k_chain2_hist(Chain2Args a) {
 // (x, y: the stored counters, X, Y: their hand-offs).  One workgroup: the
 // out-side deltas Y are summed per counter in an LDS open-addressing map, then
 // every entry reads its counters once (independent loads).
+// Counter `bin` of one side (h) as stored: one uint32, or (split layout given
+// and the bin's run unsplit) the half of the bucket's packed pair word.
+constexpr int64_t C2P_BW = int64_t(1) << 16;  // bins per bucket (chain2_partitioned.hip C2_BW)
+__device__ inline uint32_t c2_stored(const uint32_t *h, const C2Spill &sp, int side, int64_t bin) {
+  if (!sp.split) return h[bin];
+  const int64_t b = bin / C2P_BW, k = bin % C2P_BW;
+  if (sp.split[side * sp.nb + b]) return h[bin];
+  return (h[b * C2P_BW + (k & (C2P_BW / 2 - 1))] >> ((k >> 15) * 16)) & 0xFFFFu;
+}
+
 __device__ unsigned long long c2_handoff_terms(const uint32_t *h1, const uint32_t *h2, const C2Spill &sp,
                                                unsigned long long *lds) {
   constexpr uint32_t MAPN = 2048;  // slots; up to MAPN / 2 distinct out-side counters
@@ -356,7 +366,7 @@ __device__ unsigned long long c2_handoff_terms(const uint32_t *h1, const uint32_
       const int64_t b = (int64_t)x.x % sp.hl;
       const unsigned long long d = x.y >> 1;
       if (x.y & 1u) {
-        corr += d * h1[b];
+        corr += d * c2_stored(h1, sp, 0, b);
       } else {
         unsigned long long Y = 0;
         if (!map_full) {
@@ -376,7 +386,7 @@ __device__ unsigned long long c2_handoff_terms(const uint32_t *h1, const uint32_
             if ((y.y & 1u) && (int64_t)y.x % sp.hl == b) Y += y.y >> 1;
           }
         }
-        corr += d * (h2[b] + Y);
+        corr += d * (c2_stored(h2, sp, 1, b) + Y);
       }
     }
   }
@@ -445,6 +455,67 @@ __global__ __launch_bounds__(256) void k_chain2_dot(const uint32_t *h1, const ui
       __threadfence();
       const unsigned long long a0 = atomicAdd(acc, 0ull), a1 = atomicAdd(acc + 1, 0ull);
       // fin may be pinned host memory: a system-scope store
+      __hip_atomic_store(fin, (int64_t)(a0 - a1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __threadfence_system();
+    }
+  }
+}
+
+// Σ in·out over the partitioned pipeline's bucket layout (sp.split given):
+// work items = (bucket, 2 Ki-word chunk); an unsplit run's bucket holds packed
+// uint16 pairs (half the bytes of one uint32 per bin), a split run's bucket one
+// uint32 per bin — chosen per item, uniform in the workgroup.  Last workgroup:
+// the hand-off terms; last to finish: *fin = Σ − self-loops.
+constexpr int C2P_CH = 2048;
+__global__ __launch_bounds__(256) void k_chain2_dot_pairs(const uint32_t *h1, const uint32_t *h2, C2Spill sp,
+                                                          unsigned long long *acc, int64_t *fin,
+                                                          unsigned int *done) {
+  __shared__ unsigned long long lds[17];
+  unsigned long long s = 0;
+  const unsigned nblk = gridDim.x - 1;
+  if (blockIdx.x == nblk) {
+    s = c2_handoff_terms(h1, h2, sp, lds);
+  } else {
+    constexpr int64_t HALF = C2P_BW / 2, PER = HALF / C2P_CH;
+    const int64_t items = (int64_t)sp.nb * PER;
+    for (int64_t it = blockIdx.x; it < items; it += nblk) {
+      const int64_t b = it / PER, w0 = (it % PER) * C2P_CH;
+      const bool si = sp.split[b] != 0, so = sp.split[sp.nb + b] != 0;  // uniform
+      const uint32_t *a = h1 + b * C2P_BW, *c = h2 + b * C2P_BW;
+#pragma unroll
+      for (int r = 0; r < C2P_CH / (4 * 256); ++r) {
+        const int64_t w = w0 + 4 * (r * 256 + threadIdx.x);
+        uint4 alo, ahi, clo, chi;
+        if (!si) {
+          const uint4 p = *(const uint4 *)(a + w);
+          alo = make_uint4(p.x & 0xFFFF, p.y & 0xFFFF, p.z & 0xFFFF, p.w & 0xFFFF);
+          ahi = make_uint4(p.x >> 16, p.y >> 16, p.z >> 16, p.w >> 16);
+        } else {
+          alo = *(const uint4 *)(a + w);
+          ahi = *(const uint4 *)(a + w + HALF);
+        }
+        if (!so) {
+          const uint4 p = *(const uint4 *)(c + w);
+          clo = make_uint4(p.x & 0xFFFF, p.y & 0xFFFF, p.z & 0xFFFF, p.w & 0xFFFF);
+          chi = make_uint4(p.x >> 16, p.y >> 16, p.z >> 16, p.w >> 16);
+        } else {
+          clo = *(const uint4 *)(c + w);
+          chi = *(const uint4 *)(c + w + HALF);
+        }
+        s += (unsigned long long)alo.x * clo.x + (unsigned long long)alo.y * clo.y +
+             (unsigned long long)alo.z * clo.z + (unsigned long long)alo.w * clo.w +
+             (unsigned long long)ahi.x * chi.x + (unsigned long long)ahi.y * chi.y +
+             (unsigned long long)ahi.z * chi.z + (unsigned long long)ahi.w * chi.w;
+      }
+    }
+    s = block_reduce_sum(s, lds);
+  }
+  if (threadIdx.x == 0 && s) atomicAdd(acc, s);
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(done, 1u) == gridDim.x - 1) {
+      __threadfence();
+      const unsigned long long a0 = atomicAdd(acc, 0ull), a1 = atomicAdd(acc + 1, 0ull);
       __hip_atomic_store(fin, (int64_t)(a0 - a1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __threadfence_system();
     }
@@ -1297,7 +1368,10 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
       // host scalar the synchronous path reads after its sync (no D2H copy)
       int64_t *fin = s->async_out ? s->async_out : s->h_scalars;
       unsigned int *done = (unsigned int *)((unsigned long long *)acc->p + 2);
-      if (wb.ones)  // ONES: Σ in·out is invariant under the node_mix bijection (+1 block: hand-offs)
+      if (spill.split)  // the bucket layout of the partitioned pipeline (+1 block: hand-offs)
+        hipLaunchKernelGGL(k_chain2_dot_pairs, dim3(dot_grid(s->num_cus) + 1), dim3(256), 0, s->stream, h1, h2,
+                           spill, (unsigned long long *)acc->p, fin, done);
+      else if (wb.ones)  // ONES: Σ in·out is invariant under the node_mix bijection (+1 block: hand-offs)
         hipLaunchKernelGGL(k_chain2_dot<true>, dim3(grid + (spill.n ? 1 : 0)), dim3(256), 0, s->stream, h1, h2,
                            wb.map.m, lo, dot_len, (unsigned long long *)acc->p, fin, done, spill);
       else

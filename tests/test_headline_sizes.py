@@ -61,8 +61,9 @@ def test_two_hop_headline_p3_variant(gpu_session, monkeypatch, scale, rot):
     assert got == FULL[str(scale)]["two_hop"]
 
 
-@pytest.mark.parametrize("ovfk", ["0", "1"], ids=["dot_folds_log", "overflow_kernel"])
-def test_two_hop_headline_handoff_paths(gpu_session, monkeypatch, ovfk):
+@pytest.mark.parametrize("ovfk,pairs", [("0", "1"), ("0", "0"), ("1", "1")],
+                         ids=["pairs_dot_folds_log", "uint32_bins_dot_folds_log", "overflow_kernel"])
+def test_two_hop_headline_handoff_paths(gpu_session, monkeypatch, ovfk, pairs):
     """The uint16 P3 counters hand 2^15 off to a log when a hub's counter
     fills (s24 hub in-degree 369,897).  By default the dot kernel folds the
     log in (Σ Δ·other + Σ Δ_in·Δ_out, no overflow launch); CAPF_P3_OVFK=1 adds
@@ -70,6 +71,7 @@ def test_two_hop_headline_handoff_paths(gpu_session, monkeypatch, ovfk):
     ways, synchronous and asynchronous."""
     import torch
     monkeypatch.setenv("CAPF_P3_OVFK", ovfk)
+    monkeypatch.setenv("CAPF_HIST_PAIRS", pairs)  # exclusive runs' buckets as packed uint16 pairs
     g = rmat_graph(gpu_session, 24, compact=3)
     assert run(g, TWO_HOP)[0]["count"] == FULL["24"]["two_hop"]
     slot = torch.full((1,), -1, dtype=torch.int64, device="cuda")

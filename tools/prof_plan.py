@@ -34,3 +34,13 @@ for _ in range(N):
     plan_query(g, q)
 pr.disable()
 pstats.Stats(pr).sort_stats("tottime").print_stats(35)
+# records() of a materialised count (the scalar delivery after the device work)
+import statistics  # noqa: E402
+ts = []
+for _ in range(200):
+    op = plan_query(g, q)
+    op.table.size  # runs the count
+    t0 = time.perf_counter()
+    records(op, ["count"])
+    ts.append(time.perf_counter() - t0)
+print(f"records() after the count: median {statistics.median(ts) * 1e6:.1f} us", flush=True)

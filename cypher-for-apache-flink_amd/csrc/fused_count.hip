@@ -319,27 +319,43 @@ __global__ __launch_bounds__(256) void k_chain2_hist(Chain2Args a) {
 // every entry reads its counters once (independent loads).
 // Counter `bin` of one side (h) as stored: one uint32, or (split layout given
 // and the bin's run unsplit) the half of the bucket's packed pair word.
+// `split_l`: the split flags staged in LDS (null: read sp.split).
 constexpr int64_t C2P_BW = int64_t(1) << 16;  // bins per bucket (chain2_partitioned.hip C2_BW)
-__device__ inline uint32_t c2_stored(const uint32_t *h, const C2Spill &sp, int side, int64_t bin) {
+constexpr int C2_HO_BLOCKS = 4;               // workgroups computing the hand-off terms
+constexpr int C2_HO_MAXNB = 2048;             // split flags staged in LDS (2·nb ≤ this)
+__device__ inline uint32_t c2_stored(const uint32_t *h, const C2Spill &sp, int side, int64_t bin,
+                                     const uint8_t *split_l) {
   if (!sp.split) return h[bin];
   const int64_t b = bin / C2P_BW, k = bin % C2P_BW;
-  if (sp.split[side * sp.nb + b]) return h[bin];
+  const bool sp_run = split_l ? split_l[side * sp.nb + b] != 0 : sp.split[side * sp.nb + b] != 0;
+  if (sp_run) return h[bin];
   return (h[b * C2P_BW + (k & (C2P_BW / 2 - 1))] >> ((k >> 15) * 16)) & 0xFFFFu;
 }
 
+// Σ over the hand-off log of (Σ(x+X)(y+Y) − Σxy) = Σ_in Δ·(y + Y) + Σ_out Δ·x
+// (x, y: the stored counters, X, Y: their hand-offs), workgroup `part` of
+// `parts` taking every parts-th entry.  Each workgroup sums ALL out-side deltas
+// per counter in an LDS open-addressing map (the log is short: ~700 entries at
+// s24), stages the split flags in LDS, then reads one stored counter per entry
+// — dependent global loads are the cost, so the entries are spread over
+// several workgroups running beside the dot.
 __device__ unsigned long long c2_handoff_terms(const uint32_t *h1, const uint32_t *h2, const C2Spill &sp,
-                                               unsigned long long *lds) {
+                                               unsigned long long *lds, int part, int parts) {
   constexpr uint32_t MAPN = 2048;  // slots; up to MAPN / 2 distinct out-side counters
   __shared__ uint32_t mk[MAPN];
   __shared__ unsigned long long mv[MAPN];
+  __shared__ uint8_t spl[C2_HO_MAXNB];
   __shared__ int map_full;
   unsigned long long corr = 0;
   const uint32_t ne = min(*sp.n, sp.cap);
   if (ne > 0) {
+    const bool stage = sp.split && 2 * sp.nb <= C2_HO_MAXNB;
     for (uint32_t i = threadIdx.x; i < MAPN; i += blockDim.x) {
       mk[i] = 0xFFFFFFFFu;
       mv[i] = 0;
     }
+    if (stage)
+      for (int i = threadIdx.x; i < 2 * sp.nb; i += blockDim.x) spl[i] = sp.split[i] ? 1 : 0;
     if (threadIdx.x == 0) map_full = 0;
     __syncthreads();
     for (uint32_t e = threadIdx.x; e < ne; e += blockDim.x) {
@@ -361,12 +377,13 @@ __device__ unsigned long long c2_handoff_terms(const uint32_t *h1, const uint32_
       }
     }
     __syncthreads();
-    for (uint32_t e = threadIdx.x; e < ne; e += blockDim.x) {
+    const uint8_t *sl = stage ? spl : nullptr;
+    for (uint32_t e = part * blockDim.x + threadIdx.x; e < ne; e += parts * blockDim.x) {
       const uint2 x = sp.log[e];
       const int64_t b = (int64_t)x.x % sp.hl;
       const unsigned long long d = x.y >> 1;
       if (x.y & 1u) {
-        corr += d * c2_stored(h1, sp, 0, b);
+        corr += d * c2_stored(h1, sp, 0, b, sl);
       } else {
         unsigned long long Y = 0;
         if (!map_full) {
@@ -386,7 +403,7 @@ __device__ unsigned long long c2_handoff_terms(const uint32_t *h1, const uint32_
             if ((y.y & 1u) && (int64_t)y.x % sp.hl == b) Y += y.y >> 1;
           }
         }
-        corr += d * (c2_stored(h2, sp, 1, b) + Y);
+        corr += d * (c2_stored(h2, sp, 1, b, sl) + Y);
       }
     }
   }
@@ -405,9 +422,9 @@ __global__ __launch_bounds__(256) void k_chain2_dot(const uint32_t *h1, const ui
                                                     unsigned int *done = nullptr, C2Spill sp = C2Spill()) {
   __shared__ unsigned long long lds[17];
   unsigned long long s = 0;
-  const unsigned nblk = gridDim.x - (sp.n ? 1u : 0u);  // dot workgroups
-  if (sp.n && blockIdx.x == nblk) {
-    s = c2_handoff_terms(h1, h2, sp, lds);
+  const unsigned nblk = gridDim.x - (sp.n ? (unsigned)C2_HO_BLOCKS : 0u);  // dot workgroups
+  if (sp.n && blockIdx.x >= nblk) {
+    s = c2_handoff_terms(h1, h2, sp, lds, (int)(blockIdx.x - nblk), C2_HO_BLOCKS);
   } else {
     const int64_t stride = (int64_t)nblk * blockDim.x;
     // 4 counters per thread per step: dwordx4 loads of both histograms
@@ -472,9 +489,9 @@ __global__ __launch_bounds__(256) void k_chain2_dot_pairs(const uint32_t *h1, co
                                                           unsigned int *done) {
   __shared__ unsigned long long lds[17];
   unsigned long long s = 0;
-  const unsigned nblk = gridDim.x - 1;
-  if (blockIdx.x == nblk) {
-    s = c2_handoff_terms(h1, h2, sp, lds);
+  const unsigned nblk = gridDim.x - C2_HO_BLOCKS;
+  if (blockIdx.x >= nblk) {
+    s = c2_handoff_terms(h1, h2, sp, lds, (int)(blockIdx.x - nblk), C2_HO_BLOCKS);
   } else {
     constexpr int64_t HALF = C2P_BW / 2, PER = HALF / C2P_CH;
     const int64_t items = (int64_t)sp.nb * PER;
@@ -1369,10 +1386,10 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
       int64_t *fin = s->async_out ? s->async_out : s->h_scalars;
       unsigned int *done = (unsigned int *)((unsigned long long *)acc->p + 2);
       if (spill.split)  // the bucket layout of the partitioned pipeline (+1 block: hand-offs)
-        hipLaunchKernelGGL(k_chain2_dot_pairs, dim3(dot_grid(s->num_cus) + 1), dim3(256), 0, s->stream, h1, h2,
+        hipLaunchKernelGGL(k_chain2_dot_pairs, dim3(dot_grid(s->num_cus) + C2_HO_BLOCKS), dim3(256), 0, s->stream, h1, h2,
                            spill, (unsigned long long *)acc->p, fin, done);
       else if (wb.ones)  // ONES: Σ in·out is invariant under the node_mix bijection (+1 block: hand-offs)
-        hipLaunchKernelGGL(k_chain2_dot<true>, dim3(grid + (spill.n ? 1 : 0)), dim3(256), 0, s->stream, h1, h2,
+        hipLaunchKernelGGL(k_chain2_dot<true>, dim3(grid + (spill.n ? C2_HO_BLOCKS : 0)), dim3(256), 0, s->stream, h1, h2,
                            wb.map.m, lo, dot_len, (unsigned long long *)acc->p, fin, done, spill);
       else
         hipLaunchKernelGGL(k_chain2_dot<false>, dim3(grid), dim3(256), 0, s->stream, h1, h2,

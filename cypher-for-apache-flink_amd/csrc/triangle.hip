@@ -539,10 +539,9 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_packed(const uint32_t *
 constexpr uint32_t TRI_BCHUNK = 1024;
 
 struct TriPassB {
-  const uint32_t *in_rowptr;  // [len + 1] into in_words / in_eidx
-  const uint32_t *in_words;   // p | multiplicity nibbles of the pair p–q
+  const uint32_t *in_words;   // p | multiplicity nibbles of the pair p–q, by (p-block, q, p)
   const uint32_t *in_eidx;    // out-CSR index of the edge p→q (vals escape)
-  const uint2 *items;         // (q, first in-list entry) per work item
+  const uint4 *items;         // (q, first in-list entry, entries ≤ TRI_BCHUNK) per work item
   uint32_t nitems;
 };
 
@@ -566,11 +565,10 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_passb(const uint32_t *r
     if (c0 >= b.nitems) break;
     const uint64_t c1 = min<uint64_t>(c0 + 4, b.nitems);
     for (uint64_t it = c0; it < c1; ++it) {
-      const uint2 item = b.items[it];
+      const uint4 item = b.items[it];
       const uint32_t q = item.x;
       const uint32_t a = rowptr[q], dq = rowptr[q + 1] - a;
-      const uint32_t i0 = b.in_rowptr[q] + item.y;
-      const uint32_t n = min(b.in_rowptr[q + 1] - i0, TRI_BCHUNK);
+      const uint32_t i0 = item.y, n = item.z;
       const uint32_t *inw = b.in_words + i0;
       const uint32_t *ine = b.in_eidx + i0;
       if (dq > TRI_CAP) {  // long N+(q): searched in global memory
@@ -615,14 +613,51 @@ static void rocprim_call(Session *s, F &&f) {
 
 // Pass-B keys: edge e = p→q (sorted oriented keys) goes to pass B when
 // |N+(p)| < |N+(q)|: key (q << 32 | p), value e; otherwise TRI_NONE.
-__global__ void k_tri_passb_keys(const uint64_t *okey, const uint32_t *rowptr, uint32_t P, uint64_t *keys,
-                                 uint32_t *eidx) {
+// Key (block of p << 48 | q << 24 | p): pass B's in-lists grouped by p-block
+// first — blocks of 2^pshift words of N+(p) lists (block(p) = rowptr[p] >>
+// pshift) — so the waves in flight stream lists from one block, a region the
+// Infinity Cache holds, instead of from the whole CSR (node ids < 2^24).
+__global__ void k_tri_passb_keys(const uint64_t *okey, const uint32_t *rowptr, uint32_t P, int pshift,
+                                 uint64_t *keys, uint32_t *eidx) {
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < P; e += gridDim.x * blockDim.x) {
     const uint64_t k = okey[e];
     const uint32_t pp = (uint32_t)(k >> 32), q = (uint32_t)k;
-    const uint32_t dp = rowptr[pp + 1] - rowptr[pp], dq = rowptr[q + 1] - rowptr[q];
-    keys[e] = dp < dq ? ((uint64_t)q << 32) | pp : TRI_NONE;
+    const uint32_t ap = rowptr[pp];
+    const uint32_t dp = rowptr[pp + 1] - ap, dq = rowptr[q + 1] - rowptr[q];
+    keys[e] = dp < dq ? ((uint64_t)(ap >> pshift) << 48) | ((uint64_t)q << 24) | pp : TRI_NONE;
     eidx[e] = e;
+  }
+}
+
+// number of keys below TRI_NONE (sorted): one thread, binary search
+__global__ void k_tri_count_below(const uint64_t *skeys, uint32_t P, uint32_t *out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint32_t lo = 0, hi = P;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (skeys[mid] < TRI_NONE) lo = mid + 1;
+    else hi = mid;
+  }
+  *out = lo;
+}
+
+__global__ void k_tri_segkeys(const uint64_t *skeys, uint32_t n, uint64_t *seg) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    seg[i] = skeys[i] >> 24;
+}
+
+// items of segment j (a run of equal (p-block, q)): ⌈cnt / TRI_BCHUNK⌉ chunks
+__global__ void k_tri_seg_items(const uint32_t *cnt, uint32_t nseg, uint32_t *nitems) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nseg; j += gridDim.x * blockDim.x)
+    nitems[j] = (cnt[j] + TRI_BCHUNK - 1) / TRI_BCHUNK;
+}
+
+__global__ void k_tri_seg_fill(const uint64_t *useg, const uint32_t *cnt, const uint32_t *start,
+                               const uint32_t *istart, uint32_t nseg, uint4 *items) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nseg; j += gridDim.x * blockDim.x) {
+    const uint32_t q = (uint32_t)(useg[j] & 0xFFFFFFu), c = cnt[j], s0 = start[j];
+    for (uint32_t i = 0; i * TRI_BCHUNK < c; ++i)
+      items[istart[j] + i] = make_uint4(q, s0 + i * TRI_BCHUNK, min(TRI_BCHUNK, c - i * TRI_BCHUNK), 0u);
   }
 }
 
@@ -630,21 +665,7 @@ __global__ void k_tri_passb_keys(const uint64_t *okey, const uint32_t *rowptr, u
 __global__ void k_tri_inlist(const uint64_t *skeys, const uint32_t *seidx, const uint32_t *pcols, uint32_t nB,
                              uint32_t *in_words) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nB; i += gridDim.x * blockDim.x)
-    in_words[i] = (pcols[seidx[i]] & 0xFF000000u) | (uint32_t)skeys[i];
-}
-
-// Work items of pass B per q: ⌈|in-list(q)| / TRI_BCHUNK⌉ when N+(q) is non-empty.
-__global__ void k_tri_item_counts(const uint32_t *in_rowptr, const uint32_t *rowptr, uint64_t len,
-                                  uint32_t *cnt) {
-  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < len; q += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t nin = in_rowptr[q + 1] - in_rowptr[q], dq = rowptr[q + 1] - rowptr[q];
-    cnt[q] = dq > 0 ? (nin + TRI_BCHUNK - 1) / TRI_BCHUNK : 0u;
-  }
-}
-
-__global__ void k_tri_items(const uint32_t *cnt, const uint32_t *start, uint64_t len, uint2 *items) {
-  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < len; q += (uint64_t)gridDim.x * blockDim.x)
-    for (uint32_t i = 0; i < cnt[q]; ++i) items[start[q] + i] = make_uint2((uint32_t)q, i * TRI_BCHUNK);
+    in_words[i] = (pcols[seidx[i]] & 0xFF000000u) | ((uint32_t)skeys[i] & 0xFFFFFFu);
 }
 
 // Oriented CSR of the distinct node pairs of (src, dst) over [lo, lo + len).
@@ -654,7 +675,7 @@ struct TriGraph {
   BufPtr rowptr, cols, vals, loops, acc;
   BufPtr pcols;  // packed column words (node ids < 2^24), else null
   // two-pass schedule (pass B: edges with |N+(p)| < |N+(q)| counted at q)
-  BufPtr in_rowptr, in_words, in_eidx, items;
+  BufPtr in_words, in_eidx, items;
   uint32_t nB = 0, nitems = 0;
   uint32_t P = 0;
   uint64_t len = 0;
@@ -663,50 +684,73 @@ struct TriGraph {
 // In-lists and work items of pass B (built with the CSR, cached with it).
 static void tri_build_passb(Session *s, const uint64_t *okey, TriGraph &g) {
   const uint32_t P = g.P;
-  const uint64_t len = g.len;
   KernelTimer kt(s, "tri_passb_build", 40.0 * P);
+  // CAPF_TRI_PBLOCK (tuning): log2 of the N+(p) words per p-block (default 2^24 = 64 MB)
+  const char *pb = getenv("CAPF_TRI_PBLOCK");
+  const int pshift = pb ? std::max(8, std::min(31, atoi(pb))) : 24;
   BufPtr keys = s->alloc(8 * (int64_t)P), skeys = s->alloc(8 * (int64_t)P);
   BufPtr eidx = s->alloc(4 * (int64_t)P), seidx = s->alloc(4 * (int64_t)P);
   hipLaunchKernelGGL(k_tri_passb_keys, dim3(grid_for(P, 256, 256 * 64)), dim3(256), 0, s->stream, okey,
-                     (const uint32_t *)g.rowptr->p, P, (uint64_t *)keys->p, (uint32_t *)eidx->p);
+                     (const uint32_t *)g.rowptr->p, P, pshift, (uint64_t *)keys->p, (uint32_t *)eidx->p);
   KERNEL_CHECK();
   rocprim_call(s, [&](void *t, size_t &n) {
     return rocprim::radix_sort_pairs(t, n, (const uint64_t *)keys->p, (uint64_t *)skeys->p,
                                      (const uint32_t *)eidx->p, (uint32_t *)seidx->p, (size_t)P, 0, 64,
                                      s->stream);
   });
-  g.in_rowptr = s->alloc(4 * (len + 2));
-  hipLaunchKernelGGL(k_tri_rowptr, dim3(grid_for((int64_t)len + 1, 256, 256 * 64)), dim3(256), 0, s->stream,
-                     (const uint64_t *)skeys->p, P, len, (uint32_t *)g.in_rowptr->p);
+  BufPtr nb = s->alloc(16);
+  hipLaunchKernelGGL(k_tri_count_below, dim3(1), dim3(64), 0, s->stream, (const uint64_t *)skeys->p, P,
+                     (uint32_t *)nb->p);
   KERNEL_CHECK();
-  HIP_CHECK(hipMemcpyAsync(&g.nB, (uint32_t *)g.in_rowptr->p + len, 4, hipMemcpyDeviceToHost, s->stream));
+  HIP_CHECK(hipMemcpyAsync(&g.nB, nb->p, 4, hipMemcpyDeviceToHost, s->stream));
   s->sync();
   g.in_words = s->alloc(4 * std::max<uint32_t>(g.nB, 1));
   g.in_eidx = s->alloc(4 * std::max<uint32_t>(g.nB, 1));
-  if (g.nB > 0) {
-    hipLaunchKernelGGL(k_tri_inlist, dim3(grid_for(g.nB, 256, 256 * 64)), dim3(256), 0, s->stream,
-                       (const uint64_t *)skeys->p, (const uint32_t *)seidx->p, (const uint32_t *)g.pcols->p, g.nB,
-                       (uint32_t *)g.in_words->p);
-    KERNEL_CHECK();
-    HIP_CHECK(hipMemcpyAsync(g.in_eidx->p, seidx->p, 4 * (size_t)g.nB, hipMemcpyDeviceToDevice, s->stream));
+  g.nitems = 0;
+  if (g.nB == 0) {
+    g.items = s->alloc(16);
+    s->sync();
+    return;
   }
-  BufPtr cnt = s->alloc(4 * (len + 1)), start = s->alloc(4 * (len + 1));
-  hipLaunchKernelGGL(k_tri_item_counts, dim3(grid_for((int64_t)len, 256, 256 * 64)), dim3(256), 0, s->stream,
-                     (const uint32_t *)g.in_rowptr->p, (const uint32_t *)g.rowptr->p, len, (uint32_t *)cnt->p);
+  hipLaunchKernelGGL(k_tri_inlist, dim3(grid_for(g.nB, 256, 256 * 64)), dim3(256), 0, s->stream,
+                     (const uint64_t *)skeys->p, (const uint32_t *)seidx->p, (const uint32_t *)g.pcols->p, g.nB,
+                     (uint32_t *)g.in_words->p);
   KERNEL_CHECK();
-  HIP_CHECK(hipMemsetAsync((uint32_t *)cnt->p + len, 0, 4, s->stream));
+  HIP_CHECK(hipMemcpyAsync(g.in_eidx->p, seidx->p, 4 * (size_t)g.nB, hipMemcpyDeviceToDevice, s->stream));
+  // segments = runs of equal (p-block, q) → work items of ≤ TRI_BCHUNK entries
+  BufPtr seg = s->alloc(8 * (int64_t)g.nB), useg = s->alloc(8 * (int64_t)g.nB);
+  BufPtr cnt = s->alloc(4 * ((int64_t)g.nB + 1)), nseg_d = s->alloc(16);
+  hipLaunchKernelGGL(k_tri_segkeys, dim3(grid_for(g.nB, 256, 256 * 64)), dim3(256), 0, s->stream,
+                     (const uint64_t *)skeys->p, g.nB, (uint64_t *)seg->p);
+  KERNEL_CHECK();
   rocprim_call(s, [&](void *t, size_t &n) {
-    return rocprim::exclusive_scan(t, n, (const uint32_t *)cnt->p, (uint32_t *)start->p, 0u, (size_t)len + 1,
+    return rocprim::run_length_encode(t, n, (const uint64_t *)seg->p, (unsigned int)g.nB, (uint64_t *)useg->p,
+                                      (uint32_t *)cnt->p, (uint32_t *)nseg_d->p, s->stream);
+  });
+  uint32_t nseg = 0;
+  HIP_CHECK(hipMemcpyAsync(&nseg, nseg_d->p, 4, hipMemcpyDeviceToHost, s->stream));
+  s->sync();
+  BufPtr start = s->alloc(4 * ((int64_t)nseg + 1)), nit = s->alloc(4 * ((int64_t)nseg + 1)),
+         istart = s->alloc(4 * ((int64_t)nseg + 1));
+  rocprim_call(s, [&](void *t, size_t &n) {
+    return rocprim::exclusive_scan(t, n, (const uint32_t *)cnt->p, (uint32_t *)start->p, 0u, (size_t)nseg,
                                    rocprim::plus<uint32_t>(), s->stream);
   });
-  HIP_CHECK(hipMemcpyAsync(&g.nitems, (uint32_t *)start->p + len, 4, hipMemcpyDeviceToHost, s->stream));
+  hipLaunchKernelGGL(k_tri_seg_items, dim3(grid_for(nseg, 256, 256 * 64)), dim3(256), 0, s->stream,
+                     (const uint32_t *)cnt->p, nseg, (uint32_t *)nit->p);
+  KERNEL_CHECK();
+  HIP_CHECK(hipMemsetAsync((uint32_t *)nit->p + nseg, 0, 4, s->stream));
+  rocprim_call(s, [&](void *t, size_t &n) {
+    return rocprim::exclusive_scan(t, n, (const uint32_t *)nit->p, (uint32_t *)istart->p, 0u, (size_t)nseg + 1,
+                                   rocprim::plus<uint32_t>(), s->stream);
+  });
+  HIP_CHECK(hipMemcpyAsync(&g.nitems, (uint32_t *)istart->p + nseg, 4, hipMemcpyDeviceToHost, s->stream));
   s->sync();
-  g.items = s->alloc(8 * std::max<uint32_t>(g.nitems, 1));
-  if (g.nitems > 0) {
-    hipLaunchKernelGGL(k_tri_items, dim3(grid_for((int64_t)len, 256, 256 * 64)), dim3(256), 0, s->stream,
-                       (const uint32_t *)cnt->p, (const uint32_t *)start->p, len, (uint2 *)g.items->p);
-    KERNEL_CHECK();
-  }
+  g.items = s->alloc(16 * std::max<uint32_t>(g.nitems, 1));
+  hipLaunchKernelGGL(k_tri_seg_fill, dim3(grid_for(nseg, 256, 256 * 64)), dim3(256), 0, s->stream,
+                     (const uint64_t *)useg->p, (const uint32_t *)cnt->p, (const uint32_t *)start->p,
+                     (const uint32_t *)istart->p, nseg, (uint4 *)g.items->p);
+  KERNEL_CHECK();
   s->sync();  // the temporaries go back to the pool
 }
 
@@ -873,7 +917,7 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
     // CAPF_TRI_PACKED=0 (tuning): the unpacked kernel (multiplicities loaded from vals per hit)
     const bool packed = !(getenv("CAPF_TRI_PACKED") && atoi(getenv("CAPF_TRI_PACKED")) == 0);
     // CAPF_TRI_TWOPASS=0 (tuning): one pass, every wedge streamed from N+(q)
-    const bool two = packed && g.pcols && g.in_rowptr && !(getenv("CAPF_TRI_TWOPASS") && atoi(getenv("CAPF_TRI_TWOPASS")) == 0);
+    const bool two = packed && g.pcols && g.in_words && !(getenv("CAPF_TRI_TWOPASS") && atoi(getenv("CAPF_TRI_TWOPASS")) == 0);
     if (packed && g.pcols) {
       auto kern = two ? (ilp <= 2 ? k_tri_count_packed<2, true> : k_tri_count_packed<4, true>)
                       : (ilp >= 8 ? k_tri_count_packed<8> : ilp <= 2 ? k_tri_count_packed<2> : k_tri_count_packed<4>);
@@ -881,8 +925,8 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
                          (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
                          (const uint2 *)g.vals->p, len, parts, part, acc + 3, acc);
       if (two && g.nitems > 0) {
-        TriPassB b{(const uint32_t *)g.in_rowptr->p, (const uint32_t *)g.in_words->p,
-                   (const uint32_t *)g.in_eidx->p, (const uint2 *)g.items->p, g.nitems};
+        TriPassB b{(const uint32_t *)g.in_words->p, (const uint32_t *)g.in_eidx->p, (const uint4 *)g.items->p,
+                   g.nitems};
         auto kb = ilp <= 2 ? k_tri_count_passb<2> : k_tri_count_passb<4>;
         hipLaunchKernelGGL(kb, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
                            (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p, (const uint2 *)g.vals->p,

@@ -26,7 +26,10 @@
 // sides carry matched flags).  Bytes per row and side: P1 read key + write
 // 12 B, P2 read 12 B + write 12 B, J read 12 B; output 16 B per pair.
 #include <algorithm>
+#include <cstring>
 #include <vector>
+
+#include <rocprim/rocprim.hpp>
 
 #include "capf_internal.h"
 #include "device_common.h"
@@ -383,6 +386,122 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_join(const RJWork *work, const
   if (!EMIT && threadIdx.x == 0) out_cnt[blockIdx.x] = item_total;
 }
 
+// Run-based join (default): the build partitions are sorted by h once
+// (segmented radix sort), so equal keys are runs; an LDS chunk of ≤ RJ_CHUNK
+// sorted build rows becomes a table of RUNS (h → start, length), found from
+// run heads with a ballot bitmask.  A probe row costs one lookup whatever its
+// key's multiplicity; EMIT hands the wave's matches out as one flattened
+// sequence (lane = output position, owner lane by a 6-step search in the
+// wave's prefix table) — coalesced, balanced writes even when one probe key
+// matches thousands of build rows (a hub node of a rel-to-rel join), where
+// the chain-walking kernel made one lane write them all.
+constexpr int RJ_RUNCAP = 4096;  // run-table slots (≤ RJ_CHUNK runs per chunk, load ≤ 1/2)
+
+template <bool EMIT>
+__global__ __launch_bounds__(RJ_JBLOCK) void k_rj_join_runs(const RJWork *work, const uint64_t *bh,
+                                                             const uint32_t *brow, const int64_t *bstart,
+                                                             const uint64_t *ph, const uint32_t *prow,
+                                                             int64_t *out_cnt, const int64_t *out_off,
+                                                             int64_t *oprobe, int64_t *obuild,
+                                                             uint8_t *pmatched, uint8_t *bmatched) {
+  __shared__ uint64_t kk[RJ_CHUNK];
+  __shared__ unsigned long long hm[RJ_CHUNK / WAVE];  // run-head bitmask
+  __shared__ uint64_t th[RJ_RUNCAP];
+  __shared__ uint32_t tv[RJ_RUNCAP];                   // start << 16 | length (chunk-relative), 0 = empty
+  constexpr int NW = RJ_JBLOCK / WAVE;
+  __shared__ uint32_t wex[NW][WAVE + 1], wst[NW][WAVE], wpr[NW][WAVE];
+  __shared__ int64_t wsum[NW];
+  const RJWork wk = work[blockIdx.x];
+  const int64_t b0 = bstart[wk.part], b1 = bstart[wk.part + 1];
+  const int wv = threadIdx.x / WAVE, lane = lane_id();
+  int64_t item_total = 0;
+  int64_t base = EMIT ? out_off[blockIdx.x] : 0;
+  for (int64_t c0 = b0; c0 < b1; c0 += RJ_CHUNK) {
+    const int nc = (int)min<int64_t>((int64_t)RJ_CHUNK, b1 - c0);
+    __syncthreads();  // the previous chunk's table is no longer read
+    for (int i = threadIdx.x; i < RJ_RUNCAP; i += RJ_JBLOCK) tv[i] = 0;
+    for (int i = threadIdx.x; i < RJ_CHUNK; i += RJ_JBLOCK) kk[i] = i < nc ? bh[c0 + i] : ~0ull;
+    __syncthreads();
+    for (int i0 = wv * WAVE; i0 < RJ_CHUNK; i0 += RJ_JBLOCK) {  // one ballot per 64 rows
+      const int i = i0 + lane;
+      const bool head = i < nc && (i == 0 || kk[i] != kk[i - 1]);
+      const unsigned long long m = __ballot(head);
+      if (lane == 0) hm[i0 / WAVE] = m;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nc; i += RJ_JBLOCK) {
+      const unsigned long long m = hm[i / WAVE];
+      if (!((m >> (i & (WAVE - 1))) & 1ull)) continue;
+      // run end = the next head (or nc): the rest of this word, then the next words
+      int e = nc;
+      const unsigned long long rest = (i & (WAVE - 1)) == WAVE - 1 ? 0ull : m >> ((i & (WAVE - 1)) + 1);
+      if (rest) {
+        e = i + 1 + __builtin_ctzll(rest);
+      } else {
+        for (int w = i / WAVE + 1; w < (nc + WAVE - 1) / WAVE; ++w)
+          if (hm[w]) {
+            e = w * WAVE + __builtin_ctzll(hm[w]);
+            break;
+          }
+      }
+      const uint64_t h = kk[i];
+      uint32_t slot = (uint32_t)h & (RJ_RUNCAP - 1);
+      while (atomicCAS(&tv[slot], 0u, ((uint32_t)i << 16) | (uint32_t)(e - i)) != 0u)
+        slot = (slot + 1) & (RJ_RUNCAP - 1);
+      th[slot] = h;
+    }
+    __syncthreads();
+    for (int64_t q0 = wk.p0; q0 < wk.p1; q0 += RJ_JBLOCK) {
+      const int64_t q = q0 + threadIdx.x;
+      const bool live = q < wk.p1;
+      const uint64_t h = live ? ph[q] : 0;
+      uint32_t cnt = 0, st = 0;
+      if (live) {
+        uint32_t slot = (uint32_t)h & (RJ_RUNCAP - 1);
+        for (uint32_t v = tv[slot]; v != 0u; slot = (slot + 1) & (RJ_RUNCAP - 1), v = tv[slot])
+          if (th[slot] == h) {
+            cnt = v & 0xFFFFu;
+            st = v >> 16;
+            break;
+          }
+      }
+      const uint32_t inc = wave_inclusive_scan(cnt);
+      const uint32_t wtot = (uint32_t)__shfl(inc, WAVE - 1, WAVE);
+      if (lane == 0) wsum[wv] = wtot;
+      if (EMIT) {
+        wex[wv][lane] = inc - cnt;
+        if (lane == WAVE - 1) wex[wv][WAVE] = inc;
+        wst[wv][lane] = st;
+        wpr[wv][lane] = live ? prow[q] : 0u;
+        if (pmatched && cnt) pmatched[prow[q]] = 1;
+      }
+      __syncthreads();
+      int64_t wave_off = 0, block_tot = 0;
+      for (int k = 0; k < NW; ++k) {
+        if (k < wv) wave_off += wsum[k];
+        block_tot += wsum[k];
+      }
+      if (EMIT) {
+        const int64_t o0 = base + wave_off;
+        for (uint32_t x = lane; x < wtot; x += WAVE) {
+          uint32_t b = 0;  // last lane with wex[b] ≤ x
+#pragma unroll
+          for (int st2 = WAVE / 2; st2 > 0; st2 >>= 1)
+            if (wex[wv][b + st2] <= x) b += st2;
+          const uint32_t br = brow[c0 + wst[wv][b] + (x - wex[wv][b])];
+          oprobe[o0 + x] = wpr[wv][b];
+          obuild[o0 + x] = br;
+          if (bmatched) bmatched[br] = 1;
+        }
+      }
+      __syncthreads();  // wsum / wave tables are rewritten by the next step
+      base += block_tot;
+      item_total += block_tot;
+    }
+  }
+  if (!EMIT && threadIdx.x == 0) out_cnt[blockIdx.x] = item_total;
+}
+
 // Work items per partition p: icnt[p] (heavy build side) or icnt[NPART + p]
 // (light); the scan of the 2·NPART counts lists the heavy items first.
 __global__ void k_rj_item_counts(const int64_t *bst, const int64_t *pst, int64_t *icnt) {
@@ -439,6 +558,26 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
   const bool p_outer = build_left ? right_outer : left_outer;
   RJSide bs = rj_partition(s, bk, B.nrows);
   RJSide ps = rj_partition(s, pk, Pr.nrows);
+  const char *rn = getenv("CAPF_RJ_RUNS");  // 0 (tuning): the chain-walking join kernel
+  const bool runs = !(rn && atoi(rn) == 0);
+  if (runs && bs.n > 0) {
+    // equal keys contiguous inside each build partition (h's top 16 bits are the partition)
+    KernelTimer kt(s, "rj_build_sort", 24.0 * (double)bs.n);
+    BufPtr sh = s->alloc(8 * bs.n), sr = s->alloc(4 * bs.n);
+    const int64_t *off = (const int64_t *)bs.pstart->p;
+    size_t tmp = 0;
+    HIP_CHECK(rocprim::segmented_radix_sort_pairs(nullptr, tmp, (const uint64_t *)bs.h->p, (uint64_t *)sh->p,
+                                                  (const uint32_t *)bs.row->p, (uint32_t *)sr->p,
+                                                  (unsigned)bs.n, (unsigned)(RJ_P * RJ_P), off, off + 1, 0, 48,
+                                                  s->stream));
+    BufPtr t = s->alloc(std::max<size_t>(tmp, 16));
+    HIP_CHECK(rocprim::segmented_radix_sort_pairs(t->p, tmp, (const uint64_t *)bs.h->p, (uint64_t *)sh->p,
+                                                  (const uint32_t *)bs.row->p, (uint32_t *)sr->p,
+                                                  (unsigned)bs.n, (unsigned)(RJ_P * RJ_P), off, off + 1, 0, 48,
+                                                  s->stream));
+    bs.h = sh;
+    bs.row = sr;
+  }
   // work items on the device: ⌈probe rows / RJ_PCHUNK⌉ per partition with rows on
   // both sides; partitions whose build side needs several LDS fills ("heavy",
   // skewed keys) are listed first so the dispatcher starts them early
@@ -459,7 +598,7 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
   int64_t total = 0;
   if (nw > 0) {
     KernelTimer kt(s, "rj_join_count", 12.0 * (double)(ps.n + bs.n));
-    hipLaunchKernelGGL(k_rj_join<false>, dim3((unsigned)nw), dim3(RJ_JBLOCK), 0, s->stream,
+    hipLaunchKernelGGL(runs ? k_rj_join_runs<false> : k_rj_join<false>, dim3((unsigned)nw), dim3(RJ_JBLOCK), 0, s->stream,
                        (const RJWork *)dw->p, (const uint64_t *)bs.h->p, (const uint32_t *)bs.row->p,
                        (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
                        (const uint32_t *)ps.row->p, (int64_t *)cnt->p, (const int64_t *)nullptr,
@@ -480,7 +619,7 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
   BufPtr oprobe = s->alloc(8 * std::max<int64_t>(cap, 1)), obuild = s->alloc(8 * std::max<int64_t>(cap, 1));
   if (nw > 0 && (total > 0 || p_outer || b_outer)) {
     KernelTimer kt(s, "rj_join_emit", 12.0 * (double)(ps.n + bs.n) + 16.0 * (double)total);
-    hipLaunchKernelGGL(k_rj_join<true>, dim3((unsigned)nw), dim3(RJ_JBLOCK), 0, s->stream,
+    hipLaunchKernelGGL(runs ? k_rj_join_runs<true> : k_rj_join<true>, dim3((unsigned)nw), dim3(RJ_JBLOCK), 0, s->stream,
                        (const RJWork *)dw->p, (const uint64_t *)bs.h->p, (const uint32_t *)bs.row->p,
                        (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
                        (const uint32_t *)ps.row->p, (int64_t *)nullptr, (const int64_t *)off->p,

@@ -478,12 +478,36 @@ __global__ __launch_bounds__(256) void k_chain2_dot(const uint32_t *h1, const ui
   }
 }
 
-// Σ in·out over the partitioned pipeline's bucket layout (sp.split given):
-// work items = (bucket, 2 Ki-word chunk); an unsplit run's bucket holds packed
-// uint16 pairs (half the bytes of one uint32 per bin), a split run's bucket one
-// uint32 per bin — chosen per item, uniform in the workgroup.  Last workgroup:
-// the hand-off terms; last to finish: *fin = Σ − self-loops.
-constexpr int C2P_CH = 2048;
+// Σ in·out over the partitioned pipeline's bucket layout (sp.split given): an
+// unsplit run's bucket holds packed uint16 pairs in its first half (half the
+// bytes of one uint32 per bin), a split run's bucket one uint32 per bin.  The
+// grid strides over quads (4 words of the half-range, both halves of a split
+// bucket): a wave's 64 quads lie in one bucket, so the format is wave-uniform,
+// and each thread keeps 4 quads' loads in flight before the first use (the
+// per-bucket flags come from LDS).  Packed buckets issue their "high" load at
+// the same address (an L1/L2 hit, no HBM bytes) so the loads stay branch-free.
+// Last C2_HO_BLOCKS workgroups: the hand-off terms; last to finish: *fin.
+__device__ __forceinline__ void c2p_quad(const uint32_t *h, int64_t q, bool split, uint4 &lo, uint4 &hi) {
+  constexpr int64_t HALF = C2P_BW / 2;
+  const int64_t b = q >> 13, w = (q & 8191) * 4;  // HALF / 4 = 8192 quads per bucket
+  const uint32_t *p = h + b * C2P_BW + w;
+  lo = *(const uint4 *)p;
+  hi = *(const uint4 *)(p + (split ? HALF : 0));
+}
+__device__ __forceinline__ unsigned long long c2p_mul(uint4 alo, uint4 ahi, bool sa, uint4 clo, uint4 chi, bool sc) {
+  if (!sa) {
+    ahi = make_uint4(alo.x >> 16, alo.y >> 16, alo.z >> 16, alo.w >> 16);
+    alo = make_uint4(alo.x & 0xFFFF, alo.y & 0xFFFF, alo.z & 0xFFFF, alo.w & 0xFFFF);
+  }
+  if (!sc) {
+    chi = make_uint4(clo.x >> 16, clo.y >> 16, clo.z >> 16, clo.w >> 16);
+    clo = make_uint4(clo.x & 0xFFFF, clo.y & 0xFFFF, clo.z & 0xFFFF, clo.w & 0xFFFF);
+  }
+  return (unsigned long long)alo.x * clo.x + (unsigned long long)alo.y * clo.y +
+         (unsigned long long)alo.z * clo.z + (unsigned long long)alo.w * clo.w +
+         (unsigned long long)ahi.x * chi.x + (unsigned long long)ahi.y * chi.y +
+         (unsigned long long)ahi.z * chi.z + (unsigned long long)ahi.w * chi.w;
+}
 __global__ __launch_bounds__(256) void k_chain2_dot_pairs(const uint32_t *h1, const uint32_t *h2, C2Spill sp,
                                                           unsigned long long *acc, int64_t *fin,
                                                           unsigned int *done) {
@@ -493,37 +517,35 @@ __global__ __launch_bounds__(256) void k_chain2_dot_pairs(const uint32_t *h1, co
   if (blockIdx.x >= nblk) {
     s = c2_handoff_terms(h1, h2, sp, lds, (int)(blockIdx.x - nblk), C2_HO_BLOCKS);
   } else {
-    constexpr int64_t HALF = C2P_BW / 2, PER = HALF / C2P_CH;
-    const int64_t items = (int64_t)sp.nb * PER;
-    for (int64_t it = blockIdx.x; it < items; it += nblk) {
-      const int64_t b = it / PER, w0 = (it % PER) * C2P_CH;
-      const bool si = sp.split[b] != 0, so = sp.split[sp.nb + b] != 0;  // uniform
-      const uint32_t *a = h1 + b * C2P_BW, *c = h2 + b * C2P_BW;
+    __shared__ uint8_t fl[C2_HO_MAXNB];
+    const bool stage = 2 * sp.nb <= C2_HO_MAXNB;
+    if (stage) {
+      for (int i = threadIdx.x; i < 2 * sp.nb; i += blockDim.x) fl[i] = sp.split[i] ? 1 : 0;
+      __syncthreads();
+    }
+    auto sa = [&](int64_t q) { return stage ? fl[q >> 13] != 0 : sp.split[q >> 13] != 0; };
+    auto sc = [&](int64_t q) { return stage ? fl[sp.nb + (q >> 13)] != 0 : sp.split[sp.nb + (q >> 13)] != 0; };
+    const int64_t nq = (int64_t)sp.nb * 8192, stride = (int64_t)nblk * blockDim.x;
+    int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; q + 3 * stride < nq; q += 4 * stride) {
+      uint4 alo[4], ahi[4], clo[4], chi[4];
+      bool fa[4], fc[4];
 #pragma unroll
-      for (int r = 0; r < C2P_CH / (4 * 256); ++r) {
-        const int64_t w = w0 + 4 * (r * 256 + threadIdx.x);
-        uint4 alo, ahi, clo, chi;
-        if (!si) {
-          const uint4 p = *(const uint4 *)(a + w);
-          alo = make_uint4(p.x & 0xFFFF, p.y & 0xFFFF, p.z & 0xFFFF, p.w & 0xFFFF);
-          ahi = make_uint4(p.x >> 16, p.y >> 16, p.z >> 16, p.w >> 16);
-        } else {
-          alo = *(const uint4 *)(a + w);
-          ahi = *(const uint4 *)(a + w + HALF);
-        }
-        if (!so) {
-          const uint4 p = *(const uint4 *)(c + w);
-          clo = make_uint4(p.x & 0xFFFF, p.y & 0xFFFF, p.z & 0xFFFF, p.w & 0xFFFF);
-          chi = make_uint4(p.x >> 16, p.y >> 16, p.z >> 16, p.w >> 16);
-        } else {
-          clo = *(const uint4 *)(c + w);
-          chi = *(const uint4 *)(c + w + HALF);
-        }
-        s += (unsigned long long)alo.x * clo.x + (unsigned long long)alo.y * clo.y +
-             (unsigned long long)alo.z * clo.z + (unsigned long long)alo.w * clo.w +
-             (unsigned long long)ahi.x * chi.x + (unsigned long long)ahi.y * chi.y +
-             (unsigned long long)ahi.z * chi.z + (unsigned long long)ahi.w * chi.w;
+      for (int k = 0; k < 4; ++k) {
+        fa[k] = sa(q + k * stride);
+        fc[k] = sc(q + k * stride);
+        c2p_quad(h1, q + k * stride, fa[k], alo[k], ahi[k]);
+        c2p_quad(h2, q + k * stride, fc[k], clo[k], chi[k]);
       }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s += c2p_mul(alo[k], ahi[k], fa[k], clo[k], chi[k], fc[k]);
+    }
+    for (; q < nq; q += stride) {
+      uint4 alo, ahi, clo, chi;
+      const bool fa = sa(q), fc = sc(q);
+      c2p_quad(h1, q, fa, alo, ahi);
+      c2p_quad(h2, q, fc, clo, chi);
+      s += c2p_mul(alo, ahi, fa, clo, chi, fc);
     }
     s = block_reduce_sum(s, lds);
   }

@@ -41,7 +41,8 @@ constexpr int RJ_TILE = 8192;      // rows per partitioning tile
 constexpr int RJ_PBLOCK = 512;     // partitioning workgroup
 constexpr int RJ_CAP = 4096;       // LDS multimap slots (h 8 B + row 4 B)
 constexpr int RJ_CHUNK = RJ_CAP / 2;  // build rows per LDS fill (load ≤ 1/2)
-constexpr int RJ_PCHUNK = 8192;    // probe rows per work item
+constexpr int RJ_PCHUNK = 8192;    // probe rows per work item (at most)
+constexpr int RJ_PCHUNK_MIN = 256; // ... and at least, when the probe side is small
 constexpr int RJ_JBLOCK = 256;     // join workgroup
 constexpr uint32_t RJ_EMPTY = 0xFFFFFFFFu;
 
@@ -504,21 +505,22 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_join_runs(const RJWork *work, 
 
 // Work items per partition p: icnt[p] (heavy build side) or icnt[NPART + p]
 // (light); the scan of the 2·NPART counts lists the heavy items first.
-__global__ void k_rj_item_counts(const int64_t *bst, const int64_t *pst, int64_t *icnt) {
+__global__ void k_rj_item_counts(const int64_t *bst, const int64_t *pst, int64_t pchunk, int64_t *icnt) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nb = bst[p + 1] - bst[p], np = pst[p + 1] - pst[p];
-  const int64_t items = nb > 0 && np > 0 ? (np + RJ_PCHUNK - 1) / RJ_PCHUNK : 0;
+  const int64_t items = nb > 0 && np > 0 ? (np + pchunk - 1) / pchunk : 0;
   const bool heavy = nb > RJ_CHUNK;
   icnt[p] = heavy ? items : 0;
   icnt[(int64_t)RJ_P * RJ_P + p] = heavy ? 0 : items;
 }
 
-__global__ void k_rj_items(const int64_t *bst, const int64_t *pst, const int64_t *ioff, RJWork *work) {
+__global__ void k_rj_items(const int64_t *bst, const int64_t *pst, int64_t pchunk, const int64_t *ioff,
+                           RJWork *work) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nb = bst[p + 1] - bst[p], q0 = pst[p], q1 = pst[p + 1];
   if (nb == 0 || q1 == q0) return;
   int64_t o = ioff[nb > RJ_CHUNK ? p : (int64_t)RJ_P * RJ_P + p];
-  for (int64_t a = q0; a < q1; a += RJ_PCHUNK) work[o++] = RJWork{p, 0, a, min(q1, a + (int64_t)RJ_PCHUNK)};
+  for (int64_t a = q0; a < q1; a += pchunk) work[o++] = RJWork{p, 0, a, min(q1, a + pchunk)};
 }
 
 __global__ void k_rj_unmatched(const uint8_t *matched, int64_t n, uint8_t *flags) {
@@ -578,20 +580,27 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
     bs.h = sh;
     bs.row = sr;
   }
-  // work items on the device: ⌈probe rows / RJ_PCHUNK⌉ per partition with rows on
+  // work items on the device: ⌈probe rows / pchunk⌉ per partition with rows on
   // both sides; partitions whose build side needs several LDS fills ("heavy",
-  // skewed keys) are listed first so the dispatcher starts them early
+  // skewed keys) are listed first so the dispatcher starts them early.  pchunk
+  // shrinks with the probe side (≈16 items per CU when the rows spread evenly,
+  // at least RJ_PCHUNK_MIN rows) so one hub key's probe rows — whose output is
+  // (its build rows) × (its probe rows) — spread over many workgroups instead
+  // of one carrying the whole product.
   constexpr int64_t NPART = (int64_t)RJ_P * RJ_P;
+  int64_t pchunk = RJ_PCHUNK;
+  while (pchunk > RJ_PCHUNK_MIN && pchunk * 16 * s->num_cus > Pr.nrows) pchunk /= 2;
+  if (const char *e = getenv("CAPF_RJ_PCHUNK")) pchunk = std::max<int64_t>(64, atoll(e));  // tuning
   BufPtr icnt = s->alloc(8 * 2 * NPART), ioff = s->alloc(8 * (2 * NPART + 1));
   hipLaunchKernelGGL(k_rj_item_counts, dim3((unsigned)(NPART / 256)), dim3(256), 0, s->stream,
-                     (const int64_t *)bs.pstart->p, (const int64_t *)ps.pstart->p, (int64_t *)icnt->p);
+                     (const int64_t *)bs.pstart->p, (const int64_t *)ps.pstart->p, pchunk, (int64_t *)icnt->p);
   KERNEL_CHECK();
   const int64_t nw = exclusive_scan_i64(s, (const int64_t *)icnt->p, (int64_t *)ioff->p, 2 * NPART);
   BufPtr dw = s->alloc(sizeof(RJWork) * std::max<int64_t>(nw, 1));
   if (nw > 0) {
     hipLaunchKernelGGL(k_rj_items, dim3((unsigned)(NPART / 256)), dim3(256), 0, s->stream,
-                       (const int64_t *)bs.pstart->p, (const int64_t *)ps.pstart->p, (const int64_t *)ioff->p,
-                       (RJWork *)dw->p);
+                       (const int64_t *)bs.pstart->p, (const int64_t *)ps.pstart->p, pchunk,
+                       (const int64_t *)ioff->p, (RJWork *)dw->p);
     KERNEL_CHECK();
   }
   BufPtr cnt = s->alloc(8 * std::max<int64_t>(nw, 1)), off = s->alloc(8 * (nw + 1));

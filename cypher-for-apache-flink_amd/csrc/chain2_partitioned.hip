@@ -408,13 +408,11 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
 constexpr int C3_TT = 256;
 // tile_loops (2-hop pipeline): the blocks of run row 0 also add their tiles'
 // self-loop counts (P1's per-tile plain stores) into *loops.
-__global__ __launch_bounds__(256) void k_c3_transpose(const uint32_t *meta, uint32_t *meta_t,
-                                                       int64_t ntiles, int nr,
-                                                       unsigned long long *run_total, int64_t tt,
-                                                       uint32_t *bsum = nullptr,
-                                                       const uint32_t *tile_loops = nullptr,
-                                                       unsigned long long *loops = nullptr) {
-  __shared__ uint32_t tilebuf[C3_TT][33];
+__device__ __forceinline__ void c3_transpose_body(uint32_t (*tilebuf)[33], const uint32_t *meta,
+                                                  uint32_t *meta_t, int64_t ntiles, int nr,
+                                                  unsigned long long *run_total, int64_t tt, uint32_t *bsum,
+                                                  const uint32_t *tile_loops, unsigned long long *loops,
+                                                  bool wait_adds = false) {
   __shared__ uint32_t part[8][33];
   const int r0 = blockIdx.y * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads = 32 × 8
@@ -440,7 +438,12 @@ __global__ __launch_bounds__(256) void k_c3_transpose(const uint32_t *meta, uint
     uint32_t c = 0;
 #pragma unroll
     for (int q = 0; q < 8; ++q) c += part[q][tx];
-    if (c && r < nr) atomicAdd(&run_total[r], (unsigned long long)c);
+    if (c && r < nr) {
+      const unsigned long long o = atomicAdd(&run_total[r], (unsigned long long)c);
+      // wait_adds: the returning add has been performed before the caller's
+      // `done` add (no fence: an agent-scope release writes back all of L2)
+      if (wait_adds) asm volatile("" ::"v"(o));
+    }
     // per-(run, tile block) key counts: the balanced P3's split points
     if (bsum && r < nr) bsum[(int64_t)r * gridDim.x + blockIdx.x] = c;
   }
@@ -450,6 +453,15 @@ __global__ __launch_bounds__(256) void k_c3_transpose(const uint32_t *meta, uint
     const int q = idx >> lt, i = idx & (int)(tt - 1);
     if (i < tn && r0 + q < nr) meta_t[(int64_t)(r0 + q) * ntiles + tb + i] = tilebuf[i][q];
   }
+}
+__global__ __launch_bounds__(256) void k_c3_transpose(const uint32_t *meta, uint32_t *meta_t,
+                                                       int64_t ntiles, int nr,
+                                                       unsigned long long *run_total, int64_t tt,
+                                                       uint32_t *bsum = nullptr,
+                                                       const uint32_t *tile_loops = nullptr,
+                                                       unsigned long long *loops = nullptr) {
+  __shared__ uint32_t tilebuf[C3_TT][33];
+  c3_transpose_body(tilebuf, meta, meta_t, ntiles, nr, run_total, tt, bsum, tile_loops, loops);
 }
 
 struct C3Unit {
@@ -491,6 +503,8 @@ struct C3Sides {
   int pairs = 0;       // (fused 2-hop, one slice) exclusive units store packed uint16
                        // pairs in the first half of their bucket's 2^16 words (half
                        // the flush and dot bytes); split runs keep one uint32 per bin
+  int32_t *claim = nullptr;  // the units kernel's split flags: non-null → P3's split units
+                             // clear their own buckets (claim / ready bits, no k_c3_zero)
 };
 
 // CAPF_P3_SPLIT (tuning): split threshold in units of the mean run size
@@ -515,30 +529,38 @@ struct C3Post {
   C2Spill *spill;  // host side: non-null → the hand-off log goes to the dot kernel
 };
 
-__global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(const unsigned long long *run_total,
-                                                         int nr, C3Sides sd, int S, C3Unit *units,
-                                                         int32_t *nunits, int32_t *split,
-                                                         int32_t *order, C3Post post) {
+// The work-list computation, one workgroup of any size (RPT runs per thread,
+// nr ≤ RPT·blockDim.x): by k_c3_units, or by the transpose's last workgroup.
+// `est` holds C3_MAXU words of LDS; run totals are read with device-scope
+// atomics when `coherent` (the transpose's other workgroups added them in this
+// same launch).
+struct C3UnitsOut {
+  C3Unit *units;
+  int32_t *nunits, *split, *order;
+  unsigned int *done;  // the transpose's finished-workgroup counter (zeroed with run_total)
+};
+template <int RPT>
+__device__ void c3_units_body(unsigned long long *run_total, int nr, const C3Sides &sd, int S,
+                              const C3UnitsOut &uo, uint32_t *est, bool coherent) {
   __shared__ unsigned long long lds64[17];
   __shared__ uint32_t lds32[17];
-  __shared__ uint32_t est[C3_MAXU];
   __shared__ uint32_t qcnt[65];
   __shared__ uint32_t maxest;
-  unsigned long long cnt[2], tot = 0;
+  unsigned long long cnt[RPT], tot = 0;
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int r = 2 * threadIdx.x + q;
-    cnt[q] = r < nr ? run_total[r] : 0ull;
+  for (int q = 0; q < RPT; ++q) {
+    const int r = RPT * threadIdx.x + q;
+    cnt[q] = r >= nr ? 0ull : coherent ? atomicAdd(&run_total[r], 0ull) : run_total[r];
     tot += cnt[q];
   }
   unsigned long long total;
   block_exclusive_scan(tot, lds64, total);
   const unsigned long long target =
       max((unsigned long long)sd.split_x16 * total / (16ull * (unsigned long long)max(nr, 1)), 65536ull);
-  uint32_t nu[2], nsum = 0;
+  uint32_t nu[RPT], nsum = 0;
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int r = 2 * threadIdx.x + q;
+  for (int q = 0; q < RPT; ++q) {
+    const int r = RPT * threadIdx.x + q;
     const int sdi = r >= sd.nb ? 1 : 0;
     const int64_t maxsplit = max<int64_t>(1, (sd.t1[sdi] - sd.t0[sdi]) / 256);
     const uint32_t hub = cnt[q] ? (uint32_t)min<int64_t>((int64_t)((cnt[q] + target - 1) / target), maxsplit) : 1u;
@@ -548,8 +570,8 @@ __global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(const unsigned long long
   uint32_t ntot;
   uint32_t off = block_exclusive_scan(nsum, lds32, ntot);
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int r = 2 * threadIdx.x + q;
+  for (int q = 0; q < RPT; ++q) {
+    const int r = RPT * threadIdx.x + q;
     if (!nu[q]) continue;
     const int sdi = r >= sd.nb ? 1 : 0;
     const int64_t b = sd.t0[sdi], len = sd.t1[sdi] - sd.t0[sdi];
@@ -561,24 +583,27 @@ __global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(const unsigned long long
       u.t1 = cnt[q] ? b + len * (k + 1) / nu[q] : b;
       u.slice = (int32_t)(k % (uint32_t)S);
       u.pad = 0;
-      units[off + k] = u;
-      if (off + k < (uint32_t)C3_MAXU) est[off + k] = (uint32_t)min<unsigned long long>(cnt[q] / nu[q], 0xFFFFFFFFull);
+      uo.units[off + k] = u;
+      if (uo.order && off + k < (uint32_t)C3_MAXU)
+        est[off + k] = (uint32_t)min<unsigned long long>(cnt[q] / nu[q], 0xFFFFFFFFull);
     }
     off += nu[q];
-    split[r] = nu[q] > (uint32_t)S;
+    uo.split[r] = nu[q] > (uint32_t)S;
   }
-  if (threadIdx.x == 0) *nunits = (int32_t)ntot;
+  if (threadIdx.x == 0) *uo.nunits = (int32_t)ntot;
 
-  if (!order) return;
+  if (!uo.order) return;
+  int32_t *order = uo.order;
+  const int nt = blockDim.x;
   if (threadIdx.x <= 64) qcnt[threadIdx.x] = 0;
   if (threadIdx.x == 0) maxest = 0;
   __syncthreads();
   const uint32_t nu_all = min(ntot, (uint32_t)C3_MAXU);
-  for (uint32_t i = threadIdx.x; i < nu_all; i += C3_UBLOCK) atomicMax(&maxest, est[i]);
+  for (uint32_t i = threadIdx.x; i < nu_all; i += nt) atomicMax(&maxest, est[i]);
   __syncthreads();
   const unsigned long long mx = max(maxest, 1u);
   // level 0 = largest
-  for (uint32_t i = threadIdx.x; i < nu_all; i += C3_UBLOCK)
+  for (uint32_t i = threadIdx.x; i < nu_all; i += nt)
     atomicAdd(&qcnt[63 - (uint32_t)(63ull * est[i] / mx)], 1u);
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -590,9 +615,39 @@ __global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(const unsigned long long
     }
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < nu_all; i += C3_UBLOCK)
+  for (uint32_t i = threadIdx.x; i < nu_all; i += nt)
     order[atomicAdd(&qcnt[63 - (uint32_t)(63ull * est[i] / mx)], 1u)] = (int32_t)i;
-  for (uint32_t i = nu_all + threadIdx.x; i < ntot; i += C3_UBLOCK) order[i] = (int32_t)i;
+  for (uint32_t i = nu_all + threadIdx.x; i < ntot; i += nt) order[i] = (int32_t)i;
+}
+
+__global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(unsigned long long *run_total, int nr, C3Sides sd,
+                                                         int S, C3UnitsOut uo) {
+  __shared__ uint32_t est[C3_MAXU];
+  c3_units_body<2>(run_total, nr, sd, S, uo, est, false);
+}
+
+// T and U in one launch: the workgroup whose `done` add comes last (every
+// other workgroup's run-total adds have landed) builds the work list, reusing
+// its transpose tile buffer as the LPT estimate array — one kernel boundary
+// (≈ 10 µs of drain and ramp at s24) fewer than T then k_c3_units.
+constexpr int C3_TU_RPT = 8;  // runs per thread of the last workgroup: nr ≤ 2048
+__global__ __launch_bounds__(256) void k_c3_transpose_units(const uint32_t *meta, uint32_t *meta_t,
+                                                             int64_t ntiles, int nr,
+                                                             unsigned long long *run_total, int64_t tt,
+                                                             const uint32_t *tile_loops,
+                                                             unsigned long long *loops, C3Sides sd, int S,
+                                                             C3UnitsOut uo) {
+  __shared__ uint32_t tilebuf[C3_TT][33];
+  __shared__ int last;
+  // every thread's run-total adds have returned (performed at the device-scope
+  // coherence point, where the last workgroup's atomic reads see them) before
+  // this workgroup's `done` add
+  c3_transpose_body(tilebuf, meta, meta_t, ntiles, nr, run_total, tt, nullptr, tile_loops, loops, true);
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(uo.done, 1u) == gridDim.x * gridDim.y - 1;
+  __syncthreads();
+  if (!last) return;
+  c3_units_body<C3_TU_RPT>(run_total, nr, sd, S, uo, &tilebuf[0][0], true);
 }
 
 // Clears every slice of the buckets of split runs (their units flush with
@@ -877,6 +932,24 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
   const uint32_t hist_base = sch.run_total ? (uint32_t)((int64_t)u.slice * C2_BW)
                                            : (uint32_t)(u.slice * slice_stride + (int64_t)(u.run % nb) * C2_BW);
   for (int i = threadIdx.x; i < C2_WORDS + C5_CORR; i += C5_BLOCK) words[i] = 0;
+  // A split run's units flush with atomic adds into bins that must start at
+  // zero: the first unit of (run, slice) to start sets its claim bit and clears
+  // the bucket in HBM, then its ready bit; the others wait for the ready bit
+  // before flushing.  A waiter only ever waits on a workgroup already running
+  // (the claimer), so the wait ends — and k_c3_zero plus a kernel boundary go.
+  const bool zsplit = sd.claim && !u.exclusive;
+  if (zsplit) {
+    __shared__ int zown;
+    if (threadIdx.x == 0) zown = !(atomicOr(&sd.claim[u.run], 2 << u.slice) & (2 << u.slice));
+    __syncthreads();
+    if (zown) {
+      uint4 *z = (uint4 *)(hist + hist_base);
+      for (int i = threadIdx.x; i < C2_BW / 4; i += C5_BLOCK) z[i] = make_uint4(0, 0, 0, 0);
+      __threadfence();
+      __syncthreads();
+      if (threadIdx.x == 0) atomicOr(&sd.claim[u.run], 512 << u.slice);
+    }
+  }
   __syncthreads();
   // wave-uniform values live in SGPRs: uniform loop control, no exec masking
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = lane_id();
@@ -1159,6 +1232,9 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
         ovf.log[k] = make_uint2((sd.packed ? log_base : hist_base) + H, side | ((uint32_t)th << 1));
     }
   }
+  if (zsplit && threadIdx.x == 0)
+    while (!(__hip_atomic_load(&sd.claim[u.run], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) & (512 << u.slice)))
+      __builtin_amdgcn_s_sleep(4);
   __syncthreads();
   if (sd.packed) {  // exclusive static unit: one packed word per bin pair
     uint32_t *h = hist + ((int64_t)u.slice * nb + u.run % nb) * C2_WORDS;
@@ -1321,24 +1397,40 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
     sch.P = s->num_cus;
     sch.table = apportion_table;
   }
+  const C3UnitsOut uo{units, nunits, split, order, (unsigned int *)(nunits + 2)};
+  // CAPF_C3_UNITSK=0: the work list by the transpose's last workgroup (one
+  // kernel boundary fewer, but that one 256-lane workgroup's serial tail made
+  // T+U 55 µs against 35 + 6 µs + a 10 µs boundary at s24); default: k_c3_units
+  const char *uk = getenv("CAPF_C3_UNITSK");
+  const bool fuse_units = !static_units && !app && nr <= C3_TU_RPT * 256 && uk && atoi(uk) == 0;
   {
     KernelTimer kt(s, "c3_transpose", 8.0 * nr * ntiles);
-    hipLaunchKernelGGL(k_c3_transpose, dim3((unsigned)nparts, (nr + 31) / 32), dim3(256), 0,
-                       s->stream, meta, transpose ? (uint32_t *)meta_t->p : nullptr, ntiles, nr,
-                       run_total, tt, app ? (uint32_t *)bsum->p : nullptr,
-                       post ? post->tile_loops : nullptr, post ? post->acc3 + 1 : nullptr);
+    if (fuse_units)
+      hipLaunchKernelGGL(k_c3_transpose_units, dim3((unsigned)nparts, (nr + 31) / 32), dim3(256), 0,
+                         s->stream, meta, transpose ? (uint32_t *)meta_t->p : nullptr, ntiles, nr,
+                         run_total, tt, post ? post->tile_loops : nullptr, post ? post->acc3 + 1 : nullptr,
+                         sd, S, uo);
+    else
+      hipLaunchKernelGGL(k_c3_transpose, dim3((unsigned)nparts, (nr + 31) / 32), dim3(256), 0,
+                         s->stream, meta, transpose ? (uint32_t *)meta_t->p : nullptr, ntiles, nr,
+                         run_total, tt, app ? (uint32_t *)bsum->p : nullptr,
+                         post ? post->tile_loops : nullptr, post ? post->acc3 + 1 : nullptr);
     KERNEL_CHECK();
   }
+  const char *zk = getenv("CAPF_C3_ZEROK");
+  const bool zero_kernel = zk && atoi(zk) == 1;
+  C3Sides sdk = sd;  // as launched: split units clear their buckets unless k_c3_zero does
+  if (!static_units && !zero_kernel) sdk.claim = split;
   if (!static_units) {
-    KernelTimer kt(s, "c3_units", 8.0 * nr);
-    C3Post cp{};
-    if (post) cp = *post;
-    hipLaunchKernelGGL(k_c3_units, dim3(1), dim3(C3_UBLOCK), 0, s->stream,
-                       (const unsigned long long *)run_total, nr, sd, S, units, nunits, split, order, cp);
-    KERNEL_CHECK();
-    // split runs' bins cleared by a full grid (one block per (run, slice) column:
-    // the units kernel's single workgroup took 35 µs for it at s24)
-    {
+    if (!fuse_units) {
+      KernelTimer kt(s, "c3_units", 8.0 * nr);
+      hipLaunchKernelGGL(k_c3_units, dim3(1), dim3(C3_UBLOCK), 0, s->stream, run_total, nr, sd, S, uo);
+      KERNEL_CHECK();
+    }
+    // split runs' bins: cleared by their first P3 unit (C3Sides::claim), or
+    // (CAPF_C3_ZEROK=1, tuning/tests) by a full grid, one block per (run, slice)
+    // column (the units kernel's single workgroup took 35 µs for it at s24)
+    if (zero_kernel) {
       KernelTimer kz(s, "c3_zero", 0.0);
       hipLaunchKernelGGL(k_c3_zero, dim3(4, nr, S), dim3(256), 0, s->stream, (const int32_t *)split,
                          sd.nb, h_in, h_out, slice_stride);
@@ -1372,7 +1464,7 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
                        static_units ? nullptr : (const C3Unit *)units, (const int32_t *)nunits,
                        part, transpose ? (const uint32_t *)meta_t->p : meta, ntiles, sd.nb,
                        rstride, h_in, h_out, slice_stride, ovf,
-                       static_units ? nullptr : (const int32_t *)order, sd, S,
+                       static_units ? nullptr : (const int32_t *)order, sdk, S,
                        transpose ? (int64_t)1 : (int64_t)nr, sch);
     KERNEL_CHECK();
   }

@@ -321,7 +321,8 @@ __global__ __launch_bounds__(256) void k_chain2_hist(Chain2Args a) {
 // and the bin's run unsplit) the half of the bucket's packed pair word.
 // `split_l`: the split flags staged in LDS (null: read sp.split).
 constexpr int64_t C2P_BW = int64_t(1) << 16;  // bins per bucket (chain2_partitioned.hip C2_BW)
-constexpr int C2_HO_BLOCKS = 4;               // workgroups computing the hand-off terms
+constexpr int C2_HO_BLOCKS = 8;               // workgroups computing the hand-off terms (the
+                                              // FIRST ones of the grid: dispatched at once)
 constexpr int C2_HO_MAXNB = 2048;             // split flags staged in LDS (2·nb ≤ this)
 __device__ inline uint32_t c2_stored(const uint32_t *h, const C2Spill &sp, int side, int64_t bin,
                                      const uint8_t *split_l) {
@@ -413,8 +414,9 @@ __device__ unsigned long long c2_handoff_terms(const uint32_t *h1, const uint32_
 // fin != null (the fused count): the workgroup whose `done` add comes last
 // writes *fin = acc[0] − acc[1] (Σ in·out − self-loops) — into the async slot
 // or the pinned host scalar, without a separate kernel or copy.  sp.n != null
-// (the partitioned pipeline): the LAST workgroup of the grid computes the
-// hand-off terms (beside the others' dot, not after it) and adds them to acc[0].
+// (the partitioned pipeline): the first C2_HO_BLOCKS workgroups compute the
+// hand-off terms (beside the others' dot, not after it: dispatched first, their
+// chains of dependent loads overlap the streaming) and add them to acc[0].
 template <bool ONES>
 __global__ __launch_bounds__(256) void k_chain2_dot(const uint32_t *h1, const uint32_t *h2,
                                                     DMap wb, int64_t lo, int64_t len,
@@ -422,16 +424,18 @@ __global__ __launch_bounds__(256) void k_chain2_dot(const uint32_t *h1, const ui
                                                     unsigned int *done = nullptr, C2Spill sp = C2Spill()) {
   __shared__ unsigned long long lds[17];
   unsigned long long s = 0;
-  const unsigned nblk = gridDim.x - (sp.n ? (unsigned)C2_HO_BLOCKS : 0u);  // dot workgroups
-  if (sp.n && blockIdx.x >= nblk) {
-    s = c2_handoff_terms(h1, h2, sp, lds, (int)(blockIdx.x - nblk), C2_HO_BLOCKS);
+  const unsigned ho = sp.n ? (unsigned)C2_HO_BLOCKS : 0u;
+  const unsigned nblk = gridDim.x - ho;  // dot workgroups
+  if (blockIdx.x < ho) {
+    s = c2_handoff_terms(h1, h2, sp, lds, (int)blockIdx.x, C2_HO_BLOCKS);
   } else {
+    const unsigned bid = blockIdx.x - ho;
     const int64_t stride = (int64_t)nblk * blockDim.x;
     // 4 counters per thread per step: dwordx4 loads of both histograms
     const int64_t n4 = len / 4;
     const uint4 *a4 = (const uint4 *)h1;
     const uint4 *b4 = (const uint4 *)h2;
-    int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t i0 = (int64_t)bid * blockDim.x + threadIdx.x;
     if (ONES) {
       // 4 independent dwordx4 pairs in flight per thread before the first use
       for (; i0 + 3 * stride < n4; i0 += 4 * stride) {
@@ -460,7 +464,7 @@ __global__ __launch_bounds__(256) void k_chain2_dot(const uint32_t *h1, const ui
              (unsigned long long)x.w * y.w * w_of<false>(wb, k + 3);
       }
     }
-    for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < len; i += stride)
+    for (int64_t i = 4 * n4 + (int64_t)bid * blockDim.x + threadIdx.x; i < len; i += stride)
       s += (unsigned long long)h1[i] * h2[i] * (ONES ? 1ull : w_of<false>(wb, lo + i));
     s = block_reduce_sum(s, lds);
   }
@@ -486,7 +490,7 @@ __global__ __launch_bounds__(256) void k_chain2_dot(const uint32_t *h1, const ui
 // and each thread keeps 4 quads' loads in flight before the first use (the
 // per-bucket flags come from LDS).  Packed buckets issue their "high" load at
 // the same address (an L1/L2 hit, no HBM bytes) so the loads stay branch-free.
-// Last C2_HO_BLOCKS workgroups: the hand-off terms; last to finish: *fin.
+// First C2_HO_BLOCKS workgroups: the hand-off terms; last to finish: *fin.
 __device__ __forceinline__ void c2p_quad(const uint32_t *h, int64_t q, bool split, uint4 &lo, uint4 &hi) {
   constexpr int64_t HALF = C2P_BW / 2;
   const int64_t b = q >> 13, w = (q & 8191) * 4;  // HALF / 4 = 8192 quads per bucket
@@ -514,9 +518,10 @@ __global__ __launch_bounds__(256) void k_chain2_dot_pairs(const uint32_t *h1, co
   __shared__ unsigned long long lds[17];
   unsigned long long s = 0;
   const unsigned nblk = gridDim.x - C2_HO_BLOCKS;
-  if (blockIdx.x >= nblk) {
-    s = c2_handoff_terms(h1, h2, sp, lds, (int)(blockIdx.x - nblk), C2_HO_BLOCKS);
+  if (blockIdx.x < (unsigned)C2_HO_BLOCKS) {
+    s = c2_handoff_terms(h1, h2, sp, lds, (int)blockIdx.x, C2_HO_BLOCKS);
   } else {
+    const unsigned bid = blockIdx.x - C2_HO_BLOCKS;
     __shared__ uint8_t fl[C2_HO_MAXNB];
     const bool stage = 2 * sp.nb <= C2_HO_MAXNB;
     if (stage) {
@@ -526,7 +531,7 @@ __global__ __launch_bounds__(256) void k_chain2_dot_pairs(const uint32_t *h1, co
     auto sa = [&](int64_t q) { return stage ? fl[q >> 13] != 0 : sp.split[q >> 13] != 0; };
     auto sc = [&](int64_t q) { return stage ? fl[sp.nb + (q >> 13)] != 0 : sp.split[sp.nb + (q >> 13)] != 0; };
     const int64_t nq = (int64_t)sp.nb * 8192, stride = (int64_t)nblk * blockDim.x;
-    int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t q = (int64_t)bid * blockDim.x + threadIdx.x;
     for (; q + 3 * stride < nq; q += 4 * stride) {
       uint4 alo[4], ahi[4], clo[4], chi[4];
       bool fa[4], fc[4];

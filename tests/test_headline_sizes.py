@@ -81,6 +81,26 @@ def test_two_hop_headline_handoff_paths(gpu_session, monkeypatch, ovfk, pairs):
     assert slot.item() == FULL["24"]["two_hop"]
 
 
+@pytest.mark.parametrize("scale", [20, 24])
+@pytest.mark.parametrize("zerok,unitsk", [("0", "1"), ("0", "0"), ("1", "1")],
+                         ids=["claims_clear", "claims_clear_units_in_transpose", "zero_kernel"])
+def test_two_hop_headline_split_runs(gpu_session, monkeypatch, scale, zerok, unitsk):
+    """Hub-split P3 units flush with atomic adds into buckets that must start
+    at zero.  CAPF_P3_SPLIT=0.5 splits every run above half the mean, so most
+    runs split; by default the first unit of each (run, slice) clears its
+    bucket (claim / ready bits) and the others wait for it, CAPF_C3_ZEROK=1
+    clears them with k_c3_zero.  The work list comes from k_c3_units, or with
+    CAPF_C3_UNITSK=0 from the transpose's last workgroup.  Two queries
+    back to back: the second must not see the first one's counters."""
+    monkeypatch.setenv("CAPF_P3_SPLIT", "0.5")
+    monkeypatch.setenv("CAPF_C3_ZEROK", zerok)
+    monkeypatch.setenv("CAPF_C3_UNITSK", unitsk)
+    g = rmat_graph(gpu_session, scale, compact=3)
+    for _ in range(2):
+        assert run(g, TWO_HOP)[0]["count"] == FULL[str(scale)]["two_hop"]
+    assert gpu_session.last_plan() == "fused_chain2"
+
+
 def test_two_hop_headline_async_queue(gpu_session):
     """The pipelined bench mode (capf_table_count_async): 4 in-flight s24
     counts land the fixture in every slot."""

@@ -338,6 +338,9 @@ ColPtr eval_program(Session *s, const Program &p, const std::vector<std::string>
 // Predicate → compacted row index list (rows where predicate is TRUE).
 BufPtr eval_filter(Session *s, const Program &p, const std::vector<std::string> &names,
                    const Data &d, int64_t *out_count);
+// Filter of a table body in one step: the rows passing `p`, its lazy (join
+// output) columns composed by the selection kernel itself.
+DataPtr filter_select(Session *s, const Program &p, const std::vector<std::string> &names, const Data &d);
 // Gather rows (int64 indices, -1 = null row) of a column.
 ColPtr gather_column(Session *s, const ColPtr &c, const int64_t *d_idx, int64_t n,
                      bool idx_may_be_null = false);

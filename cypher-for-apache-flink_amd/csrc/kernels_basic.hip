@@ -132,6 +132,45 @@ BufPtr compact_flags(Session *s, const uint8_t *d_flags, int64_t n, int64_t *out
   return idx;
 }
 
+// Selection of the rows whose flag is set, written through up to SEL_MAX
+// sources at once: out_k[pos] = src_k ? src_k[r] : r.  A filter over a join's
+// output writes the join's composed row indexes directly (li[r], ri[r] of the
+// passing rows) instead of a selection index that each side then composes.
+// Within a tile, rows go round by round (row tile0 + k·SCAN_BLOCK + t): flag
+// reads and output writes coalesce (ballot + wave offsets per round).
+constexpr int SEL_MAX = 4;
+struct SelSrcs {
+  const int64_t *src[SEL_MAX];
+  int64_t *out[SEL_MAX];
+  int ns;
+};
+__global__ __launch_bounds__(SCAN_BLOCK) void k_select_multi(const uint8_t *flags, int64_t n,
+                                                             const int64_t *tile_off, SelSrcs ss) {
+  __shared__ uint32_t wcnt[SCAN_BLOCK / WAVE];
+  const int wv = threadIdx.x / WAVE, lane = lane_id();
+  const int64_t t0 = (int64_t)blockIdx.x * SCAN_TILE;
+  int64_t pos0 = tile_off[blockIdx.x];
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const int64_t r = t0 + (int64_t)k * SCAN_BLOCK + threadIdx.x;
+    const bool f = r < n && flags[r];
+    const unsigned long long m = __ballot(f);
+    if (lane == 0) wcnt[wv] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < SCAN_BLOCK / WAVE; ++w) {
+      before += w < wv ? wcnt[w] : 0u;
+      all += wcnt[w];
+    }
+    if (f) {
+      const int64_t pos = pos0 + before + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+      for (int q = 0; q < ss.ns; ++q) ss.out[q][pos] = ss.src[q] ? ss.src[q][r] : r;
+    }
+    pos0 += all;
+    __syncthreads();
+  }
+}
+
 // ------------------------------------------------------------ index helpers
 __global__ void k_iota(int64_t *out, int64_t start, int64_t m) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
@@ -955,15 +994,153 @@ ColPtr eval_program(Session *s, const Program &p, const std::vector<std::string>
   return o;
 }
 
-BufPtr eval_filter(Session *s, const Program &p, const std::vector<std::string> &names,
-                   const Data &d, int64_t *out_count) {
-  int64_t n = d.nrows;
-  if (n == 0) {
-    *out_count = 0;
-    return s->alloc(0);
+// ------------------------------------------------ conjunctive filter fast path
+// A WHERE that is a conjunction of comparisons — the relational planner's
+// uniqueness filters NOT(r_i = r_j) (RelationalPlanner / VarLengthExpandPlanner
+// isomorphism), key checks, `x < 5` — runs without the stack interpreter (whose
+// dynamically indexed Val stack lives in scratch): each term is [NOT] (a op b),
+// a a column, b a column or an integer literal.  A row passes iff every term is
+// TRUE (a NULL operand makes the term NULL: the row is dropped, as the 3-valued
+// AND under WHERE).  An operand still held as a lazy gather (a join output's
+// column) is read through its index (src[idx[r]], idx −1 = NULL row) instead of
+// being materialised first.
+constexpr int FT_MAX = 8;
+struct FtOperand {
+  ColView v;            // the column (or the lazy gather's source)
+  const int64_t *idx;   // lazy gather index, or null
+  int64_t lit;          // literal (v.data == null and lit_ok)
+  int32_t is_lit;
+  int32_t pad;
+};
+struct FtTerm {
+  FtOperand a, b;
+  int32_t op;   // OP_EQ … OP_GE
+  int32_t neg;  // NOT around the comparison
+};
+struct FtProgram {
+  FtTerm t[FT_MAX];
+  int32_t nt;
+};
+
+__device__ inline bool ft_load(const FtOperand &o, int64_t r, int64_t &val) {
+  if (o.is_lit) {
+    val = o.lit;
+    return true;
+  }
+  int64_t row = r;
+  if (o.idx) {
+    row = o.idx[r];
+    if (row < 0) return false;
+  }
+  if (o.v.valid && !o.v.valid[row]) return false;
+  val = o.v.type == CAPF_TYPE_BOOL ? (((const uint8_t *)o.v.data)[row] ? 1 : 0) : ld_int(o.v, row);
+  return true;
+}
+
+__global__ __launch_bounds__(256) void k_filter_terms(FtProgram fp, int64_t n, uint8_t *flags) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    bool pass = true;
+    for (int k = 0; k < fp.nt; ++k) {
+      const FtTerm &t = fp.t[k];
+      int64_t x = 0, y = 0;
+      const bool ok = ft_load(t.a, r, x) & ft_load(t.b, r, y);
+      bool res = t.op == OP_EQ   ? x == y
+                 : t.op == OP_NEQ ? x != y
+                 : t.op == OP_LT  ? x < y
+                 : t.op == OP_LE  ? x <= y
+                 : t.op == OP_GT  ? x > y
+                                  : x >= y;
+      if (t.neg) res = !res;
+      pass = pass && ok && res;
+    }
+    flags[r] = pass ? 1 : 0;
+  }
+}
+
+static bool ft_operand(const Instr &in, const std::vector<std::string> &pnames,
+                       const std::vector<std::string> &names, const Data &d, FtOperand &o, Type &t) {
+  o = FtOperand{};
+  if (in.op == OP_LIT_INT) {
+    o.is_lit = 1;
+    o.lit = in.i;
+    t = Type::Int64;
+    return true;
+  }
+  if (in.op != OP_COL || in.i < 0 || (size_t)in.i >= pnames.size()) return false;
+  int idx = -1;
+  for (size_t k = 0; k < names.size(); ++k)
+    if (names[k] == pnames[(size_t)in.i]) idx = (int)k;
+  if (idx < 0) return false;
+  const ColPtr &c = d.cols[(size_t)idx];
+  t = c->type;
+  if (t != Type::Int64 && t != Type::String && t != Type::Bool) return false;
+  std::shared_ptr<LazyGather> lz;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    lz = c->lazy;
+  }
+  if (lz && !lz->src->is_const && !lz->src->lazy) {
+    o.v = view_of(lz->src);
+    o.idx = (const int64_t *)lz->idx->p;
+  } else {
+    if (c->is_const) return false;  // (a fill: the interpreter handles it)
+    o.v = view_of(c);
+  }
+  return o.v.data != nullptr;
+}
+
+// Postfix program → terms, or false (the interpreter runs it).
+static bool ft_compile(const Program &p, const std::vector<std::string> &names, const Data &d,
+                       FtProgram &fp) {
+  fp.nt = 0;
+  const auto &c = p.code;
+  size_t end = c.size();
+  int want = 1;
+  if (end > 0 && c[end - 1].op == OP_AND) {
+    want = (int)c[end - 1].i;
+    end -= 1;
+  }
+  if (want < 1 || want > FT_MAX) return false;
+  size_t pc = 0;
+  for (int k = 0; k < want; ++k) {
+    if (pc + 3 > end) return false;
+    FtTerm &t = fp.t[fp.nt++];
+    Type ta, tb;
+    if (!ft_operand(c[pc], p.names, names, d, t.a, ta) || !ft_operand(c[pc + 1], p.names, names, d, t.b, tb))
+      return false;
+    const int32_t op = c[pc + 2].op;
+    if (op < OP_EQ || op > OP_GE || !(op == OP_EQ || op == OP_NEQ || op == OP_LT || op == OP_LE ||
+                                      op == OP_GT || op == OP_GE))
+      return false;
+    if (ta != tb) return false;  // mixed types: the interpreter's rules
+    if (ta != Type::Int64 && op != OP_EQ && op != OP_NEQ) return false;
+    t.op = op;
+    pc += 3;
+    t.neg = 0;
+    if (pc < end && c[pc].op == OP_NOT) {
+      t.neg = 1;
+      pc += 1;
+    }
+  }
+  return pc == end;
+}
+
+// Per-row pass flags of a WHERE program (n > 0).
+static BufPtr filter_flags(Session *s, const Program &p, const std::vector<std::string> &names,
+                           const Data &d) {
+  const int64_t n = d.nrows;
+  BufPtr flags = s->alloc(n);
+  const char *ft_env = getenv("CAPF_FILTER_TERMS");  // 0 (tuning/tests): always the interpreter
+  FtProgram fp{};
+  if (!(ft_env && atoi(ft_env) == 0) && ft_compile(p, names, d, fp)) {
+    KernelTimer kt(s, "filter_terms", (double)n);
+    hipLaunchKernelGGL(k_filter_terms, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s->stream, fp, n,
+                       (uint8_t *)flags->p);
+    KERNEL_CHECK();
+    return flags;
   }
   DeviceProgram dp = upload_program(s, p, names, d);
-  BufPtr flags = s->alloc(n);
   {
     KernelTimer kt(s, "filter_eval", (double)n);
     hipLaunchKernelGGL(k_eval, dim3(grid_for(n, 256)), dim3(256), 0, s->stream,
@@ -971,7 +1148,88 @@ BufPtr eval_filter(Session *s, const Program &p, const std::vector<std::string> 
                        n, (void *)nullptr, (uint8_t *)nullptr, 0, (uint8_t *)flags->p);
     KERNEL_CHECK();
   }
+  return flags;
+}
+
+BufPtr eval_filter(Session *s, const Program &p, const std::vector<std::string> &names,
+                   const Data &d, int64_t *out_count) {
+  int64_t n = d.nrows;
+  if (n == 0) {
+    *out_count = 0;
+    return s->alloc(0);
+  }
+  BufPtr flags = filter_flags(s, p, names, d);
   return compact_flags(s, (const uint8_t *)flags->p, n, out_count);
+}
+
+DataPtr filter_select(Session *s, const Program &p, const std::vector<std::string> &names, const Data &d) {
+  const int64_t n = d.nrows;
+  auto out = std::make_shared<Data>();
+  if (n == 0) {
+    *out = d;
+    return out;
+  }
+  BufPtr flags = filter_flags(s, p, names, d);
+  // the distinct lazy-gather indexes of the columns (their composed indexes are
+  // written by the selection itself) and whether a plain column needs the
+  // selection index
+  std::vector<BufPtr> lazy_idx;
+  bool plain = false;
+  for (auto &c : d.cols) {
+    std::shared_ptr<LazyGather> lz;
+    {
+      std::lock_guard<std::mutex> g(c->mu);
+      lz = c->lazy;
+    }
+    if (lz && !lz->src->is_const) {
+      bool seen = false;
+      for (auto &b : lazy_idx) seen |= b.get() == lz->idx.get();
+      if (!seen) lazy_idx.push_back(lz->idx);
+    } else if (!lz) {
+      plain = true;
+    }
+  }
+  const char *fs_env = getenv("CAPF_FILTER_SELECT");  // 0 (tuning/tests): selection index + composes
+  const int ns = (int)lazy_idx.size() + 1;
+  if ((fs_env && atoi(fs_env) == 0) || !lazy_enabled() || lazy_idx.empty() || ns > SEL_MAX) {
+    int64_t m = 0;
+    BufPtr idx = compact_flags(s, (const uint8_t *)flags->p, n, &m);
+    out->nrows = m;
+    IdxCache cache;
+    for (auto &c : d.cols) out->cols.push_back(gather_lazy(s, c, idx, m, false, &cache));
+    return out;
+  }
+  const int64_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+  BufPtr counts = s->alloc(8 * tiles), offs = s->alloc(8 * tiles);
+  hipLaunchKernelGGL(k_count_flags, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, s->stream,
+                     (const uint8_t *)flags->p, n, (int64_t *)counts->p);
+  KERNEL_CHECK();
+  const int64_t m = exclusive_scan_i64(s, (const int64_t *)counts->p, (int64_t *)offs->p, tiles);
+  out->nrows = m;
+  // the selection index itself (source 0) is written only when a plain column
+  // reads it; otherwise it is a key of the compose cache and never read
+  BufPtr sel = s->alloc(plain ? 8 * std::max<int64_t>(m, 1) : 8);
+  SelSrcs ss{};
+  ss.ns = 0;
+  if (plain) {
+    ss.src[ss.ns] = nullptr;
+    ss.out[ss.ns++] = (int64_t *)sel->p;
+  }
+  IdxCache cache;
+  for (auto &b : lazy_idx) {
+    BufPtr o = s->alloc(8 * std::max<int64_t>(m, 1));
+    ss.src[ss.ns] = (const int64_t *)b->p;
+    ss.out[ss.ns++] = (int64_t *)o->p;
+    cache.entries.emplace_back(std::make_pair((const void *)b.get(), (const void *)sel.get()), o);
+  }
+  if (m > 0) {
+    KernelTimer kt(s, "filter_select", 9.0 * (double)n);
+    hipLaunchKernelGGL(k_select_multi, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, s->stream,
+                       (const uint8_t *)flags->p, n, (const int64_t *)offs->p, ss);
+    KERNEL_CHECK();
+  }
+  for (auto &c : d.cols) out->cols.push_back(gather_lazy(s, c, sel, m, false, &cache));
+  return out;
 }
 
 }  // namespace capf

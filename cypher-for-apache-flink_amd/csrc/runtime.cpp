@@ -384,9 +384,7 @@ static DataPtr materialize_impl(const NodePtr &n) {
     }
     case Kind::Filter: {
       DataPtr c = materialize(n->kids[0]);
-      int64_t m = 0;
-      BufPtr idx = eval_filter(s, n->pred, n->kids[0]->names, *c, &m);
-      return gather_all(s, *c, idx, m);
+      return filter_select(s, n->pred, n->kids[0]->names, *c);
     }
     case Kind::Join: {
       DataPtr l = materialize(n->kids[0]);

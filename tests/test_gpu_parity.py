@@ -271,6 +271,49 @@ def test_filter_parity(pred):
     assert bag(g.filter(pred, H, {}).rows) == bag(o.filter(pred, H, {}).rows)
 
 
+JH = RecordHeader({Var("a"): "a", Var("x"): "x", Var("s"): "s", Var("ka"): "ka",
+                   Var("b"): "b", Var("y"): "y", Var("t"): "t", Var("kb"): "kb"})
+JOIN_FILTERS = [
+    Not(Equals(Var("x"), Var("y"))),  # the relational uniqueness filter r_i <> r_j
+    Ands(Not(Equals(Var("x"), Var("y"))), GreaterThan(Var("a"), IntegerLit(3))),
+    LessThan(Var("x"), Var("y")),
+    Ands(Equals(Var("s"), Var("t")), Not(Equals(Var("a"), Var("b")))),
+    Ands(Not(Equals(Var("x"), Var("y"))), Not(Equals(Var("a"), Var("b"))), LessThan(Var("b"), IntegerLit(9))),
+    Ors(Equals(Var("x"), Var("y")), IsNull(Var("a"))),  # (not a conjunction: the interpreter)
+]
+
+
+@pytest.mark.parametrize("pred", JOIN_FILTERS, ids=[str(p) for p in JOIN_FILTERS])
+@pytest.mark.parametrize("paths", ["default", "interpreter_compose"])
+@pytest.mark.usefixtures("encoding")
+def test_filter_over_join_parity(pred, paths, monkeypatch):
+    """WHERE over a join's (lazy) output: conjunctions of comparisons run as
+    terms read through the join's row indexes, and the selection writes the
+    composed indexes of both sides itself (kernels_basic.hip filter_select);
+    CAPF_FILTER_TERMS=0 / CAPF_FILTER_SELECT=0 force the interpreter and the
+    selection-index + compose path.  Many-to-many keys, NULL operands."""
+    if paths != "default":
+        monkeypatch.setenv("CAPF_FILTER_TERMS", "0")
+        monkeypatch.setenv("CAPF_FILTER_SELECT", "0")
+    rng = np.random.default_rng(11)
+    words = ["p", "q", "r", None]
+    n = 700
+    left = [("a", T_INT, [int(v) if rng.random() > 0.1 else None for v in rng.integers(0, 12, n)], None),
+            ("x", T_INT, [int(v) for v in rng.integers(0, 40, n)], None),
+            ("s", T_STRING, [words[i] for i in rng.integers(0, 4, n)], None),
+            ("ka", T_INT, [int(v) for v in rng.integers(0, 30, n)], None)]
+    right = [("b", T_INT, [int(v) if rng.random() > 0.1 else None for v in rng.integers(0, 12, n)], None),
+             ("y", T_INT, [int(v) for v in rng.integers(0, 40, n)], None),
+             ("t", T_STRING, [words[i] for i in rng.integers(0, 4, n)], None),
+             ("kb", T_INT, [int(v) for v in rng.integers(0, 30, n)], None)]
+    gl, ol = _both(left)
+    gr, orr = _both(right)
+    got = gl.join(gr, "inner", ("ka", "kb")).filter(pred, JH, {}).rows
+    want = ol.join(orr, "inner", ("ka", "kb")).filter(pred, JH, {}).rows
+    assert len(want) > 0
+    assert bag(got) == bag(want)
+
+
 EXPRS = [Add(Var("k"), IntegerLit(3)), Multiply(Var("f"), FloatLit(2.5)), Divide(Var("k"), IntegerLit(3)),
          Subtract(Var("i"), Var("k")), ToFloat(Var("k")), ToInteger(Multiply(Var("f"), FloatLit(1e3))),
          Coalesce(Var("k"), IntegerLit(-1)), Divide(Var("i"), Var("k"))]

@@ -484,15 +484,33 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_join_runs(const RJWork *work, 
       }
       if (EMIT) {
         const int64_t o0 = base + wave_off;
-        for (uint32_t x = lane; x < wtot; x += WAVE) {
-          uint32_t b = 0;  // last lane with wex[b] ≤ x
+        // 4 output positions per lane per round: their build-row loads are
+        // independent, so 4 are in flight before the first store needs one
+        // (a hub key's thousands of matches otherwise cost one load latency
+        // per 64 outputs)
+        constexpr int U = 4;
+        for (uint32_t x0 = 0; x0 < wtot; x0 += U * WAVE) {
+          uint32_t br[U], pr[U];
 #pragma unroll
-          for (int st2 = WAVE / 2; st2 > 0; st2 >>= 1)
-            if (wex[wv][b + st2] <= x) b += st2;
-          const uint32_t br = brow[c0 + wst[wv][b] + (x - wex[wv][b])];
-          oprobe[o0 + x] = wpr[wv][b];
-          obuild[o0 + x] = br;
-          if (bmatched) bmatched[br] = 1;
+          for (int k = 0; k < U; ++k) {
+            const uint32_t x = x0 + k * WAVE + lane;
+            const uint32_t xc = min(x, wtot - 1);
+            uint32_t b = 0;  // last lane with wex[b] ≤ xc
+#pragma unroll
+            for (int st2 = WAVE / 2; st2 > 0; st2 >>= 1)
+              if (wex[wv][b + st2] <= xc) b += st2;
+            br[k] = brow[c0 + wst[wv][b] + (xc - wex[wv][b])];
+            pr[k] = wpr[wv][b];
+          }
+#pragma unroll
+          for (int k = 0; k < U; ++k) {
+            const uint32_t x = x0 + k * WAVE + lane;
+            if (x < wtot) {
+              oprobe[o0 + x] = pr[k];
+              obuild[o0 + x] = br[k];
+              if (bmatched) bmatched[br[k]] = 1;
+            }
+          }
         }
       }
       __syncthreads();  // wsum / wave tables are rewritten by the next step
@@ -501,6 +519,142 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_join_runs(const RJWork *work, 
     }
   }
   if (!EMIT && threadIdx.x == 0) out_cnt[blockIdx.x] = item_total;
+}
+
+// EMIT over output ranges (default with the run-based join).  After COUNT,
+// item i (cnt[i] pairs) becomes ⌈cnt[i] / RJ_SUB_OUT⌉ sub-items, each writing
+// the pairs [lo, hi) of the item's flattened output sequence (probe-row order,
+// then the key's build run): a hub key whose (build run) × (probe rows) product
+// is millions of pairs is written by many workgroups instead of one wave of
+// one.  A sub-item repeats the item's run-table build and lookups up to its
+// range (cheap next to the writes) and flattens each 256-row step over the
+// whole workgroup (block scan of the match counts, owner row by an 8-step
+// search), 4 outputs per lane in flight.  Probe rows are flagged matched
+// (outer joins) by the sub-item holding their first pair.
+constexpr int64_t RJ_SUB_OUT = 32768;
+struct RJSub {
+  int32_t item;
+  int32_t pad;
+  int64_t lo, hi;
+};
+
+__global__ void k_rj_sub_counts(const int64_t *cnt, int64_t nw, int64_t *nsub) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (int64_t)gridDim.x * blockDim.x)
+    nsub[i] = (cnt[i] + RJ_SUB_OUT - 1) / RJ_SUB_OUT;
+}
+
+__global__ void k_rj_subs(const int64_t *cnt, const int64_t *soff, int64_t nw, RJSub *subs) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t o = soff[i];
+    for (int64_t lo = 0; lo < cnt[i]; lo += RJ_SUB_OUT) subs[o++] = RJSub{(int32_t)i, 0, lo, min(cnt[i], lo + RJ_SUB_OUT)};
+  }
+}
+
+__global__ __launch_bounds__(RJ_JBLOCK) void k_rj_emit_ranges(const RJSub *subs, const RJWork *work,
+                                                               const uint64_t *bh, const uint32_t *brow,
+                                                               const int64_t *bstart, const uint64_t *ph,
+                                                               const uint32_t *prow, const int64_t *out_off,
+                                                               int64_t *oprobe, int64_t *obuild,
+                                                               uint8_t *pmatched, uint8_t *bmatched) {
+  __shared__ uint64_t kk[RJ_CHUNK];
+  __shared__ unsigned long long hm[RJ_CHUNK / WAVE];
+  __shared__ uint64_t th[RJ_RUNCAP];
+  __shared__ uint32_t tv[RJ_RUNCAP];
+  __shared__ uint32_t bex[RJ_JBLOCK + 1], bst[RJ_JBLOCK], bpr[RJ_JBLOCK];
+  __shared__ uint32_t lds_sc[17];
+  const RJSub sb = subs[blockIdx.x];
+  const RJWork wk = work[sb.item];
+  const int64_t b0 = bstart[wk.part], b1 = bstart[wk.part + 1];
+  const int wv = threadIdx.x / WAVE, lane = lane_id();
+  const int64_t obase = out_off[sb.item];
+  int64_t rel = 0;  // pairs of the item before the current step
+  for (int64_t c0 = b0; c0 < b1 && rel < sb.hi; c0 += RJ_CHUNK) {
+    const int nc = (int)min<int64_t>((int64_t)RJ_CHUNK, b1 - c0);
+    __syncthreads();
+    for (int i = threadIdx.x; i < RJ_RUNCAP; i += RJ_JBLOCK) tv[i] = 0;
+    for (int i = threadIdx.x; i < RJ_CHUNK; i += RJ_JBLOCK) kk[i] = i < nc ? bh[c0 + i] : ~0ull;
+    __syncthreads();
+    for (int i0 = wv * WAVE; i0 < RJ_CHUNK; i0 += RJ_JBLOCK) {
+      const int i = i0 + lane;
+      const bool head = i < nc && (i == 0 || kk[i] != kk[i - 1]);
+      const unsigned long long m = __ballot(head);
+      if (lane == 0) hm[i0 / WAVE] = m;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nc; i += RJ_JBLOCK) {
+      const unsigned long long m = hm[i / WAVE];
+      if (!((m >> (i & (WAVE - 1))) & 1ull)) continue;
+      int e = nc;
+      const unsigned long long rest = (i & (WAVE - 1)) == WAVE - 1 ? 0ull : m >> ((i & (WAVE - 1)) + 1);
+      if (rest) {
+        e = i + 1 + __builtin_ctzll(rest);
+      } else {
+        for (int w = i / WAVE + 1; w < (nc + WAVE - 1) / WAVE; ++w)
+          if (hm[w]) {
+            e = w * WAVE + __builtin_ctzll(hm[w]);
+            break;
+          }
+      }
+      const uint64_t h = kk[i];
+      uint32_t slot = (uint32_t)h & (RJ_RUNCAP - 1);
+      while (atomicCAS(&tv[slot], 0u, ((uint32_t)i << 16) | (uint32_t)(e - i)) != 0u)
+        slot = (slot + 1) & (RJ_RUNCAP - 1);
+      th[slot] = h;
+    }
+    __syncthreads();
+    for (int64_t q0 = wk.p0; q0 < wk.p1 && rel < sb.hi; q0 += RJ_JBLOCK) {
+      const int64_t q = q0 + threadIdx.x;
+      const bool live = q < wk.p1;
+      const uint64_t h = live ? ph[q] : 0;
+      uint32_t cnt = 0, st = 0;
+      if (live) {
+        uint32_t slot = (uint32_t)h & (RJ_RUNCAP - 1);
+        for (uint32_t v = tv[slot]; v != 0u; slot = (slot + 1) & (RJ_RUNCAP - 1), v = tv[slot])
+          if (th[slot] == h) {
+            cnt = v & 0xFFFFu;
+            st = v >> 16;
+            break;
+          }
+      }
+      uint32_t tot;
+      const uint32_t ex = block_exclusive_scan(cnt, lds_sc, tot);  // (ends in a barrier)
+      if (rel + tot > sb.lo) {  // workgroup-uniform: this step holds pairs of the range
+        bex[threadIdx.x] = ex;
+        bst[threadIdx.x] = st;
+        bpr[threadIdx.x] = live ? prow[q] : 0u;
+        if (threadIdx.x == 0) bex[RJ_JBLOCK] = tot;
+        if (pmatched && cnt && rel + ex >= sb.lo && rel + ex < sb.hi) pmatched[prow[q]] = 1;
+        __syncthreads();
+        const uint32_t x0 = (uint32_t)max<int64_t>(0, sb.lo - rel);
+        const uint32_t x1 = (uint32_t)min<int64_t>((int64_t)tot, sb.hi - rel);
+        constexpr int U = 4;
+        for (uint32_t xb = x0; xb < x1; xb += U * RJ_JBLOCK) {
+          uint32_t br[U], pr[U];
+#pragma unroll
+          for (int k = 0; k < U; ++k) {
+            const uint32_t x = min(xb + k * RJ_JBLOCK + threadIdx.x, x1 - 1);
+            uint32_t b = 0;  // last row with bex[b] ≤ x
+#pragma unroll
+            for (int st2 = RJ_JBLOCK / 2; st2 > 0; st2 >>= 1)
+              if (bex[b + st2] <= x) b += st2;
+            br[k] = brow[c0 + bst[b] + (x - bex[b])];
+            pr[k] = bpr[b];
+          }
+#pragma unroll
+          for (int k = 0; k < U; ++k) {
+            const uint32_t x = xb + k * RJ_JBLOCK + threadIdx.x;
+            if (x < x1) {
+              oprobe[obase + rel + x] = pr[k];
+              obuild[obase + rel + x] = br[k];
+              if (bmatched) bmatched[br[k]] = 1;
+            }
+          }
+        }
+        __syncthreads();  // bex / bst / bpr are rewritten by the next step
+      }
+      rel += tot;
+    }
+  }
 }
 
 // Work items per partition p: icnt[p] (heavy build side) or icnt[NPART + p]
@@ -626,7 +780,26 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
   }
   const int64_t cap = total + (p_outer ? Pr.nrows : 0) + (b_outer ? B.nrows : 0);
   BufPtr oprobe = s->alloc(8 * std::max<int64_t>(cap, 1)), obuild = s->alloc(8 * std::max<int64_t>(cap, 1));
-  if (nw > 0 && (total > 0 || p_outer || b_outer)) {
+  const char *ranges_env = getenv("CAPF_RJ_RANGES");  // 0 (tuning): one EMIT workgroup per item
+  const bool ranges = runs && !(ranges_env && atoi(ranges_env) == 0);
+  if (ranges && nw > 0 && total > 0) {
+    BufPtr nsub = s->alloc(8 * nw), soff = s->alloc(8 * (nw + 1));
+    hipLaunchKernelGGL(k_rj_sub_counts, dim3(grid_for(nw, 256)), dim3(256), 0, s->stream, (const int64_t *)cnt->p,
+                       nw, (int64_t *)nsub->p);
+    KERNEL_CHECK();
+    const int64_t ns = exclusive_scan_i64(s, (const int64_t *)nsub->p, (int64_t *)soff->p, nw);
+    BufPtr subs = s->alloc(sizeof(RJSub) * std::max<int64_t>(ns, 1));
+    hipLaunchKernelGGL(k_rj_subs, dim3(grid_for(nw, 256)), dim3(256), 0, s->stream, (const int64_t *)cnt->p,
+                       (const int64_t *)soff->p, nw, (RJSub *)subs->p);
+    KERNEL_CHECK();
+    KernelTimer kt(s, "rj_join_emit", 12.0 * (double)(ps.n + bs.n) + 16.0 * (double)total);
+    hipLaunchKernelGGL(k_rj_emit_ranges, dim3((unsigned)ns), dim3(RJ_JBLOCK), 0, s->stream, (const RJSub *)subs->p,
+                       (const RJWork *)dw->p, (const uint64_t *)bs.h->p, (const uint32_t *)bs.row->p,
+                       (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p, (const uint32_t *)ps.row->p,
+                       (const int64_t *)off->p, (int64_t *)oprobe->p, (int64_t *)obuild->p,
+                       p_outer ? (uint8_t *)pm->p : nullptr, b_outer ? (uint8_t *)bm->p : nullptr);
+    KERNEL_CHECK();
+  } else if (nw > 0 && (total > 0 || p_outer || b_outer)) {
     KernelTimer kt(s, "rj_join_emit", 12.0 * (double)(ps.n + bs.n) + 16.0 * (double)total);
     hipLaunchKernelGGL(runs ? k_rj_join_runs<true> : k_rj_join<true>, dim3((unsigned)nw), dim3(RJ_JBLOCK), 0, s->stream,
                        (const RJWork *)dw->p, (const uint64_t *)bs.h->p, (const uint32_t *)bs.row->p,

@@ -1037,8 +1037,64 @@ __device__ inline bool ft_load(const FtOperand &o, int64_t r, int64_t &val) {
   return true;
 }
 
-__global__ __launch_bounds__(256) void k_filter_terms(FtProgram fp, int64_t n, uint8_t *flags) {
-  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+// 4 consecutive rows per thread: each term's index and value loads for the 4
+// rows are independent (in flight together), the flags go out as one word.
+__device__ inline void ft_load4(const FtOperand &o, int64_t r0, int64_t val[4], bool ok[4]) {
+  if (o.is_lit) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      val[k] = o.lit;
+      ok[k] = true;
+    }
+    return;
+  }
+  int64_t row[4];
+  if (o.idx) {
+    const longlong2 a = ((const longlong2 *)(o.idx + r0))[0], b = ((const longlong2 *)(o.idx + r0))[1];
+    row[0] = a.x;
+    row[1] = a.y;
+    row[2] = b.x;
+    row[3] = b.y;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) row[k] = r0 + k;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t rr = row[k] < 0 ? 0 : row[k];
+    ok[k] = row[k] >= 0 && !(o.v.valid && !o.v.valid[rr]);
+    val[k] = o.v.type == CAPF_TYPE_BOOL ? (((const uint8_t *)o.v.data)[rr] ? 1 : 0) : ld_int(o.v, rr);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_filter_terms4(FtProgram fp, int64_t n4, uint32_t *flags4) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x) {
+    bool pass[4] = {true, true, true, true};
+    for (int k = 0; k < fp.nt; ++k) {
+      const FtTerm &t = fp.t[k];
+      int64_t x[4], y[4];
+      bool oa[4], ob[4];
+      ft_load4(t.a, 4 * q, x, oa);
+      ft_load4(t.b, 4 * q, y, ob);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bool res = t.op == OP_EQ   ? x[e] == y[e]
+                   : t.op == OP_NEQ ? x[e] != y[e]
+                   : t.op == OP_LT  ? x[e] < y[e]
+                   : t.op == OP_LE  ? x[e] <= y[e]
+                   : t.op == OP_GT  ? x[e] > y[e]
+                                    : x[e] >= y[e];
+        if (t.neg) res = !res;
+        pass[e] = pass[e] && oa[e] && ob[e] && res;
+      }
+    }
+    flags4[q] = (pass[0] ? 1u : 0u) | (pass[1] ? 1u : 0u) << 8 | (pass[2] ? 1u : 0u) << 16 |
+                (pass[3] ? 1u : 0u) << 24;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_filter_terms(FtProgram fp, int64_t r_start, int64_t n, uint8_t *flags) {
+  for (int64_t r = r_start + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
        r += (int64_t)gridDim.x * blockDim.x) {
     bool pass = true;
     for (int k = 0; k < fp.nt; ++k) {
@@ -1135,9 +1191,16 @@ static BufPtr filter_flags(Session *s, const Program &p, const std::vector<std::
   FtProgram fp{};
   if (!(ft_env && atoi(ft_env) == 0) && ft_compile(p, names, d, fp)) {
     KernelTimer kt(s, "filter_terms", (double)n);
-    hipLaunchKernelGGL(k_filter_terms, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s->stream, fp, n,
-                       (uint8_t *)flags->p);
-    KERNEL_CHECK();
+    const int64_t n4 = n / 4;  // (device buffers are hipMalloc blocks: the int64 index pairs load as 16 B)
+    if (n4 > 0) {
+      hipLaunchKernelGGL(k_filter_terms4, dim3(grid_for(n4, 256, 8192)), dim3(256), 0, s->stream, fp, n4,
+                         (uint32_t *)flags->p);
+      KERNEL_CHECK();
+    }
+    if (4 * n4 < n) {
+      hipLaunchKernelGGL(k_filter_terms, dim3(1), dim3(64), 0, s->stream, fp, 4 * n4, n, (uint8_t *)flags->p);
+      KERNEL_CHECK();
+    }
     return flags;
   }
   DeviceProgram dp = upload_program(s, p, names, d);

@@ -468,6 +468,11 @@ struct C2Spill {
   // bin i + 2^15 high), 1 → one uint32 per bin
   const int32_t *split = nullptr;
   int nb = 0;
+  // host side: where the count goes (the pinned scalar or the async slot); the
+  // partitioned pipeline sets p3_dot when its P3 kernel wrote it (the bucket
+  // dots in P3's epilogue: no dot launch)
+  int64_t *fin = nullptr;
+  int p3_dot = 0;
 };
 // d_acc3 = [Σ in·out, self-loops, done counter] (device): the pipeline writes
 // the self-loop total into [1] and clears [0] and [2] itself (no memset needed)

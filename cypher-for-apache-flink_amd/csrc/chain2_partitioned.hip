@@ -207,13 +207,13 @@ __device__ inline C5Raw<W> c5_ld_raw(const uint8_t *p) {
 // group die as its keys appear, so the peak stays within 64 VGPRs.
 template <int W, bool ALIAS, bool CHECK, bool RAGGED, class SH, int DIAG = 0, int UPF = 0>
 // Self-loops go out as one plain uint32 per tile (tile_loops[t], summed by
-// k_c3_units); the tile-0 workgroup also clears the `zwords` words at zbuf
+// k_c3_units); every tile's workgroup also clears its share of the `zwords` words at zbuf
 // (the run totals / work-list header of the post-P1 kernels) — no memset
 // launches in front of or behind P1.
 __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_c5_partition(C5Cols<W> c, uint16_t *part,
                                                             uint32_t *meta,
                                                             uint32_t *tile_loops,
-                                                            int64_t t_base, uint32_t *zbuf, int zwords,
+                                                            int64_t t_base, uint32_t *zbuf, int64_t zwords,
                                                             unsigned long long *zacc) {
   constexpr int TILE = SH::TILE, MAXR = SH::MAXR;
   constexpr int RPT = TILE / C5_BLOCK, GROUPS = RPT / 4;
@@ -231,8 +231,10 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
                                (pb + 4) | (pb + 5) << 16, (pb + 6) | (pb + 7) << 16);
   (void)pad;  // pads are written per run after the scan (no stage prefill)
   for (int i = threadIdx.x; i <= nr; i += C5_BLOCK) cur[i] = 0;
-  if (t == 0 && zbuf)
-    for (int i = threadIdx.x; i < zwords; i += C5_BLOCK) zbuf[i] = 0;
+  if (zbuf) {  // every tile's workgroup clears its share (the hand-off log makes it ~10^5 words)
+    const int64_t per = (zwords + c.ntiles - 1) / c.ntiles, z0 = t * per, z1 = min<int64_t>(zwords, z0 + per);
+    for (int64_t i = z0 + threadIdx.x; i < z1; i += C5_BLOCK) zbuf[i] = 0;
+  }
   if (t == 0 && zacc && threadIdx.x < 3) zacc[threadIdx.x] = 0;  // [Σ, loops, done]
   __syncthreads();
   const int64_t e0 = t * TILE;
@@ -538,6 +540,7 @@ struct C3UnitsOut {
   C3Unit *units;
   int32_t *nunits, *split, *order;
   unsigned int *done;  // the transpose's finished-workgroup counter (zeroed with run_total)
+  int32_t *rnu;        // units per run (P3's bucket-dot epilogue counts them down)
 };
 template <int RPT>
 __device__ void c3_units_body(unsigned long long *run_total, int nr, const C3Sides &sd, int S,
@@ -550,7 +553,9 @@ __device__ void c3_units_body(unsigned long long *run_total, int nr, const C3Sid
 #pragma unroll
   for (int q = 0; q < RPT; ++q) {
     const int r = RPT * threadIdx.x + q;
-    cnt[q] = r >= nr ? 0ull : coherent ? atomicAdd(&run_total[r], 0ull) : run_total[r];
+    cnt[q] = r >= nr ? 0ull
+             : coherent ? __hip_atomic_load(&run_total[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : run_total[r];
     tot += cnt[q];
   }
   unsigned long long total;
@@ -589,6 +594,7 @@ __device__ void c3_units_body(unsigned long long *run_total, int nr, const C3Sid
     }
     off += nu[q];
     uo.split[r] = nu[q] > (uint32_t)S;
+    if (uo.rnu) uo.rnu[r] = (int32_t)nu[q];
   }
   if (threadIdx.x == 0) *uo.nunits = (int32_t)ntot;
 
@@ -659,6 +665,147 @@ __global__ __launch_bounds__(256) void k_c3_zero(const int32_t *split, int nb, u
   uint4 *p = (uint4 *)((r >= nb ? h_out : h_in) + blockIdx.z * slice_stride + (int64_t)(r % nb) * C2_BW);
   for (int i = blockIdx.x * 256 + threadIdx.x; i < C2_BW / 4; i += gridDim.x * 256)
     p[i] = make_uint4(0, 0, 0, 0);
+}
+
+// Σ in·out folded into P3's epilogue (the fused 2-hop count, one slice,
+// packed-pair buckets): the unit whose `bdone` add completes bucket b (all
+// units of runs b and nb + b flushed) sums in[b]·out[b] over the bucket's
+// 2^16 bins plus the bucket's hand-off terms, then every P3 workgroup counts
+// itself done and the last one writes fin = Σ − self-loops — no dot kernel
+// and one kernel boundary fewer.  The flush stores of a unit reach the
+// partner's XCD through the release fence before its `bdone` add (agent
+// scope: L2 write-back), the finisher's acquire fence after it.
+struct C3Fin {
+  const int32_t *rnu;         // units per run (k_c3_units)
+  unsigned int *bdone;        // per bucket: its units that have flushed (zeroed per query)
+  unsigned int *done;         // P3 workgroups finished (zeroed per query)
+  unsigned long long *acc3;   // [Σ in·out, self-loops]
+  int64_t *fin;               // null: the dot kernel runs after P3
+  const int32_t *split;       // per run: 0 = packed pairs, else one uint32 per bin
+  const uint2 *log;           // hand-off log (side bin, side | count << 1)
+  const uint32_t *logn;
+  uint32_t cap;
+  int64_t hl;                 // bins per side (slice stride)
+};
+
+// counter of side `side` at side bin `bin` as stored (packed pair or uint32)
+__device__ inline uint32_t c3_stored(const uint32_t *h, const C3Fin &fz, int nb, int side, int64_t bin) {
+  const int64_t b = bin >> 16, k = bin & 0xFFFF;
+  if (fz.split[side * nb + b]) return h[bin];
+  return (h[b * C2_BW + (k & (C2_WORDS - 1))] >> ((k >> 15) * 16)) & 0xFFFFu;
+}
+
+__device__ inline unsigned long long c3_bucket_dot(const uint32_t *h_in, const uint32_t *h_out, const C3Fin &fz,
+                                                   int nb, int b, uint32_t *lds_words) {
+  unsigned long long s = 0;
+  const bool si = fz.split[b] != 0, so = fz.split[nb + b] != 0;
+  const uint32_t *a = h_in + (int64_t)b * C2_BW, *c = h_out + (int64_t)b * C2_BW;
+  // 8 quads per lane (2^15 words / 1024 lanes / 4): loads in four batches of 2
+  // quads × both sides, in flight together before the first use (this runs at
+  // the tail of a unit: latency, not bandwidth, is its cost; larger batches
+  // spill next to P3's 127-VGPR main loop)
+  static_assert(C2_WORDS / 4 == 8 * C5_BLOCK, "bucket dot: 8 quads per lane");
+#pragma unroll 1
+  for (int half = 0; half < 4; ++half) {
+    uint4 a0[2], c0[2], a1[2], c1[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int q = (half * 2 + k) * C5_BLOCK + threadIdx.x;
+      a0[k] = ((const uint4 *)a)[q];
+      c0[k] = ((const uint4 *)c)[q];
+      a1[k] = ((const uint4 *)(a + (si ? C2_WORDS : 0)))[q];  // (packed: the same line again)
+      c1[k] = ((const uint4 *)(c + (so ? C2_WORDS : 0)))[q];
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const uint32_t al[4] = {a0[k].x, a0[k].y, a0[k].z, a0[k].w}, ah[4] = {a1[k].x, a1[k].y, a1[k].z, a1[k].w};
+      const uint32_t cl[4] = {c0[k].x, c0[k].y, c0[k].z, c0[k].w}, ch[4] = {c1[k].x, c1[k].y, c1[k].z, c1[k].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t xl = si ? al[e] : al[e] & 0xFFFF, xh = si ? ah[e] : al[e] >> 16;
+        const uint32_t yl = so ? cl[e] : cl[e] & 0xFFFF, yh = so ? ch[e] : cl[e] >> 16;
+        s += (unsigned long long)xl * yl + (unsigned long long)xh * yh;
+      }
+    }
+  }
+  // hand-off terms of this bucket: Σ_in Δ·(y + Y) + Σ_out Δ·x, Y = the bin's
+  // out-side hand-offs (an LDS open-addressing map over the bucket's few)
+  const uint32_t ne = min(*fz.logn, fz.cap);
+  if (ne > 0) {
+    constexpr uint32_t MAPN = 2048;
+    uint32_t *mk = lds_words;
+    unsigned long long *mv = (unsigned long long *)(lds_words + MAPN);
+    __shared__ int map_full;
+    for (uint32_t i = threadIdx.x; i < MAPN; i += C5_BLOCK) {
+      mk[i] = 0xFFFFFFFFu;
+      mv[i] = 0;
+    }
+    if (threadIdx.x == 0) map_full = 0;
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < ne; e += C5_BLOCK) {
+      const uint2 y = fz.log[e];
+      const int64_t bin = (int64_t)y.x % fz.hl;
+      if (!(y.y & 1u) || (bin >> 16) != b) continue;
+      const uint32_t kb = (uint32_t)(bin & 0xFFFF);
+      uint32_t h = (kb * 0x9E3779B1u) & (MAPN - 1), probes = 0;
+      for (;;) {
+        const uint32_t prev = atomicCAS(&mk[h], 0xFFFFFFFFu, kb);
+        if (prev == 0xFFFFFFFFu || prev == kb) {
+          atomicAdd(&mv[h], (unsigned long long)(y.y >> 1));
+          break;
+        }
+        h = (h + 1) & (MAPN - 1);
+        if (++probes > MAPN / 2) {
+          map_full = 1;
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < ne; e += C5_BLOCK) {
+      const uint2 x = fz.log[e];
+      const int64_t bin = (int64_t)x.x % fz.hl;
+      if ((bin >> 16) != b) continue;
+      const unsigned long long d = x.y >> 1;
+      if (x.y & 1u) {
+        s += d * c3_stored(h_in, fz, nb, 0, bin);
+      } else {
+        const uint32_t kb = (uint32_t)(bin & 0xFFFF);
+        unsigned long long Y = 0;
+        if (!map_full) {
+          uint32_t h = (kb * 0x9E3779B1u) & (MAPN - 1);
+          for (uint32_t k = 0; k < MAPN; ++k) {
+            const uint32_t c = mk[h];
+            if (c == kb) {
+              Y = mv[h];
+              break;
+            }
+            if (c == 0xFFFFFFFFu) break;
+            h = (h + 1) & (MAPN - 1);
+          }
+        } else {  // (pathological) scan the log
+          for (uint32_t f = 0; f < ne; ++f) {
+            const uint2 y = fz.log[f];
+            if ((y.y & 1u) && (int64_t)y.x % fz.hl == bin) Y += y.y >> 1;
+          }
+        }
+        s += d * (c3_stored(h_out, fz, nb, 1, bin) + Y);
+      }
+    }
+  }
+  return s;
+}
+
+// thread 0 of every P3 workgroup, once: the last one writes fin.
+__device__ inline void c3_fin_arrive(const C3Fin &fz) {
+  __threadfence();
+  if (atomicAdd(fz.done, 1u) == gridDim.x - 1) {
+    __threadfence();
+    const unsigned long long a0 = atomicAdd(fz.acc3, 0ull), a1 = atomicAdd(fz.acc3 + 1, 0ull);
+    // fin may be pinned host memory: a system-scope store
+    __hip_atomic_store(fz.fin, (int64_t)(a0 - a1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+  }
 }
 
 // XCD-aware unit placement.  Workgroup i runs on XCD i mod 8, and P3 holds
@@ -835,7 +982,7 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
                                                             uint32_t *h_out, int64_t slice_stride,
                                                             C3Ovf ovf, const int32_t *order,
                                                             C3Sides sd, int S, int64_t mstride,
-                                                            C5Sched sch) {
+                                                            C5Sched sch, C3Fin fz) {
   // units == null: the static work list of a node-partitioned rank — unit
   // (run, k) counts tile range k of S of the run's side into slice k, or
   // (sch.run_total) the apportioned units: (run, i) into slice base_r + i
@@ -883,9 +1030,11 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
     __syncthreads();
     nu = sbase[nrr];
   }
-  if ((int)blockIdx.x >= nu && order) return;
-  const int ui = order ? order[blockIdx.x] : c3_unit_of((int)blockIdx.x);
-  if (ui >= nu) return;
+  const int ui = (int)blockIdx.x >= nu && order ? nu : order ? order[blockIdx.x] : c3_unit_of((int)blockIdx.x);
+  if (ui >= nu) {
+    if (fz.fin && threadIdx.x == 0) c3_fin_arrive(fz);
+    return;
+  }
   const unsigned long long t_start = ovf.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
   extern __shared__ __attribute__((aligned(16))) uint32_t words[];
   constexpr int NW = C5_BLOCK / WAVE;
@@ -1257,6 +1406,24 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
     }
   }
 
+  if (fz.fin) {
+    __shared__ int zlast;
+    __syncthreads();  // every lane's flush stores are in L2 ...
+    const int b = u.run % nb;
+    if (threadIdx.x == 0) {
+      __threadfence();  // ... and written back (one agent-scope release per workgroup)
+      const unsigned tot = (unsigned)(fz.rnu[b] + fz.rnu[nb + b]);
+      zlast = atomicAdd(&fz.bdone[b], 1u) == tot - 1;
+      if (zlast) __threadfence();  // acquire: the other units' flushes
+    }
+    __syncthreads();
+    if (zlast) {
+      __shared__ unsigned long long lds_dot[17];
+      const unsigned long long t = block_reduce_sum(c3_bucket_dot(h_in, h_out, fz, nb, b, words), lds_dot);
+      if (threadIdx.x == 0 && t) atomicAdd(fz.acc3, t);
+    }
+    if (threadIdx.x == 0) c3_fin_arrive(fz);
+  }
   if (ovf.trace) {  // diagnostics: this unit's span, where it ran
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1281,7 +1448,7 @@ __global__ __launch_bounds__(256) void k_c3_overflow(C3Ovf o, uint32_t *h_in, ui
 
 template <int W, bool ALIAS, bool CHECK, class SH>
 static void launch_c5(Session *s, const C5Cols<W> &c, uint16_t *part, uint32_t *meta,
-                      uint32_t *tile_loops, uint32_t *zbuf, int zwords, unsigned long long *zacc) {
+                      uint32_t *tile_loops, uint32_t *zbuf, int64_t zwords, unsigned long long *zacc) {
   const int64_t nfull = c.n / SH::TILE;
   if (nfull > 0) {
     const char *dg = getenv("CAPF_P1_DIAG");  // diagnostics only: wrong counts
@@ -1323,9 +1490,15 @@ static int64_t c5_post_acc_bytes(int nr, int S, int split_x16, int64_t nkeys, in
   const uint32_t ovf_cap = (uint32_t)(nkeys / (1 << 15) + 64 + 16 * (int64_t)max_units);
   if (max_units_out) *max_units_out = max_units;
   if (ovf_cap_out) *ovf_cap_out = ovf_cap;
-  return 8 * nr + 16 + 4 * nr + (int64_t)sizeof(C3Unit) * max_units + 8 * (int64_t)ovf_cap;
+  // run_total[nr] | nunits[4] | bdone[nr] | hand-off log | split[nr] | rnu[nr] | units
+  return 8 * nr + 16 + 12 * nr + (int64_t)sizeof(C3Unit) * max_units + 8 * (int64_t)ovf_cap;
 }
-static int c5_post_zero_words(int nr) { return (8 * nr + 16) / 4; }
+// words that start at zero: run totals, unit / event / done counters, bucket counters
+// (and the hand-off log: P3's bucket-dot epilogue may read a reserved slot
+// that another bucket's unit has not written yet — a zero entry adds nothing)
+static int64_t c5_post_zero_words(int nr, uint32_t ovf_cap) {
+  return (8 * (int64_t)nr + 16 + 4 * (int64_t)nr + 8 * (int64_t)ovf_cap) / 4;
+}
 
 static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, const C3Sides &sd,
                     int64_t ntiles, int64_t rstride, int64_t nkeys, int S, uint32_t *h_in,
@@ -1363,8 +1536,11 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   BufPtr acc = acc_pre ? acc_pre : s->alloc(acc_bytes);
   unsigned long long *run_total = (unsigned long long *)acc->p;
   int32_t *nunits = (int32_t *)(run_total + nr);  // [0] units, [1] overflow events
-  int32_t *split = nunits + 4;
-  C3Unit *units = (C3Unit *)(split + nr);
+  unsigned int *bdone = (unsigned int *)(nunits + 4);  // per bucket (P3's bucket-dot epilogue)
+  uint2 *log = (uint2 *)(bdone + nr);                    // (12·nr + 16 B in: 8-B aligned, nr even)
+  int32_t *split = (int32_t *)(log + ovf_cap);
+  int32_t *rnu = split + nr;
+  C3Unit *units = (C3Unit *)(rnu + nr);
   // CAPF_P3_LPT=1: largest-first unit order instead of the XCD-grouped run order
   const char *lpt_env = getenv("CAPF_P3_LPT");
   const bool lpt = lpt_env && atoi(lpt_env) == 1;
@@ -1372,7 +1548,7 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   int32_t *order = lpt ? (int32_t *)order_buf->p : nullptr;
   C3Ovf ovf{};
   ovf.n = (uint32_t *)(nunits + 1);
-  ovf.log = (uint2 *)(units + max_units);
+  ovf.log = log;
   ovf.cap = ovf_cap;
   ovf.trace = nullptr;
   // the hand-off log is folded in by the dot kernel (no overflow kernel) when
@@ -1386,7 +1562,7 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
     HIP_CHECK(hipMemsetAsync(trace->p, 0, 32 * (size_t)max_units, s->stream));
     ovf.trace = (unsigned long long *)trace->p;
   }
-  if (!acc_pre) HIP_CHECK(hipMemsetAsync(acc->p, 0, 8 * nr + 16, s->stream));
+  if (!acc_pre) HIP_CHECK(hipMemsetAsync(acc->p, 0, 4 * (size_t)c5_post_zero_words(nr, ovf_cap), s->stream));
   BufPtr bsum = app ? s->alloc(4 * (int64_t)nr * nparts) : BufPtr();
   C5Sched sch{};
   if (app) {
@@ -1397,7 +1573,7 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
     sch.P = s->num_cus;
     sch.table = apportion_table;
   }
-  const C3UnitsOut uo{units, nunits, split, order, (unsigned int *)(nunits + 2)};
+  const C3UnitsOut uo{units, nunits, split, order, (unsigned int *)(nunits + 2), rnu};
   // CAPF_C3_UNITSK=0: the work list by the transpose's last workgroup (one
   // kernel boundary fewer, but that one 256-lane workgroup's serial tail made
   // T+U 55 µs against 35 + 6 µs + a 10 µs boundary at s24); default: k_c3_units
@@ -1460,13 +1636,34 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
     const int grid = app            ? (s->num_cus + nr + 255) / 256 * 256
                      : static_units ? (nr * S + 255) / 256 * 256
                                     : max_units;
+    // CAPF_P3_DOT=1: the fused count's Σ in·out and the final count in P3's
+    // epilogue (no dot kernel, one boundary fewer); default: the dot kernel
+    // after P3 — the epilogue's per-unit tail (release fence, the finisher's
+    // 256 KiB bucket read and hand-off scan) measured 0.51 ms for P3 against
+    // 0.44 + 0.027 ms + a ~10 µs boundary
+    const char *pd = getenv("CAPF_P3_DOT");
+    C3Fin fz{};
+    if (log_to_dot && sd.pairs && S == 1 && !static_units && !app && post->spill->fin && post->acc3 &&
+        pd && atoi(pd) == 1) {
+      fz.rnu = rnu;
+      fz.bdone = bdone;
+      fz.done = (unsigned int *)(nunits + 3);
+      fz.acc3 = post->acc3;
+      fz.fin = post->spill->fin;
+      fz.split = split;
+      fz.log = ovf.log;
+      fz.logn = ovf.n;
+      fz.cap = ovf.cap;
+      fz.hl = slice_stride;
+    }
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(C5_BLOCK), C5_GATHER_LDS, s->stream,
                        static_units ? nullptr : (const C3Unit *)units, (const int32_t *)nunits,
                        part, transpose ? (const uint32_t *)meta_t->p : meta, ntiles, sd.nb,
                        rstride, h_in, h_out, slice_stride, ovf,
                        static_units ? nullptr : (const int32_t *)order, sdk, S,
-                       transpose ? (int64_t)1 : (int64_t)nr, sch);
+                       transpose ? (int64_t)1 : (int64_t)nr, sch, fz);
     KERNEL_CHECK();
+    if (fz.fin) post->spill->p3_dot = 1;
   }
   if (sd.packed) {  // the hand-offs are applied by k_c5_dot_packed
     *packed_ovf = ovf;
@@ -1651,13 +1848,14 @@ static void chain2_c5(Session *s, C5Cols<W> c, bool in_range, uint32_t *h_in, ui
   sd.t0[0] = sd.t0[1] = 0;
   sd.t1[0] = sd.t1[1] = c.ntiles;
   const int S = c5_slices(nr);
-  BufPtr post_acc = s->alloc(c5_post_acc_bytes(nr, S, sd.split_x16, 2 * c.n, nullptr, nullptr));
+  uint32_t ovf_cap = 0;
+  BufPtr post_acc = s->alloc(c5_post_acc_bytes(nr, S, sd.split_x16, 2 * c.n, nullptr, &ovf_cap));
   {
     KernelTimer kt(s, "c5_partition", (2.0 * W + 4.0) * c.n);
     uint16_t *pp = (uint16_t *)part->p;
     uint32_t *mp = (uint32_t *)meta->p;
     uint32_t *tlp = (uint32_t *)tl->p, *zb = (uint32_t *)post_acc->p;
-    const int zw = c5_post_zero_words(nr);
+    const int64_t zw = c5_post_zero_words(nr, ovf_cap);
     const bool alias = c.u2 == c.u1 && c.v2 == c.v1;
     if (alias && !in_range) launch_c5<W, true, true, SH>(s, c, pp, mp, tlp, zb, zw, d_acc3);
     if (alias && in_range) launch_c5<W, true, false, SH>(s, c, pp, mp, tlp, zb, zw, d_acc3);

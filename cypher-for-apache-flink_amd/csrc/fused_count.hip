@@ -512,7 +512,7 @@ __device__ __forceinline__ unsigned long long c2p_mul(uint4 alo, uint4 ahi, bool
          (unsigned long long)ahi.x * chi.x + (unsigned long long)ahi.y * chi.y +
          (unsigned long long)ahi.z * chi.z + (unsigned long long)ahi.w * chi.w;
 }
-__global__ __launch_bounds__(256) void k_chain2_dot_pairs(const uint32_t *h1, const uint32_t *h2, C2Spill sp,
+__global__ __launch_bounds__(1024) void k_chain2_dot_pairs(const uint32_t *h1, const uint32_t *h2, C2Spill sp,
                                                           unsigned long long *acc, int64_t *fin,
                                                           unsigned int *done) {
   __shared__ unsigned long long lds[17];
@@ -1386,6 +1386,10 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
       in_range = in_range && st.min >= lo && st.max <= hi;
     }
     tb = host_trace() ? host_us() : 0;
+    // the count (Σ − loops) straight into the async slot, or into the pinned
+    // host scalar the synchronous path reads after its sync (no D2H copy)
+    int64_t *fin = s->async_out ? s->async_out : s->h_scalars;
+    spill.fin = fin;
     if (n > 0 && want_part &&
         chain2_partitioned(s, pc, n, lo, hi, in_range, h1, h2, (unsigned long long *)acc->p, &spill)) {
       dot_len = chain2_hist_len(len);  // every counter written; loops accumulated on the device
@@ -1404,17 +1408,22 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
         KERNEL_CHECK();
       }
     }
-    {
+    if (spill.p3_dot) {
+      fin_done = true;  // P3's epilogue summed the buckets and wrote the count
+    } else {
       KernelTimer kt(s, "chain2_dot", 8.0 * dot_len);
       // one block per CU (s24: 256 blocks 24 µs, 2048 37 µs — same-address atomics)
       unsigned grid = grid_for(dot_len / 4 + 1, 256, dot_grid(s->num_cus));
-      // the count (Σ − loops) straight into the async slot, or into the pinned
-      // host scalar the synchronous path reads after its sync (no D2H copy)
-      int64_t *fin = s->async_out ? s->async_out : s->h_scalars;
       unsigned int *done = (unsigned int *)((unsigned long long *)acc->p + 2);
       if (spill.split)  // the bucket layout of the partitioned pipeline (+1 block: hand-offs)
-        hipLaunchKernelGGL(k_chain2_dot_pairs, dim3(dot_grid(s->num_cus) + C2_HO_BLOCKS), dim3(256), 0, s->stream, h1, h2,
+      {
+        // CAPF_DOT_BLOCK (tuning): workgroup size of the pairs dot (256 · 4 quads
+        // in flight per lane is ~4 waves per CU; larger groups keep more loads out)
+        const char *db = getenv("CAPF_DOT_BLOCK");
+        const int blk = db && (atoi(db) == 256 || atoi(db) == 512 || atoi(db) == 1024) ? atoi(db) : 256;
+        hipLaunchKernelGGL(k_chain2_dot_pairs, dim3(dot_grid(s->num_cus) + C2_HO_BLOCKS), dim3(blk), 0, s->stream, h1, h2,
                            spill, (unsigned long long *)acc->p, fin, done);
+      }
       else if (wb.ones)  // ONES: Σ in·out is invariant under the node_mix bijection (+1 block: hand-offs)
         hipLaunchKernelGGL(k_chain2_dot<true>, dim3(grid + (spill.n ? C2_HO_BLOCKS : 0)), dim3(256), 0, s->stream, h1, h2,
                            wb.map.m, lo, dot_len, (unsigned long long *)acc->p, fin, done, spill);

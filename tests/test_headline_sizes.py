@@ -101,6 +101,26 @@ def test_two_hop_headline_split_runs(gpu_session, monkeypatch, scale, zerok, uni
     assert gpu_session.last_plan() == "fused_chain2"
 
 
+@pytest.mark.parametrize("split", [None, "0.5"], ids=["runs_whole", "runs_split"])
+def test_two_hop_headline_p3_dot_epilogue(gpu_session, monkeypatch, split):
+    """CAPF_P3_DOT=1: the unit completing a bucket sums in·out over it (plus
+    the bucket's hand-off terms) in P3's epilogue and the last P3 workgroup
+    writes the count — synchronous, asynchronous, whole and split runs, two
+    queries back to back (the hand-off log and bucket counters are cleared by P1)."""
+    import torch
+    monkeypatch.setenv("CAPF_P3_DOT", "1")
+    if split:
+        monkeypatch.setenv("CAPF_P3_SPLIT", split)
+    g = rmat_graph(gpu_session, 24, compact=3)
+    for _ in range(2):
+        assert run(g, TWO_HOP)[0]["count"] == FULL["24"]["two_hop"]
+    slot = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    plan_query(g, TWO_HOP).table.count_async(slot.data_ptr())
+    gpu_session.sync()
+    assert slot.item() == FULL["24"]["two_hop"]
+
+
 def test_two_hop_headline_async_queue(gpu_session):
     """The pipelined bench mode (capf_table_count_async): 4 in-flight s24
     counts land the fixture in every slot."""

@@ -298,6 +298,10 @@ struct Session {
   // small device scratch for scalar results
   int64_t *d_scalars = nullptr;  // 64 slots
   int64_t *h_scalars = nullptr;  // pinned mirror
+  // fine-grained (coherent) pinned word the fused count's last workgroup stores
+  // the result into; the synchronous path polls it instead of waiting for the
+  // stream (the value lands before the kernel's end-of-grid flush and signal)
+  int64_t *h_fin = nullptr;
   // set by capf_table_count_async for the duration of one call: the fused
   // count writes its result to this device int64 and does not wait
   int64_t *async_out = nullptr;

@@ -1324,6 +1324,36 @@ __global__ void k_partial_minus_loops(const unsigned long long *acc, int64_t *ou
   if (threadIdx.x == 0) *out = (int64_t)(acc[0] - acc[1]);
 }
 
+// The synchronous fused count polls the coherent pinned word its last
+// workgroup stores the result into (system scope) instead of waiting for the
+// stream: the value lands before the grid's end-of-kernel flush and completion
+// signal.  The stream is queried every 1024 polls — a fault surfaces as an
+// error, a finished stream without the value is an internal error.
+// CAPF_SPIN_WAIT=1 selects it; measured at s24 (`profiles/r03_bench_s24_spin.jsonl`) the
+// median plan → scalar was 1.111 / 1.117 ms polling against 1.107 / 1.103 ms with
+// hipStreamSynchronize (which already spins) — no gain, so the default waits.
+constexpr int64_t FIN_PENDING = INT64_MIN;
+static bool spin_wait_enabled() {
+  static const bool on = getenv("CAPF_SPIN_WAIT") && atoi(getenv("CAPF_SPIN_WAIT")) == 1;
+  return on;
+}
+static int64_t spin_wait_fin(Session *s) {
+  for (uint32_t it = 1;; ++it) {
+    const int64_t v = __atomic_load_n(s->h_fin, __ATOMIC_ACQUIRE);
+    if (v != FIN_PENDING) return v;
+    if ((it & 1023) == 0) {
+      const hipError_t e = hipStreamQuery(s->stream);
+      if (e == hipSuccess) {
+        const int64_t w = __atomic_load_n(s->h_fin, __ATOMIC_ACQUIRE);
+        if (w != FIN_PENDING) return w;
+        illegal("internal: the fused count finished without delivering its result");
+      }
+      if (e != hipErrorNotReady) HIP_CHECK(e);
+    }
+    __builtin_ia32_pause();
+  }
+}
+
 static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t *out) {
   const double ta = host_trace() ? host_us() : 0;
   double tb = ta;
@@ -1353,6 +1383,7 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
   BufPtr h = s->alloc(8 * std::max<int64_t>(hlen, 1) + 64);
   BufPtr acc = s->alloc(24);  // Σ in·out, self-loops, the dot's done counter
   bool fin_done = false;  // the dot kernel wrote the async count
+  bool spin = false;      // ... into s->h_fin, polled by the synchronous path
   C2Spill spill;          // hand-offs P3 left for the dot (partitioned pipeline)
   bool acc_zeroed = false;  // the partitioned pipeline clears acc itself
   uint32_t *h1 = (uint32_t *)h->p;
@@ -1387,8 +1418,10 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
     }
     tb = host_trace() ? host_us() : 0;
     // the count (Σ − loops) straight into the async slot, or into the pinned
-    // host scalar the synchronous path reads after its sync (no D2H copy)
-    int64_t *fin = s->async_out ? s->async_out : s->h_scalars;
+    // host word the synchronous path polls (no D2H copy, no stream wait)
+    spin = !s->async_out && s->h_fin && spin_wait_enabled();
+    int64_t *fin = s->async_out ? s->async_out : spin ? s->h_fin : s->h_scalars;
+    if (spin) __atomic_store_n(s->h_fin, FIN_PENDING, __ATOMIC_RELAXED);
     spill.fin = fin;
     if (n > 0 && want_part &&
         chain2_partitioned(s, pc, n, lo, hi, in_range, h1, h2, (unsigned long long *)acc->p, &spill)) {
@@ -1451,7 +1484,9 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
     s->sync();
     s->profile["c3_handoffs"].bytes += (double)ne;
   }
-  if (fin_done) {
+  if (fin_done && spin) {
+    *out = (uint64_t)spin_wait_fin(s);
+  } else if (fin_done) {
     s->sync();
     *out = (uint64_t)s->h_scalars[0];
   } else {

@@ -184,8 +184,44 @@ def cpu_baseline(session, graph, scale, budget_s):
 PIPELINE = ("c5_partition", "c3_transpose", "c3_units", "c3_zero", "c5_gather", "c3_overflow", "chain2_hist", "message_pass",
             "semi_partition", "semi_count",
             "chain2_dot", "tri_keys", "tri_sort_keys", "tri_rle", "tri_pairs", "tri_orient",
-            "tri_sort_pairs", "tri_rowptr", "tri_split", "tri_loop3", "tri_count",
+            "tri_sort_pairs", "tri_rowptr", "tri_split", "tri_loop3", "tri_count", "tri_count_packed",
             "rj_partition1", "rj_partition2", "rj_join_count", "rj_join_emit", "gather")
+
+# kernel symbols behind a timer label (the default is "k_" + label); PMC files are
+# matched against these, template arguments stripped
+PMC_SYMBOLS = {"chain2_dot": ("k_chain2_dot", "k_chain2_dot_pairs"),
+               "tri_count_packed": ("k_tri_count_packed", "k_tri_count_passb"),
+               "semi_partition": ("k_c5_shard_partition",), "semi_count": ("k_c5_bits_count",)}
+
+
+def pmc_symbols(label):
+    return PMC_SYMBOLS.get(label, ("k_" + label,))
+
+
+def load_pmc(path, labels):
+    """A committed PMC summary (tools/make_pmc_json.py) — only when its kernels
+    are the kernels that ran: every timer label in `labels` (profiled pass) must
+    have one of its kernel symbols in the file, else the file describes another
+    build's kernels and is refused.  Returns (json or None, provenance dict)."""
+    rel = os.path.relpath(path, ROOT)
+    if not os.path.exists(path):
+        return None, {"file": rel, "rejected": "not collected"}
+    with open(path) as f:
+        j = json.load(f)
+    names = {k.split("<")[0].strip() for k in j.get("kernels", {})}
+    missing = [lb for lb in labels if not any(sym in names for sym in pmc_symbols(lb))]
+    prov = {"file": rel, "lib": j.get("lib"), "pmc_kernels": sorted(j.get("kernels", {}))}
+    if missing:
+        prov["rejected"] = f"no counters for kernels that ran: {missing}"
+        return None, prov
+    return j, prov
+
+
+def pmc_bytes_of(j, labels):
+    """Corrected HBM bytes per launch of the kernels behind `labels`."""
+    syms = {sym for lb in labels for sym in pmc_symbols(lb)}
+    return sum(v["read_bytes"] + v["write_bytes"] for k, v in j["kernels"].items()
+               if k.split("<")[0].strip() in syms)
 
 
 def pipeline_roofline(prof, steps, compulsory_bytes, traffic_per_query=None):
@@ -225,11 +261,12 @@ def tri_roofline(prof, steps, n_nodes, traffic_per_query=None):
     probes = prof.get("tri_probes", {}).get("bytes", 0.0) / steps
     hits = prof.get("tri_hits", {}).get("bytes", 0.0) / steps
     edges = prof.get("tri_oriented_edges", {}).get("bytes", 0.0) / steps
-    t = per.get("tri_count", 0.0)
+    lab = "tri_count_packed" if "tri_count_packed" in per else "tri_count"
+    t = per.get(lab, 0.0)
     algo = 4.0 * probes + 16.0 * hits + 20.0 * edges + 8.0 * n_nodes
     achieved = algo / (t * 1e-3) / 1e9 if t > 0 else None
     return {
-        "bound": "hbm", "kernel": "tri_count (closing-edge probes)",
+        "bound": "hbm", "kernel": f"{lab} (closing-edge probes)",
         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBS if achieved else None,
         "traffic": traffic_per_query, "algorithmic_bytes_per_launch": algo,
@@ -383,8 +420,10 @@ def run_reach_leg(args):
     """Config 5 at its BASELINE size: 2^16 Person nodes, R-MAT
     KNOWS rels with edge factor 30, MATCH (a:Person)-[:KNOWS*1..3]->(b:Person)
     WITH DISTINCT a, b WITH a, count(*) AS reach RETURN reach, count(*) AS n
-    through the planner (the fused var-length reach, csrc/var_length_reach.hip).
-    A step = plan call → the histogram rows on the host; value = distinct (a, b)
+    through the planner: the unchanged relational plan (join chains, UNION ALL,
+    DISTINCT, GROUP BY) whose Group the runtime recognises in its plan DAG and
+    evaluates by the fused var-length reach (fused_count.hip::try_fused_reach →
+    csrc/var_length_reach.hip).  A step = plan call → the histogram rows on the host; value = distinct (a, b)
     pairs / median step.  Parity: the histogram is the committed fixture
     (tests/golden/config5_sf10.json, C bitset BFS)."""
     import torch  # noqa: F401
@@ -402,8 +441,11 @@ def run_reach_leg(args):
     q = reach_query()
     step = lambda: run(g, q)  # noqa: E731
     t0 = time.perf_counter()
+    s.reset_profile()
     res = step()
     first_ms = (time.perf_counter() - t0) * 1e3
+    if s.last_plan() != "fused_var_length_reach":
+        raise SystemExit(f"config 5 did not take the fused reach (plan {s.last_plan()})")
     for _ in range(args.warmup):
         step()
     res, times = timed_singles(step, args.steps, s.sync)
@@ -431,11 +473,8 @@ def run_reach_leg(args):
     lev_ms = lev.get("total_ms", 0.0) / max(1, lev.get("launches", 1))
     lev_bytes = lev.get("bytes", 0.0) / max(1, lev.get("launches", 1))
     achieved = lev_bytes / (lev_ms * 1e-3) / 1e9 if lev_ms > 0 else None
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_reach_s16.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            traffic = json.load(f).get("vr_level_bytes_per_launch")
+    j, pmc_prov = load_pmc(os.path.join(ROOT, "profiles", f"pmc_reach_s{args.scale}.json"), ["vr_level"])
+    traffic = pmc_bytes_of(j, ["vr_level"]) if j is not None else None  # per vr_level dispatch
     result = {
         "metric": REACH_METRIC, "value": pairs / (median_ms * 1e-3), "unit": "distinct (a, b) pairs/s",
         "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": median_ms,
@@ -444,7 +483,9 @@ def run_reach_leg(args):
                  f"{args.edge_factor}, every node a Person, generated in HBM before timing"),
         "config": {"workload": workload_name(args), "scale": args.scale, "nodes": n, "rels": m,
                    "distinct_pairs": pairs, "sources_reaching": sum(c for _, c in hist),
-                   "plan": "fused var-length reach (planner._fused_reach → capf_var_length_reach)",
+                   "plan": ("relational plan through the Table SPI; Group(a; count) over Distinct(a, b) over the "
+                            "UNION ALL of the *1..3 join chains recognised in the runtime DAG → fused "
+                            "var-length reach (try_fused_reach)"),
                    "steps_mode": "K single queries, plan call -> histogram rows on the host; value = pairs / median",
                    "ms_per_query_mean": sum(times) * 1e3 / len(times), "ms_per_query_min": min(times) * 1e3,
                    "first_query_ms": first_ms, "parity": parity},
@@ -456,7 +497,8 @@ def run_reach_leg(args):
             "algorithmic_bytes_definition": ("8 B per rel per source word (the source's frontier word, pulled "
                                              "along every in-edge) + 24 B per node per source word (frontier, "
                                              "next frontier, visited)"),
-            "kernel_ms": lev_ms, "kernel_ms_per_query": per, "device_ms_per_query": sum(per.values())},
+            "kernel_ms": lev_ms, "kernel_ms_per_query": per, "device_ms_per_query": sum(per.values()),
+            "traffic_source": pmc_prov},
     }
     if not args.no_cpu:
         src, _ = rels.column_arrays("source")
@@ -530,18 +572,19 @@ def run_single(args):
     traffic = None
     pfx = {"triangle": "tri_", "one_hop_person": "c2_"}.get(args.query, "")
     pmc = os.path.join(ROOT, "profiles", f"pmc_{pfx}s{args.scale}.json")
-    if os.path.exists(pmc) and args.query in ("two_hop", "triangle", "one_hop_person"):
-        with open(pmc) as f:
-            j = json.load(f)
-            tri = [v["read_bytes"] + v["write_bytes"] for k, v in j.get("kernels", {}).items()
-                   if k.startswith("k_tri_count")]  # both passes of the count
-            traffic = j.get("hbm_bytes_per_query") if args.query != "triangle" else (sum(tri) if tri else None)
+    ran = sorted(k for k, v in prof.items() if k in PIPELINE and v["total_ms"] > 0)
+    if args.query == "triangle":  # the count kernels (the CSR is built by the first query)
+        ran = [k for k in ran if k.startswith("tri_count")]
+    j, pmc_prov = load_pmc(pmc, ran)
+    if j is not None:
+        traffic = pmc_bytes_of(j, ran) if args.query == "triangle" else j.get("hbm_bytes_per_query")
     ms_per_step = median_ms
     if args.query == "triangle":
         roof = tri_roofline(prof, prof_steps, n_nodes, traffic)
     else:
         roof = pipeline_roofline(prof, prof_steps, compulsory, traffic)
         roof["end_to_end_frac"] = compulsory / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS
+    roof["traffic_source"] = pmc_prov
     result = {
         "metric": {"two_hop": METRIC, "triangle": TRI_METRIC, "one_hop_person": ONE_HOP_METRIC}[args.query],
         "value": count / (median_ms * 1e-3),

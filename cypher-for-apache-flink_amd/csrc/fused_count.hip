@@ -593,6 +593,9 @@ struct JoinGraph {
   std::vector<Leaf> leaves;
   std::vector<std::pair<ColRef, ColRef>> eqs;
   std::vector<std::pair<ColRef, ColRef>> neqs;
+  // literal columns met on the way (withColumns of literals): ColRef{-2, k}
+  // refers to lits[k]
+  std::vector<Program> lits;
 };
 
 static bool collect(const NodePtr &n, JoinGraph &g, std::vector<ColRef> &out);
@@ -671,7 +674,10 @@ static bool collect(const NodePtr &n, JoinGraph &g, std::vector<ColRef> &out) {
       if (!collect(n->kids[0], g, c)) return false;
       out = c;
       out.resize(n->names.size(), ColRef{-2, -1});
-      for (int t : n->target_index) out[t] = ColRef{-2, -1};
+      for (size_t k = 0; k < n->exprs.size(); ++k) {
+        out[n->target_index[k]] = ColRef{-2, (int)g.lits.size()};
+        g.lits.push_back(n->exprs[k]);
+      }
       return true;
     }
     case Kind::Filter: {
@@ -1066,6 +1072,22 @@ static bool tree_count(Session *s, JoinGraph &g, unsigned long long *d_acc) {
 }
 
 // Union-find merge of leaves for one inclusion–exclusion term.
+// Are the values of column `col` of a (materialisable) base node non-null and
+// pairwise distinct?  Dense statistics answer at once; otherwise uniqueness is
+// verified by grouping ONCE and cached on the (immutable) column.
+static bool column_unique(const NodePtr &node, int col) {
+  DataPtr d = materialize(node);
+  const ColStats &st = column_stats(node->s, d->cols[col]);
+  if (st.non_null != d->nrows) return false;
+  if (st.dense_unique) return true;
+  const ColPtr &idc = d->cols[col];
+  if (idc->unique_flag < 0) {
+    Grouping gr = group_rows(node->s, *d, {col});
+    idc->unique_flag = gr.ngroups == d->nrows ? 1 : 0;
+  }
+  return idc->unique_flag == 1;
+}
+
 static bool apply_equalities(const JoinGraph &g, const std::vector<int> &subset, JoinGraph &out) {
   const int L = (int)g.leaves.size();
   std::vector<int> rep(L);
@@ -1084,18 +1106,7 @@ static bool apply_equalities(const JoinGraph &g, const std::vector<int> &subset,
     const Leaf &la = g.leaves[a.leaf], &lb = g.leaves[b.leaf];
     if (la.node != lb.node || !la.filters.empty() || !lb.filters.empty() || a.col != b.col)
       return false;
-    DataPtr d = materialize(la.node);
-    const ColStats &st = column_stats(la.node->s, d->cols[a.col]);
-    if (!(st.dense_unique && st.non_null == d->nrows)) {
-      // uniqueness of a non-dense id column: verified by grouping ONCE, then
-      // cached on the (immutable) column
-      const ColPtr &idc = d->cols[a.col];
-      if (idc->unique_flag < 0) {
-        Grouping gr = group_rows(la.node->s, *d, {a.col});
-        idc->unique_flag = (gr.ngroups == d->nrows && st.non_null == d->nrows) ? 1 : 0;
-      }
-      if (!idc->unique_flag) return false;
-    }
+    if (!column_unique(la.node, a.col)) return false;
     int ra = find(a.leaf), rb = find(b.leaf);
     if (ra != rb) rep[rb] = ra;
   }
@@ -1613,6 +1624,365 @@ bool try_fused_count(const NodePtr &n, int64_t *out) {
   return true;
 }
 
+
+// ============================================================ fused reach
+// Config 5 below the Table SPI.  The unchanged okapi front end lowers
+//   MATCH (a)-[:T*1..u]->(b) WITH DISTINCT a, b WITH a, count(*) AS reach
+// into (DirectedVarLengthExpandPlanner, VarLengthExpandPlanner.scala:82-259;
+// Distinct RelationalOperator.scala:325-332; Aggregate :334-346)
+//   Group(a-columns; count(*))
+//     ← [column copies] ← Distinct(a-columns, b-columns) ← [column copies]
+//     ← UNION ALL over k = 1..u of
+//         S_a ⋈[a = start(e1)] E ⋈[end(e1) = start(e2)] E … E ⋈[end(ek) = b] S_b
+//         → Filter(NOT(e_i = e_j)) → withColumns(NULL padding)
+// which would materialise every path (~1e10 rows at SF10).  When the DAG has
+// exactly this shape, the Group is evaluated by the multi-source BFS of
+// var_length_reach.hip instead — CAPF's Calcite rule set plays the same
+// physical-choice role (flink-cypher/.../api/CAPFSession.scala:83-91).
+// Exact for lower bound 1 (directed): the DISTINCT (a, b) pairs of
+// relationship-isomorphic paths of length 1..u are exactly the pairs joined by
+// a walk of length 1..u (cutting the closed sub-walk between two uses of a rel
+// leaves a shorter walk with the same endpoints), so the isomorphism filters
+// do not change the answer.  Group keys other than a's id must be columns of
+// S_a (functions of the unique id) or literals; DISTINCT columns columns of
+// S_a / S_b or literals.  Any other shape returns false (relational path).
+
+static bool prog_eq(const Program &a, const Program &b) {
+  if (a.code.size() != b.code.size() || a.names != b.names) return false;
+  for (size_t i = 0; i < a.code.size(); ++i)
+    if (a.code[i].op != b.code[i].op || a.code[i].i != b.code[i].i ||
+        __builtin_bit_cast(uint64_t, a.code[i].f) != __builtin_bit_cast(uint64_t, b.code[i].f))
+      return false;
+  return true;
+}
+
+static bool progs_eq(const std::vector<Program> &a, const std::vector<Program> &b) {
+  if (a.size() != b.size()) return false;
+  for (size_t i = 0; i < a.size(); ++i)
+    if (!prog_eq(a[i], b[i])) return false;
+  return true;
+}
+
+// A tracked column: index in the current node, or a literal.
+struct TCol {
+  int col = -1;
+  const Program *lit = nullptr;
+};
+
+static bool reach_reject(const char *why) {
+  static const bool trace = getenv("CAPF_TRACE_FUSE") && atoi(getenv("CAPF_TRACE_FUSE")) == 1;
+  if (trace) fprintf(stderr, "[capf] fused reach not applied: %s\n", why);
+  return false;
+}
+
+static bool is_literal_program(const Program &p) { return p.code.size() == 1 && p.code[0].op != OP_COL; }
+
+// Descends through column-mapping operators (Select; withColumns whose
+// expressions are column copies or literals), re-expressing the tracked
+// columns; returns the first other node.
+static NodePtr through_mappings(NodePtr n, std::vector<TCol> &cols) {
+  for (;;) {
+    if (n->kind == Kind::Select) {
+      for (auto &c : cols)
+        if (!c.lit) c.col = n->sel_index[c.col];
+      n = n->kids[0];
+      continue;
+    }
+    if (n->kind == Kind::WithColumns) {
+      for (auto &p : n->exprs)
+        if (p.code.size() != 1) return n;
+      const NodePtr &kid = n->kids[0];
+      for (auto &c : cols) {
+        if (c.lit) continue;
+        int k = -1;
+        for (size_t t = 0; t < n->target_index.size(); ++t)
+          if (n->target_index[t] == c.col) k = (int)t;
+        if (k < 0) continue;  // passes through at the same index
+        const Program &p = n->exprs[k];
+        if (is_literal_program(p)) {
+          c.lit = &p;
+          c.col = -1;
+        } else {
+          const int64_t ni = p.code[0].i;
+          if (ni < 0 || (size_t)ni >= p.names.size()) return n;
+          c.col = kid->col_index(p.names[(size_t)ni]);
+          if (c.col < 0) return n;
+        }
+      }
+      n = kid;
+      continue;
+    }
+    return n;
+  }
+}
+
+struct ReachBranch {
+  NodePtr base;
+  std::vector<TCol> cols;
+};
+
+static bool union_branches(NodePtr n, std::vector<TCol> cols, std::vector<ReachBranch> &out) {
+  n = through_mappings(n, cols);
+  if (n->kind != Kind::Union) {
+    out.push_back(ReachBranch{n, cols});
+    return out.size() <= 64;
+  }
+  std::vector<TCol> rc = cols;
+  for (auto &c : rc)
+    if (!c.lit) {
+      c.col = n->kids[1]->col_index(n->names[c.col]);
+      if (c.col < 0) return false;
+    }
+  return union_branches(n->kids[0], cols, out) && union_branches(n->kids[1], rc, out);
+}
+
+// One branch's role of a tracked column.
+struct RCol {
+  int role = -1;  // 0: S_a column, 1: S_b column, 2: literal
+  int col = -1;
+  Program lit;     // role 2 (a copy: the branch's join graph is temporary)
+};
+
+struct ReachShape {
+  Leaf sa, sb, rel;
+  int x = -1, y = -1, cs = -1, cd = -1;  // S_a / S_b id columns, rel start / end columns
+  int k = 0;                              // rel leaves in the chain
+  std::vector<RCol> roles;                // per tracked column
+};
+
+static bool leaf_eq(const Leaf &a, const Leaf &b) {
+  return a.node == b.node && progs_eq(a.filters, b.filters) && a.col_eqs == b.col_eqs;
+}
+
+// The chain S_a ⋈ E ⋈ … ⋈ E ⋈ S_b of one branch; `a_cols` are tracked columns
+// that must lie on S_a (the group keys).
+static bool reach_branch(const ReachBranch &br, const std::vector<int> &a_cols, ReachShape &sh) {
+  JoinGraph g;
+  std::vector<ColRef> refs;
+  if (br.base->kind != Kind::Join && br.base->kind != Kind::Filter) return reach_reject("branch check 1");
+  if (!collect(br.base, g, refs)) return reach_reject("branch check 2");
+  const int L = (int)g.leaves.size();
+  if (L < 3 || (int)g.eqs.size() != L - 1) return reach_reject("branch check 3");
+  // tracked column → (leaf, col) or literal
+  std::vector<ColRef> tr(br.cols.size());
+  std::vector<const Program *> tl(br.cols.size(), nullptr);
+  for (size_t i = 0; i < br.cols.size(); ++i) {
+    if (br.cols[i].lit) {
+      tl[i] = br.cols[i].lit;
+      continue;
+    }
+    tr[i] = refs[br.cols[i].col];
+    if (tr[i].leaf == -2 && tr[i].col >= 0) tl[i] = &g.lits[tr[i].col];  // copied into the roles
+    else if (tr[i].leaf < 0) return reach_reject("branch check 4");
+  }
+  int la = -1;
+  for (int i : a_cols)
+    if (!tl[i]) {
+      if (la >= 0 && tr[i].leaf != la) return reach_reject("branch check 5");
+      la = tr[i].leaf;
+    }
+  if (la < 0) return reach_reject("branch check 6");
+  auto edges_of = [&](int leaf) {
+    std::vector<std::pair<int, ColRef>> r;  // (my col, other)
+    for (auto &e : g.eqs) {
+      if (e.first.leaf == leaf) r.emplace_back(e.first.col, e.second);
+      if (e.second.leaf == leaf) r.emplace_back(e.second.col, e.first);
+    }
+    return r;
+  };
+  auto ea = edges_of(la);
+  if (ea.size() != 1) return reach_reject("branch check 7");
+  sh.sa = g.leaves[la];
+  sh.x = ea[0].first;
+  int cur = ea[0].second.leaf, entry = ea[0].second.col, prev = la, lb = -1;
+  std::vector<char> seen(L, 0);
+  seen[la] = 1;
+  sh.k = 0;
+  sh.cs = entry;
+  for (;;) {
+    if (cur < 0 || seen[cur]) return reach_reject("branch check 8");
+    seen[cur] = 1;
+    auto e = edges_of(cur);
+    if (e.size() == 1) {  // the far end: S_b
+      lb = cur;
+      sh.y = entry;
+      break;
+    }
+    if (e.size() != 2) return reach_reject("branch check 9");
+    const Leaf &lr = g.leaves[cur];
+    if (sh.k == 0) sh.rel = lr;
+    else if (!leaf_eq(lr, sh.rel)) return reach_reject("branch check 10");
+    if (entry != sh.cs) return reach_reject("branch check 11");
+    const auto &out = e[0].second.leaf == prev && e[0].first == entry ? e[1] : e[0];
+    if (out.first == entry) return reach_reject("branch check 12");
+    if (sh.k == 0) sh.cd = out.first;
+    else if (out.first != sh.cd) return reach_reject("branch check 13");
+    ++sh.k;
+    prev = cur;
+    cur = out.second.leaf;
+    entry = out.second.col;
+  }
+  for (int i = 0; i < L; ++i)
+    if (!seen[i]) return reach_reject("branch check 14");
+  if (sh.k < 1 || lb < 0) return reach_reject("branch check 15");
+  sh.sb = g.leaves[lb];
+  if (sh.sa.node == sh.rel.node || sh.sb.node == sh.rel.node) return reach_reject("branch check 16");
+  if (!sh.rel.col_eqs.empty() || !sh.sa.col_eqs.empty() || !sh.sb.col_eqs.empty()) return reach_reject("branch check 17");
+  // isomorphism filters: NOT(e_i = e_j) on one unique rel column
+  for (auto &ne : g.neqs) {
+    if (ne.first.leaf == ne.second.leaf || ne.first.col != ne.second.col) return reach_reject("branch check 18");
+    if (ne.first.leaf == la || ne.first.leaf == lb || ne.second.leaf == la || ne.second.leaf == lb)
+      return reach_reject("branch check 19");
+    if (!column_unique(sh.rel.node, ne.first.col)) return reach_reject("branch check 20");
+  }
+  // roles of the tracked columns
+  sh.roles.assign(br.cols.size(), RCol{});
+  for (size_t i = 0; i < br.cols.size(); ++i) {
+    RCol &r = sh.roles[i];
+    if (tl[i]) {
+      r.role = 2;
+      r.lit = *tl[i];
+    } else if (tr[i].leaf == la) {
+      r.role = 0;
+      r.col = tr[i].col;
+    } else if (tr[i].leaf == lb) {
+      r.role = 1;
+      r.col = tr[i].col;
+    } else {
+      return reach_reject("branch check 21");
+    }
+  }
+  return true;
+}
+
+bool try_fused_reach(const NodePtr &grp, DataPtr &result) {
+  const char *fe = getenv("CAPF_FUSED_REACH");  // 0: always the relational plan
+  if (fe && atoi(fe) == 0) return false;
+  if (grp->kind != Kind::Group || grp->key_index.empty() || grp->aggs.empty()) return false;
+  for (auto &a : grp->aggs)
+    if (a.kind != CAPF_AGG_COUNT_STAR) return false;
+  Session *s = grp->s;
+  // group keys → columns of the Distinct
+  std::vector<TCol> gk;
+  for (int k : grp->key_index) gk.push_back(TCol{k, nullptr});
+  NodePtr d = through_mappings(grp->kids[0], gk);
+  if (d->kind != Kind::Distinct || d->key_index.empty()) return reach_reject("group input is not a DISTINCT");
+  {
+    std::lock_guard<std::mutex> lk(d->mu);
+    if (d->result) return false;  // already materialised: the plain group is cheap
+  }
+  // tracked columns below the Distinct: its keys, then the group keys
+  std::vector<TCol> tracked;
+  for (int k : d->key_index) tracked.push_back(TCol{k, nullptr});
+  const size_t nd = tracked.size();
+  std::vector<int> gk_at(gk.size(), -1);  // group key → tracked index (−1: literal)
+  for (size_t i = 0; i < gk.size(); ++i) {
+    if (gk[i].lit) continue;
+    gk_at[i] = (int)tracked.size();
+    tracked.push_back(TCol{gk[i].col, nullptr});
+  }
+  std::vector<int> a_cols;
+  for (int t : gk_at)
+    if (t >= 0) a_cols.push_back(t);
+  if (a_cols.empty()) return reach_reject("no group key column");
+  std::vector<ReachBranch> brs;
+  if (!union_branches(d->kids[0], tracked, brs)) return reach_reject("union branches");
+  std::vector<ReachShape> shapes(brs.size());
+  uint64_t lengths = 0;
+  for (size_t b = 0; b < brs.size(); ++b) {
+    if (!reach_branch(brs[b], a_cols, shapes[b])) return reach_reject("a branch is not a var-length chain");
+    const ReachShape &sh = shapes[b], &s0 = shapes[0];
+    if (sh.k > 64 || (lengths >> (sh.k - 1) & 1)) return reach_reject("branch lengths");
+    lengths |= uint64_t(1) << (sh.k - 1);
+    if (!leaf_eq(sh.sa, s0.sa) || !leaf_eq(sh.sb, s0.sb) || !leaf_eq(sh.rel, s0.rel))
+      return reach_reject("branches scan different tables");
+    if (sh.x != s0.x || sh.y != s0.y || sh.cs != s0.cs || sh.cd != s0.cd)
+      return reach_reject("branches join different columns");
+    for (size_t i = 0; i < tracked.size(); ++i) {
+      const RCol &r = sh.roles[i], &r0 = s0.roles[i];
+      if (r.role != r0.role || r.col != r0.col) return reach_reject("column roles differ across branches");
+      if (r.role == 2 && !prog_eq(r.lit, r0.lit)) return reach_reject("literals differ across branches");
+    }
+  }
+  const int upper = 64 - __builtin_clzll(lengths);
+  if (lengths != (upper == 64 ? ~uint64_t(0) : (uint64_t(1) << upper) - 1))
+    return reach_reject("lengths are not 1..u");
+  const ReachShape &sh = shapes[0];
+  // DISTINCT over (a, b): both ids among its keys, every key a column of S_a /
+  // S_b or a literal; group keys: S_a columns (with the id) or literals
+  bool has_x = false, has_y = false;
+  for (size_t i = 0; i < nd; ++i) {
+    const RCol &r = sh.roles[i];
+    has_x |= r.role == 0 && r.col == sh.x;
+    has_y |= r.role == 1 && r.col == sh.y;
+  }
+  bool gx = false;
+  for (int t : a_cols) {
+    if (sh.roles[t].role == 1) return reach_reject("a group key is a target column");
+    gx |= sh.roles[t].role == 0 && sh.roles[t].col == sh.x;
+  }
+  if (!has_x || !has_y || !gx) return reach_reject("DISTINCT / group keys lack the endpoint ids");
+  if (!column_unique(sh.sa.node, sh.x) || !column_unique(sh.sb.node, sh.y))
+    return reach_reject("endpoint ids not unique");
+  // rel endpoint columns: non-null INTEGER
+  LeafData lr = leaf_data(sh.rel), la = leaf_data(sh.sa), lb = leaf_data(sh.sb);
+  const ColPtr &rs = lr.data->cols[sh.cs], &rd = lr.data->cols[sh.cd];
+  const ColPtr &xa = la.data->cols[sh.x], &yb = lb.data->cols[sh.y];
+  for (const ColPtr *c : {&rs, &rd, &xa, &yb}) {
+    force(*c);
+    if ((*c)->type != Type::Int64 || (*c)->valid) return reach_reject("nullable or non-INTEGER ids");
+  }
+  if (lr.data->nrows >= (int64_t(1) << 32)) return reach_reject("more than 2^32 rels");
+  DataPtr res = var_length_reach_rows(s, rs, rd, lr.data->nrows, xa, la.data->nrows, yb,
+                                      lb.data->nrows, upper);
+  s->last_plan = "fused_var_length_reach";
+  // output: group keys (a's id, other S_a columns gathered by a's row, literals)
+  // then one reach column per count(*)
+  const int64_t nr = res->nrows;
+  auto out = std::make_shared<Data>();
+  out->nrows = nr;
+  bool need_rows = false;
+  for (int t : a_cols) need_rows |= sh.roles[t].role == 0 && sh.roles[t].col != sh.x;
+  DataPtr a_rows;  // S_a's columns at each result row
+  std::vector<ColPtr> rcols = res->cols;
+  if (need_rows && nr > 0) {
+    Data l;
+    l.nrows = nr;
+    l.cols = {res->cols[0]};
+    JoinPairs jp;
+    const std::vector<std::pair<int, int>> keys = {{0, sh.x}};
+    if (!dense_join(s, l, *la.data, keys, CAPF_JOIN_INNER, jp))
+      jp = hash_join(s, l, *la.data, keys, CAPF_JOIN_INNER);
+    if (jp.n != nr) fail(CAPF_ERR_INTERNAL, "fused reach: source rows lost");
+    IdxCache cache;
+    if (jp.left)
+      for (auto &c : rcols) c = gather_lazy(s, c, jp.left, nr, false, &cache);
+    a_rows = std::make_shared<Data>();
+    a_rows->nrows = nr;
+    for (auto &c : la.data->cols)
+      a_rows->cols.push_back(jp.right ? gather_lazy(s, c, jp.right, nr, false, &cache) : c);
+  }
+  for (size_t i = 0; i < gk.size(); ++i) {
+    const Type t = grp->types[i];
+    if (gk_at[i] < 0) {
+      Data e;
+      e.nrows = nr;
+      out->cols.push_back(eval_program(s, *gk[i].lit, {}, e, t));
+      continue;
+    }
+    const RCol &r = sh.roles[gk_at[i]];
+    if (r.role == 2) {  // a literal in every branch (a constant label column)
+      Data e;
+      e.nrows = nr;
+      out->cols.push_back(eval_program(s, r.lit, {}, e, t));
+      continue;
+    }
+    out->cols.push_back(r.col == sh.x ? rcols[0] : a_rows->cols[r.col]);
+  }
+  for (size_t k = 0; k < grp->aggs.size(); ++k) out->cols.push_back(rcols[1]);
+  result = out;
+  return true;
+}
 }  // namespace capf
 
 // ===================================================================== C-ABI

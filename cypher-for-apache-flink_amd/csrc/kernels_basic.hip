@@ -1244,7 +1244,9 @@ DataPtr filter_select(Session *s, const Program &p, const std::vector<std::strin
       std::lock_guard<std::mutex> g(c->mu);
       lz = c->lazy;
     }
-    if (lz && !lz->src->is_const) {
+    // a lazy column over a constant is a fill in gather_lazy only when no row can
+    // be NULL; a nullable one (an outer join's constant side) composes its index
+    if (lz && !(lz->src->is_const && !lz->nullable)) {
       bool seen = false;
       for (auto &b : lazy_idx) seen |= b.get() == lz->idx.get();
       if (!seen) lazy_idx.push_back(lz->idx);

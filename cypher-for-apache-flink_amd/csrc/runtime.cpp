@@ -439,6 +439,11 @@ static DataPtr materialize_impl(const NodePtr &n) {
       return gather_all(s, *c, g.rep_row, g.ngroups);
     }
     case Kind::Group: {
+      // config 5: group(a; count(*)) over DISTINCT (a, b) of var-length paths
+      if (!n->key_index.empty()) {
+        DataPtr fused;
+        if (try_fused_reach(n, fused)) return fused;
+      }
       // fused factorised count: group(∅, count(*)) over an inner-join tree
       bool all_count_star = n->key_index.empty() && !n->aggs.empty();
       for (auto &a : n->aggs) all_count_star &= a.kind == CAPF_AGG_COUNT_STAR;
@@ -662,6 +667,7 @@ capf_status capf_session_reset_profile(capf_session *cs) {
   need(cs, "session");
   cs->impl.resolve_profile();
   cs->impl.profile.clear();
+  cs->impl.last_plan = "none";
   CAPF_API_END
 }
 

@@ -383,7 +383,7 @@ struct VrCache {
   std::shared_ptr<VrIndex> ix;
 };
 
-static DataPtr var_length_reach(Session *s, const ColPtr &rsrc, const ColPtr &rdst, int64_t m,
+DataPtr var_length_reach_rows(Session *s, const ColPtr &rsrc, const ColPtr &rdst, int64_t m,
                                 const ColPtr &sid, int64_t ns_in, const ColPtr &tid, int64_t nt,
                                 int upper) {
   auto out = std::make_shared<Data>();
@@ -523,7 +523,7 @@ extern "C" capf_status capf_var_length_reach(capf_session *cs, capf_table *rels,
     ColPtr rs = int_column_of(rels->node, dr, src_col), rd = int_column_of(rels->node, dr, dst_col);
     ColPtr si = int_column_of(sources->node, ds, source_id_col);
     ColPtr ti = int_column_of(targets->node, dt, target_id_col);
-    DataPtr d = var_length_reach(s, rs, rd, dr->nrows, si, ds->nrows, ti, dt->nrows, upper);
+    DataPtr d = var_length_reach_rows(s, rs, rd, dr->nrows, si, ds->nrows, ti, dt->nrows, upper);
     auto n = std::make_shared<Node>();
     n->s = s;
     n->kind = Kind::Source;

@@ -22,7 +22,7 @@ from dataclasses import dataclass, field
 from itertools import combinations
 from typing import List, Optional, Sequence, Tuple
 
-from .expr import (Aggregator, Ands, BoolLit, CountStar, ElementProperty, EndNode, Equals, ExistsPattern, Expr,
+from .expr import (Aggregator, Ands, BoolLit, ElementProperty, EndNode, Equals, ExistsPattern, Expr,
                    HasLabel, HasType, IntegerLit, IsNotNull, Not, NullLit, StartNode, TrueLit, Var)
 from .header import RecordHeader, owner_of
 
@@ -609,68 +609,10 @@ def _row_count(e, params, what):
     raise IllegalArgumentException(f"{what}: an integer literal or parameter, got {e}")
 
 
-def _fused_reach(graph, q: Query):
-    """Physical rewrite of
-         MATCH (a:L1)-[r:T*1..u]->(b:L2) WITH DISTINCT a, b WITH a, count(*) AS c ...
-    (VarLengthExpand → Distinct → Aggregate, the config-5 shape) into ONE
-    backend call, capf_var_length_reach (csrc/var_length_reach.hip), instead
-    of the join chain + UNION ALL + DISTINCT + GROUP BY that would materialise
-    every path.  The same role as CAPF's replaced Calcite rule set
-    (flink-cypher/.../api/CAPFSession.scala:83-91): the okapi plan is
-    unchanged, the backend picks the physical form.  Returns (Planned, the
-    remaining stages) or None when the shape does not match (then the
-    relational lowering above runs as usual).  CAPF_FUSED_REACH=0 disables it."""
-    import os
-    if os.environ.get("CAPF_FUSED_REACH", "1") == "0" or not hasattr(graph.session, "var_length_reach"):
-        return None
-    if len(q.matches) != 1 or len(q.stages) < 2:
-        return None
-    m = q.matches[0]
-    if len(m.rels) != 1 or m.where or m.optional:
-        # OPTIONAL MATCH keeps a (NULL, …) row for an empty pattern: only the
-        # relational lowering (left outer join) has that semantics
-        return None
-    r = m.rels[0]
-    if r.length is None or r.length[0] != 1 or r.direction not in ("out", "in") or r.src == r.dst:
-        return None
-    if r.direction == "in":
-        r = RelP(r.name, r.dst, r.src, r.types, "out", r.length)
-    if {n.name for n in m.nodes} - {r.src, r.dst}:
-        return None
-    st1, st2 = q.stages[0], q.stages[1]
-    plain = lambda st: not (st.where or st.order_by or st.skip is not None or st.limit is not None)  # noqa: E731
-    if not (st1.distinct and plain(st1) and len(st1.items) == 2 and not st2.distinct and plain(st2)):
-        return None
-    proj = {e.vname: a for a, e in st1.items if isinstance(e, Var)}
-    if set(proj) != {r.src, r.dst} or len(st2.items) != 2:
-        return None
-    keys = [(a, e) for a, e in st2.items if isinstance(e, Var)]
-    cnts = [a for a, e in st2.items if isinstance(e, CountStar)]
-    if len(keys) != 1 or len(cnts) != 1 or keys[0][1].vname != proj[r.src] or keys[0][0] == cnts[0]:
-        return None
-    labels = {}
-    for n in m.nodes:
-        labels.setdefault(n.name, set()).update(n.labels)
-    src_scan = graph.node_scan(r.src, sorted(labels.get(r.src, ())))
-    dst_scan = graph.node_scan(r.dst, sorted(labels.get(r.dst, ())))
-    rel_scan = graph.rel_scan(r.name, r.types)
-    e = Var(r.name, "RELATIONSHIP")
-    a_col, c_col = "__" + keys[0][0], "__" + cnts[0]
-    tab = graph.session.var_length_reach(
-        rel_scan.table, rel_scan.header.column(StartNode(e)), rel_scan.header.column(EndNode(e)),
-        src_scan.table, src_scan.header.column(Var(r.src, "NODE")),
-        dst_scan.table, dst_scan.header.column(Var(r.dst, "NODE")),
-        r.length[0], r.length[1], a_col, c_col)
-    return Planned(tab, RecordHeader({Var(keys[0][0]): a_col, Var(cnts[0]): c_col})), q.stages[2:]
-
-
 def plan_query(graph, q: Query, params=None) -> Planned:
-    fused = _fused_reach(graph, q)
-    if fused is not None:
-        op, rest = fused
-        for st in rest:
-            op = plan_stage(op, st, params, graph)
-        return op
+    """The okapi relational plan of `q`, operator for operator.  Physical
+    choices (fused counts, the fused var-length reach of config 5) are made by
+    the backend below the Table SPI from the plan DAG these calls build."""
     op = None
     for m in q.matches:
         op = plan_optional(graph, m, op, params) if m.optional else plan_match(graph, m, op, params)

@@ -159,13 +159,15 @@ int32_t capf_abi_version(void);
 capf_status capf_session_create(int32_t device, void *hip_stream, capf_session **out);
 capf_status capf_session_destroy(capf_session *s);
 capf_status capf_session_sync(capf_session *s);
-/* Per-kernel HIP-event timing of the hot kernels (off by default). */
+/* Per-kernel HIP-event timing of the hot kernels (off by default).  reset also
+ * sets the last plan back to "none". */
 capf_status capf_session_set_profiling(capf_session *s, int32_t enabled);
 capf_status capf_session_reset_profile(capf_session *s);
 capf_status capf_session_profile_count(capf_session *s, int32_t *n);
 capf_status capf_session_profile_entry(capf_session *s, int32_t i, const char **kernel,
                                        int64_t *launches, double *total_ms, double *bytes);
-/* last fused-count execution path taken ("fused_chain2", "message_passing", "materialize") */
+/* last fused execution path taken ("fused_chain2", "fused_triangle", "message_passing",
+ * "fused_var_length_reach"; "none" until one runs) */
 const char *capf_session_last_plan(capf_session *s);
 
 /* String dictionary for CAPF_TYPE_STRING columns. */

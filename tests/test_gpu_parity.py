@@ -314,6 +314,33 @@ def test_filter_over_join_parity(pred, paths, monkeypatch):
     assert bag(got) == bag(want)
 
 
+@pytest.mark.parametrize("jt", ["left_outer", "right_outer", "full_outer"])
+@pytest.mark.parametrize("pred", [Not(Equals(Var("x"), Var("y"))), IsNull(Var("c")), IsNotNull(Var("c")),
+                                  Ands(Not(Equals(Var("x"), Var("y"))), Equals(Var("c"), IntegerLit(7)))],
+                         ids=["neq", "c_null", "c_not_null", "neq_and_c"])
+def test_filter_over_outer_join_constant_column(jt, pred):
+    """An outer join turns a projected literal of the null-extended side into a
+    nullable lazy column over a constant; a WHERE over that join's output must
+    compose its index (kernels_basic.hip filter_select), not treat it as a fill
+    (the 8-B placeholder selection index was read m times)."""
+    rng = np.random.default_rng(12)
+    n = 900
+    left = [("x", T_INT, [int(v) for v in rng.integers(0, 40, n)], None),
+            ("ka", T_INT, [int(v) for v in rng.integers(0, 1500, n)], None)]  # sparse keys: unmatched rows
+    right = [("y", T_INT, [int(v) for v in rng.integers(0, 40, n)], None),
+             ("kb", T_INT, [int(v) for v in rng.integers(0, 1500, n)], None)]
+    hdr = RecordHeader({Var("x"): "x", Var("ka"): "ka", Var("y"): "y", Var("kb"): "kb", Var("c"): "c"})
+    gl, ol = _both(left)
+    gr, orr = _both(right)
+    rh = RecordHeader({Var("y"): "y", Var("kb"): "kb"})
+    gr = gr.withColumns((IntegerLit(7), "c"), header=rh, params={})
+    orr = orr.withColumns((IntegerLit(7), "c"), header=rh, params={})
+    got = gl.join(gr, jt, ("ka", "kb")).filter(pred, hdr, {}).rows
+    want = ol.join(orr, jt, ("ka", "kb")).filter(pred, hdr, {}).rows
+    assert len(want) > 0 or (jt == "right_outer" and isinstance(pred, IsNull))  # c is never NULL there
+    assert bag(got) == bag(want)
+
+
 EXPRS = [Add(Var("k"), IntegerLit(3)), Multiply(Var("f"), FloatLit(2.5)), Divide(Var("k"), IntegerLit(3)),
          Subtract(Var("i"), Var("k")), ToFloat(Var("k")), ToInteger(Multiply(Var("f"), FloatLit(1e3))),
          Coalesce(Var("k"), IntegerLit(-1)), Divide(Var("i"), Var("k"))]

@@ -1,9 +1,12 @@
-"""Fused config-5 path (csrc/var_length_reach.hip via planner._fused_reach):
-VarLengthExpand *1..u → DISTINCT (a, b) → GROUP BY a count(*) on the GPU,
-against (1) the scipy matrix-power restatement (oracle/reach.py), (2) the
-unfused relational plan on the GPU (CAPF_FUSED_REACH=0: join chain +
-isomorphism filters + UNION ALL + DISTINCT + GROUP BY) and (3) the
-isomorphic-path brute force on the reference's LDBC sample."""
+"""Fused config-5 path: the planner sends the unchanged okapi relational plan
+(VarLengthExpand join chain + isomorphism filters + UNION ALL, DISTINCT,
+GROUP BY — VarLengthExpandPlanner.scala:82-259) through the Table SPI; the
+runtime recognises Group(a; count(*)) ∘ Distinct(a, b) ∘ UNION ALL of the
+chains in its plan DAG (fused_count.hip::try_fused_reach) and runs the BFS of
+csrc/var_length_reach.hip.  Checked against (1) the scipy matrix-power
+restatement (oracle/reach.py), (2) the unfused relational plan on the GPU
+(CAPF_FUSED_REACH=0) and (3) the isomorphic-path brute force on the
+reference's LDBC sample."""
 import numpy as np
 import pytest
 
@@ -52,7 +55,9 @@ def test_oracle_on_ldbc_sample():
 def test_config5_fused_on_ldbc_sample(gpu_session):
     from test_ldbc_config5 import brute_force
     g = ScanGraph.from_data(gpu_session, ldbc_graph_data())
+    gpu_session.reset_profile()
     got = run(g, config5_query())
+    assert gpu_session.last_plan() == "fused_var_length_reach"
     assert sorted([r["reach"], r["n"]] for r in got) == brute_force()
 
 
@@ -62,7 +67,9 @@ def test_config5_fused_on_ldbc_sample(gpu_session):
 def test_reach_vs_matrix_powers(gpu_session, upper, compact):
     data, ks, kd, persons = synthetic(10)
     g = ScanGraph.from_data(gpu_session, data, compact=compact)
+    gpu_session.reset_profile()
     got = {r["a"]: r["reach"] for r in run(g, reach_query(upper))}
+    assert gpu_session.last_plan() == "fused_var_length_reach"
     assert got == oreach.reach_counts(ks, kd, persons, persons, upper)
 
 
@@ -89,9 +96,13 @@ def test_fused_equals_relational_plan(gpu_session, monkeypatch, upper):
     g = ScanGraph.from_data(gpu_session, data)
     q = reach_query(upper)
     q.stages.append(Stage([("reach", Var("reach")), ("n", CountStar())]))
+    gpu_session.reset_profile()
     fused = sorted([r["reach"], r["n"]] for r in run(g, q))
+    assert gpu_session.last_plan() == "fused_var_length_reach"
     monkeypatch.setenv("CAPF_FUSED_REACH", "0")
+    gpu_session.reset_profile()
     plain = sorted([r["reach"], r["n"]] for r in run(g, q))
+    assert gpu_session.last_plan() == "none"
     assert fused == plain
 
 
@@ -149,7 +160,9 @@ def test_config5_sf10_histogram(gpu_session):
     (C bitset BFS, tests/golden/config5_sf10.json)."""
     summary, hist = _fixture5()
     g, _ = _sf10_graph(gpu_session)
+    gpu_session.reset_profile()
     got = sorted([r["reach"], r["n"]] for r in run(g, config5_query()))
+    assert gpu_session.last_plan() == "fused_var_length_reach"
     assert got == hist
     assert sum(r * n for r, n in got) == summary["pairs"] == 1819538648
 

@@ -40,6 +40,12 @@ for k in sorted(set(fetch) | set(write)):
                          "fetch_size_raw_bytes": sum(f) / len(f)}
     tot += fb + wb
 res["hbm_bytes_per_query"] = tot
+lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "cypher-for-apache-flink_amd",
+                   "libcapf_gpu.so")
+if os.path.exists(lib):  # provenance: the build whose kernels were counted
+    import hashlib
+    with open(lib, "rb") as fh:
+        res["lib"] = "libcapf_gpu.so sha256:" + hashlib.sha256(fh.read()).hexdigest()[:16]
 res["note"] = ("read_bytes = 2 x FETCH_SIZE (gfx950 streaming-read correction); P3's scattered "
                "16-B segment reads are outside the calibrated pattern; Infinity-Cache hits are "
                "counted by the memory-side counters")

@@ -633,8 +633,7 @@ def run_distributed(args):
     per-node histograms reduce-scattered."""
     import torch
     import torch.distributed as dist
-    from capf_amd.dist import (edge_range, gpu_two_hop_count, gpu_two_hop_count_sharded,
-                               gpu_two_hop_count_sharded_async, node_partitioned_copies, padded_nodes)
+    from capf_amd.dist import edge_range, gpu_two_hop_count, gpu_two_hop_count_sharded_async, padded_nodes
     from capf_amd.synthetic import rmat_seed, thresholds
     from capf_amd.table import GpuSession
 
@@ -676,19 +675,31 @@ def run_distributed(args):
         layout = "replicated rels, oriented-CSR rows dealt round-robin over ranks; one int64 all-reduce"
         compulsory = (16.0 * m + 8.0 * n_nodes) / world
     elif args.layout == "node":
-        # ingest (untimed): every rank generates the edge stream and keeps its two copies
+        # ingest (untimed): every rank generates the edge stream and the node range,
+        # keeps its relational shards and its two count copies (dist_node_partitioned_graph)
+        from capf_amd.dist_table import DistSession, GpuExchange, dist_node_partitioned_graph
+        from capf_amd.graph import ElementTable, ScanGraph
+        from capf_amd.planner import run
         full = s.rmat_rels(args.scale, rmat_seed(args.scale), thresholds(), 0, m)
-        in_copy, out_copy = node_partitioned_copies(full, n_nodes, world, rank, compact=id_width(args))
-        del full
+        nodes = s.range_nodes(0, n_nodes, id_col="id")
+        ds = DistSession(s, GpuExchange(s))
+        g = dist_node_partitioned_graph(
+            ds, ScanGraph(s, [ElementTable("node", frozenset(), nodes, {})],
+                          [ElementTable("rel", frozenset(["E"]), full, {})]), compact=id_width(args))
+        in_copy, out_copy = g.rel_tables[0].table.prov.info["count"].copies
+        del full, nodes
         s.sync()
-        partial = torch.zeros(1, dtype=torch.int64, device="cuda")
-        step = lambda: gpu_two_hop_count_sharded(s, in_copy, out_copy, n_nodes, partial)  # noqa: E731
-        # the all-reduce of query i overlaps the kernels of query i+1 (RCCL stream)
+        q = two_hop_query()
+        # the timed step: plan call → scalar through the Table SPI (planner.run on
+        # DistTables; DistTable.group(∅, count(*)) dispatches the sharded count)
+        step = lambda: run(g, q)[0]["count"]  # noqa: E731
+        # side figure: the all-reduce of query i overlaps the kernels of query i+1
+        # (RCCL stream), the copies driven directly
         pipe = lambda slot: gpu_two_hop_count_sharded_async(s, in_copy, out_copy, n_nodes, slot,  # noqa: E731
                                                             async_op=True)
         local_rels = in_copy.size + out_copy.size
         layout = (f"node-partitioned: rank holds the rels whose target (in-copy) / source (out-copy) it "
-                  f"owns; one int64 all-reduce per query")
+                  f"owns; the planner's 2-hop plan through DistTable; one int64 all-reduce per query")
         # rank's share of the job's compulsory bytes (src+dst int64 per rel, node ids)
         compulsory = (16.0 * m + 8.0 * n_nodes) / world
     else:

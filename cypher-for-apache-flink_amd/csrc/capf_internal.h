@@ -163,7 +163,8 @@ enum Op : int32_t {
   OP_IS_NOT_NULL = CAPF_OP_IS_NOT_NULL, OP_ADD = CAPF_OP_ADD, OP_SUB = CAPF_OP_SUB,
   OP_MUL = CAPF_OP_MUL, OP_DIV = CAPF_OP_DIV, OP_MOD = CAPF_OP_MOD, OP_NEG = CAPF_OP_NEG,
   OP_TO_FLOAT = CAPF_OP_TO_FLOAT, OP_TO_INTEGER = CAPF_OP_TO_INTEGER,
-  OP_COALESCE = CAPF_OP_COALESCE
+  OP_COALESCE = CAPF_OP_COALESCE, OP_STR_LEN = CAPF_OP_STR_LEN, OP_LIST_SIZE = CAPF_OP_LIST_SIZE,
+  OP_IF = CAPF_OP_IF
 };
 
 struct Instr {
@@ -295,6 +296,9 @@ struct Session {
   std::mutex str_mu;
   std::vector<std::string> strings;
   std::unordered_map<std::string, int64_t> string_codes;
+  // device table of the strings' lengths (CAPF_OP_STR_LEN), grown on demand
+  BufPtr d_str_len;
+  size_t d_str_len_n = 0;
   // small device scratch for scalar results
   int64_t *d_scalars = nullptr;  // 64 slots
   int64_t *h_scalars = nullptr;  // pinned mirror
@@ -415,6 +419,9 @@ ColStats compute_stats(Session *s, const Column &c);
 ColPtr encode_column(Session *s, const ColPtr &c, int width = 4);
 ColPtr decode_column(Session *s, const ColPtr &c);
 
+// Device table of the session's string lengths by code (UTF-16 units), for
+// CAPF_OP_STR_LEN; *n = strings covered.
+const int64_t *string_length_table(Session *s, size_t *n);
 // Record an error for capf_last_error() (used by entry points outside runtime.cpp).
 int32_t record_error(int32_t code, const char *msg);
 

@@ -873,6 +873,25 @@ __device__ Val run_program(const Instr *code, int ncode, const ColView *cols, in
         st[sp++] = res;
         break;
       }
+      case OP_STR_LEN: {  // cols[in.i] = the session's string lengths by code
+        Val a = st[--sp];
+        st[sp++] = a.nul ? mknull(CAPF_TYPE_INT64)
+                         : mk(((const int64_t *)cols[in.i].data)[a.b], CAPF_TYPE_INT64, 0);
+        break;
+      }
+      case OP_LIST_SIZE: {  // cols[in.i]: LIST offsets [n + 1]
+        const ColView &c = cols[in.i];
+        if (!c.data || (c.valid && !c.valid[r]))
+          st[sp++] = mknull(CAPF_TYPE_INT64);
+        else
+          st[sp++] = mk(((const int64_t *)c.data)[r + 1] - ((const int64_t *)c.data)[r], CAPF_TYPE_INT64, 0);
+        break;
+      }
+      case OP_IF: {
+        Val v = st[--sp], c = st[--sp], e = st[--sp];
+        st[sp++] = (!c.nul && c.b != 0) ? v : e;
+        break;
+      }
       default: st[sp++] = mknull(CAPF_TYPE_NULL); break;
     }
   }
@@ -920,31 +939,54 @@ static DeviceProgram upload_program(Session *s, const Program &p,
                                     const std::vector<std::string> &names, const Data &d) {
   DeviceProgram dp;
   std::vector<ColView> views;
-  for (auto &nm : p.names) {
+  std::vector<char> scalar_use(p.names.size(), 0);  // read by OP_COL (not only by OP_LIST_SIZE)
+  for (auto &in : p.code)
+    if (in.op == OP_COL && in.i >= 0 && (size_t)in.i < p.names.size()) scalar_use[(size_t)in.i] = 1;
+  for (size_t j = 0; j < p.names.size(); ++j) {
+    const std::string &nm = p.names[j];
     int idx = -1;
     for (size_t k = 0; k < names.size(); ++k)
       if (names[k] == nm) idx = (int)k;
     if (idx < 0) illegal("expression references unknown column '" + nm + "'");
-    views.push_back(view_of(d.cols[idx]));
+    const ColPtr &c = d.cols[idx];
+    if (c->type == Type::List && !scalar_use[j]) {  // size(list): the offsets [n + 1]
+      ColView v{c->data ? c->data->p : nullptr, c->valid ? (const uint8_t *)c->valid->p : nullptr,
+                (int32_t)Type::List, ENC_PLAIN, 0};
+      views.push_back(v);
+    } else {
+      views.push_back(view_of(c));
+    }
   }
-  dp.ncode = (int)p.code.size();
+  std::vector<Instr> code = p.code;
+  for (auto &in : code)
+    if (in.op == OP_STR_LEN) {  // the session's string lengths as one more column view
+      size_t nstr = 0;
+      const int64_t *len = string_length_table(s, &nstr);
+      in.i = (int64_t)views.size();
+      views.push_back(ColView{len, nullptr, (int32_t)Type::Int64, ENC_PLAIN, 0});
+      for (auto &x : code)
+        if (x.op == OP_STR_LEN) x.i = in.i;
+      break;
+    }
+  dp.ncode = (int)code.size();
   dp.ncols = (int)views.size();
   // stack depth check (host) — the device stack is fixed size
   int depth = 0, maxd = 0;
-  for (auto &in : p.code) {
+  for (auto &in : code) {
     switch (in.op) {
       case OP_COL: case OP_LIT_INT: case OP_LIT_FLOAT: case OP_LIT_BOOL: case OP_LIT_STRING:
-      case OP_LIT_NULL: depth++; break;
+      case OP_LIT_NULL: case OP_LIST_SIZE: depth++; break;
       case OP_AND: case OP_OR: case OP_COALESCE: depth -= (int)in.i - 1; break;
       case OP_NOT: case OP_IS_NULL: case OP_IS_NOT_NULL: case OP_NEG: case OP_TO_FLOAT:
-      case OP_TO_INTEGER: break;
+      case OP_TO_INTEGER: case OP_STR_LEN: break;
+      case OP_IF: depth -= 2; break;
       default: depth -= 1; break;
     }
     maxd = std::max(maxd, depth);
   }
   if (maxd > MAX_STACK) not_impl("expression too deep for the GPU interpreter");
-  dp.code = s->alloc(sizeof(Instr) * p.code.size());
-  HIP_CHECK(hipMemcpyAsync(dp.code->p, p.code.data(), sizeof(Instr) * p.code.size(),
+  dp.code = s->alloc(sizeof(Instr) * code.size());
+  HIP_CHECK(hipMemcpyAsync(dp.code->p, code.data(), sizeof(Instr) * code.size(),
                            hipMemcpyHostToDevice, s->stream));
   dp.cols = s->alloc(sizeof(ColView) * std::max<size_t>(views.size(), 1));
   if (!views.empty())

@@ -488,14 +488,168 @@ __global__ void k_agg_final(int64_t ng, int kind, int fl, int out_type, const vo
         ((int64_t *)out)[g] = c > 0 ? (int64_t)a : 0;
     } else {
       int64_t a = ((const int64_t *)acc)[g];
-      // Flink AVG on a LONG column is a LONG (Java long division)
-      if (kind == CAPF_AGG_AVG && c > 0) a = a / (int64_t)c;
+      if (kind == CAPF_AGG_AVG) {  // avg over INTEGER values: the exact int64 sum / count as a FLOAT
+        ((double *)out)[g] = c > 0 ? (double)a / (double)c : 0.0;
+        continue;
+      }
       if (out_type == CAPF_TYPE_BOOL)
         ((uint8_t *)out)[g] = c > 0 ? (a != 0) : 0;
       else
         ((int64_t *)out)[g] = c > 0 ? a : 0;
     }
   }
+}
+
+// ---------------------------------------------------------- fp64 sum / avg
+// sum and avg over FLOAT (FlinkSQLExprMapper.scala:281-287) must agree with the
+// reference within 1e-12 relative error (north star) whatever the row order.
+// An fp64 atomicAdd per row is order-dependent and uncompensated, so the rows
+// are instead put in a fixed order — stable radix sort by group id, rows
+// ascending within a group — and summed in double-double (TwoSum-compensated,
+// Neumaier): per chunk of FS_CHUNK rows one wave, lane l taking rows l, l+64, …,
+// then a fixed butterfly; per group one wave over its chunk partials.  The
+// result is bit-identical from run to run and within ~2 ulp of the exact sum
+// for any input whose exact sum is not the victim of catastrophic cancellation
+// beyond the double-double's 106 bits.
+constexpr int FS_CHUNK = 2048;
+
+struct DD {
+  double hi, lo;
+};
+__device__ inline DD dd_add_d(DD x, double v) {
+  const double s = x.hi + v, bb = s - x.hi;
+  return DD{s, x.lo + ((x.hi - (s - bb)) + (v - bb))};
+}
+__device__ inline DD dd_add(DD x, DD y) {
+  const double s = x.hi + y.hi, bb = s - x.hi;
+  return DD{s, x.lo + y.lo + ((x.hi - (s - bb)) + (y.hi - bb))};
+}
+// a fixed butterfly over the 64 lanes: every lane ends with the same sum
+__device__ inline DD dd_wave_sum(DD x) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    DD y{__shfl_xor(x.hi, o, 64), __shfl_xor(x.lo, o, 64)};
+    // combine in lane order (lower lane first) so both partners compute the same value
+    x = (threadIdx.x & o) ? dd_add(y, x) : dd_add(x, y);
+  }
+  return x;
+}
+__device__ inline double dd_value(DD x) { return isfinite(x.hi) ? x.hi + x.lo : x.hi; }
+
+// sort key per row: its group, or ng (sorted last) when the argument is NULL
+__global__ void k_fs_keys(const int64_t *gid, ColView arg, int64_t n, int64_t ng, uint64_t *key, uint32_t *row,
+                          unsigned long long *cnt) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    int64_t g = gid ? gid[r] : 0;
+    if (g < 0 || (arg.valid && !arg.valid[r])) g = ng;
+    else atomicAdd(&cnt[g], 1ull);
+    key[r] = (uint64_t)g;
+    row[r] = (uint32_t)r;
+  }
+}
+
+// chunks per group → exclusive scan gives each group's first chunk
+__global__ void k_fs_nchunks(const unsigned long long *cnt, int64_t ng, uint32_t *nch) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= ng; g += (int64_t)gridDim.x * blockDim.x)
+    nch[g] = g < ng ? (uint32_t)((cnt[g] + FS_CHUNK - 1) / FS_CHUNK) : 0u;
+}
+
+// one wave per chunk: (group, chunk within group) found by a binary search over
+// the groups' first chunks; rows [off[g] + c·FS_CHUNK, …) of the sorted order
+__global__ __launch_bounds__(256) void k_fs_chunks(const uint32_t *rows, ColView arg, const int64_t *off,
+                                                   const uint32_t *chunk0, int64_t ng, uint32_t nchunks,
+                                                   double2 *part) {
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / 64, lane = threadIdx.x & 63;
+  const uint32_t nw = gridDim.x * blockDim.x / 64;
+  for (uint32_t c = wave; c < nchunks; c += nw) {
+    int64_t lo = 0, hi = ng - 1;  // last g with chunk0[g] <= c
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (chunk0[mid] <= c) lo = mid;
+      else hi = mid - 1;
+    }
+    const int64_t g = lo;
+    const int64_t b = off[g] + (int64_t)(c - chunk0[g]) * FS_CHUNK;
+    const int64_t e = min(off[g + 1], b + FS_CHUNK);
+    DD acc{0.0, 0.0};
+    for (int64_t i = b + lane; i < e; i += 64) acc = dd_add_d(acc, ((const double *)arg.data)[rows[i]]);
+    acc = dd_wave_sum(acc);
+    if (lane == 0) part[c] = make_double2(acc.hi, acc.lo);
+  }
+}
+
+// one wave per group over its chunk partials, then the final value
+__global__ __launch_bounds__(256) void k_fs_groups(const double2 *part, const uint32_t *chunk0,
+                                                   const unsigned long long *cnt, int64_t ng, int avg,
+                                                   double *out, uint8_t *valid) {
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64;
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * blockDim.x / 64;
+  for (int64_t g = wave; g < ng; g += nw) {
+    DD acc{0.0, 0.0};
+    for (uint32_t c = chunk0[g] + lane; c < chunk0[g + 1]; c += 64) {
+      const double2 p = part[c];
+      acc = dd_add(acc, DD{p.x, p.y});
+    }
+    acc = dd_wave_sum(acc);
+    if (lane == 0) {
+      const unsigned long long n = cnt[g];
+      const double v = dd_value(acc);
+      out[g] = n > 0 ? (avg ? v / (double)n : v) : 0.0;
+      valid[g] = n > 0 ? 1 : 0;
+    }
+  }
+}
+
+static void fp64_sum_groups(Session *s, const Grouping &g, int64_t nrows, const ColPtr &arg, bool avg,
+                            const ColPtr &o) {
+  const int64_t ng = g.ngroups;
+  if (nrows >= (int64_t(1) << 32)) not_impl("FLOAT sum / avg over 2^32 or more rows");
+  force(arg);
+  const ColView av = view_of(arg);
+  BufPtr cnt = s->alloc(8 * (ng + 1));
+  HIP_CHECK(hipMemsetAsync(cnt->p, 0, 8 * (ng + 1), s->stream));
+  const int64_t n1 = std::max<int64_t>(nrows, 1);
+  BufPtr key = s->alloc(8 * n1), skey = s->alloc(8 * n1), row = s->alloc(4 * n1), srow = s->alloc(4 * n1);
+  KernelTimer kt(s, "group_fsum", 16.0 * nrows);
+  if (nrows > 0) {
+    hipLaunchKernelGGL(k_fs_keys, dim3(grid_for(nrows, 256)), dim3(256), 0, s->stream,
+                       (const int64_t *)g.group_of_row->p, av, nrows, ng, (uint64_t *)key->p, (uint32_t *)row->p,
+                       (unsigned long long *)cnt->p);
+    KERNEL_CHECK();
+    int bits = 1;
+    while (bits < 64 && (uint64_t(1) << bits) <= (uint64_t)ng) ++bits;
+    size_t tmp = 0;
+    HIP_CHECK(rocprim::radix_sort_pairs(nullptr, tmp, (const uint64_t *)key->p, (uint64_t *)skey->p,
+                                        (const uint32_t *)row->p, (uint32_t *)srow->p, (size_t)nrows, 0, bits,
+                                        s->stream));
+    BufPtr t = s->alloc(std::max<size_t>(tmp, 16));
+    HIP_CHECK(rocprim::radix_sort_pairs(t->p, tmp, (const uint64_t *)key->p, (uint64_t *)skey->p,
+                                        (const uint32_t *)row->p, (uint32_t *)srow->p, (size_t)nrows, 0, bits,
+                                        s->stream));
+  }
+  // group offsets in the sorted order and first chunks
+  BufPtr off = s->alloc(8 * (ng + 1)), nch = s->alloc(4 * (ng + 1)), ch0 = s->alloc(4 * (ng + 1));
+  exclusive_scan_i64(s, (const int64_t *)cnt->p, (int64_t *)off->p, ng + 1);
+  hipLaunchKernelGGL(k_fs_nchunks, dim3(grid_for(ng + 1, 256)), dim3(256), 0, s->stream,
+                     (const unsigned long long *)cnt->p, ng, (uint32_t *)nch->p);
+  KERNEL_CHECK();
+  BufPtr tot = s->alloc(16);
+  exclusive_scan_u32_async(s, (const uint32_t *)nch->p, (uint32_t *)ch0->p, ng + 1, (uint32_t *)tot->p);
+  uint32_t nchunks = 0;
+  HIP_CHECK(hipMemcpyAsync(&nchunks, (const uint32_t *)ch0->p + ng, 4, hipMemcpyDeviceToHost, s->stream));
+  s->sync();
+  BufPtr part = s->alloc(16 * std::max<uint32_t>(nchunks, 1));
+  if (nchunks > 0) {
+    hipLaunchKernelGGL(k_fs_chunks, dim3(grid_for((int64_t)nchunks * 64, 256, (int64_t)s->num_cus * 64)),
+                       dim3(256), 0, s->stream, (const uint32_t *)srow->p, av, (const int64_t *)off->p,
+                       (const uint32_t *)ch0->p, ng, nchunks, (double2 *)part->p);
+    KERNEL_CHECK();
+  }
+  hipLaunchKernelGGL(k_fs_groups, dim3(grid_for(ng * 64, 256, (int64_t)s->num_cus * 64)), dim3(256), 0, s->stream,
+                     (const double2 *)part->p, (const uint32_t *)ch0->p, (const unsigned long long *)cnt->p, ng,
+                     avg ? 1 : 0, (double *)o->data->p, (uint8_t *)o->valid->p);
+  KERNEL_CHECK();
 }
 
 ColPtr aggregate(Session *s, const Grouping &g, const Data &d, int64_t nrows, int32_t kind,
@@ -505,6 +659,10 @@ ColPtr aggregate(Session *s, const Grouping &g, const Data &d, int64_t nrows, in
   ColPtr o = make_column(s, out_type, ng, true);
   if (ng == 0) return o;
   bool fl = arg && arg->type == Type::Float64;
+  if (fl && out_type == Type::Float64 && (kind == CAPF_AGG_SUM || kind == CAPF_AGG_AVG)) {
+    fp64_sum_groups(s, g, nrows, arg, kind == CAPF_AGG_AVG, o);
+    return o;
+  }
   BufPtr acc = s->alloc(8 * ng);
   BufPtr cnt = s->alloc(8 * ng);
   HIP_CHECK(hipMemsetAsync(cnt->p, 0, 8 * ng, s->stream));

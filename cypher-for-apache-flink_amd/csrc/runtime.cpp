@@ -197,7 +197,7 @@ Program Program::from_c(const capf_expr *e) {
 std::vector<std::string> Program::referenced() const {
   std::vector<std::string> r;
   for (auto &in : code)
-    if (in.op == OP_COL) r.push_back(names[in.i]);
+    if (in.op == OP_COL || in.op == OP_LIST_SIZE) r.push_back(names[in.i]);
   return r;
 }
 
@@ -301,6 +301,30 @@ Type infer_type(const Program &p, const std::vector<std::string> &names,
           }
         }
         st.push_back(r);
+        break;
+      }
+      case OP_STR_LEN: {
+        Type a = pop();
+        if (a != Type::String && a != Type::Null) illegal("size() of a non-string value");
+        st.push_back(Type::Int64);
+        break;
+      }
+      case OP_LIST_SIZE: {
+        if (in.i < 0 || (size_t)in.i >= p.names.size()) illegal("malformed expression program (column)");
+        const std::string &nm = p.names[in.i];
+        int idx = -1;
+        for (size_t k = 0; k < names.size(); ++k)
+          if (names[k] == nm) idx = (int)k;
+        if (idx < 0) illegal("expression references unknown column '" + nm + "'");
+        if (types[idx] != Type::List && types[idx] != Type::Null) illegal("size() of a non-list column");
+        st.push_back(Type::Int64);
+        break;
+      }
+      case OP_IF: {
+        Type v = pop(), c = pop(), e = pop();
+        if (c != Type::Bool && c != Type::Null) illegal("condition is not boolean");
+        if (v != Type::Null && e != Type::Null && v != e) illegal("branches of different types");
+        st.push_back(v != Type::Null ? v : e);
         break;
       }
       default: not_impl("expression opcode " + std::to_string(in.op));
@@ -550,6 +574,31 @@ int64_t node_size(const NodePtr &n) {
   return materialize(n)->nrows;
 }
 
+// Java String.length of a UTF-8 string: UTF-16 code units (one per code point,
+// two above U+FFFF)
+static int64_t utf16_length(const std::string &u) {
+  int64_t n = 0;
+  for (size_t i = 0; i < u.size(); ++i) {
+    const unsigned char c = (unsigned char)u[i];
+    if ((c & 0xC0) == 0x80) continue;  // continuation byte
+    n += c >= 0xF0 ? 2 : 1;
+  }
+  return n;
+}
+
+const int64_t *string_length_table(Session *s, size_t *n) {
+  std::lock_guard<std::mutex> lk(s->str_mu);
+  if (s->d_str_len_n != s->strings.size() || !s->d_str_len) {
+    std::vector<int64_t> len(std::max<size_t>(s->strings.size(), 1), 0);
+    for (size_t i = 0; i < s->strings.size(); ++i) len[i] = utf16_length(s->strings[i]);
+    s->d_str_len = s->alloc(8 * len.size());
+    HIP_CHECK(hipMemcpyAsync(s->d_str_len->p, len.data(), 8 * len.size(), hipMemcpyHostToDevice, s->stream));
+    s->sync();  // the pageable source
+    s->d_str_len_n = s->strings.size();
+  }
+  *n = s->d_str_len_n;
+  return (const int64_t *)s->d_str_len->p;
+}
 }  // namespace capf
 
 // ===================================================================== C-ABI
@@ -1586,10 +1635,13 @@ capf_status capf_table_group(capf_table *t, int32_t n_by, const char *const *by_
         case CAPF_AGG_COUNT: a.out_type = Type::Int64; break;
         case CAPF_AGG_SUM:
         case CAPF_AGG_AVG:
-          // Avg's type signature is the input type (Expr.scala:1058-1066);
-          // Flink's AVG on LONG returns LONG.
           if (at == Type::String || at == Type::Bool) not_impl("sum/avg of non-numeric");
-          a.out_type = at;
+          // avg is a FLOAT also over INTEGER values: the reference's acceptance
+          // tests expect CypherFloat(49.666666666666664) for avg(42, 23, 84) and
+          // 32.5 for avg(42, 23) (flink-cypher-testing/.../AggregationTests.scala:
+          // 852, 876, 921); avg(2, 4, 6) = 4.0 equals their CypherMap("res" -> 4)
+          // (:40-57) under Scala's numeric Map equality.  See DESIGN.md.
+          a.out_type = a.kind == CAPF_AGG_AVG && at == Type::Int64 ? Type::Float64 : at;
           break;
         case CAPF_AGG_MIN:
         case CAPF_AGG_MAX:

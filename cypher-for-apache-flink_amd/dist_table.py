@@ -51,7 +51,7 @@ import torch.distributed as dist
 
 from . import _lib
 from .expr import (AGG_AVG, AGG_COUNT, AGG_COUNT_STAR, AGG_MAX, AGG_MIN, AGG_SUM, T_BOOL, T_INT, T_NULL, T_STRING, Count,
-                   Divide, Max, Min, Sum, Var)
+                   Divide, Max, Min, Sum, ToFloat, Var)
 from .header import RecordHeader
 
 ROUTE_MAXK = 8  # routing keys per shuffle (shuffle.hip); a subset of a key tuple routes correctly
@@ -228,6 +228,8 @@ class DistSession:
         self.ex = exchange
         self.world = exchange.world
         self.rank = exchange.rank
+        # deferred inner joins over base shards (set by dist_node_partitioned_graph)
+        self.defer = False
 
     def intern(self, s):
         return self.local.intern(s)
@@ -267,27 +269,106 @@ def _dist_key_cols(table, by, header):
     return cols
 
 
+class Prov:
+    """Provenance of a table that is a projection of one base shard of a
+    node-partitioned graph (dist_node_partitioned_graph): kind "node" / "rel",
+    the shard's graph-level facts (`info`) and physical column → base column.
+    Kept through select / withColumns / drop / cache, dropped by anything that
+    changes the rows."""
+    __slots__ = ("kind", "info", "cols")
+
+    def __init__(self, kind, info, cols):
+        self.kind, self.info, self.cols = kind, info, dict(cols)
+
+    def renamed(self, pairs):
+        cols = {a: self.cols[c] for c, a in pairs if c in self.cols}
+        return Prov(self.kind, self.info, cols) if cols else None
+
+    def without(self, names):
+        cols = {c: b for c, b in self.cols.items() if c not in names}
+        return Prov(self.kind, self.info, cols) if cols else None
+
+
+class _NoMatch(Exception):
+    pass
+
+
 class DistTable:
     """Table[DistTable]: the rank's shard (`local`, a backend table) plus its
     placement.  Every method is collective: all ranks call it in the same
-    order with the same arguments (the planner is deterministic)."""
+    order with the same arguments (the planner is deterministic).
 
-    def __init__(self, session, local, part=(), placement="hash"):
+    Deferred evaluation (sessions with `defer` set, i.e. node-partitioned
+    graphs): inner joins between projections of base shards, and the filters /
+    projections over them, are recorded instead of executed.  The record is
+    replayed operator for operator — the same eager decisions, shuffles and
+    results — as soon as anything reads the rows; only group(∅, count(*)) looks
+    at the whole record first: the 2-hop chain over the rel shard then runs as
+    the node-partitioned fused count plus ONE all-reduce (_sharded_two_hop),
+    the multi-GPU path of SURVEY §8(e), below the Table SPI."""
+
+    def __init__(self, session, local=None, part=(), placement="hash", prov=None, deferred=None, cols=None):
         self.session = session
-        self.local = local
-        self.part = frozenset(part) if placement == "hash" else frozenset()
-        self.placement = placement
+        self._local = local
+        self._part = frozenset(part) if placement == "hash" else frozenset()
+        self._placement = placement
+        self.prov = prov
+        self._deferred = deferred  # (op, args…) replayed by _force
+        self._cols = cols          # physical columns of a deferred table
 
     @property
     def ex(self):
         return self.session.ex
 
-    def _wrap(self, local, part=(), placement=None):
-        return DistTable(self.session, local, part, placement or self.placement)
+    def _force(self):
+        if self._deferred is None:
+            return
+        op, *args = self._deferred
+        if op == "join":
+            out = args[0]._join_eager(args[1], args[2], *args[3])
+        elif op == "select":
+            out = args[0]._select_eager(*args[1])
+        elif op == "filter":
+            out = args[0]._filter_eager(*args[1:])
+        elif op == "withColumns":
+            out = args[0]._with_columns_eager(args[1], args[2], args[3])
+        else:  # drop
+            out = args[0]._drop_eager(*args[1])
+        self._local, self._part, self._placement = out.local, out.part, out.placement
+        self._deferred = None
+
+    @property
+    def local(self):
+        if self._deferred is not None:
+            self._force()
+        return self._local
+
+    @property
+    def part(self):
+        if self._deferred is not None:
+            self._force()
+        return self._part
+
+    @property
+    def placement(self):
+        if self._deferred is not None:
+            self._force()
+        return self._placement
+
+    def _deferrable(self):
+        return self._deferred is not None or self.prov is not None
+
+    def _defer(self, op, cols):
+        return DistTable(self.session, deferred=op, cols=list(cols))
+
+    def _wrap(self, local, part=(), placement=None, prov=None):
+        return DistTable(self.session, local, part, placement or self.placement, prov)
 
     # ------------------------------------------------------------- CypherTable
     @property
     def physicalColumns(self):
+        if self._deferred is not None:
+            return list(self._cols)
         return self.local.physicalColumns
 
     @property
@@ -328,22 +409,51 @@ class DistTable:
 
     # ------------------------------------------------------------- Table[T]
     def cache(self):
-        return self._wrap(self.local.cache(), self.part)
+        if self._deferred is not None:
+            return self
+        return self._wrap(self.local.cache(), self.part, prov=self.prov)
 
     def select(self, *cols):
         pairs = [(c, c) if isinstance(c, str) else tuple(c) for c in cols]
+        if self._deferred is not None:
+            return self._defer(("select", self, cols), [a for _, a in pairs])
+        return self._select_eager(*cols)
+
+    def _select_eager(self, *cols):
+        pairs = [(c, c) if isinstance(c, str) else tuple(c) for c in cols]
         part = {a for c, a in pairs if c in self.part}
-        return self._wrap(self.local.select(*cols), part)
+        return self._wrap(self.local.select(*cols), part, prov=self.prov.renamed(pairs) if self.prov else None)
 
     def filter(self, expr, header=None, params=None):
+        if self._deferred is not None:
+            return self._defer(("filter", self, expr, header, params), self._cols)
+        return self._filter_eager(expr, header, params)
+
+    def _filter_eager(self, expr, header=None, params=None):
         return self._wrap(self.local.filter(expr, header, params), self.part)
 
     def drop(self, *cols):
-        return self._wrap(self.local.drop(*cols), self.part - set(cols))
+        if self._deferred is not None:
+            return self._defer(("drop", self, cols), [c for c in self._cols if c not in cols])
+        return self._drop_eager(*cols)
+
+    def _drop_eager(self, *cols):
+        return self._wrap(self.local.drop(*cols), self.part - set(cols),
+                          prov=self.prov.without(set(cols)) if self.prov else None)
 
     def withColumns(self, *columns, header=None, params=None):
+        if self._deferred is not None:
+            out = list(self._cols)
+            for _, c in columns:
+                if c not in out:
+                    out.append(c)
+            return self._defer(("withColumns", self, columns, header, params), out)
+        return self._with_columns_eager(columns, header, params)
+
+    def _with_columns_eager(self, columns, header=None, params=None):
         written = {c for _, c in columns}
-        return self._wrap(self.local.withColumns(*columns, header=header, params=params), self.part - written)
+        return self._wrap(self.local.withColumns(*columns, header=header, params=params), self.part - written,
+                          prov=self.prov.without(written) if self.prov else None)
 
     def unionAll(self, other):
         if "replicated" in (self.placement, other.placement):
@@ -354,6 +464,13 @@ class DistTable:
         return self._wrap(self.local.unionAll(other.local), part, "hash")
 
     def join(self, other, join_type, *join_cols):
+        if getattr(self.session, "defer", False) and join_type == "inner" and self._deferrable() \
+                and other._deferrable():
+            return self._defer(("join", self, other, join_type, tuple(join_cols)),
+                               self.physicalColumns + other.physicalColumns)
+        return self._join_eager(other, join_type, *join_cols)
+
+    def _join_eager(self, other, join_type, *join_cols):
         jt = join_type
         pairs = list(join_cols)
         if self.placement == other.placement == "root":
@@ -428,6 +545,13 @@ class DistTable:
         return self._wrap(moved.distinct(*cols), part, "hash")
 
     def group(self, by, aggregations, header=None, params=None):
+        if self._deferred is not None and not list(by) and aggregations and \
+                all(a.kind == AGG_COUNT_STAR for a in aggregations.values()):
+            count = _sharded_two_hop(self)
+            if count is not None:
+                names = list(aggregations)
+                loc = self.session.local.table([(n, T_INT, [count], None) for n in names], nrows=1)
+                return self._wrap(loc if self.session.rank == 0 else loc.limit(0), placement="root")
         keys = _dist_key_cols(self.local, by, header)
         if self.placement == "root":
             out = self.local.group(by, aggregations, header=header, params=params)
@@ -474,7 +598,7 @@ class DistTable:
             elif a.kind == AGG_MAX:
                 partial[p] = a
                 final[name] = Max(Var(p))
-            else:  # avg = Σ sum / Σ count, integer avg by Java long division
+            else:  # avg = Σ sum / Σ count, a FLOAT also over INTEGER values
                 pc = f"__dist_c{i}"
                 partial[p] = Sum(a.expr)
                 partial[pc] = Count(a.expr)
@@ -487,7 +611,8 @@ class DistTable:
         out = rows.group([], final, header=h2, params={})
         if avgs:
             h3 = RecordHeader({Var(c): c for c in out.physicalColumns})
-            out = out.withColumns(*[(Divide(Var(s), Var(n)), name) for name, s, n in avgs], header=h3, params={})
+            out = out.withColumns(*[(Divide(ToFloat(Var(s)), Var(n)), name) for name, s, n in avgs], header=h3,
+                                  params={})
         out = out.select(*names)
         return self._wrap(out if rank0 else out.limit(0), placement="root")
 
@@ -513,3 +638,154 @@ def dist_scan_graph(dsession, graph):
     rels = [ElementTable(t.kind, t.labels, dsession.shard(t.table, t.src_col), t.props, t.id_col, t.src_col,
                          t.dst_col) for t in graph.rel_tables]
     return ScanGraph(dsession, nodes, rels)
+
+
+# ------------------------------------------------------------ sharded 2-hop count
+def _tree_refs(t, leaves, eqs, neqs):
+    """Column name → (leaf index, base column) for the columns of a deferred
+    join tree; join keys into `eqs`, NOT(r_i = r_j) filters into `neqs`."""
+    if t._deferred is None:
+        if t.prov is None:
+            raise _NoMatch
+        leaves.append(t.prov)
+        return {c: (len(leaves) - 1, b) for c, b in t.prov.cols.items()}
+    op, *a = t._deferred
+    if op == "join":
+        lr = _tree_refs(a[0], leaves, eqs, neqs)
+        rr = _tree_refs(a[1], leaves, eqs, neqs)
+        for x, y in a[3]:
+            if x not in lr or y not in rr:
+                raise _NoMatch
+            eqs.append((lr[x], rr[y]))
+        out = dict(lr)
+        out.update(rr)
+        return out
+    refs = _tree_refs(a[0], leaves, eqs, neqs)
+    if op == "select":
+        return {al: refs[c] for c, al in ((c, c) if isinstance(c, str) else tuple(c) for c in a[1])
+                if c in refs}
+    if op == "drop":
+        return {c: r for c, r in refs.items() if c not in a[1]}
+    if op == "withColumns":
+        written = {c for _, c in a[1]}
+        return {c: r for c, r in refs.items() if c not in written}
+    # filter: relationship uniqueness only (front-end rewrite, CypherParser.scala:72)
+    from .expr import Ands, Equals, Not
+    expr, header = a[1], a[2]
+    for term in (expr.exprs if isinstance(expr, Ands) else (expr,)):
+        if not (isinstance(term, Not) and isinstance(term.expr, Equals)):
+            raise _NoMatch
+        x, y = header.get(term.expr.lhs), header.get(term.expr.rhs)
+        if x not in refs or y not in refs:
+            raise _NoMatch
+        neqs.append((refs[x], refs[y]))
+    return refs
+
+
+def _sharded_two_hop(t):
+    """count(*) of MATCH (a)-->(b)-->(c) as lowered by the relational planner
+    (RelationalPlanner.scala:130-165: S_a ⋈ R1 ⋈ S_b ⋈ R2 ⋈ S_c, NOT(r1 = r2))
+    over a node-partitioned graph: every rank adds its partial
+    Σ_{b owned} in[b]·out[b] − owned self-loops (the rel shard's `count_partial`)
+    and ONE int64 all-reduce sums them.  None when `t` is not that shape (the
+    deferred operators are then replayed as usual)."""
+    leaves, eqs, neqs = [], [], []
+    try:
+        _tree_refs(t, leaves, eqs, neqs)
+    except _NoMatch:
+        return None
+    rels = [i for i, p in enumerate(leaves) if p.kind == "rel"]
+    nodes = [i for i, p in enumerate(leaves) if p.kind == "node"]
+    if len(rels) != 2 or len(nodes) != 3 or len(eqs) != 4 or len(neqs) != 1:
+        return None
+    info = leaves[rels[0]].info
+    if leaves[rels[1]].info is not info or not all(leaves[i].info.get("complete") for i in nodes):
+        return None
+    if any(leaves[i].info.get("graph") is not info.get("graph") for i in nodes):
+        return None
+    ends = {}  # (rel leaf, "src"/"dst") → node leaf
+    for x, y in eqs:
+        if leaves[x[0]].kind == "rel":
+            x, y = y, x
+        if leaves[x[0]].kind != "node" or leaves[y[0]].kind != "rel" or x[1] != leaves[x[0]].info["id"]:
+            return None
+        side = "src" if y[1] == info["src"] else "dst" if y[1] == info["dst"] else None
+        if side is None or (y[0], side) in ends:
+            return None
+        ends[(y[0], side)] = x[0]
+    (x, y), = neqs
+    if {x[0], y[0]} != set(rels) or x[1] != info["id"] or y[1] != info["id"]:
+        return None
+    r1, r2 = rels
+    if ends[(r1, "dst")] != ends[(r2, "src")]:
+        r1, r2 = r2, r1
+    b = ends[(r1, "dst")]
+    if ends[(r2, "src")] != b or len({ends[(r1, "src")], b, ends[(r2, "dst")]}) != 3:
+        return None
+    return info["count"]()
+
+
+def dist_node_partitioned_graph(dsession, graph, count_copies=None, compact=True):
+    """dist_scan_graph plus the node-partitioned layout of SURVEY §8(e) for the
+    2-hop count: rank r also holds the rels whose target it owns (in-copy) and
+    those whose source it owns (out-copy), owner(v) = the rank whose node_mix
+    bucket range holds v.  `graph` is the full ScanGraph every rank built (one
+    node table whose ids are exactly [base, base + n) — the complete node set
+    — and one rel table).  count_copies(dsession, rel element table, n, base,
+    compact) → a zero-argument function returning the count: this rank's
+    partial summed over the ranks by one all-reduce (default: the GPU copies,
+    FOR-compacted per `compact`, and capf_chain2_sharded_count).  Graph-ingest
+    work, outside any timed query."""
+    g = dist_scan_graph(dsession, graph)
+    if len(graph.node_tables) != 1 or len(graph.rel_tables) != 1:
+        return g
+    nt, rt = graph.node_tables[0], graph.rel_tables[0]
+    lo, hi, n = _int_range(nt.table, nt.id_col)
+    if n == 0 or hi - lo + 1 != n or nt.table.size != n:
+        return g
+    for c in (rt.src_col, rt.dst_col):
+        a, b, _ = _int_range(rt.table, c)
+        if a < lo or b > hi:
+            return g
+    total = (count_copies or _gpu_count_copies)(dsession, rt, n, lo, compact)
+    ginfo = object()
+    node_info = {"complete": True, "graph": ginfo, "id": nt.id_col}
+    rel_info = {"graph": ginfo, "id": rt.id_col, "src": rt.src_col, "dst": rt.dst_col, "count": total}
+    gn, gr = g.node_tables[0].table, g.rel_tables[0].table
+    gn.prov = Prov("node", node_info, {c: c for c in gn.physicalColumns})
+    gr.prov = Prov("rel", rel_info, {c: c for c in gr.physicalColumns})
+    dsession.defer = True
+    return g
+
+
+def _int_range(table, col):
+    """(min, max, non-null count) of an INTEGER column."""
+    if hasattr(table, "_h"):
+        mn, mx, nn = c_int64(), c_int64(), c_int64()
+        _lib.call("capf_table_column_range", table._h, col.encode(), byref(mn), byref(mx), byref(nn))
+        return mn.value, mx.value, nn.value
+    vals = [v for v in table.column_values(col) if v is not None]
+    return (min(vals), max(vals), len(vals)) if vals else (0, -1, 0)
+
+
+def _gpu_count_copies(dsession, rt, n, lo, compact=True):
+    """This rank's in/out copies (capf_table_node_partition, FOR-compacted) and
+    the count: its partial enqueued (capf_chain2_sharded_count) into a device
+    int64 on the session stream (= torch's current stream), summed in place by
+    ONE all-reduce (RCCL orders it after the kernels on that stream), one host
+    read."""
+    from .dist import node_partitioned_copies, sum_partials
+    from .table import chain2_sharded_count_async
+    s, world, rank = dsession.local, dsession.world, dsession.rank
+    group = getattr(dsession.ex, "group", None)
+    in_copy, out_copy = node_partitioned_copies(rt.table, n, world, rank, lo, rt.src_col, rt.dst_col,
+                                                compact=compact)
+    buf = torch.zeros(1, dtype=torch.int64, device="cuda")
+
+    def total():
+        chain2_sharded_count_async(s, in_copy, out_copy, lo, n, world, rank, buf.data_ptr(),
+                                   rt.src_col, rt.dst_col)
+        sum_partials(buf, group)
+        return int(buf.item())
+    total.copies = (in_copy, out_copy)
+    return total

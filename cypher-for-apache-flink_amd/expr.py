@@ -33,6 +33,7 @@ OP_EQ, OP_NEQ, OP_LT, OP_LE, OP_GT, OP_GE = 10, 11, 12, 13, 14, 15
 OP_NOT, OP_AND, OP_OR, OP_IS_NULL, OP_IS_NOT_NULL = 20, 21, 22, 23, 24
 OP_ADD, OP_SUB, OP_MUL, OP_DIV, OP_MOD, OP_NEG = 30, 31, 32, 33, 34, 35
 OP_TO_FLOAT, OP_TO_INTEGER, OP_COALESCE = 40, 41, 50
+OP_STR_LEN, OP_LIST_SIZE, OP_IF = 60, 61, 62
 
 # aggregators
 AGG_COUNT_STAR, AGG_COUNT, AGG_SUM, AGG_MIN, AGG_MAX, AGG_AVG, AGG_COLLECT = 0, 1, 2, 3, 4, 5, 6
@@ -223,6 +224,41 @@ class Coalesce(Expr):
         return "coalesce(" + ", ".join(map(str, self.exprs)) + ")"
 
 
+@dataclass(frozen=True)
+class ListLit(Expr):
+    """[e1, e2, …] (okapi ListLit): literal elements only on the GPU."""
+    items: Tuple[Expr, ...]
+
+    def __init__(self, *items):
+        object.__setattr__(self, "items", tuple(items))
+
+    def __str__(self):
+        return "[" + ", ".join(map(str, self.items)) + "]"
+
+
+@dataclass(frozen=True)
+class In(Expr):
+    """lhs IN rhs (okapi In; FlinkSQLExprMapper.scala:114-118): rhs a list
+    literal or a list parameter.  SQL IN semantics: NULL when lhs is NULL or
+    when nothing matches and the list holds a NULL; an empty list is FALSE."""
+    lhs: Expr
+    rhs: Expr
+
+    def __str__(self):
+        return f"({self.lhs} IN {self.rhs})"
+
+
+Id = _unary("Id", "id({})")            # FlinkSQLExprMapper.scala:134: the element's id column
+Exists = _unary("Exists", "exists({})")  # exists(n.prop) → IS NOT NULL (:90)
+Size = _unary("Size", "size({})")      # charLength / cardinality (:80-85)
+Type = _unary("Type", "type({})")      # the relationship's type name (:152-160)
+
+
+def java_length(v):
+    """Java String.length: UTF-16 code units."""
+    return len(v.encode("utf-16-le")) // 2
+
+
 class ExistsPattern(Expr):
     """EXISTS((a)-->()-->(b)) — a pattern predicate (okapi ExistsPatternExpr,
     okapi-ir/.../api/expr/Expr.scala).  `pattern` is a planner Match over
@@ -312,7 +348,50 @@ _BIN_OPS = {
     "Divide": OP_DIV, "Modulo": OP_MOD,
 }
 _UN_OPS = {"Not": OP_NOT, "IsNull": OP_IS_NULL, "IsNotNull": OP_IS_NOT_NULL, "ToFloat": OP_TO_FLOAT,
-           "ToInteger": OP_TO_INTEGER, "Negate": OP_NEG}
+           "ToInteger": OP_TO_INTEGER, "Negate": OP_NEG, "Exists": OP_IS_NOT_NULL}
+
+
+def _value_type(v):
+    """capf type of a literal / parameter value (None: not a scalar)."""
+    if v is None:
+        return T_NULL
+    if isinstance(v, bool):
+        return T_BOOL
+    if isinstance(v, int):
+        return T_INT
+    if isinstance(v, float):
+        return T_FLOAT
+    if isinstance(v, str):
+        return T_STRING
+    return None
+
+
+def _comparable(a, b):
+    """Could values of capf types a and b be equal?  (None: unknown.)"""
+    if a is None or b is None or T_NULL in (a, b):
+        return True
+    num = (T_INT, T_FLOAT)
+    return a == b or (a in num and b in num)
+
+
+def list_values(e, params):
+    """The Python values of a list literal / list parameter, or None."""
+    if isinstance(e, ListLit):
+        out = []
+        for x in e.items:
+            if isinstance(x, NullLit):
+                out.append(None)
+            elif isinstance(x, (IntegerLit, FloatLit, StringLit, BoolLit)):
+                out.append(x.v)
+            elif isinstance(x, Param):
+                out.append((params or {}).get(x.pname))
+            else:
+                return None
+        return out
+    if isinstance(e, Param):
+        v = (params or {}).get(e.pname)
+        return list(v) if isinstance(v, (list, tuple)) else None
+    return None
 
 
 def resolve_column(expr, header, columns):
@@ -323,11 +402,12 @@ def resolve_column(expr, header, columns):
     return None
 
 
-def compile_program(expr, header, columns, params=None, intern=None):
+def compile_program(expr, header, columns, params=None, intern=None, coltype=None):
     """Lower `expr` to (ops, iargs, fargs, names) for the C-ABI.
 
     header: dict Expr -> physical column; columns: set of the table's columns;
-    intern: str -> int64 code (session string dictionary).
+    intern: str -> int64 code (session string dictionary); coltype: column ->
+    capf type (for size() and IN, whose lowering depends on the operand type).
     """
     params = params or {}
     ops, ia, fa, names = [], [], [], []
@@ -355,11 +435,40 @@ def compile_program(expr, header, columns, params=None, intern=None):
             from ._lib import NotImplementedException
             raise NotImplementedException(f"literal {v!r} of type {type(v).__name__}")
 
-    def col(name):
+    def name_of(name):
         if name not in name_idx:
             name_idx[name] = len(names)
             names.append(name)
-        emit(OP_COL, name_idx[name])
+        return name_idx[name]
+
+    def col(name):
+        emit(OP_COL, name_of(name))
+
+    def column_of(e):
+        return resolve_column(e, header, columns) if header is not None and e in header else None
+
+    def static_type(e):
+        """capf type of e when known without evaluating it, else None."""
+        c = column_of(e)
+        if c is not None:
+            return coltype(c) if coltype is not None else CT_TO_CAPF.get(getattr(e, "ctype", "ANY"))
+        if isinstance(e, (IntegerLit, FloatLit, StringLit, BoolLit)):
+            return _value_type(e.v)
+        if isinstance(e, NullLit):
+            return T_NULL
+        if isinstance(e, Param):
+            return _value_type((params or {}).get(e.pname))
+        if isinstance(e, (Var, ElementProperty)):  # no column: a NULL literal
+            return T_NULL
+        if isinstance(e, (ToFloat,)):
+            return T_FLOAT
+        if isinstance(e, (ToInteger, Size, Id)):
+            return T_INT
+        return None
+
+    def not_impl(what):
+        from ._lib import NotImplementedException
+        raise NotImplementedException(f"No support for converting Cypher expression {what} to a GPU expression")
 
     def go(e):
         cls = type(e).__name__
@@ -412,6 +521,66 @@ def compile_program(expr, header, columns, params=None, intern=None):
             for x in e.exprs:
                 go(x)
             emit(OP_COALESCE, len(e.exprs))
+        elif cls == "Id":
+            go(e.expr)  # the id column (FlinkSQLExprMapper.scala:134)
+        elif isinstance(e, In):
+            vals = list_values(e.rhs, params)
+            if vals is None:
+                not_impl(e)
+            if not vals:
+                emit(OP_LIT_BOOL, 0)  # CTList(CTVoid) → FALSE (:115)
+                return
+            lt = static_type(e.lhs)
+            cand = [v for v in vals if _value_type(v) is not None and _comparable(lt, _value_type(v))]
+            if any(_value_type(v) is None for v in vals):
+                not_impl(e)  # nested lists / maps
+            if not cand:
+                emit(OP_LIT_NULL, T_BOOL)  # no element could be of lhs's type (:117)
+                return
+            # left-folded 3-valued OR of equalities: stack depth 3 whatever the list length
+            for k, v in enumerate(cand):
+                go(e.lhs)
+                lit(v)
+                emit(OP_EQ)
+                if k:
+                    emit(OP_OR, 2)
+        elif cls == "Size":
+            x = e.expr
+            vals = list_values(x, params) if isinstance(x, (ListLit, Param)) else None
+            if vals is not None:
+                emit(OP_LIT_INT, len(vals))
+                return
+            if isinstance(x, StringLit) or (isinstance(x, Param) and isinstance((params or {}).get(x.pname), str)):
+                emit(OP_LIT_INT, java_length(x.v if isinstance(x, StringLit) else params[x.pname]))
+                return
+            if isinstance(x, (NullLit, Param)):
+                emit(OP_LIT_NULL, T_INT)
+                return
+            c = column_of(x)
+            t = static_type(x)
+            if c is not None and t == T_LIST:
+                emit(OP_LIST_SIZE, name_of(c))
+            elif t == T_STRING:
+                go(x)
+                emit(OP_STR_LEN)
+            elif t == T_NULL:
+                emit(OP_LIT_NULL, T_INT)
+            else:
+                not_impl(e)
+        elif cls == "Type":
+            v = e.expr
+            if isinstance(v, NullLit):
+                emit(OP_LIT_NULL, T_STRING)  # type(null) is null (MTa/NullTests.scala:49)
+                return
+            if not isinstance(v, Var):
+                not_impl(e)  # only variables (:161-162)
+            types = sorted((h.rel_type, c) for h, c in (header.items() if header is not None else ())
+                           if isinstance(h, HasType) and h.owner == v and c in columns)
+            emit(OP_LIT_NULL, T_STRING)
+            for ty, c in types:  # acc ← HasType(v, ty) ? 'ty' : acc
+                col(c)
+                lit(ty)
+                emit(OP_IF)
         else:
             from ._lib import NotImplementedException
             raise NotImplementedException(

@@ -614,6 +614,8 @@ def plan_query(graph, q: Query, params=None) -> Planned:
     choices (fused counts, the fused var-length reach of config 5) are made by
     the backend below the Table SPI from the plan DAG these calls build."""
     op = None
+    if not q.matches:  # a leading RETURN / WITH: one row of the unit table (Start)
+        op = Planned(graph.session.unit(), RecordHeader({}))
     for m in q.matches:
         op = plan_optional(graph, m, op, params) if m.optional else plan_match(graph, m, op, params)
     for st in q.stages:

@@ -209,7 +209,8 @@ _SELECT_ARGS = {}
 
 
 def _program(expr, header, table, params):
-    return compile_program(expr, header, set(table.physicalColumns), params, table.session.intern)
+    return compile_program(expr, header, set(table.physicalColumns), params, table.session.intern,
+                           table.capf_type)
 
 
 class GpuTable:

@@ -133,7 +133,15 @@ enum {
   CAPF_OP_NEG = 35,        /* unary minus                                   */
   CAPF_OP_TO_FLOAT = 40,   /* ToFloat  → DOUBLE                             */
   CAPF_OP_TO_INTEGER = 41, /* ToInteger → Flink casts to INT (32-bit!)      */
-  CAPF_OP_COALESCE = 50    /* Coalesce, arity iarg                          */
+  CAPF_OP_COALESCE = 50,   /* Coalesce, arity iarg                          */
+  CAPF_OP_STR_LEN = 60,    /* Size(string): pop a STRING, push its length in
+                              UTF-16 units (Java String.length, Flink
+                              charLength, FlinkSQLExprMapper.scala:80-85)   */
+  CAPF_OP_LIST_SIZE = 61,  /* Size(list): push the element count of LIST
+                              column names[iarg] (Flink cardinality, :80-85) */
+  CAPF_OP_IF = 62          /* pop value, cond, else: push cond TRUE ? value :
+                              else (type(r) over the HasType columns,
+                              FlinkSQLExprMapper.scala:152-160)              */
 };
 
 typedef struct capf_expr {

@@ -13,6 +13,7 @@ package org.opencypher.gpu
 
 import scala.collection.mutable
 
+import org.opencypher.okapi.api.types._
 import org.opencypher.okapi.api.value.CypherValue._
 import org.opencypher.okapi.impl.exception.NotImplementedException
 import org.opencypher.okapi.ir.api.expr._
@@ -29,6 +30,7 @@ object GpuExprMapper {
   private final val Add_ = 30; private final val Sub = 31; private final val Mul = 32; private final val Div = 33
   private final val Neg = 35   // CAPF_OP_MOD (34) has no okapi Expr: okapi-ir has no Modulo
   private final val ToFloat_ = 40; private final val ToInteger_ = 41; private final val Coalesce_ = 50
+  private final val StrLen = 60; private final val ListSize = 61; private final val If_ = 62
 
   def program(expr: Expr, header: RecordHeader, table: GpuTable, parameters: CypherMap): Program = {
     val ops = mutable.ArrayBuffer.empty[Int]
@@ -40,7 +42,40 @@ object GpuExprMapper {
 
     def emit(op: Int, i: Long = 0L, f: Double = 0.0): Unit = { ops += op; iargs += i; fargs += f }
 
-    def col(name: String): Unit = emit(Col, names.getOrElseUpdate(name, names.size).toLong)
+    def nameIndex(name: String): Long = names.getOrElseUpdate(name, names.size).toLong
+    def col(name: String): Unit = emit(Col, nameIndex(name))
+
+    // the literal values of a list literal / list parameter (IN, size)
+    def listValues(e: Expr): Option[List[CypherValue]] = e match {
+      case ListLit(items) => Some(items.map {
+        case NullLit(_) => CypherNull
+        case IntegerLit(v) => CypherInteger(v)
+        case FloatLit(v) => CypherFloat(v)
+        case StringLit(v) => CypherString(v)
+        case TrueLit => CypherBoolean(true)
+        case FalseLit => CypherBoolean(false)
+        case Param(p) => parameters(p)
+        case other => throw NotImplementedException(s"GPU list element $other")
+      })
+      case Param(p) => parameters(p) match {
+        case CypherList(vs) => Some(vs)
+        case _ => None
+      }
+      case _ => None
+    }
+
+    // could a value of `v` be equal to a value of Cypher type `t`?
+    def comparable(t: CypherType, v: CypherValue): Boolean = (t.material, v) match {
+      case (_, CypherNull) => true
+      case (CTInteger | CTFloat | CTNumber, _: CypherInteger | _: CypherFloat) => true
+      case (CTString, _: CypherString) => true
+      case (CTBoolean, _: CypherBoolean) => true
+      case (CTAny | CTNull | CTVoid, _) => true
+      case _ => false
+    }
+
+    // Java String.length (UTF-16 units) = Flink charLength
+    def javaLength(v: String): Long = v.length.toLong
 
     def lit(v: CypherValue): Unit = v match {
       case CypherNull => emit(LitNull, Native.TypeNull)
@@ -88,6 +123,37 @@ object GpuExprMapper {
       case ToFloat(x) => go(x); emit(ToFloat_)
       case ToInteger(x) => go(x); emit(ToInteger_)                          // Flink: INT (FlinkSQLExprMapper.scala:183)
       case Coalesce(xs) => xs.foreach(go); emit(Coalesce_, xs.size.toLong)
+      case Id(x) => go(x)                                                  // FlinkSQLExprMapper.scala:134
+      case Exists(x) => go(x); emit(IsNotNull_)                            // :90
+      case In(lhs, rhs) =>                                                 // :114-118
+        val vals = listValues(rhs).getOrElse(throw NotImplementedException(s"GPU IN over $rhs"))
+        if (vals.isEmpty) emit(LitBool, 0L)                                // CTList(CTVoid) → FALSE
+        else {
+          val cand = vals.filter(v => comparable(lhs.cypherType, v))
+          if (cand.isEmpty) emit(LitNull, Native.TypeBool)                 // incompatible element type → NULL
+          else cand.zipWithIndex.foreach { case (v, k) =>                  // left-folded 3-valued OR
+            go(lhs); lit(v); emit(Eq); if (k > 0) emit(Or, 2L)
+          }
+        }
+      case Size(x) =>                                                      // :80-85
+        listValues(x) match {
+          case Some(vs) => emit(LitInt, vs.size.toLong)
+          case None => x match {
+            case StringLit(v) => emit(LitInt, javaLength(v))
+            case NullLit(_) => emit(LitNull, Native.TypeInt64)
+            case _ if x.cypherType.material.isInstanceOf[CTList] && physical(x).isDefined =>
+              emit(ListSize, nameIndex(physical(x).get))
+            case _ if x.cypherType.material == CTString => go(x); emit(StrLen)
+            case _ if physical(x).isEmpty && x.cypherType.material == CTNull => emit(LitNull, Native.TypeInt64)
+            case _ => throw NotImplementedException(s"GPU size of $x")
+          }
+        }
+      case Type(NullLit(_)) => emit(LitNull, Native.TypeString)
+      case Type(v: Var) =>                                                 // :152-160
+        emit(LitNull, Native.TypeString)
+        header.typesFor(v).toSeq.sortBy(_.relType.name).foreach { t =>
+          physical(t).foreach { c => col(c); emit(LitString, session.intern(t.relType.name)); emit(If_) }
+        }
       case other =>
         throw NotImplementedException(s"No support for converting Cypher expression $other to a GPU expression")
     }

@@ -30,8 +30,33 @@ import numpy as np
 
 from capf_amd.expr import (T_BOOL, T_FLOAT, T_INT, T_LIST, T_NULL, T_STRING, CAPF_TO_CT, CT_TO_CAPF,
                            Aggregator, Ands, BoolLit, Coalesce, ElementProperty, EndNode, FloatLit, HasLabel,
-                           HasType, IntegerLit, NullLit, Ors, Param, StartNode, StringLit, Var, AGG_AVG,
+                           HasType, IntegerLit, ListLit, NullLit, Ors, Param, StartNode, StringLit, Var, AGG_AVG,
                            AGG_COLLECT, AGG_COUNT, AGG_COUNT_STAR, AGG_MAX, AGG_MIN, AGG_SUM)
+
+
+def list_values(e, params):
+    """Values of a list literal or list parameter (None: not one)."""
+    if isinstance(e, ListLit):
+        out = []
+        for x in e.items:
+            if isinstance(x, NullLit):
+                out.append(None)
+            elif isinstance(x, Param):
+                out.append((params or {}).get(x.pname))
+            elif isinstance(x, (IntegerLit, FloatLit, StringLit, BoolLit)):
+                out.append(x.v)
+            else:
+                return None
+        return out
+    if isinstance(e, Param):
+        v = (params or {}).get(e.pname)
+        return list(v) if isinstance(v, (list, tuple)) else None
+    return None
+
+
+def java_length(v):
+    """java.lang.String.length(): UTF-16 code units."""
+    return len(v.encode("utf-16-le")) // 2
 
 
 class Col:
@@ -251,6 +276,58 @@ def evaluate(e, table, header, params):
             res = np.where(dom, not is_and, is_and)
             ok = dom | ~anynull
             return Val(T_BOOL, res.astype(bool), ok)
+        if name == "Id":  # the element's id column (FlinkSQLExprMapper.scala:134)
+            return go(x.expr)
+        if name == "Exists":  # exists(n.prop) (:90)
+            a = go(x.expr)
+            return Val(T_BOOL, a.ok.copy(), np.ones(n, bool))
+        if name == "In":  # SQL IN over a literal / parameter list (:114-118)
+            items = list_values(x.rhs, params)
+            if items is None:
+                raise NotImplementedError(f"oracle: IN over {x.rhs}")
+            if not items:
+                return const(T_BOOL, False)
+            a = go(x.lhs)
+            kind = lambda v: (None if v is None else "num" if isinstance(v, (int, float)) and not isinstance(v, bool)  # noqa: E731
+                              else type(v).__name__)
+            lk = {T_INT: "num", T_FLOAT: "num", T_STRING: "str", T_BOOL: "bool"}.get(a.t)
+            cand = [v for v in items if v is None or lk is None or kind(v) == lk]
+            if not cand:
+                return const(T_BOOL, None, False)
+            hit = np.zeros(n, bool)
+            vals = a.v
+            for v in cand:
+                if v is not None:
+                    hit |= np.array([ok and (u == v) for u, ok in zip(vals, a.ok)], dtype=bool)
+            has_null = any(v is None for v in cand)
+            ok = a.ok & (hit | (not has_null))
+            return Val(T_BOOL, hit, ok)
+        if name == "Size":  # charLength / cardinality (:80-85)
+            items = list_values(x.expr, params) if isinstance(x.expr, (ListLit, Param)) else None
+            if items is not None:
+                return const(T_INT, len(items))
+            a = go(x.expr)
+            if a.t == T_NULL:
+                return const(T_INT, None, False)
+            if a.t == T_STRING:
+                r = np.array([java_length(v) if ok else 0 for v, ok in zip(a.v, a.ok)], dtype=np.int64)
+            elif a.t == T_LIST:
+                r = np.array([len(v) if ok else 0 for v, ok in zip(a.v, a.ok)], dtype=np.int64)
+            else:
+                raise NotImplementedError(f"oracle: size of {CAPF_TO_CT[a.t]}")
+            return Val(T_INT, r, a.ok.copy())
+        if name == "Type":  # the type whose HasType column is true (:152-160)
+            if isinstance(x.expr, NullLit):
+                return const(T_STRING, None, False)
+            out = np.full(n, None, dtype=object)
+            ok = np.zeros(n, bool)
+            for h, c in (header.items() if header is not None else ()):
+                if isinstance(h, HasType) and h.owner == x.expr and c in cols:
+                    k = cols[c]
+                    t = k.ok & k.v.astype(bool)
+                    out[t] = h.rel_type
+                    ok |= t
+            return Val(T_STRING, out, ok)
         if isinstance(x, Coalesce):
             vals = [go(y) for y in x.exprs]
             t = T_NULL
@@ -534,7 +611,8 @@ class OracleTable:
             raise NotImplementedError("aggregate of strings")
         cnt = np.bincount(gid[sel], minlength=ng)
         t = v.t
-        res = _empty_vals(t if t != T_NULL else T_INT, ng)
+        out_t = T_FLOAT if agg.kind == AGG_AVG and t == T_INT else t
+        res = _empty_vals(out_t if out_t != T_NULL else T_INT, ng)
         # sequential fold in row order (Flink accumulates per group)
         acc = [None] * ng
         for g, x, ok in zip(gid.tolist(), v.v.tolist(), sel.tolist()):
@@ -552,15 +630,13 @@ class OracleTable:
             if a is None:
                 continue
             if agg.kind == AGG_AVG:
-                if t == T_FLOAT:
-                    a = a / cnt[g]
-                else:  # Java long division
-                    q = abs(int(a)) // int(cnt[g])
-                    a = q if a >= 0 else -q
-            if t == T_INT:
+                # a FLOAT also over INTEGER values (AggregationTests.scala:852, 876, 921):
+                # the exact sum as a double over the count
+                a = float(((int(a) + 2 ** 63) % 2 ** 64) - 2 ** 63 if t == T_INT else a) / float(cnt[g])
+            elif t == T_INT:
                 a = ((int(a) + 2 ** 63) % 2 ** 64) - 2 ** 63  # LONG wrap-around
             res[g] = a
-        return Col(t if t != T_NULL else T_INT, res, cnt > 0)
+        return Col(out_t if out_t != T_NULL else T_INT, res, cnt > 0)
 
     def withColumns(self, *columns, header=None, params=None):
         order = list(self._order)

@@ -83,3 +83,26 @@ class OracleExchange:
         mine = [g[self.rank] for g in got]
         order = table.physicalColumns
         return _concat(mine, order, [table.capf_type(c) for c in order])
+
+
+def oracle_count_copies(dsession, rt, n, lo, compact=True):
+    """Oracle stand-in for the GPU copies of dist_node_partitioned_graph: this
+    rank's partial Σ_{b owned} in[b]·out[b] − owned self-loops with b owned
+    when (b − lo) mod G = rank (any partition of the node ids sums to the
+    count), from the full rel table every rank holds."""
+    src = np.asarray(rt.table.column_values(rt.src_col), dtype=np.int64) - lo
+    dst = np.asarray(rt.table.column_values(rt.dst_col), dtype=np.int64) - lo
+    world, rank = dsession.world, dsession.rank
+    calls = oracle_count_copies.calls
+
+    def partial():
+        calls.append(rank)
+        own = np.arange(n) % world == rank
+        ins = np.bincount(dst, minlength=n)
+        outs = np.bincount(src, minlength=n)
+        loops = int(((src == dst) & own[src]).sum())
+        return int((ins[own].astype(object) * outs[own].astype(object)).sum()) - loops
+    return lambda: dsession.ex.all_sum(partial())
+
+
+oracle_count_copies.calls = []

@@ -11,7 +11,8 @@ Sources (relative to the reference checkout):
   MTa = morpheus-testing/src/test/scala/org/opencypher/morpheus/impl/acceptance/
 """
 import capf_import  # noqa: F401
-from capf_amd.expr import (Avg, Collect, Count, CountStar, ElementProperty, Max, Min, Sum, Var)
+from capf_amd.expr import (Avg, Collect, Count, CountStar, ElementProperty, Exists, Id, In, IntegerLit, ListLit,
+                           Max, Min, NullLit, Param, Size, StringLit, Sum, Type, Var)
 from capf_amd.planner import Match, NodeP, Query, RelP, Stage
 
 
@@ -591,12 +592,9 @@ CASES = CASES + AGG_WITH_CASES
 # ------------------------------ AggregationTests COLLECT / Combinations (FTt)
 # collect(e) is Flink's COLLECT, a MULTISET (FlinkSQLExprMapper.scala:283): the
 # reference compares the lists with .toBag, and so does conftest.bag.
-# Option "deviates": {field: value the reference test expects} marks the
-# avg-over-INTEGER fields: the reference expects a FLOAT (49.666…, 32.5) where
-# okapi types avg as its input type (Expr.scala:1058-1066) and Flink's AVG on
-# LONG divides as a long — the parity hazard recorded in SURVEY §8(c); the
-# expected rows here hold the INTEGER result (49, 32, 84) and
-# test_oracle_golden checks that only such fields deviate.
+# avg over INTEGER values is a FLOAT (49.666…, 32.5), as these reference tests
+# expect; option "typed" marks the cases whose reference test compares the
+# CypherValues directly (`rows.head("avg") should equal(CypherFloat(…))`).
 
 
 def _agg_all():
@@ -639,12 +637,12 @@ COLLECT_CASES = [
      [], {"row_count": 0}),
     ("comb_with", "FTt/acceptance/AggregationTests.scala:835-857", INTS3,
      scan_n(ret(*_agg_all()), ret(*[(a, Var(a)) for a in COMB_OUT])),
-     [{"avg": 49, "cnt": 3, "min": 23, "max": 84, "sum": 149, "col": [23, 42, 84]}],
-     {"deviates": {"avg": 49.666666666666664}}),
+     [{"avg": 49.666666666666664, "cnt": 3, "min": 23, "max": 84, "sum": 149, "col": [23, 42, 84]}],
+     {"typed": True}),
     ("comb_return", "FTt/acceptance/AggregationTests.scala:859-880", INTS3,
      scan_n(ret(*_agg_all())),
-     [{"avg": 49, "cnt": 3, "min": 23, "max": 84, "sum": 149, "col": [23, 42, 84]}],
-     {"deviates": {"avg": 49.666666666666664}}),
+     [{"avg": 49.666666666666664, "cnt": 3, "min": 23, "max": 84, "sum": 149, "col": [23, 42, 84]}],
+     {"typed": True}),
     ("comb_grouping_return", "FTt/acceptance/AggregationTests.scala:882-901", KEYED_FLOATS,
      scan_n(ret(("key", P("n", "key")), *_agg_all())),
      [{"key": "b", "avg": 84.0, "cnt": 1, "min": 84.0, "max": 84.0, "sum": 84.0, "col": [84.0]},
@@ -652,9 +650,8 @@ COLLECT_CASES = [
     ("comb_grouping_with", "FTt/acceptance/AggregationTests.scala:903-925", KEYED_INTS,
      scan_n(ret(("key", P("n", "key")), *_agg_all()),
             ret(*[(a, Var(a)) for a in ["key"] + COMB_OUT])),
-     [{"key": "a", "avg": 32, "cnt": 2, "min": 23, "max": 42, "sum": 65, "col": [23, 42]},
-      {"key": "b", "avg": 84, "cnt": 1, "min": 84, "max": 84, "sum": 84, "col": [84]}],
-     {"deviates": {"avg": "32.5 (key a), 84.0 (key b)"}}),
+     [{"key": "a", "avg": 32.5, "cnt": 2, "min": 23, "max": 42, "sum": 65, "col": [23, 42]},
+      {"key": "b", "avg": 84.0, "cnt": 1, "min": 84, "max": 84, "sum": 84, "col": [84]}]),
 ]
 CASES = CASES + COLLECT_CASES
 
@@ -680,3 +677,59 @@ CASES.append(
            [ret(("p1.name", P("p1", "name")), ("p2.name", P("p2", "name")),
                 ("post.content", P("post", "content")))]),
      [{"p1.name": "Alice", "p2.name": "Bob", "post.content": "foobar"}]))
+
+
+# ------------------------- expressions: id / exists / type / size / IN (MTa, FlinkSQLExprMapper :80-134)
+def _r(v):
+    return Var(v, "RELATIONSHIP")
+
+
+def _unit(*items):
+    return Query([], [ret(*items)])
+
+
+A3 = "CREATE (:A {val: 1}), (:A {val: 2}), (:A {val: 3})"
+EXPR_CASES = [
+    ("fn_exists", "MTa/FunctionTests.scala:596-608", "CREATE ({id: 1}), ({id: 2}), ({other: 'foo'}), ()",
+     scan_n(ret(("exists", Exists(P("n", "id"))))),
+     [{"exists": True}, {"exists": True}, {"exists": False}, {"exists": False}]),
+    ("fn_type", "MTa/FunctionTests.scala:635-647", "CREATE ()-[:KNOWS]->()-[:HATES]->()-[:REL]->()",
+     Query([Match([NodeP("_a"), NodeP("_b")], [RelP("r", "_a", "_b")])], [ret(("type(r)", Type(_r("r"))))]),
+     [{"type(r)": "KNOWS"}, {"type(r)": "HATES"}, {"type(r)": "REL"}]),
+    # the reference encodes the ids as Morpheus ids; CAPF's are the raw LONGs
+    ("fn_id_node", "MTa/FunctionTests.scala:651-657", "CREATE (),()",
+     scan_n(ret(("id(n)", Id(N("n"))))), [{"id(n)": 0}, {"id(n)": 1}]),
+    ("fn_id_rel", "MTa/FunctionTests.scala:659-665", "CREATE ()-[:REL]->()-[:REL]->()",
+     Query([Match([NodeP("_a"), NodeP("_b")], [RelP("e", "_a", "_b")])], [ret(("id(e)", Id(_r("e"))))]),
+     [{"id(e)": 2}, {"id(e)": 4}]),
+    ("fn_size_literal_list", "MTa/FunctionTests.scala:722-731", "CREATE ()",
+     scan_n(ret(("s", Size(ListLit(StringLit("Alice"), StringLit("Bob")))))), [{"s": 2}]),
+    ("fn_size_literal_string", "MTa/FunctionTests.scala:733-742", "CREATE ()",
+     scan_n(ret(("s", Size(StringLit("Alice"))))), [{"s": 5}]),
+    ("fn_size_retrieved_string", "MTa/FunctionTests.scala:744-753", "CREATE ({name: 'Alice'})",
+     Query([Match([NodeP("a")])], [ret(("s", Size(P("a", "name", "STRING"))))]), [{"s": 5}]),
+    ("fn_size_null", "MTa/FunctionTests.scala:769-779", "CREATE ()",
+     Query([Match([NodeP("a")])], [ret(("s", Size(P("a", "prop"))))]), [{"s": None}]),
+    ("pred_in", "MTa/PredicateTests.scala:56-67", A3,
+     Query([Match([NodeP("a", ("A",))], where=[In(P("a", "val"), ListLit(IntegerLit(-1), IntegerLit(2),
+                                                                          IntegerLit(5), IntegerLit(0)))])],
+           [ret(("a.val", P("a", "val")))]), [{"a.val": 2}]),
+    ("pred_in_param", "MTa/PredicateTests.scala:69-80", A3,
+     Query([Match([NodeP("a", ("A",))], where=[In(P("a", "val"), Param("list"))])],
+           [ret(("a.val", P("a", "val")))]), [{"a.val": 2}], {"params": {"list": [-1, 2, 5, 0]}}),
+    ("null_in_empty", "MTa/NullTests.scala:127", "",
+     _unit(("res", In(NullLit(), ListLit()))), [{"res": False}]),
+    ("null_in_list", "MTa/NullTests.scala:128", "",
+     _unit(("res", In(NullLit(), ListLit(IntegerLit(1), IntegerLit(2))))), [{"res": None}]),
+    ("null_in_null", "MTa/NullTests.scala:129", "",
+     _unit(("res", In(NullLit(), ListLit(NullLit())))), [{"res": None}]),
+    ("null_in_list_null", "MTa/NullTests.scala:130", "",
+     _unit(("res", In(NullLit(), ListLit(IntegerLit(1), NullLit())))), [{"res": None}]),
+    ("one_in_list_null", "MTa/NullTests.scala:131", "",
+     _unit(("res", In(IntegerLit(1), ListLit(IntegerLit(1), NullLit())))), [{"res": True}]),
+    ("two_in_list_null", "MTa/NullTests.scala:132", "",
+     _unit(("res", In(IntegerLit(2), ListLit(IntegerLit(1), NullLit())))), [{"res": None}]),
+    ("null_id", "MTa/NullTests.scala:47", "", _unit(("res", Id(NullLit()))), [{"res": None}]),
+    ("null_type", "MTa/NullTests.scala:49", "", _unit(("res", Type(NullLit()))), [{"res": None}]),
+]
+CASES = CASES + EXPR_CASES

@@ -84,6 +84,81 @@ def test_sharded_two_hop_multiprocess(world, scale):
     assert sum(r[4] for r in res) == 16 << scale  # out-copies too
 
 
+def _spi_worker(rank, world, port, scale, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import traceback
+    import torch
+    import torch.distributed as dist
+    try:
+        import capf_import  # noqa: F401
+        from capf_amd.dist_table import DistSession, GpuExchange, dist_node_partitioned_graph
+        from capf_amd.expr import CountStar
+        from capf_amd.graph import ElementTable, ScanGraph
+        from capf_amd.planner import Match, NodeP, Query, RelP, Stage, run
+        from capf_amd.synthetic import rmat_seed, thresholds
+        from capf_amd.table import GpuSession
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        s = GpuSession.on_torch_stream(0)
+        n, m = 1 << scale, 16 << scale
+        rels = s.rmat_rels(scale, rmat_seed(scale), thresholds(), 0, m)
+        nodes = s.range_nodes(0, n, id_col="id")
+        full = ScanGraph(s, [ElementTable("node", frozenset(), nodes, {})],
+                         [ElementTable("rel", frozenset(["E"]), rels, {})])
+        ds = DistSession(s, GpuExchange(s))
+        g = dist_node_partitioned_graph(ds, full)
+        two = Query([Match([NodeP("a"), NodeP("b"), NodeP("c")], [RelP("r1", "a", "b"), RelP("r2", "b", "c")])],
+                    [Stage([("count", CountStar())])])
+        s.reset_profile()
+        s.set_profiling(True)
+        counts = [run(g, two)[0]["count"] for _ in range(3)]
+        s.sync()
+        s.set_profiling(False)
+        kernels = sorted(s.profile())
+        q.put((rank, counts, kernels))
+        dist.destroy_process_group()
+    except Exception:  # noqa: BLE001 - report, do not hang the parent
+        q.put((rank, traceback.format_exc(), None))
+
+
+@pytest.mark.parametrize("world,scale", [(2, 20), (3, 16)])
+def test_sharded_two_hop_through_spi_multiprocess(world, scale):
+    """MATCH (a)-->(b)-->(c) RETURN count(*) through the unchanged planner on
+    a node-partitioned DistTable graph (dist_table.dist_node_partitioned_graph):
+    DistTable.group(∅, count(*)) recognises the deferred join chain and runs
+    capf_chain2_sharded_count on each rank's copies + ONE all-reduce — the
+    c5_* kernels run, no rows move.  Every rank returns the fixture / closed
+    form, three queries in a row."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_spi_worker, args=(r, world, port, scale, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=100) for _ in procs]
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    with open(os.path.join(ROOT, "tests", "golden", "rmat_counts.json")) as f:
+        counts = json.load(f)
+    if str(scale) in counts["full"]:
+        expect = counts["full"][str(scale)]["two_hop"]
+    else:
+        from oracle import cmodel
+        expect = cmodel.stream_counts(scale)["two_hop"]
+    for rank, got, kernels in res:
+        assert kernels is not None, got
+        assert got == [expect] * 3, (rank, got, expect)
+        assert "c5_partition" in kernels and "c5_gather" in kernels, kernels
+        assert not any(k.startswith(("route", "pack_rows", "dense_probe", "rj_")) for k in kernels), kernels
+
+
 # ------------------------------------------------ distributed Table layer
 def test_hash_route_matches_numpy_router(gpu_session):
     """capf_table_hash_route (csrc/shuffle.hip) puts every row on the owner

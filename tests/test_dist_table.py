@@ -72,3 +72,79 @@ def test_reference_cases_distributed_on_oracle(world):
         p.join(timeout=60)
     for rank, bad, n in res:
         assert n > 100 and not bad, f"rank {rank}: {len(bad)} failing cases: {bad[:5]}"
+
+
+def _two_hop_worker(rank, world, port, q):
+    try:
+        sys.path[:0] = [ROOT, HERE, os.path.join(HERE, "golden")]
+        import capf_import  # noqa: F401
+        import numpy as np
+        from conftest import bag
+        from dist_support import OracleExchange, oracle_count_copies
+        from capf_amd.dist_table import DistSession, dist_node_partitioned_graph
+        from capf_amd.expr import CountStar, IntegerLit, LessThan, Var
+        from capf_amd.graph import GraphData, ScanGraph
+        from capf_amd.planner import Match, NodeP, Query, RelP, Stage, run
+        from oracle import cmodel
+        from oracle.table_np import OracleSession
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        scale = 8
+        src, dst = cmodel.rmat(scale)
+        n = 1 << scale
+        data = GraphData([(i + 5, frozenset(), {}) for i in range(n)],
+                         [(100000 + k, int(a) + 5, int(b) + 5, "E", {}) for k, (a, b) in enumerate(zip(src, dst))])
+        full = ScanGraph.from_data(OracleSession(), data)
+        ds = DistSession(OracleSession(), OracleExchange())
+        g = dist_node_partitioned_graph(ds, full, count_copies=oracle_count_copies)
+        two = Query([Match([NodeP("a"), NodeP("b"), NodeP("c")], [RelP("r1", "a", "b"), RelP("r2", "b", "c")])],
+                    [Stage([("count", CountStar())])])
+        got = run(g, two)[0]["count"]
+        # mirrored pattern (a)<--(b)<--(c): the same chain
+        back = Query([Match([NodeP("a"), NodeP("b"), NodeP("c")],
+                            [RelP("r1", "a", "b", direction="in"), RelP("r2", "b", "c", direction="in")])],
+                     [Stage([("count", CountStar())])])
+        got_back = run(g, back)[0]["count"]
+        dispatched = len(oracle_count_copies.calls)
+        # not the 2-hop count: the deferred operators replay eagerly (shuffles, joins)
+        rows = Query([Match([NodeP("a"), NodeP("b")], [RelP("r", "a", "b")])],
+                     [Stage([("a", Var("a")), ("b", Var("b"))])])
+        got_rows = run(g, rows)
+        one = run(g, Query([Match([NodeP("a"), NodeP("b")], [RelP("r", "a", "b")])],
+                           [Stage([("count", CountStar())])]))[0]["count"]
+        ref_rows = run(full, rows)
+        # a WHERE that is not a uniqueness filter: no sharded count, the chain replays
+        where = Query([Match([NodeP("a"), NodeP("b"), NodeP("c")], [RelP("r1", "a", "b"), RelP("r2", "b", "c")],
+                             where=[LessThan(Var("a"), IntegerLit(40))])],
+                      [Stage([("count", CountStar())])])
+        got3 = run(g, where)[0]["count"]
+        want3 = run(full, where)[0]["count"]
+        q.put((rank, got, got_back, dispatched, bag(got_rows) == bag(ref_rows), one, got3 == want3 > 0,
+               cmodel.count_2hop(src, dst, n), len(src)))
+        dist.destroy_process_group()
+    except Exception:  # noqa: BLE001
+        q.put((rank, traceback.format_exc()) + (None,) * 7)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_two_hop_through_spi(world):
+    """The 2-hop count(*) through the unchanged planner on a node-partitioned
+    DistTable graph: DistTable.group(∅, count(*)) sees the deferred join
+    chain, every rank adds its partial, one all-reduce sums them (no rows
+    shuffled); the mirrored pattern is the same chain; other queries on the
+    same graph replay the deferred operators eagerly and match the
+    single-process plan."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_two_hop_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, got, got_back, dispatched, rows_ok, one, three_ok, want, m in res:
+        assert isinstance(got, int), got
+        assert got == want and got_back == want, (rank, got, got_back, want)
+        assert dispatched == 2, dispatched  # both chains took the sharded count
+        assert rows_ok and one == m and three_ok

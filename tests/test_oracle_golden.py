@@ -53,34 +53,23 @@ def test_rmat_fixtures_reproduce():
     assert counts["full"]["24"]["two_hop"] == 1341721965791
 
 
-def test_avg_ints_type_is_checked():
-    """Negative self-test of the type-exact Bag on the reference's avg-of-
-    integers case (AggregationTests.scala:49-57, INTEGER avg per
-    Expr.scala:1058-1066): the oracle returns the INTEGER 4, and a FLOAT 4.0
-    would fail the comparison."""
-    cid, src, create, query, expected, _ = case_parts(next(c for c in CASES if c[0] == "avg_ints"))
+def test_avg_of_integers_is_float():
+    """avg over INTEGER values is a FLOAT: the reference's combination tests
+    compare it as CypherFloat(49.666666666666664) (AggregationTests.scala:852,
+    876) and 32.5 (:921); its avg(2, 4, 6) tests expect CypherMap("res" -> 4)
+    (:40-57), which a 4.0 result equals under the Bag's Scala Map equality
+    (CypherValue.scala:199-203, 301-302) — and only under it: a typed
+    comparison tells 4 from 4.0."""
+    cid, src, create, query, expected, opts = case_parts(next(c for c in CASES if c[0] == "avg_ints"))
     got = run(ScanGraph.from_data(OracleSession(), parse_create(create)), query)
-    assert bag(got) == bag(expected)
-    assert type(got[0]["res"]) is int
-    assert bag([{"res": 4.0}]) != bag(expected)
-
-
-def test_deviations_are_only_integer_avg():
-    """Cases whose expected rows differ from the reference test's own values
-    ("deviates") differ only in avg over INTEGER values (okapi
-    types avg as its input, Expr.scala:1058-1066; the reference tests expect a
-    FLOAT there): the field is an avg aggregate and the oracle's value is an int."""
-    from capf_amd.expr import Avg
-    for case in CASES:
-        cid, src, create, query, expected, opts = case_parts(case)
-        dev = opts.get("deviates")
-        if not dev:
-            continue
-        items = dict(query.stages[0].items)
-        got = run(ScanGraph.from_data(OracleSession(), parse_create(create)), query)
-        for field in dev:
-            assert isinstance(items[field], Avg), (cid, field)
-            assert all(type(r[field]) is int for r in got), (cid, field, got)
+    assert type(got[0]["res"]) is float and got[0]["res"] == 4.0
+    assert check_case(got, expected, opts)
+    assert not check_case(got, expected, opts, reference=False)
+    cid, src, create, query, expected, opts = case_parts(next(c for c in CASES if c[0] == "comb_return"))
+    got = run(ScanGraph.from_data(OracleSession(), parse_create(create)), query)
+    assert got[0]["avg"] == 49.666666666666664 and opts.get("typed")
+    assert check_case(got, expected, opts)
+    assert not check_case([{**got[0], "avg": 49}], expected, opts)
 
 
 @pytest.mark.parametrize("agg", ["StDev", "StDevP", "PercentileCont", "PercentileDisc"])

@@ -537,6 +537,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_packed(const uint32_t *
 // N+(q).  Σ min(|N+(p)|, |N+(q)|) over the edges is ~2.2× below the one-pass
 // Σ |N+(q)| on R-MAT (s18 / s20).
 constexpr uint32_t TRI_BCHUNK = 1024;
+constexpr int TRI_QTILE_DEFAULT = 0;  // pass-A tile size (log2 words); 0 = row by row
 
 struct TriPassB {
   const uint32_t *in_words;   // p | multiplicity nibbles of the pair p–q, by (p-block, q, p)
@@ -677,6 +678,10 @@ struct TriGraph {
   // two-pass schedule (pass B: edges with |N+(p)| < |N+(q)| counted at q)
   BufPtr in_words, in_eidx, items;
   uint32_t nB = 0, nitems = 0;
+  // q-tiled pass A: work items (p, k0, k1) sorted by (tile of N+(q)'s position, p)
+  BufPtr aitems;
+  uint32_t naitems = 0;
+  int qshift = 0;  // log2 of the pcols words per tile (0: pass A row by row)
   uint32_t P = 0;
   uint64_t len = 0;
 };
@@ -752,6 +757,135 @@ static void tri_build_passb(Session *s, const uint64_t *okey, TriGraph &g) {
                      (const uint64_t *)useg->p, (const uint32_t *)cnt->p, (const uint32_t *)start->p,
                      (const uint32_t *)istart->p, nseg, (uint4 *)g.items->p);
   KERNEL_CHECK();
+  s->sync();  // the temporaries go back to the pool
+}
+
+// Pass A over q-tiled work items (see tri_build_qtiles): item (p, k0, k1) probes
+// the q's N+(p)[k0, k1) — N+(p) staged in LDS (≤ TRI_CAP words) or searched in
+// place — with the pass-A rule (edges with |N+(p)| < |N+(q)| belong to pass B).
+template <int ILP>
+__global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_qtiled(const uint32_t *rowptr, const uint32_t *pcols,
+                                                                 const uint2 *vals, const uint4 *items,
+                                                                 uint32_t nitems, int parts, int part,
+                                                                 unsigned long long *cursor,
+                                                                 unsigned long long *acc) {
+  __shared__ uint32_t s_cols[TRI_BLOCK / WAVE][TRI_CAP];
+  __shared__ TriBatch2 s_tab[TRI_BLOCK / WAVE];
+  __shared__ unsigned long long lds[17];
+  const int wv = threadIdx.x / WAVE, lane = lane_id();
+  uint32_t *sc = s_cols[wv];
+  TriBatch2 &tb = s_tab[wv];
+  unsigned long long t = 0, probes = 0, hits = 0;
+  uint32_t staged = 0xFFFFFFFFu;  // p whose list sits in sc
+  for (;;) {
+    unsigned long long c0 = 0;
+    if (lane == 0) c0 = atomicAdd(cursor, 1ull);
+    c0 = ((unsigned long long)__shfl((long long)c0, 0, WAVE) * parts + part) * 4;
+    if (c0 >= nitems) break;
+    const uint64_t c1 = min<uint64_t>(c0 + 4, nitems);
+    for (uint64_t it = c0; it < c1; ++it) {
+      const uint4 item = items[it];
+      const uint32_t p = item.x, k0 = item.y, nb = item.z - item.y;
+      const uint32_t a = rowptr[p], dp = rowptr[p + 1] - a;
+      if (dp > TRI_CAP) {  // long N+(p): searched in global memory
+        const uint32_t *row = pcols + a;
+        tri_row_packed<ILP, true>(a, nb, dp, rowptr, pcols, vals, tb, [&](uint32_t k) { return row[k0 + k]; },
+                                  [&](uint32_t x) { return row[x]; }, [&](uint32_t k) { return a + k0 + k; }, t,
+                                  probes, hits);
+        staged = 0xFFFFFFFFu;
+        continue;
+      }
+      if (p != staged) {
+        __builtin_amdgcn_wave_barrier();  // the previous list's searches are done
+        for (uint32_t k = lane; k < dp; k += WAVE) sc[k] = pcols[a + k];
+        __builtin_amdgcn_wave_barrier();
+        staged = p;
+      }
+      tri_row_packed<ILP, true>(a, nb, dp, rowptr, pcols, vals, tb, [&](uint32_t k) { return sc[k0 + k]; },
+                                [&](uint32_t x) { return sc[x]; }, [&](uint32_t k) { return a + k0 + k; }, t,
+                                probes, hits);
+    }
+  }
+  unsigned long long tot;
+  block_exclusive_scan(t, lds, tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(&acc[0], tot);
+  block_exclusive_scan(probes, lds, tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(&acc[4], tot);
+  block_exclusive_scan(hits, lds, tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(&acc[5], tot);
+}
+
+// ------------------------------------------------------ q-tiled pass A
+// Pass A streams N+(q) for the q's of each row p.  Row by row those lists lie
+// anywhere in the 1 GB column array (s24), so nearly every streamed word is an
+// L2 miss.  Tiled: the column array is cut into tiles of 2^qshift words; the
+// work item (p, k0, k1) is the run of N+(p) whose q's lists START in one tile
+// (tile(q) = rowptr[q] >> qshift is monotone along the sorted N+(p)), and the
+// items are processed in (tile, p) order — all waves of the chip stream lists
+// from one tile at a time, a region the caches hold, while N+(p) is staged once
+// per (p, tile).
+
+// head of an item: the first edge of a row, or the first whose q's tile differs
+// from the previous edge's; key (tile << 32 | p), value = edge index
+__global__ void k_tri_qtile_heads(const uint64_t *okey, const uint32_t *rowptr, uint32_t P, int qshift,
+                                  uint64_t *keys, uint32_t *eidx) {
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < P; e += gridDim.x * blockDim.x) {
+    const uint64_t k = okey[e];
+    const uint32_t p = (uint32_t)(k >> 32), q = (uint32_t)k;
+    const uint32_t a = rowptr[p], dp = rowptr[p + 1] - a;
+    const uint32_t t = rowptr[q] >> qshift;
+    bool head = dp >= 2;
+    if (head && e > a) head = (rowptr[(uint32_t)okey[e - 1]] >> qshift) != t;
+    keys[e] = head ? ((uint64_t)t << 32 | p) : TRI_NONE;
+    eidx[e] = e;
+  }
+}
+
+// items (p, k0, k1): k1 = the end of the head's tile run inside the row
+// (binary search: tile(q) is monotone along the row)
+__global__ void k_tri_qtile_items(const uint64_t *skeys, const uint32_t *seidx, uint32_t n,
+                                  const uint64_t *okey, const uint32_t *rowptr, int qshift, uint4 *items) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t e = seidx[i];
+    const uint32_t p = (uint32_t)(skeys[i] & 0xFFFFFFFFu), t = (uint32_t)(skeys[i] >> 32);
+    const uint32_t a = rowptr[p], end = rowptr[p + 1];
+    uint32_t lo = e + 1, hi = end;  // first edge of the row whose tile is > t
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if ((rowptr[(uint32_t)okey[mid]] >> qshift) <= t) lo = mid + 1;
+      else hi = mid;
+    }
+    items[i] = make_uint4(p, e - a, lo - a, 0u);
+  }
+}
+
+static void tri_build_qtiles(Session *s, const uint64_t *okey, TriGraph &g, int qshift) {
+  const uint32_t P = g.P;
+  KernelTimer kt(s, "tri_qtile_build", 24.0 * P);
+  BufPtr keys = s->alloc(8 * (int64_t)P), skeys = s->alloc(8 * (int64_t)P);
+  BufPtr eidx = s->alloc(4 * (int64_t)P), seidx = s->alloc(4 * (int64_t)P);
+  hipLaunchKernelGGL(k_tri_qtile_heads, dim3(grid_for(P, 256, 256 * 64)), dim3(256), 0, s->stream, okey,
+                     (const uint32_t *)g.rowptr->p, P, qshift, (uint64_t *)keys->p, (uint32_t *)eidx->p);
+  KERNEL_CHECK();
+  rocprim_call(s, [&](void *t, size_t &n) {
+    return rocprim::radix_sort_pairs(t, n, (const uint64_t *)keys->p, (uint64_t *)skeys->p,
+                                     (const uint32_t *)eidx->p, (uint32_t *)seidx->p, (size_t)P, 0, 64,
+                                     s->stream);
+  });
+  BufPtr nb = s->alloc(16);
+  hipLaunchKernelGGL(k_tri_count_below, dim3(1), dim3(64), 0, s->stream, (const uint64_t *)skeys->p, P,
+                     (uint32_t *)nb->p);
+  KERNEL_CHECK();
+  HIP_CHECK(hipMemcpyAsync(&g.naitems, nb->p, 4, hipMemcpyDeviceToHost, s->stream));
+  s->sync();
+  g.aitems = s->alloc(16 * std::max<uint32_t>(g.naitems, 1));
+  if (g.naitems > 0) {
+    hipLaunchKernelGGL(k_tri_qtile_items, dim3(grid_for(g.naitems, 256, 256 * 64)), dim3(256), 0, s->stream,
+                       (const uint64_t *)skeys->p, (const uint32_t *)seidx->p, g.naitems, okey,
+                       (const uint32_t *)g.rowptr->p, qshift, (uint4 *)g.aitems->p);
+    KERNEL_CHECK();
+  }
+  g.qshift = qshift;
   s->sync();  // the temporaries go back to the pool
 }
 
@@ -868,6 +1002,10 @@ static void tri_build(Session *s, const ColView &src, const ColView &dst, int64_
                        (const uint32_t *)g.cols->p, (const uint2 *)g.vals->p, g.P, (uint32_t *)g.pcols->p);
     KERNEL_CHECK();
     tri_build_passb(s, (const uint64_t *)ok2->p, g);
+    // CAPF_TRI_QTILE (tuning): log2 of the words per pass-A tile; 0 = row by row
+    const char *qt = getenv("CAPF_TRI_QTILE");
+    const int qshift = qt ? atoi(qt) : TRI_QTILE_DEFAULT;
+    if (qshift > 0 && g.in_words) tri_build_qtiles(s, (const uint64_t *)ok2->p, g, std::max(12, std::min(30, qshift)));
   }
 }
 
@@ -922,11 +1060,21 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
     // CAPF_TRI_TWOPASS=0 (tuning): one pass, every wedge streamed from N+(q)
     const bool two = packed && g.pcols && g.in_words && !(getenv("CAPF_TRI_TWOPASS") && atoi(getenv("CAPF_TRI_TWOPASS")) == 0);
     if (packed && g.pcols) {
-      auto kern = two ? (ilp <= 2 ? k_tri_count_packed<2, true> : k_tri_count_packed<4, true>)
-                      : (ilp >= 8 ? k_tri_count_packed<8> : ilp <= 2 ? k_tri_count_packed<2> : k_tri_count_packed<4>);
-      hipLaunchKernelGGL(kern, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
-                         (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
-                         (const uint2 *)g.vals->p, len, parts, part, acc + 3, acc);
+      if (two && g.qshift > 0) {
+        if (g.naitems > 0) {
+          auto kq = ilp <= 2 ? k_tri_count_qtiled<2> : k_tri_count_qtiled<4>;
+          hipLaunchKernelGGL(kq, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
+                             (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
+                             (const uint2 *)g.vals->p, (const uint4 *)g.aitems->p, g.naitems, parts, part,
+                             acc + 3, acc);
+        }
+      } else {
+        auto kern = two ? (ilp <= 2 ? k_tri_count_packed<2, true> : k_tri_count_packed<4, true>)
+                        : (ilp >= 8 ? k_tri_count_packed<8> : ilp <= 2 ? k_tri_count_packed<2> : k_tri_count_packed<4>);
+        hipLaunchKernelGGL(kern, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
+                           (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
+                           (const uint2 *)g.vals->p, len, parts, part, acc + 3, acc);
+      }
       if (two && g.nitems > 0) {
         TriPassB b{(const uint32_t *)g.in_words->p, (const uint32_t *)g.in_eidx->p, (const uint4 *)g.items->p,
                    g.nitems};

@@ -776,6 +776,29 @@ def test_triangle_heavy_multi_edges(gpu_session, monkeypatch, packed):
     assert got == cmodel.count_triangle_brute(src, dst, n) == cmodel.count_triangle_formula(src, dst, n)
 
 
+@pytest.mark.parametrize("qtile", ["12", "14", "18"])
+@pytest.mark.parametrize("scale", [10, 13])
+def test_triangle_qtiled(gpu_session, monkeypatch, qtile, scale):
+    """Pass A over q-tiled work items (CAPF_TRI_QTILE = log2 words per tile;
+    small tiles cut most rows into several items, some rows longer than the
+    LDS copy) gives the trace(A^3) count, alone and as 3 parts."""
+    import torch
+    from capf_amd.table import triangle_count_part_async
+    monkeypatch.setenv("CAPF_TRI_QTILE", qtile)
+    g = rmat_graph(gpu_session, scale, compact=True)
+    got = run(g, _triangle_query())[0]["count"]
+    assert gpu_session.last_plan() == "fused_triangle"
+    src, dst = cmodel.rmat(scale)
+    want = cmodel.count_triangle_formula(src, dst, 1 << scale)
+    assert got == want
+    t = gpu_session.rmat_rels(scale, cmodel.rmat_seed(scale), cmodel.thresholds(), 0, 16 << scale)
+    d = torch.zeros(3, dtype=torch.int64, device="cuda")
+    for p in range(3):
+        triangle_count_part_async(gpu_session, t, 0, 1 << scale, 3, p, d.data_ptr() + 8 * p)
+    gpu_session.sync()
+    assert int(d.sum().item()) == want
+
+
 @pytest.mark.parametrize("parts", [1, 2, 3, 5])
 def test_triangle_partials_sum(gpu_session, parts):
     """capf_triangle_count_part: the parts (row chunks dealt round-robin, loop

@@ -18,11 +18,12 @@ def owner_of(e):
 
 
 class RecordHeader:
-    __slots__ = ("_m", "_cols")
+    __slots__ = ("_m", "_cols", "_cset")
 
     def __init__(self, mapping=None):
         self._m = dict(mapping) if mapping else {}
         self._cols = None
+        self._cset = None
 
     # dict-like access used by expression lowering
     def get(self, expr, default=None):
@@ -55,9 +56,12 @@ class RecordHeader:
 
     def column_set(self):
         """The distinct physical columns as a set (planner renaming checks)."""
-        if self._cols is None:
-            self._cols = list(dict.fromkeys(self._m.values()))
-        return set(self._cols)
+        return set(self.column_frozenset())
+
+    def column_frozenset(self):
+        if self._cset is None:  # immutable: computed once
+            self._cset = frozenset(self._m.values())
+        return self._cset
 
     def owned_by(self, var):
         return [e for e in self._m if e == var or owner_of(e) == var]
@@ -82,6 +86,7 @@ class RecordHeader:
         h = RecordHeader.__new__(RecordHeader)
         h._m = m
         h._cols = None
+        h._cset = None
         return h
 
     def without(self, exprs):

@@ -79,9 +79,14 @@ class Query:
 # ------------------------------------------------------------- relational ops
 def _rename_disjoint(left: Planned, right: Planned) -> Planned:
     """withDisjointColumnNames (RelationalPlanner.scala:366-368, 524-538)."""
-    lcols = left.header.column_set()
-    lcols.update(left.table.physicalColumns)
     rcols = right.table.physicalColumns
+    hcols = left.header.column_frozenset()
+    tcols = left.table.physicalColumns
+    if hcols.isdisjoint(rcols) and (len(tcols) <= len(hcols) and hcols.issuperset(tcols)
+                                    or set(tcols).isdisjoint(rcols)):
+        return right
+    lcols = set(hcols)
+    lcols.update(tcols)
     clash = [c for c in rcols if c in lcols]
     if not clash:
         return right

@@ -49,6 +49,14 @@ bool fail(JNIEnv *env, capf_status st) {
   return true;
 }
 
+// an IllegalArgumentException (okapi's IllegalArgumentException is thrown by the
+// Scala side from it) — for argument arrays whose lengths disagree
+bool illegal_argument(JNIEnv *env, const char *msg) {
+  jclass cls = env->FindClass("java/lang/IllegalArgumentException");
+  if (cls) env->ThrowNew(cls, msg);
+  return true;
+}
+
 capf_session *S(jlong h) { return reinterpret_cast<capf_session *>(h); }
 capf_table *T(jlong h) { return reinterpret_cast<capf_table *>(h); }
 jlong H(capf_table *t) { return reinterpret_cast<jlong>(t); }
@@ -629,6 +637,10 @@ JNI(jint, tablePackRows)(JNIEnv *env, jobject, jlong t, jobjectArray cols, jintA
   JStrs c(env, cols);
   std::vector<int32_t> w = ints(env, width), nl = ints(env, nullable);
   std::vector<int64_t> b = longs(env, base);
+  if ((int64_t)w.size() != c.n() || (int64_t)b.size() != c.n() || (int64_t)nl.size() != c.n()) {
+    illegal_argument(env, "tablePackRows: width, base and nullable need one entry per column");
+    return 0;
+  }
   int32_t W = 0;
   fail(env, capf_table_pack_rows(T(t), c.n(), c.data(), w.data(), b.data(), nl.data(), &W,
                                  reinterpret_cast<void *>(d_out)));
@@ -639,6 +651,11 @@ JNI(jlong, tableFromPackedRows)(JNIEnv *env, jobject, jlong s, jobjectArray name
   JStrs nm(env, names);
   std::vector<int32_t> ty = ints(env, types), w = ints(env, width), nl = ints(env, nullable);
   std::vector<int64_t> b = longs(env, base);
+  if ((int64_t)ty.size() != nm.n() || (int64_t)w.size() != nm.n() || (int64_t)b.size() != nm.n() ||
+      (int64_t)nl.size() != nm.n()) {
+    illegal_argument(env, "tableFromPackedRows: types, width, base and nullable need one entry per column");
+    return 0;
+  }
   capf_table *out = nullptr;
   if (fail(env, capf_table_from_packed_rows(S(s), nm.n(), nm.data(), ty.data(), w.data(), b.data(), nl.data(),
                                             reinterpret_cast<const void *>(d_rows), nrows, &out)))

@@ -49,6 +49,7 @@ struct JNIEnv {
   jobject GetObjectField(jobject obj, jfieldID field);
   jobject NewObject(jclass clazz, jmethodID ctor, ...);
   jint Throw(jthrowable obj);
+  jint ThrowNew(jclass clazz, const char *message);
   jstring NewStringUTF(const char *utf);
   const char *GetStringUTFChars(jstring str, jboolean *is_copy);
   void ReleaseStringUTFChars(jstring str, const char *chars);

@@ -155,8 +155,9 @@ def test_sharded_two_hop_through_spi_multiprocess(world, scale):
     for rank, got, kernels in res:
         assert kernels is not None, got
         assert got == [expect] * 3, (rank, got, expect)
-        assert "c5_partition" in kernels and "c5_gather" in kernels, kernels
         assert not any(k.startswith(("route", "pack_rows", "dense_probe", "rj_")) for k in kernels), kernels
+    # a rank owning no node_mix bucket (s16 has one bucket of 2^16 keys) launches nothing
+    assert any("c5_partition" in k and "c5_gather" in k for _, _, k in res), [k for _, _, k in res]
 
 
 # ------------------------------------------------ distributed Table layer

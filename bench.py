@@ -185,12 +185,12 @@ PIPELINE = ("c5_partition", "c3_transpose", "c3_units", "c3_zero", "c5_gather", 
             "semi_partition", "semi_count",
             "chain2_dot", "tri_keys", "tri_sort_keys", "tri_rle", "tri_pairs", "tri_orient",
             "tri_sort_pairs", "tri_rowptr", "tri_split", "tri_loop3", "tri_count", "tri_count_packed",
+            "tri_count_qtiled", "tri_count_passb",
             "rj_partition1", "rj_partition2", "rj_join_count", "rj_join_emit", "gather")
 
 # kernel symbols behind a timer label (the default is "k_" + label); PMC files are
 # matched against these, template arguments stripped
 PMC_SYMBOLS = {"chain2_dot": ("k_chain2_dot", "k_chain2_dot_pairs"),
-               "tri_count_packed": ("k_tri_count_packed", "k_tri_count_passb"),
                "semi_partition": ("k_c5_shard_partition",), "semi_count": ("k_c5_bits_count",)}
 
 
@@ -261,8 +261,9 @@ def tri_roofline(prof, steps, n_nodes, traffic_per_query=None):
     probes = prof.get("tri_probes", {}).get("bytes", 0.0) / steps
     hits = prof.get("tri_hits", {}).get("bytes", 0.0) / steps
     edges = prof.get("tri_oriented_edges", {}).get("bytes", 0.0) / steps
-    lab = "tri_count_packed" if "tri_count_packed" in per else "tri_count"
-    t = per.get(lab, 0.0)
+    labs = [k for k in per if k.startswith("tri_count")]  # pass A (row by row or q-tiled) + pass B
+    lab = " + ".join(sorted(labs)) or "tri_count"
+    t = sum(per[k] for k in labs)
     algo = 4.0 * probes + 16.0 * hits + 20.0 * edges + 8.0 * n_nodes
     achieved = algo / (t * 1e-3) / 1e9 if t > 0 else None
     return {

@@ -1052,9 +1052,8 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
   if (g.P > 0) {
     // CAPF_TRI_PACKED=0 (tuning): the unpacked kernel (multiplicities loaded from vals per hit)
     const bool packed = !(getenv("CAPF_TRI_PACKED") && atoi(getenv("CAPF_TRI_PACKED")) == 0);
-    // the timer is named after the kernel that runs (bench.py matches it against the
+    // timers are named after the kernels that run (bench.py matches them against the
     // kernel names of the committed PMC counters)
-    KernelTimer kt(s, packed && g.pcols ? "tri_count_packed" : "tri_count", 4.0 * g.P);
     static const bool filter = getenv("CAPF_TRI_FILTER") && atoi(getenv("CAPF_TRI_FILTER")) == 1;  // measured slower (0.98 vs 0.94 s at s24)
     static const int ilp = getenv("CAPF_TRI_ILP") ? atoi(getenv("CAPF_TRI_ILP")) : TRI_ILP;  // tuning
     // CAPF_TRI_TWOPASS=0 (tuning): one pass, every wedge streamed from N+(q)
@@ -1062,6 +1061,7 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
     if (packed && g.pcols) {
       if (two && g.qshift > 0) {
         if (g.naitems > 0) {
+          KernelTimer kt(s, "tri_count_qtiled", 4.0 * g.P);
           auto kq = ilp <= 2 ? k_tri_count_qtiled<2> : k_tri_count_qtiled<4>;
           hipLaunchKernelGGL(kq, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
                              (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
@@ -1069,6 +1069,7 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
                              acc + 3, acc);
         }
       } else {
+        KernelTimer kt(s, "tri_count_packed", 4.0 * g.P);
         auto kern = two ? (ilp <= 2 ? k_tri_count_packed<2, true> : k_tri_count_packed<4, true>)
                         : (ilp >= 8 ? k_tri_count_packed<8> : ilp <= 2 ? k_tri_count_packed<2> : k_tri_count_packed<4>);
         hipLaunchKernelGGL(kern, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
@@ -1076,6 +1077,7 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
                            (const uint2 *)g.vals->p, len, parts, part, acc + 3, acc);
       }
       if (two && g.nitems > 0) {
+        KernelTimer kt(s, "tri_count_passb", 4.0 * g.P);
         TriPassB b{(const uint32_t *)g.in_words->p, (const uint32_t *)g.in_eidx->p, (const uint4 *)g.items->p,
                    g.nitems};
         auto kb = ilp <= 2 ? k_tri_count_passb<2> : k_tri_count_passb<4>;
@@ -1084,6 +1086,7 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
                            b, parts, part, acc + 6, acc);
       }
     } else {
+      KernelTimer kt(s, "tri_count", 4.0 * g.P);
       auto kern = filter ? (ilp >= 8 ? k_tri_count<true, 8> : ilp <= 2 ? k_tri_count<true, 2> : k_tri_count<true, 4>)
                          : (ilp >= 8 ? k_tri_count<false, 8> : ilp <= 2 ? k_tri_count<false, 2> : k_tri_count<false, 4>);
       hipLaunchKernelGGL(kern, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,

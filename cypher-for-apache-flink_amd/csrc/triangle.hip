@@ -537,7 +537,9 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_packed(const uint32_t *
 // N+(q).  Σ min(|N+(p)|, |N+(q)|) over the edges is ~2.2× below the one-pass
 // Σ |N+(q)| on R-MAT (s18 / s20).
 constexpr uint32_t TRI_BCHUNK = 1024;
-constexpr int TRI_QTILE_DEFAULT = 0;  // pass-A tile size (log2 words); 0 = row by row
+// pass-A tile size (log2 words; 0 = row by row).  s24 (profiles/r04_tri_sweep.txt):
+// row by row 350 ms, 2^23 268, 2^24 220, 2^25 190, 2^26 184 ms
+constexpr int TRI_QTILE_DEFAULT = 26;
 
 struct TriPassB {
   const uint32_t *in_words;   // p | multiplicity nibbles of the pair p–q, by (p-block, q, p)
@@ -693,7 +695,8 @@ static void tri_build_passb(Session *s, const uint64_t *okey, TriGraph &g) {
   // CAPF_TRI_PBLOCK (tuning): log2 of the N+(p) words per p-block (default 2^24 = 64 MB)
   const char *pb = getenv("CAPF_TRI_PBLOCK");
   // ≥ 16: the pass-B key holds the p-block id (ap >> pshift, ap < 2^32) in 16 bits at bit 48
-  const int pshift = pb ? std::max(16, std::min(31, atoi(pb))) : 24;
+  // s24: 2^22 355 ms, 2^23 338, 2^24 333, 2^25 326 (pass B)
+  const int pshift = pb ? std::max(16, std::min(31, atoi(pb))) : 25;
   BufPtr keys = s->alloc(8 * (int64_t)P), skeys = s->alloc(8 * (int64_t)P);
   BufPtr eidx = s->alloc(4 * (int64_t)P), seidx = s->alloc(4 * (int64_t)P);
   hipLaunchKernelGGL(k_tri_passb_keys, dim3(grid_for(P, 256, 256 * 64)), dim3(256), 0, s->stream, okey,
@@ -1075,6 +1078,12 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
         hipLaunchKernelGGL(kern, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
                            (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
                            (const uint2 *)g.vals->p, len, parts, part, acc + 3, acc);
+      }
+      if (s->profiling) {  // diagnostics (profiling mode only, host sync): pass A's probes
+        unsigned long long pa = 0;
+        HIP_CHECK(hipMemcpyAsync(&pa, acc + 4, 8, hipMemcpyDeviceToHost, s->stream));
+        s->sync();
+        s->profile["tri_probes_pass_a"].bytes += (double)pa;
       }
       if (two && g.nitems > 0) {
         KernelTimer kt(s, "tri_count_passb", 4.0 * g.P);

@@ -776,10 +776,10 @@ def test_triangle_heavy_multi_edges(gpu_session, monkeypatch, packed):
     assert got == cmodel.count_triangle_brute(src, dst, n) == cmodel.count_triangle_formula(src, dst, n)
 
 
-@pytest.mark.parametrize("qtile", ["12", "14", "18"])
+@pytest.mark.parametrize("qtile", ["0", "12", "14", "18"])
 @pytest.mark.parametrize("scale", [10, 13])
 def test_triangle_qtiled(gpu_session, monkeypatch, qtile, scale):
-    """Pass A over q-tiled work items (CAPF_TRI_QTILE = log2 words per tile;
+    """Pass A over q-tiled work items (CAPF_TRI_QTILE = log2 words per tile, 0 = row by row;
     small tiles cut most rows into several items, some rows longer than the
     LDS copy) gives the trace(A^3) count, alone and as 3 parts."""
     import torch

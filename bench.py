@@ -139,6 +139,22 @@ def cpu_info(threads):
             "cap_reason": "one GPU's share of the box's CPUs (OMP_NUM_THREADS=16 on the GPU box)"}
 
 
+def tri_cpu_baseline(scale):
+    """Config 4 on the host cores: the oracle's trace(A^3) count by sorted-list
+    intersection (oracle/rmat.c, threads) over a bounded sample — the same
+    R-MAT generator 4 scales down (1/16 of the rels; ~20 s on 8 threads)."""
+    from oracle import cmodel
+    sc = max(8, scale - 4)
+    src, dst = cmodel.rmat(sc)
+    th = cpu_threads()
+    t0 = time.perf_counter()
+    c = cmodel.count_triangle_trace(src, dst, 1 << sc, threads=th)
+    el = time.perf_counter() - t0
+    return {"value": c / el, "unit": "joined rows/s", "cores": th, **cpu_info(th), "kind": "port",
+            "sample": (f"R-MAT s{sc} (same generator, 1/16 of the s{scale} rels): triangle count {c} by "
+                       f"sorted-list intersection (oracle/rmat.c count_triangle_trace) in {el:.2f}s on {th} threads")}
+
+
 def cpu_baseline(session, graph, scale, budget_s):
     """Flink-shaped pipelined hash join (oracle/rmat.c) on the host cores over
     a bounded sample of the same workload: hash tables are built on the full
@@ -260,6 +276,7 @@ def tri_roofline(prof, steps, n_nodes, traffic_per_query=None):
     per = {k: v["total_ms"] / steps for k, v in prof.items() if k in PIPELINE}
     probes = prof.get("tri_probes", {}).get("bytes", 0.0) / steps
     hits = prof.get("tri_hits", {}).get("bytes", 0.0) / steps
+    probes_a = prof.get("tri_probes_pass_a", {}).get("bytes", 0.0) / steps
     edges = prof.get("tri_oriented_edges", {}).get("bytes", 0.0) / steps
     labs = [k for k in per if k.startswith("tri_count")]  # pass A (row by row or q-tiled) + pass B
     lab = " + ".join(sorted(labs)) or "tri_count"
@@ -272,6 +289,9 @@ def tri_roofline(prof, steps, n_nodes, traffic_per_query=None):
         "frac": achieved / HBM_PEAK_GBS if achieved else None,
         "traffic": traffic_per_query, "algorithmic_bytes_per_launch": algo,
         "probes_per_launch": probes, "hits_per_launch": hits, "oriented_edges": edges,
+        "probes_pass_a": probes_a, "probes_pass_b": probes - probes_a,
+        "passb_edges": prof.get("tri_passb_edges", {}).get("bytes", 0.0) / steps,
+        "passa_items": prof.get("tri_passa_items", {}).get("bytes", 0.0) / steps,
         "probes_per_s": probes / (t * 1e-3) if t > 0 else None,
         "kernel_ms": t, "pipeline_ms_per_query": sum(per.values()), "kernel_ms_per_query": per,
         "note": "compulsory 16·M + 8·N bytes are not meaningful for config 4 (SURVEY §8(d)); "
@@ -623,6 +643,8 @@ def run_single(args):
     result["config"]["parity"] = check_fixture(args, count)
     if not args.no_cpu and args.query == "two_hop":
         result["cpu_baseline"] = cpu_baseline(s, g, args.scale, args.cpu_seconds)
+    if not args.no_cpu and args.query == "triangle":
+        result["cpu_baseline"] = tri_cpu_baseline(args.scale)
     print(json.dumps(result))
 
 

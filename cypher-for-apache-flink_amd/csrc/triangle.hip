@@ -203,7 +203,7 @@ constexpr int TRI_BLOCK = 256;
 #endif
 constexpr int TRI_CAP = CAPF_TRI_CAP;  // N+(p) staged in LDS up to this many entries
 constexpr int TRI_CHUNK = 16;  // rows per cursor grab
-constexpr int TRI_ILP = 4;     // N+(q) entries per lane in flight
+constexpr int TRI_ILP = 3;     // N+(q) entries per lane in flight (s24: ILP 2 333 ms, 3 314, 4 322)
 
 // Index of w in the ascending a(0..n), or −1.
 template <class A>
@@ -372,7 +372,9 @@ constexpr uint32_t TRI_M24 = 0xFFFFFFu;
 __global__ void k_tri_pack(const uint32_t *cols, const uint2 *vals, uint32_t P, uint32_t *pcols) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < P; i += gridDim.x * blockDim.x) {
     const uint2 v = vals[i];
-    const uint32_t f = min(v.x, 15u), b = min(v.y, 15u);
+    // f = 15 sends every reader to vals, so b is then left 0: no word equals
+    // 0xFFFFFFFF (id 2^24 − 1 saturated both ways), the kernels' end marker
+    const uint32_t f = min(v.x, 15u), b = f == 15u ? 0u : min(v.y, 15u);
     pcols[i] = cols[i] | f << 24 | b << 28;
   }
 }
@@ -381,8 +383,16 @@ struct TriBatch2 {
   uint32_t pre[WAVE + 1];  // exclusive prefix of the batch's |N+(q)|, + total
   uint32_t qa[WAVE];       // N+(q) start in pcols
   uint32_t pk[WAVE];       // packed word of q in N+(p) (multiplicities of p–q)
-  uint32_t kk[WAVE];       // k: q's position in N+(p)
+  uint32_t kk[WAVE];       // k: the batch entry (pqe(k): vals index of p–q, read on escape only)
 };
+
+// packed word's multiplicity nibbles say "look the pair up in vals"
+__device__ inline bool tri_esc(uint32_t word) { return ((word >> 24) & 15u) == 15u || (word >> 28) == 15u; }
+
+// CAPF_TRI_DIAG (profiling only, wrong counts): 1 = the streamed words are
+// loaded but not searched, 2 = searched but not loaded (a synthetic id per
+// position) — the time split of the count kernels between loads and searches
+__constant__ int c_tri_diag;
 
 // (f, b) of a packed word, or of vals[e] when a nibble says "look it up"
 __device__ inline uint2 tri_fb(uint32_t word, const uint2 *vals, uint32_t e) {
@@ -398,11 +408,14 @@ __device__ inline uint2 tri_fb(uint32_t word, const uint2 *vals, uint32_t e) {
 // belong to pass B and are skipped here.  SWAP (pass B): the staged list is
 // N+(q) and the streamed lists are N+(p) of q's in-list entries — the roles
 // of the two looked-up words swap in the weight.  `pqe(k)`: the vals index of
-// the k-th batch entry's p–q pair (for a saturated nibble).
-// nb batch entries (qs), the staged list fnd holds ns words at vals index a.
+// the k-th batch entry's p–q pair (for a saturated nibble).  `qrow(k)`: the
+// k-th entry's streamed list as {start in pcols, length | p–q nibbles << 24}.
+// nb batch entries; the staged list of ns words is searched by `find`
+// (wk → found, its packed word pw, and — when pw's nibbles say "look it up" —
+// its vals index pos).
 template <int ILP, bool SPLIT = false, bool SWAP = false, class Q, class F, class E>
-__device__ inline void tri_row_packed(uint32_t a, uint32_t nb, uint32_t ns, const uint32_t *rowptr,
-                                      const uint32_t *pcols, const uint2 *vals, TriBatch2 &tb, Q qs, F fnd,
+__device__ inline void tri_row_packed(uint32_t nb, uint32_t ns, const uint32_t *pcols, const uint2 *vals,
+                                      TriBatch2 &tb, Q qrow, F find,
                                       E pqe, unsigned long long &t, unsigned long long &probes,
                                       unsigned long long &hits) {
   const int lane = lane_id();
@@ -412,10 +425,10 @@ __device__ inline void tri_row_packed(uint32_t a, uint32_t nb, uint32_t ns, cons
     const uint32_t k = kb + lane;
     uint32_t qa = 0, dq = 0, pk = 0;
     if (k < nb) {
-      pk = qs(k);
-      const uint32_t q = pk & TRI_M24;
-      qa = rowptr[q];
-      dq = rowptr[q + 1] - qa;
+      const uint2 r = qrow(k);
+      qa = r.x;
+      dq = r.y & TRI_M24;
+      pk = r.y & 0xFF000000u;
       if (SPLIT && dp < dq) dq = 0;  // pass B counts this edge
     }
     const uint32_t inc = wave_inclusive_scan(dq);
@@ -423,52 +436,55 @@ __device__ inline void tri_row_packed(uint32_t a, uint32_t nb, uint32_t ns, cons
     if (lane == WAVE - 1) tb.pre[WAVE] = inc;
     tb.qa[lane] = qa;
     tb.pk[lane] = pk;
-    tb.kk[lane] = k < nb ? pqe(k) : 0u;
+    tb.kk[lane] = k;
     const uint32_t total = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl(inc, WAVE - 1, WAVE));
     if (lane == 0) probes += total;
     __builtin_amdgcn_wave_barrier();
     uint32_t w[2][ILP], pos[2][ILP], bi[2][ILP];
     auto issue = [&](uint32_t t0, uint32_t (&ww)[ILP], uint32_t (&pp)[ILP], uint32_t (&bb)[ILP]) {
+      uint32_t xc[ILP];
 #pragma unroll
       for (int u = 0; u < ILP; ++u) {
-        const uint32_t x = t0 + u * WAVE + lane;
-        const uint32_t xc = min(x, total - 1);
-        uint32_t b = 0;  // last batch entry with pre[b] <= xc
+        xc[u] = min(t0 + u * WAVE + lane, total - 1);
+        bb[u] = 0;  // last batch entry with pre[b] <= xc (the ILP searches in lockstep)
+      }
 #pragma unroll
-        for (int st = WAVE / 2; st > 0; st >>= 1)
-          if (tb.pre[b + st] <= xc) b += st;
-        bb[u] = b;
-        pp[u] = tb.qa[b] + (xc - tb.pre[b]);
-        ww[u] = pcols[pp[u]];
-        if (x >= total) ww[u] = 0xFFFFFFFFu;  // past the end (the load stays unconditional)
+      for (int st = WAVE / 2; st > 0; st >>= 1) {
+        uint32_t v[ILP];
+#pragma unroll
+        for (int u = 0; u < ILP; ++u) v[u] = tb.pre[bb[u] + st];
+#pragma unroll
+        for (int u = 0; u < ILP; ++u) bb[u] = v[u] <= xc[u] ? bb[u] + st : bb[u];
+      }
+#pragma unroll
+      for (int u = 0; u < ILP; ++u) {
+        pp[u] = tb.qa[bb[u]] + (xc[u] - tb.pre[bb[u]]);
+        ww[u] = c_tri_diag == 2 ? (pp[u] * 2654435761u) & TRI_M24 : pcols[pp[u]];
+        if (t0 + u * WAVE + lane >= total) ww[u] = 0xFFFFFFFFu;  // past the end (the load stays unconditional)
       }
     };
     auto probe = [&](const uint32_t (&ww)[ILP], const uint32_t (&pp)[ILP], const uint32_t (&bb)[ILP]) {
+      if (c_tri_diag == 1) return;
+      uint32_t wk[ILP], pw[ILP], pos[ILP];
+      bool live[ILP], hit[ILP];
 #pragma unroll
       for (int u = 0; u < ILP; ++u) {
-        if (ww[u] == 0xFFFFFFFFu) continue;
-        const uint32_t wk = ww[u] & TRI_M24;
-        uint32_t lo = 0, n = dp;
-        while (n > 0) {
-          const uint32_t half = n >> 1;
-          if ((fnd(lo + half) & TRI_M24) < wk) {
-            lo += half + 1;
-            n -= half + 1;
-          } else {
-            n = half;
-          }
-        }
-        if (lo < dp) {
-          const uint32_t pw = fnd(lo);
-          if ((pw & TRI_M24) == wk) {
-            ++hits;
-            const uint2 a1 = tri_fb(tb.pk[bb[u]], vals, tb.kk[bb[u]]);  // p–q
-            const uint2 s2 = tri_fb(ww[u], vals, pp[u]);                 // streamed: q–w (A) / p–w (B)
-            const uint2 s3 = tri_fb(pw, vals, a + lo);                   // staged:   p–w (A) / q–w (B)
-            const uint2 a2 = SWAP ? s3 : s2, a3 = SWAP ? s2 : s3;
-            // p→q→w→p  +  p→w→q→p
-            t += (unsigned long long)a1.x * a2.x * a3.y + (unsigned long long)a3.x * a2.y * a1.y;
-          }
+        live[u] = ww[u] != 0xFFFFFFFFu;
+        wk[u] = ww[u] & TRI_M24;
+      }
+      find.template batch<ILP>(wk, live, hit, pw, pos);
+#pragma unroll
+      for (int u = 0; u < ILP; ++u) {
+        if (hit[u]) {
+          ++hits;
+          const uint32_t pkw = tb.pk[bb[u]];
+          const uint2 a1 = tri_esc(pkw) ? vals[pqe(tb.kk[bb[u]])]  // p–q
+                                        : make_uint2((pkw >> 24) & 15u, pkw >> 28);
+          const uint2 s2 = tri_fb(ww[u], vals, pp[u]);                 // streamed: q–w (A) / p–w (B)
+          const uint2 s3 = tri_fb(pw[u], vals, pos[u]);                // staged:   p–w (A) / q–w (B)
+          const uint2 a2 = SWAP ? s3 : s2, a3 = SWAP ? s2 : s3;
+          // p→q→w→p  +  p→w→q→p
+          t += (unsigned long long)a1.x * a2.x * a3.y + (unsigned long long)a3.x * a2.y * a1.y;
         }
       }
     };
@@ -484,13 +500,169 @@ __device__ inline void tri_row_packed(uint32_t a, uint32_t nb, uint32_t ns, cons
   }
 }
 
-template <int ILP, bool SPLIT = false>
+// {start, length | nibbles << 24} of the list N+(q) of the packed word w (q = w's id)
+__device__ inline uint2 tri_qrow(const uint32_t *rowptr, uint32_t w) {
+  const uint32_t q = w & TRI_M24, qa = rowptr[q];
+  return make_uint2(qa, (rowptr[q + 1] - qa) | (w & 0xFF000000u));
+}
+
+// Binary search of wk in the ascending packed words f(0..n) (vals index a + lo).
+template <class F>
+__device__ inline bool tri_bsearch(F f, uint32_t n, uint32_t a, uint32_t wk, uint32_t &pw, uint32_t &pos) {
+  uint32_t lo = 0, m = n;
+  while (m > 0) {
+    const uint32_t half = m >> 1;
+    if ((f(lo + half) & TRI_M24) < wk) {
+      lo += half + 1;
+      m -= half + 1;
+    } else {
+      m = half;
+    }
+  }
+  if (lo >= n) return false;
+  pw = f(lo);
+  pos = a + lo;
+  return (pw & TRI_M24) == wk;
+}
+
+// Finders of the staged list: batch<ILP>(wk, live → hit, packed word pw, and —
+// for an escape word — its vals index pos).  Sorted: ILP lower-bound searches
+// in lockstep by binary lifting (the list length n is wave-uniform, so every
+// lane runs the same floor(log2 n) + 1 steps, and the ILP dependent chains
+// interleave instead of running one after the other).
+template <class A>
+struct TriSorted {
+  A at;
+  uint32_t n, a;
+  template <int ILP>
+  __device__ inline void batch(const uint32_t (&wk)[ILP], const bool (&live)[ILP], bool (&hit)[ILP],
+                               uint32_t (&pw)[ILP], uint32_t (&pos)[ILP]) const {
+    // n is the staged list's length, equal on every lane: the halving loop is
+    // scalar and every probe index is in range (no guard), so the ILP reads of
+    // a step issue back to back under one wait.  base: lower bound of wk lies
+    // in [base, base + len]; at len = 1 it is base or base + 1.
+    const uint32_t nu = __builtin_amdgcn_readfirstlane(n);
+    if (nu == 0) {
+#pragma unroll
+      for (int u = 0; u < ILP; ++u) hit[u] = false;
+      return;
+    }
+    uint32_t base[ILP];
+#pragma unroll
+    for (int u = 0; u < ILP; ++u) base[u] = 0;
+    for (uint32_t len = nu; len > 1;) {
+      const uint32_t half = len >> 1;
+      uint32_t v[ILP];
+#pragma unroll
+      for (int u = 0; u < ILP; ++u) v[u] = at(base[u] + half);
+#pragma unroll
+      for (int u = 0; u < ILP; ++u) base[u] = (v[u] & TRI_M24) < wk[u] ? base[u] + half : base[u];
+      len -= half;
+    }
+    uint32_t v0[ILP], v1[ILP];
+#pragma unroll
+    for (int u = 0; u < ILP; ++u) {
+      v0[u] = at(base[u]);
+      v1[u] = at(min(base[u] + 1, nu - 1));
+    }
+#pragma unroll
+    for (int u = 0; u < ILP; ++u) {
+      const bool first = (v0[u] & TRI_M24) == wk[u];
+      const bool second = (v1[u] & TRI_M24) == wk[u] && base[u] + 1 < nu;
+      hit[u] = live[u] && (first || second);
+      pw[u] = first ? v0[u] : v1[u];
+      pos[u] = a + base[u] + (first ? 0u : 1u);
+    }
+  }
+};
+template <class A>
+__device__ inline TriSorted<A> tri_sorted(A at, uint32_t n, uint32_t a) {
+  return TriSorted<A>{at, n, a};
+}
+
+// ------------------------------------------------- LDS hash of a staged list
+// A staged list (≤ TRI_CAP words) is searched through an open-addressing table
+// in the wave's LDS slice instead of a binary search over its sorted copy: one
+// 16-B read of a 4-slot bucket (load ≤ ½, so a bucket rarely overflows into the
+// next) against ~log2(n) dependent reads — the binary search was most of the
+// count kernels' time (s24, CAPF_TRI_DIAG: pass B 244 ms searching vs 89 ms
+// loading).  Slots hold the packed words (none equals TRI_EMPTY: k_tri_pack
+// clears b when f = 15); an escape word's vals index comes from a binary
+// search of the list in global memory (rare multi-edges).
+constexpr uint32_t TRI_EMPTY = 0xFFFFFFFFu;
+
+struct TriHash {
+  const uint32_t *tab;
+  const uint32_t *row;  // the list in global memory (escape positions)
+  uint32_t mask, n, a;
+  int shift;
+};
+
+__device__ inline uint32_t tri_hash(uint32_t wk, int shift) { return (wk * 0x9E3779B1u) >> shift; }
+
+// Stage row[0..n) (vals index a) into the wave's table tab (≥ 2n words).
+__device__ inline TriHash tri_stage_hash(uint32_t *tab, const uint32_t *row, uint32_t n, uint32_t a) {
+  const int lane = lane_id();
+  uint32_t nbk = 16;  // buckets of 4 slots, 4·nbk ≥ 2n
+  while (nbk * 2 < n) nbk <<= 1;
+  const int shift = 32 - (31 - __builtin_clz(nbk));
+  uint4 *t4 = reinterpret_cast<uint4 *>(tab);
+  __builtin_amdgcn_wave_barrier();  // the previous list's searches are done
+  for (uint32_t i = lane; i < nbk; i += WAVE) t4[i] = make_uint4(TRI_EMPTY, TRI_EMPTY, TRI_EMPTY, TRI_EMPTY);
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t k = lane; k < n; k += WAVE) {
+    const uint32_t w = row[k];  // never TRI_EMPTY (k_tri_pack)
+    uint32_t b = tri_hash(w & TRI_M24, shift);
+    for (bool done = false; !done; b = (b + 1) & (nbk - 1)) {
+#pragma unroll
+      for (int j = 0; j < 4 && !done; ++j) done = atomicCAS(&tab[4 * b + j], TRI_EMPTY, w) == TRI_EMPTY;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  return TriHash{tab, row, nbk - 1, n, a, shift};
+}
+
+__device__ inline bool tri_hfind(const TriHash &h, uint32_t wk, uint32_t &pw, uint32_t &pos) {
+  const uint4 *t4 = reinterpret_cast<const uint4 *>(h.tab);
+  for (uint32_t b = tri_hash(wk, h.shift);; b = (b + 1) & h.mask) {
+    const uint4 v = t4[b];
+    uint32_t w = TRI_EMPTY;
+    if ((v.x & TRI_M24) == wk && v.x != TRI_EMPTY) w = v.x;
+    if ((v.y & TRI_M24) == wk && v.y != TRI_EMPTY) w = v.y;
+    if ((v.z & TRI_M24) == wk && v.z != TRI_EMPTY) w = v.z;
+    if ((v.w & TRI_M24) == wk && v.w != TRI_EMPTY) w = v.w;
+    if (w != TRI_EMPTY) {
+      pw = w;
+      if (tri_esc(w)) {  // escape: the pair's vals index
+        uint32_t w2;
+        tri_bsearch([&](uint32_t x) { return h.row[x]; }, h.n, h.a, wk, w2, pos);
+      }
+      return true;
+    }
+    if (v.x == TRI_EMPTY || v.y == TRI_EMPTY || v.z == TRI_EMPTY || v.w == TRI_EMPTY) return false;
+  }
+}
+
+struct TriHashFind {
+  TriHash h;
+  template <int ILP>
+  __device__ inline void batch(const uint32_t (&wk)[ILP], const bool (&live)[ILP], bool (&hit)[ILP],
+                               uint32_t (&pw)[ILP], uint32_t (&pos)[ILP]) const {
+#pragma unroll
+    for (int u = 0; u < ILP; ++u) hit[u] = live[u] && tri_hfind(h, wk[u], pw[u], pos[u]);
+  }
+};
+
+template <int ILP, bool SPLIT = false, int HCAP = 0>
 __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_packed(const uint32_t *rowptr,
                                                                  const uint32_t *pcols, const uint2 *vals,
                                                                  uint64_t len, int parts, int part,
                                                                  unsigned long long *cursor,
                                                                  unsigned long long *acc) {
-  __shared__ uint32_t s_cols[TRI_BLOCK / WAVE][TRI_CAP];
+  // HCAP > 0: staged lists of ≤ HCAP words hashed into 2·HCAP slots; 0: sorted copies of ≤ TRI_CAP
+  constexpr bool HASH = HCAP > 0;
+  constexpr uint32_t CAP = HASH ? HCAP : TRI_CAP;
+  __shared__ __attribute__((aligned(16))) uint32_t s_cols[TRI_BLOCK / WAVE][HASH ? 2 * HCAP : TRI_CAP];
   __shared__ TriBatch2 s_tab[TRI_BLOCK / WAVE];
   __shared__ unsigned long long lds[17];
   const int wv = threadIdx.x / WAVE, lane = lane_id();
@@ -506,18 +678,26 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_packed(const uint32_t *
     for (uint64_t p = r0; p < r1; ++p) {
       const uint32_t a = rowptr[p], dp = rowptr[p + 1] - a;
       if (dp < 2) continue;  // a triangle needs two out-neighbours at its lowest vertex
-      if (dp > TRI_CAP) {  // rare long row: searched in global memory
-        const uint32_t *row = pcols + a;
-        tri_row_packed<ILP, SPLIT>(a, dp, dp, rowptr, pcols, vals, tb, [&](uint32_t k) { return row[k]; },
-                                   [&](uint32_t x) { return row[x]; }, [&](uint32_t k) { return a + k; }, t,
-                                   probes, hits);
+      const uint32_t *row = pcols + a;
+      auto pqe = [&](uint32_t k) { return a + k; };
+      if (dp > CAP) {  // rare long row: searched in global memory
+        tri_row_packed<ILP, SPLIT>(dp, dp, pcols, vals, tb, [&](uint32_t k) { return tri_qrow(rowptr, row[k]); },
+                                   tri_sorted([&](uint32_t x) { return row[x]; }, dp, a),
+                                   pqe, t, probes, hits);
         continue;
       }
-      for (uint32_t k = lane; k < dp; k += WAVE) sc[k] = pcols[a + k];
-      __builtin_amdgcn_wave_barrier();
-      tri_row_packed<ILP, SPLIT>(a, dp, dp, rowptr, pcols, vals, tb, [&](uint32_t k) { return sc[k]; },
-                                 [&](uint32_t x) { return sc[x]; }, [&](uint32_t k) { return a + k; }, t, probes,
-                                 hits);
+      if constexpr (HASH) {
+        const TriHash h = tri_stage_hash(sc, row, dp, a);
+        tri_row_packed<ILP, SPLIT>(dp, dp, pcols, vals, tb, [&](uint32_t k) { return tri_qrow(rowptr, row[k]); },
+                                   TriHashFind{h},
+                                   pqe, t, probes, hits);
+      } else {
+        for (uint32_t k = lane; k < dp; k += WAVE) sc[k] = row[k];
+        __builtin_amdgcn_wave_barrier();
+        tri_row_packed<ILP, SPLIT>(dp, dp, pcols, vals, tb, [&](uint32_t k) { return tri_qrow(rowptr, sc[k]); },
+                                   tri_sorted([&](uint32_t x) { return sc[x]; }, dp, a),
+                                   pqe, t, probes, hits);
+      }
       __builtin_amdgcn_wave_barrier();  // sc is rewritten by the next row
     }
   }
@@ -543,17 +723,21 @@ constexpr int TRI_QTILE_DEFAULT = 26;
 
 struct TriPassB {
   const uint32_t *in_words;   // p | multiplicity nibbles of the pair p–q, by (p-block, q, p)
+  const uint2 *in_rows;       // the same entries as {start of N+(p), |N+(p)| | nibbles << 24}, or null
   const uint32_t *in_eidx;    // out-CSR index of the edge p→q (vals escape)
   const uint4 *items;         // (q, first in-list entry, entries ≤ TRI_BCHUNK) per work item
   uint32_t nitems;
 };
 
-template <int ILP>
+template <int ILP, int HCAP = 0>
 __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_passb(const uint32_t *rowptr, const uint32_t *pcols,
                                                                 const uint2 *vals, TriPassB b, int parts,
                                                                 int part, unsigned long long *cursor,
                                                                 unsigned long long *acc) {
-  __shared__ uint32_t s_cols[TRI_BLOCK / WAVE][TRI_CAP];
+  // HCAP > 0: staged lists of ≤ HCAP words hashed into 2·HCAP slots; 0: sorted copies of ≤ TRI_CAP
+  constexpr bool HASH = HCAP > 0;
+  constexpr uint32_t CAP = HASH ? HCAP : TRI_CAP;
+  __shared__ __attribute__((aligned(16))) uint32_t s_cols[TRI_BLOCK / WAVE][HASH ? 2 * HCAP : TRI_CAP];
   __shared__ TriBatch2 s_tab[TRI_BLOCK / WAVE];
   __shared__ unsigned long long lds[17];
   const int wv = threadIdx.x / WAVE, lane = lane_id();
@@ -561,6 +745,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_passb(const uint32_t *r
   TriBatch2 &tb = s_tab[wv];
   unsigned long long t = 0, probes = 0, hits = 0;
   uint32_t staged = 0xFFFFFFFFu;  // q whose list sits in sc
+  TriHash h{};
   for (;;) {
     unsigned long long c0 = 0;
     if (lane == 0) c0 = atomicAdd(cursor, 1ull);
@@ -574,23 +759,35 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_passb(const uint32_t *r
       const uint32_t i0 = item.y, n = item.z;
       const uint32_t *inw = b.in_words + i0;
       const uint32_t *ine = b.in_eidx + i0;
-      if (dq > TRI_CAP) {  // long N+(q): searched in global memory
-        const uint32_t *row = pcols + a;
-        tri_row_packed<ILP, false, true>(a, n, dq, rowptr, pcols, vals, tb, [&](uint32_t k) { return inw[k]; },
-                                         [&](uint32_t x) { return row[x]; }, [&](uint32_t k) { return ine[k]; },
-                                         t, probes, hits);
+      const uint32_t *row = pcols + a;
+      auto qs = [&](uint32_t k) { return b.in_rows ? b.in_rows[i0 + k] : tri_qrow(rowptr, inw[k]); };
+      auto pqe = [&](uint32_t k) { return ine[k]; };
+      if (dq > CAP) {  // long N+(q): searched in global memory
+        tri_row_packed<ILP, false, true>(n, dq, pcols, vals, tb, qs,
+                                         tri_sorted([&](uint32_t x) { return row[x]; }, dq, a),
+                                         pqe, t, probes, hits);
         staged = 0xFFFFFFFFu;
         continue;
       }
-      if (q != staged) {
-        __builtin_amdgcn_wave_barrier();  // the previous list's searches are done
-        for (uint32_t k = lane; k < dq; k += WAVE) sc[k] = pcols[a + k];
-        __builtin_amdgcn_wave_barrier();
-        staged = q;
+      if constexpr (HASH) {
+        if (q != staged) {
+          h = tri_stage_hash(sc, row, dq, a);
+          staged = q;
+        }
+        tri_row_packed<ILP, false, true>(n, dq, pcols, vals, tb, qs,
+                                         TriHashFind{h},
+                                         pqe, t, probes, hits);
+      } else {
+        if (q != staged) {
+          __builtin_amdgcn_wave_barrier();  // the previous list's searches are done
+          for (uint32_t k = lane; k < dq; k += WAVE) sc[k] = row[k];
+          __builtin_amdgcn_wave_barrier();
+          staged = q;
+        }
+        tri_row_packed<ILP, false, true>(n, dq, pcols, vals, tb, qs,
+                                         tri_sorted([&](uint32_t x) { return sc[x]; }, dq, a),
+                                         pqe, t, probes, hits);
       }
-      tri_row_packed<ILP, false, true>(a, n, dq, rowptr, pcols, vals, tb, [&](uint32_t k) { return inw[k]; },
-                                       [&](uint32_t x) { return sc[x]; }, [&](uint32_t k) { return ine[k]; },
-                                       t, probes, hits);
     }
   }
   unsigned long long tot;
@@ -671,6 +868,14 @@ __global__ void k_tri_inlist(const uint64_t *skeys, const uint32_t *seidx, const
     in_words[i] = (pcols[seidx[i]] & 0xFF000000u) | ((uint32_t)skeys[i] & 0xFFFFFFu);
 }
 
+// {start, length | nibbles << 24} of the list named by each packed word:
+// rows[i] = the list N+(x) of x = words[i]'s id (the batch entries of the count
+// kernels then need one coalesced 8-B load instead of a dependent rowptr pair).
+__global__ void k_tri_list_rows(const uint32_t *words, const uint32_t *rowptr, uint32_t n, uint2 *rows) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    rows[i] = tri_qrow(rowptr, words[i]);
+}
+
 // Oriented CSR of the distinct node pairs of (src, dst) over [lo, lo + len).
 struct TriGraph {
   // acc: [0] T, [1] Σ(L+L)·f·b, [2] Σ L(L−1)(L−2), [3] cursor, [4] probes (w ∈ N+(q)
@@ -679,6 +884,7 @@ struct TriGraph {
   BufPtr pcols;  // packed column words (node ids < 2^24), else null
   // two-pass schedule (pass B: edges with |N+(p)| < |N+(q)| counted at q)
   BufPtr in_words, in_eidx, items;
+  BufPtr erow, in_rows;  // list rows of pcols / in_words (k_tri_list_rows), or null
   uint32_t nB = 0, nitems = 0;
   // q-tiled pass A: work items (p, k0, k1) sorted by (tile of N+(q)'s position, p)
   BufPtr aitems;
@@ -687,6 +893,12 @@ struct TriGraph {
   uint32_t P = 0;
   uint64_t len = 0;
 };
+
+// CAPF_TRI_ROWS=0 (tuning): batch entries look their list up in rowptr
+static bool tri_list_rows_on() {
+  const char *e = getenv("CAPF_TRI_ROWS");
+  return !(e && atoi(e) == 0);
+}
 
 // In-lists and work items of pass B (built with the CSR, cached with it).
 static void tri_build_passb(Session *s, const uint64_t *okey, TriGraph &g) {
@@ -726,6 +938,12 @@ static void tri_build_passb(Session *s, const uint64_t *okey, TriGraph &g) {
                      (uint32_t *)g.in_words->p);
   KERNEL_CHECK();
   HIP_CHECK(hipMemcpyAsync(g.in_eidx->p, seidx->p, 4 * (size_t)g.nB, hipMemcpyDeviceToDevice, s->stream));
+  if (tri_list_rows_on()) {
+    g.in_rows = s->alloc(8 * (int64_t)g.nB);
+    hipLaunchKernelGGL(k_tri_list_rows, dim3(grid_for(g.nB, 256, 256 * 64)), dim3(256), 0, s->stream,
+                       (const uint32_t *)g.in_words->p, (const uint32_t *)g.rowptr->p, g.nB, (uint2 *)g.in_rows->p);
+    KERNEL_CHECK();
+  }
   // segments = runs of equal (p-block, q) → work items of ≤ TRI_BCHUNK entries
   BufPtr seg = s->alloc(8 * (int64_t)g.nB), useg = s->alloc(8 * (int64_t)g.nB);
   BufPtr cnt = s->alloc(4 * ((int64_t)g.nB + 1)), nseg_d = s->alloc(16);
@@ -766,13 +984,17 @@ static void tri_build_passb(Session *s, const uint64_t *okey, TriGraph &g) {
 // Pass A over q-tiled work items (see tri_build_qtiles): item (p, k0, k1) probes
 // the q's N+(p)[k0, k1) — N+(p) staged in LDS (≤ TRI_CAP words) or searched in
 // place — with the pass-A rule (edges with |N+(p)| < |N+(q)| belong to pass B).
-template <int ILP>
+template <int ILP, int HCAP = 0>
 __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_qtiled(const uint32_t *rowptr, const uint32_t *pcols,
-                                                                 const uint2 *vals, const uint4 *items,
+                                                                 const uint2 *vals, const uint2 *erow,
+                                                                 const uint4 *items,
                                                                  uint32_t nitems, int parts, int part,
                                                                  unsigned long long *cursor,
                                                                  unsigned long long *acc) {
-  __shared__ uint32_t s_cols[TRI_BLOCK / WAVE][TRI_CAP];
+  // HCAP > 0: staged lists of ≤ HCAP words hashed into 2·HCAP slots; 0: sorted copies of ≤ TRI_CAP
+  constexpr bool HASH = HCAP > 0;
+  constexpr uint32_t CAP = HASH ? HCAP : TRI_CAP;
+  __shared__ __attribute__((aligned(16))) uint32_t s_cols[TRI_BLOCK / WAVE][HASH ? 2 * HCAP : TRI_CAP];
   __shared__ TriBatch2 s_tab[TRI_BLOCK / WAVE];
   __shared__ unsigned long long lds[17];
   const int wv = threadIdx.x / WAVE, lane = lane_id();
@@ -780,6 +1002,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_qtiled(const uint32_t *
   TriBatch2 &tb = s_tab[wv];
   unsigned long long t = 0, probes = 0, hits = 0;
   uint32_t staged = 0xFFFFFFFFu;  // p whose list sits in sc
+  TriHash h{};
   for (;;) {
     unsigned long long c0 = 0;
     if (lane == 0) c0 = atomicAdd(cursor, 1ull);
@@ -790,23 +1013,35 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_qtiled(const uint32_t *
       const uint4 item = items[it];
       const uint32_t p = item.x, k0 = item.y, nb = item.z - item.y;
       const uint32_t a = rowptr[p], dp = rowptr[p + 1] - a;
-      if (dp > TRI_CAP) {  // long N+(p): searched in global memory
-        const uint32_t *row = pcols + a;
-        tri_row_packed<ILP, true>(a, nb, dp, rowptr, pcols, vals, tb, [&](uint32_t k) { return row[k0 + k]; },
-                                  [&](uint32_t x) { return row[x]; }, [&](uint32_t k) { return a + k0 + k; }, t,
-                                  probes, hits);
+      const uint32_t *row = pcols + a;
+      auto pqe = [&](uint32_t k) { return a + k0 + k; };
+      auto qrow = [&](uint32_t k) { return erow ? erow[a + k0 + k] : tri_qrow(rowptr, row[k0 + k]); };
+      if (dp > CAP) {  // long N+(p): searched in global memory
+        tri_row_packed<ILP, true>(nb, dp, pcols, vals, tb, qrow,
+                                  tri_sorted([&](uint32_t x) { return row[x]; }, dp, a),
+                                  pqe, t, probes, hits);
         staged = 0xFFFFFFFFu;
         continue;
       }
-      if (p != staged) {
-        __builtin_amdgcn_wave_barrier();  // the previous list's searches are done
-        for (uint32_t k = lane; k < dp; k += WAVE) sc[k] = pcols[a + k];
-        __builtin_amdgcn_wave_barrier();
-        staged = p;
+      if constexpr (HASH) {
+        if (p != staged) {
+          h = tri_stage_hash(sc, row, dp, a);
+          staged = p;
+        }
+        tri_row_packed<ILP, true>(nb, dp, pcols, vals, tb, qrow,
+                                  TriHashFind{h},
+                                  pqe, t, probes, hits);
+      } else {
+        if (p != staged) {
+          __builtin_amdgcn_wave_barrier();  // the previous list's searches are done
+          for (uint32_t k = lane; k < dp; k += WAVE) sc[k] = row[k];
+          __builtin_amdgcn_wave_barrier();
+          staged = p;
+        }
+        tri_row_packed<ILP, true>(nb, dp, pcols, vals, tb, qrow,
+                                  tri_sorted([&](uint32_t x) { return sc[x]; }, dp, a),
+                                  pqe, t, probes, hits);
       }
-      tri_row_packed<ILP, true>(a, nb, dp, rowptr, pcols, vals, tb, [&](uint32_t k) { return sc[k0 + k]; },
-                                [&](uint32_t x) { return sc[x]; }, [&](uint32_t k) { return a + k0 + k; }, t,
-                                probes, hits);
     }
   }
   unsigned long long tot;
@@ -1004,6 +1239,12 @@ static void tri_build(Session *s, const ColView &src, const ColView &dst, int64_
     hipLaunchKernelGGL(k_tri_pack, dim3(grid_for(g.P, 256, 256 * 64)), dim3(256), 0, s->stream,
                        (const uint32_t *)g.cols->p, (const uint2 *)g.vals->p, g.P, (uint32_t *)g.pcols->p);
     KERNEL_CHECK();
+    if (tri_list_rows_on()) {
+      g.erow = s->alloc(8 * (int64_t)g.P);
+      hipLaunchKernelGGL(k_tri_list_rows, dim3(grid_for(g.P, 256, 256 * 64)), dim3(256), 0, s->stream,
+                         (const uint32_t *)g.pcols->p, (const uint32_t *)g.rowptr->p, g.P, (uint2 *)g.erow->p);
+      KERNEL_CHECK();
+    }
     tri_build_passb(s, (const uint64_t *)ok2->p, g);
     // CAPF_TRI_QTILE (tuning): log2 of the words per pass-A tile; 0 = row by row
     const char *qt = getenv("CAPF_TRI_QTILE");
@@ -1038,6 +1279,14 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
     srcc->index_key[1] = (int64_t)len;
   }
   const TriGraph &g = *gp;
+  {
+    static const int diag = getenv("CAPF_TRI_DIAG") ? atoi(getenv("CAPF_TRI_DIAG")) : 0;
+    static bool set = false;
+    if (diag && !set) {
+      HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_tri_diag), &diag, sizeof(int)));
+      set = true;
+    }
+  }
   // per-query accumulators: T, the cached pair-loop term, Σ L(L−1)(L−2), the
   // row cursor, probes, hits
   BufPtr qacc = s->alloc(64);  // + [6] the pass-B cursor
@@ -1059,22 +1308,30 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
     // kernel names of the committed PMC counters)
     static const bool filter = getenv("CAPF_TRI_FILTER") && atoi(getenv("CAPF_TRI_FILTER")) == 1;  // measured slower (0.98 vs 0.94 s at s24)
     static const int ilp = getenv("CAPF_TRI_ILP") ? atoi(getenv("CAPF_TRI_ILP")) : TRI_ILP;  // tuning
+    // CAPF_TRI_HASH (tuning): 0 = staged lists binary-searched in sorted LDS copies;
+    // 512 / 1024 = lists up to that many words hashed in LDS (longer: global search)
+    // (s24, lockstep searches: sorted 314 ms, hash 1024 454 ms — kept off)
+    const int hash = getenv("CAPF_TRI_HASH") ? atoi(getenv("CAPF_TRI_HASH")) : 0;
     // CAPF_TRI_TWOPASS=0 (tuning): one pass, every wedge streamed from N+(q)
     const bool two = packed && g.pcols && g.in_words && !(getenv("CAPF_TRI_TWOPASS") && atoi(getenv("CAPF_TRI_TWOPASS")) == 0);
     if (packed && g.pcols) {
       if (two && g.qshift > 0) {
         if (g.naitems > 0) {
           KernelTimer kt(s, "tri_count_qtiled", 4.0 * g.P);
-          auto kq = ilp <= 2 ? k_tri_count_qtiled<2> : k_tri_count_qtiled<4>;
+          auto kq = hash == 1024 ? (ilp <= 2 ? k_tri_count_qtiled<2, 1024> : k_tri_count_qtiled<4, 1024>)
+                    : hash == 512  ? (ilp <= 2 ? k_tri_count_qtiled<2, 512> : k_tri_count_qtiled<4, 512>)
+                                   : (ilp <= 2 ? k_tri_count_qtiled<2> : ilp == 3 ? k_tri_count_qtiled<3> : k_tri_count_qtiled<4>);
           hipLaunchKernelGGL(kq, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
                              (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
-                             (const uint2 *)g.vals->p, (const uint4 *)g.aitems->p, g.naitems, parts, part,
+                             (const uint2 *)g.vals->p, g.erow ? (const uint2 *)g.erow->p : nullptr,
+                             (const uint4 *)g.aitems->p, g.naitems, parts, part,
                              acc + 3, acc);
         }
       } else {
         KernelTimer kt(s, "tri_count_packed", 4.0 * g.P);
-        auto kern = two ? (ilp <= 2 ? k_tri_count_packed<2, true> : k_tri_count_packed<4, true>)
-                        : (ilp >= 8 ? k_tri_count_packed<8> : ilp <= 2 ? k_tri_count_packed<2> : k_tri_count_packed<4>);
+        auto kern = two ? (hash ? k_tri_count_packed<4, true, 1024> : ilp <= 2 ? k_tri_count_packed<2, true>
+                                                                   : ilp == 3 ? k_tri_count_packed<3, true> : k_tri_count_packed<4, true>)
+                        : (hash ? k_tri_count_packed<4, false, 1024> : ilp <= 2 ? k_tri_count_packed<2> : k_tri_count_packed<4>);
         hipLaunchKernelGGL(kern, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
                            (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
                            (const uint2 *)g.vals->p, len, parts, part, acc + 3, acc);
@@ -1087,9 +1344,12 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
       }
       if (two && g.nitems > 0) {
         KernelTimer kt(s, "tri_count_passb", 4.0 * g.P);
-        TriPassB b{(const uint32_t *)g.in_words->p, (const uint32_t *)g.in_eidx->p, (const uint4 *)g.items->p,
+        TriPassB b{(const uint32_t *)g.in_words->p, g.in_rows ? (const uint2 *)g.in_rows->p : nullptr,
+                   (const uint32_t *)g.in_eidx->p, (const uint4 *)g.items->p,
                    g.nitems};
-        auto kb = ilp <= 2 ? k_tri_count_passb<2> : k_tri_count_passb<4>;
+        auto kb = hash == 1024 ? (ilp <= 2 ? k_tri_count_passb<2, 1024> : k_tri_count_passb<4, 1024>)
+                  : hash == 512  ? (ilp <= 2 ? k_tri_count_passb<2, 512> : k_tri_count_passb<4, 512>)
+                                 : (ilp <= 2 ? k_tri_count_passb<2> : ilp == 3 ? k_tri_count_passb<3> : k_tri_count_passb<4>);
         hipLaunchKernelGGL(kb, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
                            (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p, (const uint2 *)g.vals->p,
                            b, parts, part, acc + 6, acc);
@@ -1117,6 +1377,8 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
     s->profile["tri_probes"].bytes += (double)h[0];
     s->profile["tri_hits"].bytes += (double)h[1];
     s->profile["tri_oriented_edges"].bytes += (double)g.P;
+    s->profile["tri_passb_edges"].bytes += (double)g.nB;
+    s->profile["tri_passa_items"].bytes += (double)g.naitems;
   }
   // qacc returns to the stream-ordered pool: reuse is ordered after the kernels
 }

@@ -550,8 +550,10 @@ class DistTable:
             count = _sharded_two_hop(self)
             if count is not None:
                 names = list(aggregations)
+                # every rank holds the all-reduced count: the one row is replicated
+                # (reading it back needs no gather)
                 loc = self.session.local.table([(n, T_INT, [count], None) for n in names], nrows=1)
-                return self._wrap(loc if self.session.rank == 0 else loc.limit(0), placement="root")
+                return self._wrap(loc, placement="replicated")
         keys = _dist_key_cols(self.local, by, header)
         if self.placement == "root":
             out = self.local.group(by, aggregations, header=header, params=params)

@@ -749,14 +749,17 @@ def test_triangle_self_loops_multi_edges(gpu_session):
     assert got == cmodel.count_triangle_brute(src[ok], dst[ok], n) == cmodel.count_triangle_formula(src, dst, n)
 
 
-@pytest.mark.parametrize("packed", ["1", "0"], ids=["packed", "unpacked"])
-def test_triangle_heavy_multi_edges(gpu_session, monkeypatch, packed):
+@pytest.mark.parametrize("packed,hash_cap", [("1", "1024"), ("1", "512"), ("1", "0"), ("0", "1024")],
+                         ids=["packed-hash1024", "packed-hash512", "packed-sorted", "unpacked"])
+def test_triangle_heavy_multi_edges(gpu_session, monkeypatch, packed, hash_cap):
     """Pairs with 15+ parallel rels in either direction (the packed column
-    word's multiplicity nibbles saturate and the count reads vals), beside
-    pairs of 1-14; checked against brute force and trace(A^3)."""
+    word's multiplicity nibbles saturate and the count reads vals — through
+    the LDS hash table's escape words, or the sorted copy), beside pairs of
+    1-14; checked against brute force and trace(A^3)."""
     from capf_amd.graph import ElementTable, ScanGraph as SG
     from capf_amd.expr import T_INT
     monkeypatch.setenv("CAPF_TRI_PACKED", packed)
+    monkeypatch.setenv("CAPF_TRI_HASH", hash_cap)
     rng = np.random.default_rng(5)
     n = 40
     e = []
@@ -776,15 +779,50 @@ def test_triangle_heavy_multi_edges(gpu_session, monkeypatch, packed):
     assert got == cmodel.count_triangle_brute(src, dst, n) == cmodel.count_triangle_formula(src, dst, n)
 
 
+@pytest.mark.parametrize("rows", ["1", "0"], ids=["list-rows", "rowptr"])
+@pytest.mark.parametrize("hash_cap", ["0", "512", "1024"])
+def test_triangle_top_id_escape_word(gpu_session, monkeypatch, hash_cap, rows):
+    """Node id 2^24 − 1 in a pair saturated both ways: its packed column word
+    would be 0xFFFFFFFF — the count kernels' end-of-batch marker and the LDS
+    hash table's empty slot — unless the pack step clears b when f saturates;
+    with the pair in triangles both ways."""
+    from capf_amd.graph import ElementTable, ScanGraph as SG
+    from capf_amd.expr import T_INT
+    monkeypatch.setenv("CAPF_TRI_HASH", hash_cap)
+    monkeypatch.setenv("CAPF_TRI_ROWS", rows)
+    T, U = (1 << 24) - 1, (1 << 24) - 2
+    rng = np.random.default_rng(11)
+    e = [(T, U)] * 17 + [(U, T)] * 16 + [(U, 5)] * 15 + [(5, T)] * 20 + [(T, 5)] * 3 + [(5, U)] * 2
+    for _ in range(300):
+        x, y = (int(v) for v in rng.integers(0, 60, 2))
+        e += [(x, y)] * int(rng.choice([1, 2, 15, 16]))
+        e += [(x, T), (U, y)]
+    src = np.array([x for x, _ in e], dtype=np.int64)
+    dst = np.array([y for _, y in e], dtype=np.int64)
+    n = 1 << 24
+    rels = gpu_session.table([("id", T_INT, np.arange(len(e)), None), ("source", T_INT, src, None),
+                              ("target", T_INT, dst, None)])
+    nodes = gpu_session.range_nodes(0, n, id_col="id")
+    g = SG(gpu_session, [ElementTable("node", frozenset(["V"]), nodes, {})],
+           [ElementTable("rel", frozenset(["E"]), rels, {})])
+    got = run(g, _triangle_query())[0]["count"]
+    assert gpu_session.last_plan() == "fused_triangle"
+    assert got == cmodel.count_triangle_brute(src, dst, n)
+
+
+@pytest.mark.parametrize("rows", ["1", "0"], ids=["list-rows", "rowptr"])
+@pytest.mark.parametrize("hash_cap", ["0", "512", "1024"])
 @pytest.mark.parametrize("qtile", ["0", "12", "14", "18"])
 @pytest.mark.parametrize("scale", [10, 13])
-def test_triangle_qtiled(gpu_session, monkeypatch, qtile, scale):
+def test_triangle_qtiled(gpu_session, monkeypatch, qtile, scale, hash_cap, rows):
     """Pass A over q-tiled work items (CAPF_TRI_QTILE = log2 words per tile, 0 = row by row;
     small tiles cut most rows into several items, some rows longer than the
     LDS copy) gives the trace(A^3) count, alone and as 3 parts."""
     import torch
     from capf_amd.table import triangle_count_part_async
     monkeypatch.setenv("CAPF_TRI_QTILE", qtile)
+    monkeypatch.setenv("CAPF_TRI_HASH", hash_cap)
+    monkeypatch.setenv("CAPF_TRI_ROWS", rows)
     g = rmat_graph(gpu_session, scale, compact=True)
     got = run(g, _triangle_query())[0]["count"]
     assert gpu_session.last_plan() == "fused_triangle"

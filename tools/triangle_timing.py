@@ -26,6 +26,6 @@ for scale in map(int, sys.argv[1:]):
     run(g, q)
     s.sync()
     s.set_profiling(False)
-    prof = {k: round(v["total_ms"], 2) for k, v in s.profile().items()}
+    prof = {k: round(v["total_ms"], 2) if v["total_ms"] > 0 else v["bytes"] for k, v in s.profile().items()}
     print(f"s{scale} triangle count {c} {c2} plan {s.last_plan()} {el*1e3:.1f} ms {prof}", flush=True)
     del g

@@ -81,6 +81,15 @@ for p in parts:
     print(f"s{scale} G={G} part {p}: plan->scalar median {med:.3f} ms (min {min(times)*1e3:.3f}), "
           f"planning alone {statistics.median(plan)*1e3:.3f} ms, device {sum(prof.values()):.3f} ms {prof}, "
           f"partial {v}", flush=True)
+    if os.environ.get("SHARD_PROFILE") == "1":  # where the host time of a query goes
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        for _ in range(200):
+            run(g, q)
+        pr.disable()
+        pstats.Stats(pr).sort_stats("tottime").print_stats(30)
     del g, ds
 print(f"sum of partials {tot}; max over parts of the median plan->scalar {worst:.3f} ms")
 dist.destroy_process_group()

@@ -204,6 +204,45 @@ __host__ __device__ inline int64_t ld_int(const ColView &c, int64_t r) {
                               : ((const int64_t *)c.data)[r];
 }
 
+// A WHERE that is a conjunction of comparisons [NOT] (a op b) — a a column, b
+// a column or an integer literal (kernels_basic.hip::ft_compile): evaluated
+// without the stack interpreter by filter_select, and per output pair inside
+// the radix join's EMIT when it filters the join's output (`side`: the operand
+// is a column of the join's left (0) or right (1) input).
+constexpr int FT_MAX = 8;
+struct FtOperand {
+  ColView v;            // the column (or the lazy gather's source)
+  const int64_t *idx;   // lazy gather index, or null
+  int64_t lit;          // literal (v.data == null and lit_ok)
+  int32_t is_lit;
+  int32_t side;         // join-fused filters: 0 = left input row, 1 = right input row
+};
+struct FtTerm {
+  FtOperand a, b;
+  int32_t op;   // OP_EQ … OP_GE
+  int32_t neg;  // NOT around the comparison
+};
+struct FtProgram {
+  FtTerm t[FT_MAX];
+  int32_t nt;
+};
+
+// Operand value at row r (false: NULL — a NULL lazy row or an invalid value).
+__device__ inline bool ft_load(const FtOperand &o, int64_t r, int64_t &val) {
+  if (o.is_lit) {
+    val = o.lit;
+    return true;
+  }
+  int64_t row = r;
+  if (o.idx) {
+    row = o.idx[r];
+    if (row < 0) return false;
+  }
+  if (o.v.valid && !o.v.valid[row]) return false;
+  val = o.v.type == CAPF_TYPE_BOOL ? (((const uint8_t *)o.v.data)[row] ? 1 : 0) : ld_int(o.v, row);
+  return true;
+}
+
 // ------------------------------------------------------------- plan nodes
 enum class Kind {
   Source, Select, Filter, Join, Union, Distinct, Group, WithColumns, OrderBy, Skip, Limit
@@ -398,8 +437,20 @@ bool dense_join(Session *s, const Data &l, const Data &r, const std::vector<std:
 // large inputs (CAPF_JOIN=radix|hash forces a path).
 bool radix_join_applies(const Data &l, const Data &r, const std::vector<std::pair<int, int>> &keys,
                         int32_t join_type);
+// A Filter directly over an inner Join that would run as the radix join, whose
+// predicate compiles to terms (ft_compile over the join's output columns):
+// the join's EMIT evaluates the terms per pair and writes only the passing
+// pairs (a count pass, then the write) — no pair list, flags or selection of
+// the unfiltered join.  False when the shape does not apply (nothing ran).
+bool radix_join_filtered(Session *s, const Program &pred, const std::vector<std::string> &names, const Data &l,
+                         const Data &r, const std::vector<std::pair<int, int>> &keys, int32_t join_type,
+                         JoinPairs &out);
+bool ft_compile(const Program &p, const std::vector<std::string> &names, const Data &d, FtProgram &fp);
+bool dense_join_possible(Session *s, const Data &l, const Data &r, const std::vector<std::pair<int, int>> &keys,
+                         int32_t join_type);
 JoinPairs radix_join(Session *s, const Data &l, const Data &r,
-                     const std::vector<std::pair<int, int>> &keys, int32_t join_type);
+                     const std::vector<std::pair<int, int>> &keys, int32_t join_type,
+                     const FtProgram *pred = nullptr);
 // Aggregations over a grouping.
 ColPtr aggregate(Session *s, const Grouping &g, const Data &d, int64_t nrows, int32_t kind,
                  const ColPtr &arg, Type out_type);

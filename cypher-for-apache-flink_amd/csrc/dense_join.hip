@@ -239,6 +239,28 @@ __global__ void k_dense_pick(const int64_t *rows, int64_t m, const int64_t *brow
     out[i] = brow[rows[i]];
 }
 
+// Whether dense_join would take (l, r) — the same tests, the indexes built and
+// cached as dense_join builds them (a column without one caches "no index").
+bool dense_join_possible(Session *s, const Data &l, const Data &r, const std::vector<std::pair<int, int>> &keys,
+                         int32_t join_type) {
+  if (keys.size() != 1 || join_type == CAPF_JOIN_CROSS || join_type == CAPF_JOIN_FULL_OUTER) return false;
+  const char *mode = getenv("CAPF_JOIN");
+  if (mode && (strcmp(mode, "radix") == 0 || strcmp(mode, "hash") == 0)) return false;
+  const bool l_ok = join_type != CAPF_JOIN_LEFT_OUTER, r_ok = join_type != CAPF_JOIN_RIGHT_OUTER;
+  std::shared_ptr<DenseIndex> di;
+  bool build_left = false;
+  if (r_ok && r.nrows <= l.nrows) di = dense_index(s, r.cols[keys[0].second], r.nrows);
+  if (!di && l_ok) {
+    di = dense_index(s, l.cols[keys[0].first], l.nrows);
+    build_left = di != nullptr;
+  }
+  if (!di && r_ok && r.nrows > l.nrows) di = dense_index(s, r.cols[keys[0].second], r.nrows);
+  if (!di) return false;
+  const ColPtr &pk = (build_left ? r : l).cols[build_left ? keys[0].second : keys[0].first];
+  force(pk);
+  return pk->type == Type::Int64;
+}
+
 bool dense_join(Session *s, const Data &l, const Data &r, const std::vector<std::pair<int, int>> &keys,
                 int32_t join_type, JoinPairs &out) {
   if (keys.size() != 1 || join_type == CAPF_JOIN_CROSS || join_type == CAPF_JOIN_FULL_OUTER) return false;

@@ -1046,39 +1046,6 @@ ColPtr eval_program(Session *s, const Program &p, const std::vector<std::string>
 // AND under WHERE).  An operand still held as a lazy gather (a join output's
 // column) is read through its index (src[idx[r]], idx −1 = NULL row) instead of
 // being materialised first.
-constexpr int FT_MAX = 8;
-struct FtOperand {
-  ColView v;            // the column (or the lazy gather's source)
-  const int64_t *idx;   // lazy gather index, or null
-  int64_t lit;          // literal (v.data == null and lit_ok)
-  int32_t is_lit;
-  int32_t pad;
-};
-struct FtTerm {
-  FtOperand a, b;
-  int32_t op;   // OP_EQ … OP_GE
-  int32_t neg;  // NOT around the comparison
-};
-struct FtProgram {
-  FtTerm t[FT_MAX];
-  int32_t nt;
-};
-
-__device__ inline bool ft_load(const FtOperand &o, int64_t r, int64_t &val) {
-  if (o.is_lit) {
-    val = o.lit;
-    return true;
-  }
-  int64_t row = r;
-  if (o.idx) {
-    row = o.idx[r];
-    if (row < 0) return false;
-  }
-  if (o.v.valid && !o.v.valid[row]) return false;
-  val = o.v.type == CAPF_TYPE_BOOL ? (((const uint8_t *)o.v.data)[row] ? 1 : 0) : ld_int(o.v, row);
-  return true;
-}
-
 // 4 consecutive rows per thread: each term's index and value loads for the 4
 // rows are independent (in flight together), the flags go out as one word.
 __device__ inline void ft_load4(const FtOperand &o, int64_t r0, int64_t val[4], bool ok[4]) {
@@ -1142,7 +1109,8 @@ __global__ __launch_bounds__(256) void k_filter_terms(FtProgram fp, int64_t r_st
     for (int k = 0; k < fp.nt; ++k) {
       const FtTerm &t = fp.t[k];
       int64_t x = 0, y = 0;
-      const bool ok = ft_load(t.a, r, x) & ft_load(t.b, r, y);
+      const bool oa = ft_load(t.a, r, x), ob = ft_load(t.b, r, y);
+      const bool ok = oa && ob;
       bool res = t.op == OP_EQ   ? x == y
                  : t.op == OP_NEQ ? x != y
                  : t.op == OP_LT  ? x < y
@@ -1189,7 +1157,7 @@ static bool ft_operand(const Instr &in, const std::vector<std::string> &pnames,
 }
 
 // Postfix program → terms, or false (the interpreter runs it).
-static bool ft_compile(const Program &p, const std::vector<std::string> &names, const Data &d,
+bool ft_compile(const Program &p, const std::vector<std::string> &names, const Data &d,
                        FtProgram &fp) {
   fp.nt = 0;
   const auto &c = p.code;

@@ -550,23 +550,99 @@ __global__ void k_rj_subs(const int64_t *cnt, const int64_t *soff, int64_t nw, R
   }
 }
 
+// A filter over the join's pairs (radix_join_filtered).  Every column operand
+// is first materialised per row of its input side as int64 values + a "not
+// NULL" byte (k_rj_operand: lazy gathers, FOR decoding, validity folded once
+// per input row), in the order the EMIT meets the rows: build operands in the
+// sorted build partition order (read at the pair's build position, beside its
+// row id: coalesced), probe operands in probe partition order (staged in LDS
+// per 256-row step, beside the probe row).  A random 8-B load per pair and
+// operand ran at L1's one-line-per-clock rate (s14 var2: 1.1 ms to count).
+constexpr int RJ_PMAX = 4;  // probe-side column operands (LDS slots)
+struct RjOp {
+  const int64_t *val;  // build operand: by sorted build position
+  const uint8_t *ok;
+  int64_t lit;
+  int32_t is_lit;
+  int32_t slot;  // probe operand: its LDS slot; −1 = build operand
+};
+struct RjTerm {
+  RjOp a, b;
+  int32_t op, neg;
+};
+struct RjPred {
+  RjTerm t[FT_MAX];
+  const int64_t *pv[RJ_PMAX];  // probe operands by probe position
+  const uint8_t *po[RJ_PMAX];
+  int32_t nt, np;
+};
+
+__global__ void k_rj_operand(FtOperand o, const uint32_t *rows, int64_t n, int64_t *val, uint8_t *ok) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t v = 0;
+    ok[i] = ft_load(o, rows[i], v) ? 1 : 0;
+    val[i] = v;
+  }
+}
+
+// the terms over U pairs (build positions bi, probe step slots bl): all loads
+// of a term issued before any compare
+template <int U>
+__device__ inline void rj_pass(const RjPred &fp, const int64_t (&bi)[U], const uint32_t (&bl)[U],
+                               const int64_t (*spv)[RJ_JBLOCK], const uint8_t (*spo)[RJ_JBLOCK], bool (&pass)[U]) {
+  for (int t = 0; t < fp.nt; ++t) {
+    const RjTerm &tm = fp.t[t];
+    int64_t x[U], y[U];
+    uint8_t oa[U], ob[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      x[k] = tm.a.is_lit ? tm.a.lit : tm.a.slot >= 0 ? spv[tm.a.slot][bl[k]] : tm.a.val[bi[k]];
+      oa[k] = tm.a.is_lit ? (uint8_t)1 : tm.a.slot >= 0 ? spo[tm.a.slot][bl[k]] : tm.a.ok[bi[k]];
+      y[k] = tm.b.is_lit ? tm.b.lit : tm.b.slot >= 0 ? spv[tm.b.slot][bl[k]] : tm.b.val[bi[k]];
+      ob[k] = tm.b.is_lit ? (uint8_t)1 : tm.b.slot >= 0 ? spo[tm.b.slot][bl[k]] : tm.b.ok[bi[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      bool res = tm.op == OP_EQ   ? x[k] == y[k]
+                 : tm.op == OP_NEQ ? x[k] != y[k]
+                 : tm.op == OP_LT  ? x[k] < y[k]
+                 : tm.op == OP_LE  ? x[k] <= y[k]
+                 : tm.op == OP_GT  ? x[k] > y[k]
+                                   : x[k] >= y[k];
+      if (tm.neg) res = !res;
+      pass[k] = pass[k] && oa[k] && ob[k] && res;
+    }
+  }
+}
+
+// MODE 0: every pair of the sub-item's range [lo, hi) at out_off[item] + its
+// position.  With a filter (radix_join_filtered): MODE 1 counts the pairs that
+// pass into subcnt[sub]; MODE 2 writes them, in the same order, from
+// suboff[sub] on (per 4·256-pair round: a workgroup scan of the passes).
+template <int MODE>
 __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_emit_ranges(const RJSub *subs, const RJWork *work,
                                                                const uint64_t *bh, const uint32_t *brow,
                                                                const int64_t *bstart, const uint64_t *ph,
                                                                const uint32_t *prow, const int64_t *out_off,
                                                                int64_t *oprobe, int64_t *obuild,
-                                                               uint8_t *pmatched, uint8_t *bmatched) {
+                                                               uint8_t *pmatched, uint8_t *bmatched,
+                                                               const RjPred fp, int build_left,
+                                                               int64_t *subcnt, const int64_t *suboff) {
   __shared__ uint64_t kk[RJ_CHUNK];
   __shared__ unsigned long long hm[RJ_CHUNK / WAVE];
   __shared__ uint64_t th[RJ_RUNCAP];
   __shared__ uint32_t tv[RJ_RUNCAP];
   __shared__ uint32_t bex[RJ_JBLOCK + 1], bst[RJ_JBLOCK], bpr[RJ_JBLOCK];
   __shared__ uint32_t lds_sc[17];
+  __shared__ int64_t spv[MODE ? RJ_PMAX : 1][RJ_JBLOCK];  // probe operands of the step's rows
+  __shared__ uint8_t spo[MODE ? RJ_PMAX : 1][RJ_JBLOCK];
   const RJSub sb = subs[blockIdx.x];
   const RJWork wk = work[sb.item];
   const int64_t b0 = bstart[wk.part], b1 = bstart[wk.part + 1];
   const int wv = threadIdx.x / WAVE, lane = lane_id();
-  const int64_t obase = out_off[sb.item];
+  const int64_t obase = MODE == 0 ? out_off[sb.item] : 0;
+  int64_t fbase = MODE == 2 ? suboff[blockIdx.x] : 0;  // next filtered output position
+  uint32_t kept = 0;                                   // MODE 1: passing pairs of this thread
   int64_t rel = 0;  // pairs of the item before the current step
   for (int64_t c0 = b0; c0 < b1 && rel < sb.hi; c0 += RJ_CHUNK) {
     const int nc = (int)min<int64_t>((int64_t)RJ_CHUNK, b1 - c0);
@@ -622,6 +698,11 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_emit_ranges(const RJSub *subs,
         bex[threadIdx.x] = ex;
         bst[threadIdx.x] = st;
         bpr[threadIdx.x] = live ? prow[q] : 0u;
+        if constexpr (MODE != 0)
+          for (int j = 0; j < fp.np; ++j) {
+            spv[j][threadIdx.x] = live ? fp.pv[j][q] : 0;
+            spo[j][threadIdx.x] = live ? fp.po[j][q] : (uint8_t)0;
+          }
         if (threadIdx.x == 0) bex[RJ_JBLOCK] = tot;
         if (pmatched && cnt && rel + ex >= sb.lo && rel + ex < sb.hi) pmatched[prow[q]] = 1;
         __syncthreads();
@@ -629,24 +710,62 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_emit_ranges(const RJSub *subs,
         const uint32_t x1 = (uint32_t)min<int64_t>((int64_t)tot, sb.hi - rel);
         constexpr int U = 4;
         for (uint32_t xb = x0; xb < x1; xb += U * RJ_JBLOCK) {
-          uint32_t br[U], pr[U];
+          uint32_t br[U], pr[U], bl[U], xs[U];
+          int64_t bi[U];
+          // owner rows (last row with bex[b] ≤ x) of the U positions, searched in
+          // lockstep: the U dependent LDS chains interleave
 #pragma unroll
           for (int k = 0; k < U; ++k) {
-            const uint32_t x = min(xb + k * RJ_JBLOCK + threadIdx.x, x1 - 1);
-            uint32_t b = 0;  // last row with bex[b] ≤ x
+            xs[k] = min(xb + k * RJ_JBLOCK + threadIdx.x, x1 - 1);
+            bl[k] = 0;
+          }
 #pragma unroll
-            for (int st2 = RJ_JBLOCK / 2; st2 > 0; st2 >>= 1)
-              if (bex[b + st2] <= x) b += st2;
-            br[k] = brow[c0 + bst[b] + (x - bex[b])];
-            pr[k] = bpr[b];
+          for (int st2 = RJ_JBLOCK / 2; st2 > 0; st2 >>= 1) {
+            uint32_t v[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) v[k] = bex[bl[k] + st2];
+#pragma unroll
+            for (int k = 0; k < U; ++k) bl[k] = v[k] <= xs[k] ? bl[k] + st2 : bl[k];
           }
 #pragma unroll
           for (int k = 0; k < U; ++k) {
-            const uint32_t x = xb + k * RJ_JBLOCK + threadIdx.x;
-            if (x < x1) {
-              oprobe[obase + rel + x] = pr[k];
-              obuild[obase + rel + x] = br[k];
-              if (bmatched) bmatched[br[k]] = 1;
+            const uint32_t b = bl[k];
+            bi[k] = c0 + bst[b] + (xs[k] - bex[b]);
+            br[k] = brow[bi[k]];
+            pr[k] = bpr[b];
+          }
+          if constexpr (MODE == 0) {
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+              const uint32_t x = xb + k * RJ_JBLOCK + threadIdx.x;
+              if (x < x1) {
+                oprobe[obase + rel + x] = pr[k];
+                obuild[obase + rel + x] = br[k];
+                if (bmatched) bmatched[br[k]] = 1;
+              }
+            }
+          } else {
+            bool keep[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) keep[k] = xb + k * RJ_JBLOCK + threadIdx.x < x1;
+            rj_pass<U>(fp, bi, bl, spv, spo, keep);
+            uint32_t c = 0;
+#pragma unroll
+            for (int k = 0; k < U; ++k) c += keep[k] ? 1u : 0u;
+            if constexpr (MODE == 1) {
+              kept += c;
+            } else {
+              uint32_t tot2;
+              const uint32_t ex2 = block_exclusive_scan(c, lds_sc, tot2);
+              int64_t pos = fbase + ex2;
+#pragma unroll
+              for (int k = 0; k < U; ++k)
+                if (keep[k]) {
+                  oprobe[pos] = pr[k];
+                  obuild[pos] = br[k];
+                  ++pos;
+                }
+              fbase += tot2;
             }
           }
         }
@@ -654,6 +773,11 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_emit_ranges(const RJSub *subs,
       }
       rel += tot;
     }
+  }
+  if constexpr (MODE == 1) {
+    uint32_t tk;
+    block_exclusive_scan(kept, lds_sc, tk);
+    if (threadIdx.x == 0) subcnt[blockIdx.x] = tk;
   }
 }
 
@@ -702,7 +826,7 @@ bool radix_join_applies(const Data &l, const Data &r, const std::vector<std::pai
 }
 
 JoinPairs radix_join(Session *s, const Data &l, const Data &r,
-                     const std::vector<std::pair<int, int>> &keys, int32_t join_type) {
+                     const std::vector<std::pair<int, int>> &keys, int32_t join_type, const FtProgram *pred) {
   const bool left_outer = join_type == CAPF_JOIN_LEFT_OUTER || join_type == CAPF_JOIN_FULL_OUTER;
   const bool right_outer = join_type == CAPF_JOIN_RIGHT_OUTER || join_type == CAPF_JOIN_FULL_OUTER;
   // build = the smaller side
@@ -778,10 +902,87 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
     bm = s->alloc(std::max<int64_t>(B.nrows, 1));
     HIP_CHECK(hipMemsetAsync(bm->p, 0, std::max<int64_t>(B.nrows, 1), s->stream));
   }
-  const int64_t cap = total + (p_outer ? Pr.nrows : 0) + (b_outer ? B.nrows : 0);
-  BufPtr oprobe = s->alloc(8 * std::max<int64_t>(cap, 1)), obuild = s->alloc(8 * std::max<int64_t>(cap, 1));
   const char *ranges_env = getenv("CAPF_RJ_RANGES");  // 0 (tuning): one EMIT workgroup per item
   const bool ranges = runs && !(ranges_env && atoi(ranges_env) == 0);
+  if (pred) {  // filtered (radix_join_filtered): inner join, ranges path only
+    if (!ranges || p_outer || b_outer) illegal("radix_join: a filtered join needs the inner ranges path");
+    JoinPairs jp;
+    jp.n = 0;
+    BufPtr oprobe = s->alloc(8), obuild = s->alloc(8);
+    RjPred rp{};
+    std::vector<BufPtr> keep;  // the operand arrays, alive until the EMIT passes are enqueued
+    rp.nt = pred->nt;
+    rp.np = 0;
+    for (int k = 0; k < pred->nt; ++k) {
+      const FtOperand *src[2] = {&pred->t[k].a, &pred->t[k].b};
+      RjOp *dst[2] = {&rp.t[k].a, &rp.t[k].b};
+      for (int j = 0; j < 2; ++j) {
+        *dst[j] = RjOp{nullptr, nullptr, src[j]->lit, src[j]->is_lit, -1};
+        if (src[j]->is_lit) continue;
+        const bool on_build = (src[j]->side == 0) == build_left;
+        const RJSide &sd = on_build ? bs : ps;
+        BufPtr v = s->alloc(8 * std::max<int64_t>(sd.n, 1)), o = s->alloc(std::max<int64_t>(sd.n, 1));
+        if (sd.n > 0) {
+          hipLaunchKernelGGL(k_rj_operand, dim3(grid_for(sd.n, 256)), dim3(256), 0, s->stream, *src[j],
+                             (const uint32_t *)sd.row->p, sd.n, (int64_t *)v->p, (uint8_t *)o->p);
+          KERNEL_CHECK();
+        }
+        keep.push_back(v);
+        keep.push_back(o);
+        if (on_build) {
+          dst[j]->val = (const int64_t *)v->p;
+          dst[j]->ok = (const uint8_t *)o->p;
+        } else {
+          if (rp.np == RJ_PMAX) illegal("radix_join: too many probe-side filter operands");
+          rp.pv[rp.np] = (const int64_t *)v->p;
+          rp.po[rp.np] = (const uint8_t *)o->p;
+          dst[j]->slot = rp.np++;
+        }
+      }
+      rp.t[k].op = pred->t[k].op;
+      rp.t[k].neg = pred->t[k].neg;
+    }
+    if (nw > 0 && total > 0) {
+      BufPtr nsub = s->alloc(8 * nw), soff = s->alloc(8 * (nw + 1));
+      hipLaunchKernelGGL(k_rj_sub_counts, dim3(grid_for(nw, 256)), dim3(256), 0, s->stream,
+                         (const int64_t *)cnt->p, nw, (int64_t *)nsub->p);
+      KERNEL_CHECK();
+      const int64_t ns = exclusive_scan_i64(s, (const int64_t *)nsub->p, (int64_t *)soff->p, nw);
+      BufPtr subs = s->alloc(sizeof(RJSub) * std::max<int64_t>(ns, 1));
+      hipLaunchKernelGGL(k_rj_subs, dim3(grid_for(nw, 256)), dim3(256), 0, s->stream, (const int64_t *)cnt->p,
+                         (const int64_t *)soff->p, nw, (RJSub *)subs->p);
+      KERNEL_CHECK();
+      BufPtr subcnt = s->alloc(8 * ns), suboff = s->alloc(8 * (ns + 1));
+      {
+        KernelTimer kt(s, "rj_join_filter_count", 12.0 * (double)(ps.n + bs.n));
+        hipLaunchKernelGGL(k_rj_emit_ranges<1>, dim3((unsigned)ns), dim3(RJ_JBLOCK), 0, s->stream,
+                           (const RJSub *)subs->p, (const RJWork *)dw->p, (const uint64_t *)bs.h->p,
+                           (const uint32_t *)bs.row->p, (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
+                           (const uint32_t *)ps.row->p, (const int64_t *)off->p, (int64_t *)nullptr,
+                           (int64_t *)nullptr, (uint8_t *)nullptr, (uint8_t *)nullptr, rp, build_left ? 1 : 0,
+                           (int64_t *)subcnt->p, (const int64_t *)nullptr);
+        KERNEL_CHECK();
+      }
+      jp.n = exclusive_scan_i64(s, (const int64_t *)subcnt->p, (int64_t *)suboff->p, ns);
+      if (jp.n > 0) {
+        oprobe = s->alloc(8 * jp.n);
+        obuild = s->alloc(8 * jp.n);
+        KernelTimer kt(s, "rj_join_emit", 12.0 * (double)(ps.n + bs.n) + 16.0 * (double)jp.n);
+        hipLaunchKernelGGL(k_rj_emit_ranges<2>, dim3((unsigned)ns), dim3(RJ_JBLOCK), 0, s->stream,
+                           (const RJSub *)subs->p, (const RJWork *)dw->p, (const uint64_t *)bs.h->p,
+                           (const uint32_t *)bs.row->p, (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
+                           (const uint32_t *)ps.row->p, (const int64_t *)off->p, (int64_t *)oprobe->p,
+                           (int64_t *)obuild->p, (uint8_t *)nullptr, (uint8_t *)nullptr, rp, build_left ? 1 : 0,
+                           (int64_t *)nullptr, (const int64_t *)suboff->p);
+        KERNEL_CHECK();
+      }
+    }
+    jp.left = build_left ? obuild : oprobe;
+    jp.right = build_left ? oprobe : obuild;
+    return jp;
+  }
+  const int64_t cap = total + (p_outer ? Pr.nrows : 0) + (b_outer ? B.nrows : 0);
+  BufPtr oprobe = s->alloc(8 * std::max<int64_t>(cap, 1)), obuild = s->alloc(8 * std::max<int64_t>(cap, 1));
   if (ranges && nw > 0 && total > 0) {
     BufPtr nsub = s->alloc(8 * nw), soff = s->alloc(8 * (nw + 1));
     hipLaunchKernelGGL(k_rj_sub_counts, dim3(grid_for(nw, 256)), dim3(256), 0, s->stream, (const int64_t *)cnt->p,
@@ -793,11 +994,12 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
                        (const int64_t *)soff->p, nw, (RJSub *)subs->p);
     KERNEL_CHECK();
     KernelTimer kt(s, "rj_join_emit", 12.0 * (double)(ps.n + bs.n) + 16.0 * (double)total);
-    hipLaunchKernelGGL(k_rj_emit_ranges, dim3((unsigned)ns), dim3(RJ_JBLOCK), 0, s->stream, (const RJSub *)subs->p,
+    hipLaunchKernelGGL(k_rj_emit_ranges<0>, dim3((unsigned)ns), dim3(RJ_JBLOCK), 0, s->stream, (const RJSub *)subs->p,
                        (const RJWork *)dw->p, (const uint64_t *)bs.h->p, (const uint32_t *)bs.row->p,
                        (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p, (const uint32_t *)ps.row->p,
                        (const int64_t *)off->p, (int64_t *)oprobe->p, (int64_t *)obuild->p,
-                       p_outer ? (uint8_t *)pm->p : nullptr, b_outer ? (uint8_t *)bm->p : nullptr);
+                       p_outer ? (uint8_t *)pm->p : nullptr, b_outer ? (uint8_t *)bm->p : nullptr, RjPred{}, 0,
+                       (int64_t *)nullptr, (const int64_t *)nullptr);
     KERNEL_CHECK();
   } else if (nw > 0 && (total > 0 || p_outer || b_outer)) {
     KernelTimer kt(s, "rj_join_emit", 12.0 * (double)(ps.n + bs.n) + 16.0 * (double)total);
@@ -833,6 +1035,54 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
   jp.right = build_left ? oprobe : obuild;
   jp.n = m;
   return jp;
+}
+
+// The Filter's names are the join's output names: the left input's columns,
+// then the right input's (runtime.cpp, Kind::Join).
+bool radix_join_filtered(Session *s, const Program &pred, const std::vector<std::string> &names, const Data &l,
+                         const Data &r, const std::vector<std::pair<int, int>> &keys, int32_t join_type,
+                         JoinPairs &out) {
+  const char *fe = getenv("CAPF_RJ_FILTER");  // 0 (tuning/tests): join, then filter
+  if (fe && atoi(fe) == 0) return false;
+  if (join_type != CAPF_JOIN_INNER || names.size() != l.cols.size() + r.cols.size()) return false;
+  const char *rn = getenv("CAPF_RJ_RUNS"), *rg = getenv("CAPF_RJ_RANGES");
+  if ((rn && atoi(rn) == 0) || (rg && atoi(rg) == 0)) return false;
+  if (!radix_join_applies(l, r, keys, join_type) || dense_join_possible(s, l, r, keys, join_type)) return false;
+  Data both;
+  both.nrows = 0;
+  both.cols = l.cols;
+  both.cols.insert(both.cols.end(), r.cols.begin(), r.cols.end());
+  FtProgram fp{};
+  if (!ft_compile(pred, names, both, fp)) return false;
+  // the side of every column operand (ft_compile resolved the same names)
+  auto side_of = [&](const std::string &nm) {
+    for (size_t k = 0; k < names.size(); ++k)
+      if (names[k] == nm) return k < l.cols.size() ? 0 : 1;
+    return -1;
+  };
+  size_t pc = 0;
+  const auto &c = pred.code;
+  for (int k = 0; k < fp.nt; ++k) {
+    FtOperand *ops[2] = {&fp.t[k].a, &fp.t[k].b};
+    for (int j = 0; j < 2; ++j) {
+      const Instr &in = c[pc + (size_t)j];
+      if (in.op == OP_COL) {
+        const int sd = side_of(pred.names[(size_t)in.i]);
+        if (sd < 0) return false;
+        ops[j]->side = sd;
+      }
+    }
+    pc += 3;
+    if (pc < c.size() && c[pc].op == OP_NOT) pc += 1;
+  }
+  int per_side[2] = {0, 0};
+  for (int k = 0; k < fp.nt; ++k) {
+    if (!fp.t[k].a.is_lit) ++per_side[fp.t[k].a.side];
+    if (!fp.t[k].b.is_lit) ++per_side[fp.t[k].b.side];
+  }
+  if (per_side[0] > RJ_PMAX || per_side[1] > RJ_PMAX) return false;  // (probe operands live in LDS)
+  out = radix_join(s, l, r, keys, join_type, &fp);
+  return true;
 }
 
 }  // namespace capf

@@ -395,6 +395,26 @@ static DataPtr gather_all(Session *s, const Data &d, const BufPtr &idx, int64_t 
 }
 
 
+// The output of a join node n from its inputs' row indexes (lazy gathers).
+static DataPtr join_output(Session *s, const NodePtr &n, const Data &l, const Data &r, const BufPtr &li,
+                           const BufPtr &ri, int64_t m, int key_alias) {
+  auto out = std::make_shared<Data>();
+  out->nrows = m;
+  bool lnull = n->join_type == CAPF_JOIN_RIGHT_OUTER || n->join_type == CAPF_JOIN_FULL_OUTER;
+  bool rnull = n->join_type == CAPF_JOIN_LEFT_OUTER || n->join_type == CAPF_JOIN_FULL_OUTER;
+  IdxCache cache;  // the columns of one side share one (composed) index
+  for (auto &c : l.cols) out->cols.push_back(gather_lazy(s, c, li, m, lnull, &cache));
+  for (auto &c : r.cols) out->cols.push_back(gather_lazy(s, c, ri, m, rnull, &cache));
+  if (key_alias) {
+    // the build key column of an inner dense join IS the probe key column
+    // (equal values on every row): no gather of it
+    const size_t kl = (size_t)n->join_keys[0].first, kr = l.cols.size() + (size_t)n->join_keys[0].second;
+    if (key_alias == 1) out->cols[kl] = out->cols[kr];
+    else out->cols[kr] = out->cols[kl];
+  }
+  return out;
+}
+
 static DataPtr materialize_impl(const NodePtr &n) {
   Session *s = n->s;
   switch (n->kind) {
@@ -407,8 +427,27 @@ static DataPtr materialize_impl(const NodePtr &n) {
       return out;
     }
     case Kind::Filter: {
-      DataPtr c = materialize(n->kids[0]);
-      return filter_select(s, n->pred, n->kids[0]->names, *c);
+      const NodePtr &k = n->kids[0];
+      if (k->kind == Kind::Join && k->join_type == CAPF_JOIN_INNER) {
+        // WHERE over an inner radix join not materialised yet: the join's EMIT
+        // filters its pairs (radix_join_filtered); the join node itself stays
+        // unmaterialised (another parent would run it unfiltered)
+        bool done;
+        {
+          std::lock_guard<std::mutex> g(k->mu);
+          done = k->result != nullptr;
+        }
+        if (!done) {
+          DataPtr l = materialize(k->kids[0]);
+          DataPtr r = materialize(k->kids[1]);
+          JoinPairs jp;
+          if (radix_join_filtered(s, n->pred, k->names, *l, *r, k->join_keys, k->join_type, jp)) {
+            return join_output(s, k, *l, *r, jp.left, jp.right, jp.n, 0);
+          }
+        }
+      }
+      DataPtr c = materialize(k);
+      return filter_select(s, n->pred, k->names, *c);
     }
     case Kind::Join: {
       DataPtr l = materialize(n->kids[0]);
@@ -430,21 +469,7 @@ static DataPtr materialize_impl(const NodePtr &n) {
         m = jp.n;
         key_alias = jp.key_alias;
       }
-      auto out = std::make_shared<Data>();
-      out->nrows = m;
-      bool lnull = n->join_type == CAPF_JOIN_RIGHT_OUTER || n->join_type == CAPF_JOIN_FULL_OUTER;
-      bool rnull = n->join_type == CAPF_JOIN_LEFT_OUTER || n->join_type == CAPF_JOIN_FULL_OUTER;
-      IdxCache cache;  // the columns of one side share one (composed) index
-      for (auto &c : l->cols) out->cols.push_back(gather_lazy(s, c, li, m, lnull, &cache));
-      for (auto &c : r->cols) out->cols.push_back(gather_lazy(s, c, ri, m, rnull, &cache));
-      if (key_alias) {
-        // the build key column of an inner dense join IS the probe key column
-        // (equal values on every row): no gather of it
-        const size_t kl = (size_t)n->join_keys[0].first, kr = l->cols.size() + (size_t)n->join_keys[0].second;
-        if (key_alias == 1) out->cols[kl] = out->cols[kr];
-        else out->cols[kr] = out->cols[kl];
-      }
-      return out;
+      return join_output(s, n, *l, *r, li, ri, m, key_alias);
     }
     case Kind::Union: {
       DataPtr l = materialize(n->kids[0]);

@@ -314,6 +314,45 @@ def test_filter_over_join_parity(pred, paths, monkeypatch):
     assert bag(got) == bag(want)
 
 
+@pytest.mark.parametrize("pred", JOIN_FILTERS, ids=[str(p) for p in JOIN_FILTERS])
+@pytest.mark.parametrize("fused", ["1", "0"], ids=["fused", "join_then_filter"])
+@pytest.mark.usefixtures("encoding")
+def test_filter_fused_into_radix_join(pred, fused, monkeypatch):
+    """WHERE over an inner radix join: the join's EMIT evaluates the terms per
+    pair and writes only the passing pairs (radix_join.hip radix_join_filtered:
+    a count pass, then the write); CAPF_RJ_FILTER=0 joins, then filters.  Same
+    bag as the oracle; the fused kernels ran exactly when the predicate is a
+    conjunction of terms.  Many-to-many keys, NULL operands, hub keys."""
+    monkeypatch.setenv("CAPF_JOIN", "radix")
+    monkeypatch.setenv("CAPF_RJ_FILTER", fused)
+    rng = np.random.default_rng(13)
+    words = ["p", "q", "r", None]
+    n = 1500
+    kl = [int(v) for v in rng.integers(0, 30, n)]
+    kr = [int(v) for v in rng.integers(0, 30, n)]
+    kl[:300] = [7] * 300  # a hub key: 300 × (its right rows) pairs, split over sub-items
+    kr[:200] = [7] * 200
+    left = [("a", T_INT, [int(v) if rng.random() > 0.1 else None for v in rng.integers(0, 12, n)], None),
+            ("x", T_INT, [int(v) for v in rng.integers(0, 40, n)], None),
+            ("s", T_STRING, [words[i] for i in rng.integers(0, 4, n)], None),
+            ("ka", T_INT, kl, None)]
+    right = [("b", T_INT, [int(v) if rng.random() > 0.1 else None for v in rng.integers(0, 12, n)], None),
+             ("y", T_INT, [int(v) for v in rng.integers(0, 40, n)], None),
+             ("t", T_STRING, [words[i] for i in rng.integers(0, 4, n)], None),
+             ("kb", T_INT, kr, None)]
+    gl, ol = _both(left)
+    gr, orr = _both(right)
+    gs = pytest.gpu_session_ref
+    gs.reset_profile()
+    gs.set_profiling(True)
+    got = gl.join(gr, "inner", ("ka", "kb")).filter(pred, JH, {}).rows
+    gs.set_profiling(False)
+    want = ol.join(orr, "inner", ("ka", "kb")).filter(pred, JH, {}).rows
+    assert len(want) > 0
+    assert ("rj_join_filter_count" in gs.profile()) == (fused == "1" and not isinstance(pred, Ors))
+    assert bag(got) == bag(want)
+
+
 @pytest.mark.parametrize("jt", ["left_outer", "right_outer", "full_outer"])
 @pytest.mark.parametrize("pred", [Not(Equals(Var("x"), Var("y"))), IsNull(Var("c")), IsNotNull(Var("c")),
                                   Ands(Not(Equals(Var("x"), Var("y"))), Equals(Var("c"), IntegerLit(7)))],

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Fused radix filter with batched predicate loads: parity subset + var2 leg (fused / unfused) + kernel trace.
+set -e
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+bash tools/gpu_tests.sh rjf_tests tests/test_gpu_parity.py -m gpu -q -k "filter or join or reference"
+timeout -k 10 300 python -u bench.py --query var2_rows --scale 14 --steps 5 --warmup 2 --no-cpu > gpurun_out/var2_fused.json 2> gpurun_out/var2_fused.err
+CAPF_RJ_FILTER=0 timeout -k 10 300 python -u bench.py --query var2_rows --scale 14 --steps 5 --warmup 2 --no-cpu > gpurun_out/var2_unfused.json 2> gpurun_out/var2_unfused.err
+mkdir -p gpurun_out/prof_var2
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_var2/fused -o var2 --output-format csv -- python3 bench.py --query var2_rows --scale 14 --steps 5 --warmup 2 --no-cpu > gpurun_out/prof_var2/bench.json 2> gpurun_out/prof_var2/trace.log
+echo done

@@ -155,6 +155,33 @@ def tri_cpu_baseline(scale):
                        f"sorted-list intersection (oracle/rmat.c count_triangle_trace) in {el:.2f}s on {th} threads")}
 
 
+def c2_cpu_baseline(graph, scale):
+    """Config 2 on the host: the count over the Flink plan's inputs (Person ids,
+    all node ids, rels) as vectorised numpy on one thread — membership arrays
+    for the two node scans (the hash-table builds), then one pass over the rels
+    (the probes); the whole workload, no sample needed (well under a second)."""
+    import numpy as np
+    rel = graph.rel_tables[0].table
+    src, _ = rel.column_arrays("source")
+    dst, _ = rel.column_arrays("target")
+    pid, _ = graph.node_tables[0].table.column_arrays("id")
+    oid, _ = graph.node_tables[1].table.column_arrays("id")
+    src, dst = np.asarray(src, dtype=np.int64), np.asarray(dst, dtype=np.int64)
+    pid, oid = np.asarray(pid, dtype=np.int64), np.asarray(oid, dtype=np.int64)
+    n = 1 << scale
+    t0 = time.perf_counter()
+    person = np.zeros(n, dtype=bool)
+    person[pid] = True
+    exists = person.copy()
+    exists[oid] = True
+    ok = (src >= 0) & (src < n) & (dst >= 0) & (dst < n)
+    count = int(np.count_nonzero(person[np.where(ok, src, 0)] & exists[np.where(ok, dst, 0)] & ok))
+    el = time.perf_counter() - t0
+    return {"value": count / el, "unit": "joined rows/s", "cores": 1, **cpu_info(1), "kind": "port", "count": count,
+            "sample": (f"whole R-MAT s{scale} workload ({len(src)} rels): (a:Person)-->(b) count by numpy "
+                       f"membership arrays in {el:.3f}s on 1 thread")}
+
+
 def cpu_baseline(session, graph, scale, budget_s):
     """Flink-shaped pipelined hash join (oracle/rmat.c) on the host cores over
     a bounded sample of the same workload: hash tables are built on the full
@@ -645,6 +672,10 @@ def run_single(args):
         result["cpu_baseline"] = cpu_baseline(s, g, args.scale, args.cpu_seconds)
     if not args.no_cpu and args.query == "triangle":
         result["cpu_baseline"] = tri_cpu_baseline(args.scale)
+    if not args.no_cpu and args.query == "one_hop_person":
+        result["cpu_baseline"] = c2_cpu_baseline(g, args.scale)
+        if result["cpu_baseline"]["count"] != count:
+            raise SystemExit("config 2: the host count differs from the GPU count")
     print(json.dumps(result))
 
 

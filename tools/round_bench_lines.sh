@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 bench lines: headline (default run + rocprof/PMC), config 2, triangle with its CPU baseline.
+# Bench lines of a round (not a test): headline (default run + rocprof/PMC), config 2, triangle with its CPU baseline.
 set -e
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 300 python -u bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Triangle: guard-free lockstep searches (prefix table + staged list), ILP 2 / 3 / 4.
+# Triangle count variants (not a test): parity subset, then s24 timing by CAPF_TRI_HASH (0 = sorted LDS copy, 1024 = LDS hash) and CAPF_TRI_ILP.
 set -e
 cd $GRAFT_REPO_ROOT
 bash tools/gpu_tests.sh tri_tests_e tests/test_gpu_parity.py -m gpu -q -k "triangle"

@@ -393,6 +393,8 @@ __device__ inline bool tri_esc(uint32_t word) { return ((word >> 24) & 15u) == 1
 // loaded but not searched, 2 = searched but not loaded (a synthetic id per
 // position) — the time split of the count kernels between loads and searches
 __constant__ int c_tri_diag;
+// CAPF_TRI_GALLOP=1 (tuning): batch owners by galloping + a narrowed search
+__constant__ int c_tri_gallop;
 
 // (f, b) of a packed word, or of vals[e] when a nibble says "look it up"
 __device__ inline uint2 tri_fb(uint32_t word, const uint2 *vals, uint32_t e) {
@@ -441,20 +443,43 @@ __device__ inline void tri_row_packed(uint32_t nb, uint32_t ns, const uint32_t *
     if (lane == 0) probes += total;
     __builtin_amdgcn_wave_barrier();
     uint32_t w[2][ILP], pos[2][ILP], bi[2][ILP];
+    uint32_t bcur = 0;  // owner of the last position issued (owners only grow along the batch)
     auto issue = [&](uint32_t t0, uint32_t (&ww)[ILP], uint32_t (&pp)[ILP], uint32_t (&bb)[ILP]) {
       uint32_t xc[ILP];
 #pragma unroll
-      for (int u = 0; u < ILP; ++u) {
-        xc[u] = min(t0 + u * WAVE + lane, total - 1);
-        bb[u] = 0;  // last batch entry with pre[b] <= xc (the ILP searches in lockstep)
-      }
+      for (int u = 0; u < ILP; ++u) xc[u] = min(t0 + u * WAVE + lane, total - 1);
+      if (c_tri_gallop) {
+        // the owners (last batch entry with pre[b] <= x) of a slice of 64
+        // consecutive positions span [first lane's, last lane's]: both found by
+        // galloping from the previous slice (wave-uniform, usually 0-2 steps),
+        // then each lane halves that span (usually 1-3 entries) instead of
+        // searching all 64 entries
 #pragma unroll
-      for (int st = WAVE / 2; st > 0; st >>= 1) {
-        uint32_t v[ILP];
+        for (int u = 0; u < ILP; ++u) {
+          const uint32_t xf = min(t0 + u * WAVE, total - 1), xl = min(t0 + u * WAVE + WAVE - 1, total - 1);
+          while ((uint32_t)__builtin_amdgcn_readfirstlane(tb.pre[bcur + 1]) <= xf) ++bcur;
+          uint32_t bh = bcur;
+          while ((uint32_t)__builtin_amdgcn_readfirstlane(tb.pre[bh + 1]) <= xl) ++bh;
+          uint32_t base = bcur;
+          for (uint32_t len = bh - bcur + 1; len > 1;) {
+            const uint32_t half = len >> 1;
+            base = tb.pre[base + half] <= xc[u] ? base + half : base;
+            len -= half;
+          }
+          bb[u] = base;
+          bcur = bh;
+        }
+      } else {
 #pragma unroll
-        for (int u = 0; u < ILP; ++u) v[u] = tb.pre[bb[u] + st];
+        for (int u = 0; u < ILP; ++u) bb[u] = 0;  // the ILP searches over all 64 entries in lockstep
 #pragma unroll
-        for (int u = 0; u < ILP; ++u) bb[u] = v[u] <= xc[u] ? bb[u] + st : bb[u];
+        for (int st = WAVE / 2; st > 0; st >>= 1) {
+          uint32_t v[ILP];
+#pragma unroll
+          for (int u = 0; u < ILP; ++u) v[u] = tb.pre[bb[u] + st];
+#pragma unroll
+          for (int u = 0; u < ILP; ++u) bb[u] = v[u] <= xc[u] ? bb[u] + st : bb[u];
+        }
       }
 #pragma unroll
       for (int u = 0; u < ILP; ++u) {
@@ -488,6 +513,7 @@ __device__ inline void tri_row_packed(uint32_t nb, uint32_t ns, const uint32_t *
         }
       }
     };
+    if (c_tri_diag == 3) continue;  // (profiling only: staging and batch tables, no probes)
     if (total > 0) issue(0, w[0], pos[0], bi[0]);
     for (uint32_t t0 = 0; t0 < total; t0 += 2 * STEP) {
       if (t0 + STEP < total) issue(t0 + STEP, w[1], pos[1], bi[1]);
@@ -732,7 +758,7 @@ struct TriPassB {
 template <int ILP, int HCAP = 0>
 __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_passb(const uint32_t *rowptr, const uint32_t *pcols,
                                                                 const uint2 *vals, TriPassB b, int parts,
-                                                                int part, unsigned long long *cursor,
+                                                                int part, int grab, unsigned long long *cursor,
                                                                 unsigned long long *acc) {
   // HCAP > 0: staged lists of ≤ HCAP words hashed into 2·HCAP slots; 0: sorted copies of ≤ TRI_CAP
   constexpr bool HASH = HCAP > 0;
@@ -749,9 +775,9 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_passb(const uint32_t *r
   for (;;) {
     unsigned long long c0 = 0;
     if (lane == 0) c0 = atomicAdd(cursor, 1ull);
-    c0 = ((unsigned long long)__shfl((long long)c0, 0, WAVE) * parts + part) * 4;
+    c0 = ((unsigned long long)__shfl((long long)c0, 0, WAVE) * parts + part) * grab;
     if (c0 >= b.nitems) break;
-    const uint64_t c1 = min<uint64_t>(c0 + 4, b.nitems);
+    const uint64_t c1 = min<uint64_t>(c0 + grab, b.nitems);
     for (uint64_t it = c0; it < c1; ++it) {
       const uint4 item = b.items[it];
       const uint32_t q = item.x;
@@ -988,7 +1014,7 @@ template <int ILP, int HCAP = 0>
 __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_qtiled(const uint32_t *rowptr, const uint32_t *pcols,
                                                                  const uint2 *vals, const uint2 *erow,
                                                                  const uint4 *items,
-                                                                 uint32_t nitems, int parts, int part,
+                                                                 uint32_t nitems, int parts, int part, int grab,
                                                                  unsigned long long *cursor,
                                                                  unsigned long long *acc) {
   // HCAP > 0: staged lists of ≤ HCAP words hashed into 2·HCAP slots; 0: sorted copies of ≤ TRI_CAP
@@ -1006,9 +1032,9 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_qtiled(const uint32_t *
   for (;;) {
     unsigned long long c0 = 0;
     if (lane == 0) c0 = atomicAdd(cursor, 1ull);
-    c0 = ((unsigned long long)__shfl((long long)c0, 0, WAVE) * parts + part) * 4;
+    c0 = ((unsigned long long)__shfl((long long)c0, 0, WAVE) * parts + part) * grab;
     if (c0 >= nitems) break;
-    const uint64_t c1 = min<uint64_t>(c0 + 4, nitems);
+    const uint64_t c1 = min<uint64_t>(c0 + grab, nitems);
     for (uint64_t it = c0; it < c1; ++it) {
       const uint4 item = items[it];
       const uint32_t p = item.x, k0 = item.y, nb = item.z - item.y;
@@ -1281,10 +1307,16 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
   const TriGraph &g = *gp;
   {
     static const int diag = getenv("CAPF_TRI_DIAG") ? atoi(getenv("CAPF_TRI_DIAG")) : 0;
-    static bool set = false;
-    if (diag && !set) {
+    // CAPF_TRI_GALLOP=1 (tuning, off): s24 318.5 vs 320.1 ms — no gain
+    const int gallop = getenv("CAPF_TRI_GALLOP") ? atoi(getenv("CAPF_TRI_GALLOP")) : 0;
+    static int set_diag = -1, set_gallop = -1;
+    if (diag != set_diag) {
       HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_tri_diag), &diag, sizeof(int)));
-      set = true;
+      set_diag = diag;
+    }
+    if (gallop != set_gallop) {
+      HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_tri_gallop), &gallop, sizeof(int)));
+      set_gallop = gallop;
     }
   }
   // per-query accumulators: T, the cached pair-loop term, Σ L(L−1)(L−2), the
@@ -1312,6 +1344,14 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
     // 512 / 1024 = lists up to that many words hashed in LDS (longer: global search)
     // (s24, lockstep searches: sorted 314 ms, hash 1024 454 ms — kept off)
     const int hash = getenv("CAPF_TRI_HASH") ? atoi(getenv("CAPF_TRI_HASH")) : 0;
+    // work items per dequeue of the shared cursor (tuning).  One cursor word
+    // serves ≈ 88 dequeues/µs (MI355X_MICROARCH.md): with no probes
+    // (CAPF_TRI_DIAG=3) pass A's 2.1e7 items (s24) take 64 ms at 4 per grab and
+    // 9.5 ms at 32 — but with the probes the kernels dequeue at half that rate,
+    // and larger grabs widen the window of items in flight beyond what the
+    // caches hold: 4/4 319 ms, 32/8 415, 64/16 511, 128/32 720 ms
+    const int grab_a = std::max(1, getenv("CAPF_TRI_GRAB_A") ? atoi(getenv("CAPF_TRI_GRAB_A")) : 4);
+    const int grab_b = std::max(1, getenv("CAPF_TRI_GRAB_B") ? atoi(getenv("CAPF_TRI_GRAB_B")) : 4);
     // CAPF_TRI_TWOPASS=0 (tuning): one pass, every wedge streamed from N+(q)
     const bool two = packed && g.pcols && g.in_words && !(getenv("CAPF_TRI_TWOPASS") && atoi(getenv("CAPF_TRI_TWOPASS")) == 0);
     if (packed && g.pcols) {
@@ -1324,7 +1364,7 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
           hipLaunchKernelGGL(kq, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
                              (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
                              (const uint2 *)g.vals->p, g.erow ? (const uint2 *)g.erow->p : nullptr,
-                             (const uint4 *)g.aitems->p, g.naitems, parts, part,
+                             (const uint4 *)g.aitems->p, g.naitems, parts, part, grab_a,
                              acc + 3, acc);
         }
       } else {
@@ -1352,7 +1392,7 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
                                  : (ilp <= 2 ? k_tri_count_passb<2> : ilp == 3 ? k_tri_count_passb<3> : k_tri_count_passb<4>);
         hipLaunchKernelGGL(kb, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
                            (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p, (const uint2 *)g.vals->p,
-                           b, parts, part, acc + 6, acc);
+                           b, parts, part, grab_b, acc + 6, acc);
       }
     } else {
       KernelTimer kt(s, "tri_count", 4.0 * g.P);

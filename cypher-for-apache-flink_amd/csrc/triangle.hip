@@ -747,6 +747,23 @@ constexpr uint32_t TRI_BCHUNK = 1024;
 // row by row 350 ms, 2^23 268, 2^24 220, 2^25 190, 2^26 184 ms
 constexpr int TRI_QTILE_DEFAULT = 26;
 
+// First item of the wave's next grab.  xcd = 0: one cursor, grabs in order.
+// xcd = 1: the grabs are dealt to the 8 XCD groups (blocks b, b + 8, … share an
+// XCD and its L2) in chunks of TRI_XCHUNK consecutive grabs, each group with
+// its own cursor (cursor[32·g], a line of its own): every XCD walks the item
+// order at the same pace, its L2 seeing contiguous chunks.  Either way grab
+// index g covers items [(g·parts + part)·grab, … + grab).
+constexpr unsigned long long TRI_XCHUNK = 64;
+__device__ inline unsigned long long tri_dequeue(unsigned long long *cursor, int xcd, int parts, int part,
+                                                 int grab) {
+  const unsigned long long xg = xcd ? (blockIdx.x & 7u) : 0ull;
+  unsigned long long c0 = 0;
+  if (lane_id() == 0) c0 = atomicAdd(cursor + 32 * xg, 1ull);
+  c0 = (unsigned long long)__shfl((long long)c0, 0, WAVE);
+  if (xcd) c0 = ((c0 / TRI_XCHUNK) * 8 + xg) * TRI_XCHUNK + c0 % TRI_XCHUNK;
+  return (c0 * parts + part) * grab;
+}
+
 struct TriPassB {
   const uint32_t *in_words;   // p | multiplicity nibbles of the pair p–q, by (p-block, q, p)
   const uint2 *in_rows;       // the same entries as {start of N+(p), |N+(p)| | nibbles << 24}, or null
@@ -758,7 +775,8 @@ struct TriPassB {
 template <int ILP, int HCAP = 0>
 __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_passb(const uint32_t *rowptr, const uint32_t *pcols,
                                                                 const uint2 *vals, TriPassB b, int parts,
-                                                                int part, int grab, unsigned long long *cursor,
+                                                                int part, int grab, int xcd,
+                                                                unsigned long long *cursor,
                                                                 unsigned long long *acc) {
   // HCAP > 0: staged lists of ≤ HCAP words hashed into 2·HCAP slots; 0: sorted copies of ≤ TRI_CAP
   constexpr bool HASH = HCAP > 0;
@@ -773,9 +791,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_passb(const uint32_t *r
   uint32_t staged = 0xFFFFFFFFu;  // q whose list sits in sc
   TriHash h{};
   for (;;) {
-    unsigned long long c0 = 0;
-    if (lane == 0) c0 = atomicAdd(cursor, 1ull);
-    c0 = ((unsigned long long)__shfl((long long)c0, 0, WAVE) * parts + part) * grab;
+    const unsigned long long c0 = tri_dequeue(cursor, xcd, parts, part, grab);
     if (c0 >= b.nitems) break;
     const uint64_t c1 = min<uint64_t>(c0 + grab, b.nitems);
     for (uint64_t it = c0; it < c1; ++it) {
@@ -1015,6 +1031,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_qtiled(const uint32_t *
                                                                  const uint2 *vals, const uint2 *erow,
                                                                  const uint4 *items,
                                                                  uint32_t nitems, int parts, int part, int grab,
+                                                                 int xcd,
                                                                  unsigned long long *cursor,
                                                                  unsigned long long *acc) {
   // HCAP > 0: staged lists of ≤ HCAP words hashed into 2·HCAP slots; 0: sorted copies of ≤ TRI_CAP
@@ -1030,9 +1047,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_qtiled(const uint32_t *
   uint32_t staged = 0xFFFFFFFFu;  // p whose list sits in sc
   TriHash h{};
   for (;;) {
-    unsigned long long c0 = 0;
-    if (lane == 0) c0 = atomicAdd(cursor, 1ull);
-    c0 = ((unsigned long long)__shfl((long long)c0, 0, WAVE) * parts + part) * grab;
+    const unsigned long long c0 = tri_dequeue(cursor, xcd, parts, part, grab);
     if (c0 >= nitems) break;
     const uint64_t c1 = min<uint64_t>(c0 + grab, nitems);
     for (uint64_t it = c0; it < c1; ++it) {
@@ -1322,6 +1337,10 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
   // per-query accumulators: T, the cached pair-loop term, Σ L(L−1)(L−2), the
   // row cursor, probes, hits
   BufPtr qacc = s->alloc(64);  // + [6] the pass-B cursor
+  // per-XCD-group cursors of the q-tiled pass A and of pass B (tri_dequeue)
+  BufPtr xcur = s->alloc(2 * 8 * 32 * 8);
+  HIP_CHECK(hipMemsetAsync(xcur->p, 0, 2 * 8 * 32 * 8, s->stream));
+  unsigned long long *xa = (unsigned long long *)xcur->p, *xb = xa + 8 * 32;
   HIP_CHECK(hipMemsetAsync(qacc->p, 0, 64, s->stream));
   if (part == 0)
     HIP_CHECK(hipMemcpyAsync((char *)qacc->p + 8, (const char *)g.acc->p + 8, 8,
@@ -1350,8 +1369,13 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
     // 9.5 ms at 32 — but with the probes the kernels dequeue at half that rate,
     // and larger grabs widen the window of items in flight beyond what the
     // caches hold: 4/4 319 ms, 32/8 415, 64/16 511, 128/32 720 ms
-    const int grab_a = std::max(1, getenv("CAPF_TRI_GRAB_A") ? atoi(getenv("CAPF_TRI_GRAB_A")) : 4);
+    const int grab_a = std::max(1, getenv("CAPF_TRI_GRAB_A") ? atoi(getenv("CAPF_TRI_GRAB_A")) : 2);
     const int grab_b = std::max(1, getenv("CAPF_TRI_GRAB_B") ? atoi(getenv("CAPF_TRI_GRAB_B")) : 4);
+    // CAPF_TRI_XCD_A / _B (tuning): 1 = grabs dealt to the XCD groups in chunks
+    // (tri_dequeue).  s24, one box: A/B one cursor 121/223 ms; per XCD group,
+    // grabs 4/4 109/238, 2/2 103/229, 1/1 109/220 — on for pass A (grab 2) only
+    const int xcd_a = getenv("CAPF_TRI_XCD_A") ? atoi(getenv("CAPF_TRI_XCD_A")) : 1;
+    const int xcd_b = getenv("CAPF_TRI_XCD_B") ? atoi(getenv("CAPF_TRI_XCD_B")) : 0;
     // CAPF_TRI_TWOPASS=0 (tuning): one pass, every wedge streamed from N+(q)
     const bool two = packed && g.pcols && g.in_words && !(getenv("CAPF_TRI_TWOPASS") && atoi(getenv("CAPF_TRI_TWOPASS")) == 0);
     if (packed && g.pcols) {
@@ -1364,8 +1388,8 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
           hipLaunchKernelGGL(kq, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
                              (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
                              (const uint2 *)g.vals->p, g.erow ? (const uint2 *)g.erow->p : nullptr,
-                             (const uint4 *)g.aitems->p, g.naitems, parts, part, grab_a,
-                             acc + 3, acc);
+                             (const uint4 *)g.aitems->p, g.naitems, parts, part, grab_a, xcd_a,
+                             xcd_a ? xa : acc + 3, acc);
         }
       } else {
         KernelTimer kt(s, "tri_count_packed", 4.0 * g.P);
@@ -1392,7 +1416,7 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
                                  : (ilp <= 2 ? k_tri_count_passb<2> : ilp == 3 ? k_tri_count_passb<3> : k_tri_count_passb<4>);
         hipLaunchKernelGGL(kb, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
                            (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p, (const uint2 *)g.vals->p,
-                           b, parts, part, grab_b, acc + 6, acc);
+                           b, parts, part, grab_b, xcd_b, xcd_b ? xb : acc + 6, acc);
       }
     } else {
       KernelTimer kt(s, "tri_count", 4.0 * g.P);

@@ -742,7 +742,8 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_packed(const uint32_t *
 // in-list spreads over waves) stream their N+(p) and binary-search each w in
 // N+(q).  Σ min(|N+(p)|, |N+(q)|) over the edges is ~2.2× below the one-pass
 // Σ |N+(q)| on R-MAT (s18 / s20).
-constexpr uint32_t TRI_BCHUNK = 1024;
+// (s24, one box: 256 217.6 ms, 1024 223.6, 4096 231.2, 16384 235.6 — pass B)
+constexpr uint32_t TRI_BCHUNK = 256;
 // pass-A tile size (log2 words; 0 = row by row).  s24 (profiles/r04_tri_sweep.txt):
 // row by row 350 ms, 2^23 268, 2^24 220, 2^25 190, 2^26 184 ms
 constexpr int TRI_QTILE_DEFAULT = 26;
@@ -889,17 +890,17 @@ __global__ void k_tri_segkeys(const uint64_t *skeys, uint32_t n, uint64_t *seg) 
 }
 
 // items of segment j (a run of equal (p-block, q)): ⌈cnt / TRI_BCHUNK⌉ chunks
-__global__ void k_tri_seg_items(const uint32_t *cnt, uint32_t nseg, uint32_t *nitems) {
+__global__ void k_tri_seg_items(const uint32_t *cnt, uint32_t nseg, uint32_t bchunk, uint32_t *nitems) {
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nseg; j += gridDim.x * blockDim.x)
-    nitems[j] = (cnt[j] + TRI_BCHUNK - 1) / TRI_BCHUNK;
+    nitems[j] = (cnt[j] + bchunk - 1) / bchunk;
 }
 
 __global__ void k_tri_seg_fill(const uint64_t *useg, const uint32_t *cnt, const uint32_t *start,
-                               const uint32_t *istart, uint32_t nseg, uint4 *items) {
+                               const uint32_t *istart, uint32_t nseg, uint32_t bchunk, uint4 *items) {
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nseg; j += gridDim.x * blockDim.x) {
     const uint32_t q = (uint32_t)(useg[j] & 0xFFFFFFu), c = cnt[j], s0 = start[j];
-    for (uint32_t i = 0; i * TRI_BCHUNK < c; ++i)
-      items[istart[j] + i] = make_uint4(q, s0 + i * TRI_BCHUNK, min(TRI_BCHUNK, c - i * TRI_BCHUNK), 0u);
+    for (uint32_t i = 0; i * bchunk < c; ++i)
+      items[istart[j] + i] = make_uint4(q, s0 + i * bchunk, min(bchunk, c - i * bchunk), 0u);
   }
 }
 
@@ -1005,8 +1006,10 @@ static void tri_build_passb(Session *s, const uint64_t *okey, TriGraph &g) {
     return rocprim::exclusive_scan(t, n, (const uint32_t *)cnt->p, (uint32_t *)start->p, 0u, (size_t)nseg,
                                    rocprim::plus<uint32_t>(), s->stream);
   });
+  // CAPF_TRI_BCHUNK (tuning): in-list entries per pass-B work item
+  const uint32_t bchunk = getenv("CAPF_TRI_BCHUNK") ? (uint32_t)std::max(64, atoi(getenv("CAPF_TRI_BCHUNK"))) : TRI_BCHUNK;
   hipLaunchKernelGGL(k_tri_seg_items, dim3(grid_for(nseg, 256, 256 * 64)), dim3(256), 0, s->stream,
-                     (const uint32_t *)cnt->p, nseg, (uint32_t *)nit->p);
+                     (const uint32_t *)cnt->p, nseg, bchunk, (uint32_t *)nit->p);
   KERNEL_CHECK();
   HIP_CHECK(hipMemsetAsync((uint32_t *)nit->p + nseg, 0, 4, s->stream));
   rocprim_call(s, [&](void *t, size_t &n) {
@@ -1018,7 +1021,7 @@ static void tri_build_passb(Session *s, const uint64_t *okey, TriGraph &g) {
   g.items = s->alloc(16 * std::max<uint32_t>(g.nitems, 1));
   hipLaunchKernelGGL(k_tri_seg_fill, dim3(grid_for(nseg, 256, 256 * 64)), dim3(256), 0, s->stream,
                      (const uint64_t *)useg->p, (const uint32_t *)cnt->p, (const uint32_t *)start->p,
-                     (const uint32_t *)istart->p, nseg, (uint4 *)g.items->p);
+                     (const uint32_t *)istart->p, nseg, bchunk, (uint4 *)g.items->p);
   KERNEL_CHECK();
   s->sync();  // the temporaries go back to the pool
 }

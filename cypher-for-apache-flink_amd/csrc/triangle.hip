@@ -606,6 +606,60 @@ __device__ inline TriSorted<A> tri_sorted(A at, uint32_t n, uint32_t a) {
   return TriSorted<A>{at, n, a};
 }
 
+// The same search over an LDS copy that holds the ids alone (the nibbles in a
+// byte array beside it): no mask per step; the packed word is rebuilt on a hit.
+struct TriSortedIds {
+  const uint32_t *ids;
+  const uint8_t *nib;
+  uint32_t n, a;
+  template <int ILP>
+  __device__ inline void batch(const uint32_t (&wk)[ILP], const bool (&live)[ILP], bool (&hit)[ILP],
+                               uint32_t (&pw)[ILP], uint32_t (&pos)[ILP]) const {
+    const uint32_t nu = __builtin_amdgcn_readfirstlane(n);
+    if (nu == 0) {
+#pragma unroll
+      for (int u = 0; u < ILP; ++u) hit[u] = false;
+      return;
+    }
+    uint32_t base[ILP];
+#pragma unroll
+    for (int u = 0; u < ILP; ++u) base[u] = 0;
+    for (uint32_t len = nu; len > 1;) {
+      const uint32_t half = len >> 1;
+      uint32_t v[ILP];
+#pragma unroll
+      for (int u = 0; u < ILP; ++u) v[u] = ids[base[u] + half];
+#pragma unroll
+      for (int u = 0; u < ILP; ++u) base[u] = v[u] < wk[u] ? base[u] + half : base[u];
+      len -= half;
+    }
+    uint32_t v0[ILP], v1[ILP];
+#pragma unroll
+    for (int u = 0; u < ILP; ++u) {
+      v0[u] = ids[base[u]];
+      v1[u] = ids[min(base[u] + 1, nu - 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < ILP; ++u) {
+      const bool first = v0[u] == wk[u];
+      const bool second = v1[u] == wk[u] && base[u] + 1 < nu;
+      hit[u] = live[u] && (first || second);
+      const uint32_t at = base[u] + (first ? 0u : 1u);
+      pos[u] = a + at;
+      pw[u] = hit[u] ? wk[u] | (uint32_t)nib[min(at, nu - 1)] << 24 : 0u;
+    }
+  }
+};
+
+// stage row[0..n) into the ids / nibbles LDS copy
+__device__ inline void tri_stage_ids(uint32_t *ids, uint8_t *nib, const uint32_t *row, uint32_t n) {
+  for (uint32_t k = lane_id(); k < n; k += WAVE) {
+    const uint32_t w = row[k];
+    ids[k] = w & TRI_M24;
+    nib[k] = (uint8_t)(w >> 24);
+  }
+}
+
 // ------------------------------------------------- LDS hash of a staged list
 // A staged list (≤ TRI_CAP words) is searched through an open-addressing table
 // in the wave's LDS slice instead of a binary search over its sorted copy: one
@@ -689,10 +743,12 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_packed(const uint32_t *
   constexpr bool HASH = HCAP > 0;
   constexpr uint32_t CAP = HASH ? HCAP : TRI_CAP;
   __shared__ __attribute__((aligned(16))) uint32_t s_cols[TRI_BLOCK / WAVE][HASH ? 2 * HCAP : TRI_CAP];
+  __shared__ uint8_t s_nib[TRI_BLOCK / WAVE][HASH ? 1 : TRI_CAP];
   __shared__ TriBatch2 s_tab[TRI_BLOCK / WAVE];
   __shared__ unsigned long long lds[17];
   const int wv = threadIdx.x / WAVE, lane = lane_id();
   uint32_t *sc = s_cols[wv];
+  uint8_t *sn = s_nib[wv];
   TriBatch2 &tb = s_tab[wv];
   unsigned long long t = 0, probes = 0, hits = 0;
   for (;;) {
@@ -718,11 +774,10 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_packed(const uint32_t *
                                    TriHashFind{h},
                                    pqe, t, probes, hits);
       } else {
-        for (uint32_t k = lane; k < dp; k += WAVE) sc[k] = row[k];
+        tri_stage_ids(sc, sn, row, dp);
         __builtin_amdgcn_wave_barrier();
-        tri_row_packed<ILP, SPLIT>(dp, dp, pcols, vals, tb, [&](uint32_t k) { return tri_qrow(rowptr, sc[k]); },
-                                   tri_sorted([&](uint32_t x) { return sc[x]; }, dp, a),
-                                   pqe, t, probes, hits);
+        tri_row_packed<ILP, SPLIT>(dp, dp, pcols, vals, tb, [&](uint32_t k) { return tri_qrow(rowptr, row[k]); },
+                                   TriSortedIds{sc, sn, dp, a}, pqe, t, probes, hits);
       }
       __builtin_amdgcn_wave_barrier();  // sc is rewritten by the next row
     }
@@ -774,7 +829,7 @@ struct TriPassB {
 };
 
 template <int ILP, int HCAP = 0>
-__global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_passb(const uint32_t *rowptr, const uint32_t *pcols,
+__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(5))) void k_tri_count_passb(const uint32_t *rowptr, const uint32_t *pcols,
                                                                 const uint2 *vals, TriPassB b, int parts,
                                                                 int part, int grab, int xcd,
                                                                 unsigned long long *cursor,
@@ -783,10 +838,12 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_passb(const uint32_t *r
   constexpr bool HASH = HCAP > 0;
   constexpr uint32_t CAP = HASH ? HCAP : TRI_CAP;
   __shared__ __attribute__((aligned(16))) uint32_t s_cols[TRI_BLOCK / WAVE][HASH ? 2 * HCAP : TRI_CAP];
+  __shared__ uint8_t s_nib[TRI_BLOCK / WAVE][HASH ? 1 : TRI_CAP];
   __shared__ TriBatch2 s_tab[TRI_BLOCK / WAVE];
   __shared__ unsigned long long lds[17];
-  const int wv = threadIdx.x / WAVE, lane = lane_id();
+  const int wv = threadIdx.x / WAVE;
   uint32_t *sc = s_cols[wv];
+  uint8_t *sn = s_nib[wv];
   TriBatch2 &tb = s_tab[wv];
   unsigned long long t = 0, probes = 0, hits = 0;
   uint32_t staged = 0xFFFFFFFFu;  // q whose list sits in sc
@@ -823,12 +880,11 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_passb(const uint32_t *r
       } else {
         if (q != staged) {
           __builtin_amdgcn_wave_barrier();  // the previous list's searches are done
-          for (uint32_t k = lane; k < dq; k += WAVE) sc[k] = row[k];
+          tri_stage_ids(sc, sn, row, dq);
           __builtin_amdgcn_wave_barrier();
           staged = q;
         }
-        tri_row_packed<ILP, false, true>(n, dq, pcols, vals, tb, qs,
-                                         tri_sorted([&](uint32_t x) { return sc[x]; }, dq, a),
+        tri_row_packed<ILP, false, true>(n, dq, pcols, vals, tb, qs, TriSortedIds{sc, sn, dq, a},
                                          pqe, t, probes, hits);
       }
     }
@@ -1030,7 +1086,7 @@ static void tri_build_passb(Session *s, const uint64_t *okey, TriGraph &g) {
 // the q's N+(p)[k0, k1) — N+(p) staged in LDS (≤ TRI_CAP words) or searched in
 // place — with the pass-A rule (edges with |N+(p)| < |N+(q)| belong to pass B).
 template <int ILP, int HCAP = 0>
-__global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_qtiled(const uint32_t *rowptr, const uint32_t *pcols,
+__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(5))) void k_tri_count_qtiled(const uint32_t *rowptr, const uint32_t *pcols,
                                                                  const uint2 *vals, const uint2 *erow,
                                                                  const uint4 *items,
                                                                  uint32_t nitems, int parts, int part, int grab,
@@ -1041,10 +1097,12 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_qtiled(const uint32_t *
   constexpr bool HASH = HCAP > 0;
   constexpr uint32_t CAP = HASH ? HCAP : TRI_CAP;
   __shared__ __attribute__((aligned(16))) uint32_t s_cols[TRI_BLOCK / WAVE][HASH ? 2 * HCAP : TRI_CAP];
+  __shared__ uint8_t s_nib[TRI_BLOCK / WAVE][HASH ? 1 : TRI_CAP];
   __shared__ TriBatch2 s_tab[TRI_BLOCK / WAVE];
   __shared__ unsigned long long lds[17];
-  const int wv = threadIdx.x / WAVE, lane = lane_id();
+  const int wv = threadIdx.x / WAVE;
   uint32_t *sc = s_cols[wv];
+  uint8_t *sn = s_nib[wv];
   TriBatch2 &tb = s_tab[wv];
   unsigned long long t = 0, probes = 0, hits = 0;
   uint32_t staged = 0xFFFFFFFFu;  // p whose list sits in sc
@@ -1078,12 +1136,11 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_qtiled(const uint32_t *
       } else {
         if (p != staged) {
           __builtin_amdgcn_wave_barrier();  // the previous list's searches are done
-          for (uint32_t k = lane; k < dp; k += WAVE) sc[k] = row[k];
+          tri_stage_ids(sc, sn, row, dp);
           __builtin_amdgcn_wave_barrier();
           staged = p;
         }
-        tri_row_packed<ILP, true>(nb, dp, pcols, vals, tb, qrow,
-                                  tri_sorted([&](uint32_t x) { return sc[x]; }, dp, a),
+        tri_row_packed<ILP, true>(nb, dp, pcols, vals, tb, qrow, TriSortedIds{sc, sn, dp, a},
                                   pqe, t, probes, hits);
       }
     }

@@ -470,16 +470,25 @@ __device__ inline void tri_row_packed(uint32_t nb, uint32_t ns, const uint32_t *
           bcur = bh;
         }
       } else {
+        // the ILP searches over all 64 entries in lockstep (positions as pointers:
+        // one add per step gives the probe address)
+        const uint32_t *bp[ILP];
 #pragma unroll
-        for (int u = 0; u < ILP; ++u) bb[u] = 0;  // the ILP searches over all 64 entries in lockstep
+        for (int u = 0; u < ILP; ++u) bp[u] = tb.pre;
 #pragma unroll
         for (int st = WAVE / 2; st > 0; st >>= 1) {
+          const uint32_t *cand[ILP];
           uint32_t v[ILP];
 #pragma unroll
-          for (int u = 0; u < ILP; ++u) v[u] = tb.pre[bb[u] + st];
+          for (int u = 0; u < ILP; ++u) {
+            cand[u] = bp[u] + st;
+            v[u] = *cand[u];
+          }
 #pragma unroll
-          for (int u = 0; u < ILP; ++u) bb[u] = v[u] <= xc[u] ? bb[u] + st : bb[u];
+          for (int u = 0; u < ILP; ++u) bp[u] = v[u] <= xc[u] ? cand[u] : bp[u];
         }
+#pragma unroll
+        for (int u = 0; u < ILP; ++u) bb[u] = (uint32_t)(bp[u] - tb.pre);
       }
 #pragma unroll
       for (int u = 0; u < ILP; ++u) {
@@ -621,22 +630,29 @@ struct TriSortedIds {
       for (int u = 0; u < ILP; ++u) hit[u] = false;
       return;
     }
-    uint32_t base[ILP];
+    // the search position as an element pointer: one add per step gives the
+    // probe address, and the select keeps it (no index → address arithmetic)
+    const uint32_t *bp[ILP];
 #pragma unroll
-    for (int u = 0; u < ILP; ++u) base[u] = 0;
+    for (int u = 0; u < ILP; ++u) bp[u] = ids;
     for (uint32_t len = nu; len > 1;) {
       const uint32_t half = len >> 1;
+      const uint32_t *cand[ILP];
       uint32_t v[ILP];
 #pragma unroll
-      for (int u = 0; u < ILP; ++u) v[u] = ids[base[u] + half];
+      for (int u = 0; u < ILP; ++u) {
+        cand[u] = bp[u] + half;
+        v[u] = *cand[u];
+      }
 #pragma unroll
-      for (int u = 0; u < ILP; ++u) base[u] = v[u] < wk[u] ? base[u] + half : base[u];
+      for (int u = 0; u < ILP; ++u) bp[u] = v[u] < wk[u] ? cand[u] : bp[u];
       len -= half;
     }
-    uint32_t v0[ILP], v1[ILP];
+    uint32_t base[ILP], v0[ILP], v1[ILP];
 #pragma unroll
     for (int u = 0; u < ILP; ++u) {
-      v0[u] = ids[base[u]];
+      base[u] = (uint32_t)(bp[u] - ids);
+      v0[u] = *bp[u];
       v1[u] = ids[min(base[u] + 1, nu - 1)];
     }
 #pragma unroll

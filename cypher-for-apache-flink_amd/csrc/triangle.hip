@@ -203,7 +203,10 @@ constexpr int TRI_BLOCK = 256;
 #endif
 constexpr int TRI_CAP = CAPF_TRI_CAP;  // N+(p) staged in LDS up to this many entries
 constexpr int TRI_CHUNK = 16;  // rows per cursor grab
-constexpr int TRI_ILP = 3;     // N+(q) entries per lane in flight (s24: ILP 2 333 ms, 3 314, 4 322)
+// N+(q) entries per lane in flight.  s24 at the round-4 closing kernels (5
+// waves/SIMD): ILP 2 308 ms, 3 290, 4 269; before the ids-only copies and the
+// pointer-form searches: 2 333, 3 314, 4 322
+constexpr int TRI_ILP = 4;
 
 // Index of w in the ascending a(0..n), or −1.
 template <class A>
@@ -844,17 +847,17 @@ struct TriPassB {
   uint32_t nitems;
 };
 
-template <int ILP, int HCAP = 0>
-__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(5))) void k_tri_count_passb(const uint32_t *rowptr, const uint32_t *pcols,
+template <int ILP, int HCAP = 0, int WPE = 5, int SCAP = TRI_CAP>
+__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_tri_count_passb(const uint32_t *rowptr, const uint32_t *pcols,
                                                                 const uint2 *vals, TriPassB b, int parts,
                                                                 int part, int grab, int xcd,
                                                                 unsigned long long *cursor,
                                                                 unsigned long long *acc) {
   // HCAP > 0: staged lists of ≤ HCAP words hashed into 2·HCAP slots; 0: sorted copies of ≤ TRI_CAP
   constexpr bool HASH = HCAP > 0;
-  constexpr uint32_t CAP = HASH ? HCAP : TRI_CAP;
-  __shared__ __attribute__((aligned(16))) uint32_t s_cols[TRI_BLOCK / WAVE][HASH ? 2 * HCAP : TRI_CAP];
-  __shared__ uint8_t s_nib[TRI_BLOCK / WAVE][HASH ? 1 : TRI_CAP];
+  constexpr uint32_t CAP = HASH ? HCAP : SCAP;
+  __shared__ __attribute__((aligned(16))) uint32_t s_cols[TRI_BLOCK / WAVE][HASH ? 2 * HCAP : SCAP];
+  __shared__ uint8_t s_nib[TRI_BLOCK / WAVE][HASH ? 1 : SCAP];
   __shared__ TriBatch2 s_tab[TRI_BLOCK / WAVE];
   __shared__ unsigned long long lds[17];
   const int wv = threadIdx.x / WAVE;
@@ -1101,8 +1104,8 @@ static void tri_build_passb(Session *s, const uint64_t *okey, TriGraph &g) {
 // Pass A over q-tiled work items (see tri_build_qtiles): item (p, k0, k1) probes
 // the q's N+(p)[k0, k1) — N+(p) staged in LDS (≤ TRI_CAP words) or searched in
 // place — with the pass-A rule (edges with |N+(p)| < |N+(q)| belong to pass B).
-template <int ILP, int HCAP = 0>
-__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(5))) void k_tri_count_qtiled(const uint32_t *rowptr, const uint32_t *pcols,
+template <int ILP, int HCAP = 0, int WPE = 5, int SCAP = TRI_CAP>
+__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_tri_count_qtiled(const uint32_t *rowptr, const uint32_t *pcols,
                                                                  const uint2 *vals, const uint2 *erow,
                                                                  const uint4 *items,
                                                                  uint32_t nitems, int parts, int part, int grab,
@@ -1111,9 +1114,9 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(5))) 
                                                                  unsigned long long *acc) {
   // HCAP > 0: staged lists of ≤ HCAP words hashed into 2·HCAP slots; 0: sorted copies of ≤ TRI_CAP
   constexpr bool HASH = HCAP > 0;
-  constexpr uint32_t CAP = HASH ? HCAP : TRI_CAP;
-  __shared__ __attribute__((aligned(16))) uint32_t s_cols[TRI_BLOCK / WAVE][HASH ? 2 * HCAP : TRI_CAP];
-  __shared__ uint8_t s_nib[TRI_BLOCK / WAVE][HASH ? 1 : TRI_CAP];
+  constexpr uint32_t CAP = HASH ? HCAP : SCAP;
+  __shared__ __attribute__((aligned(16))) uint32_t s_cols[TRI_BLOCK / WAVE][HASH ? 2 * HCAP : SCAP];
+  __shared__ uint8_t s_nib[TRI_BLOCK / WAVE][HASH ? 1 : SCAP];
   __shared__ TriBatch2 s_tab[TRI_BLOCK / WAVE];
   __shared__ unsigned long long lds[17];
   const int wv = threadIdx.x / WAVE;
@@ -1370,6 +1373,30 @@ static void tri_build(Session *s, const ColView &src, const ColView &dst, int64_
   }
 }
 
+// The sorted-copy count kernel for (ILP, waves/SIMD it is compiled for, LDS
+// copy capacity); unlisted combinations fall back to ILP 4 / 6 waves / TRI_CAP.
+struct TriPassbK {
+  template <int I, int W, int C>
+  static constexpr auto get() { return k_tri_count_passb<I, 0, W, C>; }
+};
+struct TriQtiledK {
+  template <int I, int W, int C>
+  static constexpr auto get() { return k_tri_count_qtiled<I, 0, W, C>; }
+};
+template <class K>
+static auto tri_pick(int ilp, int wpe, int scap) {
+  if (ilp <= 2) return K::template get<2, 5, TRI_CAP>();
+  if (ilp >= 6) return K::template get<6, 5, TRI_CAP>();
+  if (ilp == 3) return wpe == 5 ? K::template get<3, 5, TRI_CAP>()
+                       : wpe == 8 && scap == 512 ? K::template get<3, 8, 512>()
+                                                 : K::template get<3, 6, TRI_CAP>();
+  if (wpe == 4) return K::template get<4, 4, TRI_CAP>();
+  if (wpe == 5) return K::template get<4, 5, TRI_CAP>();
+  if (wpe == 7 && scap == 768) return K::template get<4, 7, 768>();
+  if (wpe == 8 && scap == 512) return K::template get<4, 8, 512>();
+  return K::template get<4, 6, TRI_CAP>();
+}
+
 // Device count (int64 at d_out) of the directed triangle over rels (src, dst)
 // with endpoints in [lo, lo + len), restricted to part `part` of `parts`
 // (row chunks dealt round-robin; the loop terms belong to part 0): the sum
@@ -1447,6 +1474,15 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
     // caches hold: 4/4 319 ms, 32/8 415, 64/16 511, 128/32 720 ms
     const int grab_a = std::max(1, getenv("CAPF_TRI_GRAB_A") ? atoi(getenv("CAPF_TRI_GRAB_A")) : 2);
     const int grab_b = std::max(1, getenv("CAPF_TRI_GRAB_B") ? atoi(getenv("CAPF_TRI_GRAB_B")) : 4);
+    // CAPF_TRI_WPE (tuning): waves/SIMD the count kernels are compiled for.  The
+    // LDS copies (≈ 24.7 KB per 4-wave block at TRI_CAP) allow 6; more VGPRs per
+    // lane cost less than fewer waves, and scratch spills cost less than both.
+    // s24, ILP 4: 4 waves (no spills) 308 ms, 5 waves 268, 6 waves 251 ms;
+    // ILP 3 at 6 waves 261; 7 waves with 768-entry copies 322, 8 with 512 369 ms
+    const int wpe = getenv("CAPF_TRI_WPE") ? atoi(getenv("CAPF_TRI_WPE")) : 6;
+    // CAPF_TRI_SCAP (tuning): longest list staged in LDS (longer: searched in
+    // global memory); smaller copies let more waves share a CU's LDS
+    const int scap = getenv("CAPF_TRI_SCAP") ? atoi(getenv("CAPF_TRI_SCAP")) : TRI_CAP;
     // CAPF_TRI_XCD_A / _B (tuning): 1 = grabs dealt to the XCD groups in chunks
     // (tri_dequeue).  s24, one box: A/B one cursor 121/223 ms; per XCD group,
     // grabs 4/4 109/238, 2/2 103/229, 1/1 109/220 — on for pass A (grab 2) only
@@ -1460,7 +1496,7 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
           KernelTimer kt(s, "tri_count_qtiled", 4.0 * g.P);
           auto kq = hash == 1024 ? (ilp <= 2 ? k_tri_count_qtiled<2, 1024> : k_tri_count_qtiled<4, 1024>)
                     : hash == 512  ? (ilp <= 2 ? k_tri_count_qtiled<2, 512> : k_tri_count_qtiled<4, 512>)
-                                   : (ilp <= 2 ? k_tri_count_qtiled<2> : ilp == 3 ? k_tri_count_qtiled<3> : k_tri_count_qtiled<4>);
+                                   : tri_pick<TriQtiledK>(ilp, wpe, scap);
           hipLaunchKernelGGL(kq, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
                              (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
                              (const uint2 *)g.vals->p, g.erow ? (const uint2 *)g.erow->p : nullptr,
@@ -1489,7 +1525,7 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
                    g.nitems};
         auto kb = hash == 1024 ? (ilp <= 2 ? k_tri_count_passb<2, 1024> : k_tri_count_passb<4, 1024>)
                   : hash == 512  ? (ilp <= 2 ? k_tri_count_passb<2, 512> : k_tri_count_passb<4, 512>)
-                                 : (ilp <= 2 ? k_tri_count_passb<2> : ilp == 3 ? k_tri_count_passb<3> : k_tri_count_passb<4>);
+                                 : tri_pick<TriPassbK>(ilp, wpe, scap);
         hipLaunchKernelGGL(kb, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
                            (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p, (const uint2 *)g.vals->p,
                            b, parts, part, grab_b, xcd_b, xcd_b ? xb : acc + 6, acc);

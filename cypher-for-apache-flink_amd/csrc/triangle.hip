@@ -386,7 +386,6 @@ struct TriBatch2 {
   uint32_t pre[WAVE + 1];  // exclusive prefix of the batch's |N+(q)|, + total
   uint32_t qa[WAVE];       // N+(q) start in pcols
   uint32_t pk[WAVE];       // packed word of q in N+(p) (multiplicities of p–q)
-  uint32_t kk[WAVE];       // k: the batch entry (pqe(k): vals index of p–q, read on escape only)
 };
 
 // packed word's multiplicity nibbles say "look the pair up in vals"
@@ -441,13 +440,14 @@ __device__ inline void tri_row_packed(uint32_t nb, uint32_t ns, const uint32_t *
     if (lane == WAVE - 1) tb.pre[WAVE] = inc;
     tb.qa[lane] = qa;
     tb.pk[lane] = pk;
-    tb.kk[lane] = k;
     const uint32_t total = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl(inc, WAVE - 1, WAVE));
-    if (lane == 0) probes += total;
+    probes += total;  // (wave-uniform: the kernels take lane 0's)
     __builtin_amdgcn_wave_barrier();
-    uint32_t w[2][ILP], pos[2][ILP], bi[2][ILP];
+    // ping-pong words and batch owners of the steps in flight; a word's pcols
+    // position is recomputed from its owner on the rare escape instead of held
+    uint32_t w[2][ILP], bi[2][ILP];
     uint32_t bcur = 0;  // owner of the last position issued (owners only grow along the batch)
-    auto issue = [&](uint32_t t0, uint32_t (&ww)[ILP], uint32_t (&pp)[ILP], uint32_t (&bb)[ILP]) {
+    auto issue = [&](uint32_t t0, uint32_t (&ww)[ILP], uint32_t (&bb)[ILP]) {
       uint32_t xc[ILP];
 #pragma unroll
       for (int u = 0; u < ILP; ++u) xc[u] = min(t0 + u * WAVE + lane, total - 1);
@@ -495,12 +495,12 @@ __device__ inline void tri_row_packed(uint32_t nb, uint32_t ns, const uint32_t *
       }
 #pragma unroll
       for (int u = 0; u < ILP; ++u) {
-        pp[u] = tb.qa[bb[u]] + (xc[u] - tb.pre[bb[u]]);
-        ww[u] = c_tri_diag == 2 ? (pp[u] * 2654435761u) & TRI_M24 : pcols[pp[u]];
+        const uint32_t pp = tb.qa[bb[u]] + (xc[u] - tb.pre[bb[u]]);
+        ww[u] = c_tri_diag == 2 ? (pp * 2654435761u) & TRI_M24 : pcols[pp];
         if (t0 + u * WAVE + lane >= total) ww[u] = 0xFFFFFFFFu;  // past the end (the load stays unconditional)
       }
     };
-    auto probe = [&](const uint32_t (&ww)[ILP], const uint32_t (&pp)[ILP], const uint32_t (&bb)[ILP]) {
+    auto probe = [&](const uint32_t (&ww)[ILP], const uint32_t (&bb)[ILP], uint32_t t0) {
       if (c_tri_diag == 1) return;
       uint32_t wk[ILP], pw[ILP], pos[ILP];
       bool live[ILP], hit[ILP];
@@ -512,12 +512,14 @@ __device__ inline void tri_row_packed(uint32_t nb, uint32_t ns, const uint32_t *
       find.template batch<ILP>(wk, live, hit, pw, pos);
 #pragma unroll
       for (int u = 0; u < ILP; ++u) {
+        hits += (unsigned long long)__popcll(__ballot(hit[u]));  // (wave-uniform)
         if (hit[u]) {
-          ++hits;
           const uint32_t pkw = tb.pk[bb[u]];
-          const uint2 a1 = tri_esc(pkw) ? vals[pqe(tb.kk[bb[u]])]  // p–q
+          const uint2 a1 = tri_esc(pkw) ? vals[pqe(kb + bb[u])]  // p–q
                                         : make_uint2((pkw >> 24) & 15u, pkw >> 28);
-          const uint2 s2 = tri_fb(ww[u], vals, pp[u]);                 // streamed: q–w (A) / p–w (B)
+          const uint32_t x = t0 + u * WAVE + lane;
+          const uint2 s2 = tri_esc(ww[u]) ? vals[tb.qa[bb[u]] + (x - tb.pre[bb[u]])]  // streamed: q–w (A) / p–w (B)
+                                          : make_uint2((ww[u] >> 24) & 15u, ww[u] >> 28);
           const uint2 s3 = tri_fb(pw[u], vals, pos[u]);                // staged:   p–w (A) / q–w (B)
           const uint2 a2 = SWAP ? s3 : s2, a3 = SWAP ? s2 : s3;
           // p→q→w→p  +  p→w→q→p
@@ -526,13 +528,13 @@ __device__ inline void tri_row_packed(uint32_t nb, uint32_t ns, const uint32_t *
       }
     };
     if (c_tri_diag == 3) continue;  // (profiling only: staging and batch tables, no probes)
-    if (total > 0) issue(0, w[0], pos[0], bi[0]);
+    if (total > 0) issue(0, w[0], bi[0]);
     for (uint32_t t0 = 0; t0 < total; t0 += 2 * STEP) {
-      if (t0 + STEP < total) issue(t0 + STEP, w[1], pos[1], bi[1]);
-      probe(w[0], pos[0], bi[0]);
+      if (t0 + STEP < total) issue(t0 + STEP, w[1], bi[1]);
+      probe(w[0], bi[0], t0);
       if (t0 + STEP >= total) break;
-      if (t0 + 2 * STEP < total) issue(t0 + 2 * STEP, w[0], pos[0], bi[0]);
-      probe(w[1], pos[1], bi[1]);
+      if (t0 + 2 * STEP < total) issue(t0 + 2 * STEP, w[0], bi[0]);
+      probe(w[1], bi[1], t0 + STEP);
     }
     __builtin_amdgcn_wave_barrier();  // the table is rewritten by the next batch
   }
@@ -804,9 +806,9 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_packed(const uint32_t *
   unsigned long long tot;
   block_exclusive_scan(t, lds, tot);
   if (threadIdx.x == 0 && tot) atomicAdd(&acc[0], tot);
-  block_exclusive_scan(probes, lds, tot);
+  block_exclusive_scan(lane_id() == 0 ? probes : 0ull, lds, tot);
   if (threadIdx.x == 0 && tot) atomicAdd(&acc[4], tot);
-  block_exclusive_scan(hits, lds, tot);
+  block_exclusive_scan(lane_id() == 0 ? hits : 0ull, lds, tot);
   if (threadIdx.x == 0 && tot) atomicAdd(&acc[5], tot);
 }
 
@@ -911,9 +913,9 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))
   unsigned long long tot;
   block_exclusive_scan(t, lds, tot);
   if (threadIdx.x == 0 && tot) atomicAdd(&acc[0], tot);
-  block_exclusive_scan(probes, lds, tot);
+  block_exclusive_scan(lane_id() == 0 ? probes : 0ull, lds, tot);
   if (threadIdx.x == 0 && tot) atomicAdd(&acc[4], tot);
-  block_exclusive_scan(hits, lds, tot);
+  block_exclusive_scan(lane_id() == 0 ? hits : 0ull, lds, tot);
   if (threadIdx.x == 0 && tot) atomicAdd(&acc[5], tot);
 }
 
@@ -1167,9 +1169,9 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))
   unsigned long long tot;
   block_exclusive_scan(t, lds, tot);
   if (threadIdx.x == 0 && tot) atomicAdd(&acc[0], tot);
-  block_exclusive_scan(probes, lds, tot);
+  block_exclusive_scan(lane_id() == 0 ? probes : 0ull, lds, tot);
   if (threadIdx.x == 0 && tot) atomicAdd(&acc[4], tot);
-  block_exclusive_scan(hits, lds, tot);
+  block_exclusive_scan(lane_id() == 0 ? hits : 0ull, lds, tot);
   if (threadIdx.x == 0 && tot) atomicAdd(&acc[5], tot);
 }
 

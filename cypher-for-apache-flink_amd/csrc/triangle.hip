@@ -385,7 +385,7 @@ __global__ void k_tri_pack(const uint32_t *cols, const uint2 *vals, uint32_t P, 
 struct TriBatch2 {
   uint32_t pre[WAVE + 1];  // exclusive prefix of the batch's |N+(q)|, + total
   uint32_t qa[WAVE];       // N+(q) start in pcols
-  uint32_t pk[WAVE];       // packed word of q in N+(p) (multiplicities of p–q)
+  uint8_t pk[WAVE];        // multiplicity nibbles of the pair p–q (the top byte of q's word)
 };
 
 // packed word's multiplicity nibbles say "look the pair up in vals"
@@ -439,7 +439,7 @@ __device__ inline void tri_row_packed(uint32_t nb, uint32_t ns, const uint32_t *
     tb.pre[lane] = inc - dq;
     if (lane == WAVE - 1) tb.pre[WAVE] = inc;
     tb.qa[lane] = qa;
-    tb.pk[lane] = pk;
+    tb.pk[lane] = (uint8_t)(pk >> 24);
     const uint32_t total = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl(inc, WAVE - 1, WAVE));
     probes += total;  // (wave-uniform: the kernels take lane 0's)
     __builtin_amdgcn_wave_barrier();
@@ -514,7 +514,7 @@ __device__ inline void tri_row_packed(uint32_t nb, uint32_t ns, const uint32_t *
       for (int u = 0; u < ILP; ++u) {
         hits += (unsigned long long)__popcll(__ballot(hit[u]));  // (wave-uniform)
         if (hit[u]) {
-          const uint32_t pkw = tb.pk[bb[u]];
+          const uint32_t pkw = (uint32_t)tb.pk[bb[u]] << 24;
           const uint2 a1 = tri_esc(pkw) ? vals[pqe(kb + bb[u])]  // p–q
                                         : make_uint2((pkw >> 24) & 15u, pkw >> 28);
           const uint32_t x = t0 + u * WAVE + lane;
@@ -620,11 +620,11 @@ __device__ inline TriSorted<A> tri_sorted(A at, uint32_t n, uint32_t a) {
   return TriSorted<A>{at, n, a};
 }
 
-// The same search over an LDS copy that holds the ids alone (the nibbles in a
-// byte array beside it): no mask per step; the packed word is rebuilt on a hit.
-struct TriSortedIds {
+// The same search over an LDS copy of rotated words (id << 8 | nibbles): they
+// sort as the ids do, so a step compares with wk << 8 and needs no mask, and
+// the nibbles need no array of their own (the copy stays at 4 B per entry).
+struct TriSortedRot {
   const uint32_t *ids;
-  const uint8_t *nib;
   uint32_t n, a;
   template <int ILP>
   __device__ inline void batch(const uint32_t (&wk)[ILP], const bool (&live)[ILP], bool (&hit)[ILP],
@@ -638,8 +638,12 @@ struct TriSortedIds {
     // the search position as an element pointer: one add per step gives the
     // probe address, and the select keeps it (no index → address arithmetic)
     const uint32_t *bp[ILP];
+    uint32_t k8[ILP];
 #pragma unroll
-    for (int u = 0; u < ILP; ++u) bp[u] = ids;
+    for (int u = 0; u < ILP; ++u) {
+      bp[u] = ids;
+      k8[u] = wk[u] << 8;
+    }
     for (uint32_t len = nu; len > 1;) {
       const uint32_t half = len >> 1;
       const uint32_t *cand[ILP];
@@ -650,7 +654,7 @@ struct TriSortedIds {
         v[u] = *cand[u];
       }
 #pragma unroll
-      for (int u = 0; u < ILP; ++u) bp[u] = v[u] < wk[u] ? cand[u] : bp[u];
+      for (int u = 0; u < ILP; ++u) bp[u] = v[u] < k8[u] ? cand[u] : bp[u];
       len -= half;
     }
     uint32_t base[ILP], v0[ILP], v1[ILP];
@@ -662,22 +666,21 @@ struct TriSortedIds {
     }
 #pragma unroll
     for (int u = 0; u < ILP; ++u) {
-      const bool first = v0[u] == wk[u];
-      const bool second = v1[u] == wk[u] && base[u] + 1 < nu;
+      const bool first = (v0[u] >> 8) == wk[u];
+      const bool second = (v1[u] >> 8) == wk[u] && base[u] + 1 < nu;
       hit[u] = live[u] && (first || second);
-      const uint32_t at = base[u] + (first ? 0u : 1u);
-      pos[u] = a + at;
-      pw[u] = hit[u] ? wk[u] | (uint32_t)nib[min(at, nu - 1)] << 24 : 0u;
+      const uint32_t r = first ? v0[u] : v1[u];
+      pos[u] = a + base[u] + (first ? 0u : 1u);
+      pw[u] = (r >> 8) | (r << 24);
     }
   }
 };
 
-// stage row[0..n) into the ids / nibbles LDS copy
-__device__ inline void tri_stage_ids(uint32_t *ids, uint8_t *nib, const uint32_t *row, uint32_t n) {
+// stage row[0..n) as rotated words into the LDS copy
+__device__ inline void tri_stage_rot(uint32_t *ids, const uint32_t *row, uint32_t n) {
   for (uint32_t k = lane_id(); k < n; k += WAVE) {
     const uint32_t w = row[k];
-    ids[k] = w & TRI_M24;
-    nib[k] = (uint8_t)(w >> 24);
+    ids[k] = (w << 8) | (w >> 24);
   }
 }
 
@@ -764,12 +767,11 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_packed(const uint32_t *
   constexpr bool HASH = HCAP > 0;
   constexpr uint32_t CAP = HASH ? HCAP : TRI_CAP;
   __shared__ __attribute__((aligned(16))) uint32_t s_cols[TRI_BLOCK / WAVE][HASH ? 2 * HCAP : TRI_CAP];
-  __shared__ uint8_t s_nib[TRI_BLOCK / WAVE][HASH ? 1 : TRI_CAP];
+
   __shared__ TriBatch2 s_tab[TRI_BLOCK / WAVE];
   __shared__ unsigned long long lds[17];
   const int wv = threadIdx.x / WAVE, lane = lane_id();
   uint32_t *sc = s_cols[wv];
-  uint8_t *sn = s_nib[wv];
   TriBatch2 &tb = s_tab[wv];
   unsigned long long t = 0, probes = 0, hits = 0;
   for (;;) {
@@ -795,10 +797,10 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_packed(const uint32_t *
                                    TriHashFind{h},
                                    pqe, t, probes, hits);
       } else {
-        tri_stage_ids(sc, sn, row, dp);
+        tri_stage_rot(sc, row, dp);
         __builtin_amdgcn_wave_barrier();
         tri_row_packed<ILP, SPLIT>(dp, dp, pcols, vals, tb, [&](uint32_t k) { return tri_qrow(rowptr, row[k]); },
-                                   TriSortedIds{sc, sn, dp, a}, pqe, t, probes, hits);
+                                   TriSortedRot{sc, dp, a}, pqe, t, probes, hits);
       }
       __builtin_amdgcn_wave_barrier();  // sc is rewritten by the next row
     }
@@ -859,12 +861,11 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))
   constexpr bool HASH = HCAP > 0;
   constexpr uint32_t CAP = HASH ? HCAP : SCAP;
   __shared__ __attribute__((aligned(16))) uint32_t s_cols[TRI_BLOCK / WAVE][HASH ? 2 * HCAP : SCAP];
-  __shared__ uint8_t s_nib[TRI_BLOCK / WAVE][HASH ? 1 : SCAP];
+
   __shared__ TriBatch2 s_tab[TRI_BLOCK / WAVE];
   __shared__ unsigned long long lds[17];
   const int wv = threadIdx.x / WAVE;
   uint32_t *sc = s_cols[wv];
-  uint8_t *sn = s_nib[wv];
   TriBatch2 &tb = s_tab[wv];
   unsigned long long t = 0, probes = 0, hits = 0;
   uint32_t staged = 0xFFFFFFFFu;  // q whose list sits in sc
@@ -901,11 +902,11 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))
       } else {
         if (q != staged) {
           __builtin_amdgcn_wave_barrier();  // the previous list's searches are done
-          tri_stage_ids(sc, sn, row, dq);
+          tri_stage_rot(sc, row, dq);
           __builtin_amdgcn_wave_barrier();
           staged = q;
         }
-        tri_row_packed<ILP, false, true>(n, dq, pcols, vals, tb, qs, TriSortedIds{sc, sn, dq, a},
+        tri_row_packed<ILP, false, true>(n, dq, pcols, vals, tb, qs, TriSortedRot{sc, dq, a},
                                          pqe, t, probes, hits);
       }
     }
@@ -1118,12 +1119,11 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))
   constexpr bool HASH = HCAP > 0;
   constexpr uint32_t CAP = HASH ? HCAP : SCAP;
   __shared__ __attribute__((aligned(16))) uint32_t s_cols[TRI_BLOCK / WAVE][HASH ? 2 * HCAP : SCAP];
-  __shared__ uint8_t s_nib[TRI_BLOCK / WAVE][HASH ? 1 : SCAP];
+
   __shared__ TriBatch2 s_tab[TRI_BLOCK / WAVE];
   __shared__ unsigned long long lds[17];
   const int wv = threadIdx.x / WAVE;
   uint32_t *sc = s_cols[wv];
-  uint8_t *sn = s_nib[wv];
   TriBatch2 &tb = s_tab[wv];
   unsigned long long t = 0, probes = 0, hits = 0;
   uint32_t staged = 0xFFFFFFFFu;  // p whose list sits in sc
@@ -1157,11 +1157,11 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))
       } else {
         if (p != staged) {
           __builtin_amdgcn_wave_barrier();  // the previous list's searches are done
-          tri_stage_ids(sc, sn, row, dp);
+          tri_stage_rot(sc, row, dp);
           __builtin_amdgcn_wave_barrier();
           staged = p;
         }
-        tri_row_packed<ILP, true>(nb, dp, pcols, vals, tb, qrow, TriSortedIds{sc, sn, dp, a},
+        tri_row_packed<ILP, true>(nb, dp, pcols, vals, tb, qrow, TriSortedRot{sc, dp, a},
                                   pqe, t, probes, hits);
       }
     }
@@ -1390,11 +1390,15 @@ static auto tri_pick(int ilp, int wpe, int scap) {
   if (ilp <= 2) return K::template get<2, 5, TRI_CAP>();
   if (ilp >= 6) return K::template get<6, 5, TRI_CAP>();
   if (ilp == 3) return wpe == 5 ? K::template get<3, 5, TRI_CAP>()
+                       : wpe == 7 ? K::template get<3, 7, TRI_CAP>()
                        : wpe == 8 && scap == 512 ? K::template get<3, 8, 512>()
+                       : wpe == 8 ? K::template get<3, 8, TRI_CAP>()
                                                  : K::template get<3, 6, TRI_CAP>();
   if (wpe == 4) return K::template get<4, 4, TRI_CAP>();
   if (wpe == 5) return K::template get<4, 5, TRI_CAP>();
   if (wpe == 7 && scap == 768) return K::template get<4, 7, 768>();
+  if (wpe == 7) return K::template get<4, 7, TRI_CAP>();
+  if (wpe == 8 && scap != 512) return K::template get<4, 8, TRI_CAP>();
   if (wpe == 8 && scap == 512) return K::template get<4, 8, 512>();
   return K::template get<4, 6, TRI_CAP>();
 }
@@ -1476,12 +1480,12 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
     // caches hold: 4/4 319 ms, 32/8 415, 64/16 511, 128/32 720 ms
     const int grab_a = std::max(1, getenv("CAPF_TRI_GRAB_A") ? atoi(getenv("CAPF_TRI_GRAB_A")) : 2);
     const int grab_b = std::max(1, getenv("CAPF_TRI_GRAB_B") ? atoi(getenv("CAPF_TRI_GRAB_B")) : 4);
-    // CAPF_TRI_WPE (tuning): waves/SIMD the count kernels are compiled for.  The
-    // LDS copies (≈ 24.7 KB per 4-wave block at TRI_CAP) allow 6; more VGPRs per
-    // lane cost less than fewer waves, and scratch spills cost less than both.
-    // s24, ILP 4: 4 waves (no spills) 308 ms, 5 waves 268, 6 waves 251 ms;
-    // ILP 3 at 6 waves 261; 7 waves with 768-entry copies 322, 8 with 512 369 ms
-    const int wpe = getenv("CAPF_TRI_WPE") ? atoi(getenv("CAPF_TRI_WPE")) : 6;
+    // CAPF_TRI_WPE (tuning): waves/SIMD the count kernels are compiled for.  With
+    // the rotated-word LDS copies a 4-wave block takes 18.8 KB, so 8 fit a CU;
+    // more waves cost less than the registers (and the scratch spills) they take.
+    // s24, ILP 4: 4 waves (no spills) 308 ms, 5 268, 6 240, 7 226, 8 222 ms
+    // (earlier layouts: 7 waves with 768-entry copies 322, 8 with 512 369 ms)
+    const int wpe = getenv("CAPF_TRI_WPE") ? atoi(getenv("CAPF_TRI_WPE")) : 8;
     // CAPF_TRI_SCAP (tuning): longest list staged in LDS (longer: searched in
     // global memory); smaller copies let more waves share a CU's LDS
     const int scap = getenv("CAPF_TRI_SCAP") ? atoi(getenv("CAPF_TRI_SCAP")) : TRI_CAP;

@@ -324,6 +324,11 @@ class DistTable:
         if self._deferred is None:
             return
         op, *args = self._deferred
+        if op == "host_rows":  # the one replicated row of a count held on the host
+            names, vals = args
+            self._local = self.session.local.table([(n, T_INT, [v], None) for n, v in zip(names, vals)], nrows=1)
+            self._part, self._placement, self._deferred = frozenset(), "replicated", None
+            return
         if op == "join":
             out = args[0]._join_eager(args[1], args[2], *args[3])
         elif op == "select":
@@ -383,7 +388,26 @@ class DistTable:
         n = self.local.size
         return n if self.placement == "replicated" else self.ex.all_sum(n)
 
+    def _host_values(self, col):
+        """The values of `col` when this table is (a projection of) a count's
+        host-held row — read without building or downloading a device table."""
+        d = self._deferred
+        if d is None:
+            return None
+        if d[0] == "host_rows":
+            names, vals = d[1], d[2]
+            return [vals[names.index(col)]] if col in names else None
+        if d[0] == "select":
+            for c in d[2]:
+                src, alias = (c, c) if isinstance(c, str) else tuple(c)
+                if alias == col:
+                    return d[1]._host_values(src)
+        return None
+
     def column_values(self, col):
+        hv = self._host_values(col)
+        if hv is not None:
+            return hv
         vals = self.local.column_values(col)
         if self.placement == "replicated":
             return vals
@@ -551,9 +575,9 @@ class DistTable:
             if count is not None:
                 names = list(aggregations)
                 # every rank holds the all-reduced count: the one row is replicated
-                # (reading it back needs no gather)
-                loc = self.session.local.table([(n, T_INT, [count], None) for n in names], nrows=1)
-                return self._wrap(loc, placement="replicated")
+                # (reading it back needs no gather), and it stays on the host until
+                # an operator needs it on the device (records read it directly)
+                return DistTable(self.session, deferred=("host_rows", names, [count] * len(names)), cols=names)
         keys = _dist_key_cols(self.local, by, header)
         if self.placement == "root":
             out = self.local.group(by, aggregations, header=header, params=params)
@@ -652,6 +676,8 @@ def _tree_refs(t, leaves, eqs, neqs):
         leaves.append(t.prov)
         return {c: (len(leaves) - 1, b) for c, b in t.prov.cols.items()}
     op, *a = t._deferred
+    if op == "host_rows":
+        raise _NoMatch
     if op == "join":
         lr = _tree_refs(a[0], leaves, eqs, neqs)
         rr = _tree_refs(a[1], leaves, eqs, neqs)

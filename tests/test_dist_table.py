@@ -82,7 +82,7 @@ def _two_hop_worker(rank, world, port, q):
         from conftest import bag
         from dist_support import OracleExchange, oracle_count_copies
         from capf_amd.dist_table import DistSession, dist_node_partitioned_graph
-        from capf_amd.expr import CountStar, IntegerLit, LessThan, Var
+        from capf_amd.expr import CountStar, IntegerLit, LessThan, Multiply, Var
         from capf_amd.graph import GraphData, ScanGraph
         from capf_amd.planner import Match, NodeP, Query, RelP, Stage, run
         from oracle import cmodel
@@ -119,7 +119,12 @@ def _two_hop_worker(rank, world, port, q):
                       [Stage([("count", CountStar())])])
         got3 = run(g, where)[0]["count"]
         want3 = run(full, where)[0]["count"]
-        q.put((rank, got, got_back, dispatched, bag(got_rows) == bag(ref_rows), one, got3 == want3 > 0,
+        # the sharded count's host-held row feeding a further projection (moved to
+        # the device only then)
+        doubled = run(g, Query(two.matches, [Stage([("c", CountStar())]),
+                                             Stage([("d", Multiply(Var("c"), IntegerLit(2)))])]))[0]["d"]
+        q.put((rank, got, got_back, dispatched, bag(got_rows) == bag(ref_rows), one,
+               got3 == want3 > 0 and doubled == 2 * got,
                cmodel.count_2hop(src, dst, n), len(src)))
         dist.destroy_process_group()
     except Exception:  # noqa: BLE001

@@ -827,19 +827,22 @@ constexpr uint32_t TRI_BCHUNK = 256;
 constexpr int TRI_QTILE_DEFAULT = 26;
 
 // First item of the wave's next grab.  xcd = 0: one cursor, grabs in order.
-// xcd = 1: the grabs are dealt to the 8 XCD groups (blocks b, b + 8, … share an
-// XCD and its L2) in chunks of TRI_XCHUNK consecutive grabs, each group with
+// xcd = C > 0: the grabs are dealt to the 8 XCD groups (blocks b, b + 8, …
+// share an XCD and its L2) in chunks of C consecutive grabs, each group with
 // its own cursor (cursor[32·g], a line of its own): every XCD walks the item
 // order at the same pace, its L2 seeing contiguous chunks.  Either way grab
 // index g covers items [(g·parts + part)·grab, … + grab).
-constexpr unsigned long long TRI_XCHUNK = 64;
+constexpr int TRI_XCHUNK = 64;
 __device__ inline unsigned long long tri_dequeue(unsigned long long *cursor, int xcd, int parts, int part,
                                                  int grab) {
   const unsigned long long xg = xcd ? (blockIdx.x & 7u) : 0ull;
   unsigned long long c0 = 0;
   if (lane_id() == 0) c0 = atomicAdd(cursor + 32 * xg, 1ull);
   c0 = (unsigned long long)__shfl((long long)c0, 0, WAVE);
-  if (xcd) c0 = ((c0 / TRI_XCHUNK) * 8 + xg) * TRI_XCHUNK + c0 % TRI_XCHUNK;
+  if (xcd) {
+    const unsigned long long ch = (unsigned long long)xcd;
+    c0 = ((c0 / ch) * 8 + xg) * ch + c0 % ch;
+  }
   return (c0 * parts + part) * grab;
 }
 
@@ -1492,8 +1495,11 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
     // CAPF_TRI_XCD_A / _B (tuning): 1 = grabs dealt to the XCD groups in chunks
     // (tri_dequeue).  s24, one box: A/B one cursor 121/223 ms; per XCD group,
     // grabs 4/4 109/238, 2/2 103/229, 1/1 109/220 — on for pass A (grab 2) only
-    const int xcd_a = getenv("CAPF_TRI_XCD_A") ? atoi(getenv("CAPF_TRI_XCD_A")) : 1;
-    const int xcd_b = getenv("CAPF_TRI_XCD_B") ? atoi(getenv("CAPF_TRI_XCD_B")) : 0;
+    // (the value: grabs per XCD chunk, 0 = one cursor; 1 means TRI_XCHUNK)
+    int xcd_a = getenv("CAPF_TRI_XCD_A") ? atoi(getenv("CAPF_TRI_XCD_A")) : TRI_XCHUNK;
+    int xcd_b = getenv("CAPF_TRI_XCD_B") ? atoi(getenv("CAPF_TRI_XCD_B")) : 0;
+    if (xcd_a == 1) xcd_a = TRI_XCHUNK;
+    if (xcd_b == 1) xcd_b = TRI_XCHUNK;
     // CAPF_TRI_TWOPASS=0 (tuning): one pass, every wedge streamed from N+(q)
     const bool two = packed && g.pcols && g.in_words && !(getenv("CAPF_TRI_TWOPASS") && atoi(getenv("CAPF_TRI_TWOPASS")) == 0);
     if (packed && g.pcols) {

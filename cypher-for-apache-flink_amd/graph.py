@@ -186,8 +186,9 @@ class ScanGraph:
 
     @staticmethod
     def _scan_from_meta(meta):
-        base, pairs, h = meta
-        return _planned(base.select(*pairs), h)
+        # the scan of (var, labels) is an immutable view of the graph's element
+        # tables: built once, then handed out again (no select call per query)
+        return meta[3]
 
     def _align_union(self, sel, h, order, types, v, flags, props, rel, meta_key=None):
         from .planner import Planned
@@ -202,9 +203,10 @@ class ScanGraph:
             base = self._build_union(sel, h, canon_order, Var(canon, v.ctype), flags, props, rel)
             self._scan_cache[key] = base
         pairs = tuple(zip(canon_order, order))
+        planned = Planned(base.select(*pairs), h)
         if meta_key is not None:
-            self._scan_meta[meta_key] = (base, pairs, h)
-        return Planned(base.select(*pairs), h)
+            self._scan_meta[meta_key] = (base, pairs, h, planned)
+        return planned
 
     def _build_union(self, sel, h, order, v, flags, props, rel):
         name = v.vname

@@ -521,6 +521,70 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_join_runs(const RJWork *work, 
   if (!EMIT && threadIdx.x == 0) out_cnt[blockIdx.x] = item_total;
 }
 
+// Unique build side (no two sorted build rows of a partition share h, tested
+// by k_rj_adjacent_dup): each probe row has at most one match, written to the
+// probe row's own position, out[prow] = build row (out prefilled with -1).
+// The output is in probe order: no COUNT, scan, sub-items or pair list, and
+// the probe side's columns pass through the join without an index.
+__global__ void k_rj_adjacent_dup(const uint64_t *h, int64_t n, int *dup) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    if (h[i] == h[i - 1]) *dup = 1;
+}
+
+__global__ __launch_bounds__(RJ_JBLOCK) void k_rj_direct(const RJWork *work, const uint64_t *bh,
+                                                         const uint32_t *brow, const int64_t *bstart,
+                                                         const uint64_t *ph, const uint32_t *prow, int64_t *out,
+                                                         unsigned long long *hits) {
+  __shared__ uint64_t th[RJ_RUNCAP];
+  __shared__ uint32_t tv[RJ_RUNCAP];  // chunk position + 1, 0 = empty
+  __shared__ unsigned long long red[RJ_JBLOCK / WAVE];
+  const RJWork wk = work[blockIdx.x];
+  const int64_t b0 = bstart[wk.part], b1 = bstart[wk.part + 1];
+  unsigned long long cnt = 0;
+  for (int64_t c0 = b0; c0 < b1; c0 += RJ_CHUNK) {
+    const int nc = (int)min<int64_t>((int64_t)RJ_CHUNK, b1 - c0);
+    __syncthreads();  // the previous chunk's table is no longer read
+    for (int i = threadIdx.x; i < RJ_RUNCAP; i += RJ_JBLOCK) tv[i] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < nc; i += RJ_JBLOCK) {
+      const uint64_t h = bh[c0 + i];
+      uint32_t slot = (uint32_t)h & (RJ_RUNCAP - 1);
+      while (atomicCAS(&tv[slot], 0u, (uint32_t)i + 1u) != 0u) slot = (slot + 1) & (RJ_RUNCAP - 1);
+      th[slot] = h;
+    }
+    __syncthreads();
+    for (int64_t q = wk.p0 + threadIdx.x; q < wk.p1; q += RJ_JBLOCK) {
+      const uint64_t h = ph[q];
+      uint32_t slot = (uint32_t)h & (RJ_RUNCAP - 1);
+      for (uint32_t v = tv[slot]; v != 0u; slot = (slot + 1) & (RJ_RUNCAP - 1), v = tv[slot])
+        if (th[slot] == h) {
+          out[prow[q]] = (int64_t)brow[c0 + v - 1];
+          ++cnt;
+          break;
+        }
+    }
+  }
+  cnt = wave_reduce_sum(cnt);
+  if (lane_id() == 0) red[threadIdx.x / WAVE] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < RJ_JBLOCK / WAVE; ++w) t += red[w];
+    if (t) atomicAdd(hits, t);
+  }
+}
+
+__global__ void k_rj_hitflags(const int64_t *brow, int64_t n, uint8_t *flags) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+    flags[r] = brow[r] >= 0 ? 1 : 0;
+}
+
+__global__ void k_rj_pick(const int64_t *rows, int64_t m, const int64_t *brow, int64_t *out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = brow[rows[i]];
+}
+
 // EMIT over output ranges (default with the run-based join).  After COUNT,
 // item i (cnt[i] pairs) becomes ⌈cnt[i] / RJ_SUB_OUT⌉ sub-items, each writing
 // the pairs [lo, hi) of the item's flattened output sequence (probe-row order,
@@ -880,6 +944,58 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
                        (const int64_t *)bs.pstart->p, (const int64_t *)ps.pstart->p, pchunk,
                        (const int64_t *)ioff->p, (RJWork *)dw->p);
     KERNEL_CHECK();
+  }
+  // a unique build side (one sorted-partition scan, one host read) joins
+  // straight into probe order (k_rj_direct); CAPF_RJ_DIRECT=0 keeps the pair list
+  const char *dn = getenv("CAPF_RJ_DIRECT");
+  if (runs && !pred && !b_outer && bs.n > 0 && !(dn && atoi(dn) == 0)) {
+    int *dflag = (int *)(s->d_scalars + 3);
+    HIP_CHECK(hipMemsetAsync(dflag, 0, 4, s->stream));
+    if (bs.n > 1) {
+      hipLaunchKernelGGL(k_rj_adjacent_dup, dim3(grid_for(bs.n, 256)), dim3(256), 0, s->stream,
+                         (const uint64_t *)bs.h->p, bs.n, dflag);
+      KERNEL_CHECK();
+    }
+    int dup = 0;
+    HIP_CHECK(hipMemcpyAsync(&dup, dflag, 4, hipMemcpyDeviceToHost, s->stream));
+    s->sync();
+    if (!dup) {
+      const int64_t n = Pr.nrows;
+      BufPtr brow = s->alloc(8 * std::max<int64_t>(n, 1)), acc = s->alloc(8);
+      HIP_CHECK(hipMemsetAsync(brow->p, 0xFF, 8 * std::max<int64_t>(n, 1), s->stream));
+      HIP_CHECK(hipMemsetAsync(acc->p, 0, 8, s->stream));
+      if (nw > 0) {
+        KernelTimer kt(s, "rj_join_direct", 12.0 * (double)(ps.n + bs.n) + 8.0 * (double)n);
+        hipLaunchKernelGGL(k_rj_direct, dim3((unsigned)nw), dim3(RJ_JBLOCK), 0, s->stream, (const RJWork *)dw->p,
+                           (const uint64_t *)bs.h->p, (const uint32_t *)bs.row->p, (const int64_t *)bs.pstart->p,
+                           (const uint64_t *)ps.h->p, (const uint32_t *)ps.row->p, (int64_t *)brow->p,
+                           (unsigned long long *)acc->p);
+        KERNEL_CHECK();
+      }
+      int64_t matched = 0;
+      HIP_CHECK(hipMemcpyAsync(&matched, acc->p, 8, hipMemcpyDeviceToHost, s->stream));
+      s->sync();
+      BufPtr pidx, bidx = brow;  // pidx null = identity over the probe rows
+      int64_t m = n;
+      if (!p_outer && matched < n) {
+        BufPtr flags = s->alloc(std::max<int64_t>(n, 1));
+        hipLaunchKernelGGL(k_rj_hitflags, dim3(grid_for(n, 256)), dim3(256), 0, s->stream, (const int64_t *)brow->p,
+                           n, (uint8_t *)flags->p);
+        KERNEL_CHECK();
+        pidx = compact_flags(s, (const uint8_t *)flags->p, n, &m);
+        bidx = s->alloc(8 * std::max<int64_t>(m, 1));
+        if (m > 0) {
+          hipLaunchKernelGGL(k_rj_pick, dim3(grid_for(m, 256)), dim3(256), 0, s->stream, (const int64_t *)pidx->p,
+                             m, (const int64_t *)brow->p, (int64_t *)bidx->p);
+          KERNEL_CHECK();
+        }
+      }
+      JoinPairs jp;
+      jp.left = build_left ? bidx : pidx;
+      jp.right = build_left ? pidx : bidx;
+      jp.n = m;
+      return jp;
+    }
   }
   BufPtr cnt = s->alloc(8 * std::max<int64_t>(nw, 1)), off = s->alloc(8 * (nw + 1));
   int64_t total = 0;

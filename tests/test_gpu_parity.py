@@ -479,6 +479,59 @@ def test_radix_join_large(gpu_session, monkeypatch, jt, sizes):
     assert got == sorted(pairs)
 
 
+@pytest.mark.parametrize("jt", ["inner", "left_outer", "right_outer", "full_outer"])
+@pytest.mark.parametrize("sizes", [(3000, 200000), (300000, 5000), (70000, 70001), (1, 1000), (50000, 1)])
+@pytest.mark.parametrize("direct", ["1", "0"], ids=["direct", "pairs"])
+def test_radix_join_unique_build(gpu_session, monkeypatch, jt, sizes, direct):
+    """The radix join whose smaller (build) side has every non-NULL key once:
+    each probe row matches at most once and the join writes the build row to
+    the probe row's position (radix_join.hip k_rj_direct, probe-order output);
+    CAPF_RJ_DIRECT=0 keeps the pair list.  Sparse int64 keys, misses on both
+    sides, NULL keys on both; checked against numpy, and the direct kernel ran
+    exactly when it may (not when the build side is outer)."""
+    monkeypatch.setenv("CAPF_JOIN", "radix")
+    monkeypatch.setenv("CAPF_RJ_DIRECT", direct)
+    rng = np.random.default_rng(sum(sizes) + 5)
+    nl, nr = sizes
+    nb, npr = min(nl, nr), max(nl, nr)
+    bkeys = rng.permutation(np.arange(2 * nb + 3, dtype=np.int64))[:nb] * 1000003 + 7  # unique, sparse
+    pkeys = rng.integers(0, 2 * nb + 3, npr).astype(np.int64) * 1000003 + 7           # some miss
+    bv = np.ones(nb, dtype=np.uint8)
+    bv[::53] = 0
+    pv = np.ones(npr, dtype=np.uint8)
+    pv[::61] = 0
+    lk, lv, rk, rv = (bkeys, bv, pkeys, pv) if nl < nr else (pkeys, pv, bkeys, bv)
+    ga = gpu_session.table([("lk", T_INT, lk, lv), ("li", T_INT, np.arange(nl), None)])
+    gb = gpu_session.table([("rk", T_INT, rk, rv), ("ri", T_INT, np.arange(nr), None)])
+    gpu_session.reset_profile()
+    gpu_session.set_profiling(True)
+    out = ga.join(gb, jt, ("lk", "rk"))
+    li, lok = out.column_arrays("li")
+    ri, rok = out.column_arrays("ri")
+    gpu_session.set_profiling(False)
+    build_outer = jt == "full_outer" or (jt == "left_outer" and nl < nr) or (jt == "right_outer" and nr <= nl)
+    assert ("rj_join_direct" in gpu_session.profile()) == (direct == "1" and not build_outer and nb > 1)
+    got = sorted(zip(np.where(lok, li, -1).tolist(), np.where(rok, ri, -1).tolist()))
+    byk = {int(rk[j]): int(j) for j in np.nonzero(rv)[0]} if nl >= nr else None
+    pairs, lm, rm = [], set(), set()
+    if byk is not None:
+        for i in np.nonzero(lv)[0]:
+            j = byk.get(int(lk[i]))
+            if j is not None:
+                pairs.append((int(i), j)); lm.add(int(i)); rm.add(j)
+    else:
+        byl = {int(lk[i]): int(i) for i in np.nonzero(lv)[0]}
+        for j in np.nonzero(rv)[0]:
+            i = byl.get(int(rk[j]))
+            if i is not None:
+                pairs.append((i, int(j))); lm.add(i); rm.add(int(j))
+    if jt in ("left_outer", "full_outer"):
+        pairs += [(i, -1) for i in range(nl) if i not in lm]
+    if jt in ("right_outer", "full_outer"):
+        pairs += [(-1, j) for j in range(nr) if j not in rm]
+    assert got == sorted(pairs)
+
+
 def test_join_overlapping_columns_raises():
     g, _ = _both(_rand_tables())
     with pytest.raises(_lib.IllegalArgumentException):

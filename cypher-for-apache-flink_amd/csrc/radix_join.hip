@@ -544,20 +544,23 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_direct(const RJWork *work, con
   unsigned long long cnt = 0;
   for (int64_t c0 = b0; c0 < b1; c0 += RJ_CHUNK) {
     const int nc = (int)min<int64_t>((int64_t)RJ_CHUNK, b1 - c0);
+    // table of ≥ 2·nc slots (a partition holds ~N / 2^16 build rows): clearing
+    // all RJ_RUNCAP slots per item cost as much as its probes
+    const uint32_t mask = (nc <= 32 ? 64u : (2u << (31 - __clz(2 * nc - 1)))) - 1u;
     __syncthreads();  // the previous chunk's table is no longer read
-    for (int i = threadIdx.x; i < RJ_RUNCAP; i += RJ_JBLOCK) tv[i] = 0;
+    for (int i = threadIdx.x; i <= (int)mask; i += RJ_JBLOCK) tv[i] = 0;
     __syncthreads();
     for (int i = threadIdx.x; i < nc; i += RJ_JBLOCK) {
       const uint64_t h = bh[c0 + i];
-      uint32_t slot = (uint32_t)h & (RJ_RUNCAP - 1);
-      while (atomicCAS(&tv[slot], 0u, (uint32_t)i + 1u) != 0u) slot = (slot + 1) & (RJ_RUNCAP - 1);
+      uint32_t slot = (uint32_t)h & mask;
+      while (atomicCAS(&tv[slot], 0u, (uint32_t)i + 1u) != 0u) slot = (slot + 1) & mask;
       th[slot] = h;
     }
     __syncthreads();
     for (int64_t q = wk.p0 + threadIdx.x; q < wk.p1; q += RJ_JBLOCK) {
       const uint64_t h = ph[q];
-      uint32_t slot = (uint32_t)h & (RJ_RUNCAP - 1);
-      for (uint32_t v = tv[slot]; v != 0u; slot = (slot + 1) & (RJ_RUNCAP - 1), v = tv[slot])
+      uint32_t slot = (uint32_t)h & mask;
+      for (uint32_t v = tv[slot]; v != 0u; slot = (slot + 1) & mask, v = tv[slot])
         if (th[slot] == h) {
           out[prow[q]] = (int64_t)brow[c0 + v - 1];
           ++cnt;
@@ -571,6 +574,47 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_direct(const RJWork *work, con
   if (threadIdx.x == 0) {
     unsigned long long t = 0;
     for (int w = 0; w < RJ_JBLOCK / WAVE; ++w) t += red[w];
+    if (t) atomicAdd(hits, t);
+  }
+}
+
+// Unique build side, probe side not partitioned (default of the unique case):
+// a probe row hashes its key, reads its partition's bounds and looks its h up
+// in the partition's sorted build hashes, starting where h's low 48 bits put
+// it (fmix64 spreads h evenly inside a partition, so the walk is a few
+// entries of one cache line).  Probe rows are read and written in order.
+__global__ __launch_bounds__(256) void k_rj_probe_sorted(ColView key, int64_t n, const uint64_t *bh,
+                                                         const uint32_t *brow, const int64_t *bstart, int64_t *out,
+                                                         unsigned long long *hits) {
+  __shared__ unsigned long long red[256 / WAVE];
+  unsigned long long cnt = 0;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    int64_t b = -1;
+    bool nul;
+    const uint64_t w = rj_word(key, r, nul);
+    if (!nul) {
+      const uint64_t h = fmix64(w);
+      const int64_t lo = bstart[h >> 48], hi = bstart[(h >> 48) + 1];
+      if (hi > lo) {
+        int64_t g = lo + (int64_t)__umul64hi(h << 16, (uint64_t)(hi - lo));
+        if (bh[g] < h) {
+          ++g;
+          while (g < hi && bh[g] < h) ++g;
+        } else {
+          while (g > lo && bh[g - 1] >= h) --g;
+        }
+        if (g < hi && bh[g] == h) b = (int64_t)brow[g];
+      }
+    }
+    out[r] = b;
+    cnt += b >= 0 ? 1u : 0u;
+  }
+  cnt = wave_reduce_sum(cnt);
+  if (lane_id() == 0) red[threadIdx.x / WAVE] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < 256 / WAVE; ++w) t += red[w];
     if (t) atomicAdd(hits, t);
   }
 }
@@ -889,6 +933,33 @@ bool radix_join_applies(const Data &l, const Data &r, const std::vector<std::pai
   return std::max(l.nrows, r.nrows) >= (int64_t(1) << 18);
 }
 
+static BufPtr rj_work_items(Session *s, const RJSide &bs, const RJSide &ps, int64_t probe_rows, int64_t &nw) {
+  // work items on the device: ⌈probe rows / pchunk⌉ per partition with rows on
+  // both sides; partitions whose build side needs several LDS fills ("heavy",
+  // skewed keys) are listed first so the dispatcher starts them early.  pchunk
+  // shrinks with the probe side (≈16 items per CU when the rows spread evenly,
+  // at least RJ_PCHUNK_MIN rows) so one hub key's probe rows — whose output is
+  // (its build rows) × (its probe rows) — spread over many workgroups instead
+  // of one carrying the whole product.
+  constexpr int64_t NPART = (int64_t)RJ_P * RJ_P;
+  int64_t pchunk = RJ_PCHUNK;
+  while (pchunk > RJ_PCHUNK_MIN && pchunk * 16 * s->num_cus > probe_rows) pchunk /= 2;
+  if (const char *e = getenv("CAPF_RJ_PCHUNK")) pchunk = std::max<int64_t>(64, atoll(e));  // tuning
+  BufPtr icnt = s->alloc(8 * 2 * NPART), ioff = s->alloc(8 * (2 * NPART + 1));
+  hipLaunchKernelGGL(k_rj_item_counts, dim3((unsigned)(NPART / 256)), dim3(256), 0, s->stream,
+                     (const int64_t *)bs.pstart->p, (const int64_t *)ps.pstart->p, pchunk, (int64_t *)icnt->p);
+  KERNEL_CHECK();
+  nw = exclusive_scan_i64(s, (const int64_t *)icnt->p, (int64_t *)ioff->p, 2 * NPART);
+  BufPtr dw = s->alloc(sizeof(RJWork) * std::max<int64_t>(nw, 1));
+  if (nw > 0) {
+    hipLaunchKernelGGL(k_rj_items, dim3((unsigned)(NPART / 256)), dim3(256), 0, s->stream,
+                       (const int64_t *)bs.pstart->p, (const int64_t *)ps.pstart->p, pchunk,
+                       (const int64_t *)ioff->p, (RJWork *)dw->p);
+    KERNEL_CHECK();
+  }
+  return dw;
+}
+
 JoinPairs radix_join(Session *s, const Data &l, const Data &r,
                      const std::vector<std::pair<int, int>> &keys, int32_t join_type, const FtProgram *pred) {
   const bool left_outer = join_type == CAPF_JOIN_LEFT_OUTER || join_type == CAPF_JOIN_FULL_OUTER;
@@ -901,7 +972,6 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
   const bool b_outer = build_left ? left_outer : right_outer;
   const bool p_outer = build_left ? right_outer : left_outer;
   RJSide bs = rj_partition(s, bk, B.nrows);
-  RJSide ps = rj_partition(s, pk, Pr.nrows);
   const char *rn = getenv("CAPF_RJ_RUNS");  // 0 (tuning): the chain-walking join kernel
   const bool runs = !(rn && atoi(rn) == 0);
   if (runs && bs.n > 0) {
@@ -922,33 +992,14 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
     bs.h = sh;
     bs.row = sr;
   }
-  // work items on the device: ⌈probe rows / pchunk⌉ per partition with rows on
-  // both sides; partitions whose build side needs several LDS fills ("heavy",
-  // skewed keys) are listed first so the dispatcher starts them early.  pchunk
-  // shrinks with the probe side (≈16 items per CU when the rows spread evenly,
-  // at least RJ_PCHUNK_MIN rows) so one hub key's probe rows — whose output is
-  // (its build rows) × (its probe rows) — spread over many workgroups instead
-  // of one carrying the whole product.
-  constexpr int64_t NPART = (int64_t)RJ_P * RJ_P;
-  int64_t pchunk = RJ_PCHUNK;
-  while (pchunk > RJ_PCHUNK_MIN && pchunk * 16 * s->num_cus > Pr.nrows) pchunk /= 2;
-  if (const char *e = getenv("CAPF_RJ_PCHUNK")) pchunk = std::max<int64_t>(64, atoll(e));  // tuning
-  BufPtr icnt = s->alloc(8 * 2 * NPART), ioff = s->alloc(8 * (2 * NPART + 1));
-  hipLaunchKernelGGL(k_rj_item_counts, dim3((unsigned)(NPART / 256)), dim3(256), 0, s->stream,
-                     (const int64_t *)bs.pstart->p, (const int64_t *)ps.pstart->p, pchunk, (int64_t *)icnt->p);
-  KERNEL_CHECK();
-  const int64_t nw = exclusive_scan_i64(s, (const int64_t *)icnt->p, (int64_t *)ioff->p, 2 * NPART);
-  BufPtr dw = s->alloc(sizeof(RJWork) * std::max<int64_t>(nw, 1));
-  if (nw > 0) {
-    hipLaunchKernelGGL(k_rj_items, dim3((unsigned)(NPART / 256)), dim3(256), 0, s->stream,
-                       (const int64_t *)bs.pstart->p, (const int64_t *)ps.pstart->p, pchunk,
-                       (const int64_t *)ioff->p, (RJWork *)dw->p);
-    KERNEL_CHECK();
-  }
-  // a unique build side (one sorted-partition scan, one host read) joins
-  // straight into probe order (k_rj_direct); CAPF_RJ_DIRECT=0 keeps the pair list
+  // a unique build side (one scan of the sorted partitions, one host read):
+  // each probe row has at most one match, written at the probe row's own
+  // position — probe-order output, no pair list.  CAPF_RJ_DIRECT: 1 (default)
+  // the probe side stays unpartitioned (k_rj_probe_sorted), 2 it is
+  // partitioned and probes the LDS tables (k_rj_direct), 0 the pair list
   const char *dn = getenv("CAPF_RJ_DIRECT");
-  if (runs && !pred && !b_outer && bs.n > 0 && !(dn && atoi(dn) == 0)) {
+  const int direct = dn ? atoi(dn) : 1;
+  if (runs && direct && !pred && !b_outer && bs.n > 0) {
     int *dflag = (int *)(s->d_scalars + 3);
     HIP_CHECK(hipMemsetAsync(dflag, 0, 4, s->stream));
     if (bs.n > 1) {
@@ -962,15 +1013,28 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
     if (!dup) {
       const int64_t n = Pr.nrows;
       BufPtr brow = s->alloc(8 * std::max<int64_t>(n, 1)), acc = s->alloc(8);
-      HIP_CHECK(hipMemsetAsync(brow->p, 0xFF, 8 * std::max<int64_t>(n, 1), s->stream));
       HIP_CHECK(hipMemsetAsync(acc->p, 0, 8, s->stream));
-      if (nw > 0) {
-        KernelTimer kt(s, "rj_join_direct", 12.0 * (double)(ps.n + bs.n) + 8.0 * (double)n);
-        hipLaunchKernelGGL(k_rj_direct, dim3((unsigned)nw), dim3(RJ_JBLOCK), 0, s->stream, (const RJWork *)dw->p,
-                           (const uint64_t *)bs.h->p, (const uint32_t *)bs.row->p, (const int64_t *)bs.pstart->p,
-                           (const uint64_t *)ps.h->p, (const uint32_t *)ps.row->p, (int64_t *)brow->p,
-                           (unsigned long long *)acc->p);
-        KERNEL_CHECK();
+      if (direct != 2) {
+        if (n > 0) {
+          KernelTimer kt(s, "rj_join_direct", (pk->enc == ENC_FOR24 ? 3.0 : pk->enc == ENC_FOR32 ? 4.0 : 8.0) * n + 8.0 * n + 32.0 * n);
+          hipLaunchKernelGGL(k_rj_probe_sorted, dim3(grid_for(n, 256, (int64_t)s->num_cus * 16)), dim3(256), 0,
+                             s->stream, view_of(pk), n, (const uint64_t *)bs.h->p, (const uint32_t *)bs.row->p,
+                             (const int64_t *)bs.pstart->p, (int64_t *)brow->p, (unsigned long long *)acc->p);
+          KERNEL_CHECK();
+        }
+      } else {
+        HIP_CHECK(hipMemsetAsync(brow->p, 0xFF, 8 * std::max<int64_t>(n, 1), s->stream));
+        RJSide ps = rj_partition(s, pk, n);
+        int64_t nw = 0;
+        BufPtr dw = rj_work_items(s, bs, ps, n, nw);
+        if (nw > 0) {
+          KernelTimer kt(s, "rj_join_direct", 12.0 * (double)(ps.n + bs.n) + 8.0 * (double)n);
+          hipLaunchKernelGGL(k_rj_direct, dim3((unsigned)nw), dim3(RJ_JBLOCK), 0, s->stream, (const RJWork *)dw->p,
+                             (const uint64_t *)bs.h->p, (const uint32_t *)bs.row->p, (const int64_t *)bs.pstart->p,
+                             (const uint64_t *)ps.h->p, (const uint32_t *)ps.row->p, (int64_t *)brow->p,
+                             (unsigned long long *)acc->p);
+          KERNEL_CHECK();
+        }
       }
       int64_t matched = 0;
       HIP_CHECK(hipMemcpyAsync(&matched, acc->p, 8, hipMemcpyDeviceToHost, s->stream));
@@ -997,6 +1061,9 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
       return jp;
     }
   }
+  RJSide ps = rj_partition(s, pk, Pr.nrows);
+  int64_t nw = 0;
+  BufPtr dw = rj_work_items(s, bs, ps, Pr.nrows, nw);
   BufPtr cnt = s->alloc(8 * std::max<int64_t>(nw, 1)), off = s->alloc(8 * (nw + 1));
   int64_t total = 0;
   if (nw > 0) {

@@ -118,7 +118,11 @@ _SIGS = {
     "capf_table_distinct_cols": (c_int32, [_T, c_int32, _STRS, _PT]),
     "capf_table_group": (c_int32, [_T, c_int32, _STRS, c_int32, POINTER(c_int32), POINTER(CapfExpr),
                                    POINTER(c_int32), _STRS, _PT]),
+    "capf_table_group_ex": (c_int32, [_T, c_int32, _STRS, c_int32, POINTER(c_int32), POINTER(CapfExpr),
+                                      POINTER(c_int32), POINTER(c_double), _STRS, _PT]),
     "capf_table_with_columns": (c_int32, [_T, c_int32, POINTER(CapfExpr), _STRS, _PT]),
+    "capf_table_explode_values": (c_int32, [_T, c_char_p, c_int32, c_int64, c_void_p, c_void_p, _PT]),
+    "capf_table_explode_list": (c_int32, [_T, c_char_p, c_char_p, _PT]),
     "capf_table_show": (c_int32, [_T, c_int32]),
     "capf_rmat_rel_table": (c_int32, [_S, c_int32, c_uint64, c_uint32, c_uint32, c_uint32, c_int64,
                                       c_int64, c_int64, c_char_p, c_char_p, c_char_p, _PT]),

@@ -164,8 +164,15 @@ enum Op : int32_t {
   OP_MUL = CAPF_OP_MUL, OP_DIV = CAPF_OP_DIV, OP_MOD = CAPF_OP_MOD, OP_NEG = CAPF_OP_NEG,
   OP_TO_FLOAT = CAPF_OP_TO_FLOAT, OP_TO_INTEGER = CAPF_OP_TO_INTEGER,
   OP_COALESCE = CAPF_OP_COALESCE, OP_STR_LEN = CAPF_OP_STR_LEN, OP_LIST_SIZE = CAPF_OP_LIST_SIZE,
-  OP_IF = CAPF_OP_IF
+  OP_IF = CAPF_OP_IF, OP_ROUND = CAPF_OP_ROUND, OP_ABS = CAPF_OP_ABS, OP_CEIL = CAPF_OP_CEIL,
+  OP_FLOOR = CAPF_OP_FLOOR, OP_SIGN = CAPF_OP_SIGN, OP_SQRT = CAPF_OP_SQRT, OP_LOG = CAPF_OP_LOG,
+  OP_LOG10 = CAPF_OP_LOG10, OP_EXP = CAPF_OP_EXP, OP_SIN = CAPF_OP_SIN, OP_COS = CAPF_OP_COS,
+  OP_TAN = CAPF_OP_TAN, OP_ASIN = CAPF_OP_ASIN, OP_ACOS = CAPF_OP_ACOS, OP_ATAN = CAPF_OP_ATAN,
+  OP_DEGREES = CAPF_OP_DEGREES, OP_RADIANS = CAPF_OP_RADIANS, OP_ATAN2 = CAPF_OP_ATAN2,
+  OP_TO_BOOLEAN = CAPF_OP_TO_BOOLEAN
 };
+// unary math opcodes (one operand, one result)
+inline bool is_math1(int32_t op) { return op >= OP_ROUND && op <= OP_RADIANS; }
 
 struct Instr {
   int32_t op;
@@ -245,12 +252,13 @@ __device__ inline bool ft_load(const FtOperand &o, int64_t r, int64_t &val) {
 
 // ------------------------------------------------------------- plan nodes
 enum class Kind {
-  Source, Select, Filter, Join, Union, Distinct, Group, WithColumns, OrderBy, Skip, Limit
+  Source, Select, Filter, Join, Union, Distinct, Group, WithColumns, OrderBy, Skip, Limit, Explode
 };
 
 struct AggSpec {
   int32_t kind;
   bool distinct;
+  double param = 0;  // percentile fraction (CAPF_AGG_PERCENTILE_*)
   Program arg;  // empty for COUNT_STAR
   std::string name;
   Type out_type;
@@ -278,6 +286,11 @@ struct Node {
   std::vector<int32_t> desc;
   // Skip / Limit
   int64_t count = 0;
+  // Explode (UNWIND): a constant list (explode_list_col < 0) or the LIST
+  // column explode_list_col of the child; the element column is the last
+  // output column
+  int explode_list_col = -1;
+  ColPtr explode_values;  // the constant list as a column of its elements
 
   // memoised result
   std::mutex mu;
@@ -338,6 +351,10 @@ struct Session {
   // device table of the strings' lengths (CAPF_OP_STR_LEN), grown on demand
   BufPtr d_str_len;
   size_t d_str_len_n = 0;
+  // device table of the strings as booleans (CAPF_OP_TO_BOOLEAN): 0 false,
+  // 1 true, 2 neither (NULL)
+  BufPtr d_str_bool;
+  size_t d_str_bool_n = 0;
   // small device scratch for scalar results
   int64_t *d_scalars = nullptr;  // 64 slots
   int64_t *h_scalars = nullptr;  // pinned mirror
@@ -453,7 +470,10 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
                      const FtProgram *pred = nullptr);
 // Aggregations over a grouping.
 ColPtr aggregate(Session *s, const Grouping &g, const Data &d, int64_t nrows, int32_t kind,
-                 const ColPtr &arg, Type out_type);
+                 const ColPtr &arg, Type out_type, double param = 0);
+// UNWIND: every row of d repeated per element (explode, kernels_basic.hip)
+DataPtr explode_values(Session *s, const Data &d, const ColPtr &values);
+DataPtr explode_list(Session *s, const Data &d, int list_col);
 // collect(arg) per group (lists.hip): a Type::List column of g.ngroups lists.
 ColPtr collect_lists(Session *s, const Grouping &g, int64_t nrows, const ColPtr &arg,
                      bool distinct);
@@ -473,6 +493,8 @@ ColPtr decode_column(Session *s, const ColPtr &c);
 // Device table of the session's string lengths by code (UTF-16 units), for
 // CAPF_OP_STR_LEN; *n = strings covered.
 const int64_t *string_length_table(Session *s, size_t *n);
+// Device table of the session's strings parsed as booleans (CAPF_OP_TO_BOOLEAN).
+const uint8_t *string_bool_table(Session *s, size_t *n);
 // Record an error for capf_last_error() (used by entry points outside runtime.cpp).
 int32_t record_error(int32_t code, const char *msg);
 

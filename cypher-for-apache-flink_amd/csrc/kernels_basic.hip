@@ -718,6 +718,50 @@ __device__ inline int cmp_vals(const Val &a, const Val &b) {
   return a.b < b.b ? -1 : (a.b > b.b ? 1 : 0);
 }
 
+// Unary math functions (FlinkSQLExprMapper.scala:199-221), NULL in NULL out.
+// Products / quotients are written with explicit _rn intrinsics so no FMA
+// contraction changes the Java double arithmetic they restate.
+__device__ inline Val math1(int32_t op, const Val &a) {
+  const bool isint = a.t == CAPF_TYPE_INT64;
+  if (a.nul) {
+    const bool keeps = op == OP_ABS || op == OP_CEIL || op == OP_FLOOR || op == OP_SIGN;
+    return mknull(keeps && isint ? CAPF_TYPE_INT64 : CAPF_TYPE_FLOAT64);
+  }
+  const double x = vf(a);
+  switch (op) {
+    case OP_ROUND: {  // half away from zero (Spark round → BigDecimal HALF_UP), a FLOAT
+      if (isint) return mkf(x);
+      double r = trunc(x);
+      const double f = x - r;  // exact
+      if (f >= 0.5) r += 1.0;
+      else if (f <= -0.5) r -= 1.0;
+      return mkf(r);
+    }
+    case OP_ABS:
+      if (isint) return mk(a.b < 0 ? (int64_t)(0 - (uint64_t)a.b) : a.b, CAPF_TYPE_INT64, 0);
+      return mkf(fabs(x));
+    case OP_CEIL: return isint ? a : mkf(ceil(x));
+    case OP_FLOOR: return isint ? a : mkf(floor(x));
+    case OP_SIGN:  // Calcite SIGN keeps the operand's type
+      if (isint) return mk(a.b > 0 ? 1 : (a.b < 0 ? -1 : 0), CAPF_TYPE_INT64, 0);
+      return mkf(x > 0 ? 1.0 : (x < 0 ? -1.0 : x));
+    case OP_SQRT: return mkf(sqrt(x));
+    case OP_LOG: return mkf(log(x));
+    case OP_LOG10: return mkf(log10(x));
+    case OP_EXP: return mkf(exp(x));
+    case OP_SIN: return mkf(sin(x));
+    case OP_COS: return mkf(cos(x));
+    case OP_TAN: return mkf(tan(x));
+    case OP_ASIN: return mkf(asin(x));
+    case OP_ACOS: return mkf(acos(x));
+    case OP_ATAN: return mkf(atan(x));
+    // Java 8 Math.toDegrees / toRadians: angrad * 180.0 / PI, angdeg / 180.0 * PI
+    case OP_DEGREES: return mkf(__ddiv_rn(__dmul_rn(x, 180.0), 3.141592653589793));
+    case OP_RADIANS: return mkf(__dmul_rn(__ddiv_rn(x, 180.0), 3.141592653589793));
+    default: return mknull(CAPF_TYPE_FLOAT64);
+  }
+}
+
 constexpr int MAX_STACK = 24;
 constexpr int MAX_LDS_CODE = 96;
 
@@ -892,6 +936,28 @@ __device__ Val run_program(const Instr *code, int ncode, const ColView *cols, in
         st[sp++] = (!c.nul && c.b != 0) ? v : e;
         break;
       }
+      case OP_ROUND: case OP_ABS: case OP_CEIL: case OP_FLOOR: case OP_SIGN: case OP_SQRT:
+      case OP_LOG: case OP_LOG10: case OP_EXP: case OP_SIN: case OP_COS: case OP_TAN:
+      case OP_ASIN: case OP_ACOS: case OP_ATAN: case OP_DEGREES: case OP_RADIANS: {
+        Val a = st[--sp];
+        st[sp++] = math1(in.op, a);
+        break;
+      }
+      case OP_ATAN2: {  // atan2(y, x): y pushed first (FlinkSQLExprMapper.scala:212)
+        Val x = st[--sp], y = st[--sp];
+        st[sp++] = (x.nul || y.nul) ? mknull(CAPF_TYPE_FLOAT64) : mkf(atan2(vf(y), vf(x)));
+        break;
+      }
+      case OP_TO_BOOLEAN: {  // cols[in.i] = the session's strings parsed as booleans
+        Val a = st[--sp];
+        if (a.nul || a.t == CAPF_TYPE_BOOL) {
+          st[sp++] = a.nul ? mknull(CAPF_TYPE_BOOL) : a;
+        } else {
+          const uint8_t b = ((const uint8_t *)cols[in.i].data)[a.b];
+          st[sp++] = b == 2 ? mknull(CAPF_TYPE_BOOL) : mkb(b == 1);
+        }
+        break;
+      }
       default: st[sp++] = mknull(CAPF_TYPE_NULL); break;
     }
   }
@@ -950,6 +1016,8 @@ static DeviceProgram upload_program(Session *s, const Program &p,
     if (idx < 0) illegal("expression references unknown column '" + nm + "'");
     const ColPtr &c = d.cols[idx];
     if (c->type == Type::List && !scalar_use[j]) {  // size(list): the offsets [n + 1]
+      force(c);
+      if (c->is_const) illegal("internal: constant LIST column");
       ColView v{c->data ? c->data->p : nullptr, c->valid ? (const uint8_t *)c->valid->p : nullptr,
                 (int32_t)Type::List, ENC_PLAIN, 0};
       views.push_back(v);
@@ -968,6 +1036,16 @@ static DeviceProgram upload_program(Session *s, const Program &p,
         if (x.op == OP_STR_LEN) x.i = in.i;
       break;
     }
+  for (auto &in : code)
+    if (in.op == OP_TO_BOOLEAN) {  // the session's strings as booleans, one more view
+      size_t nstr = 0;
+      const uint8_t *tb = string_bool_table(s, &nstr);
+      in.i = (int64_t)views.size();
+      views.push_back(ColView{tb, nullptr, (int32_t)Type::Bool, ENC_PLAIN, 0});
+      for (auto &x : code)
+        if (x.op == OP_TO_BOOLEAN) x.i = in.i;
+      break;
+    }
   dp.ncode = (int)code.size();
   dp.ncols = (int)views.size();
   // stack depth check (host) — the device stack is fixed size
@@ -978,9 +1056,11 @@ static DeviceProgram upload_program(Session *s, const Program &p,
       case OP_LIT_NULL: case OP_LIST_SIZE: depth++; break;
       case OP_AND: case OP_OR: case OP_COALESCE: depth -= (int)in.i - 1; break;
       case OP_NOT: case OP_IS_NULL: case OP_IS_NOT_NULL: case OP_NEG: case OP_TO_FLOAT:
-      case OP_TO_INTEGER: case OP_STR_LEN: break;
+      case OP_TO_INTEGER: case OP_STR_LEN: case OP_TO_BOOLEAN: break;
       case OP_IF: depth -= 2; break;
-      default: depth -= 1; break;
+      default:
+        if (!is_math1(in.op)) depth -= 1;  // binary operators; unary math keeps the depth
+        break;
     }
     maxd = std::max(maxd, depth);
   }

@@ -556,9 +556,12 @@ __global__ void k_fs_nchunks(const unsigned long long *cnt, int64_t ng, uint32_t
 
 // one wave per chunk: (group, chunk within group) found by a binary search over
 // the groups' first chunks; rows [off[g] + c·FS_CHUNK, …) of the sorted order
+// center non-null (stDev's second pass): each value is replaced by its squared
+// deviation from its group's double-double mean, the square kept exactly as
+// the pair (p, fma(d, d, −p))
 __global__ __launch_bounds__(256) void k_fs_chunks(const uint32_t *rows, ColView arg, const int64_t *off,
                                                    const uint32_t *chunk0, int64_t ng, uint32_t nchunks,
-                                                   double2 *part) {
+                                                   const double2 *center, double2 *part) {
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / 64, lane = threadIdx.x & 63;
   const uint32_t nw = gridDim.x * blockDim.x / 64;
   for (uint32_t c = wave; c < nchunks; c += nw) {
@@ -572,7 +575,18 @@ __global__ __launch_bounds__(256) void k_fs_chunks(const uint32_t *rows, ColView
     const int64_t b = off[g] + (int64_t)(c - chunk0[g]) * FS_CHUNK;
     const int64_t e = min(off[g + 1], b + FS_CHUNK);
     DD acc{0.0, 0.0};
-    for (int64_t i = b + lane; i < e; i += 64) acc = dd_add_d(acc, ((const double *)arg.data)[rows[i]]);
+    if (center) {
+      const double2 m = center[g];
+      for (int64_t i = b + lane; i < e; i += 64) {
+        const double d = (load_num<double>(arg, rows[i]) - m.x) - m.y;
+        const double p = d * d;
+        acc = dd_add(acc, DD{p, fma(d, d, -p)});
+      }
+    } else if (arg.type == CAPF_TYPE_FLOAT64) {
+      for (int64_t i = b + lane; i < e; i += 64) acc = dd_add_d(acc, ((const double *)arg.data)[rows[i]]);
+    } else {
+      for (int64_t i = b + lane; i < e; i += 64) acc = dd_add_d(acc, load_num<double>(arg, rows[i]));
+    }
     acc = dd_wave_sum(acc);
     if (lane == 0) part[c] = make_double2(acc.hi, acc.lo);
   }
@@ -581,7 +595,7 @@ __global__ __launch_bounds__(256) void k_fs_chunks(const uint32_t *rows, ColView
 // one wave per group over its chunk partials, then the final value
 __global__ __launch_bounds__(256) void k_fs_groups(const double2 *part, const uint32_t *chunk0,
                                                    const unsigned long long *cnt, int64_t ng, int avg,
-                                                   double *out, uint8_t *valid) {
+                                                   double *out, uint8_t *valid, double2 *dd_out) {
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64;
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * blockDim.x / 64;
@@ -592,7 +606,9 @@ __global__ __launch_bounds__(256) void k_fs_groups(const double2 *part, const ui
       acc = dd_add(acc, DD{p.x, p.y});
     }
     acc = dd_wave_sum(acc);
-    if (lane == 0) {
+    if (lane == 0 && dd_out) {
+      dd_out[g] = make_double2(acc.hi, acc.lo);
+    } else if (lane == 0) {
       const unsigned long long n = cnt[g];
       const double v = dd_value(acc);
       out[g] = n > 0 ? (avg ? v / (double)n : v) : 0.0;
@@ -601,63 +617,248 @@ __global__ __launch_bounds__(256) void k_fs_groups(const double2 *part, const ui
   }
 }
 
-static void fp64_sum_groups(Session *s, const Grouping &g, int64_t nrows, const ColPtr &arg, bool avg,
-                            const ColPtr &o) {
-  const int64_t ng = g.ngroups;
-  if (nrows >= (int64_t(1) << 32)) not_impl("FLOAT sum / avg over 2^32 or more rows");
-  force(arg);
-  const ColView av = view_of(arg);
-  BufPtr cnt = s->alloc(8 * (ng + 1));
-  HIP_CHECK(hipMemsetAsync(cnt->p, 0, 8 * (ng + 1), s->stream));
+// The fixed summation order of a grouping: rows with a non-NULL argument
+// sorted by group (stable), group offsets and the chunk layout of each group.
+struct FsLayout {
+  int64_t ng = 0;
+  BufPtr srow, off, ch0, cnt;
+  uint32_t nchunks = 0;
+};
+
+static FsLayout fs_layout(Session *s, const Grouping &g, int64_t nrows, const ColView &av) {
+  FsLayout L;
+  const int64_t ng = L.ng = g.ngroups;
+  if (nrows >= (int64_t(1) << 32)) not_impl("FLOAT sum / avg / stDev over 2^32 or more rows");
+  L.cnt = s->alloc(8 * (ng + 1));
+  HIP_CHECK(hipMemsetAsync(L.cnt->p, 0, 8 * (ng + 1), s->stream));
   const int64_t n1 = std::max<int64_t>(nrows, 1);
-  BufPtr key = s->alloc(8 * n1), skey = s->alloc(8 * n1), row = s->alloc(4 * n1), srow = s->alloc(4 * n1);
+  BufPtr key = s->alloc(8 * n1), skey = s->alloc(8 * n1), row = s->alloc(4 * n1);
+  L.srow = s->alloc(4 * n1);
   KernelTimer kt(s, "group_fsum", 16.0 * nrows);
   if (nrows > 0) {
     hipLaunchKernelGGL(k_fs_keys, dim3(grid_for(nrows, 256)), dim3(256), 0, s->stream,
                        (const int64_t *)g.group_of_row->p, av, nrows, ng, (uint64_t *)key->p, (uint32_t *)row->p,
-                       (unsigned long long *)cnt->p);
+                       (unsigned long long *)L.cnt->p);
     KERNEL_CHECK();
     int bits = 1;
     while (bits < 64 && (uint64_t(1) << bits) <= (uint64_t)ng) ++bits;
     size_t tmp = 0;
     HIP_CHECK(rocprim::radix_sort_pairs(nullptr, tmp, (const uint64_t *)key->p, (uint64_t *)skey->p,
-                                        (const uint32_t *)row->p, (uint32_t *)srow->p, (size_t)nrows, 0, bits,
+                                        (const uint32_t *)row->p, (uint32_t *)L.srow->p, (size_t)nrows, 0, bits,
                                         s->stream));
     BufPtr t = s->alloc(std::max<size_t>(tmp, 16));
     HIP_CHECK(rocprim::radix_sort_pairs(t->p, tmp, (const uint64_t *)key->p, (uint64_t *)skey->p,
-                                        (const uint32_t *)row->p, (uint32_t *)srow->p, (size_t)nrows, 0, bits,
+                                        (const uint32_t *)row->p, (uint32_t *)L.srow->p, (size_t)nrows, 0, bits,
                                         s->stream));
   }
   // group offsets in the sorted order and first chunks
-  BufPtr off = s->alloc(8 * (ng + 1)), nch = s->alloc(4 * (ng + 1)), ch0 = s->alloc(4 * (ng + 1));
-  exclusive_scan_i64(s, (const int64_t *)cnt->p, (int64_t *)off->p, ng + 1);
+  L.off = s->alloc(8 * (ng + 1));
+  BufPtr nch = s->alloc(4 * (ng + 1));
+  L.ch0 = s->alloc(4 * (ng + 1));
+  exclusive_scan_i64(s, (const int64_t *)L.cnt->p, (int64_t *)L.off->p, ng + 1);
   hipLaunchKernelGGL(k_fs_nchunks, dim3(grid_for(ng + 1, 256)), dim3(256), 0, s->stream,
-                     (const unsigned long long *)cnt->p, ng, (uint32_t *)nch->p);
+                     (const unsigned long long *)L.cnt->p, ng, (uint32_t *)nch->p);
   KERNEL_CHECK();
   BufPtr tot = s->alloc(16);
-  exclusive_scan_u32_async(s, (const uint32_t *)nch->p, (uint32_t *)ch0->p, ng + 1, (uint32_t *)tot->p);
-  uint32_t nchunks = 0;
-  HIP_CHECK(hipMemcpyAsync(&nchunks, (const uint32_t *)ch0->p + ng, 4, hipMemcpyDeviceToHost, s->stream));
+  exclusive_scan_u32_async(s, (const uint32_t *)nch->p, (uint32_t *)L.ch0->p, ng + 1, (uint32_t *)tot->p);
+  HIP_CHECK(hipMemcpyAsync(&L.nchunks, (const uint32_t *)L.ch0->p + ng, 4, hipMemcpyDeviceToHost, s->stream));
   s->sync();
-  BufPtr part = s->alloc(16 * std::max<uint32_t>(nchunks, 1));
-  if (nchunks > 0) {
-    hipLaunchKernelGGL(k_fs_chunks, dim3(grid_for((int64_t)nchunks * 64, 256, (int64_t)s->num_cus * 64)),
-                       dim3(256), 0, s->stream, (const uint32_t *)srow->p, av, (const int64_t *)off->p,
-                       (const uint32_t *)ch0->p, ng, nchunks, (double2 *)part->p);
+  return L;
+}
+
+// One compensated pass over the layout: per group the double-double sum of
+// the values (center null) or of the squared deviations from center[g];
+// avg / sum finals into (out, valid), or the raw sums into dd_out.
+static void fs_pass(Session *s, const FsLayout &L, const ColView &av, const double2 *center, int avg,
+                    double *out, uint8_t *valid, double2 *dd_out) {
+  BufPtr part = s->alloc(16 * std::max<uint32_t>(L.nchunks, 1));
+  if (L.nchunks > 0) {
+    hipLaunchKernelGGL(k_fs_chunks, dim3(grid_for((int64_t)L.nchunks * 64, 256, (int64_t)s->num_cus * 64)),
+                       dim3(256), 0, s->stream, (const uint32_t *)L.srow->p, av, (const int64_t *)L.off->p,
+                       (const uint32_t *)L.ch0->p, L.ng, L.nchunks, center, (double2 *)part->p);
     KERNEL_CHECK();
   }
-  hipLaunchKernelGGL(k_fs_groups, dim3(grid_for(ng * 64, 256, (int64_t)s->num_cus * 64)), dim3(256), 0, s->stream,
-                     (const double2 *)part->p, (const uint32_t *)ch0->p, (const unsigned long long *)cnt->p, ng,
-                     avg ? 1 : 0, (double *)o->data->p, (uint8_t *)o->valid->p);
+  hipLaunchKernelGGL(k_fs_groups, dim3(grid_for(L.ng * 64, 256, (int64_t)s->num_cus * 64)), dim3(256), 0,
+                     s->stream, (const double2 *)part->p, (const uint32_t *)L.ch0->p,
+                     (const unsigned long long *)L.cnt->p, L.ng, avg, out, valid, dd_out);
+  KERNEL_CHECK();
+}
+
+static void fp64_sum_groups(Session *s, const Grouping &g, int64_t nrows, const ColPtr &arg, bool avg,
+                            const ColPtr &o) {
+  force(arg);
+  const ColView av = view_of(arg);
+  FsLayout L = fs_layout(s, g, nrows, av);
+  fs_pass(s, L, av, nullptr, avg ? 1 : 0, (double *)o->data->p, (uint8_t *)o->valid->p, nullptr);
+}
+
+// ------------------------------------------------------------ stDev / stDevP
+// StDev / StDevP (Expr.scala:1120-1128 → Flink stddevSamp / stddevPop,
+// FlinkSQLExprMapper.scala:223-224) over the same fixed order as sum: the
+// double-double mean of each group (pass 1 ÷ n, a DD quotient), then the
+// double-double sum of squared deviations (pass 2), sqrt(M2 / (n − 1)) or
+// sqrt(M2 / n).  The deviations are taken from the DD mean, so the result
+// stays within a few ulp of the exact value also when mean ≫ spread.
+__global__ void k_dd_mean(const double2 *sum, const unsigned long long *cnt, int64_t ng, double2 *mean) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ng; g += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned long long c = cnt[g];
+    if (c == 0) {
+      mean[g] = make_double2(0.0, 0.0);
+      continue;
+    }
+    const double n = (double)c, q1 = sum[g].x / n;
+    const double r = fma(-q1, n, sum[g].x) + sum[g].y;  // sum − q1·n, exact in its first term
+    mean[g] = make_double2(q1, r / n);
+  }
+}
+
+__global__ void k_stdev_final(const double2 *m2, const unsigned long long *cnt, int64_t ng, int samp, double *out,
+                              uint8_t *valid) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ng; g += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned long long c = cnt[g];
+    const bool ok = samp ? c >= 2 : c >= 1;
+    valid[g] = ok ? 1 : 0;
+    const double ss = m2[g].x + m2[g].y;
+    out[g] = ok ? sqrt(ss / (double)(samp ? c - 1 : c)) : 0.0;
+  }
+}
+
+static void stdev_groups(Session *s, const Grouping &g, int64_t nrows, const ColPtr &arg, bool samp,
+                         const ColPtr &o) {
+  force(arg);
+  const ColView av = view_of(arg);
+  FsLayout L = fs_layout(s, g, nrows, av);
+  const int64_t ng = L.ng;
+  BufPtr sums = s->alloc(16 * ng), mean = s->alloc(16 * ng), m2 = s->alloc(16 * ng);
+  fs_pass(s, L, av, nullptr, 0, nullptr, nullptr, (double2 *)sums->p);
+  hipLaunchKernelGGL(k_dd_mean, dim3(grid_for(ng, 256)), dim3(256), 0, s->stream, (const double2 *)sums->p,
+                     (const unsigned long long *)L.cnt->p, ng, (double2 *)mean->p);
+  KERNEL_CHECK();
+  fs_pass(s, L, av, (const double2 *)mean->p, 0, nullptr, nullptr, (double2 *)m2->p);
+  hipLaunchKernelGGL(k_stdev_final, dim3(grid_for(ng, 256)), dim3(256), 0, s->stream, (const double2 *)m2->p,
+                     (const unsigned long long *)L.cnt->p, ng, samp ? 1 : 0, (double *)o->data->p,
+                     (uint8_t *)o->valid->p);
+  KERNEL_CHECK();
+}
+
+// ------------------------------------------------------- percentiles
+// PercentileCont / PercentileDisc (Expr.scala:1096-1118) with the semantics of
+// the Spark backend's UDAFs (morpheus-spark-cypher/.../impl/expressions/
+// PercentileUdafs.scala:59-96; the Flink mapper has no case for them): the
+// group's non-NULL values sorted ascending (stable radix sorts: by value, then
+// by group, NULL arguments last), then per group one thread picks
+//   disc: v[pos − 1] (v[0] when pos = 0), pos = Math.round(n · p)
+//   cont: x = 1 + (n − 1) · p, v[x − 1] when x is integral, else
+//         (1 − w) · v[⌈x⌉ − 1] + w · v[⌊x⌋ − 1] with w = ⌈x⌉ − x
+// in IEEE double arithmetic without contraction (as the JVM computes it).
+__global__ void k_pct_keys(const int64_t *gid, ColView arg, int64_t n, int64_t ng, uint64_t *gkey,
+                           uint64_t *vkey, unsigned long long *cnt) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    int64_t g = gid ? gid[r] : 0;
+    if (g < 0 || (arg.valid && !arg.valid[r])) g = ng;
+    else atomicAdd(&cnt[g], 1ull);
+    gkey[r] = (uint64_t)g;
+    uint64_t k;
+    if (arg.type == CAPF_TYPE_FLOAT64) {
+      uint64_t b = ((const uint64_t *)arg.data)[r];
+      if (b == 0x8000000000000000ull) b = 0;
+      k = (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+    } else {
+      k = (uint64_t)ld_int(arg, r) ^ 0x8000000000000000ull;
+    }
+    vkey[r] = k;
+  }
+}
+
+__device__ inline double pct_round(double x) {  // Scala Double.round (Math.round) for x >= 0
+  double r = floor(x);
+  if (x - r >= 0.5) r += 1.0;
+  return r;
+}
+
+__global__ void k_pct_final(const int64_t *perm, const int64_t *off, const unsigned long long *cnt, int64_t ng,
+                            ColView arg, int cont, double p, int out_int, void *out, uint8_t *valid) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ng; g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = (int64_t)cnt[g];
+    valid[g] = c > 0 ? 1 : 0;
+    if (c == 0) {
+      if (out_int) ((int64_t *)out)[g] = 0;
+      else ((double *)out)[g] = 0.0;
+      continue;
+    }
+    const int64_t *v = perm + off[g];
+    if (!cont) {
+      const int64_t pos = (int64_t)pct_round(__dmul_rn((double)c, p));
+      const int64_t row = v[pos == 0 ? 0 : pos - 1];
+      if (out_int) ((int64_t *)out)[g] = ld_int(arg, row);
+      else ((double *)out)[g] = load_num<double>(arg, row);
+      continue;
+    }
+    const double x = __dadd_rn(1.0, __dmul_rn((double)(c - 1), p));
+    const double fl = floor(x), ce = ceil(x);
+    const int64_t prec = (int64_t)fl, succ = (int64_t)ce;
+    const double w = __dsub_rn(ce, x);
+    double res;
+    if (x == ce) {
+      res = load_num<double>(arg, v[prec - 1]);
+    } else {
+      const double a = load_num<double>(arg, v[succ - 1]), b = load_num<double>(arg, v[prec - 1]);
+      res = __dadd_rn(__dmul_rn(__dsub_rn(1.0, w), a), __dmul_rn(w, b));
+    }
+    ((double *)out)[g] = res;
+  }
+}
+
+static void radix_pass(Session *s, const uint64_t *keys_in, BufPtr &perm, int64_t n, int bits);
+
+static void percentile_groups(Session *s, const Grouping &g, int64_t nrows, const ColPtr &arg, bool cont,
+                              double p, const ColPtr &o) {
+  force(arg);
+  const ColView av = view_of(arg);
+  const int64_t ng = g.ngroups;
+  BufPtr cnt = s->alloc(8 * (ng + 1));
+  HIP_CHECK(hipMemsetAsync(cnt->p, 0, 8 * (ng + 1), s->stream));
+  const int64_t n1 = std::max<int64_t>(nrows, 1);
+  BufPtr gkey = s->alloc(8 * n1), vkey = s->alloc(8 * n1);
+  BufPtr perm = iota_index(s, 0, nrows);
+  if (nrows > 0) {
+    hipLaunchKernelGGL(k_pct_keys, dim3(grid_for(nrows, 256)), dim3(256), 0, s->stream,
+                       (const int64_t *)g.group_of_row->p, av, nrows, ng, (uint64_t *)gkey->p, (uint64_t *)vkey->p,
+                       (unsigned long long *)cnt->p);
+    KERNEL_CHECK();
+    int bits = 1;
+    while (bits < 64 && (uint64_t(1) << bits) <= (uint64_t)ng) ++bits;
+    radix_pass(s, (const uint64_t *)vkey->p, perm, nrows, 64);
+    radix_pass(s, (const uint64_t *)gkey->p, perm, nrows, bits);
+  }
+  BufPtr off = s->alloc(8 * (ng + 1));
+  exclusive_scan_i64(s, (const int64_t *)cnt->p, (int64_t *)off->p, ng + 1);
+  const bool out_int = o->type == Type::Int64;
+  hipLaunchKernelGGL(k_pct_final, dim3(grid_for(ng, 256)), dim3(256), 0, s->stream, (const int64_t *)perm->p,
+                     (const int64_t *)off->p, (const unsigned long long *)cnt->p, ng, av, cont ? 1 : 0, p,
+                     out_int ? 1 : 0, o->data->p, (uint8_t *)o->valid->p);
   KERNEL_CHECK();
 }
 
 ColPtr aggregate(Session *s, const Grouping &g, const Data &d, int64_t nrows, int32_t kind,
-                 const ColPtr &arg, Type out_type) {
+                 const ColPtr &arg, Type out_type, double param) {
   (void)d;
   int64_t ng = g.ngroups;
   ColPtr o = make_column(s, out_type, ng, true);
   if (ng == 0) return o;
+  if (kind == CAPF_AGG_STDEV || kind == CAPF_AGG_STDEV_POP || kind == CAPF_AGG_PERCENTILE_CONT ||
+      kind == CAPF_AGG_PERCENTILE_DISC) {
+    if (!arg || arg->type == Type::Null || nrows == 0) {  // no values anywhere: NULL per group
+      HIP_CHECK(hipMemsetAsync(o->data->p, 0, type_width(out_type) * ng, s->stream));
+      HIP_CHECK(hipMemsetAsync(o->valid->p, 0, ng, s->stream));
+      return o;
+    }
+    if (kind == CAPF_AGG_STDEV || kind == CAPF_AGG_STDEV_POP)
+      stdev_groups(s, g, nrows, arg, kind == CAPF_AGG_STDEV, o);
+    else
+      percentile_groups(s, g, nrows, arg, kind == CAPF_AGG_PERCENTILE_CONT, param, o);
+    return o;
+  }
   bool fl = arg && arg->type == Type::Float64;
   if (fl && out_type == Type::Float64 && (kind == CAPF_AGG_SUM || kind == CAPF_AGG_AVG)) {
     fp64_sum_groups(s, g, nrows, arg, kind == CAPF_AGG_AVG, o);

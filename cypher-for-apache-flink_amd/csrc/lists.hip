@@ -152,4 +152,98 @@ ColPtr gather_list(Session *s, const ColPtr &c, const int64_t *d_idx, int64_t m)
   return o;
 }
 
+// ---------------------------------------------------------------- UNWIND
+// withColumns(Explode(list) AS item) (RelationalPlanner.scala:99-101): row i of
+// the output is input row i / k with element i % k of the constant list
+// (k elements): two index columns, every input column a lazy gather of the
+// first, the element column a gather of the second.
+__global__ void k_explode_idx(int64_t m, int64_t k, int64_t *row, int64_t *elem) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / k;
+    row[i] = r;
+    elem[i] = i - r * k;
+  }
+}
+
+DataPtr explode_values(Session *s, const Data &d, const ColPtr &values) {
+  const int64_t k = values->n, m = d.nrows * k;
+  auto out = std::make_shared<Data>();
+  out->nrows = m;
+  BufPtr row = s->alloc(8 * std::max<int64_t>(m, 1)), elem = s->alloc(8 * std::max<int64_t>(m, 1));
+  if (m > 0) {
+    hipLaunchKernelGGL(k_explode_idx, dim3(grid_for(m, 256)), dim3(256), 0, s->stream, m, k,
+                       (int64_t *)row->p, (int64_t *)elem->p);
+    KERNEL_CHECK();
+  }
+  IdxCache cache;
+  for (auto &c : d.cols) out->cols.push_back(gather_lazy(s, c, row, m, false, &cache));
+  out->cols.push_back(m > 0 ? gather_column(s, values, (const int64_t *)elem->p, m)
+                            : (values->type == Type::Null ? null_column(s, Type::Null, 0)
+                                                          : make_column(s, values->type, 0, false)));
+  return out;
+}
+
+// a LIST column: output rows [off[r], off[r+1]) come from input row r and
+// hold its elements in order (the element column is the list's child, as is)
+__global__ void k_explode_list_rows(const int64_t *off, const uint8_t *valid, int64_t n, int64_t *row) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    if (valid && !valid[r]) continue;
+    for (int64_t q = off[r]; q < off[r + 1]; ++q) row[q] = r;
+  }
+}
+// drop the elements of NULL lists: their element rows keep row = -1
+__global__ void k_row_flags(const int64_t *row, int64_t n, uint8_t *flags) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    flags[i] = row[i] >= 0 ? 1 : 0;
+}
+
+DataPtr explode_list(Session *s, const Data &d, int list_col) {
+  const ColPtr &lc = d.cols[(size_t)list_col];
+  auto out = std::make_shared<Data>();
+  if (lc->type == Type::Null || d.nrows == 0) {  // nothing to unwind
+    out->nrows = 0;
+    BufPtr none = s->alloc(8);
+    for (auto &c : d.cols) out->cols.push_back(gather_column(s, c, (const int64_t *)none->p, 0, false));
+    out->cols.push_back(null_column(s, lc->type == Type::Null ? Type::Null : lc->child->type, 0));
+    return out;
+  }
+  force(lc);
+  int64_t total = 0;
+  HIP_CHECK(hipMemcpyAsync(&total, (const int64_t *)lc->data->p + d.nrows, 8, hipMemcpyDeviceToHost, s->stream));
+  s->sync();
+  BufPtr row = s->alloc(8 * std::max<int64_t>(total, 1));
+  ColPtr elems = lc->child;
+  int64_t m = total;
+  if (total > 0) {
+    HIP_CHECK(hipMemsetAsync(row->p, 0xFF, 8 * total, s->stream));
+    hipLaunchKernelGGL(k_explode_list_rows, dim3(grid_for(d.nrows, 256)), dim3(256), 0, s->stream,
+                       (const int64_t *)lc->data->p, lc->valid ? (const uint8_t *)lc->valid->p : nullptr, d.nrows,
+                       (int64_t *)row->p);
+    KERNEL_CHECK();
+    if (lc->valid) {  // elements of NULL lists (if any were stored) are dropped
+      BufPtr flags = s->alloc(total);
+      hipLaunchKernelGGL(k_row_flags, dim3(grid_for(total, 256)), dim3(256), 0, s->stream,
+                         (const int64_t *)row->p, total, (uint8_t *)flags->p);
+      KERNEL_CHECK();
+      BufPtr keep = compact_flags(s, (const uint8_t *)flags->p, total, &m);
+      if (m != total) {
+        ColPtr r64 = std::make_shared<Column>();
+        r64->type = Type::Int64;
+        r64->n = total;
+        r64->data = row;
+        row = gather_column(s, r64, (const int64_t *)keep->p, m)->data;
+        elems = gather_column(s, elems, (const int64_t *)keep->p, m);
+      }
+    }
+  }
+  out->nrows = m;
+  IdxCache cache;
+  for (auto &c : d.cols) out->cols.push_back(gather_lazy(s, c, row, m, false, &cache));
+  out->cols.push_back(elems);
+  return out;
+}
+
 }  // namespace capf

@@ -323,8 +323,34 @@ Type infer_type(const Program &p, const std::vector<std::string> &names,
       case OP_IF: {
         Type v = pop(), c = pop(), e = pop();
         if (c != Type::Bool && c != Type::Null) illegal("condition is not boolean");
-        if (v != Type::Null && e != Type::Null && v != e) illegal("branches of different types");
+        if (v != Type::Null && e != Type::Null && v != e) {
+          if (!(is_numeric(v) && is_numeric(e))) illegal("branches of different types");
+          v = Type::Float64;  // numeric branches widen (Calcite's CASE type)
+        }
         st.push_back(v != Type::Null ? v : e);
+        break;
+      }
+      case OP_ROUND: case OP_ABS: case OP_CEIL: case OP_FLOOR: case OP_SIGN: case OP_SQRT:
+      case OP_LOG: case OP_LOG10: case OP_EXP: case OP_SIN: case OP_COS: case OP_TAN:
+      case OP_ASIN: case OP_ACOS: case OP_ATAN: case OP_DEGREES: case OP_RADIANS: {
+        Type a = pop();
+        if (a != Type::Null && !is_numeric(a)) not_impl(std::string("math function on ") + type_name(a));
+        const bool keeps = in.op == OP_ABS || in.op == OP_CEIL || in.op == OP_FLOOR || in.op == OP_SIGN;
+        st.push_back(keeps && a == Type::Int64 ? Type::Int64 : Type::Float64);
+        break;
+      }
+      case OP_ATAN2: {
+        Type b = pop(), a = pop();
+        if ((a != Type::Null && !is_numeric(a)) || (b != Type::Null && !is_numeric(b)))
+          not_impl("atan2 of non-numeric values");
+        st.push_back(Type::Float64);
+        break;
+      }
+      case OP_TO_BOOLEAN: {
+        Type a = pop();
+        if (a != Type::Null && a != Type::Bool && a != Type::String)
+          not_impl(std::string("toBoolean on ") + type_name(a));
+        st.push_back(Type::Bool);
         break;
       }
       default: not_impl("expression opcode " + std::to_string(in.op));
@@ -544,9 +570,14 @@ static DataPtr materialize_impl(const NodePtr &n) {
           out->cols.push_back(aggregate(s, g2, *c, dg.ngroups, a.kind, darg, a.out_type));
           continue;
         }
-        out->cols.push_back(aggregate(s, g, *c, c->nrows, a.kind, arg, a.out_type));
+        out->cols.push_back(aggregate(s, g, *c, c->nrows, a.kind, arg, a.out_type, a.param));
       }
       return out;
+    }
+    case Kind::Explode: {
+      DataPtr c = materialize(n->kids[0]);
+      return n->explode_list_col >= 0 ? explode_list(s, *c, n->explode_list_col)
+                                      : explode_values(s, *c, n->explode_values);
     }
     case Kind::WithColumns: {
       DataPtr c = materialize(n->kids[0]);
@@ -623,6 +654,31 @@ const int64_t *string_length_table(Session *s, size_t *n) {
   }
   *n = s->d_str_len_n;
   return (const int64_t *)s->d_str_len->p;
+}
+
+// Flink's CAST(string AS BOOLEAN) (FlinkSQLExprMapper.scala:185): 'true' /
+// 'false' in any case, surrounding blanks ignored; anything else is NULL
+static uint8_t parse_bool(const std::string &u) {
+  size_t b = 0, e = u.size();
+  while (b < e && (unsigned char)u[b] <= ' ') ++b;
+  while (e > b && (unsigned char)u[e - 1] <= ' ') --e;
+  std::string t = u.substr(b, e - b);
+  for (auto &ch : t) ch = (char)std::tolower((unsigned char)ch);
+  return t == "true" ? 1 : t == "false" ? 0 : 2;
+}
+
+const uint8_t *string_bool_table(Session *s, size_t *n) {
+  std::lock_guard<std::mutex> lk(s->str_mu);
+  if (s->d_str_bool_n != s->strings.size() || !s->d_str_bool) {
+    std::vector<uint8_t> v(std::max<size_t>(s->strings.size(), 1), 2);
+    for (size_t i = 0; i < s->strings.size(); ++i) v[i] = parse_bool(s->strings[i]);
+    s->d_str_bool = s->alloc(v.size());
+    HIP_CHECK(hipMemcpyAsync(s->d_str_bool->p, v.data(), v.size(), hipMemcpyHostToDevice, s->stream));
+    s->sync();  // the pageable source
+    s->d_str_bool_n = s->strings.size();
+  }
+  *n = s->d_str_bool_n;
+  return (const uint8_t *)s->d_str_bool->p;
 }
 }  // namespace capf
 
@@ -1630,6 +1686,15 @@ capf_status capf_table_group(capf_table *t, int32_t n_by, const char *const *by_
                              int32_t n_aggs, const int32_t *agg_kinds,
                              const capf_expr *agg_args, const int32_t *agg_distinct,
                              const char *const *agg_names, capf_table **out) {
+  return capf_table_group_ex(t, n_by, by_cols, n_aggs, agg_kinds, agg_args, agg_distinct, nullptr, agg_names,
+                             out);
+}
+
+capf_status capf_table_group_ex(capf_table *t, int32_t n_by, const char *const *by_cols,
+                                int32_t n_aggs, const int32_t *agg_kinds,
+                                const capf_expr *agg_args, const int32_t *agg_distinct,
+                                const double *agg_params, const char *const *agg_names,
+                                capf_table **out) {
   CAPF_API_BEGIN
   need(t, "table");
   need(out, "out");
@@ -1647,7 +1712,13 @@ capf_status capf_table_group(capf_table *t, int32_t n_by, const char *const *by_
     a.kind = agg_kinds[i];
     a.distinct = agg_distinct && agg_distinct[i];
     a.name = agg_names[i];
-    if (a.kind < CAPF_AGG_COUNT_STAR || a.kind > CAPF_AGG_COLLECT) illegal("bad aggregator kind");
+    if (a.kind < CAPF_AGG_COUNT_STAR || a.kind > CAPF_AGG_PERCENTILE_DISC) illegal("bad aggregator kind");
+    if (a.kind == CAPF_AGG_PERCENTILE_CONT || a.kind == CAPF_AGG_PERCENTILE_DISC) {
+      if (!agg_params) illegal("percentile aggregator without its fraction (capf_table_group_ex)");
+      a.param = agg_params[i];
+      // Neo4j / openCypher: the percentile must lie in [0, 1]
+      if (!(a.param >= 0.0 && a.param <= 1.0)) illegal("percentile must be between 0.0 and 1.0");
+    }
     if (a.kind == CAPF_AGG_COUNT_STAR) {
       a.out_type = Type::Int64;
     } else {
@@ -1674,6 +1745,16 @@ capf_status capf_table_group(capf_table *t, int32_t n_by, const char *const *by_
           a.out_type = at;
           break;
         case CAPF_AGG_COLLECT: a.out_type = Type::List; break;
+        case CAPF_AGG_STDEV:
+        case CAPF_AGG_STDEV_POP:
+        case CAPF_AGG_PERCENTILE_CONT:
+          if (at != Type::Null && !is_numeric(at)) not_impl("stDev / percentile of non-numeric values");
+          a.out_type = Type::Float64;
+          break;
+        case CAPF_AGG_PERCENTILE_DISC:
+          if (at != Type::Null && !is_numeric(at)) not_impl("percentileDisc of non-numeric values");
+          a.out_type = at == Type::Null ? Type::Float64 : at;
+          break;
       }
     }
     nn->names.push_back(a.name);
@@ -1708,6 +1789,63 @@ capf_status capf_table_with_columns(capf_table *t, int32_t n, const capf_expr *e
     }
     nn->exprs.push_back(std::move(p));
     nn->target_index.push_back(idx);
+  }
+  *out = wrap(nn);
+  CAPF_API_END
+}
+
+capf_status capf_table_explode_values(capf_table *t, const char *name, int32_t type, int64_t n,
+                                      const void *values, const uint8_t *valid, capf_table **out) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(name, "name");
+  need(out, "out");
+  if (n < 0) illegal("negative list length");
+  if (type < CAPF_TYPE_NULL || type > CAPF_TYPE_STRING) illegal("bad list element type");
+  const NodePtr &c = t->node;
+  if (c->col_index(name) >= 0) illegal(std::string("column '") + name + "' already exists");
+  Type ty = (Type)type;
+  if (n > 0 && ty != Type::Null && !values) illegal("list values missing");
+  auto nn = new_node(c->s, Kind::Explode);
+  nn->kids.push_back(c);
+  nn->names = c->names;
+  nn->types = c->types;
+  nn->names.emplace_back(name);
+  nn->types.push_back(ty);
+  Session *s = c->s;
+  ColPtr v = make_column(s, ty, n, valid != nullptr);
+  if (n > 0 && ty != Type::Null)
+    HIP_CHECK(hipMemcpyAsync(v->data->p, values, type_width(ty) * n, hipMemcpyHostToDevice, s->stream));
+  if (n > 0 && valid) HIP_CHECK(hipMemcpyAsync(v->valid->p, valid, n, hipMemcpyHostToDevice, s->stream));
+  s->sync();  // pageable host sources
+  nn->explode_values = v;
+  *out = wrap(nn);
+  CAPF_API_END
+}
+
+capf_status capf_table_explode_list(capf_table *t, const char *list_col, const char *name, capf_table **out) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(list_col, "list_col");
+  need(name, "name");
+  need(out, "out");
+  const NodePtr &c = t->node;
+  int li = c->col_index_or_throw(list_col);
+  if (c->types[li] != Type::List && c->types[li] != Type::Null) illegal("UNWIND of a non-list column");
+  if (c->col_index(name) >= 0) illegal(std::string("column '") + name + "' already exists");
+  auto nn = new_node(c->s, Kind::Explode);
+  nn->kids.push_back(c);
+  nn->names = c->names;
+  nn->types = c->types;
+  nn->names.emplace_back(name);
+  // the element type is known once the list column exists; a NULL-typed
+  // column explodes to nothing
+  nn->types.push_back(Type::Null);
+  nn->explode_list_col = li;
+  if (c->types[li] == Type::List) {
+    DataPtr d = materialize(c);
+    const ColPtr &lc = d->cols[li];
+    nn->types.back() = lc->child ? lc->child->type : Type::Null;
   }
   *out = wrap(nn);
   CAPF_API_END

@@ -51,7 +51,7 @@ import torch.distributed as dist
 
 from . import _lib
 from .expr import (AGG_AVG, AGG_COUNT, AGG_COUNT_STAR, AGG_MAX, AGG_MIN, AGG_SUM, T_BOOL, T_INT, T_NULL, T_STRING, Count,
-                   Divide, Max, Min, Sum, ToFloat, Var)
+                   Divide, Explode, Max, Min, Sum, ToFloat, Var)
 from .header import RecordHeader
 
 ROUTE_MAXK = 8  # routing keys per shuffle (shuffle.hip); a subset of a key tuple routes correctly
@@ -466,6 +466,11 @@ class DistTable:
                           prov=self.prov.without(set(cols)) if self.prov else None)
 
     def withColumns(self, *columns, header=None, params=None):
+        if any(isinstance(e, Explode) for e, _ in columns):
+            # UNWIND multiplies each rank's rows in place: the placement stays,
+            # the projection provenance does not (rows changed)
+            local = self.local.withColumns(*columns, header=header, params=params)
+            return self._wrap(local, self.part - {c for _, c in columns})
         if self._deferred is not None:
             out = list(self._cols)
             for _, c in columns:
@@ -771,10 +776,16 @@ def dist_node_partitioned_graph(dsession, graph, count_copies=None, compact=True
     lo, hi, n = _int_range(nt.table, nt.id_col)
     if n == 0 or hi - lo + 1 != n or nt.table.size != n:
         return g
+    m = rt.table.size
     for c in (rt.src_col, rt.dst_col):
-        a, b, _ = _int_range(rt.table, c)
-        if a < lo or b > hi:
+        a, b, nn = _int_range(rt.table, c)
+        if a < lo or b > hi or nn != m:  # a NULL endpoint: no node-partitioned layout
             return g
+    # Σ in·out − self-loops equals the plan's NOT(r1 = r2) filter only when rel
+    # ids are unique (a repeated id would also drop pairs of distinct rels):
+    # otherwise the chain replays as planned
+    if _int_range(rt.table, rt.id_col)[2] != m or rt.table.select(rt.id_col).distinct().size != m:
+        return g
     total = (count_copies or _gpu_count_copies)(dsession, rt, n, lo, compact)
     ginfo = object()
     node_info = {"complete": True, "graph": ginfo, "id": nt.id_col}

@@ -34,9 +34,13 @@ OP_NOT, OP_AND, OP_OR, OP_IS_NULL, OP_IS_NOT_NULL = 20, 21, 22, 23, 24
 OP_ADD, OP_SUB, OP_MUL, OP_DIV, OP_MOD, OP_NEG = 30, 31, 32, 33, 34, 35
 OP_TO_FLOAT, OP_TO_INTEGER, OP_COALESCE = 40, 41, 50
 OP_STR_LEN, OP_LIST_SIZE, OP_IF = 60, 61, 62
+OP_ROUND, OP_ABS, OP_CEIL, OP_FLOOR, OP_SIGN, OP_SQRT, OP_LOG, OP_LOG10, OP_EXP = 70, 71, 72, 73, 74, 75, 76, 77, 78
+OP_SIN, OP_COS, OP_TAN, OP_ASIN, OP_ACOS, OP_ATAN, OP_DEGREES, OP_RADIANS = 79, 80, 81, 82, 83, 84, 85, 86
+OP_ATAN2, OP_TO_BOOLEAN = 87, 88
 
 # aggregators
 AGG_COUNT_STAR, AGG_COUNT, AGG_SUM, AGG_MIN, AGG_MAX, AGG_AVG, AGG_COLLECT = 0, 1, 2, 3, 4, 5, 6
+AGG_STDEV, AGG_STDEV_POP, AGG_PERCENTILE_CONT, AGG_PERCENTILE_DISC = 7, 8, 9, 10
 
 
 class Expr:
@@ -248,6 +252,77 @@ class In(Expr):
         return f"({self.lhs} IN {self.rhs})"
 
 
+# Mathematical functions (okapi Expr.scala UnaryMathematicalFunctionExpr …;
+# FlinkSQLExprMapper.scala:199-221).  Round: half away from zero, a FLOAT (the
+# Spark mapping round(x).cast(Double), SparkSQLExprMapper.scala:286 — Flink's
+# own case is `child0.round(???)`, which throws).
+Round = _unary("Round", "round({})")
+Abs = _unary("Abs", "abs({})")
+Ceil = _unary("Ceil", "ceil({})")
+Floor = _unary("Floor", "floor({})")
+Sign = _unary("Sign", "sign({})")
+Sqrt = _unary("Sqrt", "sqrt({})")
+Log = _unary("Log", "log({})")
+Log10 = _unary("Log10", "log10({})")
+Exp = _unary("Exp", "exp({})")
+Sin = _unary("Sin", "sin({})")
+Cos = _unary("Cos", "cos({})")
+Tan = _unary("Tan", "tan({})")
+Asin = _unary("Asin", "asin({})")
+Acos = _unary("Acos", "acos({})")
+Atan = _unary("Atan", "atan({})")
+Degrees = _unary("Degrees", "degrees({})")
+Radians = _unary("Radians", "radians({})")
+Cot = _unary("Cot", "cot({})")            # Divide(1, Tan(e)) (:208)
+Haversin = _unary("Haversin", "haversin({})")  # Divide(Subtract(1, Cos(e)), 2) (:210)
+Atan2 = _binary("Atan2", ",")             # atan2(y, x) (:207)
+ToBoolean = _unary("ToBoolean", "toBoolean({})")  # cast to BOOLEAN (:185)
+ToString = _unary("ToString", "toString({})")     # cast to STRING (:184): not on the GPU
+# startNode(r) / endNode(r): the rel's start / end node column (:179-180)
+StartNodeFunction = _unary("StartNodeFunction", "startNode({})")
+EndNodeFunction = _unary("EndNodeFunction", "endNode({})")
+# UNWIND's Explode(list) (RelationalPlanner.scala:99-101; Explode, :101): a
+# withColumns item whose value is each element of the list in turn
+Explode = _unary("Explode", "explode({})")
+
+
+@dataclass(frozen=True)
+class E_(Expr):
+    """e() (okapi E, FlinkSQLExprMapper.scala:196): Math.E"""
+
+    def __str__(self):
+        return "e()"
+
+
+@dataclass(frozen=True)
+class Pi_(Expr):
+    """pi() (okapi Pi, FlinkSQLExprMapper.scala:197): Math.PI"""
+
+    def __str__(self):
+        return "pi()"
+
+
+E = E_()
+Pi = Pi_()
+
+
+@dataclass(frozen=True)
+class CaseExpr(Expr):
+    """CASE WHEN p1 THEN v1 … [ELSE d] END (okapi CaseExpr; FlinkSQLExprMapper
+    .scala:242-260: a chain of If(pred, value, rest), the last rest the default
+    or a NULL)."""
+    alternatives: Tuple[Tuple[Expr, Expr], ...]
+    default: object = None
+
+    def __init__(self, alternatives, default=None):
+        object.__setattr__(self, "alternatives", tuple(tuple(a) for a in alternatives))
+        object.__setattr__(self, "default", default)
+
+    def __str__(self):
+        alts = " ".join(f"WHEN {p} THEN {v}" for p, v in self.alternatives)
+        return f"CASE {alts}{'' if self.default is None else f' ELSE {self.default}'} END"
+
+
 Id = _unary("Id", "id({})")            # FlinkSQLExprMapper.scala:134: the element's id column
 Exists = _unary("Exists", "exists({})")  # exists(n.prop) → IS NOT NULL (:90)
 Size = _unary("Size", "size({})")      # charLength / cardinality (:80-85)
@@ -348,7 +423,15 @@ _BIN_OPS = {
     "Divide": OP_DIV, "Modulo": OP_MOD,
 }
 _UN_OPS = {"Not": OP_NOT, "IsNull": OP_IS_NULL, "IsNotNull": OP_IS_NOT_NULL, "ToFloat": OP_TO_FLOAT,
-           "ToInteger": OP_TO_INTEGER, "Negate": OP_NEG, "Exists": OP_IS_NOT_NULL}
+           "ToInteger": OP_TO_INTEGER, "Negate": OP_NEG, "Exists": OP_IS_NOT_NULL,
+           "Round": OP_ROUND, "Abs": OP_ABS, "Ceil": OP_CEIL, "Floor": OP_FLOOR, "Sign": OP_SIGN,
+           "Sqrt": OP_SQRT, "Log": OP_LOG, "Log10": OP_LOG10, "Exp": OP_EXP, "Sin": OP_SIN, "Cos": OP_COS,
+           "Tan": OP_TAN, "Asin": OP_ASIN, "Acos": OP_ACOS, "Atan": OP_ATAN, "Degrees": OP_DEGREES,
+           "Radians": OP_RADIANS, "ToBoolean": OP_TO_BOOLEAN}
+# math functions whose result is a FLOAT whatever the operand (Calcite's
+# DOUBLE-returning functions)
+_FLOAT_FUNCS = {"Round", "Sqrt", "Log", "Log10", "Exp", "Sin", "Cos", "Tan", "Asin", "Acos", "Atan", "Degrees",
+                "Radians", "Cot", "Haversin", "Atan2"}
 
 
 def _value_type(v):
@@ -392,6 +475,31 @@ def list_values(e, params):
         v = (params or {}).get(e.pname)
         return list(v) if isinstance(v, (list, tuple)) else None
     return None
+
+
+def explode_values(e, params):
+    """(capf element type, python values) of a literal / parameter list to
+    UNWIND, or None when `e` is not one.  INTEGER and FLOAT elements widen to
+    FLOAT together; NULL elements stay; other mixes are NotImplemented."""
+    vals = list_values(e, params)
+    if vals is None:
+        if isinstance(e, NullLit) or (isinstance(e, Param) and (params or {}).get(e.pname) is None):
+            return T_NULL, []  # UNWIND null: no rows (Spark explode of a NULL array)
+        return None
+    kinds = {_value_type(v) for v in vals if v is not None}
+    if None in kinds:
+        from ._lib import NotImplementedException
+        raise NotImplementedException(f"UNWIND of nested lists / maps: {e}")
+    if not kinds:
+        return T_NULL, vals
+    if kinds <= {T_INT, T_FLOAT}:
+        if T_FLOAT in kinds:
+            return T_FLOAT, [None if v is None else float(v) for v in vals]
+        return T_INT, vals
+    if len(kinds) == 1:
+        return kinds.pop(), vals
+    from ._lib import NotImplementedException
+    raise NotImplementedException(f"UNWIND of a list of mixed types: {e}")
 
 
 def resolve_column(expr, header, columns):
@@ -460,10 +568,12 @@ def compile_program(expr, header, columns, params=None, intern=None, coltype=Non
             return _value_type((params or {}).get(e.pname))
         if isinstance(e, (Var, ElementProperty)):  # no column: a NULL literal
             return T_NULL
-        if isinstance(e, (ToFloat,)):
+        if isinstance(e, (ToFloat,)) or type(e).__name__ in _FLOAT_FUNCS or isinstance(e, (E_, Pi_)):
             return T_FLOAT
         if isinstance(e, (ToInteger, Size, Id)):
             return T_INT
+        if isinstance(e, ToBoolean):
+            return T_BOOL
         return None
 
     def not_impl(what):
@@ -523,6 +633,43 @@ def compile_program(expr, header, columns, params=None, intern=None, coltype=Non
             emit(OP_COALESCE, len(e.exprs))
         elif cls == "Id":
             go(e.expr)  # the id column (FlinkSQLExprMapper.scala:134)
+        elif cls in ("StartNodeFunction", "EndNodeFunction"):
+            v = e.expr  # header.startNodeFor / endNodeFor of the rel var (:179-180)
+            if not isinstance(v, Var):
+                not_impl(e)
+            go(StartNode(v) if cls == "StartNodeFunction" else EndNode(v))
+        elif isinstance(e, E_):
+            emit(OP_LIT_FLOAT, 0, 2.718281828459045)
+        elif isinstance(e, Pi_):
+            emit(OP_LIT_FLOAT, 0, 3.141592653589793)
+        elif cls == "Cot":  # Divide(IntegerLit(1), Tan(e)) (:208)
+            emit(OP_LIT_INT, 1)
+            go(e.expr)
+            emit(OP_TAN)
+            emit(OP_DIV)
+        elif cls == "Haversin":  # Divide(Subtract(1, Cos(e)), 2) (:210)
+            emit(OP_LIT_INT, 1)
+            go(e.expr)
+            emit(OP_COS)
+            emit(OP_SUB)
+            emit(OP_LIT_INT, 2)
+            emit(OP_DIV)
+        elif cls == "Atan2":  # atan2(child0, child1) (:207)
+            go(e.lhs)
+            go(e.rhs)
+            emit(OP_ATAN2)
+        elif isinstance(e, CaseExpr):
+            if not e.alternatives:
+                not_impl(e)
+            # If(p1, v1, If(p2, v2, … default)): innermost first in postfix
+            if e.default is None:
+                emit(OP_LIT_NULL, T_INT)  # expressions.Null(Types.LONG) (:256)
+            else:
+                go(e.default)
+            for p, v in reversed(e.alternatives):
+                go(p)
+                go(v)
+                emit(OP_IF)
         elif isinstance(e, In):
             vals = list_values(e.rhs, params)
             if vals is None:
@@ -604,12 +751,13 @@ class Collect(Aggregator):
         return f"collect({'DISTINCT ' if self.distinct else ''}{self.expr})"
 
 
-# Aggregators of the okapi IR that the Flink backend does not map
-# (FlinkSQLExprMapper.scala:281-290 has no case for them): planning them raises
-# NotImplementedException, as the reference does.
 @dataclass(frozen=True)
 class StDev(Aggregator):
+    """stDev(e) (Expr.scala:1120-1123): Flink child0.stddevSamp
+    (FlinkSQLExprMapper.scala:223) — the sample standard deviation of the
+    non-NULL values as a FLOAT, NULL with fewer than two values."""
     expr: Expr
+    kind = AGG_STDEV
 
     def __str__(self):
         return f"stDev({self.expr})"
@@ -617,16 +765,39 @@ class StDev(Aggregator):
 
 @dataclass(frozen=True)
 class StDevP(Aggregator):
+    """stDevP(e) (Expr.scala:1125-1128): Flink child0.stddevPop (:224),
+    NULL without values."""
     expr: Expr
+    kind = AGG_STDEV_POP
 
     def __str__(self):
         return f"stDevP({self.expr})"
 
 
+def percentile_value(p, params=None):
+    """The percentile argument: a float / integer literal or parameter (the
+    Spark backend requires a literal, SparkSQLExprMapper.scala:451-462)."""
+    from ._lib import IllegalArgumentException
+    v = p
+    if isinstance(p, (FloatLit, IntegerLit)):
+        v = p.v
+    elif isinstance(p, Param):
+        v = (params or {}).get(p.pname)
+    if isinstance(v, bool) or not isinstance(v, (int, float)):
+        raise IllegalArgumentException(f"Literal as percentage for percentile, got {p}")
+    v = float(v)
+    if not 0.0 <= v <= 1.0:
+        raise IllegalArgumentException(f"percentile must be between 0.0 and 1.0, got {v}")
+    return v
+
+
 @dataclass(frozen=True)
 class PercentileCont(Aggregator):
+    """percentileCont(e, p) (Expr.scala:1096-1106), the Spark backend's UDAF
+    semantics (PercentileUdafs.scala:83-96): linear interpolation, a FLOAT."""
     expr: Expr
-    percentile: float
+    percentile: object
+    kind = AGG_PERCENTILE_CONT
 
     def __str__(self):
         return f"percentileCont({self.expr}, {self.percentile})"
@@ -634,11 +805,54 @@ class PercentileCont(Aggregator):
 
 @dataclass(frozen=True)
 class PercentileDisc(Aggregator):
+    """percentileDisc(e, p) (Expr.scala:1108-1118; PercentileUdafs.scala:
+    59-81): the value at rank round(n·p), in the input's type."""
     expr: Expr
-    percentile: float
+    percentile: object
+    kind = AGG_PERCENTILE_DISC
 
     def __str__(self):
         return f"percentileDisc({self.expr}, {self.percentile})"
+
+
+def aggregators_in(e):
+    """Aggregator sub-expressions of a projection item, outermost first
+    (RETURN round(stDev(x) * 1000) / 1000.0 aggregates stDev(x), then
+    projects the rest over it)."""
+    if isinstance(e, Aggregator):
+        return [e]
+    out = []
+    for name in ("lhs", "rhs", "expr"):
+        c = getattr(e, name, None)
+        if isinstance(c, Expr):
+            out += aggregators_in(c)
+    for c in getattr(e, "exprs", ()) or ():
+        if isinstance(c, Expr):
+            out += aggregators_in(c)
+    if isinstance(e, CaseExpr):
+        for p, v in e.alternatives:
+            out += aggregators_in(p) + aggregators_in(v)
+        if isinstance(e.default, Expr):
+            out += aggregators_in(e.default)
+    return out
+
+
+def replace_exprs(e, m):
+    """`e` with every sub-expression found in the dict m replaced."""
+    if e in m:
+        return m[e]
+    import dataclasses
+    if isinstance(e, CaseExpr):
+        return CaseExpr([(replace_exprs(p, m), replace_exprs(v, m)) for p, v in e.alternatives],
+                        None if e.default is None else replace_exprs(e.default, m))
+    if isinstance(e, (Ands, Ors, Coalesce)):
+        return type(e)(*[replace_exprs(x, m) for x in e.exprs])
+    if dataclasses.is_dataclass(e) and not isinstance(e, (Var, ElementProperty)):
+        ch = {f.name: replace_exprs(getattr(e, f.name), m) for f in dataclasses.fields(e)
+              if isinstance(getattr(e, f.name), Expr)}
+        if ch:
+            return dataclasses.replace(e, **ch)
+    return e
 
 
 # ----------------------------------------------------------- hash caching

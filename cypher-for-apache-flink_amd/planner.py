@@ -22,8 +22,9 @@ from dataclasses import dataclass, field
 from itertools import combinations
 from typing import List, Optional, Sequence, Tuple
 
-from .expr import (Aggregator, Ands, BoolLit, ElementProperty, EndNode, Equals, ExistsPattern, Expr,
-                   HasLabel, HasType, IntegerLit, IsNotNull, Not, NullLit, StartNode, TrueLit, Var)
+from .expr import (Aggregator, Ands, BoolLit, ElementProperty, EndNode, Equals, ExistsPattern, Explode, Expr,
+                   HasLabel, HasType, IntegerLit, IsNotNull, Not, NullLit, StartNode, TrueLit, Var,
+                   aggregators_in, replace_exprs)
 from .header import RecordHeader, owner_of
 
 
@@ -71,8 +72,16 @@ class Stage:
 
 
 @dataclass
+class Unwind:
+    """UNWIND list AS alias (logical Unwind, RelationalPlanner.scala:99-101:
+    `in.add(Explode(list) as item)`); a clause of Query.matches, in order."""
+    list: Expr
+    alias: str
+
+
+@dataclass
 class Query:
-    matches: List[Match]
+    matches: List[object]  # Match / Unwind clauses in query order
     stages: List[Stage]
 
 
@@ -542,7 +551,42 @@ def plan_optional(graph, m: Match, lhs: Planned, params=None) -> Planned:
     return Planned(joined, head)
 
 
+def plan_unwind(op: Planned, u: Unwind, params=None) -> Planned:
+    """Unwind → `add(Explode(list) as item)` (RelationalPlanner.scala:99-101):
+    withColumns with the Explode item; the alias var reads the new column."""
+    v = Var(u.alias)
+    col = op.header.get(v) or "__" + u.alias
+    tab = op.table.withColumns((Explode(u.list), col), header=op.header, params=params or {})
+    return Planned(tab, op.header.with_expr(v, col))
+
+
+def _split_aggregates(st: Stage) -> Stage:
+    """Items that compute over aggregates (RETURN round(stDev(x) * 1000) /
+    1000.0): each aggregator becomes its own item, aggregated first, and the
+    item is projected over the aggregate columns by a following stage (the
+    okapi IR plans the Aggregate below a Project of the outer expression)."""
+    inner = [it for it in st.items if not aggregators_in(it[1]) or isinstance(it[1], Aggregator)]
+    nested = [it for it in st.items if it not in inner]
+    if not nested:
+        return None
+    hidden, mapping = [], {}
+    for _, e in nested:
+        for a in aggregators_in(e):
+            if a not in mapping:
+                name = f"__agg{len(mapping)}"
+                mapping[a] = Var(name)
+                hidden.append((name, a))
+    first = Stage([(a, e) for a, e in st.items if (a, e) in inner] + hidden)
+    outer = [(a, Var(a)) if (a, e) in inner else (a, replace_exprs(e, mapping)) for a, e in st.items]
+    second = Stage(outer, distinct=st.distinct, where=st.where, order_by=st.order_by, skip=st.skip,
+                   limit=st.limit)
+    return first, second
+
+
 def plan_stage(op: Planned, st: Stage, params=None, graph=None) -> Planned:
+    split = _split_aggregates(st)
+    if split is not None:
+        return plan_stage(plan_stage(op, split[0], params, graph), split[1], params, graph)
     aggs = [(a, e) for a, e in st.items if isinstance(e, Aggregator)]
     projs = [(a, e) for a, e in st.items if not isinstance(e, Aggregator)]
     for _, e in projs:
@@ -622,6 +666,11 @@ def plan_query(graph, q: Query, params=None) -> Planned:
     if not q.matches:  # a leading RETURN / WITH: one row of the unit table (Start)
         op = Planned(graph.session.unit(), RecordHeader({}))
     for m in q.matches:
+        if isinstance(m, Unwind):
+            if op is None:  # a leading UNWIND: over the unit table (Start)
+                op = Planned(graph.session.unit(), RecordHeader({}))
+            op = plan_unwind(op, m, params)
+            continue
         op = plan_optional(graph, m, op, params) if m.optional else plan_match(graph, m, op, params)
     for st in q.stages:
         op = plan_stage(op, st, params, graph)

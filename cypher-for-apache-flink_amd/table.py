@@ -18,7 +18,7 @@ import numpy as np
 
 from . import _lib
 from .expr import (AGG_COUNT_STAR, CAPF_TO_CT, T_BOOL, T_FLOAT, T_INT, T_LIST, T_NULL, T_STRING, Aggregator,
-                   compile_program)
+                   Explode, Var, compile_program, explode_values, percentile_value)
 
 JOIN_TYPES = {"inner": 0, "left_outer": 1, "right_outer": 2, "full_outer": 3, "cross": 4}
 
@@ -413,7 +413,7 @@ class GpuTable:
                 if c in self.physicalColumns and c not in cols:
                     cols.append(c)
         names = list(aggregations)
-        kinds, progs, dist = [], [], []
+        kinds, progs, dist, pars = [], [], [], []
         for name in names:
             agg = aggregations[name]
             if not isinstance(agg, Aggregator):
@@ -423,13 +423,50 @@ class GpuTable:
                     f"No support for converting Cypher expression {agg} to a GPU expression")
             kinds.append(agg.kind)
             dist.append(1 if getattr(agg, "distinct", False) else 0)
+            pars.append(percentile_value(agg.percentile, params) if hasattr(agg, "percentile") else 0.0)
             progs.append(None if agg.kind == AGG_COUNT_STAR else _program(agg.expr, header, self, params))
         arr, keep = _lib.expr_array(progs)
         k = len(names)
-        return self._new("capf_table_group", self._h, len(cols), _lib.strs(cols), k,
-                         (c_int32 * max(k, 1))(*kinds), arr, (c_int32 * max(k, 1))(*dist), _lib.strs(names))
+        return self._new("capf_table_group_ex", self._h, len(cols), _lib.strs(cols), k,
+                         (c_int32 * max(k, 1))(*kinds), arr, (c_int32 * max(k, 1))(*dist),
+                         (c_double * max(k, 1))(*pars), _lib.strs(names))
+
+    def _explode(self, e, col, header, params):
+        """UNWIND: withColumns(Explode(list) AS col) — a literal / parameter
+        list (capf_table_explode_values) or a LIST column (capf_table_explode_list)."""
+        ev = explode_values(e.expr, params)
+        if ev is not None:
+            t, vals = ev
+            n = len(vals)
+            valid = None
+            if any(v is None for v in vals):
+                valid = np.array([v is not None for v in vals], dtype=np.uint8)
+            if t == T_NULL:
+                data = None
+            elif t == T_STRING:
+                data = np.array([self.session.intern(v) if v is not None else 0 for v in vals], dtype=np.int64)
+            else:
+                data = np.array([v if v is not None else 0 for v in vals], dtype=_NP_DTYPE[t])
+            return self._new("capf_table_explode_values", self._h, col.encode(), int(t), n,
+                             data.ctypes.data if data is not None and n else None,
+                             valid.ctypes.data if valid is not None and n else None)
+        src = header.get(e.expr) if header is not None else None
+        if src is None or src not in self.physicalColumns:
+            if isinstance(e.expr, Var) or type(e.expr).__name__ == "NullLit":  # UNWIND null: no rows
+                return self._new("capf_table_explode_values", self._h, col.encode(), int(T_NULL), 0, None, None)
+            raise _lib.NotImplementedException(f"UNWIND of {e.expr}")
+        return self._new("capf_table_explode_list", self._h, src.encode(), col.encode())
 
     def withColumns(self, *columns, header=None, params=None):
+        if any(isinstance(e, Explode) for e, _ in columns):
+            t = self
+            plain = [(e, c) for e, c in columns if not isinstance(e, Explode)]
+            if plain:
+                t = t.withColumns(*plain, header=header, params=params)
+            for e, c in columns:
+                if isinstance(e, Explode):
+                    t = t._explode(e, c, header, params)
+            return t
         progs = [_program(e, header, self, params) for e, _ in columns]
         arr, keep = _lib.expr_array(progs)
         return self._new("capf_table_with_columns", self._h, len(columns), arr,

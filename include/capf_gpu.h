@@ -97,7 +97,24 @@ enum {
    * agg_distinct drops duplicate values.  Flink's COLLECT is a MULTISET: the
    * element order is not part of the result (here: ascending values, string
    * elements in dictionary-code order). */
-  CAPF_AGG_COLLECT = 6
+  CAPF_AGG_COLLECT = 6,
+  /* StDev / StDevP (Expr.scala:1120-1128; Flink child0.stddevSamp / stddevPop,
+   * FlinkSQLExprMapper.scala:223-224): the sample / population standard
+   * deviation of the group's non-NULL numeric values as a FLOAT; NULL for a
+   * group without values (AggregationTests.scala:610-617, 637-644) and, for
+   * the sample form, with one value (Calcite's STDDEV_SAMP divides by
+   * count - 1 and yields NULL for count = 1).  Two-pass, double-double sums. */
+  CAPF_AGG_STDEV = 7,
+  CAPF_AGG_STDEV_POP = 8,
+  /* PercentileCont / PercentileDisc (Expr.scala:1096-1118) with the fraction
+   * p = agg_params[i] in [0, 1] of capf_table_group_ex.  The semantics of the
+   * Spark backend of the same SPI (morpheus-spark-cypher/.../impl/expressions/
+   * PercentileUdafs.scala:59-96; Flink has no mapping): over the sorted
+   * non-NULL values v[0..n), disc = v[max(round(n·p), 1) − 1] in the input's
+   * type; cont = linear interpolation at position 1 + (n − 1)·p, a FLOAT.
+   * NULL for a group without values.                                        */
+  CAPF_AGG_PERCENTILE_CONT = 9,
+  CAPF_AGG_PERCENTILE_DISC = 10
 };
 
 /*
@@ -139,9 +156,39 @@ enum {
                               charLength, FlinkSQLExprMapper.scala:80-85)   */
   CAPF_OP_LIST_SIZE = 61,  /* Size(list): push the element count of LIST
                               column names[iarg] (Flink cardinality, :80-85) */
-  CAPF_OP_IF = 62          /* pop value, cond, else: push cond TRUE ? value :
+  CAPF_OP_IF = 62,         /* pop value, cond, else: push cond TRUE ? value :
                               else (type(r) over the HasType columns,
-                              FlinkSQLExprMapper.scala:152-160)              */
+                              FlinkSQLExprMapper.scala:152-160; CaseExpr
+                              as a chain of Ifs, :242-260); numeric branches
+                              of different types widen to FLOAT             */
+  /* Mathematical functions (FlinkSQLExprMapper.scala:199-221).  Unary: pop x,
+   * push f(x); NULL in, NULL out.  ROUND rounds half away from zero and
+   * yields a FLOAT (the Spark mapping round(x).cast(Double),
+   * SparkSQLExprMapper.scala:286; Flink's is `???`); CEIL / FLOOR yield
+   * FLOAT for FLOAT input, INTEGER input unchanged; SIGN an INTEGER; ABS
+   * keeps the type; the rest FLOAT (Java Math.* over doubles).               */
+  CAPF_OP_ROUND = 70,
+  CAPF_OP_ABS = 71,
+  CAPF_OP_CEIL = 72,
+  CAPF_OP_FLOOR = 73,
+  CAPF_OP_SIGN = 74,
+  CAPF_OP_SQRT = 75,
+  CAPF_OP_LOG = 76,
+  CAPF_OP_LOG10 = 77,
+  CAPF_OP_EXP = 78,
+  CAPF_OP_SIN = 79,
+  CAPF_OP_COS = 80,
+  CAPF_OP_TAN = 81,
+  CAPF_OP_ASIN = 82,
+  CAPF_OP_ACOS = 83,
+  CAPF_OP_ATAN = 84,
+  CAPF_OP_DEGREES = 85,
+  CAPF_OP_RADIANS = 86,
+  CAPF_OP_ATAN2 = 87,      /* binary: pop x, y; push atan2(y, x)             */
+  /* ToBoolean (:185, Flink cast to BOOLEAN): BOOLEAN unchanged, STRING
+   * 'true' / 'false' (any case, trimmed) → TRUE / FALSE, any other string
+   * → NULL.  Uses the session's device table of string → boolean codes.     */
+  CAPF_OP_TO_BOOLEAN = 88
 };
 
 typedef struct capf_expr {
@@ -296,9 +343,33 @@ capf_status capf_table_group(capf_table *t, int32_t n_by, const char *const *by_
                              int32_t n_aggs, const int32_t *agg_kinds,
                              const capf_expr *agg_args, const int32_t *agg_distinct,
                              const char *const *agg_names, capf_table **out);
+/* group with per-aggregator parameters: agg_params[i] is the percentile
+ * fraction of CAPF_AGG_PERCENTILE_CONT / _DISC (ignored for the others; may
+ * be NULL when no percentile is requested).  capf_table_group is this call
+ * with agg_params = NULL.                                                  */
+capf_status capf_table_group_ex(capf_table *t, int32_t n_by, const char *const *by_cols,
+                                int32_t n_aggs, const int32_t *agg_kinds,
+                                const capf_expr *agg_args, const int32_t *agg_distinct,
+                                const double *agg_params, const char *const *agg_names,
+                                capf_table **out);
 /* withColumns((expr, col)*)(header, params) (Table.scala:170) */
 capf_status capf_table_with_columns(capf_table *t, int32_t n, const capf_expr *exprs,
                                     const char *const *names, capf_table **out);
+/* UNWIND: withColumns(Explode(list) AS item) (RelationalPlanner.scala:99-101,
+ * Explode = FlinkSQLExprMapper.scala:101; row semantics of Spark's explode,
+ * SparkSQLExprMapper.scala:146-149): every row of t is repeated once per
+ * element of the list, the new column `name` holding the element (rows in
+ * input order, elements in list order; an empty list drops the row).
+ * capf_table_explode_values: the same literal / parameter list for every row:
+ *   n elements of capf type `type` (INT64 / FLOAT64 / BOOL / STRING codes /
+ *   NULL), values n × (8 or 1) bytes (NULL for a NULL-typed list), valid
+ *   NULL (no NULL elements) or n bytes.
+ * capf_table_explode_list: the elements of LIST column list_col (a NULL list
+ *   drops the row, like an empty one).                                      */
+capf_status capf_table_explode_values(capf_table *t, const char *name, int32_t type, int64_t n,
+                                      const void *values, const uint8_t *valid, capf_table **out);
+capf_status capf_table_explode_list(capf_table *t, const char *list_col, const char *name,
+                                    capf_table **out);
 /* show(n) (Table.scala:177): prints to stdout */
 capf_status capf_table_show(capf_table *t, int32_t rows);
 

@@ -467,6 +467,35 @@ JNI(jlong, tableGroup)(JNIEnv *env, jobject, jlong t, jobjectArray by, jintArray
              ? 0
              : H(out);
 }
+// group with the percentile fractions (capf_table_group_ex)
+JNI(jlong, tableGroupEx)(JNIEnv *env, jobject, jlong t, jobjectArray by, jintArray kinds,
+                         jobjectArray args, jbooleanArray distinct, jdoubleArray params, jobjectArray names) {
+  JStrs b(env, by), nm(env, names);
+  std::vector<int32_t> k = ints(env, kinds), d = bools(env, distinct);
+  std::vector<double> p = doubles(env, params);
+  Programs a(env, args);
+  capf_table *out = nullptr;
+  return fail(env, capf_table_group_ex(T(t), b.n(), b.data(), (int32_t)k.size(), k.data(), a.data(),
+                                       d.data(), p.data(), nm.data(), &out))
+             ? 0
+             : H(out);
+}
+// UNWIND (RelationalPlanner.scala:99-101): a literal / parameter list given as
+// direct buffers (n elements, 8 or 1 bytes each; valid = n bytes or null)
+JNI(jlong, tableExplodeValues)(JNIEnv *env, jobject, jlong t, jstring name, jint type, jlong n,
+                               jobject values, jobject valid) {
+  JStr nm(env, name);
+  capf_table *out = nullptr;
+  return fail(env, capf_table_explode_values(T(t), nm.p, type, n, values ? direct(env, values) : nullptr,
+                                             valid ? (const uint8_t *)direct(env, valid) : nullptr, &out))
+             ? 0
+             : H(out);
+}
+JNI(jlong, tableExplodeList)(JNIEnv *env, jobject, jlong t, jstring list_col, jstring name) {
+  JStr l(env, list_col), nm(env, name);
+  capf_table *out = nullptr;
+  return fail(env, capf_table_explode_list(T(t), l.p, nm.p, &out)) ? 0 : H(out);
+}
 JNI(jlong, tableWithColumns)(JNIEnv *env, jobject, jlong t, jobjectArray exprs,
                              jobjectArray names) {  // Table.scala:170
   Programs e(env, exprs);

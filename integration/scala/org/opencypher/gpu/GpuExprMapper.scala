@@ -15,7 +15,7 @@ import scala.collection.mutable
 
 import org.opencypher.okapi.api.types._
 import org.opencypher.okapi.api.value.CypherValue._
-import org.opencypher.okapi.impl.exception.NotImplementedException
+import org.opencypher.okapi.impl.exception.{IllegalArgumentException, NotImplementedException}
 import org.opencypher.okapi.ir.api.expr._
 import org.opencypher.okapi.relational.impl.table.RecordHeader
 
@@ -31,6 +31,14 @@ object GpuExprMapper {
   private final val Neg = 35   // CAPF_OP_MOD (34) has no okapi Expr: okapi-ir has no Modulo
   private final val ToFloat_ = 40; private final val ToInteger_ = 41; private final val Coalesce_ = 50
   private final val StrLen = 60; private final val ListSize = 61; private final val If_ = 62
+  // math functions (FlinkSQLExprMapper.scala:199-221) and casts (:185)
+  private final val Round_ = 70; private final val Abs_ = 71; private final val Ceil_ = 72
+  private final val Floor_ = 73; private final val Sign_ = 74; private final val Sqrt_ = 75
+  private final val Log_ = 76; private final val Log10_ = 77; private final val Exp_ = 78
+  private final val Sin_ = 79; private final val Cos_ = 80; private final val Tan_ = 81
+  private final val Asin_ = 82; private final val Acos_ = 83; private final val Atan_ = 84
+  private final val Degrees_ = 85; private final val Radians_ = 86; private final val Atan2_ = 87
+  private final val ToBoolean_ = 88
 
   def program(expr: Expr, header: RecordHeader, table: GpuTable, parameters: CypherMap): Program = {
     val ops = mutable.ArrayBuffer.empty[Int]
@@ -154,6 +162,44 @@ object GpuExprMapper {
         header.typesFor(v).toSeq.sortBy(_.relType.name).foreach { t =>
           physical(t).foreach { c => col(c); emit(LitString, session.intern(t.relType.name)); emit(If_) }
         }
+      case StartNodeFunction(x) => x.owner match {                       // :179
+        case Some(v) => go(header.startNodeFor(v))
+        case None => throw NotImplementedException(s"GPU startNode of $x")
+      }
+      case EndNodeFunction(x) => x.owner match {                         // :180
+        case Some(v) => go(header.endNodeFor(v))
+        case None => throw NotImplementedException(s"GPU endNode of $x")
+      }
+      case ToBoolean(x) => go(x); emit(ToBoolean_)                        // :185
+      case E => emit(LitFloat, 0L, math.E)                                // :196
+      case Pi => emit(LitFloat, 0L, math.Pi)                              // :197
+      case Sqrt(x) => go(x); emit(Sqrt_)                                  // :199-221
+      case Log(x) => go(x); emit(Log_)
+      case Log10(x) => go(x); emit(Log10_)
+      case Exp(x) => go(x); emit(Exp_)
+      case Abs(x) => go(x); emit(Abs_)
+      case Ceil(x) => go(x); emit(Ceil_)
+      case Floor(x) => go(x); emit(Floor_)
+      case Round(x) => go(x); emit(Round_)    // Spark round(x).cast(Double), SparkSQLExprMapper.scala:286
+      case Sign(x) => go(x); emit(Sign_)
+      case Acos(x) => go(x); emit(Acos_)
+      case Asin(x) => go(x); emit(Asin_)
+      case Atan(x) => go(x); emit(Atan_)
+      case Atan2(y, x) => go(y); go(x); emit(Atan2_)
+      case Cos(x) => go(x); emit(Cos_)
+      case Cot(x) => emit(LitInt, 1L); go(x); emit(Tan_); emit(Div)       // Divide(1, Tan(e))
+      case Degrees(x) => go(x); emit(Degrees_)
+      case Haversin(x) =>                                                 // Divide(Subtract(1, Cos(e)), 2)
+        emit(LitInt, 1L); go(x); emit(Cos_); emit(Sub); emit(LitInt, 2L); emit(Div)
+      case Radians(x) => go(x); emit(Radians_)
+      case Sin(x) => go(x); emit(Sin_)
+      case Tan(x) => go(x); emit(Tan_)
+      case c: CaseExpr if c.alternatives.nonEmpty =>                      // :242-260, Ifs innermost first
+        c.default match {
+          case Some(d) => go(d)
+          case None => emit(LitNull, Native.TypeInt64)                    // expressions.Null(Types.LONG)
+        }
+        c.alternatives.reverse.foreach { case (p, v) => go(p); go(v); emit(If_) }
       case other =>
         throw NotImplementedException(s"No support for converting Cypher expression $other to a GPU expression")
     }
@@ -162,17 +208,41 @@ object GpuExprMapper {
     new Program(ops.toArray, iargs.toArray, fargs.toArray, names.keys.toArray)
   }
 
-  /** (CAPF_AGG_* kind, argument program, distinct) — the aggregators of
-    * FlinkSQLExprMapper.scala:281-287 (Expr.scala:1031-1140). */
-  def aggregator(agg: Aggregator, header: RecordHeader, table: GpuTable, parameters: CypherMap): (Int, Program, Boolean) =
+  /** The percentile fraction: a FLOAT / INTEGER literal or parameter in [0, 1]
+    * (the Spark backend takes a literal, SparkSQLExprMapper.scala:451-462). */
+  private def percentile(p: Expr, parameters: CypherMap): Double = {
+    val v = p match {
+      case FloatLit(d) => d
+      case IntegerLit(i) => i.toDouble
+      case Param(n) => parameters(n) match {
+        case CypherFloat(d) => d
+        case CypherInteger(i) => i.toDouble
+        case other => throw IllegalArgumentException("Literal as percentage for percentile", other)
+      }
+      case other => throw IllegalArgumentException("Literal as percentage for percentile", other)
+    }
+    if (v < 0.0 || v > 1.0) throw IllegalArgumentException("a percentile between 0.0 and 1.0", v)
+    v
+  }
+
+  /** (CAPF_AGG_* kind, argument program, distinct, parameter) — the aggregators of
+    * FlinkSQLExprMapper.scala:223-224, 281-287 (Expr.scala:1031-1140). */
+  def aggregator(agg: Aggregator, header: RecordHeader, table: GpuTable,
+                 parameters: CypherMap): (Int, Program, Boolean, Double) = {
+    def arg(e: Expr) = program(e, header, table, parameters)
     agg match {
-      case CountStar => (Native.AggCountStar, Program.empty, false)        // case object, Expr.scala:1071
-      case Count(e, distinct) => (Native.AggCount, program(e, header, table, parameters), distinct)
-      case Sum(e) => (Native.AggSum, program(e, header, table, parameters), false)
-      case Min(e) => (Native.AggMin, program(e, header, table, parameters), false)
-      case Max(e) => (Native.AggMax, program(e, header, table, parameters), false)
-      case Avg(e) => (Native.AggAvg, program(e, header, table, parameters), false)
-      case Collect(e, distinct) => (Native.AggCollect, program(e, header, table, parameters), distinct)
+      case CountStar => (Native.AggCountStar, Program.empty, false, 0.0)   // case object, Expr.scala:1071
+      case Count(e, distinct) => (Native.AggCount, arg(e), distinct, 0.0)
+      case Sum(e) => (Native.AggSum, arg(e), false, 0.0)
+      case Min(e) => (Native.AggMin, arg(e), false, 0.0)
+      case Max(e) => (Native.AggMax, arg(e), false, 0.0)
+      case Avg(e) => (Native.AggAvg, arg(e), false, 0.0)
+      case Collect(e, distinct) => (Native.AggCollect, arg(e), distinct, 0.0)
+      case StDev(e) => (Native.AggStDev, arg(e), false, 0.0)
+      case StDevP(e) => (Native.AggStDevPop, arg(e), false, 0.0)
+      case PercentileCont(e, p) => (Native.AggPercentileCont, arg(e), false, percentile(p, parameters))
+      case PercentileDisc(e, p) => (Native.AggPercentileDisc, arg(e), false, percentile(p, parameters))
       case other => throw NotImplementedException(s"GPU aggregator $other")
     }
+  }
 }

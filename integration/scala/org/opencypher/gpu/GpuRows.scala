@@ -38,6 +38,37 @@ object GpuRows {
     Iterator.range(0, n.toInt).map(i => (c: String) => data(c)(i))
   }
 
+  /** UNWIND of a literal / parameter list (capf_table_explode_values): the
+    * elements as one typed buffer — INTEGER and FLOAT widen to FLOAT, NULL
+    * elements kept — returns the new handle. */
+  def explodeValues(t: GpuTable, col: String, vs: Seq[CypherValue]): Long = {
+    val present = vs.filter(_ != CypherNull)
+    val ty =
+      if (present.isEmpty) Native.TypeNull
+      else if (present.forall(v => v.isInstanceOf[CypherInteger])) Native.TypeInt64
+      else if (present.forall(v => v.isInstanceOf[CypherInteger] || v.isInstanceOf[CypherFloat])) Native.TypeFloat64
+      else if (present.forall(_.isInstanceOf[CypherBoolean])) Native.TypeBool
+      else if (present.forall(_.isInstanceOf[CypherString])) Native.TypeString
+      else throw new UnsupportedOperationException(s"UNWIND of a list of mixed types: $vs")
+    val n = vs.size
+    val width = if (ty == Native.TypeBool) 1 else 8
+    val values = ByteBuffer.allocateDirect(math.max(1, n * width)).order(ByteOrder.nativeOrder())
+    val valid = ByteBuffer.allocateDirect(math.max(1, n))
+    vs.zipWithIndex.foreach { case (v, i) =>
+      valid.put(i, if (v == CypherNull) 0.toByte else 1.toByte)
+      v match {
+        case CypherInteger(x) if ty == Native.TypeFloat64 => values.putDouble(8 * i, x.toDouble)
+        case CypherInteger(x) => values.putLong(8 * i, x)
+        case CypherFloat(x) => values.putDouble(8 * i, x)
+        case CypherBoolean(b) => values.put(i, if (b) 1.toByte else 0.toByte)
+        case CypherString(s) => values.putLong(8 * i, Native.guard(Native.stringIntern(t.session.handle, s)))
+        case _ =>
+      }
+    }
+    Native.guard(Native.tableExplodeValues(t.handle, col, ty, n.toLong,
+      if (ty == Native.TypeNull) null else values, valid))
+  }
+
   /** A LIST column (collect): offsets + elements (capf_table_download_list). */
   private def lists(t: GpuTable, c: String, n: Long): Int => CypherValue = {
     val nv = Array(0L)

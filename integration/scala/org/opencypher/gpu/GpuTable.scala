@@ -10,8 +10,8 @@ package org.opencypher.gpu
 import java.lang.ref.Cleaner
 
 import org.opencypher.okapi.api.types.CypherType
-import org.opencypher.okapi.api.value.CypherValue.{CypherMap, CypherValue}
-import org.opencypher.okapi.impl.exception.IllegalArgumentException
+import org.opencypher.okapi.api.value.CypherValue._
+import org.opencypher.okapi.impl.exception.{IllegalArgumentException, NotImplementedException}
 import org.opencypher.okapi.ir.api.expr._
 import org.opencypher.okapi.relational.api.table.Table
 import org.opencypher.okapi.relational.impl.planning._
@@ -94,14 +94,47 @@ final class GpuTable private (private[gpu] val handle: Long)(implicit val sessio
     val byCols = by.toSeq.flatMap(v => header.ownedBy(v).toSeq.map(header.column)).distinct
     val aggs = aggregations.toSeq
     val lowered = aggs.map { case (_, agg) => GpuExprMapper.aggregator(agg, header, this, parameters) }
-    wrap(Native.tableGroup(handle, byCols.toArray, lowered.map(_._1).toArray, lowered.map(_._2).toArray,
-      lowered.map(_._3).toArray, aggs.map(_._1).toArray))
+    wrap(Native.tableGroupEx(handle, byCols.toArray, lowered.map(_._1).toArray, lowered.map(_._2).toArray,
+      lowered.map(_._3).toArray, lowered.map(_._4).toArray, aggs.map(_._1).toArray))
   }
 
-  override def withColumns(columns: (Expr, String)*)(implicit header: RecordHeader, parameters: CypherMap): GpuTable = // :170
-    wrap(Native.tableWithColumns(handle,
-      columns.map { case (e, _) => GpuExprMapper.program(e, header, this, parameters) }.toArray,
-      columns.map(_._2).toArray))
+  override def withColumns(columns: (Expr, String)*)(implicit header: RecordHeader, parameters: CypherMap): GpuTable = { // :170
+    val (explodes, plain) = columns.partition { case (e, _) => e.isInstanceOf[Explode] }
+    val base =
+      if (plain.isEmpty) this
+      else wrap(Native.tableWithColumns(handle,
+        plain.map { case (e, _) => GpuExprMapper.program(e, header, this, parameters) }.toArray,
+        plain.map(_._2).toArray))
+    explodes.foldLeft(base) { case (t, (Explode(list), col)) => t.explode(list, col, header, parameters) }
+  }
+
+  /** UNWIND list AS item = add(Explode(list) as item) (RelationalPlanner.scala:99-101). */
+  private def explode(list: Expr, col: String, header: RecordHeader, parameters: CypherMap): GpuTable = {
+    val literal: Option[Seq[CypherValue]] = list match {
+      case ListLit(items) => Some(items.map {
+        case NullLit(_) => CypherNull
+        case IntegerLit(v) => CypherInteger(v)
+        case FloatLit(v) => CypherFloat(v)
+        case StringLit(v) => CypherString(v)
+        case TrueLit => CypherBoolean(true)
+        case FalseLit => CypherBoolean(false)
+        case Param(p) => parameters(p)
+        case other => throw NotImplementedException(s"GPU UNWIND element $other")
+      })
+      case Param(p) => parameters(p) match {
+        case CypherList(vs) => Some(vs)
+        case CypherNull => Some(Seq.empty)
+        case other => throw NotImplementedException(s"GPU UNWIND of $other")
+      }
+      case NullLit(_) => Some(Seq.empty)
+      case _ => None
+    }
+    literal match {
+      case Some(vs) => wrap(GpuRows.explodeValues(this, col, vs))
+      case None if header.contains(list) => wrap(Native.tableExplodeList(handle, header.column(list), col))
+      case None => throw NotImplementedException(s"GPU UNWIND of $list")
+    }
+  }
 
   override def show(rows: Int): Unit = Native.guard(Native.tableShow(handle, rows))        // :177
 

@@ -53,6 +53,10 @@ object Native {
   final val AggMax = 4
   final val AggAvg = 5
   final val AggCollect = 6
+  final val AggStDev = 7            // stddevSamp (FlinkSQLExprMapper.scala:223)
+  final val AggStDevPop = 8         // stddevPop (:224)
+  final val AggPercentileCont = 9   // PercentileUdafs.scala:83-96 (Spark backend semantics)
+  final val AggPercentileDisc = 10  // PercentileUdafs.scala:59-81
 
   /** Runs a native call, rethrowing its failure as the okapi exception of that kind
     * (okapi-api/.../impl/exception/InternalException.scala:36-65). */
@@ -126,7 +130,13 @@ object Native {
   @native def tableDistinctCols(table: Long, cols: Array[String]): Long
   @native def tableGroup(table: Long, by: Array[String], kinds: Array[Int], args: Array[Program],
                          distinct: Array[Boolean], names: Array[String]): Long
+  @native def tableGroupEx(table: Long, by: Array[String], kinds: Array[Int], args: Array[Program],
+                           distinct: Array[Boolean], params: Array[Double], names: Array[String]): Long
   @native def tableWithColumns(table: Long, exprs: Array[Program], names: Array[String]): Long
+  // UNWIND: withColumns(Explode(list) as item) (RelationalPlanner.scala:99-101)
+  @native def tableExplodeValues(table: Long, name: String, elemType: Int, n: Long, values: java.nio.ByteBuffer,
+                                 valid: java.nio.ByteBuffer): Long
+  @native def tableExplodeList(table: Long, listCol: String, name: String): Long
   @native def tableShow(table: Long, rows: Int): Unit
 
   // graph inputs (EdgeListDataSource.scala:56-92; synthetic R-MAT / node ranges)

@@ -57,6 +57,8 @@ def lib():
         l.pipeline_build.restype = P
         l.pipeline_probe.argtypes = [P, i64, i64, i32]
         l.pipeline_probe.restype = u64
+        l.onehop_label_count.argtypes = [P, i64, P, i64, P, P, i64, i32]
+        l.onehop_label_count.restype = u64
         l.pipeline_free.argtypes = [P]
         l.pipeline_free.restype = None
         l.rmat_stream_counts.argtypes = [i32, u64, u32, u32, u32, i64, i32, P]
@@ -139,6 +141,18 @@ def stream_counts(scale, edge_factor=16, threads=8):
                              res.ctypes.data)
     keys = ("two_hop", "self_loops", "one_hop_person", "max_in", "max_out")
     return {k: int(v) for k, v in zip(keys, res)}
+
+
+def onehop_label_count(person_ids, node_ids, src, dst, threads=8):
+    """Config 2's Flink plan shape on the host (oracle/rmat.c): hash-join
+    builds on the Person scan and the all-node scan, rels streamed through both
+    probes on `threads` workers."""
+    p = np.ascontiguousarray(person_ids, dtype=np.int64)
+    a = np.ascontiguousarray(node_ids, dtype=np.int64)
+    s = np.ascontiguousarray(src, dtype=np.int64)
+    d = np.ascontiguousarray(dst, dtype=np.int64)
+    return int(lib().onehop_label_count(p.ctypes.data, len(p), a.ctypes.data, len(a), s.ctypes.data,
+                                        d.ctypes.data, len(s), threads))
 
 
 def count_2hop(src, dst, n):

@@ -310,6 +310,85 @@ void pipeline_free(void *handle) {
   free(p);
 }
 
+/* ------------------------------- config 2: (a:Person)-->(b) count, Flink shape
+ * S_a (Person scan) ⋈[a = start(r)] R ⋈[end(r) = b] S_b (all nodes): the two
+ * hash-join builds on the node scans (open-addressing sets, as above), then the
+ * rels stream through both probes on `threads` workers (contiguous rel ranges)
+ * and the matches are counted — RelationalPlanner.scala:130-165 with the label
+ * pushed into the S_a scan (ScanGraph.scala:59-105). */
+typedef struct {
+  int64_t *keys;
+  uint64_t mask;
+} IdSet;
+
+static void idset_build(IdSet *h, const int64_t *ids, int64_t n) {
+  uint64_t cap = 1024;
+  while (cap < 2 * (uint64_t)n) cap <<= 1;
+  h->mask = cap - 1;
+  h->keys = (int64_t *)malloc(cap * 8);
+  for (uint64_t i = 0; i < cap; ++i) h->keys[i] = INT64_MIN;
+  for (int64_t i = 0; i < n; ++i) {
+    uint64_t s = hmix(ids[i]) & h->mask;
+    while (h->keys[s] != INT64_MIN && h->keys[s] != ids[i]) s = (s + 1) & h->mask;
+    h->keys[s] = ids[i];
+  }
+}
+
+static int idset_has(const IdSet *h, int64_t k) {
+  uint64_t s = hmix(k) & h->mask;
+  for (;;) {
+    int64_t c = h->keys[s];
+    if (c == k) return 1;
+    if (c == INT64_MIN) return 0;
+    s = (s + 1) & h->mask;
+  }
+}
+
+typedef struct {
+  const IdSet *a, *b;
+  const int64_t *src, *dst;
+  int64_t lo, hi;
+  uint64_t count;
+} OneHopTask;
+
+static void *onehop_worker(void *arg) {
+  OneHopTask *t = (OneHopTask *)arg;
+  uint64_t c = 0;
+  for (int64_t r = t->lo; r < t->hi; ++r)
+    if (idset_has(t->a, t->src[r]) && idset_has(t->b, t->dst[r])) ++c;
+  t->count = c;
+  return NULL;
+}
+
+uint64_t onehop_label_count(const int64_t *person_ids, int64_t n_person, const int64_t *node_ids, int64_t n_nodes,
+                            const int64_t *src, const int64_t *dst, int64_t m, int threads) {
+  if (threads < 1) threads = 1;
+  IdSet a, b;
+  idset_build(&a, person_ids, n_person);
+  idset_build(&b, node_ids, n_nodes);
+  pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * threads);
+  OneHopTask *tasks = (OneHopTask *)malloc(sizeof(OneHopTask) * threads);
+  for (int t = 0; t < threads; ++t) {
+    tasks[t].a = &a;
+    tasks[t].b = &b;
+    tasks[t].src = src;
+    tasks[t].dst = dst;
+    tasks[t].lo = m * t / threads;
+    tasks[t].hi = m * (t + 1) / threads;
+    pthread_create(&th[t], NULL, onehop_worker, &tasks[t]);
+  }
+  uint64_t c = 0;
+  for (int t = 0; t < threads; ++t) {
+    pthread_join(th[t], NULL);
+    c += tasks[t].count;
+  }
+  free(th);
+  free(tasks);
+  free(a.keys);
+  free(b.keys);
+  return c;
+}
+
 /* ------------------------------------------- full-size counts (fixtures) */
 /* Streaming closed forms at the headline sizes (R-MAT s22/s24): every thread
  * generates its contiguous edge range with rmat_edges' arithmetic and keeps

@@ -28,10 +28,16 @@ Everything materialises with numpy; sizes are the small parity cases.
 """
 import numpy as np
 
+import math
+from decimal import Decimal, localcontext
+from fractions import Fraction
+
 from capf_amd.expr import (T_BOOL, T_FLOAT, T_INT, T_LIST, T_NULL, T_STRING, CAPF_TO_CT, CT_TO_CAPF,
-                           Aggregator, Ands, BoolLit, Coalesce, ElementProperty, EndNode, FloatLit, HasLabel,
-                           HasType, IntegerLit, ListLit, NullLit, Ors, Param, StartNode, StringLit, Var, AGG_AVG,
-                           AGG_COLLECT, AGG_COUNT, AGG_COUNT_STAR, AGG_MAX, AGG_MIN, AGG_SUM)
+                           Aggregator, Ands, BoolLit, CaseExpr, Coalesce, E_, ElementProperty, EndNode, Explode,
+                           FloatLit, HasLabel, HasType, IntegerLit, ListLit, NullLit, Ors, Param, Pi_, StartNode,
+                           StringLit, Var, AGG_AVG, AGG_COLLECT, AGG_COUNT, AGG_COUNT_STAR, AGG_MAX, AGG_MIN,
+                           AGG_PERCENTILE_CONT, AGG_PERCENTILE_DISC, AGG_STDEV, AGG_STDEV_POP, AGG_SUM,
+                           explode_values, percentile_value)
 
 
 def list_values(e, params):
@@ -328,6 +334,55 @@ def evaluate(e, table, header, params):
                     out[t] = h.rel_type
                     ok |= t
             return Val(T_STRING, out, ok)
+        if name in _MATH1:
+            return _math1(name, go(x.expr), n)
+        if name == "Atan2":  # atan2(child0, child1) (FlinkSQLExprMapper.scala:207)
+            y, z = go(x.lhs), go(x.rhs)
+            with np.errstate(all="ignore"):
+                return Val(T_FLOAT, np.arctan2(_num(y).astype(np.float64), _num(z).astype(np.float64)), y.ok & z.ok)
+        if name == "Cot":  # Divide(IntegerLit(1), Tan(e)) (:208)
+            t = _math1("Tan", go(x.expr), n)
+            return _arith(const(T_INT, 1), t, "div")
+        if name == "Haversin":  # Divide(Subtract(1, Cos(e)), 2) (:210)
+            c = _math1("Cos", go(x.expr), n)
+            return _arith(_arith(const(T_INT, 1), c, "sub"), const(T_INT, 2), "div")
+        if isinstance(x, E_):
+            return const(T_FLOAT, math.e)
+        if isinstance(x, Pi_):
+            return const(T_FLOAT, math.pi)
+        if name in ("StartNodeFunction", "EndNodeFunction"):  # (:179-180)
+            return go(StartNode(x.expr) if name == "StartNodeFunction" else EndNode(x.expr))
+        if name == "ToBoolean":  # cast to BOOLEAN (:185)
+            a = go(x.expr)
+            if a.t in (T_BOOL, T_NULL):
+                return Val(T_BOOL, a.v.astype(bool), a.ok.copy())
+            if a.t != T_STRING:
+                raise NotImplementedError(f"oracle: toBoolean of {CAPF_TO_CT[a.t]}")
+            parsed = [(str(v).strip().lower() if ok else None) for v, ok in zip(a.v, a.ok)]
+            return Val(T_BOOL, np.array([p == "true" for p in parsed], bool),
+                       np.array([p in ("true", "false") for p in parsed], bool))
+        if isinstance(x, CaseExpr):  # If(p1, v1, If(p2, v2, … default)) (:242-260)
+            acc = go(x.default) if x.default is not None else const(T_INT, None, False)
+            for p, v in reversed(x.alternatives):
+                c, val = go(p), go(v)
+                take = c.ok & c.v.astype(bool)
+                t = val.t if val.t != T_NULL else acc.t
+                if T_NULL not in (val.t, acc.t) and val.t != acc.t:
+                    if {val.t, acc.t} <= {T_INT, T_FLOAT}:
+                        t = T_FLOAT
+                    else:
+                        raise TypeError("branches of different types")
+                vv = _num(val).astype(np.float64) if t == T_FLOAT else val.v
+                av = _num(acc).astype(np.float64) if t == T_FLOAT else acc.v
+                if t == T_NULL:
+                    acc = Val(T_NULL, np.zeros(n, np.int64), np.zeros(n, bool))
+                    continue
+                if val.t == T_NULL:
+                    vv = _empty_vals(t, n)
+                if acc.t == T_NULL:
+                    av = _empty_vals(t, n)
+                acc = Val(t, np.where(take, vv, av), np.where(take, val.ok, acc.ok))
+            return acc
         if isinstance(x, Coalesce):
             vals = [go(y) for y in x.exprs]
             t = T_NULL
@@ -347,6 +402,80 @@ def evaluate(e, table, header, params):
         raise NotImplementedError(f"oracle: unsupported expression {x}")
 
     return go(e)
+
+
+_MATH1 = {"Round", "Abs", "Ceil", "Floor", "Sign", "Sqrt", "Log", "Log10", "Exp", "Sin", "Cos", "Tan", "Asin",
+          "Acos", "Atan", "Degrees", "Radians"}
+
+
+def _math1(name, a, n):
+    """FlinkSQLExprMapper.scala:199-221 over doubles (Java Math); ROUND half
+    away from zero as a FLOAT (Spark's round(x).cast(Double)); ABS / CEIL /
+    FLOOR / SIGN keep an INTEGER operand's type (Calcite ARG0)."""
+    keeps = name in ("Abs", "Ceil", "Floor", "Sign")
+    if a.t == T_NULL:
+        return Val(T_FLOAT, np.zeros(n), np.zeros(n, bool))
+    if a.t not in (T_INT, T_FLOAT):
+        raise NotImplementedError(f"oracle: {name} of {CAPF_TO_CT[a.t]}")
+    if a.t == T_INT and keeps:
+        v = a.v.astype(np.int64)
+        r = {"Abs": np.abs(v), "Ceil": v, "Floor": v, "Sign": np.sign(v)}[name]
+        return Val(T_INT, r.astype(np.int64), a.ok.copy())
+    x = _num(a).astype(np.float64)
+    with np.errstate(all="ignore"):
+        if name == "Round":
+            r = np.trunc(x)
+            f = x - r
+            r = np.where(f >= 0.5, r + 1.0, np.where(f <= -0.5, r - 1.0, r))
+        elif name == "Sign":
+            r = np.where(x > 0, 1.0, np.where(x < 0, -1.0, x))
+        elif name == "Degrees":
+            r = x * 180.0 / math.pi
+        elif name == "Radians":
+            r = x / 180.0 * math.pi
+        else:
+            r = {"Abs": np.abs, "Ceil": np.ceil, "Floor": np.floor, "Sqrt": np.sqrt, "Log": np.log,
+                 "Log10": np.log10, "Exp": np.exp, "Sin": np.sin, "Cos": np.cos, "Tan": np.tan, "Asin": np.arcsin,
+                 "Acos": np.arccos, "Atan": np.arctan}[name](x)
+    return Val(T_FLOAT, np.asarray(r, dtype=np.float64), a.ok.copy())
+
+
+def _exact_stdev(vals, samp):
+    """The exact standard deviation of floats, rounded once: Fraction mean
+    and squared deviations, a 60-digit square root."""
+    n = len(vals)
+    if n < (2 if samp else 1):
+        return None
+    fr = [Fraction(v) for v in vals]
+    mean = sum(fr) / n
+    m2 = sum((f - mean) ** 2 for f in fr) / (n - 1 if samp else n)
+    with localcontext() as ctx:
+        ctx.prec = 60
+        return float((Decimal(m2.numerator) / Decimal(m2.denominator)).sqrt())
+
+
+def _percentile(vals, p, cont):
+    """PercentileUdafs.scala:59-96 (the Spark backend's UDAFs): over the
+    ascending values as doubles."""
+    sv = sorted(vals)
+    n = len(sv)
+    if n == 0:
+        return None
+    if not cont:
+        x = n * p
+        pos = math.floor(x)
+        if x - pos >= 0.5:  # Math.round, ties up
+            pos += 1
+        return sv[0] if pos == 0 else sv[pos - 1]
+    sv = [float(v) for v in sv]
+    exact = 1 + ((n - 1) * p)
+    prec, succ = math.floor(exact), math.ceil(exact)
+    w = succ - exact
+    if exact < 1:
+        return (1 - w) * sv[succ] + w * sv[prec]
+    if exact == succ:
+        return sv[prec - 1]
+    return (1 - w) * sv[succ - 1] + w * sv[prec - 1]
 
 
 def _key_codes(cols, null_is_group=True):
@@ -607,6 +736,26 @@ class OracleTable:
                         cnt[g] += 1
                 return Col(T_INT, cnt, np.ones(ng, bool))
             return Col(T_INT, np.bincount(gid[sel], minlength=ng).astype(np.int64), np.ones(ng, bool))
+        if agg.kind in (AGG_STDEV, AGG_STDEV_POP, AGG_PERCENTILE_CONT, AGG_PERCENTILE_DISC):
+            if v.t not in (T_INT, T_FLOAT, T_NULL):
+                raise NotImplementedError("stDev / percentile of non-numeric values")
+            groups = [[] for _ in range(ng)]
+            if v.t != T_NULL:
+                for g, x, ok in zip(gid.tolist(), v.v.tolist(), sel.tolist()):
+                    if ok:
+                        groups[g].append(x)
+            if agg.kind in (AGG_STDEV, AGG_STDEV_POP):
+                res = [_exact_stdev([float(x) for x in xs], agg.kind == AGG_STDEV) for xs in groups]
+                out_t = T_FLOAT
+            else:
+                p = percentile_value(agg.percentile, params)
+                res = [_percentile(xs, p, agg.kind == AGG_PERCENTILE_CONT) for xs in groups]
+                out_t = T_FLOAT if agg.kind == AGG_PERCENTILE_CONT or v.t != T_INT else T_INT
+            arr = _empty_vals(out_t, ng)
+            for g, r in enumerate(res):
+                if r is not None:
+                    arr[g] = r
+            return Col(out_t, arr, np.array([r is not None for r in res], bool))
         if v.t == T_STRING and agg.kind != AGG_COUNT:
             raise NotImplementedError("aggregate of strings")
         cnt = np.bincount(gid[sel], minlength=ng)
@@ -638,7 +787,56 @@ class OracleTable:
             res[g] = a
         return Col(out_t if out_t != T_NULL else T_INT, res, cnt > 0)
 
+    def _explode(self, e, name, header, params):
+        """UNWIND: Explode(list) AS name (RelationalPlanner.scala:99-101),
+        every row repeated per element (Spark explode: a NULL / empty list
+        yields no row)."""
+        ev = explode_values(e.expr, params)
+        if ev is not None:
+            t, vals = ev
+            k = len(vals)
+            idx = np.repeat(np.arange(self._n), k)
+            el = np.tile(np.arange(k), self._n)
+            ev_col = Col(t, np.array([v if v is not None else (0 if t != T_STRING else None) for v in vals],
+                                     dtype=_NP[t]) if k else _empty_vals(t, 0),
+                         np.array([v is not None for v in vals], bool))
+        else:
+            src = header.get(e.expr) if header is not None else None
+            if src is None or src not in self._cols:
+                if isinstance(e.expr, (Var, NullLit)):
+                    return self._mk(self._order + [name], {**{c: k.take([]) for c, k in self._cols.items()},
+                                                           name: Col(T_NULL, _empty_vals(T_NULL, 0), [])}, 0)
+                raise NotImplementedError(f"oracle: UNWIND of {e.expr}")
+            lc = self._cols[src]
+            if lc.t != T_LIST:
+                raise ValueError("UNWIND of a non-list column")
+            rows, els = [], []
+            for i, (lst, ok) in enumerate(zip(lc.v, lc.ok)):
+                if ok and lst is not None:
+                    rows += [i] * len(lst)
+                    els += list(lst)
+            idx = np.array(rows, dtype=np.int64)
+            el = np.arange(len(els))
+            et = T_NULL
+            for x in els:
+                et = T_FLOAT if isinstance(x, float) else T_BOOL if isinstance(x, bool) else \
+                    T_STRING if isinstance(x, str) else T_INT
+                break
+            ev_col = Col(et, np.array(els, dtype=_NP[et]) if els else _empty_vals(et, 0), np.ones(len(els), bool))
+        cols = {c: k.take(idx) for c, k in self._cols.items()}
+        cols[name] = ev_col.take(el)
+        return self._mk(self._order + [name], cols, len(idx))
+
     def withColumns(self, *columns, header=None, params=None):
+        if any(isinstance(e, Explode) for e, _ in columns):
+            t = self
+            plain = [(e, c) for e, c in columns if not isinstance(e, Explode)]
+            if plain:
+                t = t.withColumns(*plain, header=header, params=params)
+            for e, c in columns:
+                if isinstance(e, Explode):
+                    t = t._explode(e, c, header, params)
+            return t
         order = list(self._order)
         cols = dict(self._cols)
         for e, name in columns:

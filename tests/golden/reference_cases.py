@@ -11,7 +11,7 @@ Sources (relative to the reference checkout):
   MTa = morpheus-testing/src/test/scala/org/opencypher/morpheus/impl/acceptance/
 """
 import capf_import  # noqa: F401
-from capf_amd.expr import (Avg, Collect, Count, CountStar, ElementProperty, Exists, Id, In, IntegerLit, ListLit,
+from capf_amd.expr import (Avg, Collect, Count, CountStar, ElementProperty, Exists, FloatLit, Id, In, IntegerLit, ListLit,
                            Max, Min, NullLit, Param, Size, StringLit, Sum, Type, Var)
 from capf_amd.planner import Match, NodeP, Query, RelP, Stage
 
@@ -733,3 +733,73 @@ EXPR_CASES = [
     ("null_type", "MTa/NullTests.scala:49", "", _unit(("res", Type(NullLit()))), [{"res": None}]),
 ]
 CASES = CASES + EXPR_CASES
+
+
+# ------------------- AggregationTests stDev / stDevP / percentiles (FTt :593-730)
+# UNWIND <list literal> AS x is the relational `add(Explode(list) as x)`
+# (RelationalPlanner.scala:99-101) over the unit table; round(agg * 1000) /
+# 1000.0 aggregates first, then projects (okapi plans the Aggregate below the
+# Project).  stDev / stDevP are Flink's stddevSamp / stddevPop
+# (FlinkSQLExprMapper.scala:223-224); the percentiles follow the Spark
+# backend's UDAFs (PercentileUdafs.scala:59-96) — Flink has no mapping.
+def _unwind(values, alias, *items):
+    from capf_amd.planner import Unwind
+    lit = ListLit(*[NullLit() if v is None else FloatLit(v) if isinstance(v, float) else IntegerLit(v)
+                    for v in values])
+    return Query([Unwind(lit, alias)], [ret(*items)])
+
+
+def _round3(agg):
+    from capf_amd.expr import Divide, FloatLit as F, Multiply, Round
+    return Divide(Round(Multiply(agg, IntegerLit(1000))), F(1000.0))
+
+
+STDEV5 = [98.17, 112.3, 102.6, 94.3, 108.1]
+STDEV5N = [98.17, None, 102.6, 94.3, 108.1]
+
+
+def _stat_cases():
+    from capf_amd.expr import PercentileCont, PercentileDisc, StDev, StDevP
+    x = lambda v: Var(v)  # noqa: E731
+    src = "FTt/acceptance/AggregationTests.scala:"
+    return [
+        ("stdev_floats", src + "594-600", "",
+         _unwind(STDEV5, "numbers", ("res", _round3(StDev(x("numbers"))))), [{"res": 7.274}]),
+        ("stdev_nullable_floats", src + "602-608", "",
+         _unwind(STDEV5N, "numbers", ("res", _round3(StDev(x("numbers"))))), [{"res": 5.936}]),
+        ("stdev_null", src + "610-617", "", _unit(("res", StDev(NullLit()))), [{"res": None}]),
+        ("stdevp_floats", src + "621-627", "",
+         _unwind(STDEV5, "numbers", ("res", _round3(StDevP(x("numbers"))))), [{"res": 6.506}]),
+        ("stdevp_nullable_floats", src + "629-635", "",
+         _unwind(STDEV5N, "numbers", ("res", _round3(StDevP(x("numbers"))))), [{"res": 5.140}]),
+        ("stdevp_null", src + "637-644", "", _unit(("res", StDevP(NullLit()))), [{"res": None}]),
+        ("pcont_ints", src + "648-654", "",
+         _unwind([1, 2], "values", ("res", PercentileCont(x("values"), FloatLit(0.5)))), [{"res": 1.5}]),
+        ("pcont_one", src + "656-662", "",
+         _unwind([2, 10, 5, 6], "values", ("res", PercentileCont(x("values"), FloatLit(1.0)))), [{"res": 10.0}]),
+        ("pcont_zero", src + "664-670", "",
+         _unwind([2, 10, 5, 6], "values", ("res", PercentileCont(x("values"), FloatLit(0.0)))), [{"res": 2.0}]),
+        ("pcont_floats_null", src + "672-678", "",
+         _unwind([10.0, None, 2.0, 6.0], "values", ("res", _round3(PercentileCont(x("values"), FloatLit(0.62))))),
+         [{"res": 6.96}]),
+        ("pcont_floats", src + "680-686", "",
+         _unwind([10.0, 5.0, 2.0, 6.0], "values", ("res", PercentileCont(x("values"), FloatLit(0.6)))),
+         [{"res": 5.8}]),
+        ("pdisc_ints", src + "690-696", "",
+         _unwind([10, 5, 2, 6], "values", ("res", PercentileDisc(x("values"), FloatLit(0.5)))), [{"res": 5}]),
+        ("pdisc_one", src + "698-704", "",
+         _unwind([10.0, 5.0, 2.0, 6.0], "values", ("res", PercentileDisc(x("values"), FloatLit(1.0)))),
+         [{"res": 10.0}]),
+        ("pdisc_zero", src + "706-712", "",
+         _unwind([10.0, 5.0, 2.0, 6.0], "values", ("res", PercentileDisc(x("values"), FloatLit(0.0)))),
+         [{"res": 2.0}]),
+        ("pdisc_floats_null", src + "714-720", "",
+         _unwind([10.0, None, 2.0, 6.0], "values", ("res", PercentileDisc(x("values"), FloatLit(0.6)))),
+         [{"res": 6.0}]),
+        ("pdisc_floats_graph", src + "722-729", "CREATE ({age: 10.0}), ({age: 2.0}), ({age: 5.0}), ({age: 6.0})",
+         scan_n(ret(("res", PercentileDisc(P("n", "age"), FloatLit(0.5))))), [{"res": 5.0}]),
+    ]
+
+
+STAT_CASES = _stat_cases()
+CASES = CASES + STAT_CASES

@@ -123,8 +123,22 @@ def _two_hop_worker(rank, world, port, q):
         # the device only then)
         doubled = run(g, Query(two.matches, [Stage([("c", CountStar())]),
                                              Stage([("d", Multiply(Var("c"), IntegerLit(2)))])]))[0]["d"]
+        # duplicate rel ids (two rels sharing id 100000) or a NULL endpoint: no
+        # node-partitioned layout, the plan replays and matches the single-process one
+        extra = []
+        for rels in ([(100000 if k == 7 else 100000 + k, int(a) + 5, int(b) + 5, "E", {})
+                      for k, (a, b) in enumerate(zip(src, dst))],
+                     [(100000 + k, None if k == 3 else int(a) + 5, int(b) + 5, "E", {})
+                      for k, (a, b) in enumerate(zip(src, dst))]):
+            d2 = GraphData(data.nodes, rels)
+            full2 = ScanGraph.from_data(OracleSession(), d2)
+            before = len(oracle_count_copies.calls)
+            g2 = dist_node_partitioned_graph(DistSession(OracleSession(), OracleExchange()), full2,
+                                             count_copies=oracle_count_copies)
+            extra.append((run(g2, two)[0]["count"], run(full2, two)[0]["count"],
+                          len(oracle_count_copies.calls) - before))
         q.put((rank, got, got_back, dispatched, bag(got_rows) == bag(ref_rows), one,
-               got3 == want3 > 0 and doubled == 2 * got,
+               got3 == want3 > 0 and doubled == 2 * got and all(a == b and k == 0 for a, b, k in extra),
                cmodel.count_2hop(src, dst, n), len(src)))
         dist.destroy_process_group()
     except Exception:  # noqa: BLE001

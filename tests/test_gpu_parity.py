@@ -995,15 +995,213 @@ def test_collect_list_ops_fail_loudly(gpu_session):
         run(ScanGraph.from_data(gpu_session, _collect_graph(200)), q)
 
 
-@pytest.mark.parametrize("agg", ["StDev", "PercentileDisc"])
-def test_unmapped_aggregators_raise_on_gpu(gpu_session, agg):
+def _stat_table(session, n, ng, seed, nulls, ints=False):
+    """n rows in ng groups: values X / 2^20 with integer X near 2^39 (mean
+    about 5e5, spread below 1: a naive one-pass variance loses ~12 digits),
+    one group holding most rows, optional NULLs; returns (table, header,
+    gid, X, valid)."""
+    rng = np.random.default_rng(seed)
+    gid = rng.integers(0, ng, n)
+    gid[rng.random(n) < 0.3] = 0  # a huge group
+    X = (1 << 39) + rng.integers(0, 1 << 20, n) * (1 + (gid % 5))
+    if ints:
+        X = rng.integers(-(1 << 40), 1 << 40, n)
+    valid = rng.random(n) > 0.05 if nulls else np.ones(n, bool)
+    vals = X.astype(np.float64) / 2.0 ** 20 if not ints else X
+    t = session.table([("k", T_INT, gid, None), ("v", T_INT if ints else T_FLOAT, vals, valid.astype(np.uint8))])
+    h = RecordHeader({Var("k"): "k", Var("v"): "v"})
+    return t, h, gid, X, valid
+
+
+def _isum(a):
+    """Exact sum of an int64 array as a Python int (chunks far below 2^63)."""
+    return sum(int(c.sum()) for c in np.array_split(a, len(a) // 500_000 + 1)) if len(a) else 0
+
+
+def _exact_stdev_groups(gid, X, valid, ng, scale, samp):
+    """Exact per-group standard deviation of X / scale with integer
+    arithmetic: var = (n·ΣX² − (ΣX)²) / (n·(n − 1)) / scale², one rounding in
+    a 60-digit Decimal square root."""
+    from decimal import Decimal, localcontext
+    s1 = np.zeros(ng, dtype=object)
+    s2 = np.zeros(ng, dtype=object)
+    cnt = np.bincount(gid[valid], minlength=ng)
+    for g in range(ng):
+        xs = X[(gid == g) & valid]
+        hi, lo = xs >> 20, xs & ((1 << 20) - 1)  # exact squares from 20-bit halves
+        s1[g] = _isum(xs)
+        s2[g] = (_isum(hi * hi) << 40) + (_isum(2 * hi * lo) << 20) + _isum(lo * lo)
+    out = []
+    for g in range(ng):
+        n = int(cnt[g])
+        if n < (2 if samp else 1):
+            out.append(None)
+            continue
+        num = n * s2[g] - s1[g] * s1[g]
+        den = n * (n - 1 if samp else n) * scale * scale
+        with localcontext() as ctx:
+            ctx.prec = 60
+            out.append(float((Decimal(num) / Decimal(den)).sqrt()))
+    return out
+
+
+@pytest.mark.parametrize("nulls", [False, True])
+def test_stdev_exact_at_size(gpu_session, nulls):
+    """Grouped stDev / stDevP over 1e7 rows against the exact value within
+    the north star's 1e-12 (the reference's stddevSamp / stddevPop,
+    FlinkSQLExprMapper.scala:223-224); bit-identical run to run."""
+    from capf_amd.expr import StDev, StDevP
+    n, ng = 10_000_000, 1009
+    t, h, gid, X, valid = _stat_table(gpu_session, n, ng, 7, nulls)
+    for samp in (True, False):
+        agg = StDev(Var("v")) if samp else StDevP(Var("v"))
+        out = t.group([Var("k")], {"s": agg}, header=h)
+        keys, vals = out.column_values("k"), out.column_values("s")
+        want = _exact_stdev_groups(gid, X, valid, ng, 1 << 20, samp)
+        for k, v in zip(keys, vals):
+            w = want[k]
+            assert (v is None) == (w is None), (k, v, w)
+            if w is not None:
+                assert abs(v - w) <= 1e-12 * w, (k, v, w, abs(v - w) / w)
+        again = t.group([Var("k")], {"s": agg}, header=h).column_values("s")
+        assert again == vals
+    # the global aggregate, and INTEGER values (exact integers, no scaling)
+    g = t.group([], {"s": StDev(Var("v"))}, header=h).column_values("s")[0]
+    w = _exact_stdev_groups(np.zeros(n, np.int64), X, valid, 1, 1 << 20, True)[0]
+    assert abs(g - w) <= 1e-12 * w
+    ti, hi_, gi, Xi, vi = _stat_table(gpu_session, 200_000, 17, 9, nulls, ints=True)
+    got = ti.group([Var("k")], {"s": StDevP(Var("v"))}, header=hi_)
+    assert got.capf_type("s") == T_FLOAT
+    want = _exact_stdev_groups(gi, Xi, vi, 17, 1, False)
+    for k, v in zip(got.column_values("k"), got.column_values("s")):
+        assert abs(v - want[k]) <= 1e-12 * want[k]
+
+
+@pytest.mark.parametrize("kind", ["PercentileCont", "PercentileDisc"])
+@pytest.mark.parametrize("p", [0.0, 0.05, 0.5, 0.62, 1.0])
+@pytest.mark.parametrize("ints", [False, True])
+def test_percentiles_parity(gpu_session, kind, p, ints):
+    """percentileCont / percentileDisc grouped over 3e5 rows (NULLs, ties,
+    one huge group) bit-exact against the oracle's restatement of the Spark
+    UDAFs (PercentileUdafs.scala:59-96), in every encoding of the values."""
     import capf_amd.expr as ex
-    cls = getattr(ex, agg)
-    P = ElementProperty(Var("n", "NODE"), "val")
-    a = cls(P) if agg == "StDev" else cls(P, 0.5)
-    q = Query([Match([NodeP("n")])], [Stage([("res", a)])])
-    with pytest.raises(_lib.NotImplementedException):
-        run(ScanGraph.from_data(gpu_session, parse_create("CREATE ({val: 1}), ({val: 2})")), q)
+    rng = np.random.default_rng(int(p * 100) + ints)
+    n, ng = 300_000, 777
+    gid = rng.integers(0, ng, n)
+    gid[rng.random(n) < 0.4] = 3
+    vals = rng.integers(-50, 50, n) if ints else np.round(rng.normal(0, 1e3, n), 3)
+    valid = (rng.random(n) > 0.1).astype(np.uint8)
+    cols = [("k", T_INT, gid, None), ("v", T_INT if ints else T_FLOAT, vals, valid)]
+    h = RecordHeader({Var("k"): "k", Var("v"): "v"})
+    agg = {"q": getattr(ex, kind)(Var("v"), ex.FloatLit(p))}
+    gt = gpu_session.table(cols)
+    ot = OracleSession().table([(c, t, [x if ok else None for x, ok in zip(v, valid)] if c == "v" else v.tolist(),
+                                 None) for c, t, v, _ in cols])
+    for table in ([gt, gt.compact(3)] if ints else [gt]):
+        got = table.group([Var("k")], agg, header=h)
+        want = ot.group([Var("k")], agg, header=h)
+        assert got.capf_type("q") == want.capf_type("q")
+        assert sorted(zip(got.column_values("k"), got.column_values("q"))) == \
+            sorted(zip(want.column_values("k"), want.column_values("q")))
+
+
+def test_unwind_on_gpu(gpu_session):
+    """UNWIND (RelationalPlanner.scala:99-101): a literal list over a scan (NULL
+    elements kept, INTEGER/FLOAT widened), a parameter list, an empty list, and
+    a collected LIST column; against the oracle."""
+    from capf_amd.expr import Collect, FloatLit, ListLit
+    from capf_amd.planner import Unwind, plan_query, plan_stage, plan_unwind, records
+    create = "CREATE ({v: 1, s: 'a'}), ({v: 2, s: 'b'}), ({v: 2})"
+    P = lambda k: ElementProperty(Var("n", "NODE"), k)  # noqa: E731
+    queries = [
+        Query([Match([NodeP("n")]), Unwind(ListLit(IntegerLit(3), NullLit(), FloatLit(4.5)), "x")],
+              [Stage([("x", Var("x")), ("v", P("v"))])]),
+        Query([Unwind(ListLit(), "x"), Match([NodeP("n")])], [Stage([("x", Var("x"))])]),
+        Query([Unwind(ListLit(StringLit("p"), StringLit("q")), "x"), Match([NodeP("n")])],
+              [Stage([("x", Var("x")), ("c", CountStar())])]),
+    ]
+    for q in queries:
+        got = run(ScanGraph.from_data(gpu_session, parse_create(create)), q, {})
+        want = run(ScanGraph.from_data(OracleSession(), parse_create(create)), q, {})
+        assert bag(got) == bag(want), (got, want)
+    from capf_amd.expr import Param
+    q = Query([Unwind(Param("xs"), "x")], [Stage([("x", Var("x"))])])
+    got = run(ScanGraph.from_data(gpu_session, parse_create(create)), q, {"xs": [5, 6, 7]})
+    assert sorted(r["x"] for r in got) == [5, 6, 7]
+    for sess in (gpu_session, OracleSession()):
+        g = ScanGraph.from_data(sess, parse_create(create))
+        op = plan_query(g, Query([Match([NodeP("n")])], [Stage([("k", P("s")), ("xs", Collect(P("v")))])]))
+        op = plan_stage(plan_unwind(op, Unwind(Var("xs"), "y")), Stage([("k", Var("k")), ("y", Var("y"))]))
+        rows = records(op, ["k", "y"])
+        assert sorted((r["k"] or "", r["y"]) for r in rows) == [("", 2), ("a", 1), ("b", 2)]
+
+
+MATH = ["Round", "Abs", "Ceil", "Floor", "Sign", "Sqrt", "Log", "Log10", "Exp", "Sin", "Cos", "Tan", "Asin",
+        "Acos", "Atan", "Degrees", "Radians", "Cot", "Haversin"]
+
+
+@pytest.mark.parametrize("fn", MATH)
+def test_math_functions_parity(gpu_session, fn):
+    """FlinkSQLExprMapper.scala:199-221 on the GPU against the oracle: exact for
+    round / abs / ceil / floor / sign / degrees / radians, within 1e-15
+    relative (the device libm against numpy's) for the transcendental ones."""
+    import capf_amd.expr as ex
+    rng = np.random.default_rng(len(fn))
+    n = 4096
+    f = np.concatenate([rng.normal(0, 10, n - 12), [0.5, -0.5, 1.5, -2.5, 2.4999999999999996, 0.0, -0.0, 1e300,
+                                                    -1e-300, np.inf, -np.inf, np.nan]])
+    iv = rng.integers(-1000, 1000, n)
+    valid = (rng.random(n) > 0.1).astype(np.uint8)
+    cols = [("f", T_FLOAT, f, valid), ("i", T_INT, iv, valid)]
+    h = RecordHeader({Var("f"): "f", Var("i"): "i"})
+    ot = OracleSession().table([(c, t, [x if ok else None for x, ok in zip(v.tolist(), valid)], None)
+                                for c, t, v, _ in cols])
+    for src in ("f", "i"):
+        e = getattr(ex, fn)(Var(src))
+        got = gpu_session.table(cols).withColumns((e, "o"), header=h)
+        want = ot.withColumns((e, "o"), header=h)
+        assert got.capf_type("o") == want.capf_type("o"), (fn, src)
+        gv, wv = got.column_values("o"), want.column_values("o")
+        exact = fn in ("Round", "Abs", "Ceil", "Floor", "Sign", "Degrees", "Radians")
+        for a, b in zip(gv, wv):
+            if a is None or b is None or (isinstance(b, float) and (b != b or b in (np.inf, -np.inf))):
+                assert (a is None) == (b is None) and (b is None or repr(a) == repr(b) or (a != a and b != b))
+            elif exact:
+                assert a == b and repr(a) == repr(b), (fn, src, a, b)
+            else:
+                assert abs(a - b) <= 1e-15 * max(abs(a), abs(b)) + 1e-300, (fn, src, a, b)
+
+
+def test_case_atan2_toboolean_parity(gpu_session):
+    """CASE (FlinkSQLExprMapper.scala:242-260, numeric branches widened),
+    atan2 (:207), toBoolean over strings (:185), e() / pi(), startNode(r)."""
+    import capf_amd.expr as ex
+    rng = np.random.default_rng(5)
+    n = 2000
+    x = rng.normal(0, 3, n)
+    y = rng.integers(-5, 5, n)
+    words = ["true", "FALSE", " True ", "yes", "", "false"]
+    s = [words[i % len(words)] if i % 7 else None for i in range(n)]
+    cols = [("x", T_FLOAT, x.tolist(), None), ("y", T_INT, y.tolist(), None), ("s", T_STRING, s, None)]
+    h = RecordHeader({Var("x"): "x", Var("y"): "y", Var("s"): "s"})
+    exprs = [
+        ex.CaseExpr([(GreaterThan(Var("x"), FloatLit(1.0)), Var("y")), (LessThan(Var("y"), IntegerLit(0)), Var("x"))],
+                    ex.NullLit("FLOAT")),
+        ex.CaseExpr([(Equals(Var("y"), IntegerLit(2)), IntegerLit(20))], Var("y")),
+        ex.CaseExpr([(IsNull(Var("s")), StringLit("none"))], Var("s")),
+        ex.CaseExpr([(GreaterThan(Var("y"), IntegerLit(3)), IntegerLit(1))]),
+        ex.Atan2(Var("x"), Var("y")),
+        ex.ToBoolean(Var("s")),
+        Add(Var("x"), ex.Pi), Multiply(ex.E, Var("y")),
+    ]
+    gt = gpu_session.table(cols)
+    ot = OracleSession().table(cols)
+    for e in exprs:
+        got = gt.withColumns((e, "o"), header=h)
+        want = ot.withColumns((e, "o"), header=h)
+        assert got.capf_type("o") == want.capf_type("o"), e
+        for a, b in zip(got.column_values("o"), want.column_values("o")):
+            assert a == b or (isinstance(a, float) and abs(a - b) <= 1e-15 * abs(b)), (str(e), a, b)
 
 
 @pytest.mark.parametrize("hot", ["sampled", "none", "owned", "foreign", "dup", "range"])

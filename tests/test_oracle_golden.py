@@ -73,16 +73,57 @@ def test_avg_of_integers_is_float():
 
 
 @pytest.mark.parametrize("agg", ["StDev", "StDevP", "PercentileCont", "PercentileDisc"])
-def test_unmapped_aggregators_raise(agg):
-    """stDev / stDevP / percentileCont / percentileDisc
-    (AggregationTests.scala:593-730) have no case in the Flink mapper
-    (FlinkSQLExprMapper.scala:281-290): the reference backend raises
-    NotImplementedException, and so do the oracle and the product table."""
+def test_stat_aggregators_on_oracle(agg):
+    """stDev / stDevP (Flink stddevSamp / stddevPop, FlinkSQLExprMapper.scala:
+    223-224) and the percentiles (the Spark backend's UDAFs,
+    PercentileUdafs.scala:59-96) over a keyed graph, against Python's
+    statistics module and the UDAF formulas restated by hand."""
+    import statistics
     import capf_amd.expr as ex
-    from capf_amd._lib import NotImplementedException
-    from reference_cases import INTS3, P, scan_n, ret
+    from reference_cases import P, scan_n, ret
+    vals = {"a": [3.5, -1.25, 8.0, 2.0, 2.0], "b": [7.0], "c": []}
+    create = "CREATE " + ", ".join(
+        [f"({{key: '{k}', val: {v}}})" for k, vs in vals.items() for v in vs] + ["({key: 'c'})"])
     cls = getattr(ex, agg)
-    a = cls(P("n", "val")) if agg.startswith("StDev") else cls(P("n", "val"), 0.5)
-    g = ScanGraph.from_data(OracleSession(), parse_create(INTS3))
-    with pytest.raises((NotImplementedException, NotImplementedError)):
-        run(g, scan_n(ret(("res", a))))
+    a = cls(P("n", "val")) if agg.startswith("StDev") else cls(P("n", "val"), ex.FloatLit(0.4))
+    g = ScanGraph.from_data(OracleSession(), parse_create(create))
+    got = {r["k"]: r["res"] for r in run(g, scan_n(ret(("k", P("n", "key")), ("res", a))))}
+    for k, vs in vals.items():
+        if agg == "StDev":
+            want = statistics.stdev(vs) if len(vs) > 1 else None
+        elif agg == "StDevP":
+            want = statistics.pstdev(vs) if vs else None
+        elif not vs:
+            want = None
+        elif agg == "PercentileDisc":
+            s = sorted(vs)
+            pos = int(len(s) * 0.4 + 0.5)
+            want = s[max(pos, 1) - 1]
+        else:
+            s = sorted(vs)
+            x = 1 + (len(s) - 1) * 0.4
+            lo, hi = int(x // 1), -int(-x // 1)
+            want = s[lo - 1] if lo == hi else (1 - (hi - x)) * s[hi - 1] + (hi - x) * s[lo - 1]
+        assert (got[k] is None) == (want is None), (k, got[k], want)
+        if want is not None:
+            assert abs(got[k] - want) <= 1e-15 * abs(want), (k, got[k], want)
+
+
+def test_unwind_on_oracle():
+    """UNWIND over the unit table and over a collected list column."""
+    from capf_amd.expr import Collect, IntegerLit, ListLit, NullLit, Var
+    from capf_amd.planner import Match, NodeP, Query, Stage, Unwind
+    from reference_cases import P
+    g = ScanGraph.from_data(OracleSession(), parse_create("CREATE ({v: 1}), ({v: 2})"))
+    q = Query([Unwind(ListLit(IntegerLit(3), NullLit(), IntegerLit(4)), "x"), Match([NodeP("n")])],
+              [Stage([("x", Var("x")), ("v", P("n", "v"))])])
+    got = sorted(((r["x"] is None, r["x"] or 0), r["v"]) for r in run(g, q))
+    assert got == [((False, 3), 1), ((False, 3), 2), ((False, 4), 1), ((False, 4), 2),
+                   ((True, 0), 1), ((True, 0), 2)]
+    q = Query([Match([NodeP("n")])], [Stage([("xs", Collect(P("n", "v")))])])
+    from capf_amd.planner import plan_query, plan_stage, plan_unwind
+    op = plan_query(g, q)
+    op = plan_unwind(op, Unwind(Var("xs"), "y"))
+    op = plan_stage(op, Stage([("y", Var("y"))]))
+    from capf_amd.planner import records
+    assert sorted(r["y"] for r in records(op, ["y"])) == [1, 2]

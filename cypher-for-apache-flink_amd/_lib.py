@@ -156,6 +156,16 @@ _SIGS = {
                                               POINTER(c_int64), POINTER(c_int32), c_void_p, c_int64,
                                               POINTER(_T)]),
     "capf_dot_u32": (c_int32, [_S, c_void_p, c_void_p, c_int64, POINTER(c_uint64)]),
+    "capf_comm_unique_id": (c_int32, [c_void_p]),
+    "capf_comm_init": (c_int32, [_S, c_int32, c_int32, c_void_p, _PT]),
+    "capf_comm_destroy": (c_int32, [c_void_p]),
+    "capf_comm_rank": (c_int32, [c_void_p, POINTER(c_int32), POINTER(c_int32)]),
+    "capf_comm_all_reduce_i64": (c_int32, [c_void_p, c_void_p, c_int64, c_int32]),
+    "capf_comm_all_gather_bytes": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "capf_comm_all_to_all_bytes": (c_int32, [c_void_p, c_void_p, POINTER(c_int64), c_void_p, POINTER(c_int64)]),
+    "capf_session_alloc": (c_int32, [_S, c_int64, POINTER(c_void_p)]),
+    "capf_session_free": (c_int32, [_S, c_void_p]),
+    "capf_session_copy": (c_int32, [_S, c_void_p, c_void_p, c_int64, c_int32]),
 }
 
 EXPORTED_SYMBOLS = sorted(_SIGS)

@@ -335,6 +335,9 @@ struct Session {
   int device = 0;
   int num_cus = 256;  // compute units of the device (persistent-grid sizing)
   BlockCache cache;
+  // buffers handed out by capf_session_alloc (kept alive until capf_session_free)
+  std::mutex user_mu;
+  std::map<void *, std::shared_ptr<DevBuf>> user_bufs;
   std::vector<PendingTiming> pending;   // recorded, not yet resolved
   std::vector<hipEvent_t> event_pool;
   hipEvent_t get_event();

@@ -719,9 +719,10 @@ __device__ inline int cmp_vals(const Val &a, const Val &b) {
 }
 
 // Unary math functions (FlinkSQLExprMapper.scala:199-221), NULL in NULL out.
-// Products / quotients are written with explicit _rn intrinsics so no FMA
-// contraction changes the Java double arithmetic they restate.
+// FP contraction is off here: no FMA changes the Java double arithmetic
+// they restate.
 __device__ inline Val math1(int32_t op, const Val &a) {
+#pragma clang fp contract(off)
   const bool isint = a.t == CAPF_TYPE_INT64;
   if (a.nul) {
     const bool keeps = op == OP_ABS || op == OP_CEIL || op == OP_FLOOR || op == OP_SIGN;
@@ -756,8 +757,8 @@ __device__ inline Val math1(int32_t op, const Val &a) {
     case OP_ACOS: return mkf(acos(x));
     case OP_ATAN: return mkf(atan(x));
     // Java 8 Math.toDegrees / toRadians: angrad * 180.0 / PI, angdeg / 180.0 * PI
-    case OP_DEGREES: return mkf(__ddiv_rn(__dmul_rn(x, 180.0), 3.141592653589793));
-    case OP_RADIANS: return mkf(__dmul_rn(__ddiv_rn(x, 180.0), 3.141592653589793));
+    case OP_DEGREES: return mkf(x * 180.0 / 3.141592653589793);
+    case OP_RADIANS: return mkf(x / 180.0 * 3.141592653589793);
     default: return mknull(CAPF_TYPE_FLOAT64);
   }
 }

@@ -778,6 +778,7 @@ __device__ inline double pct_round(double x) {  // Scala Double.round (Math.roun
 
 __global__ void k_pct_final(const int64_t *perm, const int64_t *off, const unsigned long long *cnt, int64_t ng,
                             ColView arg, int cont, double p, int out_int, void *out, uint8_t *valid) {
+#pragma clang fp contract(off)  // the JVM's separately rounded * and + (no FMA)
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ng; g += (int64_t)gridDim.x * blockDim.x) {
     const int64_t c = (int64_t)cnt[g];
     valid[g] = c > 0 ? 1 : 0;
@@ -788,22 +789,22 @@ __global__ void k_pct_final(const int64_t *perm, const int64_t *off, const unsig
     }
     const int64_t *v = perm + off[g];
     if (!cont) {
-      const int64_t pos = (int64_t)pct_round(__dmul_rn((double)c, p));
+      const int64_t pos = (int64_t)pct_round((double)c * p);
       const int64_t row = v[pos == 0 ? 0 : pos - 1];
       if (out_int) ((int64_t *)out)[g] = ld_int(arg, row);
       else ((double *)out)[g] = load_num<double>(arg, row);
       continue;
     }
-    const double x = __dadd_rn(1.0, __dmul_rn((double)(c - 1), p));
+    const double x = 1.0 + (double)(c - 1) * p;
     const double fl = floor(x), ce = ceil(x);
     const int64_t prec = (int64_t)fl, succ = (int64_t)ce;
-    const double w = __dsub_rn(ce, x);
+    const double w = ce - x;
     double res;
     if (x == ce) {
       res = load_num<double>(arg, v[prec - 1]);
     } else {
       const double a = load_num<double>(arg, v[succ - 1]), b = load_num<double>(arg, v[prec - 1]);
-      res = __dadd_rn(__dmul_rn(__dsub_rn(1.0, w), a), __dmul_rn(w, b));
+      res = (1.0 - w) * a + w * b;
     }
     ((double *)out)[g] = res;
   }

@@ -785,6 +785,39 @@ capf_status capf_session_sync(capf_session *cs) {
   CAPF_API_END
 }
 
+capf_status capf_session_alloc(capf_session *cs, int64_t bytes, void **d_out) {
+  CAPF_API_BEGIN
+  need(cs, "session");
+  need(d_out, "d_out");
+  if (bytes < 0) illegal("negative size");
+  BufPtr b = cs->impl.alloc((size_t)std::max<int64_t>(bytes, 16));
+  std::lock_guard<std::mutex> g(cs->impl.user_mu);
+  cs->impl.user_bufs[b->p] = b;
+  *d_out = b->p;
+  CAPF_API_END
+}
+
+capf_status capf_session_free(capf_session *cs, void *d) {
+  CAPF_API_BEGIN
+  need(cs, "session");
+  std::lock_guard<std::mutex> g(cs->impl.user_mu);
+  if (!cs->impl.user_bufs.erase(d)) illegal("not a buffer of capf_session_alloc");
+  CAPF_API_END
+}
+
+capf_status capf_session_copy(capf_session *cs, void *dst, const void *src, int64_t bytes, int32_t kind) {
+  CAPF_API_BEGIN
+  need(cs, "session");
+  if (bytes < 0 || kind < 1 || kind > 3) illegal("bad copy");
+  if (bytes == 0) return CAPF_OK;
+  need(dst, "dst");
+  need(src, "src");
+  const hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+  HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)bytes, k, cs->impl.stream));
+  cs->impl.sync();
+  CAPF_API_END
+}
+
 capf_status capf_session_set_profiling(capf_session *cs, int32_t enabled) {
   CAPF_API_BEGIN
   need(cs, "session");

@@ -554,6 +554,40 @@ capf_status capf_table_from_packed_rows(capf_session *s, int32_t ncols, const ch
                                         const int32_t *nullable, const void *d_rows, int64_t nrows,
                                         capf_table **out);
 
+/* ------------------------------------------------- rank communicator (RCCL)
+ * The exchange of the distributed Table layer for hosts without a framework
+ * communicator (the JVM twin DistGpuTable.scala; the Python layer uses
+ * torch.distributed for the same collectives): RCCL over xGMI, one process per
+ * GPU, every collective enqueued on the session's stream (ordered with the
+ * kernels that produce and consume its buffers).  It replaces Flink's hash
+ * repartition between operator instances (FlinkTable.scala:123-196).
+ * capf_comm_unique_id: rank 0 creates the id (128 bytes) and sends it to the
+ *   other ranks out of band; every rank then calls capf_comm_init with it.
+ * capf_comm_all_reduce_i64: in place, op CAPF_COMM_SUM / CAPF_COMM_MAX.
+ * capf_comm_all_gather_bytes: `bytes` from every rank, rank-major into d_recv
+ *   (world × bytes).
+ * capf_comm_all_to_all_bytes: send_bytes[p] bytes (consecutive in d_send, rank
+ *   order) to rank p, recv_bytes[p] from rank p into d_recv (rank order) —
+ *   the packed-row shuffle of capf_table_pack_rows.
+ * capf_session_alloc / capf_session_free: device buffers from the session's
+ *   stream-ordered pool (exchange buffers, count slots);
+ * capf_session_copy: hipMemcpyAsync on the session stream + wait (kind 1 =
+ *   host → device, 2 = device → host, 3 = device → device).               */
+#define CAPF_COMM_ID_BYTES 128
+enum { CAPF_COMM_SUM = 0, CAPF_COMM_MAX = 2 };
+typedef struct capf_comm capf_comm;
+capf_status capf_comm_unique_id(uint8_t *id_out);
+capf_status capf_comm_init(capf_session *s, int32_t world, int32_t rank, const uint8_t *id, capf_comm **out);
+capf_status capf_comm_destroy(capf_comm *c);
+capf_status capf_comm_rank(capf_comm *c, int32_t *rank, int32_t *world);
+capf_status capf_comm_all_reduce_i64(capf_comm *c, int64_t *d_buf, int64_t n, int32_t op);
+capf_status capf_comm_all_gather_bytes(capf_comm *c, const void *d_send, int64_t bytes, void *d_recv);
+capf_status capf_comm_all_to_all_bytes(capf_comm *c, const void *d_send, const int64_t *send_bytes,
+                                       void *d_recv, const int64_t *recv_bytes);
+capf_status capf_session_alloc(capf_session *s, int64_t bytes, void **d_out);
+capf_status capf_session_free(capf_session *s, void *d);
+capf_status capf_session_copy(capf_session *s, void *dst, const void *src, int64_t bytes, int32_t kind);
+
 #ifdef __cplusplus
 }
 #endif

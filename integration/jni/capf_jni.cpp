@@ -709,3 +709,70 @@ JNI(jlong, dotU32)(JNIEnv *env, jobject, jlong s, jlong d_a, jlong d_b, jlong n)
                          reinterpret_cast<const uint32_t *>(d_b), n, &r));
   return (jlong)r;
 }
+
+// ------------------------------------------------ rank communicator (RCCL, capf_comm_*)
+// the 128-byte unique id travels as a Java byte[] (rank 0 creates it, the
+// launcher hands it to every rank)
+JNI(jbyteArray, commUniqueId)(JNIEnv *env, jobject) {
+  uint8_t id[CAPF_COMM_ID_BYTES];
+  if (fail(env, capf_comm_unique_id(id))) return nullptr;
+  jbyteArray a = env->NewByteArray(CAPF_COMM_ID_BYTES);
+  env->SetByteArrayRegion(a, 0, CAPF_COMM_ID_BYTES, reinterpret_cast<const jbyte *>(id));
+  return a;
+}
+JNI(jlong, commInit)(JNIEnv *env, jobject, jlong s, jint world, jint rank, jbyteArray id) {
+  uint8_t raw[CAPF_COMM_ID_BYTES] = {0};
+  if (!id || env->GetArrayLength(id) != CAPF_COMM_ID_BYTES) {
+    illegal_argument(env, "commInit: the id must be 128 bytes");
+    return 0;
+  }
+  env->GetByteArrayRegion(id, 0, CAPF_COMM_ID_BYTES, reinterpret_cast<jbyte *>(raw));
+  capf_comm *c = nullptr;
+  if (fail(env, capf_comm_init(S(s), world, rank, raw, &c))) return 0;
+  return reinterpret_cast<jlong>(c);
+}
+JNI(void, commDestroy)(JNIEnv *env, jobject, jlong c) {
+  fail(env, capf_comm_destroy(reinterpret_cast<capf_comm *>(c)));
+}
+JNI(void, commAllReduceI64)(JNIEnv *env, jobject, jlong c, jlong d_buf, jlong n, jint op) {
+  fail(env, capf_comm_all_reduce_i64(reinterpret_cast<capf_comm *>(c), reinterpret_cast<int64_t *>(d_buf), n, op));
+}
+JNI(void, commAllGatherBytes)(JNIEnv *env, jobject, jlong c, jlong d_send, jlong bytes, jlong d_recv) {
+  fail(env, capf_comm_all_gather_bytes(reinterpret_cast<capf_comm *>(c), reinterpret_cast<const void *>(d_send),
+                                       bytes, reinterpret_cast<void *>(d_recv)));
+}
+JNI(void, commAllToAllBytes)(JNIEnv *env, jobject, jlong c, jlong d_send, jlongArray send_bytes, jlong d_recv,
+                             jlongArray recv_bytes) {
+  std::vector<int64_t> sb = longs(env, send_bytes), rb = longs(env, recv_bytes);
+  fail(env, capf_comm_all_to_all_bytes(reinterpret_cast<capf_comm *>(c), reinterpret_cast<const void *>(d_send),
+                                       sb.data(), reinterpret_cast<void *>(d_recv), rb.data()));
+}
+JNI(jint, commRank)(JNIEnv *env, jobject, jlong c) {
+  int32_t r = 0, w = 0;
+  fail(env, capf_comm_rank(reinterpret_cast<capf_comm *>(c), &r, &w));
+  return r;
+}
+JNI(jint, commWorld)(JNIEnv *env, jobject, jlong c) {
+  int32_t r = 0, w = 0;
+  fail(env, capf_comm_rank(reinterpret_cast<capf_comm *>(c), &r, &w));
+  return w;
+}
+// device buffers of the session pool (exchange buffers, count slots)
+JNI(jlong, sessionAlloc)(JNIEnv *env, jobject, jlong s, jlong bytes) {
+  void *d = nullptr;
+  if (fail(env, capf_session_alloc(S(s), bytes, &d))) return 0;
+  return reinterpret_cast<jlong>(d);
+}
+JNI(void, sessionFree)(JNIEnv *env, jobject, jlong s, jlong d) {
+  fail(env, capf_session_free(S(s), reinterpret_cast<void *>(d)));
+}
+// device ⇄ host through a direct buffer (kind 1 host → device, 2 device → host)
+JNI(void, sessionCopy)(JNIEnv *env, jobject, jlong s, jlong d, jobject host, jlong bytes, jint kind) {
+  void *h = direct(env, host);
+  if (kind == 1) fail(env, capf_session_copy(S(s), reinterpret_cast<void *>(d), h, bytes, 1));
+  else fail(env, capf_session_copy(S(s), h, reinterpret_cast<const void *>(d), bytes, 2));
+}
+// device → device
+JNI(void, sessionCopyDevice)(JNIEnv *env, jobject, jlong s, jlong dst, jlong src, jlong bytes) {
+  fail(env, capf_session_copy(S(s), reinterpret_cast<void *>(dst), reinterpret_cast<const void *>(src), bytes, 3));
+}

@@ -31,6 +31,10 @@ final class GpuCypherSession private (val device: Int, hipStream: Long)
 
   private val strings = scala.collection.mutable.HashMap.empty[String, Long]
 
+  /** Set by DistGpuTable.nodePartitioned: inner joins between projections of
+    * the base shards are recorded (the 2-hop count dispatch looks at them). */
+  @volatile private[gpu] var deferJoins: Boolean = false
+
   // the factories RelationalCypherSession.scala:101-105 leaves abstract
   override val records: GpuRecordsFactory = GpuRecordsFactory()
 

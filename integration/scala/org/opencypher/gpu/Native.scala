@@ -183,4 +183,21 @@ object Native {
                             nullable: Array[Int], dOut: Long): Int
   @native def tableFromPackedRows(session: Long, names: Array[String], types: Array[Int], width: Array[Int],
                                   base: Array[Long], nullable: Array[Int], dRows: Long, nrows: Long): Long
+
+  // rank communicator (RCCL over xGMI, capf_comm_*) and session device buffers
+  final val CommSum = 0
+  final val CommMax = 2
+  @native def commUniqueId(): Array[Byte]
+  @native def commInit(session: Long, world: Int, rank: Int, id: Array[Byte]): Long
+  @native def commDestroy(comm: Long): Unit
+  @native def commRank(comm: Long): Int
+  @native def commWorld(comm: Long): Int
+  @native def commAllReduceI64(comm: Long, dBuf: Long, n: Long, op: Int): Unit
+  @native def commAllGatherBytes(comm: Long, dSend: Long, bytes: Long, dRecv: Long): Unit
+  @native def commAllToAllBytes(comm: Long, dSend: Long, sendBytes: Array[Long], dRecv: Long,
+                                recvBytes: Array[Long]): Unit
+  @native def sessionAlloc(session: Long, bytes: Long): Long
+  @native def sessionFree(session: Long, d: Long): Unit
+  @native def sessionCopy(session: Long, d: Long, host: ByteBuffer, bytes: Long, kind: Int): Unit
+  @native def sessionCopyDevice(session: Long, dst: Long, src: Long, bytes: Long): Unit
 }

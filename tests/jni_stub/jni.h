@@ -10,6 +10,7 @@
 #define JNIEXPORT __attribute__((visibility("default")))
 #define JNICALL
 
+typedef int8_t jbyte;
 typedef int32_t jint;
 typedef int64_t jlong;
 typedef uint8_t jboolean;
@@ -26,6 +27,7 @@ class _jintArray : public _jarray {};
 class _jlongArray : public _jarray {};
 class _jdoubleArray : public _jarray {};
 class _jbooleanArray : public _jarray {};
+class _jbyteArray : public _jarray {};
 typedef _jobject *jobject;
 typedef _jclass *jclass;
 typedef _jstring *jstring;
@@ -36,6 +38,7 @@ typedef _jintArray *jintArray;
 typedef _jlongArray *jlongArray;
 typedef _jdoubleArray *jdoubleArray;
 typedef _jbooleanArray *jbooleanArray;
+typedef _jbyteArray *jbyteArray;
 struct _jmethodID;
 struct _jfieldID;
 typedef _jmethodID *jmethodID;
@@ -63,6 +66,9 @@ struct JNIEnv {
   void GetBooleanArrayRegion(jbooleanArray array, jsize start, jsize len, jboolean *buf);
   void SetLongArrayRegion(jlongArray array, jsize start, jsize len, const jlong *buf);
   void SetDoubleArrayRegion(jdoubleArray array, jsize start, jsize len, const jdouble *buf);
+  jbyteArray NewByteArray(jsize len);
+  void GetByteArrayRegion(jbyteArray array, jsize start, jsize len, jbyte *buf);
+  void SetByteArrayRegion(jbyteArray array, jsize start, jsize len, const jbyte *buf);
   void *GetDirectBufferAddress(jobject buf);
   void DeleteLocalRef(jobject obj);
 };

@@ -3,7 +3,7 @@
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
-  tests/test_gpu_parity.py -k "stdev or percentiles or unwind or math or case_atan2 or reference_case" \
+  tests/test_gpu_parity.py tests/test_comm_gpu.py -k "stdev or percentiles or unwind or math or case_atan2 or comm" \
   > gpurun_out/r05_stat.log 2>&1
 rc=$?
 tail -5 gpurun_out/r05_stat.log

@@ -361,10 +361,6 @@ struct Session {
   // small device scratch for scalar results
   int64_t *d_scalars = nullptr;  // 64 slots
   int64_t *h_scalars = nullptr;  // pinned mirror
-  // fine-grained (coherent) pinned word the fused count's last workgroup stores
-  // the result into; the synchronous path polls it instead of waiting for the
-  // stream (the value lands before the kernel's end-of-grid flush and signal)
-  int64_t *h_fin = nullptr;
   // set by capf_table_count_async for the duration of one call: the fused
   // count writes its result to this device int64 and does not wait
   int64_t *async_out = nullptr;
@@ -563,11 +559,8 @@ struct C2Spill {
   // bin i + 2^15 high), 1 → one uint32 per bin
   const int32_t *split = nullptr;
   int nb = 0;
-  // host side: where the count goes (the pinned scalar or the async slot); the
-  // partitioned pipeline sets p3_dot when its P3 kernel wrote it (the bucket
-  // dots in P3's epilogue: no dot launch)
+  // host side: where the count goes (the pinned scalar or the async slot)
   int64_t *fin = nullptr;
-  int p3_dot = 0;
 };
 // d_acc3 = [Σ in·out, self-loops, done counter] (device): the pipeline writes
 // the self-loop total into [1] and clears [0] and [2] itself (no memset needed)

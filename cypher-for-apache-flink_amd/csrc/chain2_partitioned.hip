@@ -162,10 +162,9 @@ __device__ inline void c5_tile_sum(uint32_t v, uint32_t *red, uint32_t *out) {
 // P1.  ALIAS: r1 and r2 scan the same (start, end) columns — the directed
 // 2-hop (a)-->(b)-->(c) — so one 8-B row gives both keys.  CHECK: range
 // tests needed.  RAGGED: the single last partial tile.
-// DIAG (diagnostics only, CAPF_P1_DIAG; wrong counts): 1 = no LDS sort, the
-// keys go straight from registers to the tile region (the streaming floor of
-// P1's bytes); 2 = the count phase and scan, no scatter (the stage prefill is
-// copied out).
+// (Measured floors at s24, diagnostics since removed: keys straight from
+// registers to the tile region, no LDS sort — P1's streaming floor; count
+// phase and scan only, no scatter.)
 // Raw row data of one load group (4 rows of a FOR24 / FOR32 column) and its
 // decoding to node offsets (id − lo) — the !CHECK form of c5_load4.
 template <int W>
@@ -204,8 +203,10 @@ __device__ inline C5Raw<W> c5_ld_raw(const uint8_t *p) {
 // UPF (ALIAS, in-range, full tiles, FOR24 / FOR32): every load of the tile is
 // issued before the first key is counted — 2 × GROUPS raw loads in flight per
 // thread (96 B at FOR24) instead of one group ahead; the raw registers of a
-// group die as its keys appear, so the peak stays within 64 VGPRs.
-template <int W, bool ALIAS, bool CHECK, bool RAGGED, class SH, int DIAG = 0, int UPF = 0>
+// group die as its keys appear, so the peak stays within 64 VGPRs.  UPF 2:
+// non-temporal loads (s24 P1 0.516 vs 0.521 ms with default-policy loads);
+// UPF 3: also the FOR24 fields used raw when the bases are lo (0.512 ms).
+template <int W, bool ALIAS, bool CHECK, bool RAGGED, class SH, int UPF = 0>
 // Self-loops go out as one plain uint32 per tile (tile_loops[t], summed by
 // k_c3_units); every tile's workgroup also clears its share of the `zwords` words at zbuf
 // (the run totals / work-list header of the post-P1 kernels) — no memset
@@ -243,7 +244,7 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   const uint32_t dummy = (uint32_t)nr << C2_BITS;
   uint32_t kin[RPT], kout[RPT];
   uint32_t lp = 0;
-  constexpr bool UPFRONT = UPF != 0 && ALIAS && !CHECK && !RAGGED && (W == 3 || W == 4) && DIAG == 0;
+  constexpr bool UPFRONT = UPF != 0 && ALIAS && !CHECK && !RAGGED && (W == 3 || W == 4);
   if constexpr (UPFRONT) {
     C5Raw<W> ru[GROUPS], rv[GROUPS];
 #pragma unroll
@@ -337,10 +338,8 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
       }
       lp += (in_ok & out_ok & (b == cq)) ? 1u : 0u;
       // count only (no return: no wait); positions come from a second pass
-      if (DIAG != 1) {
-        atomicAdd(&cur[kin[j] >> C2_BITS], 1u);
-        atomicAdd(&cur[kout[j] >> C2_BITS], 1u);
-      }
+      atomicAdd(&cur[kin[j] >> C2_BITS], 1u);
+      atomicAdd(&cur[kout[j] >> C2_BITS], 1u);
     }
     asm volatile("" : "+v"(lp));        // keep the self-loop sum here (no raw ids kept alive)
     __builtin_amdgcn_sched_barrier(0);  // bound what the scheduler keeps in flight
@@ -349,18 +348,6 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   // addresses alive across the scan (extra VGPRs → spills)
 #pragma unroll
   for (int j = 0; j < RPT; ++j) asm volatile("" : "+v"(kin[j]), "+v"(kout[j]));
-  if (DIAG == 1) {
-    uint4 *dst = (uint4 *)(part + t * c.rstride);
-#pragma unroll
-    for (int q = 0; q < RPT / 4; ++q)
-      dst[q * C5_BLOCK + threadIdx.x] =
-          make_uint4((kin[4 * q] & 0xFFFF) | kout[4 * q] << 16, (kin[4 * q + 1] & 0xFFFF) | kout[4 * q + 1] << 16,
-                     (kin[4 * q + 2] & 0xFFFF) | kout[4 * q + 2] << 16,
-                     (kin[4 * q + 3] & 0xFFFF) | kout[4 * q + 3] << 16);
-    if (threadIdx.x < (unsigned)nr) meta[t * nr + threadIdx.x] = 0;
-    c5_tile_sum(lp, lds_scan, tile_loops + t);
-    return;
-  }
   __syncthreads();
   // exclusive scan of the 8-padded run sizes (the dummy run nr last)
   uint32_t cs[RUNS_PT], sum = 0;
@@ -388,7 +375,6 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   // a run is free — P3 only counts)
 #pragma unroll
   for (int j = 0; j < RPT; ++j) {
-    if (DIAG == 2) break;
     stage[atomicAdd(&cur[kin[j] >> C2_BITS], 1u)] = (uint16_t)kin[j];
     stage[atomicAdd(&cur[kout[j] >> C2_BITS], 1u)] = (uint16_t)kout[j];
     if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
@@ -478,8 +464,6 @@ struct C3Unit {
 // node-partitioned graph) still needs 2 full waves of P3 units on 256 CUs, so every run is cut into S tile ranges, each counted into its own
 // slice of the histograms with plain stores; the dot sums the slices.
 static int c5_slices(int nr) {
-  const char *e = getenv("CAPF_SLICES");  // tuning
-  if (e && atoi(e) > 0) return std::min(8, atoi(e));
   // one unit per CU: G = 8 rank (64 runs) S = 4 → 0.250 ms/rank vs S = 8 0.271, S = 2 0.300
   return std::min(8, std::max(1, (256 + nr - 1) / nr));
 }
@@ -636,178 +620,6 @@ __global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(unsigned long long *run_
 // other workgroup's run-total adds have landed) builds the work list, reusing
 // its transpose tile buffer as the LPT estimate array — one kernel boundary
 // (≈ 10 µs of drain and ramp at s24) fewer than T then k_c3_units.
-constexpr int C3_TU_RPT = 8;  // runs per thread of the last workgroup: nr ≤ 2048
-__global__ __launch_bounds__(256) void k_c3_transpose_units(const uint32_t *meta, uint32_t *meta_t,
-                                                             int64_t ntiles, int nr,
-                                                             unsigned long long *run_total, int64_t tt,
-                                                             const uint32_t *tile_loops,
-                                                             unsigned long long *loops, C3Sides sd, int S,
-                                                             C3UnitsOut uo) {
-  __shared__ uint32_t tilebuf[C3_TT][33];
-  __shared__ int last;
-  // every thread's run-total adds have returned (performed at the device-scope
-  // coherence point, where the last workgroup's atomic reads see them) before
-  // this workgroup's `done` add
-  c3_transpose_body(tilebuf, meta, meta_t, ntiles, nr, run_total, tt, nullptr, tile_loops, loops, true);
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(uo.done, 1u) == gridDim.x * gridDim.y - 1;
-  __syncthreads();
-  if (!last) return;
-  c3_units_body<C3_TU_RPT>(run_total, nr, sd, S, uo, &tilebuf[0][0], true);
-}
-
-// Clears every slice of the buckets of split runs (their units flush with
-// atomic adds).
-__global__ __launch_bounds__(256) void k_c3_zero(const int32_t *split, int nb, uint32_t *h_in,
-                                                  uint32_t *h_out, int64_t slice_stride) {
-  const int r = blockIdx.y;
-  if (!split[r]) return;
-  uint4 *p = (uint4 *)((r >= nb ? h_out : h_in) + blockIdx.z * slice_stride + (int64_t)(r % nb) * C2_BW);
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < C2_BW / 4; i += gridDim.x * 256)
-    p[i] = make_uint4(0, 0, 0, 0);
-}
-
-// Σ in·out folded into P3's epilogue (the fused 2-hop count, one slice,
-// packed-pair buckets): the unit whose `bdone` add completes bucket b (all
-// units of runs b and nb + b flushed) sums in[b]·out[b] over the bucket's
-// 2^16 bins plus the bucket's hand-off terms, then every P3 workgroup counts
-// itself done and the last one writes fin = Σ − self-loops — no dot kernel
-// and one kernel boundary fewer.  The flush stores of a unit reach the
-// partner's XCD through the release fence before its `bdone` add (agent
-// scope: L2 write-back), the finisher's acquire fence after it.
-struct C3Fin {
-  const int32_t *rnu;         // units per run (k_c3_units)
-  unsigned int *bdone;        // per bucket: its units that have flushed (zeroed per query)
-  unsigned int *done;         // P3 workgroups finished (zeroed per query)
-  unsigned long long *acc3;   // [Σ in·out, self-loops]
-  int64_t *fin;               // null: the dot kernel runs after P3
-  const int32_t *split;       // per run: 0 = packed pairs, else one uint32 per bin
-  const uint2 *log;           // hand-off log (side bin, side | count << 1)
-  const uint32_t *logn;
-  uint32_t cap;
-  int64_t hl;                 // bins per side (slice stride)
-};
-
-// counter of side `side` at side bin `bin` as stored (packed pair or uint32)
-__device__ inline uint32_t c3_stored(const uint32_t *h, const C3Fin &fz, int nb, int side, int64_t bin) {
-  const int64_t b = bin >> 16, k = bin & 0xFFFF;
-  if (fz.split[side * nb + b]) return h[bin];
-  return (h[b * C2_BW + (k & (C2_WORDS - 1))] >> ((k >> 15) * 16)) & 0xFFFFu;
-}
-
-__device__ inline unsigned long long c3_bucket_dot(const uint32_t *h_in, const uint32_t *h_out, const C3Fin &fz,
-                                                   int nb, int b, uint32_t *lds_words) {
-  unsigned long long s = 0;
-  const bool si = fz.split[b] != 0, so = fz.split[nb + b] != 0;
-  const uint32_t *a = h_in + (int64_t)b * C2_BW, *c = h_out + (int64_t)b * C2_BW;
-  // 8 quads per lane (2^15 words / 1024 lanes / 4): loads in four batches of 2
-  // quads × both sides, in flight together before the first use (this runs at
-  // the tail of a unit: latency, not bandwidth, is its cost; larger batches
-  // spill next to P3's 127-VGPR main loop)
-  static_assert(C2_WORDS / 4 == 8 * C5_BLOCK, "bucket dot: 8 quads per lane");
-#pragma unroll 1
-  for (int half = 0; half < 4; ++half) {
-    uint4 a0[2], c0[2], a1[2], c1[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int q = (half * 2 + k) * C5_BLOCK + threadIdx.x;
-      a0[k] = ((const uint4 *)a)[q];
-      c0[k] = ((const uint4 *)c)[q];
-      a1[k] = ((const uint4 *)(a + (si ? C2_WORDS : 0)))[q];  // (packed: the same line again)
-      c1[k] = ((const uint4 *)(c + (so ? C2_WORDS : 0)))[q];
-    }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const uint32_t al[4] = {a0[k].x, a0[k].y, a0[k].z, a0[k].w}, ah[4] = {a1[k].x, a1[k].y, a1[k].z, a1[k].w};
-      const uint32_t cl[4] = {c0[k].x, c0[k].y, c0[k].z, c0[k].w}, ch[4] = {c1[k].x, c1[k].y, c1[k].z, c1[k].w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const uint32_t xl = si ? al[e] : al[e] & 0xFFFF, xh = si ? ah[e] : al[e] >> 16;
-        const uint32_t yl = so ? cl[e] : cl[e] & 0xFFFF, yh = so ? ch[e] : cl[e] >> 16;
-        s += (unsigned long long)xl * yl + (unsigned long long)xh * yh;
-      }
-    }
-  }
-  // hand-off terms of this bucket: Σ_in Δ·(y + Y) + Σ_out Δ·x, Y = the bin's
-  // out-side hand-offs (an LDS open-addressing map over the bucket's few)
-  const uint32_t ne = min(*fz.logn, fz.cap);
-  if (ne > 0) {
-    constexpr uint32_t MAPN = 2048;
-    uint32_t *mk = lds_words;
-    unsigned long long *mv = (unsigned long long *)(lds_words + MAPN);
-    __shared__ int map_full;
-    for (uint32_t i = threadIdx.x; i < MAPN; i += C5_BLOCK) {
-      mk[i] = 0xFFFFFFFFu;
-      mv[i] = 0;
-    }
-    if (threadIdx.x == 0) map_full = 0;
-    __syncthreads();
-    for (uint32_t e = threadIdx.x; e < ne; e += C5_BLOCK) {
-      const uint2 y = fz.log[e];
-      const int64_t bin = (int64_t)y.x % fz.hl;
-      if (!(y.y & 1u) || (bin >> 16) != b) continue;
-      const uint32_t kb = (uint32_t)(bin & 0xFFFF);
-      uint32_t h = (kb * 0x9E3779B1u) & (MAPN - 1), probes = 0;
-      for (;;) {
-        const uint32_t prev = atomicCAS(&mk[h], 0xFFFFFFFFu, kb);
-        if (prev == 0xFFFFFFFFu || prev == kb) {
-          atomicAdd(&mv[h], (unsigned long long)(y.y >> 1));
-          break;
-        }
-        h = (h + 1) & (MAPN - 1);
-        if (++probes > MAPN / 2) {
-          map_full = 1;
-          break;
-        }
-      }
-    }
-    __syncthreads();
-    for (uint32_t e = threadIdx.x; e < ne; e += C5_BLOCK) {
-      const uint2 x = fz.log[e];
-      const int64_t bin = (int64_t)x.x % fz.hl;
-      if ((bin >> 16) != b) continue;
-      const unsigned long long d = x.y >> 1;
-      if (x.y & 1u) {
-        s += d * c3_stored(h_in, fz, nb, 0, bin);
-      } else {
-        const uint32_t kb = (uint32_t)(bin & 0xFFFF);
-        unsigned long long Y = 0;
-        if (!map_full) {
-          uint32_t h = (kb * 0x9E3779B1u) & (MAPN - 1);
-          for (uint32_t k = 0; k < MAPN; ++k) {
-            const uint32_t c = mk[h];
-            if (c == kb) {
-              Y = mv[h];
-              break;
-            }
-            if (c == 0xFFFFFFFFu) break;
-            h = (h + 1) & (MAPN - 1);
-          }
-        } else {  // (pathological) scan the log
-          for (uint32_t f = 0; f < ne; ++f) {
-            const uint2 y = fz.log[f];
-            if ((y.y & 1u) && (int64_t)y.x % fz.hl == bin) Y += y.y >> 1;
-          }
-        }
-        s += d * (c3_stored(h_out, fz, nb, 1, bin) + Y);
-      }
-    }
-  }
-  return s;
-}
-
-// thread 0 of every P3 workgroup, once: the last one writes fin.
-__device__ inline void c3_fin_arrive(const C3Fin &fz) {
-  __threadfence();
-  if (atomicAdd(fz.done, 1u) == gridDim.x - 1) {
-    __threadfence();
-    const unsigned long long a0 = atomicAdd(fz.acc3, 0ull), a1 = atomicAdd(fz.acc3 + 1, 0ull);
-    // fin may be pinned host memory: a system-scope store
-    __hip_atomic_store(fz.fin, (int64_t)(a0 - a1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __threadfence_system();
-  }
-}
-
 // XCD-aware unit placement.  Workgroup i runs on XCD i mod 8, and P3 holds
 // one workgroup per CU (128 KiB LDS), 32 per XCD.  Runs r and r+1 are
 // adjacent in every tile's region, so their segments share 128-B lines:
@@ -827,7 +639,6 @@ struct C3Ovf {
   uint2 *log;  // (histogram index, side | count << 1): hand-offs (count 2^15) and hot-key totals
   uint32_t *n;
   uint32_t cap;
-  unsigned long long *trace;  // diagnostics (CAPF_P3_TRACE): 4 words per unit, else null
 };
 
 // Slow path of an overflowing add (rare: a bin reached 2^15 within the unit).
@@ -855,64 +666,6 @@ __device__ inline int64_t uniform64(int64_t v) {
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
-__device__ inline uint32_t bal_start(int w, uint32_t W, int P) {
-  return (uint32_t)(((uint64_t)w * W) / (uint64_t)P);
-}
-
-// The workgroup whose key range holds offset x < W.
-__device__ inline int bal_wg_of(uint32_t x, uint32_t W, int P) {
-  int w = (int)min<uint64_t>(((uint64_t)x * P) / max(W, 1u), (uint64_t)(P - 1));
-  while (w + 1 < P && bal_start(w + 1, W, P) <= x) ++w;
-  while (w > 0 && bal_start(w, W, P) > x) --w;
-  return w;
-}
-
-// The sub-bucket holding key offset x: the last j < nsb with pre[j] ≤ x.
-__device__ inline int bal_sb_of(const uint32_t *pre, int nsb, uint32_t x) {
-  int lo = 0, hi = nsb;
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (pre[mid] <= x) lo = mid;
-    else hi = mid;
-  }
-  return lo;
-}
-
-// Split tile of a run for key offset x (one wave): tt·(smallest block k with
-// Σ_{k' < k} bs[k'] ≥ x), at most ntiles; for x = 0 the run's first block
-// holding keys (a run's keys lie in its side's tiles only: an out-run's part 0
-// must not start at tile 0, or its waves' even tile split would hand most
-// waves the in-copy tiles, empty for this run).
-__device__ inline int64_t bal_tile(const uint32_t *bs, int nblk, int tt, int64_t ntiles, uint32_t x) {
-  const int lane = lane_id();
-  uint32_t carry = 0;
-  for (int c = 0; c < nblk; c += WAVE) {
-    const int k = c + lane;
-    const uint32_t v = k < nblk ? bs[k] : 0u;
-    const uint32_t inc = wave_inclusive_scan(v);
-    const unsigned long long hit = __ballot(k < nblk && (x == 0 ? v > 0 : carry + inc - v >= x));
-    if (hit) return min<int64_t>((int64_t)(c + __builtin_ctzll(hit)) * tt, ntiles);
-    carry += (uint32_t)__shfl(inc, WAVE - 1, WAVE);
-  }
-  return ntiles;
-}
-
-// Apportioned P3 units of a node-partitioned rank (CAPF_SHARD_SB=3): run r
-// (64 Ki-node bucket side) gets k_r = max(1, round(P·T_r / W)) units, each
-// 1/k_r of its keys — split points rounded to blocks of tt tiles from the
-// transpose's per-(run, block) counts — so every unit counts ≈ W/P keys
-// whatever the skew (a hub's run gets more units), and unit (r, i) writes
-// slice base_r + i.  Every P3 workgroup derives the table from the run totals;
-// block 0 also stores it (base, k per run) for the dot.
-constexpr int C5APP_MAXR = 520;  // runs of a rank's P1 (C5S_MAXR)
-
-struct C5Sched {
-  const unsigned long long *run_total;  // [nr] keys (null: the even split of S slices)
-  const uint32_t *bsum;                 // [nr][nblk]
-  int nblk, tt, P;
-  int32_t *table;                       // out: base[nr], k[nr]
-};
-
 // P3.  The wave takes 64 tiles of its unit at a time and treats their
 // segments (8-key padded, 16-B aligned pieces) as ONE sequence: lane l of
 // step s handles piece s·64·PPS + l (+ 64·j), found by a 6-step binary search
@@ -930,50 +683,15 @@ struct C5Sched {
 // built, piece buffers ping-pong (no register copies → no early vmcnt wait).
 //
 // What bounds it (s24, measured): 0.49 ms; loads + search alone 0.29 ms; with
-// the keys spread so no two lanes of an atomic share a word (DIAG 2) 0.30 ms.
+// the keys spread so no two lanes of an atomic share a word 0.30 ms.
 // R-MAT's skew puts ~2.4 lanes of a typical 64-lane ds_add on one word
 // (tools: simulated per run), and same-word lanes serialise in the LDS atomic
 // unit.  Voting out lane 0's key, half-wave atomics and non-returning atomics
 // were measured and do not help (the duplicates are spread over many
-// moderately hot keys).
-// The 8 packed uint16 keys of a piece rotated left by r (0..7) elements:
-// element e of the result is element (e + r) mod 8 of the piece.
-__device__ inline void c5_rotate8(uint32_t (&a)[4], uint32_t r) {
-  uint32_t b0 = (r & 4) ? a[2] : a[0], b1 = (r & 4) ? a[3] : a[1];
-  uint32_t b2 = (r & 4) ? a[0] : a[2], b3 = (r & 4) ? a[1] : a[3];
-  uint32_t c0 = (r & 2) ? b1 : b0, c1 = (r & 2) ? b2 : b1;
-  uint32_t c2 = (r & 2) ? b3 : b2, c3 = (r & 2) ? b0 : b3;
-  a[0] = (r & 1) ? __builtin_amdgcn_alignbit(c1, c0, 16) : c0;
-  a[1] = (r & 1) ? __builtin_amdgcn_alignbit(c2, c1, 16) : c1;
-  a[2] = (r & 1) ? __builtin_amdgcn_alignbit(c3, c2, 16) : c2;
-  a[3] = (r & 1) ? __builtin_amdgcn_alignbit(c0, c3, 16) : c3;
-}
-
-// Keys of a (rotated) piece and their dedup: inc[e] = multiplicity of key[e]
-// among slots e..7 if slot e holds its first occurrence, else 0.
-__device__ inline void c5_dedup8(const uint32_t (&a)[4], uint32_t (&key)[8], uint32_t (&inc)[8]) {
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    key[e] = (e & 1) ? a[e >> 1] >> 16 : a[e >> 1] & 0xFFFF;
-    inc[e] = 1;
-  }
-#pragma unroll
-  for (int e = 0; e < 8; ++e)
-#pragma unroll
-    for (int f = e + 1; f < 8; ++f) {
-      const bool eq = key[e] == key[f];
-      inc[e] += eq && inc[e] != 0 ? 1u : 0u;  // (a later duplicate of a non-first slot adds nothing)
-      inc[f] = eq ? 0u : inc[f];
-    }
-}
-
-// ROT (CAPF_P3_ROT): every piece's 8 keys are rotated by lane mod 8 elements
-// and fully deduplicated (28 compares: each distinct key of the piece added
-// once, with its multiplicity).  Slot e of lane l then holds the piece's key
-// (e + l) mod 8, so a hub key that fills 35 % of its run (R-MAT s24) no longer
-// lands in the same slot — the same ds_add — in most lanes: its ~22 same-word
-// lanes per instruction drop to ~8, spread over the 8 instructions.
-template <int PPS, int DIAG = 0, int DEPTH = 1, int HOT = 0, int ROT = 0>
+// moderately hot keys); so were a per-wave hot-key register, rotating and
+// fully deduplicating each piece's 8 keys, and a third piece buffer depth vs two
+// (no gain at s24).
+template <int PPS>
 __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
                                                             const int32_t *nunits,
                                                             const uint16_t *part,
@@ -981,61 +699,12 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
                                                             int nb, int64_t rstride, uint32_t *h_in,
                                                             uint32_t *h_out, int64_t slice_stride,
                                                             C3Ovf ovf, const int32_t *order,
-                                                            C3Sides sd, int S, int64_t mstride,
-                                                            C5Sched sch, C3Fin fz) {
+                                                            C3Sides sd, int S, int64_t mstride) {
   // units == null: the static work list of a node-partitioned rank — unit
-  // (run, k) counts tile range k of S of the run's side into slice k, or
-  // (sch.run_total) the apportioned units: (run, i) into slice base_r + i
-  __shared__ int32_t sbase[C5APP_MAXR + 1], sk[C5APP_MAXR];
-  __shared__ uint32_t lds_sc[17];
-  __shared__ int64_t sbnd[2];
-  int nu = units ? *nunits : 2 * sd.nb * S;
-  const int nrr = 2 * sd.nb;
-  if (sch.run_total) {
-    // k_r ≈ P·T_r / W with Σ k_r = P exactly (largest remainder; every
-    // non-empty run ≥ 1): one unit per CU, no second round of units
-    __shared__ unsigned long long rem[C5APP_MAXR];
-    __shared__ unsigned long long lds_w[17];
-    const int r = threadIdx.x;
-    unsigned long long T = r < nrr ? sch.run_total[r] : 0ull;  // one coalesced load
-    unsigned long long W;
-    block_exclusive_scan(T, lds_w, W);
-    W = max(W, 1ull);
-    int32_t k = 0;
-    if (r < nrr) {
-      const unsigned long long e = (unsigned long long)sch.P * T;
-      k = (int32_t)(e / W);
-      rem[r] = k == 0 && T > 0 ? ~0ull : e % W;  // forced units first
-    }
-    __syncthreads();
-    uint32_t fl;
-    block_exclusive_scan((uint32_t)k, lds_sc, fl);
-    const int deficit = sch.P - (int)fl;
-    if (r < nrr && T > 0) {
-      int ahead = 0;  // runs with a larger remainder (ties: lower index first)
-      for (int q = 0; q < nrr; ++q) ahead += rem[q] > rem[r] || (rem[q] == rem[r] && q < r);
-      if (ahead < deficit || k == 0) ++k;
-    }
-    uint32_t tot;
-    const uint32_t ex = block_exclusive_scan((uint32_t)k, lds_sc, tot);
-    if (r < nrr) {
-      sbase[r] = (int32_t)ex;
-      sk[r] = k;
-      if (blockIdx.x == 0) {
-        sch.table[r] = (int32_t)ex;
-        sch.table[nrr + r] = k;
-      }
-    }
-    if (r == 0) sbase[nrr] = (int32_t)tot;
-    __syncthreads();
-    nu = sbase[nrr];
-  }
+  // (run, k) counts tile range k of S of the run's side into slice k
+  const int nu = units ? *nunits : 2 * sd.nb * S;
   const int ui = (int)blockIdx.x >= nu && order ? nu : order ? order[blockIdx.x] : c3_unit_of((int)blockIdx.x);
-  if (ui >= nu) {
-    if (fz.fin && threadIdx.x == 0) c3_fin_arrive(fz);
-    return;
-  }
-  const unsigned long long t_start = ovf.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  if (ui >= nu) return;
   extern __shared__ __attribute__((aligned(16))) uint32_t words[];
   constexpr int NW = C5_BLOCK / WAVE;
   constexpr uint32_t STEP = WAVE * PPS;
@@ -1044,28 +713,6 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
   C3Unit u;
   if (units) {
     u = units[ui];
-  } else if (sch.run_total) {
-    // the run holding unit ui (last r with base_r ≤ ui), part i of k_r
-    int lo = 0, hi = nrr;
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (sbase[mid] <= ui) lo = mid;
-      else hi = mid;
-    }
-    const int i = ui - sbase[lo], k = sk[lo];
-    const unsigned long long T = sch.run_total[lo];
-    const int wv = threadIdx.x / WAVE;
-    if (wv < 2) {  // split tiles of the part's key range, one wave each
-      const uint32_t x = (uint32_t)(T * (unsigned long long)(i + wv) / (unsigned long long)k);
-      const int64_t t = bal_tile(sch.bsum + (int64_t)lo * sch.nblk, sch.nblk, sch.tt, ntiles, x);
-      if (lane_id() == 0) sbnd[wv] = t;
-    }
-    __syncthreads();
-    u.run = lo;
-    u.exclusive = 1;
-    u.t0 = sbnd[0];
-    u.t1 = sbnd[1];
-    u.slice = ui;  // slices are indexed by unit
   } else {
     const int k = ui % S, sdi = ui / S >= sd.nb ? 1 : 0;
     const int64_t len = sd.t1[sdi] - sd.t0[sdi];
@@ -1078,8 +725,7 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
   const uint32_t side = u.run >= nb ? 1u : 0u;
   uint32_t *hist = side ? h_out : h_in;
   const uint32_t log_base = (uint32_t)((int64_t)(u.run % nb) * C2_BW);  // packed: side bin of key 0
-  const uint32_t hist_base = sch.run_total ? (uint32_t)((int64_t)u.slice * C2_BW)
-                                           : (uint32_t)(u.slice * slice_stride + (int64_t)(u.run % nb) * C2_BW);
+  const uint32_t hist_base = (uint32_t)(u.slice * slice_stride + (int64_t)(u.run % nb) * C2_BW);
   for (int i = threadIdx.x; i < C2_WORDS + C5_CORR; i += C5_BLOCK) words[i] = 0;
   // A split run's units flush with atomic adds into bins that must start at
   // zero: the first unit of (run, slice) to start sets its claim bit and clears
@@ -1111,13 +757,6 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
   const uint32_t rs8 = (uint32_t)(rstride / 8);
   uint32_t padc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint32_t dead = 0;
-  // HOT: the wave's hot key H (wave-uniform; none = 0xFFFFFFFF).  Once a live
-  // piece shows its first key ≥ 3 times, that key (≥ C5_CORR: never a pad or
-  // dead-lane key) is H; its later copies are counted in a register (nh) and
-  // sit every atomic out, and the wave's total goes through the hand-off log
-  // (k_c3_overflow) — a run's top hub (14 % of run 0's keys at s24) otherwise
-  // puts ~9 lanes of every ds_add on one word.
-  uint32_t H = 0xFFFFFFFFu, nh = 0;
   const uint4 dead_keys = make_uint4(lane | lane << 16, lane | lane << 16, lane | lane << 16,
                                      lane | lane << 16);
   // batch setup: table of tiles [tb, tb + 64) into tab2[buf]; returns the piece total
@@ -1164,47 +803,19 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
     uint32_t old[PPS][8];
     uint32_t n0[PPS], n1[PPS];
     bool dup[PPS][8];
-    bool live0 = false;
-    uint32_t k00 = 0;
 #pragma unroll
     for (int j = 0; j < PPS; ++j) {
       const bool live = p0 + j * WAVE + lane < total;
       dead += live ? 0u : 1u;
       const uint32_t wd[4] = {live ? v[j].x : dead_keys.x, live ? v[j].y : dead_keys.y,
                               live ? v[j].z : dead_keys.z, live ? v[j].w : dead_keys.w};
-      if (ROT && DIAG == 0) {
-        uint32_t a[4] = {wd[0], wd[1], wd[2], wd[3]}, key[8], inc[8];
-        c5_rotate8(a, (uint32_t)lane & 7u);
-        c5_dedup8(a, key, inc);
-        // the hand-off check inline (olds live for this piece only: no
-        // per-step old[] array, fewer VGPRs than the slot-0/1 merge)
-        uint32_t o8[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const uint32_t add = inc[e] << ((key[e] >> 15) << 4);
-          o8[e] = inc[e] ? atomicAdd(&words[key[e] & (C2_WORDS - 1)], add) : 0u;
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const uint32_t sh = (key[e] >> 15) << 4;
-          const uint32_t nw = o8[e] + (inc[e] << sh);
-          if (inc[e] && (nw & ~o8[e] & (0x8000u << sh)))  // this add lifted its half to 2^15
-            c3_handoff(&words[key[e] & (C2_WORDS - 1)], 1u << sh, (sd.packed ? log_base : hist_base) + key[e],
-                       side, ovf);
-        }
-        continue;
-      }
-      if (DIAG == 0) {
+      {
         // hub keys: the keys of the piece equal to its first (second) key
         // are added once, as a count ≤ 8, by slot 0 (1) (R-MAT skew puts a hub's key in
         // many slots of its run's pieces, and same-word lanes of one ds_add
         // serialise); the other slots add 1 each, lanes holding a duplicate
         // sit that atomic out
         const uint32_t k0 = wd[0] & 0xFFFF, k1 = wd[0] >> 16;
-        if (j == 0) {
-          live0 = live;
-          k00 = k0;
-        }
         dup[j][0] = false;
         dup[j][1] = k1 == k0;
         n0[j] = dup[j][1] ? 2u : 1u;
@@ -1213,11 +824,9 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
         for (int e = 2; e < 8; ++e) {
           const uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
           const bool d0 = key == k0, d1 = !d0 && key == k1;  // k1 == k0 ⇒ d0 already
-          const bool d2 = HOT && !d0 && !d1 && key == H;     // H ≥ C5_CORR: never dead/pad
-          dup[j][e] = d0 || d1 || d2;
+          dup[j][e] = d0 || d1;
           n0[j] += d0 ? 1u : 0u;
           n1[j] += d1 ? 1u : 0u;
-          if (HOT) nh += d2 ? 1u : 0u;
         }
         const uint32_t inc0 = n0[j] << ((k0 >> 15) << 4);
         old[j][0] = atomicAdd(&words[k0 & (C2_WORDS - 1)], inc0);
@@ -1234,22 +843,9 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
           if (!dup[j][e]) old[j][e] = atomicAdd(&words[key & (C2_WORDS - 1)], unit);
           acc |= old[j][e] + unit;
         }
-        continue;
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
-        if (DIAG == 2) key = (key + 131u * lane + 977u * e) & 0xFFFF;  // no same-address lanes
-        const uint32_t unit = (key >> 15) * 0xFFFFu + 1u;  // 1 (low half) or 2^16 (high)
-        old[j][e] = atomicAdd(&words[key & (C2_WORDS - 1)], unit);
-        acc |= old[j][e] + unit;
       }
     }
-    if (HOT && DIAG == 0 && H == 0xFFFFFFFFu) {
-      const unsigned long long bm = __ballot(live0 && n0[0] >= 3u && k00 >= (uint32_t)C5_CORR);
-      if (bm) H = (uint32_t)__builtin_amdgcn_readlane((int)k00, __builtin_ctzll(bm));
-    }
-    if (DIAG == 0 && (acc & 0x80008000u)) {
+    if (acc & 0x80008000u) {
       // rare: some half reached 2^15 — find the add(s) that crossed it (the
       // half before the add was < 2^15 and the add took it to ≥ 2^15)
 #pragma unroll
@@ -1257,7 +853,6 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
         const bool live = p0 + j * WAVE + lane < total;
         const uint32_t wd[4] = {live ? v[j].x : dead_keys.x, live ? v[j].y : dead_keys.y,
                                 live ? v[j].z : dead_keys.z, live ? v[j].w : dead_keys.w};
-        if (ROT) continue;  // checked inline
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
@@ -1299,29 +894,7 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
         } while (total == 0);
         return true;
       };
-      if (DEPTH == 1) {
-        // ping-pong piece buffers (unrolled by 2: no register copies, so the
-        // wait before counting A covers A's loads only, not B's)
-        uint4 va[PPS], vb[PPS];
-        fetch(buf, p0, total, va);
-        for (;;) {
-          uint32_t cp0 = p0, ctot = total;
-          if (!advance()) {
-            count(va, cp0, ctot);
-            break;
-          }
-          fetch(buf, p0, total, vb);
-          count(va, cp0, ctot);
-          cp0 = p0;
-          ctot = total;
-          if (!advance()) {
-            count(vb, cp0, ctot);
-            break;
-          }
-          fetch(buf, p0, total, va);
-          count(vb, cp0, ctot);
-        }
-      } else {
+      {
         // three rotating piece buffers: the loads of steps i+1 and i+2 are in
         // flight while step i counts (unrolled by 3, no register copies)
         uint4 va[PPS], vb[PPS], vc[PPS];
@@ -1373,14 +946,6 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
   for (int e = 1; e < 8; ++e)
     if (padc[e]) atomicAdd(&corr[pcls + e], padc[e]);
   if (dead) atomicAdd(&corr[lane], 8 * dead);
-  if (HOT && H != 0xFFFFFFFFu) {
-    const unsigned long long th = wave_reduce_sum((unsigned long long)nh);
-    if (lane == 0 && th) {
-      const uint32_t k = atomicAdd(ovf.n, 1u);
-      if (k < ovf.cap)
-        ovf.log[k] = make_uint2((sd.packed ? log_base : hist_base) + H, side | ((uint32_t)th << 1));
-    }
-  }
   if (zsplit && threadIdx.x == 0)
     while (!(__hip_atomic_load(&sd.claim[u.run], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) & (512 << u.slice)))
       __builtin_amdgcn_s_sleep(4);
@@ -1406,35 +971,6 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
     }
   }
 
-  if (fz.fin) {
-    __shared__ int zlast;
-    __syncthreads();  // every lane's flush stores are in L2 ...
-    const int b = u.run % nb;
-    if (threadIdx.x == 0) {
-      __threadfence();  // ... and written back (one agent-scope release per workgroup)
-      const unsigned tot = (unsigned)(fz.rnu[b] + fz.rnu[nb + b]);
-      zlast = atomicAdd(&fz.bdone[b], 1u) == tot - 1;
-      if (zlast) __threadfence();  // acquire: the other units' flushes
-    }
-    __syncthreads();
-    if (zlast) {
-      __shared__ unsigned long long lds_dot[17];
-      const unsigned long long t = block_reduce_sum(c3_bucket_dot(h_in, h_out, fz, nb, b, words), lds_dot);
-      if (threadIdx.x == 0 && t) atomicAdd(fz.acc3, t);
-    }
-    if (threadIdx.x == 0) c3_fin_arrive(fz);
-  }
-  if (ovf.trace) {  // diagnostics: this unit's span, where it ran
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (3 << 11));           // HW_REG_XCC_ID[3:0]
-      const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));  // HW_REG_HW_ID
-      ovf.trace[4 * ui] = t_start;
-      ovf.trace[4 * ui + 1] = __builtin_amdgcn_s_memrealtime();
-      ovf.trace[4 * ui + 2] = ((unsigned long long)xcc << 32) | hw;
-      ovf.trace[4 * ui + 3] = ((unsigned long long)u.run << 32) | (uint32_t)(u.t1 - u.t0);
-    }
-  }
 }
 
 // Adds the handed-off 2^15 units (after every P3 store has landed).
@@ -1451,19 +987,9 @@ static void launch_c5(Session *s, const C5Cols<W> &c, uint16_t *part, uint32_t *
                       uint32_t *tile_loops, uint32_t *zbuf, int64_t zwords, unsigned long long *zacc) {
   const int64_t nfull = c.n / SH::TILE;
   if (nfull > 0) {
-    const char *dg = getenv("CAPF_P1_DIAG");  // diagnostics only: wrong counts
-    const int diag = dg ? atoi(dg) : 0;
-    // upfront loads, non-temporal (the default, 2; s24 P1 0.516 vs 0.521 ms with
-    // default-policy loads, 1), FOR24 fields used raw when the bases are lo (D0:
-    // 0.512 vs 0.517 ms); CAPF_P1_UPFRONT=0 (tuning): one group ahead
-    static const int upf = getenv("CAPF_P1_UPFRONT") ? atoi(getenv("CAPF_P1_UPFRONT")) : 2;
-    auto kern = diag == 1   ? k_c5_partition<W, ALIAS, CHECK, false, SH, 1>
-                : diag == 2 ? k_c5_partition<W, ALIAS, CHECK, false, SH, 2>
-                : upf >= 2 && c.bu1 == c.lo && c.bv1 == c.lo && W == 3 && !SH::WIDE
-                            ? k_c5_partition<W, ALIAS, CHECK, false, SH, 0, 3>
-                : upf == 2  ? k_c5_partition<W, ALIAS, CHECK, false, SH, 0, 2>
-                : upf       ? k_c5_partition<W, ALIAS, CHECK, false, SH, 0, 1>
-                            : k_c5_partition<W, ALIAS, CHECK, false, SH, 0>;
+    auto kern = c.bu1 == c.lo && c.bv1 == c.lo && W == 3 && !SH::WIDE
+                    ? k_c5_partition<W, ALIAS, CHECK, false, SH, 3>
+                    : k_c5_partition<W, ALIAS, CHECK, false, SH, 2>;
     hipLaunchKernelGGL(kern, dim3((unsigned)nfull), dim3(C5_BLOCK), 0, s->stream, c, part, meta,
                        tile_loops, (int64_t)0, zbuf, zwords, zacc);
     KERNEL_CHECK();
@@ -1503,30 +1029,21 @@ static int64_t c5_post_zero_words(int nr, uint32_t ovf_cap) {
 static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, const C3Sides &sd,
                     int64_t ntiles, int64_t rstride, int64_t nkeys, int S, uint32_t *h_in,
                     uint32_t *h_out, int64_t slice_stride, bool static_units = false,
-                    int32_t *apportion_table = nullptr, C3Ovf *packed_ovf = nullptr,
-                    BufPtr *keep = nullptr, const C3Post *post = nullptr, BufPtr acc_pre = BufPtr()) {
+                    C3Ovf *packed_ovf = nullptr, BufPtr *keep = nullptr, const C3Post *post = nullptr,
+                    BufPtr acc_pre = BufPtr()) {
   const int nr = 2 * sd.nb;
-  const bool app = apportion_table != nullptr;  // apportioned units (C5Sched), slices by unit
   static bool attr_set = false;
   if (!attr_set) {
-    for (const void *f : {(const void *)k_c5_gather<C5_PPS, 0>, (const void *)k_c5_gather<C5_PPS, 2>,
-                          (const void *)k_c5_gather<C5_PPS, 3>, (const void *)k_c5_gather<C5_PPS, 0, 2>,
-                          (const void *)k_c5_gather<C5_PPS, 0, 1, 1>, (const void *)k_c5_gather<C5_PPS, 0, 2, 1>,
-                          (const void *)k_c5_gather<C5_PPS, 0, 2, 0, 1>, (const void *)k_c5_gather<C5_PPS, 0, 1, 0, 1>})
-      HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, C5_GATHER_LDS));
+    HIP_CHECK(hipFuncSetAttribute((const void *)k_c5_gather<C5_PPS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  C5_GATHER_LDS));
     attr_set = true;
   }
-  // runs × slices + hub splits (≤ 2 per run beyond the slices), whole XCD waves
-  // Σ_runs max(S, ⌈cnt/target⌉) ≤ S·nr + nr + total/target, target ≥ split/16 × mean
   int max_units = 0;
   uint32_t ovf_cap = 0;
   const int64_t acc_bytes = c5_post_acc_bytes(nr, S, sd.split_x16, nkeys, &max_units, &ovf_cap);
-  // CAPF_META_T=0 (tuning): P3 reads P1's tile-major meta in place (the units
-  // of 32 consecutive runs on one XCD share its lines in L2) and the transpose
-  // kernel only sums the run totals — s24: transpose 31 → 24 µs, P3 +7..20 µs
-  const char *mt = getenv("CAPF_META_T");
-  const bool transpose = !(mt && atoi(mt) == 0);
-  BufPtr meta_t = transpose ? s->alloc(4 * nr * ntiles) : BufPtr();
+  // P3 reads run-major meta (transposed here); reading P1's tile-major meta in
+  // place saved 7 µs of transpose and cost P3 7..20 µs at s24 (measured, removed)
+  BufPtr meta_t = s->alloc(4 * nr * ntiles);
   // transpose blocks: tiles per block tt, fewer when there are few runs (≥ ~1024 blocks)
   int64_t tt = C3_TT;
   while (tt > 32 && ((ntiles + tt - 1) / tt) * ((nr + 31) / 32) < 1024) tt /= 2;
@@ -1536,134 +1053,48 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   BufPtr acc = acc_pre ? acc_pre : s->alloc(acc_bytes);
   unsigned long long *run_total = (unsigned long long *)acc->p;
   int32_t *nunits = (int32_t *)(run_total + nr);  // [0] units, [1] overflow events
-  unsigned int *bdone = (unsigned int *)(nunits + 4);  // per bucket (P3's bucket-dot epilogue)
+  unsigned int *bdone = (unsigned int *)(nunits + 4);  // (reserved: keeps the layout's alignment)
   uint2 *log = (uint2 *)(bdone + nr);                    // (12·nr + 16 B in: 8-B aligned, nr even)
   int32_t *split = (int32_t *)(log + ovf_cap);
   int32_t *rnu = split + nr;
   C3Unit *units = (C3Unit *)(rnu + nr);
-  // CAPF_P3_LPT=1: largest-first unit order instead of the XCD-grouped run order
-  const char *lpt_env = getenv("CAPF_P3_LPT");
-  const bool lpt = lpt_env && atoi(lpt_env) == 1;
-  BufPtr order_buf = lpt ? s->alloc(4 * (int64_t)max_units) : BufPtr();
-  int32_t *order = lpt ? (int32_t *)order_buf->p : nullptr;
   C3Ovf ovf{};
   ovf.n = (uint32_t *)(nunits + 1);
   ovf.log = log;
   ovf.cap = ovf_cap;
-  ovf.trace = nullptr;
   // the hand-off log is folded in by the dot kernel (no overflow kernel) when
-  // the caller takes it (CAPF_P3_OVFK=1, tuning/tests: the overflow kernel)
-  const char *ok_env = getenv("CAPF_P3_OVFK");
-  const bool log_to_dot = post && post->spill && !sd.packed && !(ok_env && atoi(ok_env) == 1);
-  const char *trace_path = getenv("CAPF_P3_TRACE");  // diagnostics only
-  BufPtr trace;
-  if (trace_path) {
-    trace = s->alloc(32 * (int64_t)max_units);
-    HIP_CHECK(hipMemsetAsync(trace->p, 0, 32 * (size_t)max_units, s->stream));
-    ovf.trace = (unsigned long long *)trace->p;
-  }
+  // the caller takes it
+  const bool log_to_dot = post && post->spill && !sd.packed;
   if (!acc_pre) HIP_CHECK(hipMemsetAsync(acc->p, 0, 4 * (size_t)c5_post_zero_words(nr, ovf_cap), s->stream));
-  BufPtr bsum = app ? s->alloc(4 * (int64_t)nr * nparts) : BufPtr();
-  C5Sched sch{};
-  if (app) {
-    sch.run_total = run_total;
-    sch.bsum = (const uint32_t *)bsum->p;
-    sch.nblk = nparts;
-    sch.tt = (int)tt;
-    sch.P = s->num_cus;
-    sch.table = apportion_table;
-  }
-  const C3UnitsOut uo{units, nunits, split, order, (unsigned int *)(nunits + 2), rnu};
-  // CAPF_C3_UNITSK=0: the work list by the transpose's last workgroup (one
-  // kernel boundary fewer, but that one 256-lane workgroup's serial tail made
-  // T+U 55 µs against 35 + 6 µs + a 10 µs boundary at s24); default: k_c3_units
-  const char *uk = getenv("CAPF_C3_UNITSK");
-  const bool fuse_units = !static_units && !app && nr <= C3_TU_RPT * 256 && uk && atoi(uk) == 0;
+  // units in the XCD-grouped run order (largest-first order: measured no gain)
+  const C3UnitsOut uo{units, nunits, split, nullptr, (unsigned int *)(nunits + 2), rnu};
   {
     KernelTimer kt(s, "c3_transpose", 8.0 * nr * ntiles);
-    if (fuse_units)
-      hipLaunchKernelGGL(k_c3_transpose_units, dim3((unsigned)nparts, (nr + 31) / 32), dim3(256), 0,
-                         s->stream, meta, transpose ? (uint32_t *)meta_t->p : nullptr, ntiles, nr,
-                         run_total, tt, post ? post->tile_loops : nullptr, post ? post->acc3 + 1 : nullptr,
-                         sd, S, uo);
-    else
-      hipLaunchKernelGGL(k_c3_transpose, dim3((unsigned)nparts, (nr + 31) / 32), dim3(256), 0,
-                         s->stream, meta, transpose ? (uint32_t *)meta_t->p : nullptr, ntiles, nr,
-                         run_total, tt, app ? (uint32_t *)bsum->p : nullptr,
-                         post ? post->tile_loops : nullptr, post ? post->acc3 + 1 : nullptr);
+    hipLaunchKernelGGL(k_c3_transpose, dim3((unsigned)nparts, (nr + 31) / 32), dim3(256), 0, s->stream, meta,
+                       (uint32_t *)meta_t->p, ntiles, nr, run_total, tt, nullptr,
+                       post ? post->tile_loops : nullptr, post ? post->acc3 + 1 : nullptr);
     KERNEL_CHECK();
   }
-  const char *zk = getenv("CAPF_C3_ZEROK");
-  const bool zero_kernel = zk && atoi(zk) == 1;
-  C3Sides sdk = sd;  // as launched: split units clear their buckets unless k_c3_zero does
-  if (!static_units && !zero_kernel) sdk.claim = split;
+  C3Sides sdk = sd;  // as launched: split units clear their buckets (claim bits)
   if (!static_units) {
-    if (!fuse_units) {
-      KernelTimer kt(s, "c3_units", 8.0 * nr);
-      hipLaunchKernelGGL(k_c3_units, dim3(1), dim3(C3_UBLOCK), 0, s->stream, run_total, nr, sd, S, uo);
-      KERNEL_CHECK();
-    }
-    // split runs' bins: cleared by their first P3 unit (C3Sides::claim), or
-    // (CAPF_C3_ZEROK=1, tuning/tests) by a full grid, one block per (run, slice)
-    // column (the units kernel's single workgroup took 35 µs for it at s24)
-    if (zero_kernel) {
-      KernelTimer kz(s, "c3_zero", 0.0);
-      hipLaunchKernelGGL(k_c3_zero, dim3(4, nr, S), dim3(256), 0, s->stream, (const int32_t *)split,
-                         sd.nb, h_in, h_out, slice_stride);
-      KERNEL_CHECK();
-    }
+    sdk.claim = split;
+    // the work list in its own one-workgroup kernel (fusing it into the
+    // transpose's last workgroup made T+U 55 µs against 35 + 6 µs + a 10 µs
+    // boundary at s24)
+    KernelTimer kt(s, "c3_units", 8.0 * nr);
+    hipLaunchKernelGGL(k_c3_units, dim3(1), dim3(C3_UBLOCK), 0, s->stream, run_total, nr, sd, S, uo);
+    KERNEL_CHECK();
   }
   {
+    // (folding the dot into P3's epilogue measured 0.51 ms for P3 against
+    // 0.44 + 0.027 ms + a ~10 µs boundary: the dot kernel runs after P3)
     KernelTimer kt(s, "c5_gather", 2.0 * nkeys);
-    // CAPF_P3_DIAG=2 (diagnostics, wrong counts): keys spread so no two lanes
-    // of an atomic share a word — measures the cost of hub-key conflicts
-    const char *dg = getenv("CAPF_P3_DIAG");
-    const char *dp = getenv("CAPF_P3_DEPTH");
-    const char *hot = getenv("CAPF_P3_HOT");
-    // depth 2 (loads of steps i+1, i+2 in flight while step i counts) is the
-    // default: 0.437 vs 0.445 ms at s24; CAPF_P3_DEPTH=1 selects depth 1
-    const bool d2 = !(dp && atoi(dp) == 1), h1 = hot && atoi(hot) == 1;
-    const char *rot = getenv("CAPF_P3_ROT");  // 1: rotated, fully deduplicated pieces
-    const bool r1 = rot && atoi(rot) == 1;
-    auto kern = dg && atoi(dg) == 2 ? k_c5_gather<C5_PPS, 2>
-                : dg && atoi(dg) == 3 ? k_c5_gather<C5_PPS, 3>
-                : d2 && r1            ? k_c5_gather<C5_PPS, 0, 2, 0, 1>
-                : r1                  ? k_c5_gather<C5_PPS, 0, 1, 0, 1>
-                : d2 && h1            ? k_c5_gather<C5_PPS, 0, 2, 1>
-                : h1                  ? k_c5_gather<C5_PPS, 0, 1, 1>
-                : d2                  ? k_c5_gather<C5_PPS, 0, 2>
-                                      : k_c5_gather<C5_PPS, 0>;
-    const int grid = app            ? (s->num_cus + nr + 255) / 256 * 256
-                     : static_units ? (nr * S + 255) / 256 * 256
-                                    : max_units;
-    // CAPF_P3_DOT=1: the fused count's Σ in·out and the final count in P3's
-    // epilogue (no dot kernel, one boundary fewer); default: the dot kernel
-    // after P3 — the epilogue's per-unit tail (release fence, the finisher's
-    // 256 KiB bucket read and hand-off scan) measured 0.51 ms for P3 against
-    // 0.44 + 0.027 ms + a ~10 µs boundary
-    const char *pd = getenv("CAPF_P3_DOT");
-    C3Fin fz{};
-    if (log_to_dot && sd.pairs && S == 1 && !static_units && !app && post->spill->fin && post->acc3 &&
-        pd && atoi(pd) == 1) {
-      fz.rnu = rnu;
-      fz.bdone = bdone;
-      fz.done = (unsigned int *)(nunits + 3);
-      fz.acc3 = post->acc3;
-      fz.fin = post->spill->fin;
-      fz.split = split;
-      fz.log = ovf.log;
-      fz.logn = ovf.n;
-      fz.cap = ovf.cap;
-      fz.hl = slice_stride;
-    }
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(C5_BLOCK), C5_GATHER_LDS, s->stream,
-                       static_units ? nullptr : (const C3Unit *)units, (const int32_t *)nunits,
-                       part, transpose ? (const uint32_t *)meta_t->p : meta, ntiles, sd.nb,
-                       rstride, h_in, h_out, slice_stride, ovf,
-                       static_units ? nullptr : (const int32_t *)order, sdk, S,
-                       transpose ? (int64_t)1 : (int64_t)nr, sch, fz);
+    const int grid = static_units ? (nr * S + 255) / 256 * 256 : max_units;
+    hipLaunchKernelGGL(k_c5_gather<C5_PPS>, dim3((unsigned)grid), dim3(C5_BLOCK), C5_GATHER_LDS, s->stream,
+                       static_units ? nullptr : (const C3Unit *)units, (const int32_t *)nunits, part,
+                       (const uint32_t *)meta_t->p, ntiles, sd.nb, rstride, h_in, h_out, slice_stride, ovf,
+                       (const int32_t *)nullptr, sdk, S, (int64_t)1);
     KERNEL_CHECK();
-    if (fz.fin) post->spill->p3_dot = 1;
   }
   if (sd.packed) {  // the hand-offs are applied by k_c5_dot_packed
     *packed_ovf = ovf;
@@ -1679,15 +1110,6 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
     KernelTimer kt(s, "c3_overflow", 0.0);
     hipLaunchKernelGGL(k_c3_overflow, dim3(16), dim3(256), 0, s->stream, ovf, h_in, h_out);
     KERNEL_CHECK();
-  }
-  if (trace_path) {  // diagnostics: append (start, end, where, run|tiles) per unit
-    std::vector<unsigned long long> h(4 * (size_t)max_units);
-    s->sync();
-    HIP_CHECK(hipMemcpy(h.data(), trace->p, 32 * (size_t)max_units, hipMemcpyDeviceToHost));
-    if (FILE *f = fopen(trace_path, "ab")) {
-      fwrite(h.data(), 8, h.size(), f);
-      fclose(f);
-    }
   }
 }
 
@@ -1734,42 +1156,6 @@ __global__ __launch_bounds__(1024) void k_c5_dot_slices(const uint32_t *si, cons
 
 // acc[0] += Σ_b Σ_i (Σ in-slices of b)·(Σ out-slices of b) over the apportioned
 // slices sl[unit][64 Ki] (table: base[2·nb], k[2·nb]; runs [0, nb) in, [nb, 2·nb) out).
-__global__ __launch_bounds__(256) void k_c5_dot_apportioned(const uint32_t *sl, const int32_t *table, int nb,
-                                                             unsigned long long *acc) {
-  __shared__ int32_t base[C5APP_MAXR], kk[C5APP_MAXR];
-  __shared__ unsigned long long lds[17];
-  for (int r = threadIdx.x; r < 2 * nb; r += 256) {
-    base[r] = table[r];
-    kk[r] = table[2 * nb + r];
-  }
-  __syncthreads();
-  constexpr int Q = C2_BW / 4;
-  const int64_t n4 = (int64_t)nb * Q;
-  unsigned long long t = 0;
-  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n4; q += (int64_t)gridDim.x * 256) {
-    const int b = (int)(q / Q);
-    const int64_t i4 = q % Q;
-    uint4 x = make_uint4(0, 0, 0, 0), y = make_uint4(0, 0, 0, 0);
-    for (int k = 0; k < kk[b]; ++k) {
-      const uint4 v = ((const uint4 *)(sl + (int64_t)(base[b] + k) * C2_BW))[i4];
-      x = make_uint4(x.x + v.x, x.y + v.y, x.z + v.z, x.w + v.w);
-    }
-    for (int k = 0; k < kk[nb + b]; ++k) {
-      const uint4 v = ((const uint4 *)(sl + (int64_t)(base[nb + b] + k) * C2_BW))[i4];
-      y = make_uint4(y.x + v.x, y.y + v.y, y.z + v.z, y.w + v.w);
-    }
-    t += (unsigned long long)x.x * y.x + (unsigned long long)x.y * y.y + (unsigned long long)x.z * y.z +
-         (unsigned long long)x.w * y.w;
-  }
-  unsigned long long tot;
-  block_exclusive_scan(t, lds, tot);
-  if (threadIdx.x == 0 && tot) atomicAdd(acc, tot);
-}
-
-// Σ_b in·out over packed slices (S per side, words as laid out by C3Sides::packed)
-// plus the hand-off log: a logged bin g gets in_g = Σ_s half + Σ its side-0
-// counts, out_g likewise, and adds in_g·out_g − (Σ halves)·(Σ halves) once (at
-// its first log entry; every block takes every grid-th entry).
 __device__ inline uint32_t packed_half_sum(const uint32_t *sl, int S, int64_t stride, int64_t g) {
   const int64_t w = (g >> C2_BITS) * C2_WORDS + (g & (C2_WORDS - 1));
   const int sh = (int)((g >> 15) & 1) * 16;
@@ -1868,20 +1254,16 @@ static void chain2_c5(Session *s, C5Cols<W> c, bool in_range, uint32_t *h_in, ui
   post.acc3 = d_acc3;
   post.spill = spill;
   const int64_t hl = (int64_t)c.nb * C2_BW;
-  {
-    const char *pe = getenv("CAPF_HIST_PAIRS");  // 0 (tuning): one uint32 per bin everywhere
-    const char *ok_env = getenv("CAPF_P3_OVFK");
-    sd.pairs = S == 1 && spill && !(pe && atoi(pe) == 0) && !(ok_env && atoi(ok_env) == 1) ? 1 : 0;
-  }
+  sd.pairs = S == 1 && spill ? 1 : 0;  // packed-pair buckets (one uint32 per bin when split)
   if (S == 1) {
     c5_post(s, (const uint16_t *)part->p, (const uint32_t *)meta->p, sd, c.ntiles, c.rstride,
-            2 * c.n, 1, h_in, h_out, hl, false, nullptr, nullptr, nullptr, &post, post_acc);
+            2 * c.n, 1, h_in, h_out, hl, false, nullptr, nullptr, &post, post_acc);
     return;
   }
   BufPtr sl = s->alloc(8 * S * hl);
   uint32_t *si = (uint32_t *)sl->p, *so = si + S * hl;
   c5_post(s, (const uint16_t *)part->p, (const uint32_t *)meta->p, sd, c.ntiles, c.rstride,
-          2 * c.n, S, si, so, hl, false, nullptr, nullptr, nullptr, &post, post_acc);
+          2 * c.n, S, si, so, hl, false, nullptr, nullptr, &post, post_acc);
   hipLaunchKernelGGL(k_c5_fold, dim3(grid_for(hl / 4, 256, 1024)), dim3(256), 0, s->stream, si, so,
                      S, hl, hl, h_in, h_out);
   KERNEL_CHECK();
@@ -1904,7 +1286,7 @@ struct C5Shard {
   int64_t lo;
   uint64_t len;
   int b0, nbl;                   // owned buckets [b0, b0 + nbl)
-  int lsub, nsb;                 // 2^lsub sub-bucket runs per bucket and side; nsb = nbl << lsub
+  int nsb;                       // runs per side: one per owned bucket (= nbl)
   int copies;                    // run counters per run (power of 2, see below)
   int gpt;                       // 4096-row groups per tile (≤ 4): tile = 4096·gpt rows
   int nhot;                      // heavy hitters (≤ C5S_MAXHOT): keys equal to hot[j] are
@@ -1916,7 +1298,7 @@ struct C5Shard {
   NodeMix mix;
 };
 
-constexpr int C5S_TILE = 32768;  // rows (= keys) per tile (at most); 16384 via CAPF_SHARD_TILE=16
+constexpr int C5S_TILE = 32768;  // rows (= keys) per tile (at most) at FOR24; 16384 otherwise
 constexpr int C5S_MAXHOT = 1;    // heavy-hitter keys of a rank (sampled at ingest, a plan hint)
 constexpr int C5S_MAXR = 520;    // runs incl. the dummy: nbl ≤ 259
 // a tile scans ONE copy, so it fills only its side's ≤ nsb ≤ 259 runs + the
@@ -1939,7 +1321,7 @@ static int c5s_copies(int nr) {
 // TR (trusted): both key columns are node-partitioned copies of this very
 // (range, parts, part) — every key is an owned node, so the ring path's keys
 // skip the 64-bit range test and the ownership test: run and key come from
-// the mixed index alone, key = ((run0 − b0·2^lsub + h >> (16 − lsub)) << 16) | (h & 0xFFFF).
+// the mixed index alone, key = ((run0 − b0 + h >> 16) << 16) | (h & 0xFFFF).
 template <int W, bool WIDE, int TILE, bool HOT, bool TR = false>
 __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_c5_shard_partition(
     C5Shard c, uint16_t *part, uint32_t *meta, uint32_t *tile_acc, int64_t rstride) {
@@ -1974,7 +1356,6 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   const int64_t kb = side ? c.bout : c.bin;
   const uint32_t dummy = (uint32_t)nr << C2_BITS;
   const uint32_t run0 = (uint32_t)(side * c.nsb);
-  const uint32_t lsub = (uint32_t)c.lsub, ssh = 16u - lsub;  // h & 0xFFFF >> 16 = 0: no sub-buckets
   uint32_t key[RPT];
   uint32_t lp = 0;
   // heavy hitter (skew handling): keys whose mixed index is c.hot[0] are not
@@ -1988,7 +1369,7 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
     const uint32_t h = node_mix_t<WIDE>(x, c.mix);
     const uint32_t b = (h >> C2_BITS) - (uint32_t)c.b0;  // wraps when below b0
     const bool ok = okx && b < (uint32_t)c.nbl;
-    const uint32_t run = run0 + (b << lsub) + ((h & 0xFFFF) >> ssh);
+    const uint32_t run = run0 + b;
     return HOT ? (ok && h != c.hot[0] ? (run << C2_BITS) | (h & 0xFFFF) : dummy | (ok ? 1u : 0u))
                : (ok ? (run << C2_BITS) | (h & 0xFFFF) : dummy);
   };
@@ -2018,11 +1399,11 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
           uint32_t q[4];
           c5_decode<(W == 3 ? 3 : 4)>(raw[g & (D - 1)], (uint32_t)dlo, q);
           if (g + D < GROUPS) issue(g + D);
-          const uint32_t run0t = run0 - ((uint32_t)c.b0 << lsub);
+          const uint32_t run0t = run0 - (uint32_t)c.b0;
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             const uint32_t h = node_mix_t<WIDE>(q[k], c.mix);
-            const uint32_t kk = ((run0t + (h >> ssh)) << C2_BITS) | (h & 0xFFFF);
+            const uint32_t kk = ((run0t + (h >> C2_BITS)) << C2_BITS) | (h & 0xFFFF);
             key[4 * g + k] = HOT ? (h != c.hot[0] ? kk : dummy | 1u) : kk;
             atomicAdd(&cur[(key[4 * g + k] >> C2_BITS) * C + my_copy], 1u);
           }
@@ -2089,7 +1470,7 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
         // a heavy hitter goes to the dummy run: counted here, never copied out
         // the heavy hitter (mixed index) goes to the dummy run as key 1 (past-the-end
         // rows as key 0): never copied out, counted in the dummy run's stage slots
-        const uint32_t run = run0 + (b << lsub) + ((h & 0xFFFF) >> ssh);
+        const uint32_t run = run0 + b;
         key[4 * g + k] = HOT ? (ok && h != c.hot[0] ? (run << C2_BITS) | (h & 0xFFFF) : dummy | (ok ? 1u : 0u))
                              : (ok ? (run << C2_BITS) | (h & 0xFFFF) : dummy);
         if (chk) lp += (ok && oky[k] && x[k] == y[k] && (uint32_t)k < dg) ? 1u : 0u;
@@ -2166,653 +1547,6 @@ __global__ __launch_bounds__(1024) void k_sharded_final(const unsigned long long
   const unsigned long long L = block_reduce_sum(lp, lds[0]), I = block_reduce_sum(hi, lds[1]),
                            O = block_reduce_sum(ho, lds[2]);
   if (threadIdx.x == 0) *out = (int64_t)(acc[0] + I * O - L);
-}
-
-// ---------------------------------------------- sharded P3, sub-bucket units
-// A rank owning few buckets (G ≥ 4 at s24: 64 or 32 buckets) has P1 cut every
-// owned 64 Ki bucket into 2^lsub sub-bucket runs per side (runs [0, nsb) in,
-// [nsb, 2·nsb) out), so ONE workgroup holds both the in- and the out-counters
-// of a sub-bucket in LDS (uint32, 2 · 2^sbits) and finishes Σ in·out itself:
-// no histogram slices in HBM, no dot / overflow / units kernels, 4 fewer
-// launches.  Waves 0..7 count the in-run over the in-copy tiles [0, t_in),
-// waves 8..15 the out-run over the out-copy tiles [t_in, ntiles).  Piece
-// walking, the pad / dead-lane correction and the hub-key merge are those of
-// k_c5_gather; uint32 bins cannot overflow (≤ 2^31 rows per copy).
-struct C5SbArgs {
-  const uint16_t *part;
-  const uint32_t *meta_t;
-  int64_t ntiles, t_in;
-  int nsb, sbits;
-  uint32_t rs8;
-  unsigned long long *acc;    // += Σ in·out
-  unsigned long long *trace;  // diagnostics (CAPF_P3_TRACE): 4 words per unit, else null
-};
-
-constexpr int C5SB_MAXBITS = 14;
-constexpr size_t c5sb_lds(int sbits) {
-  return 4 * ((size_t)2 << sbits) + 4 * 2 * C5_CORR + 2 * sizeof(C5WaveTab) * (C5_BLOCK / WAVE);
-}
-
-__global__ __launch_bounds__(C5_BLOCK) void k_c5_sb_gather(C5SbArgs a) {
-  const int ui = c3_unit_of((int)blockIdx.x);
-  if (ui >= a.nsb) return;
-  const unsigned long long t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
-  extern __shared__ __attribute__((aligned(16))) uint32_t words[];
-  __shared__ unsigned long long lds_red[17];
-  constexpr int NW = C5_BLOCK / WAVE, HW = NW / 2;
-  constexpr uint32_t STEP = WAVE * C5_PPS;
-  const int NB = 1 << a.sbits;
-  uint32_t *corr = words + 2 * NB;
-  C5WaveTab *tabs = (C5WaveTab *)(corr + 2 * C5_CORR);
-  for (int i = threadIdx.x; i < 2 * NB + 2 * C5_CORR; i += C5_BLOCK) words[i] = 0;
-  __syncthreads();
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = lane_id();
-  const int side = wave >= HW ? 1 : 0, sw = wave - side * HW;
-  uint32_t *cnt = words + side * NB;
-  const uint32_t kmask = (uint32_t)NB - 1;
-  C5WaveTab *tab2 = tabs + 2 * wave;
-  const uint4 *part4 = (const uint4 *)a.part;
-  const uint32_t *m = a.meta_t + (int64_t)(ui + side * a.nsb) * a.ntiles;
-  const int64_t s0 = side ? a.t_in : 0, s1 = side ? a.ntiles : a.t_in;
-  const int64_t w0 = uniform64(s0 + (s1 - s0) * sw / HW), w1 = uniform64(s0 + (s1 - s0) * (sw + 1) / HW);
-  uint32_t padc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  uint32_t dead = 0;
-  const uint4 dead_keys = make_uint4(lane | lane << 16, lane | lane << 16, lane | lane << 16,
-                                     lane | lane << 16);
-  uint32_t wpre = w0 + lane < w1 ? m[w0 + lane] : 0u;
-  auto setup = [&](int64_t tb, int buf) -> uint32_t {
-    const int64_t t = tb + lane;
-    const uint32_t w = wpre;
-    const uint32_t len = w >> 16, nq = (len + 7) >> 3, r = len & 7;
-#pragma unroll
-    for (int e = 1; e < 8; ++e) padc[e] += (r != 0 && r <= (uint32_t)e) ? 1u : 0u;
-    const uint32_t inc = wave_inclusive_scan(nq);
-    tab2[buf].pre[lane] = inc - nq;
-    if (lane == WAVE - 1) tab2[buf].pre[WAVE] = inc;
-    tab2[buf].qb[lane] = (uint32_t)t * a.rs8 + (w & 0xFFFF);
-    __builtin_amdgcn_sched_barrier(0);
-    const int64_t tn = tb + WAVE + lane;
-    wpre = tn < w1 ? m[tn] : 0u;
-    __builtin_amdgcn_wave_barrier();
-    return (uint32_t)__builtin_amdgcn_readfirstlane(__shfl(inc, WAVE - 1, WAVE));
-  };
-  auto fetch = [&](int buf, uint32_t p0, uint32_t total, uint4 *v) {
-    const C5WaveTab &tab = tab2[buf];
-#pragma unroll
-    for (int j = 0; j < C5_PPS; ++j) {
-      const uint32_t p = p0 + j * WAVE + lane;
-      const uint32_t pc = min(p, total - 1);
-      uint32_t k = 0;
-#pragma unroll
-      for (int b = WAVE / 2; b > 0; b >>= 1)
-        if (tab.pre[k + b] <= pc) k += b;
-      v[j] = part4[tab.qb[k] + (pc - tab.pre[k])];
-    }
-  };
-  // a piece's copies of its first (second) key are added once, as a count
-  auto count = [&](const uint4 *v, uint32_t p0, uint32_t total) {
-#pragma unroll
-    for (int j = 0; j < C5_PPS; ++j) {
-      const bool live = p0 + j * WAVE + lane < total;
-      dead += live ? 0u : 1u;
-      const uint32_t wd[4] = {live ? v[j].x : dead_keys.x, live ? v[j].y : dead_keys.y,
-                              live ? v[j].z : dead_keys.z, live ? v[j].w : dead_keys.w};
-      const uint32_t k0 = wd[0] & 0xFFFF, k1 = wd[0] >> 16;
-      uint32_t n0 = k1 == k0 ? 2u : 1u, n1 = 1;
-      bool dup[8];
-#pragma unroll
-      for (int e = 2; e < 8; ++e) {
-        const uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
-        const bool d0 = key == k0, d1 = !d0 && key == k1;
-        dup[e] = d0 || d1;
-        n0 += d0 ? 1u : 0u;
-        n1 += d1 ? 1u : 0u;
-      }
-      atomicAdd(&cnt[k0 & kmask], n0);
-      if (k1 != k0) atomicAdd(&cnt[k1 & kmask], n1);
-#pragma unroll
-      for (int e = 2; e < 8; ++e) {
-        const uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
-        if (!dup[e]) atomicAdd(&cnt[key & kmask], 1u);
-      }
-    }
-  };
-  if (w0 < w1) {
-    int64_t tb = uniform64(w0);
-    int buf = 0;
-    uint32_t total = setup(tb, buf), p0 = 0;
-    while (total == 0) {
-      tb += WAVE;
-      if (tb >= w1) break;
-      buf ^= 1;
-      total = setup(tb, buf);
-    }
-    if (total) {
-      auto advance = [&]() -> bool {
-        if (p0 + STEP < total) {
-          p0 = (uint32_t)__builtin_amdgcn_readfirstlane(p0 + STEP);
-          return true;
-        }
-        do {
-          tb = uniform64(tb + WAVE);
-          if (tb >= w1) return false;
-          buf ^= 1;
-          total = setup(tb, buf);
-          p0 = 0;
-        } while (total == 0);
-        return true;
-      };
-      // three rotating piece buffers: loads of steps i+1, i+2 in flight while step i counts
-      uint4 va[C5_PPS], vb[C5_PPS], vc[C5_PPS];
-      uint32_t pa, ta, pb, tb2, pc, tc;
-      pa = p0;
-      ta = total;
-      fetch(buf, p0, total, va);
-      if (!advance()) {
-        count(va, pa, ta);
-      } else {
-        pb = p0;
-        tb2 = total;
-        fetch(buf, p0, total, vb);
-        for (;;) {
-          if (!advance()) {
-            count(va, pa, ta);
-            count(vb, pb, tb2);
-            break;
-          }
-          pc = p0;
-          tc = total;
-          fetch(buf, p0, total, vc);
-          count(va, pa, ta);
-          if (!advance()) {
-            count(vb, pb, tb2);
-            count(vc, pc, tc);
-            break;
-          }
-          pa = p0;
-          ta = total;
-          fetch(buf, p0, total, va);
-          count(vb, pb, tb2);
-          if (!advance()) {
-            count(vc, pc, tc);
-            count(va, pa, ta);
-            break;
-          }
-          pb = p0;
-          tb2 = total;
-          fetch(buf, p0, total, vb);
-          count(vc, pc, tc);
-        }
-      }
-    }
-  }
-  uint32_t *cs = corr + side * C5_CORR;
-  const uint32_t pcls = 8u * (uint32_t)((w0 + lane) & 7);
-#pragma unroll
-  for (int e = 1; e < 8; ++e)
-    if (padc[e]) atomicAdd(&cs[pcls + e], padc[e]);
-  if (dead) atomicAdd(&cs[lane], 8 * dead);
-  __syncthreads();
-  unsigned long long t = 0;
-  for (int i = threadIdx.x; i < NB; i += C5_BLOCK) {
-    uint32_t x = words[i], y = words[NB + i];
-    if (i < C5_CORR) {
-      x -= corr[i];
-      y -= corr[C5_CORR + i];
-    }
-    t += (unsigned long long)x * y;
-  }
-  unsigned long long tot;
-  block_exclusive_scan(t, lds_red, tot);
-  if (threadIdx.x == 0 && tot) atomicAdd(a.acc, tot);
-  if (a.trace && threadIdx.x == 0) {  // diagnostics: this unit's span, where it ran
-    const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (3 << 11));
-    const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));
-    a.trace[4 * ui] = t_start;
-    a.trace[4 * ui + 1] = __builtin_amdgcn_s_memrealtime();
-    a.trace[4 * ui + 2] = ((unsigned long long)xcc << 32) | hw;
-    a.trace[4 * ui + 3] = (unsigned long long)ui << 32;
-  }
-}
-
-// Sub-bucket runs per bucket (log2) for a rank owning nbl buckets: the most
-// that keep 2·nsb + 1 runs within P1's limit; 0 (slice path) unless the
-// sub-buckets are ≤ 2^C5SB_MAXBITS nodes (LDS: 2 uint32 arrays).
-// P3 of a node-partitioned rank (CAPF_SHARD_SB, tuning): 0 = histogram
-// slices + dot, 1 = one sub-bucket per unit (k_c5_sb_gather), 2 = balanced key
-// ranges over sub-buckets (k_c5_bal_gather + k_c5_bal_fold)
-static int c5s_mode() {
-  const char *e = getenv("CAPF_SHARD_SB");
-  return e ? atoi(e) : 0;
-}
-
-static int c5sb_lsub(int nbl) {
-  // measured at s24 G = 8 and off by default: per-unit rates equal the slice
-  // path's, but 8 Ki-node sub-buckets are skewed (p99 unit 1.7×, the hub's
-  // 3.2× the median) where the slice units are not → 0.296 vs 0.235 ms/rank
-  const int mode = c5s_mode();
-  if ((mode != 1 && mode != 2) || nbl <= 0) return 0;
-  int l = 0;
-  while (l < C2_BITS && 2 * ((int64_t)nbl << (l + 1)) + 1 <= C5S_MAXR) ++l;
-  return C2_BITS - l <= C5SB_MAXBITS ? l : 0;
-}
-
-// T + P3 of the sub-bucket path: meta transpose, then one k_c5_sb_gather unit
-// per sub-bucket, adding Σ in·out into d_acc[0].
-static void c5_sb_post(Session *s, const uint16_t *part, const uint32_t *meta, int64_t ntiles,
-                       int64_t t_in, int nsb, int sbits, int64_t rstride, unsigned long long *d_acc) {
-  const int nr = 2 * nsb;
-  static bool attr_set = false;
-  if (!attr_set) {
-    HIP_CHECK(hipFuncSetAttribute((const void *)k_c5_sb_gather,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)c5sb_lds(C5SB_MAXBITS)));
-    attr_set = true;
-  }
-  BufPtr meta_t = s->alloc(4 * nr * ntiles);
-  BufPtr tot = s->alloc(8 * nr);
-  HIP_CHECK(hipMemsetAsync(tot->p, 0, 8 * nr, s->stream));
-  int64_t tt = C3_TT;
-  while (tt > 32 && ((ntiles + tt - 1) / tt) * ((nr + 31) / 32) < 1024) tt /= 2;
-  {
-    KernelTimer kt(s, "c3_transpose", 8.0 * nr * ntiles);
-    hipLaunchKernelGGL(k_c3_transpose, dim3((unsigned)((ntiles + tt - 1) / tt), (nr + 31) / 32),
-                       dim3(256), 0, s->stream, meta, (uint32_t *)meta_t->p, ntiles, nr,
-                       (unsigned long long *)tot->p, tt);
-    KERNEL_CHECK();
-  }
-  C5SbArgs a;
-  a.part = part;
-  a.meta_t = (const uint32_t *)meta_t->p;
-  a.ntiles = ntiles;
-  a.t_in = t_in;
-  a.nsb = nsb;
-  a.sbits = sbits;
-  a.rs8 = (uint32_t)(rstride / 8);
-  a.acc = d_acc;
-  a.trace = nullptr;
-  const char *trace_path = getenv("CAPF_P3_TRACE");  // diagnostics only
-  const int nblocks = (nsb + 255) / 256 * 256;       // c3_unit_of is a bijection per 256
-  BufPtr trace;
-  if (trace_path) {
-    trace = s->alloc(32 * (int64_t)nsb);
-    HIP_CHECK(hipMemsetAsync(trace->p, 0, 32 * (size_t)nsb, s->stream));
-    a.trace = (unsigned long long *)trace->p;
-  }
-  {
-    KernelTimer kt(s, "c5_gather", 2.0 * (double)rstride * ntiles);
-    hipLaunchKernelGGL(k_c5_sb_gather, dim3((unsigned)nblocks), dim3(C5_BLOCK), c5sb_lds(sbits),
-                       s->stream, a);
-    KERNEL_CHECK();
-  }
-  if (trace_path) {
-    std::vector<unsigned long long> h(4 * (size_t)nsb);
-    s->sync();
-    HIP_CHECK(hipMemcpy(h.data(), trace->p, 32 * (size_t)nsb, hipMemcpyDeviceToHost));
-    if (FILE *f = fopen(trace_path, "ab")) {
-      fwrite(h.data(), 8, h.size(), f);
-      fclose(f);
-    }
-  }
-}
-
-// ---------------------------------------- sharded P3, balanced key ranges
-// The sub-bucket runs of a rank (P1 with lsub > 0: nsb sub-buckets of 2^sbits
-// nodes, in-run j and out-run nsb + j) hold W keys.  Workgroup w of P (one
-// per CU) takes the keys [w·W/P, (w+1)·W/P) of the sequence "sub-bucket 0
-// in, out; sub-bucket 1 in, out; …" — every workgroup the same number of keys
-// whatever the skew (a hub's sub-bucket simply spans several workgroups).
-// Split points inside a run are rounded to blocks of tt tiles using the
-// transpose's per-(run, block) counts, identically by both neighbours, so
-// every tile segment is counted exactly once.  A sub-bucket lying wholly in
-// one workgroup is finished there: in and out counters (uint32, 2·2^sbits in
-// LDS) → Σ in·out added to acc, nothing written.  A split sub-bucket's
-// portions store their corrected counters into the workgroup's slot (first or
-// last portion), and k_c5_bal_fold sums the slots of each split sub-bucket
-// and adds its Σ in·out: ≤ 2 slots per workgroup, no slice or dot pass over
-// the whole node range, no overflow log (uint32 counters).
-struct C5BalArgs {
-  const uint16_t *part;
-  const uint32_t *meta_t;               // [run][tile] (start/8 | count << 16)
-  const unsigned long long *run_total;  // [run] keys
-  const uint32_t *bsum;                 // [run][nblk] keys per block of tt tiles
-  int64_t ntiles;
-  int nblk, tt;
-  int nsb, sbits;
-  uint32_t rs8;
-  int nwg;                  // P
-  uint32_t *slots;          // 2·P slots of (in, out) 2·2^sbits counters
-  unsigned long long *acc;  // += Σ in·out
-};
-
-constexpr int C5BAL_MAXSB = 512;
-
-constexpr size_t c5bal_lds(int sbits) {
-  return 4 * ((size_t)2 << sbits) + 4 * 2 * C5_CORR + 2 * sizeof(C5WaveTab) * (C5_BLOCK / WAVE);
-}
-
-__global__ __launch_bounds__(C5_BLOCK) void k_c5_bal_gather(C5BalArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t words[];
-  __shared__ uint32_t pre[C5BAL_MAXSB + 1];
-  __shared__ uint32_t tin[C5BAL_MAXSB];
-  __shared__ uint32_t lds_scan[17];
-  __shared__ unsigned long long lds_red[17];
-  __shared__ int64_t bnd[4];
-  constexpr int NW = C5_BLOCK / WAVE;
-  constexpr uint32_t STEP = WAVE * C5_PPS;
-  const int NB = 1 << a.sbits;
-  const uint32_t kmask = (uint32_t)NB - 1;
-  uint32_t *corr = words + 2 * NB;
-  C5WaveTab *tabs = (C5WaveTab *)(corr + 2 * C5_CORR);
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = lane_id();
-  const int P = a.nwg, w = blockIdx.x;
-  // the schedule: sub-bucket sizes and their exclusive prefix (every workgroup alike)
-  for (int j0 = 0; j0 < a.nsb; j0 += C5_BLOCK) {
-    const int j = j0 + threadIdx.x;
-    uint32_t tj = 0, sj = 0;
-    if (j < a.nsb) {
-      tj = (uint32_t)a.run_total[j];
-      sj = tj + (uint32_t)a.run_total[a.nsb + j];
-    }
-    uint32_t tot;
-    const uint32_t ex = block_exclusive_scan(sj, lds_scan, tot);
-    const uint32_t base = j0 ? pre[j0] : 0u;
-    if (j < a.nsb) {
-      pre[j] = base + ex;
-      tin[j] = tj;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) pre[min(j0 + C5_BLOCK, a.nsb)] = base + tot;
-    __syncthreads();
-  }
-  for (int i = threadIdx.x; i < 2 * NB + 2 * C5_CORR; i += C5_BLOCK) words[i] = 0;
-  __syncthreads();
-  const uint32_t W = pre[a.nsb];
-  const uint32_t A = bal_start(w, W, P), B = bal_start(w + 1, W, P);
-  if (A >= B) return;  // block-uniform
-  const int jfirst = bal_sb_of(pre, a.nsb, A);
-  C5WaveTab *tab2 = tabs + 2 * wave;
-  const uint4 *part4 = (const uint4 *)a.part;
-  const uint4 dead_keys = make_uint4(lane | lane << 16, lane | lane << 16, lane | lane << 16,
-                                     lane | lane << 16);
-  // count the segments of run row m over tiles [w0, w1) into cnt; pad and
-  // dead-lane keys are subtracted through cs (bins 0..63)
-  auto walk = [&](const uint32_t *m, int64_t w0, int64_t w1, uint32_t *cnt, uint32_t *cs) {
-    uint32_t padc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint32_t dead = 0;
-    uint32_t wpre = w0 + lane < w1 ? m[w0 + lane] : 0u;
-    auto setup = [&](int64_t tb, int buf) -> uint32_t {
-      const int64_t t = tb + lane;
-      const uint32_t wd = wpre;
-      const uint32_t len = wd >> 16, nq = (len + 7) >> 3, r = len & 7;
-#pragma unroll
-      for (int e = 1; e < 8; ++e) padc[e] += (r != 0 && r <= (uint32_t)e) ? 1u : 0u;
-      const uint32_t inc = wave_inclusive_scan(nq);
-      tab2[buf].pre[lane] = inc - nq;
-      if (lane == WAVE - 1) tab2[buf].pre[WAVE] = inc;
-      tab2[buf].qb[lane] = (uint32_t)t * a.rs8 + (wd & 0xFFFF);
-      __builtin_amdgcn_sched_barrier(0);
-      const int64_t tn = tb + WAVE + lane;
-      wpre = tn < w1 ? m[tn] : 0u;
-      __builtin_amdgcn_wave_barrier();
-      return (uint32_t)__builtin_amdgcn_readfirstlane(__shfl(inc, WAVE - 1, WAVE));
-    };
-    auto fetch = [&](int buf, uint32_t p0, uint32_t total, uint4 *v) {
-      const C5WaveTab &tab = tab2[buf];
-#pragma unroll
-      for (int j = 0; j < C5_PPS; ++j) {
-        const uint32_t p = p0 + j * WAVE + lane;
-        const uint32_t pc = min(p, total - 1);
-        uint32_t k = 0;
-#pragma unroll
-        for (int b = WAVE / 2; b > 0; b >>= 1)
-          if (tab.pre[k + b] <= pc) k += b;
-        v[j] = part4[tab.qb[k] + (pc - tab.pre[k])];
-      }
-    };
-    // a piece's copies of its first (second) key are added once, as a count
-    auto count = [&](const uint4 *v, uint32_t p0, uint32_t total) {
-#pragma unroll
-      for (int j = 0; j < C5_PPS; ++j) {
-        const bool live = p0 + j * WAVE + lane < total;
-        dead += live ? 0u : 1u;
-        const uint32_t wd[4] = {live ? v[j].x : dead_keys.x, live ? v[j].y : dead_keys.y,
-                                live ? v[j].z : dead_keys.z, live ? v[j].w : dead_keys.w};
-        const uint32_t k0 = wd[0] & 0xFFFF, k1 = wd[0] >> 16;
-        uint32_t n0 = k1 == k0 ? 2u : 1u, n1 = 1;
-        bool dup[8];
-#pragma unroll
-        for (int e = 2; e < 8; ++e) {
-          const uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
-          const bool d0 = key == k0, d1 = !d0 && key == k1;
-          dup[e] = d0 || d1;
-          n0 += d0 ? 1u : 0u;
-          n1 += d1 ? 1u : 0u;
-        }
-        atomicAdd(&cnt[k0 & kmask], n0);
-        if (k1 != k0) atomicAdd(&cnt[k1 & kmask], n1);
-#pragma unroll
-        for (int e = 2; e < 8; ++e) {
-          const uint32_t key = (e & 1) ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xFFFF;
-          if (!dup[e]) atomicAdd(&cnt[key & kmask], 1u);
-        }
-      }
-    };
-    if (w0 < w1) {
-      int64_t tb = uniform64(w0);
-      int buf = 0;
-      uint32_t total = setup(tb, buf), p0 = 0;
-      while (total == 0) {
-        tb += WAVE;
-        if (tb >= w1) break;
-        buf ^= 1;
-        total = setup(tb, buf);
-      }
-      if (total) {
-        auto advance = [&]() -> bool {
-          if (p0 + STEP < total) {
-            p0 = (uint32_t)__builtin_amdgcn_readfirstlane(p0 + STEP);
-            return true;
-          }
-          do {
-            tb = uniform64(tb + WAVE);
-            if (tb >= w1) return false;
-            buf ^= 1;
-            total = setup(tb, buf);
-            p0 = 0;
-          } while (total == 0);
-          return true;
-        };
-        // three rotating piece buffers: loads of steps i+1, i+2 in flight while step i counts
-        uint4 va[C5_PPS], vb[C5_PPS], vc[C5_PPS];
-        uint32_t pa, ta, pb, tb2, pc, tc;
-        pa = p0;
-        ta = total;
-        fetch(buf, p0, total, va);
-        if (!advance()) {
-          count(va, pa, ta);
-        } else {
-          pb = p0;
-          tb2 = total;
-          fetch(buf, p0, total, vb);
-          for (;;) {
-            if (!advance()) {
-              count(va, pa, ta);
-              count(vb, pb, tb2);
-              break;
-            }
-            pc = p0;
-            tc = total;
-            fetch(buf, p0, total, vc);
-            count(va, pa, ta);
-            if (!advance()) {
-              count(vb, pb, tb2);
-              count(vc, pc, tc);
-              break;
-            }
-            pa = p0;
-            ta = total;
-            fetch(buf, p0, total, va);
-            count(vb, pb, tb2);
-            if (!advance()) {
-              count(vc, pc, tc);
-              count(va, pa, ta);
-              break;
-            }
-            pb = p0;
-            tb2 = total;
-            fetch(buf, p0, total, vb);
-            count(vc, pc, tc);
-          }
-        }
-      }
-    }
-    const uint32_t pcls = 8u * (uint32_t)((w0 + lane) & 7);
-#pragma unroll
-    for (int e = 1; e < 8; ++e)
-      if (padc[e]) atomicAdd(&cs[pcls + e], padc[e]);
-    if (dead) atomicAdd(&cs[lane], 8 * dead);
-  };
-  for (int j = jfirst; j < a.nsb && pre[j] < B; ++j) {
-    const uint32_t S = pre[j + 1] - pre[j];
-    if (S == 0) continue;
-    const uint32_t lo = max(A, pre[j]) - pre[j], hi = min(B, pre[j + 1]) - pre[j];
-    const uint32_t T = tin[j];
-    if (wave < 4) {  // the four split tiles of this portion, one wave each
-      const int run = wave < 2 ? j : a.nsb + j;
-      const uint32_t x = wave == 0 ? min(lo, T) : wave == 1 ? min(hi, T) : wave == 2 ? max(lo, T) - T
-                                                                                     : max(hi, T) - T;
-      const int64_t t = bal_tile(a.bsum + (int64_t)run * a.nblk, a.nblk, a.tt, a.ntiles, x);
-      if (lane == 0) bnd[wave] = t;
-    }
-    __syncthreads();
-    const int64_t ti0 = bnd[0], li = max<int64_t>(bnd[1] - bnd[0], 0);
-    const int64_t to0 = bnd[2], lt = li + max<int64_t>(bnd[3] - bnd[2], 0);
-    // the 16 waves split the portion's tiles: in-run tiles first, then out-run
-    const int64_t v0 = uniform64(lt * wave / NW), v1 = uniform64(lt * (wave + 1) / NW);
-    if (v0 < li) walk(a.meta_t + (int64_t)j * a.ntiles, ti0 + v0, ti0 + min(v1, li), words, corr);
-    if (v1 > li)
-      walk(a.meta_t + (int64_t)(a.nsb + j) * a.ntiles, to0 + max(v0, li) - li, to0 + v1 - li, words + NB,
-           corr + C5_CORR);
-    __syncthreads();
-    if (lo == 0 && hi == S) {  // the whole sub-bucket: finish it here
-      unsigned long long t = 0;
-      for (int i = threadIdx.x; i < NB; i += C5_BLOCK) {
-        uint32_t x = words[i], y = words[NB + i];
-        if (i < C5_CORR) {
-          x -= corr[i];
-          y -= corr[C5_CORR + i];
-        }
-        t += (unsigned long long)x * y;
-      }
-      const unsigned long long tot = block_reduce_sum(t, lds_red);
-      if (threadIdx.x == 0 && tot) atomicAdd(a.acc, tot);
-    } else {  // a portion of a split sub-bucket: corrected counters to the slot
-      uint32_t *dst = a.slots + (int64_t)(2 * w + (j == jfirst ? 0 : 1)) * 2 * NB;
-      for (int i = threadIdx.x; i < NB; i += C5_BLOCK) {
-        uint32_t x = words[i], y = words[NB + i];
-        if (i < C5_CORR) {
-          x -= corr[i];
-          y -= corr[C5_CORR + i];
-        }
-        dst[i] = x;
-        dst[NB + i] = y;
-      }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < 2 * NB + 2 * C5_CORR; i += C5_BLOCK) words[i] = 0;
-    __syncthreads();
-  }
-}
-
-// One block per sub-bucket: a split one sums its portions' slots and adds Σ in·out.
-__global__ __launch_bounds__(256) void k_c5_bal_fold(C5BalArgs a) {
-  __shared__ uint32_t pre[C5BAL_MAXSB + 1];
-  __shared__ uint32_t lds_scan[17];
-  __shared__ unsigned long long lds_red[17];
-  const int NB = 1 << a.sbits;
-  const int P = a.nwg;
-  for (int j0 = 0; j0 < a.nsb; j0 += 256) {
-    const int j = j0 + threadIdx.x;
-    const uint32_t sj = j < a.nsb ? (uint32_t)a.run_total[j] + (uint32_t)a.run_total[a.nsb + j] : 0u;
-    uint32_t tot;
-    const uint32_t ex = block_exclusive_scan(sj, lds_scan, tot);
-    const uint32_t base = j0 ? pre[j0] : 0u;
-    if (j < a.nsb) pre[j] = base + ex;
-    __syncthreads();
-    if (threadIdx.x == 0) pre[min(j0 + 256, a.nsb)] = base + tot;
-    __syncthreads();
-  }
-  const int j = blockIdx.x;
-  const uint32_t W = pre[a.nsb];
-  if (pre[j + 1] == pre[j]) return;
-  const int wa = bal_wg_of(pre[j], W, P), wb = bal_wg_of(pre[j + 1] - 1, W, P);
-  if (wa == wb) return;  // finished inside its workgroup
-  unsigned long long t = 0;
-  for (int i = threadIdx.x; i < NB; i += 256) {
-    uint32_t x = 0, y = 0;
-    for (int w = wa; w <= wb; ++w) {
-      const int jf = bal_sb_of(pre, a.nsb, bal_start(w, W, P));
-      const uint32_t *src = a.slots + (int64_t)(2 * w + (jf == j ? 0 : 1)) * 2 * NB;
-      x += src[i];
-      y += src[NB + i];
-    }
-    t += (unsigned long long)x * y;
-  }
-  const unsigned long long tot = block_reduce_sum(t, lds_red);
-  if (threadIdx.x == 0 && tot) atomicAdd(a.acc, tot);
-}
-
-// T + balanced P3 + fold of the sub-bucket path (adds Σ in·out into d_acc[0]).
-static void c5_bal_post(Session *s, const uint16_t *part, const uint32_t *meta, int64_t ntiles, int nsb,
-                        int sbits, int64_t rstride, unsigned long long *d_acc) {
-  const int nr = 2 * nsb;
-  static bool attr_set = false;
-  if (!attr_set) {
-    HIP_CHECK(hipFuncSetAttribute((const void *)k_c5_bal_gather, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)c5bal_lds(C5SB_MAXBITS)));
-    attr_set = true;
-  }
-  int64_t tt = C3_TT;
-  while (tt > 32 && ((ntiles + tt - 1) / tt) * ((nr + 31) / 32) < 1024) tt /= 2;
-  const int nblk = (int)((ntiles + tt - 1) / tt);
-  const int P = s->num_cus;
-  BufPtr meta_t = s->alloc(4 * nr * ntiles);
-  BufPtr tot = s->alloc(8 * nr + 4 * (int64_t)nr * nblk);
-  unsigned long long *run_total = (unsigned long long *)tot->p;
-  uint32_t *bsum = (uint32_t *)(run_total + nr);
-  HIP_CHECK(hipMemsetAsync(tot->p, 0, 8 * nr, s->stream));
-  BufPtr slots = s->alloc(4 * (int64_t)(2 * P) * (2 << sbits));
-  {
-    KernelTimer kt(s, "c3_transpose", 8.0 * nr * ntiles);
-    hipLaunchKernelGGL(k_c3_transpose, dim3((unsigned)nblk, (nr + 31) / 32), dim3(256), 0, s->stream, meta,
-                       (uint32_t *)meta_t->p, ntiles, nr, run_total, tt, bsum);
-    KERNEL_CHECK();
-  }
-  C5BalArgs a;
-  a.part = part;
-  a.meta_t = (const uint32_t *)meta_t->p;
-  a.run_total = run_total;
-  a.bsum = bsum;
-  a.ntiles = ntiles;
-  a.nblk = nblk;
-  a.tt = (int)tt;
-  a.nsb = nsb;
-  a.sbits = sbits;
-  a.rs8 = (uint32_t)(rstride / 8);
-  a.nwg = P;
-  a.slots = (uint32_t *)slots->p;
-  a.acc = d_acc;
-  {
-    KernelTimer kt(s, "c5_gather", 2.0 * (double)rstride * ntiles);
-    hipLaunchKernelGGL(k_c5_bal_gather, dim3((unsigned)P), dim3(C5_BLOCK), c5bal_lds(sbits), s->stream, a);
-    KERNEL_CHECK();
-  }
-  {
-    KernelTimer kt(s, "chain2_dot", 0.0);
-    hipLaunchKernelGGL(k_c5_bal_fold, dim3((unsigned)nsb), dim3(256), 0, s->stream, a);
-    KERNEL_CHECK();
-  }
 }
 
 template <int TILE, bool TR>
@@ -2973,18 +1707,14 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
     c.n_out = n_out;
     c.n_diag = n_diag < 0 ? n_out : std::min(n_diag, n_out);
     c.nhot = nh;
-    {
-      const char *ue = getenv("CAPF_SHARD_UPF");  // tuning: 0 = one group ahead everywhere
-      c.upf = ue ? atoi(ue) : 1;  // 2 = the ring with non-temporal loads
-    }
+    c.upf = 1;  // raw loads D groups ahead on tiles without the loop test (nt loads: no change)
     c.hot[0] = hot[0];
     c.hot[1] = hot[1];
     // tile size: whole rounds of resident blocks (2 per CU), counting one
     // group of per-tile overhead (stage fill, scan, copy-out)
-    const char *te = getenv("CAPF_SHARD_TILE");  // tuning: 16 → 16 Ki-row tiles
-    // (32 Ki-row tiles need 32 keys per thread in VGPRs: no spills at FOR24 only)
-    // CAPF_SHARD_TILE=24 (tuning): 24 Ki-row tiles (24 keys per thread: no VGPR spills)
-    const int tile = (te && atoi(te) == 16) || W != 3 ? 16384 : (te && atoi(te) == 24) ? 24576 : C5S_TILE;
+    // (32 Ki-row tiles need 32 keys per thread in VGPRs: no spills at FOR24 only;
+    // 16 Ki / 24 Ki-row tiles at FOR24 measured no gain)
+    const int tile = W != 3 ? 16384 : C5S_TILE;
     {
       const int64_t slots = 2 * (int64_t)s->num_cus;
       int64_t best = -1;
@@ -3011,11 +1741,10 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
     c.b0 = b0;
     c.nbl = nbl;
     c.mix = node_mix_for(kbits);
-    // sub-bucket units (k_c5_sb_gather) when the runs fit P1 and the two
-    // counter arrays fit LDS; CAPF_SHARD_SB=0 (tuning) keeps the slice path
-    const int lsub = c5sb_lsub(nbl);
-    c.lsub = lsub;
-    c.nsb = nbl << lsub;
+    // one run per owned bucket and side (measured and removed: sub-bucket units
+    // and balanced key ranges — 8 Ki-node sub-buckets are skewed, p99 unit 1.7×:
+    // 0.296 vs 0.235 ms/rank at G = 8)
+    c.nsb = nbl;
     const int nr = 2 * c.nsb;
     c.copies = c5s_copies(nr);
     const int64_t rstride = ((int64_t)tile + 8 * (nr + 1) + 7) & ~int64_t(7);
@@ -3028,21 +1757,13 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
         const bool tr = trusted && W != 8 && c.upf;
         auto kern = tile == C5S_TILE ? (tr ? c5s_kernel_t<C5S_TILE, true>(W, kbits > 24, nh > 0)
                                            : c5s_kernel<C5S_TILE>(W, kbits > 24, nh > 0))
-                    : tile == 24576 ? (tr ? c5s_kernel_t<24576, true>(W, kbits > 24, nh > 0)
-                                          : c5s_kernel<24576>(W, kbits > 24, nh > 0))
                                      : (tr ? c5s_kernel_t<16384, true>(W, kbits > 24, nh > 0)
                                            : c5s_kernel<16384>(W, kbits > 24, nh > 0));
         hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(C5_BLOCK), 0, s->stream, c,
                            (uint16_t *)partb->p, (uint32_t *)meta->p, tile_acc, rstride);
         KERNEL_CHECK();
       }
-      if (lsub > 0 && c5s_mode() == 2) {
-        c5_bal_post(s, (const uint16_t *)partb->p, (const uint32_t *)meta->p, ntiles, c.nsb, 16 - lsub,
-                    rstride, d_acc);
-      } else if (lsub > 0) {
-        c5_sb_post(s, (const uint16_t *)partb->p, (const uint32_t *)meta->p, ntiles, c.t_in,
-                   c.nsb, 16 - lsub, rstride, d_acc);
-      } else {
+      {
         C3Sides sd;
         sd.split_x16 = c3_split_x16();
         sd.nb = nbl;
@@ -3052,33 +1773,20 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
         sd.t1[1] = ntiles;
         const int S = c5_slices(nr);
         const int64_t hl = (int64_t)nbl * C2_BW;
-        if (c5s_mode() == 3) {  // apportioned units: slices by unit, variable per run
-          const int umax = s->num_cus + 2 * nr;
-          BufPtr sl = s->alloc(4 * (int64_t)umax * C2_BW);
-          BufPtr tab = s->alloc(8 * (int64_t)nr);
-          uint32_t *sp = (uint32_t *)sl->p;
-          c5_post(s, (const uint16_t *)partb->p, (const uint32_t *)meta->p, sd, ntiles, rstride,
-                  n_in + n_out, (umax + nr - 1) / nr, sp, sp, C2_BW, true, (int32_t *)tab->p);
-          KernelTimer kt(s, "chain2_dot", 4.0 * umax * C2_BW);
-          hipLaunchKernelGGL(k_c5_dot_apportioned, dim3(dot_grid(s->num_cus)), dim3(256), 0, s->stream, sp,
-                             (const int32_t *)tab->p, nbl, d_acc);
-          KERNEL_CHECK();
-        } else {
-        const char *pk = getenv("CAPF_SHARD_PACKED");  // tuning: 0 = uint32 slices + overflow kernel
+        {
         // packed when several slices per run (G ≥ 4 at s24): with one slice the runs
         // are whole buckets whose hub bins log many hand-offs (measured G = 2:
         // packed dot 41 µs vs uint32 dot + overflow 22 µs)
-        sd.packed = pk ? atoi(pk) != 0 : S >= 2;
+        sd.packed = S >= 2;
         if (sd.packed) {
           // packed uint16 slices: half the slice bytes written by P3 and read by the dot
           const int64_t hw = (int64_t)nbl * C2_WORDS;
           BufPtr sl = s->alloc(8 * S * hw);
           uint32_t *si = (uint32_t *)sl->p, *so = si + S * hw;
-          const char *st = getenv("CAPF_SHARD_STATIC");  // tuning: 0 = device work list
           C3Ovf ovf{};
           BufPtr keep;
           c5_post(s, (const uint16_t *)partb->p, (const uint32_t *)meta->p, sd, ntiles, rstride,
-                  n_in + n_out, S, si, so, hw, !(st && atoi(st) == 0), nullptr, &ovf, &keep);
+                  n_in + n_out, S, si, so, hw, true, &ovf, &keep);
           KernelTimer kt(s, "chain2_dot", 8.0 * S * hw);
           hipLaunchKernelGGL(k_c5_dot_packed, dim3(grid_for(hw / 4, 1024, dot_grid(s->num_cus))), dim3(1024),
                              0, s->stream, si, so, S, hw, hw, ovf, d_acc);
@@ -3086,20 +1794,17 @@ bool chain2_sharded(Session *s, const ColView *cols, int64_t n_in, int64_t n_out
         } else {
         BufPtr sl = s->alloc(8 * S * hl);
         uint32_t *si = (uint32_t *)sl->p, *so = si + S * hl;
-        // static work list (no units / zero kernels): S tile ranges per run; a
-        // rank's runs hold ≤ 1.4 × the mean at s24 (no hub splits happen)
-        const char *st = getenv("CAPF_SHARD_STATIC");  // tuning: 0 = device work list
+        // static work list (no units kernel): S tile ranges per run; a rank's
+        // runs hold ≤ 1.4 × the mean at s24 (no hub splits happen)
         c5_post(s, (const uint16_t *)partb->p, (const uint32_t *)meta->p, sd, ntiles, rstride,
-                n_in + n_out, S, si, so, hl, !(st && atoi(st) == 0));
+                n_in + n_out, S, si, so, hl, true);
         KernelTimer kt(s, "chain2_dot", 8.0 * S * hl);
         // one block per CU: every block ends in one same-address device atomic
         // (G = 8 rank: 256 blocks 18.5 µs, 1024 24.4 µs, 2048 36 µs)
         // one block per CU (each block ends in one device atomic); 16 waves per
         // block keep 8·S·… loads in flight per CU (256 threads: latency bound)
-        const char *db = getenv("CAPF_DOT_BLOCK");  // tuning
-        const int dblk = db ? atoi(db) : 1024;
-        hipLaunchKernelGGL(k_c5_dot_slices, dim3(grid_for(hl / 4, dblk, dot_grid(s->num_cus))),
-                           dim3(dblk), 0, s->stream, si, so, S, hl, hl, d_acc);
+        hipLaunchKernelGGL(k_c5_dot_slices, dim3(grid_for(hl / 4, 1024, dot_grid(s->num_cus))),
+                           dim3(1024), 0, s->stream, si, so, S, hl, hl, d_acc);
         KERNEL_CHECK();
         }
         }
@@ -3301,7 +2006,6 @@ bool bits_count_partitioned(Session *s, const ColView &key, int64_t n, int64_t l
   c.len = (uint64_t)range;
   c.b0 = 0;
   c.nbl = nbl;
-  c.lsub = 0;
   c.nsb = nbl;
   c.mix = mix;
   const int nr = 2 * nbl;

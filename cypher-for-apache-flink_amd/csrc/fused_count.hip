@@ -1335,36 +1335,6 @@ __global__ void k_partial_minus_loops(const unsigned long long *acc, int64_t *ou
   if (threadIdx.x == 0) *out = (int64_t)(acc[0] - acc[1]);
 }
 
-// The synchronous fused count polls the coherent pinned word its last
-// workgroup stores the result into (system scope) instead of waiting for the
-// stream: the value lands before the grid's end-of-kernel flush and completion
-// signal.  The stream is queried every 1024 polls — a fault surfaces as an
-// error, a finished stream without the value is an internal error.
-// CAPF_SPIN_WAIT=1 selects it; measured at s24 (`profiles/r03_bench_s24_spin.jsonl`) the
-// median plan → scalar was 1.111 / 1.117 ms polling against 1.107 / 1.103 ms with
-// hipStreamSynchronize (which already spins) — no gain, so the default waits.
-constexpr int64_t FIN_PENDING = INT64_MIN;
-static bool spin_wait_enabled() {
-  static const bool on = getenv("CAPF_SPIN_WAIT") && atoi(getenv("CAPF_SPIN_WAIT")) == 1;
-  return on;
-}
-static int64_t spin_wait_fin(Session *s) {
-  for (uint32_t it = 1;; ++it) {
-    const int64_t v = __atomic_load_n(s->h_fin, __ATOMIC_ACQUIRE);
-    if (v != FIN_PENDING) return v;
-    if ((it & 1023) == 0) {
-      const hipError_t e = hipStreamQuery(s->stream);
-      if (e == hipSuccess) {
-        const int64_t w = __atomic_load_n(s->h_fin, __ATOMIC_ACQUIRE);
-        if (w != FIN_PENDING) return w;
-        illegal("internal: the fused count finished without delivering its result");
-      }
-      if (e != hipErrorNotReady) HIP_CHECK(e);
-    }
-    __builtin_ia32_pause();
-  }
-}
-
 static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t *out) {
   const double ta = host_trace() ? host_us() : 0;
   double tb = ta;
@@ -1394,7 +1364,6 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
   BufPtr h = s->alloc(8 * std::max<int64_t>(hlen, 1) + 64);
   BufPtr acc = s->alloc(24);  // Σ in·out, self-loops, the dot's done counter
   bool fin_done = false;  // the dot kernel wrote the async count
-  bool spin = false;      // ... into s->h_fin, polled by the synchronous path
   C2Spill spill;          // hand-offs P3 left for the dot (partitioned pipeline)
   bool acc_zeroed = false;  // the partitioned pipeline clears acc itself
   uint32_t *h1 = (uint32_t *)h->p;
@@ -1428,11 +1397,10 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
       in_range = in_range && st.min >= lo && st.max <= hi;
     }
     tb = host_trace() ? host_us() : 0;
-    // the count (Σ − loops) straight into the async slot, or into the pinned
-    // host word the synchronous path polls (no D2H copy, no stream wait)
-    spin = !s->async_out && s->h_fin && spin_wait_enabled();
-    int64_t *fin = s->async_out ? s->async_out : spin ? s->h_fin : s->h_scalars;
-    if (spin) __atomic_store_n(s->h_fin, FIN_PENDING, __ATOMIC_RELAXED);
+    // the count (Σ − loops) straight into the async slot or the pinned host
+    // scalar (no D2H copy; polling that word instead of the stream wait
+    // measured no gain at s24: 1.111 vs 1.107 ms)
+    int64_t *fin = s->async_out ? s->async_out : s->h_scalars;
     spill.fin = fin;
     if (n > 0 && want_part &&
         chain2_partitioned(s, pc, n, lo, hi, in_range, h1, h2, (unsigned long long *)acc->p, &spill)) {
@@ -1452,22 +1420,15 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
         KERNEL_CHECK();
       }
     }
-    if (spill.p3_dot) {
-      fin_done = true;  // P3's epilogue summed the buckets and wrote the count
-    } else {
+    {
       KernelTimer kt(s, "chain2_dot", 8.0 * dot_len);
       // one block per CU (s24: 256 blocks 24 µs, 2048 37 µs — same-address atomics)
       unsigned grid = grid_for(dot_len / 4 + 1, 256, dot_grid(s->num_cus));
       unsigned int *done = (unsigned int *)((unsigned long long *)acc->p + 2);
       if (spill.split)  // the bucket layout of the partitioned pipeline (+1 block: hand-offs)
-      {
-        // CAPF_DOT_BLOCK (tuning): workgroup size of the pairs dot (256 · 4 quads
-        // in flight per lane is ~4 waves per CU; larger groups keep more loads out)
-        const char *db = getenv("CAPF_DOT_BLOCK");
-        const int blk = db && (atoi(db) == 256 || atoi(db) == 512 || atoi(db) == 1024) ? atoi(db) : 256;
-        hipLaunchKernelGGL(k_chain2_dot_pairs, dim3(dot_grid(s->num_cus) + C2_HO_BLOCKS), dim3(blk), 0, s->stream, h1, h2,
-                           spill, (unsigned long long *)acc->p, fin, done);
-      }
+        // 256-lane groups: 4 quads in flight per lane, ~4 waves per CU (512 / 1024: no gain)
+        hipLaunchKernelGGL(k_chain2_dot_pairs, dim3(dot_grid(s->num_cus) + C2_HO_BLOCKS), dim3(256), 0, s->stream, h1,
+                           h2, spill, (unsigned long long *)acc->p, fin, done);
       else if (wb.ones)  // ONES: Σ in·out is invariant under the node_mix bijection (+1 block: hand-offs)
         hipLaunchKernelGGL(k_chain2_dot<true>, dim3(grid + (spill.n ? C2_HO_BLOCKS : 0)), dim3(256), 0, s->stream, h1, h2,
                            wb.map.m, lo, dot_len, (unsigned long long *)acc->p, fin, done, spill);
@@ -1495,9 +1456,7 @@ static bool run_chain2(Session *s, const JoinGraph &g, const Chain2 &c, uint64_t
     s->sync();
     s->profile["c3_handoffs"].bytes += (double)ne;
   }
-  if (fin_done && spin) {
-    *out = (uint64_t)spin_wait_fin(s);
-  } else if (fin_done) {
+  if (fin_done) {
     s->sync();
     *out = (uint64_t)s->h_scalars[0];
   } else {
@@ -2087,8 +2046,7 @@ extern "C" capf_status capf_chain2_sharded_count_diag(capf_session *cs, capf_tab
     auto owned = [&](const ColPtr &x) {
       return x->owner[3] == part && x->owner[0] == node_base && x->owner[1] == n_nodes && x->owner[2] == parts;
     };
-    const char *te = getenv("CAPF_SHARD_TRUST");  // 0 (tuning): always test every key
-    const bool trusted = owned(a) && owned(b) && !(te && atoi(te) == 0);
+    const bool trusted = owned(a) && owned(b);
     if (!chain2_sharded(s, cols, di->nrows, dout->nrows, node_base, n_nodes, parts, part,
                         d_partial, n_diag, n_hot, hot_ids, trusted))
       not_impl("sharded 2-hop count: shape outside the kernel's limits (buckets per rank, "

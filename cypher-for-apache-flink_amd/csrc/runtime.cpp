@@ -757,7 +757,6 @@ capf_status capf_session_create(int32_t device, void *hip_stream, capf_session *
   // no hipMalloc on the hot path after warm-up.
   HIP_CHECK(hipMalloc(&s.d_scalars, 64 * sizeof(int64_t)));
   HIP_CHECK(hipHostMalloc(&s.h_scalars, 64 * sizeof(int64_t), hipHostMallocDefault));
-  HIP_CHECK(hipHostMalloc(&s.h_fin, 64 * sizeof(int64_t), hipHostMallocCoherent));
   *out = cs;
   CAPF_API_END
 }
@@ -772,7 +771,6 @@ capf_status capf_session_destroy(capf_session *cs) {
   s.cache.release_all();
   (void)hipFree(s.d_scalars);
   (void)hipHostFree(s.h_scalars);
-  (void)hipHostFree(s.h_fin);
   if (s.own_stream) (void)hipStreamDestroy(s.stream);
   delete cs;
   CAPF_API_END

@@ -113,8 +113,8 @@ __global__ void k_tri_pairs(const uint64_t *ukeys, const uint32_t *cnt, const ui
 // Orient each pair from the lower to the higher (degree, id) rank; the loop
 // term Σ (L[u] + L[v])·f·b goes to acc[1].
 __global__ void k_tri_orient(const uint64_t *pair_uv, const uint2 *pair_fb, const uint32_t *nruns,
-                             const uint32_t *deg, const uint32_t *loops, const uint32_t *rank,
-                             uint64_t *okey, uint64_t *oval, unsigned long long *acc) {
+                             const uint32_t *deg, const uint32_t *loops, uint64_t *okey, uint64_t *oval,
+                             unsigned long long *acc) {
   __shared__ unsigned long long lds[17];
   const uint32_t nr = *nruns;
   unsigned long long lt = 0;
@@ -131,9 +131,7 @@ __global__ void k_tri_orient(const uint64_t *pair_uv, const uint2 *pair_fb, cons
     const bool fwd = ru < rv;
     const uint32_t p = fwd ? u : v, q = fwd ? v : u;
     const uint32_t f = fwd ? fb.x : fb.y, b = fwd ? fb.y : fb.x;  // f = #(p→q), b = #(q→p)
-    // rows and columns in (degree, id) rank order when `rank` is given: the
-    // lists of the high-rank nodes — short, read by many rows — sit together
-    okey[j] = rank ? ((uint64_t)rank[p] << 32) | rank[q] : ((uint64_t)p << 32) | q;
+    okey[j] = ((uint64_t)p << 32) | q;
     oval[j] = ((uint64_t)f << 32) | b;
     lt += (unsigned long long)(loops[u] + loops[v]) * f * b;
   }
@@ -142,24 +140,6 @@ __global__ void k_tri_orient(const uint64_t *pair_uv, const uint2 *pair_fb, cons
   if (threadIdx.x == 0 && tot) atomicAdd(&acc[1], tot);
 }
 
-__global__ void k_tri_rank_keys(const uint32_t *deg, uint64_t len, uint64_t *keys, uint32_t *ids) {
-  for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < len;
-       x += (uint64_t)gridDim.x * blockDim.x) {
-    keys[x] = ((uint64_t)deg[x] << 32) | x;
-    ids[x] = (uint32_t)x;
-  }
-}
-
-// label = position in DESCENDING (degree, id) order: the row cursor hands out
-// the hubs' rows first (ascending order left the heaviest rows for the tail)
-__global__ void k_tri_rank_scatter(const uint32_t *sorted_ids, uint64_t len, uint32_t *rank) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < len;
-       i += (uint64_t)gridDim.x * blockDim.x)
-    rank[sorted_ids[i]] = (uint32_t)(len - 1 - i);
-}
-
-// rowptr[x] = first oriented edge with p ≥ x (binary search), x ∈ [0, len];
-// rowptr[len] = P, the number of oriented edges (keys < TRI_NONE).
 __global__ void k_tri_rowptr(const uint64_t *okey, uint32_t nr, uint64_t len, uint32_t *rowptr) {
   for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x <= len;
        x += (uint64_t)gridDim.x * blockDim.x) {
@@ -293,28 +273,18 @@ __device__ inline void tri_row(uint32_t a, uint32_t dp, const uint32_t *rowptr, 
 // place.  (An LDS hash table instead of the sorted row, 12 KiB per wave,
 // measured 1.6× slower: the kernel waits on the N+(q) loads, so occupancy
 // wins.)
-// FILTER: a per-wave LDS bitmap of hash(w) over the staged N+(p) (8 Ki bits):
-// a probe whose bit is clear is a miss without the binary search (≈ 94 % of
-// the probes miss at s24).
-constexpr int TRI_BM_WORDS = 256;
-__device__ inline uint32_t tri_bit(uint32_t w) { return (w * 0x9E3779B1u) >> 19; }  // 13 bits
-
-template <bool FILTER, int ILP>
+template <int ILP>
 __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count(const uint32_t *rowptr,
                                                           const uint32_t *cols, const uint2 *vals,
                                                           uint64_t len, int parts, int part,
                                                           unsigned long long *cursor,
                                                           unsigned long long *acc) {
   __shared__ uint32_t s_cols[TRI_BLOCK / WAVE][TRI_CAP];
-  __shared__ uint32_t s_bm[FILTER ? TRI_BLOCK / WAVE : 1][FILTER ? TRI_BM_WORDS : 1];
   __shared__ TriBatch s_tab[TRI_BLOCK / WAVE];
   __shared__ unsigned long long lds[17];
   const int wv = threadIdx.x / WAVE, lane = lane_id();
   uint32_t *sc = s_cols[wv];
-  uint32_t *bm = s_bm[FILTER ? wv : 0];
   TriBatch &tb = s_tab[wv];
-  if (FILTER)
-    for (int k = lane; k < TRI_BM_WORDS; k += WAVE) bm[k] = 0;
   unsigned long long t = 0, probes = 0, hits = 0;
   for (;;) {
     unsigned long long r0 = 0;
@@ -331,28 +301,11 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_tri_count(const uint32_t *rowptr,
                 [&](int64_t x) { return row[x]; }, [](uint32_t) { return true; }, t, probes, hits);
         continue;
       }
-      for (uint32_t k = lane; k < dp; k += WAVE) {
-        const uint32_t w = cols[a + k];
-        sc[k] = w;
-        if (FILTER) {
-          const uint32_t h = tri_bit(w);
-          atomicOr(&bm[h >> 5], 1u << (h & 31));
-        }
-      }
+      for (uint32_t k = lane; k < dp; k += WAVE) sc[k] = cols[a + k];
       __builtin_amdgcn_wave_barrier();
       tri_row<ILP>(a, dp, rowptr, cols, vals, tb, [&](uint32_t k) { return sc[k]; },
-              [&](int64_t x) { return sc[x]; },
-              [&](uint32_t w) {
-                if (!FILTER) return true;
-                const uint32_t h = tri_bit(w);
-                return ((bm[h >> 5] >> (h & 31)) & 1u) != 0;
-              },
-              t, probes, hits);
+              [&](int64_t x) { return sc[x]; }, [](uint32_t) { return true; }, t, probes, hits);
       __builtin_amdgcn_wave_barrier();  // sc is rewritten by the next row
-      if (FILTER) {  // clear exactly the bits this row set
-        for (uint32_t k = lane; k < dp; k += WAVE) bm[tri_bit(sc[k]) >> 5] = 0;
-        __builtin_amdgcn_wave_barrier();
-      }
     }
   }
   unsigned long long tot;
@@ -390,13 +343,6 @@ struct TriBatch2 {
 
 // packed word's multiplicity nibbles say "look the pair up in vals"
 __device__ inline bool tri_esc(uint32_t word) { return ((word >> 24) & 15u) == 15u || (word >> 28) == 15u; }
-
-// CAPF_TRI_DIAG (profiling only, wrong counts): 1 = the streamed words are
-// loaded but not searched, 2 = searched but not loaded (a synthetic id per
-// position) — the time split of the count kernels between loads and searches
-__constant__ int c_tri_diag;
-// CAPF_TRI_GALLOP=1 (tuning): batch owners by galloping + a narrowed search
-__constant__ int c_tri_gallop;
 
 // (f, b) of a packed word, or of vals[e] when a nibble says "look it up"
 __device__ inline uint2 tri_fb(uint32_t word, const uint2 *vals, uint32_t e) {
@@ -446,62 +392,37 @@ __device__ inline void tri_row_packed(uint32_t nb, uint32_t ns, const uint32_t *
     // ping-pong words and batch owners of the steps in flight; a word's pcols
     // position is recomputed from its owner on the rare escape instead of held
     uint32_t w[2][ILP], bi[2][ILP];
-    uint32_t bcur = 0;  // owner of the last position issued (owners only grow along the batch)
     auto issue = [&](uint32_t t0, uint32_t (&ww)[ILP], uint32_t (&bb)[ILP]) {
       uint32_t xc[ILP];
 #pragma unroll
       for (int u = 0; u < ILP; ++u) xc[u] = min(t0 + u * WAVE + lane, total - 1);
-      if (c_tri_gallop) {
-        // the owners (last batch entry with pre[b] <= x) of a slice of 64
-        // consecutive positions span [first lane's, last lane's]: both found by
-        // galloping from the previous slice (wave-uniform, usually 0-2 steps),
-        // then each lane halves that span (usually 1-3 entries) instead of
-        // searching all 64 entries
+      // the ILP searches over all 64 entries in lockstep (positions as pointers:
+      // one add per step gives the probe address)
+      const uint32_t *bp[ILP];
+#pragma unroll
+      for (int u = 0; u < ILP; ++u) bp[u] = tb.pre;
+#pragma unroll
+      for (int st = WAVE / 2; st > 0; st >>= 1) {
+        const uint32_t *cand[ILP];
+        uint32_t v[ILP];
 #pragma unroll
         for (int u = 0; u < ILP; ++u) {
-          const uint32_t xf = min(t0 + u * WAVE, total - 1), xl = min(t0 + u * WAVE + WAVE - 1, total - 1);
-          while ((uint32_t)__builtin_amdgcn_readfirstlane(tb.pre[bcur + 1]) <= xf) ++bcur;
-          uint32_t bh = bcur;
-          while ((uint32_t)__builtin_amdgcn_readfirstlane(tb.pre[bh + 1]) <= xl) ++bh;
-          uint32_t base = bcur;
-          for (uint32_t len = bh - bcur + 1; len > 1;) {
-            const uint32_t half = len >> 1;
-            base = tb.pre[base + half] <= xc[u] ? base + half : base;
-            len -= half;
-          }
-          bb[u] = base;
-          bcur = bh;
-        }
-      } else {
-        // the ILP searches over all 64 entries in lockstep (positions as pointers:
-        // one add per step gives the probe address)
-        const uint32_t *bp[ILP];
-#pragma unroll
-        for (int u = 0; u < ILP; ++u) bp[u] = tb.pre;
-#pragma unroll
-        for (int st = WAVE / 2; st > 0; st >>= 1) {
-          const uint32_t *cand[ILP];
-          uint32_t v[ILP];
-#pragma unroll
-          for (int u = 0; u < ILP; ++u) {
-            cand[u] = bp[u] + st;
-            v[u] = *cand[u];
-          }
-#pragma unroll
-          for (int u = 0; u < ILP; ++u) bp[u] = v[u] <= xc[u] ? cand[u] : bp[u];
+          cand[u] = bp[u] + st;
+          v[u] = *cand[u];
         }
 #pragma unroll
-        for (int u = 0; u < ILP; ++u) bb[u] = (uint32_t)(bp[u] - tb.pre);
+        for (int u = 0; u < ILP; ++u) bp[u] = v[u] <= xc[u] ? cand[u] : bp[u];
       }
+#pragma unroll
+      for (int u = 0; u < ILP; ++u) bb[u] = (uint32_t)(bp[u] - tb.pre);
 #pragma unroll
       for (int u = 0; u < ILP; ++u) {
         const uint32_t pp = tb.qa[bb[u]] + (xc[u] - tb.pre[bb[u]]);
-        ww[u] = c_tri_diag == 2 ? (pp * 2654435761u) & TRI_M24 : pcols[pp];
+        ww[u] = pcols[pp];
         if (t0 + u * WAVE + lane >= total) ww[u] = 0xFFFFFFFFu;  // past the end (the load stays unconditional)
       }
     };
     auto probe = [&](const uint32_t (&ww)[ILP], const uint32_t (&bb)[ILP], uint32_t t0) {
-      if (c_tri_diag == 1) return;
       uint32_t wk[ILP], pw[ILP], pos[ILP];
       bool live[ILP], hit[ILP];
 #pragma unroll
@@ -527,7 +448,6 @@ __device__ inline void tri_row_packed(uint32_t nb, uint32_t ns, const uint32_t *
         }
       }
     };
-    if (c_tri_diag == 3) continue;  // (profiling only: staging and batch tables, no probes)
     if (total > 0) issue(0, w[0], bi[0]);
     for (uint32_t t0 = 0; t0 < total; t0 += 2 * STEP) {
       if (t0 + STEP < total) issue(t0 + STEP, w[1], bi[1]);
@@ -684,136 +604,6 @@ __device__ inline void tri_stage_rot(uint32_t *ids, const uint32_t *row, uint32_
   }
 }
 
-// ------------------------------------------------- LDS hash of a staged list
-// A staged list (≤ TRI_CAP words) is searched through an open-addressing table
-// in the wave's LDS slice instead of a binary search over its sorted copy: one
-// 16-B read of a 4-slot bucket (load ≤ ½, so a bucket rarely overflows into the
-// next) against ~log2(n) dependent reads — the binary search was most of the
-// count kernels' time (s24, CAPF_TRI_DIAG: pass B 244 ms searching vs 89 ms
-// loading).  Slots hold the packed words (none equals TRI_EMPTY: k_tri_pack
-// clears b when f = 15); an escape word's vals index comes from a binary
-// search of the list in global memory (rare multi-edges).
-constexpr uint32_t TRI_EMPTY = 0xFFFFFFFFu;
-
-struct TriHash {
-  const uint32_t *tab;
-  const uint32_t *row;  // the list in global memory (escape positions)
-  uint32_t mask, n, a;
-  int shift;
-};
-
-__device__ inline uint32_t tri_hash(uint32_t wk, int shift) { return (wk * 0x9E3779B1u) >> shift; }
-
-// Stage row[0..n) (vals index a) into the wave's table tab (≥ 2n words).
-__device__ inline TriHash tri_stage_hash(uint32_t *tab, const uint32_t *row, uint32_t n, uint32_t a) {
-  const int lane = lane_id();
-  uint32_t nbk = 16;  // buckets of 4 slots, 4·nbk ≥ 2n
-  while (nbk * 2 < n) nbk <<= 1;
-  const int shift = 32 - (31 - __builtin_clz(nbk));
-  uint4 *t4 = reinterpret_cast<uint4 *>(tab);
-  __builtin_amdgcn_wave_barrier();  // the previous list's searches are done
-  for (uint32_t i = lane; i < nbk; i += WAVE) t4[i] = make_uint4(TRI_EMPTY, TRI_EMPTY, TRI_EMPTY, TRI_EMPTY);
-  __builtin_amdgcn_wave_barrier();
-  for (uint32_t k = lane; k < n; k += WAVE) {
-    const uint32_t w = row[k];  // never TRI_EMPTY (k_tri_pack)
-    uint32_t b = tri_hash(w & TRI_M24, shift);
-    for (bool done = false; !done; b = (b + 1) & (nbk - 1)) {
-#pragma unroll
-      for (int j = 0; j < 4 && !done; ++j) done = atomicCAS(&tab[4 * b + j], TRI_EMPTY, w) == TRI_EMPTY;
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-  return TriHash{tab, row, nbk - 1, n, a, shift};
-}
-
-__device__ inline bool tri_hfind(const TriHash &h, uint32_t wk, uint32_t &pw, uint32_t &pos) {
-  const uint4 *t4 = reinterpret_cast<const uint4 *>(h.tab);
-  for (uint32_t b = tri_hash(wk, h.shift);; b = (b + 1) & h.mask) {
-    const uint4 v = t4[b];
-    uint32_t w = TRI_EMPTY;
-    if ((v.x & TRI_M24) == wk && v.x != TRI_EMPTY) w = v.x;
-    if ((v.y & TRI_M24) == wk && v.y != TRI_EMPTY) w = v.y;
-    if ((v.z & TRI_M24) == wk && v.z != TRI_EMPTY) w = v.z;
-    if ((v.w & TRI_M24) == wk && v.w != TRI_EMPTY) w = v.w;
-    if (w != TRI_EMPTY) {
-      pw = w;
-      if (tri_esc(w)) {  // escape: the pair's vals index
-        uint32_t w2;
-        tri_bsearch([&](uint32_t x) { return h.row[x]; }, h.n, h.a, wk, w2, pos);
-      }
-      return true;
-    }
-    if (v.x == TRI_EMPTY || v.y == TRI_EMPTY || v.z == TRI_EMPTY || v.w == TRI_EMPTY) return false;
-  }
-}
-
-struct TriHashFind {
-  TriHash h;
-  template <int ILP>
-  __device__ inline void batch(const uint32_t (&wk)[ILP], const bool (&live)[ILP], bool (&hit)[ILP],
-                               uint32_t (&pw)[ILP], uint32_t (&pos)[ILP]) const {
-#pragma unroll
-    for (int u = 0; u < ILP; ++u) hit[u] = live[u] && tri_hfind(h, wk[u], pw[u], pos[u]);
-  }
-};
-
-template <int ILP, bool SPLIT = false, int HCAP = 0>
-__global__ __launch_bounds__(TRI_BLOCK) void k_tri_count_packed(const uint32_t *rowptr,
-                                                                 const uint32_t *pcols, const uint2 *vals,
-                                                                 uint64_t len, int parts, int part,
-                                                                 unsigned long long *cursor,
-                                                                 unsigned long long *acc) {
-  // HCAP > 0: staged lists of ≤ HCAP words hashed into 2·HCAP slots; 0: sorted copies of ≤ TRI_CAP
-  constexpr bool HASH = HCAP > 0;
-  constexpr uint32_t CAP = HASH ? HCAP : TRI_CAP;
-  __shared__ __attribute__((aligned(16))) uint32_t s_cols[TRI_BLOCK / WAVE][HASH ? 2 * HCAP : TRI_CAP];
-
-  __shared__ TriBatch2 s_tab[TRI_BLOCK / WAVE];
-  __shared__ unsigned long long lds[17];
-  const int wv = threadIdx.x / WAVE, lane = lane_id();
-  uint32_t *sc = s_cols[wv];
-  TriBatch2 &tb = s_tab[wv];
-  unsigned long long t = 0, probes = 0, hits = 0;
-  for (;;) {
-    unsigned long long r0 = 0;
-    if (lane == 0) r0 = atomicAdd(cursor, 1ull);
-    r0 = ((unsigned long long)__shfl((long long)r0, 0, WAVE) * parts + part) * TRI_CHUNK;
-    if (r0 >= len) break;
-    const uint64_t r1 = min<uint64_t>(r0 + TRI_CHUNK, len);
-    for (uint64_t p = r0; p < r1; ++p) {
-      const uint32_t a = rowptr[p], dp = rowptr[p + 1] - a;
-      if (dp < 2) continue;  // a triangle needs two out-neighbours at its lowest vertex
-      const uint32_t *row = pcols + a;
-      auto pqe = [&](uint32_t k) { return a + k; };
-      if (dp > CAP) {  // rare long row: searched in global memory
-        tri_row_packed<ILP, SPLIT>(dp, dp, pcols, vals, tb, [&](uint32_t k) { return tri_qrow(rowptr, row[k]); },
-                                   tri_sorted([&](uint32_t x) { return row[x]; }, dp, a),
-                                   pqe, t, probes, hits);
-        continue;
-      }
-      if constexpr (HASH) {
-        const TriHash h = tri_stage_hash(sc, row, dp, a);
-        tri_row_packed<ILP, SPLIT>(dp, dp, pcols, vals, tb, [&](uint32_t k) { return tri_qrow(rowptr, row[k]); },
-                                   TriHashFind{h},
-                                   pqe, t, probes, hits);
-      } else {
-        tri_stage_rot(sc, row, dp);
-        __builtin_amdgcn_wave_barrier();
-        tri_row_packed<ILP, SPLIT>(dp, dp, pcols, vals, tb, [&](uint32_t k) { return tri_qrow(rowptr, row[k]); },
-                                   TriSortedRot{sc, dp, a}, pqe, t, probes, hits);
-      }
-      __builtin_amdgcn_wave_barrier();  // sc is rewritten by the next row
-    }
-  }
-  unsigned long long tot;
-  block_exclusive_scan(t, lds, tot);
-  if (threadIdx.x == 0 && tot) atomicAdd(&acc[0], tot);
-  block_exclusive_scan(lane_id() == 0 ? probes : 0ull, lds, tot);
-  if (threadIdx.x == 0 && tot) atomicAdd(&acc[4], tot);
-  block_exclusive_scan(lane_id() == 0 ? hits : 0ull, lds, tot);
-  if (threadIdx.x == 0 && tot) atomicAdd(&acc[5], tot);
-}
-
 // Pass B of the two-pass schedule (shorter list streamed): the edges p→q with
 // |N+(p)| < |N+(q)| are counted at q — N+(q) staged in LDS once, the in-list
 // p's (sorted by q, chunks of TRI_BCHUNK entries per work item so a hub's long
@@ -854,16 +644,14 @@ struct TriPassB {
   uint32_t nitems;
 };
 
-template <int ILP, int HCAP = 0, int WPE = 5, int SCAP = TRI_CAP>
+template <int ILP, int WPE, int SCAP = TRI_CAP>
 __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_tri_count_passb(const uint32_t *rowptr, const uint32_t *pcols,
                                                                 const uint2 *vals, TriPassB b, int parts,
                                                                 int part, int grab, int xcd,
                                                                 unsigned long long *cursor,
                                                                 unsigned long long *acc) {
-  // HCAP > 0: staged lists of ≤ HCAP words hashed into 2·HCAP slots; 0: sorted copies of ≤ TRI_CAP
-  constexpr bool HASH = HCAP > 0;
-  constexpr uint32_t CAP = HASH ? HCAP : SCAP;
-  __shared__ __attribute__((aligned(16))) uint32_t s_cols[TRI_BLOCK / WAVE][HASH ? 2 * HCAP : SCAP];
+  constexpr uint32_t CAP = SCAP;  // staged lists of ≤ SCAP words as sorted rotated copies
+  __shared__ __attribute__((aligned(16))) uint32_t s_cols[TRI_BLOCK / WAVE][SCAP];
 
   __shared__ TriBatch2 s_tab[TRI_BLOCK / WAVE];
   __shared__ unsigned long long lds[17];
@@ -872,7 +660,6 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))
   TriBatch2 &tb = s_tab[wv];
   unsigned long long t = 0, probes = 0, hits = 0;
   uint32_t staged = 0xFFFFFFFFu;  // q whose list sits in sc
-  TriHash h{};
   for (;;) {
     const unsigned long long c0 = tri_dequeue(cursor, xcd, parts, part, grab);
     if (c0 >= b.nitems) break;
@@ -894,24 +681,13 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))
         staged = 0xFFFFFFFFu;
         continue;
       }
-      if constexpr (HASH) {
-        if (q != staged) {
-          h = tri_stage_hash(sc, row, dq, a);
-          staged = q;
-        }
-        tri_row_packed<ILP, false, true>(n, dq, pcols, vals, tb, qs,
-                                         TriHashFind{h},
-                                         pqe, t, probes, hits);
-      } else {
-        if (q != staged) {
-          __builtin_amdgcn_wave_barrier();  // the previous list's searches are done
-          tri_stage_rot(sc, row, dq);
-          __builtin_amdgcn_wave_barrier();
-          staged = q;
-        }
-        tri_row_packed<ILP, false, true>(n, dq, pcols, vals, tb, qs, TriSortedRot{sc, dq, a},
-                                         pqe, t, probes, hits);
+      if (q != staged) {
+        __builtin_amdgcn_wave_barrier();  // the previous list's searches are done
+        tri_stage_rot(sc, row, dq);
+        __builtin_amdgcn_wave_barrier();
+        staged = q;
       }
+      tri_row_packed<ILP, false, true>(n, dq, pcols, vals, tb, qs, TriSortedRot{sc, dq, a}, pqe, t, probes, hits);
     }
   }
   unsigned long long tot;
@@ -1018,21 +794,14 @@ struct TriGraph {
   uint64_t len = 0;
 };
 
-// CAPF_TRI_ROWS=0 (tuning): batch entries look their list up in rowptr
-static bool tri_list_rows_on() {
-  const char *e = getenv("CAPF_TRI_ROWS");
-  return !(e && atoi(e) == 0);
-}
-
 // In-lists and work items of pass B (built with the CSR, cached with it).
 static void tri_build_passb(Session *s, const uint64_t *okey, TriGraph &g) {
   const uint32_t P = g.P;
   KernelTimer kt(s, "tri_passb_build", 40.0 * P);
-  // CAPF_TRI_PBLOCK (tuning): log2 of the N+(p) words per p-block (default 2^24 = 64 MB)
-  const char *pb = getenv("CAPF_TRI_PBLOCK");
-  // ≥ 16: the pass-B key holds the p-block id (ap >> pshift, ap < 2^32) in 16 bits at bit 48
+  // log2 of the N+(p) words per p-block; ≥ 16: the pass-B key holds the p-block
+  // id (ap >> pshift, ap < 2^32) in 16 bits at bit 48.
   // s24: 2^22 355 ms, 2^23 338, 2^24 333, 2^25 326 (pass B)
-  const int pshift = pb ? std::max(16, std::min(31, atoi(pb))) : 25;
+  constexpr int pshift = 25;
   BufPtr keys = s->alloc(8 * (int64_t)P), skeys = s->alloc(8 * (int64_t)P);
   BufPtr eidx = s->alloc(4 * (int64_t)P), seidx = s->alloc(4 * (int64_t)P);
   hipLaunchKernelGGL(k_tri_passb_keys, dim3(grid_for(P, 256, 256 * 64)), dim3(256), 0, s->stream, okey,
@@ -1062,12 +831,10 @@ static void tri_build_passb(Session *s, const uint64_t *okey, TriGraph &g) {
                      (uint32_t *)g.in_words->p);
   KERNEL_CHECK();
   HIP_CHECK(hipMemcpyAsync(g.in_eidx->p, seidx->p, 4 * (size_t)g.nB, hipMemcpyDeviceToDevice, s->stream));
-  if (tri_list_rows_on()) {
-    g.in_rows = s->alloc(8 * (int64_t)g.nB);
-    hipLaunchKernelGGL(k_tri_list_rows, dim3(grid_for(g.nB, 256, 256 * 64)), dim3(256), 0, s->stream,
-                       (const uint32_t *)g.in_words->p, (const uint32_t *)g.rowptr->p, g.nB, (uint2 *)g.in_rows->p);
-    KERNEL_CHECK();
-  }
+  g.in_rows = s->alloc(8 * (int64_t)g.nB);
+  hipLaunchKernelGGL(k_tri_list_rows, dim3(grid_for(g.nB, 256, 256 * 64)), dim3(256), 0, s->stream,
+                     (const uint32_t *)g.in_words->p, (const uint32_t *)g.rowptr->p, g.nB, (uint2 *)g.in_rows->p);
+  KERNEL_CHECK();
   // segments = runs of equal (p-block, q) → work items of ≤ TRI_BCHUNK entries
   BufPtr seg = s->alloc(8 * (int64_t)g.nB), useg = s->alloc(8 * (int64_t)g.nB);
   BufPtr cnt = s->alloc(4 * ((int64_t)g.nB + 1)), nseg_d = s->alloc(16);
@@ -1087,8 +854,7 @@ static void tri_build_passb(Session *s, const uint64_t *okey, TriGraph &g) {
     return rocprim::exclusive_scan(t, n, (const uint32_t *)cnt->p, (uint32_t *)start->p, 0u, (size_t)nseg,
                                    rocprim::plus<uint32_t>(), s->stream);
   });
-  // CAPF_TRI_BCHUNK (tuning): in-list entries per pass-B work item
-  const uint32_t bchunk = getenv("CAPF_TRI_BCHUNK") ? (uint32_t)std::max(64, atoi(getenv("CAPF_TRI_BCHUNK"))) : TRI_BCHUNK;
+  const uint32_t bchunk = TRI_BCHUNK;  // in-list entries per pass-B work item
   hipLaunchKernelGGL(k_tri_seg_items, dim3(grid_for(nseg, 256, 256 * 64)), dim3(256), 0, s->stream,
                      (const uint32_t *)cnt->p, nseg, bchunk, (uint32_t *)nit->p);
   KERNEL_CHECK();
@@ -1110,7 +876,7 @@ static void tri_build_passb(Session *s, const uint64_t *okey, TriGraph &g) {
 // Pass A over q-tiled work items (see tri_build_qtiles): item (p, k0, k1) probes
 // the q's N+(p)[k0, k1) — N+(p) staged in LDS (≤ TRI_CAP words) or searched in
 // place — with the pass-A rule (edges with |N+(p)| < |N+(q)| belong to pass B).
-template <int ILP, int HCAP = 0, int WPE = 5, int SCAP = TRI_CAP>
+template <int ILP, int WPE, int SCAP = TRI_CAP>
 __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_tri_count_qtiled(const uint32_t *rowptr, const uint32_t *pcols,
                                                                  const uint2 *vals, const uint2 *erow,
                                                                  const uint4 *items,
@@ -1118,10 +884,8 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))
                                                                  int xcd,
                                                                  unsigned long long *cursor,
                                                                  unsigned long long *acc) {
-  // HCAP > 0: staged lists of ≤ HCAP words hashed into 2·HCAP slots; 0: sorted copies of ≤ TRI_CAP
-  constexpr bool HASH = HCAP > 0;
-  constexpr uint32_t CAP = HASH ? HCAP : SCAP;
-  __shared__ __attribute__((aligned(16))) uint32_t s_cols[TRI_BLOCK / WAVE][HASH ? 2 * HCAP : SCAP];
+  constexpr uint32_t CAP = SCAP;  // staged lists of ≤ SCAP words as sorted rotated copies
+  __shared__ __attribute__((aligned(16))) uint32_t s_cols[TRI_BLOCK / WAVE][SCAP];
 
   __shared__ TriBatch2 s_tab[TRI_BLOCK / WAVE];
   __shared__ unsigned long long lds[17];
@@ -1130,7 +894,6 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))
   TriBatch2 &tb = s_tab[wv];
   unsigned long long t = 0, probes = 0, hits = 0;
   uint32_t staged = 0xFFFFFFFFu;  // p whose list sits in sc
-  TriHash h{};
   for (;;) {
     const unsigned long long c0 = tri_dequeue(cursor, xcd, parts, part, grab);
     if (c0 >= nitems) break;
@@ -1149,24 +912,13 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))
         staged = 0xFFFFFFFFu;
         continue;
       }
-      if constexpr (HASH) {
-        if (p != staged) {
-          h = tri_stage_hash(sc, row, dp, a);
-          staged = p;
-        }
-        tri_row_packed<ILP, true>(nb, dp, pcols, vals, tb, qrow,
-                                  TriHashFind{h},
-                                  pqe, t, probes, hits);
-      } else {
-        if (p != staged) {
-          __builtin_amdgcn_wave_barrier();  // the previous list's searches are done
-          tri_stage_rot(sc, row, dp);
-          __builtin_amdgcn_wave_barrier();
-          staged = p;
-        }
-        tri_row_packed<ILP, true>(nb, dp, pcols, vals, tb, qrow, TriSortedRot{sc, dp, a},
-                                  pqe, t, probes, hits);
+      if (p != staged) {
+        __builtin_amdgcn_wave_barrier();  // the previous list's searches are done
+        tri_stage_rot(sc, row, dp);
+        __builtin_amdgcn_wave_barrier();
+        staged = p;
       }
+      tri_row_packed<ILP, true>(nb, dp, pcols, vals, tb, qrow, TriSortedRot{sc, dp, a}, pqe, t, probes, hits);
     }
   }
   unsigned long long tot;
@@ -1300,33 +1052,11 @@ static void tri_build(Session *s, const ColView &src, const ColView &dst, int64_
   }
   uint64_t *okey = (uint64_t *)ukeys->p;  // runs ≤ m: the run keys are dead after the merge
   uint64_t *oval = kout;
-  // CAPF_TRI_RANK=1 (tuning, off): the CSR relabelled by descending (degree,
-  // id) rank (the count is label-independent).  Measured at s24: 1.24 s (1.46 s
-  // ascending) against 0.96 s in id order — R-MAT's own id order keeps the hub
-  // lists better spread over the row stream; L2 hit rate 17 % → 21 % only.
-  BufPtr rank;
-  static const bool by_rank = getenv("CAPF_TRI_RANK") && atoi(getenv("CAPF_TRI_RANK")) == 1;
-  if (by_rank && len > 0) {
-    KernelTimer kt(s, "tri_rank", 24.0 * len);
-    BufPtr rk = s->alloc(8 * len), rk2 = s->alloc(8 * len), ids = s->alloc(4 * len), ids2 = s->alloc(4 * len);
-    hipLaunchKernelGGL(k_tri_rank_keys, dim3(grid_for((int64_t)len, 256)), dim3(256), 0, s->stream,
-                       (const uint32_t *)deg->p, len, (uint64_t *)rk->p, (uint32_t *)ids->p);
-    KERNEL_CHECK();
-    rocprim_call(s, [&](void *t, size_t &n) {
-      return rocprim::radix_sort_pairs(t, n, (const uint64_t *)rk->p, (uint64_t *)rk2->p,
-                                       (const uint32_t *)ids->p, (uint32_t *)ids2->p, (size_t)len, 0, 64,
-                                       s->stream);
-    });
-    rank = s->alloc(4 * len);
-    hipLaunchKernelGGL(k_tri_rank_scatter, dim3(grid_for((int64_t)len, 256)), dim3(256), 0, s->stream,
-                       (const uint32_t *)ids2->p, len, (uint32_t *)rank->p);
-    KERNEL_CHECK();
-  }
   {
     KernelTimer kt(s, "tri_orient", 32.0 * m);
     hipLaunchKernelGGL(k_tri_orient, dim3(grid), dim3(256), 0, s->stream, (const uint64_t *)pair_uv,
                        (const uint2 *)pair_fb->p, (const uint32_t *)nruns->p, (const uint32_t *)deg->p,
-                       (const uint32_t *)loops, rank ? (const uint32_t *)rank->p : nullptr, okey, oval, acc);
+                       (const uint32_t *)loops, okey, oval, acc);
     KERNEL_CHECK();
   }
   uint32_t nr = 0;
@@ -1364,47 +1094,29 @@ static void tri_build(Session *s, const ColView &src, const ColView &dst, int64_
     hipLaunchKernelGGL(k_tri_pack, dim3(grid_for(g.P, 256, 256 * 64)), dim3(256), 0, s->stream,
                        (const uint32_t *)g.cols->p, (const uint2 *)g.vals->p, g.P, (uint32_t *)g.pcols->p);
     KERNEL_CHECK();
-    if (tri_list_rows_on()) {
-      g.erow = s->alloc(8 * (int64_t)g.P);
-      hipLaunchKernelGGL(k_tri_list_rows, dim3(grid_for(g.P, 256, 256 * 64)), dim3(256), 0, s->stream,
-                         (const uint32_t *)g.pcols->p, (const uint32_t *)g.rowptr->p, g.P, (uint2 *)g.erow->p);
-      KERNEL_CHECK();
-    }
+    g.erow = s->alloc(8 * (int64_t)g.P);
+    hipLaunchKernelGGL(k_tri_list_rows, dim3(grid_for(g.P, 256, 256 * 64)), dim3(256), 0, s->stream,
+                       (const uint32_t *)g.pcols->p, (const uint32_t *)g.rowptr->p, g.P, (uint2 *)g.erow->p);
+    KERNEL_CHECK();
     tri_build_passb(s, (const uint64_t *)ok2->p, g);
-    // CAPF_TRI_QTILE (tuning): log2 of the words per pass-A tile; 0 = row by row
+    // CAPF_TRI_QTILE (test hook): log2 of the words per pass-A tile (small tiles
+    // cut rows into many items: the tests' way to reach the item boundaries)
     const char *qt = getenv("CAPF_TRI_QTILE");
-    const int qshift = qt ? atoi(qt) : TRI_QTILE_DEFAULT;
-    if (qshift > 0 && g.in_words) tri_build_qtiles(s, (const uint64_t *)ok2->p, g, std::max(12, std::min(30, qshift)));
+    const int qshift = qt && atoi(qt) > 0 ? atoi(qt) : TRI_QTILE_DEFAULT;
+    tri_build_qtiles(s, (const uint64_t *)ok2->p, g, std::max(12, std::min(30, qshift)));
   }
 }
 
-// The sorted-copy count kernel for (ILP, waves/SIMD it is compiled for, LDS
-// copy capacity); unlisted combinations fall back to ILP 4 / 6 waves / TRI_CAP.
-struct TriPassbK {
-  template <int I, int W, int C>
-  static constexpr auto get() { return k_tri_count_passb<I, 0, W, C>; }
-};
-struct TriQtiledK {
-  template <int I, int W, int C>
-  static constexpr auto get() { return k_tri_count_qtiled<I, 0, W, C>; }
-};
-template <class K>
-static auto tri_pick(int ilp, int wpe, int scap) {
-  if (ilp <= 2) return K::template get<2, 5, TRI_CAP>();
-  if (ilp >= 6) return K::template get<6, 5, TRI_CAP>();
-  if (ilp == 3) return wpe == 5 ? K::template get<3, 5, TRI_CAP>()
-                       : wpe == 7 ? K::template get<3, 7, TRI_CAP>()
-                       : wpe == 8 && scap == 512 ? K::template get<3, 8, 512>()
-                       : wpe == 8 ? K::template get<3, 8, TRI_CAP>()
-                                                 : K::template get<3, 6, TRI_CAP>();
-  if (wpe == 4) return K::template get<4, 4, TRI_CAP>();
-  if (wpe == 5) return K::template get<4, 5, TRI_CAP>();
-  if (wpe == 7 && scap == 768) return K::template get<4, 7, 768>();
-  if (wpe == 7) return K::template get<4, 7, TRI_CAP>();
-  if (wpe == 8 && scap != 512) return K::template get<4, 8, TRI_CAP>();
-  if (wpe == 8 && scap == 512) return K::template get<4, 8, 512>();
-  return K::template get<4, 6, TRI_CAP>();
-}
+// Count kernels: ILP 4 positions per lane in flight, compiled for 8 waves/SIMD
+// (the rotated-word LDS copies take 18.8 KB per 4-wave block, 8 blocks fit a
+// CU; s24, ILP 4: 4 waves 308 ms, 5 268, 6 240, 7 226, 8 222 ms), staged
+// lists of ≤ TRI_CAP words.  Pass A deals its grabs (2 items) to the 8 XCD
+// groups in chunks of TRI_XCHUNK grabs (tri_dequeue: 121 → 103 ms at s24);
+// pass B takes 4 items per grab from one cursor (per-XCD cursors were slower).
+// Measured and removed: an LDS hash table per staged list (290 vs 222 ms),
+// galloping batch-owner search, an LDS bitmap pre-filter, relabelling the CSR
+// by degree rank, larger grabs (4/4 319 ms … 128/32 720 ms).
+constexpr int TRI_WPE = 8, TRI_GRAB_A = 2, TRI_GRAB_B = 4;
 
 // Device count (int64 at d_out) of the directed triangle over rels (src, dst)
 // with endpoints in [lo, lo + len), restricted to part `part` of `parts`
@@ -1432,27 +1144,13 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
     srcc->index_key[1] = (int64_t)len;
   }
   const TriGraph &g = *gp;
-  {
-    static const int diag = getenv("CAPF_TRI_DIAG") ? atoi(getenv("CAPF_TRI_DIAG")) : 0;
-    // CAPF_TRI_GALLOP=1 (tuning, off): s24 318.5 vs 320.1 ms — no gain
-    const int gallop = getenv("CAPF_TRI_GALLOP") ? atoi(getenv("CAPF_TRI_GALLOP")) : 0;
-    static int set_diag = -1, set_gallop = -1;
-    if (diag != set_diag) {
-      HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_tri_diag), &diag, sizeof(int)));
-      set_diag = diag;
-    }
-    if (gallop != set_gallop) {
-      HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_tri_gallop), &gallop, sizeof(int)));
-      set_gallop = gallop;
-    }
-  }
   // per-query accumulators: T, the cached pair-loop term, Σ L(L−1)(L−2), the
   // row cursor, probes, hits
   BufPtr qacc = s->alloc(64);  // + [6] the pass-B cursor
   // per-XCD-group cursors of the q-tiled pass A and of pass B (tri_dequeue)
-  BufPtr xcur = s->alloc(2 * 8 * 32 * 8);
-  HIP_CHECK(hipMemsetAsync(xcur->p, 0, 2 * 8 * 32 * 8, s->stream));
-  unsigned long long *xa = (unsigned long long *)xcur->p, *xb = xa + 8 * 32;
+  BufPtr xcur = s->alloc(8 * 32 * 8);  // per-XCD-group cursors of pass A (tri_dequeue)
+  HIP_CHECK(hipMemsetAsync(xcur->p, 0, 8 * 32 * 8, s->stream));
+  unsigned long long *xa = (unsigned long long *)xcur->p;
   HIP_CHECK(hipMemsetAsync(qacc->p, 0, 64, s->stream));
   if (part == 0)
     HIP_CHECK(hipMemcpyAsync((char *)qacc->p + 8, (const char *)g.acc->p + 8, 8,
@@ -1465,64 +1163,16 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
     KERNEL_CHECK();
   }
   if (g.P > 0) {
-    // CAPF_TRI_PACKED=0 (tuning): the unpacked kernel (multiplicities loaded from vals per hit)
-    const bool packed = !(getenv("CAPF_TRI_PACKED") && atoi(getenv("CAPF_TRI_PACKED")) == 0);
     // timers are named after the kernels that run (bench.py matches them against the
     // kernel names of the committed PMC counters)
-    static const bool filter = getenv("CAPF_TRI_FILTER") && atoi(getenv("CAPF_TRI_FILTER")) == 1;  // measured slower (0.98 vs 0.94 s at s24)
-    static const int ilp = getenv("CAPF_TRI_ILP") ? atoi(getenv("CAPF_TRI_ILP")) : TRI_ILP;  // tuning
-    // CAPF_TRI_HASH (tuning): 0 = staged lists binary-searched in sorted LDS copies;
-    // 512 / 1024 = lists up to that many words hashed in LDS (longer: global search)
-    // (s24, lockstep searches: sorted 314 ms, hash 1024 454 ms — kept off)
-    const int hash = getenv("CAPF_TRI_HASH") ? atoi(getenv("CAPF_TRI_HASH")) : 0;
-    // work items per dequeue of the shared cursor (tuning).  One cursor word
-    // serves ≈ 88 dequeues/µs (MI355X_MICROARCH.md): with no probes
-    // (CAPF_TRI_DIAG=3) pass A's 2.1e7 items (s24) take 64 ms at 4 per grab and
-    // 9.5 ms at 32 — but with the probes the kernels dequeue at half that rate,
-    // and larger grabs widen the window of items in flight beyond what the
-    // caches hold: 4/4 319 ms, 32/8 415, 64/16 511, 128/32 720 ms
-    const int grab_a = std::max(1, getenv("CAPF_TRI_GRAB_A") ? atoi(getenv("CAPF_TRI_GRAB_A")) : 2);
-    const int grab_b = std::max(1, getenv("CAPF_TRI_GRAB_B") ? atoi(getenv("CAPF_TRI_GRAB_B")) : 4);
-    // CAPF_TRI_WPE (tuning): waves/SIMD the count kernels are compiled for.  With
-    // the rotated-word LDS copies a 4-wave block takes 18.8 KB, so 8 fit a CU;
-    // more waves cost less than the registers (and the scratch spills) they take.
-    // s24, ILP 4: 4 waves (no spills) 308 ms, 5 268, 6 240, 7 226, 8 222 ms
-    // (earlier layouts: 7 waves with 768-entry copies 322, 8 with 512 369 ms)
-    const int wpe = getenv("CAPF_TRI_WPE") ? atoi(getenv("CAPF_TRI_WPE")) : 8;
-    // CAPF_TRI_SCAP (tuning): longest list staged in LDS (longer: searched in
-    // global memory); smaller copies let more waves share a CU's LDS
-    const int scap = getenv("CAPF_TRI_SCAP") ? atoi(getenv("CAPF_TRI_SCAP")) : TRI_CAP;
-    // CAPF_TRI_XCD_A / _B (tuning): 1 = grabs dealt to the XCD groups in chunks
-    // (tri_dequeue).  s24, one box: A/B one cursor 121/223 ms; per XCD group,
-    // grabs 4/4 109/238, 2/2 103/229, 1/1 109/220 — on for pass A (grab 2) only
-    // (the value: grabs per XCD chunk, 0 = one cursor; 1 means TRI_XCHUNK)
-    int xcd_a = getenv("CAPF_TRI_XCD_A") ? atoi(getenv("CAPF_TRI_XCD_A")) : TRI_XCHUNK;
-    int xcd_b = getenv("CAPF_TRI_XCD_B") ? atoi(getenv("CAPF_TRI_XCD_B")) : 0;
-    if (xcd_a == 1) xcd_a = TRI_XCHUNK;
-    if (xcd_b == 1) xcd_b = TRI_XCHUNK;
-    // CAPF_TRI_TWOPASS=0 (tuning): one pass, every wedge streamed from N+(q)
-    const bool two = packed && g.pcols && g.in_words && !(getenv("CAPF_TRI_TWOPASS") && atoi(getenv("CAPF_TRI_TWOPASS")) == 0);
-    if (packed && g.pcols) {
-      if (two && g.qshift > 0) {
-        if (g.naitems > 0) {
-          KernelTimer kt(s, "tri_count_qtiled", 4.0 * g.P);
-          auto kq = hash == 1024 ? (ilp <= 2 ? k_tri_count_qtiled<2, 1024> : k_tri_count_qtiled<4, 1024>)
-                    : hash == 512  ? (ilp <= 2 ? k_tri_count_qtiled<2, 512> : k_tri_count_qtiled<4, 512>)
-                                   : tri_pick<TriQtiledK>(ilp, wpe, scap);
-          hipLaunchKernelGGL(kq, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
-                             (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
-                             (const uint2 *)g.vals->p, g.erow ? (const uint2 *)g.erow->p : nullptr,
-                             (const uint4 *)g.aitems->p, g.naitems, parts, part, grab_a, xcd_a,
-                             xcd_a ? xa : acc + 3, acc);
-        }
-      } else {
-        KernelTimer kt(s, "tri_count_packed", 4.0 * g.P);
-        auto kern = two ? (hash ? k_tri_count_packed<4, true, 1024> : ilp <= 2 ? k_tri_count_packed<2, true>
-                                                                   : ilp == 3 ? k_tri_count_packed<3, true> : k_tri_count_packed<4, true>)
-                        : (hash ? k_tri_count_packed<4, false, 1024> : ilp <= 2 ? k_tri_count_packed<2> : k_tri_count_packed<4>);
-        hipLaunchKernelGGL(kern, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
-                           (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
-                           (const uint2 *)g.vals->p, len, parts, part, acc + 3, acc);
+    if (g.pcols) {  // node ids < 2^24: packed words, pass A q-tiled + pass B
+      if (g.naitems > 0) {
+        KernelTimer kt(s, "tri_count_qtiled", 4.0 * g.P);
+        hipLaunchKernelGGL((k_tri_count_qtiled<TRI_ILP, TRI_WPE>), dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK),
+                           0, s->stream, (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
+                           (const uint2 *)g.vals->p, (const uint2 *)g.erow->p, (const uint4 *)g.aitems->p,
+                           g.naitems, parts, part, TRI_GRAB_A, TRI_XCHUNK, xa, acc);
+        KERNEL_CHECK();
       }
       if (s->profiling) {  // diagnostics (profiling mode only, host sync): pass A's probes
         unsigned long long pa = 0;
@@ -1530,27 +1180,22 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
         s->sync();
         s->profile["tri_probes_pass_a"].bytes += (double)pa;
       }
-      if (two && g.nitems > 0) {
+      if (g.nitems > 0) {
         KernelTimer kt(s, "tri_count_passb", 4.0 * g.P);
-        TriPassB b{(const uint32_t *)g.in_words->p, g.in_rows ? (const uint2 *)g.in_rows->p : nullptr,
-                   (const uint32_t *)g.in_eidx->p, (const uint4 *)g.items->p,
-                   g.nitems};
-        auto kb = hash == 1024 ? (ilp <= 2 ? k_tri_count_passb<2, 1024> : k_tri_count_passb<4, 1024>)
-                  : hash == 512  ? (ilp <= 2 ? k_tri_count_passb<2, 512> : k_tri_count_passb<4, 512>)
-                                 : tri_pick<TriPassbK>(ilp, wpe, scap);
-        hipLaunchKernelGGL(kb, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
-                           (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p, (const uint2 *)g.vals->p,
-                           b, parts, part, grab_b, xcd_b, xcd_b ? xb : acc + 6, acc);
+        TriPassB b{(const uint32_t *)g.in_words->p, (const uint2 *)g.in_rows->p, (const uint32_t *)g.in_eidx->p,
+                   (const uint4 *)g.items->p, g.nitems};
+        hipLaunchKernelGGL((k_tri_count_passb<TRI_ILP, TRI_WPE>), dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK),
+                           0, s->stream, (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
+                           (const uint2 *)g.vals->p, b, parts, part, TRI_GRAB_B, 0, acc + 6, acc);
+        KERNEL_CHECK();
       }
-    } else {
+    } else {  // wider node ranges: one pass over the unpacked CSR
       KernelTimer kt(s, "tri_count", 4.0 * g.P);
-      auto kern = filter ? (ilp >= 8 ? k_tri_count<true, 8> : ilp <= 2 ? k_tri_count<true, 2> : k_tri_count<true, 4>)
-                         : (ilp >= 8 ? k_tri_count<false, 8> : ilp <= 2 ? k_tri_count<false, 2> : k_tri_count<false, 4>);
-      hipLaunchKernelGGL(kern, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
+      hipLaunchKernelGGL(k_tri_count<TRI_ILP>, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK), 0, s->stream,
                          (const uint32_t *)g.rowptr->p, (const uint32_t *)g.cols->p,
                          (const uint2 *)g.vals->p, len, parts, part, acc + 3, acc);
+      KERNEL_CHECK();
     }
-    KERNEL_CHECK();
   }
   hipLaunchKernelGGL(k_tri_total, dim3(1), dim3(64), 0, s->stream, (const unsigned long long *)acc,
                      d_out);

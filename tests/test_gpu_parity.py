@@ -750,17 +750,15 @@ def test_two_hop_hub_overflow(gpu_session, monkeypatch, n, compact):
     assert got == cmodel.count_2hop(src.astype(np.int64), dst.astype(np.int64), n)
 
 
-@pytest.mark.parametrize("mode", ["0", "2", "3"], ids=["slices", "balanced", "apportioned"])
 @pytest.mark.parametrize("compact", [False, True, 3], ids=["int64", "for32", "for24"])
 @pytest.mark.parametrize("scale,parts", [(10, 2), (16, 1), (16, 3), (18, 4), (18, 3), (20, 8)])
-def test_sharded_two_hop_partials(gpu_session, compact, scale, parts, mode, monkeypatch):
+def test_sharded_two_hop_partials(gpu_session, compact, scale, parts):
     """Node-partitioned layout (dist.py): every part's in/out copies hold
     exactly the rels whose target/source it owns, each part's on-device
     partial Σ_{owned b} in·out − owned loops equals the oracle's, and the
     partials sum to the closed-form 2-hop count (what the all-reduce forms).
-    Both P3 forms of a rank: histogram slices + dot, and balanced key ranges
-    over sub-buckets (split sub-buckets folded from their slots)."""
-    monkeypatch.setenv("CAPF_SHARD_SB", mode)
+    A rank's P3: S static tile ranges per run into histogram slices + the dot
+    (packed slices with their hand-off log when S ≥ 2)."""
     import torch
     from capf_amd.dist import node_partitioned_copies
     from capf_amd.table import chain2_sharded_count_async
@@ -843,24 +841,24 @@ def test_triangle_self_loops_multi_edges(gpu_session):
     assert got == cmodel.count_triangle_brute(src[ok], dst[ok], n) == cmodel.count_triangle_formula(src, dst, n)
 
 
-@pytest.mark.parametrize("packed,hash_cap", [("1", "1024"), ("1", "512"), ("1", "0"), ("0", "1024")],
-                         ids=["packed-hash1024", "packed-hash512", "packed-sorted", "unpacked"])
-def test_triangle_heavy_multi_edges(gpu_session, monkeypatch, packed, hash_cap):
+@pytest.mark.parametrize("n", [40, (1 << 24) + 40], ids=["packed", "unpacked"])
+def test_triangle_heavy_multi_edges(gpu_session, n):
     """Pairs with 15+ parallel rels in either direction (the packed column
-    word's multiplicity nibbles saturate and the count reads vals — through
-    the LDS hash table's escape words, or the sorted copy), beside pairs of
-    1-14; checked against brute force and trace(A^3)."""
+    word's multiplicity nibbles saturate and the count reads vals through the
+    sorted copy's escape words), beside pairs of 1-14; checked against brute
+    force and trace(A^3).  A node range past 2^24 takes the unpacked kernel."""
     from capf_amd.graph import ElementTable, ScanGraph as SG
     from capf_amd.expr import T_INT
-    monkeypatch.setenv("CAPF_TRI_PACKED", packed)
-    monkeypatch.setenv("CAPF_TRI_HASH", hash_cap)
+    big = n > 1000
     rng = np.random.default_rng(5)
-    n = 40
+    k = 40
     e = []
     for _ in range(120):
-        x, y = rng.integers(0, n, 2)
+        x, y = rng.integers(0, k, 2)
         e += [(int(x), int(y))] * int(rng.choice([1, 2, 3, 14, 15, 16, 23]))
     e += [(0, 1)] * 17 + [(1, 2)] * 15 + [(2, 0)] * 16 + [(1, 0)] * 19  # one heavy triangle both ways
+    if big:  # a triangle through the top of the range
+        e += [(n - 1, 3), (3, 7), (7, n - 1)] * 2
     src = np.array([x for x, _ in e], dtype=np.int64)
     dst = np.array([y for _, y in e], dtype=np.int64)
     rels = gpu_session.table([("id", T_INT, np.arange(len(e)), None), ("source", T_INT, src, None),
@@ -870,20 +868,19 @@ def test_triangle_heavy_multi_edges(gpu_session, monkeypatch, packed, hash_cap):
            [ElementTable("rel", frozenset(["E"]), rels, {})])
     got = run(g, _triangle_query())[0]["count"]
     assert gpu_session.last_plan() == "fused_triangle"
-    assert got == cmodel.count_triangle_brute(src, dst, n) == cmodel.count_triangle_formula(src, dst, n)
+    remap = {v: i for i, v in enumerate(sorted(set(src.tolist()) | set(dst.tolist())))}
+    s2 = np.array([remap[v] for v in src.tolist()], dtype=np.int64)
+    d2 = np.array([remap[v] for v in dst.tolist()], dtype=np.int64)
+    want = cmodel.count_triangle_brute(s2, d2, len(remap))
+    assert got == want == cmodel.count_triangle_formula(s2, d2, len(remap))
 
 
-@pytest.mark.parametrize("rows", ["1", "0"], ids=["list-rows", "rowptr"])
-@pytest.mark.parametrize("hash_cap", ["0", "512", "1024"])
-def test_triangle_top_id_escape_word(gpu_session, monkeypatch, hash_cap, rows):
+def test_triangle_top_id_escape_word(gpu_session):
     """Node id 2^24 − 1 in a pair saturated both ways: its packed column word
-    would be 0xFFFFFFFF — the count kernels' end-of-batch marker and the LDS
-    hash table's empty slot — unless the pack step clears b when f saturates;
-    with the pair in triangles both ways."""
+    would be 0xFFFFFFFF — the count kernels' end-of-batch marker — unless the
+    pack step clears b when f saturates; with the pair in triangles both ways."""
     from capf_amd.graph import ElementTable, ScanGraph as SG
     from capf_amd.expr import T_INT
-    monkeypatch.setenv("CAPF_TRI_HASH", hash_cap)
-    monkeypatch.setenv("CAPF_TRI_ROWS", rows)
     T, U = (1 << 24) - 1, (1 << 24) - 2
     rng = np.random.default_rng(11)
     e = [(T, U)] * 17 + [(U, T)] * 16 + [(U, 5)] * 15 + [(5, T)] * 20 + [(T, 5)] * 3 + [(5, U)] * 2
@@ -904,19 +901,15 @@ def test_triangle_top_id_escape_word(gpu_session, monkeypatch, hash_cap, rows):
     assert got == cmodel.count_triangle_brute(src, dst, n)
 
 
-@pytest.mark.parametrize("rows", ["1", "0"], ids=["list-rows", "rowptr"])
-@pytest.mark.parametrize("hash_cap", ["0", "512", "1024"])
-@pytest.mark.parametrize("qtile", ["0", "12", "14", "18"])
+@pytest.mark.parametrize("qtile", ["12", "14", "18", "26"])
 @pytest.mark.parametrize("scale", [10, 13])
-def test_triangle_qtiled(gpu_session, monkeypatch, qtile, scale, hash_cap, rows):
-    """Pass A over q-tiled work items (CAPF_TRI_QTILE = log2 words per tile, 0 = row by row;
+def test_triangle_qtiled(gpu_session, monkeypatch, qtile, scale):
+    """Pass A over q-tiled work items (CAPF_TRI_QTILE = log2 words per tile;
     small tiles cut most rows into several items, some rows longer than the
     LDS copy) gives the trace(A^3) count, alone and as 3 parts."""
     import torch
     from capf_amd.table import triangle_count_part_async
     monkeypatch.setenv("CAPF_TRI_QTILE", qtile)
-    monkeypatch.setenv("CAPF_TRI_HASH", hash_cap)
-    monkeypatch.setenv("CAPF_TRI_ROWS", rows)
     g = rmat_graph(gpu_session, scale, compact=True)
     got = run(g, _triangle_query())[0]["count"]
     assert gpu_session.last_plan() == "fused_triangle"

@@ -49,29 +49,12 @@ def test_two_hop_headline(gpu_session, scale, compact):
     assert got == FULL[str(scale)]["two_hop"]
 
 
-@pytest.mark.parametrize("scale", [20, 24])
-@pytest.mark.parametrize("rot", ["1"], ids=["p3_rotated_dedup"])
-def test_two_hop_headline_p3_variant(gpu_session, monkeypatch, scale, rot):
-    """The rotated, fully deduplicated P3 pieces (CAPF_P3_ROT=1) — including
-    the inline uint16 hand-off of the s24 hub (in-degree 369,897) — give the fixture."""
-    monkeypatch.setenv("CAPF_P3_ROT", rot)
-    g = rmat_graph(gpu_session, scale, compact=3)
-    got = run(g, TWO_HOP)[0]["count"]
-    assert gpu_session.last_plan() == "fused_chain2"
-    assert got == FULL[str(scale)]["two_hop"]
-
-
-@pytest.mark.parametrize("ovfk,pairs", [("0", "1"), ("0", "0"), ("1", "1")],
-                         ids=["pairs_dot_folds_log", "uint32_bins_dot_folds_log", "overflow_kernel"])
-def test_two_hop_headline_handoff_paths(gpu_session, monkeypatch, ovfk, pairs):
+def test_two_hop_headline_handoff_sync_async(gpu_session):
     """The uint16 P3 counters hand 2^15 off to a log when a hub's counter
-    fills (s24 hub in-degree 369,897).  By default the dot kernel folds the
-    log in (Σ Δ·other + Σ Δ_in·Δ_out, no overflow launch); CAPF_P3_OVFK=1 adds
-    it to the histograms with the overflow kernel first.  Same fixture both
-    ways, synchronous and asynchronous."""
+    fills (s24 hub in-degree 369,897); the dot kernel folds the log in
+    (Σ Δ·other + Σ Δ_in·Δ_out, no overflow launch).  Same fixture
+    synchronous and asynchronous."""
     import torch
-    monkeypatch.setenv("CAPF_P3_OVFK", ovfk)
-    monkeypatch.setenv("CAPF_HIST_PAIRS", pairs)  # exclusive runs' buckets as packed uint16 pairs
     g = rmat_graph(gpu_session, 24, compact=3)
     assert run(g, TWO_HOP)[0]["count"] == FULL["24"]["two_hop"]
     slot = torch.full((1,), -1, dtype=torch.int64, device="cuda")
@@ -82,43 +65,18 @@ def test_two_hop_headline_handoff_paths(gpu_session, monkeypatch, ovfk, pairs):
 
 
 @pytest.mark.parametrize("scale", [20, 24])
-@pytest.mark.parametrize("zerok,unitsk", [("0", "1"), ("0", "0"), ("1", "1")],
-                         ids=["claims_clear", "claims_clear_units_in_transpose", "zero_kernel"])
-def test_two_hop_headline_split_runs(gpu_session, monkeypatch, scale, zerok, unitsk):
+def test_two_hop_headline_split_runs(gpu_session, monkeypatch, scale):
     """Hub-split P3 units flush with atomic adds into buckets that must start
     at zero.  CAPF_P3_SPLIT=0.5 splits every run above half the mean, so most
-    runs split; by default the first unit of each (run, slice) clears its
-    bucket (claim / ready bits) and the others wait for it, CAPF_C3_ZEROK=1
-    clears them with k_c3_zero.  The work list comes from k_c3_units, or with
-    CAPF_C3_UNITSK=0 from the transpose's last workgroup.  Two queries
-    back to back: the second must not see the first one's counters."""
+    runs split (uint32 bins for split runs, packed pairs for the rest); the
+    first unit of each (run, slice) clears its bucket (claim / ready bits) and
+    the others wait for it.  Two queries back to back: the second must not see
+    the first one's counters."""
     monkeypatch.setenv("CAPF_P3_SPLIT", "0.5")
-    monkeypatch.setenv("CAPF_C3_ZEROK", zerok)
-    monkeypatch.setenv("CAPF_C3_UNITSK", unitsk)
     g = rmat_graph(gpu_session, scale, compact=3)
     for _ in range(2):
         assert run(g, TWO_HOP)[0]["count"] == FULL[str(scale)]["two_hop"]
     assert gpu_session.last_plan() == "fused_chain2"
-
-
-@pytest.mark.parametrize("split", [None, "0.5"], ids=["runs_whole", "runs_split"])
-def test_two_hop_headline_p3_dot_epilogue(gpu_session, monkeypatch, split):
-    """CAPF_P3_DOT=1: the unit completing a bucket sums in·out over it (plus
-    the bucket's hand-off terms) in P3's epilogue and the last P3 workgroup
-    writes the count — synchronous, asynchronous, whole and split runs, two
-    queries back to back (the hand-off log and bucket counters are cleared by P1)."""
-    import torch
-    monkeypatch.setenv("CAPF_P3_DOT", "1")
-    if split:
-        monkeypatch.setenv("CAPF_P3_SPLIT", split)
-    g = rmat_graph(gpu_session, 24, compact=3)
-    for _ in range(2):
-        assert run(g, TWO_HOP)[0]["count"] == FULL["24"]["two_hop"]
-    slot = torch.full((1,), -1, dtype=torch.int64, device="cuda")
-    torch.cuda.synchronize()
-    plan_query(g, TWO_HOP).table.count_async(slot.data_ptr())
-    gpu_session.sync()
-    assert slot.item() == FULL["24"]["two_hop"]
 
 
 def test_two_hop_headline_async_queue(gpu_session):

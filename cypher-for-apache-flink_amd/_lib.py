@@ -240,8 +240,26 @@ def strs(values):
     return arr
 
 
+_EXPR_STRUCTS = {}  # id(program) -> (program, struct, refs): memoised programs are reused
+
+
 def _keepalive_expr(program):
-    """Build a CapfExpr from (ops, iargs, fargs, names); returns (struct, refs)."""
+    """Build a CapfExpr from (ops, iargs, fargs, names); returns (struct, refs).
+    Immutable (tuple) programs — compile_program's memoised ones — keep their
+    struct: the C-ABI copies a program on every call that takes one."""
+    if type(program[0]) is tuple:
+        ent = _EXPR_STRUCTS.get(id(program))
+        if ent is not None and ent[0] is program:
+            return ent[1], ent[2]
+        e, refs = _build_expr(program)
+        if len(_EXPR_STRUCTS) >= 4096:
+            _EXPR_STRUCTS.clear()
+        _EXPR_STRUCTS[id(program)] = (program, e, refs)  # holds the program: its id stays its own
+        return e, refs
+    return _build_expr(program)
+
+
+def _build_expr(program):
     ops, iargs, fargs, names = program
     n = len(ops)
     o = (c_int32 * n)(*ops)

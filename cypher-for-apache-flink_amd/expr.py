@@ -510,7 +510,139 @@ def resolve_column(expr, header, columns):
     return None
 
 
+_MISSING = object()
+_PROGRAM_MEMO = {}  # repr(expr) -> (lookups made while compiling it, program)
+
+
+def _memo_key(expr):
+    """repr(expr), kept on the instance: unlike Expr equality it tells 1 from
+    True and 1 from 1.0 inside literals, which lower to different programs."""
+    d = expr.__dict__
+    k = d.get("_mk")
+    if k is None:
+        k = d["_mk"] = repr(expr)
+    return k
+
+
+class _Lookups:
+    """Recording views of compile_program's inputs: every header / column /
+    type / parameter / string-code lookup and its answer, so a later call with
+    the same expression reuses the program when every answer is the same."""
+    __slots__ = ("log", "cacheable", "h", "cols", "par", "intern_fn", "type_fn")
+
+    def __init__(self, header, columns, params, intern, coltype):
+        self.log, self.cacheable = [], True
+        self.h, self.cols, self.par = header, columns, params or {}
+        self.intern_fn, self.type_fn = intern, coltype
+
+    # header view
+    def get(self, e, default=None):
+        v = self.h.get(e, _MISSING)
+        self.log.append((0, e, v))
+        return default if v is _MISSING else v
+
+    def __contains__(self, e):
+        return self.get(e, _MISSING) is not _MISSING
+
+    def items(self):  # the whole header: not recorded, the program is not reused
+        self.cacheable = False
+        return self.h.items()
+
+
+class _ColumnsView:
+    __slots__ = ("rec",)
+
+    def __init__(self, rec):
+        self.rec = rec
+
+    def __contains__(self, c):
+        v = c in self.rec.cols
+        self.rec.log.append((1, c, v))
+        return v
+
+
+class _ParamsView:
+    __slots__ = ("rec",)
+
+    def __init__(self, rec):
+        self.rec = rec
+
+    def __bool__(self):
+        return True
+
+    def get(self, k, default=None):
+        v = self.rec.par.get(k, _MISSING)
+        self.rec.log.append((2, k, _MISSING if v is _MISSING else repr(v)))
+        return default if v is _MISSING else v
+
+    def __getitem__(self, k):
+        v = self.get(k, _MISSING)
+        if v is _MISSING:
+            raise KeyError(k)
+        return v
+
+
+def _lookups_hold(log, header, columns, params, intern, coltype):
+    params = params or {}
+    for kind, k, v in log:
+        if kind == 0:
+            if header.get(k, _MISSING) != v:
+                return False
+        elif kind == 1:
+            if (k in columns) != v:
+                return False
+        elif kind == 2:
+            w = params.get(k, _MISSING)
+            if (_MISSING if w is _MISSING else repr(w)) != v:
+                return False
+        elif kind == 3:
+            if coltype is None or coltype(k) != v:
+                return False
+        elif intern is None or intern(k) != v:
+            return False
+    return True
+
+
 def compile_program(expr, header, columns, params=None, intern=None, coltype=None):
+    """Lower `expr` to (ops, iargs, fargs, names) for the C-ABI — memoised per
+    expression: a program is reused when every lookup its compilation made
+    (header columns, column presence and types, parameters, string codes)
+    gives the same answer again (the planner re-plans the same predicates and
+    aggregates query after query).  Programs are immutable once returned."""
+    try:
+        key = _memo_key(expr)
+    except AttributeError:  # not an Expr instance: compile every time
+        return _compile_program(expr, header, columns, params, intern, coltype)
+    ent = _PROGRAM_MEMO.get(key)
+    if ent is not None and header is not None and ent[0] is not None and \
+            _lookups_hold(ent[0], header, columns, params, intern, coltype):
+        return ent[1]
+    if header is None:
+        return _compile_program(expr, header, columns, params, intern, coltype)
+    rec = _Lookups(header, columns, params, intern, coltype)
+
+    def rec_type(c):
+        v = coltype(c)
+        rec.log.append((3, c, v))
+        return v
+
+    def rec_intern(x):
+        v = intern(x)
+        rec.log.append((4, x, v))
+        return v
+
+    prog = _compile_program(expr, rec, _ColumnsView(rec), _ParamsView(rec),
+                            rec_intern if intern is not None else None,
+                            rec_type if coltype is not None else None)
+    prog = (tuple(prog[0]), tuple(prog[1]), tuple(prog[2]), tuple(prog[3]))
+    if rec.cacheable:
+        if len(_PROGRAM_MEMO) >= 4096:
+            _PROGRAM_MEMO.clear()
+        _PROGRAM_MEMO[key] = (rec.log, prog)
+    return prog
+
+
+def _compile_program(expr, header, columns, params=None, intern=None, coltype=None):
     """Lower `expr` to (ops, iargs, fargs, names) for the C-ABI.
 
     header: dict Expr -> physical column; columns: set of the table's columns;
@@ -873,6 +1005,7 @@ def _cached_hash(gen):
 def _expr_getstate(self):
     d = dict(self.__dict__)
     d.pop("_hc", None)
+    d.pop("_mk", None)
     return d
 
 

@@ -20,6 +20,7 @@ are out of scope: the front end stays unchanged in the real deployment).
 """
 from dataclasses import dataclass, field
 from itertools import combinations
+from functools import lru_cache
 from typing import List, Optional, Sequence, Tuple
 
 from .expr import (Aggregator, Ands, BoolLit, ElementProperty, EndNode, Equals, ExistsPattern, Explode, Expr,
@@ -86,6 +87,14 @@ class Query:
 
 
 # ------------------------------------------------------------- relational ops
+@lru_cache(maxsize=16384)
+def _mk(cls, *args):
+    """One shared instance per expression the planner builds for a query's
+    variables (Var, StartNode(r), …): its hash is computed once and header
+    lookups hit on identity (the same plan is built query after query)."""
+    return cls(*args)
+
+
 def _rename_disjoint(left: Planned, right: Planned) -> Planned:
     """withDisjointColumnNames (RelationalPlanner.scala:366-368, 524-538)."""
     rcols = right.table.physicalColumns
@@ -181,9 +190,9 @@ def _rewrite_owner(e, old, new):
 def expand(graph, source: Var, rel: RelP, target: Var, src_op: Planned, tgt_op: Planned,
            direction: str) -> Planned:
     """RelationalPlanner Expand (RelationalPlanner.scala:130-165)."""
-    r = Var(rel.name, "RELATIONSHIP")
+    r = _mk(Var, rel.name, "RELATIONSHIP")
     second = graph.rel_scan(rel.name, rel.types)
-    start, end = StartNode(r), EndNode(r)
+    start, end = _mk(StartNode, r), _mk(EndNode, r)
     if direction == "out":
         tmp = join(src_op, second, [(source, start)])
         return join(tmp, tgt_op, [(end, target)])
@@ -362,7 +371,7 @@ def plan_match(graph, m: Match, prev: Optional[Planned], params=None) -> Planned
     for r in rels:
         si = next(i for i, (vs, _) in enumerate(plans) if r.src in vs)
         ti = next(i for i, (vs, _) in enumerate(plans) if r.dst in vs)
-        s, t = Var(r.src, "NODE"), Var(r.dst, "NODE")
+        s, t = _mk(Var, r.src, "NODE"), _mk(Var, r.dst, "NODE")
         if r.length is not None:
             if si == ti:
                 op = var_length_expand(graph, s, r, t, plans[si][1], plans[si][1], True)
@@ -387,8 +396,8 @@ def plan_match(graph, m: Match, prev: Optional[Planned], params=None) -> Planned
         p = _rename_disjoint(op, p)
         op = Planned(op.table.join(p.table, "cross"), op.header.union(p.header))
     # WHERE conjuncts, then front-end uniqueness predicates, one Filter each
-    fixed = [Var(r.name, "RELATIONSHIP") for r in rels if r.length is None]
-    preds = list(m.where) + extra_where + [Not(Equals(a, b)) for a, b in combinations(fixed, 2)]
+    fixed = [_mk(Var, r.name, "RELATIONSHIP") for r in rels if r.length is None]
+    preds = list(m.where) + extra_where + [_mk(Not, _mk(Equals, a, b)) for a, b in combinations(fixed, 2)]
     for p in preds:
         op = plan_subqueries(graph, op, p, params)
         op = filter_(op, p, params)
@@ -615,11 +624,11 @@ def plan_stage(op: Planned, st: Stage, params=None, graph=None) -> Planned:
             h2 = h2.with_expr(v, c)
         op = Planned(tab, h2)
     if aggs:
-        group_vars = [Var(a) for a, _ in projs]
+        group_vars = [_mk(Var, a) for a, _ in projs]
         agg_cols = {"__" + a: e for a, e in aggs}
         tab = op.table.group(group_vars, agg_cols, header=op.header, params=params or {})
         hh = dict(new_h)
-        hh.update({Var(a): "__" + a for a, _ in aggs})
+        hh.update({_mk(Var, a): "__" + a for a, _ in aggs})
         op = Planned(tab, RecordHeader(hh))
     else:
         cols = list(dict.fromkeys(new_h.values()))

@@ -399,8 +399,7 @@ constexpr int C3_TT = 256;
 __device__ __forceinline__ void c3_transpose_body(uint32_t (*tilebuf)[33], const uint32_t *meta,
                                                   uint32_t *meta_t, int64_t ntiles, int nr,
                                                   unsigned long long *run_total, int64_t tt, uint32_t *bsum,
-                                                  const uint32_t *tile_loops, unsigned long long *loops,
-                                                  bool wait_adds = false) {
+                                                  const uint32_t *tile_loops, unsigned long long *loops) {
   __shared__ uint32_t part[8][33];
   const int r0 = blockIdx.y * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads = 32 × 8
@@ -426,12 +425,7 @@ __device__ __forceinline__ void c3_transpose_body(uint32_t (*tilebuf)[33], const
     uint32_t c = 0;
 #pragma unroll
     for (int q = 0; q < 8; ++q) c += part[q][tx];
-    if (c && r < nr) {
-      const unsigned long long o = atomicAdd(&run_total[r], (unsigned long long)c);
-      // wait_adds: the returning add has been performed before the caller's
-      // `done` add (no fence: an agent-scope release writes back all of L2)
-      if (wait_adds) asm volatile("" ::"v"(o));
-    }
+    if (c && r < nr) atomicAdd(&run_total[r], (unsigned long long)c);
     // per-(run, tile block) key counts: the balanced P3's split points
     if (bsum && r < nr) bsum[(int64_t)r * gridDim.x + blockIdx.x] = c;
   }
@@ -499,12 +493,6 @@ static int c3_split_x16() {
   return e ? std::max(1, (int)(16.0 * atof(e))) : 32;
 }
 
-// Units are also ordered largest-first (LPT: `order` lists unit indexes by
-// decreasing estimated keys, a 64-level counting sort): P3 workgroups are
-// dispatched in blockIdx order, so the heavy (hub) units start in the first
-// wave and the short ones fill the tail.
-constexpr int C3_MAXU = 4096;  // LDS capacity of the ordering pass
-
 // The P1 → P3 path of the fused 2-hop count: P1's per-tile self-loops (summed
 // into acc3[1] by the transpose), acc3 = [Σ in·out, self-loops, done] cleared
 // by P1's tile-0 workgroup, and where the hand-off log goes.
@@ -515,31 +503,23 @@ struct C3Post {
   C2Spill *spill;  // host side: non-null → the hand-off log goes to the dot kernel
 };
 
-// The work-list computation, one workgroup of any size (RPT runs per thread,
-// nr ≤ RPT·blockDim.x): by k_c3_units, or by the transpose's last workgroup.
-// `est` holds C3_MAXU words of LDS; run totals are read with device-scope
-// atomics when `coherent` (the transpose's other workgroups added them in this
-// same launch).
+// The work-list computation (one workgroup, RPT runs per thread, nr ≤
+// RPT·blockDim.x).  (Per-(run, block) partial rows stored by the transpose
+// and summed here instead of the run-total adds: T 38 vs 34 µs, U 12 vs 9 µs.)
 struct C3UnitsOut {
   C3Unit *units;
-  int32_t *nunits, *split, *order;
-  unsigned int *done;  // the transpose's finished-workgroup counter (zeroed with run_total)
-  int32_t *rnu;        // units per run (P3's bucket-dot epilogue counts them down)
+  int32_t *nunits, *split;
 };
 template <int RPT>
-__device__ void c3_units_body(unsigned long long *run_total, int nr, const C3Sides &sd, int S,
-                              const C3UnitsOut &uo, uint32_t *est, bool coherent) {
+__device__ void c3_units_body(const unsigned long long *run_total, int nr, const C3Sides &sd, int S,
+                              const C3UnitsOut &uo) {
   __shared__ unsigned long long lds64[17];
   __shared__ uint32_t lds32[17];
-  __shared__ uint32_t qcnt[65];
-  __shared__ uint32_t maxest;
   unsigned long long cnt[RPT], tot = 0;
 #pragma unroll
   for (int q = 0; q < RPT; ++q) {
     const int r = RPT * threadIdx.x + q;
-    cnt[q] = r >= nr ? 0ull
-             : coherent ? __hip_atomic_load(&run_total[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                        : run_total[r];
+    cnt[q] = r >= nr ? 0ull : run_total[r];
     tot += cnt[q];
   }
   unsigned long long total;
@@ -573,53 +553,19 @@ __device__ void c3_units_body(unsigned long long *run_total, int nr, const C3Sid
       u.slice = (int32_t)(k % (uint32_t)S);
       u.pad = 0;
       uo.units[off + k] = u;
-      if (uo.order && off + k < (uint32_t)C3_MAXU)
-        est[off + k] = (uint32_t)min<unsigned long long>(cnt[q] / nu[q], 0xFFFFFFFFull);
     }
     off += nu[q];
     uo.split[r] = nu[q] > (uint32_t)S;
-    if (uo.rnu) uo.rnu[r] = (int32_t)nu[q];
   }
   if (threadIdx.x == 0) *uo.nunits = (int32_t)ntot;
-
-  if (!uo.order) return;
-  int32_t *order = uo.order;
-  const int nt = blockDim.x;
-  if (threadIdx.x <= 64) qcnt[threadIdx.x] = 0;
-  if (threadIdx.x == 0) maxest = 0;
-  __syncthreads();
-  const uint32_t nu_all = min(ntot, (uint32_t)C3_MAXU);
-  for (uint32_t i = threadIdx.x; i < nu_all; i += nt) atomicMax(&maxest, est[i]);
-  __syncthreads();
-  const unsigned long long mx = max(maxest, 1u);
-  // level 0 = largest
-  for (uint32_t i = threadIdx.x; i < nu_all; i += nt)
-    atomicAdd(&qcnt[63 - (uint32_t)(63ull * est[i] / mx)], 1u);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t a = 0;
-    for (int l = 0; l < 64; ++l) {
-      const uint32_t c = qcnt[l];
-      qcnt[l] = a;
-      a += c;
-    }
-  }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < nu_all; i += nt)
-    order[atomicAdd(&qcnt[63 - (uint32_t)(63ull * est[i] / mx)], 1u)] = (int32_t)i;
-  for (uint32_t i = nu_all + threadIdx.x; i < ntot; i += nt) order[i] = (int32_t)i;
 }
+
 
 __global__ __launch_bounds__(C3_UBLOCK) void k_c3_units(unsigned long long *run_total, int nr, C3Sides sd,
                                                          int S, C3UnitsOut uo) {
-  __shared__ uint32_t est[C3_MAXU];
-  c3_units_body<2>(run_total, nr, sd, S, uo, est, false);
+  c3_units_body<2>(run_total, nr, sd, S, uo);
 }
 
-// T and U in one launch: the workgroup whose `done` add comes last (every
-// other workgroup's run-total adds have landed) builds the work list, reusing
-// its transpose tile buffer as the LPT estimate array — one kernel boundary
-// (≈ 10 µs of drain and ramp at s24) fewer than T then k_c3_units.
 // XCD-aware unit placement.  Workgroup i runs on XCD i mod 8, and P3 holds
 // one workgroup per CU (128 KiB LDS), 32 per XCD.  Runs r and r+1 are
 // adjacent in every tile's region, so their segments share 128-B lines:
@@ -698,12 +644,12 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
                                                             const uint32_t *meta_t, int64_t ntiles,
                                                             int nb, int64_t rstride, uint32_t *h_in,
                                                             uint32_t *h_out, int64_t slice_stride,
-                                                            C3Ovf ovf, const int32_t *order,
+                                                            C3Ovf ovf,
                                                             C3Sides sd, int S, int64_t mstride) {
   // units == null: the static work list of a node-partitioned rank — unit
   // (run, k) counts tile range k of S of the run's side into slice k
   const int nu = units ? *nunits : 2 * sd.nb * S;
-  const int ui = (int)blockIdx.x >= nu && order ? nu : order ? order[blockIdx.x] : c3_unit_of((int)blockIdx.x);
+  const int ui = c3_unit_of((int)blockIdx.x);
   if (ui >= nu) return;
   extern __shared__ __attribute__((aligned(16))) uint32_t words[];
   constexpr int NW = C5_BLOCK / WAVE;
@@ -1046,7 +992,9 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   BufPtr meta_t = s->alloc(4 * nr * ntiles);
   // transpose blocks: tiles per block tt, fewer when there are few runs (≥ ~1024 blocks)
   int64_t tt = C3_TT;
-  // (s24: 128 tiles per block 34 µs, 64 41 µs, 32 54 µs — fewer, longer blocks win)
+  // (s24: 128 tiles per block 34 µs, 64 41 µs, 32 54 µs — fewer, longer blocks win;
+  // the same launch again right after takes 19 µs: ~15 µs of T is P1's dirty
+  // lines written back at the boundary, paid by whichever kernel follows P1)
   while (tt > 32 && ((ntiles + tt - 1) / tt) * ((nr + 31) / 32) < 1024) tt /= 2;
   const int nparts = (int)((ntiles + tt - 1) / tt);
   // acc_pre: allocated by the caller, its first c5_post_zero_words words
@@ -1068,7 +1016,7 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   const bool log_to_dot = post && post->spill && !sd.packed;
   if (!acc_pre) HIP_CHECK(hipMemsetAsync(acc->p, 0, 4 * (size_t)c5_post_zero_words(nr, ovf_cap), s->stream));
   // units in the XCD-grouped run order (largest-first order: measured no gain)
-  const C3UnitsOut uo{units, nunits, split, nullptr, (unsigned int *)(nunits + 2), rnu};
+  const C3UnitsOut uo{units, nunits, split};
   {
     KernelTimer kt(s, "c3_transpose", 8.0 * nr * ntiles);
     hipLaunchKernelGGL(k_c3_transpose, dim3((unsigned)nparts, (nr + 31) / 32), dim3(256), 0, s->stream, meta,
@@ -1094,7 +1042,7 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
     hipLaunchKernelGGL(k_c5_gather<C5_PPS>, dim3((unsigned)grid), dim3(C5_BLOCK), C5_GATHER_LDS, s->stream,
                        static_units ? nullptr : (const C3Unit *)units, (const int32_t *)nunits, part,
                        (const uint32_t *)meta_t->p, ntiles, sd.nb, rstride, h_in, h_out, slice_stride, ovf,
-                       (const int32_t *)nullptr, sdk, S, (int64_t)1);
+                       sdk, S, (int64_t)1);
     KERNEL_CHECK();
   }
   if (sd.packed) {  // the hand-offs are applied by k_c5_dot_packed

@@ -442,6 +442,10 @@ struct JoinPairs {
   // inner join whose key values are equal on every output row: 1 = the left
   // key column may be replaced by the right one, 2 = the other way round
   int key_alias = 0;
+  // the build side's row index is never read (dense_join: every probe row
+  // matches, the build side holds only its key and constant columns): no
+  // index for it — 1 = left, 2 = right; its key column is the alias above
+  int build_unread = 0;
 };
 JoinPairs hash_join(Session *s, const Data &l, const Data &r,
                     const std::vector<std::pair<int, int>> &keys, int32_t join_type);
@@ -483,6 +487,8 @@ BufPtr sort_permutation(Session *s, const std::vector<ColPtr> &keys,
                         const std::vector<int32_t> &desc, int64_t n);
 // Column statistics kernel.
 ColStats compute_stats(Session *s, const Column &c);
+// m rows of the constant column c's value (c.is_const)
+ColPtr const_column(Session *s, const Column &c, int64_t m);
 // Frame-of-reference encodings: FOR32 stores an INTEGER column whose value
 // range spans < 2^32 as uint32 offsets from `base` (half the HBM bytes).
 // encode_column returns the input when the range does not fit.

@@ -284,6 +284,41 @@ bool dense_join(Session *s, const Data &l, const Data &r, const std::vector<std:
   if (pk->type != Type::Int64) return false;
   const int64_t n = Pr.nrows;
   const bool probe_outer = join_type != CAPF_JOIN_INNER;
+  // every probe key provably matches (no NULL, the key's range inside the dense
+  // build range): from the probe column's cached statistics, or — a lazy gather
+  // without NULL rows — from its source column's (computed once when the
+  // source is far shorter than the probe side: the rel column behind a 2-path
+  // join's end node)
+  const bool all_match = [&] {
+    if (n == 0 || di->hashed) return false;
+    auto inside = [&](const ColStats &st, int64_t rows) {
+      return st.non_null == rows && st.min >= di->min && st.max < di->min + di->n;
+    };
+    if (pk->stats) return inside(*pk->stats, n);
+    if (pk->lazy && !pk->lazy->nullable) {
+      const ColPtr &src = pk->lazy->src;
+      if (src->stats || 4 * src->n <= n) return inside(column_stats(s, src), src->n);
+    }
+    return false;
+  }();
+  // ... and the build side carries nothing but its key and constant columns:
+  // its row index would never be read — no probe at all, the probe rows pass
+  // through (inner join: the build key is the probe key)
+  const Data &B = build_left ? l : r;
+  const int bk = build_left ? keys[0].first : keys[0].second;
+  bool unread = all_match && join_type == CAPF_JOIN_INNER;
+  for (int j = 0; unread && j < (int)B.cols.size(); ++j) {
+    const ColPtr &c = B.cols[j];
+    unread = j == bk || (c->is_const && c->n > 0) ||
+             (c->lazy && !c->lazy->nullable && c->lazy->src->is_const && c->lazy->src->n > 0);
+  }
+  if (unread) {
+    out.left = out.right = BufPtr();
+    out.n = n;
+    out.key_alias = build_left ? 1 : 2;
+    out.build_unread = build_left ? 1 : 2;
+    return true;
+  }
   BufPtr brow = s->alloc(8 * std::max<int64_t>(n, 1));
   BufPtr acc = s->alloc(8);
   HIP_CHECK(hipMemsetAsync(acc->p, 0, 8, s->stream));
@@ -303,14 +338,10 @@ bool dense_join(Session *s, const Data &l, const Data &r, const std::vector<std:
                          (unsigned long long *)acc->p);
     KERNEL_CHECK();
   }
-  // every probe key provably matches (no NULL, the key's range inside the dense
-  // build range — cached column statistics): no match count to read back, so
-  // the join stays asynchronous; otherwise one host read of the count.  Only
-  // statistics already cached count: computing them here would cost more syncs
-  // than the one readback they save.
+  // all_match: no match count to read back, so the join stays asynchronous;
+  // otherwise one host read of the count
   int64_t matched = 0;
-  const std::optional<ColStats> &pst = pk->stats;
-  if (n > 0 && !di->hashed && pst && pst->non_null == n && pst->min >= di->min && pst->max < di->min + di->n) {
+  if (all_match) {
     matched = n;
   } else {
     HIP_CHECK(hipMemcpyAsync(s->h_scalars, acc->p, 8, hipMemcpyDeviceToHost, s->stream));

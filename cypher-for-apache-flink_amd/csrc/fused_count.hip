@@ -1918,8 +1918,13 @@ bool try_fused_reach(const NodePtr &grp, DataPtr &result) {
       for (auto &c : rcols) c = gather_lazy(s, c, jp.left, nr, false, &cache);
     a_rows = std::make_shared<Data>();
     a_rows->nrows = nr;
-    for (auto &c : la.data->cols)
-      a_rows->cols.push_back(jp.right ? gather_lazy(s, c, jp.right, nr, false, &cache) : c);
+    for (size_t j = 0; j < la.data->cols.size(); ++j) {
+      const ColPtr &c = la.data->cols[j];
+      if (jp.build_unread == 2)  // S_a holds its key and constants only: no row index
+        a_rows->cols.push_back((int)j == sh.x ? rcols[0] : const_column(s, c->is_const ? *c : *c->lazy->src, nr));
+      else
+        a_rows->cols.push_back(jp.right ? gather_lazy(s, c, jp.right, nr, false, &cache) : c);
+    }
   }
   for (size_t i = 0; i < gk.size(); ++i) {
     const Type t = grp->types[i];

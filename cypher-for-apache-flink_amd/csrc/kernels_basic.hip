@@ -268,7 +268,7 @@ __global__ void k_fill_u64(uint64_t *p, uint64_t v, int64_t n) {
 }
 
 // m rows of a constant column's value (no validity: no NULLs)
-static ColPtr const_column(Session *s, const Column &c, int64_t m) {
+ColPtr const_column(Session *s, const Column &c, int64_t m) {
   ColPtr o = make_column(s, c.type, m, false);
   o->is_const = true;
   o->const_bits = c.const_bits;

@@ -12,14 +12,15 @@
 //                bucket in LDS and written out run by run (coalesced) into
 //                contiguous buckets; the second pass runs per first-level
 //                bucket, so (b1, b2) = 65 536 contiguous partitions per side
-//   J            one workgroup per work item (a partition, or a 8 Ki-row probe
-//                chunk of a big one): the build partition goes into an LDS
-//                open-addressing multimap (4 Ki slots = 48 KiB, chunks of 2 Ki
-//                build rows when larger), every probe row walks its chain;
-//                COUNT pass → one scan of the per-item counts → EMIT pass at
-//                the item's offset, each lane's matches placed by a wave64
-//                prefix sum (ballot popcount when every lane has 0 or 1) and
-//                one block scan: no global atomics, deterministic placement
+//   sort         the build partitions sorted by h (segmented radix sort):
+//                equal keys are runs
+//   J            one workgroup per work item (a partition, or a probe chunk
+//                of a big one): a chunk of ≤ 2 Ki sorted build rows becomes an
+//                LDS table of runs (h → start, length); COUNT pass → one scan
+//                of the per-item counts → EMIT over output ranges (sub-items
+//                of ≤ 32 Ki pairs, a hub key's product spread over many
+//                workgroups), each step's matches flattened over the
+//                workgroup: no global atomics, deterministic placement
 //   outer sides  matched flags set in the emit pass, the unmatched rows (NULL
 //                keys included) appended by a flag compaction
 // The build side is the smaller input (inner and outer joins alike: both
@@ -44,7 +45,6 @@ constexpr int RJ_CHUNK = RJ_CAP / 2;  // build rows per LDS fill (load ≤ 1/2)
 constexpr int RJ_PCHUNK = 8192;    // probe rows per work item (at most)
 constexpr int RJ_PCHUNK_MIN = 256; // ... and at least, when the probe side is small
 constexpr int RJ_JBLOCK = 256;     // join workgroup
-constexpr uint32_t RJ_EMPTY = 0xFFFFFFFFu;
 
 __device__ inline uint64_t rj_word(const ColView &c, int64_t r, bool &nul) {
   if (c.type == CAPF_TYPE_NULL || !c.data || (c.valid && !c.valid[r])) {
@@ -290,133 +290,34 @@ static RJSide rj_partition(Session *s, const ColPtr &col, int64_t n) {
 
 // ---------------------------------------------------------------- join
 struct RJWork {
-  int32_t part;
-  int32_t pad;
-  int64_t p0, p1;  // probe rows of the item (partition-relative positions in the probe arrays)
+  int32_t part;    // first partition of the item's group
+  int32_t np;      // partitions in the group (consecutive: their sorted build rows are one sorted run of h)
+  int64_t p0, p1;  // probe rows of the item (positions in the probe arrays)
 };
 
-// COUNT (emit == false: out_cnt[item] = matches) or EMIT (pairs at out_off[item]).
-template <bool EMIT>
-__global__ __launch_bounds__(RJ_JBLOCK) void k_rj_join(const RJWork *work, const uint64_t *bh,
-                                                        const uint32_t *brow, const int64_t *bstart,
-                                                        const uint64_t *ph, const uint32_t *prow,
-                                                        int64_t *out_cnt, const int64_t *out_off,
-                                                        int64_t *oprobe, int64_t *obuild,
-                                                        uint8_t *pmatched, uint8_t *bmatched) {
-  __shared__ uint64_t th[RJ_CAP];
-  __shared__ uint32_t tr[RJ_CAP];
-  __shared__ int64_t lds_scan[17];
-  const RJWork wk = work[blockIdx.x];
-  const int64_t b0 = bstart[wk.part], b1 = bstart[wk.part + 1];
-  int64_t item_total = 0;
-  int64_t base = EMIT ? out_off[blockIdx.x] : 0;
-  for (int64_t c0 = b0; c0 < b1; c0 += RJ_CHUNK) {
-    const int64_t c1 = min(c0 + (int64_t)RJ_CHUNK, b1);
-    for (int i = threadIdx.x; i < RJ_CAP; i += RJ_JBLOCK) tr[i] = RJ_EMPTY;
-    __syncthreads();
-    for (int64_t i = c0 + threadIdx.x; i < c1; i += RJ_JBLOCK) {
-      const uint64_t h = bh[i];
-      uint32_t slot = (uint32_t)h & (RJ_CAP - 1);
-      while (atomicCAS(&tr[slot], RJ_EMPTY, (uint32_t)(i - c0)) != RJ_EMPTY) slot = (slot + 1) & (RJ_CAP - 1);
-      th[slot] = h;
-    }
-    __syncthreads();
-    for (int64_t q0 = wk.p0; q0 < wk.p1; q0 += RJ_JBLOCK) {
-      const int64_t q = q0 + threadIdx.x;
-      const bool live = q < wk.p1;
-      const uint64_t h = live ? ph[q] : 0;
-      uint32_t cnt = 0;
-      if (live) {
-        uint32_t slot = (uint32_t)h & (RJ_CAP - 1);
-        for (uint32_t e = tr[slot]; e != RJ_EMPTY; slot = (slot + 1) & (RJ_CAP - 1), e = tr[slot])
-          cnt += th[slot] == h ? 1u : 0u;
-      }
-      // wave64 compaction: ballot + popcount when every lane has ≤ 1 match
-      // (a unique build key, the Expand case), else a wave scan
-      int64_t ex, tot;
-      {
-        const unsigned long long many = __ballot(cnt > 1);
-        uint32_t wex, wtot;
-        if (!many) {
-          const unsigned long long m = __ballot(cnt == 1);
-          wex = (uint32_t)__popcll(m & ((1ull << lane_id()) - 1));
-          wtot = (uint32_t)__popcll(m);
-        } else {
-          const uint32_t inc = wave_inclusive_scan(cnt);
-          wex = inc - cnt;
-          wtot = __shfl(inc, WAVE - 1, WAVE);
-        }
-        // block: one value per wave
-        int64_t wave_off, block_tot;
-        {
-          __shared__ int64_t wsum[RJ_JBLOCK / WAVE];
-          const int wv = threadIdx.x / WAVE;
-          if (lane_id() == 0) wsum[wv] = wtot;
-          __syncthreads();
-          int64_t acc = 0, all = 0;
-          for (int k = 0; k < RJ_JBLOCK / WAVE; ++k) {
-            if (k < wv) acc += wsum[k];
-            all += wsum[k];
-          }
-          wave_off = acc;
-          block_tot = all;
-          __syncthreads();
-        }
-        ex = wave_off + wex;
-        tot = block_tot;
-      }
-      if (EMIT && cnt) {
-        int64_t o = base + ex;
-        uint32_t slot = (uint32_t)h & (RJ_CAP - 1);
-        for (uint32_t e = tr[slot]; e != RJ_EMPTY; slot = (slot + 1) & (RJ_CAP - 1), e = tr[slot])
-          if (th[slot] == h) {
-            const uint32_t br = brow[c0 + e];
-            oprobe[o] = prow[q];
-            obuild[o] = br;
-            if (bmatched) bmatched[br] = 1;
-            ++o;
-          }
-        if (pmatched) pmatched[prow[q]] = 1;
-      }
-      base += tot;
-      item_total += tot;
-    }
-    __syncthreads();
-  }
-  (void)lds_scan;
-  if (!EMIT && threadIdx.x == 0) out_cnt[blockIdx.x] = item_total;
-}
-
-// Run-based join (default): the build partitions are sorted by h once
-// (segmented radix sort), so equal keys are runs; an LDS chunk of ≤ RJ_CHUNK
-// sorted build rows becomes a table of RUNS (h → start, length), found from
-// run heads with a ballot bitmask.  A probe row costs one lookup whatever its
-// key's multiplicity; EMIT hands the wave's matches out as one flattened
-// sequence (lane = output position, owner lane by a 6-step search in the
-// wave's prefix table) — coalesced, balanced writes even when one probe key
-// matches thousands of build rows (a hub node of a rel-to-rel join), where
-// the chain-walking kernel made one lane write them all.
+// COUNT pass of the run-based join: the build partitions are sorted by h
+// once (segmented radix sort), so equal keys are runs; an LDS chunk of ≤
+// RJ_CHUNK sorted build rows becomes a table of RUNS (h → start, length),
+// found from run heads with a ballot bitmask.  A probe row costs one lookup
+// whatever its key's multiplicity; out_cnt[item] = the item's pairs (the EMIT
+// pass is k_rj_emit_ranges over output ranges).  (Measured and removed: a
+// chain-walking multimap join, and an EMIT inside this kernel — one wave wrote
+// a hub key's whole product.)
 constexpr int RJ_RUNCAP = 4096;  // run-table slots (≤ RJ_CHUNK runs per chunk, load ≤ 1/2)
 
-template <bool EMIT>
 __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_join_runs(const RJWork *work, const uint64_t *bh,
-                                                             const uint32_t *brow, const int64_t *bstart,
-                                                             const uint64_t *ph, const uint32_t *prow,
-                                                             int64_t *out_cnt, const int64_t *out_off,
-                                                             int64_t *oprobe, int64_t *obuild,
-                                                             uint8_t *pmatched, uint8_t *bmatched) {
+                                                             const int64_t *bstart, const uint64_t *ph,
+                                                             int64_t *out_cnt) {
   __shared__ uint64_t kk[RJ_CHUNK];
   __shared__ unsigned long long hm[RJ_CHUNK / WAVE];  // run-head bitmask
   __shared__ uint64_t th[RJ_RUNCAP];
   __shared__ uint32_t tv[RJ_RUNCAP];                   // start << 16 | length (chunk-relative), 0 = empty
   constexpr int NW = RJ_JBLOCK / WAVE;
-  __shared__ uint32_t wex[NW][WAVE + 1], wst[NW][WAVE], wpr[NW][WAVE];
   __shared__ int64_t wsum[NW];
   const RJWork wk = work[blockIdx.x];
-  const int64_t b0 = bstart[wk.part], b1 = bstart[wk.part + 1];
+  const int64_t b0 = bstart[wk.part], b1 = bstart[wk.part + wk.np];
   const int wv = threadIdx.x / WAVE, lane = lane_id();
   int64_t item_total = 0;
-  int64_t base = EMIT ? out_off[blockIdx.x] : 0;
   for (int64_t c0 = b0; c0 < b1; c0 += RJ_CHUNK) {
     const int nc = (int)min<int64_t>((int64_t)RJ_CHUNK, b1 - c0);
     __syncthreads();  // the previous chunk's table is no longer read
@@ -456,180 +357,29 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_join_runs(const RJWork *work, 
       const int64_t q = q0 + threadIdx.x;
       const bool live = q < wk.p1;
       const uint64_t h = live ? ph[q] : 0;
-      uint32_t cnt = 0, st = 0;
+      uint32_t cnt = 0;
       if (live) {
         uint32_t slot = (uint32_t)h & (RJ_RUNCAP - 1);
         for (uint32_t v = tv[slot]; v != 0u; slot = (slot + 1) & (RJ_RUNCAP - 1), v = tv[slot])
           if (th[slot] == h) {
             cnt = v & 0xFFFFu;
-            st = v >> 16;
             break;
           }
       }
       const uint32_t inc = wave_inclusive_scan(cnt);
       const uint32_t wtot = (uint32_t)__shfl(inc, WAVE - 1, WAVE);
       if (lane == 0) wsum[wv] = wtot;
-      if (EMIT) {
-        wex[wv][lane] = inc - cnt;
-        if (lane == WAVE - 1) wex[wv][WAVE] = inc;
-        wst[wv][lane] = st;
-        wpr[wv][lane] = live ? prow[q] : 0u;
-        if (pmatched && cnt) pmatched[prow[q]] = 1;
-      }
       __syncthreads();
-      int64_t wave_off = 0, block_tot = 0;
-      for (int k = 0; k < NW; ++k) {
-        if (k < wv) wave_off += wsum[k];
-        block_tot += wsum[k];
-      }
-      if (EMIT) {
-        const int64_t o0 = base + wave_off;
-        // 4 output positions per lane per round: their build-row loads are
-        // independent, so 4 are in flight before the first store needs one
-        // (a hub key's thousands of matches otherwise cost one load latency
-        // per 64 outputs)
-        constexpr int U = 4;
-        for (uint32_t x0 = 0; x0 < wtot; x0 += U * WAVE) {
-          uint32_t br[U], pr[U];
-#pragma unroll
-          for (int k = 0; k < U; ++k) {
-            const uint32_t x = x0 + k * WAVE + lane;
-            const uint32_t xc = min(x, wtot - 1);
-            uint32_t b = 0;  // last lane with wex[b] ≤ xc
-#pragma unroll
-            for (int st2 = WAVE / 2; st2 > 0; st2 >>= 1)
-              if (wex[wv][b + st2] <= xc) b += st2;
-            br[k] = brow[c0 + wst[wv][b] + (xc - wex[wv][b])];
-            pr[k] = wpr[wv][b];
-          }
-#pragma unroll
-          for (int k = 0; k < U; ++k) {
-            const uint32_t x = x0 + k * WAVE + lane;
-            if (x < wtot) {
-              oprobe[o0 + x] = pr[k];
-              obuild[o0 + x] = br[k];
-              if (bmatched) bmatched[br[k]] = 1;
-            }
-          }
-        }
-      }
-      __syncthreads();  // wsum / wave tables are rewritten by the next step
-      base += block_tot;
+      int64_t block_tot = 0;
+      for (int k = 0; k < NW; ++k) block_tot += wsum[k];
+      __syncthreads();  // wsum is rewritten by the next step
       item_total += block_tot;
     }
   }
-  if (!EMIT && threadIdx.x == 0) out_cnt[blockIdx.x] = item_total;
+  if (threadIdx.x == 0) out_cnt[blockIdx.x] = item_total;
 }
 
-// Unique build side (no two sorted build rows of a partition share h, tested
-// by k_rj_adjacent_dup): each probe row has at most one match, written to the
-// probe row's own position, out[prow] = build row (out prefilled with -1).
-// The output is in probe order: no COUNT, scan, sub-items or pair list, and
-// the probe side's columns pass through the join without an index.
-__global__ void k_rj_adjacent_dup(const uint64_t *h, int64_t n, int *dup) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; i < n;
-       i += (int64_t)gridDim.x * blockDim.x)
-    if (h[i] == h[i - 1]) *dup = 1;
-}
-
-__global__ __launch_bounds__(RJ_JBLOCK) void k_rj_direct(const RJWork *work, const uint64_t *bh,
-                                                         const uint32_t *brow, const int64_t *bstart,
-                                                         const uint64_t *ph, const uint32_t *prow, int64_t *out,
-                                                         unsigned long long *hits) {
-  __shared__ uint64_t th[RJ_RUNCAP];
-  __shared__ uint32_t tv[RJ_RUNCAP];  // chunk position + 1, 0 = empty
-  __shared__ unsigned long long red[RJ_JBLOCK / WAVE];
-  const RJWork wk = work[blockIdx.x];
-  const int64_t b0 = bstart[wk.part], b1 = bstart[wk.part + 1];
-  unsigned long long cnt = 0;
-  for (int64_t c0 = b0; c0 < b1; c0 += RJ_CHUNK) {
-    const int nc = (int)min<int64_t>((int64_t)RJ_CHUNK, b1 - c0);
-    // table of ≥ 2·nc slots (a partition holds ~N / 2^16 build rows): clearing
-    // all RJ_RUNCAP slots per item cost as much as its probes
-    const uint32_t mask = (nc <= 32 ? 64u : (2u << (31 - __clz(2 * nc - 1)))) - 1u;
-    __syncthreads();  // the previous chunk's table is no longer read
-    for (int i = threadIdx.x; i <= (int)mask; i += RJ_JBLOCK) tv[i] = 0;
-    __syncthreads();
-    for (int i = threadIdx.x; i < nc; i += RJ_JBLOCK) {
-      const uint64_t h = bh[c0 + i];
-      uint32_t slot = (uint32_t)h & mask;
-      while (atomicCAS(&tv[slot], 0u, (uint32_t)i + 1u) != 0u) slot = (slot + 1) & mask;
-      th[slot] = h;
-    }
-    __syncthreads();
-    for (int64_t q = wk.p0 + threadIdx.x; q < wk.p1; q += RJ_JBLOCK) {
-      const uint64_t h = ph[q];
-      uint32_t slot = (uint32_t)h & mask;
-      for (uint32_t v = tv[slot]; v != 0u; slot = (slot + 1) & mask, v = tv[slot])
-        if (th[slot] == h) {
-          out[prow[q]] = (int64_t)brow[c0 + v - 1];
-          ++cnt;
-          break;
-        }
-    }
-  }
-  cnt = wave_reduce_sum(cnt);
-  if (lane_id() == 0) red[threadIdx.x / WAVE] = cnt;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long t = 0;
-    for (int w = 0; w < RJ_JBLOCK / WAVE; ++w) t += red[w];
-    if (t) atomicAdd(hits, t);
-  }
-}
-
-// Unique build side, probe side not partitioned (default of the unique case):
-// a probe row hashes its key, reads its partition's bounds and looks its h up
-// in the partition's sorted build hashes, starting where h's low 48 bits put
-// it (fmix64 spreads h evenly inside a partition, so the walk is a few
-// entries of one cache line).  Probe rows are read and written in order.
-__global__ __launch_bounds__(256) void k_rj_probe_sorted(ColView key, int64_t n, const uint64_t *bh,
-                                                         const uint32_t *brow, const int64_t *bstart, int64_t *out,
-                                                         unsigned long long *hits) {
-  __shared__ unsigned long long red[256 / WAVE];
-  unsigned long long cnt = 0;
-  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
-    int64_t b = -1;
-    bool nul;
-    const uint64_t w = rj_word(key, r, nul);
-    if (!nul) {
-      const uint64_t h = fmix64(w);
-      const int64_t lo = bstart[h >> 48], hi = bstart[(h >> 48) + 1];
-      if (hi > lo) {
-        int64_t g = lo + (int64_t)__umul64hi(h << 16, (uint64_t)(hi - lo));
-        if (bh[g] < h) {
-          ++g;
-          while (g < hi && bh[g] < h) ++g;
-        } else {
-          while (g > lo && bh[g - 1] >= h) --g;
-        }
-        if (g < hi && bh[g] == h) b = (int64_t)brow[g];
-      }
-    }
-    out[r] = b;
-    cnt += b >= 0 ? 1u : 0u;
-  }
-  cnt = wave_reduce_sum(cnt);
-  if (lane_id() == 0) red[threadIdx.x / WAVE] = cnt;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long t = 0;
-    for (int w = 0; w < 256 / WAVE; ++w) t += red[w];
-    if (t) atomicAdd(hits, t);
-  }
-}
-
-__global__ void k_rj_hitflags(const int64_t *brow, int64_t n, uint8_t *flags) {
-  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
-    flags[r] = brow[r] >= 0 ? 1 : 0;
-}
-
-__global__ void k_rj_pick(const int64_t *rows, int64_t m, const int64_t *brow, int64_t *out) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
-    out[i] = brow[rows[i]];
-}
-
-// EMIT over output ranges (default with the run-based join).  After COUNT,
+// EMIT over output ranges.  After COUNT,
 // item i (cnt[i] pairs) becomes ⌈cnt[i] / RJ_SUB_OUT⌉ sub-items, each writing
 // the pairs [lo, hi) of the item's flattened output sequence (probe-row order,
 // then the key's build run): a hub key whose (build run) × (probe rows) product
@@ -746,7 +496,7 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_emit_ranges(const RJSub *subs,
   __shared__ uint8_t spo[MODE ? RJ_PMAX : 1][RJ_JBLOCK];
   const RJSub sb = subs[blockIdx.x];
   const RJWork wk = work[sb.item];
-  const int64_t b0 = bstart[wk.part], b1 = bstart[wk.part + 1];
+  const int64_t b0 = bstart[wk.part], b1 = bstart[wk.part + wk.np];
   const int wv = threadIdx.x / WAVE, lane = lane_id();
   const int64_t obase = MODE == 0 ? out_off[sb.item] : 0;
   int64_t fbase = MODE == 2 ? suboff[blockIdx.x] : 0;  // next filtered output position
@@ -889,24 +639,30 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_emit_ranges(const RJSub *subs,
   }
 }
 
-// Work items per partition p: icnt[p] (heavy build side) or icnt[NPART + p]
-// (light); the scan of the 2·NPART counts lists the heavy items first.
-__global__ void k_rj_item_counts(const int64_t *bst, const int64_t *pst, int64_t pchunk, int64_t *icnt) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t nb = bst[p + 1] - bst[p], np = pst[p + 1] - pst[p];
+// Work items per group g of G consecutive partitions: icnt[g] (heavy build
+// side) or icnt[NG + g] (light); the scan of the 2·NG counts lists the heavy
+// items first.
+__global__ void k_rj_item_counts(const int64_t *bst, const int64_t *pst, int64_t pchunk, int G, int NG,
+                                 int64_t *icnt) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= NG) return;
+  const int64_t p = (int64_t)g * G;
+  const int64_t nb = bst[p + G] - bst[p], np = pst[p + G] - pst[p];
   const int64_t items = nb > 0 && np > 0 ? (np + pchunk - 1) / pchunk : 0;
   const bool heavy = nb > RJ_CHUNK;
-  icnt[p] = heavy ? items : 0;
-  icnt[(int64_t)RJ_P * RJ_P + p] = heavy ? 0 : items;
+  icnt[g] = heavy ? items : 0;
+  icnt[NG + g] = heavy ? 0 : items;
 }
 
-__global__ void k_rj_items(const int64_t *bst, const int64_t *pst, int64_t pchunk, const int64_t *ioff,
-                           RJWork *work) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t nb = bst[p + 1] - bst[p], q0 = pst[p], q1 = pst[p + 1];
+__global__ void k_rj_items(const int64_t *bst, const int64_t *pst, int64_t pchunk, int G, int NG,
+                           const int64_t *ioff, RJWork *work) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= NG) return;
+  const int64_t p = (int64_t)g * G;
+  const int64_t nb = bst[p + G] - bst[p], q0 = pst[p], q1 = pst[p + G];
   if (nb == 0 || q1 == q0) return;
-  int64_t o = ioff[nb > RJ_CHUNK ? p : (int64_t)RJ_P * RJ_P + p];
-  for (int64_t a = q0; a < q1; a += pchunk) work[o++] = RJWork{p, 0, a, min(q1, a + pchunk)};
+  int64_t o = ioff[nb > RJ_CHUNK ? g : (int64_t)NG + g];
+  for (int64_t a = q0; a < q1; a += pchunk) work[o++] = RJWork{(int32_t)p, G, a, min(q1, a + pchunk)};
 }
 
 __global__ void k_rj_unmatched(const uint8_t *matched, int64_t n, uint8_t *flags) {
@@ -942,18 +698,25 @@ static BufPtr rj_work_items(Session *s, const RJSide &bs, const RJSide &ps, int6
   // (its build rows) × (its probe rows) — spread over many workgroups instead
   // of one carrying the whole product.
   constexpr int64_t NPART = (int64_t)RJ_P * RJ_P;
+  // partitions grouped G at a time (a group's sorted build rows are one sorted
+  // run of h, its probe rows contiguous) so an item holds about half an LDS
+  // chunk of build rows: small inputs otherwise spread a few rows over each of
+  // 65 536 items (s14 var2: 4 build rows per partition)
+  int G = 1;
+  while (G < 256 && 2 * G * bs.n <= (int64_t)(RJ_CHUNK / 2) * NPART) G *= 2;
+  const int NG = (int)(NPART / G);
   int64_t pchunk = RJ_PCHUNK;
   while (pchunk > RJ_PCHUNK_MIN && pchunk * 16 * s->num_cus > probe_rows) pchunk /= 2;
-  if (const char *e = getenv("CAPF_RJ_PCHUNK")) pchunk = std::max<int64_t>(64, atoll(e));  // tuning
-  BufPtr icnt = s->alloc(8 * 2 * NPART), ioff = s->alloc(8 * (2 * NPART + 1));
-  hipLaunchKernelGGL(k_rj_item_counts, dim3((unsigned)(NPART / 256)), dim3(256), 0, s->stream,
-                     (const int64_t *)bs.pstart->p, (const int64_t *)ps.pstart->p, pchunk, (int64_t *)icnt->p);
+  BufPtr icnt = s->alloc(8 * 2 * NG), ioff = s->alloc(8 * (2 * NG + 1));
+  hipLaunchKernelGGL(k_rj_item_counts, dim3(grid_for(NG, 256)), dim3(256), 0, s->stream,
+                     (const int64_t *)bs.pstart->p, (const int64_t *)ps.pstart->p, pchunk, G, NG,
+                     (int64_t *)icnt->p);
   KERNEL_CHECK();
-  nw = exclusive_scan_i64(s, (const int64_t *)icnt->p, (int64_t *)ioff->p, 2 * NPART);
+  nw = exclusive_scan_i64(s, (const int64_t *)icnt->p, (int64_t *)ioff->p, 2 * NG);
   BufPtr dw = s->alloc(sizeof(RJWork) * std::max<int64_t>(nw, 1));
   if (nw > 0) {
-    hipLaunchKernelGGL(k_rj_items, dim3((unsigned)(NPART / 256)), dim3(256), 0, s->stream,
-                       (const int64_t *)bs.pstart->p, (const int64_t *)ps.pstart->p, pchunk,
+    hipLaunchKernelGGL(k_rj_items, dim3(grid_for(NG, 256)), dim3(256), 0, s->stream,
+                       (const int64_t *)bs.pstart->p, (const int64_t *)ps.pstart->p, pchunk, G, NG,
                        (const int64_t *)ioff->p, (RJWork *)dw->p);
     KERNEL_CHECK();
   }
@@ -972,95 +735,34 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
   const bool b_outer = build_left ? left_outer : right_outer;
   const bool p_outer = build_left ? right_outer : left_outer;
   RJSide bs = rj_partition(s, bk, B.nrows);
-  const char *rn = getenv("CAPF_RJ_RUNS");  // 0 (tuning): the chain-walking join kernel
-  const bool runs = !(rn && atoi(rn) == 0);
-  if (runs && bs.n > 0) {
+  if (bs.n > 0) {
     // equal keys contiguous inside each build partition (h's top 16 bits are the partition)
     KernelTimer kt(s, "rj_build_sort", 24.0 * (double)bs.n);
     BufPtr sh = s->alloc(8 * bs.n), sr = s->alloc(4 * bs.n);
     const int64_t *off = (const int64_t *)bs.pstart->p;
     size_t tmp = 0;
-    HIP_CHECK(rocprim::segmented_radix_sort_pairs(nullptr, tmp, (const uint64_t *)bs.h->p, (uint64_t *)sh->p,
-                                                  (const uint32_t *)bs.row->p, (uint32_t *)sr->p,
-                                                  (unsigned)bs.n, (unsigned)(RJ_P * RJ_P), off, off + 1, 0, 48,
-                                                  s->stream));
+    // few rows per partition: one sort of the whole side by all 64 bits (the
+    // top 16 are the partition, so every partition keeps its range); the
+    // segmented sort's per-segment cost dominates below ~64 rows a segment
+    const bool whole = bs.n < 64 * (int64_t)RJ_P * RJ_P;
+    auto sort = [&](void *t) {
+      if (whole)
+        return rocprim::radix_sort_pairs(t, tmp, (const uint64_t *)bs.h->p, (uint64_t *)sh->p,
+                                         (const uint32_t *)bs.row->p, (uint32_t *)sr->p, (size_t)bs.n, 0, 64,
+                                         s->stream);
+      return rocprim::segmented_radix_sort_pairs(t, tmp, (const uint64_t *)bs.h->p, (uint64_t *)sh->p,
+                                                 (const uint32_t *)bs.row->p, (uint32_t *)sr->p, (unsigned)bs.n,
+                                                 (unsigned)(RJ_P * RJ_P), off, off + 1, 0, 48, s->stream);
+    };
+    HIP_CHECK(sort(nullptr));
     BufPtr t = s->alloc(std::max<size_t>(tmp, 16));
-    HIP_CHECK(rocprim::segmented_radix_sort_pairs(t->p, tmp, (const uint64_t *)bs.h->p, (uint64_t *)sh->p,
-                                                  (const uint32_t *)bs.row->p, (uint32_t *)sr->p,
-                                                  (unsigned)bs.n, (unsigned)(RJ_P * RJ_P), off, off + 1, 0, 48,
-                                                  s->stream));
+    HIP_CHECK(sort(t->p));
     bs.h = sh;
     bs.row = sr;
   }
-  // a unique build side (one scan of the sorted partitions, one host read):
-  // each probe row has at most one match, written at the probe row's own
-  // position — probe-order output, no pair list.  CAPF_RJ_DIRECT: 1 (default)
-  // the probe side stays unpartitioned (k_rj_probe_sorted), 2 it is
-  // partitioned and probes the LDS tables (k_rj_direct), 0 the pair list
-  const char *dn = getenv("CAPF_RJ_DIRECT");
-  const int direct = dn ? atoi(dn) : 1;
-  if (runs && direct && !pred && !b_outer && bs.n > 0) {
-    int *dflag = (int *)(s->d_scalars + 3);
-    HIP_CHECK(hipMemsetAsync(dflag, 0, 4, s->stream));
-    if (bs.n > 1) {
-      hipLaunchKernelGGL(k_rj_adjacent_dup, dim3(grid_for(bs.n, 256)), dim3(256), 0, s->stream,
-                         (const uint64_t *)bs.h->p, bs.n, dflag);
-      KERNEL_CHECK();
-    }
-    int dup = 0;
-    HIP_CHECK(hipMemcpyAsync(&dup, dflag, 4, hipMemcpyDeviceToHost, s->stream));
-    s->sync();
-    if (!dup) {
-      const int64_t n = Pr.nrows;
-      BufPtr brow = s->alloc(8 * std::max<int64_t>(n, 1)), acc = s->alloc(8);
-      HIP_CHECK(hipMemsetAsync(acc->p, 0, 8, s->stream));
-      if (direct != 2) {
-        if (n > 0) {
-          KernelTimer kt(s, "rj_join_direct", (pk->enc == ENC_FOR24 ? 3.0 : pk->enc == ENC_FOR32 ? 4.0 : 8.0) * n + 8.0 * n + 32.0 * n);
-          hipLaunchKernelGGL(k_rj_probe_sorted, dim3(grid_for(n, 256, (int64_t)s->num_cus * 16)), dim3(256), 0,
-                             s->stream, view_of(pk), n, (const uint64_t *)bs.h->p, (const uint32_t *)bs.row->p,
-                             (const int64_t *)bs.pstart->p, (int64_t *)brow->p, (unsigned long long *)acc->p);
-          KERNEL_CHECK();
-        }
-      } else {
-        HIP_CHECK(hipMemsetAsync(brow->p, 0xFF, 8 * std::max<int64_t>(n, 1), s->stream));
-        RJSide ps = rj_partition(s, pk, n);
-        int64_t nw = 0;
-        BufPtr dw = rj_work_items(s, bs, ps, n, nw);
-        if (nw > 0) {
-          KernelTimer kt(s, "rj_join_direct", 12.0 * (double)(ps.n + bs.n) + 8.0 * (double)n);
-          hipLaunchKernelGGL(k_rj_direct, dim3((unsigned)nw), dim3(RJ_JBLOCK), 0, s->stream, (const RJWork *)dw->p,
-                             (const uint64_t *)bs.h->p, (const uint32_t *)bs.row->p, (const int64_t *)bs.pstart->p,
-                             (const uint64_t *)ps.h->p, (const uint32_t *)ps.row->p, (int64_t *)brow->p,
-                             (unsigned long long *)acc->p);
-          KERNEL_CHECK();
-        }
-      }
-      int64_t matched = 0;
-      HIP_CHECK(hipMemcpyAsync(&matched, acc->p, 8, hipMemcpyDeviceToHost, s->stream));
-      s->sync();
-      BufPtr pidx, bidx = brow;  // pidx null = identity over the probe rows
-      int64_t m = n;
-      if (!p_outer && matched < n) {
-        BufPtr flags = s->alloc(std::max<int64_t>(n, 1));
-        hipLaunchKernelGGL(k_rj_hitflags, dim3(grid_for(n, 256)), dim3(256), 0, s->stream, (const int64_t *)brow->p,
-                           n, (uint8_t *)flags->p);
-        KERNEL_CHECK();
-        pidx = compact_flags(s, (const uint8_t *)flags->p, n, &m);
-        bidx = s->alloc(8 * std::max<int64_t>(m, 1));
-        if (m > 0) {
-          hipLaunchKernelGGL(k_rj_pick, dim3(grid_for(m, 256)), dim3(256), 0, s->stream, (const int64_t *)pidx->p,
-                             m, (const int64_t *)brow->p, (int64_t *)bidx->p);
-          KERNEL_CHECK();
-        }
-      }
-      JoinPairs jp;
-      jp.left = build_left ? bidx : pidx;
-      jp.right = build_left ? pidx : bidx;
-      jp.n = m;
-      return jp;
-    }
-  }
+  // (A unique build side is the dense / hashed index's join, dense_join.hip;
+  // probe-order kernels for it here — a probe of the sorted build partitions
+  // and one of LDS tables — ran 3× slower and were removed.)
   RJSide ps = rj_partition(s, pk, Pr.nrows);
   int64_t nw = 0;
   BufPtr dw = rj_work_items(s, bs, ps, Pr.nrows, nw);
@@ -1068,11 +770,9 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
   int64_t total = 0;
   if (nw > 0) {
     KernelTimer kt(s, "rj_join_count", 12.0 * (double)(ps.n + bs.n));
-    hipLaunchKernelGGL(runs ? k_rj_join_runs<false> : k_rj_join<false>, dim3((unsigned)nw), dim3(RJ_JBLOCK), 0, s->stream,
-                       (const RJWork *)dw->p, (const uint64_t *)bs.h->p, (const uint32_t *)bs.row->p,
-                       (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
-                       (const uint32_t *)ps.row->p, (int64_t *)cnt->p, (const int64_t *)nullptr,
-                       (int64_t *)nullptr, (int64_t *)nullptr, (uint8_t *)nullptr, (uint8_t *)nullptr);
+    hipLaunchKernelGGL(k_rj_join_runs, dim3((unsigned)nw), dim3(RJ_JBLOCK), 0, s->stream, (const RJWork *)dw->p,
+                       (const uint64_t *)bs.h->p, (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
+                       (int64_t *)cnt->p);
     KERNEL_CHECK();
     total = exclusive_scan_i64(s, (const int64_t *)cnt->p, (int64_t *)off->p, nw);
   }
@@ -1085,10 +785,8 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
     bm = s->alloc(std::max<int64_t>(B.nrows, 1));
     HIP_CHECK(hipMemsetAsync(bm->p, 0, std::max<int64_t>(B.nrows, 1), s->stream));
   }
-  const char *ranges_env = getenv("CAPF_RJ_RANGES");  // 0 (tuning): one EMIT workgroup per item
-  const bool ranges = runs && !(ranges_env && atoi(ranges_env) == 0);
-  if (pred) {  // filtered (radix_join_filtered): inner join, ranges path only
-    if (!ranges || p_outer || b_outer) illegal("radix_join: a filtered join needs the inner ranges path");
+  if (pred) {  // filtered (radix_join_filtered): inner join only
+    if (p_outer || b_outer) illegal("radix_join: a filtered join must be inner");
     JoinPairs jp;
     jp.n = 0;
     BufPtr oprobe = s->alloc(8), obuild = s->alloc(8);
@@ -1166,7 +864,7 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
   }
   const int64_t cap = total + (p_outer ? Pr.nrows : 0) + (b_outer ? B.nrows : 0);
   BufPtr oprobe = s->alloc(8 * std::max<int64_t>(cap, 1)), obuild = s->alloc(8 * std::max<int64_t>(cap, 1));
-  if (ranges && nw > 0 && total > 0) {
+  if (nw > 0 && total > 0) {
     BufPtr nsub = s->alloc(8 * nw), soff = s->alloc(8 * (nw + 1));
     hipLaunchKernelGGL(k_rj_sub_counts, dim3(grid_for(nw, 256)), dim3(256), 0, s->stream, (const int64_t *)cnt->p,
                        nw, (int64_t *)nsub->p);
@@ -1184,16 +882,8 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
                        p_outer ? (uint8_t *)pm->p : nullptr, b_outer ? (uint8_t *)bm->p : nullptr, RjPred{}, 0,
                        (int64_t *)nullptr, (const int64_t *)nullptr);
     KERNEL_CHECK();
-  } else if (nw > 0 && (total > 0 || p_outer || b_outer)) {
-    KernelTimer kt(s, "rj_join_emit", 12.0 * (double)(ps.n + bs.n) + 16.0 * (double)total);
-    hipLaunchKernelGGL(runs ? k_rj_join_runs<true> : k_rj_join<true>, dim3((unsigned)nw), dim3(RJ_JBLOCK), 0, s->stream,
-                       (const RJWork *)dw->p, (const uint64_t *)bs.h->p, (const uint32_t *)bs.row->p,
-                       (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
-                       (const uint32_t *)ps.row->p, (int64_t *)nullptr, (const int64_t *)off->p,
-                       (int64_t *)oprobe->p, (int64_t *)obuild->p,
-                       p_outer ? (uint8_t *)pm->p : nullptr, b_outer ? (uint8_t *)bm->p : nullptr);
-    KERNEL_CHECK();
   }
+  // (total = 0: no pair, the outer sides' flags stay clear — every row is unmatched)
   int64_t m = total;
   // unmatched rows of the outer sides (NULL keys included: never flagged)
   auto append_unmatched = [&](const BufPtr &matched, int64_t n, int64_t *own, int64_t *other) {
@@ -1228,8 +918,6 @@ bool radix_join_filtered(Session *s, const Program &pred, const std::vector<std:
   const char *fe = getenv("CAPF_RJ_FILTER");  // 0 (tuning/tests): join, then filter
   if (fe && atoi(fe) == 0) return false;
   if (join_type != CAPF_JOIN_INNER || names.size() != l.cols.size() + r.cols.size()) return false;
-  const char *rn = getenv("CAPF_RJ_RUNS"), *rg = getenv("CAPF_RJ_RANGES");
-  if ((rn && atoi(rn) == 0) || (rg && atoi(rg) == 0)) return false;
   if (!radix_join_applies(l, r, keys, join_type) || dense_join_possible(s, l, r, keys, join_type)) return false;
   Data both;
   both.nrows = 0;

@@ -423,14 +423,23 @@ static DataPtr gather_all(Session *s, const Data &d, const BufPtr &idx, int64_t 
 
 // The output of a join node n from its inputs' row indexes (lazy gathers).
 static DataPtr join_output(Session *s, const NodePtr &n, const Data &l, const Data &r, const BufPtr &li,
-                           const BufPtr &ri, int64_t m, int key_alias) {
+                           const BufPtr &ri, int64_t m, int key_alias, int build_unread = 0) {
   auto out = std::make_shared<Data>();
   out->nrows = m;
   bool lnull = n->join_type == CAPF_JOIN_RIGHT_OUTER || n->join_type == CAPF_JOIN_FULL_OUTER;
   bool rnull = n->join_type == CAPF_JOIN_LEFT_OUTER || n->join_type == CAPF_JOIN_FULL_OUTER;
   IdxCache cache;  // the columns of one side share one (composed) index
-  for (auto &c : l.cols) out->cols.push_back(gather_lazy(s, c, li, m, lnull, &cache));
-  for (auto &c : r.cols) out->cols.push_back(gather_lazy(s, c, ri, m, rnull, &cache));
+  // a build side without a row index: constants fill, the key is aliased below
+  auto unread = [&](const ColPtr &c, bool key) -> ColPtr {
+    if (key) return c;
+    return const_column(s, c->is_const ? *c : *c->lazy->src, m);
+  };
+  for (size_t i = 0; i < l.cols.size(); ++i)
+    out->cols.push_back(build_unread == 1 ? unread(l.cols[i], (int)i == n->join_keys[0].first)
+                                          : gather_lazy(s, l.cols[i], li, m, lnull, &cache));
+  for (size_t i = 0; i < r.cols.size(); ++i)
+    out->cols.push_back(build_unread == 2 ? unread(r.cols[i], (int)i == n->join_keys[0].second)
+                                          : gather_lazy(s, r.cols[i], ri, m, rnull, &cache));
   if (key_alias) {
     // the build key column of an inner dense join IS the probe key column
     // (equal values on every row): no gather of it
@@ -480,7 +489,7 @@ static DataPtr materialize_impl(const NodePtr &n) {
       DataPtr r = materialize(n->kids[1]);
       BufPtr li, ri;
       int64_t m = 0;
-      int key_alias = 0;
+      int key_alias = 0, build_unread = 0;
       if (n->join_type == CAPF_JOIN_CROSS) {
         m = l->nrows * r->nrows;
         cross_index(s, l->nrows, r->nrows, li, ri);
@@ -494,8 +503,9 @@ static DataPtr materialize_impl(const NodePtr &n) {
         ri = jp.right;
         m = jp.n;
         key_alias = jp.key_alias;
+        build_unread = jp.build_unread;
       }
-      return join_output(s, n, *l, *r, li, ri, m, key_alias);
+      return join_output(s, n, *l, *r, li, ri, m, key_alias, build_unread);
     }
     case Kind::Union: {
       DataPtr l = materialize(n->kids[0]);

@@ -100,7 +100,35 @@ def test_one_hop_rows_rmat(gpu_session, compact):
     gpu_session.set_profiling(False)
     src, dst = cmodel.rmat(12)
     assert sorted(zip(a.tolist(), b.tolist())) == sorted(zip(src.tolist(), dst.tolist()))
-    assert gpu_session.profile()["dense_probe"]["launches"] == 2
+    # both node scans hold only their id (the join key): every rel endpoint lies
+    # in the dense id range (cached statistics), so no build row index is ever
+    # read and neither dense probe runs — the rel rows pass through
+    assert "dense_probe" not in gpu_session.profile()
+
+
+@pytest.mark.parametrize("misses", [False, True], ids=["all_match", "misses"])
+def test_dense_join_unread_build_side(gpu_session, misses):
+    """Inner dense join whose build side is its key plus a constant (label)
+    column: when every probe key provably matches (probe statistics inside the
+    dense id range) the probe is skipped — the key column is the probe key, the
+    label a fill; with keys that miss, the probe runs.  Same bag as the oracle
+    either way."""
+    from capf_amd.expr import BoolLit
+    from capf_amd.header import RecordHeader
+    nodes, rels = _tables(4000, 30000, "shuffled", misses, False, seed=11)
+    nodes = nodes[:1]  # the id column only
+    gn = gpu_session.table(nodes).compact(4)
+    gn = gn.withColumns((BoolLit(True), "n:Person"), header=RecordHeader({}), params={})
+    gr = gpu_session.table(rels).compact(4)
+    on = OracleSession().table(nodes).withColumns((BoolLit(True), "n:Person"), header=RecordHeader({}),
+                                                  params={})
+    orl = OracleSession().table(rels)
+    gpu_session.reset_profile()
+    gpu_session.set_profiling(True)
+    got = gr.join(gn, "inner", ("src", "id")).rows
+    gpu_session.set_profiling(False)
+    assert bag(got) == bag(orl.join(on, "inner", ("src", "id")).rows)
+    assert ("dense_probe" in gpu_session.profile()) == misses
 
 
 def _sparse_tables(n_nodes, n_rels, misses, nulls, dups, seed):

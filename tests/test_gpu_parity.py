@@ -481,25 +481,19 @@ def test_radix_join_large(gpu_session, monkeypatch, jt, sizes):
 
 @pytest.mark.parametrize("jt", ["inner", "left_outer", "right_outer", "full_outer"])
 @pytest.mark.parametrize("sizes", [(3000, 200000), (300000, 5000), (70000, 70001), (1, 1000), (50000, 1)])
-@pytest.mark.parametrize("direct", ["1", "2", "0"], ids=["probe_sorted", "partitioned", "pairs"])
-def test_radix_join_unique_build(gpu_session, monkeypatch, jt, sizes, direct):
-    """The radix join whose smaller (build) side has every non-NULL key once:
-    each probe row matches at most once and the join writes the build row to
-    the probe row's position (probe-order output): the unpartitioned probe
-    side looks its hash up in the sorted build partitions (k_rj_probe_sorted,
-    default), or CAPF_RJ_DIRECT=2 partitions it and probes LDS tables
-    (k_rj_direct); CAPF_RJ_DIRECT=0 keeps the pair list.  Sparse int64 keys, misses on both
-    sides, NULL keys on both; checked against numpy, and the direct kernel ran
-    exactly when it may (not when the build side is outer)."""
+def test_radix_join_unique_build(gpu_session, monkeypatch, jt, sizes):
+    """The radix join (forced) whose smaller (build) side has every non-NULL
+    key once — including a one-row build side — through the run-based COUNT
+    and the ranges EMIT: sparse int64 keys, misses on both sides, NULL keys on
+    both; checked against numpy."""
     monkeypatch.setenv("CAPF_JOIN", "radix")
-    monkeypatch.setenv("CAPF_RJ_DIRECT", direct)
     rng = np.random.default_rng(sum(sizes) + 5)
     nl, nr = sizes
     nb, npr = min(nl, nr), max(nl, nr)
     bkeys = rng.permutation(np.arange(2 * nb + 3, dtype=np.int64))[:nb] * 1000003 + 7  # unique, sparse
     pkeys = rng.integers(0, 2 * nb + 3, npr).astype(np.int64) * 1000003 + 7           # some miss
     bv = np.ones(nb, dtype=np.uint8)
-    bv[::53] = 0
+    bv[1::53] = 0  # (row 0 keeps its key: the one-row build side joins a real key)
     pv = np.ones(npr, dtype=np.uint8)
     pv[::61] = 0
     lk, lv, rk, rv = (bkeys, bv, pkeys, pv) if nl < nr else (pkeys, pv, bkeys, bv)
@@ -511,8 +505,7 @@ def test_radix_join_unique_build(gpu_session, monkeypatch, jt, sizes, direct):
     li, lok = out.column_arrays("li")
     ri, rok = out.column_arrays("ri")
     gpu_session.set_profiling(False)
-    build_outer = jt == "full_outer" or (jt == "left_outer" and nl < nr) or (jt == "right_outer" and nr <= nl)
-    assert ("rj_join_direct" in gpu_session.profile()) == (direct != "0" and not build_outer and nb > 1)
+    assert "rj_partition1" in gpu_session.profile()  # the radix path ran
     got = sorted(zip(np.where(lok, li, -1).tolist(), np.where(rok, ri, -1).tolist()))
     byk = {int(rk[j]): int(j) for j in np.nonzero(rv)[0]} if nl >= nr else None
     pairs, lm, rm = [], set(), set()

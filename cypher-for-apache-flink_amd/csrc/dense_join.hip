@@ -257,8 +257,7 @@ bool dense_join_possible(Session *s, const Data &l, const Data &r, const std::ve
   if (!di && r_ok && r.nrows > l.nrows) di = dense_index(s, r.cols[keys[0].second], r.nrows);
   if (!di) return false;
   const ColPtr &pk = (build_left ? r : l).cols[build_left ? keys[0].second : keys[0].first];
-  force(pk);
-  return pk->type == Type::Int64;
+  return pk->type == Type::Int64;  // (a lazy column carries its type: no gather here)
 }
 
 bool dense_join(Session *s, const Data &l, const Data &r, const std::vector<std::pair<int, int>> &keys,
@@ -280,7 +279,8 @@ bool dense_join(Session *s, const Data &l, const Data &r, const std::vector<std:
   if (!di) return false;
   const Data &Pr = build_left ? r : l;
   const ColPtr &pk = Pr.cols[build_left ? keys[0].second : keys[0].first];
-  force(pk);
+  // not forced: a lazy probe key (a join's output column) may be provably
+  // matching from its source's statistics, and then it is never gathered
   if (pk->type != Type::Int64) return false;
   const int64_t n = Pr.nrows;
   const bool probe_outer = join_type != CAPF_JOIN_INNER;

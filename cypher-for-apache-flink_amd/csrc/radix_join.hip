@@ -474,9 +474,12 @@ __device__ inline void rj_pass(const RjPred &fp, const int64_t (&bi)[U], const u
 }
 
 // MODE 0: every pair of the sub-item's range [lo, hi) at out_off[item] + its
-// position.  With a filter (radix_join_filtered): MODE 1 counts the pairs that
-// pass into subcnt[sub]; MODE 2 writes them, in the same order, from
-// suboff[sub] on (per 4·256-pair round: a workgroup scan of the passes).
+// position.  With a filter (radix_join_filtered): MODE 3 writes the passing
+// pairs at the same positions and appends the positions of the failing ones
+// to holes[] (the caller then moves tail pairs into the holes: the output is
+// a bag — one pass, no count of the passes first); MODE 1 counts the passes
+// per sub-item into subcnt[sub] and MODE 2 writes them from suboff[sub] on
+// (two passes, when the holes overflow their buffer).
 template <int MODE>
 __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_emit_ranges(const RJSub *subs, const RJWork *work,
                                                                const uint64_t *bh, const uint32_t *brow,
@@ -485,7 +488,8 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_emit_ranges(const RJSub *subs,
                                                                int64_t *oprobe, int64_t *obuild,
                                                                uint8_t *pmatched, uint8_t *bmatched,
                                                                const RjPred fp, int build_left,
-                                                               int64_t *subcnt, const int64_t *suboff) {
+                                                               int64_t *subcnt, const int64_t *suboff,
+                                                               unsigned long long *nholes, int64_t hcap) {
   __shared__ uint64_t kk[RJ_CHUNK];
   __shared__ unsigned long long hm[RJ_CHUNK / WAVE];
   __shared__ uint64_t th[RJ_RUNCAP];
@@ -498,7 +502,7 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_emit_ranges(const RJSub *subs,
   const RJWork wk = work[sb.item];
   const int64_t b0 = bstart[wk.part], b1 = bstart[wk.part + wk.np];
   const int wv = threadIdx.x / WAVE, lane = lane_id();
-  const int64_t obase = MODE == 0 ? out_off[sb.item] : 0;
+  const int64_t obase = MODE == 0 || MODE == 3 ? out_off[sb.item] : 0;
   int64_t fbase = MODE == 2 ? suboff[blockIdx.x] : 0;  // next filtered output position
   uint32_t kept = 0;                                   // MODE 1: passing pairs of this thread
   int64_t rel = 0;  // pairs of the item before the current step
@@ -610,7 +614,22 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_emit_ranges(const RJSub *subs,
             uint32_t c = 0;
 #pragma unroll
             for (int k = 0; k < U; ++k) c += keep[k] ? 1u : 0u;
-            if constexpr (MODE == 1) {
+            if constexpr (MODE == 3) {
+#pragma unroll
+              for (int k = 0; k < U; ++k) {
+                const uint32_t x = xb + k * RJ_JBLOCK + threadIdx.x;
+                if (x >= x1) continue;
+                const int64_t pos = obase + rel + x;
+                if (keep[k]) {
+                  oprobe[pos] = pr[k];
+                  obuild[pos] = br[k];
+                } else {
+                  const unsigned long long h = atomicAdd(nholes, 1ull);
+                  if ((int64_t)h < hcap) subcnt[h] = pos;
+                }
+              }
+              (void)c;
+            } else if constexpr (MODE == 1) {
               kept += c;
             } else {
               uint32_t tot2;
@@ -636,6 +655,25 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_emit_ranges(const RJSub *subs,
     uint32_t tk;
     block_exclusive_scan(kept, lds_sc, tk);
     if (threadIdx.x == 0) subcnt[blockIdx.x] = tk;
+  }
+}
+
+// MODE 3's holes (sorted): the pairs of the tail [total − nh, total) that are
+// not holes move into the holes below it, largest tail position first.  One
+// thread: the filters fused here (relationship uniqueness) fail on a handful
+// of pairs (a self-loop rel met twice).
+__global__ void k_rj_fill_holes(const uint64_t *holes, int64_t nh, int64_t total, int64_t *op, int64_t *ob) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int64_t m = total - nh;
+  int64_t hi = nh - 1, src = total - 1;
+  for (int64_t k = 0; k < nh && (int64_t)holes[k] < m; ++k) {
+    while (hi >= 0 && (int64_t)holes[hi] == src) {
+      --hi;
+      --src;
+    }
+    op[holes[k]] = op[src];
+    ob[holes[k]] = ob[src];
+    --src;
   }
 }
 
@@ -833,29 +871,66 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
       hipLaunchKernelGGL(k_rj_subs, dim3(grid_for(nw, 256)), dim3(256), 0, s->stream, (const int64_t *)cnt->p,
                          (const int64_t *)soff->p, nw, (RJSub *)subs->p);
       KERNEL_CHECK();
-      BufPtr subcnt = s->alloc(8 * ns), suboff = s->alloc(8 * (ns + 1));
+      // one pass: passing pairs at their unfiltered positions, failing ones
+      // listed as holes, then the tail's pairs moved into them
+      const int64_t hcap = std::min<int64_t>(total, int64_t(1) << 20);
+      BufPtr holes = s->alloc(8 * hcap), nh = s->alloc(8);
+      HIP_CHECK(hipMemsetAsync(nh->p, 0, 8, s->stream));
+      oprobe = s->alloc(8 * total);
+      obuild = s->alloc(8 * total);
       {
-        KernelTimer kt(s, "rj_join_filter_count", 12.0 * (double)(ps.n + bs.n));
-        hipLaunchKernelGGL(k_rj_emit_ranges<1>, dim3((unsigned)ns), dim3(RJ_JBLOCK), 0, s->stream,
-                           (const RJSub *)subs->p, (const RJWork *)dw->p, (const uint64_t *)bs.h->p,
-                           (const uint32_t *)bs.row->p, (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
-                           (const uint32_t *)ps.row->p, (const int64_t *)off->p, (int64_t *)nullptr,
-                           (int64_t *)nullptr, (uint8_t *)nullptr, (uint8_t *)nullptr, rp, build_left ? 1 : 0,
-                           (int64_t *)subcnt->p, (const int64_t *)nullptr);
-        KERNEL_CHECK();
-      }
-      jp.n = exclusive_scan_i64(s, (const int64_t *)subcnt->p, (int64_t *)suboff->p, ns);
-      if (jp.n > 0) {
-        oprobe = s->alloc(8 * jp.n);
-        obuild = s->alloc(8 * jp.n);
-        KernelTimer kt(s, "rj_join_emit", 12.0 * (double)(ps.n + bs.n) + 16.0 * (double)jp.n);
-        hipLaunchKernelGGL(k_rj_emit_ranges<2>, dim3((unsigned)ns), dim3(RJ_JBLOCK), 0, s->stream,
+        KernelTimer kt(s, "rj_join_filter_emit", 12.0 * (double)(ps.n + bs.n) + 16.0 * (double)total);
+        hipLaunchKernelGGL(k_rj_emit_ranges<3>, dim3((unsigned)ns), dim3(RJ_JBLOCK), 0, s->stream,
                            (const RJSub *)subs->p, (const RJWork *)dw->p, (const uint64_t *)bs.h->p,
                            (const uint32_t *)bs.row->p, (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
                            (const uint32_t *)ps.row->p, (const int64_t *)off->p, (int64_t *)oprobe->p,
                            (int64_t *)obuild->p, (uint8_t *)nullptr, (uint8_t *)nullptr, rp, build_left ? 1 : 0,
-                           (int64_t *)nullptr, (const int64_t *)suboff->p);
+                           (int64_t *)holes->p, (const int64_t *)nullptr, (unsigned long long *)nh->p, hcap);
         KERNEL_CHECK();
+      }
+      int64_t nholes = 0;
+      HIP_CHECK(hipMemcpyAsync(&nholes, nh->p, 8, hipMemcpyDeviceToHost, s->stream));
+      s->sync();
+      if (nholes <= hcap) {
+        if (nholes > 0) {
+          BufPtr sorted = s->alloc(8 * nholes);
+          size_t tmp = 0;
+          HIP_CHECK(rocprim::radix_sort_keys(nullptr, tmp, (const uint64_t *)holes->p, (uint64_t *)sorted->p,
+                                             (size_t)nholes, 0, 64, s->stream));
+          BufPtr t = s->alloc(std::max<size_t>(tmp, 16));
+          HIP_CHECK(rocprim::radix_sort_keys(t->p, tmp, (const uint64_t *)holes->p, (uint64_t *)sorted->p,
+                                             (size_t)nholes, 0, 64, s->stream));
+          hipLaunchKernelGGL(k_rj_fill_holes, dim3(1), dim3(64), 0, s->stream, (const uint64_t *)sorted->p, nholes,
+                             total, (int64_t *)oprobe->p, (int64_t *)obuild->p);
+          KERNEL_CHECK();
+        }
+        jp.n = total - nholes;
+      } else {
+        // many failing pairs: count the passes per sub-item, then write them
+        BufPtr subcnt = s->alloc(8 * ns), suboff = s->alloc(8 * (ns + 1));
+        {
+          KernelTimer kt(s, "rj_join_filter_count", 12.0 * (double)(ps.n + bs.n));
+          hipLaunchKernelGGL(k_rj_emit_ranges<1>, dim3((unsigned)ns), dim3(RJ_JBLOCK), 0, s->stream,
+                             (const RJSub *)subs->p, (const RJWork *)dw->p, (const uint64_t *)bs.h->p,
+                             (const uint32_t *)bs.row->p, (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
+                             (const uint32_t *)ps.row->p, (const int64_t *)off->p, (int64_t *)nullptr,
+                             (int64_t *)nullptr, (uint8_t *)nullptr, (uint8_t *)nullptr, rp, build_left ? 1 : 0,
+                             (int64_t *)subcnt->p, (const int64_t *)nullptr, (unsigned long long *)nullptr,
+                             (int64_t)0);
+          KERNEL_CHECK();
+        }
+        jp.n = exclusive_scan_i64(s, (const int64_t *)subcnt->p, (int64_t *)suboff->p, ns);
+        if (jp.n > 0) {
+          KernelTimer kt(s, "rj_join_emit", 12.0 * (double)(ps.n + bs.n) + 16.0 * (double)jp.n);
+          hipLaunchKernelGGL(k_rj_emit_ranges<2>, dim3((unsigned)ns), dim3(RJ_JBLOCK), 0, s->stream,
+                             (const RJSub *)subs->p, (const RJWork *)dw->p, (const uint64_t *)bs.h->p,
+                             (const uint32_t *)bs.row->p, (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
+                             (const uint32_t *)ps.row->p, (const int64_t *)off->p, (int64_t *)oprobe->p,
+                             (int64_t *)obuild->p, (uint8_t *)nullptr, (uint8_t *)nullptr, rp, build_left ? 1 : 0,
+                             (int64_t *)nullptr, (const int64_t *)suboff->p, (unsigned long long *)nullptr,
+                             (int64_t)0);
+          KERNEL_CHECK();
+        }
       }
     }
     jp.left = build_left ? obuild : oprobe;
@@ -880,7 +955,7 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
                        (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p, (const uint32_t *)ps.row->p,
                        (const int64_t *)off->p, (int64_t *)oprobe->p, (int64_t *)obuild->p,
                        p_outer ? (uint8_t *)pm->p : nullptr, b_outer ? (uint8_t *)bm->p : nullptr, RjPred{}, 0,
-                       (int64_t *)nullptr, (const int64_t *)nullptr);
+                       (int64_t *)nullptr, (const int64_t *)nullptr, (unsigned long long *)nullptr, (int64_t)0);
     KERNEL_CHECK();
   }
   // (total = 0: no pair, the outer sides' flags stay clear — every row is unmatched)

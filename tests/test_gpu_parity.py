@@ -320,9 +320,10 @@ def test_filter_over_join_parity(pred, paths, monkeypatch):
 def test_filter_fused_into_radix_join(pred, fused, monkeypatch):
     """WHERE over an inner radix join: the join's EMIT evaluates the terms per
     pair and writes only the passing pairs (radix_join.hip radix_join_filtered:
-    a count pass, then the write); CAPF_RJ_FILTER=0 joins, then filters.  Same
-    bag as the oracle; the fused kernels ran exactly when the predicate is a
-    conjunction of terms.  Many-to-many keys, NULL operands, hub keys."""
+    one pass, failing pairs' slots refilled from the tail); CAPF_RJ_FILTER=0
+    joins, then filters.  Same bag as the oracle; the fused kernels ran exactly
+    when the predicate is a conjunction of terms.  Many-to-many keys, NULL
+    operands, hub keys."""
     monkeypatch.setenv("CAPF_JOIN", "radix")
     monkeypatch.setenv("CAPF_RJ_FILTER", fused)
     rng = np.random.default_rng(13)
@@ -349,8 +350,42 @@ def test_filter_fused_into_radix_join(pred, fused, monkeypatch):
     gs.set_profiling(False)
     want = ol.join(orr, "inner", ("ka", "kb")).filter(pred, JH, {}).rows
     assert len(want) > 0
-    assert ("rj_join_filter_count" in gs.profile()) == (fused == "1" and not isinstance(pred, Ors))
+    assert ("rj_join_filter_emit" in gs.profile()) == (fused == "1" and not isinstance(pred, Ors))
     assert bag(got) == bag(want)
+
+
+@pytest.mark.parametrize("fail", ["few", "many"])
+def test_filter_fused_radix_holes(gpu_session, monkeypatch, fail):
+    """The one-pass filtered EMIT: failing pairs leave holes that the tail's
+    pairs fill (a few: the uniqueness filter's self-loop pairs); past 2^20
+    holes (here x < y fails on ~1.2 M of 2.56 M hub pairs) the join counts the
+    passes per sub-item first and writes them compactly.  Exact pair set
+    against numpy."""
+    monkeypatch.setenv("CAPF_JOIN", "radix")
+    rng = np.random.default_rng(31)
+    n = 1600
+    x = rng.integers(0, 40, n).astype(np.int64)
+    y = rng.integers(0, 40, n).astype(np.int64)
+    if fail == "few":
+        y = np.full(n, 1000, dtype=np.int64)  # x < y everywhere but in the right rows set below
+        y[::97] = -1
+    k = np.full(n, 7, dtype=np.int64)
+    gl = gpu_session.table([("x", T_INT, x, None), ("ka", T_INT, k, None), ("li", T_INT, np.arange(n), None)])
+    gr = gpu_session.table([("y", T_INT, y, None), ("kb", T_INT, k, None), ("ri", T_INT, np.arange(n), None)])
+    hdr = RecordHeader({Var("x"): "x", Var("y"): "y", Var("ka"): "ka", Var("kb"): "kb",
+                        Var("li"): "li", Var("ri"): "ri"})
+    gpu_session.reset_profile()
+    gpu_session.set_profiling(True)
+    out = gl.join(gr, "inner", ("ka", "kb")).filter(LessThan(Var("x"), Var("y")), hdr, {})
+    li, _ = out.column_arrays("li")
+    ri, _ = out.column_arrays("ri")
+    gpu_session.set_profiling(False)
+    prof = gpu_session.profile()
+    assert "rj_join_filter_emit" in prof
+    assert ("rj_join_filter_count" in prof) == (fail == "many")
+    wl, wr = np.nonzero(x[:, None] < y[None, :])
+    got = np.sort(li.astype(np.int64) * n + ri)
+    assert np.array_equal(got, np.sort(wl.astype(np.int64) * n + wr))
 
 
 @pytest.mark.parametrize("jt", ["left_outer", "right_outer", "full_outer"])

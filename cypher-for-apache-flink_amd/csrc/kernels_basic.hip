@@ -224,11 +224,55 @@ __global__ void k_gather(const T *src, const uint8_t *sval, const int64_t *idx, 
 // values stored as one 4·sizeof(T) vector and the validity as one u32 (a
 // 1-B store per row leaves the byte columns at ~1 TB/s).
 template <typename T>
+__device__ inline void gather_quad_store(T *dst, uint8_t *dval, int64_t q, const T (&v)[4], uint32_t vm) {
+  if (dst) {
+    if (sizeof(T) == 1) {
+      ((uint32_t *)dst)[q] = (uint32_t)(uint8_t)v[0] | (uint32_t)(uint8_t)v[1] << 8 |
+                             (uint32_t)(uint8_t)v[2] << 16 | (uint32_t)(uint8_t)v[3] << 24;
+    } else if (sizeof(T) == 4) {
+      ((uint4 *)dst)[q] = make_uint4((uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]);
+    } else {
+      ((longlong2 *)dst)[2 * q] = make_longlong2((long long)v[0], (long long)v[1]);
+      ((longlong2 *)dst)[2 * q + 1] = make_longlong2((long long)v[2], (long long)v[3]);
+    }
+  }
+  if (dval) ((uint32_t *)dval)[q] = vm;
+}
+
+// Two quads per thread per step: both quads' index loads, then all eight
+// value loads, are in flight together (one quad at a time left the gather
+// latency bound: 0.48 ms for 119 M FOR32 rows).
+template <typename T>
 __global__ void k_gather4(const T *src, const uint8_t *sval, const int64_t *idx, T *dst,
                           uint8_t *dval, int64_t m) {
   const int64_t m4 = m / 4;
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m4;
-       q += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; q + stride < m4; q += 2 * stride) {
+    const int64_t qq[2] = {q, q + stride};
+    int64_t j[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const longlong2 a = ((const longlong2 *)idx)[2 * qq[h]], b = ((const longlong2 *)idx)[2 * qq[h] + 1];
+      j[h][0] = a.x;
+      j[h][1] = a.y;
+      j[h][2] = b.x;
+      j[h][3] = b.y;
+    }
+    T v[2][4];
+    uint32_t vm[2] = {0, 0};
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool ok = j[h][k] >= 0;
+        v[h][k] = ok && dst ? src[j[h][k]] : T(0);
+        vm[h] |= (uint32_t)(ok ? (sval ? sval[j[h][k]] : 1) : 0) << (8 * k);
+      }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) gather_quad_store(dst, dval, qq[h], v[h], vm[h]);
+  }
+  for (; q < m4; q += stride) {
     const longlong2 a = ((const longlong2 *)idx)[2 * q], b = ((const longlong2 *)idx)[2 * q + 1];
     const int64_t j[4] = {a.x, a.y, b.x, b.y};
     T v[4];
@@ -239,18 +283,7 @@ __global__ void k_gather4(const T *src, const uint8_t *sval, const int64_t *idx,
       v[k] = ok && dst ? src[j[k]] : T(0);
       vm |= (uint32_t)(ok ? (sval ? sval[j[k]] : 1) : 0) << (8 * k);
     }
-    if (dst) {
-      if (sizeof(T) == 1) {
-        ((uint32_t *)dst)[q] = (uint32_t)(uint8_t)v[0] | (uint32_t)(uint8_t)v[1] << 8 |
-                               (uint32_t)(uint8_t)v[2] << 16 | (uint32_t)(uint8_t)v[3] << 24;
-      } else if (sizeof(T) == 4) {
-        ((uint4 *)dst)[q] = make_uint4((uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]);
-      } else {
-        ((longlong2 *)dst)[2 * q] = make_longlong2((long long)v[0], (long long)v[1]);
-        ((longlong2 *)dst)[2 * q + 1] = make_longlong2((long long)v[2], (long long)v[3]);
-      }
-    }
-    if (dval) ((uint32_t *)dval)[q] = vm;
+    gather_quad_store(dst, dval, q, v, vm);
   }
   if (blockIdx.x == 0 && threadIdx.x < (unsigned)(m - 4 * m4)) {
     const int64_t i = 4 * m4 + threadIdx.x;

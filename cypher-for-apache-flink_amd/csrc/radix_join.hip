@@ -659,21 +659,44 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_emit_ranges(const RJSub *subs,
 }
 
 // MODE 3's holes (sorted): the pairs of the tail [total − nh, total) that are
-// not holes move into the holes below it, largest tail position first.  One
-// thread: the filters fused here (relationship uniqueness) fail on a handful
-// of pairs (a self-loop rel met twice).
-__global__ void k_rj_fill_holes(const uint64_t *holes, int64_t nh, int64_t total, int64_t *op, int64_t *ob) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// not holes move into the holes below it — the k-th hole below the tail
+// takes the k-th non-hole tail position counted from the end, p = total − 1 −
+// k − #{tail holes > p}, found by fixed-point steps (binary searches of the
+// sorted holes) and stepped down past holes.  One workgroup; the filters fused
+// here (relationship uniqueness) fail on few pairs (a self-loop rel met twice).
+__device__ inline int64_t rj_count_above(const uint64_t *h, int64_t lo, int64_t hi, int64_t p) {
+  // entries of the sorted h[lo, hi) greater than p
+  int64_t a = lo, b = hi;
+  while (a < b) {
+    const int64_t mid = (a + b) >> 1;
+    if ((int64_t)h[mid] > p) b = mid;
+    else a = mid + 1;
+  }
+  return hi - a;
+}
+
+__global__ __launch_bounds__(1024) void k_rj_fill_holes(const uint64_t *holes, int64_t nh, int64_t total,
+                                                        int64_t *op, int64_t *ob) {
   const int64_t m = total - nh;
-  int64_t hi = nh - 1, src = total - 1;
-  for (int64_t k = 0; k < nh && (int64_t)holes[k] < m; ++k) {
-    while (hi >= 0 && (int64_t)holes[hi] == src) {
-      --hi;
-      --src;
+  // holes below the tail: holes[0, nb)
+  int64_t a = 0, b = nh;
+  while (a < b) {
+    const int64_t mid = (a + b) >> 1;
+    if ((int64_t)holes[mid] < m) a = mid + 1;
+    else b = mid;
+  }
+  const int64_t nb = a;
+  for (int64_t k = threadIdx.x; k < nb; k += blockDim.x) {
+    int64_t p = total - 1 - k;
+    for (;;) {
+      const int64_t q = total - 1 - k - rj_count_above(holes, nb, nh, p);
+      if (q == p) break;
+      p = q;
     }
-    op[holes[k]] = op[src];
-    ob[holes[k]] = ob[src];
-    --src;
+    while (rj_count_above(holes, nb, nh, p - 1) != rj_count_above(holes, nb, nh, p)) --p;  // p is a hole
+    const int64_t d = (int64_t)holes[k];
+    op[d] = op[p];
+    ob[d] = ob[p];
   }
 }
 
@@ -900,7 +923,7 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
           BufPtr t = s->alloc(std::max<size_t>(tmp, 16));
           HIP_CHECK(rocprim::radix_sort_keys(t->p, tmp, (const uint64_t *)holes->p, (uint64_t *)sorted->p,
                                              (size_t)nholes, 0, 64, s->stream));
-          hipLaunchKernelGGL(k_rj_fill_holes, dim3(1), dim3(64), 0, s->stream, (const uint64_t *)sorted->p, nholes,
+          hipLaunchKernelGGL(k_rj_fill_holes, dim3(1), dim3(1024), 0, s->stream, (const uint64_t *)sorted->p, nholes,
                              total, (int64_t *)oprobe->p, (int64_t *)obuild->p);
           KERNEL_CHECK();
         }

@@ -40,7 +40,7 @@ namespace capf {
 constexpr int RJ_P = 256;          // buckets per radix pass
 constexpr int RJ_TILE = 8192;      // rows per partitioning tile
 constexpr int RJ_PBLOCK = 512;     // partitioning workgroup
-constexpr int RJ_CAP = 4096;       // LDS multimap slots (h 8 B + row 4 B)
+constexpr int RJ_CAP = 2048;       // LDS build rows per chunk × 2 (2 Ki: 3 join workgroups per CU)
 constexpr int RJ_CHUNK = RJ_CAP / 2;  // build rows per LDS fill (load ≤ 1/2)
 constexpr int RJ_PCHUNK = 8192;    // probe rows per work item (at most)
 constexpr int RJ_PCHUNK_MIN = 256; // ... and at least, when the probe side is small
@@ -303,7 +303,7 @@ struct RJWork {
 // pass is k_rj_emit_ranges over output ranges).  (Measured and removed: a
 // chain-walking multimap join, and an EMIT inside this kernel — one wave wrote
 // a hub key's whole product.)
-constexpr int RJ_RUNCAP = 4096;  // run-table slots (≤ RJ_CHUNK runs per chunk, load ≤ 1/2)
+constexpr int RJ_RUNCAP = 2048;  // run-table slots (≤ RJ_CHUNK runs per chunk, load ≤ 1/2)
 
 __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_join_runs(const RJWork *work, const uint64_t *bh,
                                                              const int64_t *bstart, const uint64_t *ph,

@@ -988,8 +988,12 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   uint32_t ovf_cap = 0;
   const int64_t acc_bytes = c5_post_acc_bytes(nr, S, sd.split_x16, nkeys, &max_units, &ovf_cap);
   // P3 reads run-major meta (transposed here); reading P1's tile-major meta in
-  // place saved 7 µs of transpose and cost P3 7..20 µs at s24 (measured, removed)
-  BufPtr meta_t = s->alloc(4 * nr * ntiles);
+  // place saved 7 µs of transpose and cost P3 7..20 µs at s24 (measured).  A
+  // node-partitioned rank's static work list needs no run totals, and its few
+  // runs (≤ 64 at G = 8) share each tile's meta lines: P3 reads them in place,
+  // no transpose launch.
+  const bool in_place = static_units && !post;
+  BufPtr meta_t = in_place ? BufPtr() : s->alloc(4 * nr * ntiles);
   // transpose blocks: tiles per block tt, fewer when there are few runs (≥ ~1024 blocks)
   int64_t tt = C3_TT;
   // (s24: 128 tiles per block 34 µs, 64 41 µs, 32 54 µs — fewer, longer blocks win;
@@ -1017,7 +1021,7 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   if (!acc_pre) HIP_CHECK(hipMemsetAsync(acc->p, 0, 4 * (size_t)c5_post_zero_words(nr, ovf_cap), s->stream));
   // units in the XCD-grouped run order (largest-first order: measured no gain)
   const C3UnitsOut uo{units, nunits, split};
-  {
+  if (!in_place) {
     KernelTimer kt(s, "c3_transpose", 8.0 * nr * ntiles);
     hipLaunchKernelGGL(k_c3_transpose, dim3((unsigned)nparts, (nr + 31) / 32), dim3(256), 0, s->stream, meta,
                        (uint32_t *)meta_t->p, ntiles, nr, run_total, tt, nullptr,
@@ -1041,8 +1045,8 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
     const int grid = static_units ? (nr * S + 255) / 256 * 256 : max_units;
     hipLaunchKernelGGL(k_c5_gather<C5_PPS>, dim3((unsigned)grid), dim3(C5_BLOCK), C5_GATHER_LDS, s->stream,
                        static_units ? nullptr : (const C3Unit *)units, (const int32_t *)nunits, part,
-                       (const uint32_t *)meta_t->p, ntiles, sd.nb, rstride, h_in, h_out, slice_stride, ovf,
-                       sdk, S, (int64_t)1);
+                       in_place ? meta : (const uint32_t *)meta_t->p, ntiles, sd.nb, rstride, h_in, h_out,
+                       slice_stride, ovf, sdk, S, in_place ? (int64_t)nr : (int64_t)1);
     KERNEL_CHECK();
   }
   if (sd.packed) {  // the hand-offs are applied by k_c5_dot_packed

@@ -982,6 +982,23 @@ __device__ Val run_program(const Instr *code, int ncode, const ColView *cols, in
         st[sp++] = (x.nul || y.nul) ? mknull(CAPF_TYPE_FLOAT64) : mkf(atan2(vf(y), vf(x)));
         break;
       }
+      case OP_IN_SET: {  // cols[in.i] = sorted set values, base = their count
+        Val a = st[--sp];
+        if (a.nul) {
+          st[sp++] = mknull(CAPF_TYPE_BOOL);
+          break;
+        }
+        const int64_t *v = (const int64_t *)cols[in.i].data;
+        int64_t lo = 0, hi = cols[in.i].base;
+        while (lo < hi) {
+          const int64_t mid = (lo + hi) >> 1;
+          if (v[mid] < a.b) lo = mid + 1;
+          else hi = mid;
+        }
+        const bool hit = lo < cols[in.i].base && v[lo] == a.b;
+        st[sp++] = hit ? mkb(true) : in.f != 0.0 ? mknull(CAPF_TYPE_BOOL) : mkb(false);
+        break;
+      }
       case OP_TO_BOOLEAN: {  // cols[in.i] = the session's strings parsed as booleans
         Val a = st[--sp];
         if (a.nul || a.t == CAPF_TYPE_BOOL) {
@@ -1044,6 +1061,14 @@ static DeviceProgram upload_program(Session *s, const Program &p,
     if (in.op == OP_COL && in.i >= 0 && (size_t)in.i < p.names.size()) scalar_use[(size_t)in.i] = 1;
   for (size_t j = 0; j < p.names.size(); ++j) {
     const std::string &nm = p.names[j];
+    if (is_literal_set_name(nm)) {  // sorted set values, count in `base`
+      const long id = atol(nm.c_str() + 5);
+      std::lock_guard<std::mutex> g(s->user_mu);
+      if (id < 0 || (size_t)id >= s->literal_sets.size()) illegal("unknown literal set '" + nm.substr(1) + "'");
+      const auto &ls = s->literal_sets[(size_t)id];
+      views.push_back(ColView{ls.first->p, nullptr, (int32_t)Type::Int64, ENC_PLAIN, ls.second});
+      continue;
+    }
     int idx = -1;
     for (size_t k = 0; k < names.size(); ++k)
       if (names[k] == nm) idx = (int)k;
@@ -1090,7 +1115,7 @@ static DeviceProgram upload_program(Session *s, const Program &p,
       case OP_LIT_NULL: case OP_LIST_SIZE: depth++; break;
       case OP_AND: case OP_OR: case OP_COALESCE: depth -= (int)in.i - 1; break;
       case OP_NOT: case OP_IS_NULL: case OP_IS_NOT_NULL: case OP_NEG: case OP_TO_FLOAT:
-      case OP_TO_INTEGER: case OP_STR_LEN: case OP_TO_BOOLEAN: break;
+      case OP_TO_INTEGER: case OP_STR_LEN: case OP_TO_BOOLEAN: case OP_IN_SET: break;
       case OP_IF: depth -= 2; break;
       default:
         if (!is_math1(in.op)) depth -= 1;  // binary operators; unary math keeps the depth

@@ -303,6 +303,14 @@ Type infer_type(const Program &p, const std::vector<std::string> &names,
         st.push_back(r);
         break;
       }
+      case OP_IN_SET: {
+        if (in.i < 0 || (size_t)in.i >= p.names.size() || !is_literal_set_name(p.names[in.i]))
+          illegal("malformed expression program (literal set)");
+        Type a = pop();
+        if (a != Type::Int64 && a != Type::String && a != Type::Null) illegal("IN set over a non-integer value");
+        st.push_back(Type::Bool);
+        break;
+      }
       case OP_STR_LEN: {
         Type a = pop();
         if (a != Type::String && a != Type::Null) illegal("size() of a non-string value");
@@ -823,6 +831,31 @@ capf_status capf_session_copy(capf_session *cs, void *dst, const void *src, int6
   const hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
   HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)bytes, k, cs->impl.stream));
   cs->impl.sync();
+  CAPF_API_END
+}
+
+capf_status capf_session_literal_set(capf_session *cs, const int64_t *values, int64_t n, int32_t *set_id) {
+  CAPF_API_BEGIN
+  need(cs, "session");
+  need(set_id, "set_id");
+  if (n < 0 || (n > 0 && !values)) illegal("bad literal set");
+  std::vector<int64_t> v(values, values + n);
+  std::sort(v.begin(), v.end());
+  v.erase(std::unique(v.begin(), v.end()), v.end());
+  Session &s = cs->impl;
+  std::lock_guard<std::mutex> g(s.user_mu);
+  auto it = s.literal_set_ids.find(v);
+  if (it != s.literal_set_ids.end()) {
+    *set_id = it->second;
+    return CAPF_OK;
+  }
+  BufPtr b = s.alloc(8 * std::max<int64_t>((int64_t)v.size(), 1));
+  if (!v.empty()) HIP_CHECK(hipMemcpyAsync(b->p, v.data(), 8 * v.size(), hipMemcpyHostToDevice, s.stream));
+  s.sync();  // (pageable source)
+  const int32_t id = (int32_t)s.literal_sets.size();
+  s.literal_sets.emplace_back(b, (int64_t)v.size());
+  s.literal_set_ids.emplace(std::move(v), id);
+  *set_id = id;
   CAPF_API_END
 }
 

@@ -36,7 +36,8 @@ OP_TO_FLOAT, OP_TO_INTEGER, OP_COALESCE = 40, 41, 50
 OP_STR_LEN, OP_LIST_SIZE, OP_IF = 60, 61, 62
 OP_ROUND, OP_ABS, OP_CEIL, OP_FLOOR, OP_SIGN, OP_SQRT, OP_LOG, OP_LOG10, OP_EXP = 70, 71, 72, 73, 74, 75, 76, 77, 78
 OP_SIN, OP_COS, OP_TAN, OP_ASIN, OP_ACOS, OP_ATAN, OP_DEGREES, OP_RADIANS = 79, 80, 81, 82, 83, 84, 85, 86
-OP_ATAN2, OP_TO_BOOLEAN = 87, 88
+OP_ATAN2, OP_TO_BOOLEAN, OP_IN_SET = 87, 88, 89
+IN_SET_MIN = 17  # list length from which IN runs as a session-set lookup (shorter: an OR of equalities)
 
 # aggregators
 AGG_COUNT_STAR, AGG_COUNT, AGG_SUM, AGG_MIN, AGG_MAX, AGG_AVG, AGG_COLLECT = 0, 1, 2, 3, 4, 5, 6
@@ -582,7 +583,7 @@ class _ParamsView:
         return v
 
 
-def _lookups_hold(log, header, columns, params, intern, coltype):
+def _lookups_hold(log, header, columns, params, intern, coltype, lset=None):
     params = params or {}
     for kind, k, v in log:
         if kind == 0:
@@ -598,12 +599,15 @@ def _lookups_hold(log, header, columns, params, intern, coltype):
         elif kind == 3:
             if coltype is None or coltype(k) != v:
                 return False
+        elif kind == 5:
+            if lset is None or lset(k) != v:
+                return False
         elif intern is None or intern(k) != v:
             return False
     return True
 
 
-def compile_program(expr, header, columns, params=None, intern=None, coltype=None):
+def compile_program(expr, header, columns, params=None, intern=None, coltype=None, lset=None):
     """Lower `expr` to (ops, iargs, fargs, names) for the C-ABI — memoised per
     expression: a program is reused when every lookup its compilation made
     (header columns, column presence and types, parameters, string codes)
@@ -612,13 +616,13 @@ def compile_program(expr, header, columns, params=None, intern=None, coltype=Non
     try:
         key = _memo_key(expr)
     except AttributeError:  # not an Expr instance: compile every time
-        return _compile_program(expr, header, columns, params, intern, coltype)
+        return _compile_program(expr, header, columns, params, intern, coltype, lset)
     ent = _PROGRAM_MEMO.get(key)
     if ent is not None and header is not None and ent[0] is not None and \
-            _lookups_hold(ent[0], header, columns, params, intern, coltype):
+            _lookups_hold(ent[0], header, columns, params, intern, coltype, lset):
         return ent[1]
     if header is None:
-        return _compile_program(expr, header, columns, params, intern, coltype)
+        return _compile_program(expr, header, columns, params, intern, coltype, lset)
     rec = _Lookups(header, columns, params, intern, coltype)
 
     def rec_type(c):
@@ -631,9 +635,15 @@ def compile_program(expr, header, columns, params=None, intern=None, coltype=Non
         rec.log.append((4, x, v))
         return v
 
+    def rec_lset(vals):
+        v = lset(vals)
+        rec.log.append((5, vals, v))
+        return v
+
     prog = _compile_program(expr, rec, _ColumnsView(rec), _ParamsView(rec),
                             rec_intern if intern is not None else None,
-                            rec_type if coltype is not None else None)
+                            rec_type if coltype is not None else None,
+                            rec_lset if lset is not None else None)
     prog = (tuple(prog[0]), tuple(prog[1]), tuple(prog[2]), tuple(prog[3]))
     if rec.cacheable:
         if len(_PROGRAM_MEMO) >= 4096:
@@ -642,7 +652,7 @@ def compile_program(expr, header, columns, params=None, intern=None, coltype=Non
     return prog
 
 
-def _compile_program(expr, header, columns, params=None, intern=None, coltype=None):
+def _compile_program(expr, header, columns, params=None, intern=None, coltype=None, lset=None):
     """Lower `expr` to (ops, iargs, fargs, names) for the C-ABI.
 
     header: dict Expr -> physical column; columns: set of the table's columns;
@@ -815,6 +825,16 @@ def _compile_program(expr, header, columns, params=None, intern=None, coltype=No
                 not_impl(e)  # nested lists / maps
             if not cand:
                 emit(OP_LIT_NULL, T_BOOL)  # no element could be of lhs's type (:117)
+                return
+            vals_nn = [v for v in cand if v is not None]
+            same = (lt == T_INT and all(_value_type(v) == T_INT for v in vals_nn)) or \
+                (lt == T_STRING and intern is not None and all(isinstance(v, str) for v in vals_nn))
+            if lset is not None and same and len(cand) >= IN_SET_MIN:
+                # a long list: one binary search per row in a sorted session set
+                # (an element NULL → a miss is NULL, as the OR of equalities gives)
+                codes = tuple(sorted(set(intern(v) if lt == T_STRING else int(v) for v in vals_nn)))
+                go(e.lhs)
+                emit(OP_IN_SET, name_of(lset(codes)), 1.0 if len(vals_nn) < len(cand) else 0.0)
                 return
             # left-folded 3-valued OR of equalities: stack depth 3 whatever the list length
             for k, v in enumerate(cand):

@@ -36,6 +36,19 @@ class GpuSession:
         self._h = h
         self._strings = {}
         self._codes = {}
+        self._sets = {}
+
+    def literal_set(self, values):
+        """Program name of the session literal set of `values` (int64 values
+        or string codes) for CAPF_OP_IN_SET: "\x01set:<id>"."""
+        key = tuple(sorted(set(values)))
+        nm = self._sets.get(key)
+        if nm is None:
+            arr = (c_int64 * max(len(key), 1))(*key)
+            sid = c_int32()
+            _lib.call("capf_session_literal_set", self._h, arr, len(key), byref(sid))
+            nm = self._sets[key] = "\x01set:%d" % sid.value
+        return nm
 
     @classmethod
     def on_torch_stream(cls, device=0):
@@ -210,7 +223,7 @@ _SELECT_ARGS = {}
 
 def _program(expr, header, table, params):
     return compile_program(expr, header, set(table.physicalColumns), params, table.session.intern,
-                           table.capf_type)
+                           table.capf_type, getattr(table.session, "literal_set", None))
 
 
 class GpuTable:

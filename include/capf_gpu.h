@@ -188,7 +188,13 @@ enum {
   /* ToBoolean (:185, Flink cast to BOOLEAN): BOOLEAN unchanged, STRING
    * 'true' / 'false' (any case, trimmed) → TRUE / FALSE, any other string
    * → NULL.  Uses the session's device table of string → boolean codes.     */
-  CAPF_OP_TO_BOOLEAN = 88
+  CAPF_OP_TO_BOOLEAN = 88,
+  /* x IN [list] over a long INTEGER / STRING list (FlinkSQLExprMapper.scala:
+   * 114-118 lowers IN to Flink's `in`): pops x; pushes TRUE when x is in the
+   * session literal set names[i] (capf_session_literal_set, referenced as
+   * "\x01set:<id>"), else NULL when x is NULL or farg != 0 (the list held a
+   * NULL), else FALSE.  One binary search per row over the sorted set.       */
+  CAPF_OP_IN_SET = 89
 };
 
 typedef struct capf_expr {
@@ -587,6 +593,12 @@ capf_status capf_comm_all_to_all_bytes(capf_comm *c, const void *d_send, const i
 capf_status capf_session_alloc(capf_session *s, int64_t bytes, void **d_out);
 capf_status capf_session_free(capf_session *s, void *d);
 capf_status capf_session_copy(capf_session *s, void *dst, const void *src, int64_t bytes, int32_t kind);
+
+/* A literal set for CAPF_OP_IN_SET: the n int64 values (INTEGER values or
+ * STRING dictionary codes) sorted and deduplicated into device memory owned by
+ * the session; *set_id names it in programs as "\x01set:<set_id>".  The same
+ * values registered again return the same id. */
+capf_status capf_session_literal_set(capf_session *s, const int64_t *values, int64_t n, int32_t *set_id);
 
 #ifdef __cplusplus
 }

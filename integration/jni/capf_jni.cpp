@@ -772,6 +772,13 @@ JNI(void, sessionCopy)(JNIEnv *env, jobject, jlong s, jlong d, jobject host, jlo
   if (kind == 1) fail(env, capf_session_copy(S(s), reinterpret_cast<void *>(d), h, bytes, 1));
   else fail(env, capf_session_copy(S(s), h, reinterpret_cast<const void *>(d), bytes, 2));
 }
+// the session literal set of a long IN list (CAPF_OP_IN_SET): its id
+JNI(jint, sessionLiteralSet)(JNIEnv *env, jobject, jlong s, jlongArray values) {
+  const std::vector<int64_t> v = longs(env, values);
+  int32_t id = -1;
+  if (fail(env, capf_session_literal_set(S(s), v.data(), (int64_t)v.size(), &id))) return -1;
+  return id;
+}
 // device → device
 JNI(void, sessionCopyDevice)(JNIEnv *env, jobject, jlong s, jlong dst, jlong src, jlong bytes) {
   fail(env, capf_session_copy(S(s), reinterpret_cast<void *>(dst), reinterpret_cast<const void *>(src), bytes, 3));

@@ -47,6 +47,14 @@ final class GpuCypherSession private (val device: Int, hipStream: Long)
     strings.getOrElseUpdate(s, Native.guard(Native.stringIntern(handle, s)))
   }
 
+  private val sets = scala.collection.mutable.HashMap.empty[Seq[Long], String]
+
+  /** Program name of the session literal set of `values` (CAPF_OP_IN_SET). */
+  def literalSet(values: Seq[Long]): String = sets.synchronized {
+    val key = values.distinct.sorted
+    sets.getOrElseUpdate(key, "\u0001set:" + Native.sessionLiteralSet(handle, key.toArray))
+  }
+
   // ------------------------------------------------------------ table sources
   /** The one-row, zero-column table (RelationalCypherRecordsFactory.unit). */
   def unitTable(): GpuTable = GpuTable(Native.guard(Native.tableUnit(handle)))

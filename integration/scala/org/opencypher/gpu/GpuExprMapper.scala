@@ -38,7 +38,8 @@ object GpuExprMapper {
   private final val Sin_ = 79; private final val Cos_ = 80; private final val Tan_ = 81
   private final val Asin_ = 82; private final val Acos_ = 83; private final val Atan_ = 84
   private final val Degrees_ = 85; private final val Radians_ = 86; private final val Atan2_ = 87
-  private final val ToBoolean_ = 88
+  private final val ToBoolean_ = 88; private final val InSet = 89
+  private final val InSetMin = 17  // IN lists from this length: one set lookup per row (expr.py IN_SET_MIN)
 
   def program(expr: Expr, header: RecordHeader, table: GpuTable, parameters: CypherMap): Program = {
     val ops = mutable.ArrayBuffer.empty[Int]
@@ -138,8 +139,18 @@ object GpuExprMapper {
         if (vals.isEmpty) emit(LitBool, 0L)                                // CTList(CTVoid) → FALSE
         else {
           val cand = vals.filter(v => comparable(lhs.cypherType, v))
+          val nonNull = cand.filter(_ != CypherNull)
+          val keys: Option[Seq[Long]] = lhs.cypherType.material match {
+            case CTInteger if nonNull.forall(_.isInstanceOf[CypherInteger]) =>
+              Some(nonNull.map(_.asInstanceOf[CypherInteger].value))
+            case CTString if nonNull.forall(_.isInstanceOf[CypherString]) =>
+              Some(nonNull.map(v => session.intern(v.asInstanceOf[CypherString].value)))
+            case _ => None
+          }
           if (cand.isEmpty) emit(LitNull, Native.TypeBool)                 // incompatible element type → NULL
-          else cand.zipWithIndex.foreach { case (v, k) =>                  // left-folded 3-valued OR
+          else if (cand.size >= InSetMin && keys.isDefined) {              // a long list: sorted-set lookup
+            go(lhs); emit(InSet, nameIndex(session.literalSet(keys.get)), if (nonNull.size < cand.size) 1.0 else 0.0)
+          } else cand.zipWithIndex.foreach { case (v, k) =>                // left-folded 3-valued OR
             go(lhs); lit(v); emit(Eq); if (k > 0) emit(Or, 2L)
           }
         }

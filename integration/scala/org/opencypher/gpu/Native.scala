@@ -200,4 +200,5 @@ object Native {
   @native def sessionFree(session: Long, d: Long): Unit
   @native def sessionCopy(session: Long, d: Long, host: ByteBuffer, bytes: Long, kind: Int): Unit
   @native def sessionCopyDevice(session: Long, dst: Long, src: Long, bytes: Long): Unit
+  @native def sessionLiteralSet(session: Long, values: Array[Long]): Int
 }

@@ -1263,3 +1263,42 @@ def test_sharded_heavy_hitter_hints(gpu_session, hot):
         assert int(part.item()) == expect, (p, hot, out_copy.hot_ids)
         total += expect
     assert total == cmodel.count_2hop(src, dst, n)
+
+
+@pytest.mark.usefixtures("encoding")
+@pytest.mark.parametrize("case", ["ints", "ints_with_null", "strings", "param_ids", "short"])
+def test_in_long_list_set_lookup(case):
+    """x IN a long list (≥ 17 elements, FlinkSQLExprMapper.scala:114-118): one
+    binary search per row in a sorted session literal set (CAPF_OP_IN_SET)
+    instead of an OR of equalities per element; three-valued as the OR — a NULL
+    x, or a miss when the list holds a NULL, is NULL.  Same rows as the oracle,
+    a second query reuses the memoised program, and the program carries the
+    set opcode exactly for the long lists."""
+    from capf_amd.expr import In, ListLit, Param, OP_IN_SET, compile_program
+    rng = np.random.default_rng(17)
+    n = 4000
+    ids = [int(x) if rng.random() > 0.05 else None for x in rng.integers(0, 3000, n)]
+    words = [f"w{int(x)}" if rng.random() > 0.05 else None for x in rng.integers(0, 60, n)]
+    cols = [("k", T_INT, ids, None), ("s", T_STRING, words, None), ("i", T_INT, list(range(n)), None)]
+    g, o = _both(cols)
+    h = RecordHeader({Var("k"): "k", Var("s"): "s", Var("i"): "i"})
+    params = {}
+    if case == "ints":
+        pred = In(Var("k"), ListLit(*[IntegerLit(int(v)) for v in rng.integers(0, 3000, 40)]))
+    elif case == "ints_with_null":
+        pred = Not(In(Var("k"), ListLit(*([IntegerLit(int(v)) for v in rng.integers(0, 3000, 30)]
+                                                    + [NullLit("INTEGER")]))))
+    elif case == "strings":
+        pred = In(Var("s"), ListLit(*[StringLit(f"w{int(v)}") for v in rng.integers(0, 80, 25)]))
+    elif case == "param_ids":
+        params = {"ids": [int(v) for v in rng.integers(0, 3000, 1000)]}
+        pred = In(Var("k"), Param("ids"))
+    else:  # below the threshold: the OR of equalities
+        pred = In(Var("k"), ListLit(*[IntegerLit(int(v)) for v in rng.integers(0, 3000, 5)]))
+    for _ in range(2):
+        got = g.filter(pred, h, params).rows
+        want = o.filter(pred, h, params).rows
+        assert bag(got) == bag(want)
+    prog = compile_program(pred, h, set(g.physicalColumns), params, g.session.intern, g.capf_type,
+                           g.session.literal_set)
+    assert (OP_IN_SET in prog[0]) == (case != "short")

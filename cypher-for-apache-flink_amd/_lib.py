@@ -13,7 +13,9 @@ import os
 from ctypes import POINTER, c_char_p, c_double, c_int32, c_int64, c_uint8, c_uint32, c_uint64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcapf_gpu.so")
+# CAPF_LIB_AB (A/B timing of two builds only): an alternative in-tree build
+# of the same library, e.g. ab/libcapf_gpu_a.so; never set in production.
+LIB_PATH = os.path.join(_HERE, os.environ.get("CAPF_LIB_AB", "libcapf_gpu.so"))
 
 
 class CypherException(RuntimeError):

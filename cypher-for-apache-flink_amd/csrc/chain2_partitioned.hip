@@ -723,7 +723,7 @@ __global__ __launch_bounds__(C5_BLOCK) void k_c5_gather(const C3Unit *units,
     const int64_t tn = tb + WAVE + lane;
     wpre = tn < w1 ? m[tn * mstride] : 0u;
     __builtin_amdgcn_wave_barrier();
-    return (uint32_t)__builtin_amdgcn_readfirstlane(__shfl(inc, WAVE - 1, WAVE));
+    return (uint32_t)__builtin_amdgcn_readlane(inc, WAVE - 1);
   };
   // total > 0.  Past-the-end lanes load a valid piece (the last one) and
   // replace it with their dead keys: every load is unconditional, so the

@@ -61,9 +61,23 @@ inline NodeMix node_mix_for(int kbits) {
 
 __device__ inline int lane_id() { return threadIdx.x & (WAVE - 1); }
 
-// Inclusive wave64 prefix sum.
+// Inclusive wave64 prefix sum.  32-bit values scan through DPP: row_shr 1, 2,
+// 4, 8 inside each 16-lane row, then row_bcast15 / row_bcast31 carry row
+// totals across; out-of-range sources read the `old` operand (0).  No lane
+// address registers stay live, unlike the ds_bpermute form below, which
+// kept six per-lane shuffle addresses alive (spilled in the triangle loop).
 template <typename T>
 __device__ inline T wave_inclusive_scan(T v) {
+  if constexpr (sizeof(T) == 4) {
+    int x = (int)v;
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
+    return (T)x;
+  }
   const int lane = lane_id();
 #pragma unroll
   for (int d = 1; d < WAVE; d <<= 1) {

@@ -234,7 +234,7 @@ __device__ inline void tri_row(uint32_t a, uint32_t dp, const uint32_t *rowptr, 
     if (lane == WAVE - 1) tb.pre[WAVE] = inc;
     tb.qa[lane] = qa;
     tb.pq[lane] = pq;
-    const uint32_t total = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl(inc, WAVE - 1, WAVE));
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane(inc, WAVE - 1);
     if (lane == 0) probes += total;
     __builtin_amdgcn_wave_barrier();
     for (uint32_t t0 = 0; t0 < total; t0 += ILP * WAVE) {
@@ -386,7 +386,7 @@ __device__ inline void tri_row_packed(uint32_t nb, uint32_t ns, const uint32_t *
     if (lane == WAVE - 1) tb.pre[WAVE] = inc;
     tb.qa[lane] = qa;
     tb.pk[lane] = (uint8_t)(pk >> 24);
-    const uint32_t total = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl(inc, WAVE - 1, WAVE));
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane(inc, WAVE - 1);
     probes += total;  // (wave-uniform: the kernels take lane 0's)
     __builtin_amdgcn_wave_barrier();
     // ping-pong words and batch owners of the steps in flight; a word's pcols
@@ -418,8 +418,10 @@ __device__ inline void tri_row_packed(uint32_t nb, uint32_t ns, const uint32_t *
 #pragma unroll
       for (int u = 0; u < ILP; ++u) {
         const uint32_t pp = tb.qa[bb[u]] + (xc[u] - tb.pre[bb[u]]);
+        // past the end: a clamped position, masked by `live` in probe.  (Masking
+        // the word here made the compiler wait on each load before the next
+        // slice's lookups, serialising the ILP loads: s24 231 → 210 ms.)
         ww[u] = pcols[pp];
-        if (t0 + u * WAVE + lane >= total) ww[u] = 0xFFFFFFFFu;  // past the end (the load stays unconditional)
       }
     };
     auto probe = [&](const uint32_t (&ww)[ILP], const uint32_t (&bb)[ILP], uint32_t t0) {
@@ -427,7 +429,7 @@ __device__ inline void tri_row_packed(uint32_t nb, uint32_t ns, const uint32_t *
       bool live[ILP], hit[ILP];
 #pragma unroll
       for (int u = 0; u < ILP; ++u) {
-        live[u] = ww[u] != 0xFFFFFFFFu;
+        live[u] = t0 + u * WAVE + lane < total;
         wk[u] = ww[u] & TRI_M24;
       }
       find.template batch<ILP>(wk, live, hit, pw, pos);
@@ -633,7 +635,13 @@ __device__ inline unsigned long long tri_dequeue(unsigned long long *cursor, int
     const unsigned long long ch = (unsigned long long)xcd;
     c0 = ((c0 / ch) * 8 + xg) * ch + c0 % ch;
   }
-  return (c0 * parts + part) * grab;
+  const unsigned long long g = (c0 * parts + part) * grab;
+  // wave-uniform: the item loads and everything derived from them stay scalar
+  // (as VGPRs they pushed the 8-wave count kernels into scratch: 92 / 84 B per
+  // lane of spills → 60 / 76 B)
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)g);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(g >> 32));
+  return ((unsigned long long)hi << 32) | lo;
 }
 
 struct TriPassB {

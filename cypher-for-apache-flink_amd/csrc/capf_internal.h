@@ -96,9 +96,10 @@ struct Column;
 struct LazyGather {
   Session *s = nullptr;
   std::shared_ptr<Column> src;  // never lazy itself
-  BufPtr idx;  // int64 [m], -1 = NULL row (nullable)
+  BufPtr idx;  // int64 [m] (iw 8) or int32 [m] (iw 4), -1 = NULL row (nullable)
   int64_t m = 0;
   bool nullable = false;
+  int32_t iw = 8;  // index width in bytes
 };
 
 struct Column {
@@ -221,10 +222,12 @@ __host__ __device__ inline int64_t ld_int(const ColView &c, int64_t r) {
 constexpr int FT_MAX = 8;
 struct FtOperand {
   ColView v;            // the column (or the lazy gather's source)
-  const int64_t *idx;   // lazy gather index, or null
+  const void *idx;      // lazy gather index (int64, or int32 when iw == 4), or null
   int64_t lit;          // literal (v.data == null and lit_ok)
   int32_t is_lit;
   int32_t side;         // join-fused filters: 0 = left input row, 1 = right input row
+  int32_t iw;           // idx width in bytes (8 or 4)
+  int32_t pad_;
 };
 struct FtTerm {
   FtOperand a, b;
@@ -244,7 +247,7 @@ __device__ inline bool ft_load(const FtOperand &o, int64_t r, int64_t &val) {
   }
   int64_t row = r;
   if (o.idx) {
-    row = o.idx[r];
+    row = o.iw == 4 ? (int64_t)((const int32_t *)o.idx)[r] : ((const int64_t *)o.idx)[r];
     if (row < 0) return false;
   }
   if (o.v.valid && !o.v.valid[row]) return false;
@@ -409,17 +412,24 @@ BufPtr eval_filter(Session *s, const Program &p, const std::vector<std::string> 
 // Filter of a table body in one step: the rows passing `p`, its lazy (join
 // output) columns composed by the selection kernel itself.
 DataPtr filter_select(Session *s, const Program &p, const std::vector<std::string> &names, const Data &d);
+// Row index entry i of an index of iw bytes per entry (-1 = NULL row).
+__host__ __device__ inline int64_t idx_at(const void *idx, int iw, int64_t i) {
+  return iw == 4 ? (int64_t)((const int32_t *)idx)[i] : ((const int64_t *)idx)[i];
+}
 // Gather rows (int64 indices, -1 = null row) of a column.
 ColPtr gather_column(Session *s, const ColPtr &c, const int64_t *d_idx, int64_t n,
                      bool idx_may_be_null = false);
+// The same with an index of iw bytes per row (8 = int64, 4 = int32).
+ColPtr gather_column_w(Session *s, const ColPtr &c, const void *d_idx, int iw, int64_t n, bool idx_may_be_null);
 // Late-materialised gather (LazyGather): rows idx of c, composed with c's own
 // index when c is lazy; `cache` shares one composition among the columns of
 // a side (keyed by the two index buffers).
 struct IdxCache {
   std::vector<std::pair<std::pair<const void *, const void *>, BufPtr>> entries;
 };
+// iw: bytes per index entry (8, or 4 for a join's int32 pair list).
 ColPtr gather_lazy(Session *s, const ColPtr &c, const BufPtr &idx, int64_t n, bool idx_may_be_null,
-                   IdxCache *cache);
+                   IdxCache *cache, int iw = 8);
 // Computes a lazy column in place (no-op otherwise).
 void force(const ColPtr &c);
 BufPtr iota_index(Session *s, int64_t start, int64_t m);
@@ -444,6 +454,7 @@ Grouping group_rows(Session *s, const Data &d, const std::vector<int> &keys);
 struct JoinPairs {
   BufPtr left, right;  // int64 [n], -1 for a null-extended side; null = identity (n rows)
   int64_t n = 0;
+  int iw = 8;  // bytes per index entry: 4 = int32 (radix join, both sides < 2^31 rows)
   // inner join whose key values are equal on every output row: 1 = the left
   // key column may be replaced by the right one, 2 = the other way round
   int key_alias = 0;

@@ -1917,7 +1917,7 @@ bool try_fused_reach(const NodePtr &grp, DataPtr &result) {
     if (jp.n != nr) fail(CAPF_ERR_INTERNAL, "fused reach: source rows lost");
     IdxCache cache;
     if (jp.left)
-      for (auto &c : rcols) c = gather_lazy(s, c, jp.left, nr, false, &cache);
+      for (auto &c : rcols) c = gather_lazy(s, c, jp.left, nr, false, &cache, jp.iw);
     a_rows = std::make_shared<Data>();
     a_rows->nrows = nr;
     for (size_t j = 0; j < la.data->cols.size(); ++j) {
@@ -1925,7 +1925,7 @@ bool try_fused_reach(const NodePtr &grp, DataPtr &result) {
       if (jp.build_unread == 2)  // S_a holds its key and constants only: no row index
         a_rows->cols.push_back((int)j == sh.x ? rcols[0] : const_column(s, c->is_const ? *c : *c->lazy->src, nr));
       else
-        a_rows->cols.push_back(jp.right ? gather_lazy(s, c, jp.right, nr, false, &cache) : c);
+        a_rows->cols.push_back(jp.right ? gather_lazy(s, c, jp.right, nr, false, &cache, jp.iw) : c);
     }
   }
   for (size_t i = 0; i < gk.size(); ++i) {

@@ -140,8 +140,9 @@ BufPtr compact_flags(Session *s, const uint8_t *d_flags, int64_t n, int64_t *out
 // reads and output writes coalesce (ballot + wave offsets per round).
 constexpr int SEL_MAX = 4;
 struct SelSrcs {
-  const int64_t *src[SEL_MAX];
-  int64_t *out[SEL_MAX];
+  const void *src[SEL_MAX];  // int64 (w 8) or int32 (w 4) row indexes, or null (the row itself, int64)
+  void *out[SEL_MAX];        // written at the source's width
+  int w[SEL_MAX];
   int ns;
 };
 __global__ __launch_bounds__(SCAN_BLOCK) void k_select_multi(const uint8_t *flags, int64_t n,
@@ -164,7 +165,11 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_select_multi(const uint8_t *flag
     }
     if (f) {
       const int64_t pos = pos0 + before + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-      for (int q = 0; q < ss.ns; ++q) ss.out[q][pos] = ss.src[q] ? ss.src[q][r] : r;
+      for (int q = 0; q < ss.ns; ++q) {
+        if (!ss.src[q]) ((int64_t *)ss.out[q])[pos] = r;
+        else if (ss.w[q] == 4) ((int32_t *)ss.out[q])[pos] = ((const int32_t *)ss.src[q])[r];
+        else ((int64_t *)ss.out[q])[pos] = ((const int64_t *)ss.src[q])[r];
+      }
     }
     pos0 += all;
     __syncthreads();
@@ -242,8 +247,26 @@ __device__ inline void gather_quad_store(T *dst, uint8_t *dval, int64_t q, const
 // Two quads per thread per step: both quads' index loads, then all eight
 // value loads, are in flight together (one quad at a time left the gather
 // latency bound: 0.48 ms for 119 M FOR32 rows).
-template <typename T>
-__global__ void k_gather4(const T *src, const uint8_t *sval, const int64_t *idx, T *dst,
+// the 4 index entries of quad q (int64: two 16-B loads, int32: one)
+template <typename I>
+__device__ inline void idx_quad(const I *idx, int64_t q, int64_t j[4]) {
+  if constexpr (sizeof(I) == 8) {
+    const longlong2 a = ((const longlong2 *)idx)[2 * q], b = ((const longlong2 *)idx)[2 * q + 1];
+    j[0] = a.x;
+    j[1] = a.y;
+    j[2] = b.x;
+    j[3] = b.y;
+  } else {
+    const int4 a = ((const int4 *)idx)[q];
+    j[0] = a.x;
+    j[1] = a.y;
+    j[2] = a.z;
+    j[3] = a.w;
+  }
+}
+
+template <typename T, typename I>
+__global__ void k_gather4(const T *src, const uint8_t *sval, const I *idx, T *dst,
                           uint8_t *dval, int64_t m) {
   const int64_t m4 = m / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -252,13 +275,7 @@ __global__ void k_gather4(const T *src, const uint8_t *sval, const int64_t *idx,
     const int64_t qq[2] = {q, q + stride};
     int64_t j[2][4];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const longlong2 a = ((const longlong2 *)idx)[2 * qq[h]], b = ((const longlong2 *)idx)[2 * qq[h] + 1];
-      j[h][0] = a.x;
-      j[h][1] = a.y;
-      j[h][2] = b.x;
-      j[h][3] = b.y;
-    }
+    for (int h = 0; h < 2; ++h) idx_quad(idx, qq[h], j[h]);
     T v[2][4];
     uint32_t vm[2] = {0, 0};
 #pragma unroll
@@ -273,8 +290,8 @@ __global__ void k_gather4(const T *src, const uint8_t *sval, const int64_t *idx,
     for (int h = 0; h < 2; ++h) gather_quad_store(dst, dval, qq[h], v[h], vm[h]);
   }
   for (; q < m4; q += stride) {
-    const longlong2 a = ((const longlong2 *)idx)[2 * q], b = ((const longlong2 *)idx)[2 * q + 1];
-    const int64_t j[4] = {a.x, a.y, b.x, b.y};
+    int64_t j[4];
+    idx_quad(idx, q, j);
     T v[4];
     uint32_t vm = 0;
 #pragma unroll
@@ -287,7 +304,7 @@ __global__ void k_gather4(const T *src, const uint8_t *sval, const int64_t *idx,
   }
   if (blockIdx.x == 0 && threadIdx.x < (unsigned)(m - 4 * m4)) {
     const int64_t i = 4 * m4 + threadIdx.x;
-    const int64_t j = idx[i];
+    const int64_t j = (int64_t)idx[i];
     const bool ok = j >= 0;
     if (dst) dst[i] = ok ? src[j] : T(0);
     if (dval) dval[i] = ok ? (sval ? sval[j] : 1) : 0;
@@ -318,11 +335,12 @@ ColPtr const_column(Session *s, const Column &c, int64_t m) {
 
 // FOR24 rows gathered into FOR32 (same base): the gathered rows are no
 // longer a scan-order stream, 4-B rows keep every later access aligned
-__global__ void k_gather_u24(const void *src, const uint8_t *sval, const int64_t *idx,
+template <typename I>
+__global__ void k_gather_u24(const void *src, const uint8_t *sval, const I *idx,
                              uint32_t *dst, uint8_t *dval, int64_t m) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
        i += (int64_t)gridDim.x * blockDim.x) {
-    int64_t j = idx[i];
+    int64_t j = (int64_t)idx[i];
     bool ok = j >= 0;
     if (dst) dst[i] = ok ? ld_u24(src, j) : 0u;
     if (dval) dval[i] = ok ? (sval ? sval[j] : 1) : 0;
@@ -330,12 +348,38 @@ __global__ void k_gather_u24(const void *src, const uint8_t *sval, const int64_t
 }
 
 // ------------------------------------------------------ late materialisation
-__global__ void k_compose_idx(const int64_t *outer, const int64_t *inner, int64_t *out, int64_t m) {
+// out = inner ∘ outer, written at the inner index's width (its values)
+template <typename IO, typename II>
+__global__ void k_compose_idx(const IO *outer, const II *inner, II *out, int64_t m) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t j = outer[i];
-    out[i] = j < 0 ? -1 : inner[j];
+    const int64_t j = (int64_t)outer[i];
+    out[i] = j < 0 ? II(-1) : inner[j];
   }
+}
+
+// int32 row indexes widened to int64 (for the few consumers that take int64 only)
+__global__ void k_widen_idx(const int32_t *in, int64_t *out, int64_t m) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = in[i];
+}
+
+static void launch_compose(Session *s, const void *outer, int ow, const void *inner, int iw, void *out, int64_t m) {
+  const dim3 g(grid_for(m, 256)), b(256);
+  if (ow == 8 && iw == 8)
+    hipLaunchKernelGGL((k_compose_idx<int64_t, int64_t>), g, b, 0, s->stream, (const int64_t *)outer,
+                       (const int64_t *)inner, (int64_t *)out, m);
+  else if (ow == 8)
+    hipLaunchKernelGGL((k_compose_idx<int64_t, int32_t>), g, b, 0, s->stream, (const int64_t *)outer,
+                       (const int32_t *)inner, (int32_t *)out, m);
+  else if (iw == 8)
+    hipLaunchKernelGGL((k_compose_idx<int32_t, int64_t>), g, b, 0, s->stream, (const int32_t *)outer,
+                       (const int64_t *)inner, (int64_t *)out, m);
+  else
+    hipLaunchKernelGGL((k_compose_idx<int32_t, int32_t>), g, b, 0, s->stream, (const int32_t *)outer,
+                       (const int32_t *)inner, (int32_t *)out, m);
+  KERNEL_CHECK();
 }
 
 static bool lazy_enabled() {
@@ -346,7 +390,7 @@ static bool lazy_enabled() {
 void force(const ColPtr &c) {
   if (!c || !c->lazy) return;
   const std::shared_ptr<LazyGather> lz = c->lazy;
-  ColPtr g = gather_column(lz->s, lz->src, (const int64_t *)lz->idx->p, lz->m, lz->nullable);
+  ColPtr g = gather_column_w(lz->s, lz->src, lz->idx->p, lz->iw, lz->m, lz->nullable);
   c->data = g->data;
   c->valid = g->valid;
   c->enc = g->enc;
@@ -355,12 +399,13 @@ void force(const ColPtr &c) {
 }
 
 ColPtr gather_lazy(Session *s, const ColPtr &c, const BufPtr &idx, int64_t m, bool nullable,
-                   IdxCache *cache) {
+                   IdxCache *cache, int iw) {
   if (!idx && m == c->n) return c;  // identity: the column passes through, lazy or not
   if (!idx || !lazy_enabled() || c->type == Type::Null || c->type == Type::List || m == 0)
-    return gather_column(s, c, idx ? (const int64_t *)idx->p : nullptr, m, nullable);
+    return gather_column_w(s, c, idx ? idx->p : nullptr, iw, m, nullable);
   ColPtr src = c;
   BufPtr id = idx;
+  int id_w = iw;
   if (c->lazy && c->lazy->src->is_const && !nullable && !c->lazy->nullable) {
     src = c->lazy->src;  // a constant gathers to a fill: the composed index is never read
   } else if (c->lazy) {
@@ -370,13 +415,12 @@ ColPtr gather_lazy(Session *s, const ColPtr &c, const BufPtr &idx, int64_t m, bo
       for (auto &e : cache->entries)
         if (e.first == key) composed = e.second;
     if (!composed) {
-      composed = s->alloc(8 * m);
-      hipLaunchKernelGGL(k_compose_idx, dim3(grid_for(m, 256)), dim3(256), 0, s->stream,
-                         (const int64_t *)idx->p, (const int64_t *)c->lazy->idx->p, (int64_t *)composed->p, m);
-      KERNEL_CHECK();
+      composed = s->alloc((int64_t)c->lazy->iw * m);
+      launch_compose(s, idx->p, iw, c->lazy->idx->p, c->lazy->iw, composed->p, m);
       if (cache) cache->entries.emplace_back(key, composed);
     }
     id = composed;
+    id_w = c->lazy->iw;  // the composed entries are the inner index's values
     nullable = nullable || c->lazy->nullable;
     src = c->lazy->src;
   }
@@ -389,18 +433,33 @@ ColPtr gather_lazy(Session *s, const ColPtr &c, const BufPtr &idx, int64_t m, bo
   o->lazy->idx = id;
   o->lazy->m = m;
   o->lazy->nullable = nullable;
+  o->lazy->iw = id_w;
   return o;
 }
 
 ColPtr gather_column(Session *s, const ColPtr &c, const int64_t *d_idx, int64_t m,
                      bool idx_may_be_null) {
+  return gather_column_w(s, c, d_idx, 8, m, idx_may_be_null);
+}
+
+ColPtr gather_column_w(Session *s, const ColPtr &c, const void *d_idx, int iw, int64_t m, bool idx_may_be_null) {
   force(c);
   if (!d_idx) {
     if (m == c->n) return c;
     illegal("internal: identity gather with mismatched length");
   }
+  if (iw != 4 && iw != 8) illegal("internal: row index width");
   if (c->type == Type::Null) return null_column(s, Type::Null, m);
-  if (c->type == Type::List) return gather_list(s, c, d_idx, m);
+  if (c->type == Type::List) {
+    if (iw == 8) return gather_list(s, c, (const int64_t *)d_idx, m);
+    BufPtr w = s->alloc(8 * std::max<int64_t>(m, 1));
+    if (m > 0) {
+      hipLaunchKernelGGL(k_widen_idx, dim3(grid_for(m, 256)), dim3(256), 0, s->stream, (const int32_t *)d_idx,
+                         (int64_t *)w->p, m);
+      KERNEL_CHECK();
+    }
+    return gather_list(s, c, (const int64_t *)w->p, m);  // (w returns to the stream-ordered pool)
+  }
   if (c->is_const && !idx_may_be_null && c->n > 0) return const_column(s, *c, m);
   if (!c->data || c->n == 0) {
     // empty source (outer join against an empty side): every index is the
@@ -431,19 +490,25 @@ ColPtr gather_column(Session *s, const ColPtr &c, const int64_t *d_idx, int64_t 
   uint8_t *dval = o->valid ? (uint8_t *)o->valid->p : nullptr;
   unsigned g = grid_for(m, 256);
   const unsigned g4 = grid_for((m + 3) / 4, 256);
-  if (c->type == Type::Bool)
-    hipLaunchKernelGGL(k_gather4<uint8_t>, dim3(g4), dim3(256), 0, s->stream,
-                       (const uint8_t *)c->data->p, sval, d_idx, (uint8_t *)o->data->p, dval, m);
-  else if (c->enc == ENC_FOR24)
-    hipLaunchKernelGGL(k_gather_u24, dim3(g), dim3(256), 0, s->stream, (const void *)c->data->p, sval,
-                       d_idx, (uint32_t *)o->data->p, dval, m);
-  else if (c->enc == ENC_FOR32)
-    hipLaunchKernelGGL(k_gather4<uint32_t>, dim3(g4), dim3(256), 0, s->stream,
-                       (const uint32_t *)c->data->p, sval, d_idx, (uint32_t *)o->data->p, dval, m);
-  else
-    hipLaunchKernelGGL(k_gather4<int64_t>, dim3(g4), dim3(256), 0, s->stream,
-                       (const int64_t *)c->data->p, sval, d_idx, (int64_t *)o->data->p, dval, m);
-  KERNEL_CHECK();
+  auto launch = [&](auto ityp) {
+    using I = decltype(ityp);
+    const I *ix = (const I *)d_idx;
+    if (c->type == Type::Bool)
+      hipLaunchKernelGGL((k_gather4<uint8_t, I>), dim3(g4), dim3(256), 0, s->stream,
+                         (const uint8_t *)c->data->p, sval, ix, (uint8_t *)o->data->p, dval, m);
+    else if (c->enc == ENC_FOR24)
+      hipLaunchKernelGGL((k_gather_u24<I>), dim3(g), dim3(256), 0, s->stream, (const void *)c->data->p, sval,
+                         ix, (uint32_t *)o->data->p, dval, m);
+    else if (c->enc == ENC_FOR32)
+      hipLaunchKernelGGL((k_gather4<uint32_t, I>), dim3(g4), dim3(256), 0, s->stream,
+                         (const uint32_t *)c->data->p, sval, ix, (uint32_t *)o->data->p, dval, m);
+    else
+      hipLaunchKernelGGL((k_gather4<int64_t, I>), dim3(g4), dim3(256), 0, s->stream,
+                         (const int64_t *)c->data->p, sval, ix, (int64_t *)o->data->p, dval, m);
+    KERNEL_CHECK();
+  };
+  if (iw == 4) launch(int32_t{});
+  else launch(int64_t{});
   return o;
 }
 
@@ -1198,11 +1263,8 @@ __device__ inline void ft_load4(const FtOperand &o, int64_t r0, int64_t val[4], 
   }
   int64_t row[4];
   if (o.idx) {
-    const longlong2 a = ((const longlong2 *)(o.idx + r0))[0], b = ((const longlong2 *)(o.idx + r0))[1];
-    row[0] = a.x;
-    row[1] = a.y;
-    row[2] = b.x;
-    row[3] = b.y;
+    if (o.iw == 4) idx_quad((const int32_t *)o.idx, r0 / 4, row);
+    else idx_quad((const int64_t *)o.idx, r0 / 4, row);
   } else {
 #pragma unroll
     for (int k = 0; k < 4; ++k) row[k] = r0 + k;
@@ -1287,7 +1349,8 @@ static bool ft_operand(const Instr &in, const std::vector<std::string> &pnames,
   }
   if (lz && !lz->src->is_const && !lz->src->lazy) {
     o.v = view_of(lz->src);
-    o.idx = (const int64_t *)lz->idx->p;
+    o.idx = lz->idx->p;
+    o.iw = lz->iw;
   } else {
     if (c->is_const) return false;  // (a fill: the interpreter handles it)
     o.v = view_of(c);
@@ -1386,6 +1449,7 @@ DataPtr filter_select(Session *s, const Program &p, const std::vector<std::strin
   // written by the selection itself) and whether a plain column needs the
   // selection index
   std::vector<BufPtr> lazy_idx;
+  std::vector<int> lazy_w;
   bool plain = false;
   for (auto &c : d.cols) {
     std::shared_ptr<LazyGather> lz;
@@ -1398,7 +1462,10 @@ DataPtr filter_select(Session *s, const Program &p, const std::vector<std::strin
     if (lz && !(lz->src->is_const && !lz->nullable)) {
       bool seen = false;
       for (auto &b : lazy_idx) seen |= b.get() == lz->idx.get();
-      if (!seen) lazy_idx.push_back(lz->idx);
+      if (!seen) {
+        lazy_idx.push_back(lz->idx);
+        lazy_w.push_back(lz->iw);
+      }
     } else if (!lz) {
       plain = true;
     }
@@ -1427,13 +1494,16 @@ DataPtr filter_select(Session *s, const Program &p, const std::vector<std::strin
   ss.ns = 0;
   if (plain) {
     ss.src[ss.ns] = nullptr;
-    ss.out[ss.ns++] = (int64_t *)sel->p;
+    ss.w[ss.ns] = 8;
+    ss.out[ss.ns++] = sel->p;
   }
   IdxCache cache;
-  for (auto &b : lazy_idx) {
-    BufPtr o = s->alloc(8 * std::max<int64_t>(m, 1));
-    ss.src[ss.ns] = (const int64_t *)b->p;
-    ss.out[ss.ns++] = (int64_t *)o->p;
+  for (size_t k = 0; k < lazy_idx.size(); ++k) {
+    const BufPtr &b = lazy_idx[k];
+    BufPtr o = s->alloc((int64_t)lazy_w[k] * std::max<int64_t>(m, 1));
+    ss.src[ss.ns] = b->p;
+    ss.w[ss.ns] = lazy_w[k];
+    ss.out[ss.ns++] = o->p;
     cache.entries.emplace_back(std::make_pair((const void *)b.get(), (const void *)sel.get()), o);
   }
   if (m > 0) {

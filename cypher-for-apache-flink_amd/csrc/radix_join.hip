@@ -480,12 +480,14 @@ __device__ inline void rj_pass(const RjPred &fp, const int64_t (&bi)[U], const u
 // a bag — one pass, no count of the passes first); MODE 1 counts the passes
 // per sub-item into subcnt[sub] and MODE 2 writes them from suboff[sub] on
 // (two passes, when the holes overflow their buffer).
-template <int MODE>
+// I: the pair list's row index type (int32 when both sides have < 2^31 rows:
+// half the EMIT's bytes and of every gather through the pairs later).
+template <int MODE, typename I>
 __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_emit_ranges(const RJSub *subs, const RJWork *work,
                                                                const uint64_t *bh, const uint32_t *brow,
                                                                const int64_t *bstart, const uint64_t *ph,
                                                                const uint32_t *prow, const int64_t *out_off,
-                                                               int64_t *oprobe, int64_t *obuild,
+                                                               I *oprobe, I *obuild,
                                                                uint8_t *pmatched, uint8_t *bmatched,
                                                                const RjPred fp, int build_left,
                                                                int64_t *subcnt, const int64_t *suboff,
@@ -601,8 +603,8 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_emit_ranges(const RJSub *subs,
             for (int k = 0; k < U; ++k) {
               const uint32_t x = xb + k * RJ_JBLOCK + threadIdx.x;
               if (x < x1) {
-                oprobe[obase + rel + x] = pr[k];
-                obuild[obase + rel + x] = br[k];
+                oprobe[obase + rel + x] = (I)pr[k];
+                obuild[obase + rel + x] = (I)br[k];
                 if (bmatched) bmatched[br[k]] = 1;
               }
             }
@@ -621,8 +623,8 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_emit_ranges(const RJSub *subs,
                 if (x >= x1) continue;
                 const int64_t pos = obase + rel + x;
                 if (keep[k]) {
-                  oprobe[pos] = pr[k];
-                  obuild[pos] = br[k];
+                  oprobe[pos] = (I)pr[k];
+                  obuild[pos] = (I)br[k];
                 } else {
                   const unsigned long long h = atomicAdd(nholes, 1ull);
                   if ((int64_t)h < hcap) subcnt[h] = pos;
@@ -638,8 +640,8 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_emit_ranges(const RJSub *subs,
 #pragma unroll
               for (int k = 0; k < U; ++k)
                 if (keep[k]) {
-                  oprobe[pos] = pr[k];
-                  obuild[pos] = br[k];
+                  oprobe[pos] = (I)pr[k];
+                  obuild[pos] = (I)br[k];
                   ++pos;
                 }
               fbase += tot2;
@@ -675,8 +677,9 @@ __device__ inline int64_t rj_count_above(const uint64_t *h, int64_t lo, int64_t 
   return hi - a;
 }
 
+template <typename I>
 __global__ __launch_bounds__(1024) void k_rj_fill_holes(const uint64_t *holes, int64_t nh, int64_t total,
-                                                        int64_t *op, int64_t *ob) {
+                                                        I *op, I *ob) {
   const int64_t m = total - nh;
   // holes below the tail: holes[0, nb)
   int64_t a = 0, b = nh;
@@ -732,11 +735,12 @@ __global__ void k_rj_unmatched(const uint8_t *matched, int64_t n, uint8_t *flags
     flags[r] = matched[r] ? 0 : 1;
 }
 
-__global__ void k_rj_append(const int64_t *rows, int64_t m, int64_t off, int64_t *own, int64_t *other) {
+template <typename I>
+__global__ void k_rj_append(const int64_t *rows, int64_t m, int64_t off, I *own, I *other) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
        i += (int64_t)gridDim.x * blockDim.x) {
-    own[off + i] = rows[i];
-    other[off + i] = -1;
+    own[off + i] = (I)rows[i];
+    other[off + i] = I(-1);
   }
 }
 
@@ -837,175 +841,188 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
     KERNEL_CHECK();
     total = exclusive_scan_i64(s, (const int64_t *)cnt->p, (int64_t *)off->p, nw);
   }
-  BufPtr pm, bm;
-  if (p_outer) {
-    pm = s->alloc(std::max<int64_t>(Pr.nrows, 1));
-    HIP_CHECK(hipMemsetAsync(pm->p, 0, std::max<int64_t>(Pr.nrows, 1), s->stream));
-  }
-  if (b_outer) {
-    bm = s->alloc(std::max<int64_t>(B.nrows, 1));
-    HIP_CHECK(hipMemsetAsync(bm->p, 0, std::max<int64_t>(B.nrows, 1), s->stream));
-  }
-  if (pred) {  // filtered (radix_join_filtered): inner join only
-    if (p_outer || b_outer) illegal("radix_join: a filtered join must be inner");
-    JoinPairs jp;
-    jp.n = 0;
-    BufPtr oprobe = s->alloc(8), obuild = s->alloc(8);
-    RjPred rp{};
-    std::vector<BufPtr> keep;  // the operand arrays, alive until the EMIT passes are enqueued
-    rp.nt = pred->nt;
-    rp.np = 0;
-    for (int k = 0; k < pred->nt; ++k) {
-      const FtOperand *src[2] = {&pred->t[k].a, &pred->t[k].b};
-      RjOp *dst[2] = {&rp.t[k].a, &rp.t[k].b};
-      for (int j = 0; j < 2; ++j) {
-        *dst[j] = RjOp{nullptr, nullptr, src[j]->lit, src[j]->is_lit, -1};
-        if (src[j]->is_lit) continue;
-        const bool on_build = (src[j]->side == 0) == build_left;
-        const RJSide &sd = on_build ? bs : ps;
-        BufPtr v = s->alloc(8 * std::max<int64_t>(sd.n, 1)), o = s->alloc(std::max<int64_t>(sd.n, 1));
-        if (sd.n > 0) {
-          hipLaunchKernelGGL(k_rj_operand, dim3(grid_for(sd.n, 256)), dim3(256), 0, s->stream, *src[j],
-                             (const uint32_t *)sd.row->p, sd.n, (int64_t *)v->p, (uint8_t *)o->p);
+  // the pair list's row indexes: int32 when both sides have < 2^31 rows (half the
+  // EMIT's bytes and half the index bytes of every later gather); CAPF_IDX64=1
+  // keeps int64 (tests run both)
+  const char *i64env = getenv("CAPF_IDX64");
+  const bool idx32 = !(i64env && atoi(i64env) != 0) && l.nrows < (int64_t(1) << 31) && r.nrows < (int64_t(1) << 31);
+  auto emit = [&](auto ityp) -> JoinPairs {
+    using I = decltype(ityp);
+    BufPtr pm, bm;
+    if (p_outer) {
+      pm = s->alloc(std::max<int64_t>(Pr.nrows, 1));
+      HIP_CHECK(hipMemsetAsync(pm->p, 0, std::max<int64_t>(Pr.nrows, 1), s->stream));
+    }
+    if (b_outer) {
+      bm = s->alloc(std::max<int64_t>(B.nrows, 1));
+      HIP_CHECK(hipMemsetAsync(bm->p, 0, std::max<int64_t>(B.nrows, 1), s->stream));
+    }
+    if (pred) {  // filtered (radix_join_filtered): inner join only
+      if (p_outer || b_outer) illegal("radix_join: a filtered join must be inner");
+      JoinPairs jp;
+      jp.n = 0;
+      jp.iw = (int)sizeof(I);
+      BufPtr oprobe = s->alloc(8), obuild = s->alloc(8);
+      RjPred rp{};
+      std::vector<BufPtr> keep;  // the operand arrays, alive until the EMIT passes are enqueued
+      rp.nt = pred->nt;
+      rp.np = 0;
+      for (int k = 0; k < pred->nt; ++k) {
+        const FtOperand *src[2] = {&pred->t[k].a, &pred->t[k].b};
+        RjOp *dst[2] = {&rp.t[k].a, &rp.t[k].b};
+        for (int j = 0; j < 2; ++j) {
+          *dst[j] = RjOp{nullptr, nullptr, src[j]->lit, src[j]->is_lit, -1};
+          if (src[j]->is_lit) continue;
+          const bool on_build = (src[j]->side == 0) == build_left;
+          const RJSide &sd = on_build ? bs : ps;
+          BufPtr v = s->alloc(8 * std::max<int64_t>(sd.n, 1)), o = s->alloc(std::max<int64_t>(sd.n, 1));
+          if (sd.n > 0) {
+            hipLaunchKernelGGL(k_rj_operand, dim3(grid_for(sd.n, 256)), dim3(256), 0, s->stream, *src[j],
+                               (const uint32_t *)sd.row->p, sd.n, (int64_t *)v->p, (uint8_t *)o->p);
+            KERNEL_CHECK();
+          }
+          keep.push_back(v);
+          keep.push_back(o);
+          if (on_build) {
+            dst[j]->val = (const int64_t *)v->p;
+            dst[j]->ok = (const uint8_t *)o->p;
+          } else {
+            if (rp.np == RJ_PMAX) illegal("radix_join: too many probe-side filter operands");
+            rp.pv[rp.np] = (const int64_t *)v->p;
+            rp.po[rp.np] = (const uint8_t *)o->p;
+            dst[j]->slot = rp.np++;
+          }
+        }
+        rp.t[k].op = pred->t[k].op;
+        rp.t[k].neg = pred->t[k].neg;
+      }
+      if (nw > 0 && total > 0) {
+        BufPtr nsub = s->alloc(8 * nw), soff = s->alloc(8 * (nw + 1));
+        hipLaunchKernelGGL(k_rj_sub_counts, dim3(grid_for(nw, 256)), dim3(256), 0, s->stream,
+                           (const int64_t *)cnt->p, nw, (int64_t *)nsub->p);
+        KERNEL_CHECK();
+        const int64_t ns = exclusive_scan_i64(s, (const int64_t *)nsub->p, (int64_t *)soff->p, nw);
+        BufPtr subs = s->alloc(sizeof(RJSub) * std::max<int64_t>(ns, 1));
+        hipLaunchKernelGGL(k_rj_subs, dim3(grid_for(nw, 256)), dim3(256), 0, s->stream, (const int64_t *)cnt->p,
+                           (const int64_t *)soff->p, nw, (RJSub *)subs->p);
+        KERNEL_CHECK();
+        // one pass: passing pairs at their unfiltered positions, failing ones
+        // listed as holes, then the tail's pairs moved into them
+        const int64_t hcap = std::min<int64_t>(total, int64_t(1) << 20);
+        BufPtr holes = s->alloc(8 * hcap), nh = s->alloc(8);
+        HIP_CHECK(hipMemsetAsync(nh->p, 0, 8, s->stream));
+        oprobe = s->alloc(sizeof(I) * total);
+        obuild = s->alloc(sizeof(I) * total);
+        {
+          KernelTimer kt(s, "rj_join_filter_emit", 12.0 * (double)(ps.n + bs.n) + 16.0 * (double)total);
+          hipLaunchKernelGGL((k_rj_emit_ranges<3, I>), dim3((unsigned)ns), dim3(RJ_JBLOCK), 0, s->stream,
+                             (const RJSub *)subs->p, (const RJWork *)dw->p, (const uint64_t *)bs.h->p,
+                             (const uint32_t *)bs.row->p, (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
+                             (const uint32_t *)ps.row->p, (const int64_t *)off->p, (I *)oprobe->p,
+                             (I *)obuild->p, (uint8_t *)nullptr, (uint8_t *)nullptr, rp, build_left ? 1 : 0,
+                             (int64_t *)holes->p, (const int64_t *)nullptr, (unsigned long long *)nh->p, hcap);
           KERNEL_CHECK();
         }
-        keep.push_back(v);
-        keep.push_back(o);
-        if (on_build) {
-          dst[j]->val = (const int64_t *)v->p;
-          dst[j]->ok = (const uint8_t *)o->p;
+        int64_t nholes = 0;
+        HIP_CHECK(hipMemcpyAsync(&nholes, nh->p, 8, hipMemcpyDeviceToHost, s->stream));
+        s->sync();
+        if (nholes <= hcap) {
+          if (nholes > 0) {
+            BufPtr sorted = s->alloc(8 * nholes);
+            size_t tmp = 0;
+            HIP_CHECK(rocprim::radix_sort_keys(nullptr, tmp, (const uint64_t *)holes->p, (uint64_t *)sorted->p,
+                                               (size_t)nholes, 0, 64, s->stream));
+            BufPtr t = s->alloc(std::max<size_t>(tmp, 16));
+            HIP_CHECK(rocprim::radix_sort_keys(t->p, tmp, (const uint64_t *)holes->p, (uint64_t *)sorted->p,
+                                               (size_t)nholes, 0, 64, s->stream));
+            hipLaunchKernelGGL(k_rj_fill_holes<I>, dim3(1), dim3(1024), 0, s->stream, (const uint64_t *)sorted->p, nholes,
+                               total, (I *)oprobe->p, (I *)obuild->p);
+            KERNEL_CHECK();
+          }
+          jp.n = total - nholes;
         } else {
-          if (rp.np == RJ_PMAX) illegal("radix_join: too many probe-side filter operands");
-          rp.pv[rp.np] = (const int64_t *)v->p;
-          rp.po[rp.np] = (const uint8_t *)o->p;
-          dst[j]->slot = rp.np++;
+          // many failing pairs: count the passes per sub-item, then write them
+          BufPtr subcnt = s->alloc(8 * ns), suboff = s->alloc(8 * (ns + 1));
+          {
+            KernelTimer kt(s, "rj_join_filter_count", 12.0 * (double)(ps.n + bs.n));
+            hipLaunchKernelGGL((k_rj_emit_ranges<1, I>), dim3((unsigned)ns), dim3(RJ_JBLOCK), 0, s->stream,
+                               (const RJSub *)subs->p, (const RJWork *)dw->p, (const uint64_t *)bs.h->p,
+                               (const uint32_t *)bs.row->p, (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
+                               (const uint32_t *)ps.row->p, (const int64_t *)off->p, (I *)nullptr,
+                               (I *)nullptr, (uint8_t *)nullptr, (uint8_t *)nullptr, rp, build_left ? 1 : 0,
+                               (int64_t *)subcnt->p, (const int64_t *)nullptr, (unsigned long long *)nullptr,
+                               (int64_t)0);
+            KERNEL_CHECK();
+          }
+          jp.n = exclusive_scan_i64(s, (const int64_t *)subcnt->p, (int64_t *)suboff->p, ns);
+          if (jp.n > 0) {
+            KernelTimer kt(s, "rj_join_emit", 12.0 * (double)(ps.n + bs.n) + 16.0 * (double)jp.n);
+            hipLaunchKernelGGL((k_rj_emit_ranges<2, I>), dim3((unsigned)ns), dim3(RJ_JBLOCK), 0, s->stream,
+                               (const RJSub *)subs->p, (const RJWork *)dw->p, (const uint64_t *)bs.h->p,
+                               (const uint32_t *)bs.row->p, (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
+                               (const uint32_t *)ps.row->p, (const int64_t *)off->p, (I *)oprobe->p,
+                               (I *)obuild->p, (uint8_t *)nullptr, (uint8_t *)nullptr, rp, build_left ? 1 : 0,
+                               (int64_t *)nullptr, (const int64_t *)suboff->p, (unsigned long long *)nullptr,
+                               (int64_t)0);
+            KERNEL_CHECK();
+          }
         }
       }
-      rp.t[k].op = pred->t[k].op;
-      rp.t[k].neg = pred->t[k].neg;
+      jp.left = build_left ? obuild : oprobe;
+      jp.right = build_left ? oprobe : obuild;
+      return jp;
     }
+    const int64_t cap = total + (p_outer ? Pr.nrows : 0) + (b_outer ? B.nrows : 0);
+    BufPtr oprobe = s->alloc(sizeof(I) * std::max<int64_t>(cap, 1)),
+           obuild = s->alloc(sizeof(I) * std::max<int64_t>(cap, 1));
     if (nw > 0 && total > 0) {
       BufPtr nsub = s->alloc(8 * nw), soff = s->alloc(8 * (nw + 1));
-      hipLaunchKernelGGL(k_rj_sub_counts, dim3(grid_for(nw, 256)), dim3(256), 0, s->stream,
-                         (const int64_t *)cnt->p, nw, (int64_t *)nsub->p);
+      hipLaunchKernelGGL(k_rj_sub_counts, dim3(grid_for(nw, 256)), dim3(256), 0, s->stream, (const int64_t *)cnt->p,
+                         nw, (int64_t *)nsub->p);
       KERNEL_CHECK();
       const int64_t ns = exclusive_scan_i64(s, (const int64_t *)nsub->p, (int64_t *)soff->p, nw);
       BufPtr subs = s->alloc(sizeof(RJSub) * std::max<int64_t>(ns, 1));
       hipLaunchKernelGGL(k_rj_subs, dim3(grid_for(nw, 256)), dim3(256), 0, s->stream, (const int64_t *)cnt->p,
                          (const int64_t *)soff->p, nw, (RJSub *)subs->p);
       KERNEL_CHECK();
-      // one pass: passing pairs at their unfiltered positions, failing ones
-      // listed as holes, then the tail's pairs moved into them
-      const int64_t hcap = std::min<int64_t>(total, int64_t(1) << 20);
-      BufPtr holes = s->alloc(8 * hcap), nh = s->alloc(8);
-      HIP_CHECK(hipMemsetAsync(nh->p, 0, 8, s->stream));
-      oprobe = s->alloc(8 * total);
-      obuild = s->alloc(8 * total);
-      {
-        KernelTimer kt(s, "rj_join_filter_emit", 12.0 * (double)(ps.n + bs.n) + 16.0 * (double)total);
-        hipLaunchKernelGGL(k_rj_emit_ranges<3>, dim3((unsigned)ns), dim3(RJ_JBLOCK), 0, s->stream,
-                           (const RJSub *)subs->p, (const RJWork *)dw->p, (const uint64_t *)bs.h->p,
-                           (const uint32_t *)bs.row->p, (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
-                           (const uint32_t *)ps.row->p, (const int64_t *)off->p, (int64_t *)oprobe->p,
-                           (int64_t *)obuild->p, (uint8_t *)nullptr, (uint8_t *)nullptr, rp, build_left ? 1 : 0,
-                           (int64_t *)holes->p, (const int64_t *)nullptr, (unsigned long long *)nh->p, hcap);
-        KERNEL_CHECK();
-      }
-      int64_t nholes = 0;
-      HIP_CHECK(hipMemcpyAsync(&nholes, nh->p, 8, hipMemcpyDeviceToHost, s->stream));
-      s->sync();
-      if (nholes <= hcap) {
-        if (nholes > 0) {
-          BufPtr sorted = s->alloc(8 * nholes);
-          size_t tmp = 0;
-          HIP_CHECK(rocprim::radix_sort_keys(nullptr, tmp, (const uint64_t *)holes->p, (uint64_t *)sorted->p,
-                                             (size_t)nholes, 0, 64, s->stream));
-          BufPtr t = s->alloc(std::max<size_t>(tmp, 16));
-          HIP_CHECK(rocprim::radix_sort_keys(t->p, tmp, (const uint64_t *)holes->p, (uint64_t *)sorted->p,
-                                             (size_t)nholes, 0, 64, s->stream));
-          hipLaunchKernelGGL(k_rj_fill_holes, dim3(1), dim3(1024), 0, s->stream, (const uint64_t *)sorted->p, nholes,
-                             total, (int64_t *)oprobe->p, (int64_t *)obuild->p);
-          KERNEL_CHECK();
-        }
-        jp.n = total - nholes;
-      } else {
-        // many failing pairs: count the passes per sub-item, then write them
-        BufPtr subcnt = s->alloc(8 * ns), suboff = s->alloc(8 * (ns + 1));
-        {
-          KernelTimer kt(s, "rj_join_filter_count", 12.0 * (double)(ps.n + bs.n));
-          hipLaunchKernelGGL(k_rj_emit_ranges<1>, dim3((unsigned)ns), dim3(RJ_JBLOCK), 0, s->stream,
-                             (const RJSub *)subs->p, (const RJWork *)dw->p, (const uint64_t *)bs.h->p,
-                             (const uint32_t *)bs.row->p, (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
-                             (const uint32_t *)ps.row->p, (const int64_t *)off->p, (int64_t *)nullptr,
-                             (int64_t *)nullptr, (uint8_t *)nullptr, (uint8_t *)nullptr, rp, build_left ? 1 : 0,
-                             (int64_t *)subcnt->p, (const int64_t *)nullptr, (unsigned long long *)nullptr,
-                             (int64_t)0);
-          KERNEL_CHECK();
-        }
-        jp.n = exclusive_scan_i64(s, (const int64_t *)subcnt->p, (int64_t *)suboff->p, ns);
-        if (jp.n > 0) {
-          KernelTimer kt(s, "rj_join_emit", 12.0 * (double)(ps.n + bs.n) + 16.0 * (double)jp.n);
-          hipLaunchKernelGGL(k_rj_emit_ranges<2>, dim3((unsigned)ns), dim3(RJ_JBLOCK), 0, s->stream,
-                             (const RJSub *)subs->p, (const RJWork *)dw->p, (const uint64_t *)bs.h->p,
-                             (const uint32_t *)bs.row->p, (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
-                             (const uint32_t *)ps.row->p, (const int64_t *)off->p, (int64_t *)oprobe->p,
-                             (int64_t *)obuild->p, (uint8_t *)nullptr, (uint8_t *)nullptr, rp, build_left ? 1 : 0,
-                             (int64_t *)nullptr, (const int64_t *)suboff->p, (unsigned long long *)nullptr,
-                             (int64_t)0);
-          KERNEL_CHECK();
-        }
-      }
-    }
-    jp.left = build_left ? obuild : oprobe;
-    jp.right = build_left ? oprobe : obuild;
-    return jp;
-  }
-  const int64_t cap = total + (p_outer ? Pr.nrows : 0) + (b_outer ? B.nrows : 0);
-  BufPtr oprobe = s->alloc(8 * std::max<int64_t>(cap, 1)), obuild = s->alloc(8 * std::max<int64_t>(cap, 1));
-  if (nw > 0 && total > 0) {
-    BufPtr nsub = s->alloc(8 * nw), soff = s->alloc(8 * (nw + 1));
-    hipLaunchKernelGGL(k_rj_sub_counts, dim3(grid_for(nw, 256)), dim3(256), 0, s->stream, (const int64_t *)cnt->p,
-                       nw, (int64_t *)nsub->p);
-    KERNEL_CHECK();
-    const int64_t ns = exclusive_scan_i64(s, (const int64_t *)nsub->p, (int64_t *)soff->p, nw);
-    BufPtr subs = s->alloc(sizeof(RJSub) * std::max<int64_t>(ns, 1));
-    hipLaunchKernelGGL(k_rj_subs, dim3(grid_for(nw, 256)), dim3(256), 0, s->stream, (const int64_t *)cnt->p,
-                       (const int64_t *)soff->p, nw, (RJSub *)subs->p);
-    KERNEL_CHECK();
-    KernelTimer kt(s, "rj_join_emit", 12.0 * (double)(ps.n + bs.n) + 16.0 * (double)total);
-    hipLaunchKernelGGL(k_rj_emit_ranges<0>, dim3((unsigned)ns), dim3(RJ_JBLOCK), 0, s->stream, (const RJSub *)subs->p,
-                       (const RJWork *)dw->p, (const uint64_t *)bs.h->p, (const uint32_t *)bs.row->p,
-                       (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p, (const uint32_t *)ps.row->p,
-                       (const int64_t *)off->p, (int64_t *)oprobe->p, (int64_t *)obuild->p,
-                       p_outer ? (uint8_t *)pm->p : nullptr, b_outer ? (uint8_t *)bm->p : nullptr, RjPred{}, 0,
-                       (int64_t *)nullptr, (const int64_t *)nullptr, (unsigned long long *)nullptr, (int64_t)0);
-    KERNEL_CHECK();
-  }
-  // (total = 0: no pair, the outer sides' flags stay clear — every row is unmatched)
-  int64_t m = total;
-  // unmatched rows of the outer sides (NULL keys included: never flagged)
-  auto append_unmatched = [&](const BufPtr &matched, int64_t n, int64_t *own, int64_t *other) {
-    if (n == 0) return;
-    BufPtr flags = s->alloc(n);
-    hipLaunchKernelGGL(k_rj_unmatched, dim3(grid_for(n, 256)), dim3(256), 0, s->stream,
-                       (const uint8_t *)matched->p, n, (uint8_t *)flags->p);
-    KERNEL_CHECK();
-    int64_t k = 0;
-    BufPtr rows = compact_flags(s, (const uint8_t *)flags->p, n, &k);
-    if (k > 0) {
-      hipLaunchKernelGGL(k_rj_append, dim3(grid_for(k, 256)), dim3(256), 0, s->stream,
-                         (const int64_t *)rows->p, k, m, own, other);
+      KernelTimer kt(s, "rj_join_emit", 12.0 * (double)(ps.n + bs.n) + 16.0 * (double)total);
+      hipLaunchKernelGGL((k_rj_emit_ranges<0, I>), dim3((unsigned)ns), dim3(RJ_JBLOCK), 0, s->stream, (const RJSub *)subs->p,
+                         (const RJWork *)dw->p, (const uint64_t *)bs.h->p, (const uint32_t *)bs.row->p,
+                         (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p, (const uint32_t *)ps.row->p,
+                         (const int64_t *)off->p, (I *)oprobe->p, (I *)obuild->p,
+                         p_outer ? (uint8_t *)pm->p : nullptr, b_outer ? (uint8_t *)bm->p : nullptr, RjPred{}, 0,
+                         (int64_t *)nullptr, (const int64_t *)nullptr, (unsigned long long *)nullptr, (int64_t)0);
       KERNEL_CHECK();
     }
-    m += k;
+    // (total = 0: no pair, the outer sides' flags stay clear — every row is unmatched)
+    int64_t m = total;
+    // unmatched rows of the outer sides (NULL keys included: never flagged)
+    auto append_unmatched = [&](const BufPtr &matched, int64_t n, I *own, I *other) {
+      if (n == 0) return;
+      BufPtr flags = s->alloc(n);
+      hipLaunchKernelGGL(k_rj_unmatched, dim3(grid_for(n, 256)), dim3(256), 0, s->stream,
+                         (const uint8_t *)matched->p, n, (uint8_t *)flags->p);
+      KERNEL_CHECK();
+      int64_t k = 0;
+      BufPtr rows = compact_flags(s, (const uint8_t *)flags->p, n, &k);
+      if (k > 0) {
+        hipLaunchKernelGGL(k_rj_append<I>, dim3(grid_for(k, 256)), dim3(256), 0, s->stream,
+                           (const int64_t *)rows->p, k, m, own, other);
+        KERNEL_CHECK();
+      }
+      m += k;
+    };
+    if (p_outer) append_unmatched(pm, Pr.nrows, (I *)oprobe->p, (I *)obuild->p);
+    if (b_outer) append_unmatched(bm, B.nrows, (I *)obuild->p, (I *)oprobe->p);
+    JoinPairs jp;
+    jp.left = build_left ? obuild : oprobe;
+    jp.right = build_left ? oprobe : obuild;
+    jp.n = m;
+    jp.iw = (int)sizeof(I);
+    return jp;
+
   };
-  if (p_outer) append_unmatched(pm, Pr.nrows, (int64_t *)oprobe->p, (int64_t *)obuild->p);
-  if (b_outer) append_unmatched(bm, B.nrows, (int64_t *)obuild->p, (int64_t *)oprobe->p);
-  JoinPairs jp;
-  jp.left = build_left ? obuild : oprobe;
-  jp.right = build_left ? oprobe : obuild;
-  jp.n = m;
-  return jp;
+  return idx32 ? emit(int32_t{}) : emit(int64_t{});
 }
 
 // The Filter's names are the join's output names: the left input's columns,

@@ -431,7 +431,7 @@ static DataPtr gather_all(Session *s, const Data &d, const BufPtr &idx, int64_t 
 
 // The output of a join node n from its inputs' row indexes (lazy gathers).
 static DataPtr join_output(Session *s, const NodePtr &n, const Data &l, const Data &r, const BufPtr &li,
-                           const BufPtr &ri, int64_t m, int key_alias, int build_unread = 0) {
+                           const BufPtr &ri, int64_t m, int key_alias, int build_unread = 0, int iw = 8) {
   auto out = std::make_shared<Data>();
   out->nrows = m;
   bool lnull = n->join_type == CAPF_JOIN_RIGHT_OUTER || n->join_type == CAPF_JOIN_FULL_OUTER;
@@ -444,10 +444,10 @@ static DataPtr join_output(Session *s, const NodePtr &n, const Data &l, const Da
   };
   for (size_t i = 0; i < l.cols.size(); ++i)
     out->cols.push_back(build_unread == 1 ? unread(l.cols[i], (int)i == n->join_keys[0].first)
-                                          : gather_lazy(s, l.cols[i], li, m, lnull, &cache));
+                                          : gather_lazy(s, l.cols[i], li, m, lnull, &cache, iw));
   for (size_t i = 0; i < r.cols.size(); ++i)
     out->cols.push_back(build_unread == 2 ? unread(r.cols[i], (int)i == n->join_keys[0].second)
-                                          : gather_lazy(s, r.cols[i], ri, m, rnull, &cache));
+                                          : gather_lazy(s, r.cols[i], ri, m, rnull, &cache, iw));
   if (key_alias) {
     // the build key column of an inner dense join IS the probe key column
     // (equal values on every row): no gather of it
@@ -485,7 +485,7 @@ static DataPtr materialize_impl(const NodePtr &n) {
           DataPtr r = materialize(k->kids[1]);
           JoinPairs jp;
           if (radix_join_filtered(s, n->pred, k->names, *l, *r, k->join_keys, k->join_type, jp)) {
-            return join_output(s, k, *l, *r, jp.left, jp.right, jp.n, 0);
+            return join_output(s, k, *l, *r, jp.left, jp.right, jp.n, 0, 0, jp.iw);
           }
         }
       }
@@ -497,7 +497,7 @@ static DataPtr materialize_impl(const NodePtr &n) {
       DataPtr r = materialize(n->kids[1]);
       BufPtr li, ri;
       int64_t m = 0;
-      int key_alias = 0, build_unread = 0;
+      int key_alias = 0, build_unread = 0, iw = 8;
       if (n->join_type == CAPF_JOIN_CROSS) {
         m = l->nrows * r->nrows;
         cross_index(s, l->nrows, r->nrows, li, ri);
@@ -512,8 +512,9 @@ static DataPtr materialize_impl(const NodePtr &n) {
         m = jp.n;
         key_alias = jp.key_alias;
         build_unread = jp.build_unread;
+        iw = jp.iw;
       }
-      return join_output(s, n, *l, *r, li, ri, m, key_alias, build_unread);
+      return join_output(s, n, *l, *r, li, ri, m, key_alias, build_unread, iw);
     }
     case Kind::Union: {
       DataPtr l = materialize(n->kids[0]);

@@ -355,13 +355,15 @@ def test_filter_fused_into_radix_join(pred, fused, monkeypatch):
 
 
 @pytest.mark.parametrize("fail", ["few", "many"])
-def test_filter_fused_radix_holes(gpu_session, monkeypatch, fail):
+@pytest.mark.parametrize("idx", ["int32", "int64"])
+def test_filter_fused_radix_holes(gpu_session, monkeypatch, fail, idx):
     """The one-pass filtered EMIT: failing pairs leave holes that the tail's
     pairs fill (a few: the uniqueness filter's self-loop pairs); past 2^20
     holes (here x < y fails on ~1.2 M of 2.56 M hub pairs) the join counts the
     passes per sub-item first and writes them compactly.  Exact pair set
-    against numpy."""
+    against numpy (int32 and int64 pair indexes)."""
     monkeypatch.setenv("CAPF_JOIN", "radix")
+    monkeypatch.setenv("CAPF_IDX64", "1" if idx == "int64" else "0")
     rng = np.random.default_rng(31)
     n = 1600
     x = rng.integers(0, 40, n).astype(np.int64)
@@ -472,11 +474,15 @@ def test_join_parity(jt):
 
 @pytest.mark.parametrize("jt", ["inner", "left_outer", "right_outer", "full_outer"])
 @pytest.mark.parametrize("sizes", [(0, 500), (500, 0), (3000, 200000), (300000, 5000), (70000, 70000)])
-def test_radix_join_large(gpu_session, monkeypatch, jt, sizes):
+@pytest.mark.parametrize("idx", ["int32", "int64"])
+def test_radix_join_large(gpu_session, monkeypatch, jt, sizes, idx):
     """The radix join at sizes that fill many partitions, with skewed keys
     (one key on 20 % of the rows: chunked LDS builds and split probe items),
-    NULL keys on both sides, empty sides; checked against numpy."""
+    NULL keys on both sides, empty sides; checked against numpy.  Both widths
+    of the pair list's row indexes (int32 by default below 2^31 rows;
+    CAPF_IDX64=1 keeps int64)."""
     monkeypatch.setenv("CAPF_JOIN", "radix")
+    monkeypatch.setenv("CAPF_IDX64", "1" if idx == "int64" else "0")
     rng = np.random.default_rng(sum(sizes))
     nl, nr = sizes
     def keys(n, hot):

@@ -440,6 +440,8 @@ BufPtr compact_flags(Session *s, const uint8_t *d_flags, int64_t n, int64_t *out
 ColPtr concat_columns(Session *s, const ColPtr &a, const ColPtr &b, Type t);
 // Exclusive scan of int64 counts; returns total.
 int64_t exclusive_scan_i64(Session *s, const int64_t *d_in, int64_t *d_out, int64_t n);
+// int64 exclusive scan, the total left in the device int64 d_total (no host sync).
+void exclusive_scan_i64_async(Session *s, const int64_t *d_in, int64_t *d_out, int64_t n, int64_t *d_total);
 // uint32 exclusive scan (total < 2^32) left on the device, no host sync.
 void exclusive_scan_u32_async(Session *s, const uint32_t *d_in, uint32_t *d_out, int64_t n,
                               uint32_t *d_total);
@@ -455,6 +457,10 @@ struct JoinPairs {
   BufPtr left, right;  // int64 [n], -1 for a null-extended side; null = identity (n rows)
   int64_t n = 0;
   int iw = 8;  // bytes per index entry: 4 = int32 (radix join, both sides < 2^31 rows)
+  // radix join: the build side's columns in sorted order, indexed by the pairs'
+  // build entries (null: those index the build side's own rows)
+  std::shared_ptr<Data> build_sorted;
+  bool build_is_left = false;
   // inner join whose key values are equal on every output row: 1 = the left
   // key column may be replaced by the right one, 2 = the other way round
   int key_alias = 0;

@@ -49,14 +49,15 @@ __global__ void k_add_tile_offsets(T *out, const T *tile_off, int64_t n) {
 template <typename T>
 static void scan_rec(Session *s, const T *in, T *out, int64_t n, T *total_dev) {
   int64_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+  if (tiles == 1) {  // one tile: its sum is the total (no copy launch)
+    hipLaunchKernelGGL(k_scan_tiles<T>, dim3(1), dim3(SCAN_BLOCK), 0, s->stream, in, out, total_dev, n);
+    KERNEL_CHECK();
+    return;
+  }
   BufPtr sums = s->alloc(sizeof(T) * (tiles + 1));
   hipLaunchKernelGGL(k_scan_tiles<T>, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, s->stream, in,
                      out, (T *)sums->p, n);
   KERNEL_CHECK();
-  if (tiles == 1) {
-    HIP_CHECK(hipMemcpyAsync(total_dev, sums->p, sizeof(T), hipMemcpyDeviceToDevice, s->stream));
-    return;
-  }
   BufPtr offs = s->alloc(sizeof(T) * tiles);
   scan_rec<T>(s, (const T *)sums->p, (T *)offs->p, tiles, total_dev);
   hipLaunchKernelGGL(k_add_tile_offsets<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
@@ -70,6 +71,15 @@ int64_t exclusive_scan_i64(Session *s, const int64_t *d_in, int64_t *d_out, int6
   HIP_CHECK(hipMemcpyAsync(s->h_scalars, s->d_scalars, 8, hipMemcpyDeviceToHost, s->stream));
   s->sync();
   return s->h_scalars[0];
+}
+
+// The same without the host read: the total goes to the device int64 d_total.
+void exclusive_scan_i64_async(Session *s, const int64_t *d_in, int64_t *d_out, int64_t n, int64_t *d_total) {
+  if (n <= 0) {
+    HIP_CHECK(hipMemsetAsync(d_total, 0, 8, s->stream));
+    return;
+  }
+  scan_rec<int64_t>(s, d_in, d_out, n, d_total);
 }
 
 // uint32 variant (totals < 2^32), asynchronous: the total stays on the device.

@@ -158,9 +158,12 @@ struct RJTile2 {
   int32_t local;        // this tile's index inside its bucket
 };
 
+// The grids of pass 2 are an upper bound of the tile count (nt1 + 256: no host
+// read of the tile list); blocks past *nt2 exit (their count rows stay 0).
 __global__ __launch_bounds__(RJ_PBLOCK) void k_rj_hist2(const uint64_t *h1, const RJTile2 *tiles,
-                                                         int64_t *counts) {
+                                                         const int64_t *nt2, int64_t *counts) {
   __shared__ uint32_t hist[RJ_P];
+  if ((int64_t)blockIdx.x >= *nt2) return;
   for (int i = threadIdx.x; i < RJ_P; i += RJ_PBLOCK) hist[i] = 0;
   __syncthreads();
   const RJTile2 tl = tiles[blockIdx.x];
@@ -172,20 +175,19 @@ __global__ __launch_bounds__(RJ_PBLOCK) void k_rj_hist2(const uint64_t *h1, cons
 }
 
 __global__ __launch_bounds__(RJ_SBLOCK) void k_rj_scatter2(const uint64_t *h1, const uint32_t *r1,
-                                                            const RJTile2 *tiles, const int64_t *offs,
-                                                            uint64_t *oh, uint32_t *orow) {
+                                                            const RJTile2 *tiles, const int64_t *nt2,
+                                                            const int64_t *offs, uint64_t *oh, uint32_t *orow) {
+  if ((int64_t)blockIdx.x >= *nt2) return;
   const RJTile2 tl = tiles[blockIdx.x];
   rj_scatter_tile<2>(ColView{}, h1, r1, tl.start, tl.end, offs + tl.region + tl.local, tl.ntb, oh, orow);
 }
 
 // Partition starts: pstart[p] for p = b1·256 + b2 (65 536 partitions), + total.
-__global__ void k_rj_pstart(const int64_t *offs2, const RJTile2 *first_tile_of_bucket_region,
-                            const int64_t *bucket_start, const int32_t *bucket_ntiles,
-                            const int64_t *bucket_region, int64_t total, int64_t *pstart) {
-  (void)first_tile_of_bucket_region;
+__global__ void k_rj_pstart(const int64_t *offs2, const int64_t *bucket_start, const int32_t *bucket_ntiles,
+                            const int64_t *bucket_region, const int64_t *total, int64_t *pstart) {
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p <= RJ_P * RJ_P; p += gridDim.x * blockDim.x) {
     if (p == RJ_P * RJ_P) {
-      pstart[p] = total;
+      pstart[p] = *total;
       continue;
     }
     const int b1 = p >> 8, b2 = p & 255;
@@ -194,8 +196,26 @@ __global__ void k_rj_pstart(const int64_t *offs2, const RJTile2 *first_tile_of_b
   }
 }
 
-__global__ void k_rj_bucket_starts(const int64_t *o1, int64_t nt1, int64_t *bstart) {
-  bstart[threadIdx.x] = o1[(int64_t)threadIdx.x * nt1];
+// The pass-2 tile list on the device (one workgroup of RJ_P lanes, lane b =
+// first-level bucket b): tiles of ≤ RJ_TILE rows never straddling a bucket,
+// bucket-major; bucket starts / tile counts / count regions for k_rj_pstart.
+__global__ __launch_bounds__(RJ_P) void k_rj_tiles2(const int64_t *o1, int64_t nt1, const int64_t *total,
+                                                    RJTile2 *tiles, int64_t *bstart, int32_t *bnt, int64_t *breg,
+                                                    int64_t *nt2) {
+  __shared__ int64_t lds[17];
+  const int b = threadIdx.x;
+  const int64_t lo = o1[(int64_t)b * nt1];
+  const int64_t hi = b + 1 < RJ_P ? o1[(int64_t)(b + 1) * nt1] : *total;
+  const int64_t nt = (hi - lo + RJ_TILE - 1) / RJ_TILE;
+  int64_t all;
+  const int64_t tb = block_exclusive_scan(nt, lds, all);
+  bstart[b] = lo;
+  bnt[b] = (int32_t)nt;
+  breg[b] = (int64_t)RJ_P * tb;
+  for (int64_t k = 0; k < nt; ++k)
+    tiles[tb + k] = RJTile2{lo + k * RJ_TILE, min(hi, lo + (k + 1) * RJ_TILE), (int64_t)RJ_P * tb, (int32_t)nt,
+                            (int32_t)k};
+  if (b == 0) *nt2 = all;
 }
 
 // Partitioned side: (h, row) in partition order + partition starts.
@@ -204,13 +224,21 @@ struct RJSide {
   int64_t n = 0;  // partitioned (non-null) rows
 };
 
+// Host-synchronous only when the key column may hold NULLs (the partitioned
+// row count is then read back); otherwise every step stays on the stream: the
+// partitioned rows are n, the pass-2 tile list is built on the device and the
+// pass-2 grids are its upper bound.
 static RJSide rj_partition(Session *s, const ColPtr &col, int64_t n) {
   RJSide out;
   out.pstart = s->alloc(8 * (RJ_P * RJ_P + 1));
   const ColView key = view_of(col);
+  if (n >= (int64_t(1) << 32)) not_impl("radix join side with 2^32 or more rows");
   const int64_t nt1 = std::max<int64_t>(1, (n + RJ_TILE - 1) / RJ_TILE);
+  const int64_t nt2max = nt1 + RJ_P;  // Σ_b ⌈rows_b / TILE⌉ ≤ Σ_b rows_b / TILE + 256
   BufPtr c1 = s->alloc(8 * RJ_P * nt1), o1 = s->alloc(8 * (RJ_P * nt1 + 1));
-  int64_t total = 0;
+  // device scalars: [0] partitioned rows, [1] pass-2 tiles, [2] pass-2 scan total (unread)
+  BufPtr sc = s->alloc(24);
+  int64_t *d_total = (int64_t *)sc->p, *d_nt2 = d_total + 1;
   {
     KernelTimer kt(s, "rj_partition1", 12.0 * n);
     if (n > 0) {
@@ -220,10 +248,16 @@ static RJSide rj_partition(Session *s, const ColPtr &col, int64_t n) {
     } else {
       HIP_CHECK(hipMemsetAsync(c1->p, 0, 8 * RJ_P * nt1, s->stream));
     }
-    total = exclusive_scan_i64(s, (const int64_t *)c1->p, (int64_t *)o1->p, RJ_P * nt1);
+    exclusive_scan_i64_async(s, (const int64_t *)c1->p, (int64_t *)o1->p, RJ_P * nt1, d_total);
+  }
+  const bool all_null = key.type == CAPF_TYPE_NULL || !key.data || n == 0;
+  int64_t total = all_null ? 0 : n;
+  if (!all_null && key.valid) {  // NULL keys are not partitioned: the count decides the sizes
+    HIP_CHECK(hipMemcpyAsync(s->h_scalars, d_total, 8, hipMemcpyDeviceToHost, s->stream));
+    s->sync();
+    total = s->h_scalars[0];
   }
   out.n = total;
-  if (total >= (int64_t(1) << 32)) not_impl("radix join side with 2^32 or more rows");
   BufPtr h1 = s->alloc(8 * std::max<int64_t>(total, 1)), r1 = s->alloc(4 * std::max<int64_t>(total, 1));
   if (n > 0) {
     KernelTimer kt(s, "rj_partition1", 12.0 * total);
@@ -231,61 +265,35 @@ static RJSide rj_partition(Session *s, const ColPtr &col, int64_t n) {
                        (const int64_t *)o1->p, (uint64_t *)h1->p, (uint32_t *)r1->p);
     KERNEL_CHECK();
   }
-  // first-level bucket starts (257 values, gathered on the device) → the
-  // pass-2 tile list on the host
-  std::vector<int64_t> bstart(RJ_P + 1);
-  {
-    BufPtr bs = s->alloc(8 * RJ_P);
-    hipLaunchKernelGGL(k_rj_bucket_starts, dim3(1), dim3(RJ_P), 0, s->stream, (const int64_t *)o1->p, nt1,
-                       (int64_t *)bs->p);
-    KERNEL_CHECK();
-    HIP_CHECK(hipMemcpyAsync(bstart.data(), bs->p, 8 * RJ_P, hipMemcpyDeviceToHost, s->stream));
-    s->sync();
-    bstart[RJ_P] = total;
-  }
-  std::vector<RJTile2> tiles;
-  std::vector<int32_t> bnt(RJ_P);
-  std::vector<int64_t> breg(RJ_P);
-  for (int b = 0; b < RJ_P; ++b) {
-    const int64_t lo = bstart[b], hi = bstart[b + 1];
-    const int32_t nt = (int32_t)((hi - lo + RJ_TILE - 1) / RJ_TILE);
-    bnt[b] = nt;
-    breg[b] = (int64_t)RJ_P * (int64_t)tiles.size();
-    for (int32_t k = 0; k < nt; ++k)
-      tiles.push_back(RJTile2{lo + (int64_t)k * RJ_TILE, std::min(hi, lo + (int64_t)(k + 1) * RJ_TILE), breg[b], nt, k});
-  }
-  const int64_t nt2 = (int64_t)tiles.size();
-  BufPtr dt = s->alloc(sizeof(RJTile2) * std::max<int64_t>(nt2, 1));
+  BufPtr dt = s->alloc(sizeof(RJTile2) * nt2max);
   BufPtr meta = s->alloc(8 * RJ_P + 4 * RJ_P + 8 * RJ_P);
   int64_t *d_bstart = (int64_t *)meta->p;
   int32_t *d_bnt = (int32_t *)(d_bstart + RJ_P);
   int64_t *d_breg = (int64_t *)(d_bnt + RJ_P);
-  if (nt2 > 0)
-    HIP_CHECK(hipMemcpyAsync(dt->p, tiles.data(), sizeof(RJTile2) * nt2, hipMemcpyHostToDevice, s->stream));
-  HIP_CHECK(hipMemcpyAsync(d_bstart, bstart.data(), 8 * RJ_P, hipMemcpyHostToDevice, s->stream));
-  HIP_CHECK(hipMemcpyAsync(d_bnt, bnt.data(), 4 * RJ_P, hipMemcpyHostToDevice, s->stream));
-  HIP_CHECK(hipMemcpyAsync(d_breg, breg.data(), 8 * RJ_P, hipMemcpyHostToDevice, s->stream));
+  hipLaunchKernelGGL(k_rj_tiles2, dim3(1), dim3(RJ_P), 0, s->stream, (const int64_t *)o1->p, nt1,
+                     (const int64_t *)d_total, (RJTile2 *)dt->p, d_bstart, d_bnt, d_breg, d_nt2);
+  KERNEL_CHECK();
   out.h = s->alloc(8 * std::max<int64_t>(total, 1));
   out.row = s->alloc(4 * std::max<int64_t>(total, 1));
-  BufPtr o2 = s->alloc(8 * (RJ_P * std::max<int64_t>(nt2, 1) + 1));
-  if (nt2 > 0) {
+  BufPtr o2 = s->alloc(8 * (RJ_P * nt2max + 1));
+  if (total > 0) {
     KernelTimer kt(s, "rj_partition2", 24.0 * total);
-    BufPtr c2 = s->alloc(8 * RJ_P * nt2);
-    hipLaunchKernelGGL(k_rj_hist2, dim3((unsigned)nt2), dim3(RJ_PBLOCK), 0, s->stream,
-                       (const uint64_t *)h1->p, (const RJTile2 *)dt->p, (int64_t *)c2->p);
+    BufPtr c2 = s->alloc(8 * RJ_P * nt2max);
+    HIP_CHECK(hipMemsetAsync(c2->p, 0, 8 * RJ_P * nt2max, s->stream));  // rows of the unused tiles
+    hipLaunchKernelGGL(k_rj_hist2, dim3((unsigned)nt2max), dim3(RJ_PBLOCK), 0, s->stream,
+                       (const uint64_t *)h1->p, (const RJTile2 *)dt->p, (const int64_t *)d_nt2, (int64_t *)c2->p);
     KERNEL_CHECK();
-    exclusive_scan_i64(s, (const int64_t *)c2->p, (int64_t *)o2->p, RJ_P * nt2);
-    hipLaunchKernelGGL(k_rj_scatter2, dim3((unsigned)nt2), dim3(RJ_SBLOCK), 0, s->stream,
+    exclusive_scan_i64_async(s, (const int64_t *)c2->p, (int64_t *)o2->p, RJ_P * nt2max, d_nt2 + 1);
+    hipLaunchKernelGGL(k_rj_scatter2, dim3((unsigned)nt2max), dim3(RJ_SBLOCK), 0, s->stream,
                        (const uint64_t *)h1->p, (const uint32_t *)r1->p, (const RJTile2 *)dt->p,
-                       (const int64_t *)o2->p, (uint64_t *)out.h->p, (uint32_t *)out.row->p);
+                       (const int64_t *)d_nt2, (const int64_t *)o2->p, (uint64_t *)out.h->p, (uint32_t *)out.row->p);
     KERNEL_CHECK();
   }
   hipLaunchKernelGGL(k_rj_pstart, dim3((RJ_P * RJ_P + 256) / 256), dim3(256), 0, s->stream,
-                     (const int64_t *)o2->p, (const RJTile2 *)nullptr, (const int64_t *)d_bstart,
-                     (const int32_t *)d_bnt, (const int64_t *)d_breg, total, (int64_t *)out.pstart->p);
+                     (const int64_t *)o2->p, (const int64_t *)d_bstart, (const int32_t *)d_bnt,
+                     (const int64_t *)d_breg, (const int64_t *)d_total, (int64_t *)out.pstart->p);
   KERNEL_CHECK();
-  s->sync();  // the host tile list / metadata go out of scope
-  return out;
+  return out;  // (the temporaries return to the stream-ordered pool)
 }
 
 // ---------------------------------------------------------------- join
@@ -305,15 +313,20 @@ struct RJWork {
 // a hub key's whole product.)
 constexpr int RJ_RUNCAP = 2048;  // run-table slots (≤ RJ_CHUNK runs per chunk, load ≤ 1/2)
 
-__global__ __launch_bounds__(RJ_JBLOCK) void k_rj_join_runs(const RJWork *work, const uint64_t *bh,
-                                                             const int64_t *bstart, const uint64_t *ph,
-                                                             int64_t *out_cnt) {
+// (grid: an upper bound of the item count; blocks past *nw count 0 pairs)
+__global__ __launch_bounds__(RJ_JBLOCK) void k_rj_join_runs(const RJWork *work, const int64_t *nw,
+                                                             const uint64_t *bh, const int64_t *bstart,
+                                                             const uint64_t *ph, int64_t *out_cnt) {
   __shared__ uint64_t kk[RJ_CHUNK];
   __shared__ unsigned long long hm[RJ_CHUNK / WAVE];  // run-head bitmask
   __shared__ uint64_t th[RJ_RUNCAP];
   __shared__ uint32_t tv[RJ_RUNCAP];                   // start << 16 | length (chunk-relative), 0 = empty
   constexpr int NW = RJ_JBLOCK / WAVE;
   __shared__ int64_t wsum[NW];
+  if ((int64_t)blockIdx.x >= *nw) {
+    if (threadIdx.x == 0) out_cnt[blockIdx.x] = 0;
+    return;
+  }
   const RJWork wk = work[blockIdx.x];
   const int64_t b0 = bstart[wk.part], b1 = bstart[wk.part + wk.np];
   const int wv = threadIdx.x / WAVE, lane = lane_id();
@@ -489,7 +502,7 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_emit_ranges(const RJSub *subs,
                                                                const uint32_t *prow, const int64_t *out_off,
                                                                I *oprobe, I *obuild,
                                                                uint8_t *pmatched, uint8_t *bmatched,
-                                                               const RjPred fp, int build_left,
+                                                               const RjPred fp, int build_left, int build_pos,
                                                                int64_t *subcnt, const int64_t *suboff,
                                                                unsigned long long *nholes, int64_t hcap) {
   __shared__ uint64_t kk[RJ_CHUNK];
@@ -595,7 +608,9 @@ __global__ __launch_bounds__(RJ_JBLOCK) void k_rj_emit_ranges(const RJSub *subs,
           for (int k = 0; k < U; ++k) {
             const uint32_t b = bl[k];
             bi[k] = c0 + bst[b] + (xs[k] - bex[b]);
-            br[k] = brow[bi[k]];
+            // build_pos: the build side's sorted position (its columns were permuted
+            // into sorted order: later gathers through it stream), else its row
+            br[k] = build_pos ? (uint32_t)bi[k] : brow[bi[k]];
             pr[k] = bpr[b];
           }
           if constexpr (MODE == 0) {
@@ -754,7 +769,11 @@ bool radix_join_applies(const Data &l, const Data &r, const std::vector<std::pai
   return std::max(l.nrows, r.nrows) >= (int64_t(1) << 18);
 }
 
-static BufPtr rj_work_items(Session *s, const RJSide &bs, const RJSide &ps, int64_t probe_rows, int64_t &nw) {
+// The item list stays on the device: *d_nw items, `nw_max` (returned) an upper
+// bound sizing the list and the COUNT grid (Σ_g ⌈np_g / pchunk⌉ ≤ NG + probe
+// rows / pchunk).
+static BufPtr rj_work_items(Session *s, const RJSide &bs, const RJSide &ps, int64_t probe_rows, int64_t &nw_max,
+                            int64_t *d_nw) {
   // work items on the device: ⌈probe rows / pchunk⌉ per partition with rows on
   // both sides; partitions whose build side needs several LDS fills ("heavy",
   // skewed keys) are listed first so the dispatcher starts them early.  pchunk
@@ -777,14 +796,13 @@ static BufPtr rj_work_items(Session *s, const RJSide &bs, const RJSide &ps, int6
                      (const int64_t *)bs.pstart->p, (const int64_t *)ps.pstart->p, pchunk, G, NG,
                      (int64_t *)icnt->p);
   KERNEL_CHECK();
-  nw = exclusive_scan_i64(s, (const int64_t *)icnt->p, (int64_t *)ioff->p, 2 * NG);
-  BufPtr dw = s->alloc(sizeof(RJWork) * std::max<int64_t>(nw, 1));
-  if (nw > 0) {
-    hipLaunchKernelGGL(k_rj_items, dim3(grid_for(NG, 256)), dim3(256), 0, s->stream,
-                       (const int64_t *)bs.pstart->p, (const int64_t *)ps.pstart->p, pchunk, G, NG,
-                       (const int64_t *)ioff->p, (RJWork *)dw->p);
-    KERNEL_CHECK();
-  }
+  exclusive_scan_i64_async(s, (const int64_t *)icnt->p, (int64_t *)ioff->p, 2 * NG, d_nw);
+  nw_max = NG + ps.n / pchunk + 1;
+  BufPtr dw = s->alloc(sizeof(RJWork) * nw_max);
+  hipLaunchKernelGGL(k_rj_items, dim3(grid_for(NG, 256)), dim3(256), 0, s->stream,
+                     (const int64_t *)bs.pstart->p, (const int64_t *)ps.pstart->p, pchunk, G, NG,
+                     (const int64_t *)ioff->p, (RJWork *)dw->p);
+  KERNEL_CHECK();
   return dw;
 }
 
@@ -829,23 +847,56 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
   // probe-order kernels for it here — a probe of the sorted build partitions
   // and one of LDS tables — ran 3× slower and were removed.)
   RJSide ps = rj_partition(s, pk, Pr.nrows);
+  // COUNT, the pair offsets and the EMIT's sub-items are enqueued without a
+  // host read; ONE sync then fetches the pair total (the output's size) and
+  // the sub-item count (the EMIT grid)
+  BufPtr dsc = s->alloc(24);  // [0] items, [1] pairs, [2] sub-items
+  int64_t *d_nw = (int64_t *)dsc->p;
   int64_t nw = 0;
-  BufPtr dw = rj_work_items(s, bs, ps, Pr.nrows, nw);
-  BufPtr cnt = s->alloc(8 * std::max<int64_t>(nw, 1)), off = s->alloc(8 * (nw + 1));
-  int64_t total = 0;
-  if (nw > 0) {
+  BufPtr dw = rj_work_items(s, bs, ps, Pr.nrows, nw, d_nw);
+  BufPtr cnt = s->alloc(8 * nw), off = s->alloc(8 * (nw + 1));
+  BufPtr nsub = s->alloc(8 * nw), soff = s->alloc(8 * (nw + 1));
+  {
     KernelTimer kt(s, "rj_join_count", 12.0 * (double)(ps.n + bs.n));
     hipLaunchKernelGGL(k_rj_join_runs, dim3((unsigned)nw), dim3(RJ_JBLOCK), 0, s->stream, (const RJWork *)dw->p,
-                       (const uint64_t *)bs.h->p, (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
-                       (int64_t *)cnt->p);
+                       (const int64_t *)d_nw, (const uint64_t *)bs.h->p, (const int64_t *)bs.pstart->p,
+                       (const uint64_t *)ps.h->p, (int64_t *)cnt->p);
     KERNEL_CHECK();
-    total = exclusive_scan_i64(s, (const int64_t *)cnt->p, (int64_t *)off->p, nw);
   }
+  exclusive_scan_i64_async(s, (const int64_t *)cnt->p, (int64_t *)off->p, nw, d_nw + 1);
+  hipLaunchKernelGGL(k_rj_sub_counts, dim3(grid_for(nw, 256)), dim3(256), 0, s->stream, (const int64_t *)cnt->p,
+                     nw, (int64_t *)nsub->p);
+  KERNEL_CHECK();
+  exclusive_scan_i64_async(s, (const int64_t *)nsub->p, (int64_t *)soff->p, nw, d_nw + 2);
+  HIP_CHECK(hipMemcpyAsync(s->h_scalars, d_nw + 1, 16, hipMemcpyDeviceToHost, s->stream));
+  s->sync();
+  const int64_t total = s->h_scalars[0], ns = s->h_scalars[1];
   // the pair list's row indexes: int32 when both sides have < 2^31 rows (half the
   // EMIT's bytes and half the index bytes of every later gather); CAPF_IDX64=1
   // keeps int64 (tests run both)
   const char *i64env = getenv("CAPF_IDX64");
   const bool idx32 = !(i64env && atoi(i64env) != 0) && l.nrows < (int64_t(1) << 31) && r.nrows < (int64_t(1) << 31);
+  // Output far larger than the build side (a hub key's build rows repeat in
+  // many pairs): the build side's columns are gathered once into sorted order
+  // and the pairs carry sorted positions, so every later gather of a build
+  // column reads consecutive rows of a run instead of one random row per pair
+  // (var2 s14: the build column's gather 650 → ~200 µs).  Not for an outer
+  // build side (its unmatched rows are appended by original row).
+  const bool build_pos = idx32 && !b_outer && bs.n > 0 && total >= 4 * bs.n;
+  DataPtr bsorted;
+  if (build_pos) {
+    bsorted = std::make_shared<Data>();
+    bsorted->nrows = bs.n;
+    for (const ColPtr &c : B.cols)
+      bsorted->cols.push_back(c->is_const && c->n > 0 ? const_column(s, *c, bs.n)
+                                                     : gather_column_w(s, c, bs.row->p, 4, bs.n, false));
+  }
+  BufPtr subs = s->alloc(sizeof(RJSub) * std::max<int64_t>(ns, 1));
+  if (ns > 0) {
+    hipLaunchKernelGGL(k_rj_subs, dim3(grid_for(nw, 256)), dim3(256), 0, s->stream, (const int64_t *)cnt->p,
+                       (const int64_t *)soff->p, nw, (RJSub *)subs->p);
+    KERNEL_CHECK();
+  }
   auto emit = [&](auto ityp) -> JoinPairs {
     using I = decltype(ityp);
     BufPtr pm, bm;
@@ -862,6 +913,8 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
       JoinPairs jp;
       jp.n = 0;
       jp.iw = (int)sizeof(I);
+      jp.build_sorted = bsorted;
+      jp.build_is_left = build_left;
       BufPtr oprobe = s->alloc(8), obuild = s->alloc(8);
       RjPred rp{};
       std::vector<BufPtr> keep;  // the operand arrays, alive until the EMIT passes are enqueued
@@ -896,16 +949,7 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
         rp.t[k].op = pred->t[k].op;
         rp.t[k].neg = pred->t[k].neg;
       }
-      if (nw > 0 && total > 0) {
-        BufPtr nsub = s->alloc(8 * nw), soff = s->alloc(8 * (nw + 1));
-        hipLaunchKernelGGL(k_rj_sub_counts, dim3(grid_for(nw, 256)), dim3(256), 0, s->stream,
-                           (const int64_t *)cnt->p, nw, (int64_t *)nsub->p);
-        KERNEL_CHECK();
-        const int64_t ns = exclusive_scan_i64(s, (const int64_t *)nsub->p, (int64_t *)soff->p, nw);
-        BufPtr subs = s->alloc(sizeof(RJSub) * std::max<int64_t>(ns, 1));
-        hipLaunchKernelGGL(k_rj_subs, dim3(grid_for(nw, 256)), dim3(256), 0, s->stream, (const int64_t *)cnt->p,
-                           (const int64_t *)soff->p, nw, (RJSub *)subs->p);
-        KERNEL_CHECK();
+      if (total > 0) {
         // one pass: passing pairs at their unfiltered positions, failing ones
         // listed as holes, then the tail's pairs moved into them
         const int64_t hcap = std::min<int64_t>(total, int64_t(1) << 20);
@@ -919,7 +963,7 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
                              (const RJSub *)subs->p, (const RJWork *)dw->p, (const uint64_t *)bs.h->p,
                              (const uint32_t *)bs.row->p, (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
                              (const uint32_t *)ps.row->p, (const int64_t *)off->p, (I *)oprobe->p,
-                             (I *)obuild->p, (uint8_t *)nullptr, (uint8_t *)nullptr, rp, build_left ? 1 : 0,
+                             (I *)obuild->p, (uint8_t *)nullptr, (uint8_t *)nullptr, rp, build_left ? 1 : 0, build_pos ? 1 : 0,
                              (int64_t *)holes->p, (const int64_t *)nullptr, (unsigned long long *)nh->p, hcap);
           KERNEL_CHECK();
         }
@@ -949,7 +993,7 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
                                (const RJSub *)subs->p, (const RJWork *)dw->p, (const uint64_t *)bs.h->p,
                                (const uint32_t *)bs.row->p, (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
                                (const uint32_t *)ps.row->p, (const int64_t *)off->p, (I *)nullptr,
-                               (I *)nullptr, (uint8_t *)nullptr, (uint8_t *)nullptr, rp, build_left ? 1 : 0,
+                               (I *)nullptr, (uint8_t *)nullptr, (uint8_t *)nullptr, rp, build_left ? 1 : 0, build_pos ? 1 : 0,
                                (int64_t *)subcnt->p, (const int64_t *)nullptr, (unsigned long long *)nullptr,
                                (int64_t)0);
             KERNEL_CHECK();
@@ -961,7 +1005,7 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
                                (const RJSub *)subs->p, (const RJWork *)dw->p, (const uint64_t *)bs.h->p,
                                (const uint32_t *)bs.row->p, (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p,
                                (const uint32_t *)ps.row->p, (const int64_t *)off->p, (I *)oprobe->p,
-                               (I *)obuild->p, (uint8_t *)nullptr, (uint8_t *)nullptr, rp, build_left ? 1 : 0,
+                               (I *)obuild->p, (uint8_t *)nullptr, (uint8_t *)nullptr, rp, build_left ? 1 : 0, build_pos ? 1 : 0,
                                (int64_t *)nullptr, (const int64_t *)suboff->p, (unsigned long long *)nullptr,
                                (int64_t)0);
             KERNEL_CHECK();
@@ -975,22 +1019,13 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
     const int64_t cap = total + (p_outer ? Pr.nrows : 0) + (b_outer ? B.nrows : 0);
     BufPtr oprobe = s->alloc(sizeof(I) * std::max<int64_t>(cap, 1)),
            obuild = s->alloc(sizeof(I) * std::max<int64_t>(cap, 1));
-    if (nw > 0 && total > 0) {
-      BufPtr nsub = s->alloc(8 * nw), soff = s->alloc(8 * (nw + 1));
-      hipLaunchKernelGGL(k_rj_sub_counts, dim3(grid_for(nw, 256)), dim3(256), 0, s->stream, (const int64_t *)cnt->p,
-                         nw, (int64_t *)nsub->p);
-      KERNEL_CHECK();
-      const int64_t ns = exclusive_scan_i64(s, (const int64_t *)nsub->p, (int64_t *)soff->p, nw);
-      BufPtr subs = s->alloc(sizeof(RJSub) * std::max<int64_t>(ns, 1));
-      hipLaunchKernelGGL(k_rj_subs, dim3(grid_for(nw, 256)), dim3(256), 0, s->stream, (const int64_t *)cnt->p,
-                         (const int64_t *)soff->p, nw, (RJSub *)subs->p);
-      KERNEL_CHECK();
+    if (total > 0) {
       KernelTimer kt(s, "rj_join_emit", 12.0 * (double)(ps.n + bs.n) + 16.0 * (double)total);
       hipLaunchKernelGGL((k_rj_emit_ranges<0, I>), dim3((unsigned)ns), dim3(RJ_JBLOCK), 0, s->stream, (const RJSub *)subs->p,
                          (const RJWork *)dw->p, (const uint64_t *)bs.h->p, (const uint32_t *)bs.row->p,
                          (const int64_t *)bs.pstart->p, (const uint64_t *)ps.h->p, (const uint32_t *)ps.row->p,
                          (const int64_t *)off->p, (I *)oprobe->p, (I *)obuild->p,
-                         p_outer ? (uint8_t *)pm->p : nullptr, b_outer ? (uint8_t *)bm->p : nullptr, RjPred{}, 0,
+                         p_outer ? (uint8_t *)pm->p : nullptr, b_outer ? (uint8_t *)bm->p : nullptr, RjPred{}, 0, build_pos ? 1 : 0,
                          (int64_t *)nullptr, (const int64_t *)nullptr, (unsigned long long *)nullptr, (int64_t)0);
       KERNEL_CHECK();
     }
@@ -1019,6 +1054,8 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
     jp.right = build_left ? oprobe : obuild;
     jp.n = m;
     jp.iw = (int)sizeof(I);
+    jp.build_sorted = bsorted;
+    jp.build_is_left = build_left;
     return jp;
 
   };

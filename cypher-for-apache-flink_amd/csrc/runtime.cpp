@@ -485,7 +485,9 @@ static DataPtr materialize_impl(const NodePtr &n) {
           DataPtr r = materialize(k->kids[1]);
           JoinPairs jp;
           if (radix_join_filtered(s, n->pred, k->names, *l, *r, k->join_keys, k->join_type, jp)) {
-            return join_output(s, k, *l, *r, jp.left, jp.right, jp.n, 0, 0, jp.iw);
+            const Data &lb = jp.build_sorted && jp.build_is_left ? *jp.build_sorted : *l;
+            const Data &rb = jp.build_sorted && !jp.build_is_left ? *jp.build_sorted : *r;
+            return join_output(s, k, lb, rb, jp.left, jp.right, jp.n, 0, 0, jp.iw);
           }
         }
       }
@@ -498,6 +500,7 @@ static DataPtr materialize_impl(const NodePtr &n) {
       BufPtr li, ri;
       int64_t m = 0;
       int key_alias = 0, build_unread = 0, iw = 8;
+      DataPtr sorted_l, sorted_r;  // a radix join's build side in sorted order
       if (n->join_type == CAPF_JOIN_CROSS) {
         m = l->nrows * r->nrows;
         cross_index(s, l->nrows, r->nrows, li, ri);
@@ -513,8 +516,10 @@ static DataPtr materialize_impl(const NodePtr &n) {
         key_alias = jp.key_alias;
         build_unread = jp.build_unread;
         iw = jp.iw;
+        (jp.build_is_left ? sorted_l : sorted_r) = jp.build_sorted;
       }
-      return join_output(s, n, *l, *r, li, ri, m, key_alias, build_unread, iw);
+      return join_output(s, n, sorted_l ? *sorted_l : *l, sorted_r ? *sorted_r : *r, li, ri, m, key_alias,
+                         build_unread, iw);
     }
     case Kind::Union: {
       DataPtr l = materialize(n->kids[0]);

@@ -887,9 +887,27 @@ JoinPairs radix_join(Session *s, const Data &l, const Data &r,
   if (build_pos) {
     bsorted = std::make_shared<Data>();
     bsorted->nrows = bs.n;
-    for (const ColPtr &c : B.cols)
-      bsorted->cols.push_back(c->is_const && c->n > 0 ? const_column(s, *c, bs.n)
-                                                     : gather_column_w(s, c, bs.row->p, 4, bs.n, false));
+    for (const ColPtr &c : B.cols) {
+      ColPtr pc = c->is_const && c->n > 0 ? const_column(s, *c, bs.n) : gather_column_w(s, c, bs.row->p, 4, bs.n, false);
+      // no NULL key: the sorted columns are permutations of the build columns, so
+      // their statistics (min / max / non-null / dense-unique, uniqueness) carry
+      // over — a base column's are computed once and kept; a later dense join
+      // proving its keys match then needs no statistics pass per query
+      if (bs.n == B.nrows && !pc->is_const && c->type != Type::List && c->type != Type::Null) {
+        std::optional<ColStats> st;
+        int8_t uq;
+        if (!c->lazy) st = column_stats(s, c);
+        {
+          std::lock_guard<std::mutex> g(c->mu);
+          if (!st && c->stats) st = c->stats;
+          uq = c->unique_flag;
+        }
+        std::lock_guard<std::mutex> g(pc->mu);
+        if (st) pc->stats = st;
+        pc->unique_flag = uq;
+      }
+      bsorted->cols.push_back(pc);
+    }
   }
   BufPtr subs = s->alloc(sizeof(RJSub) * std::max<int64_t>(ns, 1));
   if (ns > 0) {

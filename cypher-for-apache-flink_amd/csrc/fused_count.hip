@@ -686,10 +686,10 @@ static bool collect(const NodePtr &n, JoinGraph &g, std::vector<ColRef> &out) {
       out = c;
       const NodePtr &kid = n->kids[0];
       std::vector<int> refs;
-      for (auto &nm : n->pred.names) refs.push_back(is_literal_set_name(nm) ? -1 : kid->col_index(nm));
+      for (auto &nm : n->pred.names) refs.push_back(is_session_table_name(nm) ? -1 : kid->col_index(nm));
       std::set<int> leaves;
       for (size_t k = 0; k < refs.size(); ++k) {
-        if (is_literal_set_name(n->pred.names[k])) continue;
+        if (is_session_table_name(n->pred.names[k])) continue;
         const int r = refs[k];
         if (r < 0 || c[r].leaf < 0) return false;
         leaves.insert(c[r].leaf);
@@ -699,7 +699,7 @@ static bool collect(const NodePtr &n, JoinGraph &g, std::vector<ColRef> &out) {
         int lf = *leaves.begin();
         Program p = n->pred;
         for (size_t k = 0; k < p.names.size(); ++k)
-          if (!is_literal_set_name(p.names[k])) p.names[k] = g.leaves[lf].node->names[c[refs[k]].col];
+          if (!is_session_table_name(p.names[k])) p.names[k] = g.leaves[lf].node->names[c[refs[k]].col];
         g.leaves[lf].filters.push_back(std::move(p));
         return true;
       }

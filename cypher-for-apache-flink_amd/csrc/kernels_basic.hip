@@ -1074,6 +1074,13 @@ __device__ Val run_program(const Instr *code, int ncode, const ColView *cols, in
         st[sp++] = hit ? mkb(true) : in.f != 0.0 ? mknull(CAPF_TYPE_BOOL) : mkb(false);
         break;
       }
+      case OP_STR_MAP: {  // cols[in.i] = a code map (base = its length)
+        Val a = st[--sp];
+        const int64_t c = a.nul ? -1 : a.b;
+        const int64_t m = c >= 0 && c < cols[in.i].base ? ((const int64_t *)cols[in.i].data)[c] : -1;
+        st[sp++] = m < 0 ? mknull(CAPF_TYPE_STRING) : mk(m, CAPF_TYPE_STRING, 0);
+        break;
+      }
       case OP_TO_BOOLEAN: {  // cols[in.i] = the session's strings parsed as booleans
         Val a = st[--sp];
         if (a.nul || a.t == CAPF_TYPE_BOOL) {
@@ -1144,6 +1151,14 @@ static DeviceProgram upload_program(Session *s, const Program &p,
       views.push_back(ColView{ls.first->p, nullptr, (int32_t)Type::Int64, ENC_PLAIN, ls.second});
       continue;
     }
+    if (is_code_map_name(nm)) {  // code → code table, its length in `base`
+      const long id = atol(nm.c_str() + 5);
+      std::lock_guard<std::mutex> g(s->user_mu);
+      if (id < 0 || (size_t)id >= s->code_maps.size()) illegal("unknown code map '" + nm.substr(1) + "'");
+      const auto &cm = s->code_maps[(size_t)id];
+      views.push_back(ColView{cm.first->p, nullptr, (int32_t)Type::Int64, ENC_PLAIN, cm.second});
+      continue;
+    }
     int idx = -1;
     for (size_t k = 0; k < names.size(); ++k)
       if (names[k] == nm) idx = (int)k;
@@ -1190,7 +1205,7 @@ static DeviceProgram upload_program(Session *s, const Program &p,
       case OP_LIT_NULL: case OP_LIST_SIZE: depth++; break;
       case OP_AND: case OP_OR: case OP_COALESCE: depth -= (int)in.i - 1; break;
       case OP_NOT: case OP_IS_NULL: case OP_IS_NOT_NULL: case OP_NEG: case OP_TO_FLOAT:
-      case OP_TO_INTEGER: case OP_STR_LEN: case OP_TO_BOOLEAN: case OP_IN_SET: break;
+      case OP_TO_INTEGER: case OP_STR_LEN: case OP_TO_BOOLEAN: case OP_IN_SET: case OP_STR_MAP: break;
       case OP_IF: depth -= 2; break;
       default:
         if (!is_math1(in.op)) depth -= 1;  // binary operators; unary math keeps the depth

@@ -317,6 +317,14 @@ Type infer_type(const Program &p, const std::vector<std::string> &names,
         st.push_back(Type::Int64);
         break;
       }
+      case OP_STR_MAP: {
+        if (in.i < 0 || (size_t)in.i >= p.names.size() || !is_code_map_name(p.names[in.i]))
+          illegal("malformed expression program (code map)");
+        Type a = pop();
+        if (a != Type::String && a != Type::Null) illegal("string function of a non-string value");
+        st.push_back(Type::String);
+        break;
+      }
       case OP_LIST_SIZE: {
         if (in.i < 0 || (size_t)in.i >= p.names.size()) illegal("malformed expression program (column)");
         const std::string &nm = p.names[in.i];
@@ -837,6 +845,21 @@ capf_status capf_session_copy(capf_session *cs, void *dst, const void *src, int6
   const hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
   HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)bytes, k, cs->impl.stream));
   cs->impl.sync();
+  CAPF_API_END
+}
+
+capf_status capf_session_code_map(capf_session *cs, const int64_t *codes, int64_t n, int32_t *map_id) {
+  CAPF_API_BEGIN
+  need(cs, "session");
+  need(map_id, "map_id");
+  if (n < 0 || (n > 0 && !codes)) illegal("bad code map");
+  Session &s = cs->impl;
+  BufPtr b = s.alloc(8 * std::max<int64_t>(n, 1));
+  if (n > 0) HIP_CHECK(hipMemcpyAsync(b->p, codes, 8 * n, hipMemcpyHostToDevice, s.stream));
+  s.sync();  // (pageable source)
+  std::lock_guard<std::mutex> g(s.user_mu);
+  *map_id = (int32_t)s.code_maps.size();
+  s.code_maps.emplace_back(b, n);
   CAPF_API_END
 }
 

@@ -36,7 +36,7 @@ OP_TO_FLOAT, OP_TO_INTEGER, OP_COALESCE = 40, 41, 50
 OP_STR_LEN, OP_LIST_SIZE, OP_IF = 60, 61, 62
 OP_ROUND, OP_ABS, OP_CEIL, OP_FLOOR, OP_SIGN, OP_SQRT, OP_LOG, OP_LOG10, OP_EXP = 70, 71, 72, 73, 74, 75, 76, 77, 78
 OP_SIN, OP_COS, OP_TAN, OP_ASIN, OP_ACOS, OP_ATAN, OP_DEGREES, OP_RADIANS = 79, 80, 81, 82, 83, 84, 85, 86
-OP_ATAN2, OP_TO_BOOLEAN, OP_IN_SET = 87, 88, 89
+OP_ATAN2, OP_TO_BOOLEAN, OP_IN_SET, OP_STR_MAP = 87, 88, 89, 90
 IN_SET_MIN = 17  # list length from which IN runs as a session-set lookup (shorter: an OR of equalities)
 
 # aggregators
@@ -324,6 +324,142 @@ class CaseExpr(Expr):
         return f"CASE {alts}{'' if self.default is None else f' ELSE {self.default}'} END"
 
 
+# String functions (FlinkSQLExprMapper.scala:187-195): one STRING operand and
+# literal arguments — on the GPU a code map of the session dictionary
+# (CAPF_OP_STR_MAP), the function applied per dictionary string on the host.
+ToUpper = _unary("ToUpper", "toUpper({})")  # upperCase (:190)
+ToLower = _unary("ToLower", "toLower({})")  # lowerCase (:191)
+Trim = _unary("Trim", "trim({})")           # trim(): SQL TRIM(BOTH ' ') (:187)
+LTrim = _unary("LTrim", "lTrim({})")        # (:188)
+RTrim = _unary("RTrim", "rTrim({})")        # (:189)
+
+
+@dataclass(frozen=True)
+class Substring(Expr):
+    """substring(s, start[, length]) (okapi Substring; FlinkSQLExprMapper.scala
+    :195: child0.substring(child1 + 1, child2 — or 1 when absent)): Calcite's
+    1-based SUBSTRING over UTF-16 units."""
+    expr: Expr
+    start: Expr
+    length: object = None
+
+    def __str__(self):
+        return f"substring({self.expr}, {self.start}{'' if self.length is None else f', {self.length}'})"
+
+
+@dataclass(frozen=True)
+class Replace(Expr):
+    """replace(s, search, replacement) (okapi Replace; FlinkSQLExprMapper.scala:
+    193: child0.regexpReplace(child1, child2) — `search` is a Java regex)."""
+    expr: Expr
+    search: Expr
+    replacement: Expr
+
+    def __str__(self):
+        return f"replace({self.expr}, {self.search}, {self.replacement})"
+
+
+def java_long_str(v):
+    """Long.toString."""
+    return str(int(v))
+
+
+def java_double_str(d):
+    """Double.toString: the shortest digits that round-trip, decimal notation for
+    1e-3 <= |d| < 1e7 (at least one fractional digit), else d.dddE<exp>."""
+    import math
+    if math.isnan(d):
+        return "NaN"
+    if math.isinf(d):
+        return "Infinity" if d > 0 else "-Infinity"
+    if d == 0:
+        return "-0.0" if math.copysign(1.0, d) < 0 else "0.0"
+    sign = "-" if d < 0 else ""
+    digits, exp = _shortest_digits(abs(d))  # value = 0.d1d2… × 10^exp
+    if 1e-3 <= abs(d) < 1e7:
+        if exp <= 0:
+            txt = "0." + "0" * (-exp) + digits
+        elif exp >= len(digits):
+            txt = digits + "0" * (exp - len(digits)) + ".0"
+        else:
+            txt = digits[:exp] + "." + digits[exp:]
+        return sign + txt
+    mant = digits[0] + "." + (digits[1:] or "0")
+    return f"{sign}{mant}E{exp - 1}"
+
+
+def _shortest_digits(a):
+    r = repr(a)  # shortest round-trip (as the JDK's since 19)
+    if "e" in r or "E" in r:
+        m, e = r.lower().split("e")
+        e = int(e)
+    else:
+        m, e = r, 0
+    if "." in m:
+        ip, fp = m.split(".")
+    else:
+        ip, fp = m, ""
+    ds = (ip + fp).lstrip("0")
+    lead = len(ip.lstrip("0")) if ip.strip("0") else -(len(fp) - len(fp.lstrip("0")))
+    ds = ds.rstrip("0") or "0"
+    return ds, lead + e
+
+
+def cypher_to_string(v):
+    """A literal cast to STRING (Flink CAST(x AS VARCHAR))."""
+    if v is None:
+        return None
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, int):
+        return java_long_str(v)
+    if isinstance(v, float):
+        return java_double_str(v)
+    return v
+
+
+def _utf16(sv):
+    return sv.encode("utf-16-le", "surrogatepass")
+
+
+def _from_utf16(b):
+    return b.decode("utf-16-le", "surrogatepass")
+
+
+def string_fn(key, sv):
+    """The string function `key` (a tuple: name, literal args) of the string sv,
+    with the JVM semantics Flink's lowering gives it (None: NULL)."""
+    import re
+    name = key[0]
+    if name == "upper":
+        return sv.upper()
+    if name == "lower":
+        return sv.lower()
+    if name in ("trim", "ltrim", "rtrim"):  # SQL TRIM of ' ' (not all whitespace)
+        return sv.strip(" ") if name == "trim" else sv.lstrip(" ") if name == "ltrim" else sv.rstrip(" ")
+    if name == "substring":  # Calcite SqlFunctions.substring(s, from, for), UTF-16 units
+        u = _utf16(sv)
+        lc = len(u) // 2
+        frm, ln = key[1], key[2]
+        if frm < 0:
+            frm += lc + 1
+        e = frm + ln
+        if frm > lc or e < 1:
+            return ""
+        s1, e1 = max(frm, 1), min(e, lc + 1)
+        return _from_utf16(u[2 * (s1 - 1):2 * (e1 - 1)])
+    if name == "replace":  # REGEXP_REPLACE(s, regex, replacement)
+        return re.sub(key[1], lambda m: key[2], sv)
+    if name == "concat_r":  # s + literal
+        return sv + key[1]
+    if name == "concat_l":  # literal + s
+        return key[1] + sv
+    raise ValueError(f"unknown string function {key}")
+
+
+_STR_FUNCS = {"ToUpper": "upper", "ToLower": "lower", "Trim": "trim", "LTrim": "ltrim", "RTrim": "rtrim"}
+
+
 Id = _unary("Id", "id({})")            # FlinkSQLExprMapper.scala:134: the element's id column
 Exists = _unary("Exists", "exists({})")  # exists(n.prop) → IS NOT NULL (:90)
 Size = _unary("Size", "size({})")      # charLength / cardinality (:80-85)
@@ -583,7 +719,7 @@ class _ParamsView:
         return v
 
 
-def _lookups_hold(log, header, columns, params, intern, coltype, lset=None):
+def _lookups_hold(log, header, columns, params, intern, coltype, lset=None, smap=None):
     params = params or {}
     for kind, k, v in log:
         if kind == 0:
@@ -602,12 +738,15 @@ def _lookups_hold(log, header, columns, params, intern, coltype, lset=None):
         elif kind == 5:
             if lset is None or lset(k) != v:
                 return False
+        elif kind == 6:
+            if smap is None or smap(k) != v:
+                return False
         elif intern is None or intern(k) != v:
             return False
     return True
 
 
-def compile_program(expr, header, columns, params=None, intern=None, coltype=None, lset=None):
+def compile_program(expr, header, columns, params=None, intern=None, coltype=None, lset=None, smap=None):
     """Lower `expr` to (ops, iargs, fargs, names) for the C-ABI — memoised per
     expression: a program is reused when every lookup its compilation made
     (header columns, column presence and types, parameters, string codes)
@@ -616,13 +755,13 @@ def compile_program(expr, header, columns, params=None, intern=None, coltype=Non
     try:
         key = _memo_key(expr)
     except AttributeError:  # not an Expr instance: compile every time
-        return _compile_program(expr, header, columns, params, intern, coltype, lset)
+        return _compile_program(expr, header, columns, params, intern, coltype, lset, smap)
     ent = _PROGRAM_MEMO.get(key)
     if ent is not None and header is not None and ent[0] is not None and \
-            _lookups_hold(ent[0], header, columns, params, intern, coltype, lset):
+            _lookups_hold(ent[0], header, columns, params, intern, coltype, lset, smap):
         return ent[1]
     if header is None:
-        return _compile_program(expr, header, columns, params, intern, coltype, lset)
+        return _compile_program(expr, header, columns, params, intern, coltype, lset, smap)
     rec = _Lookups(header, columns, params, intern, coltype)
 
     def rec_type(c):
@@ -640,10 +779,16 @@ def compile_program(expr, header, columns, params=None, intern=None, coltype=Non
         rec.log.append((5, vals, v))
         return v
 
+    def rec_smap(k):
+        v = smap(k)
+        rec.log.append((6, k, v))
+        return v
+
     prog = _compile_program(expr, rec, _ColumnsView(rec), _ParamsView(rec),
                             rec_intern if intern is not None else None,
                             rec_type if coltype is not None else None,
-                            rec_lset if lset is not None else None)
+                            rec_lset if lset is not None else None,
+                            rec_smap if smap is not None else None)
     prog = (tuple(prog[0]), tuple(prog[1]), tuple(prog[2]), tuple(prog[3]))
     if rec.cacheable:
         if len(_PROGRAM_MEMO) >= 4096:
@@ -652,7 +797,7 @@ def compile_program(expr, header, columns, params=None, intern=None, coltype=Non
     return prog
 
 
-def _compile_program(expr, header, columns, params=None, intern=None, coltype=None, lset=None):
+def _compile_program(expr, header, columns, params=None, intern=None, coltype=None, lset=None, smap=None):
     """Lower `expr` to (ops, iargs, fargs, names) for the C-ABI.
 
     header: dict Expr -> physical column; columns: set of the table's columns;
@@ -716,7 +861,40 @@ def _compile_program(expr, header, columns, params=None, intern=None, coltype=No
             return T_INT
         if isinstance(e, ToBoolean):
             return T_BOOL
+        if type(e).__name__ in _STR_FUNCS or isinstance(e, (Substring, Replace, ToString)):
+            return T_STRING
+        if type(e).__name__ == "Add":
+            ta, tb = static_type(e.lhs), static_type(e.rhs)
+            if T_STRING in (ta, tb):
+                return T_STRING
         return None
+
+    def literal_value(x):
+        """(True, value) of a literal / parameter operand, else (False, None)."""
+        if isinstance(x, (IntegerLit, FloatLit, StringLit, BoolLit)):
+            return True, x.v
+        if isinstance(x, NullLit):
+            return True, None
+        if isinstance(x, Param):
+            return True, (params or {}).get(x.pname)
+        return False, None
+
+    def string_map(x, key):
+        """f(x) for a STRING operand x: folded for a literal, else a code map."""
+        isl, v = literal_value(x)
+        if isl:
+            if v is not None and not isinstance(v, str):
+                not_impl(x)
+            lit(None if v is None else string_fn(key, v))
+            return
+        t = static_type(x)
+        if t == T_NULL:
+            emit(OP_LIT_NULL, T_STRING)
+            return
+        if t != T_STRING or smap is None:
+            not_impl(x)
+        go(x)
+        emit(OP_STR_MAP, name_of(smap(key)))
 
     def not_impl(what):
         from ._lib import NotImplementedException
@@ -748,10 +926,74 @@ def _compile_program(expr, header, columns, params=None, intern=None, coltype=No
             emit(OP_LIT_NULL, CT_TO_CAPF.get(e.ctype, T_NULL))
         elif isinstance(e, Param):
             lit(params[e.pname])
+        elif cls == "Add" and T_STRING in (static_type(e.lhs), static_type(e.rhs)):
+            # string concatenation (:120-128): concat with the other side cast to
+            # STRING; on the GPU one side must be a literal (a code map of the other)
+            la, va = literal_value(e.lhs)
+            lb, vb = literal_value(e.rhs)
+            if la and lb:
+                lit(None if va is None or vb is None else cypher_to_string(va) + cypher_to_string(vb))
+            elif lb:
+                if vb is None:
+                    emit(OP_LIT_NULL, T_STRING)
+                else:
+                    string_map(e.lhs, ("concat_r", cypher_to_string(vb)))
+            elif la:
+                if va is None:
+                    emit(OP_LIT_NULL, T_STRING)
+                else:
+                    string_map(e.rhs, ("concat_l", cypher_to_string(va)))
+            else:
+                not_impl(e)  # two string columns: a new string per row pair
         elif cls in _BIN_OPS:
             go(e.lhs)
             go(e.rhs)
             emit(_BIN_OPS[cls])
+        elif cls in _STR_FUNCS:
+            string_map(e.expr, (_STR_FUNCS[cls],))
+        elif isinstance(e, Substring):
+            ok1, st = literal_value(e.start)
+            ok2, ln = literal_value(e.length) if e.length is not None else (True, 1)
+            if not (ok1 and ok2) or any(isinstance(v, bool) or not isinstance(v, (int, type(None))) for v in (st, ln)):
+                not_impl(e)
+            if st is None or ln is None:
+                emit(OP_LIT_NULL, T_STRING)
+            elif ln < 0:
+                from ._lib import IllegalArgumentException
+                raise IllegalArgumentException(f"negative substring length {ln}")
+            else:
+                string_map(e.expr, ("substring", int(st) + 1, int(ln)))
+        elif isinstance(e, Replace):
+            ok1, se = literal_value(e.search)
+            ok2, rp = literal_value(e.replacement)
+            if not (ok1 and ok2) or not all(isinstance(v, (str, type(None))) for v in (se, rp)):
+                not_impl(e)
+            if se is None or rp is None:
+                emit(OP_LIT_NULL, T_STRING)
+            elif "$" in rp or "\\" in rp:
+                not_impl(e)  # Java regex replacement groups
+            else:
+                string_map(e.expr, ("replace", se, rp))
+        elif isinstance(e, ToString):  # cast to STRING (:184)
+            isl, v = literal_value(e.expr)
+            t = static_type(e.expr)
+            if isl:
+                lit(cypher_to_string(v))
+            elif t == T_STRING:
+                go(e.expr)
+            elif t == T_NULL:
+                emit(OP_LIT_NULL, T_STRING)
+            elif t == T_BOOL:  # NULL ← IF(NOT x, 'false', ·) ← IF(x, 'true', ·)
+                emit(OP_LIT_NULL, T_STRING)
+                go(e.expr)
+                emit(OP_NOT)
+                lit("false")
+                emit(OP_IF)
+                go(e.expr)
+                lit("true")
+                emit(OP_IF)
+            else:
+                not_impl(e)  # INTEGER / FLOAT columns: a new string per value
         elif cls in _UN_OPS:
             go(e.expr)
             emit(_UN_OPS[cls])

@@ -37,6 +37,7 @@ class GpuSession:
         self._strings = {}
         self._codes = {}
         self._sets = {}
+        self._maps = {}
 
     def literal_set(self, values):
         """Program name of the session literal set of `values` (int64 values
@@ -48,6 +49,29 @@ class GpuSession:
             sid = c_int32()
             _lib.call("capf_session_literal_set", self._h, arr, len(key), byref(sid))
             nm = self._sets[key] = "\x01set:%d" % sid.value
+        return nm
+
+    def string_map(self, key):
+        """Program name of the session code map of string function `key`
+        (expr.string_fn) for CAPF_OP_STR_MAP: "\x01map:<id>".  The function runs
+        on the host over every dictionary string (results interned); a map is
+        extended and re-registered when the dictionary has grown since."""
+        from .expr import string_fn
+        cnt, dig = c_int64(), c_uint64()
+        _lib.call("capf_string_digest", self._h, byref(cnt), byref(dig))
+        n = cnt.value
+        ent = self._maps.get(key)
+        if ent is not None and ent[0] >= n:
+            return ent[2]
+        codes = list(ent[1]) if ent is not None else []
+        for c in range(len(codes), n):
+            r = string_fn(key, self.lookup(c))
+            codes.append(-1 if r is None else self.intern(r))
+        arr = (c_int64 * max(len(codes), 1))(*codes)
+        mid = c_int32()
+        _lib.call("capf_session_code_map", self._h, arr, len(codes), byref(mid))
+        nm = "\x01map:%d" % mid.value
+        self._maps[key] = (n, codes, nm)
         return nm
 
     @classmethod
@@ -223,7 +247,8 @@ _SELECT_ARGS = {}
 
 def _program(expr, header, table, params):
     return compile_program(expr, header, set(table.physicalColumns), params, table.session.intern,
-                           table.capf_type, getattr(table.session, "literal_set", None))
+                           table.capf_type, getattr(table.session, "literal_set", None),
+                           getattr(table.session, "string_map", None))
 
 
 class GpuTable:

@@ -194,7 +194,15 @@ enum {
    * session literal set names[i] (capf_session_literal_set, referenced as
    * "\x01set:<id>"), else NULL when x is NULL or farg != 0 (the list held a
    * NULL), else FALSE.  One binary search per row over the sorted set.       */
-  CAPF_OP_IN_SET = 89
+  CAPF_OP_IN_SET = 89,
+  /* String functions of one STRING operand and literal arguments (toUpper /
+   * toLower / trim / lTrim / rTrim / substring / replace / concatenation with
+   * a literal, FlinkSQLExprMapper.scala:120-128, 187-195): pops a STRING code
+   * c; pushes entry c of the code map names[iarg] — the function applied to
+   * dictionary string c by the caller and interned (capf_session_code_map,
+   * referenced as "\x01map:<id>"); NULL in, an entry < 0 (a NULL result) or
+   * c past the map → NULL.                                                   */
+  CAPF_OP_STR_MAP = 90
 };
 
 typedef struct capf_expr {
@@ -599,6 +607,11 @@ capf_status capf_session_copy(capf_session *s, void *dst, const void *src, int64
  * the session; *set_id names it in programs as "\x01set:<set_id>".  The same
  * values registered again return the same id. */
 capf_status capf_session_literal_set(capf_session *s, const int64_t *values, int64_t n, int32_t *set_id);
+/* A code map of CAPF_OP_STR_MAP: codes[c] = the STRING code the function gives
+ * dictionary string c (−1: NULL), for c < n.  The caller (the shim) applies the
+ * function on the host with the JVM's string semantics and interns the
+ * results; the map is referenced in programs as "\x01map:<id>" (*map_id).  */
+capf_status capf_session_code_map(capf_session *s, const int64_t *codes, int64_t n, int32_t *map_id);
 
 #ifdef __cplusplus
 }

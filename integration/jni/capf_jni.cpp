@@ -779,6 +779,13 @@ JNI(jint, sessionLiteralSet)(JNIEnv *env, jobject, jlong s, jlongArray values) {
   if (fail(env, capf_session_literal_set(S(s), v.data(), (int64_t)v.size(), &id))) return -1;
   return id;
 }
+// a code map of CAPF_OP_STR_MAP (codes[c] = the function's result code for string c): its id
+JNI(jint, sessionCodeMap)(JNIEnv *env, jobject, jlong s, jlongArray codes) {
+  const std::vector<int64_t> v = longs(env, codes);
+  int32_t id = -1;
+  if (fail(env, capf_session_code_map(S(s), v.data(), (int64_t)v.size(), &id))) return -1;
+  return id;
+}
 // device → device
 JNI(void, sessionCopyDevice)(JNIEnv *env, jobject, jlong s, jlong dst, jlong src, jlong bytes) {
   fail(env, capf_session_copy(S(s), reinterpret_cast<void *>(dst), reinterpret_cast<const void *>(src), bytes, 3));

@@ -55,6 +55,28 @@ final class GpuCypherSession private (val device: Int, hipStream: Long)
     sets.getOrElseUpdate(key, "\u0001set:" + Native.sessionLiteralSet(handle, key.toArray))
   }
 
+  private val maps = scala.collection.mutable.HashMap.empty[Seq[Any], (Long, Array[Long], String)]
+
+  /** Program name of the session code map of string function `key` (CAPF_OP_STR_MAP,
+    * GpuStringFunctions.apply): the function applied to every dictionary string
+    * with the JVM's own String semantics, the results interned; extended and
+    * re-registered when the dictionary has grown since (the shim's twin of
+    * table.py GpuSession.string_map). */
+  def stringMap(key: Seq[Any]): String = maps.synchronized {
+    val n = { val d = new Array[Long](2); Native.guard(Native.stringDigest(handle, d)); d(0) }
+    maps.get(key) match {
+      case Some((m, _, name)) if m >= n => name
+      case prev =>
+        val old = prev.map(_._2).getOrElse(Array.empty[Long])
+        val codes = old ++ (old.length.toLong until n).map { c =>
+          GpuStringFunctions(key, Native.stringLookup(handle, c)).map(intern).getOrElse(-1L)
+        }
+        val name = "\u0001map:" + Native.sessionCodeMap(handle, codes)
+        maps.update(key, (n, codes, name))
+        name
+    }
+  }
+
   // ------------------------------------------------------------ table sources
   /** The one-row, zero-column table (RelationalCypherRecordsFactory.unit). */
   def unitTable(): GpuTable = GpuTable(Native.guard(Native.tableUnit(handle)))

@@ -38,7 +38,7 @@ object GpuExprMapper {
   private final val Sin_ = 79; private final val Cos_ = 80; private final val Tan_ = 81
   private final val Asin_ = 82; private final val Acos_ = 83; private final val Atan_ = 84
   private final val Degrees_ = 85; private final val Radians_ = 86; private final val Atan2_ = 87
-  private final val ToBoolean_ = 88; private final val InSet = 89
+  private final val ToBoolean_ = 88; private final val InSet = 89; private final val StrMap = 90
   private final val InSetMin = 17  // IN lists from this length: one set lookup per row (expr.py IN_SET_MIN)
 
   def program(expr: Expr, header: RecordHeader, table: GpuTable, parameters: CypherMap): Program = {
@@ -97,6 +97,29 @@ object GpuExprMapper {
 
     def physical(e: Expr): Option[String] =
       if (header.contains(e)) Some(header.column(e)).filter(columns.contains) else None
+
+    // the value of a literal / parameter operand
+    def literal(e: Expr): Option[CypherValue] = e match {
+      case IntegerLit(v) => Some(CypherInteger(v))
+      case FloatLit(v) => Some(CypherFloat(v))
+      case StringLit(v) => Some(CypherString(v))
+      case TrueLit => Some(CypherBoolean(true))
+      case FalseLit => Some(CypherBoolean(false))
+      case NullLit(_) => Some(CypherNull)
+      case Param(p) => Some(parameters(p))
+      case _ => None
+    }
+
+    def isString(e: Expr): Boolean = e.cypherType.material == CTString
+
+    // f(x) of a STRING operand: folded for a literal, else a code map (CAPF_OP_STR_MAP)
+    def stringMap(x: Expr, key: Seq[Any]): Unit = literal(x) match {
+      case Some(CypherNull) => emit(LitNull, Native.TypeString)
+      case Some(CypherString(v)) => lit(GpuStringFunctions(key, v).map(CypherString(_)).getOrElse(CypherNull))
+      case Some(other) => throw NotImplementedException(s"GPU string function of $other")
+      case None if x.cypherType.material == CTNull => emit(LitNull, Native.TypeString)
+      case None => go(x); emit(StrMap, nameIndex(session.stringMap(key)))
+    }
 
     def go(e: Expr): Unit = e match {
       case _: Var | _: HasLabel | _: HasType | _: StartNode | _: EndNode | _: ElementProperty =>
@@ -205,6 +228,45 @@ object GpuExprMapper {
       case Radians(x) => go(x); emit(Radians_)
       case Sin(x) => go(x); emit(Sin_)
       case Tan(x) => go(x); emit(Tan_)
+      case Add(l, r) if isString(l) || isString(r) =>                    // concat (:120-128)
+        (literal(l), literal(r)) match {
+          case (Some(a), Some(b)) => lit(if (a == CypherNull || b == CypherNull) CypherNull
+                                         else CypherString(GpuStringFunctions.cast(a) + GpuStringFunctions.cast(b)))
+          case (_, Some(CypherNull)) | (Some(CypherNull), _) => emit(LitNull, Native.TypeString)
+          case (None, Some(b)) => stringMap(l, Seq("concat_r", GpuStringFunctions.cast(b)))
+          case (Some(a), None) => stringMap(r, Seq("concat_l", GpuStringFunctions.cast(a)))
+          case _ => throw NotImplementedException(s"GPU concatenation of two string columns $e")
+        }
+      case ToUpper(x) => stringMap(x, Seq("upper"))                       // :190
+      case ToLower(x) => stringMap(x, Seq("lower"))                       // :191
+      case Trim(x) => stringMap(x, Seq("trim"))                           // :187
+      case LTrim(x) => stringMap(x, Seq("ltrim"))                         // :188
+      case RTrim(x) => stringMap(x, Seq("rtrim"))                         // :189
+      case Substring(x, start, len) =>                                    // :195 (length 1 when absent)
+        (literal(start), len.map(literal).getOrElse(Some(CypherInteger(1L)))) match {
+          case (Some(CypherInteger(s)), Some(CypherInteger(n))) if n >= 0 => stringMap(x, Seq("substring", s + 1, n))
+          case (Some(CypherNull), _) | (_, Some(CypherNull)) => emit(LitNull, Native.TypeString)
+          case _ => throw NotImplementedException(s"GPU substring $e")
+        }
+      case Replace(x, search, repl) =>                                    // :193 (a Java regex)
+        (literal(search), literal(repl)) match {
+          case (Some(CypherString(a)), Some(CypherString(b))) if !b.contains("$") && !b.contains("\\") =>
+            stringMap(x, Seq("replace", a, b))
+          case (Some(CypherNull), _) | (_, Some(CypherNull)) => emit(LitNull, Native.TypeString)
+          case _ => throw NotImplementedException(s"GPU replace $e")
+        }
+      case ToString(x) =>                                                 // :184
+        literal(x) match {
+          case Some(v) => lit(if (v == CypherNull) CypherNull else CypherString(GpuStringFunctions.cast(v)))
+          case None => x.cypherType.material match {
+            case CTString => go(x)
+            case CTBoolean =>                                             // NULL ← If(¬x, 'false') ← If(x, 'true')
+              emit(LitNull, Native.TypeString); go(x); emit(Not_); emit(LitString, session.intern("false")); emit(If_)
+              go(x); emit(LitString, session.intern("true")); emit(If_)
+            case CTNull | CTVoid => emit(LitNull, Native.TypeString)
+            case _ => throw NotImplementedException(s"GPU toString of a ${x.cypherType} column")
+          }
+        }
       case c: CaseExpr if c.alternatives.nonEmpty =>                      // :242-260, Ifs innermost first
         c.default match {
           case Some(d) => go(d)

@@ -201,4 +201,5 @@ object Native {
   @native def sessionCopy(session: Long, d: Long, host: ByteBuffer, bytes: Long, kind: Int): Unit
   @native def sessionCopyDevice(session: Long, dst: Long, src: Long, bytes: Long): Unit
   @native def sessionLiteralSet(session: Long, values: Array[Long]): Int
+  @native def sessionCodeMap(session: Long, codes: Array[Long]): Int
 }

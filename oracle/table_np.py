@@ -29,6 +29,7 @@ Everything materialises with numpy; sizes are the small parity cases.
 import numpy as np
 
 import math
+import re
 from decimal import Decimal, localcontext
 from fractions import Fraction
 
@@ -236,6 +237,14 @@ def evaluate(e, table, header, params):
                    "GreaterThanOrEqual": "ge"}
         if name in cmp_ops:
             return _cmp(go(x.lhs), go(x.rhs), cmp_ops[name])
+        if name == "Add":  # string concatenation (FlinkSQLExprMapper.scala:120-128)
+            a, b = go(x.lhs), go(x.rhs)
+            if T_STRING in (a.t, b.t):
+                if {a.t, b.t} - {T_STRING, T_INT, T_FLOAT, T_NULL}:
+                    raise NotImplementedError(f"oracle: {x}")
+                out = np.array([_jstr(u, a.t) + _jstr(v, b.t) if oa and ob else None
+                                for u, v, oa, ob in zip(a.v, b.v, a.ok, b.ok)], dtype=object)
+                return Val(T_STRING, out, a.ok & b.ok)
         ar_ops = {"Add": "add", "Subtract": "sub", "Multiply": "mul", "Divide": "div", "Modulo": "mod"}
         if name in ar_ops:
             return _arith(go(x.lhs), go(x.rhs), ar_ops[name])
@@ -361,6 +370,32 @@ def evaluate(e, table, header, params):
             parsed = [(str(v).strip().lower() if ok else None) for v, ok in zip(a.v, a.ok)]
             return Val(T_BOOL, np.array([p == "true" for p in parsed], bool),
                        np.array([p in ("true", "false") for p in parsed], bool))
+        if name in _STR1 or name in ("Substring", "Replace"):  # (:187-195)
+            a = go(x.expr)
+            if a.t == T_NULL:
+                return const(T_STRING, None, False)
+            if a.t != T_STRING:
+                raise NotImplementedError(f"oracle: {name} of {CAPF_TO_CT[a.t]}")
+            if name == "Substring":
+                st = go(x.start)
+                ln = go(x.length) if x.length is not None else const(T_INT, 1)  # (:195: default 1)
+                args = [(int(u), int(w), ou and ow) for u, w, ou, ow in zip(st.v, ln.v, st.ok, ln.ok)]
+                out = [_substring(v, u + 1, w) if ok and aok else None for v, aok, (u, w, ok) in zip(a.v, a.ok, args)]
+            elif name == "Replace":
+                se, rp = go(x.search), go(x.replacement)
+                out = [re.sub(p1, lambda m, r=p2: r, v) if ok and o1 and o2 else None
+                       for v, ok, p1, p2, o1, o2 in zip(a.v, a.ok, se.v, rp.v, se.ok, rp.ok)]
+            else:
+                f = _STR1[name]
+                out = [f(v) if ok else None for v, ok in zip(a.v, a.ok)]
+            ok = np.array([v is not None for v in out], bool)
+            return Val(T_STRING, np.array(out, dtype=object), ok)
+        if name == "ToString":  # cast to STRING (:184)
+            a = go(x.expr)
+            if a.t == T_NULL:
+                return const(T_STRING, None, False)
+            out = np.array([_jstr(v, a.t) if ok else None for v, ok in zip(a.v, a.ok)], dtype=object)
+            return Val(T_STRING, out, a.ok.copy())
         if isinstance(x, CaseExpr):  # If(p1, v1, If(p2, v2, … default)) (:242-260)
             acc = go(x.default) if x.default is not None else const(T_INT, None, False)
             for p, v in reversed(x.alternatives):
@@ -402,6 +437,59 @@ def evaluate(e, table, header, params):
         raise NotImplementedError(f"oracle: unsupported expression {x}")
 
     return go(e)
+
+
+# Flink's string functions as the JVM runs them (FlinkSQLExprMapper.scala:187-191):
+# upperCase / lowerCase, SQL TRIM of the space character
+_STR1 = {"ToUpper": str.upper, "ToLower": str.lower, "Trim": lambda v: v.strip(" "),
+         "LTrim": lambda v: v.lstrip(" "), "RTrim": lambda v: v.rstrip(" ")}
+
+
+def _substring(v, frm, ln):
+    """Calcite SqlFunctions.substring(s, from, for): 1-based, UTF-16 units."""
+    u = v.encode("utf-16-le", "surrogatepass")
+    n = len(u) // 2
+    if ln < 0:
+        raise ValueError("negative substring length")
+    if frm < 0:
+        frm += n + 1
+    end = frm + ln
+    if frm > n or end < 1:
+        return ""
+    lo, hi = max(frm, 1), min(end, n + 1)
+    return u[2 * (lo - 1):2 * (hi - 1)].decode("utf-16-le", "surrogatepass")
+
+
+def _jstr(v, t):
+    """CAST(v AS VARCHAR) on the JVM: Long.toString, Double.toString, 'true'/'false'."""
+    if t == T_STRING:
+        return v
+    if t == T_BOOL:
+        return "true" if v else "false"
+    if t == T_INT:
+        return str(int(v))
+    if t == T_FLOAT:
+        d = float(v)
+        if d != d:
+            return "NaN"
+        if d in (math.inf, -math.inf):
+            return "Infinity" if d > 0 else "-Infinity"
+        if d == 0:
+            return "-0.0" if math.copysign(1, d) < 0 else "0.0"
+        if 1e-3 <= abs(d) < 1e7:
+            r = repr(d)
+            if "e" in r:  # repr's exponent form inside the decimal range (e.g. 1e-03)
+                r = format(Decimal(r), "f")
+            return r if "." in r else r + ".0"
+        m, e = f"{d:.17e}".split("e")
+        # the shortest round-trip mantissa digits, Java's d.dddE<exp>
+        digits = Decimal(repr(d)).normalize()
+        sign, dg, ex = digits.as_tuple()
+        ds = "".join(map(str, dg))
+        exp10 = len(dg) + ex - 1
+        mant = ds[0] + "." + (ds[1:] or "0")
+        return ("-" if sign else "") + f"{mant}E{exp10}"
+    raise NotImplementedError(f"oracle: toString of {CAPF_TO_CT[t]}")
 
 
 _MATH1 = {"Round", "Abs", "Ceil", "Floor", "Sign", "Sqrt", "Log", "Log10", "Exp", "Sin", "Cos", "Tan", "Asin",

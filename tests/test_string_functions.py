@@ -1,0 +1,122 @@
+"""String functions of the expression mapper (FlinkSQLExprMapper.scala:120-128
+concatenation, :184 toString, :187-195 trim / lTrim / rTrim / toUpper /
+toLower / replace / substring).
+
+On the GPU a function of one STRING operand with literal arguments is a code
+map of the session dictionary (CAPF_OP_STR_MAP: the function applied per
+dictionary string on the host, the results interned, one table lookup per
+row).  The oracle restates the JVM semantics independently
+(oracle/table_np.py).  The Flink test suites hold no case for these functions,
+so parity here is against the oracle's restatement only (parity unpinned by
+reference fixtures).
+"""
+import numpy as np
+import pytest
+
+from capf_amd import _lib
+from capf_amd.expr import (Add, BoolLit, Equals, FloatLit, IntegerLit, LTrim, NullLit, Param, Replace, RTrim,
+                           StringLit, Substring, ToLower, ToString, ToUpper, Trim, Var, T_BOOL, T_FLOAT, T_INT,
+                           T_STRING, java_double_str, string_fn)
+from capf_amd.header import RecordHeader
+from oracle.table_np import OracleSession, _jstr
+
+WORDS = ["alpha", "  Beta ", "GAMMA  ", " delta", "", "straße", "ÉCOLE", "a-b-a", "x\U0001F600yz", None]
+
+
+def _cols(n=400, seed=5):
+    rng = np.random.default_rng(seed)
+    return [("s", T_STRING, [WORDS[i] for i in rng.integers(0, len(WORDS), n)], None),
+            ("t", T_STRING, [WORDS[i] for i in rng.integers(0, len(WORDS), n)], None),
+            ("k", T_INT, [int(x) if rng.random() > 0.1 else None for x in rng.integers(-50, 50, n)], None),
+            ("b", T_BOOL, [bool(x) if rng.random() > 0.1 else None for x in rng.integers(0, 2, n)], None)]
+
+
+H = RecordHeader({Var("s"): "s", Var("t"): "t", Var("k"): "k", Var("b"): "b"})
+
+EXPRS = [
+    ToUpper(Var("s")), ToLower(Var("s")), Trim(Var("s")), LTrim(Var("s")), RTrim(Var("s")),
+    Substring(Var("s"), IntegerLit(1), IntegerLit(3)), Substring(Var("s"), IntegerLit(0)),
+    Substring(Var("s"), IntegerLit(2), IntegerLit(100)), Substring(Var("s"), IntegerLit(-3), IntegerLit(2)),
+    Replace(Var("s"), StringLit("a"), StringLit("<>")), Replace(Var("s"), StringLit("[a-c]"), StringLit("")),
+    Add(Var("s"), StringLit("!")), Add(StringLit(">"), Var("s")), Add(Var("s"), IntegerLit(7)),
+    Add(FloatLit(1.5), Var("s")), Add(Var("s"), NullLit("STRING")),
+    ToUpper(Trim(Var("s"))), Add(ToLower(Var("t")), StringLit("?")),
+    ToString(Var("s")), ToString(Var("b")), ToString(IntegerLit(42)), ToString(FloatLit(1e7)),
+    ToString(BoolLit(False)), ToUpper(StringLit("lit")), ToUpper(NullLit("STRING")),
+    Add(StringLit("a"), IntegerLit(1)), ToUpper(Param("p")),
+]
+
+
+def test_java_double_to_string_known_answers():
+    """Double.toString as the JVM prints it (the cast of a FLOAT to STRING)."""
+    known = [(1.0, "1.0"), (0.001, "0.001"), (1e-4, "1.0E-4"), (1e7, "1.0E7"), (9999999.0, "9999999.0"),
+             (123456.789, "123456.789"), (12345678.9, "1.23456789E7"), (-0.5, "-0.5"), (1e21, "1.0E21"),
+             (1.5e-10, "1.5E-10"), (0.0, "0.0"), (-0.0, "-0.0"), (float("inf"), "Infinity")]
+    for d, want in known:
+        assert java_double_str(d) == want
+        assert _jstr(d, T_FLOAT) == want
+
+
+def test_string_fn_semantics():
+    """Calcite SUBSTRING (1-based, UTF-16 units, clipped), SQL TRIM of ' ' only,
+    REGEXP_REPLACE, concatenation."""
+    assert string_fn(("substring", 1, 3), "alpha") == "alp"
+    assert string_fn(("substring", 3, 100), "alpha") == "pha"
+    assert string_fn(("substring", 9, 2), "alpha") == ""
+    assert string_fn(("substring", -2, 2), "alpha") == "ha"  # from the end (Calcite)
+    assert string_fn(("substring", 2, 2), "x\U0001F600yz") == "\U0001F600"  # a surrogate pair is 2 units
+    assert string_fn(("trim",), "\t a \t") == "\t a \t"  # only the space character
+    assert string_fn(("trim",), "  a  ") == "a"
+    assert string_fn(("replace", "[a-c]", ""), "abcd") == "d"
+    assert string_fn(("concat_l", "x"), "y") == "xy"
+
+
+@pytest.mark.parametrize("e", EXPRS, ids=[str(e) for e in EXPRS])
+def test_oracle_string_functions_run(e):
+    o = OracleSession().table(_cols())
+    rows = o.withColumns((e, "x"), header=H, params={"p": "param"}).rows
+    assert len(rows) == 400
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("e", EXPRS, ids=[str(e) for e in EXPRS])
+def test_string_functions_gpu_parity(gpu_session, e):
+    """withColumns of each function: the GPU column equals the oracle's row by
+    row (NULLs, unicode, empty strings, surrogate pairs)."""
+    cols = _cols()
+    g, o = gpu_session.table(cols), OracleSession().table(cols)
+    rg = g.withColumns((e, "x"), header=H, params={"p": "param"}).rows
+    ro = o.withColumns((e, "x"), header=H, params={"p": "param"}).rows
+    assert [r["x"] for r in rg] == [r["x"] for r in ro]
+
+
+@pytest.mark.gpu
+def test_string_function_in_filter_and_memo(gpu_session):
+    """A string function inside a WHERE, planned twice (the program memo reuses
+    the code map) and again after new strings entered the dictionary (the map
+    is extended)."""
+    cols = _cols()
+    pred = Equals(ToUpper(Trim(Var("s"))), StringLit("BETA"))
+    o = OracleSession().table(cols)
+    want = len(o.filter(pred, H, {}).rows)
+    assert want > 0
+    g = gpu_session.table(cols)
+    assert len(g.filter(pred, H, {}).rows) == want
+    assert len(g.filter(pred, H, {}).rows) == want
+    more = [("s", T_STRING, ["  beta", "zeta", "BeTa  "], None), ("t", T_STRING, ["a", "b", "c"], None),
+            ("k", T_INT, [1, 2, 3], None), ("b", T_BOOL, [True, False, True], None)]
+    g2 = gpu_session.table(more)
+    assert len(g2.filter(pred, H, {}).rows) == 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("e", [Add(Var("s"), Var("t")), ToString(Var("k")), Substring(Var("s"), Var("k")),
+                               Replace(Var("s"), StringLit("a"), StringLit("$1"))],
+                         ids=["concat_columns", "to_string_integer_column", "substring_column_start",
+                              "replace_group_ref"])
+def test_string_shapes_not_on_gpu_raise(gpu_session, e):
+    """Shapes that would build a new string per row (or Java regex replacement
+    groups) raise NotImplementedException instead of running elsewhere."""
+    g = gpu_session.table(_cols())
+    with pytest.raises(_lib.NotImplementedException):
+        g.withColumns((e, "x"), header=H, params={}).rows

@@ -170,14 +170,19 @@ enum Op : int32_t {
   OP_LOG10 = CAPF_OP_LOG10, OP_EXP = CAPF_OP_EXP, OP_SIN = CAPF_OP_SIN, OP_COS = CAPF_OP_COS,
   OP_TAN = CAPF_OP_TAN, OP_ASIN = CAPF_OP_ASIN, OP_ACOS = CAPF_OP_ACOS, OP_ATAN = CAPF_OP_ATAN,
   OP_DEGREES = CAPF_OP_DEGREES, OP_RADIANS = CAPF_OP_RADIANS, OP_ATAN2 = CAPF_OP_ATAN2,
-  OP_TO_BOOLEAN = CAPF_OP_TO_BOOLEAN, OP_IN_SET = CAPF_OP_IN_SET, OP_STR_MAP = CAPF_OP_STR_MAP
+  OP_TO_BOOLEAN = CAPF_OP_TO_BOOLEAN, OP_IN_SET = CAPF_OP_IN_SET, OP_STR_MAP = CAPF_OP_STR_MAP,
+  OP_VALUE_MAP = CAPF_OP_VALUE_MAP
 };
 // a program name that refers to a session literal set ("\x01set:<id>"), not a column
 inline bool is_literal_set_name(const std::string &nm) { return nm.size() > 5 && nm.compare(0, 5, "\x01set:") == 0; }
 // ... or to a session code map of CAPF_OP_STR_MAP ("\x01map:<id>")
 inline bool is_code_map_name(const std::string &nm) { return nm.size() > 5 && nm.compare(0, 5, "\x01map:") == 0; }
-// a program name that is a session table (literal set or code map), not a column
-inline bool is_session_table_name(const std::string &nm) { return is_literal_set_name(nm) || is_code_map_name(nm); }
+// ... or to a session value map of CAPF_OP_VALUE_MAP ("\x01vmap:<id>")
+inline bool is_value_map_name(const std::string &nm) { return nm.size() > 6 && nm.compare(0, 6, "\x01vmap:") == 0; }
+// a program name that is a session table (literal set, code or value map), not a column
+inline bool is_session_table_name(const std::string &nm) {
+  return is_literal_set_name(nm) || is_code_map_name(nm) || is_value_map_name(nm);
+}
 // unary math opcodes (one operand, one result)
 inline bool is_math1(int32_t op) { return op >= OP_ROUND && op <= OP_RADIANS; }
 
@@ -351,6 +356,14 @@ struct Session {
   std::vector<std::pair<std::shared_ptr<DevBuf>, int64_t>> literal_sets;
   // code maps of CAPF_OP_STR_MAP: int64 STRING code per dictionary code (−1 NULL)
   std::vector<std::pair<std::shared_ptr<DevBuf>, int64_t>> code_maps;
+  // value maps of CAPF_OP_VALUE_MAP: [keys n][keys2 n (pairs)][codes n] on the
+  // device, n, pair flag
+  struct ValueMap {
+    std::shared_ptr<DevBuf> buf;
+    int64_t n;
+    bool pairs;
+  };
+  std::vector<ValueMap> value_maps;
   std::map<std::vector<int64_t>, int32_t> literal_set_ids;
   std::vector<PendingTiming> pending;   // recorded, not yet resolved
   std::vector<hipEvent_t> event_pool;

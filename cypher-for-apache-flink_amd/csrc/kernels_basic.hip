@@ -1074,6 +1074,26 @@ __device__ Val run_program(const Instr *code, int ncode, const ColView *cols, in
         st[sp++] = hit ? mkb(true) : in.f != 0.0 ? mknull(CAPF_TYPE_BOOL) : mkb(false);
         break;
       }
+      case OP_VALUE_MAP: {  // cols[in.i]: [keys][keys2 (enc = 1)][codes], base = n
+        Val y = in.f != 0.0 ? st[--sp] : Val{};
+        Val a = st[--sp];
+        const ColView &m = cols[in.i];
+        const int64_t n = m.base;
+        const int64_t *k1 = (const int64_t *)m.data, *k2 = k1 + n, *cd = k1 + (m.enc ? 2 : 1) * n;
+        int64_t r = -1;
+        if (!a.nul && !(in.f != 0.0 && y.nul)) {
+          int64_t lo = 0, hi = n;
+          while (lo < hi) {  // first entry ≥ (a, y)
+            const int64_t mid = (lo + hi) >> 1;
+            const bool less = k1[mid] < a.b || (m.enc && k1[mid] == a.b && k2[mid] < y.b);
+            if (less) lo = mid + 1;
+            else hi = mid;
+          }
+          if (lo < n && k1[lo] == a.b && (!m.enc || k2[lo] == y.b)) r = cd[lo];
+        }
+        st[sp++] = r < 0 ? mknull(CAPF_TYPE_STRING) : mk(r, CAPF_TYPE_STRING, 0);
+        break;
+      }
       case OP_STR_MAP: {  // cols[in.i] = a code map (base = its length)
         Val a = st[--sp];
         const int64_t c = a.nul ? -1 : a.b;
@@ -1151,6 +1171,14 @@ static DeviceProgram upload_program(Session *s, const Program &p,
       views.push_back(ColView{ls.first->p, nullptr, (int32_t)Type::Int64, ENC_PLAIN, ls.second});
       continue;
     }
+    if (is_value_map_name(nm)) {  // [keys][keys2][codes], n in `base`, pairs in `enc`
+      const long id = atol(nm.c_str() + 6);
+      std::lock_guard<std::mutex> g(s->user_mu);
+      if (id < 0 || (size_t)id >= s->value_maps.size()) illegal("unknown value map '" + nm.substr(1) + "'");
+      const auto &vm = s->value_maps[(size_t)id];
+      views.push_back(ColView{vm.buf->p, nullptr, (int32_t)Type::Int64, vm.pairs ? 1 : 0, vm.n});
+      continue;
+    }
     if (is_code_map_name(nm)) {  // code → code table, its length in `base`
       const long id = atol(nm.c_str() + 5);
       std::lock_guard<std::mutex> g(s->user_mu);
@@ -1207,6 +1235,7 @@ static DeviceProgram upload_program(Session *s, const Program &p,
       case OP_NOT: case OP_IS_NULL: case OP_IS_NOT_NULL: case OP_NEG: case OP_TO_FLOAT:
       case OP_TO_INTEGER: case OP_STR_LEN: case OP_TO_BOOLEAN: case OP_IN_SET: case OP_STR_MAP: break;
       case OP_IF: depth -= 2; break;
+      case OP_VALUE_MAP: depth -= in.f != 0.0 ? 1 : 0; break;
       default:
         if (!is_math1(in.op)) depth -= 1;  // binary operators; unary math keeps the depth
         break;

@@ -317,6 +317,14 @@ Type infer_type(const Program &p, const std::vector<std::string> &names,
         st.push_back(Type::Int64);
         break;
       }
+      case OP_VALUE_MAP: {
+        if (in.i < 0 || (size_t)in.i >= p.names.size() || !is_value_map_name(p.names[in.i]))
+          illegal("malformed expression program (value map)");
+        pop();
+        if (in.f != 0.0) pop();
+        st.push_back(Type::String);
+        break;
+      }
       case OP_STR_MAP: {
         if (in.i < 0 || (size_t)in.i >= p.names.size() || !is_code_map_name(p.names[in.i]))
           illegal("malformed expression program (code map)");
@@ -845,6 +853,30 @@ capf_status capf_session_copy(capf_session *cs, void *dst, const void *src, int6
   const hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
   HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)bytes, k, cs->impl.stream));
   cs->impl.sync();
+  CAPF_API_END
+}
+
+capf_status capf_session_value_map(capf_session *cs, const int64_t *keys, const int64_t *keys2,
+                                   const int64_t *codes, int64_t n, int32_t *map_id) {
+  CAPF_API_BEGIN
+  need(cs, "session");
+  need(map_id, "map_id");
+  if (n < 0 || (n > 0 && (!keys || !codes))) illegal("bad value map");
+  for (int64_t i = 1; i < n; ++i)
+    if (keys[i - 1] > keys[i] || (keys[i - 1] == keys[i] && (!keys2 || keys2[i - 1] >= keys2[i])))
+      illegal("value map keys must be sorted and unique");
+  const int64_t k = keys2 ? 3 : 2;
+  std::vector<int64_t> h((size_t)(k * std::max<int64_t>(n, 1)), 0);
+  std::copy(keys, keys + n, h.begin());
+  if (keys2) std::copy(keys2, keys2 + n, h.begin() + n);
+  std::copy(codes, codes + n, h.begin() + (k - 1) * n);
+  Session &s = cs->impl;
+  BufPtr b = s.alloc(8 * h.size());
+  HIP_CHECK(hipMemcpyAsync(b->p, h.data(), 8 * h.size(), hipMemcpyHostToDevice, s.stream));
+  s.sync();  // (pageable source)
+  std::lock_guard<std::mutex> g(s.user_mu);
+  *map_id = (int32_t)s.value_maps.size();
+  s.value_maps.push_back(Session::ValueMap{b, n, keys2 != nullptr});
   CAPF_API_END
 }
 

@@ -36,7 +36,7 @@ OP_TO_FLOAT, OP_TO_INTEGER, OP_COALESCE = 40, 41, 50
 OP_STR_LEN, OP_LIST_SIZE, OP_IF = 60, 61, 62
 OP_ROUND, OP_ABS, OP_CEIL, OP_FLOOR, OP_SIGN, OP_SQRT, OP_LOG, OP_LOG10, OP_EXP = 70, 71, 72, 73, 74, 75, 76, 77, 78
 OP_SIN, OP_COS, OP_TAN, OP_ASIN, OP_ACOS, OP_ATAN, OP_DEGREES, OP_RADIANS = 79, 80, 81, 82, 83, 84, 85, 86
-OP_ATAN2, OP_TO_BOOLEAN, OP_IN_SET, OP_STR_MAP = 87, 88, 89, 90
+OP_ATAN2, OP_TO_BOOLEAN, OP_IN_SET, OP_STR_MAP, OP_VALUE_MAP = 87, 88, 89, 90, 91
 IN_SET_MIN = 17  # list length from which IN runs as a session-set lookup (shorter: an OR of equalities)
 
 # aggregators
@@ -746,7 +746,8 @@ def _lookups_hold(log, header, columns, params, intern, coltype, lset=None, smap
     return True
 
 
-def compile_program(expr, header, columns, params=None, intern=None, coltype=None, lset=None, smap=None):
+def compile_program(expr, header, columns, params=None, intern=None, coltype=None, lset=None, smap=None,
+                    vmap=None):
     """Lower `expr` to (ops, iargs, fargs, names) for the C-ABI — memoised per
     expression: a program is reused when every lookup its compilation made
     (header columns, column presence and types, parameters, string codes)
@@ -755,13 +756,13 @@ def compile_program(expr, header, columns, params=None, intern=None, coltype=Non
     try:
         key = _memo_key(expr)
     except AttributeError:  # not an Expr instance: compile every time
-        return _compile_program(expr, header, columns, params, intern, coltype, lset, smap)
+        return _compile_program(expr, header, columns, params, intern, coltype, lset, smap, vmap)
     ent = _PROGRAM_MEMO.get(key)
     if ent is not None and header is not None and ent[0] is not None and \
             _lookups_hold(ent[0], header, columns, params, intern, coltype, lset, smap):
         return ent[1]
     if header is None:
-        return _compile_program(expr, header, columns, params, intern, coltype, lset, smap)
+        return _compile_program(expr, header, columns, params, intern, coltype, lset, smap, vmap)
     rec = _Lookups(header, columns, params, intern, coltype)
 
     def rec_type(c):
@@ -784,11 +785,16 @@ def compile_program(expr, header, columns, params=None, intern=None, coltype=Non
         rec.log.append((6, k, v))
         return v
 
+    def rec_vmap(kind, exprs):  # depends on the table's data: never memoised
+        rec.cacheable = False
+        return vmap(kind, exprs)
+
     prog = _compile_program(expr, rec, _ColumnsView(rec), _ParamsView(rec),
                             rec_intern if intern is not None else None,
                             rec_type if coltype is not None else None,
                             rec_lset if lset is not None else None,
-                            rec_smap if smap is not None else None)
+                            rec_smap if smap is not None else None,
+                            rec_vmap if vmap is not None else None)
     prog = (tuple(prog[0]), tuple(prog[1]), tuple(prog[2]), tuple(prog[3]))
     if rec.cacheable:
         if len(_PROGRAM_MEMO) >= 4096:
@@ -797,7 +803,8 @@ def compile_program(expr, header, columns, params=None, intern=None, coltype=Non
     return prog
 
 
-def _compile_program(expr, header, columns, params=None, intern=None, coltype=None, lset=None, smap=None):
+def _compile_program(expr, header, columns, params=None, intern=None, coltype=None, lset=None, smap=None,
+                     vmap=None):
     """Lower `expr` to (ops, iargs, fargs, names) for the C-ABI.
 
     header: dict Expr -> physical column; columns: set of the table's columns;
@@ -943,8 +950,13 @@ def _compile_program(expr, header, columns, params=None, intern=None, coltype=No
                     emit(OP_LIT_NULL, T_STRING)
                 else:
                     string_map(e.rhs, ("concat_l", cypher_to_string(va)))
-            else:
-                not_impl(e)  # two string columns: a new string per row pair
+            else:  # two columns: a new string per distinct value pair (a value map)
+                ta, tb = static_type(e.lhs), static_type(e.rhs)
+                if vmap is None or not {ta, tb} <= {T_STRING, T_INT, T_FLOAT}:
+                    not_impl(e)
+                go(e.lhs)
+                go(e.rhs)
+                emit(OP_VALUE_MAP, name_of(vmap("concat", (e.lhs, e.rhs))), 1.0)
         elif cls in _BIN_OPS:
             go(e.lhs)
             go(e.rhs)
@@ -992,8 +1004,11 @@ def _compile_program(expr, header, columns, params=None, intern=None, coltype=No
                 go(e.expr)
                 lit("true")
                 emit(OP_IF)
+            elif t in (T_INT, T_FLOAT) and vmap is not None:  # a new string per distinct value
+                go(e.expr)
+                emit(OP_VALUE_MAP, name_of(vmap("tostring", (e.expr,))), 0.0)
             else:
-                not_impl(e)  # INTEGER / FLOAT columns: a new string per value
+                not_impl(e)
         elif cls in _UN_OPS:
             go(e.expr)
             emit(_UN_OPS[cls])

@@ -97,7 +97,9 @@ class GpuSession:
         c = self._codes.get(s)
         if c is None:
             v = c_int64()
-            _lib.call("capf_string_intern", self._h, s.encode(), byref(v))
+            # (surrogatepass: a Java string may hold a lone UTF-16 surrogate, e.g. a
+            # substring splitting a pair; the dictionary keeps it as WTF-8 bytes)
+            _lib.call("capf_string_intern", self._h, s.encode("utf-8", "surrogatepass"), byref(v))
             c = v.value
             self._codes[s] = c
             self._strings[c] = s
@@ -108,7 +110,7 @@ class GpuSession:
         if s is None:
             p = c_char_p()
             _lib.call("capf_string_lookup", self._h, int(code), byref(p))
-            s = p.value.decode()
+            s = p.value.decode("utf-8", "surrogatepass")
             self._strings[code] = s
         return s
 
@@ -248,7 +250,8 @@ _SELECT_ARGS = {}
 def _program(expr, header, table, params):
     return compile_program(expr, header, set(table.physicalColumns), params, table.session.intern,
                            table.capf_type, getattr(table.session, "literal_set", None),
-                           getattr(table.session, "string_map", None))
+                           getattr(table.session, "string_map", None),
+                           lambda kind, exprs: table._value_map(kind, exprs, header, params))
 
 
 class GpuTable:
@@ -494,6 +497,42 @@ class GpuTable:
                 return self._new("capf_table_explode_values", self._h, col.encode(), int(T_NULL), 0, None, None)
             raise _lib.NotImplementedException(f"UNWIND of {e.expr}")
         return self._new("capf_table_explode_list", self._h, src.encode(), col.encode())
+
+    def _value_map(self, kind, exprs, header, params):
+        """Program name of a session value map (CAPF_OP_VALUE_MAP) giving the STRING
+        of each distinct value (toString) or value pair (concatenation) the
+        operand expressions take over this table: the operands are evaluated
+        and their distinct rows downloaded, the strings built with the JVM's
+        casts (Long.toString / Double.toString) and interned."""
+        import struct
+        from .expr import cypher_to_string
+        names = [f"\x02vm{i}" for i in range(len(exprs))]
+        t = self.withColumns(*zip(exprs, names), header=header, params=params).select(*names)
+        types = [t.capf_type(c) for c in names]
+        t = t.distinct(*names)
+        cols = [t.column_values(c) for c in names]
+
+        def key(v, ty):
+            if ty == T_FLOAT:
+                return struct.unpack("<q", struct.pack("<d", float(v)))[0]
+            if ty == T_STRING:
+                return self.session.intern(v)
+            return int(v)
+
+        entries = []
+        for vals in zip(*cols):
+            if any(v is None for v in vals):
+                continue
+            txt = "".join(cypher_to_string(float(v) if ty == T_FLOAT else v) for v, ty in zip(vals, types))
+            entries.append((tuple(key(v, ty) for v, ty in zip(vals, types)), self.session.intern(txt)))
+        entries.sort()
+        n = len(entries)
+        k1 = (c_int64 * max(n, 1))(*[e[0][0] for e in entries])
+        k2 = (c_int64 * max(n, 1))(*[e[0][1] for e in entries]) if len(exprs) > 1 else None
+        cd = (c_int64 * max(n, 1))(*[e[1] for e in entries])
+        mid = c_int32()
+        _lib.call("capf_session_value_map", self.session._h, k1, k2, cd, n, byref(mid))
+        return "\x01vmap:%d" % mid.value
 
     def withColumns(self, *columns, header=None, params=None):
         if any(isinstance(e, Explode) for e, _ in columns):

@@ -202,7 +202,15 @@ enum {
    * dictionary string c by the caller and interned (capf_session_code_map,
    * referenced as "\x01map:<id>"); NULL in, an entry < 0 (a NULL result) or
    * c past the map → NULL.                                                   */
-  CAPF_OP_STR_MAP = 90
+  CAPF_OP_STR_MAP = 90,
+  /* A new STRING per value (toString of an INTEGER / FLOAT column, the
+   * concatenation of two columns, :120-128, :184): pops x (farg == 0) or
+   * y then x (farg != 0); pushes the code of the value map names[iarg] entry
+   * whose key is x's value (INTEGER / STRING code) or bit pattern (FLOAT), or
+   * the key pair (x, y); NULL in or no entry → NULL.  The caller evaluated the
+   * operands' distinct values, built their strings and interned them
+   * (capf_session_value_map, "\x01vmap:<id>").                                */
+  CAPF_OP_VALUE_MAP = 91
 };
 
 typedef struct capf_expr {
@@ -612,6 +620,11 @@ capf_status capf_session_literal_set(capf_session *s, const int64_t *values, int
  * function on the host with the JVM's string semantics and interns the
  * results; the map is referenced in programs as "\x01map:<id>" (*map_id).  */
 capf_status capf_session_code_map(capf_session *s, const int64_t *codes, int64_t n, int32_t *map_id);
+/* A value map of CAPF_OP_VALUE_MAP: n keys (keys2 = NULL) or key pairs sorted
+ * ascending as signed int64 (pairs lexicographically), codes[i] the STRING code
+ * of entry i; referenced as "\x01vmap:<id>" (*map_id).                      */
+capf_status capf_session_value_map(capf_session *s, const int64_t *keys, const int64_t *keys2, const int64_t *codes,
+                                   int64_t n, int32_t *map_id);
 
 #ifdef __cplusplus
 }

@@ -786,6 +786,16 @@ JNI(jint, sessionCodeMap)(JNIEnv *env, jobject, jlong s, jlongArray codes) {
   if (fail(env, capf_session_code_map(S(s), v.data(), (int64_t)v.size(), &id))) return -1;
   return id;
 }
+// a value map of CAPF_OP_VALUE_MAP (sorted keys / key pairs → STRING codes): its id
+JNI(jint, sessionValueMap)(JNIEnv *env, jobject, jlong s, jlongArray keys, jlongArray keys2, jlongArray codes) {
+  const std::vector<int64_t> k = longs(env, keys), c = longs(env, codes);
+  std::vector<int64_t> k2;
+  if (keys2) k2 = longs(env, keys2);
+  int32_t id = -1;
+  if (fail(env, capf_session_value_map(S(s), k.data(), keys2 ? k2.data() : nullptr, c.data(), (int64_t)k.size(), &id)))
+    return -1;
+  return id;
+}
 // device → device
 JNI(void, sessionCopyDevice)(JNIEnv *env, jobject, jlong s, jlong dst, jlong src, jlong bytes) {
   fail(env, capf_session_copy(S(s), reinterpret_cast<void *>(dst), reinterpret_cast<const void *>(src), bytes, 3));

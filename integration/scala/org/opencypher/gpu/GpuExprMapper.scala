@@ -39,6 +39,7 @@ object GpuExprMapper {
   private final val Asin_ = 82; private final val Acos_ = 83; private final val Atan_ = 84
   private final val Degrees_ = 85; private final val Radians_ = 86; private final val Atan2_ = 87
   private final val ToBoolean_ = 88; private final val InSet = 89; private final val StrMap = 90
+  private final val ValueMap = 91
   private final val InSetMin = 17  // IN lists from this length: one set lookup per row (expr.py IN_SET_MIN)
 
   def program(expr: Expr, header: RecordHeader, table: GpuTable, parameters: CypherMap): Program = {
@@ -111,6 +112,26 @@ object GpuExprMapper {
     }
 
     def isString(e: Expr): Boolean = e.cypherType.material == CTString
+
+    // CAPF_OP_VALUE_MAP of the operands' distinct values (pairs) over this table: the
+    // JVM's casts (Long.toString / Double.toString) of each, concatenated, interned
+    // (the shim's twin of table.py GpuTable._value_map)
+    def valueMap(xs: Seq[Expr]): String = {
+      val names = xs.indices.map(i => s"\u0002vm$i")
+      val t = table.withColumns(xs.zip(names): _*)(header, parameters).distinct(names: _*)
+      def key(v: CypherValue): Long = v match {
+        case CypherInteger(i) => i
+        case CypherFloat(d) => java.lang.Double.doubleToRawLongBits(d)
+        case CypherString(s) => session.intern(s)
+        case other => throw NotImplementedException(s"GPU string of $other")
+      }
+      val entries = t.rows.map(row => names.map(row)).filterNot(_.contains(CypherNull))
+        .map(vs => (vs.map(key), session.intern(vs.map(GpuStringFunctions.cast).mkString)))
+        .toSeq.sortWith { case ((a, _), (b, _)) => (a zip b).find(p => p._1 != p._2).exists(p => p._1 < p._2) }
+      val id = Native.guard(Native.sessionValueMap(session.handle, entries.map(_._1.head).toArray,
+        if (xs.size > 1) entries.map(_._1(1)).toArray else null, entries.map(_._2).toArray))
+      "\u0001vmap:" + id
+    }
 
     // f(x) of a STRING operand: folded for a literal, else a code map (CAPF_OP_STR_MAP)
     def stringMap(x: Expr, key: Seq[Any]): Unit = literal(x) match {
@@ -235,7 +256,9 @@ object GpuExprMapper {
           case (_, Some(CypherNull)) | (Some(CypherNull), _) => emit(LitNull, Native.TypeString)
           case (None, Some(b)) => stringMap(l, Seq("concat_r", GpuStringFunctions.cast(b)))
           case (Some(a), None) => stringMap(r, Seq("concat_l", GpuStringFunctions.cast(a)))
-          case _ => throw NotImplementedException(s"GPU concatenation of two string columns $e")
+          case _ if Seq(l, r).forall(x => Set[CypherType](CTString, CTInteger, CTFloat)(x.cypherType.material)) =>
+            go(l); go(r); emit(ValueMap, nameIndex(valueMap(Seq(l, r))), 1.0)  // a string per value pair
+          case _ => throw NotImplementedException(s"GPU concatenation $e")
         }
       case ToUpper(x) => stringMap(x, Seq("upper"))                       // :190
       case ToLower(x) => stringMap(x, Seq("lower"))                       // :191
@@ -264,6 +287,7 @@ object GpuExprMapper {
               emit(LitNull, Native.TypeString); go(x); emit(Not_); emit(LitString, session.intern("false")); emit(If_)
               go(x); emit(LitString, session.intern("true")); emit(If_)
             case CTNull | CTVoid => emit(LitNull, Native.TypeString)
+            case CTInteger | CTFloat => go(x); emit(ValueMap, nameIndex(valueMap(Seq(x))), 0.0)
             case _ => throw NotImplementedException(s"GPU toString of a ${x.cypherType} column")
           }
         }

@@ -28,10 +28,13 @@ def _cols(n=400, seed=5):
     return [("s", T_STRING, [WORDS[i] for i in rng.integers(0, len(WORDS), n)], None),
             ("t", T_STRING, [WORDS[i] for i in rng.integers(0, len(WORDS), n)], None),
             ("k", T_INT, [int(x) if rng.random() > 0.1 else None for x in rng.integers(-50, 50, n)], None),
-            ("b", T_BOOL, [bool(x) if rng.random() > 0.1 else None for x in rng.integers(0, 2, n)], None)]
+            ("b", T_BOOL, [bool(x) if rng.random() > 0.1 else None for x in rng.integers(0, 2, n)], None),
+            ("f", T_FLOAT, [float(x) if rng.random() > 0.1 else None
+                            for x in np.concatenate([rng.normal(0, 1e4, n - 8),
+                                                     [0.0, -0.0, 1e7, 1e-4, 0.001, 1e21, 2.5, -7.0]])], None)]
 
 
-H = RecordHeader({Var("s"): "s", Var("t"): "t", Var("k"): "k", Var("b"): "b"})
+H = RecordHeader({Var("s"): "s", Var("t"): "t", Var("k"): "k", Var("b"): "b", Var("f"): "f"})
 
 EXPRS = [
     ToUpper(Var("s")), ToLower(Var("s")), Trim(Var("s")), LTrim(Var("s")), RTrim(Var("s")),
@@ -44,6 +47,9 @@ EXPRS = [
     ToString(Var("s")), ToString(Var("b")), ToString(IntegerLit(42)), ToString(FloatLit(1e7)),
     ToString(BoolLit(False)), ToUpper(StringLit("lit")), ToUpper(NullLit("STRING")),
     Add(StringLit("a"), IntegerLit(1)), ToUpper(Param("p")),
+    # a new string per distinct value / value pair (value maps)
+    ToString(Var("k")), ToString(Var("f")), Add(Var("s"), Var("t")), Add(Var("s"), Var("k")),
+    Add(Var("f"), Var("s")), Add(ToUpper(Var("s")), ToString(Var("k"))),
 ]
 
 
@@ -110,13 +116,12 @@ def test_string_function_in_filter_and_memo(gpu_session):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("e", [Add(Var("s"), Var("t")), ToString(Var("k")), Substring(Var("s"), Var("k")),
-                               Replace(Var("s"), StringLit("a"), StringLit("$1"))],
-                         ids=["concat_columns", "to_string_integer_column", "substring_column_start",
-                              "replace_group_ref"])
+@pytest.mark.parametrize("e", [Substring(Var("s"), Var("k")), Replace(Var("s"), StringLit("a"), StringLit("$1")),
+                               Add(Var("s"), Var("b"))],
+                         ids=["substring_column_start", "replace_group_ref", "concat_boolean"])
 def test_string_shapes_not_on_gpu_raise(gpu_session, e):
-    """Shapes that would build a new string per row (or Java regex replacement
-    groups) raise NotImplementedException instead of running elsewhere."""
+    """Shapes outside the mapping (per-row function arguments, Java regex
+    replacement groups, a BOOLEAN operand) raise instead of running elsewhere."""
     g = gpu_session.table(_cols())
     with pytest.raises(_lib.NotImplementedException):
         g.withColumns((e, "x"), header=H, params={}).rows

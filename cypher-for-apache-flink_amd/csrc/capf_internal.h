@@ -266,7 +266,7 @@ __device__ inline bool ft_load(const FtOperand &o, int64_t r, int64_t &val) {
 
 // ------------------------------------------------------------- plan nodes
 enum class Kind {
-  Source, Select, Filter, Join, Union, Distinct, Group, WithColumns, OrderBy, Skip, Limit, Explode
+  Source, Select, Filter, Join, Union, Distinct, Group, WithColumns, OrderBy, Skip, Limit, Explode, NameList
 };
 
 struct AggSpec {
@@ -305,6 +305,11 @@ struct Node {
   // output column
   int explode_list_col = -1;
   ColPtr explode_values;  // the constant list as a column of its elements
+  // NameList (labels(n) / keys(n)): the child's columns name_cols, tested per
+  // row (kind 0: BOOLEAN TRUE, 1: not NULL), name_codes[j] listed for each hit
+  std::vector<int> name_cols;
+  std::vector<int32_t> name_kinds;
+  std::vector<int64_t> name_codes;
 
   // memoised result
   std::mutex mu;
@@ -517,6 +522,9 @@ ColPtr aggregate(Session *s, const Grouping &g, const Data &d, int64_t nrows, in
                  const ColPtr &arg, Type out_type, double param = 0);
 // UNWIND: every row of d repeated per element (explode, kernels_basic.hip)
 DataPtr explode_values(Session *s, const Data &d, const ColPtr &values);
+// LIST<STRING> column of the names whose column tests true per row (labels / keys, lists.hip)
+ColPtr name_list_column(Session *s, const Data &d, const std::vector<int> &cols, const std::vector<int32_t> &kinds,
+                        const std::vector<int64_t> &codes);
 DataPtr explode_list(Session *s, const Data &d, int list_col);
 // collect(arg) per group (lists.hip): a Type::List column of g.ngroups lists.
 ColPtr collect_lists(Session *s, const Grouping &g, int64_t nrows, const ColPtr &arg,

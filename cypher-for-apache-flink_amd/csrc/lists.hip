@@ -246,4 +246,74 @@ DataPtr explode_list(Session *s, const Data &d, int list_col) {
   return out;
 }
 
+// ---------------------------------------------------------- labels / keys
+// labels(n) / keys(n) (FlinkSQLExprMapper.scala:136-153, the GetLabels /
+// GetKeys UDFs at :310-329): per row the names (STRING codes, caller-sorted)
+// of the label columns holding TRUE (kind 0) or of the property columns
+// holding a value (kind 1).  A row with none gets the empty list (the UDFs
+// return an empty array, never NULL).  Two passes: per-row counts → offsets
+// (exclusive scan) → the codes written in column order.
+constexpr int NL_MAX = 64;
+struct NameCols {
+  ColView c[NL_MAX];
+  int32_t kind[NL_MAX];
+  int64_t code[NL_MAX];
+  int32_t n;
+};
+
+__device__ inline bool nl_hit(const NameCols &nc, int j, int64_t r) {
+  const ColView &v = nc.c[j];
+  if (v.type == CAPF_TYPE_NULL || !v.data || (v.valid && !v.valid[r])) return false;
+  return nc.kind[j] ? true : ((const uint8_t *)v.data)[r] != 0;
+}
+
+__global__ void k_name_counts(NameCols nc, int64_t n, int64_t *cnt) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    int64_t k = 0;
+    for (int j = 0; j < nc.n; ++j) k += nl_hit(nc, j, r) ? 1 : 0;
+    cnt[r] = k;
+  }
+}
+
+__global__ void k_name_fill(NameCols nc, int64_t n, const int64_t *off, int64_t *codes) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    int64_t o = off[r];
+    for (int j = 0; j < nc.n; ++j)
+      if (nl_hit(nc, j, r)) codes[o++] = nc.code[j];
+  }
+}
+
+ColPtr name_list_column(Session *s, const Data &d, const std::vector<int> &cols, const std::vector<int32_t> &kinds,
+                        const std::vector<int64_t> &codes) {
+  if (cols.size() > (size_t)NL_MAX) not_impl("labels / keys over more than 64 columns");
+  NameCols nc{};
+  nc.n = (int32_t)cols.size();
+  for (size_t j = 0; j < cols.size(); ++j) {
+    const ColPtr &c = d.cols[(size_t)cols[j]];
+    if (kinds[j] == 0 && c->type != Type::Bool && c->type != Type::Null) illegal("label column is not BOOLEAN");
+    if (c->type == Type::List) not_impl("keys() over a LIST property");
+    nc.c[j] = c->type == Type::Null ? ColView{nullptr, nullptr, CAPF_TYPE_NULL, ENC_PLAIN, 0} : view_of(c);
+    nc.kind[j] = kinds[j];
+    nc.code[j] = codes[j];
+  }
+  const int64_t n = d.nrows;
+  BufPtr off = s->alloc(8 * (n + 1));
+  int64_t total = 0;
+  if (n > 0) {
+    BufPtr cnt = s->alloc(8 * n);
+    hipLaunchKernelGGL(k_name_counts, dim3(grid_for(n, 256)), dim3(256), 0, s->stream, nc, n, (int64_t *)cnt->p);
+    KERNEL_CHECK();
+    total = exclusive_scan_i64(s, (const int64_t *)cnt->p, (int64_t *)off->p, n);
+  }
+  HIP_CHECK(hipMemcpyAsync((int64_t *)off->p + n, &total, 8, hipMemcpyHostToDevice, s->stream));
+  ColPtr child = make_column(s, Type::String, total, false);
+  if (total > 0) {
+    hipLaunchKernelGGL(k_name_fill, dim3(grid_for(n, 256)), dim3(256), 0, s->stream, nc, n, (const int64_t *)off->p,
+                       (int64_t *)child->data->p);
+    KERNEL_CHECK();
+  }
+  s->sync();  // (the pageable total)
+  return list_column(s, n, off, child);
+}
+
 }  // namespace capf

@@ -619,6 +619,14 @@ static DataPtr materialize_impl(const NodePtr &n) {
       return n->explode_list_col >= 0 ? explode_list(s, *c, n->explode_list_col)
                                       : explode_values(s, *c, n->explode_values);
     }
+    case Kind::NameList: {
+      DataPtr c = materialize(n->kids[0]);
+      auto out = std::make_shared<Data>();
+      out->nrows = c->nrows;
+      out->cols = c->cols;
+      out->cols.push_back(name_list_column(s, *c, n->name_cols, n->name_kinds, n->name_codes));
+      return out;
+    }
     case Kind::WithColumns: {
       DataPtr c = materialize(n->kids[0]);
       auto out = std::make_shared<Data>();
@@ -1954,6 +1962,31 @@ capf_status capf_table_explode_values(capf_table *t, const char *name, int32_t t
   if (n > 0 && valid) HIP_CHECK(hipMemcpyAsync(v->valid->p, valid, n, hipMemcpyHostToDevice, s->stream));
   s->sync();  // pageable host sources
   nn->explode_values = v;
+  *out = wrap(nn);
+  CAPF_API_END
+}
+
+capf_status capf_table_name_list(capf_table *t, int32_t n, const char *const *cols, const int32_t *kinds,
+                                 const int64_t *codes, const char *name, capf_table **out) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(name, "name");
+  need(out, "out");
+  if (n < 0 || (n > 0 && (!cols || !kinds || !codes))) illegal("bad name list");
+  const NodePtr &c = t->node;
+  if (c->col_index(name) >= 0) illegal(std::string("column '") + name + "' already exists");
+  auto nn = new_node(c->s, Kind::NameList);
+  nn->kids.push_back(c);
+  nn->names = c->names;
+  nn->types = c->types;
+  for (int32_t j = 0; j < n; ++j) {
+    nn->name_cols.push_back(c->col_index_or_throw(cols[j]));
+    if (kinds[j] != 0 && kinds[j] != 1) illegal("bad name list kind");
+    nn->name_kinds.push_back(kinds[j]);
+    nn->name_codes.push_back(codes[j]);
+  }
+  nn->names.emplace_back(name);
+  nn->types.push_back(Type::List);
   *out = wrap(nn);
   CAPF_API_END
 }

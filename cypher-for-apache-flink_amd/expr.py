@@ -460,6 +460,30 @@ def string_fn(key, sv):
 _STR_FUNCS = {"ToUpper": "upper", "ToLower": "lower", "Trim": "trim", "LTrim": "ltrim", "RTrim": "rtrim"}
 
 
+# labels(n) / keys(n) (FlinkSQLExprMapper.scala:136-153): a LIST of the label names
+# whose flag column is TRUE / of the property keys holding a value, sorted by
+# name — a table operation (capf_table_name_list), as a withColumns item only
+Labels = _unary("Labels", "labels({})")
+Keys = _unary("Keys", "keys({})")
+
+
+def name_list_columns(e, header, columns):
+    """(columns, kinds, names) of labels(v) / keys(v) over the header: the
+    label flag columns (kind 0) or property columns (kind 1) of v, by name."""
+    v = e.expr
+    is_labels = type(e).__name__ == "Labels"
+    found = []
+    for h, c in (header.items() if header is not None else ()):
+        if c not in columns:
+            continue
+        if is_labels and isinstance(h, HasLabel) and h.owner == v:
+            found.append((h.label, c))
+        elif not is_labels and isinstance(h, ElementProperty) and h.owner == v:
+            found.append((h.key, c))
+    found.sort()
+    return [c for _, c in found], [0 if is_labels else 1] * len(found), [nm for nm, _ in found]
+
+
 Id = _unary("Id", "id({})")            # FlinkSQLExprMapper.scala:134: the element's id column
 Exists = _unary("Exists", "exists({})")  # exists(n.prop) → IS NOT NULL (:90)
 Size = _unary("Size", "size({})")      # charLength / cardinality (:80-85)

@@ -535,6 +535,20 @@ class GpuTable:
         return "\x01vmap:%d" % mid.value
 
     def withColumns(self, *columns, header=None, params=None):
+        lists = [(e, c) for e, c in columns if type(e).__name__ in ("Labels", "Keys")]
+        if lists:  # labels(n) / keys(n): LIST columns built by capf_table_name_list
+            from .expr import name_list_columns
+            plain = [(e, c) for e, c in columns if type(e).__name__ not in ("Labels", "Keys")]
+            t = self.withColumns(*plain, header=header, params=params) if plain else self
+            for e, c in lists:
+                if not isinstance(e.expr, Var):
+                    raise _lib.NotImplementedException(f"{e} of a non-variable")
+                cols, kinds, names = name_list_columns(e, header, set(t.physicalColumns))
+                n = len(cols)
+                ka = (c_int32 * max(n, 1))(*kinds)
+                ca = (c_int64 * max(n, 1))(*[self.session.intern(x) for x in names])
+                t = t._new("capf_table_name_list", t._h, n, _lib.strs(cols), ka, ca, c.encode())
+            return t
         if any(isinstance(e, Explode) for e, _ in columns):
             t = self
             plain = [(e, c) for e, c in columns if not isinstance(e, Explode)]

@@ -620,6 +620,13 @@ capf_status capf_session_literal_set(capf_session *s, const int64_t *values, int
  * function on the host with the JVM's string semantics and interns the
  * results; the map is referenced in programs as "\x01map:<id>" (*map_id).  */
 capf_status capf_session_code_map(capf_session *s, const int64_t *codes, int64_t n, int32_t *map_id);
+/* labels(n) / keys(n) (FlinkSQLExprMapper.scala:136-153; the GetLabels /
+ * GetKeys UDFs, :310-329): appends LIST<STRING> column `name` holding, per row,
+ * codes[j] for each column cols[j] that holds TRUE (kinds[j] = 0, a label flag)
+ * or any value (kinds[j] = 1, a property), in the given order (the shim sorts
+ * by label / key name); never NULL (an empty list).                        */
+capf_status capf_table_name_list(capf_table *t, int32_t n, const char *const *cols, const int32_t *kinds,
+                                 const int64_t *codes, const char *name, capf_table **out);
 /* A value map of CAPF_OP_VALUE_MAP: n keys (keys2 = NULL) or key pairs sorted
  * ascending as signed int64 (pairs lexicographically), codes[i] the STRING code
  * of entry i; referenced as "\x01vmap:<id>" (*map_id).                      */

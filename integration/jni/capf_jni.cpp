@@ -496,6 +496,17 @@ JNI(jlong, tableExplodeList)(JNIEnv *env, jobject, jlong t, jstring list_col, js
   capf_table *out = nullptr;
   return fail(env, capf_table_explode_list(T(t), l.p, nm.p, &out)) ? 0 : H(out);
 }
+// labels(n) / keys(n) (FlinkSQLExprMapper.scala:136-153): a LIST<STRING> column
+JNI(jlong, tableNameList)(JNIEnv *env, jobject, jlong t, jobjectArray cols, jintArray kinds, jlongArray codes,
+                          jstring name) {
+  JStrs c(env, cols);
+  JStr nm(env, name);
+  const std::vector<int32_t> k = ints(env, kinds);
+  const std::vector<int64_t> cd = longs(env, codes);
+  capf_table *out = nullptr;
+  return fail(env, capf_table_name_list(T(t), (int32_t)k.size(), c.data(), k.data(), cd.data(), nm.p, &out)) ? 0
+                                                                                                           : H(out);
+}
 JNI(jlong, tableWithColumns)(JNIEnv *env, jobject, jlong t, jobjectArray exprs,
                              jobjectArray names) {  // Table.scala:170
   Programs e(env, exprs);

@@ -99,13 +99,31 @@ final class GpuTable private (private[gpu] val handle: Long)(implicit val sessio
   }
 
   override def withColumns(columns: (Expr, String)*)(implicit header: RecordHeader, parameters: CypherMap): GpuTable = { // :170
-    val (explodes, plain) = columns.partition { case (e, _) => e.isInstanceOf[Explode] }
+    val (lists, rest) = columns.partition { case (e, _) => e.isInstanceOf[Labels] || e.isInstanceOf[Keys] }
+    val (explodes, plain) = rest.partition { case (e, _) => e.isInstanceOf[Explode] }
     val base =
       if (plain.isEmpty) this
       else wrap(Native.tableWithColumns(handle,
         plain.map { case (e, _) => GpuExprMapper.program(e, header, this, parameters) }.toArray,
         plain.map(_._2).toArray))
-    explodes.foldLeft(base) { case (t, (Explode(list), col)) => t.explode(list, col, header, parameters) }
+    val withLists = lists.foldLeft(base) { case (t, (e, col)) => t.nameList(e, col, header) }
+    explodes.foldLeft(withLists) { case (t, (Explode(list), col)) => t.explode(list, col, header, parameters) }
+  }
+
+  /** labels(n) / keys(n) (FlinkSQLExprMapper.scala:136-153): the label flag columns
+    * (TRUE) or property columns (any value) of n, sorted by name, as a LIST<STRING>
+    * column.  keys lists every property holding a value (GetKeys, :321-329, matches
+    * `case (key, true)` on the VALUE — a reference bug not reproduced). */
+  private def nameList(e: Expr, col: String, header: RecordHeader): GpuTable = {
+    val present = physicalColumns.toSet
+    val (found, kind) = e match {
+      case Labels(v) => (header.labelsFor(v.owner.get).toSeq.map(l => l.label.name -> header.column(l)), 0)
+      case Keys(v) => (header.propertiesFor(v.owner.get).toSeq.map(p => p.key.name -> header.column(p)), 1)
+      case other => throw NotImplementedException(s"GPU list function $other")
+    }
+    val cols = found.filter { case (_, c) => present(c) }.sortBy(_._1)
+    wrap(Native.tableNameList(handle, cols.map(_._2).toArray, Array.fill(cols.size)(kind),
+      cols.map { case (n, _) => session.intern(n) }.toArray, col))
   }
 
   /** UNWIND list AS item = add(Explode(list) as item) (RelationalPlanner.scala:99-101). */

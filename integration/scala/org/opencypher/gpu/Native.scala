@@ -137,6 +137,7 @@ object Native {
   @native def tableExplodeValues(table: Long, name: String, elemType: Int, n: Long, values: java.nio.ByteBuffer,
                                  valid: java.nio.ByteBuffer): Long
   @native def tableExplodeList(table: Long, listCol: String, name: String): Long
+  @native def tableNameList(table: Long, cols: Array[String], kinds: Array[Int], codes: Array[Long], name: String): Long
   @native def tableShow(table: Long, rows: Int): Unit
 
   // graph inputs (EdgeListDataSource.scala:56-92; synthetic R-MAT / node ranges)

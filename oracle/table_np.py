@@ -390,6 +390,20 @@ def evaluate(e, table, header, params):
                 out = [f(v) if ok else None for v, ok in zip(a.v, a.ok)]
             ok = np.array([v is not None for v in out], bool)
             return Val(T_STRING, np.array(out, dtype=object), ok)
+        if name in ("Labels", "Keys"):  # GetLabels / GetKeys (FlinkSQLExprMapper.scala:136-153, 310-329)
+            found = []
+            for h, c in (header.items() if header is not None else ()):
+                if c not in cols:
+                    continue
+                if name == "Labels" and isinstance(h, HasLabel) and h.owner == x.expr:
+                    found.append((h.label, cols[c], True))
+                elif name == "Keys" and isinstance(h, ElementProperty) and h.owner == x.expr:
+                    found.append((h.key, cols[c], False))
+            found.sort(key=lambda f: f[0])
+            out = np.empty(n, dtype=object)
+            for i in range(n):
+                out[i] = [nm for nm, k, flag in found if k.ok[i] and (bool(k.v[i]) if flag else True)]
+            return Val(T_LIST, out, np.ones(n, bool))
         if name == "ToString":  # cast to STRING (:184)
             a = go(x.expr)
             if a.t == T_NULL:

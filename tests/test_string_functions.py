@@ -125,3 +125,45 @@ def test_string_shapes_not_on_gpu_raise(gpu_session, e):
     g = gpu_session.table(_cols())
     with pytest.raises(_lib.NotImplementedException):
         g.withColumns((e, "x"), header=H, params={}).rows
+
+
+# labels(n) / keys(n) (FlinkSQLExprMapper.scala:136-153, GetLabels / GetKeys at
+# :310-329): the planner's RETURN through withColumns → capf_table_name_list.
+LK_CREATE = ("CREATE (:A:B {name: 'x', age: 3}), (:A {name: 'y'}), (:B {age: 7, flag: true}), (), "
+             "(:C {name: null, age: 1})")
+
+
+def _lk_query():
+    from capf_amd.expr import Keys, Labels
+    from capf_amd.planner import Match, NodeP, Query, Stage
+    return Query([Match([NodeP("n")], [])],
+                 [Stage([("l", Labels(Var("n", "NODE"))), ("k", Keys(Var("n", "NODE")))])])
+
+
+def _canon(rows):
+    return sorted((tuple(r["l"]), tuple(r["k"])) for r in rows)
+
+
+def test_labels_keys_oracle():
+    """Per node: its labels and the keys of its non-NULL properties, each sorted
+    by name; never NULL (GetKeys itself lists only properties whose value is
+    TRUE — a reference UDF bug not reproduced: keys(n) lists every property
+    holding a value, Cypher's semantics)."""
+    from capf_amd.graph import ScanGraph
+    from capf_amd.planner import run
+    from oracle.create_parser import parse_create
+    og = ScanGraph.from_data(OracleSession(), parse_create(LK_CREATE))
+    got = _canon(run(og, _lk_query()))
+    assert got == sorted([(("A", "B"), ("age", "name")), (("A",), ("name",)), (("B",), ("age", "flag")),
+                          ((), ()), (("C",), ("age",))])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("compact", [False, True], ids=["int64", "for32"])
+def test_labels_keys_gpu(gpu_session, compact):
+    from capf_amd.graph import ScanGraph
+    from capf_amd.planner import run
+    from oracle.create_parser import parse_create
+    g = ScanGraph.from_data(gpu_session, parse_create(LK_CREATE), compact=compact)
+    og = ScanGraph.from_data(OracleSession(), parse_create(LK_CREATE))
+    assert _canon(run(g, _lk_query())) == _canon(run(og, _lk_query()))

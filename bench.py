@@ -139,20 +139,43 @@ def cpu_info(threads):
             "cap_reason": "one GPU's share of the box's CPUs (OMP_NUM_THREADS=16 on the GPU box)"}
 
 
-def tri_cpu_baseline(scale):
-    """Config 4 on the host cores: the oracle's trace(A^3) count by sorted-list
-    intersection (oracle/rmat.c, threads) over a bounded sample — the same
-    R-MAT generator 4 scales down (1/16 of the rels; ~20 s on 8 threads)."""
+def tri_cpu_baseline(session, graph, scale, budget_s):
+    """Config 4 on the host cores, Flink plan shape (oracle/rmat.c
+    pipeline_triangles): hash tables on the full node scan, the start-keyed R2
+    and the (start, end)-keyed R3 (built, not timed), then the first K r1 rows
+    expand through R2 — every wedge row materialised — and probe R3 on both
+    keys with the three uniqueness filters (RelationalPlanner.scala:130-189).
+    value = triangle rows / probe seconds over that bounded sample."""
+    import numpy as np
     from oracle import cmodel
-    sc = max(8, scale - 4)
-    src, dst = cmodel.rmat(sc)
+    rel = graph.rel_tables[0].table
+    src, _ = rel.column_arrays("source")
+    dst, _ = rel.column_arrays("target")
+    ids, _ = rel.column_arrays("id")
+    nodes = np.arange(1 << scale, dtype=np.int64)
     th = cpu_threads()
     t0 = time.perf_counter()
-    c = cmodel.count_triangle_trace(src, dst, 1 << sc, threads=th)
-    el = time.perf_counter() - t0
-    return {"value": c / el, "unit": "joined rows/s", "cores": th, **cpu_info(th), "kind": "port",
-            "sample": (f"R-MAT s{sc} (same generator, 1/16 of the s{scale} rels): triangle count {c} by "
-                       f"sorted-list intersection (oracle/rmat.c count_triangle_trace) in {el:.2f}s on {th} threads")}
+    pipe = cmodel.Pipeline(nodes, ids, src, dst, threads=th)
+    pipe.build_pairs(th)
+    build_s = time.perf_counter() - t0
+    m = len(src)
+    k = min(m, 1 << 12)
+    tris, wedges, probe_s, lo = 0, 0, 0.0, 0
+    while lo < m:  # grow the sample until the probe budget is used
+        hi = min(m, lo + k)
+        t0 = time.perf_counter()
+        c, w = pipe.triangles(lo, hi, th)
+        probe_s += time.perf_counter() - t0
+        tris, wedges, lo = tris + c, wedges + w, hi
+        if probe_s >= budget_s:
+            break
+        k *= 2
+    pipe.close()
+    return {"value": tris / probe_s if probe_s > 0 else None, "unit": "joined rows/s", "cores": th,
+            **cpu_info(th), "kind": "port",
+            "sample": (f"R-MAT s{scale} triangle, Flink plan shape (hash tables on the node scan, start-keyed R2 "
+                       f"and (start, end)-keyed R3, {build_s:.1f}s build, not timed); r1 rows [0,{lo}) of {m}: "
+                       f"{wedges} wedge rows probed, {tris} triangle rows in {probe_s:.2f}s on {th} threads")}
 
 
 def c2_cpu_baseline(graph, scale):
@@ -695,7 +718,7 @@ def run_single(args):
     if not args.no_cpu and args.query == "two_hop":
         result["cpu_baseline"] = cpu_baseline(s, g, args.scale, args.cpu_seconds)
     if not args.no_cpu and args.query == "triangle":
-        result["cpu_baseline"] = tri_cpu_baseline(args.scale)
+        result["cpu_baseline"] = tri_cpu_baseline(s, g, args.scale, args.cpu_seconds)
     if not args.no_cpu and args.query == "one_hop_person":
         result["cpu_baseline"] = c2_cpu_baseline(g, args.scale)
         if result["cpu_baseline"]["count"] != count:

@@ -59,6 +59,10 @@ def lib():
         l.pipeline_probe.restype = u64
         l.onehop_label_count.argtypes = [P, i64, P, i64, P, P, i64, i32]
         l.onehop_label_count.restype = u64
+        l.pipeline_build_pairs.argtypes = [P, i32]
+        l.pipeline_build_pairs.restype = None
+        l.pipeline_triangles.argtypes = [P, i64, i64, i32, P]
+        l.pipeline_triangles.restype = u64
         l.pipeline_free.argtypes = [P]
         l.pipeline_free.restype = None
         l.rmat_stream_counts.argtypes = [i32, u64, u32, u32, u32, i64, i32, P]
@@ -180,6 +184,17 @@ class Pipeline:
 
     def probe(self, lo, hi, threads):
         return lib().pipeline_probe(self._h, lo, hi, threads)
+
+    def build_pairs(self, threads):
+        """The (start, end)-keyed R3 table of the triangle's ExpandInto join."""
+        lib().pipeline_build_pairs(self._h, threads)
+
+    def triangles(self, lo, hi, threads):
+        """(triangle rows, wedge rows) of r1 rows [lo, hi): the relational plan's
+        Expand, Expand, ExpandInto with the uniqueness filters."""
+        w = ctypes.c_uint64()
+        c = lib().pipeline_triangles(self._h, lo, hi, threads, ctypes.byref(w))
+        return int(c), int(w.value)
 
     def close(self):
         if self._h:

@@ -200,6 +200,9 @@ static void *probe_worker(void *arg) {
 typedef struct {
   JoinState js;
   int64_t n_nodes, m;
+  /* config 4: R3 keyed by (start, end) (pipeline_build_pairs), or null */
+  int64_t *r3_off, *r3_rows;
+  uint64_t r3_mask;
 } Pipeline;
 
 typedef struct {
@@ -301,9 +304,131 @@ uint64_t pipeline_probe(void *handle, int64_t lo, int64_t hi, int threads) {
   return c;
 }
 
+/* --------------------------- config 4: the triangle, Flink plan shape
+ * Expand, Expand, ExpandInto (RelationalPlanner.scala:130-189): the wedges
+ * S_a ⋈ R1 ⋈ S_b ⋈ R2 ⋈ S_c through the start-keyed R2 table above, then the
+ * closing rel R3 by a hash join on the TWO keys (start(r3) = c, end(r3) = a)
+ * — a (start, end)-keyed table built here — and the uniqueness filters
+ * NOT(r1 = r2), NOT(r1 = r3), NOT(r2 = r3); count(*).  Every wedge is
+ * materialised and probed, as the relational plan does (no degree order, no
+ * set intersection). */
+static inline uint64_t pair_key(int64_t s, int64_t d) { return hmix(s) ^ (hmix(d) * 0x9e3779b97f4a7c15ull); }
+
+typedef struct {
+  Pipeline *p;
+  uint64_t blo, bhi;
+  int64_t *fill;
+  int phase;
+} PairBuildTask;
+
+static void *pair_build_worker(void *arg) {
+  PairBuildTask *t = (PairBuildTask *)arg;
+  Pipeline *p = t->p;
+  for (int64_t r = 0; r < p->m; ++r) {
+    uint64_t b = pair_key(p->js.src[r], p->js.dst[r]) & p->r3_mask;
+    if (b < t->blo || b >= t->bhi) continue;
+    if (t->phase == 0)
+      p->r3_off[b + 1]++;
+    else
+      p->r3_rows[p->r3_off[b] + t->fill[b]++] = r;
+  }
+  return NULL;
+}
+
+void pipeline_build_pairs(void *handle, int threads) {
+  Pipeline *p = (Pipeline *)handle;
+  if (threads < 1) threads = 1;
+  uint64_t nb = 1024;
+  while (nb < (uint64_t)p->m) nb <<= 1;
+  p->r3_mask = nb - 1;
+  p->r3_off = (int64_t *)calloc(nb + 1, 8);
+  p->r3_rows = (int64_t *)malloc((size_t)(p->m > 0 ? p->m : 1) * 8);
+  int64_t *fill = (int64_t *)calloc(nb, 8);
+  pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * threads);
+  PairBuildTask *tasks = (PairBuildTask *)malloc(sizeof(PairBuildTask) * threads);
+  for (int phase = 0; phase < 2; ++phase) {
+    if (phase == 1)
+      for (uint64_t b = 0; b < nb; ++b) p->r3_off[b + 1] += p->r3_off[b];
+    for (int t = 0; t < threads; ++t) {
+      tasks[t].p = p;
+      tasks[t].blo = nb * (uint64_t)t / threads;
+      tasks[t].bhi = nb * (uint64_t)(t + 1) / threads;
+      tasks[t].fill = fill;
+      tasks[t].phase = phase;
+      pthread_create(&th[t], NULL, pair_build_worker, &tasks[t]);
+    }
+    for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+  }
+  free(th);
+  free(tasks);
+  free(fill);
+}
+
+typedef struct {
+  const Pipeline *p;
+  int64_t lo, hi;
+  uint64_t count, wedges;
+} WedgeTask;
+
+static void *wedge_worker(void *arg) {
+  WedgeTask *t = (WedgeTask *)arg;
+  const Pipeline *p = t->p;
+  const JoinState *js = &p->js;
+  uint64_t c = 0, w = 0;
+  for (int64_t r1 = t->lo; r1 < t->hi; ++r1) {
+    const int64_t a = js->src[r1], b = js->dst[r1];
+    if (!node_probe(js, a) || !node_probe(js, b)) continue;
+    const uint64_t bk = hmix(b) & js->r2_mask;
+    for (int64_t j = js->r2_off[bk]; j < js->r2_off[bk + 1]; ++j) {  /* ⋈ R2 on end(r1) = start(r2) */
+      const int64_t r2 = js->r2_rows[j];
+      if (js->src[r2] != b) continue;
+      const int64_t cc = js->dst[r2];
+      if (!node_probe(js, cc)) continue;
+      if (js->id[r1] == js->id[r2]) continue;                       /* NOT(r1 = r2) */
+      ++w;                                                           /* a wedge row */
+      const uint64_t pk = pair_key(cc, a) & p->r3_mask;              /* ⋈ R3 on (start, end) = (c, a) */
+      for (int64_t k = p->r3_off[pk]; k < p->r3_off[pk + 1]; ++k) {
+        const int64_t r3 = p->r3_rows[k];
+        if (js->src[r3] != cc || js->dst[r3] != a) continue;
+        if (js->id[r3] != js->id[r1] && js->id[r3] != js->id[r2]) ++c;
+      }
+    }
+  }
+  t->count = c;
+  t->wedges = w;
+  return NULL;
+}
+
+/* Triangle rows of r1 rows [lo, hi); *wedges = the wedge rows probed. */
+uint64_t pipeline_triangles(void *handle, int64_t lo, int64_t hi, int threads, uint64_t *wedges) {
+  Pipeline *p = (Pipeline *)handle;
+  if (threads < 1) threads = 1;
+  pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * threads);
+  WedgeTask *tasks = (WedgeTask *)malloc(sizeof(WedgeTask) * threads);
+  const int64_t span = hi - lo;
+  for (int t = 0; t < threads; ++t) {
+    tasks[t].p = p;
+    tasks[t].lo = lo + span * t / threads;
+    tasks[t].hi = lo + span * (t + 1) / threads;
+    pthread_create(&th[t], NULL, wedge_worker, &tasks[t]);
+  }
+  uint64_t c = 0, w = 0;
+  for (int t = 0; t < threads; ++t) {
+    pthread_join(th[t], NULL);
+    c += tasks[t].count;
+    w += tasks[t].wedges;
+  }
+  free(th);
+  free(tasks);
+  if (wedges) *wedges = w;
+  return c;
+}
+
 void pipeline_free(void *handle) {
   Pipeline *p = (Pipeline *)handle;
   if (!p) return;
+  free(p->r3_off);
+  free(p->r3_rows);
   free(p->js.node_keys);
   free(p->js.r2_off);
   free(p->js.r2_rows);

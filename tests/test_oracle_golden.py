@@ -127,3 +127,27 @@ def test_unwind_on_oracle():
     op = plan_stage(op, Stage([("y", Var("y"))]))
     from capf_amd.planner import records
     assert sorted(r["y"] for r in records(op, ["y"])) == [1, 2]
+
+
+def test_flink_shaped_triangle_pipeline_matches_fixture():
+    """The CPU baseline of config 4 (oracle/rmat.c pipeline_triangles: every
+    wedge of the Expand, Expand joins probed into the (start, end)-keyed R3,
+    the three uniqueness filters) counts exactly the committed triangle
+    fixture over all r1 rows, and its wedge rows are the 2-hop fixture."""
+    import json
+    import os
+    import numpy as np
+    from oracle import cmodel
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "rmat_counts.json")
+    counts = json.load(open(path))
+    for sc in (8, 10, 12):
+        s, d = cmodel.rmat(sc)
+        p = cmodel.Pipeline(np.arange(1 << sc), np.arange(len(s)), s, d, threads=4)
+        p.build_pairs(4)
+        t, w = p.triangles(0, len(s), 4)
+        half = p.triangles(0, len(s) // 2, 4)[0] + p.triangles(len(s) // 2, len(s), 4)[0]
+        p.close()
+        assert t == half == cmodel.count_triangle_brute(s, d, 1 << sc)
+        if str(sc) in counts["triangle"]:
+            assert t == counts["triangle"][str(sc)]
+        assert w == counts["rmat"][str(sc)]["two_hop"]

@@ -75,16 +75,18 @@ def check_case(got, expected, opts, reference=True):
     """A reference case's assertion: Bag equality (OT/Bag.scala), or the
     ordered row list ({"ordered": True}), or only the row count.
 
-    reference=True: the reference test's own comparison — a Bag of CypherMaps,
-    whose equality is Scala Map equality over the unwrapped values
-    (okapi-api/.../value/CypherValue.scala:199-203, 301-302): numeric values
-    compare by value there (CypherMap("res" -> 4) equals a 4.0 result), unless
-    the case records a typed assertion ({"typed": True}: the reference test
-    compares CypherValues directly, e.g. `should equal(CypherFloat(…))`).
+    reference=True: against the reference test's expectation, typed (an
+    INTEGER / FLOAT slip fails), except the cases marked {"coop": True}: the
+    reference test's Bag of CypherMaps compares by Scala Map equality over the
+    unwrapped values (okapi-api/.../value/CypherValue.scala:199-203, 301-302),
+    where numeric values compare by value (CypherMap("res" -> 4) equals the 4.0
+    that avg over INTEGER values is) — the only three cases whose expectation
+    differs from the result in type (avg_ints*).  ({"typed": True} marks the
+    cases whose reference test compares CypherValues directly.)
     reference=False (backend against oracle): typed, always."""
     if "row_count" in opts:
         return len(got) == opts["row_count"]
-    coop = reference and not opts.get("typed")
+    coop = reference and bool(opts.get("coop")) and not opts.get("typed")
     if opts.get("ordered"):
         return [bag([r], coop) for r in got] == [bag([r], coop) for r in expected]
     return bag(got, coop) == bag(expected, coop)

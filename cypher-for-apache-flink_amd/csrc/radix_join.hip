@@ -159,11 +159,15 @@ struct RJTile2 {
 };
 
 // The grids of pass 2 are an upper bound of the tile count (nt1 + 256: no host
-// read of the tile list); blocks past *nt2 exit (their count rows stay 0).
+// read of the tile list); a block past *nt2 zeroes the count row its index
+// would own (the tiles' rows fill [0, 256·nt2), these [256·nt2, 256·grid)) and exits.
 __global__ __launch_bounds__(RJ_PBLOCK) void k_rj_hist2(const uint64_t *h1, const RJTile2 *tiles,
                                                          const int64_t *nt2, int64_t *counts) {
   __shared__ uint32_t hist[RJ_P];
-  if ((int64_t)blockIdx.x >= *nt2) return;
+  if ((int64_t)blockIdx.x >= *nt2) {
+    for (int b = threadIdx.x; b < RJ_P; b += RJ_PBLOCK) counts[(int64_t)blockIdx.x * RJ_P + b] = 0;
+    return;
+  }
   for (int i = threadIdx.x; i < RJ_P; i += RJ_PBLOCK) hist[i] = 0;
   __syncthreads();
   const RJTile2 tl = tiles[blockIdx.x];
@@ -278,8 +282,7 @@ static RJSide rj_partition(Session *s, const ColPtr &col, int64_t n) {
   BufPtr o2 = s->alloc(8 * (RJ_P * nt2max + 1));
   if (total > 0) {
     KernelTimer kt(s, "rj_partition2", 24.0 * total);
-    BufPtr c2 = s->alloc(8 * RJ_P * nt2max);
-    HIP_CHECK(hipMemsetAsync(c2->p, 0, 8 * RJ_P * nt2max, s->stream));  // rows of the unused tiles
+    BufPtr c2 = s->alloc(8 * RJ_P * nt2max);  // (the unused tiles' rows zeroed by k_rj_hist2)
     hipLaunchKernelGGL(k_rj_hist2, dim3((unsigned)nt2max), dim3(RJ_PBLOCK), 0, s->stream,
                        (const uint64_t *)h1->p, (const RJTile2 *)dt->p, (const int64_t *)d_nt2, (int64_t *)c2->p);
     KERNEL_CHECK();

@@ -151,3 +151,26 @@ def test_flink_shaped_triangle_pipeline_matches_fixture():
         if str(sc) in counts["triangle"]:
             assert t == counts["triangle"][str(sc)]
         assert w == counts["rmat"][str(sc)]["two_hop"]
+
+
+def test_flink_shaped_pipelines_pin_fixtures_at_s14_s16():
+    """The committed closed-form fixtures checked by the relational plan shape
+    itself at larger scales than the s <= 12 pipeline checks: the 2-hop count
+    at s14 and s16 (every 2-path enumerated through the start-keyed R2 hash
+    table with NOT(r1 = r2)) and the triangle count at s14 (every wedge probed
+    into the (start, end)-keyed R3) — the same C plans the bench's
+    cpu_baseline legs time."""
+    import json
+    import os
+    import numpy as np
+    from oracle import cmodel
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "rmat_counts.json")
+    counts = json.load(open(path))
+    for sc in (14, 16):
+        s, d = cmodel.rmat(sc)
+        p = cmodel.Pipeline(np.arange(1 << sc), np.arange(len(s)), s, d, threads=8)
+        assert p.probe(0, len(s), 8) == counts["rmat"][str(sc)]["two_hop"]
+        if sc == 14:
+            p.build_pairs(8)
+            assert p.triangles(0, len(s), 8)[0] == counts["triangle"]["14"]
+        p.close()

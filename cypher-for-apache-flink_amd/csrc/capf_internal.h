@@ -616,6 +616,10 @@ struct C2Spill {
   int nb = 0;
   // host side: where the count goes (the pinned scalar or the async slot)
   int64_t *fin = nullptr;
+  // non-null: P1's per-tile self-loop counts, summed into acc[1] by the dot
+  // (the pipeline without a transpose kernel)
+  const uint32_t *tile_loops = nullptr;
+  int64_t ntiles = 0;
 };
 // d_acc3 = [Σ in·out, self-loops, done counter] (device): the pipeline writes
 // the self-loop total into [1] and clears [0] and [2] itself (no memset needed)

@@ -206,6 +206,15 @@ __device__ inline C5Raw<W> c5_ld_raw(const uint8_t *p) {
 // group die as its keys appear, so the peak stays within 64 VGPRs.  UPF 2:
 // non-temporal loads (s24 P1 0.516 vs 0.521 ms with default-policy loads);
 // UPF 3: also the FOR24 fields used raw when the bases are lo (0.512 ms).
+// run_major: meta goes out run-major ([run][tile], what P3 reads: no transpose
+// launch) and the full tiles are dealt to the XCDs in contiguous ranges (block b
+// runs on XCD b mod 8), so the 32 tiles sharing a 128-B meta line are written
+// through one L2 at about the same time and leave as whole lines.
+__device__ inline int64_t c5_xcd_tile(int64_t b, int64_t g) {
+  const int64_t per = g / 8;
+  return b < 8 * per ? (b % 8) * per + b / 8 : b;
+}
+
 template <int W, bool ALIAS, bool CHECK, bool RAGGED, class SH, int UPF = 0>
 // Self-loops go out as one plain uint32 per tile (tile_loops[t], summed by
 // k_c3_units); every tile's workgroup also clears its share of the `zwords` words at zbuf
@@ -215,7 +224,7 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
                                                             uint32_t *meta,
                                                             uint32_t *tile_loops,
                                                             int64_t t_base, uint32_t *zbuf, int64_t zwords,
-                                                            unsigned long long *zacc) {
+                                                            unsigned long long *zacc, int run_major) {
   constexpr int TILE = SH::TILE, MAXR = SH::MAXR;
   constexpr int RPT = TILE / C5_BLOCK, GROUPS = RPT / 4;
   constexpr int STAGE = c5_stage_keys<SH>();
@@ -224,7 +233,7 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
   __shared__ uint32_t cur[MAXR];
   __shared__ uint32_t lds_scan[17];
   uint16_t *stage = (uint16_t *)stage4;
-  const int64_t t = t_base + blockIdx.x;
+  const int64_t t = t_base + (run_major && !RAGGED ? c5_xcd_tile(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x);
   const int nr = 2 * c.nb;
   // pad keys: 8·(t mod 8) + slot-in-piece (P3 subtracts them per bin)
   const uint32_t pb = 8u * (uint32_t)(t & 7);
@@ -364,7 +373,7 @@ __global__ __launch_bounds__(C5_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) v
     const int r = RUNS_PT * threadIdx.x + q;
     if (r <= nr) cur[r] = ex;
     if (r < nr) {
-      meta[t * nr + r] = (ex >> 3) | (cs[q] << 16);  // [tile][run], transposed later
+      meta[run_major ? (int64_t)r * c.ntiles + t : t * nr + r] = (ex >> 3) | (cs[q] << 16);  // [tile][run] or [run][tile]
       // pad slots of the run's last piece: 8·(t mod 8) + slot (P3 subtracts them per bin)
       for (uint32_t p = ex + cs[q]; p & 7u; ++p) stage[p] = (uint16_t)(pb + (p & 7u));
     }
@@ -930,19 +939,20 @@ __global__ __launch_bounds__(256) void k_c3_overflow(C3Ovf o, uint32_t *h_in, ui
 
 template <int W, bool ALIAS, bool CHECK, class SH>
 static void launch_c5(Session *s, const C5Cols<W> &c, uint16_t *part, uint32_t *meta,
-                      uint32_t *tile_loops, uint32_t *zbuf, int64_t zwords, unsigned long long *zacc) {
+                      uint32_t *tile_loops, uint32_t *zbuf, int64_t zwords, unsigned long long *zacc,
+                      int run_major = 0) {
   const int64_t nfull = c.n / SH::TILE;
   if (nfull > 0) {
     auto kern = c.bu1 == c.lo && c.bv1 == c.lo && W == 3 && !SH::WIDE
                     ? k_c5_partition<W, ALIAS, CHECK, false, SH, 3>
                     : k_c5_partition<W, ALIAS, CHECK, false, SH, 2>;
     hipLaunchKernelGGL(kern, dim3((unsigned)nfull), dim3(C5_BLOCK), 0, s->stream, c, part, meta,
-                       tile_loops, (int64_t)0, zbuf, zwords, zacc);
+                       tile_loops, (int64_t)0, zbuf, zwords, zacc, run_major);
     KERNEL_CHECK();
   }
   if (nfull < c.ntiles) {  // the ragged last tile
     hipLaunchKernelGGL((k_c5_partition<W, ALIAS, true, true, SH>), dim3(1), dim3(C5_BLOCK), 0,
-                       s->stream, c, part, meta, tile_loops, nfull, zbuf, zwords, zacc);
+                       s->stream, c, part, meta, tile_loops, nfull, zbuf, zwords, zacc, run_major);
     KERNEL_CHECK();
   }
 }
@@ -968,15 +978,15 @@ static int64_t c5_post_acc_bytes(int nr, int S, int split_x16, int64_t nkeys, in
 // words that start at zero: run totals, unit / event / done counters, bucket counters
 // (and the hand-off log: P3's bucket-dot epilogue may read a reserved slot
 // that another bucket's unit has not written yet — a zero entry adds nothing)
-static int64_t c5_post_zero_words(int nr, uint32_t ovf_cap) {
-  return (8 * (int64_t)nr + 16 + 4 * (int64_t)nr + 8 * (int64_t)ovf_cap) / 4;
+static int64_t c5_post_zero_words(int nr, uint32_t ovf_cap, bool with_split = false) {
+  return (8 * (int64_t)nr + 16 + 4 * (int64_t)nr + 8 * (int64_t)ovf_cap + (with_split ? 4 * (int64_t)nr : 0)) / 4;
 }
 
 static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, const C3Sides &sd,
                     int64_t ntiles, int64_t rstride, int64_t nkeys, int S, uint32_t *h_in,
                     uint32_t *h_out, int64_t slice_stride, bool static_units = false,
                     C3Ovf *packed_ovf = nullptr, BufPtr *keep = nullptr, const C3Post *post = nullptr,
-                    BufPtr acc_pre = BufPtr()) {
+                    BufPtr acc_pre = BufPtr(), bool direct = false) {
   const int nr = 2 * sd.nb;
   static bool attr_set = false;
   if (!attr_set) {
@@ -992,7 +1002,10 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
   // node-partitioned rank's static work list needs no run totals, and its few
   // runs (≤ 64 at G = 8) share each tile's meta lines: P3 reads them in place,
   // no transpose launch.
-  const bool in_place = static_units && !post;
+  // direct (2-hop pipeline, one slice): P1 wrote run-major meta and every run is
+  // one exclusive unit — no transpose, no work list; the dot adds the
+  // self-loops and the split flags (all 0) were cleared by P1
+  const bool in_place = (static_units && !post) || direct;
   BufPtr meta_t = in_place ? BufPtr() : s->alloc(4 * nr * ntiles);
   // transpose blocks: tiles per block tt, fewer when there are few runs (≥ ~1024 blocks)
   int64_t tt = C3_TT;
@@ -1029,7 +1042,8 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
     KERNEL_CHECK();
   }
   C3Sides sdk = sd;  // as launched: split units clear their buckets (claim bits)
-  if (!static_units) {
+  const bool stat = static_units || direct;
+  if (!stat) {
     sdk.claim = split;
     // the work list in its own one-workgroup kernel (fusing it into the
     // transpose's last workgroup made T+U 55 µs against 35 + 6 µs + a 10 µs
@@ -1042,11 +1056,11 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
     // (folding the dot into P3's epilogue measured 0.51 ms for P3 against
     // 0.44 + 0.027 ms + a ~10 µs boundary: the dot kernel runs after P3)
     KernelTimer kt(s, "c5_gather", 2.0 * nkeys);
-    const int grid = static_units ? (nr * S + 255) / 256 * 256 : max_units;
+    const int grid = stat ? (nr * S + 255) / 256 * 256 : max_units;
     hipLaunchKernelGGL(k_c5_gather<C5_PPS>, dim3((unsigned)grid), dim3(C5_BLOCK), C5_GATHER_LDS, s->stream,
-                       static_units ? nullptr : (const C3Unit *)units, (const int32_t *)nunits, part,
+                       stat ? nullptr : (const C3Unit *)units, (const int32_t *)nunits, part,
                        in_place ? meta : (const uint32_t *)meta_t->p, ntiles, sd.nb, rstride, h_in, h_out,
-                       slice_stride, ovf, sdk, S, in_place ? (int64_t)nr : (int64_t)1);
+                       slice_stride, ovf, sdk, S, in_place && !direct ? (int64_t)nr : (int64_t)1);
     KERNEL_CHECK();
   }
   if (sd.packed) {  // the hand-offs are applied by k_c5_dot_packed
@@ -1059,6 +1073,8 @@ static void c5_post(Session *s, const uint16_t *part, const uint32_t *meta, cons
     post->spill->hl = slice_stride;
     post->spill->split = sd.pairs ? split : nullptr;  // per run: 1 = uint32 bins, 0 = packed pairs
     post->spill->nb = sd.nb;
+    post->spill->tile_loops = direct ? post->tile_loops : nullptr;  // (direct: no transpose summed them)
+    post->spill->ntiles = direct ? post->ntiles : 0;
   } else {
     KernelTimer kt(s, "c3_overflow", 0.0);
     hipLaunchKernelGGL(k_c3_overflow, dim3(16), dim3(256), 0, s->stream, ovf, h_in, h_out);
@@ -1189,17 +1205,27 @@ static void chain2_c5(Session *s, C5Cols<W> c, bool in_range, uint32_t *h_in, ui
   const int S = c5_slices(nr);
   uint32_t ovf_cap = 0;
   BufPtr post_acc = s->alloc(c5_post_acc_bytes(nr, S, sd.split_x16, 2 * c.n, nullptr, &ovf_cap));
+  // One slice (≥ 256 runs): no transpose and no work-list kernel — P1 writes
+  // run-major meta, every run is one exclusive P3 unit (hash-partitioned runs
+  // are near-uniform: no hub split at s24), the dot adds the self-loops.  s24
+  // (profiles/r05_ab_direct.txt): pipeline 1.000 → 0.980 ms, T 37 + U 8 µs
+  // gone, P1 +8 µs (scattered meta lines), P3 +13 µs (it now pays P1's dirty-line
+  // write-back that T used to).  CAPF_C5_DIRECT=0 keeps the transpose pipeline.
+  const char *de = getenv("CAPF_C5_DIRECT");
+  const bool direct_env = !(de && atoi(de) == 0);
+  const bool direct = direct_env && S == 1 && spill != nullptr;
   {
     KernelTimer kt(s, "c5_partition", (2.0 * W + 4.0) * c.n);
     uint16_t *pp = (uint16_t *)part->p;
     uint32_t *mp = (uint32_t *)meta->p;
     uint32_t *tlp = (uint32_t *)tl->p, *zb = (uint32_t *)post_acc->p;
-    const int64_t zw = c5_post_zero_words(nr, ovf_cap);
+    const int64_t zw = c5_post_zero_words(nr, ovf_cap, direct);
     const bool alias = c.u2 == c.u1 && c.v2 == c.v1;
-    if (alias && !in_range) launch_c5<W, true, true, SH>(s, c, pp, mp, tlp, zb, zw, d_acc3);
-    if (alias && in_range) launch_c5<W, true, false, SH>(s, c, pp, mp, tlp, zb, zw, d_acc3);
-    if (!alias && !in_range) launch_c5<W, false, true, SH>(s, c, pp, mp, tlp, zb, zw, d_acc3);
-    if (!alias && in_range) launch_c5<W, false, false, SH>(s, c, pp, mp, tlp, zb, zw, d_acc3);
+    const int rm = direct ? 1 : 0;
+    if (alias && !in_range) launch_c5<W, true, true, SH>(s, c, pp, mp, tlp, zb, zw, d_acc3, rm);
+    if (alias && in_range) launch_c5<W, true, false, SH>(s, c, pp, mp, tlp, zb, zw, d_acc3, rm);
+    if (!alias && !in_range) launch_c5<W, false, true, SH>(s, c, pp, mp, tlp, zb, zw, d_acc3, rm);
+    if (!alias && in_range) launch_c5<W, false, false, SH>(s, c, pp, mp, tlp, zb, zw, d_acc3, rm);
   }
   C3Post post{};
   post.tile_loops = (const uint32_t *)tl->p;
@@ -1210,7 +1236,7 @@ static void chain2_c5(Session *s, C5Cols<W> c, bool in_range, uint32_t *h_in, ui
   sd.pairs = S == 1 && spill ? 1 : 0;  // packed-pair buckets (one uint32 per bin when split)
   if (S == 1) {
     c5_post(s, (const uint16_t *)part->p, (const uint32_t *)meta->p, sd, c.ntiles, c.rstride,
-            2 * c.n, 1, h_in, h_out, hl, false, nullptr, nullptr, &post, post_acc);
+            2 * c.n, 1, h_in, h_out, hl, false, nullptr, nullptr, &post, post_acc, direct);
     return;
   }
   BufPtr sl = s->alloc(8 * S * hl);

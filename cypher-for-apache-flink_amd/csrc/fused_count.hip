@@ -555,6 +555,14 @@ __global__ __launch_bounds__(1024) void k_chain2_dot_pairs(const uint32_t *h1, c
     s = block_reduce_sum(s, lds);
   }
   if (threadIdx.x == 0 && s) atomicAdd(acc, s);
+  if (sp.tile_loops) {  // the self-loops (no transpose summed P1's per-tile counts)
+    unsigned long long l = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < sp.ntiles; i += (int64_t)gridDim.x * blockDim.x)
+      l += sp.tile_loops[i];
+    __syncthreads();  // lds reused
+    l = block_reduce_sum(l, lds);
+    if (threadIdx.x == 0 && l) atomicAdd(acc + 1, l);
+  }
   if (threadIdx.x == 0) {
     __threadfence();
     if (atomicAdd(done, 1u) == gridDim.x - 1) {

@@ -73,10 +73,29 @@ def test_two_hop_headline_split_runs(gpu_session, monkeypatch, scale):
     the others wait for it.  Two queries back to back: the second must not see
     the first one's counters."""
     monkeypatch.setenv("CAPF_P3_SPLIT", "0.5")
+    monkeypatch.setenv("CAPF_C5_DIRECT", "0")  # (the one-slice pipeline has no split units)
     g = rmat_graph(gpu_session, scale, compact=3)
     for _ in range(2):
         assert run(g, TWO_HOP)[0]["count"] == FULL[str(scale)]["two_hop"]
     assert gpu_session.last_plan() == "fused_chain2"
+
+
+@pytest.mark.parametrize("direct", ["1", "0"], ids=["no_transpose", "transpose"])
+def test_two_hop_headline_s24_both_pipelines(gpu_session, monkeypatch, direct):
+    """s24 (one slice): the default pipeline without the transpose and work-list
+    kernels (P1 writes run-major meta, one exclusive P3 unit per run, the dot
+    sums the self-loops) and the transpose pipeline (CAPF_C5_DIRECT=0) give the
+    fixture, twice in a row, synchronously and through count_async."""
+    import torch
+    monkeypatch.setenv("CAPF_C5_DIRECT", direct)
+    g = rmat_graph(gpu_session, 24, compact=3)
+    for _ in range(2):
+        assert run(g, TWO_HOP)[0]["count"] == FULL["24"]["two_hop"]
+    slot = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    plan_query(g, TWO_HOP).table.count_async(slot.data_ptr())
+    gpu_session.sync()
+    assert slot.item() == FULL["24"]["two_hop"]
 
 
 def test_two_hop_headline_async_queue(gpu_session):

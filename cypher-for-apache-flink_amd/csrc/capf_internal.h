@@ -369,6 +369,9 @@ struct Session {
     bool pairs;
   };
   std::vector<ValueMap> value_maps;
+  // content → id of the code / value maps: a program compiled again over the same
+  // dictionary / data re-registers the same map (no device buffer per query)
+  std::map<std::vector<int64_t>, int32_t> code_map_ids, value_map_ids;
   std::map<std::vector<int64_t>, int32_t> literal_set_ids;
   std::vector<PendingTiming> pending;   // recorded, not yet resolved
   std::vector<hipEvent_t> event_pool;

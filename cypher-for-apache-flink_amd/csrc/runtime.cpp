@@ -879,12 +879,24 @@ capf_status capf_session_value_map(capf_session *cs, const int64_t *keys, const 
   if (keys2) std::copy(keys2, keys2 + n, h.begin() + n);
   std::copy(codes, codes + n, h.begin() + (k - 1) * n);
   Session &s = cs->impl;
+  std::vector<int64_t> key(h);
+  key.push_back(keys2 ? 1 : 0);
+  key.push_back(n);
+  {
+    std::lock_guard<std::mutex> g(s.user_mu);
+    auto it = s.value_map_ids.find(key);
+    if (it != s.value_map_ids.end()) {
+      *map_id = it->second;
+      return CAPF_OK;
+    }
+  }
   BufPtr b = s.alloc(8 * h.size());
   HIP_CHECK(hipMemcpyAsync(b->p, h.data(), 8 * h.size(), hipMemcpyHostToDevice, s.stream));
   s.sync();  // (pageable source)
   std::lock_guard<std::mutex> g(s.user_mu);
   *map_id = (int32_t)s.value_maps.size();
   s.value_maps.push_back(Session::ValueMap{b, n, keys2 != nullptr});
+  s.value_map_ids.emplace(std::move(key), *map_id);
   CAPF_API_END
 }
 
@@ -894,12 +906,22 @@ capf_status capf_session_code_map(capf_session *cs, const int64_t *codes, int64_
   need(map_id, "map_id");
   if (n < 0 || (n > 0 && !codes)) illegal("bad code map");
   Session &s = cs->impl;
+  std::vector<int64_t> key(codes, codes + n);
+  {
+    std::lock_guard<std::mutex> g(s.user_mu);
+    auto it = s.code_map_ids.find(key);
+    if (it != s.code_map_ids.end()) {
+      *map_id = it->second;
+      return CAPF_OK;
+    }
+  }
   BufPtr b = s.alloc(8 * std::max<int64_t>(n, 1));
   if (n > 0) HIP_CHECK(hipMemcpyAsync(b->p, codes, 8 * n, hipMemcpyHostToDevice, s.stream));
   s.sync();  // (pageable source)
   std::lock_guard<std::mutex> g(s.user_mu);
   *map_id = (int32_t)s.code_maps.size();
   s.code_maps.emplace_back(b, n);
+  s.code_map_ids.emplace(std::move(key), *map_id);
   CAPF_API_END
 }
 

@@ -242,6 +242,10 @@ class GpuSession:
         _lib.call("capf_session_sync", self._h)
 
 
+# distinct operand values (pairs) a value map may hold (toString of a number
+# column, concatenation of two columns): each becomes a host-built string
+VALUE_MAP_MAX = 1 << 22
+
 # encoded argument arrays of select() per column tuple (scans and renames
 # repeat the same selections every query)
 _SELECT_ARGS = {}
@@ -510,6 +514,9 @@ class GpuTable:
         t = self.withColumns(*zip(exprs, names), header=header, params=params).select(*names)
         types = [t.capf_type(c) for c in names]
         t = t.distinct(*names)
+        if t.size > VALUE_MAP_MAX:  # every distinct value becomes a host string and a dictionary entry
+            raise _lib.NotImplementedException(
+                f"a new string per value over {t.size} distinct values (more than {VALUE_MAP_MAX})")
         cols = [t.column_values(c) for c in names]
 
         def key(v, ty):

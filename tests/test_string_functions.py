@@ -167,3 +167,14 @@ def test_labels_keys_gpu(gpu_session, compact):
     g = ScanGraph.from_data(gpu_session, parse_create(LK_CREATE), compact=compact)
     og = ScanGraph.from_data(OracleSession(), parse_create(LK_CREATE))
     assert _canon(run(g, _lk_query())) == _canon(run(og, _lk_query()))
+
+
+@pytest.mark.gpu
+def test_value_map_cap_raises(gpu_session, monkeypatch):
+    """More distinct operand values than VALUE_MAP_MAX: NotImplementedException
+    (no host string per value of a huge column)."""
+    import capf_amd.table as tb
+    monkeypatch.setattr(tb, "VALUE_MAP_MAX", 10)
+    g = gpu_session.table(_cols())
+    with pytest.raises(_lib.NotImplementedException):
+        g.withColumns((ToString(Var("k")), "x"), header=H, params={}).rows

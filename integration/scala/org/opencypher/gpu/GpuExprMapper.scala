@@ -119,6 +119,8 @@ object GpuExprMapper {
     def valueMap(xs: Seq[Expr]): String = {
       val names = xs.indices.map(i => s"\u0002vm$i")
       val t = table.withColumns(xs.zip(names): _*)(header, parameters).distinct(names: _*)
+      if (t.size > (1L << 22))  // every distinct value becomes a host string (table.py VALUE_MAP_MAX)
+        throw NotImplementedException(s"a new string per value over ${t.size} distinct values")
       def key(v: CypherValue): Long = v match {
         case CypherInteger(i) => i
         case CypherFloat(d) => java.lang.Double.doubleToRawLongBits(d)

@@ -163,19 +163,37 @@ capf_status capf_comm_all_to_all_bytes(capf_comm *c, const void *d_send, const i
   const Rccl &r = rccl();
   // one group of point-to-point pairs: RCCL schedules them over the xGMI links
   // together (the shape of an all-to-allv; per-link bound on xGMI)
-  int64_t so = 0, ro = 0;
-  check(r.group_start(), "ncclGroupStart");
+  // every argument is checked before the group opens: a throw inside the
+  // group would leave it open, and the next collective would join it
+  int64_t st = 0, rt = 0;
   for (int p = 0; p < c->world; ++p) {
     if (send_bytes[p] < 0 || recv_bytes[p] < 0) illegal("negative byte count");
-    if (send_bytes[p] > 0)
-      check(r.send((const uint8_t *)d_send + so, (size_t)send_bytes[p], ncclUint8, p, c->comm, stream_of(c)),
-            "ncclSend");
-    if (recv_bytes[p] > 0)
-      check(r.recv((uint8_t *)d_recv + ro, (size_t)recv_bytes[p], ncclUint8, p, c->comm, stream_of(c)), "ncclRecv");
+    st += send_bytes[p];
+    rt += recv_bytes[p];
+  }
+  if ((st > 0 && !d_send) || (rt > 0 && !d_recv)) illegal("null buffer");
+  int64_t so = 0, ro = 0;
+  check(r.group_start(), "ncclGroupStart");
+  ncclResult_t first = ncclSuccess;
+  const char *what = nullptr;
+  for (int p = 0; p < c->world && first == ncclSuccess; ++p) {
+    if (send_bytes[p] > 0) {
+      ncclResult_t rc = r.send((const uint8_t *)d_send + so, (size_t)send_bytes[p], ncclUint8, p, c->comm,
+                               stream_of(c));
+      if (rc != ncclSuccess) first = rc, what = "ncclSend";
+    }
+    if (first == ncclSuccess && recv_bytes[p] > 0) {
+      ncclResult_t rc = r.recv((uint8_t *)d_recv + ro, (size_t)recv_bytes[p], ncclUint8, p, c->comm,
+                               stream_of(c));
+      if (rc != ncclSuccess) first = rc, what = "ncclRecv";
+    }
     so += send_bytes[p];
     ro += recv_bytes[p];
   }
-  check(r.group_end(), "ncclGroupEnd");
+  // the group is always closed, then the first error is raised
+  ncclResult_t end = r.group_end();
+  if (first != ncclSuccess) check(first, what);
+  check(end, "ncclGroupEnd");
   COMM_API_END
 }
 

@@ -1042,7 +1042,14 @@ __device__ Val run_program(const Instr *code, int ncode, const ColView *cols, in
       }
       case OP_IF: {
         Val v = st[--sp], c = st[--sp], e = st[--sp];
-        st[sp++] = (!c.nul && c.b != 0) ? v : e;
+        Val r = (!c.nul && c.b != 0) ? v : e;
+        // an INTEGER and a FLOAT branch: the CASE is a FLOAT (Calcite's CASE
+        // type; the compiler types it so) — widen the chosen value here, not
+        // only at the final store, so an enclosing Divide / Modulo sees a FLOAT
+        const bool mixed = (v.t == CAPF_TYPE_FLOAT64 && e.t == CAPF_TYPE_INT64) ||
+                           (v.t == CAPF_TYPE_INT64 && e.t == CAPF_TYPE_FLOAT64);
+        if (mixed && r.t == CAPF_TYPE_INT64) r = r.nul ? mknull(CAPF_TYPE_FLOAT64) : mkf(vf(r));
+        st[sp++] = r;
         break;
       }
       case OP_ROUND: case OP_ABS: case OP_CEIL: case OP_FLOOR: case OP_SIGN: case OP_SQRT:

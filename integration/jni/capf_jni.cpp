@@ -253,6 +253,11 @@ JNI(jlong, tableFromHost)(JNIEnv *env, jobject, jlong s, jobjectArray names, jin
                           jobjectArray data, jobjectArray valid, jlong nrows) {
   JStrs nm(env, names);
   std::vector<int32_t> ty = ints(env, types);
+  if ((int32_t)ty.size() != nm.n() || !data || env->GetArrayLength(data) != nm.n() ||
+      (valid && env->GetArrayLength(valid) != nm.n())) {
+    illegal_argument(env, "tableFromHost: types, data and valid need one entry per column");
+    return 0;
+  }
   std::vector<const void *> d(nm.n(), nullptr);
   std::vector<const uint8_t *> v(nm.n(), nullptr);
   for (int32_t i = 0; i < nm.n(); ++i) {
@@ -276,6 +281,10 @@ JNI(jlong, tableFromDevice)(JNIEnv *env, jobject, jlong s, jobjectArray names, j
   JStrs nm(env, names);
   std::vector<int32_t> ty = ints(env, types);
   std::vector<int64_t> dp = longs(env, data), vp = longs(env, valid);
+  if ((int32_t)ty.size() != nm.n() || (int32_t)dp.size() != nm.n() || (!vp.empty() && (int32_t)vp.size() != nm.n())) {
+    illegal_argument(env, "tableFromDevice: types, data and valid need one entry per column");
+    return 0;
+  }
   std::vector<void *> d(nm.n(), nullptr);
   std::vector<uint8_t *> v(nm.n(), nullptr);
   for (int32_t i = 0; i < nm.n(); ++i) {
@@ -461,6 +470,10 @@ JNI(jlong, tableGroup)(JNIEnv *env, jobject, jlong t, jobjectArray by, jintArray
   JStrs b(env, by), nm(env, names);
   std::vector<int32_t> k = ints(env, kinds), d = bools(env, distinct);
   Programs a(env, args);
+  if (a.n() != (int32_t)k.size() || (int32_t)d.size() != (int32_t)k.size() || nm.n() != (int32_t)k.size()) {
+    illegal_argument(env, "tableGroup: args, distinct and names need one entry per aggregation");
+    return 0;
+  }
   capf_table *out = nullptr;
   return fail(env, capf_table_group(T(t), b.n(), b.data(), (int32_t)k.size(), k.data(), a.data(),
                                     d.data(), nm.data(), &out))
@@ -474,6 +487,11 @@ JNI(jlong, tableGroupEx)(JNIEnv *env, jobject, jlong t, jobjectArray by, jintArr
   std::vector<int32_t> k = ints(env, kinds), d = bools(env, distinct);
   std::vector<double> p = doubles(env, params);
   Programs a(env, args);
+  if (a.n() != (int32_t)k.size() || (int32_t)d.size() != (int32_t)k.size() || (int32_t)p.size() != (int32_t)k.size() ||
+      nm.n() != (int32_t)k.size()) {
+    illegal_argument(env, "tableGroupEx: args, distinct, params and names need one entry per aggregation");
+    return 0;
+  }
   capf_table *out = nullptr;
   return fail(env, capf_table_group_ex(T(t), b.n(), b.data(), (int32_t)k.size(), k.data(), a.data(),
                                        d.data(), p.data(), nm.data(), &out))
@@ -755,6 +773,12 @@ JNI(void, commAllGatherBytes)(JNIEnv *env, jobject, jlong c, jlong d_send, jlong
 JNI(void, commAllToAllBytes)(JNIEnv *env, jobject, jlong c, jlong d_send, jlongArray send_bytes, jlong d_recv,
                              jlongArray recv_bytes) {
   std::vector<int64_t> sb = longs(env, send_bytes), rb = longs(env, recv_bytes);
+  int32_t rank = 0, world = 0;
+  if (fail(env, capf_comm_rank(reinterpret_cast<capf_comm *>(c), &rank, &world))) return;
+  if ((int32_t)sb.size() != world || (int32_t)rb.size() != world) {
+    illegal_argument(env, "commAllToAllBytes: sendBytes and recvBytes need one entry per rank");
+    return;
+  }
   fail(env, capf_comm_all_to_all_bytes(reinterpret_cast<capf_comm *>(c), reinterpret_cast<const void *>(d_send),
                                        sb.data(), reinterpret_cast<void *>(d_recv), rb.data()));
 }
@@ -780,6 +804,10 @@ JNI(void, sessionFree)(JNIEnv *env, jobject, jlong s, jlong d) {
 // device ⇄ host through a direct buffer (kind 1 host → device, 2 device → host)
 JNI(void, sessionCopy)(JNIEnv *env, jobject, jlong s, jlong d, jobject host, jlong bytes, jint kind) {
   void *h = direct(env, host);
+  if (!h || bytes < 0 || env->GetDirectBufferCapacity(host) < bytes) {
+    illegal_argument(env, "sessionCopy: a direct buffer of at least `bytes` bytes is required");
+    return;
+  }
   if (kind == 1) fail(env, capf_session_copy(S(s), reinterpret_cast<void *>(d), h, bytes, 1));
   else fail(env, capf_session_copy(S(s), h, reinterpret_cast<const void *>(d), bytes, 2));
 }
@@ -802,6 +830,10 @@ JNI(jint, sessionValueMap)(JNIEnv *env, jobject, jlong s, jlongArray keys, jlong
   const std::vector<int64_t> k = longs(env, keys), c = longs(env, codes);
   std::vector<int64_t> k2;
   if (keys2) k2 = longs(env, keys2);
+  if (c.size() != k.size() || (keys2 && k2.size() != k.size())) {
+    illegal_argument(env, "sessionValueMap: keys, keys2 and codes need the same length");
+    return -1;
+  }
   int32_t id = -1;
   if (fail(env, capf_session_value_map(S(s), k.data(), keys2 ? k2.data() : nullptr, c.data(), (int64_t)k.size(), &id)))
     return -1;

@@ -70,6 +70,7 @@ struct JNIEnv {
   void GetByteArrayRegion(jbyteArray array, jsize start, jsize len, jbyte *buf);
   void SetByteArrayRegion(jbyteArray array, jsize start, jsize len, const jbyte *buf);
   void *GetDirectBufferAddress(jobject buf);
+  jlong GetDirectBufferCapacity(jobject buf);
   void DeleteLocalRef(jobject obj);
 };
 

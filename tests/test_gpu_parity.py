@@ -1223,6 +1223,13 @@ def test_case_atan2_toboolean_parity(gpu_session):
         ex.Atan2(Var("x"), Var("y")),
         ex.ToBoolean(Var("s")),
         Add(Var("x"), ex.Pi), Multiply(ex.E, Var("y")),
+        # a widened CASE (INTEGER and FLOAT branches) inside an enclosing
+        # operator: the chosen INTEGER branch is already a FLOAT there (1 / 2 =
+        # 0.5, not integer division) — ADVICE r5
+        ex.Divide(ex.CaseExpr([(GreaterThan(Var("x"), FloatLit(1.0)), IntegerLit(1))], FloatLit(2.5)),
+                  IntegerLit(2)),
+        ex.Modulo(ex.CaseExpr([(LessThan(Var("y"), IntegerLit(0)), Var("y"))], Var("x")), IntegerLit(2)),
+        ex.Divide(ex.CaseExpr([(GreaterThan(Var("y"), IntegerLit(0)), Var("y"))], FloatLit(0.5)), Var("y")),
     ]
     gt = gpu_session.table(cols)
     ot = OracleSession().table(cols)

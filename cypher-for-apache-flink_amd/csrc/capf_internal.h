@@ -171,7 +171,8 @@ enum Op : int32_t {
   OP_TAN = CAPF_OP_TAN, OP_ASIN = CAPF_OP_ASIN, OP_ACOS = CAPF_OP_ACOS, OP_ATAN = CAPF_OP_ATAN,
   OP_DEGREES = CAPF_OP_DEGREES, OP_RADIANS = CAPF_OP_RADIANS, OP_ATAN2 = CAPF_OP_ATAN2,
   OP_TO_BOOLEAN = CAPF_OP_TO_BOOLEAN, OP_IN_SET = CAPF_OP_IN_SET, OP_STR_MAP = CAPF_OP_STR_MAP,
-  OP_VALUE_MAP = CAPF_OP_VALUE_MAP
+  OP_VALUE_MAP = CAPF_OP_VALUE_MAP, OP_STR_TO_NUM = CAPF_OP_STR_TO_NUM, OP_RAND = CAPF_OP_RAND,
+  OP_LIST_INDEX = CAPF_OP_LIST_INDEX
 };
 // a program name that refers to a session literal set ("\x01set:<id>"), not a column
 inline bool is_literal_set_name(const std::string &nm) { return nm.size() > 5 && nm.compare(0, 5, "\x01set:") == 0; }
@@ -393,6 +394,9 @@ struct Session {
   // 1 true, 2 neither (NULL)
   BufPtr d_str_bool;
   size_t d_str_bool_n = 0;
+  // device table of the strings as numbers (CAPF_OP_STR_TO_NUM)
+  BufPtr d_str_num;
+  size_t d_str_num_n = 0;
   // small device scratch for scalar results
   int64_t *d_scalars = nullptr;  // 64 slots
   int64_t *h_scalars = nullptr;  // pinned mirror
@@ -552,6 +556,9 @@ ColPtr decode_column(Session *s, const ColPtr &c);
 const int64_t *string_length_table(Session *s, size_t *n);
 // Device table of the session's strings parsed as booleans (CAPF_OP_TO_BOOLEAN).
 const uint8_t *string_bool_table(Session *s, size_t *n);
+// Device table of the session's strings parsed as numbers (CAPF_OP_STR_TO_NUM):
+// [double n][int64 n][uint8 flags n] (bit 0: a DOUBLE, bit 1: an INTEGER).
+const void *string_num_table(Session *s, size_t *n);
 // Record an error for capf_last_error() (used by entry points outside runtime.cpp).
 int32_t record_error(int32_t code, const char *msg);
 

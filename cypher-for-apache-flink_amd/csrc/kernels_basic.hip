@@ -1108,6 +1108,41 @@ __device__ Val run_program(const Instr *code, int ncode, const ColView *cols, in
         st[sp++] = m < 0 ? mknull(CAPF_TYPE_STRING) : mk(m, CAPF_TYPE_STRING, 0);
         break;
       }
+      case OP_STR_TO_NUM: {  // cols[in.i] = [double n][int64 n][flags n], n in base; f: 1 DOUBLE, 0 INTEGER
+        Val a = st[--sp];
+        const bool fl = in.f != 0.0;
+        const int64_t n = cols[in.i].base;
+        if (a.nul || a.b < 0 || a.b >= n) {
+          st[sp++] = mknull(fl ? CAPF_TYPE_FLOAT64 : CAPF_TYPE_INT64);
+        } else {
+          const uint8_t *base = (const uint8_t *)cols[in.i].data;
+          const uint8_t f = base[16 * n + a.b];
+          if (fl)
+            st[sp++] = (f & 1) ? mkf(((const double *)base)[a.b]) : mknull(CAPF_TYPE_FLOAT64);
+          else
+            st[sp++] = (f & 2) ? mk(((const int64_t *)(base + 8 * n))[a.b], CAPF_TYPE_INT64, 0)
+                               : mknull(CAPF_TYPE_INT64);
+        }
+        break;
+      }
+      case OP_RAND: {  // uniform in [0, 1): 53 bits of splitmix64(seed, row)
+        const uint64_t h = splitmix64((uint64_t)in.i ^ splitmix64((uint64_t)r + 0x9E3779B97F4A7C15ull));
+        st[sp++] = mkf((double)(h >> 11) * 0x1.0p-53);
+        break;
+      }
+      case OP_LIST_INDEX: {  // cols[in.i] LIST offsets [n + 1]; cols[(int)in.f] the element column
+        Val ix = st[--sp];
+        const ColView &c = cols[in.i];
+        const int ev = (int)in.f;
+        if (ev < 0 || ix.nul || !c.data || (c.valid && !c.valid[r])) {
+          st[sp++] = mknull(ev < 0 ? CAPF_TYPE_NULL : cols[ev].type);
+          break;
+        }
+        const int64_t o0 = ((const int64_t *)c.data)[r], len = ((const int64_t *)c.data)[r + 1] - o0;
+        int64_t k = ix.b < 0 ? ix.b + len : ix.b;
+        st[sp++] = (k < 0 || k >= len) ? mknull(cols[ev].type) : load_col(cols[ev], o0 + k);
+        break;
+      }
       case OP_TO_BOOLEAN: {  // cols[in.i] = the session's strings parsed as booleans
         Val a = st[--sp];
         if (a.nul || a.t == CAPF_TYPE_BOOL) {
@@ -1221,6 +1256,34 @@ static DeviceProgram upload_program(Session *s, const Program &p,
       break;
     }
   for (auto &in : code)
+    if (in.op == OP_STR_TO_NUM) {  // the session's strings as numbers, one more view
+      size_t nstr = 0;
+      const void *tn = string_num_table(s, &nstr);
+      const int64_t vi = (int64_t)views.size();
+      views.push_back(ColView{tn, nullptr, (int32_t)Type::Float64, ENC_PLAIN, (int64_t)std::max<size_t>(nstr, 1)});
+      for (auto &x : code)
+        if (x.op == OP_STR_TO_NUM) {
+          x.f = (double)x.i;  // 1 DOUBLE, 0 INTEGER
+          x.i = vi;
+        }
+      break;
+    }
+  for (auto &in : code)
+    if (in.op == OP_LIST_INDEX) {  // the element column of the list as one more view (index in f)
+      int idx = -1;
+      for (size_t k = 0; k < names.size(); ++k)
+        if (names[k] == p.names[(size_t)in.i]) idx = (int)k;
+      if (idx < 0) illegal("expression references unknown column '" + p.names[(size_t)in.i] + "'");
+      const ColPtr &c = d.cols[idx];
+      if (c->type != Type::List || !c->child) {
+        in.f = -1.0;  // a NULL-typed column: every row NULL
+        continue;
+      }
+      force(c->child);
+      in.f = (double)views.size();
+      views.push_back(view_of(c->child));
+    }
+  for (auto &in : code)
     if (in.op == OP_TO_BOOLEAN) {  // the session's strings as booleans, one more view
       size_t nstr = 0;
       const uint8_t *tb = string_bool_table(s, &nstr);
@@ -1237,10 +1300,11 @@ static DeviceProgram upload_program(Session *s, const Program &p,
   for (auto &in : code) {
     switch (in.op) {
       case OP_COL: case OP_LIT_INT: case OP_LIT_FLOAT: case OP_LIT_BOOL: case OP_LIT_STRING:
-      case OP_LIT_NULL: case OP_LIST_SIZE: depth++; break;
+      case OP_LIT_NULL: case OP_LIST_SIZE: case OP_RAND: depth++; break;
       case OP_AND: case OP_OR: case OP_COALESCE: depth -= (int)in.i - 1; break;
       case OP_NOT: case OP_IS_NULL: case OP_IS_NOT_NULL: case OP_NEG: case OP_TO_FLOAT:
-      case OP_TO_INTEGER: case OP_STR_LEN: case OP_TO_BOOLEAN: case OP_IN_SET: case OP_STR_MAP: break;
+      case OP_TO_INTEGER: case OP_STR_LEN: case OP_TO_BOOLEAN: case OP_IN_SET: case OP_STR_MAP:
+      case OP_STR_TO_NUM: case OP_LIST_INDEX: break;
       case OP_IF: depth -= 2; break;
       case OP_VALUE_MAP: depth -= in.f != 0.0 ? 1 : 0; break;
       default:

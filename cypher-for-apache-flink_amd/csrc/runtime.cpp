@@ -5,7 +5,10 @@
 // FlinkTable (flink-cypher/.../impl/table/FlinkTable.scala:49-199).  Like the
 // Flink Table API, operations only build a plan; materialisation happens on
 // size / download (FlinkTable.scala:57-61).
+#include <cctype>
+#include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <sstream>
 
 #include "capf_internal.h"
@@ -197,7 +200,7 @@ Program Program::from_c(const capf_expr *e) {
 std::vector<std::string> Program::referenced() const {
   std::vector<std::string> r;
   for (auto &in : code)
-    if (in.op == OP_COL || in.op == OP_LIST_SIZE) r.push_back(names[in.i]);
+    if (in.op == OP_COL || in.op == OP_LIST_SIZE || in.op == OP_LIST_INDEX) r.push_back(names[in.i]);
   return r;
 }
 
@@ -375,6 +378,28 @@ Type infer_type(const Program &p, const std::vector<std::string> &names,
         if (a != Type::Null && a != Type::Bool && a != Type::String)
           not_impl(std::string("toBoolean on ") + type_name(a));
         st.push_back(Type::Bool);
+        break;
+      }
+      case OP_STR_TO_NUM: {
+        Type a = pop();
+        if (a != Type::Null && a != Type::String) illegal("toFloat / toInteger of a string: operand is not a STRING");
+        st.push_back(in.i == 1 ? Type::Float64 : Type::Int64);
+        break;
+      }
+      case OP_RAND: st.push_back(Type::Float64); break;
+      case OP_LIST_INDEX: {
+        if (in.i < 0 || (size_t)in.i >= p.names.size()) illegal("malformed expression program (column)");
+        const std::string &nm = p.names[in.i];
+        int idx = -1;
+        for (size_t k = 0; k < names.size(); ++k)
+          if (names[k] == nm) idx = (int)k;
+        if (idx < 0) illegal("expression references unknown column '" + nm + "'");
+        if (types[idx] != Type::List && types[idx] != Type::Null) illegal("index into a non-list column");
+        Type ix = pop();
+        if (ix != Type::Null && ix != Type::Int64) illegal("a list index must be an INTEGER");
+        const int et = (int)in.f;
+        if (et < 0 || et > 4) illegal("list element type out of range");
+        st.push_back((Type)et);
         break;
       }
       default: not_impl("expression opcode " + std::to_string(in.op));
@@ -727,6 +752,94 @@ const uint8_t *string_bool_table(Session *s, size_t *n) {
   }
   *n = s->d_str_bool_n;
   return (const uint8_t *)s->d_str_bool->p;
+}
+// CAST(string AS DOUBLE): java.lang.Double.valueOf after String.trim —
+// [+-] (NaN | Infinity | digits[.digits] | .digits)([eE][+-]digits)? [fFdD]?
+static bool parse_java_double(const std::string &u, double *out) {
+  size_t b = 0, e = u.size();
+  while (b < e && (unsigned char)u[b] <= ' ') ++b;
+  while (e > b && (unsigned char)u[e - 1] <= ' ') --e;
+  std::string t = u.substr(b, e - b);
+  if (t.empty()) return false;
+  size_t i = 0;
+  if (t[i] == '+' || t[i] == '-') ++i;
+  const std::string rest = t.substr(i);
+  if (rest == "NaN" || rest == "Infinity") {
+    *out = rest == "NaN" ? std::nan("") : (t[0] == '-' ? -HUGE_VAL : HUGE_VAL);
+    return true;
+  }
+  size_t d0 = i, nd = 0;
+  while (i < t.size() && isdigit((unsigned char)t[i])) ++i, ++nd;
+  if (i < t.size() && t[i] == '.') {
+    ++i;
+    while (i < t.size() && isdigit((unsigned char)t[i])) ++i, ++nd;
+  }
+  if (nd == 0) return false;
+  if (i < t.size() && (t[i] == 'e' || t[i] == 'E')) {
+    ++i;
+    if (i < t.size() && (t[i] == '+' || t[i] == '-')) ++i;
+    size_t ne = 0;
+    while (i < t.size() && isdigit((unsigned char)t[i])) ++i, ++ne;
+    if (ne == 0) return false;
+  }
+  const size_t num_end = i;
+  if (i < t.size() && strchr("fFdD", t[i])) ++i;
+  if (i != t.size()) return false;
+  (void)d0;
+  *out = strtod(t.substr(0, num_end).c_str(), nullptr);
+  return true;
+}
+
+// CAST(string AS INT), the semantics the reference expectations pin
+// (FunctionTests.scala:1101-1152): a decimal integer after trim, a fractional
+// part truncated ('82.9' -> 82), within 32 bits; anything else NULL
+static bool parse_int32(const std::string &u, int64_t *out) {
+  size_t b = 0, e = u.size();
+  while (b < e && (unsigned char)u[b] <= ' ') ++b;
+  while (e > b && (unsigned char)u[e - 1] <= ' ') --e;
+  size_t i = b;
+  bool neg = false;
+  if (i < e && (u[i] == '+' || u[i] == '-')) neg = u[i++] == '-';
+  int64_t v = 0;
+  size_t nd = 0;
+  while (i < e && isdigit((unsigned char)u[i])) {
+    v = v * 10 + (u[i++] - '0');
+    if (v > (int64_t)1 << 32) v = (int64_t)1 << 32;  // saturate: out of range below
+    ++nd;
+  }
+  if (nd == 0) return false;
+  if (i < e && u[i] == '.') {
+    ++i;
+    while (i < e && isdigit((unsigned char)u[i])) ++i;
+  }
+  if (i != e) return false;
+  if (neg) v = -v;
+  if (v < -2147483648LL || v > 2147483647LL) return false;
+  *out = v;
+  return true;
+}
+
+const void *string_num_table(Session *s, size_t *n) {
+  std::lock_guard<std::mutex> lk(s->str_mu);
+  if (s->d_str_num_n != s->strings.size() || !s->d_str_num) {
+    const size_t m = std::max<size_t>(s->strings.size(), 1);
+    std::vector<uint8_t> buf(m * 17, 0);
+    double *f = (double *)buf.data();
+    int64_t *iv = (int64_t *)(buf.data() + 8 * m);
+    uint8_t *fl = buf.data() + 16 * m;
+    for (size_t i = 0; i < s->strings.size(); ++i) {
+      double d = 0;
+      int64_t v = 0;
+      if (parse_java_double(s->strings[i], &d)) f[i] = d, fl[i] |= 1;
+      if (parse_int32(s->strings[i], &v)) iv[i] = v, fl[i] |= 2;
+    }
+    s->d_str_num = s->alloc(buf.size());
+    HIP_CHECK(hipMemcpyAsync(s->d_str_num->p, buf.data(), buf.size(), hipMemcpyHostToDevice, s->stream));
+    s->sync();  // the pageable source
+    s->d_str_num_n = s->strings.size();
+  }
+  *n = s->d_str_num_n;
+  return s->d_str_num->p;
 }
 }  // namespace capf
 
@@ -1984,6 +2097,52 @@ capf_status capf_table_explode_values(capf_table *t, const char *name, int32_t t
   if (n > 0 && valid) HIP_CHECK(hipMemcpyAsync(v->valid->p, valid, n, hipMemcpyHostToDevice, s->stream));
   s->sync();  // pageable host sources
   nn->explode_values = v;
+  *out = wrap(nn);
+  CAPF_API_END
+}
+
+capf_status capf_table_add_list(capf_table *t, const char *name, int32_t elem_type, const int64_t *offsets,
+                                const void *values, const uint8_t *valid, capf_table **out) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(name, "name");
+  need(offsets, "offsets");
+  need(out, "out");
+  if (elem_type < CAPF_TYPE_INT64 || elem_type > CAPF_TYPE_STRING) illegal("bad list element type");
+  const NodePtr &c = t->node;
+  if (c->col_index(name) >= 0) illegal(std::string("column '") + name + "' already exists");
+  DataPtr d = materialize(c);
+  Session *s = c->s;
+  const int64_t n = d->nrows;
+  if (offsets[0] != 0) illegal("list offsets must start at 0");
+  for (int64_t i = 0; i < n; ++i)
+    if (offsets[i + 1] < offsets[i]) illegal("list offsets must not decrease");
+  const int64_t nv = offsets[n];
+  if (nv > 0 && !values) illegal("list values missing");
+  const Type et = (Type)elem_type;
+  auto child = make_column(s, et, nv, false);
+  if (nv > 0) HIP_CHECK(hipMemcpyAsync(child->data->p, values, type_width(et) * nv, hipMemcpyHostToDevice, s->stream));
+  auto lc = std::make_shared<Column>();
+  lc->type = Type::List;
+  lc->n = n;
+  lc->child = child;
+  lc->data = s->alloc(8 * (size_t)(n + 1));
+  HIP_CHECK(hipMemcpyAsync(lc->data->p, offsets, 8 * (size_t)(n + 1), hipMemcpyHostToDevice, s->stream));
+  if (valid && n > 0) {
+    lc->valid = s->alloc((size_t)n);
+    HIP_CHECK(hipMemcpyAsync(lc->valid->p, valid, (size_t)n, hipMemcpyHostToDevice, s->stream));
+  }
+  s->sync();  // pageable host sources
+  auto nn = new_node(s, Kind::Source);
+  nn->names = c->names;
+  nn->types = c->types;
+  nn->names.emplace_back(name);
+  nn->types.push_back(Type::List);
+  auto e = std::make_shared<Data>();
+  e->nrows = n;
+  e->cols = d->cols;
+  e->cols.push_back(lc);
+  nn->result = e;
   *out = wrap(nn);
   CAPF_API_END
 }

@@ -23,6 +23,8 @@ T_NULL, T_INT, T_FLOAT, T_BOOL, T_STRING, T_LIST = 0, 1, 2, 3, 4, 5
 CT_TO_CAPF = {
     "NULL": T_NULL, "INTEGER": T_INT, "FLOAT": T_FLOAT, "BOOLEAN": T_BOOL, "STRING": T_STRING,
     "NODE": T_INT, "RELATIONSHIP": T_INT, "ANY": T_NULL,
+    # CTList properties (LIST columns: int64 offsets + an element column)
+    "LIST(INTEGER)": T_LIST, "LIST(FLOAT)": T_LIST, "LIST(BOOLEAN)": T_LIST, "LIST(STRING)": T_LIST,
 }
 CAPF_TO_CT = {T_NULL: "NULL", T_INT: "INTEGER", T_FLOAT: "FLOAT", T_BOOL: "BOOLEAN", T_STRING: "STRING",
               T_LIST: "LIST"}
@@ -37,6 +39,7 @@ OP_STR_LEN, OP_LIST_SIZE, OP_IF = 60, 61, 62
 OP_ROUND, OP_ABS, OP_CEIL, OP_FLOOR, OP_SIGN, OP_SQRT, OP_LOG, OP_LOG10, OP_EXP = 70, 71, 72, 73, 74, 75, 76, 77, 78
 OP_SIN, OP_COS, OP_TAN, OP_ASIN, OP_ACOS, OP_ATAN, OP_DEGREES, OP_RADIANS = 79, 80, 81, 82, 83, 84, 85, 86
 OP_ATAN2, OP_TO_BOOLEAN, OP_IN_SET, OP_STR_MAP, OP_VALUE_MAP = 87, 88, 89, 90, 91
+OP_STR_TO_NUM, OP_RAND, OP_LIST_INDEX = 92, 93, 94
 IN_SET_MIN = 17  # list length from which IN runs as a session-set lookup (shorter: an OR of equalities)
 
 # aggregators
@@ -178,6 +181,12 @@ Subtract = _binary("Subtract", "-")
 Multiply = _binary("Multiply", "*")
 Divide = _binary("Divide", "/")
 Modulo = _binary("Modulo", "%")
+# lhs =~ rhs (okapi RegexMatch, Expr.scala:418): Cypher's whole-string Java
+# regex match.  Flink lowers it to child0.regexpExtract(child1)
+# (FlinkSQLExprMapper.scala:99) — a STRING, which a WHERE cannot take; the
+# backend evaluates the predicate the reference expectations pin
+# (ExpressionTests.scala:246-312, NullTests.scala:93).
+RegexMatch = _binary("RegexMatch", "=~")
 
 
 def _unary(name, fmt):
@@ -303,8 +312,18 @@ class Pi_(Expr):
         return "pi()"
 
 
+@dataclass(frozen=True)
+class Rand_(Expr):
+    """rand() (okapi Rand, FlinkSQLExprMapper.scala:207: Flink rand()): a
+    uniform double in [0, 1), drawn per row and per evaluation."""
+
+    def __str__(self):
+        return "rand()"
+
+
 E = E_()
 Pi = Pi_()
+Rand = Rand_()
 
 
 @dataclass(frozen=True)
@@ -450,6 +469,8 @@ def string_fn(key, sv):
         return _from_utf16(u[2 * (s1 - 1):2 * (e1 - 1)])
     if name == "replace":  # REGEXP_REPLACE(s, regex, replacement)
         return re.sub(key[1], lambda m: key[2], sv)
+    if name == "regex":  # s =~ pattern: 'true' / 'false' (then cast to BOOLEAN)
+        return "true" if re.fullmatch(key[1], sv) else "false"
     if name == "concat_r":  # s + literal
         return sv + key[1]
     if name == "concat_l":  # literal + s
@@ -458,6 +479,21 @@ def string_fn(key, sv):
 
 
 _STR_FUNCS = {"ToUpper": "upper", "ToLower": "lower", "Trim": "trim", "LTrim": "ltrim", "RTrim": "rtrim"}
+
+
+@dataclass(frozen=True)
+class ContainerIndex(Expr):
+    """container[index] (okapi ContainerIndex, Expr.scala:1240; Flink
+    `container.at(index)`, FlinkSQLExprMapper.scala:262-269) on a list: the
+    element at the 0-based index (negative from the end), NULL out of range —
+    Cypher's indexing, which the reference expectations pin
+    (ExpressionTests.scala:863-918).  Flink's ARRAY `at` is 1-based, so the
+    Flink path returns the next element (a hazard)."""
+    container: Expr
+    index: Expr
+
+    def __str__(self):
+        return f"{self.container}[{self.index}]"
 
 
 # labels(n) / keys(n) (FlinkSQLExprMapper.scala:136-153): a LIST of the label names
@@ -886,11 +922,13 @@ def _compile_program(expr, header, columns, params=None, intern=None, coltype=No
             return _value_type((params or {}).get(e.pname))
         if isinstance(e, (Var, ElementProperty)):  # no column: a NULL literal
             return T_NULL
-        if isinstance(e, (ToFloat,)) or type(e).__name__ in _FLOAT_FUNCS or isinstance(e, (E_, Pi_)):
+        if isinstance(e, (ToFloat,)) or type(e).__name__ in _FLOAT_FUNCS or isinstance(e, (E_, Pi_, Rand_)):
             return T_FLOAT
+        if type(e).__name__ in ("Labels", "Keys") and isinstance(e.expr, NullLit):
+            return T_NULL
         if isinstance(e, (ToInteger, Size, Id)):
             return T_INT
-        if isinstance(e, ToBoolean):
+        if isinstance(e, ToBoolean) or type(e).__name__ == "RegexMatch":
             return T_BOOL
         if type(e).__name__ in _STR_FUNCS or isinstance(e, (Substring, Replace, ToString)):
             return T_STRING
@@ -901,14 +939,30 @@ def _compile_program(expr, header, columns, params=None, intern=None, coltype=No
         return None
 
     def literal_value(x):
-        """(True, value) of a literal / parameter operand, else (False, None)."""
+        """(True, value) of a literal / parameter operand — string concatenations
+        of literals folded ('l' + 'l', FunctionTests.scala:480-487) — else
+        (False, None)."""
         if isinstance(x, (IntegerLit, FloatLit, StringLit, BoolLit)):
             return True, x.v
         if isinstance(x, NullLit):
             return True, None
         if isinstance(x, Param):
             return True, (params or {}).get(x.pname)
+        if type(x).__name__ == "Add":
+            la, va = literal_value(x.lhs)
+            lb, vb = literal_value(x.rhs)
+            if la and lb and (isinstance(va, str) or isinstance(vb, str)):
+                if va is None or vb is None:
+                    return True, None
+                if not all(isinstance(v, (str, int, float)) and not isinstance(v, bool) for v in (va, vb)):
+                    return False, None
+                return True, cypher_to_string(va) + cypher_to_string(vb)
         return False, None
+
+    def no_memo():
+        """The program depends on more than its lookups (rand()'s seed)."""
+        if isinstance(header, _Lookups):
+            header.cacheable = False
 
     def string_map(x, key):
         """f(x) for a STRING operand x: folded for a literal, else a code map."""
@@ -930,6 +984,55 @@ def _compile_program(expr, header, columns, params=None, intern=None, coltype=No
     def not_impl(what):
         from ._lib import NotImplementedException
         raise NotImplementedException(f"No support for converting Cypher expression {what} to a GPU expression")
+
+    def container_index(e):
+        """xs[i] (FlinkSQLExprMapper.scala:262-269), Cypher's 0-based indexing:
+        a literal / parameter list with a literal index folds; with a column
+        index it is a chain of IFs over the index values; a LIST column is
+        CAPF_OP_LIST_INDEX (the element type from the column)."""
+        from ._lib import IllegalArgumentException
+        isl, iv = literal_value(e.index)
+        if isl and (isinstance(iv, bool) or not isinstance(iv, (int, type(None)))):
+            raise IllegalArgumentException(f"a list index must be an INTEGER, got {e.index}")
+        vals = list_values(e.container, params) if isinstance(e.container, (ListLit, Param)) else None
+        if vals is not None:
+            kinds = {_value_type(v) for v in vals if v is not None}
+            if None in kinds:
+                not_impl(e)  # nested lists / maps
+            t = (T_FLOAT if kinds <= {T_INT, T_FLOAT} and T_FLOAT in kinds else
+                 kinds.pop() if len(kinds) == 1 else T_NULL if not kinds else None)
+            if t is None:
+                not_impl(e)  # a list of mixed types
+            conv = (lambda v: None if v is None else float(v)) if t == T_FLOAT else (lambda v: v)
+            n = len(vals)
+            if isl:
+                k = None if iv is None else (iv + n if iv < 0 else iv)
+                if k is None or not 0 <= k < n:
+                    emit(OP_LIT_NULL, t)
+                else:
+                    lit(conv(vals[k]))
+                return
+            emit(OP_LIT_NULL, t)  # acc: out of range
+            for k in reversed(range(n)):  # IF(i = k OR i = k − n, v_k, acc)
+                go(e.index)
+                lit(k)
+                emit(OP_EQ)
+                go(e.index)
+                lit(k - n)
+                emit(OP_EQ)
+                emit(OP_OR, 2)
+                lit(conv(vals[k]))
+                emit(OP_IF)
+            return
+        if isinstance(e.container, NullLit):
+            emit(OP_LIT_NULL, T_NULL)
+            return
+        c = column_of(e.container)
+        if c is None or static_type(e.container) != T_LIST or coltype is None:
+            not_impl(e)
+        et = coltype(("elem", c))
+        go(e.index)
+        emit(OP_LIST_INDEX, name_of(c), float(et))
 
     def go(e):
         cls = type(e).__name__
@@ -981,6 +1084,23 @@ def _compile_program(expr, header, columns, params=None, intern=None, coltype=No
                 go(e.lhs)
                 go(e.rhs)
                 emit(OP_VALUE_MAP, name_of(vmap("concat", (e.lhs, e.rhs))), 1.0)
+        elif cls == "RegexMatch":
+            # a code map of the dictionary: each string's match as 'true' / 'false',
+            # then the session's string → BOOLEAN table (CAPF_OP_TO_BOOLEAN)
+            okp, pat = literal_value(e.rhs)
+            if not okp or not isinstance(pat, (str, type(None))):
+                not_impl(e)  # a per-row pattern
+            if pat is None:
+                emit(OP_LIT_NULL, T_BOOL)
+                return
+            import re
+            try:
+                re.compile(pat)
+            except re.error as err:
+                from ._lib import IllegalArgumentException
+                raise IllegalArgumentException(f"invalid regular expression {pat!r}: {err}")
+            string_map(e.lhs, ("regex", pat))
+            emit(OP_TO_BOOLEAN)
         elif cls in _BIN_OPS:
             go(e.lhs)
             go(e.rhs)
@@ -1033,9 +1153,20 @@ def _compile_program(expr, header, columns, params=None, intern=None, coltype=No
                 emit(OP_VALUE_MAP, name_of(vmap("tostring", (e.expr,))), 0.0)
             else:
                 not_impl(e)
+        elif cls in ("ToFloat", "ToInteger") and static_type(e.expr) == T_STRING:
+            # CAST(string AS DOUBLE / INT) (FlinkSQLExprMapper.scala:182-183): the
+            # dictionary strings parsed once per session (a device table)
+            go(e.expr)
+            emit(OP_STR_TO_NUM, 1 if cls == "ToFloat" else 0)
+        elif cls in ("Labels", "Keys") and isinstance(e.expr, NullLit):
+            emit(OP_LIT_NULL, T_NULL)  # labels(null) / keys(null) is NULL (MTa/NullTests.scala:50, 53)
         elif cls in _UN_OPS:
             go(e.expr)
             emit(_UN_OPS[cls])
+        elif isinstance(e, Rand_):  # a fresh seed per compilation: never memoised
+            import os
+            no_memo()
+            emit(OP_RAND, int.from_bytes(os.urandom(8), "little") >> 1)
         elif isinstance(e, Ands):
             if not e.exprs:
                 emit(OP_LIT_BOOL, 1)
@@ -1058,6 +1189,9 @@ def _compile_program(expr, header, columns, params=None, intern=None, coltype=No
             go(e.expr)  # the id column (FlinkSQLExprMapper.scala:134)
         elif cls in ("StartNodeFunction", "EndNodeFunction"):
             v = e.expr  # header.startNodeFor / endNodeFor of the rel var (:179-180)
+            if isinstance(v, NullLit):
+                emit(OP_LIT_NULL, T_INT)  # startNode(null) is NULL (MTa/NullTests.scala:53-54)
+                return
             if not isinstance(v, Var):
                 not_impl(e)
             go(StartNode(v) if cls == "StartNodeFunction" else EndNode(v))
@@ -1095,6 +1229,9 @@ def _compile_program(expr, header, columns, params=None, intern=None, coltype=No
                 emit(OP_IF)
         elif isinstance(e, In):
             vals = list_values(e.rhs, params)
+            if vals is None and literal_value(e.rhs) == (True, None):
+                emit(OP_LIT_NULL, T_BOOL)  # x IN null: the rhs type is not a list (:117)
+                return
             if vals is None:
                 not_impl(e)
             if not vals:
@@ -1124,6 +1261,21 @@ def _compile_program(expr, header, columns, params=None, intern=None, coltype=No
                 emit(OP_EQ)
                 if k:
                     emit(OP_OR, 2)
+        elif isinstance(e, ContainerIndex):
+            container_index(e)
+        elif cls == "Size" and type(e.expr).__name__ in ("Labels", "Keys") and isinstance(e.expr.expr, Var):
+            # size(labels(n)) / size(keys(n)): the number of TRUE label flags /
+            # of property columns holding a value, summed per row
+            cols, kinds, _ = name_list_columns(e.expr, header, columns)
+            emit(OP_LIT_INT, 0)
+            for c, k in zip(cols, kinds):
+                emit(OP_LIT_INT, 0)  # else
+                col(c)
+                if k == 1:
+                    emit(OP_IS_NOT_NULL)
+                emit(OP_LIT_INT, 1)  # then
+                emit(OP_IF)
+                emit(OP_ADD)
         elif cls == "Size":
             x = e.expr
             vals = list_values(x, params) if isinstance(x, (ListLit, Param)) else None

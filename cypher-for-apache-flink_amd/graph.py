@@ -43,6 +43,12 @@ def ctype_of(v):
         return "FLOAT"
     if isinstance(v, str):
         return "STRING"
+    if isinstance(v, (list, tuple)):  # CTList: the join of the element types
+        et = None
+        for x in v:
+            if x is not None:
+                et = _join_type(et, ctype_of(x))
+        return f"LIST({et or 'INTEGER'})"
     raise NotImplementedError(f"property value {v!r} of type {type(v).__name__}")
 
 
@@ -53,6 +59,8 @@ def _join_type(a, b):
         return a
     if {a, b} == {"INTEGER", "FLOAT"}:
         return "FLOAT"
+    if {a, b} == {"LIST(INTEGER)", "LIST(FLOAT)"}:
+        return "LIST(FLOAT)"
     raise NotImplementedError(f"property with conflicting types {a} / {b}")
 
 
@@ -257,4 +265,6 @@ def _coerce(v, ct):
         return None
     if ct == "FLOAT":
         return float(v)
+    if ct == "LIST(FLOAT)":
+        return [None if x is None else float(x) for x in v]
     return v

@@ -605,7 +605,10 @@ def plan_stage(op: Planned, st: Stage, params=None, graph=None) -> Planned:
     adds, new_h = [], {}
     for alias, e in projs:
         owned = [x for x in h.owned_by(e) if x != e] if isinstance(e, Var) and e in h else []
-        v = Var(alias, e.ctype if isinstance(e, Var) else "ANY")
+        # startNode(r) / endNode(r) are CTNode (okapi Expr.scala): a node holding
+        # only the rel's start / end id column (FlinkSQLExprMapper.scala:179-180)
+        v = Var(alias, e.ctype if isinstance(e, Var) else
+                "NODE" if type(e).__name__ in ("StartNodeFunction", "EndNodeFunction") else "ANY")
         col = "__" + alias
         adds.append((e, col))
         new_h[v] = col

@@ -119,6 +119,13 @@ class GpuSession:
         """columns: list of (name, capf_type, values, valid-or-None).
 
         values: sequence of python values (None = NULL) or a numpy array."""
+        lists = [c for c in columns if c[1] == T_LIST]
+        if lists:  # CTList properties: the scalar columns first, then each LIST column
+            t = self.table([c for c in columns if c[1] != T_LIST],
+                           nrows=len(lists[0][2]) if nrows is None else nrows)
+            for name, _, values, valid in lists:
+                t = t.add_list(name, values, valid)
+            return t.select(*[c[0] for c in columns])
         names, types, datas, valids, keep = [], [], [], [], []
         n = nrows
         for name, t, values, valid in columns:
@@ -253,7 +260,7 @@ _SELECT_ARGS = {}
 
 def _program(expr, header, table, params):
     return compile_program(expr, header, set(table.physicalColumns), params, table.session.intern,
-                           table.capf_type, getattr(table.session, "literal_set", None),
+                           table._coltype, getattr(table.session, "literal_set", None),
                            getattr(table.session, "string_map", None),
                            lambda kind, exprs: table._value_map(kind, exprs, header, params))
 
@@ -290,6 +297,18 @@ class GpuTable:
         t = c_int32()
         _lib.call("capf_table_column_type", self._h, col.encode(), byref(t))
         return t.value
+
+    def _coltype(self, col):
+        """capf type of a column; ("elem", col): the element type of a LIST column."""
+        if isinstance(col, tuple):
+            return self.list_elem_type(col[1])
+        return self.capf_type(col)
+
+    def list_elem_type(self, col):
+        """Element type of a LIST column (capf_table_list_info: evaluates the table)."""
+        et, nv = c_int32(), c_int64()
+        _lib.call("capf_table_list_info", self._h, col.encode(), byref(et), byref(nv))
+        return et.value
 
     @property
     def columnType(self):
@@ -502,6 +521,34 @@ class GpuTable:
             raise _lib.NotImplementedException(f"UNWIND of {e.expr}")
         return self._new("capf_table_explode_list", self._h, src.encode(), col.encode())
 
+    def add_list(self, name, values, valid=None):
+        """This table plus LIST column `name` from host lists (None = a NULL
+        list): capf_table_add_list.  INTEGER and FLOAT elements widen to FLOAT
+        together; NULL elements are NotImplemented (LIST columns hold none)."""
+        kinds = set()
+        for xs in values:
+            for x in xs or ():
+                if x is None:
+                    raise _lib.NotImplementedException("NULL elements in a LIST property")
+                kinds.add(T_BOOL if isinstance(x, bool) else T_INT if isinstance(x, int) else
+                          T_FLOAT if isinstance(x, float) else T_STRING if isinstance(x, str) else None)
+        if None in kinds or len(kinds - {T_INT, T_FLOAT}) > (0 if kinds & {T_INT, T_FLOAT} else 1):
+            raise _lib.NotImplementedException(f"LIST property '{name}' of mixed or nested elements")
+        et = T_FLOAT if T_FLOAT in kinds else kinds.pop() if kinds else T_INT
+        offs = np.zeros(len(values) + 1, dtype=np.int64)
+        flat = []
+        for i, xs in enumerate(values):
+            flat += list(xs or ())
+            offs[i + 1] = len(flat)
+        if et == T_STRING:
+            data = np.array([self.session.intern(x) for x in flat], dtype=np.int64)
+        else:
+            data = np.array(flat, dtype=_NP_DTYPE[et]) if flat else np.zeros(1, dtype=_NP_DTYPE[et])
+        ok = np.array([xs is not None for xs in values], dtype=np.uint8) if valid is None else \
+            np.ascontiguousarray(np.asarray(valid, dtype=np.uint8))
+        return self._new("capf_table_add_list", self._h, name.encode(), int(et), offs.ctypes.data,
+                         data.ctypes.data, ok.ctypes.data if len(values) else None)
+
     def _value_map(self, kind, exprs, header, params):
         """Program name of a session value map (CAPF_OP_VALUE_MAP) giving the STRING
         of each distinct value (toString) or value pair (concatenation) the
@@ -542,10 +589,11 @@ class GpuTable:
         return "\x01vmap:%d" % mid.value
 
     def withColumns(self, *columns, header=None, params=None):
-        lists = [(e, c) for e, c in columns if type(e).__name__ in ("Labels", "Keys")]
+        is_list = lambda e: type(e).__name__ in ("Labels", "Keys") and type(e.expr).__name__ != "NullLit"  # noqa: E731
+        lists = [(e, c) for e, c in columns if is_list(e)]
         if lists:  # labels(n) / keys(n): LIST columns built by capf_table_name_list
             from .expr import name_list_columns
-            plain = [(e, c) for e, c in columns if type(e).__name__ not in ("Labels", "Keys")]
+            plain = [(e, c) for e, c in columns if not is_list(e)]
             t = self.withColumns(*plain, header=header, params=params) if plain else self
             for e, c in lists:
                 if not isinstance(e.expr, Var):

@@ -210,7 +210,22 @@ enum {
    * the key pair (x, y); NULL in or no entry → NULL.  The caller evaluated the
    * operands' distinct values, built their strings and interned them
    * (capf_session_value_map, "\x01vmap:<id>").                                */
-  CAPF_OP_VALUE_MAP = 91
+  CAPF_OP_VALUE_MAP = 91,
+  /* toFloat / toInteger of a STRING (FlinkSQLExprMapper.scala:182-183, CAST
+   * to DOUBLE / INT): pops a STRING code; iarg 1 pushes it parsed as a
+   * DOUBLE (Java Double.valueOf grammar after trim: decimal / exponent forms,
+   * NaN, Infinity, an f / d suffix), iarg 0 as an INTEGER (a decimal integer,
+   * a fractional part truncated, within 32 bits).  An unparsable string (or
+   * NULL) pushes NULL.  Uses the session's device table of parsed strings.   */
+  CAPF_OP_STR_TO_NUM = 92,
+  /* rand() (:207): pushes a uniform DOUBLE in [0, 1) — splitmix64 of
+   * (iarg seed, row); the caller draws a fresh seed per evaluation.          */
+  CAPF_OP_RAND = 93,
+  /* xs[i] on a LIST column (ContainerIndex, :262-269): pops an INTEGER i;
+   * pushes element i of the row's list in LIST column names[iarg] (i < 0
+   * counts from the end); NULL for a NULL list, a NULL index or an index out
+   * of range.  farg = the element's capf type (CAPF_TYPE_*).                 */
+  CAPF_OP_LIST_INDEX = 94
 };
 
 typedef struct capf_expr {
@@ -620,6 +635,15 @@ capf_status capf_session_literal_set(capf_session *s, const int64_t *values, int
  * function on the host with the JVM's string semantics and interns the
  * results; the map is referenced in programs as "\x01map:<id>" (*map_id).  */
 capf_status capf_session_code_map(capf_session *s, const int64_t *codes, int64_t n, int32_t *map_id);
+/* A LIST property column from host data (CTList properties of element tables,
+ * CAPFElementTable.create / FlinkConversions.scala:43-117 map CTList to an
+ * ARRAY column): appends LIST column `name` to t's rows (t is materialised):
+ * row i holds values[offsets[i] .. offsets[i + 1]) (offsets: size + 1 int64,
+ * offsets[0] = 0), elements of capf type elem_type (INTEGER / FLOAT / BOOLEAN
+ * / STRING codes, 8 B each, BOOLEAN 1 B; no NULL elements); valid (size
+ * bytes or NULL): 0 = a NULL list.                                         */
+capf_status capf_table_add_list(capf_table *t, const char *name, int32_t elem_type, const int64_t *offsets,
+                                const void *values, const uint8_t *valid, capf_table **out);
 /* labels(n) / keys(n) (FlinkSQLExprMapper.scala:136-153; the GetLabels /
  * GetKeys UDFs, :310-329): appends LIST<STRING> column `name` holding, per row,
  * codes[j] for each column cols[j] that holds TRUE (kinds[j] = 0, a label flag)

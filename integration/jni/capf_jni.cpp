@@ -514,6 +514,22 @@ JNI(jlong, tableExplodeList)(JNIEnv *env, jobject, jlong t, jstring list_col, js
   capf_table *out = nullptr;
   return fail(env, capf_table_explode_list(T(t), l.p, nm.p, &out)) ? 0 : H(out);
 }
+// a LIST property column (CTList) from direct buffers: offsets (size + 1 int64),
+// element values (8 B, BOOLEAN 1 B), list validity (size bytes) or null
+JNI(jlong, tableAddList)(JNIEnv *env, jobject, jlong t, jstring name, jint elem_type, jobject offsets,
+                         jobject values, jobject valid) {
+  JStr nm(env, name);
+  if (!offsets || !direct(env, offsets)) {
+    illegal_argument(env, "tableAddList: offsets must be a direct buffer");
+    return 0;
+  }
+  capf_table *out = nullptr;
+  return fail(env, capf_table_add_list(T(t), nm.p, elem_type, (const int64_t *)direct(env, offsets),
+                                       values ? direct(env, values) : nullptr,
+                                       valid ? (const uint8_t *)direct(env, valid) : nullptr, &out))
+             ? 0
+             : H(out);
+}
 // labels(n) / keys(n) (FlinkSQLExprMapper.scala:136-153): a LIST<STRING> column
 JNI(jlong, tableNameList)(JNIEnv *env, jobject, jlong t, jobjectArray cols, jintArray kinds, jlongArray codes,
                           jstring name) {

@@ -137,6 +137,9 @@ object Native {
   @native def tableExplodeValues(table: Long, name: String, elemType: Int, n: Long, values: java.nio.ByteBuffer,
                                  valid: java.nio.ByteBuffer): Long
   @native def tableExplodeList(table: Long, listCol: String, name: String): Long
+  // a LIST property column (CTList) from direct buffers: offsets, element values, list validity
+  @native def tableAddList(table: Long, name: String, elemType: Int, offsets: java.nio.ByteBuffer,
+                           values: java.nio.ByteBuffer, valid: java.nio.ByteBuffer): Long
   @native def tableNameList(table: Long, cols: Array[String], kinds: Array[Int], codes: Array[Long], name: String): Long
   @native def tableShow(table: Long, rows: Int): Unit
 

@@ -73,8 +73,15 @@ class _P:
         if k == "name" and v.upper() in ("NULL", "TRUE", "FALSE"):
             self.i += 1
             return {"NULL": None, "TRUE": True, "FALSE": False}[v.upper()]
-        if k == "sym" and v == "[":
-            raise NotImplementedError("list property values")
+        if k == "sym" and v == "[":  # a list property value (CTList)
+            self.i += 1
+            out = []
+            while self.peek() != ("sym", "]"):
+                out.append(self.value())
+                if self.peek() == ("sym", ","):
+                    self.take()
+            self.take("sym", "]")
+            return out
         raise ValueError(f"bad value {self.peek()}")
 
     def props(self):

@@ -106,6 +106,10 @@ class OracleSession:
             ok = np.array([x is not None for x in lst], dtype=bool) if valid is None else np.asarray(valid, bool)
             if t == T_STRING:
                 v = np.array(lst, dtype=object)
+            elif t == T_LIST:  # one Python list per row (np.array would build a 2-D array)
+                v = np.empty(m, dtype=object)
+                for i, x in enumerate(lst):
+                    v[i] = list(x) if x is not None else []
             elif t == T_NULL:
                 v = np.zeros(m, dtype=np.int64)
                 ok = np.zeros(m, dtype=bool)
@@ -260,6 +264,52 @@ def evaluate(e, table, header, params):
         if name == "Negate":
             a = go(x.expr)
             return Val(a.t, -a.v, a.ok)
+        if name in ("ToFloat", "ToInteger") and x.expr is not None:
+            a = go(x.expr)
+            if a.t == T_STRING:  # CAST(string AS DOUBLE / INT): see _parse_double / _parse_int
+                f = _parse_double if name == "ToFloat" else _parse_int
+                vals = [f(v) if ok else None for v, ok in zip(a.v, a.ok)]
+                t = T_FLOAT if name == "ToFloat" else T_INT
+                return Val(t, np.array([0 if v is None else v for v in vals], dtype=_NP[t]),
+                           np.array([v is not None for v in vals], bool))
+        if name == "ContainerIndex":  # xs[i], 0-based, negative from the end, NULL out of range
+            ix = go(x.index)
+            lits = list_values(x.container, params) if isinstance(x.container, (ListLit, Param)) else None
+            if lits is not None:
+                rows = [lits] * n
+                okc = np.ones(n, bool)
+            else:
+                c = go(x.container)
+                if c.t == T_NULL:
+                    return const(T_NULL, None, False)
+                if c.t != T_LIST:
+                    raise NotImplementedError(f"oracle: index into {CAPF_TO_CT[c.t]}")
+                rows, okc = list(c.v), c.ok
+            elems = [v for r in rows for v in r if v is not None]
+            t = (T_FLOAT if any(isinstance(v, float) for v in elems) else
+                 T_BOOL if elems and isinstance(elems[0], bool) else
+                 T_STRING if elems and isinstance(elems[0], str) else T_INT if elems else T_NULL)
+            out, ok = [], []
+            for r, rok, i, iok in zip(rows, okc, ix.v, ix.ok):
+                k = int(i) + len(r) if iok and int(i) < 0 else int(i)
+                hit = bool(rok and iok and 0 <= k < len(r) and r[k] is not None)
+                v = r[k] if hit else None
+                out.append(float(v) if hit and t == T_FLOAT else v)
+                ok.append(hit)
+            if t == T_STRING:
+                return Val(t, np.array(out, dtype=object), np.array(ok, bool))
+            return Val(t, np.array([0 if v is None else v for v in out], dtype=_NP[t]), np.array(ok, bool))
+        if name == "RegexMatch":  # whole-string regex match (Java String.matches)
+            a, pt = go(x.lhs), go(x.rhs)
+            if a.t not in (T_STRING, T_NULL) or pt.t not in (T_STRING, T_NULL):
+                raise NotImplementedError("oracle: =~ of non-strings")
+            hit = [bool(ao and po and re.fullmatch(p_, v) is not None)
+                   for v, p_, ao, po in zip(a.v, pt.v, a.ok, pt.ok)]
+            return Val(T_BOOL, np.array(hit, bool), a.ok & pt.ok)
+        if name == "Rand_":  # rand(): uniform in [0, 1) per row
+            return Val(T_FLOAT, np.random.default_rng().random(n), np.ones(n, bool))
+        if name in ("Labels", "Keys") and isinstance(x.expr, NullLit):
+            return const(T_NULL, None, False)
         if name == "ToFloat":
             a = go(x.expr)
             if a.t == T_BOOL:
@@ -298,6 +348,9 @@ def evaluate(e, table, header, params):
             return Val(T_BOOL, a.ok.copy(), np.ones(n, bool))
         if name == "In":  # SQL IN over a literal / parameter list (:114-118)
             items = list_values(x.rhs, params)
+            if items is None and (isinstance(x.rhs, NullLit) or
+                                  (isinstance(x.rhs, Param) and params.get(x.rhs.pname) is None)):
+                return const(T_BOOL, None, False)  # x IN null (MTa/NullTests.scala:98)
             if items is None:
                 raise NotImplementedError(f"oracle: IN over {x.rhs}")
             if not items:
@@ -457,6 +510,42 @@ def evaluate(e, table, header, params):
 # upperCase / lowerCase, SQL TRIM of the space character
 _STR1 = {"ToUpper": str.upper, "ToLower": str.lower, "Trim": lambda v: v.strip(" "),
          "LTrim": lambda v: v.lstrip(" "), "RTrim": lambda v: v.rstrip(" ")}
+
+
+_DOUBLE_RE = re.compile(r"[+-]?(NaN|Infinity|((\d+\.?\d*|\.\d+)([eE][+-]?\d+)?)[fFdD]?)")
+_INT_RE = re.compile(r"[+-]?\d+(\.\d*)?")
+
+
+def _jtrim(v):
+    """java.lang.String.trim: strip chars <= ' '."""
+    b, e = 0, len(v)
+    while b < e and v[b] <= " ":
+        b += 1
+    while e > b and v[e - 1] <= " ":
+        e -= 1
+    return v[b:e]
+
+
+def _parse_double(v):
+    """toFloat(string): Double.valueOf(s.trim()) — decimal / exponent forms,
+    NaN, Infinity, an optional f / d suffix; anything else NULL (Flink's CAST
+    throws there, the reference expectation is NULL: FunctionTests.scala)."""
+    t = _jtrim(v)
+    if not _DOUBLE_RE.fullmatch(t):
+        return None
+    t = t.rstrip("fFdD") if t[-1:] in "fFdD" and "Infinity" not in t else t
+    return float(t.replace("Infinity", "inf"))
+
+
+def _parse_int(v):
+    """toInteger(string): the decimal integer, a fractional part truncated
+    ('82.9' -> 82, FunctionTests.scala:1117-1127), NULL when unparsable or
+    outside INT (32 bit: Flink casts to INT, FlinkSQLExprMapper.scala:183)."""
+    t = _jtrim(v)
+    if not _INT_RE.fullmatch(t):
+        return None
+    r = int(t.split(".")[0])
+    return r if -2 ** 31 <= r < 2 ** 31 else None
 
 
 def _substring(v, frm, ln):

@@ -86,6 +86,10 @@ def check_case(got, expected, opts, reference=True):
     reference=False (backend against oracle): typed, always."""
     if "row_count" in opts:
         return len(got) == opts["row_count"]
+    if "rand" in opts:  # rand(): one FLOAT per row in [0, 1) (FunctionTests.scala:1422-1429)
+        col = opts["rand"]
+        return len(got) == len(expected) and all(
+            isinstance(r[col], float) and 0.0 <= r[col] < 1.0 for r in got)
     coop = reference and bool(opts.get("coop")) and not opts.get("typed")
     if opts.get("ordered"):
         return [bag([r], coop) for r in got] == [bag([r], coop) for r in expected]

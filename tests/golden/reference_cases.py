@@ -807,3 +807,14 @@ def _stat_cases():
 
 STAT_CASES = _stat_cases()
 CASES = CASES + STAT_CASES
+
+
+# ------------------------------------------ FunctionTests (MTa), VERDICT r5 item 3
+from function_cases import FUNCTION_CASES  # noqa: E402
+
+CASES = CASES + FUNCTION_CASES
+
+# ----------------------- NullTests / ExpressionTests (MTa), VERDICT r5 items 3, 7
+from expression_cases import EXPRESSION_CASES  # noqa: E402
+
+CASES = CASES + EXPRESSION_CASES

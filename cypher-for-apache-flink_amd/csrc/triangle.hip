@@ -1125,6 +1125,15 @@ static void tri_build(Session *s, const ColView &src, const ColView &dst, int64_
 // galloping batch-owner search, an LDS bitmap pre-filter, relabelling the CSR
 // by degree rank, larger grabs (4/4 319 ms … 128/32 720 ms).
 constexpr int TRI_WPE = 8, TRI_GRAB_A = 2, TRI_GRAB_B = 4;
+// CAPF_TRI_ILP=3 (A/B of the spill trade-off): ILP 3 compiles the two count
+// kernels with 24 / 48 B per lane of scratch against 56 / 80 B at ILP 4
+static int tri_ilp() {
+  static const int v = [] {
+    const char *e = getenv("CAPF_TRI_ILP");
+    return e && atoi(e) == 3 ? 3 : TRI_ILP;
+  }();
+  return v;
+}
 
 // Device count (int64 at d_out) of the directed triangle over rels (src, dst)
 // with endpoints in [lo, lo + len), restricted to part `part` of `parts`
@@ -1176,7 +1185,8 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
     if (g.pcols) {  // node ids < 2^24: packed words, pass A q-tiled + pass B
       if (g.naitems > 0) {
         KernelTimer kt(s, "tri_count_qtiled", 4.0 * g.P);
-        hipLaunchKernelGGL((k_tri_count_qtiled<TRI_ILP, TRI_WPE>), dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK),
+        auto kq = tri_ilp() == 3 ? k_tri_count_qtiled<3, TRI_WPE> : k_tri_count_qtiled<TRI_ILP, TRI_WPE>;
+        hipLaunchKernelGGL(kq, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK),
                            0, s->stream, (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
                            (const uint2 *)g.vals->p, (const uint2 *)g.erow->p, (const uint4 *)g.aitems->p,
                            g.naitems, parts, part, TRI_GRAB_A, TRI_XCHUNK, xa, acc);
@@ -1192,7 +1202,8 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
         KernelTimer kt(s, "tri_count_passb", 4.0 * g.P);
         TriPassB b{(const uint32_t *)g.in_words->p, (const uint2 *)g.in_rows->p, (const uint32_t *)g.in_eidx->p,
                    (const uint4 *)g.items->p, g.nitems};
-        hipLaunchKernelGGL((k_tri_count_passb<TRI_ILP, TRI_WPE>), dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK),
+        auto kb = tri_ilp() == 3 ? k_tri_count_passb<3, TRI_WPE> : k_tri_count_passb<TRI_ILP, TRI_WPE>;
+        hipLaunchKernelGGL(kb, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK),
                            0, s->stream, (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
                            (const uint2 *)g.vals->p, b, parts, part, TRI_GRAB_B, 0, acc + 6, acc);
         KERNEL_CHECK();

@@ -226,6 +226,9 @@ class DistSession:
     def __init__(self, local_session, exchange):
         self.local = local_session
         self.ex = exchange
+        # value maps (toString / concatenation of columns) intern the union of
+        # every rank's values: the ranks' string dictionaries stay equal
+        local_session.value_map_gather = exchange.all_gather_obj
         self.world = exchange.world
         self.rank = exchange.rank
         # deferred inner joins over base shards (set by dist_node_partitioned_graph)

@@ -496,6 +496,30 @@ class ContainerIndex(Expr):
         return f"{self.container}[{self.index}]"
 
 
+@dataclass(frozen=True)
+class MapExpression(Expr):
+    """{k1: e1, k2: e2, …} (okapi MapExpression, Expr.scala:511; Flink
+    MapConstructor, FlinkSQLExprMapper.scala:271-278).  A MAP value is held as
+    a struct of columns: the planner projects one column per entry plus a
+    presence flag (planner.py `_map_entries`); `m.k` / `m['k']` read the
+    entry's column (ElementProperty on the MAP variable), records() rebuilds
+    the Python dict."""
+    items: Tuple[Tuple[str, Expr], ...]
+
+    def __init__(self, items=()):
+        pairs = items.items() if isinstance(items, dict) else items
+        object.__setattr__(self, "items", tuple((str(k), v) for k, v in pairs))
+
+    def __str__(self):
+        return "{" + ", ".join(f"{k}: {v}" for k, v in self.items) + "}"
+
+
+# properties(x) (okapi Properties, Expr.scala:851; FlinkSQLExprMapper.scala:167-177):
+# the MAP of a node's / relationship's property columns (every key of its
+# header, NULL values included), or a MAP itself
+Properties = _unary("Properties", "properties({})")
+
+
 # labels(n) / keys(n) (FlinkSQLExprMapper.scala:136-153): a LIST of the label names
 # whose flag column is TRUE / of the property keys holding a value, sorted by
 # name — a table operation (capf_table_name_list), as a withColumns item only
@@ -1026,6 +1050,16 @@ def _compile_program(expr, header, columns, params=None, intern=None, coltype=No
             return
         if isinstance(e.container, NullLit):
             emit(OP_LIT_NULL, T_NULL)
+            return
+        if isinstance(e.container, Var) and e.container.ctype == "MAP":
+            # m['k'] on a MAP held as a struct of columns: the entry's column
+            okk, key = literal_value(e.index)
+            if not okk or not isinstance(key, (str, type(None))):
+                not_impl(e)  # a per-row key
+            if key is None:
+                emit(OP_LIT_NULL, T_NULL)
+            else:
+                go(ElementProperty(e.container, key))
             return
         c = column_of(e.container)
         if c is None or static_type(e.container) != T_LIST or coltype is None:

@@ -592,6 +592,29 @@ def _split_aggregates(st: Stage) -> Stage:
     return first, second
 
 
+def _map_entries(e, h):
+    """(presence expression, [(key, expression)]) of a MAP-valued projection
+    item — a map literal (MapExpression) or properties(x) — else None.
+    properties(n) of an element lists every property key of its header (NULL
+    values included, ExpressionTests.scala:1289-1333); of NULL it is NULL."""
+    from .expr import BoolLit, IsNotNull, MapExpression, NullLit
+    from ._lib import NotImplementedException
+    if isinstance(e, MapExpression):
+        for k, x in e.items:
+            if isinstance(x, MapExpression) or type(x).__name__ == "Properties":
+                raise NotImplementedException(f"nested maps: {e}")
+        return BoolLit(True), list(e.items)
+    if type(e).__name__ != "Properties":
+        return None
+    x = e.expr
+    if isinstance(x, NullLit):
+        return NullLit("BOOLEAN"), []
+    if isinstance(x, Var) and x in h:
+        props = sorted(((p.key, p) for p in h.owned_by(x) if isinstance(p, ElementProperty)), key=lambda kp: kp[0])
+        return IsNotNull(x), props
+    raise NotImplementedException(f"properties of {x}")
+
+
 def plan_stage(op: Planned, st: Stage, params=None, graph=None) -> Planned:
     split = _split_aggregates(st)
     if split is not None:
@@ -604,6 +627,17 @@ def plan_stage(op: Planned, st: Stage, params=None, graph=None) -> Planned:
     h = op.header
     adds, new_h = [], {}
     for alias, e in projs:
+        me = _map_entries(e, h)
+        if me is not None:  # a MAP value: a presence flag plus one column per entry
+            present, entries = me
+            v = Var(alias, "MAP")
+            adds.append((present, "__" + alias))
+            new_h[v] = "__" + alias
+            for k, x in entries:
+                c = f"__{alias}.{k}"
+                adds.append((x, c))
+                new_h[ElementProperty(v, k)] = c
+            continue
         owned = [x for x in h.owned_by(e) if x != e] if isinstance(e, Var) and e in h else []
         # startNode(r) / endNode(r) are CTNode (okapi Expr.scala): a node holding
         # only the rel's start / end id column (FlinkSQLExprMapper.scala:179-180)
@@ -756,7 +790,13 @@ def records(op: Planned, aliases: Sequence[str]):
     out_cols = {}
     for a in aliases:
         v = next((e for e in op.header.vars() if e.vname == a), Var(a))
-        if v.ctype in ("NODE", "RELATIONSHIP") and len(op.header.owned_by(v)) >= 1:
+        if v.ctype == "MAP":  # a struct of columns: presence flag + one column per entry
+            present = data(op.header.column(v))
+            ents = [(x.key, data(op.header.column(x))) for x in op.header.owned_by(v)
+                    if isinstance(x, ElementProperty)]
+            out_cols[a] = [None if p is None else {k: vals[i] for k, vals in ents}
+                           for i, p in enumerate(present)]
+        elif v.ctype in ("NODE", "RELATIONSHIP") and len(op.header.owned_by(v)) >= 1:
             out_cols[a] = _element_values(op, v, data)
         else:
             out_cols[a] = data(op.header.column(v))

@@ -565,6 +565,13 @@ class GpuTable:
             raise _lib.NotImplementedException(
                 f"a new string per value over {t.size} distinct values (more than {VALUE_MAP_MAX})")
         cols = [t.column_values(c) for c in names]
+        rows = sorted({r for r in zip(*cols) if not any(v is None for v in r)})
+        gather = getattr(self.session, "value_map_gather", None)
+        if gather is not None:
+            # distributed (dist_table.DistSession): every rank interns the union
+            # of all ranks' values in one order, so the string dictionaries stay
+            # equal and STRING codes can cross ranks
+            rows = sorted({r for part in gather(rows) for r in part})
 
         def key(v, ty):
             if ty == T_FLOAT:
@@ -574,9 +581,7 @@ class GpuTable:
             return int(v)
 
         entries = []
-        for vals in zip(*cols):
-            if any(v is None for v in vals):
-                continue
+        for vals in rows:
             txt = "".join(cypher_to_string(float(v) if ty == T_FLOAT else v) for v, ty in zip(vals, types))
             entries.append((tuple(key(v, ty) for v, ty in zip(vals, types)), self.session.intern(txt)))
         entries.sort()

@@ -40,6 +40,8 @@ object GpuExprMapper {
   private final val Degrees_ = 85; private final val Radians_ = 86; private final val Atan2_ = 87
   private final val ToBoolean_ = 88; private final val InSet = 89; private final val StrMap = 90
   private final val ValueMap = 91
+  // round 6: string → number casts, rand(), xs[i] on LIST columns
+  private final val StrToNum = 92; private final val Rand_ = 93; private final val ListIndex = 94
   private final val InSetMin = 17  // IN lists from this length: one set lookup per row (expr.py IN_SET_MIN)
 
   def program(expr: Expr, header: RecordHeader, table: GpuTable, parameters: CypherMap): Program = {
@@ -175,8 +177,22 @@ object GpuExprMapper {
       case Subtract(l, r) => go(l); go(r); emit(Sub)
       case Multiply(l, r) => go(l); go(r); emit(Mul)
       case Divide(l, r) => go(l); go(r); emit(Div)
+      case ToFloat(x) if isString(x) => go(x); emit(StrToNum, 1L)         // CAST(string AS DOUBLE) (:182)
+      case ToInteger(x) if isString(x) => go(x); emit(StrToNum, 0L)       // CAST(string AS INT) (:183)
       case ToFloat(x) => go(x); emit(ToFloat_)
       case ToInteger(x) => go(x); emit(ToInteger_)                          // Flink: INT (FlinkSQLExprMapper.scala:183)
+      case Rand => emit(Rand_, scala.util.Random.nextLong() >>> 1)          // :207, a fresh seed per program
+      case RegexMatch(l, r) =>                                             // :99 — the predicate, not regexpExtract
+        literal(r) match {
+          case Some(CypherNull) => emit(LitNull, Native.TypeBool)
+          case Some(CypherString(pat)) => stringMap(l, Seq("regex", pat)); emit(ToBoolean_)
+          case _ => throw NotImplementedException(s"GPU =~ with a per-row pattern $e")
+        }
+      case ContainerIndex(c, i) if c.cypherType.material.isInstanceOf[CTList] && physical(c).isDefined =>
+        // xs[i] on a LIST column (:262-269), 0-based as the reference expectations
+        // (Flink's ARRAY `at` is 1-based); farg = the element type
+        val elem = GpuTypes.fromCypher(c.cypherType.material.asInstanceOf[CTList].inner)
+        go(i); emit(ListIndex, nameIndex(physical(c).get), elem.toDouble)
       case Coalesce(xs) => xs.foreach(go); emit(Coalesce_, xs.size.toLong)
       case Id(x) => go(x)                                                  // FlinkSQLExprMapper.scala:134
       case Exists(x) => go(x); emit(IsNotNull_)                            // :90
@@ -228,6 +244,7 @@ object GpuExprMapper {
         case None => throw NotImplementedException(s"GPU endNode of $x")
       }
       case ToBoolean(x) => go(x); emit(ToBoolean_)                        // :185
+      case Labels(NullLit(_)) | Keys(NullLit(_)) => emit(LitNull, Native.TypeNull)
       case E => emit(LitFloat, 0L, math.E)                                // :196
       case Pi => emit(LitFloat, 0L, math.Pi)                              // :197
       case Sqrt(x) => go(x); emit(Sqrt_)                                  // :199-221

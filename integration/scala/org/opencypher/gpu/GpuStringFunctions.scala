@@ -17,6 +17,7 @@ object GpuStringFunctions {
     case Seq("rtrim") => Some(trimSpaces(s, leading = false, trailing = true))
     case Seq("substring", from: Long, len: Long) => Some(substring(s, from, len))
     case Seq("replace", regex: String, replacement: String) => Some(s.replaceAll(regex, replacement))
+    case Seq("regex", pattern: String) => Some(if (s.matches(pattern)) "true" else "false")  // s =~ pattern
     case Seq("concat_r", lit: String) => Some(s + lit)
     case Seq("concat_l", lit: String) => Some(lit + s)
     case other => throw new IllegalArgumentException(s"unknown string function $other")

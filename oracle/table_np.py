@@ -272,6 +272,13 @@ def evaluate(e, table, header, params):
                 t = T_FLOAT if name == "ToFloat" else T_INT
                 return Val(t, np.array([0 if v is None else v for v in vals], dtype=_NP[t]),
                            np.array([v is not None for v in vals], bool))
+        if name == "ContainerIndex" and isinstance(x.container, Var) and x.container.ctype == "MAP":
+            # m[key] on a MAP held as a struct of columns: the entry's column
+            key = x.index.v if isinstance(x.index, StringLit) else (
+                params.get(x.index.pname) if isinstance(x.index, Param) else None)
+            if key is None and not isinstance(x.index, (StringLit, Param, NullLit)):
+                raise NotImplementedError("oracle: a per-row map key")
+            return go(ElementProperty(x.container, key)) if key is not None else const(T_NULL, None, False)
         if name == "ContainerIndex":  # xs[i], 0-based, negative from the end, NULL out of range
             ix = go(x.index)
             lits = list_values(x.container, params) if isinstance(x.container, (ListLit, Param)) else None

@@ -9,7 +9,7 @@ HasLabel.
 Not transcribed from NullTests (no Flink mapping: FlinkSQLExprMapper.scala
 raises NotImplemented for StartsWith / EndsWith / Contains :96-98, and has no
 case for head / last / tail / split / reverse / range): :55-57, :62-63, :89-91,
-:107; properties(null) (:69) is below with the MAP support.
+:107.
 """
 import capf_import  # noqa: F401
 from capf_amd.expr import (Abs, Acos, Add, Ands, Asin, Atan, Atan2, Avg, BoolLit, Ceil, Collect, ContainerIndex, Cos,
@@ -106,16 +106,60 @@ def _container_index_cases():
     v1 = ElementProperty(Var("n", "NODE"), "v1")
     g = "CREATE ({v1: [1, 2, 3]})"
     ints = lambda *xs: ListLit(*[IntegerLit(x) for x in xs])  # noqa: E731
+    # local_only: a LIST property column is not routed between ranks by the
+    # distributed layer (capf_table_hash_route)
+    lo = {"local_only": True}
     return [
         ("expr_index_literal", ET + "864-879", g,
-         Query([Match([NodeP("n")])], [ret(("val", ContainerIndex(v1, IntegerLit(1))))]), [{"val": 2}]),
+         Query([Match([NodeP("n")])], [ret(("val", ContainerIndex(v1, IntegerLit(1))))]), [{"val": 2}], lo),
         ("expr_index_expression", ET + "881-898", g,
          Query([Match([NodeP("n")]), Unwind(ints(0, 1, 2), "i")], [ret(("val", ContainerIndex(v1, Var("i"))))]),
-         [{"val": 1}, {"val": 2}, {"val": 3}]),
+         [{"val": 1}, {"val": 2}, {"val": 3}], lo),
         ("expr_index_out_of_bounds", ET + "900-917", g,
          Query([Match([NodeP("n")]), Unwind(ints(3, 4, 5), "i")], [ret(("val", ContainerIndex(v1, Var("i"))))]),
-         [{"val": None}, {"val": None}, {"val": None}]),
+         [{"val": None}, {"val": None}, {"val": None}], lo),
     ]
 
 
-EXPRESSION_CASES = _null_cases() + _regex_cases() + _container_index_cases()
+def _map_cases():
+    """MAP values as a struct of columns (planner._map_entries); properties(x)
+    of an element lists every property key (NULL values included).  Flink
+    lowers properties(n) to an ARRAY of the property columns
+    (FlinkSQLExprMapper.scala:167-173) — a hazard; MapConstructor matches."""
+    from capf_amd.expr import MapExpression, Param, Properties
+    m = Var("myMap", "MAP")
+    mk = MapExpression([("foo", StringLit("bar")), ("baz", IntegerLit(42))])
+    with_map = lambda *items: Query([], [ret(("myMap", mk)), ret(*items)])  # noqa: E731
+    props = lambda v, rel=False: Query(  # noqa: E731
+        [Match([NodeP("a", ("A",))])] if not rel else
+        [Match([NodeP("_x"), NodeP("_y")], [RelP("rel", "_x", "_y", ("REL",))])],
+        [ret(("props", Properties(Var(v, "RELATIONSHIP" if rel else "NODE"))))])
+    return [
+        ("expr_properties_nodes", ET + "1290-1309",
+         'CREATE (:A {val1: "foo", val2: 42}) CREATE (:A {val1: "bar", val2: 21}) CREATE (:A)', props("a"),
+         [{"props": {"val1": "foo", "val2": 42}}, {"props": {"val1": "bar", "val2": 21}},
+          {"props": {"val1": None, "val2": None}}]),
+        ("expr_properties_rels", ET + "1311-1331",
+         'CREATE (a), (b) CREATE (a)-[:REL {val1: "foo", val2: 42}]->(b) CREATE (a)-[:REL {val1: "bar", val2: 21}]->(b) '
+         'CREATE (a)-[:REL]->(b)', props("rel", rel=True),
+         [{"props": {"val1": "foo", "val2": 42}}, {"props": {"val1": "bar", "val2": 21}},
+          {"props": {"val1": None, "val2": None}}]),
+        ("null_69", NT + "69", "", unit(("res", Properties(NL))), [{"res": None}]),
+        ("expr_map_static", ET + "1359-1371", "", unit(("myMap", mk)), [{"myMap": {"foo": "bar", "baz": 42}}]),
+        ("expr_map_expression_values", ET + "1373-1384", "",
+         Query([Unwind(ListLit(IntegerLit(21), IntegerLit(42)), "value")],
+               [ret(("myMap", MapExpression([("foo", Var("value"))])))]),
+         [{"myMap": {"foo": 21}}, {"myMap": {"foo": 42}}]),
+        ("expr_map_empty", ET + "1406-1416", "", unit(("myMap", MapExpression())), [{"myMap": {}}]),
+        ("expr_map_literal_key", ET + "1420-1433", "",
+         with_map(("foo", ContainerIndex(m, StringLit("foo"))), ("baz", ContainerIndex(m, StringLit("baz")))),
+         [{"foo": "bar", "baz": 42}]),
+        ("expr_map_missing_key", ET + "1435-1448", "", with_map(("barbaz", ContainerIndex(m, StringLit("barbaz")))),
+         [{"barbaz": None}]),
+        ("expr_map_param_key", ET + "1450-1463", "",
+         with_map(("foo", ContainerIndex(m, Param("fooKey"))), ("baz", ContainerIndex(m, Param("bazKey")))),
+         [{"foo": "bar", "baz": 42}], {"params": {"fooKey": "foo", "bazKey": "baz"}}),
+    ]
+
+
+EXPRESSION_CASES = _null_cases() + _regex_cases() + _container_index_cases() + _map_cases()

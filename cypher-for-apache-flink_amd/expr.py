@@ -1015,6 +1015,16 @@ def _compile_program(expr, header, columns, params=None, intern=None, coltype=No
         index it is a chain of IFs over the index values; a LIST column is
         CAPF_OP_LIST_INDEX (the element type from the column)."""
         from ._lib import IllegalArgumentException
+        if isinstance(e.container, Var) and e.container.ctype == "MAP":
+            # m['k'] on a MAP held as a struct of columns: the entry's column
+            okk, key = literal_value(e.index)
+            if not okk or not isinstance(key, (str, type(None))):
+                not_impl(e)  # a per-row key
+            if key is None:
+                emit(OP_LIT_NULL, T_NULL)
+            else:
+                go(ElementProperty(e.container, key))
+            return
         isl, iv = literal_value(e.index)
         if isl and (isinstance(iv, bool) or not isinstance(iv, (int, type(None)))):
             raise IllegalArgumentException(f"a list index must be an INTEGER, got {e.index}")
@@ -1050,16 +1060,6 @@ def _compile_program(expr, header, columns, params=None, intern=None, coltype=No
             return
         if isinstance(e.container, NullLit):
             emit(OP_LIT_NULL, T_NULL)
-            return
-        if isinstance(e.container, Var) and e.container.ctype == "MAP":
-            # m['k'] on a MAP held as a struct of columns: the entry's column
-            okk, key = literal_value(e.index)
-            if not okk or not isinstance(key, (str, type(None))):
-                not_impl(e)  # a per-row key
-            if key is None:
-                emit(OP_LIT_NULL, T_NULL)
-            else:
-                go(ElementProperty(e.container, key))
             return
         c = column_of(e.container)
         if c is None or static_type(e.container) != T_LIST or coltype is None:
@@ -1133,7 +1133,26 @@ def _compile_program(expr, header, columns, params=None, intern=None, coltype=No
             except re.error as err:
                 from ._lib import IllegalArgumentException
                 raise IllegalArgumentException(f"invalid regular expression {pat!r}: {err}")
-            string_map(e.lhs, ("regex", pat))
+            okl, sv = literal_value(e.lhs)
+            if okl:  # a literal subject folds
+                if sv is not None and not isinstance(sv, str):
+                    not_impl(e)
+                if sv is None:
+                    emit(OP_LIT_NULL, T_BOOL)
+                else:
+                    emit(OP_LIT_BOOL, 1 if re.fullmatch(pat, sv) else 0)
+                return
+            t = static_type(e.lhs)
+            if t == T_NULL:
+                emit(OP_LIT_NULL, T_BOOL)
+                return
+            if t != T_STRING or vmap is None:
+                not_impl(e)
+            # the match of each DISTINCT subject value of this table (a value map
+            # over STRING codes) — not of the whole dictionary, where one long
+            # unrelated string can make a backtracking pattern exponential
+            go(e.lhs)
+            emit(OP_VALUE_MAP, name_of(vmap(("regex", pat), (e.lhs,))), 0.0)
             emit(OP_TO_BOOLEAN)
         elif cls in _BIN_OPS:
             go(e.lhs)

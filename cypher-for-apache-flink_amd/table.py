@@ -582,7 +582,11 @@ class GpuTable:
 
         entries = []
         for vals in rows:
-            txt = "".join(cypher_to_string(float(v) if ty == T_FLOAT else v) for v, ty in zip(vals, types))
+            if isinstance(kind, tuple) and kind[0] == "regex":  # s =~ pattern, then cast to BOOLEAN
+                import re
+                txt = "true" if re.fullmatch(kind[1], vals[0]) else "false"
+            else:
+                txt = "".join(cypher_to_string(float(v) if ty == T_FLOAT else v) for v, ty in zip(vals, types))
             entries.append((tuple(key(v, ty) for v, ty in zip(vals, types)), self.session.intern(txt)))
         entries.sort()
         n = len(entries)

@@ -118,7 +118,7 @@ object GpuExprMapper {
     // CAPF_OP_VALUE_MAP of the operands' distinct values (pairs) over this table: the
     // JVM's casts (Long.toString / Double.toString) of each, concatenated, interned
     // (the shim's twin of table.py GpuTable._value_map)
-    def valueMap(xs: Seq[Expr]): String = {
+    def valueMap(xs: Seq[Expr], regex: Option[String] = None): String = {
       val names = xs.indices.map(i => s"\u0002vm$i")
       val t = table.withColumns(xs.zip(names): _*)(header, parameters).distinct(names: _*)
       if (t.size > (1L << 22))  // every distinct value becomes a host string (table.py VALUE_MAP_MAX)
@@ -130,7 +130,10 @@ object GpuExprMapper {
         case other => throw NotImplementedException(s"GPU string of $other")
       }
       val entries = t.rows.map(row => names.map(row)).filterNot(_.contains(CypherNull))
-        .map(vs => (vs.map(key), session.intern(vs.map(GpuStringFunctions.cast).mkString)))
+        .map(vs => (vs.map(key), session.intern(regex match {
+          case Some(p) => if (GpuStringFunctions.cast(vs.head).matches(p)) "true" else "false"  // s =~ p
+          case None => vs.map(GpuStringFunctions.cast).mkString
+        })))
         .toSeq.sortWith { case ((a, _), (b, _)) => (a zip b).find(p => p._1 != p._2).exists(p => p._1 < p._2) }
       val id = Native.guard(Native.sessionValueMap(session.handle, entries.map(_._1.head).toArray,
         if (xs.size > 1) entries.map(_._1(1)).toArray else null, entries.map(_._2).toArray))
@@ -185,7 +188,16 @@ object GpuExprMapper {
       case RegexMatch(l, r) =>                                             // :99 — the predicate, not regexpExtract
         literal(r) match {
           case Some(CypherNull) => emit(LitNull, Native.TypeBool)
-          case Some(CypherString(pat)) => stringMap(l, Seq("regex", pat)); emit(ToBoolean_)
+          // the match of each distinct subject value of this table (not of the
+          // whole dictionary: a backtracking pattern over an unrelated long
+          // string can be exponential), then the string → BOOLEAN cast
+          case Some(CypherString(pat)) if literal(l).isDefined =>
+            lit(literal(l).get match {
+              case CypherString(v) => CypherBoolean(v.matches(pat))
+              case _ => CypherNull
+            })
+          case Some(CypherString(pat)) =>
+            go(l); emit(ValueMap, nameIndex(valueMap(Seq(l), Some(pat))), 0.0); emit(ToBoolean_)
           case _ => throw NotImplementedException(s"GPU =~ with a per-row pattern $e")
         }
       case ContainerIndex(c, i) if c.cypherType.material.isInstanceOf[CTList] && physical(c).isDefined =>

@@ -1127,6 +1127,15 @@ static void tri_build(Session *s, const ColView &src, const ColView &dst, int64_
 constexpr int TRI_WPE = 8, TRI_GRAB_A = 2, TRI_GRAB_B = 4;
 // CAPF_TRI_ILP=3 (A/B of the spill trade-off): ILP 3 compiles the two count
 // kernels with 24 / 48 B per lane of scratch against 56 / 80 B at ILP 4
+// CAPF_TRI_WPE=6 / 7 (A/B): the count kernels held at 6 / 7 waves per SIMD
+// (80 / 72 VGPRs: 0 / 24 B per lane of scratch in pass A, 8 / 40 B in pass B)
+static int tri_wpe() {
+  static const int v = [] {
+    const char *e = getenv("CAPF_TRI_WPE");
+    return e ? atoi(e) : TRI_WPE;
+  }();
+  return v;
+}
 static int tri_ilp() {
   static const int v = [] {
     const char *e = getenv("CAPF_TRI_ILP");
@@ -1185,7 +1194,9 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
     if (g.pcols) {  // node ids < 2^24: packed words, pass A q-tiled + pass B
       if (g.naitems > 0) {
         KernelTimer kt(s, "tri_count_qtiled", 4.0 * g.P);
-        auto kq = tri_ilp() == 3 ? k_tri_count_qtiled<3, TRI_WPE> : k_tri_count_qtiled<TRI_ILP, TRI_WPE>;
+        auto kq = tri_ilp() == 3 ? k_tri_count_qtiled<3, TRI_WPE>
+                  : tri_wpe() == 6 ? k_tri_count_qtiled<TRI_ILP, 6>
+                  : tri_wpe() == 7 ? k_tri_count_qtiled<TRI_ILP, 7> : k_tri_count_qtiled<TRI_ILP, TRI_WPE>;
         hipLaunchKernelGGL(kq, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK),
                            0, s->stream, (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
                            (const uint2 *)g.vals->p, (const uint2 *)g.erow->p, (const uint4 *)g.aitems->p,
@@ -1202,7 +1213,9 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
         KernelTimer kt(s, "tri_count_passb", 4.0 * g.P);
         TriPassB b{(const uint32_t *)g.in_words->p, (const uint2 *)g.in_rows->p, (const uint32_t *)g.in_eidx->p,
                    (const uint4 *)g.items->p, g.nitems};
-        auto kb = tri_ilp() == 3 ? k_tri_count_passb<3, TRI_WPE> : k_tri_count_passb<TRI_ILP, TRI_WPE>;
+        auto kb = tri_ilp() == 3 ? k_tri_count_passb<3, TRI_WPE>
+                  : tri_wpe() == 6 ? k_tri_count_passb<TRI_ILP, 6>
+                  : tri_wpe() == 7 ? k_tri_count_passb<TRI_ILP, 7> : k_tri_count_passb<TRI_ILP, TRI_WPE>;
         hipLaunchKernelGGL(kb, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK),
                            0, s->stream, (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
                            (const uint2 *)g.vals->p, b, parts, part, TRI_GRAB_B, 0, acc + 6, acc);

@@ -153,7 +153,7 @@ class JniRoute:
         nat = self.native
         A = {}
 
-        def new_table(method, *jargs):
+        def new_table(method, jargs):
             def f(*a):
                 r = nat(method, L, *jargs(*a[:-1]))
                 out(a[-1], r)
@@ -316,7 +316,7 @@ class JniRoute:
             (h(s), h(rels), self.jstr(a), self.jstr(b), h(src), self.jstr(si), h(tgt), self.jstr(ti), (I, lo),
              (I, up), self.jstr(os_), self.jstr(or_)))
 
-        def id_of(method, *jargs):
+        def id_of(method, jargs):
             def f(*a):
                 out(a[-1], nat(method, I, *jargs(*a[:-1])))
                 return self.done()

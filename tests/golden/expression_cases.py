@@ -162,4 +162,156 @@ def _map_cases():
     ]
 
 
-EXPRESSION_CASES = _null_cases() + _regex_cases() + _container_index_cases() + _map_cases()
+def _arith_cases():
+    """Comparison / arithmetic / CASE / projected EXISTS cases of
+    ExpressionTests.scala (the simple CASE `CASE x WHEN v` is the generic
+    CaseExpr over Equals(x, v) the front end normalises it to)."""
+    from capf_amd.expr import CaseExpr, ExistsPattern, Modulo  # noqa: F401
+    n = lambda k: ElementProperty(Var("n", "NODE"), k)  # noqa: E731
+    m = lambda k: ElementProperty(Var("m", "NODE"), k)  # noqa: E731
+    a = lambda k: ElementProperty(Var("a", "NODE"), k)  # noqa: E731
+    b = lambda k: ElementProperty(Var("b", "NODE"), k)  # noqa: E731
+    x = lambda k: ElementProperty(Var("_x", "NODE"), k)  # noqa: E731
+    nm = lambda labels=(): Match([NodeP("n", labels), NodeP("m", labels)], [RelP("_r", "n", "m")])  # noqa: E731
+    chain = "CREATE ({val: 4})-[:REL]->({val: 5})-[:REL]->({val: 5})-[:REL]->({val: 2})-[:REL]->()"
+    pv = lambda: Query([Match([NodeP("n")])],  # noqa: E731
+                       [ret(("n.val", n("val")), ("result", CaseExpr([(Equals(n("val"), StringLit("foo")), IntegerLit(1)),
+                                                                      (Equals(n("val"), StringLit("bar")), IntegerLit(2))],
+                                                                     IntegerLit(3))))])
+    persons = 'CREATE (:Person {val: "foo"}) CREATE (:Person {val: "bar"}) CREATE (:Person {val: "baz"})'
+    case_rows = [{"n.val": "foo", "result": 1}, {"n.val": "bar", "result": 2}, {"n.val": "baz", "result": 3}]
+    ex = lambda nodes, rels, where=(): ExistsPattern(Match(nodes, rels, list(where)))  # noqa: E731
+    ab = lambda con, rels=None, where=None, pre=None: Query(  # noqa: E731
+        [pre or Match([NodeP("a"), NodeP("b")], [RelP("_r0", "a", "b")])],
+        [ret(("a", Var("a", "NODE")), ("b", Var("b", "NODE")), ("con", con)),
+         ret(("a.id", a("id")), ("b.id", b("id")), ("con", Var("con")))])
+    a_only = lambda con, labels=(), alias="con": Query(  # noqa: E731
+        [Match([NodeP("a", labels)])],
+        [ret(("a", Var("a", "NODE")), (alias, con)), ret(("a.id", a("id")), (alias, Var(alias)))])
+    out = [
+        ("expr_case_generic", ET + "83-111", persons, pv(), case_rows),
+        ("expr_case_simple", ET + "113-141", persons, pv(), case_rows),
+        ("expr_case_inner_sum", ET + "143-172",
+         'CREATE (:Person {val: "foo", amount: 42 }) CREATE (:Person {val: "bar", amount: 23 }) '
+         'CREATE (:Person {val: "baz", amount: 84 })',
+         Query([Match([NodeP("n")])],
+               [ret(("n.val", n("val")),
+                    ("result", Sum(CaseExpr([(Equals(n("val"), StringLit("foo")), n("amount")),
+                                             (Equals(n("val"), StringLit("bar")), IntegerLit(1984))],
+                                            IntegerLit(0)))))]),
+         [{"n.val": "foo", "result": 42}, {"n.val": "bar", "result": 1984}, {"n.val": "baz", "result": 0}]),
+        ("expr_prop_unknown_label", ET + "176-193", 'CREATE (p:Person {firstName: "Alice", lastName: "Foo"})',
+         Query([Match([NodeP("a", ("Animal",))])], [ret(("a.name", a("name")))]), []),
+        ("expr_prop_unknown", ET + "195-211", 'CREATE (p:Person {firstName: "Alice", lastName: "Foo"})',
+         Query([Match([NodeP("a", ("Person",))])], [ret(("a.firstName", a("firstName")), ("a.age", a("age")))]),
+         [{"a.age": None, "a.firstName": "Alice"}]),
+        ("expr_prop_equality", ET + "213-237",
+         "CREATE (:A {val: 1})-[:REL]->(:B {p: 2}) CREATE (:A {val: 2})-[:REL]->(:B {p: 1}) "
+         "CREATE (:A {val: 100})-[:REL]->(:B {p: 100}) CREATE (:A {val: 1})-[:REL]->(:B) "
+         "CREATE (:A)-[:REL]->(:B {p: 2}) CREATE (:A)-[:REL]->(:B)",
+         Query([Match([NodeP("a", ("A",)), NodeP("b", ("B",))], [RelP("_r", "a", "b")])],
+               [ret(("eq", Equals(a("val"), b("p"))))]),
+         [{"eq": False}, {"eq": False}, {"eq": True}, {"eq": None}, {"eq": None}, {"eq": None}]),
+        ("expr_prop_simple", ET + "315-327", "CREATE (:Person {name: 'Mats'})-[:REL]->(:Person {name: 'Martin'})",
+         Query([Match([NodeP("p", ("Person",))])], [ret(("p.name", ElementProperty(Var("p", "NODE"), "name")))]),
+         [{"p.name": "Mats"}, {"p.name": "Martin"}]),
+        ("expr_prop_simple_rel", ET + "329-340",
+         "CREATE (:Person {name: 'Mats'})-[:KNOWS {since: 2017}]->(:Person {name: 'Martin'})",
+         Query([Match([NodeP("a", ("Person",)), NodeP("b", ("Person",))], [RelP("r", "a", "b", ("KNOWS",))])],
+               [ret(("r.since", ElementProperty(Var("r", "RELATIONSHIP"), "since")))]), [{"r.since": 2017}]),
+        ("expr_less_than", ET + "355-370", chain,
+         Query([nm()], [ret(("n.val < m.val", LessThan(n("val"), m("val"))))]),
+         [{"n.val < m.val": v} for v in (True, False, False, None)]),
+        ("expr_less_equal", ET + "372-386", chain,
+         Query([nm()], [ret(("n.val <= m.val", LessThanOrEqual(n("val"), m("val"))))]),
+         [{"n.val <= m.val": v} for v in (True, True, False, None)]),
+        ("expr_greater_than", ET + "388-402", chain,
+         Query([nm()], [ret(("gt", GreaterThan(n("val"), m("val"))))]),
+         [{"gt": v} for v in (False, False, True, None)]),
+        ("expr_greater_equal", ET + "404-418", chain,
+         Query([nm()], [ret(("n.val >= m.val", GreaterThanOrEqual(n("val"), m("val"))))]),
+         [{"n.val >= m.val": v} for v in (False, True, True, None)]),
+        ("expr_add_after_match", ET + "444-456", "CREATE ({val: 4})-[:REL]->({val: 5, other: 3})-[:REL]->()",
+         Query([nm()], [ret(("res", Add(Add(m("other"), m("val")), n("val"))))]), [{"res": 12}, {"res": None}]),
+        ("expr_sub_named", ET + "458-470", "CREATE ({val: 4})-[:REL]->({val: 5, other: 3})-[:REL]->()",
+         Query([nm()], [ret(("res", Subtract(Subtract(m("val"), n("val")), m("other"))))]),
+         [{"res": -2}, {"res": None}]),
+        ("expr_sub_unnamed", ET + "472-483", "CREATE (:Node {val: 4})-[:REL]->(:Node {val: 5})",
+         Query([nm(("Node",))], [ret(("m.val - n.val", Subtract(m("val"), n("val"))))]), [{"m.val - n.val": 1}]),
+        ("expr_mul_int", ET + "485-498", "CREATE (:Node {val: 9})-[:REL]->(:Node {val: 2})-[:REL]->(:Node {val: 3})",
+         Query([nm(("Node",))], [ret(("n.val * m.val", Multiply(n("val"), m("val"))))]),
+         [{"n.val * m.val": 18}, {"n.val * m.val": 6}]),
+        ("expr_mul_float", ET + "500-512", "CREATE (:Node {val: 4.5D})-[:REL]->(:Node {val: 2.5D})",
+         Query([nm(("Node",))], [ret(("n.val * m.val", Multiply(n("val"), m("val"))))]), [{"n.val * m.val": 11.25}]),
+        ("expr_mul_int_float", ET + "514-526", "CREATE (:Node {val: 9})-[:REL]->(:Node {val2: 2.5D})",
+         Query([nm(("Node",))], [ret(("n.val * m.val2", Multiply(n("val"), m("val2"))))]),
+         [{"n.val * m.val2": 22.5}]),
+        ("expr_div_int", ET + "528-541", "CREATE (:Node {val: 9})-[:REL]->(:Node {val: 3})-[:REL]->(:Node {val: 2})",
+         Query([nm(("Node",))], [ret(("n.val / m.val", Divide(n("val"), m("val"))))]),
+         [{"n.val / m.val": 3}, {"n.val / m.val": 1}]),
+        ("expr_div_int_float_null", ET + "543-556",
+         "CREATE (:Node {val: 9})-[:REL]->(:Node {val2: 4.5D})-[:REL]->(:Node)",
+         Query([nm(("Node",))], [ret(("n.val / m.val2", Divide(n("val"), m("val2"))))]),
+         [{"n.val / m.val2": 2.0}, {"n.val / m.val2": None}]),
+        ("expr_div_float_literal", ET + "558-569", "CREATE (:Node {val: 4.5})",
+         Query([Match([NodeP("n", ("Node",))])], [ret(("res", Divide(n("val"), FloatLit(0.5))))]), [{"res": 9.0}]),
+        ("expr_equality", ET + "573-591",
+         "CREATE (:Node {val: 4})-[:REL]->(:Node {val: 5}) CREATE (:Node {val: 4})-[:REL]->(:Node {val: 4}) "
+         "CREATE (:Node)-[:REL]->(:Node {val: 5})",
+         Query([nm(("Node",))], [ret(("res", Equals(m("val"), n("val"))))]),
+         [{"res": False}, {"res": True}, {"res": None}]),
+        # EXISTS patterns projected as values (WITH a, b, EXISTS(...) AS con)
+        ("expr_exists_basic", ET + "594-613",
+         "CREATE (v {id: 1})-[:REL]->({id: 2})-[:REL]->(w {id: 3}) CREATE (v)-[:REL]->(w) CREATE (w)-[:REL]->({id: 4})",
+         ab(ex([NodeP("a"), NodeP("_x"), NodeP("b")], [RelP("_e1", "a", "_x"), RelP("_e2", "_x", "b")])),
+         [{"a.id": 1, "b.id": 3, "con": True}, {"a.id": 1, "b.id": 2, "con": False},
+          {"a.id": 2, "b.id": 3, "con": False}, {"a.id": 3, "b.id": 4, "con": False}]),
+        ("expr_exists_var_length", ET + "615-632", "CREATE (v {id: 1})-[:REL]->({id: 2})-[:REL]->({id: 3})<-[:REL]-(v)",
+         ab(ex([NodeP("a"), NodeP("_x"), NodeP("b")],
+               [RelP("_e1", "a", "_x", length=(1, 3)), RelP("_e2", "_x", "b")])),
+         [{"a.id": 1, "b.id": 2, "con": False}, {"a.id": 1, "b.id": 3, "con": True},
+          {"a.id": 2, "b.id": 3, "con": False}]),
+        ("expr_exists_node_predicate", ET + "634-657",
+         "CREATE ({id: 1})-[:REL]->({id: 2, name: 'foo'}) CREATE ({id: 3})-[:REL]->({id: 4, name: 'bar'})",
+         a_only(ex([NodeP("a"), NodeP("_x")], [RelP("_e", "a", "_x")], [Equals(x("name"), StringLit("foo"))])),
+         [{"a.id": 1, "con": True}, {"a.id": 2, "con": False}, {"a.id": 3, "con": False}, {"a.id": 4, "con": False}]),
+        ("expr_exists_rel_predicate", ET + "659-680",
+         "CREATE (v {id: 1})-[:REL {val: 'foo'}]->({id: 2})<-[:REL]-(v) "
+         "CREATE (w {id: 3})-[:REL {val: 'bar'}]->({id: 4})<-[:REL]-(w)",
+         Query([Match([NodeP("a"), NodeP("b")], [RelP("_r0", "a", "b")])],
+               [ret(("a", Var("a", "NODE")), ("b", Var("b", "NODE")), distinct=True),
+                ret(("a", Var("a", "NODE")), ("b", Var("b", "NODE")),
+                    ("con", ex([NodeP("a"), NodeP("b")], [RelP("_e", "a", "b")],
+                               [Equals(ElementProperty(Var("_e", "RELATIONSHIP"), "val"), StringLit("foo"))]))),
+                ret(("a.id", a("id")), ("b.id", b("id")), ("con", Var("con")))]),
+         [{"a.id": 1, "b.id": 2, "con": True}, {"a.id": 3, "b.id": 4, "con": False}]),
+        ("expr_exists_label_predicate", ET + "682-702", "CREATE (v:SRC {id: 1})-[:REL]->(:A) CREATE (w:SRC {id: 2})-[:REL]->(:B)",
+         a_only(ex([NodeP("a"), NodeP("_x", ("A",))], [RelP("_e", "a", "_x")]), labels=("SRC",)),
+         [{"a.id": 1, "con": True}, {"a.id": 2, "con": False}]),
+        ("expr_exists_type_predicate", ET + "704-724",
+         "CREATE (v {id: 1})-[:A]->({id: 2})<-[:REL]-(v) CREATE (w {id: 3})-[:B]->({id: 4})<-[:REL]-(w)",
+         ab(ex([NodeP("a"), NodeP("b")], [RelP("_e", "a", "b", ("A",))]),
+            pre=Match([NodeP("a"), NodeP("b")], [RelP("_r0", "a", "b", ("REL",))])),
+         [{"a.id": 1, "b.id": 2, "con": True}, {"a.id": 3, "b.id": 4, "con": False}]),
+        ("expr_exists_inverse", ET + "726-744", "CREATE (v {id: 1})-[:REL]->({id: 2})",
+         ab(Not(ex([NodeP("a"), NodeP("b")], [RelP("_e", "a", "b")])), pre=Match([NodeP("a"), NodeP("b")])),
+         [{"a.id": 1, "b.id": 1, "con": True}, {"a.id": 1, "b.id": 2, "con": False},
+          {"a.id": 2, "b.id": 1, "con": True}, {"a.id": 2, "b.id": 2, "con": True}]),
+        ("expr_exists_derived_predicate", ET + "746-765",
+         "CREATE ({id: 1, val: 0})-[:REL]->({id: 2, val: 2})<-[:REL]-({id: 3, val: 10})",
+         a_only(ex([NodeP("a"), NodeP("_x")], [RelP("_e", "a", "_x")],
+                   [Equals(x("val"), Add(a("val"), IntegerLit(2)))]), alias="other"),
+         [{"a.id": 1, "other": True}, {"a.id": 2, "other": False}, {"a.id": 3, "other": False}]),
+        ("expr_ands_projected", ET + "825-843", "CREATE ({v1: true, v2: true, v3: true}), ({v1: false, v2: true, v3: true})",
+         Query([Match([NodeP("n")], where=[Equals(Ands(n("v1"), n("v2"), n("v3")), BoolLit(True))])],
+               [ret(("n.v1", n("v1")))]), [{"n.v1": True}]),
+        ("expr_xor_projected", ET + "845-861",
+         "CREATE ({v1: true, v2: true, res: false}), ({v1: true, v2: false, res: true}), "
+         "({v1: false, v2: true, res: true}), ({v1: false, v2: false, res: false})",
+         Query([Match([NodeP("n")], where=[_xor(n("v1"), Equals(n("v2"), n("res")))])], [ret(("n", Var("n", "NODE")))]),
+         [], {"row_count": 4}),
+    ]
+    return out
+
+
+EXPRESSION_CASES = _null_cases() + _regex_cases() + _container_index_cases() + _map_cases() + _arith_cases()

@@ -172,7 +172,7 @@ enum Op : int32_t {
   OP_DEGREES = CAPF_OP_DEGREES, OP_RADIANS = CAPF_OP_RADIANS, OP_ATAN2 = CAPF_OP_ATAN2,
   OP_TO_BOOLEAN = CAPF_OP_TO_BOOLEAN, OP_IN_SET = CAPF_OP_IN_SET, OP_STR_MAP = CAPF_OP_STR_MAP,
   OP_VALUE_MAP = CAPF_OP_VALUE_MAP, OP_STR_TO_NUM = CAPF_OP_STR_TO_NUM, OP_RAND = CAPF_OP_RAND,
-  OP_LIST_INDEX = CAPF_OP_LIST_INDEX
+  OP_LIST_INDEX = CAPF_OP_LIST_INDEX, OP_STR_RANK = CAPF_OP_STR_RANK
 };
 // a program name that refers to a session literal set ("\x01set:<id>"), not a column
 inline bool is_literal_set_name(const std::string &nm) { return nm.size() > 5 && nm.compare(0, 5, "\x01set:") == 0; }
@@ -394,6 +394,9 @@ struct Session {
   // 1 true, 2 neither (NULL)
   BufPtr d_str_bool;
   size_t d_str_bool_n = 0;
+  // device table of the strings' sort ranks (CAPF_OP_STR_RANK)
+  BufPtr d_str_rank;
+  size_t d_str_rank_n = 0;
   // device table of the strings as numbers (CAPF_OP_STR_TO_NUM)
   BufPtr d_str_num;
   size_t d_str_num_n = 0;
@@ -556,6 +559,9 @@ ColPtr decode_column(Session *s, const ColPtr &c);
 const int64_t *string_length_table(Session *s, size_t *n);
 // Device table of the session's strings parsed as booleans (CAPF_OP_TO_BOOLEAN).
 const uint8_t *string_bool_table(Session *s, size_t *n);
+// Device table of each string's rank in UTF-16 code-unit order
+// (CAPF_OP_STR_RANK, Java String.compareTo); *n = strings covered.
+const int64_t *string_rank_table(Session *s, size_t *n);
 // Device table of the session's strings parsed as numbers (CAPF_OP_STR_TO_NUM):
 // [double n][int64 n][uint8 flags n] (bit 0: a DOUBLE, bit 1: an INTEGER).
 const void *string_num_table(Session *s, size_t *n);

@@ -1032,6 +1032,12 @@ __device__ Val run_program(const Instr *code, int ncode, const ColView *cols, in
                          : mk(((const int64_t *)cols[in.i].data)[a.b], CAPF_TYPE_INT64, 0);
         break;
       }
+      case OP_STR_RANK: {  // cols[in.i] = the session's string ranks by code
+        Val a = st[--sp];
+        st[sp++] = a.nul ? mknull(CAPF_TYPE_INT64)
+                         : mk(((const int64_t *)cols[in.i].data)[a.b], CAPF_TYPE_INT64, 0);
+        break;
+      }
       case OP_LIST_SIZE: {  // cols[in.i]: LIST offsets [n + 1]
         const ColView &c = cols[in.i];
         if (!c.data || (c.valid && !c.valid[r]))
@@ -1256,6 +1262,16 @@ static DeviceProgram upload_program(Session *s, const Program &p,
       break;
     }
   for (auto &in : code)
+    if (in.op == OP_STR_RANK) {  // the session's string sort ranks as one more column view
+      size_t nstr = 0;
+      const int64_t *rk = string_rank_table(s, &nstr);
+      in.i = (int64_t)views.size();
+      views.push_back(ColView{rk, nullptr, (int32_t)Type::Int64, ENC_PLAIN, 0});
+      for (auto &x : code)
+        if (x.op == OP_STR_RANK) x.i = in.i;
+      break;
+    }
+  for (auto &in : code)
     if (in.op == OP_STR_TO_NUM) {  // the session's strings as numbers, one more view
       size_t nstr = 0;
       const void *tn = string_num_table(s, &nstr);
@@ -1304,7 +1320,7 @@ static DeviceProgram upload_program(Session *s, const Program &p,
       case OP_AND: case OP_OR: case OP_COALESCE: depth -= (int)in.i - 1; break;
       case OP_NOT: case OP_IS_NULL: case OP_IS_NOT_NULL: case OP_NEG: case OP_TO_FLOAT:
       case OP_TO_INTEGER: case OP_STR_LEN: case OP_TO_BOOLEAN: case OP_IN_SET: case OP_STR_MAP:
-      case OP_STR_TO_NUM: case OP_LIST_INDEX: break;
+      case OP_STR_TO_NUM: case OP_LIST_INDEX: case OP_STR_RANK: break;
       case OP_IF: depth -= 2; break;
       case OP_VALUE_MAP: depth -= in.f != 0.0 ? 1 : 0; break;
       default:

@@ -5,6 +5,7 @@
 // FlinkTable (flink-cypher/.../impl/table/FlinkTable.scala:49-199).  Like the
 // Flink Table API, operations only build a plan; materialisation happens on
 // size / download (FlinkTable.scala:57-61).
+#include <algorithm>
 #include <cctype>
 #include <cmath>
 #include <cstdio>
@@ -317,6 +318,12 @@ Type infer_type(const Program &p, const std::vector<std::string> &names,
       case OP_STR_LEN: {
         Type a = pop();
         if (a != Type::String && a != Type::Null) illegal("size() of a non-string value");
+        st.push_back(Type::Int64);
+        break;
+      }
+      case OP_STR_RANK: {
+        Type a = pop();
+        if (a != Type::String && a != Type::Null) illegal("string rank of a non-string value");
         st.push_back(Type::Int64);
         break;
       }
@@ -817,6 +824,49 @@ static bool parse_int32(const std::string &u, int64_t *out) {
   if (v < -2147483648LL || v > 2147483647LL) return false;
   *out = v;
   return true;
+}
+
+// Java String.compareTo order: UTF-16 code units.  On UTF-8 bytes that is
+// code-point order except that a supplementary character (4 bytes, a
+// surrogate pair D800-DBFF first) sorts below U+E000-U+FFFF (3 bytes EE-EF).
+static int utf16_cmp(const std::string &a, const std::string &b) {
+  auto key = [](const std::string &u, size_t &i) -> uint32_t {  // next code unit class
+    const unsigned char c = (unsigned char)u[i];
+    size_t len = c < 0x80 ? 1 : c < 0xE0 ? 2 : c < 0xF0 ? 3 : 4;
+    uint32_t cp = c < 0x80 ? c : c < 0xE0 ? c & 0x1F : c < 0xF0 ? c & 0x0F : c & 0x07;
+    for (size_t k = 1; k < len && i + k < u.size(); ++k) cp = cp << 6 | ((unsigned char)u[i + k] & 0x3F);
+    i += len;
+    return cp >= 0x10000 ? 0xD800 + ((cp - 0x10000) >> 10) : cp;  // the high surrogate
+  };
+  size_t i = 0, j = 0;
+  while (i < a.size() && j < b.size()) {
+    const size_t i0 = i, j0 = j;
+    const uint32_t x = key(a, i), y = key(b, j);
+    if (x != y) return x < y ? -1 : 1;
+    if (x >= 0xD800 && x < 0xDC00) {  // equal high surrogates: compare the low ones
+      std::string ca = a.substr(i0, i - i0), cb = b.substr(j0, j - j0);
+      if (ca != cb) return ca < cb ? -1 : 1;  // same lead: byte order = low-surrogate order
+    }
+  }
+  return i < a.size() ? 1 : (j < b.size() ? -1 : 0);
+}
+
+const int64_t *string_rank_table(Session *s, size_t *n) {
+  std::lock_guard<std::mutex> lk(s->str_mu);
+  if (s->d_str_rank_n != s->strings.size() || !s->d_str_rank) {
+    const size_t m = s->strings.size();
+    std::vector<int64_t> order(m), rank(std::max<size_t>(m, 1), 0);
+    for (size_t i = 0; i < m; ++i) order[i] = (int64_t)i;
+    std::sort(order.begin(), order.end(),
+              [&](int64_t x, int64_t y) { return utf16_cmp(s->strings[x], s->strings[y]) < 0; });
+    for (size_t r = 0; r < m; ++r) rank[(size_t)order[r]] = (int64_t)r;
+    s->d_str_rank = s->alloc(8 * rank.size());
+    HIP_CHECK(hipMemcpyAsync(s->d_str_rank->p, rank.data(), 8 * rank.size(), hipMemcpyHostToDevice, s->stream));
+    s->sync();  // the pageable source
+    s->d_str_rank_n = m;
+  }
+  *n = s->d_str_rank_n;
+  return (const int64_t *)s->d_str_rank->p;
 }
 
 const void *string_num_table(Session *s, size_t *n) {
@@ -1903,7 +1953,7 @@ capf_status capf_table_order_by(capf_table *t, int32_t n, const capf_expr *keys,
   for (int i = 0; i < n; ++i) {
     Program p = Program::from_c(&keys[i]);
     Type ty = infer_type(p, c->names, c->types);
-    if (ty == Type::String) not_impl("ORDER BY on strings");
+    if (ty == Type::String) p.code.push_back(Instr{OP_STR_RANK, 0, 0, 0.0});  // sort on the ranks
     nn->exprs.push_back(std::move(p));
     nn->desc.push_back(descending ? descending[i] : 0);
   }

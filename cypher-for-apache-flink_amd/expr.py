@@ -39,7 +39,7 @@ OP_STR_LEN, OP_LIST_SIZE, OP_IF = 60, 61, 62
 OP_ROUND, OP_ABS, OP_CEIL, OP_FLOOR, OP_SIGN, OP_SQRT, OP_LOG, OP_LOG10, OP_EXP = 70, 71, 72, 73, 74, 75, 76, 77, 78
 OP_SIN, OP_COS, OP_TAN, OP_ASIN, OP_ACOS, OP_ATAN, OP_DEGREES, OP_RADIANS = 79, 80, 81, 82, 83, 84, 85, 86
 OP_ATAN2, OP_TO_BOOLEAN, OP_IN_SET, OP_STR_MAP, OP_VALUE_MAP = 87, 88, 89, 90, 91
-OP_STR_TO_NUM, OP_RAND, OP_LIST_INDEX = 92, 93, 94
+OP_STR_TO_NUM, OP_RAND, OP_LIST_INDEX, OP_STR_RANK = 92, 93, 94, 95
 IN_SET_MIN = 17  # list length from which IN runs as a session-set lookup (shorter: an OR of equalities)
 
 # aggregators
@@ -643,6 +643,7 @@ _BIN_OPS = {
     "GreaterThanOrEqual": OP_GE, "Add": OP_ADD, "Subtract": OP_SUB, "Multiply": OP_MUL,
     "Divide": OP_DIV, "Modulo": OP_MOD,
 }
+_ORDERED = ("LessThan", "LessThanOrEqual", "GreaterThan", "GreaterThanOrEqual")
 _UN_OPS = {"Not": OP_NOT, "IsNull": OP_IS_NULL, "IsNotNull": OP_IS_NOT_NULL, "ToFloat": OP_TO_FLOAT,
            "ToInteger": OP_TO_INTEGER, "Negate": OP_NEG, "Exists": OP_IS_NOT_NULL,
            "Round": OP_ROUND, "Abs": OP_ABS, "Ceil": OP_CEIL, "Floor": OP_FLOOR, "Sign": OP_SIGN,
@@ -1154,6 +1155,23 @@ def _compile_program(expr, header, columns, params=None, intern=None, coltype=No
             go(e.lhs)
             emit(OP_VALUE_MAP, name_of(vmap(("regex", pat), (e.lhs,))), 0.0)
             emit(OP_TO_BOOLEAN)
+        elif cls in _ORDERED:
+            # FlinkSQLExprMapper.scala:91-94.  STRINGs order by their rank in
+            # the session dictionary (CAPF_OP_STR_RANK, String.compareTo);
+            # operands of incomparable types compare to NULL (Cypher: 1 < 'a'
+            # is null, so a WHERE drops the row — PredicateTests.scala:195)
+            ta, tb = static_type(e.lhs), static_type(e.rhs)
+            if None not in (ta, tb) and T_NULL not in (ta, tb) and not _comparable(ta, tb):
+                emit(OP_LIT_NULL, T_BOOL)
+                return
+            strs = T_STRING in (ta, tb)
+            go(e.lhs)
+            if strs:
+                emit(OP_STR_RANK)
+            go(e.rhs)
+            if strs:
+                emit(OP_STR_RANK)
+            emit(_BIN_OPS[cls])
         elif cls in _BIN_OPS:
             go(e.lhs)
             go(e.rhs)

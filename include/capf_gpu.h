@@ -225,7 +225,13 @@ enum {
    * pushes element i of the row's list in LIST column names[iarg] (i < 0
    * counts from the end); NULL for a NULL list, a NULL index or an index out
    * of range.  farg = the element's capf type (CAPF_TYPE_*).                 */
-  CAPF_OP_LIST_INDEX = 94
+  CAPF_OP_LIST_INDEX = 94,
+  /* Ordering of strings (Flink compares VARCHARs lexicographically, Java
+   * String.compareTo; FlinkSQLExprMapper.scala:91-94 and ORDER BY): pops a
+   * STRING; pushes its INTEGER rank among the session's strings in UTF-16
+   * code-unit order, so <, <=, >, >= and sorting on ranks order the strings.
+   * NULL in, NULL out.  capf_table_order_by applies it to a STRING key itself. */
+  CAPF_OP_STR_RANK = 95
 };
 
 typedef struct capf_expr {

@@ -42,6 +42,7 @@ object GpuExprMapper {
   private final val ValueMap = 91
   // round 6: string → number casts, rand(), xs[i] on LIST columns
   private final val StrToNum = 92; private final val Rand_ = 93; private final val ListIndex = 94
+  private final val StrRank = 95  // a STRING's rank in String.compareTo order (ordered comparisons)
   private final val InSetMin = 17  // IN lists from this length: one set lookup per row (expr.py IN_SET_MIN)
 
   def program(expr: Expr, header: RecordHeader, table: GpuTable, parameters: CypherMap): Program = {
@@ -149,6 +150,22 @@ object GpuExprMapper {
       case None => go(x); emit(StrMap, nameIndex(session.stringMap(key)))
     }
 
+    // <, <=, >, >= (FlinkSQLExprMapper.scala:91-94): STRINGs compare by their
+    // dictionary rank (String.compareTo); incomparable material types give NULL
+    // (expr.py's _ORDERED lowering)
+    def ordered(l: Expr, r: Expr, op: Int): Unit = {
+      val (tl, tr) = (l.cypherType.material, r.cypherType.material)
+      val num = Set[CypherType](CTInteger, CTFloat)
+      val known = Set[CypherType](CTInteger, CTFloat, CTString, CTBoolean)
+      if (known(tl) && known(tr) && tl != tr && !(num(tl) && num(tr))) emit(LitNull, Native.TypeBool)
+      else {
+        val strs = tl == CTString || tr == CTString
+        go(l); if (strs) emit(StrRank)
+        go(r); if (strs) emit(StrRank)
+        emit(op)
+      }
+    }
+
     def go(e: Expr): Unit = e match {
       case _: Var | _: HasLabel | _: HasType | _: StartNode | _: EndNode | _: ElementProperty =>
         physical(e) match {
@@ -165,10 +182,10 @@ object GpuExprMapper {
       case Param(name) => lit(parameters(name))
       case Equals(l, r) => go(l); go(r); emit(Eq)
       case Not(Equals(l, r)) => go(l); go(r); emit(Neq)
-      case LessThan(l, r) => go(l); go(r); emit(Lt)
-      case LessThanOrEqual(l, r) => go(l); go(r); emit(Le)
-      case GreaterThan(l, r) => go(l); go(r); emit(Gt)
-      case GreaterThanOrEqual(l, r) => go(l); go(r); emit(Ge)
+      case LessThan(l, r) => ordered(l, r, Lt)
+      case LessThanOrEqual(l, r) => ordered(l, r, Le)
+      case GreaterThan(l, r) => ordered(l, r, Gt)
+      case GreaterThanOrEqual(l, r) => ordered(l, r, Ge)
       case Not(x) => go(x); emit(Not_)
       case Ands(xs) if xs.isEmpty => emit(LitBool, 1L)
       case Ands(xs) => xs.foreach(go); emit(And, xs.size.toLong)

@@ -146,17 +146,30 @@ def _num(x):
     return x.v
 
 
+def _jcmp(x, y):
+    """java.lang.String.compareTo sign: UTF-16 code-unit order."""
+    kx, ky = x.encode("utf-16-be", "surrogatepass"), y.encode("utf-16-be", "surrogatepass")
+    return (kx > ky) - (kx < ky)
+
+
 def _cmp(a, b, op):
     ok = a.ok & b.ok
     if a.t == T_NULL or b.t == T_NULL:
         return Val(T_BOOL, np.zeros(len(ok), bool), np.zeros(len(ok), bool))
     if a.t == T_STRING or b.t == T_STRING:
         if a.t != b.t:
+            if op not in ("eq", "ne"):  # Cypher: incomparable operands order to NULL
+                return Val(T_BOOL, np.zeros(len(ok), bool), np.zeros(len(ok), bool))
             raise TypeError("cannot compare STRING with non-string")
-        if op not in ("eq", "ne"):
-            raise NotImplementedError("ordering comparison on strings")
+        if op not in ("eq", "ne"):  # String.compareTo: UTF-16 code units (= UTF-16-BE bytes)
+            f = {"lt": lambda c: c < 0, "le": lambda c: c <= 0, "gt": lambda c: c > 0, "ge": lambda c: c >= 0}[op]
+            r = np.array([f(_jcmp(x, y)) if (p and q) else False for x, y, p, q in zip(a.v, b.v, a.ok, b.ok)],
+                         dtype=bool)
+            return Val(T_BOOL, r, ok)
         r = np.array([(x == y) if (p and q) else False for x, y, p, q in zip(a.v, b.v, a.ok, b.ok)], dtype=bool)
         return Val(T_BOOL, r if op == "eq" else ~r, ok)
+    if (a.t == T_BOOL) != (b.t == T_BOOL) and op not in ("eq", "ne"):
+        return Val(T_BOOL, np.zeros(len(ok), bool), np.zeros(len(ok), bool))
     x, y = _num(a), _num(b)
     with np.errstate(invalid="ignore"):
         r = {"eq": x == y, "ne": x != y, "lt": x < y, "le": x <= y, "gt": x > y, "ge": x >= y}[op]
@@ -843,8 +856,10 @@ class OracleTable:
             desc = o in ("desc", "Descending", True)
             vals = v.v[idx]
             ok = v.ok[idx]
-            if v.t == T_STRING:
-                raise NotImplementedError("ORDER BY on strings")
+            if v.t == T_STRING:  # the strings' ranks in String.compareTo order
+                enc = [x.encode("utf-16-be", "surrogatepass") if p else b"" for x, p in zip(vals, ok)]
+                rank = {k: i for i, k in enumerate(sorted(set(enc)))}
+                vals = np.array([rank[k] for k in enc], dtype=np.int64)
             key = vals.astype(np.float64) if v.t == T_FLOAT else vals.astype(np.int64)
             if desc:
                 key = -key if v.t == T_FLOAT else ~key

@@ -314,4 +314,112 @@ def _arith_cases():
     return out
 
 
-EXPRESSION_CASES = _null_cases() + _regex_cases() + _container_index_cases() + _map_cases() + _arith_cases()
+def _pred_cases():
+    """PredicateTests.scala :37-371: property / label predicates, OR / AND,
+    comparisons (mixed INTEGER / FLOAT operands compare numerically; an
+    INTEGER against a STRING is NULL, so the WHERE drops the row), range
+    chains (`0 < a.val <= 10` is Ands of the two comparisons) and float
+    division.  (The two pattern-predicate sections :373-704 are
+    reference_cases.PATTERN_PREDICATE_CASES.)"""
+    PT = "MTa/PredicateTests.scala:"
+    a = lambda k: ElementProperty(Var("a", "NODE"), k)  # noqa: E731
+    b = lambda k: ElementProperty(Var("b", "NODE"), k)  # noqa: E731
+    n = lambda k: ElementProperty(Var("n", "NODE"), k)  # noqa: E731
+    m = lambda k: ElementProperty(Var("m", "NODE"), k)  # noqa: E731
+    A = lambda: Var("a", "NODE")  # noqa: E731
+    ab = Match([NodeP("a", ("A",)), NodeP("b", ("B",))], [RelP("_r", "a", "b")])
+    nm = Match([NodeP("n", ("Node",)), NodeP("m", ("Node",))], [RelP("_r", "n", "m")])
+    mn = Match([NodeP("n", ("Node",)), NodeP("m", ("Node",))], [RelP("_r", "m", "n")])  # (n)<--(m)
+    where = lambda mt, *preds: Match(mt.nodes, mt.rels, list(preds))  # noqa: E731
+    a_val = lambda: [ret(("a.val", a("val")))]  # noqa: E731
+    mixed_lt = "CREATE (:A {val: 4})-[:REL]->(:B {val2: 1.0}), (:A {val: 1})-[:REL]->(:B {val2: 4.0})"
+    mixed_le = "CREATE (:A {val: 4})-[:REL]->(:B {val2: 4.0}), (:A {val: 1})-[:REL]->(:B {val2: 4.0})"
+    mixed_ge = "CREATE (:A {val: 4})-[:REL]->(:B {val2: 1.0}), (:A {val: 4})-[:REL]->(:B {val2: 4.0})"
+    incompat = "CREATE (:A {val: 4})-[:REL]->(:B {val2: 'string'})"
+    chain3 = "CREATE (:Node {id: 1, val: 4})-[:REL]->(:Node {id: 2, val: 5})-[:REL]->(:Node {id: 3, val: 5})"
+    out = [
+        ("pred_missing_property", PT + "37-43", "CREATE ()",
+         Query([Match([NodeP("n")], where=[Equals(n("name"), StringLit("foo"))])], [ret(("n.id", n("id")))]), []),
+        ("pred_exists", PT + "45-54", "CREATE ({id: 1}), ({id: 2}), ({other: 'foo'}), ()",
+         Query([Match([NodeP("n")], where=[IsNotNull(n("id"))])], [ret(("n.id", n("id")))]),
+         [{"n.id": 1}, {"n.id": 2}]),
+        ("pred_or", PT + "82-94", "CREATE (:A {val: 1}), (:A {val: 2}), (:A {val: 3})",
+         Query([Match([NodeP("a", ("A",))], where=[Ors(Equals(a("val"), IntegerLit(1)),
+                                                        Equals(a("val"), IntegerLit(2)))])], a_val()),
+         [{"a.val": 1}, {"a.val": 2}]),
+        ("pred_or_labels", PT + "96-108", "CREATE (:A {val: 1}), (:B {val: 2}), (:C {val: 3})",
+         Query([Match([NodeP("a")], where=[Ors(HasLabel(A(), "A"), HasLabel(A(), "B"))])], a_val()),
+         [{"a.val": 1}, {"a.val": 2}]),
+        ("pred_or_labels_properties", PT + "110-123", "CREATE (:A {val: 1}), (:B {val: 2}), (:A:B {val: 3})",
+         Query([Match([NodeP("a")], where=[Ors(Ands(HasLabel(A(), "A"), Equals(a("val"), IntegerLit(1))),
+                                               HasLabel(A(), "B"))])], a_val()),
+         [{"a.val": 1}, {"a.val": 2}, {"a.val": 3}]),
+        ("pred_or_and", PT + "125-143",
+         "CREATE (:A {val: 1, name: 'a'}) CREATE (:A {val: 2, name: 'a'}) CREATE (:A {val: 3, name: 'e'}) "
+         "CREATE (:A {val: 4}) CREATE (:A {val: 5, name: 'e'})",
+         Query([Match([NodeP("a", ("A",))],
+                      where=[Ors(Equals(a("val"), IntegerLit(1)),
+                                 Ands(GreaterThanOrEqual(a("val"), IntegerLit(4)), Equals(a("name"), StringLit("e"))))])],
+               [ret(("a.val", a("val")), ("a.name", a("name")))]),
+         [{"a.val": 1, "a.name": "a"}, {"a.val": 5, "a.name": "e"}]),
+        ("pred_property_equality", PT + "145-163",
+         "CREATE (:A {val: 1})-[:REL]->(:B {p: 2}) CREATE (:A {val: 2})-[:REL]->(:B {p: 1}) "
+         "CREATE (:A {val: 100})-[:REL]->(:B {p: 100}) CREATE (:A {val: 1})-[:REL]->(:B) "
+         "CREATE (:A)-[:REL]->(:B {p: 2}) CREATE (:A)-[:REL]->(:B)",
+         Query([where(ab, Equals(a("val"), b("p")))], [ret(("b.p", b("p")))]), [{"b.p": 100}]),
+        ("pred_lt", PT + "166-178", "CREATE (:Node {val: 4})-[:REL]->(:Node {val: 5})",
+         Query([where(nm, LessThan(n("val"), m("val")))], [ret(("n.val", n("val")))]), [{"n.val": 4}]),
+        ("pred_lt_mixed", PT + "180-195", mixed_lt,
+         Query([where(ab, LessThan(a("val"), b("val2")))], a_val()), [{"a.val": 1}]),
+        ("pred_lt_incompatible", PT + "197-207", incompat,
+         Query([where(ab, LessThan(a("val"), b("val2")))], a_val()), []),
+        ("pred_le", PT + "209-225", chain3,
+         Query([where(nm, LessThanOrEqual(n("val"), m("val")))], [ret(("n.id", n("id")), ("n.val", n("val")))]),
+         [{"n.id": 1, "n.val": 4}, {"n.id": 2, "n.val": 5}]),
+        ("pred_le_mixed", PT + "227-243", mixed_le,
+         Query([where(ab, LessThanOrEqual(a("val"), b("val2")))], a_val()), [{"a.val": 4}, {"a.val": 1}]),
+        ("pred_le_incompatible", PT + "245-255", incompat,
+         Query([where(ab, LessThanOrEqual(a("val"), b("val2")))], a_val()), []),
+        ("pred_gt", PT + "257-268", "CREATE (:Node {val: 4})-[:REL]->(:Node {val: 5})",
+         Query([where(mn, GreaterThan(n("val"), m("val")))], [ret(("n.val", n("val")))]), [{"n.val": 5}]),
+        ("pred_gt_mixed", PT + "270-285", mixed_lt,
+         Query([where(ab, GreaterThan(a("val"), b("val2")))], a_val()), [{"a.val": 4}]),
+        ("pred_gt_incompatible", PT + "287-297", incompat,
+         Query([where(ab, GreaterThan(a("val"), b("val2")))], a_val()), []),
+        ("pred_ge", PT + "299-311", chain3,
+         Query([where(mn, GreaterThanOrEqual(n("val"), m("val")))], [ret(("n.id", n("id")), ("n.val", n("val")))]),
+         [{"n.id": 2, "n.val": 5}, {"n.id": 3, "n.val": 5}]),
+        ("pred_ge_mixed", PT + "313-329", mixed_ge,
+         Query([where(ab, GreaterThanOrEqual(a("val"), b("val2")))], a_val()), [{"a.val": 4}, {"a.val": 4}]),
+        ("pred_ge_incompatible", PT + "331-341", incompat,
+         Query([where(ab, GreaterThanOrEqual(a("val"), b("val2")))], a_val()), []),
+        ("pred_range_chain", PT + "344-357", "CREATE ({val: 10}), ({val: 0}), ({val: 11})",
+         Query([Match([NodeP("a")], where=[Ands(LessThan(IntegerLit(0), a("val")),
+                                                LessThanOrEqual(a("val"), IntegerLit(10)))])], a_val()),
+         [{"a.val": 10}]),
+        ("pred_float_division", PT + "359-371",
+         "CREATE (:Node {id: 1, val: 4}), (:Node {id: 2, val: 5}), (:Node {id: 3, val: 5})",
+         Query([Match([NodeP("n", ("Node",))],
+                      where=[GreaterThanOrEqual(Divide(Multiply(n("val"), FloatLit(1.0)), n("id")), FloatLit(2.5))])],
+               [ret(("n.id", n("id")))]),
+         [{"n.id": 1}, {"n.id": 2}]),
+    ]
+    return out
+
+
+def _order_cases():
+    """ORDER BY on a STRING key (String.compareTo order; CAPF_OP_STR_RANK)."""
+    MP = "morpheus-testing/src/test/scala/org/opencypher/morpheus/impl/MorpheusRecordsPrinterTest.scala:"
+    p = lambda v, k: ElementProperty(Var(v, "NODE"), k)  # noqa: E731
+    return [
+        ("order_by_string", MP + "136-160",
+         'CREATE (a:Person {name: "Alice"})-[:LIVES_IN]->(city:City)<-[:LIVES_IN]-(b:Person {name: "Bob"})',
+         Query([Match([NodeP("a", ("Person",)), NodeP("city", ("City",)), NodeP("b", ("Person",))],
+                      [RelP("_r1", "a", "city", ("LIVES_IN",)), RelP("_r2", "b", "city", ("LIVES_IN",))])],
+               [ret(("a.name", p("a", "name")), ("b.name", p("b", "name")), order_by=[("a.name", "asc")])]),
+         [{"a.name": "Alice", "b.name": "Bob"}, {"a.name": "Bob", "b.name": "Alice"}], {"ordered": True}),
+    ]
+
+
+EXPRESSION_CASES = (_null_cases() + _regex_cases() + _container_index_cases() + _map_cases() + _arith_cases()
+                    + _pred_cases() + _order_cases())

@@ -526,7 +526,18 @@ EXISTS_CASES = [
            [ret(("a.id", P("a", "id")))]),
      [{"a.id": 1}]),
 ]
-CASES = CASES + RETURN_CASES + EXISTS_CASES
+
+# The two pattern-predicate sections before it (:373-537 `WHERE (a)-->()-->(b)`,
+# :538-704 the same under "Inline pattern predicates") hold the same graphs,
+# queries and Bags as the EXISTS(...) section; the front end turns a pattern in
+# WHERE into that section's ExistsPattern, so they are its plans under their
+# own sources.
+_PP_STARTS = {"pattern": (373, 391, 404, 421, 438, 455, 472, 486, 508, 525, 537),
+              "inline": (539, 557, 570, 587, 604, 621, 638, 652, 674, 691, 703)}
+PATTERN_PREDICATE_CASES = [
+    (c[0].replace("exists_", f"{tag}_pred_"), f"MTa/PredicateTests.scala:{st[i]}-{st[i + 1] - 1}", *c[2:])
+    for tag, st in _PP_STARTS.items() for i, c in enumerate(EXISTS_CASES)]
+CASES = CASES + RETURN_CASES + EXISTS_CASES + PATTERN_PREDICATE_CASES
 
 
 # ------------------------------- AggregationTests "in WITH" / "without alias" (FTt)

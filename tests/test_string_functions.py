@@ -14,7 +14,8 @@ import numpy as np
 import pytest
 
 from capf_amd import _lib
-from capf_amd.expr import (Add, BoolLit, Equals, FloatLit, IntegerLit, LTrim, NullLit, Param, Replace, RTrim,
+from capf_amd.expr import (Add, BoolLit, Equals, FloatLit, GreaterThan, GreaterThanOrEqual, IntegerLit, LessThan,
+                           LessThanOrEqual, LTrim, NullLit, Param, Replace, RTrim,
                            StringLit, Substring, ToLower, ToString, ToUpper, Trim, Var, T_BOOL, T_FLOAT, T_INT,
                            T_STRING, java_double_str, string_fn)
 from capf_amd.header import RecordHeader
@@ -178,3 +179,75 @@ def test_value_map_cap_raises(gpu_session, monkeypatch):
     g = gpu_session.table(_cols())
     with pytest.raises(_lib.NotImplementedException):
         g.withColumns((ToString(Var("k")), "x"), header=H, params={}).rows
+
+
+# ------------------------------------------------------- string ordering
+# <, <=, >, >= on STRINGs (FlinkSQLExprMapper.scala:91-94, Flink compares
+# VARCHARs as java.lang.String.compareTo: UTF-16 code units) and ORDER BY on a
+# STRING key: on the GPU each string's rank in the session dictionary
+# (CAPF_OP_STR_RANK, a device table rebuilt when the dictionary grows).  An
+# INTEGER against a STRING orders to NULL (PredicateTests.scala:197-207).
+ORD_WORDS = ["alpha", "Alpha", "", "b", "ab", "abc", "Z", "straße", "strasse", "x\U0001F600", "x�",
+             "x", "é", "e", None]
+
+
+def _ord_cols(n=300, seed=11):
+    rng = np.random.default_rng(seed)
+    return [("s", T_STRING, [ORD_WORDS[i] for i in rng.integers(0, len(ORD_WORDS), n)], None),
+            ("t", T_STRING, [ORD_WORDS[i] for i in rng.integers(0, len(ORD_WORDS), n)], None),
+            ("k", T_INT, [int(x) for x in rng.integers(0, 1000, n)], None)]
+
+
+def test_java_string_compare_known_answers():
+    from oracle.table_np import _jcmp
+    assert _jcmp("a", "b") < 0 and _jcmp("B", "a") < 0 and _jcmp("", "a") < 0 and _jcmp("ab", "ab") == 0
+    assert _jcmp("abc", "ab") > 0 and _jcmp("straße", "strasse") > 0
+    # a supplementary character is a surrogate pair (D83D ..) and sorts below U+E000..U+FFFF
+    assert _jcmp("x\U0001F600", "x") < 0 and _jcmp("x\U0001F600", "x�") < 0
+    assert _jcmp("x\U0001F600", "xé") > 0
+
+
+ORD_PREDS = [LessThan(Var("s"), Var("t")), LessThanOrEqual(Var("s"), StringLit("b")),
+             GreaterThan(Var("s"), StringLit("x")), GreaterThanOrEqual(StringLit("alpha"), Var("t")),
+             LessThan(ToUpper(Var("s")), Var("t")), LessThan(Var("s"), NullLit("STRING"))]
+
+
+@pytest.mark.parametrize("e", ORD_PREDS + [LessThan(Var("s"), Var("k"))], ids=str)
+def test_oracle_string_order_runs(e):
+    rows = OracleSession().table(_ord_cols()).withColumns((e, "x"), header=OH, params={}).rows
+    assert len(rows) == 300
+
+
+OH = RecordHeader({Var("s"): "s", Var("t"): "t", Var("k"): "k"})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("e", ORD_PREDS + [LessThan(Var("s"), Var("k")), GreaterThanOrEqual(Var("k"), Var("t"))],
+                         ids=str)
+def test_string_order_predicates_gpu_parity(gpu_session, e):
+    """Each comparison as a column (TRUE / FALSE / NULL per row) and as a
+    filter: equal to the oracle's String.compareTo, row by row."""
+    cols = _ord_cols()
+    g, o = gpu_session.table(cols), OracleSession().table(cols)
+    rg = g.withColumns((e, "x"), header=OH, params={}).rows
+    ro = o.withColumns((e, "x"), header=OH, params={}).rows
+    assert [r["x"] for r in rg] == [r["x"] for r in ro]
+    assert g.filter(e, OH, {}).rows == o.filter(e, OH, {}).rows
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("desc", [False, True], ids=["asc", "desc"])
+def test_order_by_string_gpu_parity(gpu_session, desc):
+    """ORDER BY s, k (and ORDER BY toUpper(t), k): the same row order as the
+    oracle, NULLs where the ascending / descending sort puts them; again after
+    new strings entered the dictionary (the rank table is rebuilt)."""
+    cols = _ord_cols()
+    d = "desc" if desc else "asc"
+    for keys in ([(Var("s"), d), (Var("k"), "asc")], [(ToUpper(Var("t")), d), (Var("k"), "asc")]):
+        g, o = gpu_session.table(cols), OracleSession().table(cols)
+        assert g.orderBy(*keys, header=OH).rows == o.orderBy(*keys, header=OH).rows
+    more = [("s", T_STRING, ["zz", "aa", "m", None, "abd"], None), ("t", T_STRING, ["q"] * 5, None),
+            ("k", T_INT, [1, 2, 3, 4, 5], None)]
+    g, o = gpu_session.table(more), OracleSession().table(more)
+    keys = [(Var("s"), d)]
+    assert g.orderBy(*keys, header=OH).rows == o.orderBy(*keys, header=OH).rows

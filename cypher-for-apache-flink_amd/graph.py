@@ -61,7 +61,10 @@ def _join_type(a, b):
         return "FLOAT"
     if {a, b} == {"LIST(INTEGER)", "LIST(FLOAT)"}:
         return "LIST(FLOAT)"
-    raise NotImplementedError(f"property with conflicting types {a} / {b}")
+    # a property schema conflict (MatchTests.scala:380-418 expect an
+    # IllegalArgumentException; Flink's unionAll rejects unequal column types)
+    from ._lib import IllegalArgumentException
+    raise IllegalArgumentException(f"property with conflicting types {a} / {b}")
 
 
 @dataclass

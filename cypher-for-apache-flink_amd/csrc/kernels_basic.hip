@@ -542,10 +542,52 @@ __global__ void k_copy_part_int(ColView src, int64_t *dst, uint8_t *dval, int64_
   }
 }
 
+// LIST a ⊕ b: the offsets [na + nb + 1] with b's shifted by a's element
+// count, and the row flags (a NULL-typed side is all NULL lists: no offsets)
+__global__ void k_concat_list_offsets(const int64_t *ao, const uint8_t *av, int64_t na, const int64_t *bo,
+                                      const uint8_t *bv, int64_t nb, int64_t *o, uint8_t *ov) {
+  const int64_t atot = ao ? ao[na] : 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= na + nb;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    o[i] = i <= na ? (ao ? ao[i] : 0) : atot + (bo ? bo[i - na] : 0);
+    if (i < na) ov[i] = ao ? (av ? av[i] : 1) : 0;
+    else if (i < na + nb) ov[i] = bo ? (bv ? bv[i - na] : 1) : 0;
+  }
+}
+
+static ColPtr concat_lists(Session *s, const ColPtr &a, const ColPtr &b) {
+  const ColPtr ca = a->type == Type::List ? a->child : nullptr, cb = b->type == Type::List ? b->child : nullptr;
+  ColPtr child;
+  if (ca && cb) {  // the element columns one after the other
+    const Type et = ca->type == Type::Null ? cb->type : ca->type;
+    if (cb->type != Type::Null && cb->type != et)
+      illegal(std::string("Equal column types for union all: LIST(") + type_name(ca->type) + ") vs LIST(" +
+              type_name(cb->type) + ")");
+    child = concat_columns(s, ca, cb, et);
+  } else {  // one side holds no elements: the other's element column as is
+    child = ca ? ca : cb ? cb : null_column(s, Type::Null, 0);
+  }
+  const int64_t m = a->n + b->n;
+  auto o = std::make_shared<Column>();
+  o->type = Type::List;
+  o->n = m;
+  o->data = s->alloc(8 * (m + 1));
+  o->valid = s->alloc(std::max<int64_t>(m, 1));
+  o->child = child;
+  const bool al = a->type == Type::List && a->data, bl = b->type == Type::List && b->data;
+  hipLaunchKernelGGL(k_concat_list_offsets, dim3(grid_for(m + 1, 256)), dim3(256), 0, s->stream,
+                     al ? (const int64_t *)a->data->p : nullptr, al && a->valid ? (const uint8_t *)a->valid->p : nullptr,
+                     a->n, bl ? (const int64_t *)b->data->p : nullptr,
+                     bl && b->valid ? (const uint8_t *)b->valid->p : nullptr, b->n, (int64_t *)o->data->p,
+                     (uint8_t *)o->valid->p);
+  KERNEL_CHECK();
+  return o;
+}
+
 ColPtr concat_columns(Session *s, const ColPtr &a, const ColPtr &b, Type t) {
-  if (t == Type::List) not_impl("unionAll of list columns");
   force(a);
   force(b);
+  if (t == Type::List) return concat_lists(s, a, b);
   int64_t m = a->n + b->n;
   if (t == Type::Null) return null_column(s, t, m);
   bool with_valid = a->valid || b->valid || a->type == Type::Null || b->type == Type::Null;

@@ -1935,7 +1935,6 @@ capf_status capf_table_union_all(capf_table *l, capf_table *r, capf_table **out)
     if (x != y && x != Type::Null && y != Type::Null)
       illegal(std::string("Equal column types for union all: ") + a->names[i] + " " +
               type_name(x) + " vs " + type_name(y));
-    if (x == Type::List || y == Type::List) not_impl("unionAll of list columns");
     nn->types.push_back(x == Type::Null ? y : x);
   }
   *out = wrap(nn);

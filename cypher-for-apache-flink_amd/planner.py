@@ -83,7 +83,7 @@ class Unwind:
 @dataclass
 class Query:
     matches: List[object]  # Match / Unwind clauses in query order
-    stages: List[Stage]
+    stages: List[object]   # Stage (WITH / RETURN) and Unwind clauses after the first WITH
 
 
 # ------------------------------------------------------------- relational ops
@@ -718,8 +718,8 @@ def plan_query(graph, q: Query, params=None) -> Planned:
             op = plan_unwind(op, m, params)
             continue
         op = plan_optional(graph, m, op, params) if m.optional else plan_match(graph, m, op, params)
-    for st in q.stages:
-        op = plan_stage(op, st, params, graph)
+    for st in q.stages:  # WITH ... UNWIND list AS x ... RETURN (UnwindTests.scala:82-145)
+        op = plan_unwind(op, st, params) if isinstance(st, Unwind) else plan_stage(op, st, params, graph)
     return op
 
 

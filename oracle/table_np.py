@@ -839,8 +839,6 @@ class OracleTable:
         cols = {}
         for c in self._order:
             a, b = self._cols[c], other._cols[c]
-            if T_LIST in (a.t, b.t):
-                raise NotImplementedError("unionAll of list columns")
             t = a.t if a.t != T_NULL else b.t
             if a.t != b.t and T_NULL not in (a.t, b.t):
                 raise ValueError(f"Equal column types for union all: {c}")
@@ -1021,6 +1019,9 @@ class OracleTable:
                                                            name: Col(T_NULL, _empty_vals(T_NULL, 0), [])}, 0)
                 raise NotImplementedError(f"oracle: UNWIND of {e.expr}")
             lc = self._cols[src]
+            if lc.t == T_NULL:  # every row's list is NULL: no rows
+                return self._mk(self._order + [name], {**{c: k.take([]) for c, k in self._cols.items()},
+                                                       name: Col(T_NULL, _empty_vals(T_NULL, 0), [])}, 0)
             if lc.t != T_LIST:
                 raise ValueError("UNWIND of a non-list column")
             rows, els = [], []

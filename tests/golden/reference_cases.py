@@ -829,3 +829,8 @@ CASES = CASES + FUNCTION_CASES
 from expression_cases import EXPRESSION_CASES  # noqa: E402
 
 CASES = CASES + EXPRESSION_CASES
+
+# ------------------- MatchTests / UnwindTests / WithTests / ReturnTests / OptionalMatchTests (MTa)
+from clause_cases import CLAUSE_CASES, ERROR_CASES  # noqa: E402,F401
+
+CASES = CASES + CLAUSE_CASES

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 from conftest import bag, case_parts, check_case
-from reference_cases import CASES
+from reference_cases import CASES, ERROR_CASES
 
 from capf_amd import _lib
 from capf_amd.expr import (Add, Ands, Avg, BoolLit, Coalesce, Count, CountStar, Divide, ElementProperty,
@@ -43,6 +43,15 @@ def test_reference_case_on_gpu(gpu_session, case, compact, monkeypatch):
     want = run(og, query, opts.get("params"))
     assert check_case(got, want, {k: v for k, v in opts.items() if k != "row_count"}, reference=False) \
         if "row_count" not in opts else len(got) == len(want)
+
+
+@pytest.mark.parametrize("case", ERROR_CASES, ids=[c[0] for c in ERROR_CASES])
+def test_reference_error_case_on_gpu(gpu_session, case):
+    """The exception class the reference test expects (MatchTests.scala:380-418)."""
+    cid, src, create, query, exc = case
+    with pytest.raises(Exception) as ei:
+        run(ScanGraph.from_data(gpu_session, parse_create(create)), query)
+    assert type(ei.value).__name__ == exc, f"{cid} ({src}): {ei.value!r}"
 
 
 TWO_HOP = Query([Match([NodeP("a"), NodeP("b"), NodeP("c")], [RelP("r1", "a", "b"), RelP("r2", "b", "c")])],

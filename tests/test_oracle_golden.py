@@ -3,7 +3,7 @@ results of the reference's own acceptance tests (tests/golden/reference_cases.py
 import pytest
 
 from conftest import bag, case_parts, check_case
-from reference_cases import CASES
+from reference_cases import CASES, ERROR_CASES
 
 from capf_amd.graph import ScanGraph
 from capf_amd.planner import run
@@ -17,6 +17,15 @@ def test_reference_case_on_oracle(case):
     g = ScanGraph.from_data(OracleSession(), parse_create(create))
     got = run(g, query, opts.get("params"))
     assert check_case(got, expected, opts), f"{cid} ({src}): {got}"
+
+
+@pytest.mark.parametrize("case", ERROR_CASES, ids=[c[0] for c in ERROR_CASES])
+def test_reference_error_case_on_oracle(case):
+    """The reference test expects an exception of this class (MatchTests.scala:380-418)."""
+    cid, src, create, query, exc = case
+    with pytest.raises(Exception) as ei:
+        run(ScanGraph.from_data(OracleSession(), parse_create(create)), query)
+    assert type(ei.value).__name__ == exc, f"{cid} ({src}): {ei.value!r}"
 
 
 def test_create_parser_ids():

@@ -86,6 +86,16 @@ class Query:
     stages: List[object]   # Stage (WITH / RETURN) and Unwind clauses after the first WITH
 
 
+@dataclass
+class UnionQuery:
+    """q1 UNION [ALL] q2 (logical TabularUnionAll, RelationalPlanner.scala:123-124;
+    UNION adds a Distinct over the returned fields): both sides return the same
+    aliases."""
+    left: object   # Query | UnionQuery
+    right: Query
+    all: bool = False
+
+
 # ------------------------------------------------------------- relational ops
 @lru_cache(maxsize=16384)
 def _mk(cls, *args):
@@ -141,6 +151,34 @@ def union_all(a: Planned, b: Planned) -> Planned:
     tb = b.table.select(*[(b.header.column(e), a.header.column(e)) for e in exprs])
     ta = a.table.select(*[a.header.column(e) for e in exprs])
     return Planned(ta.unionAll(tb), RecordHeader({e: a.header.column(e) for e in exprs}))
+
+
+def union_queries(a: Planned, b: Planned) -> Planned:
+    """unionAll of two query results (RelationalPlanner.scala:374-391): the
+    combined header; each side's elements aligned to it — a label / type the
+    side lacks is FALSE, a property it lacks NULL of the other side's type
+    (alignExpressions :447-500) — every column renamed to one name per
+    expression (alignColumnNames), then TabularUnionAll (RelationalOperator
+    .scala:451-482; unequal column types raise there)."""
+    from .expr import BoolLit, HasLabel, HasType, NullLit
+    target = list(dict.fromkeys(a.header.expressions + b.header.expressions))
+    names = {e: f"__u{i}" for i, e in enumerate(target)}
+
+    def align(p: Planned, other: Planned) -> Planned:
+        missing = [e for e in target if e not in p.header]
+        for e in missing:
+            if isinstance(e, Var):
+                from ._lib import IllegalArgumentException
+                raise IllegalArgumentException(f"UNION: both sides must return the same columns ({e.vname})")
+        adds = [(BoolLit(False) if isinstance(e, (HasLabel, HasType)) else NullLit(getattr(e, "ctype", "ANY")),
+                 names[e]) for e in missing]
+        tab = p.table.select(*[(p.header.column(e), names[e]) for e in target if e in p.header])
+        if adds:
+            tab = tab.withColumns(*adds, header=RecordHeader({}), params={})
+        return Planned(tab.select(*[names[e] for e in target]), RecordHeader(names))
+
+    la, lb = align(a, b), align(b, a)
+    return Planned(la.table.unionAll(lb.table), la.header)
 
 
 def add_into(op: Planned, items: Sequence[Tuple[Expr, Expr]], params=None) -> Planned:
@@ -708,6 +746,9 @@ def plan_query(graph, q: Query, params=None) -> Planned:
     """The okapi relational plan of `q`, operator for operator.  Physical
     choices (fused counts, the fused var-length reach of config 5) are made by
     the backend below the Table SPI from the plan DAG these calls build."""
+    if isinstance(q, UnionQuery):
+        op = union_queries(plan_query(graph, q.left, params), plan_query(graph, q.right, params))
+        return op if q.all else Planned(op.table.distinct(), op.header)
     op = None
     if not q.matches:  # a leading RETURN / WITH: one row of the unit table (Start)
         op = Planned(graph.session.unit(), RecordHeader({}))
@@ -817,6 +858,10 @@ def records(op: Planned, aliases: Sequence[str]):
     return [dict(zip(aliases, row)) for row in zip(*cols)]
 
 
+def _aliases(q):
+    return _aliases(q.left) if isinstance(q, UnionQuery) else [a for a, _ in q.stages[-1].items]
+
+
 def run(graph, q: Query, params=None):
     op = plan_query(graph, q, params)
-    return records(op, [a for a, _ in q.stages[-1].items])
+    return records(op, _aliases(q))

@@ -19,13 +19,14 @@ import capf_import  # noqa: F401
 from capf_amd.expr import (Add, Ands, BoolLit, Collect, ElementProperty, Equals, GreaterThan, GreaterThanOrEqual, Id,
                            IntegerLit, LessThanOrEqual, ListLit, MapExpression, Not, NullLit, Param, StringLit, Type,
                            Var)
-from capf_amd.planner import CypherNode, Match, NodeP, Query, RelP, Stage, Unwind
+from capf_amd.planner import CypherNode, CypherRelationship, Match, NodeP, Query, RelP, Stage, UnionQuery, Unwind
 
 MT = "MTa/MatchTests.scala:"
 UT = "MTa/UnwindTests.scala:"
 WT = "MTa/WithTests.scala:"
 RT = "MTa/ReturnTests.scala:"
 OT = "MTa/OptionalMatchTests.scala:"
+NT = "MTa/UnionTests.scala:"
 
 
 def ret(*items, **kw):
@@ -319,7 +320,48 @@ def _optional_cases():
     ]
 
 
-CLAUSE_CASES = _match_cases() + _unwind_cases() + _with_cases() + _return_cases() + _optional_cases()
+def _union_cases():
+    """UnionTests.scala :39-264 (tabular UNION / UNION ALL; the graph unions
+    :266-300 are catalog features)."""
+    one = lambda v: Query([], [ret(("one", IntegerLit(v)))])  # noqa: E731
+    unw = lambda *xs: Query([Unwind(_ints(*xs), "i")], [ret(("i", Var("i")))])  # noqa: E731
+    ab = 'CREATE (a: A {val: "foo"}) CREATE (b: B {bar: "baz"})'
+    na, nb = node(0, ("A",), val="foo"), node(1, ("B",), bar="baz")
+    rels = ab + " CREATE (a)-[:REL1 {foo: 42}]->(b) CREATE (b)-[:REL2 {bar: true}]->(a)"
+    side = lambda v, lab: Query([Match([NodeP(v, (lab,)), NodeP("_t")], [RelP("r", v, "_t")])],  # noqa: E731
+                                [ret(("node", N(v)), ("rel", Var("r", "RELATIONSHIP")))])
+    pair = lambda x, lx, y, ly: Query([Match([NodeP(x, (lx,)), NodeP(y, (ly,))])],  # noqa: E731
+                                      [ret(("node1", N(x)), ("node2", N(y)))])
+    nodes_of = lambda v, lab: Query([Match([NodeP(v, (lab,))])], [ret(("node", N(v)))])  # noqa: E731
+    return [
+        ("union_all_simple", NT + "39-51", "", UnionQuery(one(1), one(2), all=True), [{"one": 1}, {"one": 2}]),
+        ("union_all_stacked", NT + "53-71", "",
+         UnionQuery(UnionQuery(UnionQuery(one(1), one(2), True), one(2), True), one(3), True),
+         [{"one": 1}, {"one": 2}, {"one": 2}, {"one": 3}]),
+        ("union_all_unwind", NT + "73-90", "", UnionQuery(unw(1, 2), unw(1, 2, 6), all=True),
+         [{"i": 1}, {"i": 2}, {"i": 1}, {"i": 2}, {"i": 6}]),
+        ("union_all_nodes", NT + "92-112", ab, UnionQuery(nodes_of("a", "A"), nodes_of("b", "B"), all=True),
+         [{"node": na}, {"node": nb}]),
+        ("union_all_nodes_rels", NT + "114-136", rels, UnionQuery(side("a", "A"), side("b", "B"), all=True),
+         [{"node": na, "rel": CypherRelationship(2, 0, 1, "REL1", (("foo", 42),))},
+          {"node": nb, "rel": CypherRelationship(3, 1, 0, "REL2", (("bar", True),))}]),
+        ("union_simple", NT + "140-152", "", UnionQuery(one(1), one(2)), [{"one": 1}, {"one": 2}]),
+        ("union_duplicates", NT + "154-165", "", UnionQuery(one(1), one(1)), [{"one": 1}]),
+        ("union_stacked", NT + "167-184", "", UnionQuery(UnionQuery(UnionQuery(one(1), one(2)), one(2)), one(3)),
+         [{"one": 1}, {"one": 2}, {"one": 3}]),
+        ("union_unwind", NT + "186-201", "", UnionQuery(unw(1, 2), unw(1, 2, 6)), [{"i": 1}, {"i": 2}, {"i": 6}]),
+        ("union_nodes", NT + "203-223", ab, UnionQuery(pair("a", "A", "b", "B"), pair("b", "B", "a", "A")),
+         [{"node1": na, "node2": nb}, {"node1": nb, "node2": na}]),
+        ("union_duplicate_nodes", NT + "225-243", 'CREATE (a: A {val: "foo"})',
+         UnionQuery(nodes_of("a", "A"), nodes_of("a", "A")), [{"node": node(0, ("A",), val="foo")}]),
+        ("union_duplicate_rels", NT + "245-264", "CREATE (a) CREATE (a)-[:REL {val: 42}]->(a)",
+         UnionQuery(*[Query([Match([NodeP("_s"), NodeP("_t")], [RelP("r", "_s", "_t")])],
+                            [ret(("rel", Var("r", "RELATIONSHIP")))])] * 2),
+         [{"rel": CypherRelationship(1, 0, 0, "REL", (("val", 42),))}]),
+    ]
+
+
+CLAUSE_CASES = _match_cases() + _unwind_cases() + _with_cases() + _return_cases() + _optional_cases() + _union_cases()
 
 # expected exception class name instead of a Bag (MatchTests.scala:380-418:
 # a property whose types conflict across label scans)

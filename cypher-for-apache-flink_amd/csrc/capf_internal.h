@@ -267,7 +267,8 @@ __device__ inline bool ft_load(const FtOperand &o, int64_t r, int64_t &val) {
 
 // ------------------------------------------------------------- plan nodes
 enum class Kind {
-  Source, Select, Filter, Join, Union, Distinct, Group, WithColumns, OrderBy, Skip, Limit, Explode, NameList
+  Source, Select, Filter, Join, Union, Distinct, Group, WithColumns, OrderBy, Skip, Limit, Explode, NameList,
+  ListColumns
 };
 
 struct AggSpec {
@@ -311,6 +312,9 @@ struct Node {
   std::vector<int> name_cols;
   std::vector<int32_t> name_kinds;
   std::vector<int64_t> name_codes;
+  // ListColumns (a list literal of per-row elements): the child's columns
+  // name_cols, row i's list = (col0[i], ..., colk-1[i]) of element type list_elem
+  Type list_elem = Type::Null;
 
   // memoised result
   std::mutex mu;
@@ -536,6 +540,8 @@ DataPtr explode_values(Session *s, const Data &d, const ColPtr &values);
 ColPtr name_list_column(Session *s, const Data &d, const std::vector<int> &cols, const std::vector<int32_t> &kinds,
                         const std::vector<int64_t> &codes);
 DataPtr explode_list(Session *s, const Data &d, int list_col);
+// LIST column whose row i is (d.cols[cols[0]][i], ..., d.cols[cols[k-1]][i]) (lists.hip)
+ColPtr list_from_columns(Session *s, const Data &d, const std::vector<int> &cols, Type elem);
 // collect(arg) per group (lists.hip): a Type::List column of g.ngroups lists.
 ColPtr collect_lists(Session *s, const Grouping &g, int64_t nrows, const ColPtr &arg,
                      bool distinct);

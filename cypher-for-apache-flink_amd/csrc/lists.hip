@@ -316,4 +316,55 @@ ColPtr name_list_column(Session *s, const Data &d, const std::vector<int> &cols,
   return list_column(s, n, off, child);
 }
 
+// ------------------------------------------------- list literals per row
+// Element j of every row: child[i * k + j] = column j's value (an INTEGER
+// widened to FLOAT when the list's element type is FLOAT); a NULL element
+// raises the flag (LIST columns hold no NULL elements).
+__global__ void k_list_elem(ColView c, int64_t n, int32_t k, int32_t j, int32_t elem, void *child,
+                            uint32_t *null_seen) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (c.type == CAPF_TYPE_NULL || (c.valid && !c.valid[i])) null_seen[0] = 1u;
+    const int64_t o = i * k + j;
+    if (elem == CAPF_TYPE_BOOL) {
+      ((uint8_t *)child)[o] = c.data ? (((const uint8_t *)c.data)[i] ? 1 : 0) : 0;
+    } else if (elem == CAPF_TYPE_FLOAT64) {
+      ((double *)child)[o] = !c.data ? 0.0
+                             : c.type == CAPF_TYPE_FLOAT64 ? ((const double *)c.data)[i] : (double)ld_int(c, i);
+    } else {
+      ((int64_t *)child)[o] = c.data ? ld_int(c, i) : 0;
+    }
+  }
+}
+
+__global__ void k_list_offsets_stride(int64_t *off, int64_t n, int32_t k) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x)
+    off[i] = i * k;
+}
+
+ColPtr list_from_columns(Session *s, const Data &d, const std::vector<int> &cols, Type elem) {
+  const int64_t n = d.nrows;
+  const int32_t k = (int32_t)cols.size();
+  BufPtr off = s->alloc(8 * (n + 1));
+  hipLaunchKernelGGL(k_list_offsets_stride, dim3(grid_for(n + 1, 256)), dim3(256), 0, s->stream,
+                     (int64_t *)off->p, n, k);
+  KERNEL_CHECK();
+  ColPtr child = k == 0 ? empty_elements(s, elem) : make_column(s, elem, n * k, false);
+  if (n > 0 && k > 0) {
+    BufPtr flag = s->alloc(4);
+    HIP_CHECK(hipMemsetAsync(flag->p, 0, 4, s->stream));
+    for (int32_t j = 0; j < k; ++j) {
+      const ColPtr &c = d.cols[(size_t)cols[(size_t)j]];
+      const ColView v = c->type == Type::Null ? ColView{nullptr, nullptr, CAPF_TYPE_NULL, ENC_PLAIN, 0} : view_of(c);
+      hipLaunchKernelGGL(k_list_elem, dim3(grid_for(n, 256)), dim3(256), 0, s->stream, v, n, k, j, (int32_t)elem,
+                         child->data->p, (uint32_t *)flag->p);
+      KERNEL_CHECK();
+    }
+    uint32_t seen = 0;
+    HIP_CHECK(hipMemcpyAsync(&seen, flag->p, 4, hipMemcpyDeviceToHost, s->stream));
+    s->sync();
+    if (seen) not_impl("a NULL element in a list (LIST columns hold no NULL elements)");
+  }
+  return list_column(s, n, off, child);
+}
+
 }  // namespace capf

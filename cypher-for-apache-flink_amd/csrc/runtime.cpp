@@ -659,6 +659,14 @@ static DataPtr materialize_impl(const NodePtr &n) {
       out->cols.push_back(name_list_column(s, *c, n->name_cols, n->name_kinds, n->name_codes));
       return out;
     }
+    case Kind::ListColumns: {
+      DataPtr c = materialize(n->kids[0]);
+      auto out = std::make_shared<Data>();
+      out->nrows = c->nrows;
+      out->cols = c->cols;
+      out->cols.push_back(list_from_columns(s, *c, n->name_cols, n->list_elem));
+      return out;
+    }
     case Kind::WithColumns: {
       DataPtr c = materialize(n->kids[0]);
       auto out = std::make_shared<Data>();
@@ -2215,6 +2223,39 @@ capf_status capf_table_name_list(capf_table *t, int32_t n, const char *const *co
     nn->name_kinds.push_back(kinds[j]);
     nn->name_codes.push_back(codes[j]);
   }
+  nn->names.emplace_back(name);
+  nn->types.push_back(Type::List);
+  *out = wrap(nn);
+  CAPF_API_END
+}
+
+capf_status capf_table_list_columns(capf_table *t, int32_t n, const char *const *cols, const char *name,
+                                    capf_table **out) {
+  CAPF_API_BEGIN
+  need(t, "table");
+  need(name, "name");
+  need(out, "out");
+  if (n < 0 || (n > 0 && !cols)) illegal("bad list element columns");
+  const NodePtr &c = t->node;
+  if (c->col_index(name) >= 0) illegal(std::string("column '") + name + "' already exists");
+  auto nn = new_node(c->s, Kind::ListColumns);
+  nn->kids.push_back(c);
+  nn->names = c->names;
+  nn->types = c->types;
+  Type et = Type::Null;
+  for (int32_t j = 0; j < n; ++j) {
+    const int idx = c->col_index_or_throw(cols[j]);
+    const Type ct = c->types[(size_t)idx];
+    if (ct == Type::List) not_impl("nested lists");
+    if (ct == Type::Null) not_impl("a NULL element in a list (LIST columns hold no NULL elements)");
+    if (et == Type::Null || et == ct) et = ct;
+    else if ((et == Type::Int64 || et == Type::Float64) && (ct == Type::Int64 || ct == Type::Float64))
+      et = Type::Float64;  // INTEGER and FLOAT elements widen together
+    else
+      not_impl(std::string("a list of mixed element types ") + type_name(et) + " / " + type_name(ct));
+    nn->name_cols.push_back(idx);
+  }
+  nn->list_elem = et;
   nn->names.emplace_back(name);
   nn->types.push_back(Type::List);
   *out = wrap(nn);

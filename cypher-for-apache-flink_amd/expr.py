@@ -671,6 +671,22 @@ def _value_type(v):
     return None
 
 
+def literal_expr(v):
+    """The literal expression of a host value (a list parameter's element)."""
+    if v is None:
+        return NullLit()
+    if isinstance(v, bool):
+        return BoolLit(v)
+    if isinstance(v, int):
+        return IntegerLit(v)
+    if isinstance(v, float):
+        return FloatLit(v)
+    if isinstance(v, str):
+        return StringLit(v)
+    from ._lib import NotImplementedException
+    raise NotImplementedException(f"a list element {v!r} of type {type(v).__name__}")
+
+
 def _comparable(a, b):
     """Could values of capf types a and b be equal?  (None: unknown.)"""
     if a is None or b is None or T_NULL in (a, b):

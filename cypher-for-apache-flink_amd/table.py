@@ -598,6 +598,19 @@ class GpuTable:
         return "\x01vmap:%d" % mid.value
 
     def withColumns(self, *columns, header=None, params=None):
+        lit = [(e, c) for e, c in columns if _list_items(e, params) is not None]
+        if lit:  # [x, y, ...] / $list: LIST columns of per-row elements (capf_table_list_columns)
+            plain = [(e, c) for e, c in columns if (e, c) not in lit]
+            t = self.withColumns(*plain, header=header, params=params) if plain else self
+            keep = list(t.physicalColumns)
+            for i, (e, c) in enumerate(lit):
+                items = _list_items(e, params)
+                tmp = [f"\x03le{i}.{j}" for j in range(len(items))]
+                if items:
+                    t = t.withColumns(*zip(items, tmp), header=header, params=params)
+                t = t._new("capf_table_list_columns", t._h, len(tmp), _lib.strs(tmp), c.encode())
+                keep.append(c)
+            return t.select(*keep)
         is_list = lambda e: type(e).__name__ in ("Labels", "Keys") and type(e.expr).__name__ != "NullLit"  # noqa: E731
         lists = [(e, c) for e, c in columns if is_list(e)]
         if lists:  # labels(n) / keys(n): LIST columns built by capf_table_name_list
@@ -649,6 +662,20 @@ class GpuTable:
         _lib.call("capf_chain2_local_hists", self.session._h, self._h, src_col.encode(), dst_col.encode(),
                   int(node_base), int(n_nodes), c_void_p(d_in), c_void_p(d_out), byref(loops))
         return loops.value
+
+
+def _list_items(e, params):
+    """The element expressions of a list-valued projection item — a list
+    literal, or a parameter holding a list (FlinkSQLExprMapper.scala:71, 75) —
+    else None."""
+    from .expr import ListLit, Param, literal_expr
+    if isinstance(e, ListLit):
+        return list(e.items)
+    if isinstance(e, Param):
+        v = (params or {}).get(e.pname)
+        if isinstance(v, (list, tuple)):
+            return [literal_expr(x) for x in v]
+    return None
 
 
 def compact_as(table, compact):

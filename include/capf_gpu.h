@@ -650,6 +650,15 @@ capf_status capf_session_code_map(capf_session *s, const int64_t *codes, int64_t
  * bytes or NULL): 0 = a NULL list.                                         */
 capf_status capf_table_add_list(capf_table *t, const char *name, int32_t elem_type, const int64_t *offsets,
                                 const void *values, const uint8_t *valid, capf_table **out);
+
+/* This table plus LIST column `name` whose row i holds (cols[0][i], ...,
+ * cols[n-1][i]) — a list literal of per-row elements, `[n.val * 10, $p]`
+ * (replaces FlinkSQLExprMapper.scala:71 `array(...)` over the converted
+ * children).  The element columns share one type (INTEGER and FLOAT widen to
+ * FLOAT); a NULL-typed or NULL-holding element is NotImplemented (LIST columns
+ * hold no NULL elements), as are nested lists.  n = 0: the empty list.       */
+capf_status capf_table_list_columns(capf_table *t, int32_t n, const char *const *cols, const char *name,
+                                    capf_table **out);
 /* labels(n) / keys(n) (FlinkSQLExprMapper.scala:136-153; the GetLabels /
  * GetKeys UDFs, :310-329): appends LIST<STRING> column `name` holding, per row,
  * codes[j] for each column cols[j] that holds TRUE (kinds[j] = 0, a label flag)

@@ -541,6 +541,13 @@ JNI(jlong, tableNameList)(JNIEnv *env, jobject, jlong t, jobjectArray cols, jint
   return fail(env, capf_table_name_list(T(t), (int32_t)k.size(), c.data(), k.data(), cd.data(), nm.p, &out)) ? 0
                                                                                                            : H(out);
 }
+// a list literal of per-row elements (FlinkSQLExprMapper.scala:71 array(...))
+JNI(jlong, tableListColumns)(JNIEnv *env, jobject, jlong t, jobjectArray cols, jstring name) {
+  JStrs c(env, cols);
+  JStr nm(env, name);
+  capf_table *out = nullptr;
+  return fail(env, capf_table_list_columns(T(t), c.n(), c.data(), nm.p, &out)) ? 0 : H(out);
+}
 JNI(jlong, tableWithColumns)(JNIEnv *env, jobject, jlong t, jobjectArray exprs,
                              jobjectArray names) {  // Table.scala:170
   Programs e(env, exprs);

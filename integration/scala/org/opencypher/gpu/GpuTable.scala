@@ -99,6 +99,18 @@ final class GpuTable private (private[gpu] val handle: Long)(implicit val sessio
   }
 
   override def withColumns(columns: (Expr, String)*)(implicit header: RecordHeader, parameters: CypherMap): GpuTable = { // :170
+    val (literalLists, others) = columns.partition { case (e, _) => listItems(e, parameters).isDefined }
+    if (literalLists.nonEmpty) {  // [x, y, ...] / $list (FlinkSQLExprMapper.scala:71, 75): capf_table_list_columns
+      val base = if (others.isEmpty) this else withColumns(others: _*)
+      val keep = base.physicalColumns
+      val built = literalLists.zipWithIndex.foldLeft(base) { case (t, ((e, col), i)) =>
+        val items = listItems(e, parameters).get
+        val tmp = items.indices.map(j => s"\u0003le$i.$j")
+        val withItems = if (items.isEmpty) t else t.withColumns(items.zip(tmp): _*)
+        wrap(Native.tableListColumns(withItems.handle, tmp.toArray, col))
+      }
+      return built.select(keep ++ literalLists.map(_._2): _*)
+    }
     val (lists, rest) = columns.partition { case (e, _) => e.isInstanceOf[Labels] || e.isInstanceOf[Keys] }
     val (explodes, plain) = rest.partition { case (e, _) => e.isInstanceOf[Explode] }
     val base =
@@ -108,6 +120,23 @@ final class GpuTable private (private[gpu] val handle: Long)(implicit val sessio
         plain.map(_._2).toArray))
     val withLists = lists.foldLeft(base) { case (t, (e, col)) => t.nameList(e, col, header) }
     explodes.foldLeft(withLists) { case (t, (Explode(list), col)) => t.explode(list, col, header, parameters) }
+  }
+
+  /** The element expressions of a list literal, or of a parameter holding a list. */
+  private def listItems(e: Expr, parameters: CypherMap): Option[Seq[Expr]] = e match {
+    case ListLit(items) => Some(items)
+    case Param(p) => parameters.value.get(p) match {
+      case Some(CypherList(vs)) => Some(vs.map {
+        case CypherNull => NullLit()
+        case CypherInteger(v) => IntegerLit(v)
+        case CypherFloat(v) => FloatLit(v)
+        case CypherString(v) => StringLit(v)
+        case CypherBoolean(v) => if (v) TrueLit else FalseLit
+        case other => throw NotImplementedException(s"GPU list element $other")
+      })
+      case _ => None
+    }
+    case _ => None
   }
 
   /** labels(n) / keys(n) (FlinkSQLExprMapper.scala:136-153): the label flag columns

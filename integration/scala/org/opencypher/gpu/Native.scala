@@ -141,6 +141,7 @@ object Native {
   @native def tableAddList(table: Long, name: String, elemType: Int, offsets: java.nio.ByteBuffer,
                            values: java.nio.ByteBuffer, valid: java.nio.ByteBuffer): Long
   @native def tableNameList(table: Long, cols: Array[String], kinds: Array[Int], codes: Array[Long], name: String): Long
+  @native def tableListColumns(table: Long, cols: Array[String], name: String): Long
   @native def tableShow(table: Long, rows: Int): Unit
 
   // graph inputs (EdgeListDataSource.scala:56-92; synthetic R-MAT / node ranges)

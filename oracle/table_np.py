@@ -244,6 +244,19 @@ def evaluate(e, table, header, params):
             return const(T_STRING, x.v)
         if isinstance(x, NullLit):
             return const(CT_TO_CAPF.get(x.ctype, T_NULL), None, False)
+        if isinstance(x, ListLit) or (isinstance(x, Param) and isinstance(params.get(x.pname), (list, tuple))):
+            # a list value per row (FlinkSQLExprMapper.scala:71 array(...), :75):
+            # INTEGER elements widen to FLOAT beside a FLOAT one
+            items = [go(y) for y in x.items] if isinstance(x, ListLit) else None
+            vals = list(params[x.pname]) if items is None else None
+            out = np.empty(n, dtype=object)
+            for i in range(n):
+                row = vals if items is None else [(y.v[i].item() if hasattr(y.v[i], "item") else y.v[i])
+                                                  if y.ok[i] else None for y in items]
+                if any(isinstance(v, float) for v in row):
+                    row = [float(v) if isinstance(v, int) and not isinstance(v, bool) else v for v in row]
+                out[i] = list(row)
+            return Val(T_LIST, out, np.ones(n, bool))
         if isinstance(x, Param):
             p = params[x.pname]
             if p is None:

@@ -16,7 +16,7 @@ MatchTests schema conflicts (:380-418) expect an exception, not a Bag:
 ERROR_CASES.
 """
 import capf_import  # noqa: F401
-from capf_amd.expr import (Add, Ands, BoolLit, Collect, ElementProperty, Equals, GreaterThan, GreaterThanOrEqual, Id,
+from capf_amd.expr import (Add, Ands, BoolLit, Collect, Count, ElementProperty, Equals, GreaterThan, GreaterThanOrEqual, Id,
                            IntegerLit, LessThanOrEqual, ListLit, MapExpression, Not, NullLit, Param, StringLit, Type,
                            Var)
 from capf_amd.planner import CypherNode, CypherRelationship, Match, NodeP, Query, RelP, Stage, UnionQuery, Unwind
@@ -361,7 +361,19 @@ def _union_cases():
     ]
 
 
-CLAUSE_CASES = _match_cases() + _unwind_cases() + _with_cases() + _return_cases() + _optional_cases() + _union_cases()
+# AggregationTests.scala holds four-fifths of its cases in the Flink copy too
+# (FTt/acceptance/AggregationTests.scala, transcribed in reference_cases.py);
+# the morpheus-only ones are temporal (no Flink lowering) and this one
+AGG_CASES = [
+    ("count_distinct_grouped", "MTa/AggregationTests.scala:258-277",
+     'CREATE (a:Start{id: 1}) CREATE (a)-[:REL]->({val: "foo"}) CREATE (a)-[:REL]->({val: "foo"})',
+     Query([Match([NodeP("a", ("Start",)), NodeP("b")], [RelP("_r", "a", "b")])],
+           [ret(("a.id", P("a", "id")), ("val", Count(P("b", "val"), True)))]),
+     [{"a.id": 1, "val": 1}]),
+]
+
+
+CLAUSE_CASES = _match_cases() + _unwind_cases() + _with_cases() + _return_cases() + _optional_cases() + _union_cases() + AGG_CASES
 
 # expected exception class name instead of a Bag (MatchTests.scala:380-418:
 # a property whose types conflict across label scans)
@@ -377,4 +389,6 @@ ERROR_CASES = [
      "IllegalArgumentException"),
     ("match_conflict_bool_int_string", MT + "412-418", "CREATE (:A {f: true}), (:B {f: 1}), (:C {f: 'hi'})",
      _CONFLICT, "IllegalArgumentException"),
+    ("expr_property_any_type", "MTa/ExpressionTests.scala:342-352", "CREATE (:A {val: 'foo'}), (:B {val: 1}), (:C)",
+     Query([Match([NodeP("a")])], [ret(("a.val", P("a", "val")))]), "IllegalArgumentException"),
 ]

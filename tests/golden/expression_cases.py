@@ -421,5 +421,61 @@ def _order_cases():
     ]
 
 
+def _literal_cases():
+    """ExpressionTests.scala: addition of literals (:420-442 — the reference
+    draws 100 random pairs per run; eight fixed draws each here, sums that fit
+    an INTEGER: an overflowing literal sum is the front end's SemanticError),
+    list literals and list parameters as values (:769-808, :1146-1165; the
+    FlinkSQLExprMapper.scala:71 `array`), string concatenation (:923-978)."""
+    import random
+    from capf_amd.expr import ListLit, Multiply, Param
+    rnd = random.Random(420)
+    ints = []
+    while len(ints) < 8:
+        a, b = rnd.randint(-2 ** 63, 2 ** 63 - 1), rnd.randint(-2 ** 63, 2 ** 63 - 1)
+        if -2 ** 63 <= a + b < 2 ** 63:
+            ints.append((a, b))
+    ints += [(0, 0), (-1, 1), (2 ** 62, 2 ** 62 - 1)]
+    floats = [(rnd.uniform(-1e300, 1e300), rnd.uniform(-1e300, 1e300)) for _ in range(4)]
+    floats += [(rnd.gauss(0, 1), rnd.gauss(0, 1e-300)) for _ in range(4)]
+    floats += [(1.7976931348623157e308, 1.7976931348623157e308), (0.1, 0.2), (-0.0, 0.0)]
+    out = [(f"expr_int_add_{i}", ET + "420-433", "", unit(("result", Add(IntegerLit(a), IntegerLit(b)))),
+            [{"result": a + b}]) for i, (a, b) in enumerate(ints)]
+    out += [(f"expr_float_add_{i}", ET + "435-442", "", unit(("result", Add(FloatLit(a), FloatLit(b)))),
+             [{"result": a + b}]) for i, (a, b) in enumerate(floats)]
+    n = lambda v, k: ElementProperty(Var(v, "NODE"), k)  # noqa: E731
+    ab = lambda *items: Query([Match([NodeP("a", ("A",)), NodeP("b", ("B",))])], [ret(*items)])  # noqa: E731
+    with_list = lambda lst, alias: [ret((alias, lst)), ret((alias, Var(alias)))]  # noqa: E731
+    out += [
+        ("expr_list_string_params", ET + "769-780", "CREATE ()",
+         Query([], with_list(ListLit(Param("a"), Param("b")), "strings")), [{"strings": ["bar", "foo"]}],
+         {"params": {"a": "bar", "b": "foo"}}),
+        ("expr_list_strings", ET + "782-793", "CREATE ()",
+         Query([], with_list(ListLit(StringLit("bar"), StringLit("foo")), "strings")), [{"strings": ["bar", "foo"]}]),
+        ("expr_list_expressions", ET + "795-808", "CREATE ({val: 1}), ({val: 2})",
+         Query([Match([NodeP("n")])],
+               with_list(ListLit(Multiply(n("n", "val"), IntegerLit(10)), Multiply(n("n", "val"), IntegerLit(100))),
+                         "vals")),
+         [{"vals": [10, 100]}, {"vals": [20, 200]}]),
+        ("expr_list_parameter", ET + "1146-1151", "", unit(("res", Param("listParam"))), [{"res": [1, 2]}],
+         {"params": {"listParam": [1, 2]}}),
+        ("expr_list_empty_parameter", ET + "1160-1165", "", unit(("res", Param("listParam"))), [{"res": []}],
+         {"params": {"listParam": []}}),
+        ("expr_concat_literals", ET + "923-930", "", unit(("hello", Add(StringLit("Hello"), StringLit("World")))),
+         [{"hello": "HelloWorld"}]),
+        ("expr_concat_properties", ET + "932-946", 'CREATE (:A {a: "Hello"}) CREATE (:B {b: "World"})',
+         ab(("hello", Add(n("a", "a"), n("b", "b")))), [{"hello": "HelloWorld"}]),
+        ("expr_concat_string_integer", ET + "948-962",
+         'CREATE (:A {a1: "Hello", a2: 42}) CREATE (:B {b1: 42, b2: "Hello"})',
+         ab(("hello", Add(n("a", "a1"), n("b", "b1"))), ("world", Add(n("a", "a2"), n("b", "b2")))),
+         [{"hello": "Hello42", "world": "42Hello"}]),
+        ("expr_concat_string_float", ET + "964-978",
+         'CREATE (:A {a1: "Hello", a2: 42.0}) CREATE (:B {b1: 42.0, b2: "Hello"})',
+         ab(("hello", Add(n("a", "a1"), n("b", "b1"))), ("world", Add(n("a", "a2"), n("b", "b2")))),
+         [{"hello": "Hello42.0", "world": "42.0Hello"}]),
+    ]
+    return out
+
+
 EXPRESSION_CASES = (_null_cases() + _regex_cases() + _container_index_cases() + _map_cases() + _arith_cases()
-                    + _pred_cases() + _order_cases())
+                    + _pred_cases() + _order_cases() + _literal_cases())

@@ -299,6 +299,8 @@ class JniRoute:
         A["capf_table_name_list"] = new_table("tableNameList", lambda t, k, cols, kinds, codes, col:
                                               (h(t), self.jstrs(cols, k), self.jints(kinds, k),
                                                self.jlongs(codes, k), self.jstr(col)))
+        A["capf_table_list_columns"] = new_table("tableListColumns", lambda t, k, cols, col:
+                                                 (h(t), self.jstrs(cols, k), self.jstr(col)))
         A["capf_table_add_list"] = new_table(
             "tableAddList", lambda t, col, et, offs, vals, valid:
             (h(t), self.jstr(col), (I, et), self.direct(offs), self.direct(vals), self.direct(valid)))

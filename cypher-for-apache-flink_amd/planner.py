@@ -84,6 +84,10 @@ class Unwind:
 class Query:
     matches: List[object]  # Match / Unwind clauses in query order
     stages: List[object]   # Stage (WITH / RETURN) and Unwind clauses after the first WITH
+    # the driving table of `session.cypher(query, drivingTable = records)`
+    # (RelationalCypherSession.scala:122-145): (name, capf type, values, valid)
+    # columns, each bound to the variable of its name
+    driving: Optional[List[tuple]] = None
 
 
 @dataclass
@@ -750,7 +754,9 @@ def plan_query(graph, q: Query, params=None) -> Planned:
         op = union_queries(plan_query(graph, q.left, params), plan_query(graph, q.right, params))
         return op if q.all else Planned(op.table.distinct(), op.header)
     op = None
-    if not q.matches:  # a leading RETURN / WITH: one row of the unit table (Start)
+    if q.driving is not None:  # Start over the driving table's records (RelationalPlanner.scala:90)
+        op = Planned(graph.session.table(list(q.driving)), RecordHeader({Var(c[0]): c[0] for c in q.driving}))
+    if not q.matches and op is None:  # a leading RETURN / WITH: one row of the unit table (Start)
         op = Planned(graph.session.unit(), RecordHeader({}))
     for m in q.matches:
         if isinstance(m, Unwind):

@@ -361,6 +361,32 @@ def _union_cases():
     ]
 
 
+def _driving_cases():
+    """DrivingTableTests.scala :54-137: `cypher(query, drivingTable = records)`
+    — the records (age INTEGER, name STRING) are the plan's Start table."""
+    from capf_amd.expr import T_INT, T_STRING
+    DT = "MTa/DrivingTableTests.scala:"
+    drv = [("age", T_INT, [10, 20, 15], None), ("name", T_STRING, ["Alice", "Bob", "Carol"], None)]
+    people = ('CREATE (:Person {name: "George", age: 20}) CREATE (:Person {name: "Frank", age: 50}) '
+              'CREATE (:Person {name: "Jon", age: 15})')
+    pn = [ret(("p.name", P("p", "name")), ("name", Var("name")))]
+    want = [{"p.name": "George", "name": "Bob"}, {"p.name": "Jon", "name": "Carol"}]
+    by_age = Match([NodeP("p", ("Person",))], [], [Equals(P("p", "age"), Var("age"))])
+    return [
+        ("driving_return", DT + "54-63", "", Query([], [ret(("age", Var("age")), ("name", Var("name")))], drv),
+         [{"age": 10, "name": "Alice"}, {"age": 20, "name": "Bob"}, {"age": 15, "name": "Carol"}]),
+        ("driving_unwind", DT + "65-78", "",
+         Query([Unwind(_ints(1, 2), "i")], [ret(("i", Var("i")), ("age", Var("age")), ("name", Var("name")))], drv),
+         [{"i": i, "age": a, "name": n} for i in (1, 2) for a, n in ((10, "Alice"), (20, "Bob"), (15, "Carol"))]),
+        ("driving_filter", DT + "82-99", people, Query([by_age], pn, drv), want),
+        ("driving_pattern_properties", DT + "101-117", people, Query([by_age], pn, drv), want),
+        ("driving_complex_match", DT + "119-137",
+         'CREATE (b:B) CREATE (:Person {name: "George", age: 20})-[:REL]->(b) '
+         'CREATE (:Person {name: "Frank", age: 50})-[:REL]->(b) CREATE (:Person {name: "Jon", age: 15})-[:REL]->(b)',
+         Query([by_age, Match([NodeP("p"), NodeP("_t")], [RelP("_r", "p", "_t")])], pn, drv), want),
+    ]
+
+
 # AggregationTests.scala holds four-fifths of its cases in the Flink copy too
 # (FTt/acceptance/AggregationTests.scala, transcribed in reference_cases.py);
 # the morpheus-only ones are temporal (no Flink lowering) and this one
@@ -373,7 +399,7 @@ AGG_CASES = [
 ]
 
 
-CLAUSE_CASES = _match_cases() + _unwind_cases() + _with_cases() + _return_cases() + _optional_cases() + _union_cases() + AGG_CASES
+CLAUSE_CASES = _match_cases() + _unwind_cases() + _with_cases() + _return_cases() + _optional_cases() + _union_cases() + _driving_cases() + AGG_CASES
 
 # expected exception class name instead of a Bag (MatchTests.scala:380-418:
 # a property whose types conflict across label scans)

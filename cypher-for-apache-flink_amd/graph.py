@@ -83,17 +83,18 @@ class ElementTable:
 
 
 class ScanGraph:
-    def __init__(self, session, node_tables, rel_tables):
+    def __init__(self, session, node_tables, rel_tables, validate=True):
         self.session = session
         self.node_tables = list(node_tables)
         self.rel_tables = list(rel_tables)
         # ScanGraph.validate: one table per label combination / rel type
-        # (okapi-relational/.../impl/graph/ScanGraph.scala:115-143)
+        # (okapi-relational/.../impl/graph/ScanGraph.scala:115-143); a union
+        # graph scans every member's tables (UnionGraph.scala:74-115)
         combos = [t.labels for t in self.node_tables]
-        if len(combos) != len(set(combos)):
+        if validate and len(combos) != len(set(combos)):
             raise ValueError("more than one node table per label combination")
         types = [t.labels for t in self.rel_tables]
-        if len(types) != len(set(types)):
+        if validate and len(types) != len(set(types)):
             raise ValueError("more than one relationship table per type")
         # aligned scans per (element tables, labels, properties), built once
         # with canonical column names and renamed per variable by a zero-copy
@@ -145,6 +146,28 @@ class ScanGraph:
             t = session.table(cols, nrows=len(rows))
             rel_tables.append(ElementTable("rel", frozenset([typ]), compact_as(t, compact), keys))
         return ScanGraph(session, node_tables, rel_tables)
+
+    def union_all(self, *others):
+        """graph.unionAll(others) (RelationalCypherGraph.scala:124-139): member i
+        is PrefixedGraph(g, i) — every element id (and rel endpoint) tagged with
+        the graph's index in its top byte (PrefixId; ids are LONGs here, so the
+        tag is i << 56 on ids below 2^56) — and the union scans all members'
+        tables (UnionGraph.scala:74-115)."""
+        from ._lib import IllegalArgumentException
+        from .expr import Add, IntegerLit
+        nodes, rels = [], []
+        for i, g in enumerate((self,) + others):
+            if g.session is not self.session:
+                raise IllegalArgumentException("union of graphs of different sessions")
+            for t in g.node_tables + g.rel_tables:
+                cols = [t.id_col] + ([t.src_col, t.dst_col] if t.kind == "rel" else [])
+                tab = t.table
+                if i:
+                    h = RecordHeader({Var(c): c for c in cols})
+                    tab = tab.withColumns(*[(Add(Var(c), IntegerLit(i << 56)), c) for c in cols], header=h, params={})
+                e = ElementTable(t.kind, t.labels, tab, t.props, t.id_col, t.src_col, t.dst_col)
+                (nodes if t.kind == "node" else rels).append(e)
+        return ScanGraph(self.session, nodes, rels, validate=False)
 
     # ------------------------------------------------------------ scans
     def node_scan(self, var_name, labels=()):

@@ -54,6 +54,11 @@ def test_reference_error_case_on_gpu(gpu_session, case):
     assert type(ei.value).__name__ == exc, f"{cid} ({src}): {ei.value!r}"
 
 
+def test_union_graph_on_gpu(gpu_session):
+    from test_oracle_golden import check_union_graph
+    check_union_graph(gpu_session)
+
+
 TWO_HOP = Query([Match([NodeP("a"), NodeP("b"), NodeP("c")], [RelP("r1", "a", "b"), RelP("r2", "b", "c")])],
                 [Stage([("count", CountStar())])])
 ONE_HOP_PERSON = Query([Match([NodeP("a", ("Person",)), NodeP("b")], [RelP("r", "a", "b")])],

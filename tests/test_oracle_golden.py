@@ -28,6 +28,31 @@ def test_reference_error_case_on_oracle(case):
     assert type(ei.value).__name__ == exc, f"{cid} ({src}): {ei.value!r}"
 
 
+def union_graph_query():
+    """FTt/CAPFUnionGraphTest.scala:42-44: MATCH (n) RETURN DISTINCT id(n) over
+    testGraph1.unionAll(testGraph2) has 2 rows (both graphs' node 0, told apart
+    by the graph prefix); the names come along."""
+    from capf_amd.expr import ElementProperty, Id, Var
+    from capf_amd.planner import Match, NodeP, Query, Stage
+    n = Var("n", "NODE")
+    return (Query([Match([NodeP("n")])], [Stage([("id(n)", Id(n))], distinct=True)]),
+            Query([Match([NodeP("n")])], [Stage([("n.name", ElementProperty(n, "name"))])]))
+
+
+def check_union_graph(session):
+    g1 = ScanGraph.from_data(session, parse_create("CREATE (:Person {name: 'Mats'})"))
+    g2 = ScanGraph.from_data(session, parse_create("CREATE (:Person {name: 'Phil'})"))
+    ids, names = union_graph_query()
+    u = g1.union_all(g2)
+    got = run(u, ids)
+    assert len(got) == 2 and {r["id(n)"] for r in got} == {0, 1 << 56}
+    assert sorted(r["n.name"] for r in run(u, names)) == ["Mats", "Phil"]
+
+
+def test_union_graph_on_oracle():
+    check_union_graph(OracleSession())
+
+
 def test_create_parser_ids():
     # CreateQueryParser.scala:150-200: one counter, chain processed left-nested
     g = parse_create("CREATE (a:N)-[:R]->(b:N)-[:R]->(c:N)")

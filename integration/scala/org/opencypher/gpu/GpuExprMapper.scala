@@ -224,6 +224,10 @@ object GpuExprMapper {
         go(i); emit(ListIndex, nameIndex(physical(c).get), elem.toDouble)
       case Coalesce(xs) => xs.foreach(go); emit(Coalesce_, xs.size.toLong)
       case Id(x) => go(x)                                                  // FlinkSQLExprMapper.scala:134
+      case ToId(x) => go(x)                                                // ids are LONGs (FlinkConversions.scala:47-53)
+      // graph.unionAll's member tag (RelationalPlanner.scala:429-432): the graph
+      // index in the id's top byte, as graph.py ScanGraph.union_all does
+      case PrefixId(x, prefix) => go(x); emit(LitInt, (prefix.toLong & 0xFFL) << 56); emit(Add_)
       case Exists(x) => go(x); emit(IsNotNull_)                            // :90
       case In(lhs, rhs) =>                                                 // :114-118
         val vals = listValues(rhs).getOrElse(throw NotImplementedException(s"GPU IN over $rhs"))

@@ -49,8 +49,39 @@ def check_union_graph(session):
     assert sorted(r["n.name"] for r in run(u, names)) == ["Mats", "Phil"]
 
 
+def check_union_graph_scans(session):
+    """morpheus-testing/.../impl/UnionGraphTest.scala:48-52 (g.unionAll(g) has both copies of its node)
+    and :64-85 (a node scan over a Person graph ∪ a Book graph: each member's
+    label flags FALSE / properties NULL where the other member's table lacks
+    them, ids tagged by member; FTt/CAPFGraphTestData.scala:31-62)."""
+    from capf_amd.expr import ElementProperty, HasLabel, Var
+    from capf_amd.planner import CypherNode, Match, NodeP, Query, Stage
+    g = ScanGraph.from_data(session, parse_create("CREATE ()"))
+    n = Var("n", "NODE")
+    assert len(run(g.union_all(g), Query([Match([NodeP("n")])], [Stage([("n", n)])]))) == 2
+    person = ScanGraph.from_data(session, parse_create(
+        'CREATE (p1:Person {name: "Mats", luckyNumber: 23}) CREATE (p2:Person {name: "Martin", luckyNumber: 42}) '
+        'CREATE (p3:Person {name: "Max", luckyNumber: 1337}) CREATE (p4:Person {name: "Stefan", luckyNumber: 9})'))
+    book = ScanGraph.from_data(session, parse_create(
+        'CREATE (b1:Book {title: "1984", year: 1949}) CREATE (b2:Book {title: "Cryptonomicon", year: 1999}) '
+        'CREATE (b3:Book {title: "The Eye of the World", year: 1990}) CREATE (b4:Book {title: "The Circle", year: 2013})'))
+    cols = [("n", n), ("book", HasLabel(n, "Book")), ("person", HasLabel(n, "Person"))] + \
+        [(k, ElementProperty(n, k)) for k in ("luckyNumber", "name", "title", "year")]
+    got = run(person.union_all(book), Query([Match([NodeP("n")])], [Stage(cols)]))
+    tag = 1 << 56
+    want = [(i, False, True, lk, nm, None, None)
+            for i, (nm, lk) in enumerate([("Mats", 23), ("Martin", 42), ("Max", 1337), ("Stefan", 9)])]
+    want += [(tag + i, True, False, None, None, t, y)
+             for i, (t, y) in enumerate([("1984", 1949), ("Cryptonomicon", 1999), ("The Eye of the World", 1990),
+                                         ("The Circle", 2013)])]
+    rows = sorted((r["n"].id, r["book"], r["person"], r["luckyNumber"], r["name"], r["title"], r["year"]) for r in got)
+    assert rows == sorted(want), rows
+    assert all(isinstance(r["n"], CypherNode) for r in got)
+
+
 def test_union_graph_on_oracle():
     check_union_graph(OracleSession())
+    check_union_graph_scans(OracleSession())
 
 
 def test_create_parser_ids():

@@ -581,9 +581,11 @@ bool try_fused_count(const NodePtr &n, int64_t *out);
 // the (a-keys, reach) rows by multi-source BFS; false: not that shape.
 bool try_fused_reach(const NodePtr &grp, DataPtr &out);
 // Multi-source BFS reach (var_length_reach.hip): rows (a, #targets reachable
-// by a walk of length 1..upper) for every source reaching one.
+// by a walk of length 1..upper) for every source reaching one; include_self
+// (lower bound 0): every source, (a, a) counted once whatever its labels.
 DataPtr var_length_reach_rows(Session *s, const ColPtr &rsrc, const ColPtr &rdst, int64_t m,
-                              const ColPtr &sid, int64_t ns_in, const ColPtr &tid, int64_t nt, int upper);
+                              const ColPtr &sid, int64_t ns_in, const ColPtr &tid, int64_t nt, int upper,
+                              bool include_self = false);
 // Radix-partitioned LDS histograms of the 2-hop count (chain2_partitioned.hip).
 // cols = {start(r1), end(r1), start(r2), end(r2)}, all plain or all FOR32.
 // Histograms hold chain2_hist_len(hi − lo + 1) counters indexed by

@@ -1856,6 +1856,21 @@ bool try_fused_reach(const NodePtr &grp, DataPtr &result) {
   if (a_cols.empty()) return reach_reject("no group key column");
   std::vector<ReachBranch> brs;
   if (!union_branches(d->kids[0], tracked, brs)) return reach_reject("union branches");
+  // lower bound 0: one branch is the copyElement branch (VarLengthExpandPlanner.scala:180-205),
+  // S_a itself with b's columns copied from a's — no join below the mappings
+  int zero = -1;
+  for (size_t b = 0; b < brs.size(); ++b)
+    if (brs[b].base->kind != Kind::Join) {
+      JoinGraph g0;
+      std::vector<ColRef> r0;
+      if (collect(brs[b].base, g0, r0) && g0.leaves.size() == 1 && g0.eqs.empty()) {
+        if (zero >= 0) return reach_reject("two zero-length branches");
+        zero = (int)b;
+      }
+    }
+  const ReachBranch zbr = zero >= 0 ? brs[(size_t)zero] : ReachBranch{};
+  if (zero >= 0) brs.erase(brs.begin() + zero);
+  if (brs.empty()) return reach_reject("no var-length chain");
   std::vector<ReachShape> shapes(brs.size());
   uint64_t lengths = 0;
   for (size_t b = 0; b < brs.size(); ++b) {
@@ -1891,6 +1906,30 @@ bool try_fused_reach(const NodePtr &grp, DataPtr &result) {
     gx |= sh.roles[t].role == 0 && sh.roles[t].col == sh.x;
   }
   if (!has_x || !has_y || !gx) return reach_reject("DISTINCT / group keys lack the endpoint ids");
+  if (zero >= 0) {  // the copy branch: S_a's leaf, a's columns where the chains have a's / b's
+    JoinGraph g0;
+    std::vector<ColRef> r0;
+    if (!collect(zbr.base, g0, r0) || g0.leaves.size() != 1 || !g0.neqs.empty() || !leaf_eq(g0.leaves[0], sh.sa))
+      return reach_reject("the zero-length branch is not the source scan");
+    const bool same_scan = leaf_eq(sh.sa, sh.sb);
+    for (size_t i = 0; i < tracked.size(); ++i) {
+      const RCol &r = sh.roles[i];
+      const TCol &z = zbr.cols[i];
+      const Program *zl = z.lit;
+      ColRef zr{-1, -1};
+      if (!zl) {
+        zr = r0[(size_t)z.col];
+        if (zr.leaf == -2 && zr.col >= 0) zl = &g0.lits[(size_t)zr.col];
+      }
+      if (r.role == 2) {
+        if (!zl || !prog_eq(*zl, r.lit)) return reach_reject("zero-length branch: a literal differs");
+        continue;
+      }
+      if (zl || zr.leaf != 0) return reach_reject("zero-length branch: a column is not the source's");
+      const int want = r.role == 0 ? r.col : r.col == sh.y ? sh.x : same_scan ? r.col : -1;
+      if (want < 0 || zr.col != want) return reach_reject("zero-length branch: b's column is not a's");
+    }
+  }
   if (!column_unique(sh.sa.node, sh.x) || !column_unique(sh.sb.node, sh.y))
     return reach_reject("endpoint ids not unique");
   // rel endpoint columns: non-null INTEGER
@@ -1903,7 +1942,7 @@ bool try_fused_reach(const NodePtr &grp, DataPtr &result) {
   }
   if (lr.data->nrows >= (int64_t(1) << 32)) return reach_reject("more than 2^32 rels");
   DataPtr res = var_length_reach_rows(s, rs, rd, lr.data->nrows, xa, la.data->nrows, yb,
-                                      lb.data->nrows, upper);
+                                      lb.data->nrows, upper, zero >= 0);
   s->last_plan = "fused_var_length_reach";
   // output: group keys (a's id, other S_a columns gathered by a's row, literals)
   // then one reach column per count(*)

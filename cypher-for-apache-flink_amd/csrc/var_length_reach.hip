@@ -250,6 +250,24 @@ __global__ void k_vr_out(const int64_t *rows, int64_t n, const int64_t *src_node
   }
 }
 
+// lower bound 0 (the copyElement branch, VarLengthExpandPlanner.scala:180-205):
+// every source also pairs with itself — once, so +1 unless a walk of the
+// batch already reached the source as a target
+__global__ void k_vr_self(const unsigned long long *vis, const uint8_t *tflag, const int64_t *src_nodes,
+                          int64_t K, int64_t s0, int64_t nb, int64_t *reach) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = src_nodes[s0 + i];
+    const bool hit = tflag[p] && ((vis[p * K + (i >> 6)] >> (i & 63)) & 1ull);
+    if (!hit) reach[s0 + i] += 1;
+  }
+}
+
+__global__ void k_vr_ones(int64_t *r, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    r[i] = 1;
+}
+
 __global__ void k_vr_pos(const int64_t *reach, int64_t n, uint8_t *flag) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -385,9 +403,18 @@ struct VrCache {
 
 DataPtr var_length_reach_rows(Session *s, const ColPtr &rsrc, const ColPtr &rdst, int64_t m,
                                 const ColPtr &sid, int64_t ns_in, const ColPtr &tid, int64_t nt,
-                                int upper) {
+                                int upper, bool include_self) {
   auto out = std::make_shared<Data>();
   out->cols = {make_column(s, Type::Int64, 0, false), make_column(s, Type::Int64, 0, false)};
+  if (include_self && ns_in > 0 && (m == 0 || nt == 0)) {  // no walks: every (a, a) alone (unique ids: the caller's)
+    ColPtr a = decode_column(s, sid), r = make_column(s, Type::Int64, ns_in, false);
+    hipLaunchKernelGGL(k_vr_ones, dim3(grid_for(ns_in, 256)), dim3(256), 0, s->stream, (int64_t *)r->data->p,
+                       ns_in);
+    KERNEL_CHECK();
+    out->nrows = ns_in;
+    out->cols = {a, r};
+    return out;
+  }
   if (m == 0 || ns_in == 0 || nt == 0) return out;
   if (m >= (int64_t(1) << 32)) not_impl("var-length reach: more than 2^32 rels");
   std::shared_ptr<VrIndex> ix;
@@ -470,9 +497,16 @@ DataPtr var_length_reach_rows(Session *s, const ColPtr &rsrc, const ColPtr &rdst
                            K, s0, nb, (int64_t *)reach->p);
       }
       KERNEL_CHECK();
+      if (include_self) {
+        hipLaunchKernelGGL(k_vr_self, dim3(grid_for(nb, 256)), dim3(256), 0, s->stream,
+                           (const unsigned long long *)vis->p, (const uint8_t *)tflag->p,
+                           (const int64_t *)src_nodes->p, K, s0, nb, (int64_t *)reach->p);
+        KERNEL_CHECK();
+      }
     }
   }
-  // 5. rows (a, reach) for the sources that reach at least one target
+  // 5. rows (a, reach) for the sources that reach at least one target (every
+  // source from lower bound 0)
   BufPtr pos = s->alloc(std::max<int64_t>(ns, 1));
   hipLaunchKernelGGL(k_vr_pos, dim3(grid_for(ns, 256)), dim3(256), 0, s->stream,
                      (const int64_t *)reach->p, ns, (uint8_t *)pos->p);
@@ -514,7 +548,7 @@ extern "C" capf_status capf_var_length_reach(capf_session *cs, capf_table *rels,
     if (!cs || !rels || !src_col || !dst_col || !sources || !source_id_col || !targets ||
         !target_id_col || !out_source_col || !out_reach_col || !out)
       illegal("null argument");
-    if (lower != 1) not_impl("var-length reach: only lower bound 1 is fused");
+    if (lower != 1 && lower != 0) not_impl("var-length reach: only lower bounds 0 and 1 are fused");
     if (upper < 1 || upper > 64) illegal("var-length reach: upper bound out of range");
     if (!strcmp(out_source_col, out_reach_col)) illegal("output column names must differ");
     Session *s = &cs->impl;
@@ -523,7 +557,7 @@ extern "C" capf_status capf_var_length_reach(capf_session *cs, capf_table *rels,
     ColPtr rs = int_column_of(rels->node, dr, src_col), rd = int_column_of(rels->node, dr, dst_col);
     ColPtr si = int_column_of(sources->node, ds, source_id_col);
     ColPtr ti = int_column_of(targets->node, dt, target_id_col);
-    DataPtr d = var_length_reach_rows(s, rs, rd, dr->nrows, si, ds->nrows, ti, dt->nrows, upper);
+    DataPtr d = var_length_reach_rows(s, rs, rd, dr->nrows, si, ds->nrows, ti, dt->nrows, upper, lower == 0);
     auto n = std::make_shared<Node>();
     n->s = s;
     n->kind = Kind::Source;

@@ -462,9 +462,11 @@ capf_status capf_edge_list_read(capf_session *s, const char *path, const char *s
  * node scan `sources` and the target node scan `targets`: one row
  * (out_source_col = a's id, out_reach_col = #distinct b) per source a that
  * reaches at least one target — the rows the relational plan produces,
- * without materialising the paths.  Only lower = 1 is fused (for it, rel
- * isomorphism cannot change the distinct pairs); other bounds return
- * CAPF_ERR_NOT_IMPLEMENTED and the caller plans the join chain.            */
+ * without materialising the paths.  lower = 1 (rel isomorphism cannot change
+ * the distinct pairs) and lower = 0 (the copyElement branch,
+ * VarLengthExpandPlanner.scala:180-205: every source also pairs with itself,
+ * so every source has a row; source ids unique) are fused; other bounds
+ * return CAPF_ERR_NOT_IMPLEMENTED and the caller plans the join chain.     */
 capf_status capf_var_length_reach(capf_session *s, capf_table *rels, const char *src_col,
                                   const char *dst_col, capf_table *sources,
                                   const char *source_id_col, capf_table *targets,

@@ -14,8 +14,11 @@ import numpy as np
 import scipy.sparse as sp
 
 
-def reach_counts(src, dst, sources, targets, upper):
-    """{source id: #distinct targets reachable in 1..upper hops} (> 0 only)."""
+def reach_counts(src, dst, sources, targets, upper, lower=1):
+    """{source id: #distinct targets reachable in 1..upper hops} (> 0 only).
+    lower=0 adds the zero-length path of the copyElement branch
+    (VarLengthExpandPlanner.scala:180-205): every source also pairs with
+    itself, once, whatever its labels — so every source has an entry."""
     ids = np.unique(np.concatenate([src, dst, sources, targets]).astype(np.int64))
     ix = lambda v: np.searchsorted(ids, np.asarray(v, dtype=np.int64))  # noqa: E731
     n = len(ids)
@@ -39,6 +42,8 @@ def reach_counts(src, dst, sources, targets, upper):
     for row, node in enumerate(s):
         cols = r.indices[r.indptr[row]:r.indptr[row + 1]]
         c = int(tmask[cols].sum())
+        if lower == 0 and not (tmask[node] and node in set(cols.tolist())):
+            c += 1
         if c:
             out[int(ids[node])] = c
     return out

@@ -35,9 +35,9 @@ def synthetic(scale, person_frac=0.6, seed=5):
     return (GraphData(nodes, rels), ids[src[knows]], ids[dst[knows]], ids[person])
 
 
-def reach_query(upper, direction="out"):
+def reach_query(upper, direction="out", lower=1):
     return Query([Match([NodeP("a", ("Person",)), NodeP("b", ("Person",))],
-                        [RelP("k", "a", "b", ("KNOWS",), direction=direction, length=(1, upper))])],
+                        [RelP("k", "a", "b", ("KNOWS",), direction=direction, length=(lower, upper))])],
                  [Stage([("a", Var("a")), ("b", Var("b"))], distinct=True),
                   Stage([("a", Var("a")), ("reach", CountStar())])])
 
@@ -86,15 +86,41 @@ def test_reach_incoming_direction(gpu_session):
     assert got == oreach.reach_counts(ks, kd, persons, persons, 3)
 
 
+@pytest.mark.parametrize("upper", [1, 3])
+def test_relational_from_zero_on_oracle(upper):
+    """The relational lowering of *0..u (join chains + the copyElement branch,
+    DISTINCT, GROUP BY) on the oracle equals the matrix-power restatement with
+    the self pair: pins the lower-bound-0 semantics the fused path follows."""
+    from oracle.table_np import OracleSession
+    data, ks, kd, persons = synthetic(6)
+    got = {r["a"]: r["reach"] for r in run(ScanGraph.from_data(OracleSession(), data),
+                                           reach_query(upper, lower=0))}
+    assert got == oreach.reach_counts(ks, kd, persons, persons, upper, lower=0)
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("upper", [2, 3])
-def test_fused_equals_relational_plan(gpu_session, monkeypatch, upper):
+@pytest.mark.parametrize("upper", [1, 3])
+@pytest.mark.parametrize("compact", [False, True], ids=["int64", "for32"])
+def test_reach_from_zero_vs_matrix_powers(gpu_session, upper, compact):
+    data, ks, kd, persons = synthetic(10)
+    g = ScanGraph.from_data(gpu_session, data, compact=compact)
+    gpu_session.reset_profile()
+    got = {r["a"]: r["reach"] for r in run(g, reach_query(upper, lower=0))}
+    assert gpu_session.last_plan() == "fused_var_length_reach"
+    assert got == oreach.reach_counts(ks, kd, persons, persons, upper, lower=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lower,upper", [(1, 2), (1, 3), (0, 1), (0, 3)])
+def test_fused_equals_relational_plan(gpu_session, monkeypatch, lower, upper):
     """The fused operator and the okapi relational lowering (join chain with
     relationship-isomorphism filters, UNION ALL, DISTINCT, GROUP BY) agree
-    row for row on the GPU, self-loops and multi-edges included."""
+    row for row on the GPU, self-loops and multi-edges included; lower bound
+    0 adds the copyElement branch (VarLengthExpandPlanner.scala:180-205):
+    every source pairs with itself once."""
     data, *_ = synthetic(6)
     g = ScanGraph.from_data(gpu_session, data)
-    q = reach_query(upper)
+    q = reach_query(upper, lower=lower)
     q.stages.append(Stage([("reach", Var("reach")), ("n", CountStar())]))
     gpu_session.reset_profile()
     fused = sorted([r["reach"], r["n"]] for r in run(g, q))

@@ -552,7 +552,7 @@ Type = _unary("Type", "type({})")      # the relationship's type name (:152-160)
 
 def java_length(v):
     """Java String.length: UTF-16 code units."""
-    return len(v.encode("utf-16-le")) // 2
+    return len(v.encode("utf-16-le", "surrogatepass")) // 2
 
 
 class ExistsPattern(Expr):

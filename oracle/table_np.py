@@ -63,7 +63,7 @@ def list_values(e, params):
 
 def java_length(v):
     """java.lang.String.length(): UTF-16 code units."""
-    return len(v.encode("utf-16-le")) // 2
+    return len(v.encode("utf-16-le", "surrogatepass")) // 2
 
 
 class Col:

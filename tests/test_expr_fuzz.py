@@ -194,3 +194,63 @@ def test_random_predicates_gpu_vs_oracle(gpu_session):
         if got != want:
             bad.append((k, str(p), len(got), len(want)))
     assert not bad, f"{len(bad)} of 120 predicates differ: {bad[:4]}"
+
+
+# ------------------------------------------------- random grouped aggregates
+def groups(n=60, seed=99):
+    """(group key vars, {column: aggregator}) pairs over the fuzz table:
+    count(*), count([DISTINCT] e), sum / min / max / avg of numeric
+    expressions, collect([DISTINCT] e) (FlinkTable.scala:123-150,
+    FlinkSQLExprMapper.scala:281-287)."""
+    from capf_amd.expr import Avg, Collect, Count, CountStar, Max, Min, Sum
+    g = Gen(seed)
+    out = []
+    for _ in range(n):
+        keys = g.r.sample([Var("i"), Var("s"), Var("b")], g.r.randint(0, 2))
+        aggs = {}
+        for k in range(g.r.randint(1, 3)):
+            kind = g.r.randrange(6)
+            if kind == 0:
+                a = CountStar()
+            elif kind == 1:
+                a = Count(g.any_(2), g.r.random() < 0.4)
+            elif kind == 2:
+                a = g.pick(Sum, Min, Max)(g.int_(2))
+            elif kind == 3:
+                a = g.pick(Sum, Avg, Min, Max)(g.float_(2))
+            elif kind == 4:
+                a = Avg(g.int_(2))
+            else:
+                a = Collect(g.pick(g.int_, g.str_)(2), g.r.random() < 0.4)
+            aggs[f"a{k}"] = a
+        out.append((keys, aggs))
+    return out
+
+
+def _norm(v):
+    return sorted((repr(x) for x in v)) if isinstance(v, list) else v
+
+
+def _group_rows(session, keys, aggs):
+    t = session.table(_table_cols())
+    rows = t.group(keys, aggs, header=H, params={}).rows
+    names = [k.vname for k in keys] + list(aggs)
+    return sorted((tuple(_norm(r[c]) for c in names) for r in rows), key=repr)
+
+
+def test_group_generator_runs_on_oracle():
+    for keys, aggs in groups(20):
+        assert _group_rows(OracleSession(), keys, aggs) is not None
+
+
+@pytest.mark.gpu
+def test_random_groups_gpu_vs_oracle(gpu_session):
+    bad = []
+    for k, (keys, aggs) in enumerate(groups()):
+        want = _group_rows(OracleSession(), keys, aggs)
+        got = _group_rows(gpu_session, keys, aggs)
+        ok = len(got) == len(want) and all(len(x) == len(y) and all(_same(a, b) or a == b for a, b in zip(x, y))
+                                           for x, y in zip(got, want))
+        if not ok:
+            bad.append((k, [str(v) for v in keys], {c: str(a) for c, a in aggs.items()}, got[:2], want[:2]))
+    assert not bad, f"{len(bad)} of 60 groupings differ: {bad[:3]}"

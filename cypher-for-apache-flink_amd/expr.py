@@ -644,6 +644,7 @@ _BIN_OPS = {
     "Divide": OP_DIV, "Modulo": OP_MOD,
 }
 _ORDERED = ("LessThan", "LessThanOrEqual", "GreaterThan", "GreaterThanOrEqual")
+_CMP_NAMES = ("Equals",) + _ORDERED
 _UN_OPS = {"Not": OP_NOT, "IsNull": OP_IS_NULL, "IsNotNull": OP_IS_NOT_NULL, "ToFloat": OP_TO_FLOAT,
            "ToInteger": OP_TO_INTEGER, "Negate": OP_NEG, "Exists": OP_IS_NOT_NULL,
            "Round": OP_ROUND, "Abs": OP_ABS, "Ceil": OP_CEIL, "Floor": OP_FLOOR, "Sign": OP_SIGN,
@@ -973,10 +974,28 @@ def _compile_program(expr, header, columns, params=None, intern=None, coltype=No
             return T_BOOL
         if type(e).__name__ in _STR_FUNCS or isinstance(e, (Substring, Replace, ToString)):
             return T_STRING
-        if type(e).__name__ == "Add":
+        name = type(e).__name__
+        if name in ("Add", "Subtract", "Multiply", "Divide", "Modulo"):
             ta, tb = static_type(e.lhs), static_type(e.rhs)
-            if T_STRING in (ta, tb):
+            if name == "Add" and T_STRING in (ta, tb):
                 return T_STRING
+            if ta in (T_INT, T_FLOAT) and tb in (T_INT, T_FLOAT):
+                return T_FLOAT if T_FLOAT in (ta, tb) else T_INT
+            return None
+        if name in ("Negate", "Abs", "Ceil", "Floor", "Sign"):
+            t = static_type(e.expr)
+            return t if t in (T_INT, T_FLOAT) else None
+        if name in _CMP_NAMES or isinstance(e, (Ands, Ors, In)) or name in ("Not", "IsNull", "IsNotNull", "Exists"):
+            return T_BOOL
+        if isinstance(e, (Coalesce, CaseExpr)):  # the branches' common type (INTEGER and FLOAT: FLOAT)
+            parts = list(e.exprs) if isinstance(e, Coalesce) else \
+                [v for _, v in e.alternatives] + ([e.default] if e.default is not None else [])
+            ts = {static_type(x) for x in parts} - {T_NULL}
+            if None in ts or not ts:
+                return None if None in ts else T_NULL
+            if ts == {T_INT, T_FLOAT}:
+                return T_FLOAT
+            return ts.pop() if len(ts) == 1 else None
         return None
 
     def literal_value(x):

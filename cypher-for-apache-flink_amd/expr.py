@@ -1036,10 +1036,20 @@ def _compile_program(expr, header, columns, params=None, intern=None, coltype=No
         if t == T_NULL:
             emit(OP_LIT_NULL, T_STRING)
             return
-        if t != T_STRING or smap is None:
+        if t != T_STRING or (smap is None and vmap is None):
             not_impl(x)
         go(x)
-        emit(OP_STR_MAP, name_of(smap(key)))
+        nm = smap(key) if smap is not None else None
+        if nm is not None:  # a code map of the whole (small) dictionary
+            emit(OP_STR_MAP, name_of(nm))
+        elif vmap is not None:
+            # f over the operand's DISTINCT values in this table (a value map):
+            # a code map over a large dictionary would apply f to every string
+            # and intern every result, and each such map grows the dictionary
+            # the next one must cover
+            emit(OP_VALUE_MAP, name_of(vmap(("fn", key), (x,))), 0.0)
+        else:
+            not_impl(x)
 
     def not_impl(what):
         from ._lib import NotImplementedException

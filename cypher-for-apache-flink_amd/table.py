@@ -60,6 +60,8 @@ class GpuSession:
         cnt, dig = c_int64(), c_uint64()
         _lib.call("capf_string_digest", self._h, byref(cnt), byref(dig))
         n = cnt.value
+        if n > CODE_MAP_MAX:  # None: the caller maps the operand's distinct values instead
+            return None
         ent = self._maps.get(key)
         if ent is not None and ent[0] >= n:
             return ent[2]
@@ -252,6 +254,10 @@ class GpuSession:
 # distinct operand values (pairs) a value map may hold (toString of a number
 # column, concatenation of two columns): each becomes a host-built string
 VALUE_MAP_MAX = 1 << 22
+# a string function runs over the whole dictionary (a code map) only while the
+# dictionary holds at most this many strings; beyond, over the distinct values
+# of its operand in the table (a value map)
+CODE_MAP_MAX = 1 << 16
 
 # encoded argument arrays of select() per column tuple (scans and renames
 # repeat the same selections every query)
@@ -585,6 +591,11 @@ class GpuTable:
             if isinstance(kind, tuple) and kind[0] == "regex":  # s =~ pattern, then cast to BOOLEAN
                 import re
                 txt = "true" if re.fullmatch(kind[1], vals[0]) else "false"
+            elif isinstance(kind, tuple) and kind[0] == "fn":  # a string function (expr.string_fn)
+                from .expr import string_fn
+                txt = string_fn(kind[1], vals[0])
+                if txt is None:  # (no entry: the lookup misses, NULL)
+                    continue
             else:
                 txt = "".join(cypher_to_string(float(v) if ty == T_FLOAT else v) for v, ty in zip(vals, types))
             entries.append((tuple(key(v, ty) for v, ty in zip(vals, types)), self.session.intern(txt)))

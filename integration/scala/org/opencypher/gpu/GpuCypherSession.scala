@@ -62,10 +62,11 @@ final class GpuCypherSession private (val device: Int, hipStream: Long)
     * with the JVM's own String semantics, the results interned; extended and
     * re-registered when the dictionary has grown since (the shim's twin of
     * table.py GpuSession.string_map). */
-  def stringMap(key: Seq[Any]): String = maps.synchronized {
+  def stringMap(key: Seq[Any]): Option[String] = maps.synchronized {
     val n = { val d = new Array[Long](2); Native.guard(Native.stringDigest(handle, d)); d(0) }
+    if (n > GpuCypherSession.CodeMapMax) return None  // a large dictionary: the caller's value map
     maps.get(key) match {
-      case Some((m, _, name)) if m >= n => name
+      case Some((m, _, name)) if m >= n => Some(name)
       case prev =>
         val old = prev.map(_._2).getOrElse(Array.empty[Long])
         val codes = old ++ (old.length.toLong until n).map { c =>
@@ -73,7 +74,7 @@ final class GpuCypherSession private (val device: Int, hipStream: Long)
         }
         val name = "\u0001map:" + Native.sessionCodeMap(handle, codes)
         maps.update(key, (n, codes, name))
-        name
+        Some(name)
     }
   }
 
@@ -104,6 +105,10 @@ final class GpuCypherSession private (val device: Int, hipStream: Long)
 }
 
 object GpuCypherSession {
+
+  /** String functions run over the whole dictionary (a code map) only while it
+    * holds at most this many strings (table.py CODE_MAP_MAX). */
+  final val CodeMapMax: Long = 1L << 16
 
   /** A session on one GPU (CAPFSession.local(), CAPFSession.scala:79): device 0
     * by default, the backend's own stream. */

@@ -119,7 +119,7 @@ object GpuExprMapper {
     // CAPF_OP_VALUE_MAP of the operands' distinct values (pairs) over this table: the
     // JVM's casts (Long.toString / Double.toString) of each, concatenated, interned
     // (the shim's twin of table.py GpuTable._value_map)
-    def valueMap(xs: Seq[Expr], regex: Option[String] = None): String = {
+    def valueMap(xs: Seq[Expr], regex: Option[String] = None, fn: Option[Seq[Any]] = None): String = {
       val names = xs.indices.map(i => s"\u0002vm$i")
       val t = table.withColumns(xs.zip(names): _*)(header, parameters).distinct(names: _*)
       if (t.size > (1L << 22))  // every distinct value becomes a host string (table.py VALUE_MAP_MAX)
@@ -131,10 +131,13 @@ object GpuExprMapper {
         case other => throw NotImplementedException(s"GPU string of $other")
       }
       val entries = t.rows.map(row => names.map(row)).filterNot(_.contains(CypherNull))
-        .map(vs => (vs.map(key), session.intern(regex match {
-          case Some(p) => if (GpuStringFunctions.cast(vs.head).matches(p)) "true" else "false"  // s =~ p
-          case None => vs.map(GpuStringFunctions.cast).mkString
-        })))
+        .flatMap(vs => (fn match {
+          case Some(k) => GpuStringFunctions(k, GpuStringFunctions.cast(vs.head))  // f(s); None: NULL
+          case None => Some(regex match {
+            case Some(p) => if (GpuStringFunctions.cast(vs.head).matches(p)) "true" else "false"  // s =~ p
+            case None => vs.map(GpuStringFunctions.cast).mkString
+          })
+        }).map(txt => (vs.map(key), session.intern(txt))))
         .toSeq.sortWith { case ((a, _), (b, _)) => (a zip b).find(p => p._1 != p._2).exists(p => p._1 < p._2) }
       val id = Native.guard(Native.sessionValueMap(session.handle, entries.map(_._1.head).toArray,
         if (xs.size > 1) entries.map(_._1(1)).toArray else null, entries.map(_._2).toArray))
@@ -147,7 +150,13 @@ object GpuExprMapper {
       case Some(CypherString(v)) => lit(GpuStringFunctions(key, v).map(CypherString(_)).getOrElse(CypherNull))
       case Some(other) => throw NotImplementedException(s"GPU string function of $other")
       case None if x.cypherType.material == CTNull => emit(LitNull, Native.TypeString)
-      case None => go(x); emit(StrMap, nameIndex(session.stringMap(key)))
+      case None =>
+        go(x)
+        session.stringMap(key) match {  // a code map while the dictionary is small,
+          case Some(name) => emit(StrMap, nameIndex(name))
+          // else f over the operand's distinct values here (table.py CODE_MAP_MAX)
+          case None => emit(ValueMap, nameIndex(valueMap(Seq(x), fn = Some(key))), 0.0)
+        }
     }
 
     // <, <=, >, >= (FlinkSQLExprMapper.scala:91-94): STRINGs compare by their

@@ -251,3 +251,23 @@ def test_order_by_string_gpu_parity(gpu_session, desc):
     g, o = gpu_session.table(more), OracleSession().table(more)
     keys = [(Var("s"), d)]
     assert g.orderBy(*keys, header=OH).rows == o.orderBy(*keys, header=OH).rows
+
+
+@pytest.mark.gpu
+def test_string_functions_over_distinct_values(gpu_session, monkeypatch):
+    """Past CODE_MAP_MAX dictionary strings a string function maps the distinct
+    values of its operand in the table (a value map) instead of the whole
+    dictionary — a code map over a large dictionary interns a result per
+    string and grows the dictionary the next map must cover.  Same rows as the
+    oracle either way."""
+    import capf_amd.table as tb
+    monkeypatch.setattr(tb, "CODE_MAP_MAX", 0)
+    cols = _cols()
+    bad = []
+    for e in EXPRS:
+        g, o = gpu_session.table(cols), OracleSession().table(cols)
+        rg = g.withColumns((e, "x"), header=H, params={"p": "param"}).rows
+        ro = o.withColumns((e, "x"), header=H, params={"p": "param"}).rows
+        if [r["x"] for r in rg] != [r["x"] for r in ro]:
+            bad.append(str(e))
+    assert not bad, bad

@@ -102,8 +102,13 @@ def test_pattern_generator_runs_on_oracle():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("compact", [False, 3], ids=["int64", "for24"])
-def test_random_patterns_gpu_vs_oracle(gpu_session, compact):
+@pytest.mark.parametrize("compact,join", [(False, None), (3, None), (True, "radix")],
+                         ids=["int64", "for24", "for32-radix"])
+def test_random_patterns_gpu_vs_oracle(gpu_session, monkeypatch, compact, join):
+    """(for32-radix: every join through the radix-partitioned path, which the
+    planner otherwise keeps for large inputs.)"""
+    if join:
+        monkeypatch.setenv("CAPF_JOIN", join)
     bad = []
     for gs, qs in CASES:
         g, q = graph(gs), query(qs)

@@ -167,3 +167,50 @@ def test_sharded_two_hop_through_spi(world):
         assert got == want and got_back == want, (rank, got, got_back, want)
         assert dispatched == 2, dispatched  # both chains took the sharded count
         assert rows_ok and one == m and three_ok
+
+
+def _fuzz_worker(rank, world, port, q):
+    try:
+        sys.path[:0] = [ROOT, HERE, os.path.join(HERE, "golden")]
+        import capf_import  # noqa: F401
+        from conftest import bag
+        from dist_support import OracleExchange
+        from test_pattern_fuzz import CASES, graph, query
+
+        from capf_amd.dist_table import DistSession, dist_scan_graph
+        from capf_amd.graph import ScanGraph
+        from capf_amd.planner import run
+        from oracle.table_np import OracleSession
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        ds = DistSession(OracleSession(), OracleExchange())
+        bad = []
+        for gs, qs in CASES[::3]:
+            g, qy = graph(gs), query(qs)
+            want = run(ScanGraph.from_data(OracleSession(), g), qy)
+            try:
+                got = run(dist_scan_graph(ds, ScanGraph.from_data(OracleSession(), g)), qy)
+                if bag(got) != bag(want):
+                    bad.append((gs, qs, len(got), len(want)))
+            except Exception as e:  # noqa: BLE001 - reported per case
+                bad.append((gs, qs, repr(e)[:200]))
+        q.put((rank, bad))
+        dist.destroy_process_group()
+    except Exception:  # noqa: BLE001
+        q.put((rank, [("worker", traceback.format_exc())]))
+
+
+def test_random_patterns_distributed_on_oracle():
+    """The 100 seeded pattern cases of tests/test_pattern_fuzz.py (every third)
+    over 2 DistTable ranks: the same bags as one session."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fuzz_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, bad in res:
+        assert not bad, f"rank {rank}: {len(bad)} failing cases: {bad[:4]}"

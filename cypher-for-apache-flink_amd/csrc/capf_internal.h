@@ -274,6 +274,7 @@ enum class Kind {
 struct AggSpec {
   int32_t kind;
   bool distinct;
+  bool rank_to_code = false;  // min / max of STRINGs: aggregated as ranks, mapped back to codes
   double param = 0;  // percentile fraction (CAPF_AGG_PERCENTILE_*)
   Program arg;  // empty for COUNT_STAR
   std::string name;
@@ -398,8 +399,8 @@ struct Session {
   // 1 true, 2 neither (NULL)
   BufPtr d_str_bool;
   size_t d_str_bool_n = 0;
-  // device table of the strings' sort ranks (CAPF_OP_STR_RANK)
-  BufPtr d_str_rank;
+  // device table of the strings' sort ranks (CAPF_OP_STR_RANK) and its inverse
+  BufPtr d_str_rank, d_str_order;
   size_t d_str_rank_n = 0;
   // device table of the strings as numbers (CAPF_OP_STR_TO_NUM)
   BufPtr d_str_num;
@@ -568,6 +569,10 @@ const uint8_t *string_bool_table(Session *s, size_t *n);
 // Device table of each string's rank in UTF-16 code-unit order
 // (CAPF_OP_STR_RANK, Java String.compareTo); *n = strings covered.
 const int64_t *string_rank_table(Session *s, size_t *n);
+// Its inverse: the code of the string of each rank.
+const int64_t *string_order_table(Session *s, size_t *n);
+// STRING column of the codes of an INTEGER column of ranks (NULLs kept).
+ColPtr ranks_to_codes(Session *s, const ColPtr &ranks);
 // Device table of the session's strings parsed as numbers (CAPF_OP_STR_TO_NUM):
 // [double n][int64 n][uint8 flags n] (bit 0: a DOUBLE, bit 1: an INTEGER).
 const void *string_num_table(Session *s, size_t *n);

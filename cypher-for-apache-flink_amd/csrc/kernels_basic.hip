@@ -584,6 +584,30 @@ static ColPtr concat_lists(Session *s, const ColPtr &a, const ColPtr &b) {
   return o;
 }
 
+__global__ void k_rank_codes(ColView r, const int64_t *order, int64_t n, int64_t *out, uint8_t *ok) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const bool v = r.type != CAPF_TYPE_NULL && r.data && !(r.valid && !r.valid[i]);
+    out[i] = v ? order[ld_int(r, i)] : 0;
+    ok[i] = v ? 1 : 0;
+  }
+}
+
+ColPtr ranks_to_codes(Session *s, const ColPtr &ranks) {
+  force(ranks);
+  size_t ns = 0;
+  const int64_t *order = string_order_table(s, &ns);
+  const int64_t n = ranks->n;
+  ColPtr o = make_column(s, Type::String, n, true);
+  if (n > 0) {
+    const ColView v = ranks->type == Type::Null ? ColView{nullptr, nullptr, CAPF_TYPE_NULL, ENC_PLAIN, 0}
+                                                : view_of(ranks);
+    hipLaunchKernelGGL(k_rank_codes, dim3(grid_for(n, 256)), dim3(256), 0, s->stream, v, order, n,
+                       (int64_t *)o->data->p, (uint8_t *)o->valid->p);
+    KERNEL_CHECK();
+  }
+  return o;
+}
+
 ColPtr concat_columns(Session *s, const ColPtr &a, const ColPtr &b, Type t) {
   force(a);
   force(b);

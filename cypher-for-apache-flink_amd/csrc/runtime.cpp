@@ -642,6 +642,10 @@ static DataPtr materialize_impl(const NodePtr &n) {
           out->cols.push_back(aggregate(s, g2, *c, dg.ngroups, a.kind, darg, a.out_type));
           continue;
         }
+        if (a.rank_to_code) {  // min / max of STRINGs: over their ranks, back to codes
+          out->cols.push_back(ranks_to_codes(s, aggregate(s, g, *c, c->nrows, a.kind, arg, Type::Int64)));
+          continue;
+        }
         out->cols.push_back(aggregate(s, g, *c, c->nrows, a.kind, arg, a.out_type, a.param));
       }
       return out;
@@ -870,11 +874,20 @@ const int64_t *string_rank_table(Session *s, size_t *n) {
     for (size_t r = 0; r < m; ++r) rank[(size_t)order[r]] = (int64_t)r;
     s->d_str_rank = s->alloc(8 * rank.size());
     HIP_CHECK(hipMemcpyAsync(s->d_str_rank->p, rank.data(), 8 * rank.size(), hipMemcpyHostToDevice, s->stream));
-    s->sync();  // the pageable source
+    if (order.empty()) order.push_back(0);
+    s->d_str_order = s->alloc(8 * order.size());
+    HIP_CHECK(hipMemcpyAsync(s->d_str_order->p, order.data(), 8 * order.size(), hipMemcpyHostToDevice, s->stream));
+    s->sync();  // the pageable sources
     s->d_str_rank_n = m;
   }
   *n = s->d_str_rank_n;
   return (const int64_t *)s->d_str_rank->p;
+}
+
+const int64_t *string_order_table(Session *s, size_t *n) {
+  string_rank_table(s, n);
+  std::lock_guard<std::mutex> lk(s->str_mu);
+  return (const int64_t *)s->d_str_order->p;
 }
 
 const void *string_num_table(Session *s, size_t *n) {
@@ -2076,7 +2089,10 @@ capf_status capf_table_group_ex(capf_table *t, int32_t n_by, const char *const *
           break;
         case CAPF_AGG_MIN:
         case CAPF_AGG_MAX:
-          if (at == Type::String) not_impl("min/max of strings");
+          if (at == Type::String) {  // String.compareTo order: aggregate the ranks
+            a.arg.code.push_back(Instr{OP_STR_RANK, 0, 0, 0.0});
+            a.rank_to_code = true;
+          }
           a.out_type = at;
           break;
         case CAPF_AGG_COLLECT: a.out_type = Type::List; break;

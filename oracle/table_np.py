@@ -980,6 +980,13 @@ class OracleTable:
                 if r is not None:
                     arr[g] = r
             return Col(out_t, arr, np.array([r is not None for r in res], bool))
+        if v.t == T_STRING and agg.kind in (AGG_MIN, AGG_MAX):  # String.compareTo order
+            best = [None] * ng
+            for g, x, ok in zip(gid.tolist(), v.v.tolist(), sel.tolist()):
+                if ok and (best[g] is None or (_jcmp(x, best[g]) < 0) == (agg.kind == AGG_MIN)
+                           and _jcmp(x, best[g]) != 0):
+                    best[g] = x
+            return Col(T_STRING, np.array(best, dtype=object), np.array([b is not None for b in best], bool))
         if v.t == T_STRING and agg.kind != AGG_COUNT:
             raise NotImplementedError("aggregate of strings")
         cnt = np.bincount(gid[sel], minlength=ng)

@@ -200,7 +200,7 @@ def test_random_predicates_gpu_vs_oracle(gpu_session):
 def groups(n=60, seed=99):
     """(group key vars, {column: aggregator}) pairs over the fuzz table:
     count(*), count([DISTINCT] e), sum / min / max / avg of numeric
-    expressions, collect([DISTINCT] e) (FlinkTable.scala:123-150,
+    expressions, min / max of strings, collect([DISTINCT] e) (FlinkTable.scala:123-150,
     FlinkSQLExprMapper.scala:281-287)."""
     from capf_amd.expr import Avg, Collect, Count, CountStar, Max, Min, Sum
     g = Gen(seed)
@@ -209,7 +209,7 @@ def groups(n=60, seed=99):
         keys = g.r.sample([Var("i"), Var("s"), Var("b")], g.r.randint(0, 2))
         aggs = {}
         for k in range(g.r.randint(1, 3)):
-            kind = g.r.randrange(6)
+            kind = g.r.randrange(7)
             if kind == 0:
                 a = CountStar()
             elif kind == 1:
@@ -220,8 +220,10 @@ def groups(n=60, seed=99):
                 a = g.pick(Sum, Avg, Min, Max)(g.float_(2))
             elif kind == 4:
                 a = Avg(g.int_(2))
-            else:
+            elif kind == 5:
                 a = Collect(g.pick(g.int_, g.str_)(2), g.r.random() < 0.4)
+            else:  # String.compareTo order (CAPF_OP_STR_RANK, ranks mapped back to codes)
+                a = g.pick(Min, Max)(g.str_(2))
             aggs[f"a{k}"] = a
         out.append((keys, aggs))
     return out

@@ -623,9 +623,10 @@ static DataPtr materialize_impl(const NodePtr &n) {
           out->cols.push_back(collect_lists(s, g, c->nrows, arg, a.distinct));
           continue;
         }
-        if (a.distinct && a.kind == CAPF_AGG_COUNT && c->nrows > 0) {
-          // count(DISTINCT e): Spark semantics (SparkSQLExprMapper.scala:427-429);
-          // Flink ignores the flag (FlinkSQLExprMapper.scala:282), see DESIGN.md.
+        if (a.distinct && c->nrows > 0) {
+          // agg(DISTINCT e) over the distinct (group, value) pairs: Spark semantics
+          // (SparkSQLExprMapper.scala:427-429); Flink ignores the flag
+          // (FlinkSQLExprMapper.scala:281-287), see DESIGN.md.
           auto gid = std::make_shared<Column>();
           gid->type = Type::Int64;
           gid->n = c->nrows;
@@ -639,7 +640,10 @@ static DataPtr materialize_impl(const NodePtr &n) {
           g2.ngroups = g.ngroups;
           g2.group_of_row = gather_column(s, gid, reps, dg.ngroups)->data;
           ColPtr darg = gather_column(s, arg, reps, dg.ngroups);
-          out->cols.push_back(aggregate(s, g2, *c, dg.ngroups, a.kind, darg, a.out_type));
+          if (a.rank_to_code)
+            out->cols.push_back(ranks_to_codes(s, aggregate(s, g2, *c, dg.ngroups, a.kind, darg, Type::Int64)));
+          else
+            out->cols.push_back(aggregate(s, g2, *c, dg.ngroups, a.kind, darg, a.out_type, a.param));
           continue;
         }
         if (a.rank_to_code) {  // min / max of STRINGs: over their ranks, back to codes
@@ -2072,8 +2076,6 @@ capf_status capf_table_group_ex(capf_table *t, int32_t n_by, const char *const *
     } else {
       a.arg = Program::from_c(&agg_args[i]);
       Type at = infer_type(a.arg, c->names, c->types);
-      if (a.distinct && a.kind != CAPF_AGG_COUNT && a.kind != CAPF_AGG_COLLECT)
-        not_impl("DISTINCT modifier on aggregator other than count / collect");
       if (at == Type::List) not_impl("aggregation of list values");
       switch (a.kind) {
         case CAPF_AGG_COUNT: a.out_type = Type::Int64; break;

@@ -1330,3 +1330,28 @@ def test_in_long_list_set_lookup(case):
     prog = compile_program(pred, h, set(g.physicalColumns), params, g.session.intern, g.capf_type,
                            g.session.literal_set)
     assert (OP_IN_SET in prog[0]) == (case != "short")
+
+
+def test_distinct_flag_on_every_aggregator(gpu_session):
+    """capf_table_group_ex honours the DISTINCT flag of every aggregator (the
+    okapi IR carries it on count / collect only, Expr.scala:1077, 1136; the
+    C-ABI takes one per aggregation): sum / avg / min / max over the distinct
+    (group, value) pairs."""
+    from dataclasses import dataclass
+    from capf_amd.expr import Avg, Max, Min, Sum, T_INT, Var
+    from capf_amd.header import RecordHeader
+
+    def distinct(cls):
+        @dataclass(frozen=True)
+        class D(cls):
+            distinct = True
+        return D
+
+    k = [0, 0, 0, 1, 1, 1, 1, 2]
+    v = [5, 5, 7, 1, 1, None, 3, 4]
+    t = gpu_session.table([("k", T_INT, k, None), ("v", T_INT, v, None)])
+    h = RecordHeader({Var("k"): "k", Var("v"): "v"})
+    aggs = {"s": distinct(Sum)(Var("v")), "a": distinct(Avg)(Var("v")), "lo": distinct(Min)(Var("v")),
+            "hi": distinct(Max)(Var("v"))}
+    rows = sorted((r["k"], r["s"], r["a"], r["lo"], r["hi"]) for r in t.group([Var("k")], aggs, header=h, params={}).rows)
+    assert rows == [(0, 12, 6.0, 5, 7), (1, 4, 2.0, 1, 3), (2, 4, 4.0, 4, 4)]

@@ -64,8 +64,8 @@ final class GpuCypherSession private (val device: Int, hipStream: Long)
     * table.py GpuSession.string_map). */
   def stringMap(key: Seq[Any]): Option[String] = maps.synchronized {
     val n = { val d = new Array[Long](2); Native.guard(Native.stringDigest(handle, d)); d(0) }
-    if (n > GpuCypherSession.CodeMapMax) return None  // a large dictionary: the caller's value map
-    maps.get(key) match {
+    if (n > GpuCypherSession.CodeMapMax) None  // a large dictionary: the caller's value map
+    else maps.get(key) match {
       case Some((m, _, name)) if m >= n => Some(name)
       case prev =>
         val old = prev.map(_._2).getOrElse(Array.empty[Long])

@@ -145,3 +145,21 @@ def test_fixture_matches_reference():
     import make_okapi_api
     with open(FIXTURE) as f:
         assert make_okapi_api.build(REFERENCE) == json.load(f)
+
+
+def test_fs_graph_source_twin_matches_python_layout():
+    """GpuFSGraphSource.scala reads and writes the files capf_amd/fs_source.py
+    does: same file / directory names, canonical key columns, GPU LONG parser
+    for all-INTEGER tables, okapi's own schema JSON and name encoding."""
+    from capf_amd import fs_source as fs
+    text = sc.strip_comments(sc.integration_sources()["GpuFSGraphSource.scala"])
+    for const, value in [("SchemaFile", fs.SCHEMA_FILE), ("MetaDataFile", fs.META_FILE),
+                         ("NodesDir", fs.NODES_DIR), ("RelsDir", fs.RELS_DIR),
+                         ("IdKey", "id"), ("SourceKey", "source"), ("TargetKey", "target")]:
+        assert f'val {const} = "{value}"' in text, const
+    assert "Native.csvReadLongs(" in text and "gpu.fromHost(" in text
+    assert "PropertyGraphSchema.fromJson(" in text and "schema.toJson" in text
+    assert "encodeSpecialCharacters" in text and "toPropertyColumnName" in text
+    parents, over = sc.classes(text)["GpuFSGraphSource"]
+    assert "PropertyGraphDataSource" in parents
+    assert {"hasGraph", "graph", "schema", "store", "delete", "graphNames"} <= set(over)

@@ -170,6 +170,7 @@ _SIGS = {
     "capf_session_copy": (c_int32, [_S, c_void_p, c_void_p, c_int64, c_int32]),
     "capf_session_literal_set": (c_int32, [_S, POINTER(c_int64), c_int64, POINTER(c_int32)]),
     "capf_session_code_map": (c_int32, [_S, POINTER(c_int64), c_int64, POINTER(c_int32)]),
+    "capf_session_code_map_extend": (c_int32, [_S, c_int32, POINTER(c_int64), c_int64, POINTER(c_int32)]),
     "capf_table_add_list": (c_int32, [_T, c_char_p, c_int32, c_void_p, c_void_p, c_void_p, _PT]),
     "capf_table_name_list": (c_int32, [_T, c_int32, _STRS, POINTER(c_int32), POINTER(c_int64), c_char_p, _PT]),
     "capf_table_list_columns": (c_int32, [_T, c_int32, _STRS, c_char_p, _PT]),

@@ -367,6 +367,7 @@ struct Session {
   std::vector<std::pair<std::shared_ptr<DevBuf>, int64_t>> literal_sets;
   // code maps of CAPF_OP_STR_MAP: int64 STRING code per dictionary code (−1 NULL)
   std::vector<std::pair<std::shared_ptr<DevBuf>, int64_t>> code_maps;
+  std::vector<int32_t> code_map_refs;  // registrations naming each map (extend in place at 1)
   // value maps of CAPF_OP_VALUE_MAP: [keys n][keys2 n (pairs)][codes n] on the
   // device, n, pair flag
   struct ValueMap {

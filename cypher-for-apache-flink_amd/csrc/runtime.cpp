@@ -1100,6 +1100,7 @@ capf_status capf_session_code_map(capf_session *cs, const int64_t *codes, int64_
     auto it = s.code_map_ids.find(key);
     if (it != s.code_map_ids.end()) {
       *map_id = it->second;
+      ++s.code_map_refs[(size_t)it->second];
       return CAPF_OK;
     }
   }
@@ -1107,9 +1108,57 @@ capf_status capf_session_code_map(capf_session *cs, const int64_t *codes, int64_
   if (n > 0) HIP_CHECK(hipMemcpyAsync(b->p, codes, 8 * n, hipMemcpyHostToDevice, s.stream));
   s.sync();  // (pageable source)
   std::lock_guard<std::mutex> g(s.user_mu);
+  auto it = s.code_map_ids.find(key);  // registered meanwhile by another thread
+  if (it != s.code_map_ids.end()) {
+    *map_id = it->second;
+    ++s.code_map_refs[(size_t)it->second];
+    return CAPF_OK;
+  }
   *map_id = (int32_t)s.code_maps.size();
   s.code_maps.emplace_back(b, n);
+  s.code_map_refs.push_back(1);
   s.code_map_ids.emplace(std::move(key), *map_id);
+  CAPF_API_END
+}
+
+capf_status capf_session_code_map_extend(capf_session *cs, int32_t map_id, const int64_t *codes, int64_t n,
+                                         int32_t *new_id) {
+  CAPF_API_BEGIN
+  need(cs, "session");
+  need(new_id, "new_id");
+  if (n < 0 || (n > 0 && !codes)) illegal("bad code map");
+  Session &s = cs->impl;
+  std::vector<int64_t> key(codes, codes + n);
+  bool in_place;
+  {
+    std::lock_guard<std::mutex> g(s.user_mu);
+    if (map_id < 0 || (size_t)map_id >= s.code_maps.size()) illegal("unknown code map");
+    const int64_t old_n = s.code_maps[(size_t)map_id].second;
+    if (n < old_n) illegal("a code map only grows");
+    auto old = std::find_if(s.code_map_ids.begin(), s.code_map_ids.end(),
+                            [&](const std::pair<const std::vector<int64_t>, int32_t> &e) { return e.second == map_id; });
+    if (old == s.code_map_ids.end() || !std::equal(old->first.begin(), old->first.end(), key.begin()))
+      illegal("the extended code map must start with the map's codes");
+    // shared by several registrations (equal maps of different functions), or
+    // the longer map exists already: a map of its own, the old one untouched
+    in_place = s.code_map_refs[(size_t)map_id] == 1 && !s.code_map_ids.count(key);
+    if (!in_place) --s.code_map_refs[(size_t)map_id];
+  }
+  if (!in_place) return capf_session_code_map(cs, codes, n, new_id);
+  BufPtr b = s.alloc(8 * std::max<int64_t>(n, 1));
+  if (n > 0) HIP_CHECK(hipMemcpyAsync(b->p, codes, 8 * n, hipMemcpyHostToDevice, s.stream));
+  s.sync();  // (pageable source)
+  std::lock_guard<std::mutex> g(s.user_mu);
+  for (auto it = s.code_map_ids.begin(); it != s.code_map_ids.end(); ++it)
+    if (it->second == map_id) {
+      s.code_map_ids.erase(it);
+      break;
+    }
+  // the old table returns to the stream-ordered cache: launches already
+  // enqueued keep reading it; programs naming map_id read the superset from now on
+  s.code_maps[(size_t)map_id] = std::make_pair(b, n);
+  s.code_map_ids.emplace(std::move(key), map_id);
+  *new_id = map_id;
   CAPF_API_END
 }
 
@@ -1756,6 +1805,72 @@ capf_status capf_table_download(capf_table *t, const char *col, void *values_out
   CAPF_API_END
 }
 
+// Element type of LIST column i of plan node n, read off the plan without
+// running it (UNWIND and list_info used to materialise the child
+// while the plan was being built).  False when the plan does not say — a
+// computed list expression or a source without data — and the caller then
+// materialises.  Mirrors what materialize_impl produces column by column.
+static bool static_list_elem(const NodePtr &n, int i, Type &et, int depth = 0) {
+  if (depth > 256 || i < 0 || i >= (int)n->types.size()) return false;
+  if (n->types[(size_t)i] == Type::Null) {  // a NULL column concatenated with a list adds no elements
+    et = Type::Null;
+    return true;
+  }
+  if (n->types[(size_t)i] != Type::List) return false;
+  {
+    std::lock_guard<std::mutex> g(n->mu);
+    if (n->result) {
+      const ColPtr &c = n->result->cols[(size_t)i];
+      et = c->child ? c->child->type : Type::Null;
+      return true;
+    }
+  }
+  const int nk = n->kids.empty() ? 0 : (int)n->kids[0]->names.size();
+  switch (n->kind) {
+    case Kind::Source: return false;
+    case Kind::Select: return static_list_elem(n->kids[0], n->sel_index[(size_t)i], et, depth + 1);
+    case Kind::Filter:
+    case Kind::Distinct:
+    case Kind::OrderBy:
+    case Kind::Skip:
+    case Kind::Limit: return static_list_elem(n->kids[0], i, et, depth + 1);
+    case Kind::Join:
+      return i < nk ? static_list_elem(n->kids[0], i, et, depth + 1)
+                    : static_list_elem(n->kids[1], i - nk, et, depth + 1);
+    case Kind::Union: {  // concat_lists: the non-NULL side's element type, equal types otherwise
+      Type a, b;
+      if (!static_list_elem(n->kids[0], i, a, depth + 1) ||
+          !static_list_elem(n->kids[1], n->kids[1]->col_index(n->names[(size_t)i]), b, depth + 1))
+        return false;
+      if (a != Type::Null && b != Type::Null && a != b) return false;  // the union reports the mismatch
+      et = a == Type::Null ? b : a;
+      return true;
+    }
+    case Kind::Group: {
+      const int nkey = (int)n->key_index.size();
+      if (i < nkey) return static_list_elem(n->kids[0], n->key_index[(size_t)i], et, depth + 1);
+      const AggSpec &a = n->aggs[(size_t)(i - nkey)];
+      if (a.kind != CAPF_AGG_COLLECT) return false;
+      et = infer_type(a.arg, n->kids[0]->names, n->kids[0]->types);  // collect_lists: the argument's type
+      return true;
+    }
+    case Kind::NameList:
+      if (i < nk) return static_list_elem(n->kids[0], i, et, depth + 1);
+      et = Type::String;
+      return true;
+    case Kind::ListColumns:
+      if (i < nk) return static_list_elem(n->kids[0], i, et, depth + 1);
+      et = n->list_elem;
+      return true;
+    case Kind::Explode: return i < nk && static_list_elem(n->kids[0], i, et, depth + 1);
+    case Kind::WithColumns:
+      for (int t : n->target_index)
+        if (t == i) return false;  // a computed list
+      return i < nk && static_list_elem(n->kids[0], i, et, depth + 1);
+  }
+  return false;
+}
+
 capf_status capf_table_list_info(capf_table *t, const char *col, int32_t *elem_type,
                                  int64_t *n_values) {
   CAPF_API_BEGIN
@@ -1763,6 +1878,11 @@ capf_status capf_table_list_info(capf_table *t, const char *col, int32_t *elem_t
   need(col, "col");
   int i = t->node->col_index_or_throw(col);
   if (t->node->types[i] != Type::List) illegal("column '" + std::string(col) + "' is not a LIST");
+  Type st;
+  if (!n_values && elem_type && static_list_elem(t->node, i, st)) {  // the type alone: no evaluation
+    *elem_type = (int32_t)st;
+    return CAPF_OK;
+  }
   DataPtr d = materialize(t->node);
   const ColPtr &c = d->cols[i];
   Session *s = t->node->s;
@@ -2300,9 +2420,14 @@ capf_status capf_table_explode_list(capf_table *t, const char *list_col, const c
   nn->types.push_back(Type::Null);
   nn->explode_list_col = li;
   if (c->types[li] == Type::List) {
-    DataPtr d = materialize(c);
-    const ColPtr &lc = d->cols[li];
-    nn->types.back() = lc->child ? lc->child->type : Type::Null;
+    Type et;
+    if (static_list_elem(c, li, et)) {
+      nn->types.back() = et;
+    } else {  // a computed list: its element type is known once it exists
+      DataPtr d = materialize(c);
+      const ColPtr &lc = d->cols[li];
+      nn->types.back() = lc->child ? lc->child->type : Type::Null;
+    }
   }
   *out = wrap(nn);
   CAPF_API_END

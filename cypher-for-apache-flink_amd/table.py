@@ -71,7 +71,11 @@ class GpuSession:
             codes.append(-1 if r is None else self.intern(r))
         arr = (c_int64 * max(len(codes), 1))(*codes)
         mid = c_int32()
-        _lib.call("capf_session_code_map", self._h, arr, len(codes), byref(mid))
+        if ent is None:
+            _lib.call("capf_session_code_map", self._h, arr, len(codes), byref(mid))
+        else:  # the same map grown (in place: no device table left behind per growth)
+            _lib.call("capf_session_code_map_extend", self._h, int(ent[2].rsplit(":", 1)[1]), arr, len(codes),
+                      byref(mid))
         nm = "\x01map:%d" % mid.value
         self._maps[key] = (n, codes, nm)
         return nm
@@ -311,9 +315,10 @@ class GpuTable:
         return self.capf_type(col)
 
     def list_elem_type(self, col):
-        """Element type of a LIST column (capf_table_list_info: evaluates the table)."""
-        et, nv = c_int32(), c_int64()
-        _lib.call("capf_table_list_info", self._h, col.encode(), byref(et), byref(nv))
+        """Element type of a LIST column (capf_table_list_info without a value
+        count: read off the plan when it says, else the table is evaluated)."""
+        et = c_int32()
+        _lib.call("capf_table_list_info", self._h, col.encode(), byref(et), None)
         return et.value
 
     @property

@@ -320,7 +320,10 @@ capf_status capf_table_count_async(capf_table *t, int64_t *d_count);
 capf_status capf_table_download(capf_table *t, const char *col, void *values_out,
                                 uint8_t *valid_out);
 /* LIST columns (CAPF_TYPE_LIST, from CAPF_AGG_COLLECT).  capf_table_list_info:
- * the element type (CAPF_TYPE_*) and the total element count of column col.
+ * the element type (CAPF_TYPE_*) and the total element count of column col
+ * (n_values NULL: the type alone, read off the plan without evaluating the
+ * table whenever the plan determines it — collect, a list literal, labels /
+ * keys, or a column passed through select / filter / join / union / sort).
  * capf_table_download_list: offsets_out[size + 1] (int64, list i = elements
  * [offsets[i], offsets[i+1])), values_out[n_values] elements (8 or 1 bytes
  * each, never NULL), valid_out[size] list validity (may be NULL).
@@ -408,7 +411,9 @@ capf_status capf_table_with_columns(capf_table *t, int32_t n, const capf_expr *e
  *   NULL), values n × (8 or 1) bytes (NULL for a NULL-typed list), valid
  *   NULL (no NULL elements) or n bytes.
  * capf_table_explode_list: the elements of LIST column list_col (a NULL list
- *   drops the row, like an empty one).                                      */
+ *   drops the row, like an empty one).  Lazy like every other operator: t is
+ *   evaluated with the result, unless list_col is a computed list expression
+ *   (its element type is then only known once it exists).                  */
 capf_status capf_table_explode_values(capf_table *t, const char *name, int32_t type, int64_t n,
                                       const void *values, const uint8_t *valid, capf_table **out);
 capf_status capf_table_explode_list(capf_table *t, const char *list_col, const char *name,
@@ -643,6 +648,14 @@ capf_status capf_session_literal_set(capf_session *s, const int64_t *values, int
  * function on the host with the JVM's string semantics and interns the
  * results; the map is referenced in programs as "\x01map:<id>" (*map_id).  */
 capf_status capf_session_code_map(capf_session *s, const int64_t *codes, int64_t n, int32_t *map_id);
+/* The code map map_id grown to n entries after the dictionary has grown:
+ * codes[0 .. old n) must be the map's codes.  Replaced in place (*new_id =
+ * map_id; the old table is released once the launches already enqueued have
+ * read it, and programs naming the id read the longer map) when this is the
+ * map's only registration; otherwise (equal maps registered for several
+ * functions) a new map is registered and *new_id names it.               */
+capf_status capf_session_code_map_extend(capf_session *s, int32_t map_id, const int64_t *codes, int64_t n,
+                                         int32_t *new_id);
 /* A LIST property column from host data (CTList properties of element tables,
  * CAPFElementTable.create / FlinkConversions.scala:43-117 map CTList to an
  * ARRAY column): appends LIST column `name` to t's rows (t is materialised):

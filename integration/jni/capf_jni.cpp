@@ -359,13 +359,16 @@ JNI(void, tableDownload)(JNIEnv *env, jobject, jlong t, jstring col, jobject val
   fail(env, capf_table_download(T(t), c.p, direct(env, values), (uint8_t *)direct(env, valid)));
 }
 // LIST columns (collect): returns the element type; element count → nValuesOut[0]
+// (nValuesOut null: the type alone, read off the plan without evaluating it)
 JNI(jint, tableListInfo)(JNIEnv *env, jobject, jlong t, jstring col, jlongArray nValuesOut) {
   JStr c(env, col);
   int32_t elem = 0;
   int64_t nv = 0;
-  if (fail(env, capf_table_list_info(T(t), c.p, &elem, &nv))) return 0;
-  jlong v = nv;
-  env->SetLongArrayRegion(nValuesOut, 0, 1, &v);
+  if (fail(env, capf_table_list_info(T(t), c.p, &elem, nValuesOut ? &nv : nullptr))) return 0;
+  if (nValuesOut) {
+    jlong v = nv;
+    env->SetLongArrayRegion(nValuesOut, 0, 1, &v);
+  }
   return elem;
 }
 JNI(void, tableDownloadList)(JNIEnv *env, jobject, jlong t, jstring col, jobject offsets,
@@ -847,6 +850,13 @@ JNI(jint, sessionCodeMap)(JNIEnv *env, jobject, jlong s, jlongArray codes) {
   int32_t id = -1;
   if (fail(env, capf_session_code_map(S(s), v.data(), (int64_t)v.size(), &id))) return -1;
   return id;
+}
+// the code map `id` grown to the dictionary's current size: its id (the same one when replaced in place)
+JNI(jint, sessionCodeMapExtend)(JNIEnv *env, jobject, jlong s, jint id, jlongArray codes) {
+  const std::vector<int64_t> v = longs(env, codes);
+  int32_t nid = -1;
+  if (fail(env, capf_session_code_map_extend(S(s), id, v.data(), (int64_t)v.size(), &nid))) return -1;
+  return nid;
 }
 // a value map of CAPF_OP_VALUE_MAP (sorted keys / key pairs → STRING codes): its id
 JNI(jint, sessionValueMap)(JNIEnv *env, jobject, jlong s, jlongArray keys, jlongArray keys2, jlongArray codes) {

@@ -59,8 +59,8 @@ final class GpuCypherSession private (val device: Int, hipStream: Long)
 
   /** Program name of the session code map of string function `key` (CAPF_OP_STR_MAP,
     * GpuStringFunctions.apply): the function applied to every dictionary string
-    * with the JVM's own String semantics, the results interned; extended and
-    * re-registered when the dictionary has grown since (the shim's twin of
+    * with the JVM's own String semantics, the results interned; extended in
+    * place when the dictionary has grown since (the shim's twin of
     * table.py GpuSession.string_map). */
   def stringMap(key: Seq[Any]): Option[String] = maps.synchronized {
     val n = { val d = new Array[Long](2); Native.guard(Native.stringDigest(handle, d)); d(0) }
@@ -72,7 +72,11 @@ final class GpuCypherSession private (val device: Int, hipStream: Long)
         val codes = old ++ (old.length.toLong until n).map { c =>
           GpuStringFunctions(key, Native.stringLookup(handle, c)).map(intern).getOrElse(-1L)
         }
-        val name = "\u0001map:" + Native.sessionCodeMap(handle, codes)
+        val id = Native.guard(prev match {  // a grown map replaces its table in place (capf_session_code_map_extend)
+          case Some((_, _, was)) => Native.sessionCodeMapExtend(handle, was.stripPrefix("\u0001map:").toInt, codes)
+          case None => Native.sessionCodeMap(handle, codes)
+        })
+        val name = "\u0001map:" + id
         maps.update(key, (n, codes, name))
         Some(name)
     }

@@ -207,5 +207,6 @@ object Native {
   @native def sessionCopyDevice(session: Long, dst: Long, src: Long, bytes: Long): Unit
   @native def sessionLiteralSet(session: Long, values: Array[Long]): Int
   @native def sessionCodeMap(session: Long, codes: Array[Long]): Int
+  @native def sessionCodeMapExtend(session: Long, mapId: Int, codes: Array[Long]): Int
   @native def sessionValueMap(session: Long, keys: Array[Long], keys2: Array[Long], codes: Array[Long]): Int
 }

@@ -249,6 +249,9 @@ class JniRoute:
             nat("tableDownload", None, h(t), self.jstr(col), self.direct(vals), self.direct(valid)), self.done())[1]
 
         def list_info(t, col, et, nv):
+            if nv is None:  # the type alone (a null nValuesOut)
+                out(et, nat("tableListInfo", I, h(t), self.jstr(col), None))
+                return self.done()
             o = self.lib.fj_longs(None, 1)
             out(et, nat("tableListInfo", I, h(t), self.jstr(col), o))
             v = (c_int64 * 1)()
@@ -325,6 +328,8 @@ class JniRoute:
             return f
         A["capf_session_literal_set"] = id_of("sessionLiteralSet", lambda s, arr, n: (h(s), self.jlongs(arr, n)))
         A["capf_session_code_map"] = id_of("sessionCodeMap", lambda s, arr, n: (h(s), self.jlongs(arr, n)))
+        A["capf_session_code_map_extend"] = id_of("sessionCodeMapExtend", lambda s, mid, arr, n:
+                                                  (h(s), (I, mid), self.jlongs(arr, n)))
         A["capf_session_value_map"] = id_of(
             "sessionValueMap", lambda s, k1, k2, cd, n:
             (h(s), self.jlongs(k1, n), self.jlongs(k2, n) if k2 is not None else None, self.jlongs(cd, n)))

@@ -1178,6 +1178,51 @@ def test_unwind_on_gpu(gpu_session):
         assert sorted((r["k"] or "", r["y"]) for r in rows) == [("", 2), ("a", 1), ("b", 2)]
 
 
+def test_unwind_and_list_type_read_off_the_plan(gpu_session):
+    """capf_table_explode_list and the type-only capf_table_list_info
+    take a LIST column's element type from the plan (collect's argument type, a
+    list literal's widened type, labels() → STRING, passed through select /
+    filter / join / union / sort) instead of running the child while the plan is
+    built — no upstream kernel (the filter's) runs before the result is asked
+    for — and the unwound rows match the oracle."""
+    from capf_amd.expr import Collect, Explode, ListLit
+    cols = [("k", T_INT, [1, 1, 2, 3, 3, 3], None), ("x", T_INT, [4, 5, 6, 7, 8, 9], None),
+            ("f", T_FLOAT, [0.5, 1.5, 2.5, 3.5, 4.5, 5.5], None)]
+    h = RecordHeader({Var(c): c for c in ["k", "x", "f", "xs", "ys", "e", "l"]})
+
+    def plans(sess):
+        t = sess.table(cols).filter(GreaterThan(Var("x"), IntegerLit(4)), h, {})
+        g = t.group([Var("k")], {"xs": Collect(Var("x")), "ys": Collect(Var("f"))}, header=h)
+        lit = t.withColumns((ListLit(Var("x"), Var("f")), "l"), header=h, params={})
+        return {
+            "collect": g.withColumns((Explode(Var("xs")), "e"), header=h, params={}),
+            "collect_sorted_renamed": g.orderBy((Var("k"), "desc"), header=h, params={})
+                                       .select(("ys", "xs"), ("k", "k"))
+                                       .withColumns((Explode(Var("xs")), "e"), header=h, params={}),
+            "union": g.select(("k", "k"), ("xs", "xs")).unionAll(g.select(("k", "k"), ("xs", "xs")))
+                      .withColumns((Explode(Var("xs")), "e"), header=h, params={}),
+            "list_literal": lit.withColumns((Explode(Var("l")), "e"), header=h, params={}),
+        }, g, lit
+
+    want, _, _ = plans(OracleSession())
+    gpu_session.reset_profile()
+    gpu_session.set_profiling(True)
+    try:
+        got, g, lit = plans(gpu_session)
+        assert g.list_elem_type("xs") == T_INT and g.list_elem_type("ys") == T_FLOAT
+        assert lit.list_elem_type("l") == T_FLOAT  # INTEGER and FLOAT elements widen
+        ran = [k for k in gpu_session.profile() if k.startswith("filter")]
+        assert not ran, f"the plan ran while it was being built: {ran}"
+        for name, t in got.items():
+            assert t.capf_type("e") == want[name].capf_type("e"), name
+            # (k, element) pairs: the order inside a collected list is not part of the contract
+            assert bag({"k": r["k"], "e": r["e"]} for r in t.rows) == \
+                bag({"k": r["k"], "e": r["e"]} for r in want[name].rows), name
+        assert any(k.startswith("filter") for k in gpu_session.profile())
+    finally:
+        gpu_session.set_profiling(False)
+
+
 MATH = ["Round", "Abs", "Ceil", "Floor", "Sign", "Sqrt", "Log", "Log10", "Exp", "Sin", "Cos", "Tan", "Asin",
         "Acos", "Atan", "Degrees", "Radians", "Cot", "Haversin"]
 

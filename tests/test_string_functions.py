@@ -271,3 +271,37 @@ def test_string_functions_over_distinct_values(gpu_session, monkeypatch):
         if [r["x"] for r in rg] != [r["x"] for r in ro]:
             bad.append(str(e))
     assert not bad, bad
+
+
+@pytest.mark.gpu
+def test_code_map_grows_in_place():
+    """a code map extended after the dictionary grew replaces its
+    device table under the same id (capf_session_code_map_extend) rather than
+    registering one more table per growth; a map two functions share (equal
+    contents) stays as it is and the growing function gets a map of its own;
+    a program planned before the growth evaluates right after it."""
+    from capf_amd.table import GpuSession
+    s = GpuSession(0)
+    try:
+        h = RecordHeader({Var("s"): "s"})
+        up, tr = ToUpper(Var("s")), Trim(Var("s"))
+
+        def col(t, e):
+            return [r["x"] for r in t.withColumns((e, "x"), header=h, params={}).rows]
+
+        t1 = s.table([("s", T_STRING, ["AB", "CD"], None)])
+        assert col(t1, up) == ["AB", "CD"] and col(t1, tr) == ["AB", "CD"]
+        before = {k: v[2] for k, v in s._maps.items()}
+        assert before[("upper",)] == before[("trim",)]  # identity on this dictionary: one shared map
+        early = t1.withColumns((up, "x"), header=h, params={})  # planned now, evaluated below
+        t2 = s.table([("s", T_STRING, ["ef ", " G", None], None)])
+        assert col(t2, up) == ["EF ", " G", None]
+        grown = s._maps[("upper",)][2]
+        assert grown != before[("upper",)]  # the shared map was not touched ...
+        assert col(t2, tr) == ["ef", "G", None]  # ... and trim's grows in place (its only user now)
+        assert s._maps[("trim",)][2] == before[("trim",)]
+        t3 = s.table([("s", T_STRING, ["hi", "jk "], None)])
+        assert col(t3, up) == ["HI", "JK "] and s._maps[("upper",)][2] == grown  # in place
+        assert [r["x"] for r in early.rows] == ["AB", "CD"]
+    finally:
+        s.close()

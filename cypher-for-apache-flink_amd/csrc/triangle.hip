@@ -391,8 +391,10 @@ __device__ inline void tri_row_packed(uint32_t nb, uint32_t ns, const uint32_t *
     __builtin_amdgcn_wave_barrier();
     // ping-pong words and batch owners of the steps in flight; a word's pcols
     // position is recomputed from its owner on the rare escape instead of held
-    uint32_t w[2][ILP], bi[2][ILP];
-    auto issue = [&](uint32_t t0, uint32_t (&ww)[ILP], uint32_t (&bb)[ILP]) {
+    // (owners are < 64: one byte each, ILP of them packed in one register)
+    uint32_t w[2][ILP], bi[2];
+    static_assert(ILP <= 4, "owner bytes of one register");
+    auto issue = [&](uint32_t t0, uint32_t (&ww)[ILP], uint32_t &bbp) {
       uint32_t xc[ILP];
 #pragma unroll
       for (int u = 0; u < ILP; ++u) xc[u] = min(t0 + u * WAVE + lane, total - 1);
@@ -413,8 +415,12 @@ __device__ inline void tri_row_packed(uint32_t nb, uint32_t ns, const uint32_t *
 #pragma unroll
         for (int u = 0; u < ILP; ++u) bp[u] = v[u] <= xc[u] ? cand[u] : bp[u];
       }
+      uint32_t bb[ILP];
 #pragma unroll
       for (int u = 0; u < ILP; ++u) bb[u] = (uint32_t)(bp[u] - tb.pre);
+      bbp = 0;
+#pragma unroll
+      for (int u = 0; u < ILP; ++u) bbp |= bb[u] << (8 * u);
 #pragma unroll
       for (int u = 0; u < ILP; ++u) {
         const uint32_t pp = tb.qa[bb[u]] + (xc[u] - tb.pre[bb[u]]);
@@ -424,26 +430,29 @@ __device__ inline void tri_row_packed(uint32_t nb, uint32_t ns, const uint32_t *
         ww[u] = pcols[pp];
       }
     };
-    auto probe = [&](const uint32_t (&ww)[ILP], const uint32_t (&bb)[ILP], uint32_t t0) {
-      uint32_t wk[ILP], pw[ILP], pos[ILP];
+    auto probe = [&](const uint32_t (&ww)[ILP], uint32_t bbp, uint32_t t0) {
+      uint32_t wk[ILP], fp[ILP];
       bool live[ILP], hit[ILP];
 #pragma unroll
       for (int u = 0; u < ILP; ++u) {
         live[u] = t0 + u * WAVE + lane < total;
         wk[u] = ww[u] & TRI_M24;
       }
-      find.template batch<ILP>(wk, live, hit, pw, pos);
+      find.template batch<ILP>(wk, live, hit, fp);
 #pragma unroll
       for (int u = 0; u < ILP; ++u) {
         hits += (unsigned long long)__popcll(__ballot(hit[u]));  // (wave-uniform)
         if (hit[u]) {
-          const uint32_t pkw = (uint32_t)tb.pk[bb[u]] << 24;
-          const uint2 a1 = tri_esc(pkw) ? vals[pqe(kb + bb[u])]  // p–q
+          const uint32_t bo = (bbp >> (8 * u)) & 0xFFu;
+          const uint32_t pkw = (uint32_t)tb.pk[bo] << 24;
+          const uint2 a1 = tri_esc(pkw) ? vals[pqe(kb + bo)]  // p–q
                                         : make_uint2((pkw >> 24) & 15u, pkw >> 28);
           const uint32_t x = t0 + u * WAVE + lane;
-          const uint2 s2 = tri_esc(ww[u]) ? vals[tb.qa[bb[u]] + (x - tb.pre[bb[u]])]  // streamed: q–w (A) / p–w (B)
+          const uint2 s2 = tri_esc(ww[u]) ? vals[tb.qa[bo] + (x - tb.pre[bo])]  // streamed: q–w (A) / p–w (B)
                                           : make_uint2((ww[u] >> 24) & 15u, ww[u] >> 28);
-          const uint2 s3 = tri_fb(pw[u], vals, pos[u]);                // staged:   p–w (A) / q–w (B)
+          const uint32_t sn = fp[u] >> 24;                             // staged:   p–w (A) / q–w (B)
+          const uint2 s3 = ((sn & 15u) == 15u || (sn >> 4) == 15u) ? vals[find.a + (fp[u] & TRI_M24)]
+                                                                    : make_uint2(sn & 15u, sn >> 4);
           const uint2 a2 = SWAP ? s3 : s2, a3 = SWAP ? s2 : s3;
           // p→q→w→p  +  p→w→q→p
           t += (unsigned long long)a1.x * a2.x * a3.y + (unsigned long long)a3.x * a2.y * a1.y;
@@ -487,8 +496,9 @@ __device__ inline bool tri_bsearch(F f, uint32_t n, uint32_t a, uint32_t wk, uin
   return (pw & TRI_M24) == wk;
 }
 
-// Finders of the staged list: batch<ILP>(wk, live → hit, packed word pw, and —
-// for an escape word — its vals index pos).  Sorted: ILP lower-bound searches
+// Finders of the staged list: batch<ILP>(wk, live → hit, fp = the found word's
+// multiplicity nibbles << 24 | its index in the list — vals index a + index
+// when a nibble says "look it up"; one register per search, not two).  Sorted: ILP lower-bound searches
 // in lockstep by binary lifting (the list length n is wave-uniform, so every
 // lane runs the same floor(log2 n) + 1 steps, and the ILP dependent chains
 // interleave instead of running one after the other).
@@ -498,7 +508,7 @@ struct TriSorted {
   uint32_t n, a;
   template <int ILP>
   __device__ inline void batch(const uint32_t (&wk)[ILP], const bool (&live)[ILP], bool (&hit)[ILP],
-                               uint32_t (&pw)[ILP], uint32_t (&pos)[ILP]) const {
+                               uint32_t (&fp)[ILP]) const {
     // n is the staged list's length, equal on every lane: the halving loop is
     // scalar and every probe index is in range (no guard), so the ILP reads of
     // a step issue back to back under one wait.  base: lower bound of wk lies
@@ -532,8 +542,7 @@ struct TriSorted {
       const bool first = (v0[u] & TRI_M24) == wk[u];
       const bool second = (v1[u] & TRI_M24) == wk[u] && base[u] + 1 < nu;
       hit[u] = live[u] && (first || second);
-      pw[u] = first ? v0[u] : v1[u];
-      pos[u] = a + base[u] + (first ? 0u : 1u);
+      fp[u] = ((first ? v0[u] : v1[u]) & 0xFF000000u) | (base[u] + (first ? 0u : 1u));
     }
   }
 };
@@ -550,7 +559,7 @@ struct TriSortedRot {
   uint32_t n, a;
   template <int ILP>
   __device__ inline void batch(const uint32_t (&wk)[ILP], const bool (&live)[ILP], bool (&hit)[ILP],
-                               uint32_t (&pw)[ILP], uint32_t (&pos)[ILP]) const {
+                               uint32_t (&fp)[ILP]) const {
     const uint32_t nu = __builtin_amdgcn_readfirstlane(n);
     if (nu == 0) {
 #pragma unroll
@@ -592,8 +601,7 @@ struct TriSortedRot {
       const bool second = (v1[u] >> 8) == wk[u] && base[u] + 1 < nu;
       hit[u] = live[u] && (first || second);
       const uint32_t r = first ? v0[u] : v1[u];
-      pos[u] = a + base[u] + (first ? 0u : 1u);
-      pw[u] = (r >> 8) | (r << 24);
+      fp[u] = (r << 24) | (base[u] + (first ? 0u : 1u));
     }
   }
 };

@@ -363,7 +363,7 @@ __device__ inline uint2 tri_fb(uint32_t word, const uint2 *vals, uint32_t e) {
 // nb batch entries; the staged list of ns words is searched by `find`
 // (wk → found, its packed word pw, and — when pw's nibbles say "look it up" —
 // its vals index pos).
-template <int ILP, bool SPLIT = false, bool SWAP = false, class Q, class F, class E>
+template <int ILP, bool SPLIT = false, bool SWAP = false, bool STATS = true, class Q, class F, class E>
 __device__ inline void tri_row_packed(uint32_t nb, uint32_t ns, const uint32_t *pcols, const uint2 *vals,
                                       TriBatch2 &tb, Q qrow, F find,
                                       E pqe, unsigned long long &t, unsigned long long &probes,
@@ -387,7 +387,7 @@ __device__ inline void tri_row_packed(uint32_t nb, uint32_t ns, const uint32_t *
     tb.qa[lane] = qa;
     tb.pk[lane] = (uint8_t)(pk >> 24);
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane(inc, WAVE - 1);
-    probes += total;  // (wave-uniform: the kernels take lane 0's)
+    if (STATS) probes += total;  // (wave-uniform: the kernels take lane 0's)
     __builtin_amdgcn_wave_barrier();
     // ping-pong words and batch owners of the steps in flight; a word's pcols
     // position is recomputed from its owner on the rare escape instead of held
@@ -441,7 +441,7 @@ __device__ inline void tri_row_packed(uint32_t nb, uint32_t ns, const uint32_t *
       find.template batch<ILP>(wk, live, hit, fp);
 #pragma unroll
       for (int u = 0; u < ILP; ++u) {
-        hits += (unsigned long long)__popcll(__ballot(hit[u]));  // (wave-uniform)
+        if (STATS) hits += (unsigned long long)__popcll(__ballot(hit[u]));  // (wave-uniform)
         if (hit[u]) {
           const uint32_t bo = (bbp >> (8 * u)) & 0xFFu;
           const uint32_t pkw = (uint32_t)tb.pk[bo] << 24;
@@ -660,7 +660,7 @@ struct TriPassB {
   uint32_t nitems;
 };
 
-template <int ILP, int WPE, int SCAP = TRI_CAP>
+template <int ILP, int WPE, bool STATS, int SCAP = TRI_CAP>
 __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_tri_count_passb(const uint32_t *rowptr, const uint32_t *pcols,
                                                                 const uint2 *vals, TriPassB b, int parts,
                                                                 int part, int grab, int xcd,
@@ -691,7 +691,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))
       auto qs = [&](uint32_t k) { return b.in_rows ? b.in_rows[i0 + k] : tri_qrow(rowptr, inw[k]); };
       auto pqe = [&](uint32_t k) { return ine[k]; };
       if (dq > CAP) {  // long N+(q): searched in global memory
-        tri_row_packed<ILP, false, true>(n, dq, pcols, vals, tb, qs,
+        tri_row_packed<ILP, false, true, STATS>(n, dq, pcols, vals, tb, qs,
                                          tri_sorted([&](uint32_t x) { return row[x]; }, dq, a),
                                          pqe, t, probes, hits);
         staged = 0xFFFFFFFFu;
@@ -703,16 +703,18 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))
         __builtin_amdgcn_wave_barrier();
         staged = q;
       }
-      tri_row_packed<ILP, false, true>(n, dq, pcols, vals, tb, qs, TriSortedRot{sc, dq, a}, pqe, t, probes, hits);
+      tri_row_packed<ILP, false, true, STATS>(n, dq, pcols, vals, tb, qs, TriSortedRot{sc, dq, a}, pqe, t, probes, hits);
     }
   }
   unsigned long long tot;
   block_exclusive_scan(t, lds, tot);
   if (threadIdx.x == 0 && tot) atomicAdd(&acc[0], tot);
-  block_exclusive_scan(lane_id() == 0 ? probes : 0ull, lds, tot);
-  if (threadIdx.x == 0 && tot) atomicAdd(&acc[4], tot);
-  block_exclusive_scan(lane_id() == 0 ? hits : 0ull, lds, tot);
-  if (threadIdx.x == 0 && tot) atomicAdd(&acc[5], tot);
+  if (STATS) {
+    block_exclusive_scan(lane_id() == 0 ? probes : 0ull, lds, tot);
+    if (threadIdx.x == 0 && tot) atomicAdd(&acc[4], tot);
+    block_exclusive_scan(lane_id() == 0 ? hits : 0ull, lds, tot);
+    if (threadIdx.x == 0 && tot) atomicAdd(&acc[5], tot);
+  }
 }
 
 __global__ void k_tri_total(const unsigned long long *acc, int64_t *out) {
@@ -892,7 +894,7 @@ static void tri_build_passb(Session *s, const uint64_t *okey, TriGraph &g) {
 // Pass A over q-tiled work items (see tri_build_qtiles): item (p, k0, k1) probes
 // the q's N+(p)[k0, k1) — N+(p) staged in LDS (≤ TRI_CAP words) or searched in
 // place — with the pass-A rule (edges with |N+(p)| < |N+(q)| belong to pass B).
-template <int ILP, int WPE, int SCAP = TRI_CAP>
+template <int ILP, int WPE, bool STATS, int SCAP = TRI_CAP>
 __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_tri_count_qtiled(const uint32_t *rowptr, const uint32_t *pcols,
                                                                  const uint2 *vals, const uint2 *erow,
                                                                  const uint4 *items,
@@ -922,7 +924,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))
       auto pqe = [&](uint32_t k) { return a + k0 + k; };
       auto qrow = [&](uint32_t k) { return erow ? erow[a + k0 + k] : tri_qrow(rowptr, row[k0 + k]); };
       if (dp > CAP) {  // long N+(p): searched in global memory
-        tri_row_packed<ILP, true>(nb, dp, pcols, vals, tb, qrow,
+        tri_row_packed<ILP, true, false, STATS>(nb, dp, pcols, vals, tb, qrow,
                                   tri_sorted([&](uint32_t x) { return row[x]; }, dp, a),
                                   pqe, t, probes, hits);
         staged = 0xFFFFFFFFu;
@@ -934,16 +936,18 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))
         __builtin_amdgcn_wave_barrier();
         staged = p;
       }
-      tri_row_packed<ILP, true>(nb, dp, pcols, vals, tb, qrow, TriSortedRot{sc, dp, a}, pqe, t, probes, hits);
+      tri_row_packed<ILP, true, false, STATS>(nb, dp, pcols, vals, tb, qrow, TriSortedRot{sc, dp, a}, pqe, t, probes, hits);
     }
   }
   unsigned long long tot;
   block_exclusive_scan(t, lds, tot);
   if (threadIdx.x == 0 && tot) atomicAdd(&acc[0], tot);
-  block_exclusive_scan(lane_id() == 0 ? probes : 0ull, lds, tot);
-  if (threadIdx.x == 0 && tot) atomicAdd(&acc[4], tot);
-  block_exclusive_scan(lane_id() == 0 ? hits : 0ull, lds, tot);
-  if (threadIdx.x == 0 && tot) atomicAdd(&acc[5], tot);
+  if (STATS) {
+    block_exclusive_scan(lane_id() == 0 ? probes : 0ull, lds, tot);
+    if (threadIdx.x == 0 && tot) atomicAdd(&acc[4], tot);
+    block_exclusive_scan(lane_id() == 0 ? hits : 0ull, lds, tot);
+    if (threadIdx.x == 0 && tot) atomicAdd(&acc[5], tot);
+  }
 }
 
 // ------------------------------------------------------ q-tiled pass A
@@ -1200,34 +1204,67 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
     // timers are named after the kernels that run (bench.py matches them against the
     // kernel names of the committed PMC counters)
     if (g.pcols) {  // node ids < 2^24: packed words, pass A q-tiled + pass B
-      if (g.naitems > 0) {
-        KernelTimer kt(s, "tri_count_qtiled", 4.0 * g.P);
-        auto kq = tri_ilp() == 3 ? k_tri_count_qtiled<3, TRI_WPE>
-                  : tri_wpe() == 6 ? k_tri_count_qtiled<TRI_ILP, 6>
-                  : tri_wpe() == 7 ? k_tri_count_qtiled<TRI_ILP, 7> : k_tri_count_qtiled<TRI_ILP, TRI_WPE>;
-        hipLaunchKernelGGL(kq, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK),
+      // STATS: the probe / hit counters of the profiling diagnostics (their
+      // registers push the 8-wave kernels into scratch: 44 / 48 B per lane with,
+      // 20 / 32 B without), so the timed kernels run without them and a
+      // profiled query counts them in an untimed second launch
+      auto kq = [&](bool st) {
+        const int ilp = tri_ilp(), wpe = tri_wpe();
+        if (st) return ilp == 3 ? k_tri_count_qtiled<3, TRI_WPE, true>
+                       : wpe == 6 ? k_tri_count_qtiled<TRI_ILP, 6, true>
+                       : wpe == 7 ? k_tri_count_qtiled<TRI_ILP, 7, true> : k_tri_count_qtiled<TRI_ILP, TRI_WPE, true>;
+        return ilp == 3 ? k_tri_count_qtiled<3, TRI_WPE, false>
+               : wpe == 6 ? k_tri_count_qtiled<TRI_ILP, 6, false>
+               : wpe == 7 ? k_tri_count_qtiled<TRI_ILP, 7, false> : k_tri_count_qtiled<TRI_ILP, TRI_WPE, false>;
+      };
+      auto kb = [&](bool st) {
+        const int ilp = tri_ilp(), wpe = tri_wpe();
+        if (st) return ilp == 3 ? k_tri_count_passb<3, TRI_WPE, true>
+                       : wpe == 6 ? k_tri_count_passb<TRI_ILP, 6, true>
+                       : wpe == 7 ? k_tri_count_passb<TRI_ILP, 7, true> : k_tri_count_passb<TRI_ILP, TRI_WPE, true>;
+        return ilp == 3 ? k_tri_count_passb<3, TRI_WPE, false>
+               : wpe == 6 ? k_tri_count_passb<TRI_ILP, 6, false>
+               : wpe == 7 ? k_tri_count_passb<TRI_ILP, 7, false> : k_tri_count_passb<TRI_ILP, TRI_WPE, false>;
+      };
+      auto ptr = [](const BufPtr &x) { return x ? x->p : nullptr; };  // (no pass-B buffers without items)
+      TriPassB b{(const uint32_t *)ptr(g.in_words), (const uint2 *)ptr(g.in_rows), (const uint32_t *)ptr(g.in_eidx),
+                 (const uint4 *)ptr(g.items), g.nitems};
+      auto pass_a = [&](bool st, unsigned long long *cur, unsigned long long *ac) {
+        hipLaunchKernelGGL(kq(st), dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK),
                            0, s->stream, (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
                            (const uint2 *)g.vals->p, (const uint2 *)g.erow->p, (const uint4 *)g.aitems->p,
-                           g.naitems, parts, part, TRI_GRAB_A, TRI_XCHUNK, xa, acc);
+                           g.naitems, parts, part, TRI_GRAB_A, TRI_XCHUNK, cur, ac);
         KERNEL_CHECK();
-      }
-      if (s->profiling) {  // diagnostics (profiling mode only, host sync): pass A's probes
-        unsigned long long pa = 0;
-        HIP_CHECK(hipMemcpyAsync(&pa, acc + 4, 8, hipMemcpyDeviceToHost, s->stream));
-        s->sync();
-        s->profile["tri_probes_pass_a"].bytes += (double)pa;
+      };
+      auto pass_b = [&](bool st, unsigned long long *ac) {
+        hipLaunchKernelGGL(kb(st), dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK),
+                           0, s->stream, (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
+                           (const uint2 *)g.vals->p, b, parts, part, TRI_GRAB_B, 0, ac + 6, ac);
+        KERNEL_CHECK();
+      };
+      if (g.naitems > 0) {
+        KernelTimer kt(s, "tri_count_qtiled", 4.0 * g.P);
+        pass_a(false, xa, acc);
       }
       if (g.nitems > 0) {
         KernelTimer kt(s, "tri_count_passb", 4.0 * g.P);
-        TriPassB b{(const uint32_t *)g.in_words->p, (const uint2 *)g.in_rows->p, (const uint32_t *)g.in_eidx->p,
-                   (const uint4 *)g.items->p, g.nitems};
-        auto kb = tri_ilp() == 3 ? k_tri_count_passb<3, TRI_WPE>
-                  : tri_wpe() == 6 ? k_tri_count_passb<TRI_ILP, 6>
-                  : tri_wpe() == 7 ? k_tri_count_passb<TRI_ILP, 7> : k_tri_count_passb<TRI_ILP, TRI_WPE>;
-        hipLaunchKernelGGL(kb, dim3((unsigned)(s->num_cus * 8)), dim3(TRI_BLOCK),
-                           0, s->stream, (const uint32_t *)g.rowptr->p, (const uint32_t *)g.pcols->p,
-                           (const uint2 *)g.vals->p, b, parts, part, TRI_GRAB_B, 0, acc + 6, acc);
-        KERNEL_CHECK();
+        pass_b(false, acc);
+      }
+      if (s->profiling) {  // diagnostics (profiling mode only, untimed, host sync): probes and hits
+        BufPtr sacc = s->alloc(64), scur = s->alloc(8 * 32 * 8);
+        unsigned long long *sa = (unsigned long long *)sacc->p;
+        HIP_CHECK(hipMemsetAsync(sacc->p, 0, 64, s->stream));
+        HIP_CHECK(hipMemsetAsync(scur->p, 0, 8 * 32 * 8, s->stream));
+        unsigned long long h[2] = {0, 0};
+        if (g.naitems > 0) pass_a(true, (unsigned long long *)scur->p, sa);
+        HIP_CHECK(hipMemcpyAsync(h, sa + 4, 8, hipMemcpyDeviceToHost, s->stream));
+        s->sync();
+        s->profile["tri_probes_pass_a"].bytes += (double)h[0];
+        if (g.nitems > 0) pass_b(true, sa);
+        HIP_CHECK(hipMemcpyAsync(h, sa + 4, 16, hipMemcpyDeviceToHost, s->stream));
+        s->sync();
+        s->profile["tri_probes"].bytes += (double)h[0];
+        s->profile["tri_hits"].bytes += (double)h[1];
       }
     } else {  // wider node ranges: one pass over the unpacked CSR
       KernelTimer kt(s, "tri_count", 4.0 * g.P);
@@ -1244,11 +1281,13 @@ void triangle_count_async(Session *s, const ColPtr &srcc, const ColPtr &dstc, in
     // diagnostics (profiling mode only, host sync): the count kernel's work —
     // probes (w ∈ N+(q) searched in N+(p)), hits, oriented edges — as
     // byte-only profile entries, for bench.py's probe-traffic roofline
-    unsigned long long h[2];
-    HIP_CHECK(hipMemcpyAsync(h, acc + 4, 16, hipMemcpyDeviceToHost, s->stream));
-    s->sync();
-    s->profile["tri_probes"].bytes += (double)h[0];
-    s->profile["tri_hits"].bytes += (double)h[1];
+    if (!g.pcols) {  // (the packed path counted them in its untimed stats launch)
+      unsigned long long h[2];
+      HIP_CHECK(hipMemcpyAsync(h, acc + 4, 16, hipMemcpyDeviceToHost, s->stream));
+      s->sync();
+      s->profile["tri_probes"].bytes += (double)h[0];
+      s->profile["tri_hits"].bytes += (double)h[1];
+    }
     s->profile["tri_oriented_edges"].bytes += (double)g.P;
     s->profile["tri_passb_edges"].bytes += (double)g.nB;
     s->profile["tri_passa_items"].bytes += (double)g.naitems;

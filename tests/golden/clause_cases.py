@@ -116,6 +116,21 @@ def _match_cases():
                 Match([NodeP("a"), NodeP("b")], [RelP("_r", "a", "b", direction="both")])],
                [ret(("a.prop", P("a", "prop")), ("b.prop", P("b", "prop")))]),
          [{"a.prop": "a", "b.prop": "b"}, {"a.prop": "a", "b.prop": "b"}]),
+        # (a)--(a): an undirected self-loop matches once per rel (2 loops × {a's
+        # other loop, b→a} = 4 rows, not 8)
+        ("match_mixed_directed_undirected", MT + "320-341",
+         """CREATE (a:A {prop: 'a'})
+            CREATE (b:B {prop: 'b'})
+            CREATE (c:C {prop: 'c'})
+            CREATE (a)-[:T]->(a)
+            CREATE (a)-[:T]->(a)
+            CREATE (b)-[:T]->(a)
+            CREATE (a)-[:T]->(c)""",
+         Query([Match([NodeP("a", ("A",)), NodeP("other")],
+                      [RelP("_r1", "a", "a", direction="both"), RelP("_r2", "other", "a")])],
+               [ret(("a.prop", P("a", "prop")), ("other.prop", P("other", "prop")))]),
+         [{"a.prop": "a", "other.prop": "a"}, {"a.prop": "a", "other.prop": "a"},
+          {"a.prop": "a", "other.prop": "b"}, {"a.prop": "a", "other.prop": "b"}]),
         ("match_expand_into_var_length", MT + "443-454", SPRAWL,
          Query([Match([NodeP("a", ("Person",)), NodeP("c", ("City",)), NodeP("b", ("Person",))],
                       [RelP("_r1", "a", "c", ("LIVES_IN",)), RelP("_r2", "b", "c", ("LIVES_IN",)),

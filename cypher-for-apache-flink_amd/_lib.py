@@ -30,6 +30,11 @@ class NotImplementedException(CypherException):
     pass
 
 
+class SchemaException(CypherException):
+    """okapi's SchemaException: a property graph schema whose property types
+    cannot share one column (CAPFSchema.asCapf, CAPFSchema.scala:42-72)."""
+
+
 class IllegalStateException(CypherException):
     pass
 

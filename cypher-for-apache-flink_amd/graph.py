@@ -67,6 +67,48 @@ def _join_type(a, b):
     raise IllegalArgumentException(f"property with conflicting types {a} / {b}")
 
 
+def _check_schema(node_tables, rel_tables):
+    """CAPFSchema.asCapf (flink-cypher/.../schema/CAPFSchema.scala:42-72) over
+    the schema of these element tables: the property types of one label
+    combination / relationship type are joined across its tables (a union
+    graph's members), and any two label combinations that share a label must
+    agree on the keys they share — one column per property key and label.
+    A conflict is okapi's SchemaException, worded as CAPF words it."""
+    from ._lib import IllegalArgumentException, SchemaException
+
+    def fmt(combo):
+        return "[" + ", ".join(sorted(combo)) + "]"
+
+    def merged(tables):
+        out = {}
+        for t in tables:
+            keys = out.setdefault(t.labels, {})
+            for k, ct in t.props.items():
+                try:
+                    keys[k] = _join_type(keys.get(k), ct)
+                except IllegalArgumentException:
+                    raise SchemaException(
+                        f"The property type 'UNION({keys[k]}, {ct})' for property '{k}' can not be stored in a "
+                        f"Flink column. The unsupported type is specified on label combination "
+                        f"{fmt(t.labels)}.") from None
+        return out
+
+    combos = merged(node_tables)
+    merged(rel_tables)
+    for label in sorted(set().union(*combos) if combos else ()):
+        with_label = sorted((c for c in combos if label in c), key=sorted)
+        for i, c1 in enumerate(with_label):
+            for c2 in with_label[i + 1:]:
+                for k in sorted(set(combos[c1]) & set(combos[c2])):
+                    try:
+                        _join_type(combos[c1][k], combos[c2][k])
+                    except IllegalArgumentException:
+                        raise SchemaException(
+                            f"The property type 'UNION({combos[c1][k]}, {combos[c2][k]})' for property '{k}' can "
+                            f"not be stored in a Flink column. The conflict appears between label combinations "
+                            f"{fmt(c1)} and {fmt(c2)}.") from None
+
+
 @dataclass
 class ElementTable:
     kind: str                 # "node" | "rel"
@@ -167,6 +209,7 @@ class ScanGraph:
                     tab = tab.withColumns(*[(Add(Var(c), IntegerLit(i << 56)), c) for c in cols], header=h, params={})
                 e = ElementTable(t.kind, t.labels, tab, t.props, t.id_col, t.src_col, t.dst_col)
                 (nodes if t.kind == "node" else rels).append(e)
+        _check_schema(nodes, rels)  # the union's schema (UnionTests.scala:284-301)
         return ScanGraph(self.session, nodes, rels, validate=False)
 
     # ------------------------------------------------------------ scans

@@ -55,9 +55,10 @@ def test_reference_error_case_on_gpu(gpu_session, case):
 
 
 def test_union_graph_on_gpu(gpu_session):
-    from test_oracle_golden import check_union_graph, check_union_graph_scans
+    from test_oracle_golden import check_union_graph, check_union_graph_scans, check_union_graph_schema
     check_union_graph(gpu_session)
     check_union_graph_scans(gpu_session)
+    check_union_graph_schema(gpu_session)
 
 
 TWO_HOP = Query([Match([NodeP("a"), NodeP("b"), NodeP("c")], [RelP("r1", "a", "b"), RelP("r2", "b", "c")])],

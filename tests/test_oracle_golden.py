@@ -79,9 +79,33 @@ def check_union_graph_scans(session):
     assert all(isinstance(r["n"], CypherNode) for r in got)
 
 
+def check_union_graph_schema(session):
+    """MTa/UnionTests.scala:268-301: FROM a RETURN GRAPH UNION ALL FROM b RETURN
+    GRAPH has both graphs' nodes; with (:one {test: 1}) ∪ (:one {test: 'hello'})
+    it fails with a SchemaException naming the label, the key and both types
+    (CAPFSchema.asCapf, flink-cypher/.../schema/CAPFSchema.scala:42-72)."""
+    import pytest
+    from capf_amd._lib import SchemaException
+    from capf_amd.expr import Var
+    from capf_amd.planner import Match, NodeP, Query, Stage
+    a = ScanGraph.from_data(session, parse_create("CREATE ()"))
+    assert len(run(a.union_all(a), Query([Match([NodeP("n")])], [Stage([("n", Var("n", "NODE"))])]))) == 2
+    one_int = ScanGraph.from_data(session, parse_create("CREATE (:one{test:1})"))
+    one_str = ScanGraph.from_data(session, parse_create("CREATE (:one{test:'hello'})"))
+    with pytest.raises(SchemaException) as e:
+        one_int.union_all(one_str)
+    assert all(w in str(e.value) for w in ("one", "test", "STRING", "INTEGER")), str(e.value)
+    # a conflict between two combinations sharing a label fails the same way;
+    # combinations without a shared label may differ (a scan over both then fails)
+    with pytest.raises(SchemaException):
+        one_int.union_all(ScanGraph.from_data(session, parse_create("CREATE (:one:two{test:'x'})")))
+    one_int.union_all(ScanGraph.from_data(session, parse_create("CREATE (:two{test:'x'})")))
+
+
 def test_union_graph_on_oracle():
     check_union_graph(OracleSession())
     check_union_graph_scans(OracleSession())
+    check_union_graph_schema(OracleSession())
 
 
 def test_create_parser_ids():

@@ -61,6 +61,11 @@ def test_union_graph_on_gpu(gpu_session):
     check_union_graph_schema(gpu_session)
 
 
+def test_scan_graph_schema_on_gpu(gpu_session):
+    from test_oracle_golden import check_scan_graph_schema
+    check_scan_graph_schema(gpu_session)
+
+
 TWO_HOP = Query([Match([NodeP("a"), NodeP("b"), NodeP("c")], [RelP("r1", "a", "b"), RelP("r2", "b", "c")])],
                 [Stage([("count", CountStar())])])
 ONE_HOP_PERSON = Query([Match([NodeP("a", ("Person",)), NodeP("b")], [RelP("r", "a", "b")])],

@@ -102,6 +102,36 @@ def check_union_graph_schema(session):
     one_int.union_all(ScanGraph.from_data(session, parse_create("CREATE (:two{test:'x'})")))
 
 
+SPEAKS_GRAPH = """CREATE (max:Person:Astronaut {name: "Max"})
+CREATE (martin:Person:Martian {name: "Martin"})
+CREATE (swedish:Language {title: "Swedish"})
+CREATE (german:Language {title: "German"})
+CREATE (orbital:Language {title: "Orbital"})
+CREATE (max)-[:SPEAKS]->(swedish)
+CREATE (max)-[:SPEAKS]->(german)
+CREATE (martin)-[:SPEAKS]->(german)
+CREATE (martin)-[:SPEAKS]->(orbital)"""
+
+
+def check_scan_graph_schema(session):
+    """flink-cypher-testing/.../creation/graphs/CAPFTestGraphFactoryTest.scala:42-117
+    (testSchema): the scan graph of the CREATE query has one element table per
+    label combination / relationship type with the schema's property types —
+    {Person, Astronaut} and {Person, Martian}: name STRING, {Language}: title
+    STRING, SPEAKS without properties — and its 9 elements."""
+    g = ScanGraph.from_data(session, parse_create(SPEAKS_GRAPH))
+    assert {t.labels: t.props for t in g.node_tables} == {
+        frozenset({"Person", "Astronaut"}): {"name": "STRING"},
+        frozenset({"Person", "Martian"}): {"name": "STRING"},
+        frozenset({"Language"}): {"title": "STRING"}}
+    assert {t.labels: t.props for t in g.rel_tables} == {frozenset({"SPEAKS"}): {}}
+    assert sum(t.table.size for t in g.node_tables + g.rel_tables) == 9
+
+
+def test_scan_graph_schema_on_oracle():
+    check_scan_graph_schema(OracleSession())
+
+
 def test_union_graph_on_oracle():
     check_union_graph(OracleSession())
     check_union_graph_scans(OracleSession())

@@ -283,7 +283,9 @@ def load_pmc(path, labels):
         j = json.load(f)
     names = {k.split("<")[0].strip() for k in j.get("kernels", {})}
     missing = [lb for lb in labels if not any(sym in names for sym in pmc_symbols(lb))]
-    prov = {"file": rel, "lib": j.get("lib"), "pmc_kernels": sorted(j.get("kernels", {}))}
+    prov = {"file": rel, "lib": j.get("lib"), "pmc_kernels": sorted(j.get("kernels", {})),
+            # which kernel symbols each timer label of the line stands for
+            "timer_kernels": {lb: list(pmc_symbols(lb)) for lb in labels}}
     if missing:
         prov["rejected"] = f"no counters for kernels that ran: {missing}"
         return None, prov

@@ -193,6 +193,8 @@ __global__ __launch_bounds__(256) void k_dense_probe(ColView key, int64_t n, int
 }
 
 // Probe of the hashed index: one 16-B slot load per step of the linear probe.
+// WRITE = false: the match count only (no build row per probe row).
+template <bool WRITE>
 __global__ __launch_bounds__(256) void k_hidx_probe(ColView key, int64_t n, const HSlot *t, int64_t cap,
                                                     int64_t *brow, unsigned long long *matched) {
   __shared__ unsigned long long red[256 / WAVE];
@@ -214,7 +216,7 @@ __global__ __launch_bounds__(256) void k_hidx_probe(ColView key, int64_t n, cons
         h = (h + 1) & mask;
       }
     }
-    brow[r] = b;
+    if (WRITE) brow[r] = b;
     cnt += b >= 0 ? 1u : 0u;
   }
   cnt = wave_reduce_sum(cnt);
@@ -306,11 +308,32 @@ bool dense_join(Session *s, const Data &l, const Data &r, const std::vector<std:
   // through (inner join: the build key is the probe key)
   const Data &B = build_left ? l : r;
   const int bk = build_left ? keys[0].first : keys[0].second;
-  bool unread = all_match && join_type == CAPF_JOIN_INNER;
-  for (int j = 0; unread && j < (int)B.cols.size(); ++j) {
+  bool b_key_only = join_type == CAPF_JOIN_INNER;
+  for (int j = 0; b_key_only && j < (int)B.cols.size(); ++j) {
     const ColPtr &c = B.cols[j];
-    unread = j == bk || (c->is_const && c->n > 0) ||
-             (c->lazy && !c->lazy->nullable && c->lazy->src->is_const && c->lazy->src->n > 0);
+    b_key_only = j == bk || (c->is_const && c->n > 0) ||
+                 (c->lazy && !c->lazy->nullable && c->lazy->src->is_const && c->lazy->src->n > 0);
+  }
+  bool unread = all_match && b_key_only;
+  // a hashed (sparse-id) index cannot prove every probe key present from
+  // statistics: when the build side's rows would never be read, count the
+  // matches first (no build row written per probe row) — the Expand case, where
+  // every rel endpoint is a node, then passes the probe rows through as the
+  // dense index does; a probe key without a node falls back to the full probe
+  if (!unread && b_key_only && di->hashed && n > 0) {
+    BufPtr cacc = s->alloc(8);
+    HIP_CHECK(hipMemsetAsync(cacc->p, 0, 8, s->stream));
+    {
+      const double kw = pk->enc == ENC_FOR24 ? 3.0 : pk->enc == ENC_FOR32 ? 4.0 : 8.0;
+      KernelTimer kt(s, "hidx_probe", (kw + 16.0) * n);
+      const unsigned grid = grid_for(n, 256, (int64_t)s->num_cus * 8);
+      hipLaunchKernelGGL(k_hidx_probe<false>, dim3(grid), dim3(256), 0, s->stream, view_of(pk), n,
+                         (const HSlot *)di->hslots->p, di->cap, (int64_t *)nullptr, (unsigned long long *)cacc->p);
+      KERNEL_CHECK();
+    }
+    HIP_CHECK(hipMemcpyAsync(s->h_scalars, cacc->p, 8, hipMemcpyDeviceToHost, s->stream));
+    s->sync();
+    unread = s->h_scalars[0] == n;
   }
   if (unread) {
     out.left = out.right = BufPtr();
@@ -327,7 +350,7 @@ bool dense_join(Session *s, const Data &l, const Data &r, const std::vector<std:
     KernelTimer kt(s, di->hashed ? "hidx_probe" : "dense_probe", (kw + 8.0 + (di->hashed ? 16.0 : 0.0)) * n);
     const unsigned grid = grid_for(n, 256, (int64_t)s->num_cus * 8);
     if (di->hashed)
-      hipLaunchKernelGGL(k_hidx_probe, dim3(grid), dim3(256), 0, s->stream, view_of(pk), n,
+      hipLaunchKernelGGL(k_hidx_probe<true>, dim3(grid), dim3(256), 0, s->stream, view_of(pk), n,
                          (const HSlot *)di->hslots->p, di->cap, (int64_t *)brow->p, (unsigned long long *)acc->p);
     else if (di->ident)
       hipLaunchKernelGGL(k_dense_probe<true>, dim3(grid), dim3(256), 0, s->stream, view_of(pk), n, di->min,

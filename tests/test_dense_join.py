@@ -178,6 +178,27 @@ def test_hashed_index_join_parity(gpu_session, jt, index_left, misses, nulls, du
     assert "dense_probe" not in gpu_session.profile()
 
 
+@pytest.mark.parametrize("misses,nulls", [(False, False), (True, False), (False, True)],
+                         ids=["all_match", "misses", "nulls"])
+@pytest.mark.parametrize("index_left", [True, False], ids=["nodes_left", "nodes_right"])
+def test_hashed_index_key_only_build_side(gpu_session, misses, nulls, index_left):
+    """Inner join on a sparse-id node table holding only its key: the matches
+    are counted first (no build row written per probe row) and, when every
+    probe key has its node, the probe rows pass through with the key as the
+    node id; a missing key or a NULL falls back to the full probe.  Same bag as
+    the oracle either way."""
+    nodes, rels = _sparse_tables(3000, 20000, misses, nulls, False, seed=5 + int(misses) + 2 * int(nulls))
+    nodes = nodes[:1]  # the id column only
+    gn, gr = gpu_session.table(nodes), gpu_session.table(rels)
+    on, orl = OracleSession().table(nodes), OracleSession().table(rels)
+    if index_left:
+        got, want = gn.join(gr, "inner", ("id", "src")).rows, on.join(orl, "inner", ("id", "src")).rows
+    else:
+        got, want = gr.join(gn, "inner", ("src", "id")).rows, orl.join(on, "inner", ("src", "id")).rows
+    assert len(want) == 20000 or misses or nulls
+    assert bag(got) == bag(want)
+
+
 @pytest.mark.parametrize("compact", [False, True], ids=["int64", "for32"])
 def test_one_hop_rows_rmat_sparse_ids(gpu_session, compact):
     """MATCH (a)-->(b) RETURN a, b on R-MAT s12 with node ids v·1000003 + 7:

@@ -203,3 +203,34 @@ def test_device_error_surfaces_as_mapped_exception(route):
         assert t.column_values("x") == [1, 2, 3]  # the session stays usable
     finally:
         route.uninstall()
+
+
+@pytest.mark.gpu
+def test_random_programs_and_list_chains_through_jni(route):
+    """Seeded expression trees (tests/test_expr_fuzz.py: projections, WHERE
+    predicates, grouped aggregates) and LIST chains (tests/test_list_fuzz.py)
+    through the adapter — Program objects of every opcode the generators emit,
+    session code / value maps registered over JNI, LIST columns in and out —
+    against the same calls over ctypes."""
+    import test_expr_fuzz as ef
+    import test_list_fuzz as lf
+    from capf_amd.table import GpuSession
+    s_direct = GpuSession(0)
+
+    def run_all(s):
+        out = [ef._eval(s, e) for e in ef.expressions(60, seed=31)]
+        g = ef.Gen(5)
+        out += [s.table(ef._table_cols()).filter(g.bool_(3), ef.H, {}).rows for _ in range(30)]
+        out += [ef._group_rows(s, keys, aggs) for keys, aggs in ef.groups(20, seed=7)]
+        out += [lf.rows(lf.chain(s, seed)) for seed in range(30)]
+        return out
+
+    want = run_all(s_direct)
+    route.install()
+    try:
+        got = run_all(GpuSession(0))
+    finally:
+        route.uninstall()
+    bad = [i for i, (x, y) in enumerate(zip(got, want)) if x != y and not (
+        isinstance(x, list) and len(x) == len(y) and all(ef._same(a, b) or a == b for a, b in zip(x, y)))]
+    assert len(got) == len(want) and not bad, bad[:5]

@@ -1266,6 +1266,10 @@ __global__ void k_eval(const Instr *code, int ncode, const ColView *cols, int nc
 struct DeviceProgram {
   BufPtr code, cols;
   int ncode, ncols;
+  // session tables the views point into, held until the launches that read
+  // them are enqueued (a code map grown meanwhile returns its old table to the
+  // stream-ordered cache only after these)
+  std::vector<BufPtr> keep;
 };
 
 static DeviceProgram upload_program(Session *s, const Program &p,
@@ -1283,6 +1287,7 @@ static DeviceProgram upload_program(Session *s, const Program &p,
       if (id < 0 || (size_t)id >= s->literal_sets.size()) illegal("unknown literal set '" + nm.substr(1) + "'");
       const auto &ls = s->literal_sets[(size_t)id];
       views.push_back(ColView{ls.first->p, nullptr, (int32_t)Type::Int64, ENC_PLAIN, ls.second});
+      dp.keep.push_back(ls.first);
       continue;
     }
     if (is_value_map_name(nm)) {  // [keys][keys2][codes], n in `base`, pairs in `enc`
@@ -1291,6 +1296,7 @@ static DeviceProgram upload_program(Session *s, const Program &p,
       if (id < 0 || (size_t)id >= s->value_maps.size()) illegal("unknown value map '" + nm.substr(1) + "'");
       const auto &vm = s->value_maps[(size_t)id];
       views.push_back(ColView{vm.buf->p, nullptr, (int32_t)Type::Int64, vm.pairs ? 1 : 0, vm.n});
+      dp.keep.push_back(vm.buf);
       continue;
     }
     if (is_code_map_name(nm)) {  // code → code table, its length in `base`
@@ -1299,6 +1305,7 @@ static DeviceProgram upload_program(Session *s, const Program &p,
       if (id < 0 || (size_t)id >= s->code_maps.size()) illegal("unknown code map '" + nm.substr(1) + "'");
       const auto &cm = s->code_maps[(size_t)id];
       views.push_back(ColView{cm.first->p, nullptr, (int32_t)Type::Int64, ENC_PLAIN, cm.second});
+      dp.keep.push_back(cm.first);
       continue;
     }
     int idx = -1;
@@ -1333,6 +1340,7 @@ static DeviceProgram upload_program(Session *s, const Program &p,
       const int64_t *rk = string_rank_table(s, &nstr);
       in.i = (int64_t)views.size();
       views.push_back(ColView{rk, nullptr, (int32_t)Type::Int64, ENC_PLAIN, 0});
+      dp.keep.push_back(s->d_str_rank);
       for (auto &x : code)
         if (x.op == OP_STR_RANK) x.i = in.i;
       break;

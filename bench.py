@@ -438,6 +438,17 @@ def run_rows_leg(args):
     # var2: both rel scans are read (the path step and its start/target joins)
     compulsory = (32.0 if var2 else 16.0) * m + 16.0 * n_nodes + 18.0 * rows
     ms = elapsed * 1e3 / args.steps
+    # the sparse-id leg's HBM bytes per step: the PMC passes of
+    # tools/collect_rows_pmc.sh over its hashed-index probes (the step's
+    # dominant kernel, two launches per step), when collected for this build
+    traffic, tsrc = None, None
+    if not var2 and args.id_stride != 1 and per.get("hidx_probe"):
+        j, tsrc = load_pmc(os.path.join(ROOT, "profiles", f"pmc_rows_sparse_s{args.scale}.json"), ["hidx_probe"])
+        if j is not None and tsrc.get("lib") == "libcapf_gpu.so sha256:" + lib_digest():
+            launches = prof.get("hidx_probe", {}).get("launches", 2 * prof_steps) / prof_steps
+            traffic = pmc_bytes_of(j, ["hidx_probe"]) * launches
+        elif j is not None:
+            tsrc["rejected"] = "collected for another build"
     print(json.dumps({
         "metric": ROWS_METRIC, "value": rows * args.steps / elapsed, "unit": "joined rows/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
@@ -459,7 +470,8 @@ def run_rows_leg(args):
         "roofline": ({"bound": "hbm", "kernel": "whole step (2 joins + gathers + scans), wall time",
                       "achieved": compulsory / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": compulsory / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                      "traffic": None, "algorithmic_bytes_per_launch": compulsory,
+                      "traffic": traffic, "traffic_scope": "hidx_probe launches of one step" if traffic else None,
+                      "traffic_source": tsrc, "algorithmic_bytes_per_launch": compulsory,
                       "timed_kernels_ms_per_step": per, "timed_kernels_ms_sum": kern_ms}
                      if kern_ms > 0 else
                      {"bound": "hbm", "kernel": "none: no kernel ran — the result's (a, b) columns ARE the rel "

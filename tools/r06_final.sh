@@ -11,6 +11,8 @@ bash tools/collect_reach_profiles.sh > gpurun_out/rpmc.log 2>&1
 cp gpurun_out/rprof/pmc_reach_s16.json profiles/pmc_reach_s16.json
 bash tools/collect_tri_profiles.sh 24 > gpurun_out/tpmc.log 2>&1
 cp gpurun_out/tprof/pmc_tri_s24.json profiles/pmc_tri_s24.json
+bash tools/collect_rows_pmc.sh > gpurun_out/rows_pmc.log 2>&1
+cp gpurun_out/prof_rows/pmc_rows_sparse_s22.json profiles/pmc_rows_sparse_s22.json
 timeout -k 10 300 python -u bench.py > gpurun_out/closing_bench.json 2> gpurun_out/closing_bench.err
 bash tools/r06_legs.sh
 timeout -k 10 240 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/closing_smoke.log 2>&1
